@@ -1,0 +1,99 @@
+/*
+ * orbref.h -- CPU restatement of ORB-SLAM2's front-end hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity oracle: tests/, the smoke
+ * check in __graft_entry__.py and bench.py's cpu_baseline leg are the only
+ * callers.  The product (liborbgpu.so) never links or calls it.
+ *
+ * PARITY STATUS: unpinned against a real OpenCV-2.4 build.  The reference
+ * (SFXiang/ORB-SLAM2-Annotation) ships no tests, golden vectors or fixtures
+ * for this path, and its ORBextractor.cpp cannot be compiled here (OpenCV
+ * 2.4 is absent; writing header stand-ins for it is not allowed).  The
+ * OpenCV-2.4 primitive arithmetic restated here (resize INTER_LINEAR,
+ * GaussianBlur 7x7, FAST-9/16, fastAtan2, cvRound) is written down in
+ * DESIGN.md section "Spec decisions".  glibc sinf/cosf IS pinned: the
+ * restatement matches the host libm bit-for-bit on every float in [0, 6.3]
+ * (tools/check_sincosf.c).
+ *
+ * All functions are plain C ABI so tests can load liborbref.so via ctypes.
+ */
+#ifndef ORBREF_H
+#define ORBREF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same layout as cv::KeyPoint (OpenCV 2.4): pt.x, pt.y, size, angle,
+ * response, octave, class_id -- 28 bytes. */
+typedef struct orbref_kp {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbref_kp;
+
+typedef struct orbref_extractor orbref_extractor;
+
+/* ORBextractor::ORBextractor  (ORBextractor.cpp:412-472) */
+orbref_extractor* orbref_create(int nfeatures, float scale_factor, int nlevels,
+                                int ini_th_fast, int min_th_fast);
+void orbref_destroy(orbref_extractor* ex);
+
+/* ORBextractor::operator()  (ORBextractor.cpp:1053-1117).
+ * Returns the number of keypoints written (>= 0), or -1 if `capacity` is too
+ * small (nothing is written then).  desc: n x 32 bytes. */
+int orbref_extract(orbref_extractor* ex, const uint8_t* img, int width, int height,
+                   size_t step, orbref_kp* kps, uint8_t* desc, int capacity);
+
+/* Accessors for the state the last orbref_extract() left behind. */
+int orbref_level_count(const orbref_extractor* ex);
+int orbref_level_size(const orbref_extractor* ex, int level, int* w, int* h);
+/* copies level `level` of mvImagePyramid (tight rows, w*h bytes) */
+int orbref_level_copy(const orbref_extractor* ex, int level, uint8_t* dst);
+/* FAST candidates of a level in vToDistributeKeys order, coordinates
+ * relative to (minBorderX, minBorderY) = (16, 16): returns count, writes up
+ * to cap entries of (x, y, score). */
+int orbref_level_candidates(const orbref_extractor* ex, int level, int* xys, int cap);
+/* keypoints kept by DistributeOctTree for a level, in list order, before the
+ * +16 border shift: (x, y, score) */
+int orbref_level_octree(const orbref_extractor* ex, int level, int* xys, int cap);
+int orbref_features_per_level(const orbref_extractor* ex, int* out);
+void orbref_scale_factors(const orbref_extractor* ex, float* scale, float* inv_scale,
+                          float* sigma2, float* inv_sigma2);
+
+/* --- primitives (OpenCV 2.4 semantics as restated in DESIGN.md) --- */
+void orbref_resize_linear_u8(const uint8_t* src, int sw, int sh, size_t sstep,
+                             uint8_t* dst, int dw, int dh, size_t dstep);
+void orbref_gaussian7_u8(const uint8_t* src, int w, int h, size_t sstep,
+                         uint8_t* dst, size_t dstep);
+/* cv::FAST(img, kps, threshold, nonmax=true), TYPE_9_16; writes (x, y, score)
+ * row-major; returns count (or -1 when cap exceeded). */
+int orbref_fast(const uint8_t* img, int w, int h, size_t step, int threshold,
+                int* xys, int cap);
+float orbref_fast_atan2(float y, float x);
+float orbref_sinf(float x);  /* glibc 2.35 sinf restatement */
+float orbref_cosf(float x);  /* glibc 2.35 cosf restatement */
+int orbref_descriptor_distance(const uint8_t* a, const uint8_t* b);
+/* one rBRIEF descriptor: img must be the blurred level, (cx, cy) integral */
+void orbref_orb_descriptor(const uint8_t* blurred, size_t step, int cx, int cy,
+                           float angle_deg, uint8_t* desc32);
+float orbref_ic_angle(const uint8_t* img, size_t step, int cx, int cy);
+
+/* --- matcher --------------------------------------------------------- */
+/* ORBmatcher::SearchForInitialization (ORBmatcher.cpp:474-590) for a frame
+ * pair with no distortion (mvKeysUn == mvKeys, image bounds [0,W]x[0,H]).
+ * prev_xy: float[2*n1], updated in place (vbPrevMatched).  matches12: int[n1].
+ * check_ori: rotation-consistency test; histo_bug: use the annotated tree's
+ * factor 1/HISTO_LENGTH instead of HISTO_LENGTH/360.  Returns nmatches. */
+int orbref_search_for_initialization(const orbref_kp* kps1, const uint8_t* desc1, int n1,
+                                     const orbref_kp* kps2, const uint8_t* desc2, int n2,
+                                     int img_w, int img_h, float* prev_xy, int window,
+                                     float nnratio, int check_ori, int histo_bug,
+                                     int* matches12);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

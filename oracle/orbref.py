@@ -1,0 +1,168 @@
+"""ctypes binding of the CPU parity oracle (liborbref.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by the product.  Parity status: see
+orbref.h (unpinned vs OpenCV 2.4; glibc sinf/cosf pinned exhaustively).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+_LIB = None
+
+
+class KeyPoint(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("size", ctypes.c_float),
+                ("angle", ctypes.c_float), ("response", ctypes.c_float),
+                ("octave", ctypes.c_int32), ("class_id", ctypes.c_int32)]
+
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is None:
+        path = _HERE / "liborbref.so"
+        if not path.exists():
+            raise RuntimeError(f"oracle not built: {path} (run make -C oracle)")
+        L = ctypes.CDLL(str(path))
+        vp, i, f, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+        L.orbref_create.restype = vp
+        L.orbref_create.argtypes = [i, f, i, i, i]
+        L.orbref_destroy.argtypes = [vp]
+        L.orbref_extract.restype = i
+        L.orbref_extract.argtypes = [vp, vp, i, i, sz, vp, vp, i]
+        L.orbref_level_size.argtypes = [vp, i, ctypes.POINTER(i), ctypes.POINTER(i)]
+        L.orbref_level_copy.argtypes = [vp, i, vp]
+        L.orbref_level_candidates.argtypes = [vp, i, vp, i]
+        L.orbref_level_octree.argtypes = [vp, i, vp, i]
+        L.orbref_features_per_level.argtypes = [vp, vp]
+        L.orbref_scale_factors.argtypes = [vp, vp, vp, vp, vp]
+        L.orbref_resize_linear_u8.argtypes = [vp, i, i, sz, vp, i, i, sz]
+        L.orbref_gaussian7_u8.argtypes = [vp, i, i, sz, vp, sz]
+        L.orbref_fast.argtypes = [vp, i, i, sz, i, vp, i]
+        L.orbref_fast_atan2.restype = f
+        L.orbref_fast_atan2.argtypes = [f, f]
+        L.orbref_sinf.restype = f
+        L.orbref_sinf.argtypes = [f]
+        L.orbref_cosf.restype = f
+        L.orbref_cosf.argtypes = [f]
+        L.orbref_descriptor_distance.argtypes = [vp, vp]
+        L.orbref_orb_descriptor.argtypes = [vp, sz, i, i, f, vp]
+        L.orbref_ic_angle.restype = f
+        L.orbref_ic_angle.argtypes = [vp, sz, i, i]
+        L.orbref_search_for_initialization.argtypes = [vp, vp, i, vp, vp, i, i, i, vp, i, f, i, i, vp]
+        _LIB = L
+    return _LIB
+
+
+def _p(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class Extractor:
+    """ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)."""
+
+    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7):
+        self.nlevels = nlevels
+        self.h = lib().orbref_create(nfeatures, scale_factor, nlevels, ini_th, min_th)
+        if not self.h:
+            raise ValueError("bad extractor parameters")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orbref_destroy(self.h)
+            self.h = None
+
+    def extract(self, img: np.ndarray):
+        img = np.ascontiguousarray(img, np.uint8)
+        cap = 1 << 16
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = lib().orbref_extract(self.h, _p(img), img.shape[1], img.shape[0], img.strides[0],
+                                 _p(kps), _p(desc), cap)
+        if n < 0:
+            raise RuntimeError("keypoint capacity exceeded")
+        return kps[:n].copy(), desc[:n].copy()
+
+    def level(self, l: int) -> np.ndarray:
+        w, h = ctypes.c_int(), ctypes.c_int()
+        if lib().orbref_level_size(self.h, l, ctypes.byref(w), ctypes.byref(h)) != 0:
+            raise IndexError(l)
+        out = np.zeros((h.value, w.value), np.uint8)
+        lib().orbref_level_copy(self.h, l, _p(out))
+        return out
+
+    def _xys(self, fn, l: int) -> np.ndarray:
+        n = fn(self.h, l, None, 0)
+        out = np.zeros((max(n, 1), 3), np.int32)
+        fn(self.h, l, _p(out), n)
+        return out[:n]
+
+    def candidates(self, l: int) -> np.ndarray:
+        return self._xys(lib().orbref_level_candidates, l)
+
+    def octree(self, l: int) -> np.ndarray:
+        return self._xys(lib().orbref_level_octree, l)
+
+    def features_per_level(self) -> np.ndarray:
+        out = np.zeros(self.nlevels, np.int32)
+        lib().orbref_features_per_level(self.h, _p(out))
+        return out
+
+    def scale_factors(self):
+        arrs = [np.zeros(self.nlevels, np.float32) for _ in range(4)]
+        lib().orbref_scale_factors(self.h, *[_p(a) for a in arrs])
+        return arrs
+
+
+def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros((dh, dw), np.uint8)
+    lib().orbref_resize_linear_u8(_p(src), src.shape[1], src.shape[0], src.strides[0], _p(dst), dw, dh, dw)
+    return dst
+
+
+def gaussian7(src: np.ndarray) -> np.ndarray:
+    src = np.ascontiguousarray(src, np.uint8)
+    dst = np.zeros_like(src)
+    lib().orbref_gaussian7_u8(_p(src), src.shape[1], src.shape[0], src.strides[0], _p(dst), dst.strides[0])
+    return dst
+
+
+def fast(img: np.ndarray, threshold: int) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.uint8)
+    cap = img.size
+    out = np.zeros((cap, 3), np.int32)
+    n = lib().orbref_fast(_p(img), img.shape[1], img.shape[0], img.strides[0], threshold, _p(out), cap)
+    return out[:n]
+
+
+def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().orbref_descriptor_distance(_p(a), _p(b))
+
+
+def search_for_initialization(kps1, desc1, kps2, desc2, img_w, img_h, prev_xy=None,
+                              window=100, nnratio=0.9, check_ori=True, histo_bug=False):
+    """Returns (nmatches, matches12, prev_xy_updated)."""
+    kps1 = np.ascontiguousarray(kps1, KP_DTYPE)
+    kps2 = np.ascontiguousarray(kps2, KP_DTYPE)
+    desc1 = np.ascontiguousarray(desc1, np.uint8)
+    desc2 = np.ascontiguousarray(desc2, np.uint8)
+    if prev_xy is None:
+        prev_xy = np.stack([kps1["x"], kps1["y"]], axis=1).astype(np.float32)
+    prev = np.ascontiguousarray(prev_xy, np.float32).copy()
+    m12 = np.full(len(kps1), -1, np.int32)
+    n = lib().orbref_search_for_initialization(_p(kps1), _p(desc1), len(kps1), _p(kps2), _p(desc2), len(kps2),
+                                               img_w, img_h, _p(prev), window, nnratio, int(check_ori),
+                                               int(histo_bug), _p(m12))
+    return n, m12, prev

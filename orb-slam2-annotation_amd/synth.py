@@ -1,0 +1,105 @@
+"""Seeded synthetic mono/stereo image streams.
+
+The reference's datasets (TUM fr1_xyz, KITTI 00, EuRoC MH_01) are not in the
+repository, so every benchmark and parity test runs on these streams:
+
+* a 2048x2048 base texture: 1/f background + 8000 random rectangles and
+  ellipses with uniform-random intensities (dense enough that FAST finds
+  thousands of candidates per 640x480 frame, like a real indoor sequence);
+* frame t = a crop of the base texture centred at (1024 + 2t, 1024 + t),
+  rotated by 0.5 deg * t (bilinear), plus N(0, 2^2) noise, clamped to u8.
+  Consecutive frames therefore have true correspondences for matching;
+* edge fixtures: a flat image (no keypoints) and i.i.d. uniform noise
+  (maximum FAST candidate count).
+
+Everything is numpy on the host; tests hand the same bytes to the oracle and
+to the HIP path.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+BASE_SIZE = 2048
+N_SHAPES = 8000
+
+
+def _upsample(a: np.ndarray, size: int) -> np.ndarray:
+    """Bilinear upsample of a small square array to size x size."""
+    n = a.shape[0]
+    c = np.linspace(0, n - 1, size)
+    i0 = np.floor(c).astype(np.int64)
+    i1 = np.minimum(i0 + 1, n - 1)
+    f = c - i0
+    rows = a[i0] * (1 - f)[:, None] + a[i1] * f[:, None]
+    return rows[:, i0] * (1 - f)[None, :] + rows[:, i1] * f[None, :]
+
+
+def base_texture(seed: int = 0x0B5E) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    img = np.zeros((BASE_SIZE, BASE_SIZE), np.float64)
+    amp = 60.0
+    for n in (8, 16, 32, 64, 128, 256, 512, 1024):  # 1/f-like background
+        img += amp * _upsample(rng.standard_normal((n, n)), BASE_SIZE)
+        amp *= 0.6
+    img += 128.0
+    yy, xx = np.mgrid[0:256, 0:256]
+    for _ in range(N_SHAPES):
+        w, h = rng.integers(4, 96, size=2)
+        x0 = int(rng.integers(0, BASE_SIZE - w))
+        y0 = int(rng.integers(0, BASE_SIZE - h))
+        val = float(rng.uniform(0, 255))
+        if rng.random() < 0.5:
+            img[y0:y0 + h, x0:x0 + w] = val
+        else:
+            cy, cx = (h - 1) / 2.0, (w - 1) / 2.0
+            m = ((yy[:h, :w] - cy) / max(cy, 1)) ** 2 + ((xx[:h, :w] - cx) / max(cx, 1)) ** 2 <= 1.0
+            img[y0:y0 + h, x0:x0 + w][m] = val
+    return img
+
+
+def render_frame(base: np.ndarray, t: int, width: int, height: int, seed: int = 0,
+                 baseline_px: float = 0.0, noise_sigma: float = 2.0) -> np.ndarray:
+    """Frame t of the stream (u8, height x width).  baseline_px shifts the
+    virtual camera horizontally (right image of a stereo pair)."""
+    th = np.deg2rad(0.5 * t)
+    c, s = np.cos(th), np.sin(th)
+    v, u = np.mgrid[0:height, 0:width].astype(np.float64)
+    u -= (width - 1) / 2.0
+    v -= (height - 1) / 2.0
+    u += baseline_px
+    cx = BASE_SIZE / 2 + 2.0 * t
+    cy = BASE_SIZE / 2 + 1.0 * t
+    sx = c * u - s * v + cx
+    sy = s * u + c * v + cy
+    x0 = np.clip(np.floor(sx).astype(np.int64), 0, BASE_SIZE - 2)
+    y0 = np.clip(np.floor(sy).astype(np.int64), 0, BASE_SIZE - 2)
+    fx = np.clip(sx - x0, 0, 1)
+    fy = np.clip(sy - y0, 0, 1)
+    val = (base[y0, x0] * (1 - fx) * (1 - fy) + base[y0, x0 + 1] * fx * (1 - fy)
+           + base[y0 + 1, x0] * (1 - fx) * fy + base[y0 + 1, x0 + 1] * fx * fy)
+    rng = np.random.default_rng((seed << 20) + t)
+    val += rng.normal(0.0, noise_sigma, val.shape)
+    return np.clip(np.rint(val), 0, 255).astype(np.uint8)
+
+
+def mono_stream(n: int, width: int = 640, height: int = 480, seed: int = 0x0B5E,
+                t0: int = 0) -> np.ndarray:
+    """n consecutive frames, shape (n, height, width) u8."""
+    base = base_texture(seed)
+    return np.stack([render_frame(base, t0 + t, width, height, seed) for t in range(n)])
+
+
+def stereo_stream(n: int, width: int, height: int, seed: int, baseline_px: float = 24.0) -> np.ndarray:
+    """n stereo pairs, shape (n, 2, height, width): [:,0] left, [:,1] right."""
+    base = base_texture(seed)
+    return np.stack([np.stack([render_frame(base, t, width, height, seed),
+                               render_frame(base, t, width, height, seed + 1, baseline_px)])
+                     for t in range(n)])
+
+
+def flat_image(width: int = 640, height: int = 480, value: int = 128) -> np.ndarray:
+    return np.full((height, width), value, np.uint8)
+
+
+def noise_image(width: int = 640, height: int = 480, seed: int = 7) -> np.ndarray:
+    return np.random.default_rng(seed).integers(0, 256, (height, width), dtype=np.uint8)
