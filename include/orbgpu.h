@@ -1,0 +1,144 @@
+/*
+ * orbgpu.h -- C ABI of the MI355X-native ORB-SLAM2 front-end hot path.
+ *
+ * Drop-in boundary for the reference classes (paths relative to
+ * /root/reference/ORB-SLAM2):
+ *   ORBextractor            include/ORBextractor.h:47-111, src/ORBextractor.cpp
+ *   ORBmatcher (subset)     include/ORBmatcher.h:37-141,  src/ORBmatcher.cpp
+ * A header-only C++ adapter with the reference's class surface sits on top
+ * of this ABI (include/orbslam2_amd/ORBextractor.h, ORBmatcher.h); the ctypes
+ * / cgo-style binding a maintainer would add is shown in INTEGRATION.md.
+ *
+ * Conventions: every function returns an int status (ORBGPU_OK = 0, or a
+ * negative ORBGPU_ERR_*); orbgpu_last_error() returns a thread-local message
+ * for the last failure.  Plain pointers and sizes only.  "d_" pointers are
+ * device (HBM) pointers; the rest are host pointers.  A handle may be used
+ * by one thread at a time (like the reference's ORBextractor, which keeps
+ * per-call state in mvImagePyramid).  Stream arguments are hipStream_t
+ * passed as void* (NULL = the default stream).
+ */
+#ifndef ORBGPU_H
+#define ORBGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    ORBGPU_OK = 0,
+    ORBGPU_ERR_ARG = -1,         /* invalid argument                         */
+    ORBGPU_ERR_HIP = -2,         /* HIP runtime failure                      */
+    ORBGPU_ERR_CAPACITY = -3,    /* an output / internal capacity exceeded   */
+    ORBGPU_ERR_UNSUPPORTED = -4, /* geometry outside the supported envelope  */
+    ORBGPU_ERR_NO_DEVICE = -5    /* no usable gfx950 device                  */
+};
+
+/* Bit-identical to cv::KeyPoint of OpenCV 2.4 (28 bytes):
+ * Point2f pt; float size; float angle; float response; int octave; int class_id. */
+typedef struct orbgpu_keypoint {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orbgpu_keypoint;
+
+typedef struct orbgpu_extractor orbgpu_extractor;
+
+typedef struct orbgpu_extractor_info {
+    int nlevels;
+    int width, height;              /* level-0 frame size                  */
+    int max_batch;
+    int max_keypoints;              /* per-frame upper bound of output N   */
+    int level_width[32], level_height[32];
+    int features_per_level[32];     /* mnFeaturesPerLevel                  */
+} orbgpu_extractor_info;
+
+const char* orbgpu_last_error(void);
+/* 0 on success; fills the gfx arch name of the current device */
+int orbgpu_device_arch(char* buf, int buflen);
+
+/* ---------------------------------------------------------------------- */
+/* ORBextractor                                                            */
+/* ---------------------------------------------------------------------- */
+
+/* Replaces ORBextractor::ORBextractor(nfeatures, scaleFactor, nlevels,
+ * iniThFAST, minThFAST) (ORBextractor.h:51-52, ORBextractor.cpp:412-472).
+ * width/height fix the frame geometry (the pyramid and cell grids are
+ * precomputed); max_batch bounds orbgpu_extract_batch_device(). */
+int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels,
+                            int ini_th_fast, int min_th_fast, int width, int height,
+                            int max_batch, orbgpu_extractor** out);
+int orbgpu_extractor_destroy(orbgpu_extractor* ex);
+int orbgpu_extractor_get_info(const orbgpu_extractor* ex, orbgpu_extractor_info* info);
+
+/* GetScaleFactors / GetInverseScaleFactors / GetScaleSigmaSquares /
+ * GetInverseScaleSigmaSquares (ORBextractor.h:63-83).  Arrays of nlevels. */
+int orbgpu_extractor_get_scales(const orbgpu_extractor* ex, float* scale, float* inv_scale,
+                                float* sigma2, float* inv_sigma2);
+
+/* ORBextractor::operator()(image, mask, keypoints, descriptors)
+ * (ORBextractor.h:56-61, ORBextractor.cpp:1053-1117), host to host, one frame.
+ * image: CV_8UC1 width x height with row pitch `step` bytes.  Writes n <=
+ * capacity keypoints and n x 32 descriptor bytes (levels 0..L-1 in order).
+ * An empty image (NULL / zero size) returns ORBGPU_OK with *n = -1 and
+ * touches no output, like the reference's early return (:1056). */
+int orbgpu_extract(orbgpu_extractor* ex, const uint8_t* image, int width, int height, size_t step,
+                   orbgpu_keypoint* keypoints, uint8_t* descriptors, int capacity, int* n);
+
+/* Batched, HBM-resident form of operator(): frame b is at
+ * d_images + b*frame_step with row pitch row_step.  Frame b's keypoints go
+ * to d_kps + b*kp_capacity, descriptors to d_desc + b*kp_capacity*32, count
+ * to d_counts[b].  kp_capacity must be >= info.max_keypoints.  Asynchronous
+ * on `stream`; call orbgpu_extractor_sync() to collect internal errors. */
+int orbgpu_extract_batch_device(orbgpu_extractor* ex, const uint8_t* d_images, int batch,
+                                size_t row_step, size_t frame_step, orbgpu_keypoint* d_kps,
+                                uint8_t* d_desc, int* d_counts, int kp_capacity, void* stream);
+
+/* Synchronise `stream` and report any capacity overflow the kernels flagged
+ * since the last call (ORBGPU_ERR_CAPACITY) -- never silently truncated. */
+int orbgpu_extractor_sync(orbgpu_extractor* ex, void* stream);
+
+/* mvImagePyramid[level] of frame `frame` of the last extraction, copied to
+ * host (ORBextractor.h:85; read by Frame::ComputeStereoMatches). */
+int orbgpu_extractor_copy_level(orbgpu_extractor* ex, int frame, int level, uint8_t* dst,
+                                size_t dst_step);
+
+/* ---------------------------------------------------------------------- */
+/* ORBmatcher                                                              */
+/* ---------------------------------------------------------------------- */
+
+#define ORBGPU_MATCH_CHECK_ORI 1      /* mbCheckOrientation                 */
+#define ORBGPU_MATCH_ANNOTATED_HISTO 2 /* 注释版 rotation-bin factor 1/30   */
+
+/* ORBmatcher::DescriptorDistance (ORBmatcher.cpp:1838-1854) for n
+ * descriptor pairs resident in HBM: d_dist[i] = popcount(a_i xor b_i). */
+int orbgpu_hamming_pairs_device(const uint8_t* d_a, const uint8_t* d_b, int n, int* d_dist, void* stream);
+
+/* ORBmatcher(nnratio, checkOri).SearchForInitialization(F1, F2,
+ * vbPrevMatched, vnMatches12, windowSize) (ORBmatcher.h:60,
+ * ORBmatcher.cpp:474-590) for frames without distortion (mvKeysUn ==
+ * mvKeys, image bounds [0,W]x[0,H], Frame.cpp:525-529), batched over pairs.
+ * Pair b: F1 keypoints d_kps1 + b*stride1 (count d_n1[b], levels in
+ * extractor order), descriptors d_desc1 + b*stride1*32; same for F2.
+ * d_prev_xy (nullable): float2 per F1 keypoint at + b*stride1*2, read and
+ * updated (vbPrevMatched); NULL means vbPrevMatched = F1 positions.
+ * d_matches12: int per F1 keypoint at + b*stride1; d_nmatches[b]. */
+int orbgpu_search_for_initialization_batch_device(
+    int batch, int img_width, int img_height,
+    const orbgpu_keypoint* d_kps1, const uint8_t* d_desc1, const int* d_n1, size_t stride1,
+    const orbgpu_keypoint* d_kps2, const uint8_t* d_desc2, const int* d_n2, size_t stride2,
+    float* d_prev_xy, int window, float nnratio, int flags,
+    int* d_matches12, int* d_nmatches, void* stream);
+
+/* Host-pointer convenience form for one pair; returns nmatches in *n. */
+int orbgpu_search_for_initialization(int img_width, int img_height,
+                                     const orbgpu_keypoint* kps1, const uint8_t* desc1, int n1,
+                                     const orbgpu_keypoint* kps2, const uint8_t* desc2, int n2,
+                                     float* prev_xy, int window, float nnratio, int flags,
+                                     int* matches12, int* nmatches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

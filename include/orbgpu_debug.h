@@ -1,0 +1,32 @@
+/*
+ * orbgpu_debug.h -- stage-level accessors of the last extraction, used by the
+ * parity tests to localise a divergence (pyramid / FAST cells / octree).
+ * Not part of the drop-in surface.  Synchronous; host outputs.
+ */
+#ifndef ORBGPU_DEBUG_H
+#define ORBGPU_DEBUG_H
+
+#include "orbgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* FAST candidates of (frame, level) in vToDistributeKeys order (cells
+ * row-major, FAST order inside a cell), as (x, y, score) relative to
+ * (minBorderX, minBorderY).  Returns the count (writes at most cap). */
+int orbgpu_debug_level_candidates(orbgpu_extractor* ex, int frame, int level, int* xys, int cap);
+
+/* DistributeOctTree output of (frame, level) in list order, (x, y, score)
+ * relative to the border.  Returns the count (writes at most cap). */
+int orbgpu_debug_level_octree(orbgpu_extractor* ex, int frame, int level, int* xys, int cap);
+
+/* Per-pass trace of the octree kernel for frame 0 (enable before extracting;
+ * out: per level 512 ints = [passes, 0, then 8 ints per pass: inner, nL, C,
+ * S, nToExpand, kstop, nkeys, N]). */
+int orbgpu_debug_octree_trace(orbgpu_extractor* ex, int enable, int* out, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

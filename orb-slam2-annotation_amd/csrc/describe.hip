@@ -1,0 +1,243 @@
+// describe.hip -- per-keypoint tail of ORBextractor::operator():
+//   IC_Angle on the unblurred level (ORBextractor.cpp:79-106, :474-481),
+//   GaussianBlur 7x7 sigma 2 REFLECT_101 of the level (:1097-1098, restated
+//   per keypoint on the 37x37 neighbourhood rBRIEF can touch),
+//   computeOrbDescriptor (:110-149) and the final keypoint fields
+//   (:847-857, :1107-1115).
+//
+// One wave per keypoint slot.  The 43x43 raw neighbourhood is staged in LDS
+// once (REFLECT_101 applied on load, exactly the rows/columns the
+// reference's separable filter reads), then: moments by a 64-lane reduction;
+// the exact-integer row pass and the column pass with OpenCV-2.4's two
+// roundings (SSE2 float path = half-to-even on x < 4*floor(w/4), scalar
+// FixedPtCastEx tail = half-up); 256 tests as 4 wave ballots (bit t of the
+// descriptor = test t = lane t%64 of ballot t/64).  sin/cos of the angle use
+// the glibc-2.35 sinf/cosf restatement (fp64 polynomial), pinned bit-exact
+// against libm over every float in [0, 6.3].
+#include "orbgpu_internal.h"
+#include "orbgpu_kernels.h"
+#include "../../include/orbgpu.h"
+
+namespace orbgpu {
+
+namespace {
+
+__constant__ signed char c_pattern[1024] = {
+#include "bit_pattern_31.inc"
+};
+// umax of the 31-px disc (ORBextractor.cpp:456-471); checked against the
+// construction on the host at extractor creation.
+__constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+__constant__ int c_gk[7] = {18, 34, 49, 55, 49, 34, 18};
+
+constexpr int kRawPitch = 44;
+constexpr int kBlurPitch = 40;
+
+__device__ inline int reflect101(int p, int n) {
+    while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
+    return p;
+}
+
+// OpenCV 2.4 fastAtan2 (mathfuncs.cpp); explicit _rn ops: never contracted.
+__device__ inline float fast_atan2(float y, float x) {
+    const float k = (float)(180 / M_PI);
+    const float p1 = 0.9997878412794807f * k, p3 = -0.3258083974640975f * k;
+    const float p5 = 0.1555786518463281f * k, p7 = -0.04432655554792128f * k;
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float eps = (float)2.220446049250313080847e-16;  // (float)DBL_EPSILON
+    float a, c, c2;
+    if (ax >= ay) {
+        c = __fdiv_rn(ay, __fadd_rn(ax, eps));
+        c2 = __fmul_rn(c, c);
+        a = __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c);
+    } else {
+        c = __fdiv_rn(ax, __fadd_rn(ay, eps));
+        c2 = __fmul_rn(c, c);
+        a = __fsub_rn(90.f, __fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(__fadd_rn(__fmul_rn(p7, c2), p5), c2), p3), c2), p1), c));
+    }
+    if (x < 0) a = __fsub_rn(180.f, a);
+    if (y < 0) a = __fsub_rn(360.f, a);
+    return a;
+}
+
+// glibc 2.35 sinf/cosf (sysdeps/ieee754/flt-32, FMA variant), |y| < 120.
+struct SinCosTab { double sign[4], hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3; };
+__constant__ SinCosTab c_sc[2] = {
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, 0x1p0, -0x1.ffffffd0c621cp-2,
+     0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16, -0x1.555545995a603p-3,
+     0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13},
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, -0x1p0, 0x1.ffffffd0c621cp-2,
+     -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10, -0x1.99343027bf8c3p-16, -0x1.555545995a603p-3,
+     0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13}};
+
+__device__ inline uint32_t top12(float x) { return (__float_as_uint(x) >> 20) & 0x7ff; }
+
+__device__ inline float sc_poly(double x, double x2, const SinCosTab* p, int n) {
+    if ((n & 1) == 0) {
+        const double x3 = __dmul_rn(x, x2);
+        const double s1 = __fma_rn(x2, p->s3, p->s2);
+        const double x7 = __dmul_rn(x3, x2);
+        const double s = __fma_rn(x3, p->s1, x);
+        return __double2float_rn(__fma_rn(x7, s1, s));
+    }
+    const double x4 = __dmul_rn(x2, x2);
+    const double c2 = __fma_rn(x2, p->c4, p->c3);
+    const double c1 = __fma_rn(x2, p->c1, p->c0);
+    const double x6 = __dmul_rn(x4, x2);
+    const double c = __fma_rn(x4, p->c2, c1);
+    return __double2float_rn(__fma_rn(x6, c2, c));
+}
+
+__device__ inline void glibc_sincosf(float y, float* sinp, float* cosp) {
+    double x = y;
+    if (top12(y) < top12(0x1.921FB6p-1f)) {
+        if (top12(y) < top12(0x1p-12f)) { *sinp = y; *cosp = 1.0f; return; }
+        const double x2 = __dmul_rn(x, x);
+        *sinp = sc_poly(x, x2, &c_sc[0], 0);
+        *cosp = sc_poly(x, x2, &c_sc[0], 1);
+        return;
+    }
+    const double r = __dmul_rn(x, c_sc[0].hpi_inv);
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    x = __fma_rn(-(double)n, c_sc[0].hpi, x);
+    const double s = c_sc[0].sign[n & 3];
+    const SinCosTab* p = (n & 2) ? &c_sc[1] : &c_sc[0];
+    const double xs = __dmul_rn(x, s), x2 = __dmul_rn(x, x);
+    *sinp = sc_poly(xs, x2, p, n);
+    *cosp = sc_poly(xs, x2, p, n ^ 1);
+}
+
+__device__ inline int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __restrict__ img0, size_t row0,
+                                                      size_t frame0, const uint8_t* __restrict__ pyr,
+                                                      const uint32_t* __restrict__ oct_out,
+                                                      const int* __restrict__ oct_count,
+                                                      orbgpu_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                      int* __restrict__ counts, int kp_cap) {
+    __shared__ uint8_t s_raw[kPatch * kRawPitch];
+    __shared__ uint16_t s_row[kPatch * kBlur];
+    __shared__ uint8_t s_blur[kBlur * kBlurPitch];
+    const int lane = threadIdx.x;
+    const int f = blockIdx.y, slot = blockIdx.x;
+    int l = 0;
+    while (l + 1 < g.nlevels && slot >= g.lv[l + 1].out_offset) ++l;
+    const LevelGeom& L = g.lv[l];
+    const int i = slot - L.out_offset;
+    const int* oc = oct_count + (size_t)f * g.nlevels;
+    int before = 0, total = 0;
+    for (int ll = 0; ll < g.nlevels; ++ll) {
+        const int c = oc[ll];
+        total += c;
+        if (ll < l) before += c;
+    }
+    if (slot == 0 && lane == 0) counts[f] = total;
+    if (i >= oc[l]) return;
+    const uint32_t key = oct_out[(size_t)f * g.slots_frame + slot];
+    const int cx = key_x(key) + kBorder, cy = key_y(key) + kBorder;
+    const uint8_t* base = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
+    const size_t pitch = l == 0 ? row0 : (size_t)L.pitch;
+
+    for (int idx = lane; idx < kPatch * kPatch; idx += 64) {
+        const int r = idx / kPatch, c = idx - r * kPatch;
+        const int yy = reflect101(cy - kPatchR + r, L.h), xx = reflect101(cx - kPatchR + c, L.w);
+        s_raw[r * kRawPitch + c] = base[(size_t)yy * pitch + xx];
+    }
+    __syncthreads();
+
+    // intensity centroid over the disc (integer moments: order-free)
+    int m10 = 0, m01 = 0;
+    for (int idx = lane; idx < 31 * 31; idx += 64) {
+        const int v = idx / 31 - 15, u = idx % 31 - 15;
+        if (abs(u) <= c_umax[abs(v)]) {
+            const int p = s_raw[(kPatchR + v) * kRawPitch + kPatchR + u];
+            m10 += u * p;
+            m01 += v * p;
+        }
+    }
+    m10 = wave_sum(m10);
+    m01 = wave_sum(m01);
+    const float angle = fast_atan2((float)m01, (float)m10);
+
+    // row pass (exact int): rows 0..42, output cols 0..36 <-> patch cols 3..39
+    for (int idx = lane; idx < kPatch * kBlur; idx += 64) {
+        const int r = idx / kBlur, c = idx - r * kBlur;
+        const uint8_t* p = s_raw + r * kRawPitch + c;
+        int acc = 0;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) acc += c_gk[j] * p[j];
+        s_row[r * kBlur + c] = (uint16_t)acc;
+    }
+    __syncthreads();
+    // column pass with the SIMD/scalar rounding split on the level's x
+    const int w4 = L.w & ~3;
+    for (int idx = lane; idx < kBlur * kBlur; idx += 64) {
+        const int r = idx / kBlur, c = idx - r * kBlur;
+        int v = 0;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) v += c_gk[k] * (int)s_row[(r + k) * kBlur + c];
+        const int x = cx - kBlurR + c;
+        int o;
+        if (x < w4) {
+            const int q = v >> 16, rem = v & 0xFFFF;
+            o = q + ((rem > 32768) | ((rem == 32768) & (q & 1)));
+        } else {
+            o = (v + 32768) >> 16;
+        }
+        s_blur[r * kBlurPitch + c] = (uint8_t)min(o, 255);
+    }
+    __syncthreads();
+
+    // rBRIEF
+    const float ang = __fmul_rn(angle, (float)(M_PI / 180.f));
+    float sa, ca;
+    glibc_sincosf(ang, &sa, &ca);
+    const float a = ca, b = sa;
+    unsigned long long words[4];
+#pragma unroll
+    for (int rnd = 0; rnd < 4; ++rnd) {
+        const int t = rnd * 64 + lane;
+        int val[2];
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+            const float px = (float)c_pattern[4 * t + 2 * pp], py = (float)c_pattern[4 * t + 2 * pp + 1];
+            const int ry = __float2int_rn(__fadd_rn(__fmul_rn(px, b), __fmul_rn(py, a)));
+            const int rx = __float2int_rn(__fsub_rn(__fmul_rn(px, a), __fmul_rn(py, b)));
+            val[pp] = s_blur[(kBlurR + ry) * kBlurPitch + kBlurR + rx];
+        }
+        words[rnd] = __ballot(val[0] < val[1]);
+    }
+
+    const size_t o = (size_t)f * kp_cap + before + i;
+    if (lane < 4) reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = words[lane];
+    if (lane == 0) {
+        orbgpu_keypoint kp;
+        const float fx = (float)cx, fy = (float)cy;
+        kp.x = l == 0 ? fx : __fmul_rn(fx, L.scale);
+        kp.y = l == 0 ? fy : __fmul_rn(fy, L.scale);
+        kp.size = (float)L.size_i;
+        kp.angle = angle;
+        kp.response = (float)key_s(key);
+        kp.octave = l;
+        kp.class_id = -1;
+        kps[o] = kp;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
+                           const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
+                           orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
+                           hipStream_t stream) {
+    dim3 grid(g.slots_frame, batch);
+    hipLaunchKernelGGL(describe_kernel, grid, dim3(64), 0, stream, g, img0, row0, frame0, pyr, oct_out, oct_count,
+                       kps, desc, counts, kp_cap);
+    return hipGetLastError();
+}
+
+}  // namespace orbgpu

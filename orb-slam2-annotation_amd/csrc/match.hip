@@ -1,0 +1,221 @@
+// match.hip -- ORBmatcher::SearchForInitialization (ORBmatcher.cpp:474-590)
+// with Frame::GetFeaturesInArea / AssignFeaturesToGrid semantics
+// (Frame.cpp:241-259, :379-443) for distortion-free frames.
+//
+// One wave per frame pair.  Only octave-0 keypoints take part (F1 queries
+// skip level > 0, F2 candidates are filtered to level 0), and in extractor
+// output order they are the first n0 keypoints of each frame, so F2's
+// level-0 set (positions, 64x48 grid cell, descriptors, matched distance,
+// reverse match) lives in LDS.  The query loop is sequential by contract
+// (vMatchedDistance and the "steal" of an earlier match feed later queries,
+// SURVEY H5); inside a query the candidates are spread over the 64 lanes:
+// window/grid test, 256-bit Hamming via 4x popcll, then a wave min-reduction
+// of (dist, grid-order key) -- the reference keeps the FIRST minimum in
+// GetFeaturesInArea order (cell ix outer, iy inner, index) -- and a second
+// reduction for bestDist2.  The rotation histogram, ComputeThreeMaxima and
+// the cull run on the same wave.
+#include "orbgpu_internal.h"
+#include "orbgpu_kernels.h"
+#include "../../include/orbgpu.h"
+
+namespace orbgpu {
+
+namespace {
+
+constexpr int kMaxK0 = 1024;  // level-0 keypoints per frame held in LDS
+constexpr int kGC = 64, kGR = 48, kHL = 30, kThLow = 50;
+
+__device__ inline unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long t = __shfl_xor(v, o, 64);
+        v = t < v ? t : v;
+    }
+    return v;
+}
+
+__device__ inline int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// number of leading octave-0 keypoints
+__device__ int level0_count(const orbgpu_keypoint* k, int n) {
+    int lo = 0, hi = n;  // first index with octave != 0
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (k[mid].octave == 0) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(64) void match_init_kernel(int img_w, int img_h,
+                                                        const orbgpu_keypoint* __restrict__ kps1,
+                                                        const uint8_t* __restrict__ desc1, const int* __restrict__ n1p,
+                                                        size_t stride1, const orbgpu_keypoint* __restrict__ kps2,
+                                                        const uint8_t* __restrict__ desc2, const int* __restrict__ n2p,
+                                                        size_t stride2, float* __restrict__ prev_xy, int window,
+                                                        float nnratio, int flags, int* __restrict__ matches12,
+                                                        int* __restrict__ nmatches_out, int* __restrict__ err) {
+    __shared__ float s_x[kMaxK0], s_y[kMaxK0];
+    __shared__ int s_cell[kMaxK0];           // grid cell ix*48+iy, or -1 when not in the grid
+    __shared__ int s_mdist[kMaxK0];          // vMatchedDistance
+    __shared__ int s_m21[kMaxK0];            // vnMatches21
+    __shared__ unsigned long long s_d2[kMaxK0][4];
+    __shared__ int s_m12[kMaxK0];            // vnMatches12 for F1 level-0
+    __shared__ signed char s_bin[kMaxK0];    // rotation bin pushed for i1, or -1
+    __shared__ int s_hist[kHL];
+    const int lane = threadIdx.x;
+    const int b = blockIdx.x;
+    const orbgpu_keypoint* K1 = kps1 + (size_t)b * stride1;
+    const orbgpu_keypoint* K2 = kps2 + (size_t)b * stride2;
+    const uint8_t* D1 = desc1 + (size_t)b * stride1 * 32;
+    const uint8_t* D2 = desc2 + (size_t)b * stride2 * 32;
+    const int n1 = n1p[b], n2 = n2p[b];
+    int* M12 = matches12 + (size_t)b * stride1;
+    float* prev = prev_xy ? prev_xy + (size_t)b * stride1 * 2 : nullptr;
+    const int n10 = level0_count(K1, n1), n20 = level0_count(K2, n2);
+    if (n10 > kMaxK0 || n20 > kMaxK0) {
+        if (lane == 0) { atomicOr(err, kErrMatchCap); nmatches_out[b] = 0; }
+        for (int i = lane; i < n1; i += 64) M12[i] = -1;
+        return;
+    }
+    // Frame bounds without distortion and grid inverses (Frame.cpp:221-224, 525-529)
+    const float minX = 0.f, minY = 0.f, maxX = (float)img_w, maxY = (float)img_h;
+    const float invW = __fdiv_rn((float)kGC, __fsub_rn(maxX, minX));
+    const float invH = __fdiv_rn((float)kGR, __fsub_rn(maxY, minY));
+    for (int j = lane; j < n20; j += 64) {
+        const float x = K2[j].x, y = K2[j].y;
+        s_x[j] = x;
+        s_y[j] = y;
+        const int px = (int)roundf(__fmul_rn(__fsub_rn(x, minX), invW));
+        const int py = (int)roundf(__fmul_rn(__fsub_rn(y, minY), invH));
+        s_cell[j] = (px < 0 || px >= kGC || py < 0 || py >= kGR) ? -1 : px * kGR + py;
+        s_mdist[j] = 0x7FFFFFFF;
+        s_m21[j] = -1;
+        const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D2 + (size_t)j * 32);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s_d2[j][q] = d[q];
+    }
+    for (int i = lane; i < n10; i += 64) { s_m12[i] = -1; s_bin[i] = -1; }
+    if (lane < kHL) s_hist[lane] = 0;
+    __syncthreads();
+
+    const float r = (float)window;
+    const float factor = (flags & ORBGPU_MATCH_ANNOTATED_HISTO) ? __fdiv_rn(1.0f, (float)kHL) : __fdiv_rn((float)kHL, 360.0f);
+    int nmatches = 0;
+    for (int i1 = 0; i1 < n10; ++i1) {
+        const float x = prev ? prev[2 * i1] : K1[i1].x;
+        const float y = prev ? prev[2 * i1 + 1] : K1[i1].y;
+        const int cx0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, minX), r), invW)));
+        const int cx1 = min(kGC - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, minX), r), invW)));
+        const int cy0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, minY), r), invH)));
+        const int cy1 = min(kGR - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, minY), r), invH)));
+        if (cx0 >= kGC || cx1 < 0 || cy0 >= kGR || cy1 < 0) continue;
+        const unsigned long long* d1 = reinterpret_cast<const unsigned long long*>(D1 + (size_t)i1 * 32);
+        const unsigned long long q0 = d1[0], q1 = d1[1], q2 = d1[2], q3 = d1[3];
+        unsigned long long best = ~0ull;  // (dist << 32) | order key
+        int second = 0x7FFFFFFF;
+        for (int j = lane; j < n20; j += 64) {
+            const int cell = s_cell[j];
+            if (cell < 0) continue;
+            const int ix = cell / kGR, iy = cell - ix * kGR;
+            if (ix < cx0 || ix > cx1 || iy < cy0 || iy > cy1) continue;
+            if (!(fabsf(__fsub_rn(s_x[j], x)) < r && fabsf(__fsub_rn(s_y[j], y)) < r)) continue;
+            const int dist = __popcll(q0 ^ s_d2[j][0]) + __popcll(q1 ^ s_d2[j][1]) +
+                             __popcll(q2 ^ s_d2[j][2]) + __popcll(q3 ^ s_d2[j][3]);
+            if (s_mdist[j] <= dist) continue;
+            const unsigned long long key = ((unsigned long long)dist << 32) | ((unsigned)cell << 16) | (unsigned)j;
+            if (key < best) {
+                if (best != ~0ull) second = min(second, (int)(best >> 32));
+                best = key;
+            } else {
+                second = min(second, dist);
+            }
+        }
+        const unsigned long long wbest = wave_min_u64(best);
+        if (wbest == ~0ull) continue;  // no usable candidate
+        const int contrib = best == wbest ? second : (best == ~0ull ? 0x7FFFFFFF : (int)(best >> 32));
+        const int best2 = wave_min_i(contrib);
+        const int bestDist = (int)(wbest >> 32);
+        const int bidx = (int)(wbest & 0xFFFF);
+        if (bestDist <= kThLow && (float)bestDist < __fmul_rn((float)best2, nnratio)) {
+            if (lane == 0) {
+                const int prev21 = s_m21[bidx];
+                if (prev21 >= 0) s_m12[prev21] = -1;
+                s_m12[i1] = bidx;
+                s_m21[bidx] = i1;
+                s_mdist[bidx] = bestDist;
+                if (flags & ORBGPU_MATCH_CHECK_ORI) {
+                    float rot = __fsub_rn(K1[i1].angle, K2[bidx].angle);
+                    if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+                    int bin = (int)roundf(__fmul_rn(rot, factor));
+                    if (bin == kHL) bin = 0;
+                    s_bin[i1] = (signed char)bin;
+                    s_hist[bin] += 1;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    if (flags & ORBGPU_MATCH_CHECK_ORI) {
+        // ComputeThreeMaxima (ORBmatcher.cpp:1792-1833), then cull other bins
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < kHL; ++i) {
+            const int s = s_hist[i];
+            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+            else if (s > max3) { max3 = s; ind3 = i; }
+        }
+        if ((float)max2 < __fmul_rn(0.1f, (float)max1)) { ind2 = -1; ind3 = -1; }
+        else if ((float)max3 < __fmul_rn(0.1f, (float)max1)) ind3 = -1;
+        for (int i = lane; i < n10; i += 64) {
+            const int bin = s_bin[i];
+            if (bin >= 0 && bin != ind1 && bin != ind2 && bin != ind3) s_m12[i] = -1;
+        }
+        __syncthreads();
+    }
+    for (int i = lane; i < n1; i += 64) {
+        const int m = i < n10 ? s_m12[i] : -1;
+        M12[i] = m;
+        if (m >= 0) {
+            ++nmatches;
+            if (prev) { prev[2 * i] = s_x[m]; prev[2 * i + 1] = s_y[m]; }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nmatches += __shfl_xor(nmatches, o, 64);
+    if (lane == 0) nmatches_out[b] = nmatches;
+}
+
+__global__ __launch_bounds__(256) void hamming_pairs_kernel(const uint8_t* __restrict__ a,
+                                                            const uint8_t* __restrict__ b, int n,
+                                                            int* __restrict__ dist) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const ulonglong4 x = reinterpret_cast<const ulonglong4*>(a)[i];
+    const ulonglong4 y = reinterpret_cast<const ulonglong4*>(b)[i];
+    dist[i] = __popcll(x.x ^ y.x) + __popcll(x.y ^ y.y) + __popcll(x.z ^ y.z) + __popcll(x.w ^ y.w);
+}
+
+}  // namespace
+
+hipError_t launch_hamming_pairs(const uint8_t* a, const uint8_t* b, int n, int* dist, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(hamming_pairs_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a, b, n, dist);
+    return hipGetLastError();
+}
+
+hipError_t launch_match_init(int batch, int img_w, int img_h,
+                             const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,
+                             const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2, size_t stride2,
+                             float* prev_xy, int window, float nnratio, int flags,
+                             int* matches12, int* nmatches, int* err, hipStream_t stream) {
+    hipLaunchKernelGGL(match_init_kernel, dim3(batch), dim3(64), 0, stream, img_w, img_h, kps1, desc1, n1, stride1,
+                       kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags, matches12, nmatches, err);
+    return hipGetLastError();
+}
+
+}  // namespace orbgpu

@@ -1,0 +1,412 @@
+// octree.hip -- ORBextractor::DistributeOctTree (ORBextractor.cpp:541-770)
+// for one (frame, level) per 256-thread workgroup.
+//
+// The reference mutates a std::list of quadtree nodes.  This kernel restates
+// it as level-synchronous passes over flat arrays, keeping the list ORDER
+// (which is the output order) exact:
+//   * node array = the list in order; a pass writes the next list into a
+//     ping-pong buffer: children of the divided nodes in reverse push order
+//     (push_front), then the untouched nodes in their old order;
+//   * main-loop pass (:610-669): every node with > 1 key is divided, in list
+//     order;
+//   * inner-loop pass (:681-743): the nodes with > 1 key (== the reference's
+//     vSizeAndPointerToNode at that point) are divided in descending
+//     (size, creation seq) order and the pass stops right after the division
+//     that makes the list reach N -- found with a prefix sum of (children-1);
+//   * each key carries its node index; a pass is two sweeps over the keys
+//     (quadrant histogram via LDS atomics, then remap to the child/new slot);
+//   * finally the max-response key per node (first in candidate order on
+//     ties, :751-767) via one LDS atomicMax of (score << 24 | ~index).
+// The reference breaks size ties by heap address (:690); here ties are
+// broken by creation sequence number, the documented deviation,
+// identical to the oracle.
+#include "orbgpu_internal.h"
+#include "orbgpu_kernels.h"
+
+namespace orbgpu {
+
+namespace {
+
+constexpr int kThreads = 256;
+
+struct ONode {
+    uint32_t r0;   // x0 | y0 << 16
+    uint32_t r1;   // x1 | y1 << 16
+    uint32_t cnt;  // keys in node
+    uint32_t seq;  // creation sequence number
+};
+
+__device__ inline int node_quad(const ONode& n, uint32_t key) {
+    const int x0 = n.r0 & 0xFFFF, y0 = n.r0 >> 16, x1 = n.r1 & 0xFFFF, y1 = n.r1 >> 16;
+    const int mx = x0 + ((x1 - x0 + 1) >> 1);  // ceil((float)(UR.x-UL.x)/2), ExtractorNode::DivideNode :485
+    const int my = y0 + ((y1 - y0 + 1) >> 1);
+    return (key_x(key) < mx ? 0 : 1) + (key_y(key) < my ? 0 : 2);
+}
+
+__device__ inline ONode child_rect(const ONode& n, int q) {
+    const int x0 = n.r0 & 0xFFFF, y0 = n.r0 >> 16, x1 = n.r1 & 0xFFFF, y1 = n.r1 >> 16;
+    const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
+    const int cx0 = (q & 1) ? mx : x0, cx1 = (q & 1) ? x1 : mx;
+    const int cy0 = (q & 2) ? my : y0, cy1 = (q & 2) ? y1 : my;
+    ONode c;
+    c.r0 = (uint32_t)cx0 | ((uint32_t)cy0 << 16);
+    c.r1 = (uint32_t)cx1 | ((uint32_t)cy1 << 16);
+    c.cnt = 0;
+    c.seq = 0;
+    return c;
+}
+
+__device__ inline int wave_incl_scan(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// In-place exclusive scan of a[0..n) in LDS by the whole block; returns total.
+__device__ int block_scan(int* a, int n, int* s_tmp) {
+    const int per = (n + kThreads - 1) / kThreads;
+    const int beg = min(n, (int)threadIdx.x * per), end = min(n, beg + per);
+    int sum = 0;
+    for (int i = beg; i < end; ++i) sum += a[i];
+    const int incl = wave_incl_scan(sum);
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 63) s_tmp[wave] = incl;
+    __syncthreads();
+    int off = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) {
+        const int t = s_tmp[w];
+        if (w < wave) off += t;
+        total += t;
+    }
+    int run = off + incl - sum;
+    for (int i = beg; i < end; ++i) {
+        const int v = a[i];
+        a[i] = run;
+        run += v;
+    }
+    __syncthreads();
+    return total;
+}
+
+// Key storage: LDS when the level's candidates fit, else an HBM scratch
+// region.  Accessed through a uniform branch so that the LDS case compiles
+// to ds_* instructions (a generic pointer would force flat_* accesses).
+template <bool LDS>
+struct KeyStore {
+    uint32_t* keys;
+    uint16_t* nodes;
+    __device__ uint32_t key(int k) const { return keys[k]; }
+    __device__ int node(int k) const { return (int)nodes[k]; }
+    __device__ void set_key(int k, uint32_t v) const { keys[k] = v; }
+    __device__ void set_node(int k, int v) const { nodes[k] = (uint16_t)v; }
+};
+
+__device__ inline int pow2ceil(int v) {
+    int p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+template <bool LDS>
+__device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int nk, int ncells, int ncap, int ncap2,
+                            const uint32_t* __restrict__ cand, uint32_t* __restrict__ out,
+                            int* __restrict__ oct_count, int* __restrict__ err, int* __restrict__ trace,
+                            KeyStore<LDS> ks, int* s_misc, unsigned long long* s_sortk, ONode* s_node0,
+                            ONode* s_node1, uint32_t* s_qc, int* s_aux0, int* s_aux1, uint8_t* s_flag,
+                            int* s_cellofs) {
+    const int tid = threadIdx.x;
+    int* s_tmp = s_misc;
+
+    const int N = L.nfeat;
+    const int nini = L.nini;
+    if (nini > ncap) {
+        if (tid == 0) { atomicOr(err, kErrNodeCap); oct_count[f * g.nlevels + l] = 0; }
+        return;
+    }
+
+    // 2. roots (:545-587): keys -> root index (int)(x / hX)
+    for (int i = tid; i < nini; i += kThreads) s_aux0[i] = 0;
+    __syncthreads();
+    const uint32_t* cbase = cand + (size_t)f * g.cand_frame + L.cand_offset;
+    for (int k = tid; k < nk; k += kThreads) {
+        int lo = 0, hi = ncells - 1;  // last cell with cellofs <= k
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_cellofs[mid] <= k) lo = mid; else hi = mid - 1;
+        }
+        const uint32_t key = cbase[(size_t)lo * L.cell_cap + (k - s_cellofs[lo])];
+        ks.set_key(k, key);
+        int r = (int)__fdiv_rn((float)key_x(key), L.hx);
+        r = min(r, nini - 1);
+        ks.set_node(k, r);
+        atomicAdd(&s_aux0[r], 1);
+    }
+    __syncthreads();
+    // non-empty roots keep their order; empty ones are erased.  Computed by
+    // thread r (no single-lane loop: see tools/check_scc.py for the ROCm 7.2
+    // miscompile a uniform-address select in such a loop triggered).
+    for (int r = tid; r < nini; r += kThreads) s_aux1[r] = s_aux0[r] > 0 ? 1 : 0;
+    __syncthreads();
+    const int nroots = block_scan(s_aux1, nini, s_tmp);
+    for (int r = tid; r < nini; r += kThreads) {
+        const int c = s_aux0[r];
+        const int pos = s_aux1[r];
+        if (c > 0) {
+            ONode nd;
+            const int x0 = (int)(L.hx * (float)r), x1 = (int)(L.hx * (float)(r + 1));
+            nd.r0 = (uint32_t)x0;
+            nd.r1 = (uint32_t)x1 | ((uint32_t)(L.max_by - kBorder) << 16);
+            nd.cnt = (uint32_t)c;
+            nd.seq = (uint32_t)r;
+            s_node0[pos] = nd;
+        }
+        s_aux1[r] = c > 0 ? pos : -1;
+    }
+    __syncthreads();
+    for (int k = tid; k < nk; k += kThreads) ks.set_node(k, s_aux1[ks.node(k)]);
+    __syncthreads();
+
+    // 3. passes.  The pass state (list size, buffer, phase, next seq) is kept
+    // in registers: every thread derives it from the same block-scan totals.
+    int nL = nroots, cur = 0, nseq = nini;
+    bool inner = false;
+    for (int guard = 0; guard < 4096; ++guard) {
+        ONode* old = cur ? s_node1 : s_node0;
+        ONode* nw = cur ? s_node0 : s_node1;
+        // quadrant histogram of every node with > 1 key
+        for (int i = tid; i < nL * 4; i += kThreads) s_qc[i] = 0;
+        __syncthreads();
+        for (int k = tid; k < nk; k += kThreads) {
+            const int i = ks.node(k);
+            const ONode nd = old[i];
+            if (nd.cnt > 1) atomicAdd(&s_qc[i * 4 + node_quad(nd, ks.key(k))], 1u);
+        }
+        __syncthreads();
+        // processing order and push bases
+        int C;  // children pushed this pass
+        if (!inner) {
+            for (int i = tid; i < nL; i += kThreads) {
+                const bool div = old[i].cnt > 1;
+                int nch = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) nch += s_qc[i * 4 + q] > 0;
+                s_aux0[i] = div ? nch : 0;
+                s_flag[i] = div;
+            }
+            __syncthreads();
+            C = block_scan(s_aux0, nL, s_tmp);  // aux0 = push base (list order)
+        } else {
+            // compact the nodes with > 1 key, sort descending by (cnt, seq)
+            for (int i = tid; i < nL; i += kThreads) s_aux1[i] = old[i].cnt > 1;
+            __syncthreads();
+            const int m = block_scan(s_aux1, nL, s_tmp);
+            const int P = pow2ceil(max(m, 1));
+            for (int i = tid; i < P; i += kThreads) s_sortk[i] = 0ull;
+            __syncthreads();
+            for (int i = tid; i < nL; i += kThreads)
+                if (old[i].cnt > 1)
+                    s_sortk[s_aux1[i]] = ((unsigned long long)min(old[i].cnt, 0xFFFFFFu) << 40) |
+                                         ((unsigned long long)(old[i].seq & 0xFFFFFFFu) << 12) | (unsigned)i;
+            __syncthreads();
+            for (int k = 2; k <= P; k <<= 1)
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    for (int i = tid; i < P; i += kThreads) {
+                        const int ixj = i ^ j;
+                        if (ixj > i) {
+                            const unsigned long long a = s_sortk[i], b = s_sortk[ixj];
+                            const bool desc = (i & k) == 0;
+                            if (desc ? (a < b) : (a > b)) { s_sortk[i] = b; s_sortk[ixj] = a; }
+                        }
+                    }
+                    __syncthreads();
+                }
+            // rank r -> (nch - 1); inclusive scan; first r reaching N
+            for (int r = tid; r < m; r += kThreads) {
+                const int i = (int)(s_sortk[r] & 0xFFF);
+                int nch = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) nch += s_qc[i * 4 + q] > 0;
+                s_aux1[r] = nch - 1;
+            }
+            if (tid == 0) s_misc[8] = m - 1;
+            __syncthreads();
+            block_scan(s_aux1, m, s_tmp);  // exclusive prefix of (nch-1)
+            for (int r = tid; r < m; r += kThreads) {
+                const int i = (int)(s_sortk[r] & 0xFFF);
+                int nch = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) nch += s_qc[i * 4 + q] > 0;
+                if (nL + s_aux1[r] + nch - 1 >= N) atomicMin(&s_misc[8], r);
+            }
+            for (int i = tid; i < nL; i += kThreads) { s_flag[i] = 0; s_aux0[i] = 0; }
+            __syncthreads();
+            const int kstop = s_misc[8];
+            // push bases over ranks 0..kstop, scattered to node index
+            for (int r = tid; r < m; r += kThreads) {
+                const int i = (int)(s_sortk[r] & 0xFFF);
+                int nch = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) nch += s_qc[i * 4 + q] > 0;
+                s_aux1[r] = r <= kstop ? nch : 0;
+            }
+            __syncthreads();
+            C = block_scan(s_aux1, m, s_tmp);
+            for (int r = tid; r <= kstop && r < m; r += kThreads) {
+                const int i = (int)(s_sortk[r] & 0xFFF);
+                s_aux0[i] = s_aux1[r];
+                s_flag[i] = 1;
+            }
+            __syncthreads();
+        }
+        // survivors keep their order after the C pushed children
+        for (int i = tid; i < nL; i += kThreads) s_aux1[i] = s_flag[i] ? 0 : 1;
+        __syncthreads();
+        const int S = block_scan(s_aux1, nL, s_tmp);
+        const int nNew = C + S;
+        if (nNew > ncap || nseq + C > 0x0FFFFFFF) {
+            if (tid == 0) { atomicOr(err, nNew > ncap ? kErrNodeCap : kErrSeqCap); oct_count[f * g.nlevels + l] = 0; }
+            return;
+        }
+        if (tid == 0) s_misc[9] = 0;
+        __syncthreads();
+        for (int i = tid; i < nL; i += kThreads) {
+            const ONode nd = old[i];
+            if (s_flag[i]) {
+                int p = s_aux0[i];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t c = s_qc[i * 4 + q];
+                    if (c > 0) {
+                        const int pos = C - 1 - p;
+                        ONode ch = child_rect(nd, q);
+                        ch.cnt = c;
+                        ch.seq = (uint32_t)(nseq + p);
+                        nw[pos] = ch;
+                        s_qc[i * 4 + q] = (uint32_t)pos;
+                        if (c > 1) atomicAdd(&s_misc[9], 1);
+                        ++p;
+                    }
+                }
+            } else {
+                const int pos = C + s_aux1[i];
+                nw[pos] = nd;
+                s_aux1[i] = pos;
+            }
+        }
+        __syncthreads();
+        for (int k = tid; k < nk; k += kThreads) {
+            const int i = ks.node(k);
+            ks.set_node(k, s_flag[i] ? (int)s_qc[i * 4 + node_quad(old[i], ks.key(k))] : s_aux1[i]);
+        }
+        __syncthreads();
+        if (tid == 0 && trace && f == 0 && guard < 60) {
+            int* t = trace + l * 512 + 2 + guard * 8;
+            t[0] = inner; t[1] = nL; t[2] = C; t[3] = S; t[4] = s_misc[9]; t[5] = s_misc[8]; t[6] = nk; t[7] = N;
+            trace[l * 512] = guard + 1;
+        }
+        const int nexp = s_misc[9];  // children with > 1 key (nToExpand)
+        const bool done = nNew >= N || nNew == nL;  // :673 / :740
+        if (!inner && nNew + nexp * 3 > N) inner = true;  // :678
+        nseq += C;
+        cur ^= 1;
+        nL = nNew;
+        __syncthreads();  // s_misc[9] is reset by the next pass
+        if (done) break;
+    }
+
+    // 4. best key per node (max response, first in candidate order)
+    for (int i = tid; i < nL; i += kThreads) s_qc[i] = 0;
+    __syncthreads();
+    for (int k = tid; k < nk; k += kThreads)
+        atomicMax(&s_qc[ks.node(k)], ((uint32_t)key_s(ks.key(k)) << 24) | (0xFFFFFFu - (uint32_t)k));
+    __syncthreads();
+    if (nL > L.ocap) {
+        if (tid == 0) { atomicOr(err, kErrNodeCap); oct_count[f * g.nlevels + l] = 0; }
+        return;
+    }
+    for (int i = tid; i < nL; i += kThreads) out[i] = ks.key((int)(0xFFFFFFu - (s_qc[i] & 0xFFFFFFu)));
+    if (tid == 0) oct_count[f * g.nlevels + l] = nL;
+}
+
+__global__ __launch_bounds__(kThreads) void octree_kernel(Geom g, const uint32_t* __restrict__ cand,
+                                                          const int* __restrict__ cell_counts,
+                                                          uint32_t* __restrict__ gkeys,
+                                                          uint16_t* __restrict__ gknode,
+                                                          uint32_t* __restrict__ oct_out,
+                                                          int* __restrict__ oct_count, int* __restrict__ err,
+                                                          int kcap, int ncap, int* __restrict__ trace) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int l = blockIdx.x, f = blockIdx.y;
+    const int tid = threadIdx.x;
+    const LevelGeom& L = g.lv[l];
+    const int ncells = L.ncols * L.nrows;
+    const int ncap2 = pow2ceil(ncap);
+
+    // LDS carve (byte offsets must match octree_lds_bytes)
+    const size_t o_sortk = 64;
+    const size_t o_node0 = o_sortk + (size_t)ncap2 * 8;
+    const size_t o_node1 = o_node0 + (size_t)ncap * 16;
+    const size_t o_qc = o_node1 + (size_t)ncap * 16;
+    const size_t o_aux0 = o_qc + (size_t)ncap * 16;
+    const size_t o_aux1 = o_aux0 + (size_t)ncap * 4;
+    const size_t o_flag = o_aux1 + (size_t)ncap * 4;
+    const size_t o_cell = o_flag + (((size_t)ncap + 15) & ~(size_t)15);
+    const size_t o_keys = o_cell + (((size_t)(g.max_cells_level + 1) * 4 + 15) & ~(size_t)15);
+    const size_t o_knode = o_keys + (size_t)kcap * 4;
+    int* s_misc = reinterpret_cast<int*>(smem);
+    unsigned long long* s_sortk = reinterpret_cast<unsigned long long*>(smem + o_sortk);
+    ONode* s_node0 = reinterpret_cast<ONode*>(smem + o_node0);
+    ONode* s_node1 = reinterpret_cast<ONode*>(smem + o_node1);
+    uint32_t* s_qc = reinterpret_cast<uint32_t*>(smem + o_qc);
+    int* s_aux0 = reinterpret_cast<int*>(smem + o_aux0);
+    int* s_aux1 = reinterpret_cast<int*>(smem + o_aux1);
+    uint8_t* s_flag = smem + o_flag;
+    int* s_cellofs = reinterpret_cast<int*>(smem + o_cell);
+    int* s_tmp = s_misc;  // [0..3] scan scratch, [4..] scalars
+
+    // 1. candidate order: cells row-major, within a cell FAST order (:797-838)
+    const int* cc = cell_counts + (size_t)f * g.total_cells + L.cell_base;
+    for (int i = tid; i < ncells; i += kThreads) s_cellofs[i] = cc[i];
+    if (tid == 0) s_cellofs[ncells] = 0;
+    __syncthreads();
+    const int nk = block_scan(s_cellofs, ncells + 1, s_tmp);
+    uint32_t* out = oct_out + (size_t)f * g.slots_frame + L.out_offset;
+    if (nk <= kcap) {
+        KeyStore<true> ks{reinterpret_cast<uint32_t*>(smem + o_keys), reinterpret_cast<uint16_t*>(smem + o_knode)};
+        octree_body<true>(g, L, l, f, nk, ncells, ncap, ncap2, cand, out, oct_count, err, trace, ks, s_misc, s_sortk,
+                          s_node0, s_node1, s_qc, s_aux0, s_aux1, s_flag, s_cellofs);
+    } else {  // too many candidates for LDS: the same algorithm on an HBM scratch region
+        KeyStore<false> ks{gkeys + (size_t)f * g.cand_frame + L.cand_offset,
+                           gknode + (size_t)f * g.cand_frame + L.cand_offset};
+        octree_body<false>(g, L, l, f, nk, ncells, ncap, ncap2, cand, out, oct_count, err, trace, ks, s_misc, s_sortk,
+                           s_node0, s_node1, s_qc, s_aux0, s_aux1, s_flag, s_cellofs);
+    }
+}
+
+}  // namespace
+
+size_t octree_lds_bytes(const Geom& g, int kcap, int ncap) {
+    auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    int ncap2 = 1;
+    while (ncap2 < ncap) ncap2 <<= 1;
+    return r16(16 * 4) + r16((size_t)ncap2 * 8) + 2 * r16((size_t)ncap * 16) + r16((size_t)ncap * 16) +
+           2 * r16((size_t)ncap * 4) + r16((size_t)ncap) + r16((size_t)(g.max_cells_level + 1) * 4) +
+           r16((size_t)kcap * 4) + r16((size_t)kcap * 2);
+}
+
+hipError_t launch_octree(const Geom& g, int batch, const uint32_t* cand, const int* cell_counts,
+                         uint32_t* gkeys, uint16_t* gknode, uint32_t* oct_out, int* oct_count,
+                         int* err, int kcap, int ncap, int* trace, hipStream_t stream) {
+    const size_t lds = octree_lds_bytes(g, kcap, ncap);
+    dim3 grid(g.nlevels, batch);
+    hipLaunchKernelGGL(octree_kernel, grid, dim3(kThreads), lds, stream, g, cand, cell_counts, gkeys, gknode,
+                       oct_out, oct_count, err, kcap, ncap, trace);
+    return hipGetLastError();
+}
+
+}  // namespace orbgpu

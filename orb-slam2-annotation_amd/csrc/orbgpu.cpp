@@ -1,0 +1,610 @@
+// orbgpu.cpp -- host driver and C ABI (include/orbgpu.h).
+//
+// Owns the per-extractor geometry (computed once, with the reference's own
+// float arithmetic: ORBextractor.cpp:412-472, :781-795, :545-547, :1127-1128
+// and OpenCV-2.4 resize()'s tap tables), the HBM buffers sized for
+// max_batch frames, and the launch sequence of one extraction:
+//   pyramid level 1..L-1  ->  FAST cells (all levels)  ->  octree (frame x
+//   level)  ->  angle + blur + rBRIEF + keypoint fields (one wave per slot).
+// Errors raised inside kernels (capacity overflows) are accumulated in a
+// device word and reported by orbgpu_extractor_sync(); nothing is silently
+// truncated.  There is no CPU fallback: without a gfx950 device every entry
+// point fails with ORBGPU_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/orbgpu.h"
+#include "../../include/orbgpu_debug.h"
+#include "orbgpu_internal.h"
+#include "orbgpu_kernels.h"
+
+using namespace orbgpu;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define ORB_HIP(expr)                                                                               \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                     \
+        if (e_ != hipSuccess) return fail(ORBGPU_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// OpenCV 2.4 cvRound / cvFloor on the host (SSE2 cvtsd2si = half to even)
+inline int cv_round(double v) { return (int)std::nearbyint(v); }
+inline int cv_floor(double v) { const int i = cv_round(v); return i - (v < (double)i); }
+inline int sat_s16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+inline size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+int check_device() {
+    int dev = 0, n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(ORBGPU_ERR_NO_DEVICE, "no HIP device visible");
+    ORB_HIP(hipGetDevice(&dev));
+    hipDeviceProp_t p;
+    ORB_HIP(hipGetDeviceProperties(&p, dev));
+    if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
+        return fail(ORBGPU_ERR_NO_DEVICE, std::string("device is ") + p.gcnArchName + ", this build targets gfx950");
+    return ORBGPU_OK;
+}
+
+int vresize_simd_end(int width) {
+    int x = 0;
+    while (x <= width - 16) x += 16;
+    while (x < width - 4) x += 4;
+    return x;
+}
+
+// resize(src sw x sh -> dw x dh, INTER_LINEAR) tap tables, as cv::resize
+// (2.4, imgwarp.cpp) computes xofs/ialpha and yofs/ibeta for 8U.
+void build_resize_tables(int sw, int sh, int dw, int dh, std::vector<int2>& xt, std::vector<int2>& yt) {
+    const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+    const double scale_x = 1.0 / inv_sx, scale_y = 1.0 / inv_sy;
+    xt.resize(dw);
+    yt.resize(dh);
+    int xmax = dw;
+    std::vector<int> sxs(dw), a0s(dw), a1s(dw);
+    for (int dx = 0; dx < dw; ++dx) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cv_floor(fx);
+        fx -= (float)sx;
+        if (sx < 0) { fx = 0.f; sx = 0; }
+        if (sx + 1 >= sw) {
+            xmax = std::min(xmax, dx);
+            if (sx >= sw - 1) { fx = 0.f; sx = sw - 1; }
+        }
+        sxs[dx] = sx;
+        a0s[dx] = sat_s16(cv_round((1.f - fx) * 2048.f));
+        a1s[dx] = sat_s16(cv_round(fx * 2048.f));
+    }
+    for (int dx = 0; dx < dw; ++dx) {
+        int sx0 = sxs[dx], sx1 = sxs[dx] + 1, a0 = a0s[dx], a1 = a1s[dx];
+        if (dx >= xmax) { sx1 = sx0; a0 = 2048; a1 = 0; }  // HResizeLinear tail: S[sx]*ONE
+        xt[dx].x = sx0 | (sx1 << 16);
+        xt[dx].y = (a0 & 0xFFFF) | (a1 << 16);
+    }
+    for (int dy = 0; dy < dh; ++dy) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cv_floor(fy);
+        fy -= (float)sy;
+        const int b0 = sat_s16(cv_round((1.f - fy) * 2048.f)), b1 = sat_s16(cv_round(fy * 2048.f));
+        const int y0 = std::min(std::max(sy, 0), sh - 1), y1 = std::min(std::max(sy + 1, 0), sh - 1);
+        yt[dy].x = y0 | (y1 << 16);
+        yt[dy].y = (b0 & 0xFFFF) | (b1 << 16);
+    }
+}
+
+template <class T>
+int dalloc(T** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    ORB_HIP(hipMalloc((void**)p, count * sizeof(T)));
+    return ORBGPU_OK;
+}
+
+}  // namespace
+
+struct orbgpu_extractor {
+    Geom g;
+    int nfeatures = 0, nlevels = 0, ini_th = 0, min_th = 0;
+    float scale_factor = 0.f;
+    std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+    int W = 0, H = 0, max_batch = 0, max_kps = 0;
+    int kcap = 0, ncap = 0;
+    // device buffers
+    uint8_t* d_pyr = nullptr;
+    size_t pyr_bytes = 0;
+    int2* d_xtab = nullptr;
+    int2* d_ytab = nullptr;
+    uint32_t* d_cand = nullptr;
+    int* d_cell_counts = nullptr;
+    uint32_t* d_gkeys = nullptr;
+    uint16_t* d_gknode = nullptr;
+    uint32_t* d_oct_out = nullptr;
+    int* d_oct_count = nullptr;
+    int* d_err = nullptr;
+    int* d_trace = nullptr;  // optional octree pass trace (debug API)
+    // host-image path
+    uint8_t* d_img = nullptr;
+    size_t img_pitch = 0;
+    orbgpu_keypoint* d_kps1 = nullptr;
+    uint8_t* d_desc1 = nullptr;
+    int* d_count1 = nullptr;
+    hipStream_t stream = nullptr;
+    // last extraction (for copy_level)
+    const uint8_t* last_img = nullptr;
+    size_t last_row = 0, last_frame = 0;
+    int last_batch = 0;
+
+    ~orbgpu_extractor() {
+        void* ptrs[] = {d_pyr, d_xtab, d_ytab, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
+                        d_oct_count, d_err, d_trace, d_img, d_kps1, d_desc1, d_count1};
+        for (void* p : ptrs)
+            if (p) (void)hipFree(p);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+// ORBextractor ctor arithmetic (ORBextractor.cpp:417-448) + per-level layout.
+int build_geometry(orbgpu_extractor* e, std::vector<int2>& xtab, std::vector<int2>& ytab) {
+    const int L = e->nlevels;
+    e->scale.assign(L, 1.f);
+    e->sigma2.assign(L, 1.f);
+    for (int i = 1; i < L; ++i) {
+        e->scale[i] = e->scale[i - 1] * e->scale_factor;
+        e->sigma2[i] = e->scale[i] * e->scale[i];
+    }
+    e->inv_scale.resize(L);
+    e->inv_sigma2.resize(L);
+    for (int i = 0; i < L; ++i) {
+        e->inv_scale[i] = 1.0f / e->scale[i];
+        e->inv_sigma2[i] = 1.0f / e->sigma2[i];
+    }
+    std::vector<int> nfeat(L);
+    const float factor = 1.0f / e->scale_factor;
+    float per_scale = e->nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)L));
+    int sum = 0;
+    for (int l = 0; l < L - 1; ++l) {
+        nfeat[l] = cv_round(per_scale);
+        sum += nfeat[l];
+        per_scale *= factor;
+    }
+    nfeat[L - 1] = std::max(e->nfeatures - sum, 0);
+
+    Geom& g = e->g;
+    std::memset(&g, 0, sizeof(g));
+    g.nlevels = L;
+    g.width = e->W;
+    g.height = e->H;
+    g.ini_th = std::min(std::max(e->ini_th, 0), 255);
+    g.min_th = std::min(std::max(e->min_th, 0), 255);
+    size_t pyr_off = 0, cand_off = 0;
+    int cell_base = 0, out_off = 0, max_cells = 0, ncap = 0;
+    xtab.clear();
+    ytab.clear();
+    for (int l = 0; l < L; ++l) {
+        LevelGeom& v = g.lv[l];
+        v.w = cv_round((float)e->W * e->inv_scale[l]);
+        v.h = cv_round((float)e->H * e->inv_scale[l]);
+        v.scale = e->scale[l];
+        v.size_i = (int)(31 * e->scale[l]);
+        v.nfeat = nfeat[l];
+        v.pitch = (int)round_up((size_t)v.w, 16);
+        if (l > 0) {
+            v.frame_bytes = (size_t)v.pitch * v.h;
+            v.offset = pyr_off;
+            pyr_off += round_up(v.frame_bytes * e->max_batch, 256);
+        }
+        // cells
+        v.max_bx = v.w - kEdge + 3;
+        v.max_by = v.h - kEdge + 3;
+        const float width = (float)(v.max_bx - kBorder), height = (float)(v.max_by - kBorder);
+        if (!(width >= 30.f && height >= 30.f))
+            return fail(ORBGPU_ERR_UNSUPPORTED, "level " + std::to_string(l) + " is smaller than one FAST cell");
+        v.ncols = (int)(width / 30.f);
+        v.nrows = (int)(height / 30.f);
+        v.wcell = (int)std::ceil(width / v.ncols);
+        v.hcell = (int)std::ceil(height / v.nrows);
+        if (v.wcell + 6 > kMaxWin || v.hcell + 6 > kMaxWin)
+            return fail(ORBGPU_ERR_UNSUPPORTED, "FAST cell window larger than the LDS tile");
+        if (v.max_bx - kBorder > 2047 || v.max_by - kBorder > 2047)
+            return fail(ORBGPU_ERR_UNSUPPORTED, "levels wider/taller than 2079 px are not supported");
+        v.cell_base = cell_base;
+        v.cell_cap = ((v.wcell + 1) / 2) * ((v.hcell + 1) / 2);
+        v.cand_offset = cand_off;
+        cell_base += v.ncols * v.nrows;
+        cand_off += (size_t)v.ncols * v.nrows * v.cell_cap;
+        max_cells = std::max(max_cells, v.ncols * v.nrows);
+        // octree roots (:545-547)
+        v.nini = (int)std::round((float)(v.max_bx - kBorder) / (float)(v.max_by - kBorder));
+        if (v.nini < 1) return fail(ORBGPU_ERR_UNSUPPORTED, "image aspect gives zero initial octree nodes");
+        v.hx = (float)(v.max_bx - kBorder) / v.nini;
+        v.ocap = std::max(v.nfeat + 3, 4 * v.nini);
+        v.out_offset = out_off;
+        out_off += v.ocap;
+        ncap = std::max(ncap, std::max(v.ocap, v.nini));
+        // resize tables
+        if (l > 0) {
+            const LevelGeom& p = g.lv[l - 1];
+            std::vector<int2> xt, yt;
+            build_resize_tables(p.w, p.h, v.w, v.h, xt, yt);
+            v.simd_end = vresize_simd_end(v.w);
+            v.xtab_offset = (int)xtab.size();
+            v.ytab_offset = (int)ytab.size();
+            xtab.insert(xtab.end(), xt.begin(), xt.end());
+            ytab.insert(ytab.end(), yt.begin(), yt.end());
+            if (p.w + 16 > pyr_max_src_width())
+                return fail(ORBGPU_ERR_UNSUPPORTED, "source row wider than the resize LDS staging");
+            const int rows = pyr_rows_per_block();
+            for (int dy0 = 0; dy0 < v.h; dy0 += rows) {
+                const int dyl = std::min(dy0 + rows, v.h) - 1;
+                if ((yt[dyl].x >> 16) - (yt[dy0].x & 0xFFFF) + 1 > rows + 3)
+                    return fail(ORBGPU_ERR_UNSUPPORTED, "scale factor too large for the resize row band");
+            }
+        }
+    }
+    g.total_cells = cell_base;
+    g.cand_frame = cand_off;
+    g.slots_frame = out_off;
+    g.max_cells_level = max_cells;
+    e->pyr_bytes = pyr_off;
+    e->max_kps = out_off;
+    e->ncap = (int)round_up((size_t)ncap, 16);
+    if (e->ncap > 4096) return fail(ORBGPU_ERR_UNSUPPORTED, "more than 4092 features per level");
+    // keys in LDS up to a 64 KiB workgroup budget; larger levels use HBM scratch
+    const size_t fixed = octree_lds_bytes(g, 0, e->ncap);
+    const long budget = 65536 - (long)fixed - 64;
+    e->kcap = budget > 0 ? (int)(budget / 6) & ~63 : 0;
+    return ORBGPU_OK;
+}
+
+int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_step, size_t frame_step,
+              orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap, hipStream_t s) {
+    const Geom& g = e->g;
+    for (int l = 1; l < g.nlevels; ++l) {
+        const LevelGeom& p = g.lv[l - 1];
+        const LevelGeom& v = g.lv[l];
+        const uint8_t* src = l == 1 ? imgs : e->d_pyr + p.offset;
+        const int src_pitch = l == 1 ? (int)row_step : p.pitch;
+        const size_t src_frame = l == 1 ? frame_step : p.frame_bytes;
+        ORB_HIP(launch_pyramid_level(src, src_pitch, src_frame, p.w, p.h, e->d_pyr + v.offset, v.pitch, v.frame_bytes,
+                                     v.w, v.h, v.simd_end, e->d_xtab + v.xtab_offset, e->d_ytab + v.ytab_offset,
+                                     batch, s));
+    }
+    ORB_HIP(launch_fast_cells(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_cand, e->d_cell_counts, e->d_err, s));
+    ORB_HIP(launch_octree(g, batch, e->d_cand, e->d_cell_counts, e->d_gkeys, e->d_gknode, e->d_oct_out,
+                          e->d_oct_count, e->d_err, e->kcap, e->ncap, e->d_trace, s));
+    ORB_HIP(launch_describe(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_oct_out, e->d_oct_count, kps,
+                            desc, counts, kp_cap, s));
+    e->last_img = imgs;
+    e->last_row = row_step;
+    e->last_frame = frame_step;
+    e->last_batch = batch;
+    return ORBGPU_OK;
+}
+
+int collect_errors(orbgpu_extractor* e, hipStream_t s) {
+    ORB_HIP(hipStreamSynchronize(s));
+    int err = 0;
+    ORB_HIP(hipMemcpy(&err, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (err) {
+        ORB_HIP(hipMemset(e->d_err, 0, sizeof(int)));
+        std::string m = "kernel capacity overflow:";
+        if (err & kErrCellCap) m += " FAST-cell";
+        if (err & kErrNodeCap) m += " octree-nodes";
+        if (err & kErrKeyCap) m += " octree-keys";
+        if (err & kErrMatchCap) m += " matcher-level0";
+        if (err & kErrSeqCap) m += " octree-seq";
+        return fail(ORBGPU_ERR_CAPACITY, m);
+    }
+    return ORBGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* orbgpu_last_error(void) { return g_err.c_str(); }
+
+int orbgpu_device_arch(char* buf, int buflen) {
+    int dev = 0, n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(ORBGPU_ERR_NO_DEVICE, "no HIP device visible");
+    ORB_HIP(hipGetDevice(&dev));
+    hipDeviceProp_t p;
+    ORB_HIP(hipGetDeviceProperties(&p, dev));
+    if (buf && buflen > 0) {
+        std::strncpy(buf, p.gcnArchName, (size_t)buflen - 1);
+        buf[buflen - 1] = 0;
+    }
+    return ORBGPU_OK;
+}
+
+int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int ini_th, int min_th, int width,
+                            int height, int max_batch, orbgpu_extractor** out) {
+    if (!out) return fail(ORBGPU_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    if (nfeatures <= 0 || nlevels <= 0 || nlevels > kMaxLevels || !(scale_factor > 1.f) || width <= 0 ||
+        height <= 0 || max_batch <= 0)
+        return fail(ORBGPU_ERR_ARG, "invalid extractor parameters");
+    int rc = check_device();
+    if (rc) return rc;
+    orbgpu_extractor* e = new orbgpu_extractor();
+    e->nfeatures = nfeatures;
+    e->scale_factor = scale_factor;
+    e->nlevels = nlevels;
+    e->ini_th = ini_th;
+    e->min_th = min_th;
+    e->W = width;
+    e->H = height;
+    e->max_batch = max_batch;
+    std::vector<int2> xtab, ytab;
+    rc = build_geometry(e, xtab, ytab);
+    if (rc) { delete e; return rc; }
+    const Geom& g = e->g;
+    const size_t B = (size_t)max_batch;
+    e->img_pitch = round_up((size_t)width, 16);
+    if ((rc = dalloc(&e->d_pyr, e->pyr_bytes)) || (rc = dalloc(&e->d_xtab, xtab.size())) ||
+        (rc = dalloc(&e->d_ytab, ytab.size())) || (rc = dalloc(&e->d_cand, g.cand_frame * B)) ||
+        (rc = dalloc(&e->d_cell_counts, (size_t)g.total_cells * B)) || (rc = dalloc(&e->d_gkeys, g.cand_frame * B)) ||
+        (rc = dalloc(&e->d_gknode, g.cand_frame * B)) || (rc = dalloc(&e->d_oct_out, (size_t)g.slots_frame * B)) ||
+        (rc = dalloc(&e->d_oct_count, (size_t)g.nlevels * B)) || (rc = dalloc(&e->d_err, 1)) ||
+        (rc = dalloc(&e->d_img, e->img_pitch * height)) || (rc = dalloc(&e->d_kps1, (size_t)e->max_kps)) ||
+        (rc = dalloc(&e->d_desc1, (size_t)e->max_kps * 32)) || (rc = dalloc(&e->d_count1, 1))) {
+        delete e;
+        return rc;
+    }
+    if (hipMemcpy(e->d_xtab, xtab.data(), xtab.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(e->d_ytab, ytab.data(), ytab.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(e->d_err, 0, sizeof(int)) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete e;
+        return fail(ORBGPU_ERR_HIP, "buffer initialisation failed");
+    }
+    *out = e;
+    return ORBGPU_OK;
+}
+
+int orbgpu_extractor_destroy(orbgpu_extractor* e) {
+    delete e;
+    return ORBGPU_OK;
+}
+
+int orbgpu_extractor_get_info(const orbgpu_extractor* e, orbgpu_extractor_info* info) {
+    if (!e || !info) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    std::memset(info, 0, sizeof(*info));
+    info->nlevels = e->nlevels;
+    info->width = e->W;
+    info->height = e->H;
+    info->max_batch = e->max_batch;
+    info->max_keypoints = e->max_kps;
+    for (int l = 0; l < e->nlevels && l < 32; ++l) {
+        info->level_width[l] = e->g.lv[l].w;
+        info->level_height[l] = e->g.lv[l].h;
+        info->features_per_level[l] = e->g.lv[l].nfeat;
+    }
+    return ORBGPU_OK;
+}
+
+int orbgpu_extractor_get_scales(const orbgpu_extractor* e, float* s, float* is, float* s2, float* is2) {
+    if (!e) return fail(ORBGPU_ERR_ARG, "NULL extractor");
+    for (int l = 0; l < e->nlevels; ++l) {
+        if (s) s[l] = e->scale[l];
+        if (is) is[l] = e->inv_scale[l];
+        if (s2) s2[l] = e->sigma2[l];
+        if (is2) is2[l] = e->inv_sigma2[l];
+    }
+    return ORBGPU_OK;
+}
+
+int orbgpu_extract_batch_device(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_step,
+                                size_t frame_step, orbgpu_keypoint* kps, uint8_t* desc, int* counts,
+                                int kp_cap, void* stream) {
+    if (!e || !imgs || !kps || !desc || !counts) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    if (batch <= 0 || batch > e->max_batch) return fail(ORBGPU_ERR_ARG, "batch outside [1, max_batch]");
+    if (kp_cap < e->max_kps) return fail(ORBGPU_ERR_CAPACITY, "kp_capacity < max_keypoints");
+    if (row_step < (size_t)e->W || row_step % 16 || ((uintptr_t)imgs & 15) || (batch > 1 && frame_step % 16) ||
+        (batch > 1 && frame_step < row_step * e->H))
+        return fail(ORBGPU_ERR_ARG, "images must be 16-byte aligned with row_step and frame_step multiples of 16");
+    return run_batch(e, imgs, batch, row_step, frame_step, kps, desc, counts, kp_cap, (hipStream_t)stream);
+}
+
+int orbgpu_extractor_sync(orbgpu_extractor* e, void* stream) {
+    if (!e) return fail(ORBGPU_ERR_ARG, "NULL extractor");
+    return collect_errors(e, (hipStream_t)stream);
+}
+
+int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int height, size_t step,
+                   orbgpu_keypoint* keypoints, uint8_t* descriptors, int capacity, int* n) {
+    if (!e || !n) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    if (!image || width <= 0 || height <= 0) {  // ORBextractor.cpp:1056
+        *n = -1;
+        return ORBGPU_OK;
+    }
+    if (width != e->W || height != e->H) return fail(ORBGPU_ERR_ARG, "image size differs from the extractor geometry");
+    if (step < (size_t)width) return fail(ORBGPU_ERR_ARG, "step < width");
+    hipStream_t s = e->stream;
+    ORB_HIP(hipMemcpy2DAsync(e->d_img, e->img_pitch, image, step, width, height, hipMemcpyHostToDevice, s));
+    int rc = run_batch(e, e->d_img, 1, e->img_pitch, e->img_pitch * height, e->d_kps1, e->d_desc1, e->d_count1,
+                       e->max_kps, s);
+    if (rc) return rc;
+    int count = 0;
+    ORB_HIP(hipMemcpyAsync(&count, e->d_count1, sizeof(int), hipMemcpyDeviceToHost, s));
+    rc = collect_errors(e, s);
+    if (rc) return rc;
+    if (count > capacity) return fail(ORBGPU_ERR_CAPACITY, "keypoint capacity too small");
+    if (count > 0) {
+        if (keypoints) ORB_HIP(hipMemcpy(keypoints, e->d_kps1, (size_t)count * sizeof(orbgpu_keypoint), hipMemcpyDeviceToHost));
+        if (descriptors) ORB_HIP(hipMemcpy(descriptors, e->d_desc1, (size_t)count * 32, hipMemcpyDeviceToHost));
+    }
+    *n = count;
+    return ORBGPU_OK;
+}
+
+int orbgpu_extractor_copy_level(orbgpu_extractor* e, int frame, int level, uint8_t* dst, size_t dst_step) {
+    if (!e || !dst) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    if (!e->last_img || frame < 0 || frame >= e->last_batch || level < 0 || level >= e->nlevels)
+        return fail(ORBGPU_ERR_ARG, "no such frame/level in the last extraction");
+    const LevelGeom& v = e->g.lv[level];
+    if (dst_step < (size_t)v.w) return fail(ORBGPU_ERR_ARG, "dst_step < level width");
+    const uint8_t* src = level == 0 ? e->last_img + (size_t)frame * e->last_frame
+                                    : e->d_pyr + v.offset + (size_t)frame * v.frame_bytes;
+    const size_t pitch = level == 0 ? e->last_row : (size_t)v.pitch;
+    ORB_HIP(hipStreamSynchronize(e->stream));
+    ORB_HIP(hipMemcpy2D(dst, dst_step, src, pitch, v.w, v.h, hipMemcpyDeviceToHost));
+    return ORBGPU_OK;
+}
+
+int orbgpu_hamming_pairs_device(const uint8_t* a, const uint8_t* b, int n, int* dist, void* stream) {
+    if (n < 0 || (n > 0 && (!a || !b || !dist))) return fail(ORBGPU_ERR_ARG, "invalid argument");
+    if (((uintptr_t)a | (uintptr_t)b) & 31) return fail(ORBGPU_ERR_ARG, "descriptors must be 32-byte aligned");
+    ORB_HIP(launch_hamming_pairs(a, b, n, dist, (hipStream_t)stream));
+    return ORBGPU_OK;
+}
+
+static int g_match_err_init = 0;
+static int* g_match_err = nullptr;
+
+static int match_err_word(int** p) {
+    if (!g_match_err_init) {
+        ORB_HIP(hipMalloc((void**)&g_match_err, sizeof(int)));
+        ORB_HIP(hipMemset(g_match_err, 0, sizeof(int)));
+        g_match_err_init = 1;
+    }
+    *p = g_match_err;
+    return ORBGPU_OK;
+}
+
+int orbgpu_search_for_initialization_batch_device(int batch, int img_w, int img_h, const orbgpu_keypoint* kps1,
+                                                  const uint8_t* desc1, const int* n1, size_t stride1,
+                                                  const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2,
+                                                  size_t stride2, float* prev_xy, int window, float nnratio,
+                                                  int flags, int* matches12, int* nmatches, void* stream) {
+    if (batch <= 0 || !kps1 || !kps2 || !desc1 || !desc2 || !n1 || !n2 || !matches12 || !nmatches || img_w <= 0 ||
+        img_h <= 0)
+        return fail(ORBGPU_ERR_ARG, "invalid argument");
+    int* err = nullptr;
+    int rc = match_err_word(&err);
+    if (rc) return rc;
+    ORB_HIP(launch_match_init(batch, img_w, img_h, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy,
+                              window, nnratio, flags, matches12, nmatches, err, (hipStream_t)stream));
+    return ORBGPU_OK;
+}
+
+int orbgpu_search_for_initialization(int img_w, int img_h, const orbgpu_keypoint* kps1, const uint8_t* desc1,
+                                     int n1, const orbgpu_keypoint* kps2, const uint8_t* desc2, int n2,
+                                     float* prev_xy, int window, float nnratio, int flags, int* matches12,
+                                     int* nmatches) {
+    if (n1 < 0 || n2 < 0 || !matches12 || !nmatches) return fail(ORBGPU_ERR_ARG, "invalid argument");
+    int rc = check_device();
+    if (rc) return rc;
+    const size_t n1c = std::max(n1, 1), n2c = std::max(n2, 1);
+    orbgpu_keypoint *dk1 = nullptr, *dk2 = nullptr;
+    uint8_t *dd1 = nullptr, *dd2 = nullptr;
+    int *dn = nullptr, *dm = nullptr;
+    float* dp = nullptr;
+    auto cleanup = [&]() {
+        void* ptrs[] = {dk1, dk2, dd1, dd2, dn, dm, dp};
+        for (void* p : ptrs)
+            if (p) (void)hipFree(p);
+    };
+    if (hipMalloc((void**)&dk1, n1c * sizeof(orbgpu_keypoint)) != hipSuccess ||
+        hipMalloc((void**)&dk2, n2c * sizeof(orbgpu_keypoint)) != hipSuccess ||
+        hipMalloc((void**)&dd1, n1c * 32) != hipSuccess || hipMalloc((void**)&dd2, n2c * 32) != hipSuccess ||
+        hipMalloc((void**)&dn, 3 * sizeof(int)) != hipSuccess || hipMalloc((void**)&dm, n1c * sizeof(int)) != hipSuccess ||
+        (prev_xy && hipMalloc((void**)&dp, n1c * 2 * sizeof(float)) != hipSuccess)) {
+        cleanup();
+        return fail(ORBGPU_ERR_HIP, "device allocation failed");
+    }
+    const int ns[2] = {n1, n2};
+    bool ok = hipMemcpy(dk1, kps1, (size_t)n1 * sizeof(orbgpu_keypoint), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(dk2, kps2, (size_t)n2 * sizeof(orbgpu_keypoint), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(dd1, desc1, (size_t)n1 * 32, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(dd2, desc2, (size_t)n2 * 32, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(dn, ns, 2 * sizeof(int), hipMemcpyHostToDevice) == hipSuccess &&
+              (!prev_xy || hipMemcpy(dp, prev_xy, (size_t)n1 * 2 * sizeof(float), hipMemcpyHostToDevice) == hipSuccess);
+    if (!ok) { cleanup(); return fail(ORBGPU_ERR_HIP, "upload failed"); }
+    rc = orbgpu_search_for_initialization_batch_device(1, img_w, img_h, dk1, dd1, dn, n1c, dk2, dd2, dn + 1, n2c, dp,
+                                                       window, nnratio, flags, dm, dn + 2, nullptr);
+    if (rc) { cleanup(); return rc; }
+    int err = 0;
+    ok = hipDeviceSynchronize() == hipSuccess &&
+         hipMemcpy(matches12, dm, (size_t)n1 * sizeof(int), hipMemcpyDeviceToHost) == hipSuccess &&
+         hipMemcpy(nmatches, dn + 2, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess &&
+         (!prev_xy || hipMemcpy(prev_xy, dp, (size_t)n1 * 2 * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess) &&
+         hipMemcpy(&err, g_match_err, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess;
+    cleanup();
+    if (!ok) return fail(ORBGPU_ERR_HIP, "matcher failed");
+    if (err) {
+        (void)hipMemset(g_match_err, 0, sizeof(int));
+        return fail(ORBGPU_ERR_CAPACITY, "matcher: more level-0 keypoints than the LDS capacity");
+    }
+    return ORBGPU_OK;
+}
+
+int orbgpu_debug_level_candidates(orbgpu_extractor* e, int frame, int level, int* xys, int cap) {
+    if (!e || frame < 0 || frame >= e->last_batch || level < 0 || level >= e->nlevels)
+        return fail(ORBGPU_ERR_ARG, "no such frame/level in the last extraction");
+    const Geom& g = e->g;
+    const LevelGeom& v = g.lv[level];
+    const int ncells = v.ncols * v.nrows;
+    std::vector<int> counts(ncells);
+    std::vector<uint32_t> slots((size_t)ncells * v.cell_cap);
+    ORB_HIP(hipStreamSynchronize(e->stream));
+    ORB_HIP(hipDeviceSynchronize());
+    ORB_HIP(hipMemcpy(counts.data(), e->d_cell_counts + (size_t)frame * g.total_cells + v.cell_base,
+                      ncells * sizeof(int), hipMemcpyDeviceToHost));
+    ORB_HIP(hipMemcpy(slots.data(), e->d_cand + (size_t)frame * g.cand_frame + v.cand_offset,
+                      slots.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    int n = 0;
+    for (int c = 0; c < ncells; ++c)
+        for (int k = 0; k < counts[c]; ++k, ++n)
+            if (n < cap && xys) {
+                const uint32_t key = slots[(size_t)c * v.cell_cap + k];
+                xys[3 * n] = key_x(key); xys[3 * n + 1] = key_y(key); xys[3 * n + 2] = key_s(key);
+            }
+    return n;
+}
+
+int orbgpu_debug_octree_trace(orbgpu_extractor* e, int enable, int* out, int cap) {
+    if (!e) return fail(ORBGPU_ERR_ARG, "NULL extractor");
+    const size_t n = (size_t)kMaxLevels * 512;
+    if (enable && !e->d_trace) {
+        ORB_HIP(hipMalloc((void**)&e->d_trace, n * sizeof(int)));
+        ORB_HIP(hipMemset(e->d_trace, 0, n * sizeof(int)));
+    }
+    if (out && e->d_trace) {
+        ORB_HIP(hipDeviceSynchronize());
+        ORB_HIP(hipMemcpy(out, e->d_trace, std::min(n, (size_t)cap) * sizeof(int), hipMemcpyDeviceToHost));
+    }
+    return ORBGPU_OK;
+}
+
+int orbgpu_debug_level_octree(orbgpu_extractor* e, int frame, int level, int* xys, int cap) {
+    if (!e || frame < 0 || frame >= e->last_batch || level < 0 || level >= e->nlevels)
+        return fail(ORBGPU_ERR_ARG, "no such frame/level in the last extraction");
+    const Geom& g = e->g;
+    const LevelGeom& v = g.lv[level];
+    int n = 0;
+    ORB_HIP(hipDeviceSynchronize());
+    ORB_HIP(hipMemcpy(&n, e->d_oct_count + (size_t)frame * g.nlevels + level, sizeof(int), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> keys(std::max(n, 1));
+    ORB_HIP(hipMemcpy(keys.data(), e->d_oct_out + (size_t)frame * g.slots_frame + v.out_offset,
+                      (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n && i < cap && xys; ++i) {
+        xys[3 * i] = key_x(keys[i]); xys[3 * i + 1] = key_y(keys[i]); xys[3 * i + 2] = key_s(keys[i]);
+    }
+    return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,68 @@
+// orbgpu_internal.h -- geometry and buffer layout shared by the host driver
+// (orbgpu.cpp) and the HIP kernels.  Everything here is precomputed once per
+// extractor on the host (it depends only on the frame size and the
+// ORBextractor parameters) and handed to kernels by value.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace orbgpu {
+
+constexpr int kMaxLevels = 16;
+constexpr int kEdge = 19;              // EDGE_THRESHOLD (ORBextractor.cpp:76)
+constexpr int kBorder = kEdge - 3;     // minBorderX/Y (ORBextractor.cpp:781)
+constexpr int kMaxWin = 72;            // FAST cell window <= (wCell+6) x (hCell+6)
+constexpr int kPatchR = 21;            // raw patch radius for blur+rBRIEF
+constexpr int kPatch = 2 * kPatchR + 1;  // 43
+constexpr int kBlurR = 18;             // blurred patch radius (13*sqrt2 rounded)
+constexpr int kBlur = 2 * kBlurR + 1;    // 37
+
+// Candidate key packing (FAST output, octree input/output):
+//   bits 0..10  x relative to minBorderX (level x - 16)
+//   bits 11..21 y relative to minBorderY
+//   bits 22..29 FAST score (cornerScore, <= 254)
+__host__ __device__ inline uint32_t pack_key(int x, int y, int s) {
+    return (uint32_t)x | ((uint32_t)y << 11) | ((uint32_t)s << 22);
+}
+__host__ __device__ inline int key_x(uint32_t k) { return (int)(k & 0x7FF); }
+__host__ __device__ inline int key_y(uint32_t k) { return (int)((k >> 11) & 0x7FF); }
+__host__ __device__ inline int key_s(uint32_t k) { return (int)(k >> 22); }
+
+struct LevelGeom {
+    int w, h;                 // level size (ComputePyramid, ORBextractor.cpp:1128)
+    int pitch;                // row pitch in the pyramid buffer (levels >= 1)
+    int simd_end;             // resize: VResizeLinearVec_32s8u coverage
+    size_t frame_bytes;       // bytes per frame of this level in the pyramid buffer
+    size_t offset;            // byte offset of this level's region (levels >= 1)
+    float scale;              // mvScaleFactor[l]
+    int size_i;               // (int)(PATCH_SIZE * mvScaleFactor[l])
+    int nfeat;                // mnFeaturesPerLevel[l]
+    // FAST cells (ORBextractor.cpp:781-814)
+    int max_bx, max_by;       // maxBorderX/Y
+    int ncols, nrows, wcell, hcell;
+    int cell_base;            // first cell index of this level within a frame
+    int cell_cap;             // candidate slots per cell
+    size_t cand_offset;       // u32 offset of this level's candidate slots in a frame
+    // DistributeOctTree roots (ORBextractor.cpp:545-565)
+    int nini;
+    float hx;
+    int ocap;                 // output slots (max list size)
+    int out_offset;           // slot offset of this level within a frame
+    // resize tables (levels >= 1)
+    int xtab_offset, ytab_offset;
+};
+
+struct Geom {
+    int nlevels;
+    int width, height;
+    int ini_th, min_th;
+    int total_cells;          // cells per frame over all levels
+    size_t cand_frame;        // u32 candidate slots per frame
+    int slots_frame;          // octree output slots per frame (= sum ocap)
+    int max_cells_level;
+    LevelGeom lv[kMaxLevels];
+};
+
+}  // namespace orbgpu

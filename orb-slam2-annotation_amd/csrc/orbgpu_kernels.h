@@ -1,0 +1,48 @@
+// orbgpu_kernels.h -- host-side launchers of the HIP kernels (one per stage).
+#pragma once
+
+#include "orbgpu_internal.h"
+
+struct orbgpu_keypoint;
+
+namespace orbgpu {
+
+int pyr_max_src_width();
+int pyr_rows_per_block();
+hipError_t launch_pyramid_level(const uint8_t* src, int src_pitch, size_t src_frame, int sw, int sh,
+                                uint8_t* dst, int dst_pitch, size_t dst_frame, int dw, int dh,
+                                int simd_end, const int2* xtab, const int2* ytab, int batch,
+                                hipStream_t stream);
+
+hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
+                             const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err,
+                             hipStream_t stream);
+
+size_t octree_lds_bytes(const Geom& g, int kcap, int ncap);
+hipError_t launch_octree(const Geom& g, int batch, const uint32_t* cand, const int* cell_counts,
+                         uint32_t* gkeys, uint16_t* gknode, uint32_t* oct_out, int* oct_count,
+                         int* err, int kcap, int ncap, int* trace, hipStream_t stream);
+
+hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
+                           const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
+                           orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
+                           hipStream_t stream);
+
+hipError_t launch_match_init(int batch, int img_w, int img_h,
+                             const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,
+                             const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2, size_t stride2,
+                             float* prev_xy, int window, float nnratio, int flags,
+                             int* matches12, int* nmatches, int* err, hipStream_t stream);
+
+hipError_t launch_hamming_pairs(const uint8_t* a, const uint8_t* b, int n, int* dist, hipStream_t stream);
+
+// error bits written to the device error word
+enum : int {
+    kErrCellCap = 1,     // FAST cell candidates overflowed cell_cap
+    kErrNodeCap = 2,     // octree list exceeded ncap / ocap
+    kErrKeyCap = 4,      // octree key count exceeded the scratch region
+    kErrMatchCap = 8,    // matcher: level-0 keypoints exceed LDS capacity
+    kErrSeqCap = 16,     // octree creation sequence overflow
+};
+
+}  // namespace orbgpu

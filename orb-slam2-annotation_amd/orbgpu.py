@@ -1,0 +1,239 @@
+"""Python binding of liborbgpu.so (the MI355X ORB front-end) via ctypes.
+
+This is a thin host-side mirror of the reference's class surface for tests
+and the benchmark:
+
+* ``Extractor``  ~ ORB_SLAM2::ORBextractor  (ORBextractor.h:47-111):
+  ``extract(img)`` is ``operator()`` for one host image; ``extract_batch``
+  runs B HBM-resident frames in one launch sequence.
+* ``search_for_initialization`` / ``search_for_initialization_batch`` ~
+  ORBmatcher::SearchForInitialization (ORBmatcher.cpp:474-590).
+
+No CPU fallback exists: if the shared library is missing, or the process has
+no gfx950 device, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "liborbgpu.so"
+_LIB = None
+
+OK, ERR_ARG, ERR_HIP, ERR_CAPACITY, ERR_UNSUPPORTED, ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5
+MATCH_CHECK_ORI = 1
+MATCH_ANNOTATED_HISTO = 2
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+
+class OrbGpuError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what} failed ({code}): {last_error()}")
+        self.code = code
+
+
+class _Info(ctypes.Structure):
+    _fields_ = [("nlevels", ctypes.c_int), ("width", ctypes.c_int), ("height", ctypes.c_int),
+                ("max_batch", ctypes.c_int), ("max_keypoints", ctypes.c_int),
+                ("level_width", ctypes.c_int * 32), ("level_height", ctypes.c_int * 32),
+                ("features_per_level", ctypes.c_int * 32)]
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"HIP extension not built: {LIB_PATH} (run __graft_entry__.build())")
+        L = ctypes.CDLL(str(LIB_PATH))
+        vp, i, f, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+        L.orbgpu_last_error.restype = ctypes.c_char_p
+        L.orbgpu_device_arch.argtypes = [ctypes.c_char_p, i]
+        L.orbgpu_extractor_create.argtypes = [i, f, i, i, i, i, i, i, ctypes.POINTER(vp)]
+        L.orbgpu_extractor_destroy.argtypes = [vp]
+        L.orbgpu_extractor_get_info.argtypes = [vp, ctypes.POINTER(_Info)]
+        L.orbgpu_extractor_get_scales.argtypes = [vp, vp, vp, vp, vp]
+        L.orbgpu_extract.argtypes = [vp, vp, i, i, sz, vp, vp, i, ctypes.POINTER(i)]
+        L.orbgpu_extract_batch_device.argtypes = [vp, vp, i, sz, sz, vp, vp, vp, i, vp]
+        L.orbgpu_extractor_sync.argtypes = [vp, vp]
+        L.orbgpu_extractor_copy_level.argtypes = [vp, i, i, vp, sz]
+        L.orbgpu_hamming_pairs_device.argtypes = [vp, vp, i, vp, vp]
+        L.orbgpu_search_for_initialization_batch_device.argtypes = [
+            i, i, i, vp, vp, vp, sz, vp, vp, vp, sz, vp, i, f, i, vp, vp, vp]
+        L.orbgpu_debug_level_candidates.argtypes = [vp, i, i, vp, i]
+        L.orbgpu_debug_level_octree.argtypes = [vp, i, i, vp, i]
+        L.orbgpu_debug_octree_trace.argtypes = [vp, i, vp, i]
+        L.orbgpu_search_for_initialization.argtypes = [i, i, vp, vp, i, vp, vp, i, vp, i, f, i, vp,
+                                                       ctypes.POINTER(i)]
+        _LIB = L
+    return _LIB
+
+
+def last_error() -> str:
+    return lib().orbgpu_last_error().decode(errors="replace")
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != OK:
+        raise OrbGpuError(rc, what)
+
+
+def device_arch() -> str:
+    buf = ctypes.create_string_buffer(64)
+    _check(lib().orbgpu_device_arch(buf, 64), "orbgpu_device_arch")
+    return buf.value.decode()
+
+
+def _ptr(a) -> int:
+    """data pointer of a numpy array or a torch tensor"""
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    return a.ctypes.data
+
+
+def _stream_ptr(stream) -> int | None:
+    if stream is None:
+        return None
+    return getattr(stream, "cuda_stream", stream)
+
+
+class Extractor:
+    """ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST) for
+    frames of a fixed width x height, batched up to ``max_batch`` frames."""
+
+    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7,
+                 width=640, height=480, max_batch=1):
+        h = ctypes.c_void_p()
+        _check(lib().orbgpu_extractor_create(nfeatures, scale_factor, nlevels, ini_th, min_th,
+                                             width, height, max_batch, ctypes.byref(h)),
+               "orbgpu_extractor_create")
+        self.h = h
+        info = _Info()
+        _check(lib().orbgpu_extractor_get_info(self.h, ctypes.byref(info)), "get_info")
+        self.nlevels = info.nlevels
+        self.width, self.height = info.width, info.height
+        self.max_batch = info.max_batch
+        self.max_keypoints = info.max_keypoints
+        self.level_sizes = [(info.level_width[l], info.level_height[l]) for l in range(self.nlevels)]
+        self.features_per_level = [info.features_per_level[l] for l in range(self.nlevels)]
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().orbgpu_extractor_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def scale_factors(self):
+        arrs = [np.zeros(self.nlevels, np.float32) for _ in range(4)]
+        _check(lib().orbgpu_extractor_get_scales(self.h, *[a.ctypes.data for a in arrs]), "get_scales")
+        return arrs
+
+    def extract(self, img: np.ndarray):
+        """operator()(image) for one host image -> (keypoints, descriptors)."""
+        img = np.ascontiguousarray(img, np.uint8)
+        cap = self.max_keypoints
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = ctypes.c_int()
+        _check(lib().orbgpu_extract(self.h, img.ctypes.data, img.shape[1], img.shape[0], img.strides[0],
+                                    kps.ctypes.data, desc.ctypes.data, cap, ctypes.byref(n)), "orbgpu_extract")
+        if n.value < 0:
+            return None
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def extract_batch(self, images, kps, desc, counts, stream=None, row_step=None, frame_step=None):
+        """Device path.  images: uint8 (B, H, pitch) tensor on the GPU;
+        kps: (B, cap, 7) float32/int32 view of orbgpu_keypoint (28 B each);
+        desc: (B, cap, 32) uint8; counts: (B,) int32.  Asynchronous."""
+        B = images.shape[0]
+        rs = row_step if row_step is not None else images.stride(1) * images.element_size()
+        fs = frame_step if frame_step is not None else images.stride(0) * images.element_size()
+        cap = desc.shape[1]
+        _check(lib().orbgpu_extract_batch_device(self.h, _ptr(images), B, rs, fs, _ptr(kps), _ptr(desc),
+                                                 _ptr(counts), cap, _stream_ptr(stream)),
+               "orbgpu_extract_batch_device")
+
+    def sync(self, stream=None):
+        _check(lib().orbgpu_extractor_sync(self.h, _stream_ptr(stream)), "orbgpu_extractor_sync")
+
+    def _debug_xys(self, fn, level: int, frame: int) -> np.ndarray:
+        n = fn(self.h, frame, level, None, 0)
+        if n < 0:
+            raise OrbGpuError(n, fn.__name__)
+        out = np.zeros((max(n, 1), 3), np.int32)
+        fn(self.h, frame, level, out.ctypes.data, n)
+        return out[:n]
+
+    def candidates(self, level: int, frame: int = 0) -> np.ndarray:
+        """FAST candidates (x, y, score) of the last extraction, oracle order."""
+        return self._debug_xys(lib().orbgpu_debug_level_candidates, level, frame)
+
+    def octree(self, level: int, frame: int = 0) -> np.ndarray:
+        """DistributeOctTree output (x, y, score) in list order."""
+        return self._debug_xys(lib().orbgpu_debug_level_octree, level, frame)
+
+    def enable_octree_trace(self):
+        _check(lib().orbgpu_debug_octree_trace(self.h, 1, None, 0), "octree_trace")
+
+    def octree_trace(self):
+        out = np.zeros(16 * 512, np.int32)
+        _check(lib().orbgpu_debug_octree_trace(self.h, 0, out.ctypes.data, out.size), "octree_trace")
+        res = []
+        for l in range(self.nlevels):
+            t = out[l * 512:(l + 1) * 512]
+            res.append(t[2:2 + 8 * t[0]].reshape(-1, 8))
+        return res
+
+    def level(self, level: int, frame: int = 0) -> np.ndarray:
+        """mvImagePyramid[level] of `frame` of the last extraction."""
+        w, h = self.level_sizes[level]
+        out = np.zeros((h, w), np.uint8)
+        _check(lib().orbgpu_extractor_copy_level(self.h, frame, level, out.ctypes.data, w), "copy_level")
+        return out
+
+
+def keypoints_from_raw(raw: np.ndarray) -> np.ndarray:
+    """View a (N, 28) uint8 / (N, 7) 4-byte array as KP_DTYPE records."""
+    return np.ascontiguousarray(raw).view(np.uint8).reshape(-1, 28).view(KP_DTYPE).reshape(-1)
+
+
+def search_for_initialization(kps1, desc1, kps2, desc2, img_w, img_h, prev_xy=None, window=100,
+                              nnratio=0.9, check_ori=True, annotated_histo=False):
+    """Host form: returns (nmatches, matches12, prev_xy_updated)."""
+    kps1 = np.ascontiguousarray(kps1, KP_DTYPE)
+    kps2 = np.ascontiguousarray(kps2, KP_DTYPE)
+    desc1 = np.ascontiguousarray(desc1, np.uint8)
+    desc2 = np.ascontiguousarray(desc2, np.uint8)
+    if prev_xy is None:
+        prev_xy = np.stack([kps1["x"], kps1["y"]], axis=1)
+    prev = np.ascontiguousarray(prev_xy, np.float32).copy()
+    m12 = np.full(max(len(kps1), 1), -1, np.int32)
+    n = ctypes.c_int()
+    flags = (MATCH_CHECK_ORI if check_ori else 0) | (MATCH_ANNOTATED_HISTO if annotated_histo else 0)
+    _check(lib().orbgpu_search_for_initialization(img_w, img_h, kps1.ctypes.data, desc1.ctypes.data, len(kps1),
+                                                  kps2.ctypes.data, desc2.ctypes.data, len(kps2),
+                                                  prev.ctypes.data, window, nnratio, flags,
+                                                  m12.ctypes.data, ctypes.byref(n)),
+           "orbgpu_search_for_initialization")
+    return n.value, m12[:len(kps1)], prev
+
+
+def search_for_initialization_batch(img_w, img_h, kps1, desc1, n1, kps2, desc2, n2, matches12, nmatches,
+                                    prev_xy=None, window=100, nnratio=0.9, flags=MATCH_CHECK_ORI, stream=None):
+    """Device form over B pairs (tensors on the GPU, see include/orbgpu.h)."""
+    B = n2.shape[0]
+    _check(lib().orbgpu_search_for_initialization_batch_device(
+        B, img_w, img_h, _ptr(kps1), _ptr(desc1), _ptr(n1), desc1.shape[1], _ptr(kps2), _ptr(desc2), _ptr(n2),
+        desc2.shape[1], _ptr(prev_xy) if prev_xy is not None else None, window, nnratio, flags,
+        _ptr(matches12), _ptr(nmatches), _stream_ptr(stream)), "orbgpu_search_for_initialization_batch_device")
+
+
+def hamming_pairs(a, b, out, stream=None):
+    """DescriptorDistance over n pairs of device descriptors (n, 32) uint8."""
+    _check(lib().orbgpu_hamming_pairs_device(_ptr(a), _ptr(b), a.shape[0], _ptr(out), _stream_ptr(stream)),
+           "orbgpu_hamming_pairs_device")

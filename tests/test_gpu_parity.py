@@ -1,0 +1,140 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle on
+the same seeded inputs.  Bit-exact for every integer/byte output and for the
+float keypoint fields (they are computed with identical IEEE operations)."""
+import numpy as np
+import pytest
+
+import orbref
+import synth
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _gpu():
+    import orbgpu
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return orbgpu
+
+
+def _assert_same_kps(kg, dg, kr, dr):
+    assert len(kg) == len(kr), (len(kg), len(kr))
+    for f in ("x", "y", "size", "angle", "response", "octave", "class_id"):
+        a, b = kg[f], kr[f]
+        bad = np.nonzero(a.view(np.uint32) != b.view(np.uint32))[0] if a.dtype.kind == "f" else np.nonzero(a != b)[0]
+        assert len(bad) == 0, f"field {f}: {len(bad)} mismatches, first {bad[:5]} gpu={a[bad[:5]]} ref={b[bad[:5]]}"
+    bad = np.nonzero((dg != dr).any(axis=1))[0]
+    assert len(bad) == 0, f"descriptors differ at {len(bad)} keypoints, first {bad[:5]}"
+
+
+def test_device_is_gfx950():
+    og = _gpu()
+    assert og.device_arch().startswith("gfx950")
+
+
+@pytest.mark.parametrize("frame", [0, 3])
+def test_pyramid_levels(mono_frames, frame):
+    og = _gpu()
+    ex = og.Extractor()
+    ref = orbref.Extractor()
+    img = mono_frames[frame]
+    ex.extract(img)
+    ref.extract(img)
+    for l in range(8):
+        a, b = ex.level(l), ref.level(l)
+        assert a.shape == b.shape
+        d = np.nonzero(a != b)
+        assert len(d[0]) == 0, f"level {l}: {len(d[0])} pixels differ, first {list(zip(*d))[:5]}"
+
+
+@pytest.mark.parametrize("frame", [0, 1, 2, 5])
+def test_extract_mono_640x480(mono_frames, frame):
+    og = _gpu()
+    ex = og.Extractor()
+    ref = orbref.Extractor()
+    kg, dg = ex.extract(mono_frames[frame])
+    kr, dr = ref.extract(mono_frames[frame])
+    _assert_same_kps(kg, dg, kr, dr)
+
+
+def test_extract_noise_and_flat():
+    og = _gpu()
+    ex = og.Extractor()
+    ref = orbref.Extractor()
+    for img in (synth.noise_image(), synth.flat_image()):
+        kg, dg = ex.extract(img)
+        kr, dr = ref.extract(img)
+        _assert_same_kps(kg, dg, kr, dr)
+
+
+def test_empty_image_untouched():
+    og = _gpu()
+    ex = og.Extractor()
+    assert ex.extract(np.zeros((0, 0), np.uint8)) is None
+
+
+@pytest.mark.parametrize("w,h,nf", [(1241, 376, 2000), (752, 480, 1200)])
+def test_extract_stereo_geometries(w, h, nf):
+    og = _gpu()
+    ex = og.Extractor(nfeatures=nf, width=w, height=h)
+    ref = orbref.Extractor(nfeatures=nf)
+    frames = synth.stereo_stream(1, w, h, seed=11)
+    for img in frames[0]:
+        kg, dg = ex.extract(img)
+        kr, dr = ref.extract(img)
+        _assert_same_kps(kg, dg, kr, dr)
+
+
+def test_batch_device_matches_single(mono_frames):
+    og = _gpu()
+    B = len(mono_frames)
+    ex = og.Extractor(max_batch=B)
+    imgs = torch.from_numpy(mono_frames).cuda()
+    cap = ex.max_keypoints
+    kps = torch.zeros((B, cap, 7), dtype=torch.float32, device="cuda")
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(B, dtype=torch.int32, device="cuda")
+    ex.extract_batch(imgs, kps, desc, counts)
+    ex.sync()
+    ref = orbref.Extractor()
+    kk, dd, cc = kps.cpu().numpy(), desc.cpu().numpy(), counts.cpu().numpy()
+    for b in range(B):
+        kr, dr = ref.extract(mono_frames[b])
+        kg = og.keypoints_from_raw(kk[b, :cc[b]])
+        _assert_same_kps(kg, dd[b, :cc[b]], kr, dr)
+
+
+@pytest.mark.parametrize("check_ori,annotated", [(True, False), (False, False), (True, True)])
+def test_search_for_initialization(mono_frames, check_ori, annotated):
+    og = _gpu()
+    ref = orbref.Extractor()
+    k1, d1 = ref.extract(mono_frames[0])
+    k2, d2 = ref.extract(mono_frames[1])
+    n_r, m_r, p_r = orbref.search_for_initialization(k1, d1, k2, d2, 640, 480, check_ori=check_ori,
+                                                     histo_bug=annotated)
+    n_g, m_g, p_g = og.search_for_initialization(k1, d1, k2, d2, 640, 480, check_ori=check_ori,
+                                                 annotated_histo=annotated)
+    assert n_g == n_r
+    np.testing.assert_array_equal(m_g, m_r)
+    np.testing.assert_array_equal(p_g.view(np.uint32), p_r.view(np.uint32))
+
+
+@pytest.mark.parametrize("w,h,nf", [(640, 480, 1000), (1241, 376, 2000), (752, 480, 1200)])
+def test_stages_candidates_and_octree(w, h, nf):
+    """Stage-level parity: FAST candidates and octree output per level."""
+    og = _gpu()
+    ex = og.Extractor(nfeatures=nf, width=w, height=h)
+    ref = orbref.Extractor(nfeatures=nf)
+    img = synth.mono_stream(1, w, h, seed=5)[0]
+    ex.extract(img)
+    ref.extract(img)
+    for l in range(8):
+        np.testing.assert_array_equal(ex.level(l), ref.level(l), err_msg=f"pyramid level {l}")
+        cg, cr = ex.candidates(l), ref.candidates(l)
+        assert cg.shape == cr.shape, f"level {l}: {len(cg)} vs {len(cr)} candidates"
+        np.testing.assert_array_equal(cg, cr, err_msg=f"candidates level {l}")
+        og_, or_ = ex.octree(l), ref.octree(l)
+        assert og_.shape == or_.shape, f"level {l}: octree {len(og_)} vs {len(or_)}"
+        np.testing.assert_array_equal(og_, or_, err_msg=f"octree level {l}")

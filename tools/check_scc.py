@@ -1,0 +1,57 @@
+"""Guard against a ROCm 7.2 (LLVM 22) gfx950 miscompile found in this repo.
+
+Pattern: a value loaded from LDS at a wave-uniform address is compared with
+a VALU `v_cmp_* vcc, ...`, and the select that consumes the comparison is
+emitted as a scalar `s_cselect_*`, which reads SCC -- a flag the v_cmp never
+wrote -- so the select takes a stale SCC from an earlier scalar op
+(reproducer: tools/scc_repro.hip).  This script scans device assembly
+(`hipcc -S --cuda-device-only`) and reports every s_cselect / s_cbranch_scc*
+whose nearest preceding definition of SCC-or-VCC in the same basic block is
+a VALU compare into VCC.  build() runs it over every kernel and fails the
+build on a hit.
+"""
+from __future__ import annotations
+
+import re
+import sys
+
+SCC_WRITERS = re.compile(
+    r"^\s*s_(cmp|cmpk|and|or|xor|andn2|orn2|nand|nor|xnor|add|addc|sub|subb|min|max|lshl|lshr|ashr|bfe|"
+    r"not|abs|bitcmp|absdiff|lshl\d_add|mul_hi|cselect_b|movk)_?")
+VCC_CMP = re.compile(r"^\s*v_cmp\w*_e32\s+vcc")
+CONSUMER = re.compile(r"^\s*(s_cselect_b(32|64)|s_cbranch_scc[01])\b")
+LABEL = re.compile(r"^\S+:")
+
+
+def scan(lines):
+    hits = []
+    for i, line in enumerate(lines):
+        if not CONSUMER.match(line):
+            continue
+        for j in range(i - 1, max(-1, i - 40), -1):
+            prev = lines[j]
+            if LABEL.match(prev):
+                break
+            if prev.lstrip().startswith(";"):
+                continue
+            if SCC_WRITERS.match(prev) and not prev.lstrip().startswith("s_cselect"):
+                break
+            if VCC_CMP.match(prev):
+                hits.append((i + 1, line.strip(), j + 1, prev.strip()))
+                break
+    return hits
+
+
+def main(paths) -> int:
+    bad = 0
+    for p in paths:
+        with open(p) as fh:
+            lines = fh.read().splitlines()
+        for ln, ins, pln, pins in scan(lines):
+            print(f"{p}:{ln}: '{ins}' consumes SCC but the flag was last computed by VALU '{pins}' (line {pln})")
+            bad += 1
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))
