@@ -99,6 +99,14 @@ int orbgpu_extract_batch_device(orbgpu_extractor* ex, const uint8_t* d_images, i
  * since the last call (ORBGPU_ERR_CAPACITY) -- never silently truncated. */
 int orbgpu_extractor_sync(orbgpu_extractor* ex, void* stream);
 
+/* Stage timing.  While enabled, every extraction records HIP events on its
+ * own stream around the four launch groups [pyramid (levels 1..L-1), FAST
+ * cells, octree, angle+blur+rBRIEF].  orbgpu_extractor_stage_times()
+ * synchronises and returns the summed milliseconds per group over all
+ * extractions since the last reset, and their count. */
+int orbgpu_extractor_profile(orbgpu_extractor* ex, int enable);
+int orbgpu_extractor_stage_times(orbgpu_extractor* ex, float* ms4, int* nbatches, int reset);
+
 /* mvImagePyramid[level] of frame `frame` of the last extraction, copied to
  * host (ORBextractor.h:85; read by Frame::ComputeStereoMatches). */
 int orbgpu_extractor_copy_level(orbgpu_extractor* ex, int frame, int level, uint8_t* dst,

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -140,6 +141,10 @@ struct orbgpu_extractor {
     uint8_t* d_desc1 = nullptr;
     int* d_count1 = nullptr;
     hipStream_t stream = nullptr;
+    // stage timing
+    bool profile = false;
+    std::vector<std::array<hipEvent_t, 5>> ev;
+    size_t ev_used = 0;
     // last extraction (for copy_level)
     const uint8_t* last_img = nullptr;
     size_t last_row = 0, last_frame = 0;
@@ -151,6 +156,8 @@ struct orbgpu_extractor {
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
         if (stream) (void)hipStreamDestroy(stream);
+        for (auto& a : ev)
+            for (hipEvent_t x : a) (void)hipEventDestroy(x);
     }
 };
 
@@ -272,6 +279,16 @@ int build_geometry(orbgpu_extractor* e, std::vector<int2>& xtab, std::vector<int
 int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_step, size_t frame_step,
               orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap, hipStream_t s) {
     const Geom& g = e->g;
+    hipEvent_t* evs = nullptr;
+    if (e->profile) {
+        if (e->ev_used == e->ev.size()) {
+            std::array<hipEvent_t, 5> a;
+            for (hipEvent_t& x : a) ORB_HIP(hipEventCreate(&x));
+            e->ev.push_back(a);
+        }
+        evs = e->ev[e->ev_used++].data();
+        ORB_HIP(hipEventRecord(evs[0], s));
+    }
     for (int l = 1; l < g.nlevels; ++l) {
         const LevelGeom& p = g.lv[l - 1];
         const LevelGeom& v = g.lv[l];
@@ -282,11 +299,15 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
                                      v.w, v.h, v.simd_end, e->d_xtab + v.xtab_offset, e->d_ytab + v.ytab_offset,
                                      batch, s));
     }
+    if (evs) ORB_HIP(hipEventRecord(evs[1], s));
     ORB_HIP(launch_fast_cells(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_cand, e->d_cell_counts, e->d_err, s));
+    if (evs) ORB_HIP(hipEventRecord(evs[2], s));
     ORB_HIP(launch_octree(g, batch, e->d_cand, e->d_cell_counts, e->d_gkeys, e->d_gknode, e->d_oct_out,
                           e->d_oct_count, e->d_err, e->kcap, e->ncap, e->d_trace, s));
+    if (evs) ORB_HIP(hipEventRecord(evs[3], s));
     ORB_HIP(launch_describe(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_oct_out, e->d_oct_count, kps,
                             desc, counts, kp_cap, s));
+    if (evs) ORB_HIP(hipEventRecord(evs[4], s));
     e->last_img = imgs;
     e->last_row = row_step;
     e->last_frame = frame_step;
@@ -448,6 +469,30 @@ int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int hei
         if (descriptors) ORB_HIP(hipMemcpy(descriptors, e->d_desc1, (size_t)count * 32, hipMemcpyDeviceToHost));
     }
     *n = count;
+    return ORBGPU_OK;
+}
+
+int orbgpu_extractor_profile(orbgpu_extractor* e, int enable) {
+    if (!e) return fail(ORBGPU_ERR_ARG, "NULL extractor");
+    e->profile = enable != 0;
+    return ORBGPU_OK;
+}
+
+int orbgpu_extractor_stage_times(orbgpu_extractor* e, float* ms4, int* nbatches, int reset) {
+    if (!e) return fail(ORBGPU_ERR_ARG, "NULL extractor");
+    float acc[4] = {0, 0, 0, 0};
+    for (size_t i = 0; i < e->ev_used; ++i) {
+        ORB_HIP(hipEventSynchronize(e->ev[i][4]));
+        for (int k = 0; k < 4; ++k) {
+            float ms = 0.f;
+            ORB_HIP(hipEventElapsedTime(&ms, e->ev[i][k], e->ev[i][k + 1]));
+            acc[k] += ms;
+        }
+    }
+    if (ms4)
+        for (int k = 0; k < 4; ++k) ms4[k] = acc[k];
+    if (nbatches) *nbatches = (int)e->ev_used;
+    if (reset) e->ev_used = 0;
     return ORBGPU_OK;
 }
 

@@ -60,6 +60,8 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_extract.argtypes = [vp, vp, i, i, sz, vp, vp, i, ctypes.POINTER(i)]
         L.orbgpu_extract_batch_device.argtypes = [vp, vp, i, sz, sz, vp, vp, vp, i, vp]
         L.orbgpu_extractor_sync.argtypes = [vp, vp]
+        L.orbgpu_extractor_profile.argtypes = [vp, i]
+        L.orbgpu_extractor_stage_times.argtypes = [vp, vp, ctypes.POINTER(i), i]
         L.orbgpu_extractor_copy_level.argtypes = [vp, i, i, vp, sz]
         L.orbgpu_hamming_pairs_device.argtypes = [vp, vp, i, vp, vp]
         L.orbgpu_search_for_initialization_batch_device.argtypes = [
@@ -160,6 +162,19 @@ class Extractor:
 
     def sync(self, stream=None):
         _check(lib().orbgpu_extractor_sync(self.h, _stream_ptr(stream)), "orbgpu_extractor_sync")
+
+    STAGES = ("pyramid", "fast_cells", "octree", "describe")
+
+    def profile(self, enable: bool = True):
+        _check(lib().orbgpu_extractor_profile(self.h, int(enable)), "profile")
+
+    def stage_times(self, reset: bool = True):
+        """(dict stage -> summed ms, number of extractions) since last reset."""
+        ms = np.zeros(4, np.float32)
+        n = ctypes.c_int()
+        _check(lib().orbgpu_extractor_stage_times(self.h, ms.ctypes.data, ctypes.byref(n), int(reset)),
+               "stage_times")
+        return dict(zip(self.STAGES, ms.tolist())), n.value
 
     def _debug_xys(self, fn, level: int, frame: int) -> np.ndarray:
         n = fn(self.h, frame, level, None, 0)

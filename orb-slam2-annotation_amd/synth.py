@@ -103,3 +103,35 @@ def flat_image(width: int = 640, height: int = 480, value: int = 128) -> np.ndar
 
 def noise_image(width: int = 640, height: int = 480, seed: int = 7) -> np.ndarray:
     return np.random.default_rng(seed).integers(0, 256, (height, width), dtype=np.uint8)
+
+
+def torch_stream(n: int, width: int, height: int, seed: int = 0x0B5E, device="cuda", t0: int = 0,
+                 noise_sigma: float = 2.0, pitch: int | None = None, chunk: int = 64):
+    """GPU-rendered version of mono_stream for benchmark batches (same scene
+    geometry; bilinear sampling and noise come from torch, so frames are not
+    byte-identical to mono_stream -- parity tests use the numpy renderer).
+    Returns a (n, height, pitch) uint8 tensor (pitch >= width, zero padded)."""
+    import torch
+
+    pitch = pitch or width
+    base = torch.from_numpy(base_texture(seed)).to(device=device, dtype=torch.float32)[None, None]
+    out = torch.zeros((n, height, pitch), dtype=torch.uint8, device=device)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed * 7919 + t0)
+    v, u = torch.meshgrid(torch.arange(height, device=device, dtype=torch.float32),
+                          torch.arange(width, device=device, dtype=torch.float32), indexing="ij")
+    u = u - (width - 1) / 2.0
+    v = v - (height - 1) / 2.0
+    for s in range(0, n, chunk):
+        m = min(chunk, n - s)
+        t = torch.arange(t0 + s, t0 + s + m, device=device, dtype=torch.float32)
+        th = torch.deg2rad(0.5 * t)[:, None, None]
+        c, sn = torch.cos(th), torch.sin(th)
+        sx = c * u - sn * v + (BASE_SIZE / 2 + 2.0 * t)[:, None, None]
+        sy = sn * u + c * v + (BASE_SIZE / 2 + 1.0 * t)[:, None, None]
+        grid = torch.stack([sx / (BASE_SIZE - 1) * 2 - 1, sy / (BASE_SIZE - 1) * 2 - 1], dim=-1)
+        img = torch.nn.functional.grid_sample(base.expand(m, -1, -1, -1), grid, mode="bilinear",
+                                              padding_mode="border", align_corners=True)[:, 0]
+        img = img + noise_sigma * torch.randn(img.shape, generator=gen, device=device)
+        out[s:s + m, :, :width] = img.round().clamp(0, 255).to(torch.uint8)
+    return out
