@@ -72,6 +72,24 @@ def pyramid_bytes_per_frame(level_sizes):
     return sum(px[l - 1] + px[l] for l in range(1, len(px)))
 
 
+def aggregate(elapsed: float, frames_local: int, device=None):
+    """Whole-job numbers across ranks: max elapsed (the job ends when the
+    slowest rank ends) and the sum of frames.  No-op without a process group."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return elapsed, frames_local
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    n = torch.tensor([frames_local], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(n, op=dist.ReduceOp.SUM)
+    return float(t.item()), int(n.item())
+
+
+def rank_seed(rank: int) -> int:
+    """Each rank renders its own independent synthetic stream (weak scaling)."""
+    return 0x0B5E + 1009 * rank
+
+
 def cpu_baseline(frames_np, W, H, nf, seconds):
     """Oracle extract + match on host cores: one extractor per thread."""
     import orbref
@@ -130,7 +148,7 @@ def main():
     pitch = (W + 15) // 16 * 16
     ex = orbgpu.Extractor(nfeatures=NF, width=W, height=H, max_batch=B)
     cap = ex.max_keypoints
-    frames = synth.torch_stream(B, W, H, seed=0x0B5E + 1009 * rank, device=dev, pitch=pitch)
+    frames = synth.torch_stream(B, W, H, seed=rank_seed(rank), device=dev, pitch=pitch)
     kps = torch.zeros((B, cap, 7), dtype=torch.float32, device=dev)
     desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
     counts = torch.zeros(B, dtype=torch.int32, device=dev)
@@ -189,11 +207,9 @@ def main():
         step(evs[i])
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    elapsed, frames_total = aggregate(elapsed, B * args.steps, device=dev)
     if world > 1:
         import torch.distributed as dist
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
         dist.barrier()
     ex.sync(stream)
     stage_ms, nb = ex.stage_times(reset=True)
@@ -206,7 +222,6 @@ def main():
             dist.destroy_process_group()
         return
 
-    frames_total = world * B * args.steps
     fps = frames_total / elapsed
     per_step = {k: v / max(nb, 1) for k, v in stage_ms.items()}
     per_step["match"] = match_ms / args.steps

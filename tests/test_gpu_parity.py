@@ -1,6 +1,8 @@
 """GPU parity: the HIP path (through the C ABI) against the CPU oracle on
 the same seeded inputs.  Bit-exact for every integer/byte output and for the
 float keypoint fields (they are computed with identical IEEE operations)."""
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -138,3 +140,46 @@ def test_stages_candidates_and_octree(w, h, nf):
         og_, or_ = ex.octree(l), ref.octree(l)
         assert og_.shape == or_.shape, f"level {l}: octree {len(og_)} vs {len(or_)}"
         np.testing.assert_array_equal(og_, or_, err_msg=f"octree level {l}")
+
+
+@pytest.mark.parametrize("name,w,h,nf,seed,n", [("mono640_f0", 640, 480, 1000, 0x0B5E, 2),
+                                                ("kitti_f0", 1241, 376, 2000, 21, 1),
+                                                ("euroc_f0", 752, 480, 1200, 22, 1)])
+def test_gpu_against_golden_fixtures(name, w, h, nf, seed, n):
+    """HIP path vs the committed oracle fixtures (tests/golden, see make_golden.py)."""
+    og = _gpu()
+    g = np.load(Path(__file__).resolve().parent / "golden" / f"{name}.npz")
+    frames = synth.mono_stream(n, w, h, seed=seed)
+    ex = og.Extractor(nfeatures=nf, width=w, height=h)
+    k, d = ex.extract(frames[0])
+    assert k.view(np.uint8).reshape(-1, 28).tobytes() == g["kps"].tobytes()
+    assert np.array_equal(d, g["desc"])
+    if n > 1:
+        k1, d1 = ex.extract(frames[1])
+        nm, m12, _ = og.search_for_initialization(k, d, k1, d1, w, h)
+        assert nm == int(g["nmatches"]) and np.array_equal(m12, g["matches12"])
+
+
+def test_batch_matcher_device_path(mono_frames):
+    """search_for_initialization_batch over consecutive pairs == host form."""
+    og = _gpu()
+    B = 4
+    ex = og.Extractor(max_batch=B)
+    imgs = torch.from_numpy(mono_frames[:B]).cuda()
+    cap = ex.max_keypoints
+    kps = torch.zeros((B, cap, 7), dtype=torch.float32, device="cuda")
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(B, dtype=torch.int32, device="cuda")
+    ex.extract_batch(imgs, kps, desc, counts)
+    m12 = torch.full((B - 1, cap), -7, dtype=torch.int32, device="cuda")
+    nm = torch.zeros(B - 1, dtype=torch.int32, device="cuda")
+    og.search_for_initialization_batch(640, 480, kps[:-1], desc[:-1], counts[:-1], kps[1:], desc[1:], counts[1:],
+                                       m12, nm)
+    ex.sync()
+    kk, dd, cc = kps.cpu().numpy(), desc.cpu().numpy(), counts.cpu().numpy()
+    for b in range(B - 1):
+        k1 = og.keypoints_from_raw(kk[b, :cc[b]])
+        k2 = og.keypoints_from_raw(kk[b + 1, :cc[b + 1]])
+        n_r, m_r, _ = orbref.search_for_initialization(k1, dd[b, :cc[b]], k2, dd[b + 1, :cc[b + 1]], 640, 480)
+        assert int(nm[b]) == n_r
+        np.testing.assert_array_equal(m12[b, :cc[b]].cpu().numpy(), m_r)

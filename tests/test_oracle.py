@@ -1,0 +1,192 @@
+"""CPU tests of the parity oracle (oracle/liborbref.so).
+
+The reference has no tests or golden vectors for this path, so
+the oracle is checked (a) against the host libm for sinf/cosf (exhaustively
+by tools/check_sincosf.c; sampled here), (b) against independent Python
+restatements (tests/pyref.py) written from the reference sources, (c) for
+known answers of the reference constructor, and (d) against committed
+fixtures of its own earlier output (tests/golden, regression lock)."""
+import ctypes
+import hashlib
+import math
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import orbref
+import pyref
+import synth
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def test_sincosf_matches_libm_sampled():
+    libm = ctypes.CDLL("libm.so.6")
+    libm.sinf.restype = libm.cosf.restype = ctypes.c_float
+    libm.sinf.argtypes = libm.cosf.argtypes = [ctypes.c_float]
+    rng = np.random.default_rng(3)
+    # random floats in [0, 6.3] plus every angle fastAtan2 yields for small moments
+    xs = list(rng.uniform(0, 6.3, 20000).astype(np.float32))
+    fp = np.float32(math.pi / 180.0)
+    for m01 in range(-40, 41, 7):
+        for m10 in range(-40, 41, 5):
+            xs.append(np.float32(orbref.lib().orbref_fast_atan2(m01, m10)) * fp)
+    xs += [np.float32(v) for v in (0.0, 1e-30, 0.7853981, 0.7853982, 1.5707964, 3.1415927, 6.2831855)]
+    for x in xs:
+        x = float(np.float32(x))
+        assert np.float32(orbref.lib().orbref_sinf(x)).tobytes() == np.float32(libm.sinf(x)).tobytes(), x
+        assert np.float32(orbref.lib().orbref_cosf(x)).tobytes() == np.float32(libm.cosf(x)).tobytes(), x
+
+
+def test_fast_atan2_known_values_and_accuracy():
+    f = orbref.lib().orbref_fast_atan2
+    assert f(0.0, 1.0) == 0.0
+    assert abs(f(1.0, 0.0) - 90.0) < 1e-4
+    assert abs(f(0.0, -1.0) - 180.0) < 1e-4
+    assert abs(f(-1.0, 0.0) - 270.0) < 1e-4
+    rng = np.random.default_rng(0)
+    for y, x in rng.integers(-5000, 5000, (2000, 2)):
+        a = f(float(y), float(x))
+        ref = math.degrees(math.atan2(y, x)) % 360.0
+        d = abs(a - ref)
+        assert min(d, 360 - d) < 0.02 and 0.0 <= a <= 360.0
+
+
+def test_extractor_constructor_known_answers():
+    ex = orbref.Extractor(1000, 1.2, 8, 20, 7)
+    assert list(ex.features_per_level()) == [217, 181, 151, 126, 105, 87, 73, 60]
+    s, inv, s2, inv2 = ex.scale_factors()
+    assert s[0] == 1.0 and abs(s[7] - 3.5831808) < 1e-6
+    ex2 = orbref.Extractor(2000, 1.2, 8, 20, 7)
+    assert list(ex2.features_per_level()) == [434, 362, 302, 251, 209, 175, 145, 122]
+    ex3 = orbref.Extractor(1200, 1.2, 8, 20, 7)
+    assert sum(ex3.features_per_level()) == 1200
+
+
+def test_pyramid_geometry_table():
+    ex = orbref.Extractor()
+    ex.extract(synth.flat_image())
+    sizes = [ex.level(l).shape[::-1] for l in range(8)]
+    assert sizes == [(640, 480), (533, 400), (444, 333), (370, 278), (309, 231), (257, 193), (214, 161), (179, 134)]
+
+
+def test_gaussian_kernel_and_gain():
+    img = np.full((40, 41), 128, np.uint8)
+    out = orbref.gaussian7(img)
+    # kernel [18,34,49,55,49,34,18] sums to 257 -> 2-D gain 66049/65536
+    assert np.all(out == 129)
+    # an impulse reproduces the separable kernel (column-SIMD / row-scalar mix)
+    imp = np.zeros((21, 21), np.uint8)
+    imp[10, 10] = 255
+    out = orbref.gaussian7(imp)
+    k = np.array([18, 34, 49, 55, 49, 34, 18])
+    v = np.outer(k, k) * 255
+    simd = np.floor(v / 65536 + 0.5)  # no exact .5 ties here
+    assert np.array_equal(out[7:14, 7:14], simd.astype(np.uint8))
+
+
+@pytest.mark.parametrize("shape,dst", [((37, 45), (31, 38)), ((60, 53), (50, 44)), ((24, 20), (20, 17))])
+def test_resize_matches_python_restatement(shape, dst):
+    rng = np.random.default_rng(sum(shape))
+    src = rng.integers(0, 256, shape, dtype=np.uint8)
+    a = orbref.resize_linear(src, dst[0], dst[1])
+    b = pyref.resize_linear(src, dst[0], dst[1])
+    np.testing.assert_array_equal(a, b)
+
+
+def test_resize_constant_image():
+    src = np.full((480, 640), 77, np.uint8)
+    assert np.all(orbref.resize_linear(src, 533, 400) == 77)
+
+
+@pytest.mark.parametrize("t", [20, 7])
+def test_fast_matches_python_restatement(t):
+    img = synth.mono_stream(1, 640, 480)[0][100:140, 200:246]
+    noise = synth.noise_image(30, 24, seed=4)
+    for im in (img, noise):
+        got = [tuple(r) for r in orbref.fast(im, t)]
+        assert got == pyref.fast(im, t)
+
+
+def test_octree_matches_python_restatement():
+    frame = synth.mono_stream(1, 640, 480)[0]
+    ex = orbref.Extractor()
+    ex.extract(frame)
+    for l, (w, h) in [(0, (640, 480)), (3, (370, 278)), (7, (179, 134))]:
+        cands = [tuple(map(int, r)) for r in ex.candidates(l)]
+        N = int(ex.features_per_level()[l])
+        kept = pyref.distribute_octree(cands, 16, w - 16, 16, h - 16, N)
+        want = np.array([cands[k] for k in kept], np.int32).reshape(-1, 3)
+        np.testing.assert_array_equal(ex.octree(l), want)
+
+
+def test_octree_noise_heavy_level():
+    ex = orbref.Extractor()
+    ex.extract(synth.noise_image())
+    cands = [tuple(map(int, r)) for r in ex.candidates(6)]
+    kept = pyref.distribute_octree(cands, 16, 214 - 16, 16, 161 - 16, int(ex.features_per_level()[6]))
+    np.testing.assert_array_equal(ex.octree(6), np.array([cands[k] for k in kept], np.int32).reshape(-1, 3))
+
+
+def test_descriptor_distance():
+    rng = np.random.default_rng(1)
+    for _ in range(50):
+        a = rng.integers(0, 256, 32, dtype=np.uint8)
+        b = rng.integers(0, 256, 32, dtype=np.uint8)
+        assert orbref.descriptor_distance(a, b) == pyref.descriptor_distance(a, b)
+
+
+def test_flat_and_empty_images():
+    ex = orbref.Extractor()
+    k, d = ex.extract(synth.flat_image())
+    assert len(k) == 0 and d.shape == (0, 32)
+
+
+def test_extract_invariants():
+    ex = orbref.Extractor()
+    k, d = ex.extract(synth.mono_stream(1)[0])
+    assert 990 <= len(k) <= 1010
+    assert np.all(np.diff(k["octave"]) >= 0)  # levels concatenated in order
+    assert np.all((k["angle"] >= 0) & (k["angle"] <= 360))
+    assert np.all(k["class_id"] == -1)
+    sizes = {int(o): float(s) for o, s in zip(k["octave"], k["size"])}
+    assert sizes[0] == 31.0 and sizes[7] == 111.0
+
+
+def _golden(name):
+    return np.load(GOLDEN / f"{name}.npz")
+
+
+@pytest.mark.parametrize("name,w,h,nf,seed,n", [("mono640_f0", 640, 480, 1000, 0x0B5E, 2),
+                                                ("kitti_f0", 1241, 376, 2000, 21, 1),
+                                                ("euroc_f0", 752, 480, 1200, 22, 1)])
+def test_oracle_against_golden_fixtures(name, w, h, nf, seed, n):
+    g = _golden(name)
+    frames = synth.mono_stream(n, w, h, seed=seed)
+    assert hashlib.sha256(frames[0].tobytes()).hexdigest() == str(g["image_sha256"])
+    ex = orbref.Extractor(nfeatures=nf)
+    k, d = ex.extract(frames[0])
+    assert k.view(np.uint8).reshape(-1, 28).tobytes() == g["kps"].tobytes()
+    assert np.array_equal(d, g["desc"])
+    if n > 1:
+        k1, d1 = ex.extract(frames[1])
+        nm, m12, _ = orbref.search_for_initialization(k, d, k1, d1, w, h)
+        assert nm == int(g["nmatches"]) and np.array_equal(m12, g["matches12"])
+
+
+def test_matcher_invariants():
+    fr = synth.mono_stream(2)
+    ex = orbref.Extractor()
+    k1, d1 = ex.extract(fr[0])
+    k2, d2 = ex.extract(fr[1])
+    n, m12, prev = orbref.search_for_initialization(k1, d1, k2, d2, 640, 480)
+    assert n == int((m12 >= 0).sum()) > 50
+    valid = m12[m12 >= 0]
+    assert len(set(valid.tolist())) == len(valid)  # one-to-one
+    assert np.all(k1["octave"][m12 >= 0] == 0) and np.all(k2["octave"][valid] == 0)
+    for i in np.nonzero(m12 >= 0)[0][:40]:
+        assert pyref.descriptor_distance(d1[i], d2[m12[i]]) <= 50
+        assert prev[i, 0] == k2["x"][m12[i]]
+    n0, m0, _ = orbref.search_for_initialization(k1, d1, k2, d2, 640, 480, check_ori=False)
+    assert n0 >= n
