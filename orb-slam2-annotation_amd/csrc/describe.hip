@@ -30,7 +30,7 @@ __constant__ signed char c_pattern[1024] = {
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 __constant__ int c_gk[7] = {18, 34, 49, 55, 49, 34, 18};
 
-constexpr int kRawPitch = 44;
+constexpr int kRawPitch = 48;
 constexpr int kBlurPitch = 40;
 
 __device__ inline int reflect101(int p, int n) {
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
                                                       const int* __restrict__ oct_count,
                                                       orbgpu_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                       int* __restrict__ counts, int kp_cap) {
-    __shared__ uint8_t s_raw[kPatch * kRawPitch];
+    __shared__ __attribute__((aligned(16))) uint8_t s_raw[kPatch * kRawPitch];
     __shared__ uint16_t s_row[kPatch * kBlur];
     __shared__ uint8_t s_blur[kBlur * kBlurPitch];
     const int lane = threadIdx.x;
@@ -142,10 +142,26 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     const uint8_t* base = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
     const size_t pitch = l == 0 ? row0 : (size_t)L.pitch;
 
-    for (int idx = lane; idx < kPatch * kPatch; idx += 64) {
-        const int r = idx / kPatch, c = idx - r * kPatch;
-        const int yy = reflect101(cy - kPatchR + r, L.h), xx = reflect101(cx - kPatchR + c, L.w);
-        s_raw[r * kRawPitch + c] = base[(size_t)yy * pitch + xx];
+    // raw 43x43 neighbourhood.  Interior keypoints (the common case): 12
+    // aligned dwords per row, column 0 of the tile = level x xa; edge
+    // keypoints: byte loads with REFLECT_101 applied to the coordinates.
+    const int xa = (cx - kPatchR) & ~3;
+    const bool interior = cx - kPatchR >= 0 && xa + 48 <= L.w && cy - kPatchR >= 0 && cy + kPatchR < L.h;
+    int ox;  // tile column of level x (cx - 21)
+    if (interior) {
+        ox = cx - kPatchR - xa;
+        for (int idx = lane; idx < kPatch * 12; idx += 64) {
+            const int r = idx / 12, q = idx - r * 12;
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(base + (size_t)(cy - kPatchR + r) * pitch + xa + 4 * q);
+            *reinterpret_cast<uint32_t*>(s_raw + r * kRawPitch + 4 * q) = v;
+        }
+    } else {
+        ox = 0;
+        for (int idx = lane; idx < kPatch * kPatch; idx += 64) {
+            const int r = idx / kPatch, c = idx - r * kPatch;
+            const int yy = reflect101(cy - kPatchR + r, L.h), xx = reflect101(cx - kPatchR + c, L.w);
+            s_raw[r * kRawPitch + c] = base[(size_t)yy * pitch + xx];
+        }
     }
     __syncthreads();
 
@@ -154,7 +170,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     for (int idx = lane; idx < 31 * 31; idx += 64) {
         const int v = idx / 31 - 15, u = idx % 31 - 15;
         if (abs(u) <= c_umax[abs(v)]) {
-            const int p = s_raw[(kPatchR + v) * kRawPitch + kPatchR + u];
+            const int p = s_raw[(kPatchR + v) * kRawPitch + ox + kPatchR + u];
             m10 += u * p;
             m01 += v * p;
         }
@@ -166,7 +182,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     // row pass (exact int): rows 0..42, output cols 0..36 <-> patch cols 3..39
     for (int idx = lane; idx < kPatch * kBlur; idx += 64) {
         const int r = idx / kBlur, c = idx - r * kBlur;
-        const uint8_t* p = s_raw + r * kRawPitch + c;
+        const uint8_t* p = s_raw + r * kRawPitch + ox + c;
         int acc = 0;
 #pragma unroll
         for (int j = 0; j < 7; ++j) acc += c_gk[j] * p[j];

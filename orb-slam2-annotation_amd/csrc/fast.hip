@@ -53,11 +53,16 @@ __device__ inline int arc_strength(const int d[16]) {
     return best;
 }
 
+// q = n / d for n < 65536, 0 < d < 256 via one multiply (m = ceil(2^24/d))
+__device__ inline int fast_div(int n, uint32_t m) { return (int)(((uint32_t)n * m) >> 24); }
+
 __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const uint8_t* __restrict__ img0, size_t row0,
                                                         size_t frame0, const uint8_t* __restrict__ pyr,
                                                         uint32_t* __restrict__ cand, int* __restrict__ cell_counts,
                                                         int* __restrict__ err) {
-    __shared__ uint8_t s_win[W * W];
+    // LDS tile: the cell window, re-based to a 4-byte aligned column so rows
+    // are fetched with dword loads; column c <-> level x = xa + c.
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[W * W];
     __shared__ uint8_t s_sc[W * W];
     const int lane = threadIdx.x;
     const int f = blockIdx.y;
@@ -81,35 +86,51 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const uint8_t* _
     const uint8_t* base = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
     const size_t pitch = l == 0 ? row0 : (size_t)L.pitch;
 
-    for (int idx = lane; idx < W * W; idx += 64) s_sc[idx] = 0;
-    for (int r = 0; r < wh; ++r) {
-        const uint8_t* row = base + (size_t)(iniY + r) * pitch + iniX;
-        for (int x = lane; x < ww; x += 64) s_win[r * W + x] = row[x];
+    // stage rows: dwords covering [xa, maxX), xa = iniX & ~3 (row pitch and
+    // frame base are 16-byte aligned; maxX <= w - 16, so no over-read)
+    const int xa = iniX & ~3, ox = iniX - xa;
+    const int nd = (maxX - xa + 3) >> 2;
+    const uint32_t mnd = (1u << 24) / (uint32_t)nd + 1u;
+    for (int idx = lane; idx < nd * wh; idx += 64) {
+        const int r = fast_div(idx, mnd), q = idx - r * nd;
+        const uint32_t v = *reinterpret_cast<const uint32_t*>(base + (size_t)(iniY + r) * pitch + xa + 4 * q);
+        *reinterpret_cast<uint32_t*>(s_win + r * W + 4 * q) = v;
     }
+    for (int idx = lane; idx < W * W / 4; idx += 64) reinterpret_cast<uint32_t*>(s_sc)[idx] = 0u;
     __syncthreads();
 
-    // detection region of cv::FAST on the window: [3, ww-3) x [3, wh-3)
+    // detection region of cv::FAST on the window: rows [3, wh-3), cols [3, ww-3)
     const int dw = ww - 6, dh = wh - 6;
     const int tmin = min(g.ini_th, g.min_th);
     const int ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
     const int ring_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
     if (dw > 0 && dh > 0) {
+        const uint32_t mdw = (1u << 24) / (uint32_t)dw + 1u;
         for (int idx = lane; idx < dw * dh; idx += 64) {
-            const int r = 3 + idx / dw, x = 3 + idx % dw;
+            const int rr = fast_div(idx, mdw);
+            const int r = 3 + rr, x = 3 + ox + (idx - rr * dw);
             const uint8_t* p = s_win + r * W + x;
             const int v = p[0];
-            int d[16];
-            uint32_t dark = 0, bright = 0;
+            // compass pre-test (ring 0/4/8/12): a 9-arc covers two adjacent ones
+            const int c0 = p[3 * W], c4 = p[3], c8 = p[-3 * W], c12 = p[-3];
+            const int lo = v - tmin, hi = v + tmin;
+            const uint32_t dk = (c0 < lo) | ((c4 < lo) << 1) | ((c8 < lo) << 2) | ((c12 < lo) << 3);
+            const uint32_t br = (c0 > hi) | ((c4 > hi) << 1) | ((c8 > hi) << 2) | ((c12 > hi) << 3);
+            const uint32_t dk2 = dk & ((dk >> 1) | (dk << 3)), br2 = br & ((br >> 1) | (br << 3));
+            if ((dk2 | br2) & 15) {
+                int d[16];
+                uint32_t dark = 0, bright = 0;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int q = p[ring_dy[k] * W + ring_dx[k]];
-                d[k] = v - q;
-                dark |= (uint32_t)(q < v - tmin) << k;
-                bright |= (uint32_t)(q > v + tmin) << k;
-            }
-            if (has_run9(dark) || has_run9(bright)) {
-                const int s = arc_strength(d);  // >= tmin + 1 here
-                s_sc[r * W + x] = (uint8_t)min(s, 255);
+                for (int k = 0; k < 16; ++k) {
+                    const int q = p[ring_dy[k] * W + ring_dx[k]];
+                    d[k] = v - q;
+                    dark |= (uint32_t)(q < lo) << k;
+                    bright |= (uint32_t)(q > hi) << k;
+                }
+                if (has_run9(dark) || has_run9(bright)) {
+                    const int sc = arc_strength(d);  // >= tmin + 1 here
+                    s_sc[r * W + x] = (uint8_t)min(sc, 255);
+                }
             }
         }
     }
@@ -117,15 +138,15 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const uint8_t* _
 
     int total = 0;
     for (int pass = 0; pass < 2 && total == 0 && dw > 0 && dh > 0; ++pass) {
-        const int t = pass == 0 ? g.ini_th : g.min_th;
-        const int t1 = t + 1;
+        const int t1 = (pass == 0 ? g.ini_th : g.min_th) + 1;
         for (int r = 3; r < 3 + dh; ++r) {
             for (int x0 = 3; x0 < 3 + dw; x0 += 64) {
                 const int x = x0 + lane;
                 bool keep = false;
                 int s = 0;
                 if (x < 3 + dw) {
-                    s = s_sc[r * W + x];
+                    const uint8_t* q = s_sc + r * W + x + ox;
+                    s = q[0];
                     if (s >= t1) {
                         keep = true;
 #pragma unroll
@@ -133,7 +154,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const uint8_t* _
 #pragma unroll
                             for (int dx = -1; dx <= 1; ++dx) {
                                 if (dx == 0 && dy == 0) continue;
-                                const int nb = s_sc[(r + dy) * W + x + dx];
+                                const int nb = q[dy * W + dx];
                                 const int nbv = nb >= t1 ? nb - 1 : 0;
                                 keep = keep && (s - 1 > nbv);
                             }

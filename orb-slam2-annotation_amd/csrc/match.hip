@@ -22,7 +22,7 @@ namespace orbgpu {
 
 namespace {
 
-constexpr int kMaxK0 = 1024;  // level-0 keypoints per frame held in LDS
+constexpr int kMaxK0 = 512;  // level-0 keypoints per frame held in LDS (N0+3 for nfeatures <= 2350)
 constexpr int kGC = 64, kGR = 48, kHL = 30, kThLow = 50;
 
 __device__ inline unsigned long long wave_min_u64(unsigned long long v) {
@@ -64,6 +64,8 @@ __global__ __launch_bounds__(64) void match_init_kernel(int img_w, int img_h,
     __shared__ int s_m21[kMaxK0];            // vnMatches21
     __shared__ unsigned long long s_d2[kMaxK0][4];
     __shared__ int s_m12[kMaxK0];            // vnMatches12 for F1 level-0
+    __shared__ float s_px[kMaxK0], s_py[kMaxK0], s_ang1[kMaxK0];  // F1: vbPrevMatched, angle
+    __shared__ unsigned long long s_d1[kMaxK0][4];
     __shared__ signed char s_bin[kMaxK0];    // rotation bin pushed for i1, or -1
     __shared__ int s_hist[kHL];
     const int lane = threadIdx.x;
@@ -98,7 +100,16 @@ __global__ __launch_bounds__(64) void match_init_kernel(int img_w, int img_h,
 #pragma unroll
         for (int q = 0; q < 4; ++q) s_d2[j][q] = d[q];
     }
-    for (int i = lane; i < n10; i += 64) { s_m12[i] = -1; s_bin[i] = -1; }
+    for (int i = lane; i < n10; i += 64) {
+        s_m12[i] = -1;
+        s_bin[i] = -1;
+        s_px[i] = prev ? prev[2 * i] : K1[i].x;
+        s_py[i] = prev ? prev[2 * i + 1] : K1[i].y;
+        s_ang1[i] = K1[i].angle;
+        const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D1 + (size_t)i * 32);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s_d1[i][q] = d[q];
+    }
     if (lane < kHL) s_hist[lane] = 0;
     __syncthreads();
 
@@ -106,15 +117,14 @@ __global__ __launch_bounds__(64) void match_init_kernel(int img_w, int img_h,
     const float factor = (flags & ORBGPU_MATCH_ANNOTATED_HISTO) ? __fdiv_rn(1.0f, (float)kHL) : __fdiv_rn((float)kHL, 360.0f);
     int nmatches = 0;
     for (int i1 = 0; i1 < n10; ++i1) {
-        const float x = prev ? prev[2 * i1] : K1[i1].x;
-        const float y = prev ? prev[2 * i1 + 1] : K1[i1].y;
+        const float x = s_px[i1];
+        const float y = s_py[i1];
         const int cx0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, minX), r), invW)));
         const int cx1 = min(kGC - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, minX), r), invW)));
         const int cy0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, minY), r), invH)));
         const int cy1 = min(kGR - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, minY), r), invH)));
         if (cx0 >= kGC || cx1 < 0 || cy0 >= kGR || cy1 < 0) continue;
-        const unsigned long long* d1 = reinterpret_cast<const unsigned long long*>(D1 + (size_t)i1 * 32);
-        const unsigned long long q0 = d1[0], q1 = d1[1], q2 = d1[2], q3 = d1[3];
+        const unsigned long long q0 = s_d1[i1][0], q1 = s_d1[i1][1], q2 = s_d1[i1][2], q3 = s_d1[i1][3];
         unsigned long long best = ~0ull;  // (dist << 32) | order key
         int second = 0x7FFFFFFF;
         for (int j = lane; j < n20; j += 64) {
@@ -148,7 +158,7 @@ __global__ __launch_bounds__(64) void match_init_kernel(int img_w, int img_h,
                 s_m21[bidx] = i1;
                 s_mdist[bidx] = bestDist;
                 if (flags & ORBGPU_MATCH_CHECK_ORI) {
-                    float rot = __fsub_rn(K1[i1].angle, K2[bidx].angle);
+                    float rot = __fsub_rn(s_ang1[i1], K2[bidx].angle);
                     if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
                     int bin = (int)roundf(__fmul_rn(rot, factor));
                     if (bin == kHL) bin = 0;

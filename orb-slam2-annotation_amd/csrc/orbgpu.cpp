@@ -223,7 +223,7 @@ int build_geometry(orbgpu_extractor* e, std::vector<int2>& xtab, std::vector<int
         v.nrows = (int)(height / 30.f);
         v.wcell = (int)std::ceil(width / v.ncols);
         v.hcell = (int)std::ceil(height / v.nrows);
-        if (v.wcell + 6 > kMaxWin || v.hcell + 6 > kMaxWin)
+        if (v.wcell + 9 > kMaxWin || v.hcell + 6 > kMaxWin)
             return fail(ORBGPU_ERR_UNSUPPORTED, "FAST cell window larger than the LDS tile");
         if (v.max_bx - kBorder > 2047 || v.max_by - kBorder > 2047)
             return fail(ORBGPU_ERR_UNSUPPORTED, "levels wider/taller than 2079 px are not supported");
