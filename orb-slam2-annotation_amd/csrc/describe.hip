@@ -1,17 +1,12 @@
 // describe.hip -- per-keypoint tail of ORBextractor::operator():
 //   IC_Angle on the unblurred level (ORBextractor.cpp:79-106, :474-481),
-//   GaussianBlur 7x7 sigma 2 REFLECT_101 of the level (:1097-1098, restated
-//   per keypoint on the 37x37 neighbourhood rBRIEF can touch),
-//   computeOrbDescriptor (:110-149) and the final keypoint fields
-//   (:847-857, :1107-1115).
+//   computeOrbDescriptor (:110-149) on the blurred level (blur.hip) and the
+//   final keypoint fields (:847-857, :1107-1115).
 //
-// One wave per keypoint slot.  The 43x43 raw neighbourhood is staged in LDS
-// once (REFLECT_101 applied on load, exactly the rows/columns the
-// reference's separable filter reads), then: moments by a 64-lane reduction;
-// the exact-integer row pass and the column pass with OpenCV-2.4's two
-// roundings (SSE2 float path = half-to-even on x < 4*floor(w/4), scalar
-// FixedPtCastEx tail = half-up); 256 tests as 4 wave ballots (bit t of the
-// descriptor = test t = lane t%64 of ballot t/64).  sin/cos of the angle use
+// One wave per keypoint slot: the 31x31 unblurred disc and the 37x37
+// blurred neighbourhood are staged in LDS with dword loads; moments by a
+// 64-lane reduction; 256 tests as 4 wave ballots (bit t of the descriptor =
+// test t = lane t%64 of ballot t/64).  sin/cos of the angle use
 // the glibc-2.35 sinf/cosf restatement (fp64 polynomial), pinned bit-exact
 // against libm over every float in [0, 6.3].
 #include "orbgpu_internal.h"
@@ -28,15 +23,6 @@ __constant__ signed char c_pattern[1024] = {
 // umax of the 31-px disc (ORBextractor.cpp:456-471); checked against the
 // construction on the host at extractor creation.
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
-__constant__ int c_gk[7] = {18, 34, 49, 55, 49, 34, 18};
-
-constexpr int kRawPitch = 48;
-constexpr int kBlurPitch = 40;
-
-__device__ inline int reflect101(int p, int n) {
-    while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
-    return p;
-}
 
 // OpenCV 2.4 fastAtan2 (mathfuncs.cpp); explicit _rn ops: never contracted.
 __device__ inline float fast_atan2(float y, float x) {
@@ -113,15 +99,18 @@ __device__ inline int wave_sum(int v) {
     return v;
 }
 
+constexpr int kDiscPitch = 36;   // 31-px disc rows, staged from a 4-aligned column
+constexpr int kBPitch = 40;      // 37-px blurred rows, staged from a 4-aligned column
+
 __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __restrict__ img0, size_t row0,
                                                       size_t frame0, const uint8_t* __restrict__ pyr,
+                                                      const uint8_t* __restrict__ blur,
                                                       const uint32_t* __restrict__ oct_out,
                                                       const int* __restrict__ oct_count,
                                                       orbgpu_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                       int* __restrict__ counts, int kp_cap) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_raw[kPatch * kRawPitch];
-    __shared__ uint16_t s_row[kPatch * kBlur];
-    __shared__ uint8_t s_blur[kBlur * kBlurPitch];
+    __shared__ __attribute__((aligned(16))) uint8_t s_disc[31 * kDiscPitch];
+    __shared__ __attribute__((aligned(16))) uint8_t s_blur[kBlur * kBPitch];
     const int lane = threadIdx.x;
     const int f = blockIdx.y, slot = blockIdx.x;
     int l = 0;
@@ -139,29 +128,33 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     if (i >= oc[l]) return;
     const uint32_t key = oct_out[(size_t)f * g.slots_frame + slot];
     const int cx = key_x(key) + kBorder, cy = key_y(key) + kBorder;
-    const uint8_t* base = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
-    const size_t pitch = l == 0 ? row0 : (size_t)L.pitch;
+    const uint8_t* raw = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
+    const size_t rp = l == 0 ? row0 : (size_t)L.pitch;
+    const uint8_t* bl = blur + L.blur_offset + (size_t)f * L.blur_frame_bytes;
 
-    // raw 43x43 neighbourhood.  Interior keypoints (the common case): 12
-    // aligned dwords per row, column 0 of the tile = level x xa; edge
-    // keypoints: byte loads with REFLECT_101 applied to the coordinates.
-    const int xa = (cx - kPatchR) & ~3;
-    const bool interior = cx - kPatchR >= 0 && xa + 48 <= L.w && cy - kPatchR >= 0 && cy + kPatchR < L.h;
-    int ox;  // tile column of level x (cx - 21)
-    if (interior) {
-        ox = cx - kPatchR - xa;
-        for (int idx = lane; idx < kPatch * 12; idx += 64) {
-            const int r = idx / 12, q = idx - r * 12;
-            const uint32_t v = *reinterpret_cast<const uint32_t*>(base + (size_t)(cy - kPatchR + r) * pitch + xa + 4 * q);
-            *reinterpret_cast<uint32_t*>(s_raw + r * kRawPitch + 4 * q) = v;
+    // unblurred 31x31 disc (IC_Angle; the keypoint is >= 19 px from every
+    // border, so no clamping); 9 aligned dwords per row when they stay
+    // inside the row, else bytes
+    const int xd = (cx - 15) & ~3, od = cx - 15 - xd;
+    if (xd + 36 <= L.w) {
+        for (int idx = lane; idx < 31 * 9; idx += 64) {
+            const int r = idx / 9, q = idx - r * 9;
+            *reinterpret_cast<uint32_t*>(s_disc + r * kDiscPitch + 4 * q) =
+                *reinterpret_cast<const uint32_t*>(raw + (size_t)(cy - 15 + r) * rp + xd + 4 * q);
         }
     } else {
-        ox = 0;
-        for (int idx = lane; idx < kPatch * kPatch; idx += 64) {
-            const int r = idx / kPatch, c = idx - r * kPatch;
-            const int yy = reflect101(cy - kPatchR + r, L.h), xx = reflect101(cx - kPatchR + c, L.w);
-            s_raw[r * kRawPitch + c] = base[(size_t)yy * pitch + xx];
+        for (int idx = lane; idx < 31 * 31; idx += 64) {
+            const int r = idx / 31, c = idx - r * 31;
+            s_disc[r * kDiscPitch + od + c] = raw[(size_t)(cy - 15 + r) * rp + cx - 15 + c];
         }
+    }
+    // blurred 37x37 neighbourhood rBRIEF samples from (cx-18 >= 1 always);
+    // the blur buffer is padded, so the 10-dword spans never leave it
+    const int xb = (cx - kBlurR) & ~3, ob = cx - kBlurR - xb;
+    for (int idx = lane; idx < kBlur * 10; idx += 64) {
+        const int r = idx / 10, q = idx - r * 10;
+        *reinterpret_cast<uint32_t*>(s_blur + r * kBPitch + 4 * q) =
+            *reinterpret_cast<const uint32_t*>(bl + (size_t)(cy - kBlurR + r) * L.pitch + xb + 4 * q);
     }
     __syncthreads();
 
@@ -170,7 +163,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     for (int idx = lane; idx < 31 * 31; idx += 64) {
         const int v = idx / 31 - 15, u = idx % 31 - 15;
         if (abs(u) <= c_umax[abs(v)]) {
-            const int p = s_raw[(kPatchR + v) * kRawPitch + ox + kPatchR + u];
+            const int p = s_disc[(15 + v) * kDiscPitch + od + 15 + u];
             m10 += u * p;
             m01 += v * p;
         }
@@ -179,36 +172,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     m01 = wave_sum(m01);
     const float angle = fast_atan2((float)m01, (float)m10);
 
-    // row pass (exact int): rows 0..42, output cols 0..36 <-> patch cols 3..39
-    for (int idx = lane; idx < kPatch * kBlur; idx += 64) {
-        const int r = idx / kBlur, c = idx - r * kBlur;
-        const uint8_t* p = s_raw + r * kRawPitch + ox + c;
-        int acc = 0;
-#pragma unroll
-        for (int j = 0; j < 7; ++j) acc += c_gk[j] * p[j];
-        s_row[r * kBlur + c] = (uint16_t)acc;
-    }
-    __syncthreads();
-    // column pass with the SIMD/scalar rounding split on the level's x
-    const int w4 = L.w & ~3;
-    for (int idx = lane; idx < kBlur * kBlur; idx += 64) {
-        const int r = idx / kBlur, c = idx - r * kBlur;
-        int v = 0;
-#pragma unroll
-        for (int k = 0; k < 7; ++k) v += c_gk[k] * (int)s_row[(r + k) * kBlur + c];
-        const int x = cx - kBlurR + c;
-        int o;
-        if (x < w4) {
-            const int q = v >> 16, rem = v & 0xFFFF;
-            o = q + ((rem > 32768) | ((rem == 32768) & (q & 1)));
-        } else {
-            o = (v + 32768) >> 16;
-        }
-        s_blur[r * kBlurPitch + c] = (uint8_t)min(o, 255);
-    }
-    __syncthreads();
-
-    // rBRIEF
+    // rBRIEF (computeOrbDescriptor, ORBextractor.cpp:110-149)
     const float ang = __fmul_rn(angle, (float)(M_PI / 180.f));
     float sa, ca;
     glibc_sincosf(ang, &sa, &ca);
@@ -223,7 +187,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
             const float px = (float)c_pattern[4 * t + 2 * pp], py = (float)c_pattern[4 * t + 2 * pp + 1];
             const int ry = __float2int_rn(__fadd_rn(__fmul_rn(px, b), __fmul_rn(py, a)));
             const int rx = __float2int_rn(__fsub_rn(__fmul_rn(px, a), __fmul_rn(py, b)));
-            val[pp] = s_blur[(kBlurR + ry) * kBlurPitch + kBlurR + rx];
+            val[pp] = s_blur[(kBlurR + ry) * kBPitch + ob + kBlurR + rx];
         }
         words[rnd] = __ballot(val[0] < val[1]);
     }
@@ -247,12 +211,12 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
 }  // namespace
 
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
-                           const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
+                           const uint8_t* pyr, const uint8_t* blur, const uint32_t* oct_out, const int* oct_count,
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
                            hipStream_t stream) {
     dim3 grid(g.slots_frame, batch);
-    hipLaunchKernelGGL(describe_kernel, grid, dim3(64), 0, stream, g, img0, row0, frame0, pyr, oct_out, oct_count,
-                       kps, desc, counts, kp_cap);
+    hipLaunchKernelGGL(describe_kernel, grid, dim3(64), 0, stream, g, img0, row0, frame0, pyr, blur, oct_out,
+                       oct_count, kps, desc, counts, kp_cap);
     return hipGetLastError();
 }
 

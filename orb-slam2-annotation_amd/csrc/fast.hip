@@ -18,8 +18,6 @@ namespace orbgpu {
 
 namespace {
 
-constexpr int W = kMaxWin;
-
 __device__ inline bool has_run9(uint32_t m16) {
     uint32_t m = m16 | (m16 << 16);
     uint32_t r = m & (m >> 1);   // runs >= 2
@@ -56,17 +54,153 @@ __device__ inline int arc_strength(const int d[16]) {
 // q = n / d for n < 65536, 0 < d < 256 via one multiply (m = ceil(2^24/d))
 __device__ inline int fast_div(int n, uint32_t m) { return (int)(((uint32_t)n * m) >> 24); }
 
-__global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const uint8_t* __restrict__ img0, size_t row0,
-                                                        size_t frame0, const uint8_t* __restrict__ pyr,
-                                                        uint32_t* __restrict__ cand, int* __restrict__ cell_counts,
-                                                        int* __restrict__ err) {
-    // LDS tile: the cell window, re-based to a 4-byte aligned column so rows
-    // are fetched with dword loads; column c <-> level x = xa + c.
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[W * W];
-    __shared__ uint8_t s_sc[W * W];
-    const int lane = threadIdx.x;
-    const int f = blockIdx.y;
-    const int gc = blockIdx.x;
+// The waves of a block work on different cells, so stages are ordered with
+// a wave-local LDS fence, never a block barrier.
+__device__ inline void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Wave-level stream compaction: lanes holding `pred` append `v` to list[]
+// after `n` entries (order = lane order); returns the new length.
+__device__ inline int wave_append(bool pred, uint16_t v, uint16_t* list, int n, int lane) {
+    const unsigned long long m = __ballot(pred);
+    if (pred) list[n + __popcll(m & ((1ull << lane) - 1ull))] = v;
+    return n + __popcll(m);
+}
+
+struct CellTiles {
+    const uint8_t* win;  // staged window, pitch P, column c <-> level x = xa + c
+    uint8_t* sc;         // FAST arc strength of corners, 0 elsewhere
+    uint16_t* la;        // tile offsets passing the compass pre-test
+    uint16_t* lb;        // tile offsets of corners (row-major order)
+};
+
+// FAST at threshold t on the cell's detection region: returns the number
+// of corners, their tile offsets in lb[] (row-major) and scores in sc[].
+// Stages are separated by wave compaction so each runs on dense lanes:
+// compass pre-test on every pixel -> 16-pixel contiguity test on survivors
+// -> arc strength on corners.
+__device__ int fast_corners(const CellTiles& T, int P, int dw, int dh, int ox, int t, int lane) {
+    const uint32_t mdw = (1u << 24) / (uint32_t)dw + 1u;
+    int na = 0;
+    for (int base = 0; base < dw * dh; base += 64) {
+        const int idx = base + lane;
+        bool pass = false;
+        int off = 0;
+        if (idx < dw * dh) {
+            const int rr = fast_div(idx, mdw);
+            off = (3 + rr) * P + 3 + ox + (idx - rr * dw);
+            const uint8_t* p = T.win + off;
+            const int v = p[0], lo = v - t, hi = v + t;
+            const int c0 = p[3 * P], c4 = p[3], c8 = p[-3 * P], c12 = p[-3];
+            const uint32_t dk = (c0 < lo) | ((c4 < lo) << 1) | ((c8 < lo) << 2) | ((c12 < lo) << 3);
+            const uint32_t br = (c0 > hi) | ((c4 > hi) << 1) | ((c8 > hi) << 2) | ((c12 > hi) << 3);
+            pass = ((dk & ((dk >> 1) | (dk << 3))) | (br & ((br >> 1) | (br << 3)))) & 15;
+        }
+        na = wave_append(pass, (uint16_t)off, T.la, na, lane);
+    }
+    wave_sync();
+    const int ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+    const int ring_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+    int nb = 0;
+    for (int base = 0; base < na; base += 64) {
+        const int j = base + lane;
+        bool corner = false;
+        int off = 0;
+        if (j < na) {
+            off = T.la[j];
+            const uint8_t* p = T.win + off;
+            const int v = p[0], lo = v - t, hi = v + t;
+            uint32_t dark = 0, bright = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int q = p[ring_dy[k] * P + ring_dx[k]];
+                dark |= (uint32_t)(q < lo) << k;
+                bright |= (uint32_t)(q > hi) << k;
+            }
+            corner = has_run9(dark) || has_run9(bright);
+        }
+        nb = wave_append(corner, (uint16_t)off, T.lb, nb, lane);
+    }
+    wave_sync();
+    for (int j = lane; j < nb; j += 64) {
+        const int off = T.lb[j];
+        const uint8_t* p = T.win + off;
+        const int v = p[0];
+        int d[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) d[k] = v - p[ring_dy[k] * P + ring_dx[k]];
+        T.sc[off] = (uint8_t)min(arc_strength(d), 255);  // >= t + 1 for a corner
+    }
+    wave_sync();
+    return nb;
+}
+
+// 3x3 strict NMS among the corners (cv::FAST: non-corners and pixels outside
+// the detection region count 0), emitted in lb order = row-major.
+__device__ int nms_emit(const CellTiles& T, int P, int nb, int ox, int t, int lane, int iniX, int iniY,
+                        uint32_t* out, int cap, int* err) {
+    const int t1 = t + 1;
+    int total = 0;
+    for (int base = 0; base < nb; base += 64) {
+        const int j = base + lane;
+        bool keep = false;
+        int s = 0, off = 0;
+        if (j < nb) {
+            off = T.lb[j];
+            const uint8_t* q = T.sc + off;
+            s = q[0];
+            keep = true;
+#pragma unroll
+            for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                for (int dx = -1; dx <= 1; ++dx) {
+                    if (dx == 0 && dy == 0) continue;
+                    const int v = q[dy * P + dx];
+                    keep = keep && (s - 1 > (v >= t1 ? v - 1 : 0));
+                }
+        }
+        const unsigned long long m = __ballot(keep);
+        if (keep) {
+            const int pos = total + __popcll(m & ((1ull << lane) - 1ull));
+            const int r = off / P, c = off - r * P;
+            if (pos < cap)
+                out[pos] = pack_key(iniX + c - ox - kBorder, iniY + r - kBorder, s - 1);
+            else
+                atomicOr(err, kErrCellCap);
+        }
+        total += __popcll(m);
+    }
+    return total;
+}
+
+constexpr int kCellWaves = 4;  // cells (one per wave) in flight per block
+
+__global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int ncells_total,
+                                                                     const uint8_t* __restrict__ img0, size_t row0,
+                                                                     size_t frame0, const uint8_t* __restrict__ pyr,
+                                                                     uint32_t* __restrict__ cand,
+                                                                     int* __restrict__ cell_counts,
+                                                                     int* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int P = g.win_pitch, R = g.win_rows;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t per_wave = ((size_t)2 * P * R + 4 * (size_t)g.det_max + 15) & ~(size_t)15;
+    uint8_t* ws = smem + wave * per_wave;
+    CellTiles T;
+    T.win = ws;
+    T.sc = ws + P * R;
+    T.la = reinterpret_cast<uint16_t*>(ws + 2 * P * R);
+    T.lb = T.la + g.det_max;
+    uint8_t* s_win = ws;
+
+    // one cell per wave; waves of a block take consecutive cells of a frame
+    const int item = blockIdx.x * kCellWaves + wave;
+    if (item >= ncells_total) return;
+    const int f = item / g.total_cells;
+    const int gc = item - f * g.total_cells;
     int l = 0;
     while (l + 1 < g.nlevels && gc >= g.lv[l + 1].cell_base) ++l;
     const LevelGeom& L = g.lv[l];
@@ -82,7 +216,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const uint8_t* _
         return;
     }
     const int maxY = min(iniY + L.hcell + 6, L.max_by), maxX = min(iniX + L.wcell + 6, L.max_bx);
-    const int ww = maxX - iniX, wh = maxY - iniY;
+    const int wh = maxY - iniY;
     const uint8_t* base = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
     const size_t pitch = l == 0 ? row0 : (size_t)L.pitch;
 
@@ -94,82 +228,22 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const uint8_t* _
     for (int idx = lane; idx < nd * wh; idx += 64) {
         const int r = fast_div(idx, mnd), q = idx - r * nd;
         const uint32_t v = *reinterpret_cast<const uint32_t*>(base + (size_t)(iniY + r) * pitch + xa + 4 * q);
-        *reinterpret_cast<uint32_t*>(s_win + r * W + 4 * q) = v;
+        *reinterpret_cast<uint32_t*>(s_win + r * P + 4 * q) = v;
     }
-    for (int idx = lane; idx < W * W / 4; idx += 64) reinterpret_cast<uint32_t*>(s_sc)[idx] = 0u;
-    __syncthreads();
+    for (int idx = lane; idx < P * R / 4; idx += 64) reinterpret_cast<uint32_t*>(T.sc)[idx] = 0u;
+    wave_sync();
 
     // detection region of cv::FAST on the window: rows [3, wh-3), cols [3, ww-3)
-    const int dw = ww - 6, dh = wh - 6;
-    const int tmin = min(g.ini_th, g.min_th);
-    const int ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-    const int ring_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
-    if (dw > 0 && dh > 0) {
-        const uint32_t mdw = (1u << 24) / (uint32_t)dw + 1u;
-        for (int idx = lane; idx < dw * dh; idx += 64) {
-            const int rr = fast_div(idx, mdw);
-            const int r = 3 + rr, x = 3 + ox + (idx - rr * dw);
-            const uint8_t* p = s_win + r * W + x;
-            const int v = p[0];
-            // compass pre-test (ring 0/4/8/12): a 9-arc covers two adjacent ones
-            const int c0 = p[3 * W], c4 = p[3], c8 = p[-3 * W], c12 = p[-3];
-            const int lo = v - tmin, hi = v + tmin;
-            const uint32_t dk = (c0 < lo) | ((c4 < lo) << 1) | ((c8 < lo) << 2) | ((c12 < lo) << 3);
-            const uint32_t br = (c0 > hi) | ((c4 > hi) << 1) | ((c8 > hi) << 2) | ((c12 > hi) << 3);
-            const uint32_t dk2 = dk & ((dk >> 1) | (dk << 3)), br2 = br & ((br >> 1) | (br << 3));
-            if ((dk2 | br2) & 15) {
-                int d[16];
-                uint32_t dark = 0, bright = 0;
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const int q = p[ring_dy[k] * W + ring_dx[k]];
-                    d[k] = v - q;
-                    dark |= (uint32_t)(q < lo) << k;
-                    bright |= (uint32_t)(q > hi) << k;
-                }
-                if (has_run9(dark) || has_run9(bright)) {
-                    const int sc = arc_strength(d);  // >= tmin + 1 here
-                    s_sc[r * W + x] = (uint8_t)min(sc, 255);
-                }
-            }
-        }
-    }
-    __syncthreads();
-
+    const int dw = maxX - iniX - 6, dh = wh - 6;
     int total = 0;
-    for (int pass = 0; pass < 2 && total == 0 && dw > 0 && dh > 0; ++pass) {
-        const int t1 = (pass == 0 ? g.ini_th : g.min_th) + 1;
-        for (int r = 3; r < 3 + dh; ++r) {
-            for (int x0 = 3; x0 < 3 + dw; x0 += 64) {
-                const int x = x0 + lane;
-                bool keep = false;
-                int s = 0;
-                if (x < 3 + dw) {
-                    const uint8_t* q = s_sc + r * W + x + ox;
-                    s = q[0];
-                    if (s >= t1) {
-                        keep = true;
-#pragma unroll
-                        for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-                            for (int dx = -1; dx <= 1; ++dx) {
-                                if (dx == 0 && dy == 0) continue;
-                                const int nb = q[dy * W + dx];
-                                const int nbv = nb >= t1 ? nb - 1 : 0;
-                                keep = keep && (s - 1 > nbv);
-                            }
-                    }
-                }
-                const unsigned long long m = __ballot(keep);
-                if (keep) {
-                    const int pos = total + __popcll(m & ((1ull << lane) - 1ull));
-                    if (pos < L.cell_cap)
-                        out[pos] = pack_key(iniX + x - kBorder, iniY + r - kBorder, s - 1);
-                    else
-                        atomicOr(err, kErrCellCap);
-                }
-                total += __popcll(m);
-            }
+    if (dw > 0 && dh > 0) {
+        int nb = fast_corners(T, P, dw, dh, ox, g.ini_th, lane);
+        total = nms_emit(T, P, nb, ox, g.ini_th, lane, iniX, iniY, out, L.cell_cap, err);
+        if (total == 0) {  // ORBextractor.cpp:821-825: retry the cell at minThFAST
+            for (int j = lane; j < nb; j += 64) T.sc[T.lb[j]] = 0;
+            wave_sync();
+            nb = fast_corners(T, P, dw, dh, ox, g.min_th, lane);
+            total = nms_emit(T, P, nb, ox, g.min_th, lane, iniX, iniY, out, L.cell_cap, err);
         }
     }
     if (lane == 0) *cnt_out = min(total, L.cell_cap);
@@ -180,9 +254,11 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(Geom g, const uint8_t* _
 hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                              const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err,
                              hipStream_t stream) {
-    dim3 grid(g.total_cells, batch);
-    hipLaunchKernelGGL(fast_cells_kernel, grid, dim3(64), 0, stream, g, img0, row0, frame0, pyr, cand,
-                       cell_counts, err);
+    const int items = g.total_cells * batch;
+    const size_t per_wave = ((size_t)2 * g.win_pitch * g.win_rows + 4 * (size_t)g.det_max + 15) & ~(size_t)15;
+    dim3 grid((items + kCellWaves - 1) / kCellWaves);
+    hipLaunchKernelGGL(fast_cells_kernel, grid, dim3(64 * kCellWaves), per_wave * kCellWaves, stream, g, items,
+                       img0, row0, frame0, pyr, cand, cell_counts, err);
     return hipGetLastError();
 }
 

@@ -124,6 +124,8 @@ struct orbgpu_extractor {
     // device buffers
     uint8_t* d_pyr = nullptr;
     size_t pyr_bytes = 0;
+    uint8_t* d_blur = nullptr;
+    size_t blur_bytes = 0;
     int2* d_xtab = nullptr;
     int2* d_ytab = nullptr;
     uint32_t* d_cand = nullptr;
@@ -151,7 +153,7 @@ struct orbgpu_extractor {
     int last_batch = 0;
 
     ~orbgpu_extractor() {
-        void* ptrs[] = {d_pyr, d_xtab, d_ytab, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
+        void* ptrs[] = {d_pyr, d_blur, d_xtab, d_ytab, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
                         d_oct_count, d_err, d_trace, d_img, d_kps1, d_desc1, d_count1};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
@@ -265,6 +267,27 @@ int build_geometry(orbgpu_extractor* e, std::vector<int2>& xtab, std::vector<int
     g.cand_frame = cand_off;
     g.slots_frame = out_off;
     g.max_cells_level = max_cells;
+    size_t blur_off = 0;
+    int tiles = 0;
+    for (int l = 0; l < L; ++l) {
+        LevelGeom& v = g.lv[l];
+        v.blur_frame_bytes = (size_t)v.pitch * v.h;
+        v.blur_offset = blur_off;
+        blur_off += round_up(v.blur_frame_bytes * e->max_batch, 256);
+        v.blur_tiles_x = (v.w + 63) / 64;
+        v.blur_tile_base = tiles;
+        tiles += v.blur_tiles_x * ((v.h + 31) / 32);
+    }
+    g.blur_tiles_frame = tiles;
+    e->blur_bytes = blur_off + 256;  // slack: describe reads 40-byte row spans
+    g.win_pitch = 0;
+    g.win_rows = 0;
+    g.det_max = 0;
+    for (int l = 0; l < L; ++l) {
+        g.win_pitch = std::max(g.win_pitch, (int)round_up((size_t)g.lv[l].wcell + 9, 4));
+        g.win_rows = std::max(g.win_rows, g.lv[l].hcell + 6);
+        g.det_max = std::max(g.det_max, (int)round_up((size_t)g.lv[l].wcell * g.lv[l].hcell, 8));
+    }
     e->pyr_bytes = pyr_off;
     e->max_kps = out_off;
     e->ncap = (int)round_up((size_t)ncap, 16);
@@ -305,8 +328,9 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
     ORB_HIP(launch_octree(g, batch, e->d_cand, e->d_cell_counts, e->d_gkeys, e->d_gknode, e->d_oct_out,
                           e->d_oct_count, e->d_err, e->kcap, e->ncap, e->d_trace, s));
     if (evs) ORB_HIP(hipEventRecord(evs[3], s));
-    ORB_HIP(launch_describe(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_oct_out, e->d_oct_count, kps,
-                            desc, counts, kp_cap, s));
+    ORB_HIP(launch_blur_levels(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_blur, s));
+    ORB_HIP(launch_describe(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_blur, e->d_oct_out, e->d_oct_count,
+                            kps, desc, counts, kp_cap, s));
     if (evs) ORB_HIP(hipEventRecord(evs[4], s));
     e->last_img = imgs;
     e->last_row = row_step;
@@ -375,7 +399,7 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
     const Geom& g = e->g;
     const size_t B = (size_t)max_batch;
     e->img_pitch = round_up((size_t)width, 16);
-    if ((rc = dalloc(&e->d_pyr, e->pyr_bytes)) || (rc = dalloc(&e->d_xtab, xtab.size())) ||
+    if ((rc = dalloc(&e->d_pyr, e->pyr_bytes)) || (rc = dalloc(&e->d_blur, e->blur_bytes)) || (rc = dalloc(&e->d_xtab, xtab.size())) ||
         (rc = dalloc(&e->d_ytab, ytab.size())) || (rc = dalloc(&e->d_cand, g.cand_frame * B)) ||
         (rc = dalloc(&e->d_cell_counts, (size_t)g.total_cells * B)) || (rc = dalloc(&e->d_gkeys, g.cand_frame * B)) ||
         (rc = dalloc(&e->d_gknode, g.cand_frame * B)) || (rc = dalloc(&e->d_oct_out, (size_t)g.slots_frame * B)) ||

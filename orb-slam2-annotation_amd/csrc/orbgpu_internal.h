@@ -52,6 +52,9 @@ struct LevelGeom {
     int out_offset;           // slot offset of this level within a frame
     // resize tables (levels >= 1)
     int xtab_offset, ytab_offset;
+    // blurred level (all levels, incl. 0): same row pitch as the pyramid
+    size_t blur_offset, blur_frame_bytes;
+    int blur_tiles_x, blur_tile_base;   // 64x32 output tiles
 };
 
 struct Geom {
@@ -62,6 +65,9 @@ struct Geom {
     size_t cand_frame;        // u32 candidate slots per frame
     int slots_frame;          // octree output slots per frame (= sum ocap)
     int max_cells_level;
+    int win_pitch, win_rows;  // FAST LDS tile: max over levels of (wCell+9) rounded to 4, (hCell+6)
+    int blur_tiles_frame;     // blur tiles per frame over all levels
+    int det_max;              // max FAST detection-region pixels of a cell (wCell x hCell)
     LevelGeom lv[kMaxLevels];
 };
 

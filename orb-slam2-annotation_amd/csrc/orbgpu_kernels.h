@@ -18,13 +18,16 @@ hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size
                              const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err,
                              hipStream_t stream);
 
+hipError_t launch_blur_levels(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
+                              const uint8_t* pyr, uint8_t* blur, hipStream_t stream);
+
 size_t octree_lds_bytes(const Geom& g, int kcap, int ncap);
 hipError_t launch_octree(const Geom& g, int batch, const uint32_t* cand, const int* cell_counts,
                          uint32_t* gkeys, uint16_t* gknode, uint32_t* oct_out, int* oct_count,
                          int* err, int kcap, int ncap, int* trace, hipStream_t stream);
 
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
-                           const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
+                           const uint8_t* pyr, const uint8_t* blur, const uint32_t* oct_out, const int* oct_count,
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
                            hipStream_t stream);
 
