@@ -5,10 +5,9 @@
 // float path of SymmColumnVec_32s8u) and half-up on the scalar tail
 // (FixedPtCastEx<int,uchar>, 16 bits).
 //
-// One launch over all levels of all frames: 256-thread blocks own a 64x32
-// output tile, stage the 70x38 input (REFLECT_101 on the image border) in
-// LDS, run the row pass into LDS and write 4 output bytes per thread-step.
-// Roofline: HBM streaming (read + write each level once).
+// One launch over all levels of all frames; a thread owns 4 columns x 64
+// rows (see below).  Roofline: HBM streaming (read + write each level once,
+// 6/64 halo rows re-read from L2).
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
 
@@ -16,8 +15,7 @@ namespace orbgpu {
 
 namespace {
 
-constexpr int TW = 64, TH = 32, R = 3;
-constexpr int IW = TW + 2 * R, IH = TH + 2 * R;  // 70 x 38
+constexpr int kStrip = 64;  // output rows per thread
 __constant__ int c_bk[7] = {18, 34, 49, 55, 49, 34, 18};
 
 __device__ inline int reflect101(int p, int n) {
@@ -25,64 +23,79 @@ __device__ inline int reflect101(int p, int n) {
     return p;
 }
 
-__global__ __launch_bounds__(256) void blur_levels_kernel(Geom g, const uint8_t* __restrict__ img0, size_t row0,
+// One thread = 4 adjacent output columns x a 64-row strip of one level.
+// Walking down the strip it keeps the last 7 row-pass results in registers
+// (separable filter as a sliding window), so every input row is read once
+// per strip (+6 halo rows) with three aligned dword loads.
+__global__ __launch_bounds__(256) void blur_levels_kernel(Geom g, int items_frame, int items_total,
+                                                          const uint8_t* __restrict__ img0, size_t row0,
                                                           size_t frame0, const uint8_t* __restrict__ pyr,
                                                           uint8_t* __restrict__ blur) {
-    __shared__ uint8_t s_in[IH * 72];
-    __shared__ uint16_t s_row[IH * TW];
-    const int f = blockIdx.y;
-    const int t = blockIdx.x;
+    const int item = blockIdx.x * 256 + threadIdx.x;
+    if (item >= items_total) return;
+    const int f = item / items_frame;
+    const int it = item - f * items_frame;
     int l = 0;
-    while (l + 1 < g.nlevels && t >= g.lv[l + 1].blur_tile_base) ++l;
+    while (l + 1 < g.nlevels && it >= g.lv[l + 1].blur_tile_base) ++l;
     const LevelGeom& L = g.lv[l];
-    const int tt = t - L.blur_tile_base;
-    const int ty = tt / L.blur_tiles_x, tx = tt - ty * L.blur_tiles_x;
-    const int x0 = tx * TW, y0 = ty * TH;
+    const int k = it - L.blur_tile_base;
+    const int strip = k / L.blur_tiles_x, q = k - strip * L.blur_tiles_x;
+    const int x0 = 4 * q, y0 = strip * kStrip;
+    const int y1 = min(y0 + kStrip, L.h);
     const uint8_t* src = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
     const size_t sp = l == 0 ? row0 : (size_t)L.pitch;
     uint8_t* dst = blur + L.blur_offset + (size_t)f * L.blur_frame_bytes;
-
-    for (int idx = threadIdx.x; idx < IW * IH; idx += 256) {
-        const int r = idx / IW, c = idx - r * IW;
-        const int yy = reflect101(y0 - R + r, L.h), xx = reflect101(x0 - R + c, L.w);
-        s_in[r * 72 + c] = src[(size_t)yy * sp + xx];
-    }
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < IH * TW; idx += 256) {
-        const int r = idx / TW, c = idx - r * TW;
-        const uint8_t* p = s_in + r * 72 + c;
-        int acc = 0;
-#pragma unroll
-        for (int j = 0; j < 7; ++j) acc += c_bk[j] * p[j];
-        s_row[r * TW + c] = (uint16_t)acc;
-    }
-    __syncthreads();
+    const bool interior = x0 >= 4 && x0 + 7 < L.w;  // columns x0-3 .. x0+6 need no reflection
     const int w4 = L.w & ~3;
-    for (int idx = threadIdx.x; idx < TH * (TW / 4); idx += 256) {
-        const int r = idx / (TW / 4), c4 = (idx - r * (TW / 4)) * 4;
-        const int y = y0 + r;
-        if (y >= L.h) continue;
-        uint32_t packed = 0;
+
+    int rp[7][4];  // row-pass sliding window, rows y-3 .. y+3
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int c = c4 + k;
-            int v = 0;
+    for (int i = 0; i < 7; ++i)
 #pragma unroll
-            for (int i = 0; i < 7; ++i) v += c_bk[i] * (int)s_row[(r + i) * TW + c];
-            const int x = x0 + c;
-            int o;
-            if (x < w4) {
-                const int q = v >> 16, rem = v & 0xFFFF;
-                o = q + ((rem > 32768) | ((rem == 32768) & (q & 1)));
-            } else {
-                o = (v + 32768) >> 16;
-            }
-            packed |= (uint32_t)min(o, 255) << (8 * k);
+        for (int c = 0; c < 4; ++c) rp[i][c] = 0;
+    for (int yy = y0 - 3; yy < y1 + 3; ++yy) {
+        const uint8_t* row = src + (size_t)reflect101(yy, L.h) * sp;
+        int px[10];  // level columns x0-3 .. x0+6
+        if (interior) {
+            const uint32_t a = *reinterpret_cast<const uint32_t*>(row + x0 - 4);
+            const uint32_t b = *reinterpret_cast<const uint32_t*>(row + x0);
+            const uint32_t c = *reinterpret_cast<const uint32_t*>(row + x0 + 4);
+            px[0] = (a >> 8) & 255; px[1] = (a >> 16) & 255; px[2] = a >> 24;
+            px[3] = b & 255; px[4] = (b >> 8) & 255; px[5] = (b >> 16) & 255; px[6] = b >> 24;
+            px[7] = c & 255; px[8] = (c >> 8) & 255; px[9] = (c >> 16) & 255;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 10; ++j) px[j] = row[reflect101(x0 - 3 + j, L.w)];
         }
-        const int x = x0 + c4;
-        uint8_t* d = dst + (size_t)y * L.pitch + x;
-        if (x + 3 < L.pitch) {
-            *reinterpret_cast<uint32_t*>(d) = packed;  // pitch is a multiple of 16
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) rp[i][c] = rp[i + 1][c];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            int acc = 0;
+#pragma unroll
+            for (int j = 0; j < 7; ++j) acc += c_bk[j] * px[c + j];
+            rp[6][c] = acc;
+        }
+        const int y = yy - 3;
+        if (y >= y0) {
+            uint32_t packed = 0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                int v = 0;
+#pragma unroll
+                for (int i = 0; i < 7; ++i) v += c_bk[i] * rp[i][c];
+                int o;
+                if (x0 + c < w4) {  // SymmColumnVec_32s8u: float path, round half to even
+                    const int qq = v >> 16, rem = v & 0xFFFF;
+                    o = qq + ((rem > 32768) | ((rem == 32768) & (qq & 1)));
+                } else {            // scalar tail: FixedPtCastEx, round half up
+                    o = (v + 32768) >> 16;
+                }
+                packed |= (uint32_t)min(o, 255) << (8 * c);
+            }
+            *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.pitch + x0) = packed;  // x0+3 < pitch
         }
     }
 }
@@ -91,8 +104,9 @@ __global__ __launch_bounds__(256) void blur_levels_kernel(Geom g, const uint8_t*
 
 hipError_t launch_blur_levels(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                               const uint8_t* pyr, uint8_t* blur, hipStream_t stream) {
-    dim3 grid(g.blur_tiles_frame, batch);
-    hipLaunchKernelGGL(blur_levels_kernel, grid, dim3(256), 0, stream, g, img0, row0, frame0, pyr, blur);
+    const int items = g.blur_tiles_frame * batch;
+    hipLaunchKernelGGL(blur_levels_kernel, dim3((items + 255) / 256), dim3(256), 0, stream, g, g.blur_tiles_frame,
+                       items, img0, row0, frame0, pyr, blur);
     return hipGetLastError();
 }
 

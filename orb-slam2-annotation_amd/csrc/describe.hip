@@ -13,6 +13,8 @@
 #include "orbgpu_kernels.h"
 #include "../../include/orbgpu.h"
 
+#include <algorithm>
+
 namespace orbgpu {
 
 namespace {
@@ -102,17 +104,20 @@ __device__ inline int wave_sum(int v) {
 constexpr int kDiscPitch = 36;   // 31-px disc rows, staged from a 4-aligned column
 constexpr int kBPitch = 40;      // 37-px blurred rows, staged from a 4-aligned column
 
-__global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __restrict__ img0, size_t row0,
-                                                      size_t frame0, const uint8_t* __restrict__ pyr,
-                                                      const uint8_t* __restrict__ blur,
-                                                      const uint32_t* __restrict__ oct_out,
-                                                      const int* __restrict__ oct_count,
-                                                      orbgpu_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
-                                                      int* __restrict__ counts, int kp_cap) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_disc[31 * kDiscPitch];
-    __shared__ __attribute__((aligned(16))) uint8_t s_blur[kBlur * kBPitch];
-    const int lane = threadIdx.x;
-    const int f = blockIdx.y, slot = blockIdx.x;
+// The 4 waves of a block process different keypoints: stages are ordered
+// with a wave-local LDS fence, never a block barrier.
+__device__ inline void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ void describe_one(const Geom& g, int f, int slot, int lane, uint8_t* s_disc, uint8_t* s_blur,
+                             const uint8_t* __restrict__ img0, size_t row0, size_t frame0,
+                             const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
+                             const uint32_t* __restrict__ oct_out, const int* __restrict__ oct_count,
+                             orbgpu_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                             int* __restrict__ counts, int kp_cap) {
     int l = 0;
     while (l + 1 < g.nlevels && slot >= g.lv[l + 1].out_offset) ++l;
     const LevelGeom& L = g.lv[l];
@@ -156,7 +161,7 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
         *reinterpret_cast<uint32_t*>(s_blur + r * kBPitch + 4 * q) =
             *reinterpret_cast<const uint32_t*>(bl + (size_t)(cy - kBlurR + r) * L.pitch + xb + 4 * q);
     }
-    __syncthreads();
+    wave_sync();
 
     // intensity centroid over the disc (integer moments: order-free)
     int m10 = 0, m01 = 0;
@@ -208,15 +213,39 @@ __global__ __launch_bounds__(64) void describe_kernel(Geom g, const uint8_t* __r
     }
 }
 
+constexpr int kDescWaves = 4;
+
+// One wave per (frame, slot) item, four items per block (fewer, larger
+// workgroups than one wave per block: the 1-wave form was dispatch-bound).
+__global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int items,
+                                                                   const uint8_t* __restrict__ img0, size_t row0,
+                                                                   size_t frame0, const uint8_t* __restrict__ pyr,
+                                                                   const uint8_t* __restrict__ blur,
+                                                                   const uint32_t* __restrict__ oct_out,
+                                                                   const int* __restrict__ oct_count,
+                                                                   orbgpu_keypoint* __restrict__ kps,
+                                                                   uint8_t* __restrict__ desc,
+                                                                   int* __restrict__ counts, int kp_cap) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_disc[kDescWaves][31 * kDiscPitch];
+    __shared__ __attribute__((aligned(16))) uint8_t s_blur[kDescWaves][kBlur * kBPitch];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int item = blockIdx.x * kDescWaves + wave;
+    if (item >= items) return;
+    const int f = item / g.slots_frame, slot = item - f * g.slots_frame;
+    describe_one(g, f, slot, lane, s_disc[wave], s_blur[wave], img0, row0, frame0, pyr, blur, oct_out, oct_count,
+                 kps, desc, counts, kp_cap);
+}
+
 }  // namespace
 
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                            const uint8_t* pyr, const uint8_t* blur, const uint32_t* oct_out, const int* oct_count,
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
                            hipStream_t stream) {
-    dim3 grid(g.slots_frame, batch);
-    hipLaunchKernelGGL(describe_kernel, grid, dim3(64), 0, stream, g, img0, row0, frame0, pyr, blur, oct_out,
-                       oct_count, kps, desc, counts, kp_cap);
+    const int items = g.slots_frame * batch;
+    const int blocks = (items + kDescWaves - 1) / kDescWaves;
+    hipLaunchKernelGGL(describe_kernel, dim3(blocks), dim3(64 * kDescWaves), 0, stream, g, items, img0, row0, frame0,
+                       pyr, blur, oct_out, oct_count, kps, desc, counts, kp_cap);
     return hipGetLastError();
 }
 

@@ -274,9 +274,9 @@ int build_geometry(orbgpu_extractor* e, std::vector<int2>& xtab, std::vector<int
         v.blur_frame_bytes = (size_t)v.pitch * v.h;
         v.blur_offset = blur_off;
         blur_off += round_up(v.blur_frame_bytes * e->max_batch, 256);
-        v.blur_tiles_x = (v.w + 63) / 64;
+        v.blur_tiles_x = (v.w + 3) / 4;
         v.blur_tile_base = tiles;
-        tiles += v.blur_tiles_x * ((v.h + 31) / 32);
+        tiles += v.blur_tiles_x * ((v.h + 63) / 64);
     }
     g.blur_tiles_frame = tiles;
     e->blur_bytes = blur_off + 256;  // slack: describe reads 40-byte row spans

@@ -54,7 +54,7 @@ struct LevelGeom {
     int xtab_offset, ytab_offset;
     // blurred level (all levels, incl. 0): same row pitch as the pyramid
     size_t blur_offset, blur_frame_bytes;
-    int blur_tiles_x, blur_tile_base;   // 64x32 output tiles
+    int blur_tiles_x, blur_tile_base;   // blur work items: 4-column x 64-row strips
 };
 
 struct Geom {
