@@ -123,24 +123,30 @@ int orbgpu_extractor_copy_level(orbgpu_extractor* ex, int frame, int level, uint
  * descriptor pairs resident in HBM: d_dist[i] = popcount(a_i xor b_i). */
 int orbgpu_hamming_pairs_device(const uint8_t* d_a, const uint8_t* d_b, int n, int* d_dist, void* stream);
 
+/* Frame image bounds of the 64x48 feature grid: Frame::mnMinX, mnMaxX,
+ * mnMinY, mnMaxY (Frame.cpp:505-530; [0,cols]x[0,rows] without distortion). */
+typedef struct orbgpu_grid_bounds {
+    float min_x, max_x, min_y, max_y;
+} orbgpu_grid_bounds;
+
 /* ORBmatcher(nnratio, checkOri).SearchForInitialization(F1, F2,
  * vbPrevMatched, vnMatches12, windowSize) (ORBmatcher.h:60,
- * ORBmatcher.cpp:474-590) for frames without distortion (mvKeysUn ==
- * mvKeys, image bounds [0,W]x[0,H], Frame.cpp:525-529), batched over pairs.
+ * ORBmatcher.cpp:474-590), batched over pairs; keypoints are F.mvKeysUn and
+ * F2's grid is Frame::AssignFeaturesToGrid over `bounds` (Frame.cpp:241-259).
  * Pair b: F1 keypoints d_kps1 + b*stride1 (count d_n1[b], levels in
  * extractor order), descriptors d_desc1 + b*stride1*32; same for F2.
  * d_prev_xy (nullable): float2 per F1 keypoint at + b*stride1*2, read and
  * updated (vbPrevMatched); NULL means vbPrevMatched = F1 positions.
  * d_matches12: int per F1 keypoint at + b*stride1; d_nmatches[b]. */
 int orbgpu_search_for_initialization_batch_device(
-    int batch, int img_width, int img_height,
+    int batch, orbgpu_grid_bounds bounds,
     const orbgpu_keypoint* d_kps1, const uint8_t* d_desc1, const int* d_n1, size_t stride1,
     const orbgpu_keypoint* d_kps2, const uint8_t* d_desc2, const int* d_n2, size_t stride2,
     float* d_prev_xy, int window, float nnratio, int flags,
     int* d_matches12, int* d_nmatches, void* stream);
 
 /* Host-pointer convenience form for one pair; returns nmatches in *n. */
-int orbgpu_search_for_initialization(int img_width, int img_height,
+int orbgpu_search_for_initialization(orbgpu_grid_bounds bounds,
                                      const orbgpu_keypoint* kps1, const uint8_t* desc1, int n1,
                                      const orbgpu_keypoint* kps2, const uint8_t* desc2, int n2,
                                      float* prev_xy, int window, float nnratio, int flags,

@@ -703,11 +703,10 @@ float orbref_ic_angle(const uint8_t* img, size_t step, int cx, int cy) {
 
 int orbref_search_for_initialization(const orbref_kp* k1, const uint8_t* d1, int n1,
                                      const orbref_kp* k2, const uint8_t* d2, int n2,
-                                     int img_w, int img_h, float* prev, int window, float nnratio,
+                                     float minX, float maxX, float minY, float maxY,
+                                     float* prev, int window, float nnratio,
                                      int check_ori, int histo_bug, int* m12) {
     enum { GC = 64, GR = 48, HL = 30, TH_LOW = 50 };
-    // Frame ctor, no distortion: bounds [0, cols] x [0, rows] (F:525-529)
-    const float minX = 0.f, maxX = (float)img_w, minY = 0.f, maxY = (float)img_h;
     const float invW = (float)GC / (maxX - minX), invH = (float)GR / (maxY - minY);
     std::vector<std::vector<int>> grid(GC * GR);
     for (int i = 0; i < n2; ++i) {  // AssignFeaturesToGrid / PosInGrid (F:241-259, 434-443)

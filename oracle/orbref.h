@@ -89,7 +89,8 @@ float orbref_ic_angle(const uint8_t* img, size_t step, int cx, int cy);
  * factor 1/HISTO_LENGTH instead of HISTO_LENGTH/360.  Returns nmatches. */
 int orbref_search_for_initialization(const orbref_kp* kps1, const uint8_t* desc1, int n1,
                                      const orbref_kp* kps2, const uint8_t* desc2, int n2,
-                                     int img_w, int img_h, float* prev_xy, int window,
+                                     float min_x, float max_x, float min_y, float max_y,
+                                     float* prev_xy, int window,
                                      float nnratio, int check_ori, int histo_bug,
                                      int* matches12);
 

@@ -58,7 +58,7 @@ def lib() -> ctypes.CDLL:
         L.orbref_orb_descriptor.argtypes = [vp, sz, i, i, f, vp]
         L.orbref_ic_angle.restype = f
         L.orbref_ic_angle.argtypes = [vp, sz, i, i]
-        L.orbref_search_for_initialization.argtypes = [vp, vp, i, vp, vp, i, i, i, vp, i, f, i, i, vp]
+        L.orbref_search_for_initialization.argtypes = [vp, vp, i, vp, vp, i, f, f, f, f, vp, i, f, i, i, vp]
         _LIB = L
     return _LIB
 
@@ -152,8 +152,9 @@ def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
 
 
 def search_for_initialization(kps1, desc1, kps2, desc2, img_w, img_h, prev_xy=None,
-                              window=100, nnratio=0.9, check_ori=True, histo_bug=False):
-    """Returns (nmatches, matches12, prev_xy_updated)."""
+                              window=100, nnratio=0.9, check_ori=True, histo_bug=False, bounds=None):
+    """Returns (nmatches, matches12, prev_xy_updated).  bounds = (minX, maxX,
+    minY, maxY), default the undistorted frame [0, img_w] x [0, img_h]."""
     kps1 = np.ascontiguousarray(kps1, KP_DTYPE)
     kps2 = np.ascontiguousarray(kps2, KP_DTYPE)
     desc1 = np.ascontiguousarray(desc1, np.uint8)
@@ -162,7 +163,8 @@ def search_for_initialization(kps1, desc1, kps2, desc2, img_w, img_h, prev_xy=No
         prev_xy = np.stack([kps1["x"], kps1["y"]], axis=1).astype(np.float32)
     prev = np.ascontiguousarray(prev_xy, np.float32).copy()
     m12 = np.full(len(kps1), -1, np.int32)
+    b = bounds if bounds is not None else (0.0, float(img_w), 0.0, float(img_h))
     n = lib().orbref_search_for_initialization(_p(kps1), _p(desc1), len(kps1), _p(kps2), _p(desc2), len(kps2),
-                                               img_w, img_h, _p(prev), window, nnratio, int(check_ori),
+                                               *[float(v) for v in b], _p(prev), window, nnratio, int(check_ori),
                                                int(histo_bug), _p(m12))
     return n, m12, prev

@@ -50,7 +50,7 @@ __device__ int level0_count(const orbgpu_keypoint* k, int n) {
     return lo;
 }
 
-__global__ __launch_bounds__(64) void match_init_kernel(int img_w, int img_h,
+__global__ __launch_bounds__(64) void match_init_kernel(float minX, float maxX, float minY, float maxY,
                                                         const orbgpu_keypoint* __restrict__ kps1,
                                                         const uint8_t* __restrict__ desc1, const int* __restrict__ n1p,
                                                         size_t stride1, const orbgpu_keypoint* __restrict__ kps2,
@@ -83,8 +83,7 @@ __global__ __launch_bounds__(64) void match_init_kernel(int img_w, int img_h,
         for (int i = lane; i < n1; i += 64) M12[i] = -1;
         return;
     }
-    // Frame bounds without distortion and grid inverses (Frame.cpp:221-224, 525-529)
-    const float minX = 0.f, minY = 0.f, maxX = (float)img_w, maxY = (float)img_h;
+    // grid inverses (Frame.cpp:221-224)
     const float invW = __fdiv_rn((float)kGC, __fsub_rn(maxX, minX));
     const float invH = __fdiv_rn((float)kGR, __fsub_rn(maxY, minY));
     for (int j = lane; j < n20; j += 64) {
@@ -218,12 +217,12 @@ hipError_t launch_hamming_pairs(const uint8_t* a, const uint8_t* b, int n, int* 
     return hipGetLastError();
 }
 
-hipError_t launch_match_init(int batch, int img_w, int img_h,
+hipError_t launch_match_init(int batch, float minX, float maxX, float minY, float maxY,
                              const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,
                              const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2, size_t stride2,
                              float* prev_xy, int window, float nnratio, int flags,
                              int* matches12, int* nmatches, int* err, hipStream_t stream) {
-    hipLaunchKernelGGL(match_init_kernel, dim3(batch), dim3(64), 0, stream, img_w, img_h, kps1, desc1, n1, stride1,
+    hipLaunchKernelGGL(match_init_kernel, dim3(batch), dim3(64), 0, stream, minX, maxX, minY, maxY, kps1, desc1, n1, stride1,
                        kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags, matches12, nmatches, err);
     return hipGetLastError();
 }

@@ -554,23 +554,23 @@ static int match_err_word(int** p) {
     return ORBGPU_OK;
 }
 
-int orbgpu_search_for_initialization_batch_device(int batch, int img_w, int img_h, const orbgpu_keypoint* kps1,
+int orbgpu_search_for_initialization_batch_device(int batch, orbgpu_grid_bounds bd, const orbgpu_keypoint* kps1,
                                                   const uint8_t* desc1, const int* n1, size_t stride1,
                                                   const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2,
                                                   size_t stride2, float* prev_xy, int window, float nnratio,
                                                   int flags, int* matches12, int* nmatches, void* stream) {
-    if (batch <= 0 || !kps1 || !kps2 || !desc1 || !desc2 || !n1 || !n2 || !matches12 || !nmatches || img_w <= 0 ||
-        img_h <= 0)
+    if (batch <= 0 || !kps1 || !kps2 || !desc1 || !desc2 || !n1 || !n2 || !matches12 || !nmatches ||
+        !(bd.max_x > bd.min_x) || !(bd.max_y > bd.min_y))
         return fail(ORBGPU_ERR_ARG, "invalid argument");
     int* err = nullptr;
     int rc = match_err_word(&err);
     if (rc) return rc;
-    ORB_HIP(launch_match_init(batch, img_w, img_h, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy,
+    ORB_HIP(launch_match_init(batch, bd.min_x, bd.max_x, bd.min_y, bd.max_y, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy,
                               window, nnratio, flags, matches12, nmatches, err, (hipStream_t)stream));
     return ORBGPU_OK;
 }
 
-int orbgpu_search_for_initialization(int img_w, int img_h, const orbgpu_keypoint* kps1, const uint8_t* desc1,
+int orbgpu_search_for_initialization(orbgpu_grid_bounds bd, const orbgpu_keypoint* kps1, const uint8_t* desc1,
                                      int n1, const orbgpu_keypoint* kps2, const uint8_t* desc2, int n2,
                                      float* prev_xy, int window, float nnratio, int flags, int* matches12,
                                      int* nmatches) {
@@ -603,7 +603,7 @@ int orbgpu_search_for_initialization(int img_w, int img_h, const orbgpu_keypoint
               hipMemcpy(dn, ns, 2 * sizeof(int), hipMemcpyHostToDevice) == hipSuccess &&
               (!prev_xy || hipMemcpy(dp, prev_xy, (size_t)n1 * 2 * sizeof(float), hipMemcpyHostToDevice) == hipSuccess);
     if (!ok) { cleanup(); return fail(ORBGPU_ERR_HIP, "upload failed"); }
-    rc = orbgpu_search_for_initialization_batch_device(1, img_w, img_h, dk1, dd1, dn, n1c, dk2, dd2, dn + 1, n2c, dp,
+    rc = orbgpu_search_for_initialization_batch_device(1, bd, dk1, dd1, dn, n1c, dk2, dd2, dn + 1, n2c, dp,
                                                        window, nnratio, flags, dm, dn + 2, nullptr);
     if (rc) { cleanup(); return rc; }
     int err = 0;

@@ -31,7 +31,7 @@ hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
                            hipStream_t stream);
 
-hipError_t launch_match_init(int batch, int img_w, int img_h,
+hipError_t launch_match_init(int batch, float minX, float maxX, float minY, float maxY,
                              const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,
                              const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2, size_t stride2,
                              float* prev_xy, int window, float nnratio, int flags,

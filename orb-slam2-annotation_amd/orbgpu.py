@@ -37,6 +37,17 @@ class OrbGpuError(RuntimeError):
         self.code = code
 
 
+class GridBounds(ctypes.Structure):
+    """Frame::mnMinX, mnMaxX, mnMinY, mnMaxY (Frame.cpp:505-530)."""
+    _fields_ = [("min_x", ctypes.c_float), ("max_x", ctypes.c_float),
+                ("min_y", ctypes.c_float), ("max_y", ctypes.c_float)]
+
+
+def bounds_for(img_w, img_h) -> GridBounds:
+    """Grid bounds of an undistorted frame: [0, cols] x [0, rows]."""
+    return GridBounds(0.0, float(img_w), 0.0, float(img_h))
+
+
 class _Info(ctypes.Structure):
     _fields_ = [("nlevels", ctypes.c_int), ("width", ctypes.c_int), ("height", ctypes.c_int),
                 ("max_batch", ctypes.c_int), ("max_keypoints", ctypes.c_int),
@@ -65,11 +76,11 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_extractor_copy_level.argtypes = [vp, i, i, vp, sz]
         L.orbgpu_hamming_pairs_device.argtypes = [vp, vp, i, vp, vp]
         L.orbgpu_search_for_initialization_batch_device.argtypes = [
-            i, i, i, vp, vp, vp, sz, vp, vp, vp, sz, vp, i, f, i, vp, vp, vp]
+            i, GridBounds, vp, vp, vp, sz, vp, vp, vp, sz, vp, i, f, i, vp, vp, vp]
         L.orbgpu_debug_level_candidates.argtypes = [vp, i, i, vp, i]
         L.orbgpu_debug_level_octree.argtypes = [vp, i, i, vp, i]
         L.orbgpu_debug_octree_trace.argtypes = [vp, i, vp, i]
-        L.orbgpu_search_for_initialization.argtypes = [i, i, vp, vp, i, vp, vp, i, vp, i, f, i, vp,
+        L.orbgpu_search_for_initialization.argtypes = [GridBounds, vp, vp, i, vp, vp, i, vp, i, f, i, vp,
                                                        ctypes.POINTER(i)]
         _LIB = L
     return _LIB
@@ -218,8 +229,9 @@ def keypoints_from_raw(raw: np.ndarray) -> np.ndarray:
 
 
 def search_for_initialization(kps1, desc1, kps2, desc2, img_w, img_h, prev_xy=None, window=100,
-                              nnratio=0.9, check_ori=True, annotated_histo=False):
-    """Host form: returns (nmatches, matches12, prev_xy_updated)."""
+                              nnratio=0.9, check_ori=True, annotated_histo=False, bounds=None):
+    """Host form: returns (nmatches, matches12, prev_xy_updated).  bounds
+    defaults to the undistorted frame [0, img_w] x [0, img_h]."""
     kps1 = np.ascontiguousarray(kps1, KP_DTYPE)
     kps2 = np.ascontiguousarray(kps2, KP_DTYPE)
     desc1 = np.ascontiguousarray(desc1, np.uint8)
@@ -230,7 +242,8 @@ def search_for_initialization(kps1, desc1, kps2, desc2, img_w, img_h, prev_xy=No
     m12 = np.full(max(len(kps1), 1), -1, np.int32)
     n = ctypes.c_int()
     flags = (MATCH_CHECK_ORI if check_ori else 0) | (MATCH_ANNOTATED_HISTO if annotated_histo else 0)
-    _check(lib().orbgpu_search_for_initialization(img_w, img_h, kps1.ctypes.data, desc1.ctypes.data, len(kps1),
+    bd = bounds if bounds is not None else bounds_for(img_w, img_h)
+    _check(lib().orbgpu_search_for_initialization(bd, kps1.ctypes.data, desc1.ctypes.data, len(kps1),
                                                   kps2.ctypes.data, desc2.ctypes.data, len(kps2),
                                                   prev.ctypes.data, window, nnratio, flags,
                                                   m12.ctypes.data, ctypes.byref(n)),
@@ -239,11 +252,13 @@ def search_for_initialization(kps1, desc1, kps2, desc2, img_w, img_h, prev_xy=No
 
 
 def search_for_initialization_batch(img_w, img_h, kps1, desc1, n1, kps2, desc2, n2, matches12, nmatches,
-                                    prev_xy=None, window=100, nnratio=0.9, flags=MATCH_CHECK_ORI, stream=None):
+                                    prev_xy=None, window=100, nnratio=0.9, flags=MATCH_CHECK_ORI, stream=None,
+                                    bounds=None):
     """Device form over B pairs (tensors on the GPU, see include/orbgpu.h)."""
     B = n2.shape[0]
+    bd = bounds if bounds is not None else bounds_for(img_w, img_h)
     _check(lib().orbgpu_search_for_initialization_batch_device(
-        B, img_w, img_h, _ptr(kps1), _ptr(desc1), _ptr(n1), desc1.shape[1], _ptr(kps2), _ptr(desc2), _ptr(n2),
+        B, bd, _ptr(kps1), _ptr(desc1), _ptr(n1), desc1.shape[1], _ptr(kps2), _ptr(desc2), _ptr(n2),
         desc2.shape[1], _ptr(prev_xy) if prev_xy is not None else None, window, nnratio, flags,
         _ptr(matches12), _ptr(nmatches), _stream_ptr(stream)), "orbgpu_search_for_initialization_batch_device")
 

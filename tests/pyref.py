@@ -197,3 +197,107 @@ def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
 def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
     """ORBmatcher::DescriptorDistance (ORBmatcher.cpp:1838): popcount(a^b)."""
     return int(np.unpackbits(np.bitwise_xor(a, b)).sum())
+
+
+def search_for_initialization(k1, d1, k2, d2, bounds, prev_xy, window=100, nnratio=0.9, check_ori=True,
+                              histo_factor=None):
+    """ORBmatcher::SearchForInitialization (ORBmatcher.cpp:474-590) with the
+    grid of Frame::AssignFeaturesToGrid / PosInGrid (Frame.cpp:241-259,
+    434-443), Frame::GetFeaturesInArea (Frame.cpp:379-432) and
+    ComputeThreeMaxima (ORBmatcher.cpp:1790-1835).  Float arithmetic in
+    numpy float32 scalars; k1/k2 are KP_DTYPE arrays (mvKeysUn).  Returns
+    (nmatches, matches12, prev_xy_updated)."""
+    f32 = np.float32
+    GC, GR, TH_LOW, HL = 64, 48, 50, 30
+    minX, maxX, minY, maxY = (f32(v) for v in bounds)
+    invW, invH = f32(GC) / f32(maxX - minX), f32(GR) / f32(maxY - minY)
+    grid = [[[] for _ in range(GR)] for _ in range(GC)]
+    for i in range(len(k2)):
+        # C round(): half away from zero
+        px = int(math.copysign(math.floor(abs(float(f32(f32(k2["x"][i]) - minX) * invW)) + 0.5),
+                               float(f32(f32(k2["x"][i]) - minX) * invW)))
+        py = int(math.copysign(math.floor(abs(float(f32(f32(k2["y"][i]) - minY) * invH)) + 0.5),
+                               float(f32(f32(k2["y"][i]) - minY) * invH)))
+        if 0 <= px < GC and 0 <= py < GR:
+            grid[px][py].append(i)
+    # all-pairs Hamming distances (DescriptorDistance, ORBmatcher.cpp:1838)
+    dist = np.unpackbits(np.bitwise_xor(d1[:, None, :], d2[None, :, :]), axis=2).sum(axis=2).astype(int) \
+        if len(k1) and len(k2) else np.zeros((len(k1), len(k2)), int)
+    prev = np.array(prev_xy, np.float32, copy=True)
+    m12 = [-1] * len(k1)
+    m21 = [-1] * len(k2)
+    mdist = [2 ** 31 - 1] * len(k2)
+    hist = [[] for _ in range(HL)]
+    factor = f32(HL) / f32(360.0) if histo_factor is None else f32(histo_factor)
+    r = f32(window)
+    nm = 0
+    for i1 in range(len(k1)):
+        if k1["octave"][i1] > 0:
+            continue
+        x, y = prev[i1, 0], prev[i1, 1]
+        cx0 = max(0, int(math.floor(f32(f32(x - minX) - r) * invW)))
+        cx1 = min(GC - 1, int(math.ceil(f32(f32(x - minX) + r) * invW)))
+        cy0 = max(0, int(math.floor(f32(f32(y - minY) - r) * invH)))
+        cy1 = min(GR - 1, int(math.ceil(f32(f32(y - minY) + r) * invH)))
+        if cx0 >= GC or cx1 < 0 or cy0 >= GR or cy1 < 0:
+            continue
+        cand = []
+        for ix in range(cx0, cx1 + 1):
+            for iy in range(cy0, cy1 + 1):
+                for j in grid[ix][iy]:
+                    if k2["octave"][j] != 0:
+                        continue
+                    if abs(f32(k2["x"][j] - x)) < r and abs(f32(k2["y"][j] - y)) < r:
+                        cand.append(j)
+        if not cand:
+            continue
+        best, best2, bidx = 2 ** 31 - 1, 2 ** 31 - 1, -1
+        for j in cand:
+            dd = int(dist[i1, j])
+            if mdist[j] <= dd:
+                continue
+            if dd < best:
+                best2, best, bidx = best, dd, j
+            elif dd < best2:
+                best2 = dd
+        if best <= TH_LOW and f32(best) < f32(f32(best2) * f32(nnratio)):
+            if m21[bidx] >= 0:
+                m12[m21[bidx]] = -1
+                nm -= 1
+            m12[i1], m21[bidx], mdist[bidx] = bidx, i1, best
+            nm += 1
+            if check_ori:
+                rot = f32(f32(k1["angle"][i1]) - f32(k2["angle"][bidx]))
+                if rot < 0.0:
+                    rot = f32(rot + f32(360.0))
+                v = float(f32(rot * factor))
+                b = int(math.copysign(math.floor(abs(v) + 0.5), v))
+                if b == HL:
+                    b = 0
+                hist[b].append(i1)
+    if check_ori:
+        m1 = m2 = m3 = 0
+        i1_ = i2_ = i3_ = -1
+        for i in range(HL):
+            s = len(hist[i])
+            if s > m1:
+                m3, m2, m1, i3_, i2_, i1_ = m2, m1, s, i2_, i1_, i
+            elif s > m2:
+                m3, m2, i3_, i2_ = m2, s, i2_, i
+            elif s > m3:
+                m3, i3_ = s, i
+        if m2 < f32(0.1) * f32(m1):
+            i2_ = i3_ = -1
+        elif m3 < f32(0.1) * f32(m1):
+            i3_ = -1
+        for i in range(HL):
+            if i in (i1_, i2_, i3_):
+                continue
+            for a in hist[i]:
+                if m12[a] >= 0:
+                    m12[a] = -1
+                    nm -= 1
+    for i in range(len(k1)):
+        if m12[i] >= 0:
+            prev[i, 0], prev[i, 1] = k2["x"][m12[i]], k2["y"][m12[i]]
+    return nm, np.array(m12, np.int32), prev

@@ -123,6 +123,28 @@ def test_search_for_initialization(mono_frames, check_ori, annotated):
     np.testing.assert_array_equal(p_g.view(np.uint32), p_r.view(np.uint32))
 
 
+def test_search_for_initialization_distorted_bounds(mono_frames):
+    """Undistorted keypoints (mvKeysUn) with Frame bounds other than
+    [0,W]x[0,H]: some keypoints fall outside the grid (PosInGrid rejects
+    them, Frame.cpp:434-443)."""
+    og = _gpu()
+    ref = orbref.Extractor()
+    k1, d1 = ref.extract(mono_frames[0])
+    k2, d2 = ref.extract(mono_frames[1])
+    for k in (k1, k2):  # a radial-ish warp standing in for cv::undistortPoints
+        dx, dy = k["x"] - 320.0, k["y"] - 240.0
+        r2 = (dx * dx + dy * dy).astype(np.float32) * np.float32(2e-7)
+        k["x"] = (np.float32(320.0) + dx * (np.float32(1.0) + r2)).astype(np.float32)
+        k["y"] = (np.float32(240.0) + dy * (np.float32(1.0) + r2)).astype(np.float32)
+    bounds = (-7.25, 631.5, -3.0, 470.75)
+    n_r, m_r, p_r = orbref.search_for_initialization(k1, d1, k2, d2, 640, 480, bounds=bounds)
+    n_g, m_g, p_g = og.search_for_initialization(k1, d1, k2, d2, 640, 480, bounds=og.GridBounds(*bounds))
+    assert n_r > 100
+    assert n_g == n_r
+    np.testing.assert_array_equal(m_g, m_r)
+    np.testing.assert_array_equal(p_g.view(np.uint32), p_r.view(np.uint32))
+
+
 @pytest.mark.parametrize("w,h,nf", [(640, 480, 1000), (1241, 376, 2000), (752, 480, 1200)])
 def test_stages_candidates_and_octree(w, h, nf):
     """Stage-level parity: FAST candidates and octree output per level."""

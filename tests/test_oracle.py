@@ -190,3 +190,34 @@ def test_matcher_invariants():
         assert prev[i, 0] == k2["x"][m12[i]]
     n0, m0, _ = orbref.search_for_initialization(k1, d1, k2, d2, 640, 480, check_ori=False)
     assert n0 >= n
+
+
+def _warp(k):
+    """A radial warp standing in for cv::undistortPoints (mvKeysUn != mvKeys)."""
+    k = k.copy()
+    dx, dy = k["x"] - np.float32(320.0), k["y"] - np.float32(240.0)
+    r2 = (dx * dx + dy * dy).astype(np.float32) * np.float32(2e-7)
+    k["x"] = (np.float32(320.0) + dx * (np.float32(1.0) + r2)).astype(np.float32)
+    k["y"] = (np.float32(240.0) + dy * (np.float32(1.0) + r2)).astype(np.float32)
+    return k
+
+
+@pytest.mark.parametrize("warp,bounds,check_ori", [(False, (0.0, 640.0, 0.0, 480.0), True),
+                                                   (False, (0.0, 640.0, 0.0, 480.0), False),
+                                                   (True, (-7.25, 631.5, -3.0, 470.75), True)])
+def test_matcher_oracle_vs_python_restatement(warp, bounds, check_ori):
+    """oracle SearchForInitialization == the independent restatement in pyref
+    (also covers Frame bounds other than the image rectangle)."""
+    fr = synth.mono_stream(2)
+    ex = orbref.Extractor()
+    k1, d1 = ex.extract(fr[0])
+    k2, d2 = ex.extract(fr[1])
+    if warp:
+        k1, k2 = _warp(k1), _warp(k2)
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    n_r, m_r, p_r = orbref.search_for_initialization(k1, d1, k2, d2, 640, 480, check_ori=check_ori,
+                                                     bounds=bounds)
+    n_p, m_p, p_p = pyref.search_for_initialization(k1, d1, k2, d2, bounds, prev, check_ori=check_ori)
+    assert n_r == n_p > 50
+    np.testing.assert_array_equal(m_r, m_p)
+    np.testing.assert_array_equal(p_r.view(np.uint32), p_p.view(np.uint32))
