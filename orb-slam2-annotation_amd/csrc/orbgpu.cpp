@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <cstdint>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -126,8 +127,10 @@ struct orbgpu_extractor {
     size_t pyr_bytes = 0;
     uint8_t* d_blur = nullptr;
     size_t blur_bytes = 0;
-    int2* d_xtab = nullptr;
+    int4* d_ptab = nullptr;
     int2* d_ytab = nullptr;
+    std::vector<int4> pyr_bands;   // host copy of the band table
+    int4* d_pyr_bands = nullptr;
     uint32_t* d_cand = nullptr;
     int* d_cell_counts = nullptr;
     uint32_t* d_gkeys = nullptr;
@@ -153,7 +156,7 @@ struct orbgpu_extractor {
     int last_batch = 0;
 
     ~orbgpu_extractor() {
-        void* ptrs[] = {d_pyr, d_blur, d_xtab, d_ytab, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
+        void* ptrs[] = {d_pyr, d_blur, d_ptab, d_ytab, d_pyr_bands, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
                         d_oct_count, d_err, d_trace, d_img, d_kps1, d_desc1, d_count1};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
@@ -165,8 +168,81 @@ struct orbgpu_extractor {
 
 namespace {
 
+// Row bands of the fused pyramid pass (pyramid.hip).  Band s owns rows
+// [ceil(s*h_l/S), ceil((s+1)*h_l/S)) of every level l and computes the rows it
+// owns plus the rows its next level's computed rows read (ytab is monotone,
+// so that is one contiguous range per level).  S is the smallest band count
+// whose two LDS ping-pong buffers fit 80 KiB (two blocks per CU), raised
+// while the batch alone would not fill the chip.
+int plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, int max_batch, std::vector<int4>& table) {
+    const int L = g.nlevels;
+    table.clear();
+    if (L < 2) {
+        g.pyr_bands = 1;
+        table.assign(L, int4{0, 0, 0, 0});
+        return ORBGPU_OK;
+    }
+    auto plan = [&](int S, std::vector<int4>& t, int& lds_a, int& lds_b, int& lds_y) {
+        t.assign((size_t)S * L, int4{0, 0, 0, 0});
+        lds_a = lds_b = lds_y = 0;
+        for (int s = 0; s < S; ++s) {
+            int4* b = &t[(size_t)s * L];
+            for (int l = 0; l < L; ++l) {
+                const int h = g.lv[l].h;
+                b[l].z = (int)(((long)s * h + S - 1) / S);
+                b[l].w = (int)(((long)(s + 1) * h + S - 1) / S);
+            }
+            b[L - 1].x = b[L - 1].z;
+            b[L - 1].y = b[L - 1].w;
+            for (int l = L - 1; l >= 1; --l) {
+                int lo = b[l].x, hi = b[l].y;
+                int slo = INT32_MAX, shi = INT32_MIN;
+                if (hi > lo) {
+                    const int2* yt = &ytab[(size_t)g.lv[l].ytab_offset];
+                    slo = yt[lo].x & 0xFFFF;
+                    shi = (yt[hi - 1].x >> 16) + 1;
+                }
+                if (l - 1 == 0) {
+                    b[0].x = hi > lo ? slo : 0;
+                    b[0].y = hi > lo ? shi : 0;
+                } else {
+                    const int olo = b[l - 1].z, ohi = b[l - 1].w;
+                    b[l - 1].x = std::min(olo < ohi ? olo : INT32_MAX, slo);
+                    b[l - 1].y = std::max(olo < ohi ? ohi : INT32_MIN, shi);
+                    if (b[l - 1].x >= b[l - 1].y) b[l - 1].x = b[l - 1].y = 0;
+                }
+            }
+            int yrows = 0;
+            for (int l = 0; l + 1 < L; ++l) {
+                const int bytes = (b[l].y - b[l].x) * g.lv[l].lds_pitch;
+                int& dst = (l & 1) ? lds_a : lds_b;
+                dst = std::max(dst, bytes);
+            }
+            for (int l = 1; l < L; ++l) yrows += b[l].y - b[l].x;
+            lds_y = std::max(lds_y, yrows * 16);
+        }
+    };
+    const int hmin = g.lv[L - 1].h;
+    int S = 1, lds_a = 0, lds_b = 0, lds_y = 0;
+    for (;; ++S) {
+        plan(S, table, lds_a, lds_b, lds_y);
+        if (lds_a + lds_b + lds_y + 64 <= 80 * 1024) break;
+        if (S >= hmin || S >= 256) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid band does not fit in LDS");
+    }
+    while ((long)S * max_batch < 2048 && 2 * S <= hmin / 4 && S < 64) {
+        S *= 2;
+        plan(S, table, lds_a, lds_b, lds_y);
+    }
+    g.pyr_bands = S;
+    g.pyr_lds_a = 0;
+    g.pyr_lds_b = (int)round_up((size_t)lds_a + 16, 16);
+    g.pyr_lds_y = g.pyr_lds_b + (int)round_up((size_t)lds_b + 16, 16);
+    g.pyr_lds_bytes = g.pyr_lds_y + (int)round_up((size_t)lds_y, 16);
+    return ORBGPU_OK;
+}
+
 // ORBextractor ctor arithmetic (ORBextractor.cpp:417-448) + per-level layout.
-int build_geometry(orbgpu_extractor* e, std::vector<int2>& xtab, std::vector<int2>& ytab) {
+int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int2>& ytab) {
     const int L = e->nlevels;
     e->scale.assign(L, 1.f);
     e->sigma2.assign(L, 1.f);
@@ -200,7 +276,7 @@ int build_geometry(orbgpu_extractor* e, std::vector<int2>& xtab, std::vector<int
     g.min_th = std::min(std::max(e->min_th, 0), 255);
     size_t pyr_off = 0, cand_off = 0;
     int cell_base = 0, out_off = 0, max_cells = 0, ncap = 0;
-    xtab.clear();
+    ptab.clear();
     ytab.clear();
     for (int l = 0; l < L; ++l) {
         LevelGeom& v = g.lv[l];
@@ -243,25 +319,48 @@ int build_geometry(orbgpu_extractor* e, std::vector<int2>& xtab, std::vector<int
         v.out_offset = out_off;
         out_off += v.ocap;
         ncap = std::max(ncap, std::max(v.ocap, v.nini));
-        // resize tables
+        // resize tables: ytab rows as built; columns as per-quad tap records
+        // for pyramid.hip (3 int4 per quad: (lo, wt) x 4 and the 4 perm selectors)
+        v.lds_pitch = (int)round_up((size_t)v.w, l == 0 ? 16 : 4);
+        if (l == 0) {
+            const uint64_t v4 = ((uint64_t)v.w + 15) / 16;
+            v.quad_magic = v4 < 2 ? 0xFFFFFFFFu : (uint32_t)(((1ull << 32) + v4 - 1) / v4);
+        }
         if (l > 0) {
             const LevelGeom& p = g.lv[l - 1];
             std::vector<int2> xt, yt;
             build_resize_tables(p.w, p.h, v.w, v.h, xt, yt);
+            for (const int2& t : xt)  // Q11 weights: non-negative, a0 + a1 = 2048 (+-1)
+                if ((t.y & 0xFFFF) > 2049 || (t.y >> 16) < 0 || (t.y & 0xFFFF) + (t.y >> 16) > 2049)
+                    return fail(ORBGPU_ERR_UNSUPPORTED, "unexpected resize weights");
             v.simd_end = vresize_simd_end(v.w);
-            v.xtab_offset = (int)xtab.size();
-            v.ytab_offset = (int)ytab.size();
-            xtab.insert(xtab.end(), xt.begin(), xt.end());
-            ytab.insert(ytab.end(), yt.begin(), yt.end());
-            if (p.w + 16 > pyr_max_src_width())
-                return fail(ORBGPU_ERR_UNSUPPORTED, "source row wider than the resize LDS staging");
-            const int rows = pyr_rows_per_block();
-            for (int dy0 = 0; dy0 < v.h; dy0 += rows) {
-                const int dyl = std::min(dy0 + rows, v.h) - 1;
-                if ((yt[dyl].x >> 16) - (yt[dy0].x & 0xFFFF) + 1 > rows + 3)
-                    return fail(ORBGPU_ERR_UNSUPPORTED, "scale factor too large for the resize row band");
+            const int quads = (v.w + 3) / 4;
+            if (quads < 2) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid level narrower than 5 px");
+            v.quad_magic = (uint32_t)(((1ull << 32) + quads - 1) / quads);
+            v.rgroups = pyr_threads() / quads;
+            if (v.rgroups < 1) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid level wider than 4096 px");
+            if ((size_t)v.pitch * v.h >= (1u << 31)) return fail(ORBGPU_ERR_UNSUPPORTED, "level too large");
+            v.ptab_offset = (int)ptab.size();
+            for (int q = 0; q < quads; ++q) {
+                int lo[4], wt[4], sel[4];
+                for (int k = 0; k < 4; ++k) {
+                    const int dx = 4 * q + k;
+                    const int sx = dx < v.w ? (xt[dx].x & 0xFFFF) : 0;
+                    lo[k] = sx & ~3;
+                    wt[k] = dx < v.w ? xt[dx].y : 0;
+                    sel[k] = (int)(0x0c010c00u + (uint32_t)(sx & 3) * 0x00010001u);
+                }
+                ptab.push_back(int4{lo[0], wt[0], lo[1], wt[1]});
+                ptab.push_back(int4{lo[2], wt[2], lo[3], wt[3]});
+                ptab.push_back(int4{sel[0], sel[1], sel[2], sel[3]});
             }
+            v.ytab_offset = (int)ytab.size();
+            ytab.insert(ytab.end(), yt.begin(), yt.end());
         }
+    }
+    {
+        int rc = plan_pyramid_bands(g, ytab, e->max_batch, e->pyr_bands);
+        if (rc) return rc;
     }
     g.total_cells = cell_base;
     g.cand_frame = cand_off;
@@ -312,16 +411,7 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
         evs = e->ev[e->ev_used++].data();
         ORB_HIP(hipEventRecord(evs[0], s));
     }
-    for (int l = 1; l < g.nlevels; ++l) {
-        const LevelGeom& p = g.lv[l - 1];
-        const LevelGeom& v = g.lv[l];
-        const uint8_t* src = l == 1 ? imgs : e->d_pyr + p.offset;
-        const int src_pitch = l == 1 ? (int)row_step : p.pitch;
-        const size_t src_frame = l == 1 ? frame_step : p.frame_bytes;
-        ORB_HIP(launch_pyramid_level(src, src_pitch, src_frame, p.w, p.h, e->d_pyr + v.offset, v.pitch, v.frame_bytes,
-                                     v.w, v.h, v.simd_end, e->d_xtab + v.xtab_offset, e->d_ytab + v.ytab_offset,
-                                     batch, s));
-    }
+    ORB_HIP(launch_pyramid(g, batch, e->d_pyr_bands, e->d_ptab, e->d_ytab, imgs, row_step, frame_step, e->d_pyr, s));
     if (evs) ORB_HIP(hipEventRecord(evs[1], s));
     ORB_HIP(launch_fast_cells(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_cand, e->d_cell_counts, e->d_err, s));
     if (evs) ORB_HIP(hipEventRecord(evs[2], s));
@@ -393,24 +483,29 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
     e->W = width;
     e->H = height;
     e->max_batch = max_batch;
-    std::vector<int2> xtab, ytab;
-    rc = build_geometry(e, xtab, ytab);
+    std::vector<int4> ptab;
+    std::vector<int2> ytab;
+    rc = build_geometry(e, ptab, ytab);
     if (rc) { delete e; return rc; }
     const Geom& g = e->g;
     const size_t B = (size_t)max_batch;
     e->img_pitch = round_up((size_t)width, 16);
-    if ((rc = dalloc(&e->d_pyr, e->pyr_bytes)) || (rc = dalloc(&e->d_blur, e->blur_bytes)) || (rc = dalloc(&e->d_xtab, xtab.size())) ||
+    if ((rc = dalloc(&e->d_pyr, e->pyr_bytes)) || (rc = dalloc(&e->d_blur, e->blur_bytes)) || (rc = dalloc(&e->d_ptab, ptab.size())) ||
         (rc = dalloc(&e->d_ytab, ytab.size())) || (rc = dalloc(&e->d_cand, g.cand_frame * B)) ||
         (rc = dalloc(&e->d_cell_counts, (size_t)g.total_cells * B)) || (rc = dalloc(&e->d_gkeys, g.cand_frame * B)) ||
         (rc = dalloc(&e->d_gknode, g.cand_frame * B)) || (rc = dalloc(&e->d_oct_out, (size_t)g.slots_frame * B)) ||
         (rc = dalloc(&e->d_oct_count, (size_t)g.nlevels * B)) || (rc = dalloc(&e->d_err, 1)) ||
         (rc = dalloc(&e->d_img, e->img_pitch * height)) || (rc = dalloc(&e->d_kps1, (size_t)e->max_kps)) ||
-        (rc = dalloc(&e->d_desc1, (size_t)e->max_kps * 32)) || (rc = dalloc(&e->d_count1, 1))) {
+        (rc = dalloc(&e->d_desc1, (size_t)e->max_kps * 32)) || (rc = dalloc(&e->d_count1, 1)) ||
+        (rc = dalloc(&e->d_pyr_bands, e->pyr_bands.size()))) {
         delete e;
         return rc;
     }
-    if (hipMemcpy(e->d_xtab, xtab.data(), xtab.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMemcpy(e->d_ptab, ptab.data(), ptab.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(e->d_ytab, ytab.data(), ytab.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(e->d_pyr_bands, e->pyr_bands.data(), e->pyr_bands.size() * sizeof(int4), hipMemcpyHostToDevice) !=
+            hipSuccess ||
+        pyramid_set_lds_limit((size_t)g.pyr_lds_bytes) != hipSuccess ||
         hipMemset(e->d_err, 0, sizeof(int)) != hipSuccess ||
         hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         delete e;

@@ -51,7 +51,12 @@ struct LevelGeom {
     int ocap;                 // output slots (max list size)
     int out_offset;           // slot offset of this level within a frame
     // resize tables (levels >= 1)
-    int xtab_offset, ytab_offset;
+    int ytab_offset;
+    // fused pyramid pass (pyramid.hip)
+    int lds_pitch;            // LDS row pitch: w rounded up to 4 (level 0: to 16)
+    uint32_t quad_magic;      // ceil(2^32 / d): i / d = umulhi(i, magic); d = ceil(w/4) (level 0: ceil(w/16))
+    int ptab_offset;          // int4 offset of this level's per-quad column taps (3 int4 per quad)
+    int rgroups;              // row groups of a pyramid block: threads / ceil(w/4)
     // blurred level (all levels, incl. 0): same row pitch as the pyramid
     size_t blur_offset, blur_frame_bytes;
     int blur_tiles_x, blur_tile_base;   // blur work items: 4-column x 64-row strips
@@ -68,6 +73,9 @@ struct Geom {
     int win_pitch, win_rows;  // FAST LDS tile: max over levels of (wCell+9) rounded to 4, (hCell+6)
     int blur_tiles_frame;     // blur tiles per frame over all levels
     int det_max;              // max FAST detection-region pixels of a cell (wCell x hCell)
+    // fused pyramid pass (pyramid.hip): frame bands per frame and LDS layout
+    int pyr_bands;
+    int pyr_lds_a, pyr_lds_b, pyr_lds_y, pyr_lds_bytes;  // odd levels, even levels (incl. 0), y taps
     LevelGeom lv[kMaxLevels];
 };
 

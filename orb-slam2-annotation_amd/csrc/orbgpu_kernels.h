@@ -7,12 +7,12 @@ struct orbgpu_keypoint;
 
 namespace orbgpu {
 
-int pyr_max_src_width();
-int pyr_rows_per_block();
-hipError_t launch_pyramid_level(const uint8_t* src, int src_pitch, size_t src_frame, int sw, int sh,
-                                uint8_t* dst, int dst_pitch, size_t dst_frame, int dw, int dh,
-                                int simd_end, const int2* xtab, const int2* ytab, int batch,
-                                hipStream_t stream);
+int pyr_threads();
+// all pyramid levels 1..L-1 of `batch` frames; bands: int4 [pyr_bands][nlevels]
+// = (need_lo, need_hi, own_lo, own_hi) rows per level (plan_pyramid_bands)
+hipError_t launch_pyramid(const Geom& g, int batch, const int4* bands, const int4* ptab, const int2* ytab,
+                          const uint8_t* img0, size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream);
+hipError_t pyramid_set_lds_limit(size_t bytes);
 
 hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                              const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err,
