@@ -16,6 +16,7 @@
 #include <array>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -174,6 +175,8 @@ namespace {
 // so that is one contiguous range per level).  S is the smallest band count
 // whose two LDS ping-pong buffers fit 80 KiB (two blocks per CU), raised
 // while the batch alone would not fill the chip.
+// two 1024-thread blocks per CU (measured: bigger bands at one block per CU are slower)
+constexpr int kPyrLdsBudget = 80 * 1024;
 int plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, int max_batch, std::vector<int4>& table) {
     const int L = g.nlevels;
     table.clear();
@@ -226,7 +229,7 @@ int plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, int max_batch, st
     int S = 1, lds_a = 0, lds_b = 0, lds_y = 0;
     for (;; ++S) {
         plan(S, table, lds_a, lds_b, lds_y);
-        if (lds_a + lds_b + lds_y + 64 <= 80 * 1024) break;
+        if (lds_a + lds_b + lds_y + 64 <= kPyrLdsBudget) break;
         if (S >= hmin || S >= 256) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid band does not fit in LDS");
     }
     while ((long)S * max_batch < 2048 && 2 * S <= hmin / 4 && S < 64) {
