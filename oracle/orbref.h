@@ -94,6 +94,17 @@ int orbref_search_for_initialization(const orbref_kp* kps1, const uint8_t* desc1
                                      float nnratio, int check_ori, int histo_bug,
                                      int* matches12);
 
+/* --- RANSAC (ransac_ref.cpp) ------------------------------------------- */
+/* Sim3Solver::iterate (Sim3Solver.cpp:147-221) for one solver over n_hyp
+ * given triplets (samples: 3 ints per hypothesis, indices into 0..n-1).
+ * X1, X2: float[3] per point; maxerr1/2: float per point; K: fx fy cx cy.
+ * out_ints = {found, consumed, best_inliers, best_hyp}; T12 (4x4 row-major),
+ * R12, t12, s12 and inliers (byte per point) written when best_hyp >= 0. */
+int orbref_sim3_ransac(int n, const float* X1, const float* X2, const float* maxerr1, const float* maxerr2,
+                       const float* K1, const float* K2, int fix_scale, int min_inliers, int best_inliers, int n_hyp,
+                       const int* samples, int* out_ints, float* out_T12, float* out_R12, float* out_t12,
+                       float* out_s12, uint8_t* inliers);
+
 #ifdef __cplusplus
 }
 #endif

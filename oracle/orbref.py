@@ -58,6 +58,7 @@ def lib() -> ctypes.CDLL:
         L.orbref_orb_descriptor.argtypes = [vp, sz, i, i, f, vp]
         L.orbref_ic_angle.restype = f
         L.orbref_ic_angle.argtypes = [vp, sz, i, i]
+        L.orbref_sim3_ransac.argtypes = [i, vp, vp, vp, vp, vp, vp, i, i, i, i, vp, vp, vp, vp, vp, vp, vp]
         L.orbref_search_for_initialization.argtypes = [vp, vp, i, vp, vp, i, f, f, f, f, vp, i, f, i, i, vp]
         _LIB = L
     return _LIB
@@ -168,3 +169,26 @@ def search_for_initialization(kps1, desc1, kps2, desc2, img_w, img_h, prev_xy=No
                                                *[float(v) for v in b], _p(prev), window, nnratio, int(check_ori),
                                                int(histo_bug), _p(m12))
     return n, m12, prev
+
+
+def sim3_ransac(X1, X2, maxerr1, maxerr2, K1, K2, fix_scale, min_inliers, best_inliers, samples):
+    """Sim3Solver::iterate over the given triplets (see orbref.h).  Returns a
+    dict: found, consumed, best_inliers, best_hyp, T12, R12, t12, s12, inliers."""
+    X1 = np.ascontiguousarray(X1, np.float32)
+    X2 = np.ascontiguousarray(X2, np.float32)
+    e1 = np.ascontiguousarray(maxerr1, np.float32)
+    e2 = np.ascontiguousarray(maxerr2, np.float32)
+    k1 = np.ascontiguousarray(K1, np.float32)
+    k2 = np.ascontiguousarray(K2, np.float32)
+    smp = np.ascontiguousarray(samples, np.int32).reshape(-1, 3)
+    n = len(X1)
+    ints = np.zeros(4, np.int32)
+    T = np.zeros(16, np.float32)
+    R = np.zeros(9, np.float32)
+    t = np.zeros(3, np.float32)
+    sc = np.zeros(1, np.float32)
+    inl = np.zeros(max(n, 1), np.uint8)
+    lib().orbref_sim3_ransac(n, _p(X1), _p(X2), _p(e1), _p(e2), _p(k1), _p(k2), int(fix_scale), int(min_inliers),
+                             int(best_inliers), len(smp), _p(smp), _p(ints), _p(T), _p(R), _p(t), _p(sc), _p(inl))
+    return {"found": int(ints[0]), "consumed": int(ints[1]), "best_inliers": int(ints[2]), "best_hyp": int(ints[3]),
+            "T12": T.reshape(4, 4), "R12": R.reshape(3, 3), "t12": t, "s12": float(sc[0]), "inliers": inl[:n]}

@@ -25,10 +25,11 @@
 #include "../../include/orbgpu_debug.h"
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
+#include "host_common.h"
 
 using namespace orbgpu;
 
-namespace {
+namespace orbgpu {
 
 thread_local std::string g_err;
 
@@ -36,18 +37,6 @@ int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
-
-#define ORB_HIP(expr)                                                                               \
-    do {                                                                                            \
-        hipError_t e_ = (expr);                                                                     \
-        if (e_ != hipSuccess) return fail(ORBGPU_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
-    } while (0)
-
-// OpenCV 2.4 cvRound / cvFloor on the host (SSE2 cvtsd2si = half to even)
-inline int cv_round(double v) { return (int)std::nearbyint(v); }
-inline int cv_floor(double v) { const int i = cv_round(v); return i - (v < (double)i); }
-inline int sat_s16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
-inline size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 int check_device() {
     int dev = 0, n = 0;
@@ -59,6 +48,17 @@ int check_device() {
         return fail(ORBGPU_ERR_NO_DEVICE, std::string("device is ") + p.gcnArchName + ", this build targets gfx950");
     return ORBGPU_OK;
 }
+
+}  // namespace orbgpu
+
+namespace {
+
+// OpenCV 2.4 cvRound / cvFloor on the host (SSE2 cvtsd2si = half to even)
+inline int cv_round(double v) { return (int)std::nearbyint(v); }
+inline int cv_floor(double v) { const int i = cv_round(v); return i - (v < (double)i); }
+inline int sat_s16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+inline size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
 
 int vresize_simd_end(int width) {
     int x = 0;

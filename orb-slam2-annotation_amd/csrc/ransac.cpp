@@ -1,0 +1,179 @@
+// ransac.cpp -- host side of the RANSAC entry points (include/orbgpu_ransac.h):
+// the glibc-compatible random stream and the Sim3 batch driver.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/orbgpu_ransac.h"
+#include "host_common.h"
+#include "ransac_kernels.h"
+
+using namespace orbgpu;
+
+namespace {
+
+// glibc random_r.c, TYPE_3 (x**31 + x**3 + 1), the generator behind rand():
+// srandom_r fills r[0..30] with 16807^i * seed mod (2^31 - 1) (Schrage's
+// method, seed 0 -> 1), sets front = 3, rear = 0 and discards 310 outputs;
+// random_r adds r[rear] into r[front], returns the sum >> 1 and advances
+// both indices cyclically.
+constexpr int kDeg = 31, kSep = 3;
+
+int32_t next(orbgpu_rand_state* st) {
+    uint32_t val = (uint32_t)st->r[st->f] + (uint32_t)st->r[st->b];
+    st->r[st->f] = (int32_t)val;
+    const int32_t out = (int32_t)(val >> 1);
+    if (++st->f >= kDeg) {
+        st->f = 0;
+        ++st->b;
+    } else if (++st->b >= kDeg) {
+        st->b = 0;
+    }
+    return out;
+}
+
+void seed(orbgpu_rand_state* st, unsigned int s) {
+    if (s == 0) s = 1;
+    st->r[0] = (int32_t)s;
+    int32_t word = (int32_t)s;
+    for (int i = 1; i < kDeg; ++i) {
+        const long hi = word / 127773, lo = word % 127773;
+        word = (int32_t)(16807 * lo - 2836 * hi);
+        if (word < 0) word += 2147483647;
+        st->r[i] = word;
+    }
+    st->f = kSep;
+    st->b = 0;
+    for (int k = 0; k < kDeg * 10; ++k) (void)next(st);
+}
+
+std::mutex g_rand_mu;
+orbgpu_rand_state g_rand = [] {
+    orbgpu_rand_state s;
+    seed(&s, 1);  // glibc's initial state equals srand(1)
+    return s;
+}();
+
+}  // namespace
+
+extern "C" {
+
+void orbgpu_srand_r(orbgpu_rand_state* st, unsigned int s) { seed(st, s); }
+int orbgpu_rand_r(orbgpu_rand_state* st) { return next(st); }
+
+void orbgpu_srand(unsigned int s) {
+    std::lock_guard<std::mutex> lk(g_rand_mu);
+    seed(&g_rand, s);
+}
+
+int orbgpu_rand(void) {
+    std::lock_guard<std::mutex> lk(g_rand_mu);
+    return next(&g_rand);
+}
+
+int orbgpu_random_int(int min, int max) {
+    const int d = max - min + 1;
+    return int(((double)orbgpu_rand() / ((double)2147483647 + 1.0)) * d) + min;
+}
+
+void orbgpu_rand_get_state(orbgpu_rand_state* out) {
+    std::lock_guard<std::mutex> lk(g_rand_mu);
+    *out = g_rand;
+}
+
+void orbgpu_rand_set_state(const orbgpu_rand_state* in) {
+    std::lock_guard<std::mutex> lk(g_rand_mu);
+    g_rand = *in;
+}
+
+size_t orbgpu_sim3_workspace_bytes(int total_samples) {
+    return (size_t)(total_samples > 0 ? total_samples : 1) * sim3_hyp_bytes();
+}
+
+int orbgpu_sim3_ransac_batch_device(int batch, const orbgpu_sim3_problem* d_problems, int max_hyp,
+                                    const float* d_X1, const float* d_X2, const float* d_maxerr1,
+                                    const float* d_maxerr2, const int* d_samples, void* d_workspace,
+                                    orbgpu_sim3_result* d_results, uint8_t* d_inliers, void* stream) {
+    if (batch < 0 || max_hyp < 0 ||
+        (batch > 0 && (!d_problems || !d_X1 || !d_X2 || !d_maxerr1 || !d_maxerr2 || !d_samples || !d_workspace ||
+                       !d_results || !d_inliers)))
+        return fail(ORBGPU_ERR_ARG, "invalid argument");
+    int rc = check_device();
+    if (rc) return rc;
+    ORB_HIP(launch_sim3_ransac(batch, d_problems, max_hyp, d_X1, d_X2, d_maxerr1, d_maxerr2, d_samples, d_workspace,
+                               d_results, d_inliers, (hipStream_t)stream));
+    return ORBGPU_OK;
+}
+
+int orbgpu_sim3_ransac_batch(int batch, const orbgpu_sim3_problem* problems, int total_points, const float* X1,
+                             const float* X2, const float* maxerr1, const float* maxerr2, int total_samples,
+                             const int* samples, orbgpu_sim3_result* results, uint8_t* inliers) {
+    if (batch < 0 || total_points < 0 || total_samples < 0 || (batch > 0 && (!problems || !results)))
+        return fail(ORBGPU_ERR_ARG, "invalid argument");
+    for (int b = 0; b < batch; ++b) {  // bounds of every problem against the arrays
+        const orbgpu_sim3_problem& p = problems[b];
+        if (p.n < 0 || p.offset < 0 || p.offset + p.n > total_points || p.n_hyp < 0 || p.sample_offset < 0 ||
+            p.sample_offset + p.n_hyp > total_samples)
+            return fail(ORBGPU_ERR_ARG, "problem " + std::to_string(b) + " is out of the array bounds");
+        if (p.n_hyp > 0 && p.n < 3) return fail(ORBGPU_ERR_ARG, "a hypothesis needs 3 correspondences");
+        for (int h = 0; h < 3 * p.n_hyp; ++h) {
+            const int idx = samples[3 * (size_t)p.sample_offset + h];
+            if (idx < 0 || idx >= p.n) return fail(ORBGPU_ERR_ARG, "sample index out of range");
+        }
+    }
+    int rc = check_device();
+    if (rc) return rc;
+    if (batch == 0) return ORBGPU_OK;
+    int max_hyp = 0;
+    for (int b = 0; b < batch; ++b) max_hyp = std::max(max_hyp, problems[b].n_hyp);
+    const size_t np = (size_t)(total_points > 0 ? total_points : 1), ns = (size_t)(total_samples > 0 ? total_samples : 1);
+    orbgpu_sim3_problem* dp = nullptr;
+    float *dx1 = nullptr, *dx2 = nullptr, *de1 = nullptr, *de2 = nullptr;
+    int* ds = nullptr;
+    orbgpu_sim3_result* dr = nullptr;
+    uint8_t* di = nullptr;
+    void* dw = nullptr;
+    auto cleanup = [&]() {
+        void* ptrs[] = {dp, dx1, dx2, de1, de2, ds, dr, di, dw};
+        for (void* p : ptrs)
+            if (p) (void)hipFree(p);
+    };
+    bool ok = hipMalloc((void**)&dp, sizeof(*dp) * batch) == hipSuccess &&
+              hipMalloc((void**)&dx1, 12 * np) == hipSuccess && hipMalloc((void**)&dx2, 12 * np) == hipSuccess &&
+              hipMalloc((void**)&de1, 4 * np) == hipSuccess && hipMalloc((void**)&de2, 4 * np) == hipSuccess &&
+              hipMalloc((void**)&ds, 12 * ns) == hipSuccess && hipMalloc((void**)&dr, sizeof(*dr) * batch) == hipSuccess &&
+              hipMalloc((void**)&di, np) == hipSuccess &&
+              hipMalloc(&dw, orbgpu_sim3_workspace_bytes(total_samples)) == hipSuccess;
+    if (!ok) {
+        cleanup();
+        return fail(ORBGPU_ERR_HIP, "device allocation failed");
+    }
+    ok = hipMemcpy(dp, problems, sizeof(*dp) * batch, hipMemcpyHostToDevice) == hipSuccess &&
+         (total_points == 0 ||
+          (hipMemcpy(dx1, X1, 12 * (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
+           hipMemcpy(dx2, X2, 12 * (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
+           hipMemcpy(de1, maxerr1, 4 * (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
+           hipMemcpy(de2, maxerr2, 4 * (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
+           hipMemcpy(di, inliers, (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess)) &&
+         (total_samples == 0 || hipMemcpy(ds, samples, 12 * (size_t)total_samples, hipMemcpyHostToDevice) == hipSuccess);
+    if (!ok) {
+        cleanup();
+        return fail(ORBGPU_ERR_HIP, "upload failed");
+    }
+    rc = orbgpu_sim3_ransac_batch_device(batch, dp, max_hyp, dx1, dx2, de1, de2, ds, dw, dr, di, nullptr);
+    if (rc) {
+        cleanup();
+        return rc;
+    }
+    ok = hipDeviceSynchronize() == hipSuccess &&
+         hipMemcpy(results, dr, sizeof(*dr) * batch, hipMemcpyDeviceToHost) == hipSuccess &&
+         (total_points == 0 || hipMemcpy(inliers, di, (size_t)total_points, hipMemcpyDeviceToHost) == hipSuccess);
+    cleanup();
+    if (!ok) return fail(ORBGPU_ERR_HIP, "Sim3 RANSAC failed");
+    return ORBGPU_OK;
+}
+
+}  // extern "C"

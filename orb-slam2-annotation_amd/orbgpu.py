@@ -82,6 +82,22 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_debug_octree_trace.argtypes = [vp, i, vp, i]
         L.orbgpu_search_for_initialization.argtypes = [GridBounds, vp, vp, i, vp, vp, i, vp, i, f, i, vp,
                                                        ctypes.POINTER(i)]
+        # orbgpu_ransac.h
+        L.orbgpu_srand.argtypes = [ctypes.c_uint]
+        L.orbgpu_srand.restype = None
+        L.orbgpu_rand.restype = i
+        L.orbgpu_random_int.argtypes = [i, i]
+        L.orbgpu_rand_get_state.argtypes = [vp]
+        L.orbgpu_rand_get_state.restype = None
+        L.orbgpu_rand_set_state.argtypes = [vp]
+        L.orbgpu_rand_set_state.restype = None
+        L.orbgpu_srand_r.argtypes = [vp, ctypes.c_uint]
+        L.orbgpu_srand_r.restype = None
+        L.orbgpu_rand_r.argtypes = [vp]
+        L.orbgpu_sim3_workspace_bytes.argtypes = [i]
+        L.orbgpu_sim3_workspace_bytes.restype = sz
+        L.orbgpu_sim3_ransac_batch_device.argtypes = [i, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.orbgpu_sim3_ransac_batch.argtypes = [i, vp, i, vp, vp, vp, vp, i, vp, vp, vp]
         _LIB = L
     return _LIB
 

@@ -135,3 +135,44 @@ def torch_stream(n: int, width: int, height: int, seed: int = 0x0B5E, device="cu
         img = img + noise_sigma * torch.randn(img.shape, generator=gen, device=device)
         out[s:s + m, :, :width] = img.round().clamp(0, 255).to(torch.uint8)
     return out
+
+
+def sim3_problem(n: int, inlier_frac: float, seed: int, fix_scale: bool = False, noise_px: float = 0.5):
+    """Correspondences of a loop-closure Sim3Solver (Sim3Solver.cpp:37-107):
+    points X2 in keyframe-2 camera coordinates (depth 2..12 m, in view), X1 =
+    s R X2 + t for the inliers (plus pixel-level noise), random points in view
+    for the outliers.  Octaves are drawn from the 8-level pyramid (sigma^2 =
+    1.2^(2 octave)).  Returns dict(X1, X2, sigma2_1, sigma2_2, K1, K2, s, R,
+    t, inlier)."""
+    rng = np.random.default_rng(seed)
+    K = np.array([517.3, 516.5, 318.6, 255.3], np.float64)
+    s = 1.0 if fix_scale else float(rng.uniform(0.7, 1.4))
+    ang = rng.uniform(-0.3, 0.3, size=3)  # moderate relative rotation
+    cx, cy, cz = np.cos(ang)
+    sx, sy, sz = np.sin(ang)
+    Rx = np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]])
+    Ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    Rz = np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]])
+    R = Rz @ Ry @ Rx
+    t = rng.uniform(-0.5, 0.5, size=3)
+
+    def in_view(m):
+        z = rng.uniform(2.0, 12.0, size=m)
+        u = rng.uniform(20, 620, size=m)
+        v = rng.uniform(20, 460, size=m)
+        return np.stack([(u - K[2]) / K[0] * z, (v - K[3]) / K[1] * z, z], 1)
+
+    X2 = in_view(n)
+    X1 = (s * (R @ X2.T)).T + t
+    inl = rng.uniform(size=n) < inlier_frac
+    # pixel noise on inliers: perturb X1 along the image plane
+    z1 = X1[:, 2:3]
+    X1[:, :2] += rng.normal(scale=noise_px, size=(n, 2)) / K[:2] * z1
+    out = ~inl
+    X1[out] = in_view(int(out.sum()))
+    oct1 = rng.integers(0, 8, size=n)
+    oct2 = rng.integers(0, 8, size=n)
+    sig = np.float32(1.2) ** (2 * np.arange(8))
+    return {"X1": X1.astype(np.float32), "X2": X2.astype(np.float32),
+            "sigma2_1": sig[oct1].astype(np.float32), "sigma2_2": sig[oct2].astype(np.float32),
+            "K1": K.astype(np.float32), "K2": K.astype(np.float32), "s": s, "R": R, "t": t, "inlier": inl}
