@@ -5,6 +5,7 @@
  * Reference (paths relative to /root/reference/ORB-SLAM2):
  *   DUtils::Random::RandomInt / SeedRand   Thirdparty/DBoW2/DUtils/Random.cpp:33-50
  *   Sim3Solver                              include/Sim3Solver.h:35-125, src/Sim3Solver.cpp:37-447
+ *   PnPsolver                               include/PnPsolver.h:59-188, src/PnPsolver.cpp:104-1080
  *
  * The RANSAC loops of the reference draw their minimal sets with
  * DUtils::Random::RandomInt, i.e. with the process-wide glibc rand().  The
@@ -101,6 +102,55 @@ int orbgpu_sim3_ransac_batch_device(int batch, const orbgpu_sim3_problem* d_prob
 int orbgpu_sim3_ransac_batch(int batch, const orbgpu_sim3_problem* problems, int total_points, const float* X1,
                              const float* X2, const float* maxerr1, const float* maxerr2, int total_samples,
                              const int* samples, orbgpu_sim3_result* results, uint8_t* inliers);
+
+/* ---------------------------------------------------------------------- */
+/* PnPsolver RANSAC (EPnP)                                                 */
+/* ---------------------------------------------------------------------- */
+/* One solver (= one PnPsolver object).  Correspondences [offset, offset+n):
+ *   P3w   float[3] per point: mvP3Dw (world positions of the MapPoints)
+ *   P2    float[2] per point: mvP2D (undistorted keypoints)
+ *   maxerr float per point: mvMaxError = sigma^2 * th2 (PnPsolver.cpp:190-194)
+ * Hypothesis h uses the 4-tuple samples[4*(sample_offset + h) .. +3]
+ * (indices into 0..n-1 after the reference's swap-remove draw, :229-244);
+ * sample ranges of different problems must not overlap.  The call replays
+ * iterate()'s loop body (:224-299) over n_hyp hypotheses -- the caller
+ * computes n_hyp from the reference's `||` loop condition (:224). */
+typedef struct orbgpu_pnp_problem {
+    int n, offset;
+    int min_inliers;     /* mRansacMinInliers (after SetRansacParameters)   */
+    int best_inliers;    /* mnBestInliers before this call                  */
+    int n_hyp;           /* hypotheses to run in this call                  */
+    int sample_offset;   /* first 4-tuple in samples[]                       */
+    float fu, fv, uc, vc;
+} orbgpu_pnp_problem;
+
+typedef struct orbgpu_pnp_result {
+    int found;           /* Refine() succeeded: iterate() returns mRefinedTcw */
+    int consumed;        /* hypotheses consumed (mnIterations advance)      */
+    int best_inliers;    /* mnBestInliers after the call                    */
+    int best_hyp;        /* hypothesis that last became the best, or -1     */
+    int refined_inliers; /* mnRefinedInliers when found                     */
+    float best_Tcw[16];  /* mBestTcw when best_hyp >= 0 (row-major 4x4)     */
+    float refined_Tcw[16]; /* mRefinedTcw when found                        */
+} orbgpu_pnp_result;
+
+/* Device scratch for orbgpu_pnp_ransac_batch_device(). */
+size_t orbgpu_pnp_workspace_bytes(int total_points, int total_samples);
+/* Batched, HBM-resident.  total_points / total_samples size the arrays and
+ * the workspace (orbgpu_pnp_workspace_bytes); max_hyp >= every n_hyp.
+ * d_best_mask (byte per point) is in/out: it must hold the incoming best
+ * hypothesis' inliers (mvbBestInliers) when best_inliers > 0 and is
+ * rewritten when the best changes; d_refined_mask gets mvbRefinedInliers of
+ * the last Refine().  Asynchronous on `stream`. */
+int orbgpu_pnp_ransac_batch_device(int batch, const orbgpu_pnp_problem* d_problems, int max_hyp,
+                                   int total_points, int total_samples, const float* d_P3w, const float* d_P2,
+                                   const float* d_maxerr, const int* d_samples, void* d_workspace,
+                                   orbgpu_pnp_result* d_results, uint8_t* d_best_mask, uint8_t* d_refined_mask,
+                                   void* stream);
+/* Host-pointer form (uploads, runs, downloads, synchronises). */
+int orbgpu_pnp_ransac_batch(int batch, const orbgpu_pnp_problem* problems, int total_points, const float* P3w,
+                            const float* P2, const float* maxerr, int total_samples, const int* samples,
+                            orbgpu_pnp_result* results, uint8_t* best_mask, uint8_t* refined_mask);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,226 @@
+// pnp.hip -- PnPsolver's RANSAC loop (src/PnPsolver.cpp:203-349) for a batch
+// of solvers (one per relocalisation candidate keyframe), in two launches:
+//   1  pnp_hyp_kernel: one thread per hypothesis runs EPnP (epnp.h) on its
+//      minimal set of 4 correspondences -- speculative, all n_hyp of every
+//      solver;
+//   2  pnp_score_kernel, one 256-thread block per solver, chunks of 64
+//      hypotheses: the waves score them (CheckInliers :352-386, lanes over
+//      correspondences, ballot + popcount), then the whole block replays the
+//      reference's loop body in iteration order: a hypothesis with
+//      inliers >= minInliers becomes the best if it beats it (its mask is
+//      written by all threads), and Refine() (:303-349: EPnP over all best
+//      inliers, then CheckInliers) runs on one lane; the first refinement
+//      with more than minInliers inliers ends the call.  Refine() of an
+//      unchanged best is deterministic, so it is evaluated once per best.
+// Parity with the CPU oracle is to a stated pose tolerance
+// (tests/test_pnp.py): the reference's cvSVD is restated with Jacobi
+// methods and the null space of a minimal set is only defined up to a basis.
+#include "../../include/orbgpu_ransac.h"
+#include "epnp.h"
+#include "ransac_kernels.h"
+
+namespace orbgpu {
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kChunk = 64;
+
+struct HypPose {
+    double R[9], t[3];
+};
+
+struct SampleSrc {  // the minimal set of one hypothesis
+    const float* P3;
+    const float* P2;
+    const int* idx;
+    __device__ int count() const { return 4; }
+    __device__ void get(int i, double* pw, double& u, double& v) const {
+        const int k = idx[i];
+        pw[0] = P3[3 * k];
+        pw[1] = P3[3 * k + 1];
+        pw[2] = P3[3 * k + 2];
+        u = P2[2 * k];
+        v = P2[2 * k + 1];
+    }
+};
+
+struct ListSrc {  // Refine(): the best inliers in index order
+    const float* P3;
+    const float* P2;
+    const int* list;
+    int n;
+    __device__ int count() const { return n; }
+    __device__ void get(int i, double* pw, double& u, double& v) const {
+        const int k = list[i];
+        pw[0] = P3[3 * k];
+        pw[1] = P3[3 * k + 1];
+        pw[2] = P3[3 * k + 2];
+        u = P2[2 * k];
+        v = P2[2 * k + 1];
+    }
+};
+
+// PnPsolver::CheckInliers (:352-386): camera coordinates in float from the
+// double pose, projection in double, squared error in float
+__device__ inline bool pnp_inlier(const HypPose& H, const epnp::Camera& cam, const float* P3, const float* P2,
+                                  float maxerr) {
+    const double x = P3[0], y = P3[1], z = P3[2];
+    const float Xc = (float)(H.R[0] * x + H.R[1] * y + H.R[2] * z + H.t[0]);
+    const float Yc = (float)(H.R[3] * x + H.R[4] * y + H.R[5] * z + H.t[1]);
+    const float invZc = (float)(1 / (H.R[6] * x + H.R[7] * y + H.R[8] * z + H.t[2]));
+    const double ue = cam.uc + cam.fu * (double)Xc * (double)invZc;
+    const double ve = cam.vc + cam.fv * (double)Yc * (double)invZc;
+    const float dx = (float)((double)P2[0] - ue), dy = (float)((double)P2[1] - ve);
+    const float e2 = dx * dx + dy * dy;
+    return e2 < maxerr;
+}
+
+__device__ inline epnp::Camera camera_of(const orbgpu_pnp_problem& P) {
+    return epnp::Camera{(double)P.fu, (double)P.fv, (double)P.uc, (double)P.vc};
+}
+
+__device__ inline void pose_to_tcw(const HypPose& H, float* T) {  // Rcw/tcw convertTo(CV_32F) into eye(4)
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) T[4 * i + j] = (float)H.R[3 * i + j];
+        T[4 * i + 3] = (float)H.t[i];
+    }
+    T[12] = T[13] = T[14] = 0.f;
+    T[15] = 1.f;
+}
+
+__global__ __launch_bounds__(64) void pnp_hyp_kernel(const orbgpu_pnp_problem* __restrict__ probs,
+                                                     const float* __restrict__ P3g, const float* __restrict__ P2g,
+                                                     const int* __restrict__ samples, HypPose* __restrict__ hyps) {
+    const orbgpu_pnp_problem& P = probs[blockIdx.y];
+    const int h = blockIdx.x * 64 + threadIdx.x;
+    if (h >= P.n_hyp) return;
+    const size_t slot = (size_t)P.sample_offset + h;
+    SampleSrc src{P3g + 3 * (size_t)P.offset, P2g + 2 * (size_t)P.offset, samples + 4 * slot};
+    epnp::Pose pose;
+    epnp::compute_pose(src, camera_of(P), pose);
+    HypPose& out = hyps[slot];
+    for (int k = 0; k < 9; ++k) out.R[k] = pose.R[k];
+    for (int k = 0; k < 3; ++k) out.t[k] = pose.t[k];
+}
+
+__global__ __launch_bounds__(kThreads) void pnp_score_kernel(const orbgpu_pnp_problem* __restrict__ probs,
+                                                             const HypPose* __restrict__ hyps,
+                                                             const float* __restrict__ P3g,
+                                                             const float* __restrict__ P2g,
+                                                             const float* __restrict__ errg,
+                                                             int* __restrict__ lists,
+                                                             orbgpu_pnp_result* __restrict__ results,
+                                                             uint8_t* __restrict__ best_mask,
+                                                             uint8_t* __restrict__ refined_mask) {
+    __shared__ int s_cnt[kChunk];
+    __shared__ int s_state[6];  // best, best_hyp, found, consumed, refine_tried, refined_inliers
+    __shared__ HypPose s_ref;
+    const orbgpu_pnp_problem P = probs[blockIdx.x];
+    const HypPose* HP = hyps + P.sample_offset;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const float* P3 = P3g + 3 * (size_t)P.offset;
+    const float* P2 = P2g + 2 * (size_t)P.offset;
+    const float* E = errg + P.offset;
+    uint8_t* BM = best_mask + P.offset;
+    int* list = lists + P.offset;
+    const epnp::Camera cam = camera_of(P);
+    if (tid == 0) {
+        s_state[0] = P.best_inliers;
+        s_state[1] = -1;
+        s_state[2] = 0;
+        s_state[3] = 0;
+        s_state[4] = 0;  // Refine() of the incoming best not evaluated yet
+        s_state[5] = 0;
+    }
+    __syncthreads();
+    for (int base = 0; base < P.n_hyp && !s_state[2]; base += kChunk) {
+        const int nh = min(kChunk, P.n_hyp - base);
+        for (int h = wave; h < nh; h += kThreads / 64) {
+            const HypPose& H = HP[base + h];
+            int cnt = 0;
+            for (int i = lane; i < P.n; i += 64) cnt += __popcll(__ballot(pnp_inlier(H, cam, P3 + 3 * i, P2 + 2 * i, E[i])));
+            if (lane == 0) s_cnt[h] = cnt;
+        }
+        __syncthreads();
+        for (int h = 0; h < nh; ++h) {  // block-uniform replay of the loop body (:224-299)
+            const int c = s_cnt[h];
+            if (c < P.min_inliers) continue;
+            if (c > s_state[0]) {  // new best: its inlier mask
+                const HypPose& H = HP[base + h];
+                for (int i = tid; i < P.n; i += kThreads) BM[i] = pnp_inlier(H, cam, P3 + 3 * i, P2 + 2 * i, E[i]);
+                __syncthreads();
+                if (tid == 0) {
+                    s_state[0] = c;
+                    s_state[1] = base + h;
+                    s_state[4] = 0;
+                }
+                __syncthreads();
+            }
+            if (!s_state[4]) {  // Refine() with the current best inliers
+                if (tid == 0) {
+                    int m = 0;
+                    for (int i = 0; i < P.n; ++i)
+                        if (BM[i]) list[m++] = i;
+                    ListSrc src{P3, P2, list, m};
+                    epnp::Pose pose;
+                    if (m > 0) epnp::compute_pose(src, cam, pose);
+                    for (int k = 0; k < 9; ++k) s_ref.R[k] = m > 0 ? pose.R[k] : 0.0;
+                    for (int k = 0; k < 3; ++k) s_ref.t[k] = m > 0 ? pose.t[k] : 0.0;
+                }
+                __syncthreads();
+                int cnt = 0;
+                for (int i = tid; i < P.n; i += kThreads) {
+                    const bool in = pnp_inlier(s_ref, cam, P3 + 3 * i, P2 + 2 * i, E[i]);
+                    refined_mask[P.offset + i] = in;
+                    cnt += in;
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+                if (tid == 0) s_state[5] = 0;
+                __syncthreads();
+                if (lane == 0) atomicAdd(&s_state[5], cnt);
+                __syncthreads();
+                if (tid == 0) {
+                    s_state[4] = 1;
+                    if (s_state[5] > P.min_inliers) {
+                        s_state[2] = 1;
+                        s_state[3] = base + h + 1;
+                    }
+                }
+                __syncthreads();
+                if (s_state[2]) break;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        orbgpu_pnp_result& R = results[blockIdx.x];
+        R.found = s_state[2];
+        R.consumed = s_state[2] ? s_state[3] : P.n_hyp;
+        R.best_inliers = s_state[0];
+        R.best_hyp = s_state[1];
+        R.refined_inliers = s_state[2] ? s_state[5] : 0;
+        if (s_state[1] >= 0) pose_to_tcw(HP[s_state[1]], R.best_Tcw);
+        if (s_state[2]) pose_to_tcw(s_ref, R.refined_Tcw);
+    }
+}
+
+}  // namespace
+
+size_t pnp_hyp_bytes() { return sizeof(HypPose); }
+
+hipError_t launch_pnp_ransac(int batch, const orbgpu_pnp_problem* probs, int max_hyp, const float* P3,
+                             const float* P2, const float* maxerr, const int* samples, void* hyps, int* lists,
+                             orbgpu_pnp_result* results, uint8_t* best_mask, uint8_t* refined_mask,
+                             hipStream_t stream) {
+    if (batch <= 0) return hipSuccess;
+    if (max_hyp > 0)
+        hipLaunchKernelGGL(pnp_hyp_kernel, dim3((max_hyp + 63) / 64, batch), dim3(64), 0, stream, probs, P3, P2,
+                           samples, static_cast<HypPose*>(hyps));
+    hipLaunchKernelGGL(pnp_score_kernel, dim3(batch), dim3(kThreads), 0, stream, probs,
+                       static_cast<const HypPose*>(hyps), P3, P2, maxerr, lists, results, best_mask, refined_mask);
+    return hipGetLastError();
+}
+
+}  // namespace orbgpu

@@ -1,5 +1,5 @@
 // ransac.cpp -- host side of the RANSAC entry points (include/orbgpu_ransac.h):
-// the glibc-compatible random stream and the Sim3 batch driver.
+// the glibc-compatible random stream and the Sim3 / PnP batch drivers.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -173,6 +173,100 @@ int orbgpu_sim3_ransac_batch(int batch, const orbgpu_sim3_problem* problems, int
          (total_points == 0 || hipMemcpy(inliers, di, (size_t)total_points, hipMemcpyDeviceToHost) == hipSuccess);
     cleanup();
     if (!ok) return fail(ORBGPU_ERR_HIP, "Sim3 RANSAC failed");
+    return ORBGPU_OK;
+}
+
+size_t orbgpu_pnp_workspace_bytes(int total_points, int total_samples) {
+    const size_t hyps = (size_t)(total_samples > 0 ? total_samples : 1) * pnp_hyp_bytes();
+    return (hyps + 255) / 256 * 256 + (size_t)(total_points > 0 ? total_points : 1) * sizeof(int);
+}
+
+int orbgpu_pnp_ransac_batch_device(int batch, const orbgpu_pnp_problem* d_problems, int max_hyp,
+                                   int total_points, int total_samples, const float* d_P3w, const float* d_P2,
+                                   const float* d_maxerr, const int* d_samples, void* d_workspace,
+                                   orbgpu_pnp_result* d_results, uint8_t* d_best_mask, uint8_t* d_refined_mask,
+                                   void* stream) {
+    if (batch < 0 || max_hyp < 0 || total_points < 0 || total_samples < 0 ||
+        (batch > 0 && (!d_problems || !d_P3w || !d_P2 || !d_maxerr || !d_samples || !d_workspace || !d_results ||
+                       !d_best_mask || !d_refined_mask)))
+        return fail(ORBGPU_ERR_ARG, "invalid argument");
+    int rc = check_device();
+    if (rc) return rc;
+    const size_t hyps = (size_t)(total_samples > 0 ? total_samples : 1) * pnp_hyp_bytes();
+    int* lists = reinterpret_cast<int*>(static_cast<uint8_t*>(d_workspace) + (hyps + 255) / 256 * 256);
+    ORB_HIP(launch_pnp_ransac(batch, d_problems, max_hyp, d_P3w, d_P2, d_maxerr, d_samples, d_workspace, lists,
+                              d_results, d_best_mask, d_refined_mask, (hipStream_t)stream));
+    return ORBGPU_OK;
+}
+
+int orbgpu_pnp_ransac_batch(int batch, const orbgpu_pnp_problem* problems, int total_points, const float* P3w,
+                            const float* P2, const float* maxerr, int total_samples, const int* samples,
+                            orbgpu_pnp_result* results, uint8_t* best_mask, uint8_t* refined_mask) {
+    if (batch < 0 || total_points < 0 || total_samples < 0 || (batch > 0 && (!problems || !results)))
+        return fail(ORBGPU_ERR_ARG, "invalid argument");
+    for (int b = 0; b < batch; ++b) {
+        const orbgpu_pnp_problem& p = problems[b];
+        if (p.n < 0 || p.offset < 0 || p.offset + p.n > total_points || p.n_hyp < 0 || p.sample_offset < 0 ||
+            p.sample_offset + p.n_hyp > total_samples)
+            return fail(ORBGPU_ERR_ARG, "problem " + std::to_string(b) + " is out of the array bounds");
+        if (p.n_hyp > 0 && p.n < 4) return fail(ORBGPU_ERR_ARG, "a hypothesis needs 4 correspondences");
+        for (int h = 0; h < 4 * p.n_hyp; ++h) {
+            const int idx = samples[4 * (size_t)p.sample_offset + h];
+            if (idx < 0 || idx >= p.n) return fail(ORBGPU_ERR_ARG, "sample index out of range");
+        }
+    }
+    int rc = check_device();
+    if (rc) return rc;
+    if (batch == 0) return ORBGPU_OK;
+    int max_hyp = 0;
+    for (int b = 0; b < batch; ++b) max_hyp = std::max(max_hyp, problems[b].n_hyp);
+    const size_t np = (size_t)(total_points > 0 ? total_points : 1), ns = (size_t)(total_samples > 0 ? total_samples : 1);
+    orbgpu_pnp_problem* dp = nullptr;
+    float *d3 = nullptr, *d2 = nullptr, *de = nullptr;
+    int* ds = nullptr;
+    orbgpu_pnp_result* dr = nullptr;
+    uint8_t *dbm = nullptr, *drm = nullptr;
+    void* dw = nullptr;
+    auto cleanup = [&]() {
+        void* ptrs[] = {dp, d3, d2, de, ds, dr, dbm, drm, dw};
+        for (void* p : ptrs)
+            if (p) (void)hipFree(p);
+    };
+    bool ok = hipMalloc((void**)&dp, sizeof(*dp) * batch) == hipSuccess &&
+              hipMalloc((void**)&d3, 12 * np) == hipSuccess && hipMalloc((void**)&d2, 8 * np) == hipSuccess &&
+              hipMalloc((void**)&de, 4 * np) == hipSuccess && hipMalloc((void**)&ds, 16 * ns) == hipSuccess &&
+              hipMalloc((void**)&dr, sizeof(*dr) * batch) == hipSuccess && hipMalloc((void**)&dbm, np) == hipSuccess &&
+              hipMalloc((void**)&drm, np) == hipSuccess &&
+              hipMalloc(&dw, orbgpu_pnp_workspace_bytes(total_points, total_samples)) == hipSuccess;
+    if (!ok) {
+        cleanup();
+        return fail(ORBGPU_ERR_HIP, "device allocation failed");
+    }
+    ok = hipMemcpy(dp, problems, sizeof(*dp) * batch, hipMemcpyHostToDevice) == hipSuccess &&
+         (total_points == 0 ||
+          (hipMemcpy(d3, P3w, 12 * (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
+           hipMemcpy(d2, P2, 8 * (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
+           hipMemcpy(de, maxerr, 4 * (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
+           hipMemcpy(dbm, best_mask, (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
+           hipMemcpy(drm, refined_mask, (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess)) &&
+         (total_samples == 0 || hipMemcpy(ds, samples, 16 * (size_t)total_samples, hipMemcpyHostToDevice) == hipSuccess);
+    if (!ok) {
+        cleanup();
+        return fail(ORBGPU_ERR_HIP, "upload failed");
+    }
+    rc = orbgpu_pnp_ransac_batch_device(batch, dp, max_hyp, total_points, total_samples, d3, d2, de, ds, dw, dr, dbm,
+                                        drm, nullptr);
+    if (rc) {
+        cleanup();
+        return rc;
+    }
+    ok = hipDeviceSynchronize() == hipSuccess &&
+         hipMemcpy(results, dr, sizeof(*dr) * batch, hipMemcpyDeviceToHost) == hipSuccess &&
+         (total_points == 0 ||
+          (hipMemcpy(best_mask, dbm, (size_t)total_points, hipMemcpyDeviceToHost) == hipSuccess &&
+           hipMemcpy(refined_mask, drm, (size_t)total_points, hipMemcpyDeviceToHost) == hipSuccess));
+    cleanup();
+    if (!ok) return fail(ORBGPU_ERR_HIP, "PnP RANSAC failed");
     return ORBGPU_OK;
 }
 

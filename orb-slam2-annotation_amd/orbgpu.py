@@ -98,6 +98,10 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_sim3_workspace_bytes.restype = sz
         L.orbgpu_sim3_ransac_batch_device.argtypes = [i, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.orbgpu_sim3_ransac_batch.argtypes = [i, vp, i, vp, vp, vp, vp, i, vp, vp, vp]
+        L.orbgpu_pnp_workspace_bytes.argtypes = [i, i]
+        L.orbgpu_pnp_workspace_bytes.restype = sz
+        L.orbgpu_pnp_ransac_batch_device.argtypes = [i, vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.orbgpu_pnp_ransac_batch.argtypes = [i, vp, i, vp, vp, vp, i, vp, vp, vp, vp]
         _LIB = L
     return _LIB
 

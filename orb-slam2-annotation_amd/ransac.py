@@ -186,3 +186,127 @@ class Sim3Solver:
 
     def get_estimated_scale(self):
         return self.best_s
+
+
+# --------------------------------------------------------------------------
+# PnPsolver
+# --------------------------------------------------------------------------
+class PnPProblem(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("offset", ctypes.c_int), ("min_inliers", ctypes.c_int),
+                ("best_inliers", ctypes.c_int), ("n_hyp", ctypes.c_int), ("sample_offset", ctypes.c_int),
+                ("fu", ctypes.c_float), ("fv", ctypes.c_float), ("uc", ctypes.c_float), ("vc", ctypes.c_float)]
+
+
+class PnPResult(ctypes.Structure):
+    _fields_ = [("found", ctypes.c_int), ("consumed", ctypes.c_int), ("best_inliers", ctypes.c_int),
+                ("best_hyp", ctypes.c_int), ("refined_inliers", ctypes.c_int),
+                ("best_Tcw", ctypes.c_float * 16), ("refined_Tcw", ctypes.c_float * 16)]
+
+
+def draw_sets(n: int, n_iter: int, k: int) -> np.ndarray:
+    """Minimal sets of n_iter iterations: k x (RandomInt(0, size-1), swap
+    with back, pop) from all indices (PnPsolver.cpp:229-244, k = minSet)."""
+    out = np.zeros((n_iter, k), np.int32)
+    for it in range(n_iter):
+        avail = list(range(n))
+        for j in range(k):
+            r = random_int(0, len(avail) - 1)
+            out[it, j] = avail[r]
+            avail[r] = avail[-1]
+            avail.pop()
+    return out
+
+
+def pnp_ransac_batch(problems, P3w, P2, maxerr, samples, best_mask, refined_mask):
+    """Host form of orbgpu_pnp_ransac_batch; masks updated in place."""
+    L = orbgpu.lib()
+    B = len(problems)
+    res = (PnPResult * max(B, 1))()
+    P3w = np.ascontiguousarray(P3w, np.float32)
+    P2 = np.ascontiguousarray(P2, np.float32)
+    e = np.ascontiguousarray(maxerr, np.float32)
+    smp = np.ascontiguousarray(samples, np.int32).reshape(-1, 4)
+    orbgpu._check(L.orbgpu_pnp_ransac_batch(B, ctypes.addressof(problems), len(P3w), P3w.ctypes.data, P2.ctypes.data,
+                                            e.ctypes.data, len(smp), smp.ctypes.data, ctypes.addressof(res),
+                                            best_mask.ctypes.data, refined_mask.ctypes.data),
+                  "orbgpu_pnp_ransac_batch")
+    return res
+
+
+class PnPsolver:
+    """PnPsolver(F, vpMapPointMatches) on the data its constructor gathers
+    (PnPsolver.cpp:104-139): P3w = world positions of the matched MapPoints
+    (mvP3Dw), P2 = their undistorted keypoints (mvP2D), sigma2 = level sigma^2
+    of those keypoints (mvSigma2), (fu, fv, uc, vc) = F.fx, fy, cx, cy,
+    indices = mvKeyPointIndices, n_matches = vpMapPointMatches.size()."""
+
+    def __init__(self, P3w, P2, sigma2, fu, fv, uc, vc, indices=None, n_matches=None):
+        self.P3w = np.ascontiguousarray(P3w, np.float32).reshape(-1, 3)
+        self.P2 = np.ascontiguousarray(P2, np.float32).reshape(-1, 2)
+        self.sigma2 = np.asarray(sigma2, np.float32)
+        self.cam = (float(fu), float(fv), float(uc), float(vc))
+        self.N = len(self.P3w)
+        self.indices = np.arange(self.N) if indices is None else np.asarray(indices)
+        self.n_matches = self.N if n_matches is None else int(n_matches)
+        self.iterations = 0
+        self.best_inliers = 0
+        self.best_mask = np.zeros(self.N, np.uint8)
+        self.best_Tcw = None
+        self.set_ransac_parameters()
+
+    def set_ransac_parameters(self, probability=0.99, min_inliers=8, max_iterations=300, min_set=4, epsilon=0.4,
+                              th2=5.991):
+        """PnPsolver.cpp:159-195."""
+        N = self.N
+        eps = np.float32(epsilon)
+        n_min = int(np.float32(N) * eps)
+        n_min = max(n_min, min_inliers, min_set)
+        self.min_inliers, self.min_set, self.prob = n_min, min_set, probability
+        if N and eps < np.float32(n_min) / np.float32(N):
+            eps = np.float32(n_min) / np.float32(N)
+        if n_min == N:
+            n_it = 1
+        else:
+            with np.errstate(all="ignore"):
+                v = math.log(1 - probability) / math.log(1 - float(eps) ** 3) if 0 < float(eps) < 1 else float("nan")
+            n_it = int(math.ceil(v)) if math.isfinite(v) else -(2 ** 31)
+        self.max_its = max(1, min(n_it, max_iterations))
+        self.maxerr = (self.sigma2 * np.float32(th2)).astype(np.float32)
+
+    def iterate(self, n_iterations):
+        """PnPsolver::iterate (PnPsolver.cpp:203-301): returns (Tcw or None,
+        no_more, inliers[n_matches] bool, n_inliers)."""
+        inl = np.zeros(self.n_matches, bool)
+        if self.N < self.min_inliers:
+            return None, True, np.zeros(0, bool), 0
+        # while (mnIterations < maxIts || nCurrentIterations < nIterations)
+        n_hyp = max(self.max_its - self.iterations, n_iterations)
+        snap = get_state()
+        samples = draw_sets(self.N, n_hyp, self.min_set)
+        prob = (PnPProblem * 1)()
+        p = prob[0]
+        p.n, p.offset, p.min_inliers, p.best_inliers = self.N, 0, self.min_inliers, self.best_inliers
+        p.n_hyp, p.sample_offset = n_hyp, 0
+        p.fu, p.fv, p.uc, p.vc = self.cam
+        bm = self.best_mask.copy()
+        rm = np.zeros(self.N, np.uint8)
+        r = pnp_ransac_batch(prob, self.P3w, self.P2, self.maxerr, samples, bm, rm)[0]
+        set_state(snap)  # consume exactly the draws of the iterations run
+        draw_sets(self.N, r.consumed, self.min_set)
+        self.iterations += r.consumed
+        self.best_inliers = r.best_inliers
+        if r.best_hyp >= 0:
+            self.best_mask = bm
+            self.best_Tcw = np.array(r.best_Tcw, np.float32).reshape(4, 4)
+        if r.found:
+            inl[self.indices[rm.astype(bool)]] = True
+            return np.array(r.refined_Tcw, np.float32).reshape(4, 4), False, inl, r.refined_inliers
+        no_more = self.iterations >= self.max_its
+        if no_more and self.best_inliers >= self.min_inliers:
+            inl[self.indices[self.best_mask.astype(bool)]] = True
+            return self.best_Tcw.copy(), True, inl, self.best_inliers
+        return None, no_more, np.zeros(0, bool), 0
+
+    def find(self):
+        T, _, inl, n = self.iterate(self.max_its)
+        return T, inl, n

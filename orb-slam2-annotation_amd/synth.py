@@ -176,3 +176,30 @@ def sim3_problem(n: int, inlier_frac: float, seed: int, fix_scale: bool = False,
     return {"X1": X1.astype(np.float32), "X2": X2.astype(np.float32),
             "sigma2_1": sig[oct1].astype(np.float32), "sigma2_2": sig[oct2].astype(np.float32),
             "K1": K.astype(np.float32), "K2": K.astype(np.float32), "s": s, "R": R, "t": t, "inlier": inl}
+
+
+def pnp_problem(n: int, inlier_frac: float, seed: int, noise_px: float = 0.5):
+    """Relocalisation correspondences of a PnPsolver (PnPsolver.cpp:104-139):
+    MapPoints in world coordinates seen by a camera at a random pose; inliers
+    project to their keypoint (plus pixel noise), outliers to random pixels.
+    Returns dict(P3w, P2, sigma2, cam=(fu, fv, uc, vc), R, t, inlier)."""
+    rng = np.random.default_rng(seed)
+    fu, fv, uc, vc = 517.3, 516.5, 318.6, 255.3
+    ang = rng.uniform(-0.5, 0.5, size=3)
+    cx, cy, cz = np.cos(ang)
+    sx, sy, sz = np.sin(ang)
+    R = (np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]]) @ np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]]) @
+         np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]]))
+    t = rng.uniform(-1, 1, size=3)
+    z = rng.uniform(1.5, 10.0, size=n)
+    u = rng.uniform(10, 630, size=n)
+    v = rng.uniform(10, 470, size=n)
+    Xc = np.stack([(u - uc) / fu * z, (v - vc) / fv * z, z], 1)
+    P3w = (Xc - t) @ R  # R^T (Xc - t)
+    inl = rng.uniform(size=n) < inlier_frac
+    P2 = np.stack([u, v], 1) + rng.normal(scale=noise_px, size=(n, 2))
+    P2[~inl] = np.stack([rng.uniform(0, 640, size=(~inl).sum()), rng.uniform(0, 480, size=(~inl).sum())], 1)
+    octave = rng.integers(0, 8, size=n)
+    sig = np.float32(1.2) ** (2 * np.arange(8))
+    return {"P3w": P3w.astype(np.float32), "P2": P2.astype(np.float32), "sigma2": sig[octave].astype(np.float32),
+            "cam": (fu, fv, uc, vc), "R": R, "t": t, "inlier": inl}

@@ -9,7 +9,7 @@ import pytest
 import torch
 
 ROOT = Path(__file__).resolve().parent.parent
-HEADERS = [ROOT / "include" / "orbgpu.h", ROOT / "include" / "orbgpu_debug.h"]
+HEADERS = sorted((ROOT / "include").glob("orbgpu*.h"))
 
 
 def declared_functions():
