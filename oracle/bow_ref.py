@@ -1,0 +1,210 @@
+"""CPU restatement of the DBoW2 bag-of-words path and ORBmatcher::SearchByBoW.
+
+TEST INFRASTRUCTURE ONLY: the parity oracle for csrc/bow.hip (imported by
+tests/ and nothing else).  Citations: T = /root/reference/ORB-SLAM2/
+Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h, B = .../BowVector.cpp,
+FV = .../FeatureVector.cpp, M = /root/reference/ORB-SLAM2/src/ORBmatcher.cpp.
+Integer/index results are compared bit-exactly; BowVector weights (double)
+too -- the GPU sums them in the same order.  DBoW2 ships no vocabulary or
+fixture here (ORBvoc.txt is absent): the vocabularies are synthetic, so the
+vocabulary-dependent results are "parity unpinned" against the real one.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+
+class Vocabulary:
+    """TemplatedVocabulary nodes: parent, children (file order), descriptor,
+    weight, word_id; node 0 is the root."""
+
+    def __init__(self, k, L, scoring, weighting):
+        self.k, self.L, self.scoring, self.weighting = k, L, scoring, weighting
+        self.parent = [0]
+        self.children = [[]]
+        self.desc = [np.zeros(32, np.uint8)]
+        self.weight = [0.0]
+        self.word_id = [0]
+        self.n_words = 0
+
+    def _add(self, pid, leaf, desc, weight):
+        nid = len(self.parent)
+        self.parent.append(pid)
+        self.children.append([])
+        self.children[pid].append(nid)
+        self.desc.append(np.asarray(desc, np.uint8))
+        self.weight.append(float(weight))
+        if leaf > 0:
+            self.word_id.append(self.n_words)
+            self.n_words += 1
+        else:
+            self.word_id.append(0)
+
+    @classmethod
+    def from_arrays(cls, k, L, scoring, weighting, parent, is_leaf, desc, weight):
+        v = cls(k, L, scoring, weighting)
+        for i in range(len(parent)):
+            v._add(int(parent[i]), int(is_leaf[i]), desc[i], weight[i])
+        return v
+
+    @classmethod
+    def load_text(cls, path):
+        """loadFromTextFile (T:1359-1448): the `while(!f.eof()) getline` loop
+        sees one more (empty) line when the file ends with a newline."""
+        text = open(path).read()
+        lines = text.split("\n")
+        k, L, n1, n2 = (int(x) for x in lines[0].split()[:4])
+        v = cls(k, L, n1, n2)
+        for line in lines[1:]:
+            tok = line.split()
+            pid = int(tok[0]) if len(tok) > 0 else 0
+            leaf = int(tok[1]) if len(tok) > 1 else 0
+            d = np.zeros(32, np.uint8)
+            for j in range(32):
+                if 2 + j < len(tok):
+                    d[j] = int(tok[2 + j]) & 0xFF
+            w = float(tok[34]) if len(tok) > 34 else 0.0
+            v._add(pid, leaf, d, w)
+        return v
+
+    def transform_one(self, f, levelsup):
+        """transform(feature, word, weight, nid, levelsup) (T:1242-1283)."""
+        nid_level = self.L - levelsup
+        nid = 0
+        final = 0
+        level = 0
+        while True:
+            level += 1
+            ch = self.children[final]
+            best = ch[0]
+            best_d = int(np.unpackbits(np.bitwise_xor(f, self.desc[best])).sum())
+            for c in ch[1:]:
+                d = int(np.unpackbits(np.bitwise_xor(f, self.desc[c])).sum())
+                if d < best_d:
+                    best_d, best = d, c
+            final = best
+            if level == nid_level:
+                nid = final
+            if not self.children[final]:
+                break
+        return self.word_id[final], nid, self.weight[final]
+
+    def transform(self, feats, levelsup):
+        """transform(features, BowVector, FeatureVector, levelsup) (T:1151-1230).
+        Returns (words, nodes, weights, fv: dict node -> [features],
+        bow: dict word -> value)."""
+        words, nodes, weights = [], [], []
+        bow, fv = {}, {}
+        tf = self.weighting in (0, 1)
+        for i, f in enumerate(feats):
+            w_id, nid, w = self.transform_one(f, levelsup)
+            words.append(w_id); nodes.append(nid); weights.append(w)
+            if w > 0:
+                if tf:  # BowVector::addWeight (B:34-46)
+                    bow[w_id] = bow[w_id] + w if w_id in bow else w
+                elif w_id not in bow:  # addIfNotExist (B:50-58)
+                    bow[w_id] = w
+                fv.setdefault(nid, []).append(i)  # FeatureVector::addFeature (FV:31-45)
+        bow = dict(sorted(bow.items()))
+        must = self.scoring != 5
+        if bow and not must and tf:
+            nd = float(len(bow))
+            bow = {k: v / nd for k, v in bow.items()}
+        if must:  # BowVector::normalize (B:62-90)
+            if self.scoring == 1:
+                norm = 0.0
+                for v in bow.values():
+                    norm += v * v
+                norm = math.sqrt(norm)
+            else:
+                norm = 0.0
+                for v in bow.values():
+                    norm += abs(v)
+            if norm > 0.0:
+                bow = {k: v / norm for k, v in bow.items()}
+        return words, nodes, weights, dict(sorted(fv.items())), bow
+
+
+def _dist(a, b):
+    return int(np.unpackbits(np.bitwise_xor(a, b)).sum())
+
+
+def _three_maxima(hist):
+    """ComputeThreeMaxima (M:1792-1833)."""
+    max1 = max2 = max3 = 0
+    i1 = i2 = i3 = -1
+    for i, h in enumerate(hist):
+        s = len(h)
+        if s > max1:
+            max3, max2, max1, i3, i2, i1 = max2, max1, s, i2, i1, i
+        elif s > max2:
+            max3, max2, i3, i2 = max2, s, i2, i
+        elif s > max3:
+            max3, i3 = s, i
+    if max2 < np.float32(0.1) * np.float32(max1):
+        i2 = i3 = -1
+    elif max3 < np.float32(0.1) * np.float32(max1):
+        i3 = -1
+    return i1, i2, i3
+
+
+def search_by_bow(mode, fvA, descA, angA, validA, fvB, descB, angB, validB, nnratio=0.6, check_ori=True):
+    """SearchByBoW(KF, F) (mode 0, M:205-348) and SearchByBoW(KF1, KF2)
+    (mode 1, M:604-743).  fv: dict node -> [feature indices] (ascending
+    nodes).  Returns (nmatches, match) with match indexed by F (mode 0) or
+    KF1 (mode 1)."""
+    HL, TH_LOW = 30, 50
+    factor = np.float32(HL) / np.float32(360.0)
+    nout = len(descB) if mode == 0 else len(descA)
+    match = [-1] * nout
+    matched2 = [False] * len(descB)
+    hist = [[] for _ in range(HL)]
+    nm = 0
+    for node in sorted(set(fvA) & set(fvB)):
+        for ia in fvA[node]:
+            if not validA[ia]:
+                continue
+            b1, b2, bidx = 256, 256, -1
+            for ib in fvB[node]:
+                if mode == 0:
+                    if match[ib] >= 0:
+                        continue
+                else:
+                    if matched2[ib] or not validB[ib]:
+                        continue
+                d = _dist(descA[ia], descB[ib])
+                if d < b1:
+                    b2, b1, bidx = b1, d, ib
+                elif d < b2:
+                    b2 = d
+            ok = b1 <= TH_LOW if mode == 0 else b1 < TH_LOW
+            if not ok or not (np.float32(b1) < np.float32(nnratio) * np.float32(b2)):
+                continue
+            if mode == 0:
+                match[bidx] = ia
+                out = bidx
+            else:
+                match[ia] = bidx
+                matched2[bidx] = True
+                out = ia
+            if check_ori:
+                rot = np.float32(np.float32(angA[ia]) - np.float32(angB[bidx]))
+                if rot < 0.0:
+                    rot = np.float32(rot + np.float32(360.0))
+                v = float(np.float32(rot * factor))
+                b = int(math.copysign(math.floor(abs(v) + 0.5), v))
+                if b == HL:
+                    b = 0
+                hist[b].append(out)
+            nm += 1
+    if check_ori:
+        i1, i2, i3 = _three_maxima(hist)
+        for i in range(HL):
+            if i in (i1, i2, i3):
+                continue
+            for idx in hist[i]:
+                match[idx] = -1
+                nm -= 1
+    return nm, np.array(match, np.int32)

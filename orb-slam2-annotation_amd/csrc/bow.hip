@@ -1,0 +1,359 @@
+// bow.hip -- bag-of-words kernels: DBoW2 TemplatedVocabulary::transform,
+// BowVector / FeatureVector assembly, and ORBmatcher::SearchByBoW.
+//
+//   bow_transform_kernel   one thread per descriptor walks the vocabulary
+//                          tree (TemplatedVocabulary.h:1242-1283): Hamming
+//                          distance to each child, first minimum wins, the
+//                          node passed at level L-levelsup is the direct-index
+//                          node, the leaf gives word id and weight.
+//   bow_vectors_kernel     one block per frame: (node, feature) and (word,
+//                          feature) keys sorted in LDS (bitonic) give the
+//                          FeatureVector (FeatureVector::addFeature appends
+//                          in feature order) and the BowVector (addWeight
+//                          sums a word's weights in feature order, then
+//                          normalize() divides by the L1/L2 norm summed over
+//                          words in ascending order, TemplatedVocabulary.h:
+//                          1151-1230, BowVector.cpp:34-90).
+//   search_by_bow_kernel   one block per frame pair; DBoW2 direct-index nodes
+//                          partition the features, so nodes are independent
+//                          and one lane walks one common node sequentially
+//                          (ORBmatcher.cpp:205-348, :604-743); the rotation
+//                          histogram, ComputeThreeMaxima and the cull follow.
+#include "../../include/orbgpu_bow.h"
+#include "bow_kernels.h"
+
+namespace orbgpu {
+
+namespace {
+
+constexpr int kMaxStride = 4096;
+constexpr int kHL = 30, kThLow = 50;
+
+__device__ inline int hamming32(const uint8_t* a, const uint8_t* b) {
+    const unsigned long long* x = reinterpret_cast<const unsigned long long*>(a);
+    const unsigned long long* y = reinterpret_cast<const unsigned long long*>(b);
+    return __popcll(x[0] ^ y[0]) + __popcll(x[1] ^ y[1]) + __popcll(x[2] ^ y[2]) + __popcll(x[3] ^ y[3]);
+}
+
+__global__ __launch_bounds__(256) void bow_transform_kernel(VocabDev V, int batch, const uint8_t* __restrict__ desc,
+                                                            const int* __restrict__ counts, int stride, int levelsup,
+                                                            int* __restrict__ word, int* __restrict__ node,
+                                                            double* __restrict__ weight) {
+    const long g = (long)blockIdx.x * 256 + threadIdx.x;
+    const int f = (int)(g / stride), i = (int)(g - (long)f * stride);
+    if (f >= batch || i >= counts[f]) return;
+    const size_t slot = (size_t)f * stride + i;
+    const uint8_t* d = desc + 32 * slot;
+    unsigned long long q[4];
+    for (int k = 0; k < 4; ++k) q[k] = reinterpret_cast<const unsigned long long*>(d)[k];
+    const int nid_level = V.L - levelsup;
+    int nid = 0, fin = 0, level = 0;
+    do {
+        ++level;
+        const int cs = V.child_start[fin], cc = V.child_count[fin];
+        int best = V.children[cs], best_d = 0x7FFFFFFF;
+        for (int j = 0; j < cc; ++j) {
+            const int c = V.children[cs + j];
+            const unsigned long long* e = reinterpret_cast<const unsigned long long*>(V.desc + 32 * (size_t)c);
+            const int dd = __popcll(q[0] ^ e[0]) + __popcll(q[1] ^ e[1]) + __popcll(q[2] ^ e[2]) + __popcll(q[3] ^ e[3]);
+            if (dd < best_d) {
+                best_d = dd;
+                best = c;
+            }
+        }
+        fin = best;
+        if (level == nid_level) nid = fin;
+    } while (V.child_count[fin] > 0);
+    word[slot] = V.word_id[fin];
+    node[slot] = nid;
+    weight[slot] = V.weight[fin];
+}
+
+// ascending bitonic sort of n (power of two) keys in LDS, all threads
+__device__ void bitonic_sort(unsigned long long* k, int n) {
+    for (int size = 2; size <= n; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            __syncthreads();
+            for (int i = threadIdx.x; i < n / 2; i += blockDim.x) {
+                const int lo = 2 * i - (i & (stride - 1));
+                const int hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const unsigned long long a = k[lo], b = k[hi];
+                if ((a > b) == up) {
+                    k[lo] = b;
+                    k[hi] = a;
+                }
+            }
+        }
+    __syncthreads();
+}
+
+// exclusive prefix sum of flags[0..n) (n <= kMaxStride) into pos[], total returned to all threads
+__device__ int block_scan(const unsigned char* flags, int* pos, int n, int* s_tmp) {
+    const int per = (n + blockDim.x - 1) / blockDim.x;
+    const int b = threadIdx.x * per, e = min(b + per, n);
+    int sum = 0;
+    for (int i = b; i < e; ++i) sum += flags[i];
+    s_tmp[threadIdx.x] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int t = 0; t < (int)blockDim.x; ++t) {
+            const int v = s_tmp[t];
+            s_tmp[t] = acc;
+            acc += v;
+        }
+        s_tmp[blockDim.x] = acc;
+    }
+    __syncthreads();
+    int acc = s_tmp[threadIdx.x];
+    for (int i = b; i < e; ++i) {
+        pos[i] = acc;
+        acc += flags[i];
+    }
+    const int total = s_tmp[blockDim.x];
+    __syncthreads();
+    return total;
+}
+
+__global__ __launch_bounds__(1024) void bow_vectors_kernel(VocabDev V, const int* __restrict__ counts, int stride,
+                                                           const int* __restrict__ word, const int* __restrict__ node,
+                                                           const double* __restrict__ weight,
+                                                           int* __restrict__ fv_nodes, int* __restrict__ fv_offsets,
+                                                           int* __restrict__ fv_features, int* __restrict__ fv_n,
+                                                           int* __restrict__ bow_words, double* __restrict__ bow_values,
+                                                           int* __restrict__ bow_n) {
+    __shared__ unsigned long long s_key[kMaxStride];  // later reused as the BowVector values
+    __shared__ unsigned char s_flag[kMaxStride];
+    __shared__ int s_pos[kMaxStride];
+    __shared__ int s_tmp[1025];
+    __shared__ int s_kept;
+    __shared__ double s_norm;
+    const int f = blockIdx.x;
+    const int n = counts[f];
+    const size_t base = (size_t)f * stride;
+    if (n > stride) {  // rejected, never truncated
+        if (threadIdx.x == 0) fv_n[f] = bow_n[f] = -1;
+        return;
+    }
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    if (threadIdx.x == 0) s_kept = 0;
+    // ---- FeatureVector: (node, feature) for features with weight > 0
+    int kept = 0;
+    for (int i = threadIdx.x; i < n2; i += blockDim.x) {
+        const bool in = i < n && weight[base + i] > 0;
+        kept += in;
+        s_key[i] = in ? ((unsigned long long)(unsigned)node[base + i] << 32) | (unsigned)i : ~0ull;
+    }
+    __syncthreads();
+    atomicAdd(&s_kept, kept);
+    bitonic_sort(s_key, n2);
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        s_flag[i] = s_key[i] != ~0ull && (i == 0 || (s_key[i] >> 32) != (s_key[i - 1] >> 32));
+    __syncthreads();
+    const int nnodes = block_scan(s_flag, s_pos, n, s_tmp);
+    int* FO = fv_offsets + (size_t)f * (stride + 1);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        if (s_key[i] == ~0ull) continue;
+        fv_features[base + i] = (int)(s_key[i] & 0xFFFFFFFFu);
+        if (s_flag[i]) {
+            fv_nodes[base + s_pos[i]] = (int)(s_key[i] >> 32);
+            FO[s_pos[i]] = i;
+        }
+    }
+    if (threadIdx.x == 0) {
+        FO[nnodes] = s_kept;
+        fv_n[f] = nnodes;
+    }
+    __syncthreads();
+    // ---- BowVector: (word, feature) for features with weight > 0
+    for (int i = threadIdx.x; i < n2; i += blockDim.x)
+        s_key[i] = (i < n && weight[base + i] > 0) ? ((unsigned long long)(unsigned)word[base + i] << 32) | (unsigned)i
+                                                   : ~0ull;
+    bitonic_sort(s_key, n2);
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        s_flag[i] = s_key[i] != ~0ull && (i == 0 || (s_key[i] >> 32) != (s_key[i - 1] >> 32));
+    __syncthreads();
+    const int nwords = block_scan(s_flag, s_pos, n, s_tmp);
+    const bool tf = V.weighting == 0 || V.weighting == 1;  // TF_IDF, TF: addWeight; IDF, BINARY: addIfNotExist
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        if (!s_flag[i]) continue;
+        double v = weight[base + (s_key[i] & 0xFFFFFFFFu)];
+        if (tf)  // the word's weights summed in feature order
+            for (int j = i + 1; j < n && s_key[j] != ~0ull && (s_key[j] >> 32) == (s_key[i] >> 32); ++j)
+                v += weight[base + (s_key[j] & 0xFFFFFFFFu)];
+        bow_values[base + s_pos[i]] = v;
+        bow_words[base + s_pos[i]] = (int)(s_key[i] >> 32);
+    }
+    __syncthreads();
+    double* s_val = reinterpret_cast<double*>(s_key);
+    for (int w = threadIdx.x; w < nwords; w += blockDim.x) s_val[w] = bow_values[base + w];
+    __syncthreads();
+    // mustNormalize: every scoring but DOT_PRODUCT (5); L2 norm for L2_NORM (1)
+    const bool must = V.scoring != 5;
+    if (threadIdx.x == 0) {
+        double norm = 0.0;
+        if (must) {
+            if (V.scoring == 1) {
+                for (int w = 0; w < nwords; ++w) norm += s_val[w] * s_val[w];
+                norm = sqrt(norm);
+            } else {
+                for (int w = 0; w < nwords; ++w) norm += fabs(s_val[w]);
+            }
+        }
+        s_norm = norm;
+        bow_n[f] = nwords;
+    }
+    __syncthreads();
+    const double norm = s_norm;
+    for (int w = threadIdx.x; w < nwords; w += blockDim.x) {
+        double v = s_val[w];
+        if (!must && tf) v /= (double)nwords;
+        if (must && norm > 0.0) v /= norm;
+        bow_values[base + w] = v;
+    }
+}
+
+__device__ inline int find_node(const int* nodes, int n, int key) {
+    int lo = 0, hi = n - 1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        const int v = nodes[mid];
+        if (v == key) return mid;
+        if (v < key) lo = mid + 1; else hi = mid - 1;
+    }
+    return -1;
+}
+
+__global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbgpu_bow_frame* __restrict__ A_,
+                                                            const orbgpu_bow_frame* __restrict__ B_, float nnratio,
+                                                            int check_ori, int stride, int* __restrict__ match_g,
+                                                            int* __restrict__ nmatches) {
+    __shared__ unsigned int s_used[kMaxStride / 32];  // vbMatched2 (KF_KF)
+    __shared__ signed char s_bin[kMaxStride];
+    __shared__ int s_hist[kHL];
+    __shared__ int s_ind[3];
+    __shared__ int s_cnt;
+    const orbgpu_bow_frame A = A_[blockIdx.x], B = B_[blockIdx.x];
+    const int nout = mode == ORBGPU_BOW_KF_F ? B.n : A.n;
+    int* match = match_g + (size_t)blockIdx.x * stride;
+    if (A.n > stride || B.n > stride) {  // rejected, never truncated
+        if (threadIdx.x == 0) nmatches[blockIdx.x] = -1;
+        return;
+    }
+    for (int i = threadIdx.x; i < nout; i += blockDim.x) {
+        match[i] = -1;
+        s_bin[i] = -1;
+    }
+    for (int i = threadIdx.x; i < kMaxStride / 32; i += blockDim.x) s_used[i] = 0;
+    if (threadIdx.x < kHL) s_hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    const float factor = (float)kHL / 360.0f;
+    for (int a = threadIdx.x; a < A.fv_n; a += blockDim.x) {
+        const int b = find_node(B.fv_nodes, B.fv_n, A.fv_nodes[a]);
+        if (b < 0) continue;
+        const int a0 = A.fv_offsets[a], a1 = A.fv_offsets[a + 1];
+        const int b0 = B.fv_offsets[b], b1 = B.fv_offsets[b + 1];
+        for (int ia_ = a0; ia_ < a1; ++ia_) {
+            const int ia = A.fv_features[ia_];
+            if (!A.valid[ia]) continue;
+            const uint8_t* da = A.desc + 32 * (size_t)ia;
+            int best1 = 256, best2 = 256, bidx = -1;
+            for (int ib_ = b0; ib_ < b1; ++ib_) {
+                const int ib = B.fv_features[ib_];
+                if (mode == ORBGPU_BOW_KF_F) {
+                    if (match[ib] >= 0) continue;
+                } else {
+                    if ((s_used[ib >> 5] >> (ib & 31)) & 1u) continue;
+                    if (!B.valid[ib]) continue;
+                }
+                const int dist = hamming32(da, B.desc + 32 * (size_t)ib);
+                if (dist < best1) {
+                    best2 = best1;
+                    best1 = dist;
+                    bidx = ib;
+                } else if (dist < best2) {
+                    best2 = dist;
+                }
+            }
+            const bool pass = mode == ORBGPU_BOW_KF_F ? best1 <= kThLow : best1 < kThLow;
+            if (!pass || !((float)best1 < nnratio * (float)best2)) continue;
+            int out;
+            if (mode == ORBGPU_BOW_KF_F) {
+                match[bidx] = ia;
+                out = bidx;
+            } else {
+                match[ia] = bidx;
+                atomicOr(&s_used[bidx >> 5], 1u << (bidx & 31));
+                out = ia;
+            }
+            if (check_ori) {
+                float rot = A.angle[ia] - B.angle[bidx];
+                if (rot < 0.0f) rot += 360.0f;
+                int bin = (int)roundf(rot * factor);
+                if (bin == kHL) bin = 0;
+                s_bin[out] = (signed char)bin;
+                atomicAdd(&s_hist[bin], 1);
+            }
+        }
+    }
+    __syncthreads();
+    if (check_ori && threadIdx.x == 0) {  // ComputeThreeMaxima (ORBmatcher.cpp:1792-1833)
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < kHL; ++i) {
+            const int s = s_hist[i];
+            if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+            else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+            else if (s > max3) { max3 = s; ind3 = i; }
+        }
+        if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+        else if ((float)max3 < 0.1f * (float)max1) ind3 = -1;
+        s_ind[0] = ind1;
+        s_ind[1] = ind2;
+        s_ind[2] = ind3;
+    }
+    __syncthreads();
+    int cnt = 0;
+    for (int i = threadIdx.x; i < nout; i += blockDim.x) {
+        if (match[i] < 0) continue;
+        const int bin = s_bin[i];
+        if (check_ori && bin != s_ind[0] && bin != s_ind[1] && bin != s_ind[2]) {
+            match[i] = -1;
+            continue;
+        }
+        ++cnt;
+    }
+    atomicAdd(&s_cnt, cnt);
+    __syncthreads();
+    if (threadIdx.x == 0) nmatches[blockIdx.x] = s_cnt;
+}
+
+}  // namespace
+
+int bow_max_stride() { return kMaxStride; }
+
+hipError_t launch_bow_transform(const VocabDev& V, int batch, const uint8_t* desc, const int* counts, int stride,
+                                int levelsup, int* word, int* node, double* weight, int* fv_nodes, int* fv_offsets,
+                                int* fv_features, int* fv_n, int* bow_words, double* bow_values, int* bow_n,
+                                hipStream_t stream) {
+    if (batch <= 0) return hipSuccess;
+    const long total = (long)batch * stride;
+    hipLaunchKernelGGL(bow_transform_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, V, batch,
+                       desc, counts, stride, levelsup, word, node, weight);
+    hipLaunchKernelGGL(bow_vectors_kernel, dim3(batch), dim3(1024), 0, stream, V, counts, stride, word, node, weight,
+                       fv_nodes, fv_offsets, fv_features, fv_n, bow_words, bow_values, bow_n);
+    return hipGetLastError();
+}
+
+hipError_t launch_search_by_bow(int mode, int batch, const orbgpu_bow_frame* a, const orbgpu_bow_frame* b,
+                                float nnratio, int check_ori, int stride, int* match, int* nmatches,
+                                hipStream_t stream) {
+    if (batch <= 0) return hipSuccess;
+    hipLaunchKernelGGL(search_by_bow_kernel, dim3(batch), dim3(256), 0, stream, mode, a, b, nnratio, check_ori,
+                       stride, match, nmatches);
+    return hipGetLastError();
+}
+
+}  // namespace orbgpu

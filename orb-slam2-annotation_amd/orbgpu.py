@@ -102,6 +102,16 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_pnp_workspace_bytes.restype = sz
         L.orbgpu_pnp_ransac_batch_device.argtypes = [i, vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.orbgpu_pnp_ransac_batch.argtypes = [i, vp, i, vp, vp, vp, i, vp, vp, vp, vp]
+        # orbgpu_bow.h
+        L.orbgpu_vocabulary_load_text.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
+        L.orbgpu_vocabulary_create.argtypes = [i, i, i, i, i, vp, vp, vp, vp, ctypes.POINTER(vp)]
+        L.orbgpu_vocabulary_destroy.argtypes = [vp]
+        L.orbgpu_vocabulary_get_info.argtypes = [vp, vp]
+        L.orbgpu_bow_transform_batch_device.argtypes = [vp, i, vp, vp, i, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                                        vp]
+        L.orbgpu_bow_transform.argtypes = [vp, i, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.orbgpu_search_by_bow_batch_device.argtypes = [i, i, vp, vp, f, i, i, vp, vp, vp]
+        L.orbgpu_search_by_bow.argtypes = [i, vp, vp, f, i, vp, vp]
         _LIB = L
     return _LIB
 

@@ -203,3 +203,65 @@ def pnp_problem(n: int, inlier_frac: float, seed: int, noise_px: float = 0.5):
     sig = np.float32(1.2) ** (2 * np.arange(8))
     return {"P3w": P3w.astype(np.float32), "P2": P2.astype(np.float32), "sigma2": sig[octave].astype(np.float32),
             "cam": (fu, fv, uc, vc), "R": R, "t": t, "inlier": inl}
+
+
+def synthetic_vocabulary(k: int, L: int, seed: int, flip: float = 0.22):
+    """A DBoW2-shaped vocabulary tree in file (BFS) order: node descriptors
+    derived from their parent's by flipping each bit with probability
+    `flip`, leaves at depth L with positive idf-like weights.  Returns
+    (parent, is_leaf, desc[n,32], weight) without the root (node 0)."""
+    rng = np.random.default_rng(seed)
+    parent, is_leaf, desc, weight = [], [], [], []
+    root = rng.integers(0, 256, 32, dtype=np.uint8)
+    level_nodes = [(0, root)]
+    for depth in range(1, L + 1):
+        nxt = []
+        for pid, pdesc in level_nodes:
+            for _ in range(k):
+                bits = np.unpackbits(pdesc)
+                m = rng.uniform(size=256) < flip
+                d = np.packbits(bits ^ m.astype(np.uint8))
+                nid = len(parent) + 1
+                parent.append(pid)
+                is_leaf.append(1 if depth == L else 0)
+                desc.append(d)
+                weight.append(float(rng.uniform(0.5, 5.0)) if depth == L else 0.0)
+                nxt.append((nid, d))
+        level_nodes = nxt
+    return (np.array(parent, np.int32), np.array(is_leaf, np.int32), np.array(desc, np.uint8),
+            np.array(weight, np.float64))
+
+
+def write_vocabulary_text(path, k, L, scoring, weighting, parent, is_leaf, desc, weight, trailing_newline=False):
+    """DBoW2 text format: 'k L scoring weighting', then 'parent isLeaf d0..d31
+    weight' per node (no trailing newline unless asked: the reference loader
+    turns it into a spurious node)."""
+    lines = [f"{k} {L} {scoring} {weighting}"]
+    for i in range(len(parent)):
+        lines.append(f"{parent[i]} {is_leaf[i]} " + " ".join(str(int(b)) for b in desc[i]) + " " + repr(float(weight[i])))
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + ("\n" if trailing_newline else ""))
+
+
+def bow_frame_pair(voc_desc_leaves: np.ndarray, n: int, shared: float, seed: int, flip: float = 0.04):
+    """Two frames' descriptors for SearchByBoW: frame-2 feature j for
+    j < shared*n is frame-1 feature perm[j] with a few bits flipped (true
+    correspondences), the rest are fresh; descriptors start near random
+    vocabulary leaves.  Angles: frame 2 = frame 1 + 10 deg for shared ones."""
+    rng = np.random.default_rng(seed)
+    base = voc_desc_leaves[rng.integers(0, len(voc_desc_leaves), n)]
+
+    def jitter(d, p):
+        bits = np.unpackbits(d, axis=1)
+        m = (rng.uniform(size=bits.shape) < p).astype(np.uint8)
+        return np.packbits(bits ^ m, axis=1)
+
+    d1 = jitter(base, 0.08)
+    a1 = rng.uniform(0, 360, n).astype(np.float32)
+    ns = int(shared * n)
+    perm = rng.permutation(n)
+    d2 = jitter(voc_desc_leaves[rng.integers(0, len(voc_desc_leaves), n)], 0.08)
+    a2 = rng.uniform(0, 360, n).astype(np.float32)
+    d2[:ns] = jitter(d1[perm[:ns]], flip)
+    a2[:ns] = np.mod(a1[perm[:ns]] + 10.0, 360.0).astype(np.float32)
+    return d1, a1, d2, a2

@@ -7,8 +7,11 @@ wrote -- so the select takes a stale SCC from an earlier scalar op
 (reproducer: tools/scc_repro.hip).  This script scans device assembly
 (`hipcc -S --cuda-device-only`) and reports every s_cselect / s_cbranch_scc*
 whose nearest preceding definition of SCC-or-VCC in the same basic block is
-a VALU compare into VCC.  build() runs it over every kernel and fails the
-build on a hit.
+a VALU compare into VCC, unless the SCC the consumer actually reads was set
+in that block by `s_and_b64 s, vcc, exec` -- the compiler's uniform lowering
+of an earlier compare (a later v_cmp into VCC for another purpose may sit
+in between).  build() runs it over every kernel and fails the build on a
+hit.
 """
 from __future__ import annotations
 
@@ -19,6 +22,7 @@ SCC_WRITERS = re.compile(
     r"^\s*s_(cmp|cmpk|and|or|xor|andn2|orn2|nand|nor|xnor|add|addc|sub|subb|min|max|lshl|lshr|ashr|bfe|"
     r"not|abs|bitcmp|absdiff|lshl\d_add|mul_hi|cselect_b|movk)_?")
 VCC_CMP = re.compile(r"^\s*v_cmp\w*_e32\s+vcc")
+UNIFORM_AND = re.compile(r"^\s*s_and_b64\s+s\[\d+:\d+\],\s*(vcc,\s*exec|exec,\s*vcc)\s*$")
 CONSUMER = re.compile(r"^\s*(s_cselect_b(32|64)|s_cbranch_scc[01])\b")
 LABEL = re.compile(r"^\S+:")
 
@@ -28,17 +32,22 @@ def scan(lines):
     for i, line in enumerate(lines):
         if not CONSUMER.match(line):
             continue
-        for j in range(i - 1, max(-1, i - 40), -1):
+        cmp_at = None  # nearest v_cmp into VCC above the consumer, if it comes before any SCC writer
+        for j in range(i - 1, max(-1, i - 60), -1):
             prev = lines[j]
             if LABEL.match(prev):
                 break
             if prev.lstrip().startswith(";"):
                 continue
             if SCC_WRITERS.match(prev) and not prev.lstrip().startswith("s_cselect"):
+                if cmp_at is not None and not UNIFORM_AND.match(prev):
+                    hits.append((i + 1, line.strip(), cmp_at + 1, lines[cmp_at].strip()))
+                cmp_at = None
                 break
-            if VCC_CMP.match(prev):
-                hits.append((i + 1, line.strip(), j + 1, prev.strip()))
-                break
+            if VCC_CMP.match(prev) and cmp_at is None:
+                cmp_at = j
+        if cmp_at is not None:  # reached the block start: SCC comes from another block
+            hits.append((i + 1, line.strip(), cmp_at + 1, lines[cmp_at].strip()))
     return hits
 
 
