@@ -112,6 +112,10 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_bow_transform.argtypes = [vp, i, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.orbgpu_search_by_bow_batch_device.argtypes = [i, i, vp, vp, f, i, i, vp, vp, vp]
         L.orbgpu_search_by_bow.argtypes = [i, vp, vp, f, i, vp, vp]
+        # orbgpu_proj.h
+        L.orbgpu_is_in_frustum_device.argtypes = [vp, i, vp, vp, vp, vp, f, vp, vp, vp, vp]
+        L.orbgpu_search_by_projection_batch_device.argtypes = [i, vp, i, vp, vp, vp]
+        L.orbgpu_search_by_projection.argtypes = [vp, vp, vp]
         _LIB = L
     return _LIB
 

@@ -265,3 +265,88 @@ def bow_frame_pair(voc_desc_leaves: np.ndarray, n: int, shared: float, seed: int
     d2[:ns] = jitter(d1[perm[:ns]], flip)
     a2[:ns] = np.mod(a1[perm[:ns]] + 10.0, 360.0).astype(np.float32)
     return d1, a1, d2, a2
+
+
+def _pose(rng, max_angle=0.3, max_t=0.5):
+    ang = rng.uniform(-max_angle, max_angle, size=3)
+    cx, cy, cz = np.cos(ang)
+    sx, sy, sz = np.sin(ang)
+    R = (np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]]) @ np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]]) @
+         np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]]))
+    T = np.eye(4)
+    T[:3, :3] = R
+    T[:3, 3] = rng.uniform(-max_t, max_t, size=3)
+    return T
+
+
+def projection_scenario(n_points: int, n_distractors: int, seed: int, stereo: bool = False, scale: float = 1.0):
+    """A frame observing map points, for the SearchByProjection variants:
+    world points in front of the camera (Tcw), keypoints at their projections
+    (pixel noise, octave = the level PredictScale gives, descriptor = the
+    point's with a few bits flipped) plus distractor keypoints (random, some
+    with descriptors close to points').  Returns (target dict, points dict)
+    in the layouts of proj.py / proj_ref.py; `scale` != 1 makes Tcw a Sim3."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = 517.3, 516.5, 318.6, 255.3
+    W, H = 640, 480
+    T = _pose(rng)
+    Rcw, tcw = T[:3, :3], T[:3, 3]
+    z = rng.uniform(1.0, 8.0, size=n_points)
+    u = rng.uniform(-20, W + 20, size=n_points)
+    v = rng.uniform(-20, H + 20, size=n_points)
+    Xc = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], 1)
+    Xw = (Xc - tcw) @ Rcw
+    Ow = -Rcw.T @ tcw
+    dist = np.linalg.norm(Xw - Ow, axis=1)
+    lvl_ref = rng.integers(0, 8, size=n_points)
+    sf = (np.float32(1.2) ** np.arange(8)).astype(np.float32)
+    max_dist = (dist * rng.uniform(0.9, 1.1, n_points) * sf[lvl_ref]).astype(np.float32)
+    min_dist = (max_dist / sf[7]).astype(np.float32)
+    view = (Xw - Ow) / dist[:, None]  # MapPoint normal: mean camera-to-point direction
+    normal = view + rng.normal(scale=0.15, size=view.shape)
+    normal = (normal / np.linalg.norm(normal, axis=1)[:, None]).astype(np.float32)
+    pdesc = rng.integers(0, 256, (n_points, 32), dtype=np.uint8)
+    pangle = rng.uniform(0, 360, n_points).astype(np.float32)
+    kps, kdesc = [], []
+    for i in range(n_points):
+        if not (0 <= u[i] < W and 0 <= v[i] < H) or rng.uniform() < 0.2:
+            continue
+        ratio = max_dist[i] / dist[i]
+        lv = int(np.clip(np.ceil(np.log(ratio) / np.log(1.2)), 0, 7)) + int(rng.integers(-1, 2))
+        lv = int(np.clip(lv, 0, 7))
+        bits = np.unpackbits(pdesc[i])
+        bits ^= (rng.uniform(size=256) < 0.06).astype(np.uint8)
+        kps.append((u[i] + rng.normal(scale=0.8), v[i] + rng.normal(scale=0.8), 31 * sf[lv],
+                    (pangle[i] + 15.0 + rng.normal(scale=2.0)) % 360.0, 0.0, lv, -1))
+        kdesc.append(np.packbits(bits))
+    for _ in range(n_distractors):
+        j = int(rng.integers(0, n_points))
+        near = rng.uniform() < 0.5
+        x0 = u[j] + rng.normal(scale=6) if near else rng.uniform(0, W)
+        y0 = v[j] + rng.normal(scale=6) if near else rng.uniform(0, H)
+        bits = np.unpackbits(pdesc[j])
+        bits ^= (rng.uniform(size=256) < (0.2 if near else 0.5)).astype(np.uint8)
+        lv = int(rng.integers(0, 8))
+        kps.append((np.clip(x0, 0, W - 1), np.clip(y0, 0, H - 1), 31 * sf[lv], rng.uniform(0, 360), 0.0, lv, -1))
+        kdesc.append(np.packbits(bits))
+    order = rng.permutation(len(kps))
+    kp_arr = np.zeros(len(kps), dtype=[("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                                       ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+    for o, i in enumerate(order):
+        kp_arr[o] = kps[i]
+    kdesc = np.array(kdesc, np.uint8)[order]
+    Tcw = T.copy()
+    if scale != 1.0:
+        Tcw[:3, :] *= scale
+    tgt = {"kps": kp_arr, "desc": kdesc,
+           "u_right": np.where(rng.uniform(size=len(kp_arr)) < 0.5, kp_arr["x"] - rng.uniform(5, 40, len(kp_arr)),
+                               -1.0).astype(np.float32) if stereo else None,
+           "occupied": (rng.integers(0, 3, len(kp_arr)) * (rng.uniform(size=len(kp_arr)) < 0.15)).astype(np.uint8),
+           "min_x": 0.0, "max_x": float(W), "min_y": 0.0, "max_y": float(H), "fx": fx, "fy": fy, "cx": cx, "cy": cy,
+           "bf": 40.0, "b": 0.08, "n_levels": 8, "log_scale_factor": float(np.log(np.float32(1.2))),
+           "scale_factors": sf, "Tcw": Tcw.astype(np.float32)}
+    flags = np.where(rng.uniform(size=n_points) < 0.9, 1, 0) | np.where(rng.uniform(size=n_points) < 0.9, 2, 0)
+    pts = {"flags": flags.astype(np.int32), "pos": Xw.astype(np.float32),
+           "normal": normal, "desc": pdesc, "min_dist": min_dist, "max_dist": max_dist,
+           "octave": lvl_ref.astype(np.int32), "angle": pangle}
+    return tgt, pts
