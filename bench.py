@@ -252,7 +252,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": desc_cfg, "config": args.config, "frames_per_gpu_per_step": B,
                    "width": W, "height": H, "nfeatures": NF, "parallelism": f"frame-sharded x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "pyr_level_kernel x7 (pyramid pass)",
+        "roofline": {"bound": "hbm", "kernel": "pyramid_kernel (fused pass: all levels per frame band)",
                      "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                      "traffic": traffic, "algorithmic_bytes_per_step": pyr_bytes},

@@ -130,7 +130,7 @@ typedef struct orbgpu_grid_bounds {
 } orbgpu_grid_bounds;
 
 /* ORBmatcher(nnratio, checkOri).SearchForInitialization(F1, F2,
- * vbPrevMatched, vnMatches12, windowSize) (ORBmatcher.h:60,
+ * vbPrevMatched, vnMatches12, windowSize) (ORBmatcher.h:108,
  * ORBmatcher.cpp:474-590), batched over pairs; keypoints are F.mvKeysUn and
  * F2's grid is Frame::AssignFeaturesToGrid over `bounds` (Frame.cpp:241-259).
  * Pair b: F1 keypoints d_kps1 + b*stride1 (count d_n1[b], levels in

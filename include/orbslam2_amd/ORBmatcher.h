@@ -2,7 +2,7 @@
 // functions on the hot path, for a maintainer to call from the reference's
 // ORBmatcher.cpp.  Header-only over include/orbgpu.h.
 //
-//   SearchForInitialization  ORBmatcher.h:60, ORBmatcher.cpp:474-590
+//   SearchForInitialization  ORBmatcher.h:108, ORBmatcher.cpp:474-590
 //
 // FrameT is ORB_SLAM2::Frame (or anything with the same members):
 // mvKeysUn (std::vector<cv::KeyPoint>), mDescriptors (N x 32 CV_8U) and the
