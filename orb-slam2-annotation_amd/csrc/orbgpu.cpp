@@ -129,8 +129,7 @@ struct orbgpu_extractor {
     uint8_t* d_blur = nullptr;
     size_t blur_bytes = 0;
     int4* d_ptab = nullptr;
-    int2* d_ytab = nullptr;
-    std::vector<int4> pyr_bands;   // host copy of the band table
+    std::vector<int4> pyr_bands;   // host copy of the per-band pyramid records
     int4* d_pyr_bands = nullptr;
     uint32_t* d_cand = nullptr;
     int* d_cell_counts = nullptr;
@@ -157,7 +156,7 @@ struct orbgpu_extractor {
     int last_batch = 0;
 
     ~orbgpu_extractor() {
-        void* ptrs[] = {d_pyr, d_blur, d_ptab, d_ytab, d_pyr_bands, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
+        void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_bands, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
                         d_oct_count, d_err, d_trace, d_img, d_kps1, d_desc1, d_count1};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
@@ -176,12 +175,16 @@ namespace {
 // whose two LDS ping-pong buffers fit 80 KiB (two blocks per CU), raised
 // while the batch alone would not fill the chip.
 // two 1024-thread blocks per CU (measured: bigger bands at one block per CU are slower)
-constexpr int kPyrLdsBudget = 80 * 1024;
+#ifndef ORBGPU_PYR_LDS_KB
+#define ORBGPU_PYR_LDS_KB 80
+#endif
+constexpr int kPyrLdsBudget = ORBGPU_PYR_LDS_KB * 1024;
 int plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, int max_batch, std::vector<int4>& table) {
     const int L = g.nlevels;
     table.clear();
     if (L < 2) {
         g.pyr_bands = 1;
+        g.pyr_rec_stride = L;
         table.assign(L, int4{0, 0, 0, 0});
         return ORBGPU_OK;
     }
@@ -222,7 +225,7 @@ int plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, int max_batch, st
                 dst = std::max(dst, bytes);
             }
             for (int l = 1; l < L; ++l) yrows += b[l].y - b[l].x;
-            lds_y = std::max(lds_y, yrows * 16);
+            lds_y = std::max(lds_y, (L + yrows) * 16);
         }
     };
     const int hmin = g.lv[L - 1].h;
@@ -241,6 +244,36 @@ int plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, int max_batch, st
     g.pyr_lds_b = (int)round_up((size_t)lds_a + 16, 16);
     g.pyr_lds_y = g.pyr_lds_b + (int)round_up((size_t)lds_b + 16, 16);
     g.pyr_lds_bytes = g.pyr_lds_y + (int)round_up((size_t)lds_y, 16);
+    // Per-band records, copied into LDS by the block together with its
+    // level-0 rows: the L band entries, then for levels 1..L-1 one int4 per
+    // computed row = (LDS offset of source row y0, of y1, ibeta0 << 12,
+    // ibeta1 << 12).  Nothing frame-dependent, so the kernel does no
+    // dependent table reads.
+    int stride = 0;
+    for (int s = 0; s < S; ++s) {
+        int n = L;
+        for (int l = 1; l < L; ++l) n += table[(size_t)s * L + l].y - table[(size_t)s * L + l].x;
+        stride = std::max(stride, n);
+    }
+    std::vector<int4> rec((size_t)S * stride, int4{0, 0, 0, 0});
+    for (int s = 0; s < S; ++s) {
+        const int4* b = &table[(size_t)s * L];
+        int4* r = &rec[(size_t)s * stride];
+        for (int l = 0; l < L; ++l) r[l] = b[l];
+        int off = L;
+        for (int l = 1; l < L; ++l) {
+            const int src_lo = b[l - 1].x, sp = g.lv[l - 1].lds_pitch;
+            const int base = ((l - 1) & 1) ? g.pyr_lds_a : g.pyr_lds_b;
+            const int2* yt = &ytab[(size_t)g.lv[l].ytab_offset];
+            for (int y = b[l].x; y < b[l].y; ++y) {
+                const int2 t = yt[y];
+                r[off++] = int4{base + ((t.x & 0xFFFF) - src_lo) * sp, base + ((t.x >> 16) - src_lo) * sp,
+                                (t.y & 0xFFFF) << 12, (int)(((uint32_t)t.y >> 16) << 12)};
+            }
+        }
+    }
+    table.swap(rec);
+    g.pyr_rec_stride = stride;
     return ORBGPU_OK;
 }
 
@@ -338,24 +371,67 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
                     return fail(ORBGPU_ERR_UNSUPPORTED, "unexpected resize weights");
             v.simd_end = vresize_simd_end(v.w);
             const int quads = (v.w + 3) / 4;
-            if (quads < 2) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid level narrower than 5 px");
-            v.quad_magic = (uint32_t)(((1ull << 32) + quads - 1) / quads);
-            v.rgroups = pyr_threads() / quads;
-            if (v.rgroups < 1) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid level wider than 4096 px");
+            if (quads < 3) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid level narrower than 9 px");
+            // pyramid.hip gives the last quad (the scalar tail) its own threads
+            // (or, when w is a multiple of 16, there is no tail at all)
+            if (v.simd_end == v.w && v.w % 4 == 0) v.qmain = quads;
+            else if (v.simd_end == 4 * (quads - 1)) v.qmain = quads - 1;
+            else return fail(ORBGPU_ERR_UNSUPPORTED, "resize tail is not the last quad");
+            v.quad_magic = (uint32_t)(((1ull << 32) + v.qmain - 1) / v.qmain);
+            // row groups: vector quads in whole waves from thread 0, the tail
+            // quads (one per row group) from the next wave boundary
+            {
+                const int T = pyr_threads(), has_tail = v.qmain < quads;
+                int R = T / quads;
+                while (R > 0 && (int)round_up((size_t)v.qmain * R, 64) + (has_tail ? R : 0) > T) --R;
+                if (R < 1) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid level wider than the block");
+                v.rgroups = R;
+                v.tail_base = (int)round_up((size_t)v.qmain * R, 64);
+            }
+
             if ((size_t)v.pitch * v.h >= (1u << 31)) return fail(ORBGPU_ERR_UNSUPPORTED, "level too large");
             v.ptab_offset = (int)ptab.size();
+            v.dbg_level = l;
+            // window layout if every quad's taps fit one dword-aligned 8-byte window
+            std::vector<int> wlo(quads);
+            v.pyr_win = 1;
+            for (int q = 0; q < quads && v.pyr_win; ++q) {
+                int lo = INT32_MAX, hi = INT32_MIN;
+                for (int k = 0; k < 4; ++k) {
+                    const int dx = 4 * q + k;
+                    if (dx >= v.w) continue;
+                    const int sx = xt[dx].x & 0xFFFF;
+                    lo = std::min(lo, sx);
+                    hi = std::max(hi, sx + ((xt[dx].y >> 16) != 0 ? 1 : 0));
+                }
+                const int w0 = (std::max(hi - 7, 0) + 3) & ~3;
+                if (w0 > lo) v.pyr_win = 0;
+                wlo[q] = w0;
+            }
             for (int q = 0; q < quads; ++q) {
                 int lo[4], wt[4], sel[4];
                 for (int k = 0; k < 4; ++k) {
                     const int dx = 4 * q + k;
                     const int sx = dx < v.w ? (xt[dx].x & 0xFFFF) : 0;
-                    lo[k] = sx & ~3;
                     wt[k] = dx < v.w ? xt[dx].y : 0;
-                    sel[k] = (int)(0x0c010c00u + (uint32_t)(sx & 3) * 0x00010001u);
+                    if (v.pyr_win) {
+                        const int b0 = sx - wlo[q];
+                        const int b1 = (wt[k] >> 16) != 0 ? b0 + 1 : b0;
+                        sel[k] = dx < v.w ? (int)(0x0c000c00u | (uint32_t)b0 | ((uint32_t)b1 << 16)) : (int)0x0c0c0c0cu;
+                    } else {
+                        lo[k] = sx & ~3;
+                        sel[k] = (int)(0x0c010c00u + (uint32_t)(sx & 3) * 0x00010001u);
+                    }
                 }
-                ptab.push_back(int4{lo[0], wt[0], lo[1], wt[1]});
-                ptab.push_back(int4{lo[2], wt[2], lo[3], wt[3]});
-                ptab.push_back(int4{sel[0], sel[1], sel[2], sel[3]});
+                if (v.pyr_win) {
+                    ptab.push_back(int4{wlo[q], wt[0], wt[1], wt[2]});
+                    ptab.push_back(int4{wt[3], sel[0], sel[1], sel[2]});
+                    ptab.push_back(int4{sel[3], 0, 0, 0});
+                } else {
+                    ptab.push_back(int4{lo[0], wt[0], lo[1], wt[1]});
+                    ptab.push_back(int4{lo[2], wt[2], lo[3], wt[3]});
+                    ptab.push_back(int4{sel[0], sel[1], sel[2], sel[3]});
+                }
             }
             v.ytab_offset = (int)ytab.size();
             ytab.insert(ytab.end(), yt.begin(), yt.end());
@@ -414,7 +490,7 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
         evs = e->ev[e->ev_used++].data();
         ORB_HIP(hipEventRecord(evs[0], s));
     }
-    ORB_HIP(launch_pyramid(g, batch, e->d_pyr_bands, e->d_ptab, e->d_ytab, imgs, row_step, frame_step, e->d_pyr, s));
+    ORB_HIP(launch_pyramid(g, batch, e->d_pyr_bands, e->d_ptab, imgs, row_step, frame_step, e->d_pyr, s));
     if (evs) ORB_HIP(hipEventRecord(evs[1], s));
     ORB_HIP(launch_fast_cells(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_cand, e->d_cell_counts, e->d_err, s));
     if (evs) ORB_HIP(hipEventRecord(evs[2], s));
@@ -494,7 +570,7 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
     const size_t B = (size_t)max_batch;
     e->img_pitch = round_up((size_t)width, 16);
     if ((rc = dalloc(&e->d_pyr, e->pyr_bytes)) || (rc = dalloc(&e->d_blur, e->blur_bytes)) || (rc = dalloc(&e->d_ptab, ptab.size())) ||
-        (rc = dalloc(&e->d_ytab, ytab.size())) || (rc = dalloc(&e->d_cand, g.cand_frame * B)) ||
+        (rc = dalloc(&e->d_cand, g.cand_frame * B)) ||
         (rc = dalloc(&e->d_cell_counts, (size_t)g.total_cells * B)) || (rc = dalloc(&e->d_gkeys, g.cand_frame * B)) ||
         (rc = dalloc(&e->d_gknode, g.cand_frame * B)) || (rc = dalloc(&e->d_oct_out, (size_t)g.slots_frame * B)) ||
         (rc = dalloc(&e->d_oct_count, (size_t)g.nlevels * B)) || (rc = dalloc(&e->d_err, 1)) ||
@@ -505,7 +581,6 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
         return rc;
     }
     if (hipMemcpy(e->d_ptab, ptab.data(), ptab.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(e->d_ytab, ytab.data(), ytab.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(e->d_pyr_bands, e->pyr_bands.data(), e->pyr_bands.size() * sizeof(int4), hipMemcpyHostToDevice) !=
             hipSuccess ||
         pyramid_set_lds_limit((size_t)g.pyr_lds_bytes) != hipSuccess ||

@@ -17,10 +17,10 @@
 // algorithmic bytes of the reference's level-by-level pass
 // (sum_l |P_{l-1}| + |P_l|) are larger.
 //
-// Per output pixel: two 8-byte windows of the source rows (one dword pair
-// each), v_perm_b32 spreads the tap pair into 16-bit lanes and
-// v_dot2_u32_u16 applies (ialpha0, ialpha1) -- the exact horizontal sum --
-// then the vertical rounding.  No saturation is needed: with non-negative
+// Per output quad: one 8-byte window of each of the two source rows (one
+// dword pair each), v_perm_b32 spreads each pixel's tap pair into 16-bit
+// lanes and v_dot2_u32_u16 applies (ialpha0, ialpha1) -- the exact
+// horizontal sum -- then the vertical rounding.  No saturation is needed: with non-negative
 // Q11 weights summing to 2048 (+-1), every intermediate is in range
 // (h <= 255*2048; the SIMD-path sum of the two >>16 products <= 1020).
 #include "orbgpu_internal.h"
@@ -30,39 +30,93 @@ namespace orbgpu {
 
 namespace {
 
-constexpr int kPyrThreads = 1024;
+#ifndef PYR_PROBE
+#define PYR_PROBE 0  // timing probes for tuning only (tools/pyr_variants.sh): bit 0 = no level-0 loads, bit 2 = level 1 only; 0 = the product
+#endif
+#ifndef PYR_THREADS
+#define PYR_THREADS 1024
+#endif
+constexpr int kPyrThreads = PYR_THREADS;
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
+#if PYR_PROBE & 8
+// diagnostic build only: per-block phase stamps (never read by the kernel)
+__device__ unsigned long long g_pyr_stamps[8192 * 10];
+__device__ __forceinline__ void pyr_stamp(int slot) {
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (threadIdx.x == 0 && blockIdx.x < 8192) g_pyr_stamps[blockIdx.x * 10 + slot] = t;
+}
+#define PYR_STAMP(i) pyr_stamp(i)
+__device__ unsigned long long g_pyr_iter[8192 * 8 * 16];
+#else
+#define PYR_STAMP(i) ((void)0)
+#endif
+
+// 24 x 24 -> high 32 bits of the 48-bit product (v_mul_hi_u32_u24); both
+// operands must be < 2^24
+__device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
+    return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+
+// out.byte[K] = s >> 2, other bytes preserved (SDWA destination select)
+template <int K>
+__device__ __forceinline__ void put_byte_shr2(uint32_t& out, uint32_t s) {
+    static_assert(K >= 1 && K <= 3, "byte 0 is written by a plain shift");
+    if (K == 1)
+        asm("v_lshrrev_b32_sdwa %0, 2, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+            : "+v"(out) : "v"(s));
+    else if (K == 2)
+        asm("v_lshrrev_b32_sdwa %0, 2, %1 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+            : "+v"(out) : "v"(s));
+    else
+        asm("v_lshrrev_b32_sdwa %0, 2, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+            : "+v"(out) : "v"(s));
+}
+
 // One level's band rows [r0, r1).  Thread layout: quad column q of 4 output
 // pixels x row group rg walking rows r0+rg, r0+rg+rgroups, ..., so the
-// column taps stay in registers for the whole level.  Per quad the taps come
-// from ptab (3 x int4: (lo0, wt0, lo1, wt1), (lo2, wt2, lo3, wt3), (sel0..3);
-// lo = byte offset of the dword pair holding taps sx and sx+1 -- whenever the
-// second tap has a non-zero weight; rows are padded so reading past a row end
-// is safe -- sel = the v_perm_b32 selector spreading the two taps into 16-bit
-// lanes, wt = (ialpha0, ialpha1)).  s_rows[r - r0] = (LDS offset of source
-// row y0, of y1, ibeta0, ibeta1).
-__device__ __forceinline__ void resize_band(const uint8_t* __restrict__ lds, const LevelGeom& V, int r0, int r1,
-                                            int own0, int own1, const int4* __restrict__ ptab,
-                                            const int4* __restrict__ s_rows, uint8_t* __restrict__ lds_dst,
-                                            uint8_t* __restrict__ hbm_dst) {
-    const int quads = (V.w + 3) >> 2;
-    const int rg = (int)__umulhi((uint32_t)threadIdx.x, V.quad_magic);
-    const int q = threadIdx.x - rg * quads;
-    if (rg >= V.rgroups || r0 + rg >= r1) return;
-    const int4 ta = ptab[3 * q], tb = ptab[3 * q + 1], tc = ptab[3 * q + 2];
-    const uint8_t* col[4] = {lds + ta.x, lds + ta.z, lds + tb.x, lds + tb.z};
-    const uint32_t wt[4] = {(uint32_t)ta.y, (uint32_t)ta.w, (uint32_t)tb.y, (uint32_t)tb.w};
-    const uint32_t sel[4] = {(uint32_t)tc.x, (uint32_t)tc.y, (uint32_t)tc.z, (uint32_t)tc.w};
-    // all four pixels inside VResizeLinearVec_32s8u's coverage: only the last
-    // quad of a row can reach the scalar tail
-    const bool all_simd = 4 * q + 3 < V.simd_end;
-    uint8_t* ldst = lds_dst ? lds_dst + 4 * q : nullptr;
-    uint8_t* hdst = hbm_dst + 4 * q;
-    for (int r = r0 + rg; r < r1; r += V.rgroups) {
-        const int4 yr = s_rows[r - r0];
-        uint32_t h0[4], h1[4];
+// column taps stay in registers for the whole level.  s_rows[r - r0] = (LDS
+// offset of source row y0, of y1, ibeta0 << 12, ibeta1 << 12).
+//
+// Column taps per quad (ptab, 3 x int4), two layouts chosen per level on the
+// host (LevelGeom::pyr_win):
+//  * window (WIN): all eight taps of the quad lie in one dword-aligned 8-byte
+//    window of the source row (always true for scale factors <= 4/3):
+//    (lo, wt0, wt1, wt2), (wt3, sel0, sel1, sel2), (sel3, -, -, -) -- one
+//    ds_read2_b32 per source row serves the whole quad;
+//  * pairs: (lo0, wt0, lo1, wt1), (lo2, wt2, lo3, wt3), (sel0..3) with lo_k
+//    the dword pair holding taps sx_k, sx_k + 1.
+// sel = the v_perm_b32 selector spreading a pixel's two taps into 16-bit
+// lanes, wt = (ialpha0, ialpha1); v_dot2_u32_u16 forms the exact horizontal
+// sum.  Rows are padded so reading past a row end is safe.
+//
+// Vertical pass, VResizeLinearVec_32s8u: ((h0>>4)*b0 >> 16) + ((h1>>4)*b1 >>
+// 16) + 2 >> 2, each term as mulhi24(h & ~15, b << 12) = (16 (h>>4) b 2^12)
+// >> 32.  h <= 255 * 2049 < 2^24 and b << 12 <= 2049 << 12 < 2^24.
+//
+// The last quad of every row is exactly the scalar tail (simd_end = 4 *
+// (quads - 1), checked on the host; or there is no tail when w is a multiple
+// of 16); its threads get a wave of their own (quad_taps).
+template <bool TAIL, bool WIN>
+__device__ __forceinline__ uint32_t quad_row(const uint8_t* const (&col)[4], const uint32_t (&wt)[4],
+                                             const uint32_t (&sel)[4], int4 yr) {
+    uint32_t h0[4], h1[4];
+    if (WIN) {
+        const uint32_t* a = reinterpret_cast<const uint32_t*>(col[0] + yr.x);
+        const uint32_t* b = reinterpret_cast<const uint32_t*>(col[0] + yr.y);
+        const uint32_t a0 = a[0], a1 = a[1], b0 = b[0], b1 = b[1];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t p0 = __builtin_amdgcn_perm(a1, a0, sel[k]);
+            const uint32_t p1 = __builtin_amdgcn_perm(b1, b0, sel[k]);
+            h0[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), __builtin_bit_cast(us2, wt[k]), 0u, false);
+            h1[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), __builtin_bit_cast(us2, wt[k]), 0u, false);
+        }
+    } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t* a = reinterpret_cast<const uint32_t*>(col[k] + yr.x);
@@ -72,35 +126,116 @@ __device__ __forceinline__ void resize_band(const uint8_t* __restrict__ lds, con
             h0[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), __builtin_bit_cast(us2, wt[k]), 0u, false);
             h1[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), __builtin_bit_cast(us2, wt[k]), 0u, false);
         }
-        uint32_t out = 0;
-        if (all_simd) {
-            // ((h>>4)*b0 >> 16) + ((h'>>4)*b1 >> 16) + 2, with the +2 folded
-            // into the high half of the first product (no carry: < 2^27)
+    }
+    uint32_t out;
+    if (!TAIL) {
+        const uint32_t B0 = (uint32_t)yr.z & 0xFFFFFFu, B1 = (uint32_t)yr.w & 0xFFFFFFu;
+        uint32_t sum[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t m0 = __umul24(h0[k] >> 4, (uint32_t)yr.z) + (2u << 16);
-                const uint32_t m1 = __umul24(h1[k] >> 4, (uint32_t)yr.w);
-                out |= (((m0 >> 16) + (m1 >> 16)) >> 2) << (8 * k);
-            }
-        } else {  // the last quad of a row: scalar tail for x >= simd_end
+        for (int k = 0; k < 4; ++k)
+            sum[k] = mulhi24(h0[k] & 0xFFFFF0u, B0) + mulhi24(h1[k] & 0xFFFFF0u, B1) + 2u;
+        out = sum[0] >> 2;
+        put_byte_shr2<1>(out, sum[1]);
+        put_byte_shr2<2>(out, sum[2]);
+        put_byte_shr2<3>(out, sum[3]);
+    } else {  // FixedPtCast<int, uchar, 22>: (S0*b0 + S1*b1 + 2^21) >> 22, < 2^31 (S < 2^24, b < 2^12)
+        const uint32_t b0 = (uint32_t)yr.z >> 12, b1 = (uint32_t)yr.w >> 12;
+        out = 0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int a = (int)h0[k], b = (int)h1[k];
-                const int v = 4 * q + k < V.simd_end ? ((((a >> 4) * yr.z) >> 16) + (((b >> 4) * yr.w) >> 16) + 2) >> 2
-                                                     : (a * yr.z + b * yr.w + (1 << 21)) >> 22;
-                out |= (uint32_t)v << (8 * k);
-            }
+        for (int k = 0; k < 4; ++k) out |= ((__umul24(h0[k], b0) + __umul24(h1[k], b1) + (1u << 21)) >> 22) << (8 * k);
+    }
+    return out;
+}
+
+// A thread's quad of one level: which quad and row group, and its column
+// taps, loaded one level ahead (before the barrier that ends the previous
+// level) so the table read's latency is hidden by the barrier wait.
+struct QuadTaps {
+    int4 a, b, c;
+    int q, rg;
+    int mode;  // 0 idle, 1 vector quad, 2 tail quad
+};
+
+// Thread layout of a level: vector quads fill threads [0, qmain * rgroups)
+// (row group rg = t / qmain); the tail quads of the rgroups row groups go to
+// threads [tail_base, tail_base + rgroups), where tail_base starts a wave of
+// its own -- the tail formula then never shares a wave with the vector one,
+// and no wave runs both loops.
+__device__ __forceinline__ QuadTaps quad_taps(const LevelGeom& V, const int4* __restrict__ ptab) {
+    QuadTaps tp;
+    const int t = threadIdx.x;
+    tp.mode = 0;
+    tp.q = 0;
+    tp.rg = 0;
+    if (t < V.qmain * V.rgroups) {
+        tp.rg = (int)__umulhi((uint32_t)t, V.quad_magic);
+        tp.q = t - tp.rg * V.qmain;
+        tp.mode = 1;
+    } else if (t >= V.tail_base && t < V.tail_base + V.rgroups && 4 * V.qmain < V.w) {
+        tp.rg = t - V.tail_base;
+        tp.q = V.qmain;
+        tp.mode = 2;
+    }
+    if (tp.mode) {
+        const int4* pt = ptab + V.ptab_offset + 3 * tp.q;
+        tp.a = pt[0];
+        tp.b = pt[1];
+        tp.c = pt[2];
+    }
+    return tp;
+}
+
+template <bool TAIL, bool WIN>
+__device__ __forceinline__ void resize_rows(const uint8_t* __restrict__ lds, const LevelGeom& V, const QuadTaps& tp,
+                                            int r0, int r1, int own0, int own1, const int4* __restrict__ s_rows,
+                                            uint8_t* __restrict__ lds_dst, uint8_t* __restrict__ hbm_dst) {
+    const int4 ta = tp.a, tb = tp.b, tc = tp.c;
+    const int q = tp.q;
+    const uint8_t* col[4];
+    uint32_t wt[4], sel[4];
+    if (WIN) {
+        col[0] = col[1] = col[2] = col[3] = lds + ta.x;
+        wt[0] = ta.y; wt[1] = ta.z; wt[2] = ta.w; wt[3] = tb.x;
+        sel[0] = tb.y; sel[1] = tb.z; sel[2] = tb.w; sel[3] = tc.x;
+    } else {
+        col[0] = lds + ta.x; col[1] = lds + ta.z; col[2] = lds + tb.x; col[3] = lds + tb.z;
+        wt[0] = ta.y; wt[1] = ta.w; wt[2] = tb.y; wt[3] = tb.w;
+        sel[0] = tc.x; sel[1] = tc.y; sel[2] = tc.z; sel[3] = tc.w;
+    }
+#if PYR_PROBE & 8
+    int it = 0;
+#endif
+    for (int r = r0 + tp.rg; r < r1; r += V.rgroups) {
+#if PYR_PROBE & 8
+        {
+            __builtin_amdgcn_sched_barrier(0);
+            unsigned long long t;
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if (threadIdx.x == 0 && blockIdx.x < 8192 && it < 16) g_pyr_iter[(blockIdx.x * 8 + V.dbg_level) * 16 + it] = t;
+            ++it;
         }
+#endif
+        const uint32_t out = quad_row<TAIL, WIN>(col, wt, sel, s_rows[r - r0]);
         // bytes past V.w land in the row padding (LDS pitch and HBM pitch are
         // multiples of 4 and 16)
-        if (ldst) *reinterpret_cast<uint32_t*>(ldst + (r - r0) * V.lds_pitch) = out;
-        if (r >= own0 && r < own1) *reinterpret_cast<uint32_t*>(hdst + r * V.pitch) = out;
+        if (lds_dst) *reinterpret_cast<uint32_t*>(lds_dst + (uint32_t)((r - r0) * V.lds_pitch + 4 * q)) = out;
+        if (r >= own0 && r < own1) *reinterpret_cast<uint32_t*>(hbm_dst + (uint32_t)(r * V.pitch + 4 * q)) = out;
     }
 }
 
-__global__ __launch_bounds__(kPyrThreads) void pyramid_kernel(Geom g, const int4* __restrict__ bands,
+template <bool WIN>
+__device__ __forceinline__ void resize_band(const uint8_t* __restrict__ lds, const LevelGeom& V, const QuadTaps& tp,
+                                            int r0, int r1, int own0, int own1, const int4* __restrict__ s_rows,
+                                            uint8_t* __restrict__ lds_dst, uint8_t* __restrict__ hbm_dst) {
+    if (tp.mode == 1)
+        resize_rows<false, WIN>(lds, V, tp, r0, r1, own0, own1, s_rows, lds_dst, hbm_dst);
+    else if (tp.mode == 2)
+        resize_rows<true, WIN>(lds, V, tp, r0, r1, own0, own1, s_rows, lds_dst, hbm_dst);
+}
+
+__global__ __launch_bounds__(kPyrThreads) void pyramid_kernel(Geom g, const int4* __restrict__ recs,
                                                               const int4* __restrict__ ptab,
-                                                              const int2* __restrict__ ytab,
                                                               const uint8_t* __restrict__ img0, size_t row0,
                                                               size_t frame0, uint8_t* __restrict__ pyr) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_pyr[];
@@ -108,46 +243,51 @@ __global__ __launch_bounds__(kPyrThreads) void pyramid_kernel(Geom g, const int4
     const int f = blockIdx.x / S;
     const int band = blockIdx.x - f * S;
     const int L = g.nlevels;
-    const int4* bt = bands + band * L;
-    int4* s_rows = reinterpret_cast<int4*>(s_pyr + g.pyr_lds_y);
-    // stage: this band's level-0 rows (16-byte loads; row0 is a multiple of 16)
-    // and, per band row of every level, its source rows' LDS offsets and y taps
+    const int4* rec = recs + (size_t)band * g.pyr_rec_stride;
+    int4* s_rec = reinterpret_cast<int4*>(s_pyr + g.pyr_lds_y);
+    PYR_STAMP(0);
+    QuadTaps tp = quad_taps(g.lv[1], ptab);
+    // stage: this band's level-0 rows (16-byte loads; row0 is a multiple of
+    // 16) and its record (band entries + per-row source offsets and y taps)
     {
-        const int4 b = bt[0];
+        const int4 b = rec[0];
         const int v4 = (g.lv[0].w + 15) >> 4;
         const uint8_t* src = img0 + (size_t)f * frame0 + (size_t)b.x * row0;
         uint8_t* dst = s_pyr + g.pyr_lds_b;
         const int n = (b.y - b.x) * v4;
+#if PYR_PROBE & 1
+        if (n < 0)
+#endif
         for (int i = threadIdx.x; i < n; i += kPyrThreads) {
             const int r = (int)__umulhi((uint32_t)i, g.lv[0].quad_magic);
             const int c = i - r * v4;
             *reinterpret_cast<uint4*>(dst + r * g.lv[0].lds_pitch + 16 * c) =
                 *reinterpret_cast<const uint4*>(src + (size_t)r * row0 + 16 * c);
         }
-        int off = 0;
-        for (int l = 1; l < L; ++l) {
-            const int4 bl = bt[l];
-            const int src_lo = bt[l - 1].x, sp = g.lv[l - 1].lds_pitch;
-            const int base = ((l - 1) & 1) ? g.pyr_lds_a : g.pyr_lds_b;
-            const int2* yt = ytab + g.lv[l].ytab_offset + bl.x;
-            for (int i = threadIdx.x; i < bl.y - bl.x; i += kPyrThreads) {
-                const int2 t = yt[i];
-                s_rows[off + i] = make_int4(base + ((t.x & 0xFFFF) - src_lo) * sp, base + ((t.x >> 16) - src_lo) * sp,
-                                            t.y & 0xFFFF, (int)((uint32_t)t.y >> 16));
-            }
-            off += bl.y - bl.x;
-        }
+        for (int i = threadIdx.x; i < g.pyr_rec_stride; i += kPyrThreads) s_rec[i] = rec[i];
     }
     __syncthreads();
-    int yoff = 0;
+    PYR_STAMP(1);
+    int yoff = L;
+#if PYR_PROBE & 4
+    for (int l = 1; l < 2; ++l) {
+#else
     for (int l = 1; l < L; ++l) {
+#endif
         const LevelGeom& V = g.lv[l];
-        const int4 b = bt[l];  // need [x, y), owned [z, w)
+        const int4 bv = s_rec[l];  // need [x, y), owned [z, w); uniform
+        const int bx = __builtin_amdgcn_readfirstlane(bv.x), by = __builtin_amdgcn_readfirstlane(bv.y);
+        const int bz = __builtin_amdgcn_readfirstlane(bv.z), bw = __builtin_amdgcn_readfirstlane(bv.w);
         uint8_t* dst_lds = l + 1 < L ? s_pyr + ((l & 1) ? g.pyr_lds_a : g.pyr_lds_b) : nullptr;
         uint8_t* dst_hbm = pyr + V.offset + (size_t)f * V.frame_bytes;
-        resize_band(s_pyr, V, b.x, b.y, b.z, b.w, ptab + V.ptab_offset, s_rows + yoff, dst_lds, dst_hbm);
-        yoff += b.y - b.x;
+        if (V.pyr_win)
+            resize_band<true>(s_pyr, V, tp, bx, by, bz, bw, s_rec + yoff, dst_lds, dst_hbm);
+        else
+            resize_band<false>(s_pyr, V, tp, bx, by, bz, bw, s_rec + yoff, dst_lds, dst_hbm);
+        yoff += by - bx;
+        if (l + 1 < L) tp = quad_taps(g.lv[l + 1], ptab);
         __syncthreads();
+        PYR_STAMP(1 + l);
     }
 }
 
@@ -155,13 +295,24 @@ __global__ __launch_bounds__(kPyrThreads) void pyramid_kernel(Geom g, const int4
 
 int pyr_threads() { return kPyrThreads; }
 
-hipError_t launch_pyramid(const Geom& g, int batch, const int4* bands, const int4* ptab, const int2* ytab,
-                          const uint8_t* img0, size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream) {
+hipError_t launch_pyramid(const Geom& g, int batch, const int4* recs, const int4* ptab, const uint8_t* img0,
+                          size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream) {
     if (g.nlevels < 2) return hipSuccess;
     hipLaunchKernelGGL(pyramid_kernel, dim3(g.pyr_bands * batch), dim3(kPyrThreads), g.pyr_lds_bytes, stream, g,
-                       bands, ptab, ytab, img0, row0, frame0, pyr);
+                       recs, ptab, img0, row0, frame0, pyr);
     return hipGetLastError();
 }
+
+#if PYR_PROBE & 8
+extern "C" int orbgpu_debug_pyr_iters(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pyr_iter), (size_t)n * 8 * 16 * sizeof(unsigned long long)) == hipSuccess
+               ? 0 : -2;
+}
+extern "C" int orbgpu_debug_pyr_stamps(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pyr_stamps), (size_t)n * 10 * sizeof(unsigned long long)) == hipSuccess
+               ? 0 : -2;
+}
+#endif
 
 hipError_t pyramid_set_lds_limit(size_t bytes) {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_kernel),

@@ -15,12 +15,14 @@ no gfx950 device, every call raises.
 from __future__ import annotations
 
 import ctypes
+import os
 from pathlib import Path
 
 import numpy as np
 
 _HERE = Path(__file__).resolve().parent
-LIB_PATH = _HERE / "liborbgpu.so"
+# ORBGPU_LIBRARY selects another build of the same library (e.g. a tuning variant)
+LIB_PATH = Path(os.environ.get("ORBGPU_LIBRARY", str(_HERE / "liborbgpu.so")))
 _LIB = None
 
 OK, ERR_ARG, ERR_HIP, ERR_CAPACITY, ERR_UNSUPPORTED, ERR_NO_DEVICE = 0, -1, -2, -3, -4, -5
