@@ -379,11 +379,11 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
             else return fail(ORBGPU_ERR_UNSUPPORTED, "resize tail is not the last quad");
             v.quad_magic = (uint32_t)(((1ull << 32) + v.qmain - 1) / v.qmain);
             // row groups: vector quads in whole waves from thread 0, the tail
-            // quads (one per row group) from the next wave boundary
+            // quads (one lane per row) in the wave after them
             {
                 const int T = pyr_threads(), has_tail = v.qmain < quads;
                 int R = T / quads;
-                while (R > 0 && (int)round_up((size_t)v.qmain * R, 64) + (has_tail ? R : 0) > T) --R;
+                while (R > 0 && (int)round_up((size_t)v.qmain * R, 64) + (has_tail ? 64 : 0) > T) --R;
                 if (R < 1) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid level wider than the block");
                 v.rgroups = R;
                 v.tail_base = (int)round_up((size_t)v.qmain * R, 64);

@@ -31,7 +31,7 @@ namespace orbgpu {
 namespace {
 
 #ifndef PYR_PROBE
-#define PYR_PROBE 0  // timing probes for tuning only (tools/pyr_variants.sh): bit 0 = no level-0 loads, bit 2 = level 1 only; 0 = the product
+#define PYR_PROBE 0  // timing probes for tuning only (tools/pyr_variants.sh): bit 0 = no level-0 loads, bit 2 = level 1 only, bit 3 = phase stamps; 0 = the product
 #endif
 #ifndef PYR_THREADS
 #define PYR_THREADS 1024
@@ -51,7 +51,7 @@ __device__ __forceinline__ void pyr_stamp(int slot) {
     if (threadIdx.x == 0 && blockIdx.x < 8192) g_pyr_stamps[blockIdx.x * 10 + slot] = t;
 }
 #define PYR_STAMP(i) pyr_stamp(i)
-__device__ unsigned long long g_pyr_iter[8192 * 8 * 16];
+__device__ unsigned long long g_pyr_wave[8192 * 8 * 16];
 #else
 #define PYR_STAMP(i) ((void)0)
 #endif
@@ -101,31 +101,39 @@ __device__ __forceinline__ void put_byte_shr2(uint32_t& out, uint32_t s) {
 // The last quad of every row is exactly the scalar tail (simd_end = 4 *
 // (quads - 1), checked on the host; or there is no tail when w is a multiple
 // of 16); its threads get a wave of their own (quad_taps).
+// The source bytes one output row of a quad needs: rows y0 (a) and y1 (b),
+// one dword pair per row (WIN) or per pixel.
+template <bool WIN>
+struct RowWords {
+    uint32_t a[WIN ? 2 : 8], b[WIN ? 2 : 8];
+};
+
+template <bool WIN>
+__device__ __forceinline__ RowWords<WIN> load_row(const uint8_t* const (&col)[4], int4 yr) {
+    RowWords<WIN> d;
+#pragma unroll
+    for (int k = 0; k < (WIN ? 1 : 4); ++k) {
+        const uint32_t* a = reinterpret_cast<const uint32_t*>(col[k] + yr.x);
+        const uint32_t* b = reinterpret_cast<const uint32_t*>(col[k] + yr.y);
+        d.a[2 * k] = a[0];
+        d.a[2 * k + 1] = a[1];
+        d.b[2 * k] = b[0];
+        d.b[2 * k + 1] = b[1];
+    }
+    return d;
+}
+
 template <bool TAIL, bool WIN>
-__device__ __forceinline__ uint32_t quad_row(const uint8_t* const (&col)[4], const uint32_t (&wt)[4],
+__device__ __forceinline__ uint32_t quad_row(const RowWords<WIN>& d, const uint32_t (&wt)[4],
                                              const uint32_t (&sel)[4], int4 yr) {
     uint32_t h0[4], h1[4];
-    if (WIN) {
-        const uint32_t* a = reinterpret_cast<const uint32_t*>(col[0] + yr.x);
-        const uint32_t* b = reinterpret_cast<const uint32_t*>(col[0] + yr.y);
-        const uint32_t a0 = a[0], a1 = a[1], b0 = b[0], b1 = b[1];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t p0 = __builtin_amdgcn_perm(a1, a0, sel[k]);
-            const uint32_t p1 = __builtin_amdgcn_perm(b1, b0, sel[k]);
-            h0[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), __builtin_bit_cast(us2, wt[k]), 0u, false);
-            h1[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), __builtin_bit_cast(us2, wt[k]), 0u, false);
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t* a = reinterpret_cast<const uint32_t*>(col[k] + yr.x);
-            const uint32_t* b = reinterpret_cast<const uint32_t*>(col[k] + yr.y);
-            const uint32_t p0 = __builtin_amdgcn_perm(a[1], a[0], sel[k]);
-            const uint32_t p1 = __builtin_amdgcn_perm(b[1], b[0], sel[k]);
-            h0[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), __builtin_bit_cast(us2, wt[k]), 0u, false);
-            h1[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), __builtin_bit_cast(us2, wt[k]), 0u, false);
-        }
+    for (int k = 0; k < 4; ++k) {
+        const int j = WIN ? 0 : 2 * k;
+        const uint32_t p0 = __builtin_amdgcn_perm(d.a[j + 1], d.a[j], sel[k]);
+        const uint32_t p1 = __builtin_amdgcn_perm(d.b[j + 1], d.b[j], sel[k]);
+        h0[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), __builtin_bit_cast(us2, wt[k]), 0u, false);
+        h1[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), __builtin_bit_cast(us2, wt[k]), 0u, false);
     }
     uint32_t out;
     if (!TAIL) {
@@ -157,10 +165,11 @@ struct QuadTaps {
 };
 
 // Thread layout of a level: vector quads fill threads [0, qmain * rgroups)
-// (row group rg = t / qmain); the tail quads of the rgroups row groups go to
-// threads [tail_base, tail_base + rgroups), where tail_base starts a wave of
-// its own -- the tail formula then never shares a wave with the vector one,
-// and no wave runs both loops.
+// (row group rg = t / qmain, rows rg, rg + rgroups, ...); the tail quad of
+// every row goes to the wave starting at tail_base (lane = row, rows lane,
+// lane + 64, ...) -- the tail formula then never shares a wave with the
+// vector one, no wave runs both loops, and the tail wave needs one pass for
+// bands up to 64 rows.
 __device__ __forceinline__ QuadTaps quad_taps(const LevelGeom& V, const int4* __restrict__ ptab) {
     QuadTaps tp;
     const int t = threadIdx.x;
@@ -171,7 +180,7 @@ __device__ __forceinline__ QuadTaps quad_taps(const LevelGeom& V, const int4* __
         tp.rg = (int)__umulhi((uint32_t)t, V.quad_magic);
         tp.q = t - tp.rg * V.qmain;
         tp.mode = 1;
-    } else if (t >= V.tail_base && t < V.tail_base + V.rgroups && 4 * V.qmain < V.w) {
+    } else if (t >= V.tail_base && t < V.tail_base + 64 && 4 * V.qmain < V.w) {
         tp.rg = t - V.tail_base;
         tp.q = V.qmain;
         tp.mode = 2;
@@ -202,25 +211,31 @@ __device__ __forceinline__ void resize_rows(const uint8_t* __restrict__ lds, con
         wt[0] = ta.y; wt[1] = ta.w; wt[2] = tb.y; wt[3] = tb.w;
         sel[0] = tc.x; sel[1] = tc.y; sel[2] = tc.z; sel[3] = tc.w;
     }
-#if PYR_PROBE & 8
-    int it = 0;
-#endif
-    for (int r = r0 + tp.rg; r < r1; r += V.rgroups) {
-#if PYR_PROBE & 8
-        {
-            __builtin_amdgcn_sched_barrier(0);
-            unsigned long long t;
-            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-            __builtin_amdgcn_sched_barrier(0);
-            if (threadIdx.x == 0 && blockIdx.x < 8192 && it < 16) g_pyr_iter[(blockIdx.x * 8 + V.dbg_level) * 16 + it] = t;
-            ++it;
-        }
-#endif
-        const uint32_t out = quad_row<TAIL, WIN>(col, wt, sel, s_rows[r - r0]);
+    // software-pipelined over the thread's rows: the next row's record and
+    // source words and the record after it are read while this row computes
+    // (reads past r1 are clamped to the last row: harmless)
+    int r = r0 + tp.rg;
+    if (r >= r1) return;
+    const int step = TAIL ? 64 : V.rgroups;
+    int4 yc = s_rows[r - r0];
+    int rn = r + step;
+    int4 yn = s_rows[min(rn, r1 - 1) - r0];
+    RowWords<WIN> dc = load_row<WIN>(col, yc);
+    for (;;) {
+        const int rnn = rn + step;
+        const int4 ynn = s_rows[min(rnn, r1 - 1) - r0];
+        const RowWords<WIN> dn = load_row<WIN>(col, yn);
+        const uint32_t out = quad_row<TAIL, WIN>(dc, wt, sel, yc);
         // bytes past V.w land in the row padding (LDS pitch and HBM pitch are
         // multiples of 4 and 16)
         if (lds_dst) *reinterpret_cast<uint32_t*>(lds_dst + (uint32_t)((r - r0) * V.lds_pitch + 4 * q)) = out;
         if (r >= own0 && r < own1) *reinterpret_cast<uint32_t*>(hbm_dst + (uint32_t)(r * V.pitch + 4 * q)) = out;
+        if (rn >= r1) break;
+        r = rn;
+        rn = rnn;
+        yc = yn;
+        yn = ynn;
+        dc = dn;
     }
 }
 
@@ -285,6 +300,15 @@ __global__ __launch_bounds__(kPyrThreads) void pyramid_kernel(Geom g, const int4
         else
             resize_band<false>(s_pyr, V, tp, bx, by, bz, bw, s_rec + yoff, dst_lds, dst_hbm);
         yoff += by - bx;
+#if PYR_PROBE & 8
+        {
+            __builtin_amdgcn_sched_barrier(0);
+            unsigned long long t;
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if ((threadIdx.x & 63) == 0 && blockIdx.x < 8192) g_pyr_wave[(blockIdx.x * 8 + l) * 16 + threadIdx.x / 64] = t;
+        }
+#endif
         if (l + 1 < L) tp = quad_taps(g.lv[l + 1], ptab);
         __syncthreads();
         PYR_STAMP(1 + l);
@@ -304,8 +328,8 @@ hipError_t launch_pyramid(const Geom& g, int batch, const int4* recs, const int4
 }
 
 #if PYR_PROBE & 8
-extern "C" int orbgpu_debug_pyr_iters(unsigned long long* out, int n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pyr_iter), (size_t)n * 8 * 16 * sizeof(unsigned long long)) == hipSuccess
+extern "C" int orbgpu_debug_pyr_waves(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pyr_wave), (size_t)n * 8 * 16 * sizeof(unsigned long long)) == hipSuccess
                ? 0 : -2;
 }
 extern "C" int orbgpu_debug_pyr_stamps(unsigned long long* out, int n) {

@@ -39,17 +39,11 @@ tot = st[:, 8] - st[:, 0]
 print(f"blocks {nb}: block lifetime mean {tot.mean():.0f} cyc  p10 {np.percentile(tot,10):.0f}  p90 {np.percentile(tot,90):.0f}")
 for i, n in enumerate(names):
     print(f"  {n:10s} mean {d[:, i].mean():8.0f} cyc  share {100 * d[:, i].mean() / tot.mean():5.1f} %  p90 {np.percentile(d[:, i], 90):8.0f}")
-fi = L.orbgpu_debug_pyr_iters
-fi.argtypes = [ctypes.c_void_p, ctypes.c_int]
-it = np.zeros((nb, 8, 16), np.uint64)
-assert fi(it.ctypes.data, nb) == 0
-it = it.astype(np.int64)
+fw = L.orbgpu_debug_pyr_waves
+fw.argtypes = [ctypes.c_void_p, ctypes.c_int]
+wv = np.zeros((nb, 8, 16), np.uint64)
+assert fw(wv.ctypes.data, nb) == 0
+wv = wv.astype(np.int64)
 for lv in range(1, 8):
-    a = it[:, lv, :]
-    n = (a > 0).sum(1)
-    lvl_start = st[:, lv]  # stamp after the previous barrier
-    first = a[:, 0] - lvl_start
-    steps = np.diff(a, axis=1)
-    ok = (a[:, 1:] > 0) & (a[:, :-1] > 0)
-    print(f"level {lv}: iterations(thread0) {n.mean():.1f}, level start -> first iter {first.mean():.0f} cyc, "
-          f"per-iteration {steps[ok].mean() if ok.any() else 0:.0f} cyc")
+    rel = wv[:, lv, :] - st[:, lv][:, None]
+    print(f"level {lv} wave done (cyc after level start), mean per wave:", " ".join(f"{x:.0f}" for x in rel.mean(0)))

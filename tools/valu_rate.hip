@@ -1,0 +1,65 @@
+// Microbenchmark: issue cost of the VALU instructions the pyramid pass uses
+// (wave64, 8 waves per SIMD, 8 independent chains per wave).
+// build: hipcc --offload-arch=gfx950 -O3 tools/valu_rate.hip -o tools/valu_rate
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+#define OP_KERNEL(NAME, ASM)                                                                  \
+    __global__ __launch_bounds__(256) void NAME(unsigned* out, unsigned seed, int iters) {    \
+        unsigned v0 = seed ^ threadIdx.x, v1 = v0 * 3, v2 = v0 * 5, v3 = v0 * 7, v4 = v0 * 11, \
+                 v5 = v0 * 13, v6 = v0 * 17, v7 = v0 * 19;                                     \
+        const unsigned k = seed | 0x01010101u;                                                 \
+        for (int i = 0; i < iters; ++i) {                                                      \
+            asm volatile(ASM : "+v"(v0) : "v"(k));                                             \
+            asm volatile(ASM : "+v"(v1) : "v"(k));                                             \
+            asm volatile(ASM : "+v"(v2) : "v"(k));                                             \
+            asm volatile(ASM : "+v"(v3) : "v"(k));                                             \
+            asm volatile(ASM : "+v"(v4) : "v"(k));                                             \
+            asm volatile(ASM : "+v"(v5) : "v"(k));                                             \
+            asm volatile(ASM : "+v"(v6) : "v"(k));                                             \
+            asm volatile(ASM : "+v"(v7) : "v"(k));                                             \
+        }                                                                                      \
+        out[blockIdx.x * 256 + threadIdx.x] = v0 ^ v1 ^ v2 ^ v3 ^ v4 ^ v5 ^ v6 ^ v7;          \
+    }
+
+OP_KERNEL(k_add, "v_add_u32 %0, %0, %1")
+OP_KERNEL(k_and, "v_and_b32 %0, %0, %1")
+OP_KERNEL(k_perm, "v_perm_b32 %0, %0, %1, %1")
+OP_KERNEL(k_dot2, "v_dot2_u32_u16 %0, %0, %1, 0")
+OP_KERNEL(k_mulhi24, "v_mul_hi_u32_u24 %0, %0, %1")
+OP_KERNEL(k_mul24, "v_mul_u32_u24 %0, %0, %1")
+OP_KERNEL(k_mullo, "v_mul_lo_u32 %0, %0, %1")
+OP_KERNEL(k_sdwa, "v_lshrrev_b32_sdwa %0, 2, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD")
+OP_KERNEL(k_add3, "v_add3_u32 %0, %0, %1, 2")
+
+int main() {
+    hipDeviceProp_t p;
+    hipGetDeviceProperties(&p, 0);
+    const int cus = p.multiProcessorCount;
+    const int blocks = cus * 8;  // 8 x 256 threads = 32 waves per CU = 8 per SIMD
+    unsigned* out;
+    hipMalloc(&out, (size_t)blocks * 256 * 4);
+    const int iters = 4096;
+    struct K { const char* n; void (*f)(unsigned*, unsigned, int); } ks[] = {
+        {"v_add_u32", k_add}, {"v_and_b32", k_and}, {"v_perm_b32", k_perm}, {"v_dot2_u32_u16", k_dot2},
+        {"v_mul_hi_u32_u24", k_mulhi24}, {"v_mul_u32_u24", k_mul24}, {"v_mul_lo_u32", k_mullo},
+        {"v_lshrrev_b32_sdwa", k_sdwa}, {"v_add3_u32", k_add3}};
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    printf("CUs %d, clock %d kHz\n", cus, p.clockRate);
+    for (auto& k : ks) {
+        hipLaunchKernelGGL(k.f, dim3(blocks), dim3(256), 0, 0, out, 1u, iters);
+        hipEventRecord(a);
+        hipLaunchKernelGGL(k.f, dim3(blocks), dim3(256), 0, 0, out, 1u, iters);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        // wave-instructions per SIMD = 8 waves * iters * 8
+        const double per_simd = 8.0 * iters * 8;
+        const double cyc = ms * 1e-3 * p.clockRate * 1e3;
+        printf("%-22s %.3f ms  %.2f cycles per wave64 instruction per SIMD\n", k.n, ms, cyc / per_simd);
+    }
+    return 0;
+}
