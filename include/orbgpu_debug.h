@@ -21,6 +21,11 @@ int orbgpu_debug_level_candidates(orbgpu_extractor* ex, int frame, int level, in
  * relative to the border.  Returns the count (writes at most cap). */
 int orbgpu_debug_level_octree(orbgpu_extractor* ex, int frame, int level, int* xys, int cap);
 
+/* The blurred level (GaussianBlur 7x7, sigma 2, REFLECT_101, as
+ * ORBextractor.cpp:1097-1098) of (frame, level) of the last extraction,
+ * copied row by row into dst (dst_step >= level width). */
+int orbgpu_debug_level_blur(orbgpu_extractor* ex, int frame, int level, uint8_t* dst, size_t dst_step);
+
 /* Per-pass trace of the octree kernel for frame 0 (enable before extracting;
  * out: per level 512 ints = [passes, 0, then 8 ints per pass: inner, nL, C,
  * S, nToExpand, kstop, nkeys, N]). */

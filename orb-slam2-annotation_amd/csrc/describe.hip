@@ -141,11 +141,35 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, uint8_t* 
     // border, so no clamping); 9 aligned dwords per row when they stay
     // inside the row, else bytes
     const int xd = (cx - 15) & ~3, od = cx - 15 - xd;
-    if (xd + 36 <= L.w) {
-        for (int idx = lane; idx < 31 * 9; idx += 64) {
-            const int r = idx / 9, q = idx - r * 9;
-            *reinterpret_cast<uint32_t*>(s_disc + r * kDiscPitch + 4 * q) =
-                *reinterpret_cast<const uint32_t*>(raw + (size_t)(cy - 15 + r) * rp + xd + 4 * q);
+    // Every lane issues all of its window loads (disc and blurred patch)
+    // before the first LDS store: one memory round trip per keypoint.
+    const int xb = (cx - kBlurR) & ~3, ob = cx - kBlurR - xb;
+    const uint8_t* dsrc = raw + (size_t)(cy - 15) * rp + xd;
+    const uint8_t* bsrc = bl + (size_t)(cy - kBlurR) * L.pitch + xb;
+    constexpr int kDiscWords = 31 * 9, kBlurWords = kBlur * 10;
+    constexpr int kDiscLoads = (kDiscWords + 63) / 64, kBlurLoads = (kBlurWords + 63) / 64;
+    const bool disc_words = xd + 36 <= L.w;
+    uint32_t vd[kDiscLoads], vb[kBlurLoads];
+#pragma unroll
+    for (int k = 0; k < kDiscLoads; ++k) {
+        const int idx = min(lane + 64 * k, kDiscWords - 1), r = idx / 9, q = idx - r * 9;
+        vd[k] = disc_words ? *reinterpret_cast<const uint32_t*>(dsrc + (size_t)r * rp + 4 * q) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kBlurLoads; ++k) {
+        const int idx = min(lane + 64 * k, kBlurWords - 1), r = idx / 10, q = idx - r * 10;
+        vb[k] = *reinterpret_cast<const uint32_t*>(bsrc + (size_t)r * L.pitch + 4 * q);
+    }
+#pragma unroll
+    for (int k = 0; k < kBlurLoads; ++k) {
+        const int idx = lane + 64 * k, r = idx / 10, q = idx - r * 10;
+        if (idx < kBlurWords) *reinterpret_cast<uint32_t*>(s_blur + r * kBPitch + 4 * q) = vb[k];
+    }
+    if (disc_words) {
+#pragma unroll
+        for (int k = 0; k < kDiscLoads; ++k) {
+            const int idx = lane + 64 * k, r = idx / 9, q = idx - r * 9;
+            if (idx < kDiscWords) *reinterpret_cast<uint32_t*>(s_disc + r * kDiscPitch + 4 * q) = vd[k];
         }
     } else {
         for (int idx = lane; idx < 31 * 31; idx += 64) {
@@ -153,14 +177,8 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, uint8_t* 
             s_disc[r * kDiscPitch + od + c] = raw[(size_t)(cy - 15 + r) * rp + cx - 15 + c];
         }
     }
-    // blurred 37x37 neighbourhood rBRIEF samples from (cx-18 >= 1 always);
-    // the blur buffer is padded, so the 10-dword spans never leave it
-    const int xb = (cx - kBlurR) & ~3, ob = cx - kBlurR - xb;
-    for (int idx = lane; idx < kBlur * 10; idx += 64) {
-        const int r = idx / 10, q = idx - r * 10;
-        *reinterpret_cast<uint32_t*>(s_blur + r * kBPitch + 4 * q) =
-            *reinterpret_cast<const uint32_t*>(bl + (size_t)(cy - kBlurR + r) * L.pitch + xb + 4 * q);
-    }
+    // (blurred 37x37 neighbourhood: rBRIEF samples from cx-18 >= 1 always;
+    // the blur buffer is padded, so the 10-dword spans never leave it)
     wave_sync();
 
     // intensity centroid over the disc (integer moments: order-free)
@@ -228,7 +246,8 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
                                                                    int* __restrict__ counts, int kp_cap) {
     __shared__ __attribute__((aligned(16))) uint8_t s_disc[kDescWaves][31 * kDiscPitch];
     __shared__ __attribute__((aligned(16))) uint8_t s_blur[kDescWaves][kBlur * kBPitch];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: metadata in SGPRs
     const int item = blockIdx.x * kDescWaves + wave;
     if (item >= items) return;
     const int f = item / g.slots_frame, slot = item - f * g.slots_frame;

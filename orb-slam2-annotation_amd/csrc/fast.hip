@@ -18,6 +18,28 @@ namespace orbgpu {
 
 namespace {
 
+#ifndef FAST_PROBE
+#define FAST_PROBE 0  // diagnostic build only (tools/pyr_variants.sh): 1 = per-phase cycle totals
+#endif
+#if FAST_PROBE
+__device__ unsigned long long g_fast_phase[16];
+#define FAST_CNT(i, n) do { if ((FAST_PROBE & 4) && lane == 0) atomicAdd(&g_fast_phase[i], (unsigned long long)(n)); } while (0)
+__device__ __forceinline__ unsigned long long fast_now() {
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define FAST_T(v) const unsigned long long v = fast_now()
+#define FAST_ACC(i, dt) do { if (lane == 0) atomicAdd(&g_fast_phase[i], (unsigned long long)(dt)); } while (0)
+#else
+#define FAST_T(v) ((void)0)
+#define FAST_ACC(i, dt) ((void)0)
+#define FAST_CNT(i, n) ((void)0)
+#endif
+
+
 __device__ inline bool has_run9(uint32_t m16) {
     uint32_t m = m16 | (m16 << 16);
     uint32_t r = m & (m >> 1);   // runs >= 2
@@ -83,23 +105,27 @@ struct CellTiles {
 // compass pre-test on every pixel -> 16-pixel contiguity test on survivors
 // -> arc strength on corners.
 __device__ int fast_corners(const CellTiles& T, int P, int dw, int dh, int ox, int t, int lane) {
-    const uint32_t mdw = (1u << 24) / (uint32_t)dw + 1u;
+    // compass pre-test, row-major over the detection region: 32 lanes per
+    // row when it fits (two rows per pass), else 64 (dw <= 64: host check).
+    // The tests are lane masks (v_cmp -> SGPR) combined with scalar logic.
+    const int lpr = dw > 32 ? 64 : 32;
+    const int rsub = lpr == 32 ? lane >> 5 : 0, col = lane & (lpr - 1);
+    const int rstep = 64 / lpr;
     int na = 0;
-    for (int base = 0; base < dw * dh; base += 64) {
-        const int idx = base + lane;
-        bool pass = false;
-        int off = 0;
-        if (idx < dw * dh) {
-            const int rr = fast_div(idx, mdw);
-            off = (3 + rr) * P + 3 + ox + (idx - rr * dw);
-            const uint8_t* p = T.win + off;
-            const int v = p[0], lo = v - t, hi = v + t;
-            const int c0 = p[3 * P], c4 = p[3], c8 = p[-3 * P], c12 = p[-3];
-            const uint32_t dk = (c0 < lo) | ((c4 < lo) << 1) | ((c8 < lo) << 2) | ((c12 < lo) << 3);
-            const uint32_t br = (c0 > hi) | ((c4 > hi) << 1) | ((c8 > hi) << 2) | ((c12 > hi) << 3);
-            pass = ((dk & ((dk >> 1) | (dk << 3))) | (br & ((br >> 1) | (br << 3)))) & 15;
-        }
-        na = wave_append(pass, (uint16_t)off, T.la, na, lane);
+    for (int rr = 0; rr < dh; rr += rstep) {
+        const int r = rr + rsub;
+        const int off = (3 + r) * P + 3 + ox + col;
+        const uint8_t* p = T.win + off;  // rows/cols past the region stay inside LDS: masked below
+        const int v = p[0], lo = v - t, hi = v + t;
+        const int c0 = p[3 * P], c4 = p[3], c8 = p[-3 * P], c12 = p[-3];
+        typedef unsigned long long u64;
+        const u64 D0 = __ballot(c0 < lo), D4 = __ballot(c4 < lo), D8 = __ballot(c8 < lo), D12 = __ballot(c12 < lo);
+        const u64 B0 = __ballot(c0 > hi), B4 = __ballot(c4 > hi), B8 = __ballot(c8 > hi), B12 = __ballot(c12 > hi);
+        const u64 IN = __ballot((r < dh) & (col < dw));
+        const u64 PASS = IN & ((D0 & D4) | (D4 & D8) | (D8 & D12) | (D12 & D0) | (B0 & B4) | (B4 & B8) |
+                               (B8 & B12) | (B12 & B0));
+        if ((PASS >> lane) & 1ull) T.la[na + __popcll(PASS & ((1ull << lane) - 1ull))] = (uint16_t)off;
+        na += __popcll(PASS);
     }
     wave_sync();
     const int ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
@@ -125,6 +151,13 @@ __device__ int fast_corners(const CellTiles& T, int P, int dw, int dh, int ox, i
         nb = wave_append(corner, (uint16_t)off, T.lb, nb, lane);
     }
     wave_sync();
+    FAST_CNT(8, 1);
+    FAST_CNT(9, (dh + rstep - 1) / rstep);
+    FAST_CNT(10, (na + 63) / 64);
+    FAST_CNT(11, (nb + 63) / 64);
+    FAST_CNT(12, na);
+    FAST_CNT(13, nb);
+    FAST_CNT(14, dw * dh);
     for (int j = lane; j < nb; j += 64) {
         const int off = T.lb[j];
         const uint8_t* p = T.win + off;
@@ -177,6 +210,7 @@ __device__ int nms_emit(const CellTiles& T, int P, int nb, int ox, int t, int la
 }
 
 constexpr int kCellWaves = 4;  // cells (one per wave) in flight per block
+constexpr int kStageLoads = 8;  // window dwords per lane in flight
 
 __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int ncells_total,
                                                                      const uint8_t* __restrict__ img0, size_t row0,
@@ -186,7 +220,8 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
                                                                      int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int P = g.win_pitch, R = g.win_rows;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: metadata in SGPRs
     const size_t per_wave = ((size_t)2 * P * R + 4 * (size_t)g.det_max + 15) & ~(size_t)15;
     uint8_t* ws = smem + wave * per_wave;
     CellTiles T;
@@ -222,34 +257,67 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
 
     // stage rows: dwords covering [xa, maxX), xa = iniX & ~3 (row pitch and
     // frame base are 16-byte aligned; maxX <= w - 16, so no over-read)
+    FAST_T(t0);
     const int xa = iniX & ~3, ox = iniX - xa;
     const int nd = (maxX - xa + 3) >> 2;
     const uint32_t mnd = (1u << 24) / (uint32_t)nd + 1u;
-    for (int idx = lane; idx < nd * wh; idx += 64) {
-        const int r = fast_div(idx, mnd), q = idx - r * nd;
-        const uint32_t v = *reinterpret_cast<const uint32_t*>(base + (size_t)(iniY + r) * pitch + xa + 4 * q);
-        *reinterpret_cast<uint32_t*>(s_win + r * P + 4 * q) = v;
+    // all of a lane's loads are issued before any is consumed, so the
+    // window costs one memory round trip, not one per row group
+    const uint8_t* wbase = base + (size_t)iniY * pitch + xa;
+    for (int b0 = 0; b0 < nd * wh; b0 += 64 * kStageLoads) {
+        uint32_t v[kStageLoads];
+#pragma unroll
+        for (int k = 0; k < kStageLoads; ++k) {  // unconditional (clamped) loads: no waits between them
+            const int idx = min(b0 + lane + 64 * k, nd * wh - 1);
+            const int r = fast_div(idx, mnd), q = idx - r * nd;
+            v[k] = *reinterpret_cast<const uint32_t*>(wbase + (size_t)r * pitch + 4 * q);
+        }
+#pragma unroll
+        for (int k = 0; k < kStageLoads; ++k) {
+            const int idx = b0 + lane + 64 * k;
+            const int r = fast_div(idx, mnd), q = idx - r * nd;
+            if (idx < nd * wh) *reinterpret_cast<uint32_t*>(s_win + r * P + 4 * q) = v[k];
+        }
     }
+    FAST_T(t1);
     for (int idx = lane; idx < P * R / 4; idx += 64) reinterpret_cast<uint32_t*>(T.sc)[idx] = 0u;
     wave_sync();
+    FAST_T(t2);
 
     // detection region of cv::FAST on the window: rows [3, wh-3), cols [3, ww-3)
     const int dw = maxX - iniX - 6, dh = wh - 6;
     int total = 0;
     if (dw > 0 && dh > 0) {
         int nb = fast_corners(T, P, dw, dh, ox, g.ini_th, lane);
+        FAST_T(t3);
         total = nms_emit(T, P, nb, ox, g.ini_th, lane, iniX, iniY, out, L.cell_cap, err);
+        FAST_T(t4);
+        FAST_ACC(0, t1 - t0);
+        FAST_ACC(1, t2 - t1);
+        FAST_ACC(2, t3 - t2);
+        FAST_ACC(3, t4 - t3);
+        FAST_ACC(4, 1);
         if (total == 0) {  // ORBextractor.cpp:821-825: retry the cell at minThFAST
             for (int j = lane; j < nb; j += 64) T.sc[T.lb[j]] = 0;
             wave_sync();
+            FAST_T(t5);
             nb = fast_corners(T, P, dw, dh, ox, g.min_th, lane);
             total = nms_emit(T, P, nb, ox, g.min_th, lane, iniX, iniY, out, L.cell_cap, err);
+            FAST_T(t6);
+            FAST_ACC(5, t6 - t5);
+            FAST_ACC(6, 1);
         }
     }
     if (lane == 0) *cnt_out = min(total, L.cell_cap);
 }
 
 }  // namespace
+
+#if FAST_PROBE
+extern "C" int orbgpu_debug_fast_phases(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fast_phase), 16 * sizeof(unsigned long long)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                              const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err,

@@ -314,6 +314,8 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     int cell_base = 0, out_off = 0, max_cells = 0, ncap = 0;
     ptab.clear();
     ytab.clear();
+    std::vector<int4> ptab_pairs;  // the per-pixel-pair layout of the same taps
+    bool win_ok = true;
     for (int l = 0; l < L; ++l) {
         LevelGeom& v = g.lv[l];
         v.w = cv_round((float)e->W * e->inv_scale[l]);
@@ -392,10 +394,10 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
             if ((size_t)v.pitch * v.h >= (1u << 31)) return fail(ORBGPU_ERR_UNSUPPORTED, "level too large");
             v.ptab_offset = (int)ptab.size();
             v.dbg_level = l;
-            // window layout if every quad's taps fit one dword-aligned 8-byte window
+            // both column-tap layouts (pyramid.hip); the window one is used
+            // when every quad of every level fits a dword-aligned 8-byte window
             std::vector<int> wlo(quads);
-            v.pyr_win = 1;
-            for (int q = 0; q < quads && v.pyr_win; ++q) {
+            for (int q = 0; q < quads; ++q) {
                 int lo = INT32_MAX, hi = INT32_MIN;
                 for (int k = 0; k < 4; ++k) {
                     const int dx = 4 * q + k;
@@ -405,38 +407,35 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
                     hi = std::max(hi, sx + ((xt[dx].y >> 16) != 0 ? 1 : 0));
                 }
                 const int w0 = (std::max(hi - 7, 0) + 3) & ~3;
-                if (w0 > lo) v.pyr_win = 0;
+                if (w0 > lo) win_ok = false;
                 wlo[q] = w0;
             }
             for (int q = 0; q < quads; ++q) {
-                int lo[4], wt[4], sel[4];
+                int lo[4], wt[4], wsel[4], psel[4];
                 for (int k = 0; k < 4; ++k) {
                     const int dx = 4 * q + k;
                     const int sx = dx < v.w ? (xt[dx].x & 0xFFFF) : 0;
                     wt[k] = dx < v.w ? xt[dx].y : 0;
-                    if (v.pyr_win) {
-                        const int b0 = sx - wlo[q];
-                        const int b1 = (wt[k] >> 16) != 0 ? b0 + 1 : b0;
-                        sel[k] = dx < v.w ? (int)(0x0c000c00u | (uint32_t)b0 | ((uint32_t)b1 << 16)) : (int)0x0c0c0c0cu;
-                    } else {
-                        lo[k] = sx & ~3;
-                        sel[k] = (int)(0x0c010c00u + (uint32_t)(sx & 3) * 0x00010001u);
-                    }
+                    const int b0 = sx - wlo[q];
+                    const int b1 = (wt[k] >> 16) != 0 ? b0 + 1 : b0;
+                    wsel[k] = dx < v.w ? (int)(0x0c000c00u | (uint32_t)(b0 & 7) | ((uint32_t)(b1 & 7) << 16))
+                                       : (int)0x0c0c0c0cu;
+                    lo[k] = sx & ~3;
+                    psel[k] = (int)(0x0c010c00u + (uint32_t)(sx & 3) * 0x00010001u);
                 }
-                if (v.pyr_win) {
-                    ptab.push_back(int4{wlo[q], wt[0], wt[1], wt[2]});
-                    ptab.push_back(int4{wt[3], sel[0], sel[1], sel[2]});
-                    ptab.push_back(int4{sel[3], 0, 0, 0});
-                } else {
-                    ptab.push_back(int4{lo[0], wt[0], lo[1], wt[1]});
-                    ptab.push_back(int4{lo[2], wt[2], lo[3], wt[3]});
-                    ptab.push_back(int4{sel[0], sel[1], sel[2], sel[3]});
-                }
+                ptab.push_back(int4{wlo[q], wt[0], wt[1], wt[2]});
+                ptab.push_back(int4{wt[3], wsel[0], wsel[1], wsel[2]});
+                ptab.push_back(int4{wsel[3], 0, 0, 0});
+                ptab_pairs.push_back(int4{lo[0], wt[0], lo[1], wt[1]});
+                ptab_pairs.push_back(int4{lo[2], wt[2], lo[3], wt[3]});
+                ptab_pairs.push_back(int4{psel[0], psel[1], psel[2], psel[3]});
             }
             v.ytab_offset = (int)ytab.size();
             ytab.insert(ytab.end(), yt.begin(), yt.end());
         }
     }
+    g.pyr_win = win_ok ? 1 : 0;
+    if (!win_ok) ptab.swap(ptab_pairs);
     {
         int rc = plan_pyramid_bands(g, ytab, e->max_batch, e->pyr_bands);
         if (rc) return rc;
@@ -462,6 +461,7 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     g.win_rows = 0;
     g.det_max = 0;
     for (int l = 0; l < L; ++l) {
+        if (g.lv[l].wcell > 64) return fail(ORBGPU_ERR_UNSUPPORTED, "FAST cell wider than 64 px");
         g.win_pitch = std::max(g.win_pitch, (int)round_up((size_t)g.lv[l].wcell + 9, 4));
         g.win_rows = std::max(g.win_rows, g.lv[l].hcell + 6);
         g.det_max = std::max(g.det_max, (int)round_up((size_t)g.lv[l].wcell * g.lv[l].hcell, 8));
@@ -704,6 +704,18 @@ int orbgpu_extractor_copy_level(orbgpu_extractor* e, int frame, int level, uint8
     const size_t pitch = level == 0 ? e->last_row : (size_t)v.pitch;
     ORB_HIP(hipStreamSynchronize(e->stream));
     ORB_HIP(hipMemcpy2D(dst, dst_step, src, pitch, v.w, v.h, hipMemcpyDeviceToHost));
+    return ORBGPU_OK;
+}
+
+int orbgpu_debug_level_blur(orbgpu_extractor* e, int frame, int level, uint8_t* dst, size_t dst_step) {
+    if (!e || !dst) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    if (!e->last_img || frame < 0 || frame >= e->last_batch || level < 0 || level >= e->nlevels)
+        return fail(ORBGPU_ERR_ARG, "no such frame/level in the last extraction");
+    const LevelGeom& v = e->g.lv[level];
+    if (dst_step < (size_t)v.w) return fail(ORBGPU_ERR_ARG, "dst_step < level width");
+    ORB_HIP(hipStreamSynchronize(e->stream));
+    ORB_HIP(hipMemcpy2D(dst, dst_step, e->d_blur + v.blur_offset + (size_t)frame * v.blur_frame_bytes, v.pitch, v.w,
+                        v.h, hipMemcpyDeviceToHost));
     return ORBGPU_OK;
 }
 

@@ -55,7 +55,6 @@ struct LevelGeom {
     // fused pyramid pass (pyramid.hip)
     int lds_pitch;            // LDS row pitch: w rounded up to 4 (level 0: to 16)
     int qmain;                // quads per row on VResizeLinearVec_32s8u's vector path (the rest is the tail quad)
-    int pyr_win;              // 1: every quad's column taps fit one 8-byte window (pyramid.hip WIN layout)
     int dbg_level;            // = level index (diagnostic builds)
     uint32_t quad_magic;      // ceil(2^32 / d): i / d = umulhi(i, magic); d = qmain (level 0: ceil(w/16))
     int ptab_offset;          // int4 offset of this level's per-quad column taps (3 int4 per quad)
@@ -81,6 +80,7 @@ struct Geom {
     int pyr_bands;
     int pyr_lds_a, pyr_lds_b, pyr_lds_y, pyr_lds_bytes;  // odd levels, even levels (incl. 0), y taps
     int pyr_rec_stride;       // int4s per band record (band entries + per-row source offsets)
+    int pyr_win;              // 1: every quad's column taps fit one 8-byte window (pyramid.hip WIN layout)
     LevelGeom lv[kMaxLevels];
 };
 

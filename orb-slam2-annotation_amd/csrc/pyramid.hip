@@ -82,8 +82,8 @@ __device__ __forceinline__ void put_byte_shr2(uint32_t& out, uint32_t s) {
 // column taps stay in registers for the whole level.  s_rows[r - r0] = (LDS
 // offset of source row y0, of y1, ibeta0 << 12, ibeta1 << 12).
 //
-// Column taps per quad (ptab, 3 x int4), two layouts chosen per level on the
-// host (LevelGeom::pyr_win):
+// Column taps per quad (ptab, 3 x int4), two layouts chosen for the whole
+// pyramid on the host (Geom::pyr_win; the kernel is instantiated for each):
 //  * window (WIN): all eight taps of the quad lie in one dword-aligned 8-byte
 //    window of the source row (always true for scale factors <= 4/3):
 //    (lo, wt0, wt1, wt2), (wt3, sel0, sel1, sel2), (sel3, -, -, -) -- one
@@ -249,6 +249,7 @@ __device__ __forceinline__ void resize_band(const uint8_t* __restrict__ lds, con
         resize_rows<true, WIN>(lds, V, tp, r0, r1, own0, own1, s_rows, lds_dst, hbm_dst);
 }
 
+template <bool WIN>
 __global__ __launch_bounds__(kPyrThreads) void pyramid_kernel(Geom g, const int4* __restrict__ recs,
                                                               const int4* __restrict__ ptab,
                                                               const uint8_t* __restrict__ img0, size_t row0,
@@ -295,10 +296,7 @@ __global__ __launch_bounds__(kPyrThreads) void pyramid_kernel(Geom g, const int4
         const int bz = __builtin_amdgcn_readfirstlane(bv.z), bw = __builtin_amdgcn_readfirstlane(bv.w);
         uint8_t* dst_lds = l + 1 < L ? s_pyr + ((l & 1) ? g.pyr_lds_a : g.pyr_lds_b) : nullptr;
         uint8_t* dst_hbm = pyr + V.offset + (size_t)f * V.frame_bytes;
-        if (V.pyr_win)
-            resize_band<true>(s_pyr, V, tp, bx, by, bz, bw, s_rec + yoff, dst_lds, dst_hbm);
-        else
-            resize_band<false>(s_pyr, V, tp, bx, by, bz, bw, s_rec + yoff, dst_lds, dst_hbm);
+        resize_band<WIN>(s_pyr, V, tp, bx, by, bz, bw, s_rec + yoff, dst_lds, dst_hbm);
         yoff += by - bx;
 #if PYR_PROBE & 8
         {
@@ -322,8 +320,12 @@ int pyr_threads() { return kPyrThreads; }
 hipError_t launch_pyramid(const Geom& g, int batch, const int4* recs, const int4* ptab, const uint8_t* img0,
                           size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream) {
     if (g.nlevels < 2) return hipSuccess;
-    hipLaunchKernelGGL(pyramid_kernel, dim3(g.pyr_bands * batch), dim3(kPyrThreads), g.pyr_lds_bytes, stream, g,
-                       recs, ptab, img0, row0, frame0, pyr);
+    if (g.pyr_win)
+        hipLaunchKernelGGL(pyramid_kernel<true>, dim3(g.pyr_bands * batch), dim3(kPyrThreads), g.pyr_lds_bytes,
+                           stream, g, recs, ptab, img0, row0, frame0, pyr);
+    else
+        hipLaunchKernelGGL(pyramid_kernel<false>, dim3(g.pyr_bands * batch), dim3(kPyrThreads), g.pyr_lds_bytes,
+                           stream, g, recs, ptab, img0, row0, frame0, pyr);
     return hipGetLastError();
 }
 
@@ -339,7 +341,10 @@ extern "C" int orbgpu_debug_pyr_stamps(unsigned long long* out, int n) {
 #endif
 
 hipError_t pyramid_set_lds_limit(size_t bytes) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_kernel),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_kernel<true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_kernel<false>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 

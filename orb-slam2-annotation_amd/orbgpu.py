@@ -80,6 +80,7 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_search_for_initialization_batch_device.argtypes = [
             i, GridBounds, vp, vp, vp, sz, vp, vp, vp, sz, vp, i, f, i, vp, vp, vp]
         L.orbgpu_debug_level_candidates.argtypes = [vp, i, i, vp, i]
+        L.orbgpu_debug_level_blur.argtypes = [vp, i, i, vp, sz]
         L.orbgpu_debug_level_octree.argtypes = [vp, i, i, vp, i]
         L.orbgpu_debug_octree_trace.argtypes = [vp, i, vp, i]
         L.orbgpu_search_for_initialization.argtypes = [GridBounds, vp, vp, i, vp, vp, i, vp, i, f, i, vp,
@@ -250,6 +251,13 @@ class Extractor:
             t = out[l * 512:(l + 1) * 512]
             res.append(t[2:2 + 8 * t[0]].reshape(-1, 8))
         return res
+
+    def blurred(self, level: int, frame: int = 0) -> np.ndarray:
+        """The blurred level (GaussianBlur 7x7) of `frame` of the last extraction."""
+        w, h = self.level_sizes[level]
+        out = np.zeros((h, w), np.uint8)
+        _check(lib().orbgpu_debug_level_blur(self.h, frame, level, out.ctypes.data, w), "debug_level_blur")
+        return out
 
     def level(self, level: int, frame: int = 0) -> np.ndarray:
         """mvImagePyramid[level] of `frame` of the last extraction."""

@@ -51,6 +51,21 @@ def test_pyramid_levels(mono_frames, frame):
         assert len(d[0]) == 0, f"level {l}: {len(d[0])} pixels differ, first {list(zip(*d))[:5]}"
 
 
+@pytest.mark.parametrize("w,h,nf,kind", [(640, 480, 1000, "stream"), (640, 480, 1000, "noise"),
+                                         (1241, 376, 2000, "stream"), (752, 480, 1200, "noise")])
+def test_blurred_levels(w, h, nf, kind):
+    """GaussianBlur(7x7, sigma 2, REFLECT_101) of every level, bit-exact
+    (incl. the half-to-even / half-up column rounding split at 4*floor(w/4))."""
+    og = _gpu()
+    ex = og.Extractor(nfeatures=nf, width=w, height=h)
+    img = synth.mono_stream(1, w, h, seed=11)[0] if kind == "stream" else synth.noise_image(w, h)
+    ex.extract(img)
+    for l in range(8):
+        a, b = ex.blurred(l), orbref.gaussian7(ex.level(l))
+        d = np.nonzero(a != b)
+        assert len(d[0]) == 0, f"level {l}: {len(d[0])} pixels differ, first {list(zip(*d))[:5]}"
+
+
 @pytest.mark.parametrize("frame", [0, 1, 2, 5])
 def test_extract_mono_640x480(mono_frames, frame):
     og = _gpu()

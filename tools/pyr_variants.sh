@@ -1,4 +1,4 @@
-# Build tuning variants of liborbgpu.so (pyramid probes / LDS budgets) into
+# Build tuning/diagnostic variants of liborbgpu.so into
 # exp/<name>/ -- CPU side; run them on the GPU with tools/pyr_variants_run.sh.
 # usage: tools/pyr_variants.sh name:FLAGS [name:FLAGS ...]
 #   e.g. probe1:-DPYR_PROBE=1 lds64:-DORBGPU_PYR_LDS_KB=64
@@ -9,10 +9,14 @@ H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=
 for spec in "$@"; do
     name=${spec%%:*}; flags=${spec#*:}; flags=${flags//,/ }
     d=../exp/$name; mkdir -p $d
-    $H $flags -c csrc/pyramid.hip -o $d/pyramid.hip.o &
-    $H $flags -x hip -c csrc/orbgpu.cpp -o $d/orbgpu.cpp.o &
+    # FILES (env) = the sources the flags affect; the rest are reused from build/
+    files=${FILES:-"pyramid.hip orbgpu.cpp"}
+    objs=$(ls build/*.o)
+    for f in $files; do
+        case $f in *.hip) $H $flags -c csrc/$f -o $d/$f.o & ;; *) $H $flags -x hip -c csrc/$f -o $d/$f.o & ;; esac
+        objs=$(echo "$objs" | grep -v "/$f.o")
+    done
     wait
-    objs=$(ls build/*.o | grep -v -e '/pyramid.hip.o' -e '/orbgpu.cpp.o')
-    $H -shared -o $d/liborbgpu.so $d/pyramid.hip.o $d/orbgpu.cpp.o $objs
+    $H -shared -o $d/liborbgpu.so $d/*.o $objs
     echo "built $d ($flags)"
 done

@@ -31,6 +31,34 @@ OP_KERNEL(k_mul24, "v_mul_u32_u24 %0, %0, %1")
 OP_KERNEL(k_mullo, "v_mul_lo_u32 %0, %0, %1")
 OP_KERNEL(k_sdwa, "v_lshrrev_b32_sdwa %0, 2, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD")
 OP_KERNEL(k_add3, "v_add3_u32 %0, %0, %1, 2")
+OP_KERNEL(k_fma, "v_fma_f32 %0, %0, %1, %1")
+OP_KERNEL(k_mad24, "v_mad_u32_u24 %0, %0, %1, %1")
+OP_KERNEL(k_pkmad16, "v_pk_mad_u16 %0, %0, %1, %1")
+OP_KERNEL(k_pkadd16, "v_pk_add_u16 %0, %0, %1")
+OP_KERNEL(k_cvtsdwa, "v_cvt_f32_u32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1")
+OP_KERNEL(k_cvtpku8, "v_cvt_pk_u8_f32 %0, %1, 1, %0")
+OP_KERNEL(k_min3, "v_min3_i32 %0, %0, %1, %1")
+
+#define OP64_KERNEL(NAME, ASM)                                                                \
+    __global__ __launch_bounds__(256) void NAME(unsigned* out, unsigned seed, int iters) {    \
+        typedef float f2 __attribute__((ext_vector_type(2)));                                  \
+        f2 v0 = {(float)(seed ^ threadIdx.x), 1.f}, v1 = v0 * 3.f, v2 = v0 * 5.f, v3 = v0 * 7.f;  \
+        const f2 k = {1.0001f, 0.9999f};                                                       \
+        for (int i = 0; i < iters; ++i) {                                                      \
+            asm volatile(ASM : "+v"(v0) : "v"(k));                                             \
+            asm volatile(ASM : "+v"(v1) : "v"(k));                                             \
+            asm volatile(ASM : "+v"(v2) : "v"(k));                                             \
+            asm volatile(ASM : "+v"(v3) : "v"(k));                                             \
+            asm volatile(ASM : "+v"(v0) : "v"(k));                                             \
+            asm volatile(ASM : "+v"(v1) : "v"(k));                                             \
+            asm volatile(ASM : "+v"(v2) : "v"(k));                                             \
+            asm volatile(ASM : "+v"(v3) : "v"(k));                                             \
+        }                                                                                      \
+        f2 r = v0 + v1 + v2 + v3;                                                              \
+        out[blockIdx.x * 256 + threadIdx.x] = (unsigned)(r.x + r.y);                           \
+    }
+OP64_KERNEL(k_pkfma, "v_pk_fma_f32 %0, %0, %1, %1")
+OP64_KERNEL(k_pkaddf, "v_pk_add_f32 %0, %0, %1")
 
 int main() {
     hipDeviceProp_t p;
@@ -43,7 +71,9 @@ int main() {
     struct K { const char* n; void (*f)(unsigned*, unsigned, int); } ks[] = {
         {"v_add_u32", k_add}, {"v_and_b32", k_and}, {"v_perm_b32", k_perm}, {"v_dot2_u32_u16", k_dot2},
         {"v_mul_hi_u32_u24", k_mulhi24}, {"v_mul_u32_u24", k_mul24}, {"v_mul_lo_u32", k_mullo},
-        {"v_lshrrev_b32_sdwa", k_sdwa}, {"v_add3_u32", k_add3}};
+        {"v_lshrrev_b32_sdwa", k_sdwa}, {"v_add3_u32", k_add3}, {"v_fma_f32", k_fma}, {"v_mad_u32_u24", k_mad24},
+        {"v_pk_mad_u16", k_pkmad16}, {"v_pk_add_u16", k_pkadd16}, {"v_cvt_f32_u32_sdwa", k_cvtsdwa},
+        {"v_cvt_pk_u8_f32", k_cvtpku8}, {"v_min3_i32", k_min3}, {"v_pk_fma_f32", k_pkfma}, {"v_pk_add_f32", k_pkaddf}};
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
