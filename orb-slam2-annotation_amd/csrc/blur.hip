@@ -5,9 +5,9 @@
 // float path of SymmColumnVec_32s8u) and half-up on the scalar tail
 // (FixedPtCastEx<int,uchar>, 16 bits).
 //
-// One launch over all levels of all frames; a thread owns 4 columns x 64
-// rows (see below).  Roofline: HBM streaming (read + write each level once,
-// 6/64 halo rows re-read from L2).
+// One launch over all levels of all frames; a thread owns 4 columns x 63
+// rows (see below).  Bound: VALU (packed u16 row pass, packed f32 column
+// pass); HBM: read + write each level once, 6/63 halo rows re-read from L2.
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
 
@@ -15,18 +15,52 @@ namespace orbgpu {
 
 namespace {
 
-constexpr int kStrip = 64;  // output rows per thread
-__constant__ int c_bk[7] = {18, 34, 49, 55, 49, 34, 18};
+constexpr int kStrip = kBlurStrip;
 
-__device__ inline int reflect101(int p, int n) {
-    while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
-    return p;
+// BORDER_REFLECT_101 for an overshoot of at most n - 1 (here <= 6 < n)
+__device__ inline int reflect101(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Row pass of 4 adjacent columns: packed 16-bit arithmetic, two columns per
+// register.  P[j] = (px[j], px[j+1]) with px[j] = column x0 - 3 + j.  The
+// symmetric sum 18(a+g) + 34(b+f) + 49(c+e) + 55d of 8-bit inputs is at most
+// 255 * 257 = 65535: exact in u16.  Returns the 4 sums as floats (exact).
+__device__ __forceinline__ void row_pass(const uint32_t (&P)[9], f32x2& lo, f32x2& hi) {
+    const u16x2* Q = reinterpret_cast<const u16x2*>(P);
+    const u16x2 k18 = {18, 18}, k34 = {34, 34}, k49 = {49, 49}, k55 = {55, 55};
+    const u16x2 r01 = (Q[0] + Q[6]) * k18 + (Q[1] + Q[5]) * k34 + (Q[2] + Q[4]) * k49 + Q[3] * k55;
+    const u16x2 r23 = (Q[2] + Q[8]) * k18 + (Q[3] + Q[7]) * k34 + (Q[4] + Q[6]) * k49 + Q[5] * k55;
+    lo = f32x2{(float)r01.x, (float)r01.y};
+    hi = f32x2{(float)r23.x, (float)r23.y};
 }
 
-// One thread = 4 adjacent output columns x a 64-row strip of one level.
-// Walking down the strip it keeps the last 7 row-pass results in registers
-// (separable filter as a sliding window), so every input row is read once
-// per strip (+6 halo rows) with three aligned dword loads.
+// Column pass over the 7-row window (w[i] = row y - 3 + i), two columns per
+// packed-f32 op.  Every product and partial sum is an integer below 2^24
+// unless the total is (then the result saturates to 255 either way), so the
+// float arithmetic is exact.
+__device__ __forceinline__ f32x2 col_pass(f32x2 w0, f32x2 w1, f32x2 w2, f32x2 w3, f32x2 w4, f32x2 w5, f32x2 w6) {
+    const f32x2 k18 = {18.f, 18.f}, k34 = {34.f, 34.f}, k49 = {49.f, 49.f}, k55 = {55.f, 55.f};
+    f32x2 s = w3 * k55;
+    s = __builtin_elementwise_fma(w2 + w4, k49, s);
+    s = __builtin_elementwise_fma(w1 + w5, k34, s);
+    s = __builtin_elementwise_fma(w0 + w6, k18, s);
+    return s * f32x2{1.f / 65536.f, 1.f / 65536.f};  // exact: power of two
+}
+
+// 8-bit result of one column on the scalar tail (x >= 4*floor(w/4)):
+// FixedPtCastEx rounds half up.  (The vector path, SymmColumnVec_32s8u,
+// rounds half to even: v_cvt_pk_u8_f32 in store_row.)
+__device__ __forceinline__ uint32_t to_u8(float v) {
+    return (uint32_t)fminf(__builtin_floorf(v + 0.5f), 255.f);  // v + 0.5 exact (< 2^8, 16 frac bits)
+}
+
+// One thread = 4 adjacent output columns x a 63-row strip of one level.
+// Walking down the strip it keeps the last 7 row-pass results (as floats)
+// in registers -- the window rotates statically (the row loop is unrolled
+// by 7) -- so every input row is read once per strip (+6 halo rows) with
+// three aligned dword loads.
 __global__ __launch_bounds__(256) void blur_levels_kernel(Geom g, int items_frame, int items_total,
                                                           const uint8_t* __restrict__ img0, size_t row0,
                                                           size_t frame0, const uint8_t* __restrict__ pyr,
@@ -46,56 +80,61 @@ __global__ __launch_bounds__(256) void blur_levels_kernel(Geom g, int items_fram
     const size_t sp = l == 0 ? row0 : (size_t)L.pitch;
     uint8_t* dst = blur + L.blur_offset + (size_t)f * L.blur_frame_bytes;
     const bool interior = x0 >= 4 && x0 + 7 < L.w;  // columns x0-3 .. x0+6 need no reflection
-    const int w4 = L.w & ~3;
+    const bool simd = x0 < (L.w & ~3);              // all 4 columns on the vector path, else all on the tail
+    const int W = L.w, H = L.h;
 
-    int rp[7][4];  // row-pass sliding window, rows y-3 .. y+3
-#pragma unroll
-    for (int i = 0; i < 7; ++i)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) rp[i][c] = 0;
-    for (int yy = y0 - 3; yy < y1 + 3; ++yy) {
-        const uint8_t* row = src + (size_t)reflect101(yy, L.h) * sp;
-        int px[10];  // level columns x0-3 .. x0+6
+    auto load_row = [&](int yy, f32x2& lo, f32x2& hi) {
+        const uint8_t* row = src + (size_t)reflect101(yy, H) * sp;
+        uint32_t P[9];
         if (interior) {
             const uint32_t a = *reinterpret_cast<const uint32_t*>(row + x0 - 4);
             const uint32_t b = *reinterpret_cast<const uint32_t*>(row + x0);
             const uint32_t c = *reinterpret_cast<const uint32_t*>(row + x0 + 4);
-            px[0] = (a >> 8) & 255; px[1] = (a >> 16) & 255; px[2] = a >> 24;
-            px[3] = b & 255; px[4] = (b >> 8) & 255; px[5] = (b >> 16) & 255; px[6] = b >> 24;
-            px[7] = c & 255; px[8] = (c >> 8) & 255; px[9] = (c >> 16) & 255;
+            // bytes of (b:a) / (c:b) as v_perm_b32 sees them: low word 0-3, high word 4-7
+            P[0] = __builtin_amdgcn_perm(b, a, 0x0c020c01u);
+            P[1] = __builtin_amdgcn_perm(b, a, 0x0c030c02u);
+            P[2] = __builtin_amdgcn_perm(b, a, 0x0c040c03u);
+            P[3] = __builtin_amdgcn_perm(b, a, 0x0c050c04u);
+            P[4] = __builtin_amdgcn_perm(c, b, 0x0c020c01u);
+            P[5] = __builtin_amdgcn_perm(c, b, 0x0c030c02u);
+            P[6] = __builtin_amdgcn_perm(c, b, 0x0c040c03u);
+            P[7] = __builtin_amdgcn_perm(c, b, 0x0c050c04u);
+            P[8] = __builtin_amdgcn_perm(c, b, 0x0c060c05u);
         } else {
+            int px[10];
 #pragma unroll
-            for (int j = 0; j < 10; ++j) px[j] = row[reflect101(x0 - 3 + j, L.w)];
+            for (int j = 0; j < 10; ++j) px[j] = row[reflect101(x0 - 3 + j, W)];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) P[j] = (uint32_t)px[j] | ((uint32_t)px[j + 1] << 16);
         }
-#pragma unroll
-        for (int i = 0; i < 6; ++i)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) rp[i][c] = rp[i + 1][c];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            int acc = 0;
-#pragma unroll
-            for (int j = 0; j < 7; ++j) acc += c_bk[j] * px[c + j];
-            rp[6][c] = acc;
+        row_pass(P, lo, hi);
+    };
+    auto store_row = [&](int y, f32x2 lo, f32x2 hi) {
+        uint32_t packed;
+        if (simd) {  // v_cvt_pk_u8_f32: round to nearest even, saturate, pack
+            packed = __builtin_amdgcn_cvt_pk_u8_f32(lo.x, 0, 0u);
+            packed = __builtin_amdgcn_cvt_pk_u8_f32(lo.y, 1, packed);
+            packed = __builtin_amdgcn_cvt_pk_u8_f32(hi.x, 2, packed);
+            packed = __builtin_amdgcn_cvt_pk_u8_f32(hi.y, 3, packed);
+        } else {
+            packed = to_u8(lo.x) | (to_u8(lo.y) << 8) | (to_u8(hi.x) << 16) | (to_u8(hi.y) << 24);
         }
-        const int y = yy - 3;
-        if (y >= y0) {
-            uint32_t packed = 0;
+        *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.pitch + x0) = packed;  // x0+3 < pitch
+    };
+
+    f32x2 wl[7], wh[7];  // row-pass window: slot (y - y0 + i) % 7 holds row y - 3 + i
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                int v = 0;
+    for (int i = 0; i < 6; ++i) load_row(y0 - 3 + i, wl[i], wh[i]);
+    for (int y = y0; y < y1; y += 7) {
 #pragma unroll
-                for (int i = 0; i < 7; ++i) v += c_bk[i] * rp[i][c];
-                int o;
-                if (x0 + c < w4) {  // SymmColumnVec_32s8u: float path, round half to even
-                    const int qq = v >> 16, rem = v & 0xFFFF;
-                    o = qq + ((rem > 32768) | ((rem == 32768) & (qq & 1)));
-                } else {            // scalar tail: FixedPtCastEx, round half up
-                    o = (v + 32768) >> 16;
-                }
-                packed |= (uint32_t)min(o, 255) << (8 * c);
-            }
-            *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.pitch + x0) = packed;  // x0+3 < pitch
+        for (int u = 0; u < 7; ++u) {
+            if (y + u >= y1) break;
+            load_row(y + u + 3, wl[(u + 6) % 7], wh[(u + 6) % 7]);
+            const f32x2 lo = col_pass(wl[u % 7], wl[(u + 1) % 7], wl[(u + 2) % 7], wl[(u + 3) % 7], wl[(u + 4) % 7],
+                                      wl[(u + 5) % 7], wl[(u + 6) % 7]);
+            const f32x2 hi = col_pass(wh[u % 7], wh[(u + 1) % 7], wh[(u + 2) % 7], wh[(u + 3) % 7], wh[(u + 4) % 7],
+                                      wh[(u + 5) % 7], wh[(u + 6) % 7]);
+            store_row(y + u, lo, hi);
         }
     }
 }

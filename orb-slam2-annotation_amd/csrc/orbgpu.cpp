@@ -453,7 +453,7 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
         blur_off += round_up(v.blur_frame_bytes * e->max_batch, 256);
         v.blur_tiles_x = (v.w + 3) / 4;
         v.blur_tile_base = tiles;
-        tiles += v.blur_tiles_x * ((v.h + 63) / 64);
+        tiles += v.blur_tiles_x * ((v.h + kBlurStrip - 1) / kBlurStrip);
     }
     g.blur_tiles_frame = tiles;
     e->blur_bytes = blur_off + 256;  // slack: describe reads 40-byte row spans
