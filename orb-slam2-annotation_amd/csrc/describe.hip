@@ -101,7 +101,6 @@ __device__ inline int wave_sum(int v) {
     return v;
 }
 
-constexpr int kDiscPitch = 36;   // 31-px disc rows, staged from a 4-aligned column
 constexpr int kBPitch = 40;      // 37-px blurred rows, staged from a 4-aligned column
 
 // The 4 waves of a block process different keypoints: stages are ordered
@@ -112,7 +111,7 @@ __device__ inline void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-__device__ void describe_one(const Geom& g, int f, int slot, int lane, uint8_t* s_disc, uint8_t* s_blur,
+__device__ void describe_one(const Geom& g, int f, int slot, int lane, uint8_t* s_blur,
                              const uint8_t* __restrict__ img0, size_t row0, size_t frame0,
                              const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
                              const uint32_t* __restrict__ oct_out, const int* __restrict__ oct_count,
@@ -137,23 +136,24 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, uint8_t* 
     const size_t rp = l == 0 ? row0 : (size_t)L.pitch;
     const uint8_t* bl = blur + L.blur_offset + (size_t)f * L.blur_frame_bytes;
 
-    // unblurred 31x31 disc (IC_Angle; the keypoint is >= 19 px from every
-    // border, so no clamping); 9 aligned dwords per row when they stay
-    // inside the row, else bytes
+    // Every lane issues all of its window loads (disc words and blurred
+    // patch) before any is consumed: one memory round trip per keypoint.
+    // Unblurred 31x31 disc (IC_Angle): 31 rows x 9 aligned dwords from
+    // column xd = (cx - 15) & ~3.  The keypoint is >= 19 px from every border
+    // (cx <= w - 20, cy <= h - 20), so the words end at most 1 byte past the
+    // row, inside the next row of the same frame; those bytes are outside the
+    // disc and masked off below.
     const int xd = (cx - 15) & ~3, od = cx - 15 - xd;
-    // Every lane issues all of its window loads (disc and blurred patch)
-    // before the first LDS store: one memory round trip per keypoint.
     const int xb = (cx - kBlurR) & ~3, ob = cx - kBlurR - xb;
     const uint8_t* dsrc = raw + (size_t)(cy - 15) * rp + xd;
     const uint8_t* bsrc = bl + (size_t)(cy - kBlurR) * L.pitch + xb;
     constexpr int kDiscWords = 31 * 9, kBlurWords = kBlur * 10;
     constexpr int kDiscLoads = (kDiscWords + 63) / 64, kBlurLoads = (kBlurWords + 63) / 64;
-    const bool disc_words = xd + 36 <= L.w;
     uint32_t vd[kDiscLoads], vb[kBlurLoads];
 #pragma unroll
     for (int k = 0; k < kDiscLoads; ++k) {
         const int idx = min(lane + 64 * k, kDiscWords - 1), r = idx / 9, q = idx - r * 9;
-        vd[k] = disc_words ? *reinterpret_cast<const uint32_t*>(dsrc + (size_t)r * rp + 4 * q) : 0u;
+        vd[k] = *reinterpret_cast<const uint32_t*>(dsrc + (size_t)r * rp + 4 * q);
     }
 #pragma unroll
     for (int k = 0; k < kBlurLoads; ++k) {
@@ -165,32 +165,27 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, uint8_t* 
         const int idx = lane + 64 * k, r = idx / 10, q = idx - r * 10;
         if (idx < kBlurWords) *reinterpret_cast<uint32_t*>(s_blur + r * kBPitch + 4 * q) = vb[k];
     }
-    if (disc_words) {
-#pragma unroll
-        for (int k = 0; k < kDiscLoads; ++k) {
-            const int idx = lane + 64 * k, r = idx / 9, q = idx - r * 9;
-            if (idx < kDiscWords) *reinterpret_cast<uint32_t*>(s_disc + r * kDiscPitch + 4 * q) = vd[k];
-        }
-    } else {
-        for (int idx = lane; idx < 31 * 31; idx += 64) {
-            const int r = idx / 31, c = idx - r * 31;
-            s_disc[r * kDiscPitch + od + c] = raw[(size_t)(cy - 15 + r) * rp + cx - 15 + c];
-        }
-    }
-    // (blurred 37x37 neighbourhood: rBRIEF samples from cx-18 >= 1 always;
-    // the blur buffer is padded, so the 10-dword spans never leave it)
-    wave_sync();
 
-    // intensity centroid over the disc (integer moments: order-free)
+    // Intensity centroid (IC_Angle, ORBextractor.cpp:79-106) straight from
+    // the disc words: a word of row v = r - 15 covers window columns c =
+    // 4q..4q+3, i.e. u = c - od - 15; the bytes with |u| <= umax[|v|] are
+    // kept, and v_dot4_u32_u8 gives sum(p) and sum(c * p) of the word.
+    // Integer moments: order-free, so lane partial sums are exact.
     int m10 = 0, m01 = 0;
-    for (int idx = lane; idx < 31 * 31; idx += 64) {
-        const int v = idx / 31 - 15, u = idx % 31 - 15;
-        if (abs(u) <= c_umax[abs(v)]) {
-            const int p = s_disc[(15 + v) * kDiscPitch + od + 15 + u];
-            m10 += u * p;
-            m01 += v * p;
-        }
+#pragma unroll
+    for (int k = 0; k < kDiscLoads; ++k) {
+        const int idx = lane + 64 * k, r = idx / 9, q = idx - r * 9;
+        const int v = r - 15, d = c_umax[abs(v) & 15];
+        const int s0 = min(max(od + 15 - d - 4 * q, 0), 4), e0 = min(max(od + 16 + d - 4 * q, 0), 4);
+        const uint32_t mask = e0 > s0 ? (uint32_t)(((1ull << (8 * (e0 - s0))) - 1ull) << (8 * s0)) : 0u;
+        const uint32_t w = idx < kDiscWords ? vd[k] & mask : 0u;
+        const uint32_t cols = (uint32_t)(4 * q) * 0x01010101u + 0x03020100u;
+        const int sp = (int)__builtin_amdgcn_udot4(w, 0x01010101u, 0u, false);
+        const int cp = (int)__builtin_amdgcn_udot4(w, cols, 0u, false);
+        m10 += cp - (od + 15) * sp;
+        m01 += v * sp;
     }
+    wave_sync();
     m10 = wave_sum(m10);
     m01 = wave_sum(m01);
     const float angle = fast_atan2((float)m01, (float)m10);
@@ -244,14 +239,13 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
                                                                    orbgpu_keypoint* __restrict__ kps,
                                                                    uint8_t* __restrict__ desc,
                                                                    int* __restrict__ counts, int kp_cap) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_disc[kDescWaves][31 * kDiscPitch];
     __shared__ __attribute__((aligned(16))) uint8_t s_blur[kDescWaves][kBlur * kBPitch];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: metadata in SGPRs
     const int item = blockIdx.x * kDescWaves + wave;
     if (item >= items) return;
     const int f = item / g.slots_frame, slot = item - f * g.slots_frame;
-    describe_one(g, f, slot, lane, s_disc[wave], s_blur[wave], img0, row0, frame0, pyr, blur, oct_out, oct_count,
+    describe_one(g, f, slot, lane, s_blur[wave], img0, row0, frame0, pyr, blur, oct_out, oct_count,
                  kps, desc, counts, kp_cap);
 }
 
