@@ -49,6 +49,12 @@ __device__ inline bool has_run9(uint32_t m16) {
     return r != 0;
 }
 
+// acc = 2 * acc + (a < b): the compare's VCC lane bit is the carry-in of
+// v_addc (2 VALU per ring bit instead of compare, select, shift-or)
+__device__ __forceinline__ void shift_in_lt(uint32_t& acc, int a, int b) {
+    asm("v_cmp_lt_i32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
+}
+
 // arc strength: max over the 16 arcs of 9 of max(min d, -max d), d = v - ring
 __device__ inline int arc_strength(const int d[16]) {
     int mn2[16], mx2[16];
@@ -104,7 +110,8 @@ struct CellTiles {
 // Stages are separated by wave compaction so each runs on dense lanes:
 // compass pre-test on every pixel -> 16-pixel contiguity test on survivors
 // -> arc strength on corners.
-__device__ int fast_corners(const CellTiles& T, int P, int dw, int dh, int ox, int t, int lane) {
+template <int P>
+__device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, int lane) {
     // compass pre-test, row-major over the detection region: 32 lanes per
     // row when it fits (two rows per pass), else 64 (dw <= 64: host check).
     // The tests are lane masks (v_cmp -> SGPR) combined with scalar logic.
@@ -139,12 +146,12 @@ __device__ int fast_corners(const CellTiles& T, int P, int dw, int dh, int ox, i
             off = T.la[j];
             const uint8_t* p = T.win + off;
             const int v = p[0], lo = v - t, hi = v + t;
-            uint32_t dark = 0, bright = 0;
+            uint32_t dark = 0, bright = 0;  // ring bits, position 0 ends in bit 15 (runs are order-free)
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const int q = p[ring_dy[k] * P + ring_dx[k]];
-                dark |= (uint32_t)(q < lo) << k;
-                bright |= (uint32_t)(q > hi) << k;
+                shift_in_lt(dark, q, lo);
+                shift_in_lt(bright, hi, q);
             }
             corner = has_run9(dark) || has_run9(bright);
         }
@@ -173,7 +180,8 @@ __device__ int fast_corners(const CellTiles& T, int P, int dw, int dh, int ox, i
 
 // 3x3 strict NMS among the corners (cv::FAST: non-corners and pixels outside
 // the detection region count 0), emitted in lb order = row-major.
-__device__ int nms_emit(const CellTiles& T, int P, int nb, int ox, int t, int lane, int iniX, int iniY,
+template <int P>
+__device__ int nms_emit(const CellTiles& T, int nb, int ox, int t, int lane, int iniX, int iniY,
                         uint32_t* out, int cap, int* err) {
     const int t1 = t + 1;
     int total = 0;
@@ -212,6 +220,7 @@ __device__ int nms_emit(const CellTiles& T, int P, int nb, int ox, int t, int la
 constexpr int kCellWaves = 4;  // cells (one per wave) in flight per block
 constexpr int kStageLoads = 8;  // window dwords per lane in flight
 
+template <int P>
 __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int ncells_total,
                                                                      const uint8_t* __restrict__ img0, size_t row0,
                                                                      size_t frame0, const uint8_t* __restrict__ pyr,
@@ -219,7 +228,7 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
                                                                      int* __restrict__ cell_counts,
                                                                      int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int P = g.win_pitch, R = g.win_rows;
+    const int R = g.win_rows;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: metadata in SGPRs
     const size_t per_wave = ((size_t)2 * P * R + 4 * (size_t)g.det_max + 15) & ~(size_t)15;
@@ -288,9 +297,9 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     const int dw = maxX - iniX - 6, dh = wh - 6;
     int total = 0;
     if (dw > 0 && dh > 0) {
-        int nb = fast_corners(T, P, dw, dh, ox, g.ini_th, lane);
+        int nb = fast_corners<P>(T, dw, dh, ox, g.ini_th, lane);
         FAST_T(t3);
-        total = nms_emit(T, P, nb, ox, g.ini_th, lane, iniX, iniY, out, L.cell_cap, err);
+        total = nms_emit<P>(T, nb, ox, g.ini_th, lane, iniX, iniY, out, L.cell_cap, err);
         FAST_T(t4);
         FAST_ACC(0, t1 - t0);
         FAST_ACC(1, t2 - t1);
@@ -301,8 +310,8 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
             for (int j = lane; j < nb; j += 64) T.sc[T.lb[j]] = 0;
             wave_sync();
             FAST_T(t5);
-            nb = fast_corners(T, P, dw, dh, ox, g.min_th, lane);
-            total = nms_emit(T, P, nb, ox, g.min_th, lane, iniX, iniY, out, L.cell_cap, err);
+            nb = fast_corners<P>(T, dw, dh, ox, g.min_th, lane);
+            total = nms_emit<P>(T, nb, ox, g.min_th, lane, iniX, iniY, out, L.cell_cap, err);
             FAST_T(t6);
             FAST_ACC(5, t6 - t5);
             FAST_ACC(6, 1);
@@ -325,8 +334,22 @@ hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size
     const int items = g.total_cells * batch;
     const size_t per_wave = ((size_t)2 * g.win_pitch * g.win_rows + 4 * (size_t)g.det_max + 15) & ~(size_t)15;
     dim3 grid((items + kCellWaves - 1) / kCellWaves);
-    hipLaunchKernelGGL(fast_cells_kernel, grid, dim3(64 * kCellWaves), per_wave * kCellWaves, stream, g, items,
-                       img0, row0, frame0, pyr, cand, cell_counts, err);
+    const size_t lds = per_wave * kCellWaves;
+#define ORBGPU_FAST_CASE(PP)                                                                                        \
+    case PP:                                                                                                        \
+        hipLaunchKernelGGL(fast_cells_kernel<PP>, grid, dim3(64 * kCellWaves), lds, stream, g, items, img0, row0, \
+                           frame0, pyr, cand, cell_counts, err);                                                   \
+        break;
+    switch (g.win_pitch) {
+        ORBGPU_FAST_CASE(40)
+        ORBGPU_FAST_CASE(48)
+        ORBGPU_FAST_CASE(56)
+        ORBGPU_FAST_CASE(64)
+        ORBGPU_FAST_CASE(72)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef ORBGPU_FAST_CASE
     return hipGetLastError();
 }
 

@@ -461,11 +461,14 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     g.win_rows = 0;
     g.det_max = 0;
     for (int l = 0; l < L; ++l) {
-        if (g.lv[l].wcell > 64) return fail(ORBGPU_ERR_UNSUPPORTED, "FAST cell wider than 64 px");
+        if (g.lv[l].wcell > 63) return fail(ORBGPU_ERR_UNSUPPORTED, "FAST cell wider than 63 px");
         g.win_pitch = std::max(g.win_pitch, (int)round_up((size_t)g.lv[l].wcell + 9, 4));
         g.win_rows = std::max(g.win_rows, g.lv[l].hcell + 6);
         g.det_max = std::max(g.det_max, (int)round_up((size_t)g.lv[l].wcell * g.lv[l].hcell, 8));
     }
+    // fast.hip is instantiated for window pitches 40, 48, ..., 72 (compile-time
+    // ring offsets)
+    g.win_pitch = g.win_pitch <= 40 ? 40 : (int)round_up((size_t)g.win_pitch, 8);
     e->pyr_bytes = pyr_off;
     e->max_kps = out_off;
     e->ncap = (int)round_up((size_t)ncap, 16);

@@ -39,6 +39,24 @@ OP_KERNEL(k_cvtsdwa, "v_cvt_f32_u32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_
 OP_KERNEL(k_cvtpku8, "v_cvt_pk_u8_f32 %0, %1, 1, %0")
 OP_KERNEL(k_min3, "v_min3_i32 %0, %0, %1, %1")
 
+// scalar ALU: 8 independent 64-bit chains per wave
+__global__ __launch_bounds__(256) void k_salu(unsigned* out, unsigned seed, int iters) {
+    unsigned long long a = seed, b = seed * 3ull, c = seed * 5ull, d = seed * 7ull, e = seed * 9ull, f = seed * 11ull,
+                       g = seed * 13ull, h = seed * 15ull;
+    const unsigned long long k = seed | 0x0101010101010101ull;
+    for (int i = 0; i < iters; ++i) {
+        asm volatile("s_and_b64 %0, %0, %1" : "+s"(a) : "s"(k));
+        asm volatile("s_and_b64 %0, %0, %1" : "+s"(b) : "s"(k));
+        asm volatile("s_and_b64 %0, %0, %1" : "+s"(c) : "s"(k));
+        asm volatile("s_and_b64 %0, %0, %1" : "+s"(d) : "s"(k));
+        asm volatile("s_and_b64 %0, %0, %1" : "+s"(e) : "s"(k));
+        asm volatile("s_and_b64 %0, %0, %1" : "+s"(f) : "s"(k));
+        asm volatile("s_and_b64 %0, %0, %1" : "+s"(g) : "s"(k));
+        asm volatile("s_and_b64 %0, %0, %1" : "+s"(h) : "s"(k));
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = (unsigned)(a ^ b ^ c ^ d ^ e ^ f ^ g ^ h);
+}
+
 #define OP64_KERNEL(NAME, ASM)                                                                \
     __global__ __launch_bounds__(256) void NAME(unsigned* out, unsigned seed, int iters) {    \
         typedef float f2 __attribute__((ext_vector_type(2)));                                  \
@@ -73,7 +91,7 @@ int main() {
         {"v_mul_hi_u32_u24", k_mulhi24}, {"v_mul_u32_u24", k_mul24}, {"v_mul_lo_u32", k_mullo},
         {"v_lshrrev_b32_sdwa", k_sdwa}, {"v_add3_u32", k_add3}, {"v_fma_f32", k_fma}, {"v_mad_u32_u24", k_mad24},
         {"v_pk_mad_u16", k_pkmad16}, {"v_pk_add_u16", k_pkadd16}, {"v_cvt_f32_u32_sdwa", k_cvtsdwa},
-        {"v_cvt_pk_u8_f32", k_cvtpku8}, {"v_min3_i32", k_min3}, {"v_pk_fma_f32", k_pkfma}, {"v_pk_add_f32", k_pkaddf}};
+        {"v_cvt_pk_u8_f32", k_cvtpku8}, {"v_min3_i32", k_min3}, {"v_pk_fma_f32", k_pkfma}, {"v_pk_add_f32", k_pkaddf}, {"s_and_b64 (SALU)", k_salu}};
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
