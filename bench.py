@@ -149,12 +149,12 @@ def main():
     ex = orbgpu.Extractor(nfeatures=NF, width=W, height=H, max_batch=B)
     cap = ex.max_keypoints
     frames = synth.torch_stream(B, W, H, seed=rank_seed(rank), device=dev, pitch=pitch)
-    kps = torch.zeros((B, cap, 7), dtype=torch.float32, device=dev)
-    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
-    counts = torch.zeros(B, dtype=torch.int32, device=dev)
-    kps_prev = torch.zeros((1, cap, 7), dtype=torch.float32, device=dev)
-    desc_prev = torch.zeros((1, cap, 32), dtype=torch.uint8, device=dev)
-    count_prev = torch.zeros(1, dtype=torch.int32, device=dev)
+    # frame slots 0..B: slot 0 holds the previous step's last frame, slots
+    # 1..B this step's frames, so all B (t-1, t) pairs are one matcher launch
+    kps_all = torch.zeros((B + 1, cap, 7), dtype=torch.float32, device=dev)
+    desc_all = torch.zeros((B + 1, cap, 32), dtype=torch.uint8, device=dev)
+    counts_all = torch.zeros(B + 1, dtype=torch.int32, device=dev)
+    kps, desc, counts = kps_all[1:], desc_all[1:], counts_all[1:]
     m12 = torch.zeros((B, cap), dtype=torch.int32, device=dev)
     nmatch = torch.zeros(B, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -164,16 +164,13 @@ def main():
         ex.extract_batch(frames, kps, desc, counts, stream=stream, row_step=pitch, frame_step=pitch * H)
         if ev is not None:
             ev[0].record(stream)
-        orbgpu.search_for_initialization_batch(W, H, kps_prev, desc_prev, count_prev, kps[0:1], desc[0:1],
-                                               counts[0:1], m12[0:1], nmatch[0:1], flags=flags, stream=stream)
-        if B > 1:
-            orbgpu.search_for_initialization_batch(W, H, kps[:-1], desc[:-1], counts[:-1], kps[1:], desc[1:],
-                                                   counts[1:], m12[1:], nmatch[1:], flags=flags, stream=stream)
+        orbgpu.search_for_initialization_batch(W, H, kps_all[:-1], desc_all[:-1], counts_all[:-1], kps_all[1:],
+                                               desc_all[1:], counts_all[1:], m12, nmatch, flags=flags, stream=stream)
         if ev is not None:
             ev[1].record(stream)
-        kps_prev.copy_(kps[-1:])
-        desc_prev.copy_(desc[-1:])
-        count_prev.copy_(counts[-1:])
+        kps_all[0].copy_(kps_all[B])
+        desc_all[0].copy_(desc_all[B])
+        counts_all[0].copy_(counts_all[B])
 
     for _ in range(args.warmup):
         step()
