@@ -50,14 +50,31 @@ __device__ int level0_count(const orbgpu_keypoint* k, int n) {
     return lo;
 }
 
-__global__ __launch_bounds__(64) void match_init_kernel(float minX, float maxX, float minY, float maxY,
-                                                        const orbgpu_keypoint* __restrict__ kps1,
-                                                        const uint8_t* __restrict__ desc1, const int* __restrict__ n1p,
-                                                        size_t stride1, const orbgpu_keypoint* __restrict__ kps2,
-                                                        const uint8_t* __restrict__ desc2, const int* __restrict__ n2p,
-                                                        size_t stride2, float* __restrict__ prev_xy, int window,
-                                                        float nnratio, int flags, int* __restrict__ matches12,
-                                                        int* __restrict__ nmatches_out, int* __restrict__ err) {
+constexpr int kMatchThreads = 256;
+constexpr int kTopK = 4;  // best candidate keys kept per query by the parallel phase
+
+// (dist, grid order) of a candidate as one ordered key: dist <= 256 (9 bits),
+// cell = ix * 48 + iy < 3072 (12 bits), level-0 index < 512 (9 bits)
+__device__ inline uint32_t cand_key(int dist, int cell, int j) {
+    return ((uint32_t)dist << 21) | ((uint32_t)cell << 9) | (uint32_t)j;
+}
+
+// Two phases per frame pair (one 256-thread block):
+//  1 parallel, one thread per F1 query: scan the level-0 F2 keypoints (same
+//    j for every lane: LDS broadcasts), keep the kTopK smallest (dist, grid
+//    order) keys of the candidates in the query's window, and their count;
+//  2 sequential, wave 0: the reference's query loop (ORBmatcher.cpp:510-563)
+//    over those lists -- a candidate is skipped when vMatchedDistance[i2] <=
+//    dist (state of the loop so far); best = first kept key, bestDist2 = the
+//    next kept key's dist.  A list is exact while it holds all candidates or
+//    both values are found inside it; otherwise the query is re-scanned by
+//    the whole wave against the live state (rare).
+__global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
+    float minX, float maxX, float minY, float maxY, const orbgpu_keypoint* __restrict__ kps1,
+    const uint8_t* __restrict__ desc1, const int* __restrict__ n1p, size_t stride1,
+    const orbgpu_keypoint* __restrict__ kps2, const uint8_t* __restrict__ desc2, const int* __restrict__ n2p,
+    size_t stride2, float* __restrict__ prev_xy, int window, float nnratio, int flags, int* __restrict__ matches12,
+    int* __restrict__ nmatches_out, int* __restrict__ err) {
     __shared__ float s_x[kMaxK0], s_y[kMaxK0];
     __shared__ int s_cell[kMaxK0];           // grid cell ix*48+iy, or -1 when not in the grid
     __shared__ int s_mdist[kMaxK0];          // vMatchedDistance
@@ -65,10 +82,13 @@ __global__ __launch_bounds__(64) void match_init_kernel(float minX, float maxX, 
     __shared__ unsigned long long s_d2[kMaxK0][4];
     __shared__ int s_m12[kMaxK0];            // vnMatches12 for F1 level-0
     __shared__ float s_px[kMaxK0], s_py[kMaxK0], s_ang1[kMaxK0];  // F1: vbPrevMatched, angle
-    __shared__ unsigned long long s_d1[kMaxK0][4];
+    __shared__ uint32_t s_top[kMaxK0][kTopK];
+    __shared__ int s_ncand[kMaxK0];          // candidates in the window (-1: window off the grid)
     __shared__ signed char s_bin[kMaxK0];    // rotation bin pushed for i1, or -1
     __shared__ int s_hist[kHL];
-    const int lane = threadIdx.x;
+    __shared__ int s_nm;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.x;
     const orbgpu_keypoint* K1 = kps1 + (size_t)b * stride1;
     const orbgpu_keypoint* K2 = kps2 + (size_t)b * stride2;
@@ -79,14 +99,14 @@ __global__ __launch_bounds__(64) void match_init_kernel(float minX, float maxX, 
     float* prev = prev_xy ? prev_xy + (size_t)b * stride1 * 2 : nullptr;
     const int n10 = level0_count(K1, n1), n20 = level0_count(K2, n2);
     if (n10 > kMaxK0 || n20 > kMaxK0) {
-        if (lane == 0) { atomicOr(err, kErrMatchCap); nmatches_out[b] = 0; }
-        for (int i = lane; i < n1; i += 64) M12[i] = -1;
+        if (tid == 0) { atomicOr(err, kErrMatchCap); nmatches_out[b] = 0; }
+        for (int i = tid; i < n1; i += kMatchThreads) M12[i] = -1;
         return;
     }
     // grid inverses (Frame.cpp:221-224)
     const float invW = __fdiv_rn((float)kGC, __fsub_rn(maxX, minX));
     const float invH = __fdiv_rn((float)kGR, __fsub_rn(maxY, minY));
-    for (int j = lane; j < n20; j += 64) {
+    for (int j = tid; j < n20; j += kMatchThreads) {
         const float x = K2[j].x, y = K2[j].y;
         s_x[j] = x;
         s_y[j] = y;
@@ -99,73 +119,143 @@ __global__ __launch_bounds__(64) void match_init_kernel(float minX, float maxX, 
 #pragma unroll
         for (int q = 0; q < 4; ++q) s_d2[j][q] = d[q];
     }
-    for (int i = lane; i < n10; i += 64) {
+    for (int i = tid; i < n10; i += kMatchThreads) {
         s_m12[i] = -1;
         s_bin[i] = -1;
         s_px[i] = prev ? prev[2 * i] : K1[i].x;
         s_py[i] = prev ? prev[2 * i + 1] : K1[i].y;
         s_ang1[i] = K1[i].angle;
-        const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D1 + (size_t)i * 32);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) s_d1[i][q] = d[q];
     }
-    if (lane < kHL) s_hist[lane] = 0;
+    if (tid < kHL) s_hist[tid] = 0;
+    if (tid == 0) s_nm = 0;
     __syncthreads();
 
     const float r = (float)window;
-    const float factor = (flags & ORBGPU_MATCH_ANNOTATED_HISTO) ? __fdiv_rn(1.0f, (float)kHL) : __fdiv_rn((float)kHL, 360.0f);
-    int nmatches = 0;
-    for (int i1 = 0; i1 < n10; ++i1) {
-        const float x = s_px[i1];
-        const float y = s_py[i1];
-        const int cx0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, minX), r), invW)));
-        const int cx1 = min(kGC - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, minX), r), invW)));
-        const int cy0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, minY), r), invH)));
-        const int cy1 = min(kGR - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, minY), r), invH)));
-        if (cx0 >= kGC || cx1 < 0 || cy0 >= kGR || cy1 < 0) continue;
-        const unsigned long long q0 = s_d1[i1][0], q1 = s_d1[i1][1], q2 = s_d1[i1][2], q3 = s_d1[i1][3];
-        unsigned long long best = ~0ull;  // (dist << 32) | order key
-        int second = 0x7FFFFFFF;
-        for (int j = lane; j < n20; j += 64) {
-            const int cell = s_cell[j];
-            if (cell < 0) continue;
-            const int ix = cell / kGR, iy = cell - ix * kGR;
-            if (ix < cx0 || ix > cx1 || iy < cy0 || iy > cy1) continue;
-            if (!(fabsf(__fsub_rn(s_x[j], x)) < r && fabsf(__fsub_rn(s_y[j], y)) < r)) continue;
-            const int dist = __popcll(q0 ^ s_d2[j][0]) + __popcll(q1 ^ s_d2[j][1]) +
-                             __popcll(q2 ^ s_d2[j][2]) + __popcll(q3 ^ s_d2[j][3]);
-            if (s_mdist[j] <= dist) continue;
-            const unsigned long long key = ((unsigned long long)dist << 32) | ((unsigned)cell << 16) | (unsigned)j;
-            if (key < best) {
-                if (best != ~0ull) second = min(second, (int)(best >> 32));
-                best = key;
-            } else {
-                second = min(second, dist);
+    // GetFeaturesInArea's cell range (Frame.cpp:385-395) for a query at (x, y)
+    auto cell_range = [&](float x, float y, int& cx0, int& cx1, int& cy0, int& cy1) {
+        cx0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(x, minX), r), invW)));
+        cx1 = min(kGC - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(x, minX), r), invW)));
+        cy0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(y, minY), r), invH)));
+        cy1 = min(kGR - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(y, minY), r), invH)));
+        return !(cx0 >= kGC || cx1 < 0 || cy0 >= kGR || cy1 < 0);
+    };
+    auto in_window = [&](int j, float x, float y, int cx0, int cx1, int cy0, int cy1, int& cell) {
+        cell = s_cell[j];
+        if (cell < 0) return false;
+        const int ix = cell / kGR, iy = cell - ix * kGR;
+        if (ix < cx0 || ix > cx1 || iy < cy0 || iy > cy1) return false;
+        return fabsf(__fsub_rn(s_x[j], x)) < r && fabsf(__fsub_rn(s_y[j], y)) < r;
+    };
+
+    // phase 1: per-query candidate lists (no dependence on the match state)
+    for (int i1 = tid; i1 < n10; i1 += kMatchThreads) {
+        const float x = s_px[i1], y = s_py[i1];
+        int cx0, cx1, cy0, cy1;
+        int ncand = -1;
+        uint32_t top[kTopK];
+#pragma unroll
+        for (int k = 0; k < kTopK; ++k) top[k] = 0xFFFFFFFFu;
+        if (cell_range(x, y, cx0, cx1, cy0, cy1)) {
+            ncand = 0;
+            const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D1 + (size_t)i1 * 32);
+            const unsigned long long q0 = d[0], q1 = d[1], q2 = d[2], q3 = d[3];
+            for (int j = 0; j < n20; ++j) {
+                int cell;
+                if (!in_window(j, x, y, cx0, cx1, cy0, cy1, cell)) continue;
+                const int dist = __popcll(q0 ^ s_d2[j][0]) + __popcll(q1 ^ s_d2[j][1]) +
+                                 __popcll(q2 ^ s_d2[j][2]) + __popcll(q3 ^ s_d2[j][3]);
+                uint32_t key = cand_key(dist, cell, j);
+#pragma unroll
+                for (int k = 0; k < kTopK; ++k) {  // sorted insert
+                    const uint32_t lo = min(key, top[k]);
+                    key = max(key, top[k]);
+                    top[k] = lo;
+                }
+                ++ncand;
             }
         }
-        const unsigned long long wbest = wave_min_u64(best);
-        if (wbest == ~0ull) continue;  // no usable candidate
-        const int contrib = best == wbest ? second : (best == ~0ull ? 0x7FFFFFFF : (int)(best >> 32));
-        const int best2 = wave_min_i(contrib);
-        const int bestDist = (int)(wbest >> 32);
-        const int bidx = (int)(wbest & 0xFFFF);
-        if (bestDist <= kThLow && (float)bestDist < __fmul_rn((float)best2, nnratio)) {
-            if (lane == 0) {
-                const int prev21 = s_m21[bidx];
-                if (prev21 >= 0) s_m12[prev21] = -1;
-                s_m12[i1] = bidx;
-                s_m21[bidx] = i1;
-                s_mdist[bidx] = bestDist;
-                if (flags & ORBGPU_MATCH_CHECK_ORI) {
-                    float rot = __fsub_rn(s_ang1[i1], K2[bidx].angle);
-                    if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
-                    int bin = (int)roundf(__fmul_rn(rot, factor));
-                    if (bin == kHL) bin = 0;
-                    s_bin[i1] = (signed char)bin;
-                    s_hist[bin] += 1;
+#pragma unroll
+        for (int k = 0; k < kTopK; ++k) s_top[i1][k] = top[k];
+        s_ncand[i1] = ncand;
+    }
+    __syncthreads();
+
+    // phase 2: the sequential query loop (wave 0; wave-uniform control)
+    if (wave == 0) {
+        const float factor =
+            (flags & ORBGPU_MATCH_ANNOTATED_HISTO) ? __fdiv_rn(1.0f, (float)kHL) : __fdiv_rn((float)kHL, 360.0f);
+        for (int i1 = 0; i1 < n10; ++i1) {
+            const int ncand = s_ncand[i1];
+            if (ncand <= 0) continue;  // window off the grid, or no candidate in it
+            uint32_t best = 0xFFFFFFFFu;
+            int best2 = 0x7FFFFFFF;
+            bool have2 = false;
+            const int nk = min(ncand, kTopK);
+            for (int k = 0; k < nk; ++k) {
+                const uint32_t key = s_top[i1][k];
+                const int dist = (int)(key >> 21), j = (int)(key & 511u);
+                if (s_mdist[j] <= dist) continue;
+                if (best == 0xFFFFFFFFu) {
+                    best = key;
+                } else {
+                    best2 = dist;
+                    have2 = true;
+                    break;
                 }
             }
-            __syncthreads();
+            if (!have2 && ncand > kTopK) {
+                // the list ran out: exact re-scan against the live state
+                const float x = s_px[i1], y = s_py[i1];
+                int cx0, cx1, cy0, cy1;
+                cell_range(x, y, cx0, cx1, cy0, cy1);
+                const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D1 + (size_t)i1 * 32);
+                const unsigned long long q0 = d[0], q1 = d[1], q2 = d[2], q3 = d[3];
+                unsigned long long lbest = ~0ull;
+                int second = 0x7FFFFFFF;
+                for (int j = lane; j < n20; j += 64) {
+                    int cell;
+                    if (!in_window(j, x, y, cx0, cx1, cy0, cy1, cell)) continue;
+                    const int dist = __popcll(q0 ^ s_d2[j][0]) + __popcll(q1 ^ s_d2[j][1]) +
+                                     __popcll(q2 ^ s_d2[j][2]) + __popcll(q3 ^ s_d2[j][3]);
+                    if (s_mdist[j] <= dist) continue;
+                    const unsigned long long key = ((unsigned long long)dist << 32) | ((unsigned)cell << 16) | (unsigned)j;
+                    if (key < lbest) {
+                        if (lbest != ~0ull) second = min(second, (int)(lbest >> 32));
+                        lbest = key;
+                    } else {
+                        second = min(second, dist);
+                    }
+                }
+                const unsigned long long wbest = wave_min_u64(lbest);
+                const int contrib = lbest == wbest ? second : (lbest == ~0ull ? 0x7FFFFFFF : (int)(lbest >> 32));
+                best2 = wave_min_i(contrib);
+                best = wbest == ~0ull ? 0xFFFFFFFFu
+                                      : cand_key((int)(wbest >> 32), (int)((wbest >> 16) & 0xFFFF), (int)(wbest & 0xFFFF));
+            }
+            if (best == 0xFFFFFFFFu) continue;  // no usable candidate
+            const int bestDist = (int)(best >> 21);
+            const int bidx = (int)(best & 511u);
+            if (bestDist <= kThLow && (float)bestDist < __fmul_rn((float)best2, nnratio)) {
+                if (lane == 0) {
+                    const int prev21 = s_m21[bidx];
+                    if (prev21 >= 0) s_m12[prev21] = -1;
+                    s_m12[i1] = bidx;
+                    s_m21[bidx] = i1;
+                    s_mdist[bidx] = bestDist;
+                    if (flags & ORBGPU_MATCH_CHECK_ORI) {
+                        float rot = __fsub_rn(s_ang1[i1], K2[bidx].angle);
+                        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+                        int bin = (int)roundf(__fmul_rn(rot, factor));
+                        if (bin == kHL) bin = 0;
+                        s_bin[i1] = (signed char)bin;
+                        s_hist[bin] += 1;
+                    }
+                }
+                // wave-local LDS ordering for the next query's reads
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
         }
     }
     __syncthreads();
@@ -180,13 +270,14 @@ __global__ __launch_bounds__(64) void match_init_kernel(float minX, float maxX, 
         }
         if ((float)max2 < __fmul_rn(0.1f, (float)max1)) { ind2 = -1; ind3 = -1; }
         else if ((float)max3 < __fmul_rn(0.1f, (float)max1)) ind3 = -1;
-        for (int i = lane; i < n10; i += 64) {
+        for (int i = tid; i < n10; i += kMatchThreads) {
             const int bin = s_bin[i];
             if (bin >= 0 && bin != ind1 && bin != ind2 && bin != ind3) s_m12[i] = -1;
         }
         __syncthreads();
     }
-    for (int i = lane; i < n1; i += 64) {
+    int nmatches = 0;
+    for (int i = tid; i < n1; i += kMatchThreads) {
         const int m = i < n10 ? s_m12[i] : -1;
         M12[i] = m;
         if (m >= 0) {
@@ -196,7 +287,9 @@ __global__ __launch_bounds__(64) void match_init_kernel(float minX, float maxX, 
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) nmatches += __shfl_xor(nmatches, o, 64);
-    if (lane == 0) nmatches_out[b] = nmatches;
+    if (lane == 0) atomicAdd(&s_nm, nmatches);
+    __syncthreads();
+    if (tid == 0) nmatches_out[b] = s_nm;
 }
 
 __global__ __launch_bounds__(256) void hamming_pairs_kernel(const uint8_t* __restrict__ a,
@@ -222,7 +315,8 @@ hipError_t launch_match_init(int batch, float minX, float maxX, float minY, floa
                              const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2, size_t stride2,
                              float* prev_xy, int window, float nnratio, int flags,
                              int* matches12, int* nmatches, int* err, hipStream_t stream) {
-    hipLaunchKernelGGL(match_init_kernel, dim3(batch), dim3(64), 0, stream, minX, maxX, minY, maxY, kps1, desc1, n1, stride1,
+    hipLaunchKernelGGL(match_init_kernel, dim3(batch), dim3(kMatchThreads), 0, stream, minX, maxX, minY, maxY, kps1,
+                       desc1, n1, stride1,
                        kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags, matches12, nmatches, err);
     return hipGetLastError();
 }

@@ -138,6 +138,45 @@ def test_search_for_initialization(mono_frames, check_ori, annotated):
     np.testing.assert_array_equal(p_g.view(np.uint32), p_r.view(np.uint32))
 
 
+def _conflict_frames(seed, n=420, protos=24, flips=3):
+    """Level-0 keypoints whose descriptors are noisy copies of a few
+    prototypes: most queries see many candidates at equal or near distances,
+    so matches are stolen and candidates skipped (vMatchedDistance) -- the
+    paths where the GPU's per-query top-k list runs out and re-scans."""
+    import orbgpu
+    rng = np.random.default_rng(seed)
+    P = rng.integers(0, 256, (protos, 32), dtype=np.uint8)
+
+    def frame():
+        k = np.zeros(n, orbgpu.KP_DTYPE)
+        k["x"] = rng.uniform(20, 620, n).astype(np.float32)
+        k["y"] = rng.uniform(20, 460, n).astype(np.float32)
+        k["size"] = 31.0
+        k["angle"] = rng.uniform(0, 360, n).astype(np.float32)
+        k["octave"] = 0
+        k["class_id"] = -1
+        d = P[rng.integers(0, protos, n)].copy()
+        for i in range(n):
+            for _ in range(int(rng.integers(0, flips + 1))):
+                b = int(rng.integers(0, 256))
+                d[i, b >> 3] ^= np.uint8(1 << (b & 7))
+        return k, d
+    return frame() + frame()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("check_ori", [True, False])
+def test_search_for_initialization_conflicts(seed, check_ori):
+    og = _gpu()
+    k1, d1, k2, d2 = _conflict_frames(seed)
+    n_r, m_r, p_r = orbref.search_for_initialization(k1, d1, k2, d2, 640, 480, check_ori=check_ori)
+    n_g, m_g, p_g = og.search_for_initialization(k1, d1, k2, d2, 640, 480, check_ori=check_ori)
+    assert n_r > 20
+    assert n_g == n_r
+    np.testing.assert_array_equal(m_g, m_r)
+    np.testing.assert_array_equal(p_g.view(np.uint32), p_r.view(np.uint32))
+
+
 def test_search_for_initialization_distorted_bounds(mono_frames):
     """Undistorted keypoints (mvKeysUn) with Frame bounds other than
     [0,W]x[0,H]: some keypoints fall outside the grid (PosInGrid rejects
