@@ -17,7 +17,9 @@ namespace {
 
 constexpr int kStrip = kBlurStrip;
 
-// BORDER_REFLECT_101 for an overshoot of at most n - 1 (here <= 6 < n)
+// BORDER_REFLECT_101 for an overshoot of at most n - 1 (<= 6 for the filter
+// taps; the interior strip's unused prefetches go up to 9 rows past a strip
+// and are clamped after reflection)
 __device__ inline int reflect101(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -56,12 +58,127 @@ __device__ __forceinline__ uint32_t to_u8(float v) {
     return (uint32_t)fminf(__builtin_floorf(v + 0.5f), 255.f);  // v + 0.5 exact (< 2^8, 16 frac bits)
 }
 
+// 8-bit packing of 4 filtered columns; v_cvt_pk_u8_f32 rounds to nearest
+// even and saturates (the vector path), to_u8 rounds half up (the tail).
+__device__ __forceinline__ uint32_t pack4(f32x2 lo, f32x2 hi, bool simd) {
+    if (simd) {
+        uint32_t packed = __builtin_amdgcn_cvt_pk_u8_f32(lo.x, 0, 0u);
+        packed = __builtin_amdgcn_cvt_pk_u8_f32(lo.y, 1, packed);
+        packed = __builtin_amdgcn_cvt_pk_u8_f32(hi.x, 2, packed);
+        return __builtin_amdgcn_cvt_pk_u8_f32(hi.y, 3, packed);
+    }
+    return to_u8(lo.x) | (to_u8(lo.y) << 8) | (to_u8(hi.x) << 16) | (to_u8(hi.y) << 24);
+}
+
+#ifndef BLUR_PROBE
+#define BLUR_PROBE 0  // diagnostic builds only: bit 0 = no stores in interior strips
+#endif
+
+struct Raw3 {
+    uint32_t a, b, c;  // level columns x0-4 .. x0+7
+};
+
+__device__ __forceinline__ void row_pass_raw(const Raw3& R, f32x2& lo, f32x2& hi) {
+    uint32_t P[9];
+    // bytes of (b:a) / (c:b) as v_perm_b32 sees them: low word 0-3, high word 4-7
+    P[0] = __builtin_amdgcn_perm(R.b, R.a, 0x0c020c01u);
+    P[1] = __builtin_amdgcn_perm(R.b, R.a, 0x0c030c02u);
+    P[2] = __builtin_amdgcn_perm(R.b, R.a, 0x0c040c03u);
+    P[3] = __builtin_amdgcn_perm(R.b, R.a, 0x0c050c04u);
+    P[4] = __builtin_amdgcn_perm(R.c, R.b, 0x0c020c01u);
+    P[5] = __builtin_amdgcn_perm(R.c, R.b, 0x0c030c02u);
+    P[6] = __builtin_amdgcn_perm(R.c, R.b, 0x0c040c03u);
+    P[7] = __builtin_amdgcn_perm(R.c, R.b, 0x0c050c04u);
+    P[8] = __builtin_amdgcn_perm(R.c, R.b, 0x0c060c05u);
+    row_pass(P, lo, hi);
+}
+
+// Interior strip (columns x0-3 .. x0+6 need no reflection): rows [y0, y1)
+// in groups of 7.  Row slot u of a group is consumed and immediately
+// refilled with the row 7 ahead, so 7 rows of loads are in flight and the
+// slots never move between registers (no copy waits on a pending load).
+// Rows past the level reflect (BORDER_REFLECT_101); prefetches past what the
+// strip needs are clamped to the last row and unused.
+__device__ __forceinline__ void blur_strip_interior(const uint8_t* __restrict__ src, uint32_t sp, int H, int x0,
+                                                    int y0, int y1, bool simd, uint8_t* __restrict__ dst,
+                                                    uint32_t dp) {
+    const uint8_t* base = src + x0;
+    auto fetch = [&](int yy) {
+        const int r = min(reflect101(yy, H), H - 1);
+        const uint8_t* row = base + __umul24((uint32_t)r, sp);
+        Raw3 R;
+#if BLUR_PROBE & 2
+        R.a = (uint32_t)(uintptr_t)row * 0x9E3779B1u;  // timing probe: no loads
+        R.b = R.a ^ 0x5bd1e995u;
+        R.c = R.a + 0x1b873593u;
+#else
+        R.a = *reinterpret_cast<const uint32_t*>(row - 4);
+        R.b = *reinterpret_cast<const uint32_t*>(row);
+        R.c = *reinterpret_cast<const uint32_t*>(row + 4);
+#endif
+        return R;
+    };
+    f32x2 wl[7], wh[7];  // row-pass window: slot (y - y0 + i) % 7 holds row y - 3 + i
+#pragma unroll
+    for (int i = 0; i < 6; ++i) row_pass_raw(fetch(y0 - 3 + i), wl[i], wh[i]);
+    Raw3 raw[7];  // raw[u] = row y + u + 3 of the current group
+#pragma unroll
+    for (int u = 0; u < 7; ++u) raw[u] = fetch(y0 + 3 + u);
+    for (int y = y0; y < y1; y += 7) {
+#pragma unroll
+        for (int u = 0; u < 7; ++u) {
+            row_pass_raw(raw[u], wl[(u + 6) % 7], wh[(u + 6) % 7]);
+            raw[u] = fetch(y + u + 10);
+            const f32x2 lo = col_pass(wl[u % 7], wl[(u + 1) % 7], wl[(u + 2) % 7], wl[(u + 3) % 7], wl[(u + 4) % 7],
+                                      wl[(u + 5) % 7], wl[(u + 6) % 7]);
+            const f32x2 hi = col_pass(wh[u % 7], wh[(u + 1) % 7], wh[(u + 2) % 7], wh[(u + 3) % 7], wh[(u + 4) % 7],
+                                      wh[(u + 5) % 7], wh[(u + 6) % 7]);
+#if BLUR_PROBE & 1
+            if (y + u < y1 && pack4(lo, hi, simd) == 0x12345678u) *reinterpret_cast<uint32_t*>(dst) = 0;  // timing probe: no stores
+#else
+            if (y + u < y1) *reinterpret_cast<uint32_t*>(dst + __umul24((uint32_t)(y + u), dp) + x0) = pack4(lo, hi, simd);
+#endif
+        }
+    }
+}
+
+// Edge strip (some of columns x0-3 .. x0+6 reflect): byte loads.
+__device__ __noinline__ void blur_strip_edge(const uint8_t* __restrict__ src, uint32_t sp, int W, int H, int x0, int y0,
+                                             int y1, bool simd, uint8_t* __restrict__ dst, uint32_t dp) {
+    auto filter_row = [&](int yy, f32x2& lo, f32x2& hi) {
+        const uint8_t* row = src + __umul24((uint32_t)reflect101(yy, H), sp);
+        int px[10];
+#pragma unroll
+        for (int j = 0; j < 10; ++j) px[j] = row[reflect101(x0 - 3 + j, W)];
+        uint32_t P[9];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) P[j] = (uint32_t)px[j] | ((uint32_t)px[j + 1] << 16);
+        row_pass(P, lo, hi);
+    };
+    f32x2 wl[7], wh[7];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) filter_row(y0 - 3 + i, wl[i], wh[i]);
+    for (int y = y0; y < y1; y += 7) {
+#pragma unroll
+        for (int u = 0; u < 7; ++u) {
+            filter_row(y + u + 3, wl[(u + 6) % 7], wh[(u + 6) % 7]);
+            const f32x2 lo = col_pass(wl[u % 7], wl[(u + 1) % 7], wl[(u + 2) % 7], wl[(u + 3) % 7], wl[(u + 4) % 7],
+                                      wl[(u + 5) % 7], wl[(u + 6) % 7]);
+            const f32x2 hi = col_pass(wh[u % 7], wh[(u + 1) % 7], wh[(u + 2) % 7], wh[(u + 3) % 7], wh[(u + 4) % 7],
+                                      wh[(u + 5) % 7], wh[(u + 6) % 7]);
+            if (y + u < y1) *reinterpret_cast<uint32_t*>(dst + __umul24((uint32_t)(y + u), dp) + x0) = pack4(lo, hi, simd);
+        }
+    }
+}
+
 // One thread = 4 adjacent output columns x a 63-row strip of one level.
 // Walking down the strip it keeps the last 7 row-pass results (as floats)
 // in registers -- the window rotates statically (the row loop is unrolled
-// by 7) -- so every input row is read once per strip (+6 halo rows) with
-// three aligned dword loads.
-__global__ __launch_bounds__(256) void blur_levels_kernel(Geom g, int items_frame, int items_total,
+// by 7) -- so every input row is read once per strip (+6 halo rows).
+#ifndef BLUR_WAVES_PER_EU
+#define BLUR_WAVES_PER_EU 1
+#endif
+__global__ __launch_bounds__(256, BLUR_WAVES_PER_EU) void blur_levels_kernel(Geom g, int items_frame, int items_total,
                                                           const uint8_t* __restrict__ img0, size_t row0,
                                                           size_t frame0, const uint8_t* __restrict__ pyr,
                                                           uint8_t* __restrict__ blur) {
@@ -79,64 +196,11 @@ __global__ __launch_bounds__(256) void blur_levels_kernel(Geom g, int items_fram
     const uint8_t* src = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
     const size_t sp = l == 0 ? row0 : (size_t)L.pitch;
     uint8_t* dst = blur + L.blur_offset + (size_t)f * L.blur_frame_bytes;
-    const bool interior = x0 >= 4 && x0 + 7 < L.w;  // columns x0-3 .. x0+6 need no reflection
-    const bool simd = x0 < (L.w & ~3);              // all 4 columns on the vector path, else all on the tail
-    const int W = L.w, H = L.h;
-
-    auto load_row = [&](int yy, f32x2& lo, f32x2& hi) {
-        const uint8_t* row = src + (size_t)reflect101(yy, H) * sp;
-        uint32_t P[9];
-        if (interior) {
-            const uint32_t a = *reinterpret_cast<const uint32_t*>(row + x0 - 4);
-            const uint32_t b = *reinterpret_cast<const uint32_t*>(row + x0);
-            const uint32_t c = *reinterpret_cast<const uint32_t*>(row + x0 + 4);
-            // bytes of (b:a) / (c:b) as v_perm_b32 sees them: low word 0-3, high word 4-7
-            P[0] = __builtin_amdgcn_perm(b, a, 0x0c020c01u);
-            P[1] = __builtin_amdgcn_perm(b, a, 0x0c030c02u);
-            P[2] = __builtin_amdgcn_perm(b, a, 0x0c040c03u);
-            P[3] = __builtin_amdgcn_perm(b, a, 0x0c050c04u);
-            P[4] = __builtin_amdgcn_perm(c, b, 0x0c020c01u);
-            P[5] = __builtin_amdgcn_perm(c, b, 0x0c030c02u);
-            P[6] = __builtin_amdgcn_perm(c, b, 0x0c040c03u);
-            P[7] = __builtin_amdgcn_perm(c, b, 0x0c050c04u);
-            P[8] = __builtin_amdgcn_perm(c, b, 0x0c060c05u);
-        } else {
-            int px[10];
-#pragma unroll
-            for (int j = 0; j < 10; ++j) px[j] = row[reflect101(x0 - 3 + j, W)];
-#pragma unroll
-            for (int j = 0; j < 9; ++j) P[j] = (uint32_t)px[j] | ((uint32_t)px[j + 1] << 16);
-        }
-        row_pass(P, lo, hi);
-    };
-    auto store_row = [&](int y, f32x2 lo, f32x2 hi) {
-        uint32_t packed;
-        if (simd) {  // v_cvt_pk_u8_f32: round to nearest even, saturate, pack
-            packed = __builtin_amdgcn_cvt_pk_u8_f32(lo.x, 0, 0u);
-            packed = __builtin_amdgcn_cvt_pk_u8_f32(lo.y, 1, packed);
-            packed = __builtin_amdgcn_cvt_pk_u8_f32(hi.x, 2, packed);
-            packed = __builtin_amdgcn_cvt_pk_u8_f32(hi.y, 3, packed);
-        } else {
-            packed = to_u8(lo.x) | (to_u8(lo.y) << 8) | (to_u8(hi.x) << 16) | (to_u8(hi.y) << 24);
-        }
-        *reinterpret_cast<uint32_t*>(dst + (size_t)y * L.pitch + x0) = packed;  // x0+3 < pitch
-    };
-
-    f32x2 wl[7], wh[7];  // row-pass window: slot (y - y0 + i) % 7 holds row y - 3 + i
-#pragma unroll
-    for (int i = 0; i < 6; ++i) load_row(y0 - 3 + i, wl[i], wh[i]);
-    for (int y = y0; y < y1; y += 7) {
-#pragma unroll
-        for (int u = 0; u < 7; ++u) {
-            if (y + u >= y1) break;
-            load_row(y + u + 3, wl[(u + 6) % 7], wh[(u + 6) % 7]);
-            const f32x2 lo = col_pass(wl[u % 7], wl[(u + 1) % 7], wl[(u + 2) % 7], wl[(u + 3) % 7], wl[(u + 4) % 7],
-                                      wl[(u + 5) % 7], wl[(u + 6) % 7]);
-            const f32x2 hi = col_pass(wh[u % 7], wh[(u + 1) % 7], wh[(u + 2) % 7], wh[(u + 3) % 7], wh[(u + 4) % 7],
-                                      wh[(u + 5) % 7], wh[(u + 6) % 7]);
-            store_row(y + u, lo, hi);
-        }
-    }
+    const bool simd = x0 < (L.w & ~3);  // all 4 columns on the vector path, else all on the tail
+    if (x0 >= 4 && x0 + 7 < L.w)
+        blur_strip_interior(src, (uint32_t)sp, L.h, x0, y0, y1, simd, dst, (uint32_t)L.pitch);
+    else
+        blur_strip_edge(src, (uint32_t)sp, L.w, L.h, x0, y0, y1, simd, dst, (uint32_t)L.pitch);
 }
 
 }  // namespace

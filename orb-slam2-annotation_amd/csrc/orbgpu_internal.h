@@ -13,7 +13,10 @@ namespace orbgpu {
 constexpr int kMaxLevels = 16;
 constexpr int kEdge = 19;              // EDGE_THRESHOLD (ORBextractor.cpp:76)
 constexpr int kBorder = kEdge - 3;     // minBorderX/Y (ORBextractor.cpp:781)
-constexpr int kBlurStrip = 63;  // blur.hip: output rows per thread (a multiple of its 7-row window rotation)
+#ifndef ORBGPU_BLUR_STRIP
+#define ORBGPU_BLUR_STRIP 63
+#endif
+constexpr int kBlurStrip = ORBGPU_BLUR_STRIP;  // blur.hip: output rows per thread (a multiple of its 7-row window rotation)
 constexpr int kMaxWin = 72;            // FAST cell window <= (wCell+6) x (hCell+6)
 constexpr int kPatchR = 21;            // raw patch radius for blur+rBRIEF
 constexpr int kPatch = 2 * kPatchR + 1;  // 43

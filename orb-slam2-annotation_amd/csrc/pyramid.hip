@@ -103,45 +103,51 @@ __device__ __forceinline__ void put_byte_shr2(uint32_t& out, uint32_t s) {
 // of 16); its threads get a wave of their own (quad_taps).
 // The source bytes one output row of a quad needs: rows y0 (a) and y1 (b),
 // one dword pair per row (WIN) or per pixel.
-template <bool WIN>
-struct RowWords {
-    uint32_t a[WIN ? 2 : 8], b[WIN ? 2 : 8];
+// Horizontal pass of one source row for the quad: h[k] = the exact Q11 sum
+// of pixel k's two taps (HResizeLinear), from the row at LDS offset `row`.
+struct H4 {
+    uint32_t h[4];
 };
 
 template <bool WIN>
-__device__ __forceinline__ RowWords<WIN> load_row(const uint8_t* const (&col)[4], int4 yr) {
-    RowWords<WIN> d;
+__device__ __forceinline__ H4 hrow(const uint8_t* const (&col)[4], const uint32_t (&wt)[4], const uint32_t (&sel)[4],
+                                   int row) {
+    H4 r;
+    uint32_t w[WIN ? 2 : 8];
 #pragma unroll
     for (int k = 0; k < (WIN ? 1 : 4); ++k) {
-        const uint32_t* a = reinterpret_cast<const uint32_t*>(col[k] + yr.x);
-        const uint32_t* b = reinterpret_cast<const uint32_t*>(col[k] + yr.y);
-        d.a[2 * k] = a[0];
-        d.a[2 * k + 1] = a[1];
-        d.b[2 * k] = b[0];
-        d.b[2 * k + 1] = b[1];
+        const uint32_t* a = reinterpret_cast<const uint32_t*>(col[k] + row);
+        w[2 * k] = a[0];
+        w[2 * k + 1] = a[1];
     }
-    return d;
-}
-
-template <bool TAIL, bool WIN>
-__device__ __forceinline__ uint32_t quad_row(const RowWords<WIN>& d, const uint32_t (&wt)[4],
-                                             const uint32_t (&sel)[4], int4 yr) {
-    uint32_t h0[4], h1[4];
+#if PYR_PROBE & 16
+    // timing probe: half the horizontal work (pixels 2, 3 reuse 0, 1)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+#else
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
+#endif
         const int j = WIN ? 0 : 2 * k;
-        const uint32_t p0 = __builtin_amdgcn_perm(d.a[j + 1], d.a[j], sel[k]);
-        const uint32_t p1 = __builtin_amdgcn_perm(d.b[j + 1], d.b[j], sel[k]);
-        h0[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p0), __builtin_bit_cast(us2, wt[k]), 0u, false);
-        h1[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p1), __builtin_bit_cast(us2, wt[k]), 0u, false);
+        const uint32_t p = __builtin_amdgcn_perm(w[j + 1], w[j], sel[k]);
+        r.h[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p), __builtin_bit_cast(us2, wt[k]), 0u, false);
     }
+#if PYR_PROBE & 16
+    r.h[2] = r.h[0] ^ 1; r.h[3] = r.h[1] ^ 1;
+#endif
+    return r;
+}
+
+// Vertical pass of one output quad from its two source rows' sums.
+template <bool TAIL>
+__device__ __forceinline__ uint32_t vert(const H4& h0, const H4& h1, int4 yr) {
     uint32_t out;
     if (!TAIL) {
         const uint32_t B0 = (uint32_t)yr.z & 0xFFFFFFu, B1 = (uint32_t)yr.w & 0xFFFFFFu;
         uint32_t sum[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            sum[k] = mulhi24(h0[k] & 0xFFFFF0u, B0) + mulhi24(h1[k] & 0xFFFFF0u, B1) + 2u;
+            sum[k] = mulhi24(h0.h[k] & 0xFFFFF0u, B0) + mulhi24(h1.h[k] & 0xFFFFF0u, B1) + 2u;
         out = sum[0] >> 2;
         put_byte_shr2<1>(out, sum[1]);
         put_byte_shr2<2>(out, sum[2]);
@@ -150,7 +156,8 @@ __device__ __forceinline__ uint32_t quad_row(const RowWords<WIN>& d, const uint3
         const uint32_t b0 = (uint32_t)yr.z >> 12, b1 = (uint32_t)yr.w >> 12;
         out = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) out |= ((__umul24(h0[k], b0) + __umul24(h1[k], b1) + (1u << 21)) >> 22) << (8 * k);
+        for (int k = 0; k < 4; ++k)
+            out |= ((__umul24(h0.h[k], b0) + __umul24(h1.h[k], b1) + (1u << 21)) >> 22) << (8 * k);
     }
     return out;
 }
@@ -211,31 +218,34 @@ __device__ __forceinline__ void resize_rows(const uint8_t* __restrict__ lds, con
         wt[0] = ta.y; wt[1] = ta.w; wt[2] = tb.y; wt[3] = tb.w;
         sel[0] = tc.x; sel[1] = tc.y; sel[2] = tc.z; sel[3] = tc.w;
     }
-    // software-pipelined over the thread's rows: the next row's record and
-    // source words and the record after it are read while this row computes
-    // (reads past r1 are clamped to the last row: harmless)
-    int r = r0 + tp.rg;
-    if (r >= r1) return;
-    const int step = TAIL ? 64 : V.rgroups;
-    int4 yc = s_rows[r - r0];
-    int rn = r + step;
-    int4 yn = s_rows[min(rn, r1 - 1) - r0];
-    RowWords<WIN> dc = load_row<WIN>(col, yc);
-    for (;;) {
-        const int rnn = rn + step;
-        const int4 ynn = s_rows[min(rnn, r1 - 1) - r0];
-        const RowWords<WIN> dn = load_row<WIN>(col, yn);
-        const uint32_t out = quad_row<TAIL, WIN>(dc, wt, sel, yc);
+    auto store = [&](int r, uint32_t out) {
         // bytes past V.w land in the row padding (LDS pitch and HBM pitch are
         // multiples of 4 and 16)
         if (lds_dst) *reinterpret_cast<uint32_t*>(lds_dst + (uint32_t)((r - r0) * V.lds_pitch + 4 * q)) = out;
         if (r >= own0 && r < own1) *reinterpret_cast<uint32_t*>(hbm_dst + (uint32_t)(r * V.pitch + 4 * q)) = out;
-        if (rn >= r1) break;
-        r = rn;
-        rn = rnn;
-        yc = yn;
-        yn = ynn;
-        dc = dn;
+    };
+    if (TAIL) {  // one row per lane (tail wave)
+        for (int r = r0 + tp.rg; r < r1; r += 64) {
+            const int4 y = s_rows[r - r0];
+            store(r, vert<true>(hrow<WIN>(col, wt, sel, y.x), hrow<WIN>(col, wt, sel, y.y), y));
+        }
+        return;
+    }
+    // Row groups own pairs of consecutive output rows: (r, r+1) read source
+    // rows (y0, y0+1) and (y0', y0'+1) with y0' = y0 + 1 for most pairs of a
+    // ~1.2x downscale, so the shared source row's horizontal sums are
+    // computed once (3 source rows per 2 output rows instead of 4).
+    for (int r = r0 + 2 * tp.rg; r < r1; r += 2 * V.rgroups) {
+        const bool two = r + 1 < r1;
+        const int4 ya = s_rows[r - r0];
+        const int4 yb = s_rows[(two ? r + 1 : r) - r0];
+        const H4 hA = hrow<WIN>(col, wt, sel, ya.x);
+        const H4 hB = hrow<WIN>(col, wt, sel, ya.y);
+        H4 hC, hD;
+        if (yb.x == ya.y) hC = hB; else hC = hrow<WIN>(col, wt, sel, yb.x);
+        if (yb.y == ya.y) hD = hB; else hD = hrow<WIN>(col, wt, sel, yb.y);
+        store(r, vert<false>(hA, hB, ya));
+        if (two) store(r + 1, vert<false>(hC, hD, yb));
     }
 }
 
