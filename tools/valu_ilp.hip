@@ -40,6 +40,29 @@ __global__ __launch_bounds__(64) void k_pkfma(unsigned* out, unsigned seed, int 
     out[blockIdx.x * 64 + threadIdx.x] = (unsigned)x;
 }
 
+#define OPK(NAME, ASM)                                                                       \
+    __global__ __launch_bounds__(64) void NAME(unsigned* out, unsigned seed, int iters) {     \
+        unsigned v0 = seed ^ threadIdx.x, v1 = v0 * 3, v2 = v0 * 5, v3 = v0 * 7;                \
+        for (int i = 0; i < iters; ++i) {                                                      \
+            _Pragma("unroll") for (int r = 0; r < 8; ++r) {                                    \
+                asm volatile(ASM : "+v"(v0) : "v"(seed));                                      \
+                asm volatile(ASM : "+v"(v1) : "v"(seed));                                      \
+                asm volatile(ASM : "+v"(v2) : "v"(seed));                                      \
+                asm volatile(ASM : "+v"(v3) : "v"(seed));                                      \
+            }                                                                                  \
+        }                                                                                      \
+        out[blockIdx.x * 64 + threadIdx.x] = v0 ^ v1 ^ v2 ^ v3;                                \
+    }
+OPK(k_cmpsel, "v_cmp_lt_i32_e32 vcc, %0, %1\n\tv_cndmask_b32_e32 %0, %0, %1, vcc")
+OPK(k_min, "v_min_i32_e32 %0, %0, %1")
+OPK(k_max3, "v_max3_i32 %0, %0, %1, %1")
+OPK(k_lshl, "v_lshlrev_b32_e32 %0, 1, %0")
+OPK(k_lshladd, "v_lshl_add_u32 %0, %0, 1, %1")
+OPK(k_bfe, "v_bfe_u32 %0, %0, 3, 5")
+OPK(k_cmpaddc, "v_cmp_lt_i32_e32 vcc, %0, %1\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc")
+OPK(k_sub, "v_sub_u32_e32 %0, %0, %1")
+OPK(k_alignbyte, "v_alignbyte_b32 %0, %0, %1, 1")
+
 template <class F>
 void run(const char* name, F f, int ch, int wps, int cus, unsigned* out) {
     const int iters = 2048;
@@ -63,6 +86,13 @@ int main() {
     int cus = 256;
     unsigned* out;
     (void)hipMalloc(&out, (size_t)cus * 4 * 8 * 64 * 4);
+    {
+        const char* names[] = {"cmp+cndmask(x2)", "v_min_i32", "v_max3_i32", "v_lshlrev", "v_lshl_add", "v_bfe_u32",
+                               "cmp+addc(x2)", "v_sub_u32", "v_alignbyte"};
+        void (*fs[])(unsigned*, unsigned, int) = {k_cmpsel, k_min, k_max3, k_lshl, k_lshladd, k_bfe, k_cmpaddc, k_sub,
+                                                  k_alignbyte};
+        for (int i = 0; i < 9; ++i) run(names[i], fs[i], 4, 8, cus, out);
+    }
     for (int w : {1, 2, 4, 8}) {
         run("v_add_u32", k_add<1>, 1, w, cus, out);
         run("v_add_u32", k_add<2>, 2, w, cus, out);
