@@ -17,7 +17,7 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent))
 from pmc_summary import load  # noqa: E402
 
-KERNEL = "pyramid_kernel"
+KERNEL = "pyramid_kernel"  # matched as a prefix: the kernel is a template (pyramid_kernel<WIN>)
 
 
 def main():
@@ -31,8 +31,10 @@ def main():
     a = ap.parse_args()
     f = load(a.fetch_csv)
     w = load(a.write_csv)
-    fetch_kib = f[KERNEL]["FETCH_SIZE"]
-    write_kib = w[KERNEL]["WRITE_SIZE"]
+    kf = next(k for k in f if k.startswith(KERNEL))
+    kw = next(k for k in w if k.startswith(KERNEL))
+    fetch_kib = f[kf]["FETCH_SIZE"]
+    write_kib = w[kw]["WRITE_SIZE"]
     read_b = 2.0 * fetch_kib * 1024.0
     write_b = write_kib * 1024.0
     out = {
