@@ -131,6 +131,8 @@ struct orbgpu_extractor {
     int4* d_ptab = nullptr;
     std::vector<int4> pyr_bands;   // host copy of the per-band pyramid records
     int4* d_pyr_bands = nullptr;
+    std::vector<int2> pyr_yrec;    // per-row (y0, ibeta0 | ibeta1 << 16) of levels >= 1 (frame kernel)
+    int2* d_pyr_yrec = nullptr;
     uint32_t* d_cand = nullptr;
     int* d_cell_counts = nullptr;
     uint32_t* d_gkeys = nullptr;
@@ -156,7 +158,7 @@ struct orbgpu_extractor {
     int last_batch = 0;
 
     ~orbgpu_extractor() {
-        void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_bands, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
+        void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_bands, d_pyr_yrec, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
                         d_oct_count, d_err, d_trace, d_img, d_kps1, d_desc1, d_count1};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
@@ -232,7 +234,7 @@ int plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, int max_batch, st
     int S = 1, lds_a = 0, lds_b = 0, lds_y = 0;
     for (;; ++S) {
         plan(S, table, lds_a, lds_b, lds_y);
-        if (lds_a + lds_b + lds_y + 64 <= kPyrLdsBudget) break;
+        if (lds_a + lds_b + lds_y + 96 <= kPyrLdsBudget) break;
         if (S >= hmin || S >= 256) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid band does not fit in LDS");
     }
     while ((long)S * max_batch < 2048 && 2 * S <= hmin / 4 && S < 64) {
@@ -240,8 +242,8 @@ int plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, int max_batch, st
         plan(S, table, lds_a, lds_b, lds_y);
     }
     g.pyr_bands = S;
-    g.pyr_lds_a = 0;
-    g.pyr_lds_b = (int)round_up((size_t)lds_a + 16, 16);
+    g.pyr_lds_a = 16;  // 16 bytes in front of each row buffer: column windows may start at -8
+    g.pyr_lds_b = g.pyr_lds_a + (int)round_up((size_t)lds_a + 16, 16);
     g.pyr_lds_y = g.pyr_lds_b + (int)round_up((size_t)lds_b + 16, 16);
     g.pyr_lds_bytes = g.pyr_lds_y + (int)round_up((size_t)lds_y, 16);
     // Per-band records, copied into LDS by the block together with its
@@ -268,12 +270,18 @@ int plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, int max_batch, st
             for (int y = b[l].x; y < b[l].y; ++y) {
                 const int2 t = yt[y];
                 r[off++] = int4{base + ((t.x & 0xFFFF) - src_lo) * sp, base + ((t.x >> 16) - src_lo) * sp,
-                                (t.y & 0xFFFF) << 12, (int)(((uint32_t)t.y >> 16) << 12)};
+                                t.y & 0xFFFF, (int)((uint32_t)t.y >> 16)};
             }
         }
     }
     table.swap(rec);
     g.pyr_rec_stride = stride;
+    if (stride > pyr_prefetch_rec()) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid band record too long");
+    for (int s = 0; s < S; ++s) {
+        const int4 b0 = table[(size_t)s * stride];
+        if ((long)(b0.y - b0.x) * ((g.lv[0].w + 15) / 16) > pyr_prefetch_uint4())
+            return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid band too tall for the level-0 prefetch");
+    }
     return ORBGPU_OK;
 }
 
@@ -314,8 +322,6 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     int cell_base = 0, out_off = 0, max_cells = 0, ncap = 0;
     ptab.clear();
     ytab.clear();
-    std::vector<int4> ptab_pairs;  // the per-pixel-pair layout of the same taps
-    bool win_ok = true;
     for (int l = 0; l < L; ++l) {
         LevelGeom& v = g.lv[l];
         v.w = cv_round((float)e->W * e->inv_scale[l]);
@@ -379,66 +385,92 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
             if (v.simd_end == v.w && v.w % 4 == 0) v.qmain = quads;
             else if (v.simd_end == 4 * (quads - 1)) v.qmain = quads - 1;
             else return fail(ORBGPU_ERR_UNSUPPORTED, "resize tail is not the last quad");
-            v.quad_magic = (uint32_t)(((1ull << 32) + v.qmain - 1) / v.qmain);
-            // row groups: vector quads in whole waves from thread 0, the tail
-            // quads (one lane per row) in the wave after them
+            // thread layout (pyramid.hip quad_taps): vector quads 1 .. qmain-1
+            // in row groups from thread 0, then one edge wave: lanes 0..31 the
+            // first quad of each row (its column window starts before the
+            // row), lanes 32..63 the scalar-tail quad
             {
-                const int T = pyr_threads(), has_tail = v.qmain < quads;
-                int R = T / quads;
-                while (R > 0 && (int)round_up((size_t)v.qmain * R, 64) + (has_tail ? 64 : 0) > T) --R;
+                const int qv = v.qmain - 1;
+                if (qv < 1) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid level narrower than 9 px");
+                v.quad_magic = (uint32_t)(((1ull << 32) + qv - 1) / qv);
+                const int T = pyr_threads();
+                int R = (T - 64) / qv;
+                while (R > 0 && (int)round_up((size_t)qv * R, 64) + 64 > T) --R;
                 if (R < 1) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid level wider than the block");
                 v.rgroups = R;
-                v.tail_base = (int)round_up((size_t)v.qmain * R, 64);
+                v.tail_base = (int)round_up((size_t)qv * R, 64);
             }
 
             if ((size_t)v.pitch * v.h >= (1u << 31)) return fail(ORBGPU_ERR_UNSUPPORTED, "level too large");
             v.ptab_offset = (int)ptab.size();
             v.dbg_level = l;
-            // both column-tap layouts (pyramid.hip); the window one is used
-            // when every quad of every level fits a dword-aligned 8-byte window
-            std::vector<int> wlo(quads);
+            // Column taps per quad for pyramid.hip (3 int4 per quad):
+            //   (w0, wt0, wt1, wt2), (wt3, sel0, sel1, sel2), (sel3, 0, 0, 0).
+            // The kernel reads the three dwords d0, d1, d2 at byte w0 of the
+            // source row; pixels 0..2 take their two taps from (d1:d0) and
+            // pixel 3 from (d2:d1) with v_perm_b32 (selector sel_k puts the
+            // tap bytes in the HIGH byte of each 16-bit lane, i.e. x256), and
+            // wt_k = (16 ialpha0, 16 ialpha1) so v_dot2_u32_u16 yields
+            // 4096 x the exact HResizeLinear sum: its high half is h >> 4,
+            // the operand of VResizeLinearVec_32s8u.  w0 may be -4 or -8
+            // (the LDS row buffers have 16 bytes in front).  Holds for every
+            // scale factor <= 2 (checked here per quad).
             for (int q = 0; q < quads; ++q) {
-                int lo = INT32_MAX, hi = INT32_MIN;
+                const int lo = xt[4 * q].x & 0xFFFF;
+                int w0 = 0, sel[4] = {0, 0, 0, 0};
+                bool ok = false;
+                for (int c = 0; c < 3 && !ok; ++c) {
+                    w0 = (lo & ~3) - 4 * c;
+                    ok = true;
+                    for (int k = 0; k < 4; ++k) {
+                        const int dx = 4 * q + k;
+                        if (dx >= v.w) { sel[k] = (int)0x0c0c0c0cu; continue; }
+                        const int base = w0 + (k == 3 ? 4 : 0);
+                        const int t0 = (xt[dx].x & 0xFFFF) - base;
+                        const int t1 = ((xt[dx].y >> 16) != 0 ? (xt[dx].x >> 16) : (xt[dx].x & 0xFFFF)) - base;
+                        if (t0 < 0 || t1 > 7 || t1 < t0) { ok = false; break; }
+                        sel[k] = (int)(0x000c000cu | ((uint32_t)t0 << 8) | ((uint32_t)t1 << 24));
+                    }
+                }
+                if (!ok) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid column taps do not fit a 12-byte window (scale factor > 2?)");
+                if (q > 0 && w0 < 0) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid column window before the row start");
+                int wt[4];
                 for (int k = 0; k < 4; ++k) {
                     const int dx = 4 * q + k;
-                    if (dx >= v.w) continue;
-                    const int sx = xt[dx].x & 0xFFFF;
-                    lo = std::min(lo, sx);
-                    hi = std::max(hi, sx + ((xt[dx].y >> 16) != 0 ? 1 : 0));
+                    const uint32_t a0 = dx < v.w ? (uint32_t)(xt[dx].y & 0xFFFF) : 0u;
+                    const uint32_t a1 = dx < v.w ? (uint32_t)(xt[dx].y >> 16) : 0u;
+                    wt[k] = (int)((a0 << 4) | (a1 << 20));
                 }
-                const int w0 = (std::max(hi - 7, 0) + 3) & ~3;
-                if (w0 > lo) win_ok = false;
-                wlo[q] = w0;
-            }
-            for (int q = 0; q < quads; ++q) {
-                int lo[4], wt[4], wsel[4], psel[4];
-                for (int k = 0; k < 4; ++k) {
-                    const int dx = 4 * q + k;
-                    const int sx = dx < v.w ? (xt[dx].x & 0xFFFF) : 0;
-                    wt[k] = dx < v.w ? xt[dx].y : 0;
-                    const int b0 = sx - wlo[q];
-                    const int b1 = (wt[k] >> 16) != 0 ? b0 + 1 : b0;
-                    wsel[k] = dx < v.w ? (int)(0x0c000c00u | (uint32_t)(b0 & 7) | ((uint32_t)(b1 & 7) << 16))
-                                       : (int)0x0c0c0c0cu;
-                    lo[k] = sx & ~3;
-                    psel[k] = (int)(0x0c010c00u + (uint32_t)(sx & 3) * 0x00010001u);
-                }
-                ptab.push_back(int4{wlo[q], wt[0], wt[1], wt[2]});
-                ptab.push_back(int4{wt[3], wsel[0], wsel[1], wsel[2]});
-                ptab.push_back(int4{wsel[3], 0, 0, 0});
-                ptab_pairs.push_back(int4{lo[0], wt[0], lo[1], wt[1]});
-                ptab_pairs.push_back(int4{lo[2], wt[2], lo[3], wt[3]});
-                ptab_pairs.push_back(int4{psel[0], psel[1], psel[2], psel[3]});
+                ptab.push_back(int4{w0, wt[0], wt[1], wt[2]});
+                ptab.push_back(int4{wt[3], sel[0], sel[1], sel[2]});
+                ptab.push_back(int4{sel[3], 0, 0, 0});
             }
             v.ytab_offset = (int)ytab.size();
             ytab.insert(ytab.end(), yt.begin(), yt.end());
+            // frame-kernel row records: the second source row must be y0 + 1,
+            // or y0 with a zero weight (bottom clamp)
+            v.yrec_offset = (int)e->pyr_yrec.size();
+            for (const int2& t : yt) {
+                const int y0 = t.x & 0xFFFF, y1 = t.x >> 16, b1 = (int)((uint32_t)t.y >> 16);
+                if (!(y1 == y0 + 1 || (y1 == y0 && b1 == 0)))
+                    return fail(ORBGPU_ERR_UNSUPPORTED, "unexpected resize row taps");
+                e->pyr_yrec.push_back(int2{y0, t.y});
+            }
         }
     }
-    g.pyr_win = win_ok ? 1 : 0;
-    if (!win_ok) ptab.swap(ptab_pairs);
+    g.pyr_yrec_total = (int)e->pyr_yrec.size();
     {
+        const char* m = std::getenv("ORBGPU_PYR_MODE");  // tuning/A-B only: "band" selects the LDS-band kernel
+        g.pyr_mode = (m && std::strcmp(m, "band") == 0) ? 0 : 1;
+    }
+    if (g.pyr_mode == 0) {
         int rc = plan_pyramid_bands(g, ytab, e->max_batch, e->pyr_bands);
         if (rc) return rc;
+    } else {
+        g.pyr_bands = 1;
+        e->pyr_bands.assign(1, int4{0, 0, 0, 0});
+        if ((size_t)g.pyr_yrec_total * sizeof(int2) > 64 * 1024)
+            return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid row records exceed 64 KiB of LDS");
     }
     g.total_cells = cell_base;
     g.cand_frame = cand_off;
@@ -493,7 +525,7 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
         evs = e->ev[e->ev_used++].data();
         ORB_HIP(hipEventRecord(evs[0], s));
     }
-    ORB_HIP(launch_pyramid(g, batch, e->d_pyr_bands, e->d_ptab, imgs, row_step, frame_step, e->d_pyr, s));
+    ORB_HIP(launch_pyramid(g, batch, e->d_pyr_bands, e->d_pyr_yrec, e->d_ptab, imgs, row_step, frame_step, e->d_pyr, s));
     if (evs) ORB_HIP(hipEventRecord(evs[1], s));
     ORB_HIP(launch_fast_cells(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_cand, e->d_cell_counts, e->d_err, s));
     if (evs) ORB_HIP(hipEventRecord(evs[2], s));
@@ -579,14 +611,16 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
         (rc = dalloc(&e->d_oct_count, (size_t)g.nlevels * B)) || (rc = dalloc(&e->d_err, 1)) ||
         (rc = dalloc(&e->d_img, e->img_pitch * height)) || (rc = dalloc(&e->d_kps1, (size_t)e->max_kps)) ||
         (rc = dalloc(&e->d_desc1, (size_t)e->max_kps * 32)) || (rc = dalloc(&e->d_count1, 1)) ||
-        (rc = dalloc(&e->d_pyr_bands, e->pyr_bands.size()))) {
+        (rc = dalloc(&e->d_pyr_bands, e->pyr_bands.size())) || (rc = dalloc(&e->d_pyr_yrec, e->pyr_yrec.size()))) {
         delete e;
         return rc;
     }
     if (hipMemcpy(e->d_ptab, ptab.data(), ptab.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(e->d_pyr_bands, e->pyr_bands.data(), e->pyr_bands.size() * sizeof(int4), hipMemcpyHostToDevice) !=
             hipSuccess ||
-        pyramid_set_lds_limit((size_t)g.pyr_lds_bytes) != hipSuccess ||
+        (!e->pyr_yrec.empty() && hipMemcpy(e->d_pyr_yrec, e->pyr_yrec.data(), e->pyr_yrec.size() * sizeof(int2),
+                                           hipMemcpyHostToDevice) != hipSuccess) ||
+        (g.pyr_mode == 0 && pyramid_set_lds_limit((size_t)g.pyr_lds_bytes) != hipSuccess) ||
         hipMemset(e->d_err, 0, sizeof(int)) != hipSuccess ||
         hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         delete e;

@@ -64,6 +64,7 @@ struct LevelGeom {
     int ptab_offset;          // int4 offset of this level's per-quad column taps (3 int4 per quad)
     int rgroups;              // row groups of a pyramid block (pyramid.hip quad_taps)
     int tail_base;            // first thread of the tail quads (a wave boundary)
+    int yrec_offset;          // first row record of this level (pyramid_frame_kernel)
     // blurred level (all levels, incl. 0): same row pitch as the pyramid
     size_t blur_offset, blur_frame_bytes;
     int blur_tiles_x, blur_tile_base;   // blur work items: 4-column x 64-row strips
@@ -84,7 +85,8 @@ struct Geom {
     int pyr_bands;
     int pyr_lds_a, pyr_lds_b, pyr_lds_y, pyr_lds_bytes;  // odd levels, even levels (incl. 0), y taps
     int pyr_rec_stride;       // int4s per band record (band entries + per-row source offsets)
-    int pyr_win;              // 1: every quad's column taps fit one 8-byte window (pyramid.hip WIN layout)
+    int pyr_mode;             // 0: band kernel (levels through LDS), 1: frame kernel (levels through L2)
+    int pyr_yrec_total;       // row records of all levels >= 1 (frame kernel)
     LevelGeom lv[kMaxLevels];
 };
 

@@ -11,18 +11,22 @@
 // bottom-up.  Each level's band rows (its owned rows plus the few halo rows
 // the band's next level reads, planned on the host: plan_pyramid_bands) are
 // computed from the previous level's rows held in LDS, written to LDS for the
-// next level and, for owned rows, to HBM.  The band's level-0 rows are staged
-// into LDS once with 16-byte loads.  So every level is written to HBM once and never read back by
-// this pass: HBM traffic is |P_0| (+ halo) + sum_l |P_l|, while the
+// next level and to HBM (halo rows too: the neighbouring band writes the same
+// bytes there).  The band's level-0 rows are staged into LDS once with 16-byte
+// loads.  So no level is read back from HBM by this pass: HBM traffic is
+// |P_0| + sum_l |P_l| (+ halo), while the
 // algorithmic bytes of the reference's level-by-level pass
 // (sum_l |P_{l-1}| + |P_l|) are larger.
 //
-// Per output quad: one 8-byte window of each of the two source rows (one
-// dword pair each), v_perm_b32 spreads each pixel's tap pair into 16-bit
-// lanes and v_dot2_u32_u16 applies (ialpha0, ialpha1) -- the exact
-// horizontal sum -- then the vertical rounding.  No saturation is needed: with non-negative
-// Q11 weights summing to 2048 (+-1), every intermediate is in range
-// (h <= 255*2048; the SIMD-path sum of the two >>16 products <= 1020).
+// Per output quad and source row: one 12-byte window (three dwords), v_perm_b32
+// spreads each pixel's tap pair into the high bytes of two 16-bit lanes and
+// v_dot2_u32_u16 applies (16 ialpha0, 16 ialpha1): 4096 x the exact
+// horizontal sum, whose high half is the (h >> 4) of the vertical pass.  Row
+// groups walk runs of consecutive output rows and keep the last source row's
+// sums in registers (~1.2 horizontal passes per output row).  The vertical
+// pass is four SDWA/op_sel instructions per pixel (vert_simd).
+#include <algorithm>
+
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
 
@@ -31,134 +35,102 @@ namespace orbgpu {
 namespace {
 
 #ifndef PYR_PROBE
-#define PYR_PROBE 0  // timing probes for tuning only (tools/pyr_variants.sh): bit 0 = no level-0 loads, bit 2 = level 1 only, bit 3 = phase stamps; 0 = the product
+#define PYR_PROBE 0  // timing probes for tuning only (tools/pyr_variants.sh): bit 0 = no level-0 loads, bit 2 = level 1 only, bit 3 = phase stamps, bit 5 = no HBM stores in the row loop; 0 = the product
 #endif
 #ifndef PYR_THREADS
 #define PYR_THREADS 1024
 #endif
 constexpr int kPyrThreads = PYR_THREADS;
+#ifndef PYR_MINRUN
+#define PYR_MINRUN 1
+#endif
+constexpr int kPyrMinRun = PYR_MINRUN;
+constexpr int kPyrPre = 4;     // level-0 uint4 loads per thread per item (host checks the band fits)
+constexpr int kPyrPreRec = 1;  // record int4 per thread per item (host checks pyr_rec_stride <= threads)
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
 #if PYR_PROBE & 8
 // diagnostic build only: per-block phase stamps (never read by the kernel)
 __device__ unsigned long long g_pyr_stamps[8192 * 10];
-__device__ __forceinline__ void pyr_stamp(int slot) {
+__device__ __forceinline__ void pyr_stamp_at(int item, int slot) {
     __builtin_amdgcn_sched_barrier(0);
     unsigned long long t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (threadIdx.x == 0 && blockIdx.x < 8192) g_pyr_stamps[blockIdx.x * 10 + slot] = t;
+    if (threadIdx.x == 0 && item < 8192) g_pyr_stamps[item * 10 + slot] = t;
 }
-#define PYR_STAMP(i) pyr_stamp(i)
+#define PYR_STAMP(i) pyr_stamp_at(item, i)
 __device__ unsigned long long g_pyr_wave[8192 * 8 * 16];
 #else
 #define PYR_STAMP(i) ((void)0)
 #endif
 
-// 24 x 24 -> high 32 bits of the 48-bit product (v_mul_hi_u32_u24); both
-// operands must be < 2^24
-__device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
-    return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
-}
-
-// out.byte[K] = s >> 2, other bytes preserved (SDWA destination select)
-template <int K>
-__device__ __forceinline__ void put_byte_shr2(uint32_t& out, uint32_t s) {
-    static_assert(K >= 1 && K <= 3, "byte 0 is written by a plain shift");
-    if (K == 1)
-        asm("v_lshrrev_b32_sdwa %0, 2, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-            : "+v"(out) : "v"(s));
-    else if (K == 2)
-        asm("v_lshrrev_b32_sdwa %0, 2, %1 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-            : "+v"(out) : "v"(s));
-    else
-        asm("v_lshrrev_b32_sdwa %0, 2, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-            : "+v"(out) : "v"(s));
-}
-
-// One level's band rows [r0, r1).  Thread layout: quad column q of 4 output
-// pixels x row group rg walking rows r0+rg, r0+rg+rgroups, ..., so the
-// column taps stay in registers for the whole level.  s_rows[r - r0] = (LDS
-// offset of source row y0, of y1, ibeta0 << 12, ibeta1 << 12).
-//
-// Column taps per quad (ptab, 3 x int4), two layouts chosen for the whole
-// pyramid on the host (Geom::pyr_win; the kernel is instantiated for each):
-//  * window (WIN): all eight taps of the quad lie in one dword-aligned 8-byte
-//    window of the source row (always true for scale factors <= 4/3):
-//    (lo, wt0, wt1, wt2), (wt3, sel0, sel1, sel2), (sel3, -, -, -) -- one
-//    ds_read2_b32 per source row serves the whole quad;
-//  * pairs: (lo0, wt0, lo1, wt1), (lo2, wt2, lo3, wt3), (sel0..3) with lo_k
-//    the dword pair holding taps sx_k, sx_k + 1.
-// sel = the v_perm_b32 selector spreading a pixel's two taps into 16-bit
-// lanes, wt = (ialpha0, ialpha1); v_dot2_u32_u16 forms the exact horizontal
-// sum.  Rows are padded so reading past a row end is safe.
-//
-// Vertical pass, VResizeLinearVec_32s8u: ((h0>>4)*b0 >> 16) + ((h1>>4)*b1 >>
-// 16) + 2 >> 2, each term as mulhi24(h & ~15, b << 12) = (16 (h>>4) b 2^12)
-// >> 32.  h <= 255 * 2049 < 2^24 and b << 12 <= 2049 << 12 < 2^24.
-//
-// The last quad of every row is exactly the scalar tail (simd_end = 4 *
-// (quads - 1), checked on the host; or there is no tail when w is a multiple
-// of 16); its threads get a wave of their own (quad_taps).
-// The source bytes one output row of a quad needs: rows y0 (a) and y1 (b),
-// one dword pair per row (WIN) or per pixel.
-// Horizontal pass of one source row for the quad: h[k] = the exact Q11 sum
-// of pixel k's two taps (HResizeLinear), from the row at LDS offset `row`.
-struct H4 {
-    uint32_t h[4];
+// Column taps of a thread's quad (host: build_geometry, 3 int4 per quad):
+// the byte offset w0 of a 12-byte window in the source row, the four
+// (16 ialpha0, 16 ialpha1) weight pairs and the four v_perm_b32 selectors
+// (pixels 0..2 from dwords (d1:d0), pixel 3 from (d2:d1)); each selector puts
+// a pixel's two tap bytes in the high bytes of two 16-bit lanes.
+struct Taps {
+    int w0;
+    uint32_t wt[4], sel[4];
 };
 
-template <bool WIN>
-__device__ __forceinline__ H4 hrow(const uint8_t* const (&col)[4], const uint32_t (&wt)[4], const uint32_t (&sel)[4],
-                                   int row) {
-    H4 r;
-    uint32_t w[WIN ? 2 : 8];
-#pragma unroll
-    for (int k = 0; k < (WIN ? 1 : 4); ++k) {
-        const uint32_t* a = reinterpret_cast<const uint32_t*>(col[k] + row);
-        w[2 * k] = a[0];
-        w[2 * k + 1] = a[1];
-    }
-#if PYR_PROBE & 16
-    // timing probe: half the horizontal work (pixels 2, 3 reuse 0, 1)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-#else
+// Horizontal pass of one source row for the quad: h[k] = 4096 x the exact
+// Q11 sum of pixel k's two taps (HResizeLinear), so the high half of h[k] is
+// the (h >> 4) VResizeLinearVec_32s8u multiplies (h <= 255 * 2049, so
+// 4096 h < 2^32).  `row` = LDS byte offset of the source row.
+__device__ __forceinline__ void hrow(uint32_t (&h)[4], const uint8_t* lds, const Taps& t, int row) {
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(lds + t.w0 + row);
+    const uint32_t d0 = a[0], d1 = a[1], d2 = a[2];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-#endif
-        const int j = WIN ? 0 : 2 * k;
-        const uint32_t p = __builtin_amdgcn_perm(w[j + 1], w[j], sel[k]);
-        r.h[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p), __builtin_bit_cast(us2, wt[k]), 0u, false);
+        const uint32_t p = k < 3 ? __builtin_amdgcn_perm(d1, d0, t.sel[k]) : __builtin_amdgcn_perm(d2, d1, t.sel[k]);
+        h[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p), __builtin_bit_cast(us2, t.wt[k]), 0u, false);
     }
-#if PYR_PROBE & 16
-    r.h[2] = r.h[0] ^ 1; r.h[3] = r.h[1] ^ 1;
-#endif
-    return r;
 }
 
-// Vertical pass of one output quad from its two source rows' sums.
-template <bool TAIL>
-__device__ __forceinline__ uint32_t vert(const H4& h0, const H4& h1, int4 yr) {
-    uint32_t out;
-    if (!TAIL) {
-        const uint32_t B0 = (uint32_t)yr.z & 0xFFFFFFu, B1 = (uint32_t)yr.w & 0xFFFFFFu;
-        uint32_t sum[4];
+// VResizeLinearVec_32s8u for one quad:
+//   out = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2
+// with (h >> 4) the high half of the 4096-scaled sums.  Per pixel:
+// x = (h0>>4) b0 + 2^17 (v_mad_u32_u16, op_sel picks the high half), y =
+// (h1>>4) b1 (SDWA WORD_1), then one SDWA add of the two high halves lands
+// the rounded sum + 2 in a 16-bit lane; a packed shift and one v_perm_b32
+// give the four bytes.  No saturation is needed: with non-negative Q11
+// weights every partial sum is <= 1020.
+__device__ __forceinline__ uint32_t vert_simd(const uint32_t (&h0)[4], const uint32_t (&h1)[4], uint32_t b0,
+                                              uint32_t b1) {
+    uint32_t x[4], y[4], s01, s23;
+    const uint32_t two = 2u << 16;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            sum[k] = mulhi24(h0.h[k] & 0xFFFFF0u, B0) + mulhi24(h1.h[k] & 0xFFFFF0u, B1) + 2u;
-        out = sum[0] >> 2;
-        put_byte_shr2<1>(out, sum[1]);
-        put_byte_shr2<2>(out, sum[2]);
-        put_byte_shr2<3>(out, sum[3]);
-    } else {  // FixedPtCast<int, uchar, 22>: (S0*b0 + S1*b1 + 2^21) >> 22, < 2^31 (S < 2^24, b < 2^12)
-        const uint32_t b0 = (uint32_t)yr.z >> 12, b1 = (uint32_t)yr.w >> 12;
-        out = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            out |= ((__umul24(h0.h[k], b0) + __umul24(h1.h[k], b1) + (1u << 21)) >> 22) << (8 * k);
+    for (int k = 0; k < 4; ++k) {
+        asm("v_mad_u32_u16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(x[k]) : "v"(h0[k]), "v"(b0), "s"(two));
+        asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+            : "=v"(y[k]) : "v"(h1[k]), "v"(b1));
     }
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_1"
+        : "=v"(s01) : "v"(x[0]), "v"(y[0]));
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1"
+        : "+v"(s01) : "v"(x[1]), "v"(y[1]));
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_1"
+        : "=v"(s23) : "v"(x[2]), "v"(y[2]));
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1"
+        : "+v"(s23) : "v"(x[3]), "v"(y[3]));
+    // both halves shifted by 2: the inline constant feeds the high half only
+    // through op_sel_hi (tools/sdwa_probe.hip)
+    asm("v_pk_lshrrev_b16 %0, 2, %0 op_sel_hi:[0,1]" : "+v"(s01));
+    asm("v_pk_lshrrev_b16 %0, 2, %0 op_sel_hi:[0,1]" : "+v"(s23));
+    return __builtin_amdgcn_perm(s23, s01, 0x06040200u);
+}
+
+// FixedPtCast<int, uchar, 22> (the scalar tail of VResizeLinear):
+// (S0*b0 + S1*b1 + 2^21) >> 22 with S = h = (4096 h) >> 12 < 2^20, b < 2^12.
+__device__ __forceinline__ uint32_t vert_tail(const uint32_t (&h0)[4], const uint32_t (&h1)[4], uint32_t b0,
+                                              uint32_t b1) {
+    uint32_t out = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        out |= ((__umul24(h0[k] >> 12, b0) + __umul24(h1[k] >> 12, b1) + (1u << 21)) >> 22) << (8 * k);
     return out;
 }
 
@@ -168,29 +140,34 @@ __device__ __forceinline__ uint32_t vert(const H4& h0, const H4& h1, int4 yr) {
 struct QuadTaps {
     int4 a, b, c;
     int q, rg;
-    int mode;  // 0 idle, 1 vector quad, 2 tail quad
+    int mode;  // 0 idle, 1 vector quad (1 .. qmain-1), 2 first quad, 3 scalar-tail quad
 };
 
-// Thread layout of a level: vector quads fill threads [0, qmain * rgroups)
-// (row group rg = t / qmain, rows rg, rg + rgroups, ...); the tail quad of
-// every row goes to the wave starting at tail_base (lane = row, rows lane,
-// lane + 64, ...) -- the tail formula then never shares a wave with the
-// vector one, no wave runs both loops, and the tail wave needs one pass for
-// bands up to 64 rows.
+// Thread layout of a level: vector quads 1 .. qmain-1 fill threads
+// [0, (qmain-1) * rgroups) (row group rg = t / (qmain-1) owns one run of
+// consecutive rows); the edge wave starting at tail_base takes the first quad
+// of every row on lanes 0..31 (its column window starts up to 8 bytes before
+// the row) and the scalar-tail quad on lanes 32..63 (lane = row, rows lane,
+// lane + 32, ...), so the main loop never meets either case.
 __device__ __forceinline__ QuadTaps quad_taps(const LevelGeom& V, const int4* __restrict__ ptab) {
     QuadTaps tp;
     const int t = threadIdx.x;
+    const int qv = V.qmain - 1;
     tp.mode = 0;
     tp.q = 0;
     tp.rg = 0;
-    if (t < V.qmain * V.rgroups) {
+    if (t < qv * V.rgroups) {
         tp.rg = (int)__umulhi((uint32_t)t, V.quad_magic);
-        tp.q = t - tp.rg * V.qmain;
+        tp.q = 1 + t - tp.rg * qv;
         tp.mode = 1;
-    } else if (t >= V.tail_base && t < V.tail_base + 64 && 4 * V.qmain < V.w) {
+    } else if (t >= V.tail_base && t < V.tail_base + 32) {
         tp.rg = t - V.tail_base;
-        tp.q = V.qmain;
+        tp.q = 0;
         tp.mode = 2;
+    } else if (t >= V.tail_base + 32 && t < V.tail_base + 64 && 4 * V.qmain < V.w) {
+        tp.rg = t - V.tail_base - 32;
+        tp.q = V.qmain;
+        tp.mode = 3;
     }
     if (tp.mode) {
         const int4* pt = ptab + V.ptab_offset + 3 * tp.q;
@@ -201,141 +178,396 @@ __device__ __forceinline__ QuadTaps quad_taps(const LevelGeom& V, const int4* __
     return tp;
 }
 
-template <bool TAIL, bool WIN>
+// One level's band rows [r0, r1).  s_rows[r - r0] = (LDS offset of source
+// row y0, of y1, ibeta0, ibeta1).  Stores go to the next level's LDS buffer
+// (lds_dst, if any) and to HBM.
+template <bool TAIL>
 __device__ __forceinline__ void resize_rows(const uint8_t* __restrict__ lds, const LevelGeom& V, const QuadTaps& tp,
-                                            int r0, int r1, int own0, int own1, const int4* __restrict__ s_rows,
+                                            int r0, int r1, const int4* __restrict__ s_rows,
                                             uint8_t* __restrict__ lds_dst, uint8_t* __restrict__ hbm_dst) {
-    const int4 ta = tp.a, tb = tp.b, tc = tp.c;
+    Taps t;
+    t.w0 = tp.a.x;
+    t.wt[0] = tp.a.y; t.wt[1] = tp.a.z; t.wt[2] = tp.a.w; t.wt[3] = tp.b.x;
+    t.sel[0] = tp.b.y; t.sel[1] = tp.b.z; t.sel[2] = tp.b.w; t.sel[3] = tp.c.x;
     const int q = tp.q;
-    const uint8_t* col[4];
-    uint32_t wt[4], sel[4];
-    if (WIN) {
-        col[0] = col[1] = col[2] = col[3] = lds + ta.x;
-        wt[0] = ta.y; wt[1] = ta.z; wt[2] = ta.w; wt[3] = tb.x;
-        sel[0] = tb.y; sel[1] = tb.z; sel[2] = tb.w; sel[3] = tc.x;
-    } else {
-        col[0] = lds + ta.x; col[1] = lds + ta.z; col[2] = lds + tb.x; col[3] = lds + tb.z;
-        wt[0] = ta.y; wt[1] = ta.w; wt[2] = tb.y; wt[3] = tb.w;
-        sel[0] = tc.x; sel[1] = tc.y; sel[2] = tc.z; sel[3] = tc.w;
-    }
-    auto store = [&](int r, uint32_t out) {
-        // bytes past V.w land in the row padding (LDS pitch and HBM pitch are
-        // multiples of 4 and 16)
-        if (lds_dst) *reinterpret_cast<uint32_t*>(lds_dst + (uint32_t)((r - r0) * V.lds_pitch + 4 * q)) = out;
-        if (r >= own0 && r < own1) *reinterpret_cast<uint32_t*>(hbm_dst + (uint32_t)(r * V.pitch + 4 * q)) = out;
-    };
-    if (TAIL) {  // one row per lane (tail wave)
-        for (int r = r0 + tp.rg; r < r1; r += 64) {
+    uint32_t P[4], Q[4];
+    // Every computed row goes to HBM, halo rows included: a halo row is also
+    // an owned row of the neighbouring band, computed there from the same
+    // source rows with the same arithmetic, so the two writes carry identical
+    // bytes.  Bytes past V.w land in the row padding (LDS pitch and HBM pitch
+    // are multiples of 4 and 16).
+    const uint32_t lpitch = (uint32_t)V.lds_pitch, hpitch = (uint32_t)V.pitch;
+    if (TAIL) {  // edge wave: one row per lane, first quad (mode 2) or scalar tail (mode 3)
+        for (int r = r0 + tp.rg; r < r1; r += 32) {
             const int4 y = s_rows[r - r0];
-            store(r, vert<true>(hrow<WIN>(col, wt, sel, y.x), hrow<WIN>(col, wt, sel, y.y), y));
+            hrow(P, lds, t, y.x);
+            hrow(Q, lds, t, y.y);
+            const uint32_t out = tp.mode == 2 ? vert_simd(P, Q, (uint32_t)y.z, (uint32_t)y.w)
+                                              : vert_tail(P, Q, (uint32_t)y.z, (uint32_t)y.w);
+            if (lds_dst) *reinterpret_cast<uint32_t*>(lds_dst + __umul24((uint32_t)(r - r0), lpitch) + 4 * q) = out;
+            *reinterpret_cast<uint32_t*>(hbm_dst + __umul24((uint32_t)r, hpitch) + 4 * q) = out;
         }
         return;
     }
-    // Row groups own pairs of consecutive output rows: (r, r+1) read source
-    // rows (y0, y0+1) and (y0', y0'+1) with y0' = y0 + 1 for most pairs of a
-    // ~1.2x downscale, so the shared source row's horizontal sums are
-    // computed once (3 source rows per 2 output rows instead of 4).
-    for (int r = r0 + 2 * tp.rg; r < r1; r += 2 * V.rgroups) {
-        const bool two = r + 1 < r1;
-        const int4 ya = s_rows[r - r0];
-        const int4 yb = s_rows[(two ? r + 1 : r) - r0];
-        const H4 hA = hrow<WIN>(col, wt, sel, ya.x);
-        const H4 hB = hrow<WIN>(col, wt, sel, ya.y);
-        H4 hC, hD;
-        if (yb.x == ya.y) hC = hB; else hC = hrow<WIN>(col, wt, sel, yb.x);
-        if (yb.y == ya.y) hD = hB; else hD = hrow<WIN>(col, wt, sel, yb.y);
-        store(r, vert<false>(hA, hB, ya));
-        if (two) store(r + 1, vert<false>(hC, hD, yb));
+    // Row group rg owns the run [ra, rb) of consecutive output rows.  Rows of
+    // a ~1.2x downscale share source rows (y0 of row r+1 is mostly y1 of row
+    // r), so the last source row's sums stay in registers: about 1.2
+    // horizontal passes per output row.  Unrolled by two with the roles of P
+    // and Q swapped, so the carried row needs no register moves; runs are of
+    // even length (only the last one can be odd) and at least kPyrMinRun rows.
+    const int rows = r1 - r0;
+    const int R = min(V.rgroups, (rows + kPyrMinRun - 1) / kPyrMinRun);
+    const int n = (((rows + R - 1) / R) + 1) & ~1;
+    if (tp.rg >= R) return;
+    const int ra = r0 + tp.rg * n, rb = min(ra + n, r1);
+    uint8_t* lp = lds_dst ? lds_dst + __umul24((uint32_t)(ra - r0), lpitch) + 4 * q : nullptr;
+    uint8_t* hp = hbm_dst + __umul24((uint32_t)ra, hpitch) + 4 * q;
+    const int4* rec = s_rows + (ra - r0);
+    int cur = -1;  // LDS offset of the source row whose sums are in P
+    int r = ra;
+    for (; r + 1 < rb; r += 2) {
+        const int4 y = rec[0];
+        const int4 z = rec[1];
+        rec += 2;
+        if (y.x != cur) hrow(P, lds, t, y.x);
+        hrow(Q, lds, t, y.y);
+        const uint32_t o0 = vert_simd(P, Q, (uint32_t)y.z, (uint32_t)y.w);
+        if (z.x != y.y) hrow(Q, lds, t, z.x);
+        hrow(P, lds, t, z.y);
+        const uint32_t o1 = vert_simd(Q, P, (uint32_t)z.z, (uint32_t)z.w);
+        cur = z.y;
+        if (lp) {
+            *reinterpret_cast<uint32_t*>(lp) = o0;
+            *reinterpret_cast<uint32_t*>(lp + lpitch) = o1;
+            lp += 2 * lpitch;
+        }
+#if !(PYR_PROBE & 32)
+        *reinterpret_cast<uint32_t*>(hp) = o0;
+        *reinterpret_cast<uint32_t*>(hp + hpitch) = o1;
+#endif
+        hp += 2 * hpitch;
+    }
+    if (r < rb) {
+        const int4 y = rec[0];
+        if (y.x != cur) hrow(P, lds, t, y.x);
+        hrow(Q, lds, t, y.y);
+        const uint32_t o0 = vert_simd(P, Q, (uint32_t)y.z, (uint32_t)y.w);
+        if (lp) *reinterpret_cast<uint32_t*>(lp) = o0;
+        *reinterpret_cast<uint32_t*>(hp) = o0;
     }
 }
 
-template <bool WIN>
 __device__ __forceinline__ void resize_band(const uint8_t* __restrict__ lds, const LevelGeom& V, const QuadTaps& tp,
-                                            int r0, int r1, int own0, int own1, const int4* __restrict__ s_rows,
+                                            int r0, int r1, const int4* __restrict__ s_rows,
                                             uint8_t* __restrict__ lds_dst, uint8_t* __restrict__ hbm_dst) {
     if (tp.mode == 1)
-        resize_rows<false, WIN>(lds, V, tp, r0, r1, own0, own1, s_rows, lds_dst, hbm_dst);
-    else if (tp.mode == 2)
-        resize_rows<true, WIN>(lds, V, tp, r0, r1, own0, own1, s_rows, lds_dst, hbm_dst);
+        resize_rows<false>(lds, V, tp, r0, r1, s_rows, lds_dst, hbm_dst);
+    else if (tp.mode >= 2)
+        resize_rows<true>(lds, V, tp, r0, r1, s_rows, lds_dst, hbm_dst);
 }
 
-template <bool WIN>
+// ---------------------------------------------------------------------------
+// Frame-per-block form (pyramid_frame_kernel): a 1024-thread block owns one
+// frame and computes level l from level l-1 read straight from memory (level
+// 0 = the caller's frame, levels >= 1 = this block's own writes of the
+// previous level, L2/MALL-resident), so there is no band halo and no LDS
+// staging, and every row group walks one long run of rows.  Source windows
+// come through buffer loads: the hardware range check turns the few reads
+// outside a level (the window of quad 0 starts up to 8 bytes before a row)
+// into zeros instead of faults, and those bytes are never selected by a tap.
+// Window loads run one row pair ahead of their use.
+// ---------------------------------------------------------------------------
+typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+
+struct Win {
+    uint32_t d0, d1, d2;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ Win ldwin(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
+    const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)voff, (int)soff, 0);
+    return Win{v.x, v.y, v.z};
+}
+
+// hrow() on a window already in registers
+__device__ __forceinline__ void hwin(uint32_t (&h)[4], const Win& w, const Taps& t) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t p = k < 3 ? __builtin_amdgcn_perm(w.d1, w.d0, t.sel[k]) : __builtin_amdgcn_perm(w.d2, w.d1, t.sel[k]);
+        h[k] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, p), __builtin_bit_cast(us2, t.wt[k]), 0u, false);
+    }
+}
+
+// One level of one frame.  rec[r] = (y0 of output row r, ibeta0 | ibeta1 <<
+// 16); the second source row is y0 + 1 (at the bottom clamp ibeta1 = 0, so
+// whatever that row holds is multiplied by zero).  sp = source row pitch,
+// src = buffer resource over the source level of this frame.
+template <bool TAIL>
+__device__ __forceinline__ void frame_rows(__amdgpu_buffer_rsrc_t src, uint32_t sp, const LevelGeom& V,
+                                           const QuadTaps& tp, const int2* __restrict__ rec,
+                                           uint8_t* __restrict__ dst) {
+    Taps t;
+    t.w0 = tp.a.x;
+    t.wt[0] = tp.a.y; t.wt[1] = tp.a.z; t.wt[2] = tp.a.w; t.wt[3] = tp.b.x;
+    t.sel[0] = tp.b.y; t.sel[1] = tp.b.z; t.sel[2] = tp.b.w; t.sel[3] = tp.c.x;
+    const uint32_t dp = (uint32_t)V.pitch;
+    const uint32_t q4 = 4u * (uint32_t)tp.q;
+    const int rows = V.h;
+    uint32_t P[4], Q[4];
+    auto voff = [&](int y) { return __umul24((uint32_t)y, sp) + (uint32_t)t.w0; };
+    if (TAIL) {  // edge wave: one row per lane, first quad (mode 2) or scalar tail (mode 3)
+        // The first quad's window starts at w0 = -4 or -8: on row 0 that is
+        // before the level, where a buffer load returns zeros for all three
+        // dwords, so the load starts at 0 and the dwords move up instead.
+        auto ld = [&](int o) {
+            Win w = ldwin(src, (uint32_t)max(o, 0), 0);
+            if (o == -4) {
+                w.d2 = w.d1; w.d1 = w.d0; w.d0 = 0;
+            } else if (o == -8) {
+                w.d2 = w.d0; w.d1 = 0; w.d0 = 0;
+            }
+            return w;
+        };
+        for (int r = tp.rg; r < rows; r += 32) {
+            const int2 y = rec[r];
+            const int o = (int)voff(y.x);
+            const Win w0 = ld(o), w1 = ld(o + (int)sp);
+            hwin(P, w0, t);
+            hwin(Q, w1, t);
+            const uint32_t out = tp.mode == 2 ? vert_simd(P, Q, (uint32_t)y.y, (uint32_t)y.y >> 16)
+                                              : vert_tail(P, Q, (uint32_t)y.y & 0xFFFFu, (uint32_t)y.y >> 16);
+            *reinterpret_cast<uint32_t*>(dst + __umul24((uint32_t)r, dp) + q4) = out;
+        }
+        return;
+    }
+    // row group rg: run [ra, rb) of n rows (n a multiple of 4)
+    const int R = V.rgroups;
+    const int n = ((rows + R - 1) / R + 3) & ~3;
+    const int ra = tp.rg * n;
+    if (ra >= rows) return;
+    const int rb = min(ra + n, rows);
+    uint32_t ho = __umul24((uint32_t)ra, dp) + q4;
+    int cur = -1;  // source row whose sums are in P
+    int r = ra;
+    // two output rows per step: (P, Q) for the first, (Q, P) for the second,
+    // so the carried source row never moves between registers.  The y1 row's
+    // window of every output row is loaded a pair ahead; the y0 row's only
+    // when it is not the carried row (run start, or y0 advancing by 2), on
+    // demand.
+    auto pair = [&](const int2 ya, const int2 yb, const Win& a1, const Win& b1) {
+        if (ya.x != cur) hwin(P, ldwin(src, voff(ya.x), 0), t);
+        hwin(Q, a1, t);
+        const uint32_t o0 = vert_simd(P, Q, (uint32_t)ya.y, (uint32_t)ya.y >> 16);
+        if (yb.x != ya.x + 1) hwin(Q, ldwin(src, voff(yb.x), 0), t);
+        hwin(P, b1, t);
+        const uint32_t o1 = vert_simd(Q, P, (uint32_t)yb.y, (uint32_t)yb.y >> 16);
+        cur = yb.x + 1;
+#if !(PYR_PROBE & 32)
+        *reinterpret_cast<uint32_t*>(dst + ho) = o0;
+        *reinterpret_cast<uint32_t*>(dst + ho + dp) = o1;
+#endif
+        ho += 2 * dp;
+    };
+    if (rb - ra >= 4) {
+        int2 ya = rec[r], yb = rec[r + 1];
+        Win A1 = ldwin(src, voff(ya.x), sp), B1 = ldwin(src, voff(yb.x), sp);
+        for (; r + 3 < rb; r += 4) {
+            const int2 yc = rec[r + 2], yd = rec[r + 3];
+            const Win C1 = ldwin(src, voff(yc.x), sp), D1 = ldwin(src, voff(yd.x), sp);
+            pair(ya, yb, A1, B1);
+            ya = rec[min(r + 4, rb - 1)];
+            yb = rec[min(r + 5, rb - 1)];
+            A1 = ldwin(src, voff(ya.x), sp);
+            B1 = ldwin(src, voff(yb.x), sp);
+            pair(yc, yd, C1, D1);
+        }
+    }
+    for (; r < rb; ++r) {  // the last run's remainder (< 4 rows)
+        const int2 y = rec[r];
+        const Win w0 = ldwin(src, voff(y.x), 0), w1 = ldwin(src, voff(y.x), sp);
+        if (y.x != cur) hwin(P, w0, t);
+        hwin(Q, w1, t);
+        const uint32_t o = vert_simd(P, Q, (uint32_t)y.y, (uint32_t)y.y >> 16);
+        *reinterpret_cast<uint32_t*>(dst + ho) = o;
+        ho += dp;
+        cur = y.x + 1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) P[k] = Q[k];
+    }
+}
+
+__global__ __launch_bounds__(kPyrThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void pyramid_frame_kernel(Geom g, const int2* __restrict__ yrec,
+                                                                    const int4* __restrict__ ptab,
+                                                                    const uint8_t* __restrict__ img0, size_t row0,
+                                                                    size_t frame0, uint8_t* __restrict__ pyr) {
+    extern __shared__ __attribute__((aligned(16))) int2 s_y[];
+    const int f = blockIdx.x;
+    const int L = g.nlevels;
+    for (int i = threadIdx.x; i < g.pyr_yrec_total; i += kPyrThreads) s_y[i] = yrec[i];
+    QuadTaps tp = quad_taps(g.lv[1], ptab);
+    __syncthreads();
+    for (int l = 1; l < L; ++l) {
+        const LevelGeom& V = g.lv[l];
+        const LevelGeom& Sv = g.lv[l - 1];
+        const uint8_t* src = l == 1 ? img0 + (size_t)f * frame0 : pyr + Sv.offset + (size_t)f * Sv.frame_bytes;
+        const uint32_t sp = l == 1 ? (uint32_t)row0 : (uint32_t)Sv.pitch;
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(src, sp * (uint32_t)Sv.h);
+        uint8_t* dst = pyr + V.offset + (size_t)f * V.frame_bytes;
+        if (tp.mode == 1)
+            frame_rows<false>(rs, sp, V, tp, s_y + V.yrec_offset, dst);
+        else if (tp.mode >= 2)
+            frame_rows<true>(rs, sp, V, tp, s_y + V.yrec_offset, dst);
+        if (l + 1 < L) tp = quad_taps(g.lv[l + 1], ptab);
+        // level l must be in L2 before any wave reads it as level l+1's source
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+}
+
+// Level-0 rows of a work item (one band of one frame) and its record, held
+// in registers between the issue of their loads and their LDS write: the
+// loads of item k+1 are issued right after item k's rows reach LDS and land
+// while item k's levels are computed.
+struct Prefetch {
+    uint4 px[kPyrPre];
+    int4 rec[kPyrPreRec];
+};
+
+__device__ __forceinline__ void prefetch_item(Prefetch& p, const Geom& g, const int4* __restrict__ recs,
+                                              const uint8_t* __restrict__ img0, size_t row0, size_t frame0, int item) {
+    const int S = g.pyr_bands;
+    const int f = item / S, band = item - f * S;
+    const int4* rec = recs + (size_t)band * g.pyr_rec_stride;
+    const int y0 = __builtin_amdgcn_readfirstlane(rec[0].x), y1 = __builtin_amdgcn_readfirstlane(rec[0].y);
+    const int v4 = (g.lv[0].w + 15) >> 4;
+    const int n = (y1 - y0) * v4;
+    const uint8_t* src = img0 + (size_t)f * frame0 + (size_t)y0 * row0;
+    // unconditional loads (an index past the band re-reads chunk 0), so the
+    // registers are written on every path
+    auto ld = [&](int k) {
+        int i = threadIdx.x + k * kPyrThreads;
+        i = i < n ? i : 0;
+        const int r = (int)__umulhi((uint32_t)i, g.lv[0].quad_magic);
+        const int c = i - r * v4;
+        return *reinterpret_cast<const uint4*>(src + (size_t)r * row0 + 16 * c);
+    };
+    static_assert(kPyrPre == 4 && kPyrPreRec == 1, "prefetch is written out for 4 + 1 loads");
+    p.px[0] = ld(0);
+    p.px[1] = ld(1);
+    p.px[2] = ld(2);
+    p.px[3] = ld(3);
+    p.rec[0] = rec[(int)threadIdx.x < g.pyr_rec_stride ? threadIdx.x : 0];
+}
+
+// Persistent blocks: block i processes work items i, i + gridDim.x, ... of
+// the batch (item = frame * pyr_bands + band), so the level-0 staging of the
+// next item overlaps the current item's levels.
 __global__ __launch_bounds__(kPyrThreads) void pyramid_kernel(Geom g, const int4* __restrict__ recs,
                                                               const int4* __restrict__ ptab,
                                                               const uint8_t* __restrict__ img0, size_t row0,
-                                                              size_t frame0, uint8_t* __restrict__ pyr) {
+                                                              size_t frame0, uint8_t* __restrict__ pyr, int items) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_pyr[];
     const int S = g.pyr_bands;
-    const int f = blockIdx.x / S;
-    const int band = blockIdx.x - f * S;
     const int L = g.nlevels;
-    const int4* rec = recs + (size_t)band * g.pyr_rec_stride;
     int4* s_rec = reinterpret_cast<int4*>(s_pyr + g.pyr_lds_y);
-    PYR_STAMP(0);
+    int item = blockIdx.x;
+    Prefetch pf;
+    prefetch_item(pf, g, recs, img0, row0, frame0, item);
     QuadTaps tp = quad_taps(g.lv[1], ptab);
-    // stage: this band's level-0 rows (16-byte loads; row0 is a multiple of
-    // 16) and its record (band entries + per-row source offsets and y taps)
-    {
-        const int4 b = rec[0];
-        const int v4 = (g.lv[0].w + 15) >> 4;
-        const uint8_t* src = img0 + (size_t)f * frame0 + (size_t)b.x * row0;
-        uint8_t* dst = s_pyr + g.pyr_lds_b;
-        const int n = (b.y - b.x) * v4;
-#if PYR_PROBE & 1
-        if (n < 0)
-#endif
-        for (int i = threadIdx.x; i < n; i += kPyrThreads) {
-            const int r = (int)__umulhi((uint32_t)i, g.lv[0].quad_magic);
-            const int c = i - r * v4;
-            *reinterpret_cast<uint4*>(dst + r * g.lv[0].lds_pitch + 16 * c) =
-                *reinterpret_cast<const uint4*>(src + (size_t)r * row0 + 16 * c);
-        }
-        for (int i = threadIdx.x; i < g.pyr_rec_stride; i += kPyrThreads) s_rec[i] = rec[i];
-    }
-    __syncthreads();
-    PYR_STAMP(1);
-    int yoff = L;
-#if PYR_PROBE & 4
-    for (int l = 1; l < 2; ++l) {
-#else
-    for (int l = 1; l < L; ++l) {
-#endif
-        const LevelGeom& V = g.lv[l];
-        const int4 bv = s_rec[l];  // need [x, y), owned [z, w); uniform
-        const int bx = __builtin_amdgcn_readfirstlane(bv.x), by = __builtin_amdgcn_readfirstlane(bv.y);
-        const int bz = __builtin_amdgcn_readfirstlane(bv.z), bw = __builtin_amdgcn_readfirstlane(bv.w);
-        uint8_t* dst_lds = l + 1 < L ? s_pyr + ((l & 1) ? g.pyr_lds_a : g.pyr_lds_b) : nullptr;
-        uint8_t* dst_hbm = pyr + V.offset + (size_t)f * V.frame_bytes;
-        resize_band<WIN>(s_pyr, V, tp, bx, by, bz, bw, s_rec + yoff, dst_lds, dst_hbm);
-        yoff += by - bx;
-#if PYR_PROBE & 8
+    const int v4 = (g.lv[0].w + 15) >> 4;
+    for (; item < items; item += gridDim.x) {
+        PYR_STAMP(0);
+        const int f = item / S;
+        const int band = item - f * S;
+        // this item's level-0 rows and record (band entries + per-row source
+        // offsets and y taps) from the prefetch registers into LDS
         {
-            __builtin_amdgcn_sched_barrier(0);
-            unsigned long long t;
-            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-            __builtin_amdgcn_sched_barrier(0);
-            if ((threadIdx.x & 63) == 0 && blockIdx.x < 8192) g_pyr_wave[(blockIdx.x * 8 + l) * 16 + threadIdx.x / 64] = t;
+            const int4* rec = recs + (size_t)band * g.pyr_rec_stride;
+            const int y0 = __builtin_amdgcn_readfirstlane(rec[0].x), y1 = __builtin_amdgcn_readfirstlane(rec[0].y);
+            const int n = (y1 - y0) * v4;
+            uint8_t* dst = s_pyr + g.pyr_lds_b;
+            auto st = [&](int k, const uint4& v) {
+                const int i = threadIdx.x + k * kPyrThreads;
+                if (i < n) {
+                    const int r = (int)__umulhi((uint32_t)i, g.lv[0].quad_magic);
+                    const int c = i - r * v4;
+                    *reinterpret_cast<uint4*>(dst + r * g.lv[0].lds_pitch + 16 * c) = v;
+                }
+            };
+            st(0, pf.px[0]);
+            st(1, pf.px[1]);
+            st(2, pf.px[2]);
+            st(3, pf.px[3]);
+            if ((int)threadIdx.x < g.pyr_rec_stride) s_rec[threadIdx.x] = pf.rec[0];
         }
-#endif
-        if (l + 1 < L) tp = quad_taps(g.lv[l + 1], ptab);
         __syncthreads();
-        PYR_STAMP(1 + l);
+        if (item + (int)gridDim.x < items) prefetch_item(pf, g, recs, img0, row0, frame0, item + gridDim.x);
+        PYR_STAMP(1);
+        int yoff = L;
+#if PYR_PROBE & 4
+        for (int l = 1; l < 2; ++l) {
+#else
+        for (int l = 1; l < L; ++l) {
+#endif
+            const LevelGeom& V = g.lv[l];
+            const int4 bv = s_rec[l];  // computed rows [x, y) (owned [z, w) plus halo); uniform
+            const int bx = __builtin_amdgcn_readfirstlane(bv.x), by = __builtin_amdgcn_readfirstlane(bv.y);
+            uint8_t* dst_lds = l + 1 < L ? s_pyr + ((l & 1) ? g.pyr_lds_a : g.pyr_lds_b) : nullptr;
+            uint8_t* dst_hbm = pyr + V.offset + (size_t)f * V.frame_bytes;
+            resize_band(s_pyr, V, tp, bx, by, s_rec + yoff, dst_lds, dst_hbm);
+            yoff += by - bx;
+#if PYR_PROBE & 8
+            {
+                __builtin_amdgcn_sched_barrier(0);
+                unsigned long long t;
+                asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+                __builtin_amdgcn_sched_barrier(0);
+                if ((threadIdx.x & 63) == 0 && item < 8192) g_pyr_wave[(item * 8 + l) * 16 + threadIdx.x / 64] = t;
+            }
+#endif
+            tp = quad_taps(g.lv[l + 1 < L ? l + 1 : 1], ptab);
+            __syncthreads();
+            PYR_STAMP(1 + l);
+        }
     }
 }
 
 }  // namespace
 
 int pyr_threads() { return kPyrThreads; }
+int pyr_prefetch_uint4() { return kPyrPre * kPyrThreads; }
+int pyr_prefetch_rec() { return kPyrPreRec * kPyrThreads; }
 
-hipError_t launch_pyramid(const Geom& g, int batch, const int4* recs, const int4* ptab, const uint8_t* img0,
-                          size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream) {
+hipError_t launch_pyramid(const Geom& g, int batch, const int4* recs, const int2* yrec, const int4* ptab,
+                          const uint8_t* img0, size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream) {
     if (g.nlevels < 2) return hipSuccess;
-    if (g.pyr_win)
-        hipLaunchKernelGGL(pyramid_kernel<true>, dim3(g.pyr_bands * batch), dim3(kPyrThreads), g.pyr_lds_bytes,
-                           stream, g, recs, ptab, img0, row0, frame0, pyr);
-    else
-        hipLaunchKernelGGL(pyramid_kernel<false>, dim3(g.pyr_bands * batch), dim3(kPyrThreads), g.pyr_lds_bytes,
-                           stream, g, recs, ptab, img0, row0, frame0, pyr);
+    if (g.pyr_mode == 1) {
+        hipLaunchKernelGGL(pyramid_frame_kernel, dim3(batch), dim3(kPyrThreads), (size_t)g.pyr_yrec_total * sizeof(int2),
+                           stream, g, yrec, ptab, img0, row0, frame0, pyr);
+        return hipGetLastError();
+    }
+    // persistent grid: every resident block slot once (blocks loop over items)
+    static int slots = 0, slots_lds = -1;
+    if (slots_lds != g.pyr_lds_bytes) {
+        int dev = 0, cus = 0, per_cu = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&pyramid_kernel),
+                                                             kPyrThreads, g.pyr_lds_bytes);
+        if (e != hipSuccess) return e;
+        slots = std::max(1, cus * std::max(1, per_cu));
+        slots_lds = g.pyr_lds_bytes;
+    }
+    const int items = g.pyr_bands * batch;
+#ifdef PYR_GRID_ALL
+    slots = items;  // tuning: one block per item
+#endif
+    hipLaunchKernelGGL(pyramid_kernel, dim3(std::min(items, slots)), dim3(kPyrThreads), g.pyr_lds_bytes, stream, g,
+                       recs, ptab, img0, row0, frame0, pyr, items);
     return hipGetLastError();
 }
 
@@ -351,10 +583,7 @@ extern "C" int orbgpu_debug_pyr_stamps(unsigned long long* out, int n) {
 #endif
 
 hipError_t pyramid_set_lds_limit(size_t bytes) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_kernel<true>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    if (e != hipSuccess) return e;
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_kernel<false>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
