@@ -40,6 +40,11 @@ sys.path[:0] = [str(ROOT / "orb-slam2-annotation_amd"), str(ROOT / "oracle")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+PYR_KERNEL_LABEL = {
+    "stream": "pyramid_stream_kernel (one frame per block; source rows staged through LDS per 4-row step)",
+    "frame": "pyramid_frame_kernel (one frame per block; per-lane buffer-load windows)",
+    "band": "pyramid_kernel (frame bands, all levels in LDS)",
+}
 METRIC = "frames/sec ORB extract+match (1000 feat, 640×480 mono) at 1/2/4/8 GPU; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -249,7 +254,8 @@ def main():
         "data": "synthetic",
         "config": {"workload": desc_cfg, "config": args.config, "frames_per_gpu_per_step": B,
                    "width": W, "height": H, "nfeatures": NF, "parallelism": f"frame-sharded x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "pyramid_kernel (fused pass: all levels per frame band)",
+        "roofline": {"bound": "hbm", "kernel": PYR_KERNEL_LABEL.get(os.environ.get("ORBGPU_PYR_MODE", "stream"),
+                                                               PYR_KERNEL_LABEL["stream"]),
                      "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                      "traffic": traffic, "algorithmic_bytes_per_step": pyr_bytes},

@@ -133,6 +133,8 @@ struct orbgpu_extractor {
     int4* d_pyr_bands = nullptr;
     std::vector<int2> pyr_yrec;    // per-row (y0, ibeta0 | ibeta1 << 16) of levels >= 1 (frame kernel)
     int2* d_pyr_yrec = nullptr;
+    std::vector<int> pyr_ystage;   // stream kernel: staged source-row base per (level, step, group)
+    int* d_pyr_ystage = nullptr;
     uint32_t* d_cand = nullptr;
     int* d_cell_counts = nullptr;
     uint32_t* d_gkeys = nullptr;
@@ -158,7 +160,7 @@ struct orbgpu_extractor {
     int last_batch = 0;
 
     ~orbgpu_extractor() {
-        void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_bands, d_pyr_yrec, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
+        void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_bands, d_pyr_yrec, d_pyr_ystage, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
                         d_oct_count, d_err, d_trace, d_img, d_kps1, d_desc1, d_count1};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
@@ -261,7 +263,13 @@ int plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, int max_batch, st
     for (int s = 0; s < S; ++s) {
         const int4* b = &table[(size_t)s * L];
         int4* r = &rec[(size_t)s * stride];
-        for (int l = 0; l < L; ++l) r[l] = b[l];
+        for (int l = 0; l < L; ++l) {
+            r[l] = b[l];
+            // .z = run length of a row group (even), .w unused
+            const int rows = b[l].y - b[l].x, R = l > 0 ? g.lv[l].brgroups : 1;
+            r[l].z = ((rows + R - 1) / R + 1) & ~1;
+            r[l].w = 0;
+        }
         int off = L;
         for (int l = 1; l < L; ++l) {
             const int src_lo = b[l - 1].x, sp = g.lv[l - 1].lds_pitch;
@@ -401,6 +409,15 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
                 v.tail_base = (int)round_up((size_t)qv * R, 64);
             }
 
+            {  // band-kernel layout (pyramid.hip band_taps)
+                const int T = pyr_threads();
+                int R = (T - 64) / v.qmain;
+                while (R > 0 && (int)round_up((size_t)v.qmain * R, 64) + 64 > T) --R;
+                if (R < 1 || R > 64) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid level width outside the band layout");
+                v.brgroups = R;
+                v.bquad_magic = (uint32_t)(((1ull << 32) + v.qmain - 1) / v.qmain);
+                v.btail_base = (int)round_up((size_t)v.qmain * R, 64);
+            }
             if ((size_t)v.pitch * v.h >= (1u << 31)) return fail(ORBGPU_ERR_UNSUPPORTED, "level too large");
             v.ptab_offset = (int)ptab.size();
             v.dbg_level = l;
@@ -460,9 +477,40 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     }
     g.pyr_yrec_total = (int)e->pyr_yrec.size();
     {
-        const char* m = std::getenv("ORBGPU_PYR_MODE");  // tuning/A-B only: "band" selects the LDS-band kernel
-        g.pyr_mode = (m && std::strcmp(m, "band") == 0) ? 0 : 1;
+        const char* m = std::getenv("ORBGPU_PYR_MODE");  // tuning/A-B only: "band" / "frame" select the other kernels
+        g.pyr_mode = (m && std::strcmp(m, "band") == 0) ? 0 : (m && std::strcmp(m, "frame") == 0) ? 1 : 2;
     }
+    // stream kernel (pyramid.hip): row group g of level l owns rows
+    // [g*run, (g+1)*run); step k covers 4 of them, whose source rows are the
+    // 6 rows from ystage[k][g] of the previous level, staged in LDS.
+    e->pyr_ystage.clear();
+    g.pyr_stage_bytes = 0;
+    for (int l = 1; l < L; ++l) {
+        LevelGeom& v = g.lv[l];
+        const LevelGeom& sv = g.lv[l - 1];
+        const int R = v.rgroups;
+        v.pyr_run = ((v.h + R - 1) / R + 3) & ~3;
+        v.pyr_steps = v.pyr_run / 4;
+        v.ystage_offset = (int)e->pyr_ystage.size();
+        const int2* yr = &e->pyr_yrec[(size_t)v.yrec_offset];
+        for (int k = 0; k < v.pyr_steps; ++k)
+            for (int gr = 0; gr < R; ++gr) {
+                const int o0 = gr * v.pyr_run + 4 * k;
+                if (o0 >= v.h) { e->pyr_ystage.push_back(0); continue; }
+                const int o1 = std::min(o0 + 3, v.h - 1);
+                const int ys = yr[o0].x;
+                if (yr[o1].x + 1 - ys > 5) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid step spans more than 6 source rows");
+                e->pyr_ystage.push_back(ys);
+            }
+        const int bytes = R * 6 * sv.pitch;
+        if (R * 6 * (sv.pitch / 16) > 2 * pyr_threads())
+            return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid staging exceeds two chunks per thread");
+        g.pyr_stage_bytes = std::max(g.pyr_stage_bytes, bytes);
+    }
+    g.pyr_ystage_total = (int)e->pyr_ystage.size();
+    g.pyr_lds_stage = (int)round_up((size_t)g.pyr_yrec_total * 8 + (size_t)g.pyr_ystage_total * 4, 16);
+    if (g.pyr_mode == 2 && g.pyr_lds_stage + 2 * g.pyr_stage_bytes > 80 * 1024)
+        return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid stream kernel needs more than 80 KiB of LDS");
     if (g.pyr_mode == 0) {
         int rc = plan_pyramid_bands(g, ytab, e->max_batch, e->pyr_bands);
         if (rc) return rc;
@@ -525,7 +573,7 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
         evs = e->ev[e->ev_used++].data();
         ORB_HIP(hipEventRecord(evs[0], s));
     }
-    ORB_HIP(launch_pyramid(g, batch, e->d_pyr_bands, e->d_pyr_yrec, e->d_ptab, imgs, row_step, frame_step, e->d_pyr, s));
+    ORB_HIP(launch_pyramid(g, batch, e->d_pyr_bands, e->d_pyr_yrec, e->d_pyr_ystage, e->d_ptab, imgs, row_step, frame_step, e->d_pyr, s));
     if (evs) ORB_HIP(hipEventRecord(evs[1], s));
     ORB_HIP(launch_fast_cells(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_cand, e->d_cell_counts, e->d_err, s));
     if (evs) ORB_HIP(hipEventRecord(evs[2], s));
@@ -611,7 +659,8 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
         (rc = dalloc(&e->d_oct_count, (size_t)g.nlevels * B)) || (rc = dalloc(&e->d_err, 1)) ||
         (rc = dalloc(&e->d_img, e->img_pitch * height)) || (rc = dalloc(&e->d_kps1, (size_t)e->max_kps)) ||
         (rc = dalloc(&e->d_desc1, (size_t)e->max_kps * 32)) || (rc = dalloc(&e->d_count1, 1)) ||
-        (rc = dalloc(&e->d_pyr_bands, e->pyr_bands.size())) || (rc = dalloc(&e->d_pyr_yrec, e->pyr_yrec.size()))) {
+        (rc = dalloc(&e->d_pyr_bands, e->pyr_bands.size())) || (rc = dalloc(&e->d_pyr_yrec, e->pyr_yrec.size())) ||
+        (rc = dalloc(&e->d_pyr_ystage, e->pyr_ystage.size()))) {
         delete e;
         return rc;
     }
@@ -620,7 +669,9 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
             hipSuccess ||
         (!e->pyr_yrec.empty() && hipMemcpy(e->d_pyr_yrec, e->pyr_yrec.data(), e->pyr_yrec.size() * sizeof(int2),
                                            hipMemcpyHostToDevice) != hipSuccess) ||
-        (g.pyr_mode == 0 && pyramid_set_lds_limit((size_t)g.pyr_lds_bytes) != hipSuccess) ||
+        (!e->pyr_ystage.empty() && hipMemcpy(e->d_pyr_ystage, e->pyr_ystage.data(), e->pyr_ystage.size() * sizeof(int),
+                                             hipMemcpyHostToDevice) != hipSuccess) ||
+        pyramid_set_lds_limit(g) != hipSuccess ||
         hipMemset(e->d_err, 0, sizeof(int)) != hipSuccess ||
         hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         delete e;

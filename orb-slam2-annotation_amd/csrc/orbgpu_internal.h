@@ -65,6 +65,12 @@ struct LevelGeom {
     int rgroups;              // row groups of a pyramid block (pyramid.hip quad_taps)
     int tail_base;            // first thread of the tail quads (a wave boundary)
     int yrec_offset;          // first row record of this level (pyramid_frame_kernel)
+    int brgroups;             // band kernel: row groups (quads 0..qmain-1 per group)
+    uint32_t bquad_magic;     // band kernel: ceil(2^32 / qmain)
+    int btail_base;           // band kernel: first thread of the tail wave (lane = row group)
+    int pyr_run;              // stream/frame kernels: output rows per row group (a multiple of 4)
+    int pyr_steps;            // stream kernel: 4-row steps per level (pyr_run / 4)
+    int ystage_offset;        // stream kernel: first staged-row base of this level ([step][group])
     // blurred level (all levels, incl. 0): same row pitch as the pyramid
     size_t blur_offset, blur_frame_bytes;
     int blur_tiles_x, blur_tile_base;   // blur work items: 4-column x 64-row strips
@@ -85,8 +91,11 @@ struct Geom {
     int pyr_bands;
     int pyr_lds_a, pyr_lds_b, pyr_lds_y, pyr_lds_bytes;  // odd levels, even levels (incl. 0), y taps
     int pyr_rec_stride;       // int4s per band record (band entries + per-row source offsets)
-    int pyr_mode;             // 0: band kernel (levels through LDS), 1: frame kernel (levels through L2)
+    int pyr_mode;             // 0: band kernel (levels through LDS), 1: frame kernel (levels through L2), 2: stream kernel
     int pyr_yrec_total;       // row records of all levels >= 1 (frame kernel)
+    int pyr_ystage_total;     // stream kernel: staged-row bases of all levels
+    int pyr_stage_bytes;      // stream kernel: bytes of one staging buffer (max over levels)
+    int pyr_lds_stage;        // stream kernel: LDS offset of the staging buffers (after the row tables)
     LevelGeom lv[kMaxLevels];
 };
 

@@ -14,9 +14,10 @@ int pyr_prefetch_rec();    // int4s a band record may hold
 // per band = (need_lo, need_hi, own_lo, own_hi) rows per level, then one
 // (src0 LDS offset, src1 LDS offset, ibeta0 << 12, ibeta1 << 12) per computed
 // row of levels 1..L-1 (plan_pyramid_bands)
-hipError_t launch_pyramid(const Geom& g, int batch, const int4* recs, const int2* yrec, const int4* ptab,
+hipError_t launch_pyramid(const Geom& g, int batch, const int4* recs, const int2* yrec, const int* ystage, const int4* ptab,
                           const uint8_t* img0, size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream);
-hipError_t pyramid_set_lds_limit(size_t bytes);
+hipError_t pyramid_set_lds_limit(const Geom& g);
+int pyr_stream_lds_bytes(const Geom& g);
 
 hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                              const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err,

@@ -35,16 +35,15 @@ namespace orbgpu {
 namespace {
 
 #ifndef PYR_PROBE
-#define PYR_PROBE 0  // timing probes for tuning only (tools/pyr_variants.sh): bit 0 = no level-0 loads, bit 2 = level 1 only, bit 3 = phase stamps, bit 5 = no HBM stores in the row loop; 0 = the product
+#define PYR_PROBE 0  // timing probes for tuning only (tools/pyr_variants.sh): bit 0 = no level-0 loads, bit 2 = level 1 only, bit 3 = phase stamps, bit 5 = no HBM stores in the row loop, bit 6 = no window loads (frame kernel), bit 7 = no store drain before the level barrier (frame kernel, wrong results), bit 8 = band kernel setup only (no rows); 0 = the product
 #endif
 #ifndef PYR_THREADS
 #define PYR_THREADS 1024
 #endif
 constexpr int kPyrThreads = PYR_THREADS;
-#ifndef PYR_MINRUN
-#define PYR_MINRUN 1
+#ifndef PYR_WAVES_EU
+#define PYR_WAVES_EU 8  // frame kernel: waves per SIMD the register budget is sized for
 #endif
-constexpr int kPyrMinRun = PYR_MINRUN;
 constexpr int kPyrPre = 4;     // level-0 uint4 loads per thread per item (host checks the band fits)
 constexpr int kPyrPreRec = 1;  // record int4 per thread per item (host checks pyr_rec_stride <= threads)
 
@@ -178,12 +177,51 @@ __device__ __forceinline__ QuadTaps quad_taps(const LevelGeom& V, const int4* __
     return tp;
 }
 
-// One level's band rows [r0, r1).  s_rows[r - r0] = (LDS offset of source
-// row y0, of y1, ibeta0, ibeta1).  Stores go to the next level's LDS buffer
-// (lds_dst, if any) and to HBM.
+// Band-kernel thread layout of a level: quads 0 .. qmain-1 (the first quad's
+// window may start before the row: the LDS row buffers have 16 bytes in
+// front) fill threads [0, qmain * brgroups), row group rg = t / qmain; the
+// scalar-tail quad of row group rg is lane rg of the wave at btail_base, so
+// it walks the same run of rows as its group.
+__device__ __forceinline__ QuadTaps band_taps(const LevelGeom& V, const int4* __restrict__ ptab) {
+    QuadTaps tp;
+    const int t = threadIdx.x;
+    tp.mode = 0;
+    tp.q = 0;
+    tp.rg = 0;
+    if (t < V.qmain * V.brgroups) {
+        tp.rg = (int)__umulhi((uint32_t)t, V.bquad_magic);
+        tp.q = t - tp.rg * V.qmain;
+        tp.mode = 1;
+    } else if (t >= V.btail_base && t < V.btail_base + V.brgroups && 4 * V.qmain < V.w) {
+        tp.rg = t - V.btail_base;
+        tp.q = V.qmain;
+        tp.mode = 3;
+    }
+    if (tp.mode) {
+        const int4* pt = ptab + V.ptab_offset + 3 * tp.q;
+        tp.a = pt[0];
+        tp.b = pt[1];
+        tp.c = pt[2];
+    }
+    return tp;
+}
+
+// One level's band rows [r0, r1) in runs of n rows per row group (n even,
+// from the band record).  s_rows[r - r0] = (LDS offset of source row y0, of
+// y1, ibeta0, ibeta1).  Stores go to the next level's LDS buffer (lds_dst, if
+// any) and to HBM: every computed row, halo rows included -- a halo row is
+// also an owned row of the neighbouring band, computed there from the same
+// source rows with the same arithmetic, so the two writes carry identical
+// bytes.  Bytes past V.w land in the row padding (LDS pitch and HBM pitch are
+// multiples of 4 and 16).
+//
+// Rows of a ~1.2x downscale share source rows (y0 of row r+1 is mostly y1 of
+// row r), so the last source row's sums stay in registers: about 1.2
+// horizontal passes per output row.  Unrolled by two with the roles of P and
+// Q swapped, so the carried row needs no register moves.
 template <bool TAIL>
 __device__ __forceinline__ void resize_rows(const uint8_t* __restrict__ lds, const LevelGeom& V, const QuadTaps& tp,
-                                            int r0, int r1, const int4* __restrict__ s_rows,
+                                            int r0, int r1, int n, const int4* __restrict__ s_rows,
                                             uint8_t* __restrict__ lds_dst, uint8_t* __restrict__ hbm_dst) {
     Taps t;
     t.w0 = tp.a.x;
@@ -191,35 +229,16 @@ __device__ __forceinline__ void resize_rows(const uint8_t* __restrict__ lds, con
     t.sel[0] = tp.b.y; t.sel[1] = tp.b.z; t.sel[2] = tp.b.w; t.sel[3] = tp.c.x;
     const int q = tp.q;
     uint32_t P[4], Q[4];
-    // Every computed row goes to HBM, halo rows included: a halo row is also
-    // an owned row of the neighbouring band, computed there from the same
-    // source rows with the same arithmetic, so the two writes carry identical
-    // bytes.  Bytes past V.w land in the row padding (LDS pitch and HBM pitch
-    // are multiples of 4 and 16).
     const uint32_t lpitch = (uint32_t)V.lds_pitch, hpitch = (uint32_t)V.pitch;
-    if (TAIL) {  // edge wave: one row per lane, first quad (mode 2) or scalar tail (mode 3)
-        for (int r = r0 + tp.rg; r < r1; r += 32) {
-            const int4 y = s_rows[r - r0];
-            hrow(P, lds, t, y.x);
-            hrow(Q, lds, t, y.y);
-            const uint32_t out = tp.mode == 2 ? vert_simd(P, Q, (uint32_t)y.z, (uint32_t)y.w)
-                                              : vert_tail(P, Q, (uint32_t)y.z, (uint32_t)y.w);
-            if (lds_dst) *reinterpret_cast<uint32_t*>(lds_dst + __umul24((uint32_t)(r - r0), lpitch) + 4 * q) = out;
-            *reinterpret_cast<uint32_t*>(hbm_dst + __umul24((uint32_t)r, hpitch) + 4 * q) = out;
-        }
-        return;
-    }
-    // Row group rg owns the run [ra, rb) of consecutive output rows.  Rows of
-    // a ~1.2x downscale share source rows (y0 of row r+1 is mostly y1 of row
-    // r), so the last source row's sums stay in registers: about 1.2
-    // horizontal passes per output row.  Unrolled by two with the roles of P
-    // and Q swapped, so the carried row needs no register moves; runs are of
-    // even length (only the last one can be odd) and at least kPyrMinRun rows.
-    const int rows = r1 - r0;
-    const int R = min(V.rgroups, (rows + kPyrMinRun - 1) / kPyrMinRun);
-    const int n = (((rows + R - 1) / R) + 1) & ~1;
-    if (tp.rg >= R) return;
+    auto vert = [&](const uint32_t (&a)[4], const uint32_t (&b)[4], const int4& y) {
+        return TAIL ? vert_tail(a, b, (uint32_t)y.z, (uint32_t)y.w) : vert_simd(a, b, (uint32_t)y.z, (uint32_t)y.w);
+    };
+#if PYR_PROBE & 256
+    const int ra = r0 + tp.rg * n, rb = ra + (((int)lpitch) >> 20);  // timing probe: setup only, no rows
+#else
     const int ra = r0 + tp.rg * n, rb = min(ra + n, r1);
+#endif
+    if (ra >= rb) return;
     uint8_t* lp = lds_dst ? lds_dst + __umul24((uint32_t)(ra - r0), lpitch) + 4 * q : nullptr;
     uint8_t* hp = hbm_dst + __umul24((uint32_t)ra, hpitch) + 4 * q;
     const int4* rec = s_rows + (ra - r0);
@@ -231,10 +250,10 @@ __device__ __forceinline__ void resize_rows(const uint8_t* __restrict__ lds, con
         rec += 2;
         if (y.x != cur) hrow(P, lds, t, y.x);
         hrow(Q, lds, t, y.y);
-        const uint32_t o0 = vert_simd(P, Q, (uint32_t)y.z, (uint32_t)y.w);
+        const uint32_t o0 = vert(P, Q, y);
         if (z.x != y.y) hrow(Q, lds, t, z.x);
         hrow(P, lds, t, z.y);
-        const uint32_t o1 = vert_simd(Q, P, (uint32_t)z.z, (uint32_t)z.w);
+        const uint32_t o1 = vert(Q, P, z);
         cur = z.y;
         if (lp) {
             *reinterpret_cast<uint32_t*>(lp) = o0;
@@ -251,19 +270,19 @@ __device__ __forceinline__ void resize_rows(const uint8_t* __restrict__ lds, con
         const int4 y = rec[0];
         if (y.x != cur) hrow(P, lds, t, y.x);
         hrow(Q, lds, t, y.y);
-        const uint32_t o0 = vert_simd(P, Q, (uint32_t)y.z, (uint32_t)y.w);
+        const uint32_t o0 = vert(P, Q, y);
         if (lp) *reinterpret_cast<uint32_t*>(lp) = o0;
         *reinterpret_cast<uint32_t*>(hp) = o0;
     }
 }
 
 __device__ __forceinline__ void resize_band(const uint8_t* __restrict__ lds, const LevelGeom& V, const QuadTaps& tp,
-                                            int r0, int r1, const int4* __restrict__ s_rows,
+                                            int r0, int r1, int n, const int4* __restrict__ s_rows,
                                             uint8_t* __restrict__ lds_dst, uint8_t* __restrict__ hbm_dst) {
     if (tp.mode == 1)
-        resize_rows<false>(lds, V, tp, r0, r1, s_rows, lds_dst, hbm_dst);
-    else if (tp.mode >= 2)
-        resize_rows<true>(lds, V, tp, r0, r1, s_rows, lds_dst, hbm_dst);
+        resize_rows<false>(lds, V, tp, r0, r1, n, s_rows, lds_dst, hbm_dst);
+    else if (tp.mode == 3)
+        resize_rows<true>(lds, V, tp, r0, r1, n, s_rows, lds_dst, hbm_dst);
 }
 
 // ---------------------------------------------------------------------------
@@ -288,8 +307,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
 }
 
 __device__ __forceinline__ Win ldwin(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
+#if PYR_PROBE & 64
+    return Win{voff, voff ^ soff, voff + soff};  // timing probe: no window loads
+#else
     const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)voff, (int)soff, 0);
     return Win{v.x, v.y, v.z};
+#endif
 }
 
 // hrow() on a window already in registers
@@ -399,7 +422,7 @@ __device__ __forceinline__ void frame_rows(__amdgpu_buffer_rsrc_t src, uint32_t 
     }
 }
 
-__global__ __launch_bounds__(kPyrThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void pyramid_frame_kernel(Geom g, const int2* __restrict__ yrec,
+__global__ __launch_bounds__(kPyrThreads) __attribute__((amdgpu_waves_per_eu(PYR_WAVES_EU, PYR_WAVES_EU))) void pyramid_frame_kernel(Geom g, const int2* __restrict__ yrec,
                                                                     const int4* __restrict__ ptab,
                                                                     const uint8_t* __restrict__ img0, size_t row0,
                                                                     size_t frame0, uint8_t* __restrict__ pyr) {
@@ -422,6 +445,186 @@ __global__ __launch_bounds__(kPyrThreads) __attribute__((amdgpu_waves_per_eu(8, 
             frame_rows<true>(rs, sp, V, tp, s_y + V.yrec_offset, dst);
         if (l + 1 < L) tp = quad_taps(g.lv[l + 1], ptab);
         // level l must be in L2 before any wave reads it as level l+1's source
+#if !(PYR_PROBE & 128)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Stream form (pyramid_stream_kernel, the default): one 1024-thread block per
+// frame, as the frame kernel, but the source rows reach the row groups through
+// LDS: row group g of level l owns output rows [g*run, (g+1)*run) and walks
+// them in steps of 4; before step k the block stages, for every group, the 6
+// source rows that group's 4 rows read (ystage[k][g] onwards), with
+// coalesced 16-byte buffer loads -- 1 KiB per load instruction instead of one
+// 12-byte window per lane -- double-buffered one step ahead.  The rows stay
+// long runs (the carried source row in registers, no halo), and a level is
+// read back from L2/MALL once, by whole-row loads.  The edge wave (first quad
+// and scalar-tail quad of every row) reads its windows straight from memory.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint4 ld16(__amdgpu_buffer_rsrc_t rs, uint32_t voff) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff, 0, 0);
+    return uint4{v.x, v.y, v.z, v.w};
+}
+
+// edge rows [r0, r1) of one level: first quad (mode 2) / scalar tail (mode 3),
+// one row per lane of the half-wave, windows from memory
+__device__ __forceinline__ void edge_rows(__amdgpu_buffer_rsrc_t src, uint32_t sp, const LevelGeom& V,
+                                          const QuadTaps& tp, const int2* __restrict__ rec, uint8_t* __restrict__ dst,
+                                          int r0, int r1) {
+    Taps t;
+    t.w0 = tp.a.x;
+    t.wt[0] = tp.a.y; t.wt[1] = tp.a.z; t.wt[2] = tp.a.w; t.wt[3] = tp.b.x;
+    t.sel[0] = tp.b.y; t.sel[1] = tp.b.z; t.sel[2] = tp.b.w; t.sel[3] = tp.c.x;
+    const uint32_t dp = (uint32_t)V.pitch;
+    const uint32_t q4 = 4u * (uint32_t)tp.q;
+    uint32_t P[4], Q[4];
+    // the first quad's window starts at w0 = -4 or -8: on row 0 that is before
+    // the level, where a buffer load returns zeros for all three dwords, so
+    // the load starts at 0 and the dwords move up instead
+    auto ld = [&](int o) {
+        Win w = ldwin(src, (uint32_t)max(o, 0), 0);
+        if (o == -4) {
+            w.d2 = w.d1; w.d1 = w.d0; w.d0 = 0;
+        } else if (o == -8) {
+            w.d2 = w.d0; w.d1 = 0; w.d0 = 0;
+        }
+        return w;
+    };
+    for (int r = r0 + tp.rg; r < r1; r += 32) {
+        const int2 y = rec[r];
+        const int o = (int)(__umul24((uint32_t)y.x, sp) + (uint32_t)t.w0);
+        const Win w0 = ld(o), w1 = ld(o + (int)sp);
+        hwin(P, w0, t);
+        hwin(Q, w1, t);
+        const uint32_t out = tp.mode == 2 ? vert_simd(P, Q, (uint32_t)y.y, (uint32_t)y.y >> 16)
+                                          : vert_tail(P, Q, (uint32_t)y.y & 0xFFFFu, (uint32_t)y.y >> 16);
+        *reinterpret_cast<uint32_t*>(dst + __umul24((uint32_t)r, dp) + q4) = out;
+    }
+}
+
+__global__ __launch_bounds__(kPyrThreads) __attribute__((amdgpu_waves_per_eu(PYR_WAVES_EU, PYR_WAVES_EU))) void
+pyramid_stream_kernel(Geom g, const int2* __restrict__ yrec, const int* __restrict__ ystage,
+                      const int4* __restrict__ ptab, const uint8_t* __restrict__ img0, size_t row0, size_t frame0,
+                      uint8_t* __restrict__ pyr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_mem[];
+    int2* s_y = reinterpret_cast<int2*>(s_mem);
+    int* s_ys = reinterpret_cast<int*>(s_mem + (size_t)g.pyr_yrec_total * sizeof(int2));
+    uint8_t* s_buf = s_mem + g.pyr_lds_stage;
+    const int f = blockIdx.x;
+    const int L = g.nlevels;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < g.pyr_yrec_total; i += kPyrThreads) s_y[i] = yrec[i];
+    for (int i = tid; i < g.pyr_ystage_total; i += kPyrThreads) s_ys[i] = ystage[i];
+    QuadTaps tp = quad_taps(g.lv[1], ptab);
+    __syncthreads();
+    const uint32_t SB = (uint32_t)g.pyr_stage_bytes;
+    for (int l = 1; l < L; ++l) {
+        const LevelGeom& V = g.lv[l];
+        const LevelGeom& Sv = g.lv[l - 1];
+        const uint8_t* src = l == 1 ? img0 + (size_t)f * frame0 : pyr + Sv.offset + (size_t)f * Sv.frame_bytes;
+        const uint32_t spg = l == 1 ? (uint32_t)row0 : (uint32_t)Sv.pitch;  // source pitch in memory
+        const uint32_t lp = (uint32_t)Sv.pitch;                              // staged pitch in LDS
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(src, spg * (uint32_t)Sv.h);
+        uint8_t* dst = pyr + V.offset + (size_t)f * V.frame_bytes;
+        const int2* rec = s_y + V.yrec_offset;
+        const int* ysl = s_ys + V.ystage_offset;
+        const int R = V.rgroups, S = V.pyr_steps, run = V.pyr_run, h = V.h;
+        // this thread's two staging chunks: (group, row j, 16-byte column c)
+        const int cpr = (int)(lp >> 4), pg = 6 * cpr, total = R * pg;
+        int sg[2], sgo[2], slo[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = tid + u * kPyrThreads;
+            const int gi = i / pg, rem = i - gi * pg, j = rem / cpr, c = rem - j * cpr;
+            sg[u] = i < total ? gi : -1;
+            sgo[u] = (int)(__umul24((uint32_t)j, spg) + 16u * (uint32_t)c);
+            slo[u] = (int)((uint32_t)(gi * 6 + j) * lp + 16u * (uint32_t)c);
+        }
+        auto gload = [&](int k, int u) {
+            uint4 v = uint4{0, 0, 0, 0};
+            if (sg[u] >= 0) v = ld16(rs, __umul24((uint32_t)ysl[k * R + sg[u]], spg) + (uint32_t)sgo[u]);
+            return v;
+        };
+        auto lstore = [&](int k, int u, const uint4& v) {
+            if (sg[u] >= 0) *reinterpret_cast<uint4*>(s_buf + (uint32_t)(k & 1) * SB + (uint32_t)slo[u]) = v;
+        };
+        {
+            const uint4 a = gload(0, 0), b = gload(0, 1);
+            lstore(0, 0, a);
+            lstore(0, 1, b);
+        }
+        __syncthreads();
+        // compute state
+        Taps t;
+        t.w0 = tp.a.x;
+        t.wt[0] = tp.a.y; t.wt[1] = tp.a.z; t.wt[2] = tp.a.w; t.wt[3] = tp.b.x;
+        t.sel[0] = tp.b.y; t.sel[1] = tp.b.z; t.sel[2] = tp.b.w; t.sel[3] = tp.c.x;
+        const uint32_t dp = (uint32_t)V.pitch;
+        const int rg = tp.rg;
+        const bool vec = tp.mode == 1 && rg * run < h;
+        const int rend = min(rg * run + run, h);
+        uint32_t ho = __umul24((uint32_t)(rg * run), dp) + 4u * (uint32_t)tp.q;
+        uint32_t P[4], Q[4];
+        int cur = -1;
+        const int E = (h + S - 1) / S;  // edge rows per step
+        for (int k = 0; k < S; ++k) {
+            uint4 na = uint4{0, 0, 0, 0}, nb = uint4{0, 0, 0, 0};
+            if (k + 1 < S) {
+                na = gload(k + 1, 0);
+                nb = gload(k + 1, 1);
+            }
+            if (vec) {
+                const int o0 = rg * run + 4 * k;
+                if (o0 < rend) {
+                    const int ys = ysl[k * R + rg];
+                    // LDS offset of staged row 0 of this group, minus ys rows
+                    const int base = (int)((uint32_t)(k & 1) * SB + (uint32_t)(rg * 6) * lp) - ys * (int)lp;
+                    auto row = [&](int y) { return base + y * (int)lp; };
+#pragma unroll
+                    for (int j = 0; j < 4; j += 2) {
+                        const int o = o0 + j;
+                        if (o < rend) {
+                            const int2 ya = rec[o];
+                            if (ya.x != cur) hrow(P, s_buf, t, row(ya.x));
+                            hrow(Q, s_buf, t, row(ya.x + 1));
+                            const uint32_t out0 = vert_simd(P, Q, (uint32_t)ya.y, (uint32_t)ya.y >> 16);
+#if !(PYR_PROBE & 32)
+                            *reinterpret_cast<uint32_t*>(dst + ho) = out0;
+#endif
+                            ho += dp;
+                            cur = ya.x + 1;
+                            if (o + 1 < rend) {
+                                const int2 yb = rec[o + 1];
+                                if (yb.x != cur) hrow(Q, s_buf, t, row(yb.x));
+                                hrow(P, s_buf, t, row(yb.x + 1));
+                                const uint32_t out1 = vert_simd(Q, P, (uint32_t)yb.y, (uint32_t)yb.y >> 16);
+#if !(PYR_PROBE & 32)
+                                *reinterpret_cast<uint32_t*>(dst + ho) = out1;
+#endif
+                                ho += dp;
+                                cur = yb.x + 1;
+                            } else {
+#pragma unroll
+                                for (int m = 0; m < 4; ++m) P[m] = Q[m];
+                            }
+                        }
+                    }
+                }
+            } else if (tp.mode >= 2) {
+                edge_rows(rs, spg, V, tp, rec, dst, k * E, min(k * E + E, h));
+            }
+            if (k + 1 < S) {
+                lstore(k + 1, 0, na);
+                lstore(k + 1, 1, nb);
+            }
+            __syncthreads();
+        }
+        tp = quad_taps(g.lv[l + 1 < L ? l + 1 : 1], ptab);
+        // level l must be in L2 before the next level stages it
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
@@ -465,7 +668,7 @@ __device__ __forceinline__ void prefetch_item(Prefetch& p, const Geom& g, const 
 // Persistent blocks: block i processes work items i, i + gridDim.x, ... of
 // the batch (item = frame * pyr_bands + band), so the level-0 staging of the
 // next item overlaps the current item's levels.
-__global__ __launch_bounds__(kPyrThreads) void pyramid_kernel(Geom g, const int4* __restrict__ recs,
+__global__ __launch_bounds__(kPyrThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void pyramid_kernel(Geom g, const int4* __restrict__ recs,
                                                               const int4* __restrict__ ptab,
                                                               const uint8_t* __restrict__ img0, size_t row0,
                                                               size_t frame0, uint8_t* __restrict__ pyr, int items) {
@@ -476,7 +679,7 @@ __global__ __launch_bounds__(kPyrThreads) void pyramid_kernel(Geom g, const int4
     int item = blockIdx.x;
     Prefetch pf;
     prefetch_item(pf, g, recs, img0, row0, frame0, item);
-    QuadTaps tp = quad_taps(g.lv[1], ptab);
+    QuadTaps tp = band_taps(g.lv[1], ptab);
     const int v4 = (g.lv[0].w + 15) >> 4;
     for (; item < items; item += gridDim.x) {
         PYR_STAMP(0);
@@ -513,11 +716,12 @@ __global__ __launch_bounds__(kPyrThreads) void pyramid_kernel(Geom g, const int4
         for (int l = 1; l < L; ++l) {
 #endif
             const LevelGeom& V = g.lv[l];
-            const int4 bv = s_rec[l];  // computed rows [x, y) (owned [z, w) plus halo); uniform
+            const int4 bv = s_rec[l];  // computed rows [x, y) (owned rows plus halo), run length z; uniform
             const int bx = __builtin_amdgcn_readfirstlane(bv.x), by = __builtin_amdgcn_readfirstlane(bv.y);
+            const int bn = __builtin_amdgcn_readfirstlane(bv.z);
             uint8_t* dst_lds = l + 1 < L ? s_pyr + ((l & 1) ? g.pyr_lds_a : g.pyr_lds_b) : nullptr;
             uint8_t* dst_hbm = pyr + V.offset + (size_t)f * V.frame_bytes;
-            resize_band(s_pyr, V, tp, bx, by, s_rec + yoff, dst_lds, dst_hbm);
+            resize_band(s_pyr, V, tp, bx, by, bn, s_rec + yoff, dst_lds, dst_hbm);
             yoff += by - bx;
 #if PYR_PROBE & 8
             {
@@ -528,7 +732,7 @@ __global__ __launch_bounds__(kPyrThreads) void pyramid_kernel(Geom g, const int4
                 if ((threadIdx.x & 63) == 0 && item < 8192) g_pyr_wave[(item * 8 + l) * 16 + threadIdx.x / 64] = t;
             }
 #endif
-            tp = quad_taps(g.lv[l + 1 < L ? l + 1 : 1], ptab);
+            tp = band_taps(g.lv[l + 1 < L ? l + 1 : 1], ptab);
             __syncthreads();
             PYR_STAMP(1 + l);
         }
@@ -541,9 +745,14 @@ int pyr_threads() { return kPyrThreads; }
 int pyr_prefetch_uint4() { return kPyrPre * kPyrThreads; }
 int pyr_prefetch_rec() { return kPyrPreRec * kPyrThreads; }
 
-hipError_t launch_pyramid(const Geom& g, int batch, const int4* recs, const int2* yrec, const int4* ptab,
+hipError_t launch_pyramid(const Geom& g, int batch, const int4* recs, const int2* yrec, const int* ystage, const int4* ptab,
                           const uint8_t* img0, size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream) {
     if (g.nlevels < 2) return hipSuccess;
+    if (g.pyr_mode == 2) {
+        hipLaunchKernelGGL(pyramid_stream_kernel, dim3(batch), dim3(kPyrThreads), (size_t)pyr_stream_lds_bytes(g),
+                           stream, g, yrec, ystage, ptab, img0, row0, frame0, pyr);
+        return hipGetLastError();
+    }
     if (g.pyr_mode == 1) {
         hipLaunchKernelGGL(pyramid_frame_kernel, dim3(batch), dim3(kPyrThreads), (size_t)g.pyr_yrec_total * sizeof(int2),
                            stream, g, yrec, ptab, img0, row0, frame0, pyr);
@@ -582,9 +791,16 @@ extern "C" int orbgpu_debug_pyr_stamps(unsigned long long* out, int n) {
 }
 #endif
 
-hipError_t pyramid_set_lds_limit(size_t bytes) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+int pyr_stream_lds_bytes(const Geom& g) { return g.pyr_lds_stage + 2 * g.pyr_stage_bytes; }
+
+hipError_t pyramid_set_lds_limit(const Geom& g) {
+    if (g.pyr_mode == 0)
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, g.pyr_lds_bytes);
+    if (g.pyr_mode == 2)
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_stream_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, pyr_stream_lds_bytes(g));
+    return hipSuccess;
 }
 
 }  // namespace orbgpu

@@ -17,7 +17,7 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent))
 from pmc_summary import load  # noqa: E402
 
-KERNEL = "pyramid_kernel"  # matched as a prefix: the kernel is a template (pyramid_kernel<WIN>)
+KERNEL = "pyramid"  # matched as a prefix: pyramid_stream_kernel / pyramid_frame_kernel / pyramid_kernel
 
 
 def main():

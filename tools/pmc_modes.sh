@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
 rm -f gpurun_out/pmc_modes.txt
-for m in frame band; do
+for m in ${MODES:-frame band}; do
     export ORBGPU_PYR_MODE=$m
     timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY --output-format csv -d gpurun_out/m1_$m -o q1 -- $B > gpurun_out/m1_$m.log 2>&1
     timeout -k 10 120 rocprofv3 --pmc SQ_BUSY_CU_CYCLES SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_INSTS_SMEM GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d gpurun_out/m2_$m -o q2 -- $B > gpurun_out/m2_$m.log 2>&1
