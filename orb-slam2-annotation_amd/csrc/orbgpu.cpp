@@ -23,8 +23,10 @@
 
 #include "../../include/orbgpu.h"
 #include "../../include/orbgpu_debug.h"
+#include "../../include/orbgpu_stereo.h"
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
+#include "stereo_kernels.h"
 #include "host_common.h"
 
 using namespace orbgpu;
@@ -950,3 +952,47 @@ int orbgpu_debug_level_octree(orbgpu_extractor* e, int frame, int level, int* xy
 }
 
 }  // extern "C"
+
+// Frame::ComputeStereoMatches (Frame.cpp:540-748) over the last extraction.
+int orbgpu_stereo_matches_batch_device(orbgpu_extractor* e, const uint8_t* d_images, size_t row_step,
+                                       size_t frame_step, int npairs, const orbgpu_keypoint* d_kps,
+                                       const uint8_t* d_desc, const int* d_counts, int kp_capacity, float bf,
+                                       float min_z, float* d_uright, float* d_depth, void* stream) {
+    if (!e || !d_images || !d_kps || !d_desc || !d_counts || !d_uright || !d_depth)
+        return fail(ORBGPU_ERR_ARG, "NULL argument");
+    if (npairs < 0 || 2 * npairs > e->max_batch) return fail(ORBGPU_ERR_ARG, "npairs exceeds max_batch / 2");
+    if (kp_capacity < e->max_kps || kp_capacity > 65535)
+        return fail(ORBGPU_ERR_ARG, "kp_capacity must be >= max_keypoints and < 65536");
+    const Geom& g = e->g;
+    StereoArgs a;
+    std::memset(&a, 0, sizeof(a));
+    for (int l = 0; l < g.nlevels; ++l) {
+        if (l == 0) {
+            a.lvl_base[0] = d_images;
+            a.lvl_frame[0] = frame_step;
+            a.lvl_pitch[0] = (int)row_step;
+        } else {
+            a.lvl_base[l] = e->d_pyr + g.lv[l].offset;
+            a.lvl_frame[l] = g.lv[l].frame_bytes;
+            a.lvl_pitch[l] = g.lv[l].pitch;
+        }
+        a.lvl_w[l] = g.lv[l].w;
+        a.lvl_h[l] = g.lv[l].h;
+        a.scale[l] = e->scale[l];
+        a.inv_scale[l] = e->inv_scale[l];
+    }
+    a.kps = d_kps;
+    a.desc = d_desc;
+    a.counts = d_counts;
+    a.cap = kp_capacity;
+    a.bf = bf;
+    a.max_d = bf / min_z;  // +inf for min_z = 0, as the reference (Frame.cpp:581)
+    a.th_orb = (100 + 50) / 2;
+    a.rr = (int)std::ceil(2.0f * e->scale[g.nlevels - 1]) + 1;
+    a.uright = d_uright;
+    a.depth = d_depth;
+    if (stereo_lds_bytes(kp_capacity, g.lv[0].h) > 160 * 1024)
+        return fail(ORBGPU_ERR_UNSUPPORTED, "stereo LDS tables exceed 160 KiB");
+    ORB_HIP(launch_stereo(a, npairs, reinterpret_cast<hipStream_t>(stream)));
+    return ORBGPU_OK;
+}

@@ -1,0 +1,279 @@
+// stereo.hip -- Frame::ComputeStereoMatches (Frame.cpp:540-748) for batches
+// of rectified stereo pairs extracted by one orbgpu_extractor (left = frame
+// 2p, right = frame 2p+1 of the last batch extraction).
+//
+// One 256-thread block per pair:
+//  A. the right keypoints go to LDS with their row band [minr, maxr]
+//     (Frame.cpp:562-576: r = 2 * scale[octave], ceil/floor of y +- r) and
+//     are bucketed by floor(y) (CSR over the image rows);
+//  B. one wave per left keypoint: lanes walk the right keypoints of the rows
+//     that can contain vL, apply the reference's row, octave and u filters
+//     (:599-629) and reduce (Hamming, index) -- the reference keeps the first
+//     strict minimum in increasing right-index order (:634); then the 11x11
+//     SAD search over 11 shifts on the keypoint's pyramid level (:656-691):
+//     lanes = (shift, window row) pairs, per-shift sums reduced in LDS;
+//     parabola fit, disparity and depth (:697-729) on lane 0;
+//  C. the median cut (:734-747): the (M/2)-th smallest SAD of the accepted
+//     matches by a two-pass 8-bit radix select in LDS, then every match with
+//     SAD >= 1.5f*1.4f*median is reset to -1.
+// Results stay in LDS until C, so each output is written once.
+//
+// Spec decisions where the reference is undefined: row-band
+// rows outside the image are skipped; a SAD window that would leave the
+// level makes the keypoint unmatched; no accepted match -> no cut.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/orbgpu.h"
+#include "orbgpu_internal.h"
+#include "stereo_kernels.h"
+
+namespace orbgpu {
+
+namespace {
+
+constexpr int kStThreads = 256;
+constexpr int kStWaves = kStThreads / 64;
+
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ uint8_t px(const StereoArgs& a, int frame, int lvl, int y, int x) {
+    return a.lvl_base[lvl][(size_t)frame * a.lvl_frame[lvl] + (size_t)y * a.lvl_pitch[lvl] + x];
+}
+
+__global__ __launch_bounds__(kStThreads) void stereo_kernel(StereoArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_mem[];
+    const int p = blockIdx.x;
+    const int fl = 2 * p, fr = 2 * p + 1;
+    const int N = a.counts[fl], Nr = a.counts[fr];
+    const int H = a.lvl_h[0];
+    const int cap = a.cap;
+    // LDS carve (host: stereo_lds_bytes)
+    float4* s_r = reinterpret_cast<float4*>(s_mem);                     // x, y, minr, maxr << 8 | octave (as int bits)
+    float* s_ur = reinterpret_cast<float*>(s_r + cap);                   // uRight
+    float* s_dp = s_ur + cap;                                            // depth
+    int* s_sad = reinterpret_cast<int*>(s_dp + cap);                     // accepted SAD or -1
+    int* s_cnt = s_sad + cap;                                            // H + 1 row starts
+    int* s_cur = s_cnt + (H + 1);                                        // H fill cursors
+    uint16_t* s_ent = reinterpret_cast<uint16_t*>(s_cur + H);            // cap entries
+    int* s_scr = reinterpret_cast<int*>(s_ent + ((cap + 1) & ~1));      // per wave 128 SAD partials
+    int* s_hist = s_scr + kStWaves * 128;                                // 256 bins + 4 scalars
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const orbgpu_keypoint* kl = a.kps + (size_t)fl * cap;
+    const orbgpu_keypoint* kr = a.kps + (size_t)fr * cap;
+    const uint8_t* dl = a.desc + (size_t)fl * cap * 32;
+    const uint8_t* dr = a.desc + (size_t)fr * cap * 32;
+
+    // A. right keypoints, row bands, buckets
+    for (int i = tid; i <= H; i += kStThreads) s_cnt[i] = 0;
+    for (int i = tid; i < N; i += kStThreads) {
+        s_ur[i] = -1.f;
+        s_dp[i] = -1.f;
+        s_sad[i] = -1;
+    }
+    __syncthreads();
+    for (int i = tid; i < Nr; i += kStThreads) {
+        const orbgpu_keypoint k = kr[i];
+        const float r = __fmul_rn(2.0f, a.scale[k.octave]);
+        const int maxr = (int)ceilf(__fadd_rn(k.y, r));
+        const int minr = (int)floorf(__fsub_rn(k.y, r));
+        s_r[i] = make_float4(k.x, k.y, __int_as_float(minr), __int_as_float((maxr << 8) | (k.octave & 0xFF)));
+        const int row = min(max((int)k.y, 0), H - 1);
+        atomicAdd(&s_cnt[row], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {  // exclusive scan over the rows (H <= a few thousand; one pass)
+        int acc = 0;
+        for (int i = 0; i < H; ++i) {
+            const int c = s_cnt[i];
+            s_cnt[i] = acc;
+            s_cur[i] = acc;
+            acc += c;
+        }
+        s_cnt[H] = acc;
+    }
+    __syncthreads();
+    for (int i = tid; i < Nr; i += kStThreads) {
+        const int row = min(max((int)s_r[i].y, 0), H - 1);
+        s_ent[atomicAdd(&s_cur[row], 1)] = (uint16_t)i;
+    }
+    __syncthreads();
+
+    // B. one wave per left keypoint
+    int* scr = s_scr + wave * 128;
+    for (int iL = wave; iL < N; iL += kStWaves) {
+        const orbgpu_keypoint k = kl[iL];
+        const int lvl = k.octave;
+        const float vL = k.y, uL = k.x;
+        const int vi = (int)vL;
+        if (vi >= H) continue;
+        const float minU = __fsub_rn(uL, a.max_d);
+        const float maxU = __fsub_rn(uL, 0.0f);
+        if (maxU < 0.f) continue;
+        const int ra = max(vi - a.rr, 0), rb = min(vi + a.rr, H - 1);
+        const int e0 = s_cnt[ra], e1 = s_cnt[rb + 1];
+        // left descriptor (same for all lanes)
+        const uint4 L0 = *reinterpret_cast<const uint4*>(dl + (size_t)iL * 32);
+        const uint4 L1 = *reinterpret_cast<const uint4*>(dl + (size_t)iL * 32 + 16);
+        int best = 0x7FFFFFFF;
+        for (int e = e0 + lane; e < e1; e += 64) {
+            const int iR = s_ent[e];
+            const float4 r = s_r[iR];
+            const int minr = __float_as_int(r.z), mo = __float_as_int(r.w);
+            const int maxr = mo >> 8, o = mo & 0xFF;
+            if (vi < minr || vi > maxr) continue;
+            if (o < lvl - 1 || o > lvl + 1) continue;
+            if (!(r.x >= minU && r.x <= maxU)) continue;
+            const uint4 R0 = *reinterpret_cast<const uint4*>(dr + (size_t)iR * 32);
+            const uint4 R1 = *reinterpret_cast<const uint4*>(dr + (size_t)iR * 32 + 16);
+            const int d = __popc(L0.x ^ R0.x) + __popc(L0.y ^ R0.y) + __popc(L0.z ^ R0.z) + __popc(L0.w ^ R0.w) +
+                          __popc(L1.x ^ R1.x) + __popc(L1.y ^ R1.y) + __popc(L1.z ^ R1.z) + __popc(L1.w ^ R1.w);
+            best = min(best, (d << 16) | iR);
+        }
+        best = wave_min(best);
+        const int bestDist = best == 0x7FFFFFFF ? 0x7FFF : (best >> 16);
+        if (bestDist >= 100 || bestDist >= a.th_orb) continue;  // TH_HIGH start (:610), thOrbDist (:645)
+        const int bestR = best & 0xFFFF;
+        // subpixel match by correlation on level lvl
+        const float uR0 = s_r[bestR].x;
+        const float sf = a.inv_scale[lvl];
+        const float su = roundf(__fmul_rn(uL, sf));
+        const float sv = roundf(__fmul_rn(vL, sf));
+        const float sr = roundf(__fmul_rn(uR0, sf));
+        const int lw = a.lvl_w[lvl], lh = a.lvl_h[lvl];
+        const int iu = (int)su, iv = (int)sv, ir = (int)sr;
+        if (iv - 5 < 0 || iv + 6 > lh || iu - 5 < 0 || iu + 6 > lw) continue;  // spec: IL inside the level
+        const float iniu = __fadd_rn(sr, 0.0f), endu = __fadd_rn(sr, 11.0f);   // scaleduR0 + L - w, + L + w + 1
+        if (iniu < 0.f || endu >= (float)lw) continue;                            // :668-671
+        if (ir - 10 < 0) continue;                                                 // spec: IR inside the level
+        const int cL = px(a, fl, lvl, iv, iu);
+        for (int c = lane; c < 121; c += 64) {
+            const int inc = c / 11 - 5, rr = c - (c / 11) * 11;
+            const int y = iv - 5 + rr;
+            const int cR = px(a, fr, lvl, iv, ir + inc);
+            int s = 0;
+#pragma unroll
+            for (int col = 0; col < 11; ++col) {
+                const int l = (int)px(a, fl, lvl, y, iu - 5 + col) - cL;
+                const int rv = (int)px(a, fr, lvl, y, ir + inc - 5 + col) - cR;
+                s += abs(l - rv);
+            }
+            scr[c] = s;
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's partials are in LDS
+        __builtin_amdgcn_wave_barrier();
+        int dsum = 0;
+        if (lane < 11)
+            for (int rr = 0; rr < 11; ++rr) dsum += scr[lane * 11 + rr];
+        __builtin_amdgcn_wave_barrier();
+        // gather the 11 shift sums to every lane
+        int dists[11];
+#pragma unroll
+        for (int j = 0; j < 11; ++j) dists[j] = __shfl(dsum, j, 64);
+        if (lane == 0) {
+            int bestSad = 0x7FFFFFFF, bestInc = 0;
+#pragma unroll
+            for (int j = 0; j < 11; ++j)
+                if ((float)dists[j] < (float)bestSad) {  // float dist vs int bestDist (:681)
+                    bestSad = dists[j];
+                    bestInc = j - 5;
+                }
+            if (bestInc != -5 && bestInc != 5) {
+                const float d1 = (float)dists[bestInc + 4], d2 = (float)dists[bestInc + 5],
+                            d3 = (float)dists[bestInc + 6];
+                const float deltaR =
+                    __fdiv_rn(__fsub_rn(d1, d3), __fmul_rn(2.0f, __fsub_rn(__fadd_rn(d1, d3), __fmul_rn(2.0f, d2))));
+                if (!(deltaR < -1.f || deltaR > 1.f)) {
+                    float bestuR = __fmul_rn(a.scale[lvl], __fadd_rn(__fadd_rn(sr, (float)bestInc), deltaR));
+                    float disparity = __fsub_rn(uL, bestuR);
+                    if (disparity >= 0.f && disparity < a.max_d) {
+                        if (disparity <= 0.f) {
+                            disparity = 0.01f;
+                            bestuR = (float)__dsub_rn((double)uL, 0.01);
+                        }
+                        s_dp[iL] = __fdiv_rn(a.bf, disparity);
+                        s_ur[iL] = bestuR;
+                        s_sad[iL] = bestSad;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    // C. median cut: (M/2)-th smallest accepted SAD (< 2^16), radix select
+    int* s_tot = s_hist + 256;
+    for (int i = tid; i < 256; i += kStThreads) s_hist[i] = 0;
+    if (tid == 0) s_tot[0] = 0;
+    __syncthreads();
+    for (int i = tid; i < N; i += kStThreads)
+        if (s_sad[i] >= 0) {
+            atomicAdd(&s_hist[(s_sad[i] >> 8) & 0xFF], 1);
+            atomicAdd(&s_tot[0], 1);
+        }
+    __syncthreads();
+    const int M = s_tot[0];
+    if (M > 0) {
+        if (tid == 0) {
+            int k = M / 2, acc = 0, b = 0;
+            for (; b < 256; ++b) {
+                if (acc + s_hist[b] > k) break;
+                acc += s_hist[b];
+            }
+            s_tot[1] = b;
+            s_tot[2] = k - acc;
+        }
+        __syncthreads();
+        const int hb = s_tot[1];
+        for (int i = tid; i < 256; i += kStThreads) s_hist[i] = 0;
+        __syncthreads();
+        for (int i = tid; i < N; i += kStThreads)
+            if (s_sad[i] >= 0 && ((s_sad[i] >> 8) & 0xFF) == hb) atomicAdd(&s_hist[s_sad[i] & 0xFF], 1);
+        __syncthreads();
+        if (tid == 0) {
+            int k = s_tot[2], acc = 0, b = 0;
+            for (; b < 256; ++b) {
+                if (acc + s_hist[b] > k) break;
+                acc += s_hist[b];
+            }
+            s_tot[3] = (hb << 8) | b;
+        }
+        __syncthreads();
+        const float median = (float)s_tot[3];
+        const float th = __fmul_rn(1.5f * 1.4f, median);
+        for (int i = tid; i < N; i += kStThreads)
+            if (s_sad[i] >= 0 && !((float)s_sad[i] < th)) {
+                s_ur[i] = -1.f;
+                s_dp[i] = -1.f;
+            }
+        __syncthreads();
+    }
+    for (int i = tid; i < N; i += kStThreads) {
+        a.uright[(size_t)p * cap + i] = s_ur[i];
+        a.depth[(size_t)p * cap + i] = s_dp[i];
+    }
+}
+
+}  // namespace
+
+size_t stereo_lds_bytes(int cap, int H) {
+    return (size_t)cap * 16 + (size_t)cap * 12 + (size_t)(2 * H + 1) * 4 + (size_t)((cap + 1) & ~1) * 2 +
+           (size_t)kStWaves * 128 * 4 + (256 + 4) * 4;
+}
+
+hipError_t launch_stereo(const StereoArgs& a, int npairs, hipStream_t stream) {
+    if (npairs <= 0) return hipSuccess;
+    const size_t lds = stereo_lds_bytes(a.cap, a.lvl_h[0]);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stereo_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(stereo_kernel, dim3(npairs), dim3(kStThreads), lds, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace orbgpu

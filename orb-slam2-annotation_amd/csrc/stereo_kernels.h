@@ -1,0 +1,34 @@
+// stereo_kernels.h -- launch interface of stereo.hip (host driver: orbgpu.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/orbgpu.h"
+#include "orbgpu_internal.h"
+
+namespace orbgpu {
+
+struct StereoArgs {
+    // pyramid level l of frame f: lvl_base[l] + f * lvl_frame[l], row pitch lvl_pitch[l]
+    const uint8_t* lvl_base[kMaxLevels];
+    size_t lvl_frame[kMaxLevels];
+    int lvl_pitch[kMaxLevels], lvl_w[kMaxLevels], lvl_h[kMaxLevels];
+    float scale[kMaxLevels], inv_scale[kMaxLevels];  // mvScaleFactors, mvInvScaleFactors
+    const orbgpu_keypoint* kps;  // extraction outputs: frame f at + f * cap
+    const uint8_t* desc;
+    const int* counts;
+    int cap;
+    float bf;      // mbf
+    float max_d;   // mbf / mb (Frame.cpp:581)
+    int th_orb;    // (TH_HIGH + TH_LOW) / 2
+    int rr;        // rows scanned either side of vL: ceil(2 * max scale) + 1
+    float* uright; // pair p: + p * cap
+    float* depth;
+};
+
+size_t stereo_lds_bytes(int cap, int H);
+hipError_t launch_stereo(const StereoArgs& a, int npairs, hipStream_t stream);
+
+}  // namespace orbgpu

@@ -85,6 +85,8 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_debug_octree_trace.argtypes = [vp, i, vp, i]
         L.orbgpu_search_for_initialization.argtypes = [GridBounds, vp, vp, i, vp, vp, i, vp, i, f, i, vp,
                                                        ctypes.POINTER(i)]
+        # orbgpu_stereo.h
+        L.orbgpu_stereo_matches_batch_device.argtypes = [vp, vp, sz, sz, i, vp, vp, vp, i, f, f, vp, vp, vp]
         # orbgpu_ransac.h
         L.orbgpu_srand.argtypes = [ctypes.c_uint]
         L.orbgpu_srand.restype = None
@@ -311,3 +313,18 @@ def hamming_pairs(a, b, out, stream=None):
     """DescriptorDistance over n pairs of device descriptors (n, 32) uint8."""
     _check(lib().orbgpu_hamming_pairs_device(_ptr(a), _ptr(b), a.shape[0], _ptr(out), _stream_ptr(stream)),
            "orbgpu_hamming_pairs_device")
+
+
+def stereo_matches_batch(ex: "Extractor", images, npairs, kps, desc, counts, bf, min_z, uright, depth,
+                         stream=None, row_step=None, frame_step=None):
+    """Frame::ComputeStereoMatches (Frame.cpp:540-748) for pairs (2p, 2p+1) of
+    the last ex.extract_batch() call (same images / kps / desc / counts
+    tensors).  uright, depth: float32 (npairs, cap) device tensors.  min_z is
+    Frame::mb at call time (0 in the reference: infinite max disparity)."""
+    rs = row_step if row_step is not None else images.stride(1) * images.element_size()
+    fs = frame_step if frame_step is not None else images.stride(0) * images.element_size()
+    cap = desc.shape[1]
+    _check(lib().orbgpu_stereo_matches_batch_device(ex.h, _ptr(images), rs, fs, npairs, _ptr(kps), _ptr(desc),
+                                                    _ptr(counts), cap, float(bf), float(min_z), _ptr(uright),
+                                                    _ptr(depth), _stream_ptr(stream)),
+           "orbgpu_stereo_matches_batch_device")
