@@ -2,7 +2,7 @@
 // of rectified stereo pairs extracted by one orbgpu_extractor (left = frame
 // 2p, right = frame 2p+1 of the last batch extraction).
 //
-// One 256-thread block per pair:
+// One 1024-thread block per pair:
 //  A. the right keypoints go to LDS with their row band [minr, maxr]
 //     (Frame.cpp:562-576: r = 2 * scale[octave], ceil/floor of y +- r) and
 //     are bucketed by floor(y) (CSR over the image rows);
@@ -33,7 +33,7 @@ namespace orbgpu {
 
 namespace {
 
-constexpr int kStThreads = 256;
+constexpr int kStThreads = 1024;
 constexpr int kStWaves = kStThreads / 64;
 
 __device__ __forceinline__ int wave_min(int v) {
