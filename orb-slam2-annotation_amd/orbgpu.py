@@ -45,6 +45,23 @@ class GridBounds(ctypes.Structure):
                 ("min_y", ctypes.c_float), ("max_y", ctypes.c_float)]
 
 
+class Camera(ctypes.Structure):
+    """orbgpu_camera: mK (fx, fy, cx, cy) and mDistCoef (k1, k2, p1, p2[, k3])."""
+    _fields_ = [("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("dist", ctypes.c_float * 5), ("ndist", ctypes.c_int)]
+
+    @classmethod
+    def make(cls, fx, fy, cx, cy, dist):
+        c = cls(fx, fy, cx, cy)
+        for i, v in enumerate(dist):
+            c.dist[i] = v
+        c.ndist = len(dist)
+        return c
+
+
+GRID_COLS, GRID_ROWS = 64, 48
+
+
 def bounds_for(img_w, img_h) -> GridBounds:
     """Grid bounds of an undistorted frame: [0, cols] x [0, rows]."""
     return GridBounds(0.0, float(img_w), 0.0, float(img_h))
@@ -62,6 +79,14 @@ def lib() -> ctypes.CDLL:
     if _LIB is None:
         if not LIB_PATH.exists():
             raise RuntimeError(f"HIP extension not built: {LIB_PATH} (run __graft_entry__.build())")
+        # One HIP runtime per process: when PyTorch is present, load the
+        # libamdhip64 it ships first, so liborbgpu's dependency resolves to the
+        # same runtime (a second runtime loaded before it cannot see the device
+        # once torch has opened it).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(str(LIB_PATH))
         vp, i, f, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
         L.orbgpu_last_error.restype = ctypes.c_char_p
@@ -85,6 +110,10 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_debug_octree_trace.argtypes = [vp, i, vp, i]
         L.orbgpu_search_for_initialization.argtypes = [GridBounds, vp, vp, i, vp, vp, i, vp, i, f, i, vp,
                                                        ctypes.POINTER(i)]
+        # orbgpu_frame.h
+        L.orbgpu_compute_image_bounds.argtypes = [ctypes.POINTER(Camera), i, i, ctypes.POINTER(GridBounds)]
+        L.orbgpu_undistort_keypoints_batch_device.argtypes = [ctypes.POINTER(Camera), i, vp, vp, i, vp, vp]
+        L.orbgpu_assign_features_to_grid_batch_device.argtypes = [i, GridBounds, vp, vp, i, vp, vp, vp]
         # orbgpu_stereo.h
         L.orbgpu_stereo_matches_batch_device.argtypes = [vp, vp, sz, sz, i, vp, vp, vp, i, f, f, vp, vp, vp]
         # orbgpu_ransac.h
@@ -328,3 +357,25 @@ def stereo_matches_batch(ex: "Extractor", images, npairs, kps, desc, counts, bf,
                                                     _ptr(counts), cap, float(bf), float(min_z), _ptr(uright),
                                                     _ptr(depth), _stream_ptr(stream)),
            "orbgpu_stereo_matches_batch_device")
+
+
+def compute_image_bounds(cam: Camera, cols: int, rows: int) -> GridBounds:
+    """Frame::ComputeImageBounds (Frame.cpp:498-530)."""
+    b = GridBounds()
+    _check(lib().orbgpu_compute_image_bounds(ctypes.byref(cam), cols, rows, ctypes.byref(b)), "compute_image_bounds")
+    return b
+
+
+def undistort_keypoints_batch(cam: Camera, kps, counts, kps_un, stream=None):
+    """Frame::UndistortKeyPoints for (B, cap, 7) keypoint tensors."""
+    _check(lib().orbgpu_undistort_keypoints_batch_device(ctypes.byref(cam), kps.shape[0], _ptr(kps), _ptr(counts),
+                                                         kps.shape[1], _ptr(kps_un), _stream_ptr(stream)),
+           "undistort_keypoints_batch_device")
+
+
+def assign_features_to_grid_batch(bounds: GridBounds, kps_un, counts, cell_start, cell_items, stream=None):
+    """Frame::AssignFeaturesToGrid -> CSR (cell_start (B, 64*48+1), cell_items (B, cap)) int32 tensors."""
+    _check(lib().orbgpu_assign_features_to_grid_batch_device(kps_un.shape[0], bounds, _ptr(kps_un), _ptr(counts),
+                                                             kps_un.shape[1], _ptr(cell_start), _ptr(cell_items),
+                                                             _stream_ptr(stream)),
+           "assign_features_to_grid_batch_device")
