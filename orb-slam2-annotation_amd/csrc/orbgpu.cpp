@@ -181,6 +181,10 @@ namespace {
 // whose two LDS ping-pong buffers fit 80 KiB (two blocks per CU), raised
 // while the batch alone would not fill the chip.
 // two 1024-thread blocks per CU (measured: bigger bands at one block per CU are slower)
+// row pitch of pyramid levels >= 1 in HBM (bytes)
+#ifndef ORBGPU_PYR_PITCH_ALIGN
+#define ORBGPU_PYR_PITCH_ALIGN 16
+#endif
 #ifndef ORBGPU_PYR_LDS_KB
 #define ORBGPU_PYR_LDS_KB 80
 #endif
@@ -339,7 +343,7 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
         v.scale = e->scale[l];
         v.size_i = (int)(31 * e->scale[l]);
         v.nfeat = nfeat[l];
-        v.pitch = (int)round_up((size_t)v.w, 16);
+        v.pitch = (int)round_up((size_t)v.w, l == 0 ? 16 : ORBGPU_PYR_PITCH_ALIGN);
         if (l > 0) {
             v.frame_bytes = (size_t)v.pitch * v.h;
             v.offset = pyr_off;
@@ -504,8 +508,9 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
                 if (yr[o1].x + 1 - ys > 5) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid step spans more than 6 source rows");
                 e->pyr_ystage.push_back(ys);
             }
-        const int bytes = R * 6 * sv.pitch;
-        if (R * 6 * (sv.pitch / 16) > 2 * pyr_threads())
+        const int lsp = (int)round_up((size_t)sv.w, 16);  // staged row pitch in LDS
+        const int bytes = R * 6 * lsp;
+        if (R * 6 * (lsp / 16) > 2 * pyr_threads())
             return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid staging exceeds two chunks per thread");
         g.pyr_stage_bytes = std::max(g.pyr_stage_bytes, bytes);
     }

@@ -527,7 +527,7 @@ pyramid_stream_kernel(Geom g, const int2* __restrict__ yrec, const int* __restri
         const LevelGeom& Sv = g.lv[l - 1];
         const uint8_t* src = l == 1 ? img0 + (size_t)f * frame0 : pyr + Sv.offset + (size_t)f * Sv.frame_bytes;
         const uint32_t spg = l == 1 ? (uint32_t)row0 : (uint32_t)Sv.pitch;  // source pitch in memory
-        const uint32_t lp = (uint32_t)Sv.pitch;                              // staged pitch in LDS
+        const uint32_t lp = ((uint32_t)Sv.w + 15u) & ~15u;                    // staged pitch in LDS
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(src, spg * (uint32_t)Sv.h);
         uint8_t* dst = pyr + V.offset + (size_t)f * V.frame_bytes;
         const int2* rec = s_y + V.yrec_offset;
