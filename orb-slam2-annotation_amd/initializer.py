@@ -1,0 +1,73 @@
+"""Host-side mirror of the monocular Initializer's model scoring over the C
+ABI in include/orbgpu_init.h (csrc/init.hip).
+
+* ``check_homography_batch`` -- Initializer::CheckHomography
+  (src/Initializer.cpp:390-495) for every RANSAC iteration's (H21, H12) at
+  once: scores (nhyp,) float32 and inlier flags (nhyp, n) uint8.
+* ``check_fundamental_batch`` -- Initializer::CheckFundamental (:497-594).
+* ``select_best`` -- FindHomography / FindFundamental's kept iteration
+  (:207-212, :264-269): first strict maximum above 0, or -1.
+
+Inputs are device tensors (torch, on the GPU); the matches are
+(u1, v1, u2, v2) = (mvKeys1[first].pt, mvKeys2[second].pt) rows.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+import orbgpu
+
+_BOUND = False
+
+
+def _lib():
+    global _BOUND
+    L = orbgpu.lib()
+    if not _BOUND:
+        vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+        L.orbgpu_init_check_homography_batch_device.argtypes = [vp, i, vp, vp, i, f, vp, vp, vp]
+        L.orbgpu_init_check_fundamental_batch_device.argtypes = [vp, i, vp, i, f, vp, vp, vp]
+        L.orbgpu_init_select_best.argtypes = [vp, i, ctypes.POINTER(ctypes.c_int)]
+        _BOUND = True
+    return L
+
+
+def _stream(stream):
+    return None if stream is None else getattr(stream, "cuda_stream", stream)
+
+
+def _shapes(pts, mats, scores, inliers):
+    n, nhyp = pts.shape[0], mats.shape[0]
+    if pts.ndim != 2 or pts.shape[1] != 4 or mats.reshape(nhyp, -1).shape[1] != 9:
+        raise ValueError("pts must be (n, 4) and matrices (nhyp, 3, 3)")
+    if tuple(scores.shape) != (nhyp,) or tuple(inliers.shape) != (nhyp, n):
+        raise ValueError("scores must be (nhyp,) and inliers (nhyp, n)")
+    for t in (pts, mats, scores, inliers):
+        if hasattr(t, "is_contiguous") and not t.is_contiguous():
+            raise ValueError("tensors must be contiguous")
+    return n, nhyp
+
+
+def check_homography_batch(pts, H21, H12, sigma, scores, inliers, stream=None):
+    n, nhyp = _shapes(pts, H21, scores, inliers)
+    if tuple(H12.shape) != tuple(H21.shape):
+        raise ValueError("H12 must match H21")
+    orbgpu._check(_lib().orbgpu_init_check_homography_batch_device(
+        orbgpu._ptr(pts), n, orbgpu._ptr(H21), orbgpu._ptr(H12), nhyp, float(sigma), orbgpu._ptr(scores),
+        orbgpu._ptr(inliers), _stream(stream)), "init_check_homography_batch_device")
+
+
+def check_fundamental_batch(pts, F21, sigma, scores, inliers, stream=None):
+    n, nhyp = _shapes(pts, F21, scores, inliers)
+    orbgpu._check(_lib().orbgpu_init_check_fundamental_batch_device(
+        orbgpu._ptr(pts), n, orbgpu._ptr(F21), nhyp, float(sigma), orbgpu._ptr(scores), orbgpu._ptr(inliers),
+        _stream(stream)), "init_check_fundamental_batch_device")
+
+
+def select_best(scores) -> int:
+    s = np.ascontiguousarray(np.asarray(scores, dtype=np.float32))
+    out = ctypes.c_int(-1)
+    orbgpu._check(_lib().orbgpu_init_select_best(s.ctypes.data, s.shape[0], ctypes.byref(out)), "init_select_best")
+    return out.value

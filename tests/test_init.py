@@ -1,0 +1,161 @@
+"""Initializer::CheckHomography / CheckFundamental and the kept-iteration
+choice of FindHomography / FindFundamental (src/Initializer.cpp:160-290,
+:390-594): the CPU restatement (oracle/init_ref.py) on known answers, and the
+batched GPU scorer (csrc/init.hip) against it -- scores and inlier flags
+bit-exact.  Parity of the restatement against the reference itself is
+unpinned (the reference needs OpenCV; no fixtures exist), see DESIGN.md §6."""
+import numpy as np
+import pytest
+
+import init_ref
+
+F = np.float32
+K = np.array([[517.3, 0, 318.6], [0, 516.5, 255.3], [0, 0, 1]])
+
+
+def _scene(n, planar, seed, outliers=0.2, noise=0.7):
+    """two views of n points (planar or not) -> ((n,4) float32 matches, H21 or F21)"""
+    rng = np.random.default_rng(seed)
+    if planar:
+        X = np.c_[rng.uniform(-2, 2, n), rng.uniform(-1.5, 1.5, n), np.full(n, 5.0)]
+    else:
+        X = np.c_[rng.uniform(-2, 2, n), rng.uniform(-1.5, 1.5, n), rng.uniform(3, 8, n)]
+    a = 0.05
+    R = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
+    t = np.array([0.3, 0.02, 0.05])
+    x1 = (K @ X.T).T
+    x2 = (K @ (R @ X.T + t[:, None])).T
+    p1, p2 = x1[:, :2] / x1[:, 2:], x2[:, :2] / x2[:, 2:]
+    p2 = p2 + rng.normal(0, noise, p2.shape)
+    m = rng.random(n) < outliers
+    p2[m] = rng.uniform([0, 0], [640, 480], (m.sum(), 2))
+    pts = np.c_[p1, p2].astype(F)
+    Ki = np.linalg.inv(K)
+    if planar:  # plane z = 5: H = K (R + t n^T / d) K^-1
+        M = K @ (R + np.outer(t, [0, 0, 1]) / 5.0) @ Ki
+    else:
+        tx = np.array([[0, -t[2], t[1]], [t[2], 0, -t[0]], [-t[1], t[0], 0]])
+        M = Ki.T @ tx @ R @ Ki
+    return pts, M / M[2, 2] if planar else M / np.linalg.norm(M)
+
+
+def _hyps(M, nhyp, seed, scale=2e-3):
+    """RANSAC-like hypotheses: the true model perturbed, plus degenerate ones"""
+    rng = np.random.default_rng(seed)
+    H = M[None] * (1 + rng.normal(0, scale, (nhyp, 3, 3)))
+    H[0] = M
+    if nhyp > 3:
+        H[1] = 0.0                 # all-zero: 0/0 -> NaN chi-squares
+        H[2] = np.diag([1.0, 1, 0])  # w = 0 on every point -> inf
+    return H.astype(F)
+
+
+def _inv(H):
+    out = np.empty_like(H)
+    for k in range(H.shape[0]):
+        try:
+            out[k] = np.linalg.inv(H[k].astype(np.float64)).astype(F)
+        except np.linalg.LinAlgError:
+            out[k] = 0.0
+    return out
+
+
+# ---- CPU: the restatement on known answers --------------------------------
+
+def test_oracle_exact_homography_scores_every_match():
+    pts, H = _scene(300, True, 1, outliers=0.0, noise=0.0)
+    H = H.astype(F)
+    s, inl = init_ref.check_homography(pts, H, np.linalg.inv(H).astype(F))
+    assert inl.all()
+    assert 2 * 300 * 5.991 * 0.999 < s <= 2 * 300 * 5.991
+
+
+def test_oracle_outliers_are_flagged():
+    pts, H = _scene(400, True, 2, outliers=0.3, noise=0.0)
+    H = H.astype(F)
+    _, inl = init_ref.check_homography(pts, H, np.linalg.inv(H).astype(F))
+    assert 0.6 < inl.mean() < 0.8
+    pts, Fm = _scene(400, False, 3, outliers=0.3, noise=0.0)
+    _, inl = init_ref.check_fundamental(pts, Fm.astype(F))
+    assert 0.6 < inl.mean() < 0.8
+
+
+def test_oracle_sequential_float_sum():
+    # two terms per match added in loop order, in float32 (:447-478)
+    pts = np.array([[10, 10, 10, 10], [20, 20, 20.5, 20]], F)
+    I = np.eye(3, dtype=F)
+    s, inl = init_ref.check_homography(pts, I, I, sigma=1.0)
+    t = F(5.991) - F(0.25)
+    want = F(F(F(F(0) + F(5.991)) + F(5.991)) + t)
+    want = F(want + t)
+    assert s == want and inl.tolist() == [True, True]
+
+
+def test_oracle_select_best_first_strict_max():
+    assert init_ref.select_best([0.0, -1.0]) == -1
+    assert init_ref.select_best([1.0, 3.0, 3.0, 2.0]) == 1
+    assert init_ref.select_best([]) == -1
+
+
+def test_select_best_abi_matches_oracle():
+    import initializer
+    rng = np.random.default_rng(5)
+    for _ in range(20):
+        s = rng.integers(-2, 5, 50).astype(F)
+        assert initializer.select_best(s) == init_ref.select_best(s)
+    assert initializer.select_best(np.zeros(0, F)) == -1
+
+
+# ---- GPU: batched scorer vs the restatement, bit-exact --------------------
+
+def _gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,nhyp,seed", [(0, 4, 0), (1, 3, 1), (255, 16, 2), (700, 200, 3), (2049, 64, 4)])
+def test_gpu_check_homography_bit_exact(n, nhyp, seed):
+    torch = _gpu()
+    import initializer
+    pts, H = _scene(max(n, 1), True, seed)
+    pts = pts[:n]
+    H21 = _hyps(H, nhyp, seed + 10)
+    H12 = _inv(H21)
+    dev = torch.device("cuda", 0)
+    scores = torch.full((nhyp,), -7.0, device=dev)
+    inl = torch.full((nhyp, n), 9, dtype=torch.uint8, device=dev)
+    initializer.check_homography_batch(torch.from_numpy(pts).to(dev), torch.from_numpy(H21).to(dev),
+                                       torch.from_numpy(H12).to(dev), 1.0, scores, inl)
+    torch.cuda.synchronize()
+    s, f = scores.cpu().numpy(), inl.cpu().numpy()
+    for h in range(nhyp):
+        ws, wi = init_ref.check_homography(pts, H21[h], H12[h], 1.0)
+        np.testing.assert_array_equal(s[h], ws, err_msg=f"hyp {h}")
+        np.testing.assert_array_equal(f[h].astype(bool), wi, err_msg=f"hyp {h}")
+    assert initializer.select_best(s) == init_ref.select_best(s)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,nhyp,seed,sigma", [(0, 2, 0, 1.0), (3, 5, 1, 1.0), (700, 200, 2, 1.0),
+                                               (1500, 32, 3, 1.6)])
+def test_gpu_check_fundamental_bit_exact(n, nhyp, seed, sigma):
+    torch = _gpu()
+    import initializer
+    pts, M = _scene(max(n, 1), False, seed)
+    pts = pts[:n]
+    F21 = _hyps(M, nhyp, seed + 20, scale=5e-3)
+    dev = torch.device("cuda", 0)
+    scores = torch.zeros(nhyp, device=dev)
+    inl = torch.zeros((nhyp, n), dtype=torch.uint8, device=dev)
+    initializer.check_fundamental_batch(torch.from_numpy(pts).to(dev), torch.from_numpy(F21).to(dev), sigma,
+                                        scores, inl)
+    torch.cuda.synchronize()
+    s, f = scores.cpu().numpy(), inl.cpu().numpy()
+    for h in range(nhyp):
+        ws, wi = init_ref.check_fundamental(pts, F21[h], sigma)
+        np.testing.assert_array_equal(s[h], ws, err_msg=f"hyp {h}")
+        np.testing.assert_array_equal(f[h].astype(bool), wi, err_msg=f"hyp {h}")
+    assert initializer.select_best(s) == init_ref.select_best(s)
