@@ -42,6 +42,13 @@ int orbgpu_init_check_homography_batch_device(const orbgpu_match_pts* d_pts, int
 int orbgpu_init_check_fundamental_batch_device(const orbgpu_match_pts* d_pts, int n, const float* d_f21, int nhyp,
                                                float sigma, float* d_scores, uint8_t* d_inliers, void* stream);
 
+/* Both of the above in one launch (nh homography + nf fundamental
+ * hypotheses side by side in one grid), as Initializer::Initialize runs the
+ * two searches concurrently (Initializer.cpp:133-138). */
+int orbgpu_init_check_both_batch_device(const orbgpu_match_pts* d_pts, int n, const float* d_h21, const float* d_h12,
+                                        int nh, const float* d_f21, int nf, float sigma, float* d_scores_h,
+                                        uint8_t* d_inliers_h, float* d_scores_f, uint8_t* d_inliers_f, void* stream);
+
 /* FindHomography / FindFundamental's selection (Initializer.cpp:207-212,
  * :264-269): *best = the first h with scores[h] greater than every earlier
  * score and than 0; -1 when no score exceeds 0 (the reference keeps score 0

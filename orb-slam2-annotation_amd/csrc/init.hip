@@ -2,11 +2,11 @@
 // CheckFundamental (:497-594) for a batch of RANSAC hypotheses over the same
 // matches (include/orbgpu_init.h).
 //
-// One 256-thread workgroup per hypothesis; the matches are walked in tiles of
-// 256, one match per lane.  Each lane evaluates both transfer errors exactly
+// One 256-thread workgroup per hypothesis; the matches are walked in chunks
+// of 4096, lanes striding over the chunk.  Each lane evaluates both transfer errors exactly
 // as the reference writes them (-ffp-contract=off, the reciprocal 1.0/w in
 // double as the reference's double literal makes it) and writes its inlier
-// byte (coalesced).  The two score terms of the tile go to LDS and lane 0
+// byte (coalesced).  The two score terms of every match of the chunk go to LDS and lane 0
 // adds them in match order, so the float score is the reference loop's sum
 // bit for bit.  A term the reference skips (chi-square above threshold) is
 // stored as +0, which leaves a score that is never -0 unchanged; a NaN
@@ -21,21 +21,29 @@
 namespace {
 
 constexpr int kInitThreads = 256;
+constexpr int kInitChunk = 4096;  // matches staged per pass: 32 KiB of terms in LDS
 
 __device__ __forceinline__ float recip_d(float w) { return (float)(1.0 / (double)w); }
 
-// per-tile score terms -> the running score, in match order (lane 0)
+// the staged score terms -> the running score, in match order (lane 0).
+// Eight 16-byte LDS reads are issued together ahead of their 32 dependent
+// adds, so the chain waits on LDS once per 16 matches, not once per 2.
 __device__ __forceinline__ float add_terms(const float* s_t, int cnt, float score) {
     const float4* s4 = reinterpret_cast<const float4*>(s_t);
     int i = 0;
-    for (; i + 2 <= cnt; i += 2) {
-        const float4 v = s4[i >> 1];
-        score += v.x;
-        score += v.y;
-        score += v.z;
-        score += v.w;
+    for (; i + 16 <= cnt; i += 16) {
+        float4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = s4[(i >> 1) + k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            score += v[k].x;
+            score += v[k].y;
+            score += v[k].z;
+            score += v[k].w;
+        }
     }
-    if (i < cnt) {
+    for (; i < cnt; ++i) {
         score += s_t[2 * i];
         score += s_t[2 * i + 1];
     }
@@ -43,13 +51,10 @@ __device__ __forceinline__ float add_terms(const float* s_t, int cnt, float scor
 }
 
 template <bool kHomography>
-__global__ __launch_bounds__(kInitThreads) void init_check_kernel(const float4* __restrict__ pts, int n,
-                                                                  const float* __restrict__ ma,
-                                                                  const float* __restrict__ mb, float inv_sigma2,
-                                                                  float* __restrict__ scores,
-                                                                  uint8_t* __restrict__ inliers) {
-    __shared__ __attribute__((aligned(16))) float s_t[2 * kInitThreads];
-    const int h = blockIdx.x;
+__device__ __forceinline__ void check_body(int h, float* s_t, const float4* __restrict__ pts, int n,
+                                           const float* __restrict__ ma, const float* __restrict__ mb,
+                                           float inv_sigma2, float* __restrict__ scores,
+                                           uint8_t* __restrict__ inliers) {
     const int tid = threadIdx.x;
     float a[9], b[9];
 #pragma unroll
@@ -60,9 +65,10 @@ __global__ __launch_bounds__(kInitThreads) void init_check_kernel(const float4* 
     }
     uint8_t* inl = inliers + (size_t)h * (size_t)n;
     float score = 0.f;
-    for (int base = 0; base < n; base += kInitThreads) {
-        const int i = base + tid;
-        if (i < n) {
+    for (int base = 0; base < n; base += kInitChunk) {
+        const int cnt = min(kInitChunk, n - base);
+        for (int j = tid; j < cnt; j += kInitThreads) {
+            const int i = base + j;
             const float4 p = pts[i];
             const float u1 = p.x, v1 = p.y, u2 = p.z, v2 = p.w;
             float chi1, chi2, th, ths;
@@ -98,15 +104,39 @@ __global__ __launch_bounds__(kInitThreads) void init_check_kernel(const float4* 
                 chi2 = (num1 * num1 / (a1 * a1 + b1 * b1)) * inv_sigma2;
             }
             const bool out1 = chi1 > th, out2 = chi2 > th;
-            s_t[2 * tid] = out1 ? 0.f : ths - chi1;
-            s_t[2 * tid + 1] = out2 ? 0.f : ths - chi2;
+            s_t[2 * j] = out1 ? 0.f : ths - chi1;
+            s_t[2 * j + 1] = out2 ? 0.f : ths - chi2;
             inl[i] = (uint8_t)!(out1 || out2);
         }
         __syncthreads();
-        if (tid == 0) score = add_terms(s_t, min(kInitThreads, n - base), score);
+        if (tid == 0) score = add_terms(s_t, cnt, score);
         __syncthreads();
     }
     if (tid == 0) scores[h] = score;
+}
+
+template <bool kHomography>
+__global__ __launch_bounds__(kInitThreads) void init_check_kernel(const float4* __restrict__ pts, int n,
+                                                                  const float* __restrict__ ma,
+                                                                  const float* __restrict__ mb, float inv_sigma2,
+                                                                  float* __restrict__ scores,
+                                                                  uint8_t* __restrict__ inliers) {
+    __shared__ __attribute__((aligned(16))) float s_t[2 * kInitChunk];
+    check_body<kHomography>(blockIdx.x, s_t, pts, n, ma, mb, inv_sigma2, scores, inliers);
+}
+
+// both models in one grid -- the reference runs FindHomography and
+// FindFundamental concurrently in two threads (Initializer.cpp:133-138)
+__global__ __launch_bounds__(kInitThreads) void init_check_both_kernel(
+    const float4* __restrict__ pts, int n, const float* __restrict__ h21, const float* __restrict__ h12, int nh,
+    const float* __restrict__ f21, float inv_sigma2, float* __restrict__ scores_h, uint8_t* __restrict__ inl_h,
+    float* __restrict__ scores_f, uint8_t* __restrict__ inl_f) {
+    __shared__ __attribute__((aligned(16))) float s_t[2 * kInitChunk];
+    const int b = blockIdx.x;
+    if (b < nh)
+        check_body<true>(b, s_t, pts, n, h21, h12, inv_sigma2, scores_h, inl_h);
+    else
+        check_body<false>(b - nh, s_t, pts, n, f21, f21, inv_sigma2, scores_f, inl_f);
 }
 
 int launch(bool homography, const orbgpu_match_pts* d_pts, int n, const float* d_a, const float* d_b, int nhyp,
@@ -143,6 +173,25 @@ extern "C" int orbgpu_init_check_fundamental_batch_device(const orbgpu_match_pts
                                                           int nhyp, float sigma, float* d_scores, uint8_t* d_inliers,
                                                           void* stream) {
     return launch(false, d_pts, n, d_f21, nullptr, nhyp, sigma, d_scores, d_inliers, stream);
+}
+
+extern "C" int orbgpu_init_check_both_batch_device(const orbgpu_match_pts* d_pts, int n, const float* d_h21,
+                                                   const float* d_h12, int nh, const float* d_f21, int nf,
+                                                   float sigma, float* d_scores_h, uint8_t* d_inliers_h,
+                                                   float* d_scores_f, uint8_t* d_inliers_f, void* stream) {
+    if ((n > 0 && !d_pts) || n < 0 || nh < 0 || nf < 0 || !(sigma > 0.f) ||
+        (nh > 0 && (!d_h21 || !d_h12 || !d_scores_h || (n > 0 && !d_inliers_h))) ||
+        (nf > 0 && (!d_f21 || !d_scores_f || (n > 0 && !d_inliers_f))))
+        return orbgpu::fail(ORBGPU_ERR_ARG, "invalid argument");
+    if (nh + nf == 0) return ORBGPU_OK;
+    if (int rc = orbgpu::check_device()) return rc;
+    (void)hipGetLastError();
+    const float inv_sigma2 = (float)(1.0 / (double)(sigma * sigma));
+    hipLaunchKernelGGL(init_check_both_kernel, dim3(nh + nf), dim3(kInitThreads), 0,
+                       reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float4*>(d_pts), n, d_h21,
+                       d_h12, nh, d_f21, inv_sigma2, d_scores_h, d_inliers_h, d_scores_f, d_inliers_f);
+    ORB_HIP(hipGetLastError());
+    return ORBGPU_OK;
 }
 
 extern "C" int orbgpu_init_select_best(const float* scores, int nhyp, int* best_out) {

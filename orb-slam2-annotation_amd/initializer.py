@@ -5,6 +5,7 @@ ABI in include/orbgpu_init.h (csrc/init.hip).
   (src/Initializer.cpp:390-495) for every RANSAC iteration's (H21, H12) at
   once: scores (nhyp,) float32 and inlier flags (nhyp, n) uint8.
 * ``check_fundamental_batch`` -- Initializer::CheckFundamental (:497-594).
+* ``check_both_batch`` -- both of the above in one launch.
 * ``select_best`` -- FindHomography / FindFundamental's kept iteration
   (:207-212, :264-269): first strict maximum above 0, or -1.
 
@@ -29,6 +30,7 @@ def _lib():
         vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
         L.orbgpu_init_check_homography_batch_device.argtypes = [vp, i, vp, vp, i, f, vp, vp, vp]
         L.orbgpu_init_check_fundamental_batch_device.argtypes = [vp, i, vp, i, f, vp, vp, vp]
+        L.orbgpu_init_check_both_batch_device.argtypes = [vp, i, vp, vp, i, vp, i, f, vp, vp, vp, vp, vp]
         L.orbgpu_init_select_best.argtypes = [vp, i, ctypes.POINTER(ctypes.c_int)]
         _BOUND = True
     return L
@@ -64,6 +66,19 @@ def check_fundamental_batch(pts, F21, sigma, scores, inliers, stream=None):
     orbgpu._check(_lib().orbgpu_init_check_fundamental_batch_device(
         orbgpu._ptr(pts), n, orbgpu._ptr(F21), nhyp, float(sigma), orbgpu._ptr(scores), orbgpu._ptr(inliers),
         _stream(stream)), "init_check_fundamental_batch_device")
+
+
+def check_both_batch(pts, H21, H12, F21, sigma, scores_h, inliers_h, scores_f, inliers_f, stream=None):
+    """both searches' hypotheses in one launch (Initialize runs them in two
+    threads, src/Initializer.cpp:133-138)"""
+    n, nh = _shapes(pts, H21, scores_h, inliers_h)
+    _, nf = _shapes(pts, F21, scores_f, inliers_f)
+    if tuple(H12.shape) != tuple(H21.shape):
+        raise ValueError("H12 must match H21")
+    orbgpu._check(_lib().orbgpu_init_check_both_batch_device(
+        orbgpu._ptr(pts), n, orbgpu._ptr(H21), orbgpu._ptr(H12), nh, orbgpu._ptr(F21), nf, float(sigma),
+        orbgpu._ptr(scores_h), orbgpu._ptr(inliers_h), orbgpu._ptr(scores_f), orbgpu._ptr(inliers_f),
+        _stream(stream)), "init_check_both_batch_device")
 
 
 def select_best(scores) -> int:

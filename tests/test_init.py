@@ -159,3 +159,29 @@ def test_gpu_check_fundamental_bit_exact(n, nhyp, seed, sigma):
         np.testing.assert_array_equal(s[h], ws, err_msg=f"hyp {h}")
         np.testing.assert_array_equal(f[h].astype(bool), wi, err_msg=f"hyp {h}")
     assert initializer.select_best(s) == init_ref.select_best(s)
+
+
+@pytest.mark.gpu
+def test_gpu_check_both_matches_separate_launches():
+    torch = _gpu()
+    import initializer
+    n = 900
+    pts, H = _scene(n, True, 7)
+    _, M = _scene(n, False, 8)
+    H21, F21 = _hyps(H, 200, 9), _hyps(M, 150, 10, scale=5e-3)
+    H12 = _inv(H21)
+    dev = torch.device("cuda", 0)
+    d = {k: torch.from_numpy(v).to(dev) for k, v in dict(p=pts, h=H21, g=H12, f=F21).items()}
+    sh, sf = torch.zeros(200, device=dev), torch.zeros(150, device=dev)
+    ih, jf = torch.zeros((200, n), dtype=torch.uint8, device=dev), torch.zeros((150, n), dtype=torch.uint8, device=dev)
+    initializer.check_both_batch(d["p"], d["h"], d["g"], d["f"], 1.0, sh, ih, sf, jf)
+    torch.cuda.synchronize()
+    s_h, i_h, s_f, i_f = sh.cpu().numpy(), ih.cpu().numpy(), sf.cpu().numpy(), jf.cpu().numpy()
+    for h in range(200):
+        ws, wi = init_ref.check_homography(pts, H21[h], H12[h], 1.0)
+        np.testing.assert_array_equal(s_h[h], ws)
+        np.testing.assert_array_equal(i_h[h].astype(bool), wi)
+    for h in range(150):
+        ws, wi = init_ref.check_fundamental(pts, F21[h], 1.0)
+        np.testing.assert_array_equal(s_f[h], ws)
+        np.testing.assert_array_equal(i_f[h].astype(bool), wi)

@@ -27,8 +27,7 @@ def main(n=1000, nhyp=200, iters=200):
     s = torch.cuda.current_stream()
 
     def step():
-        initializer.check_homography_batch(pts, H21, H12, 1.0, sh, ih, stream=s)
-        initializer.check_fundamental_batch(pts, F21, 1.0, sf, i_f, stream=s)
+        initializer.check_both_batch(pts, H21, H12, F21, 1.0, sh, ih, sf, i_f, stream=s)
 
     for _ in range(10):
         step()
