@@ -24,7 +24,8 @@ extern "C" {
 #endif
 
 /* One match of mvMatches12: (u1, v1) = mvKeys1[first].pt,
- * (u2, v2) = mvKeys2[second].pt. */
+ * (u2, v2) = mvKeys2[second].pt.  Device arrays of it must be 16-byte
+ * aligned (the kernels load a match as one float4); ORBGPU_ERR_ARG if not. */
 typedef struct orbgpu_match_pts {
     float u1, v1, u2, v2;
 } orbgpu_match_pts;

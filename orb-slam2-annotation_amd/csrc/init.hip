@@ -144,6 +144,7 @@ int launch(bool homography, const orbgpu_match_pts* d_pts, int n, const float* d
     if ((n > 0 && !d_pts) || !d_a || (homography && !d_b) || !d_scores || (n > 0 && !d_inliers) || n < 0 || nhyp < 0 ||
         !(sigma > 0.f))
         return orbgpu::fail(ORBGPU_ERR_ARG, "invalid argument");
+    if ((uintptr_t)d_pts & 15) return orbgpu::fail(ORBGPU_ERR_ARG, "d_pts must be 16-byte aligned (float4 loads)");
     if (nhyp == 0) return ORBGPU_OK;
     if (int rc = orbgpu::check_device()) return rc;
     (void)hipGetLastError();
@@ -183,6 +184,7 @@ extern "C" int orbgpu_init_check_both_batch_device(const orbgpu_match_pts* d_pts
         (nh > 0 && (!d_h21 || !d_h12 || !d_scores_h || (n > 0 && !d_inliers_h))) ||
         (nf > 0 && (!d_f21 || !d_scores_f || (n > 0 && !d_inliers_f))))
         return orbgpu::fail(ORBGPU_ERR_ARG, "invalid argument");
+    if ((uintptr_t)d_pts & 15) return orbgpu::fail(ORBGPU_ERR_ARG, "d_pts must be 16-byte aligned (float4 loads)");
     if (nh + nf == 0) return ORBGPU_OK;
     if (int rc = orbgpu::check_device()) return rc;
     (void)hipGetLastError();

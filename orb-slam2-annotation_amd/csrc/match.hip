@@ -22,7 +22,12 @@ namespace orbgpu {
 
 namespace {
 
-constexpr int kMaxK0 = 512;  // level-0 keypoints per frame held in LDS (N0+3 for nfeatures <= 2350)
+// Level-0 keypoints per frame held in LDS.  The 512 variant (45 KB of LDS)
+// covers nfeatures <= 2350; pairs above it are handed to the 1024 variant
+// (89 KB: the 2x-features initialisation extractor of KITTI mono,
+// Tracking.cpp:149, has ~870 at level 0); above 1024 a pair reports -1.
+constexpr int kMaxK0Small = 512, kMaxK0Large = 1024;
+constexpr int kNeedLarge = -2;  // nmatches sentinel: the pair waits for the large variant
 constexpr int kGC = 64, kGR = 48, kHL = 30, kThLow = 50;
 
 __device__ inline unsigned long long wave_min_u64(unsigned long long v) {
@@ -54,10 +59,14 @@ constexpr int kMatchThreads = 256;
 constexpr int kTopK = 4;  // best candidate keys kept per query by the parallel phase
 
 // (dist, grid order) of a candidate as one ordered key: dist <= 256 (9 bits),
-// cell = ix * 48 + iy < 3072 (12 bits), level-0 index < 512 (9 bits)
+// cell = ix * 48 + iy < 3072 (12 bits), level-0 index < 1024 (10 bits)
+constexpr int kKeyJBits = 10;
+constexpr uint32_t kKeyJMask = (1u << kKeyJBits) - 1;
 __device__ inline uint32_t cand_key(int dist, int cell, int j) {
-    return ((uint32_t)dist << 21) | ((uint32_t)cell << 9) | (uint32_t)j;
+    return ((uint32_t)dist << (12 + kKeyJBits)) | ((uint32_t)cell << kKeyJBits) | (uint32_t)j;
 }
+__device__ inline int key_dist(uint32_t key) { return (int)(key >> (12 + kKeyJBits)); }
+__device__ inline int key_j(uint32_t key) { return (int)(key & kKeyJMask); }
 
 // Two phases per frame pair (one 256-thread block):
 //  1 parallel, one thread per F1 query: scan the level-0 F2 keypoints (same
@@ -69,12 +78,13 @@ __device__ inline uint32_t cand_key(int dist, int cell, int j) {
 //    next kept key's dist.  A list is exact while it holds all candidates or
 //    both values are found inside it; otherwise the query is re-scanned by
 //    the whole wave against the live state (rare).
+template <int kMaxK0>
 __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     float minX, float maxX, float minY, float maxY, const orbgpu_keypoint* __restrict__ kps1,
     const uint8_t* __restrict__ desc1, const int* __restrict__ n1p, size_t stride1,
     const orbgpu_keypoint* __restrict__ kps2, const uint8_t* __restrict__ desc2, const int* __restrict__ n2p,
     size_t stride2, float* __restrict__ prev_xy, int window, float nnratio, int flags, int* __restrict__ matches12,
-    int* __restrict__ nmatches_out, int* __restrict__ err) {
+    int* __restrict__ nmatches_out) {
     __shared__ float s_x[kMaxK0], s_y[kMaxK0];
     __shared__ int s_cell[kMaxK0];           // grid cell ix*48+iy, or -1 when not in the grid
     __shared__ int s_mdist[kMaxK0];          // vMatchedDistance
@@ -97,10 +107,15 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     const int n1 = n1p[b], n2 = n2p[b];
     int* M12 = matches12 + (size_t)b * stride1;
     float* prev = prev_xy ? prev_xy + (size_t)b * stride1 * 2 : nullptr;
+    const bool large = kMaxK0 == kMaxK0Large;
+    // the large variant only takes the pairs the small one handed over
+    if (large && nmatches_out[b] != kNeedLarge) return;
     const int n10 = level0_count(K1, n1), n20 = level0_count(K2, n2);
     if (n10 > kMaxK0 || n20 > kMaxK0) {
-        if (tid == 0) { atomicOr(err, kErrMatchCap); nmatches_out[b] = 0; }
+        // per-pair status: kNeedLarge (retried by the large variant) or -1
+        // (capacity exceeded); no match is reported for the pair
         for (int i = tid; i < n1; i += kMatchThreads) M12[i] = -1;
+        if (tid == 0) nmatches_out[b] = large ? -1 : kNeedLarge;
         return;
     }
     // grid inverses (Frame.cpp:221-224)
@@ -193,7 +208,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
             const int nk = min(ncand, kTopK);
             for (int k = 0; k < nk; ++k) {
                 const uint32_t key = s_top[i1][k];
-                const int dist = (int)(key >> 21), j = (int)(key & 511u);
+                const int dist = key_dist(key), j = key_j(key);
                 if (s_mdist[j] <= dist) continue;
                 if (best == 0xFFFFFFFFu) {
                     best = key;
@@ -233,8 +248,8 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
                                       : cand_key((int)(wbest >> 32), (int)((wbest >> 16) & 0xFFFF), (int)(wbest & 0xFFFF));
             }
             if (best == 0xFFFFFFFFu) continue;  // no usable candidate
-            const int bestDist = (int)(best >> 21);
-            const int bidx = (int)(best & 511u);
+            const int bestDist = key_dist(best);
+            const int bidx = key_j(best);
             if (bestDist <= kThLow && (float)bestDist < __fmul_rn((float)best2, nnratio)) {
                 if (lane == 0) {
                     const int prev21 = s_m21[bidx];
@@ -314,10 +329,17 @@ hipError_t launch_match_init(int batch, float minX, float maxX, float minY, floa
                              const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,
                              const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2, size_t stride2,
                              float* prev_xy, int window, float nnratio, int flags,
-                             int* matches12, int* nmatches, int* err, hipStream_t stream) {
-    hipLaunchKernelGGL(match_init_kernel, dim3(batch), dim3(kMatchThreads), 0, stream, minX, maxX, minY, maxY, kps1,
-                       desc1, n1, stride1,
-                       kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags, matches12, nmatches, err);
+                             int* matches12, int* nmatches, hipStream_t stream) {
+    // small variant for every pair, then the large one for the pairs it
+    // handed over (a no-op block per pair otherwise)
+    hipLaunchKernelGGL(match_init_kernel<kMaxK0Small>, dim3(batch), dim3(kMatchThreads), 0, stream, minX, maxX, minY,
+                       maxY, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags,
+                       matches12, nmatches);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(match_init_kernel<kMaxK0Large>, dim3(batch), dim3(kMatchThreads), 0, stream, minX, maxX, minY,
+                       maxY, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags,
+                       matches12, nmatches);
     return hipGetLastError();
 }
 

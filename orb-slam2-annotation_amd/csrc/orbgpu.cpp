@@ -608,7 +608,6 @@ int collect_errors(orbgpu_extractor* e, hipStream_t s) {
         if (err & kErrCellCap) m += " FAST-cell";
         if (err & kErrNodeCap) m += " octree-nodes";
         if (err & kErrKeyCap) m += " octree-keys";
-        if (err & kErrMatchCap) m += " matcher-level0";
         if (err & kErrSeqCap) m += " octree-seq";
         return fail(ORBGPU_ERR_CAPACITY, m);
     }
@@ -821,19 +820,6 @@ int orbgpu_hamming_pairs_device(const uint8_t* a, const uint8_t* b, int n, int* 
     return ORBGPU_OK;
 }
 
-static int g_match_err_init = 0;
-static int* g_match_err = nullptr;
-
-static int match_err_word(int** p) {
-    if (!g_match_err_init) {
-        ORB_HIP(hipMalloc((void**)&g_match_err, sizeof(int)));
-        ORB_HIP(hipMemset(g_match_err, 0, sizeof(int)));
-        g_match_err_init = 1;
-    }
-    *p = g_match_err;
-    return ORBGPU_OK;
-}
-
 int orbgpu_search_for_initialization_batch_device(int batch, orbgpu_grid_bounds bd, const orbgpu_keypoint* kps1,
                                                   const uint8_t* desc1, const int* n1, size_t stride1,
                                                   const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2,
@@ -842,11 +828,8 @@ int orbgpu_search_for_initialization_batch_device(int batch, orbgpu_grid_bounds 
     if (batch <= 0 || !kps1 || !kps2 || !desc1 || !desc2 || !n1 || !n2 || !matches12 || !nmatches ||
         !(bd.max_x > bd.min_x) || !(bd.max_y > bd.min_y))
         return fail(ORBGPU_ERR_ARG, "invalid argument");
-    int* err = nullptr;
-    int rc = match_err_word(&err);
-    if (rc) return rc;
     ORB_HIP(launch_match_init(batch, bd.min_x, bd.max_x, bd.min_y, bd.max_y, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy,
-                              window, nnratio, flags, matches12, nmatches, err, (hipStream_t)stream));
+                              window, nnratio, flags, matches12, nmatches, (hipStream_t)stream));
     return ORBGPU_OK;
 }
 
@@ -886,17 +869,15 @@ int orbgpu_search_for_initialization(orbgpu_grid_bounds bd, const orbgpu_keypoin
     rc = orbgpu_search_for_initialization_batch_device(1, bd, dk1, dd1, dn, n1c, dk2, dd2, dn + 1, n2c, dp,
                                                        window, nnratio, flags, dm, dn + 2, nullptr);
     if (rc) { cleanup(); return rc; }
-    int err = 0;
     ok = hipDeviceSynchronize() == hipSuccess &&
          hipMemcpy(matches12, dm, (size_t)n1 * sizeof(int), hipMemcpyDeviceToHost) == hipSuccess &&
          hipMemcpy(nmatches, dn + 2, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess &&
-         (!prev_xy || hipMemcpy(prev_xy, dp, (size_t)n1 * 2 * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess) &&
-         hipMemcpy(&err, g_match_err, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess;
+         (!prev_xy || hipMemcpy(prev_xy, dp, (size_t)n1 * 2 * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess);
     cleanup();
     if (!ok) return fail(ORBGPU_ERR_HIP, "matcher failed");
-    if (err) {
-        (void)hipMemset(g_match_err, 0, sizeof(int));
-        return fail(ORBGPU_ERR_CAPACITY, "matcher: more level-0 keypoints than the LDS capacity");
+    if (*nmatches < 0) {
+        *nmatches = 0;
+        return fail(ORBGPU_ERR_CAPACITY, "matcher: more than 1024 level-0 keypoints in a frame");
     }
     return ORBGPU_OK;
 }

@@ -40,7 +40,7 @@ hipError_t launch_match_init(int batch, float minX, float maxX, float minY, floa
                              const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,
                              const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2, size_t stride2,
                              float* prev_xy, int window, float nnratio, int flags,
-                             int* matches12, int* nmatches, int* err, hipStream_t stream);
+                             int* matches12, int* nmatches, hipStream_t stream);
 
 hipError_t launch_hamming_pairs(const uint8_t* a, const uint8_t* b, int n, int* dist, hipStream_t stream);
 
@@ -49,7 +49,7 @@ enum : int {
     kErrCellCap = 1,     // FAST cell candidates overflowed cell_cap
     kErrNodeCap = 2,     // octree list exceeded ncap / ocap
     kErrKeyCap = 4,      // octree key count exceeded the scratch region
-    kErrMatchCap = 8,    // matcher: level-0 keypoints exceed LDS capacity
+    kErrUnused8 = 8,     // (was the matcher capacity bit; now reported per pair)
     kErrSeqCap = 16,     // octree creation sequence overflow
 };
 

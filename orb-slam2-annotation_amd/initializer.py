@@ -41,6 +41,18 @@ def _stream(stream):
 
 
 def _shapes(pts, mats, scores, inliers):
+    import torch
+    want = ((pts, torch.float32, "pts"), (mats, torch.float32, "matrices"), (scores, torch.float32, "scores"),
+            (inliers, torch.uint8, "inliers"))
+    for t, dt, name in want:
+        if not (isinstance(t, torch.Tensor) and t.is_cuda):
+            raise TypeError(f"{name} must be a torch tensor on the GPU (a host pointer would fault the kernel)")
+        if t.dtype != dt:
+            raise TypeError(f"{name} must be {dt}, got {t.dtype}")
+        if t.device != pts.device:
+            raise ValueError(f"{name} is on {t.device}, pts on {pts.device}")
+    if pts.data_ptr() % 16:
+        raise ValueError("pts must be 16-byte aligned (the kernel loads float4 rows)")
     n, nhyp = pts.shape[0], mats.shape[0]
     if pts.ndim != 2 or pts.shape[1] != 4 or mats.reshape(nhyp, -1).shape[1] != 9:
         raise ValueError("pts must be (n, 4) and matrices (nhyp, 3, 3)")
@@ -52,10 +64,16 @@ def _shapes(pts, mats, scores, inliers):
     return n, nhyp
 
 
+def _same(a, ref):
+    if a.dtype != ref.dtype or a.device != ref.device or not a.is_contiguous():
+        raise TypeError("H12 must be a contiguous float32 GPU tensor on H21's device")
+
+
 def check_homography_batch(pts, H21, H12, sigma, scores, inliers, stream=None):
     n, nhyp = _shapes(pts, H21, scores, inliers)
     if tuple(H12.shape) != tuple(H21.shape):
         raise ValueError("H12 must match H21")
+    _same(H12, H21)
     orbgpu._check(_lib().orbgpu_init_check_homography_batch_device(
         orbgpu._ptr(pts), n, orbgpu._ptr(H21), orbgpu._ptr(H12), nhyp, float(sigma), orbgpu._ptr(scores),
         orbgpu._ptr(inliers), _stream(stream)), "init_check_homography_batch_device")
@@ -75,6 +93,7 @@ def check_both_batch(pts, H21, H12, F21, sigma, scores_h, inliers_h, scores_f, i
     _, nf = _shapes(pts, F21, scores_f, inliers_f)
     if tuple(H12.shape) != tuple(H21.shape):
         raise ValueError("H12 must match H21")
+    _same(H12, H21)
     orbgpu._check(_lib().orbgpu_init_check_both_batch_device(
         orbgpu._ptr(pts), n, orbgpu._ptr(H21), orbgpu._ptr(H12), nh, orbgpu._ptr(F21), nf, float(sigma),
         orbgpu._ptr(scores_h), orbgpu._ptr(inliers_h), orbgpu._ptr(scores_f), orbgpu._ptr(inliers_f),

@@ -116,7 +116,8 @@ def _gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,nhyp,seed", [(0, 4, 0), (1, 3, 1), (255, 16, 2), (700, 200, 3), (2049, 64, 4)])
+@pytest.mark.parametrize("n,nhyp,seed", [(0, 4, 0), (1, 3, 1), (255, 16, 2), (700, 200, 3), (2049, 64, 4),
+                                          (9001, 8, 5)])  # 9001: two full 4096-match chunks + a tail
 def test_gpu_check_homography_bit_exact(n, nhyp, seed):
     torch = _gpu()
     import initializer
@@ -140,7 +141,7 @@ def test_gpu_check_homography_bit_exact(n, nhyp, seed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,nhyp,seed,sigma", [(0, 2, 0, 1.0), (3, 5, 1, 1.0), (700, 200, 2, 1.0),
-                                               (1500, 32, 3, 1.6)])
+                                               (1500, 32, 3, 1.6), (9001, 6, 4, 1.0)])
 def test_gpu_check_fundamental_bit_exact(n, nhyp, seed, sigma):
     torch = _gpu()
     import initializer
@@ -185,3 +186,45 @@ def test_gpu_check_both_matches_separate_launches():
         ws, wi = init_ref.check_fundamental(pts, F21[h], 1.0)
         np.testing.assert_array_equal(s_f[h], ws)
         np.testing.assert_array_equal(i_f[h].astype(bool), wi)
+
+
+@pytest.mark.gpu
+def test_gpu_check_both_multi_chunk():
+    """n = 9001 crosses two 4096-match chunk boundaries of init.hip's score
+    loop (the serial sum carried across chunks) and leaves a partial tail."""
+    torch = _gpu()
+    import initializer
+    n = 9001
+    pts, H = _scene(n, True, 17)
+    _, M = _scene(n, False, 18)
+    H21, F21 = _hyps(H, 5, 19), _hyps(M, 4, 20, scale=5e-3)
+    H12 = _inv(H21)
+    dev = torch.device("cuda", 0)
+    d = {k: torch.from_numpy(v).to(dev) for k, v in dict(p=pts, h=H21, g=H12, f=F21).items()}
+    sh, sf = torch.zeros(5, device=dev), torch.zeros(4, device=dev)
+    ih = torch.zeros((5, n), dtype=torch.uint8, device=dev)
+    jf = torch.zeros((4, n), dtype=torch.uint8, device=dev)
+    initializer.check_both_batch(d["p"], d["h"], d["g"], d["f"], 1.0, sh, ih, sf, jf)
+    torch.cuda.synchronize()
+    for h in range(5):
+        ws, wi = init_ref.check_homography(pts, H21[h], H12[h], 1.0)
+        np.testing.assert_array_equal(sh[h].cpu().numpy(), ws)
+        np.testing.assert_array_equal(ih[h].cpu().numpy().astype(bool), wi)
+    for h in range(4):
+        ws, wi = init_ref.check_fundamental(pts, F21[h], 1.0)
+        np.testing.assert_array_equal(sf[h].cpu().numpy(), ws)
+        np.testing.assert_array_equal(jf[h].cpu().numpy().astype(bool), wi)
+
+
+def test_binding_rejects_host_and_wrong_dtype():
+    """A host array or a float64 matrix must never reach the kernel."""
+    torch = pytest.importorskip("torch")
+    import initializer
+    pts = np.zeros((4, 4), F)
+    H = np.zeros((2, 3, 3), F)
+    with pytest.raises(TypeError):  # numpy (host) arrays
+        initializer.check_fundamental_batch(pts, H, 1.0, np.zeros(2, F), np.zeros((2, 4), np.uint8))
+    tp = torch.zeros((4, 4), dtype=torch.float32)
+    with pytest.raises(TypeError):  # CPU tensors
+        initializer.check_fundamental_batch(tp, torch.zeros((2, 3, 3)), 1.0, torch.zeros(2),
+                                            torch.zeros((2, 4), dtype=torch.uint8))

@@ -1,0 +1,114 @@
+"""SearchForInitialization capacity: the 2x-features
+initialisation extractor (Tracking.cpp:149: mpIniORBextractor with
+2*nFeatures) puts ~870 keypoints on level 0 of a KITTI 1241x376 frame, above
+the 512 the small LDS variant holds.  Such pairs run in the 1024 variant and
+stay bit-exact against the oracle; above 1024 the status is per pair
+(nmatches = -1), never a process-global flag.  Also: DescriptorDistance over
+HBM pairs (orbgpu_hamming_pairs_device) against numpy popcounts."""
+import numpy as np
+import pytest
+
+import orbref
+import synth
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _gpu():
+    import orbgpu
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return orbgpu
+
+
+def _kitti_init_pair():
+    frames = synth.mono_stream(2, 1241, 376, seed=0x0B5E + 3)
+    ref = orbref.Extractor(nfeatures=4000)
+    (k1, d1), (k2, d2) = (ref.extract(f) for f in frames)
+    return k1, d1, k2, d2
+
+
+def test_kitti_init_extractor_pair_bit_exact():
+    og = _gpu()
+    k1, d1, k2, d2 = _kitti_init_pair()
+    n0 = int((k1["octave"] == 0).sum())
+    assert n0 > 512, n0  # exercises the large variant
+    n_r, m_r, p_r = orbref.search_for_initialization(k1, d1, k2, d2, 1241, 376)
+    n_g, m_g, p_g = og.search_for_initialization(k1, d1, k2, d2, 1241, 376)
+    assert n_r > 50
+    assert n_g == n_r
+    np.testing.assert_array_equal(m_g, m_r)
+    np.testing.assert_array_equal(p_g.view(np.uint32), p_r.view(np.uint32))
+
+
+def _pack(frames, cap):
+    B = len(frames)
+    kps = np.zeros((B, cap, 7), np.float32)
+    desc = np.zeros((B, cap, 32), np.uint8)
+    counts = np.zeros(B, np.int32)
+    for b, (k, d) in enumerate(frames):
+        kps[b, :len(k)] = k.view(np.float32).reshape(-1, 7)
+        desc[b, :len(k)] = d
+        counts[b] = len(k)
+    return (torch.from_numpy(kps).cuda(), torch.from_numpy(desc).cuda(), torch.from_numpy(counts).cuda())
+
+
+def _crowded(n, seed):
+    import orbgpu
+    rng = np.random.default_rng(seed)
+    k = np.zeros(n, orbgpu.KP_DTYPE)
+    k["x"] = rng.uniform(10, 630, n).astype(np.float32)
+    k["y"] = rng.uniform(10, 470, n).astype(np.float32)
+    k["size"], k["octave"], k["class_id"] = 31.0, 0, -1
+    k["angle"] = rng.uniform(0, 360, n).astype(np.float32)
+    return k, rng.integers(0, 256, (n, 32), dtype=np.uint8)
+
+
+def test_batch_mixed_capacity_is_per_pair(mono_frames):
+    """pair 0 normal, pair 1 in the 1024 variant, pair 2 over capacity: each
+    gets its own status; a single-pair call afterwards is unaffected."""
+    og = _gpu()
+    ref = orbref.Extractor()
+    f0, f1 = ref.extract(mono_frames[0]), ref.extract(mono_frames[1])
+    mid1, mid2 = _crowded(800, 1), _crowded(800, 2)
+    big1, big2 = _crowded(1100, 3), _crowded(1100, 4)
+    cap = 1100
+    K1, D1, N1 = _pack([f0, mid1, big1], cap)
+    K2, D2, N2 = _pack([f1, mid2, big2], cap)
+    m12 = torch.full((3, cap), -7, dtype=torch.int32, device="cuda")
+    nm = torch.full((3,), 99, dtype=torch.int32, device="cuda")
+    og.search_for_initialization_batch(640, 480, K1, D1, N1, K2, D2, N2, m12, nm)
+    torch.cuda.synchronize()
+    nm, m12 = nm.cpu().numpy(), m12.cpu().numpy()
+    for b, (a, c) in enumerate([(f0, f1), (mid1, mid2)]):
+        n_r, m_r, _ = orbref.search_for_initialization(a[0], a[1], c[0], c[1], 640, 480)
+        assert nm[b] == n_r, b
+        np.testing.assert_array_equal(m12[b, :len(a[0])], m_r)
+    assert nm[2] == -1
+    assert (m12[2, :1100] == -1).all()
+    # the next single-pair call sees no stale error
+    n_r, m_r, _ = orbref.search_for_initialization(f0[0], f0[1], f1[0], f1[1], 640, 480)
+    n_g, m_g, _ = og.search_for_initialization(f0[0], f0[1], f1[0], f1[1], 640, 480)
+    assert n_g == n_r and np.array_equal(m_g, m_r)
+    with pytest.raises(og.OrbGpuError) as ei:
+        og.search_for_initialization(big1[0], big1[1], big2[0], big2[1], 640, 480)
+    assert ei.value.code == og.ERR_CAPACITY
+
+
+@pytest.mark.parametrize("n", [0, 1, 255, 256, 10007])
+def test_hamming_pairs_device(n):
+    og = _gpu()
+    rng = np.random.default_rng(n)
+    a = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    b = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    if n > 2:
+        b[0] = a[0]          # distance 0
+        b[1] = ~a[1]         # distance 256
+    out = torch.full((max(n, 1),), -1, dtype=torch.int32, device="cuda")
+    og.hamming_pairs(torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda(), out)
+    torch.cuda.synchronize()
+    want = np.unpackbits(a ^ b, axis=1).sum(1).astype(np.int32)
+    np.testing.assert_array_equal(out.cpu().numpy()[:n], want)
+    for i in range(min(n, 50)):
+        assert want[i] == orbref.descriptor_distance(a[i], b[i])
