@@ -112,3 +112,110 @@ def search_by_bow(mode, fvA, descA, angA, validA, fvB, descB, angB, validB, nnra
                                                     int(check_ori), match.ctypes.data, ctypes.byref(nm)),
                   "orbgpu_search_by_bow")
     return nm.value, match[:nout]
+
+
+# --------------------------------------------------------------------------
+# Batched, HBM-resident forms (torch tensors on the GPU)
+# --------------------------------------------------------------------------
+_BATCH_BOUND = False
+
+
+def _batch_lib():
+    global _BATCH_BOUND
+    L = orbgpu.lib()
+    if not _BATCH_BOUND:
+        vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+        L.orbgpu_bow_transform_batch_device.argtypes = [vp, i, vp, vp, i, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                                        vp]
+        L.orbgpu_search_by_bow_batch_device.argtypes = [i, i, vp, vp, f, i, i, vp, vp, vp]
+        _BATCH_BOUND = True
+    return L
+
+
+def _dev(t, dtype, name):
+    import torch
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.is_contiguous()):
+        raise TypeError(f"{name} must be a contiguous torch tensor on the GPU")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    return t.data_ptr()
+
+
+class BatchTransform:
+    """Outputs of transform() for B frames of `stride` slots, in HBM:
+    per-slot word/node/weight, FeatureVector CSR (fv_nodes, fv_offsets,
+    fv_features, fv_n) and BowVector (bow_words, bow_values, bow_n)."""
+
+    def __init__(self, B, stride, device):
+        import torch
+        i32 = dict(dtype=torch.int32, device=device)
+        self.B, self.stride = B, stride
+        self.word = torch.zeros((B, stride), **i32)
+        self.node = torch.zeros((B, stride), **i32)
+        self.weight = torch.zeros((B, stride), dtype=torch.float64, device=device)
+        self.fv_nodes = torch.zeros((B, stride), **i32)
+        self.fv_offsets = torch.zeros((B, stride + 1), **i32)
+        self.fv_features = torch.zeros((B, stride), **i32)
+        self.fv_n = torch.zeros(B, **i32)
+        self.bow_words = torch.zeros((B, stride), **i32)
+        self.bow_values = torch.zeros((B, stride), dtype=torch.float64, device=device)
+        self.bow_n = torch.zeros(B, **i32)
+
+
+def transform_batch(voc: Vocabulary, desc, counts, out: BatchTransform, levelsup=4, stream=None):
+    """Frame/KeyFrame::ComputeBoW for a batch (orbgpu_bow_transform_batch_device):
+    desc (B, stride, 32) uint8, counts (B,) int32, on the GPU."""
+    import torch
+    B, S = out.B, out.stride
+    if tuple(desc.shape) != (B, S, 32) or tuple(counts.shape) != (B,):
+        raise ValueError("desc must be (B, stride, 32) and counts (B,)")
+    _dev(desc, torch.uint8, "desc")
+    _dev(counts, torch.int32, "counts")
+    orbgpu._check(_batch_lib().orbgpu_bow_transform_batch_device(
+        voc.h, B, desc.data_ptr(), counts.data_ptr(), S, levelsup, out.word.data_ptr(), out.node.data_ptr(),
+        out.weight.data_ptr(), out.fv_nodes.data_ptr(), out.fv_offsets.data_ptr(), out.fv_features.data_ptr(),
+        out.fv_n.data_ptr(), out.bow_words.data_ptr(), out.bow_values.data_ptr(), out.bow_n.data_ptr(),
+        orbgpu._stream_ptr(stream)), "orbgpu_bow_transform_batch_device")
+
+
+def frame_table(tf: BatchTransform, desc, angle, valid, counts_host, rows=None):
+    """orbgpu_bow_frame records (host ctypes array) pointing into HBM: frame r
+    = batch row rows[r] (default all rows) of a transform output, with its
+    descriptors (B, stride, 32) u8, angles (B, stride) f32 and MapPoint flags
+    (B, stride) u8.  counts_host: features per row (numpy)."""
+    import torch
+    S = tf.stride
+    _dev(desc, torch.uint8, "desc")
+    _dev(angle, torch.float32, "angle")
+    _dev(valid, torch.uint8, "valid")
+    fv_n = tf.fv_n.cpu().numpy()
+    if (fv_n < 0).any():
+        raise orbgpu.OrbGpuError(orbgpu.ERR_CAPACITY, "transform_batch rejected a frame")
+    rows = range(tf.B) if rows is None else rows
+    rows = list(rows)
+    tab = (BowFrame * max(len(rows), 1))()
+    for r, b in enumerate(rows):
+        tab[r] = BowFrame(int(counts_host[b]), int(fv_n[b]), tf.fv_nodes.data_ptr() + 4 * S * b,
+                          tf.fv_offsets.data_ptr() + 4 * (S + 1) * b, tf.fv_features.data_ptr() + 4 * S * b,
+                          desc.data_ptr() + 32 * S * b, angle.data_ptr() + 4 * S * b, valid.data_ptr() + S * b)
+    return tab
+
+
+def to_device_table(tab, device):
+    """copy a ctypes struct array into a uint8 device tensor"""
+    import torch
+    raw = np.frombuffer(bytes(tab), np.uint8)
+    return torch.from_numpy(raw.copy()).to(device)
+
+
+def search_by_bow_batch(mode, d_frames_a, d_frames_b, batch, nnratio, check_ori, stride, match, nmatches,
+                        stream=None):
+    """ORBmatcher(nnratio, checkOri).SearchByBoW over `batch` pairs of device
+    frame tables (orbgpu_search_by_bow_batch_device): match (batch, stride)
+    int32, nmatches (batch,) int32."""
+    import torch
+    _dev(match, torch.int32, "match")
+    _dev(nmatches, torch.int32, "nmatches")
+    orbgpu._check(_batch_lib().orbgpu_search_by_bow_batch_device(
+        mode, batch, d_frames_a.data_ptr(), d_frames_b.data_ptr(), float(nnratio), int(check_ori), stride,
+        match.data_ptr(), nmatches.data_ptr(), orbgpu._stream_ptr(stream)), "orbgpu_search_by_bow_batch_device")

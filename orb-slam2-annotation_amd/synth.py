@@ -350,3 +350,187 @@ def projection_scenario(n_points: int, n_distractors: int, seed: int, stereo: bo
            "normal": normal, "desc": pdesc, "min_dist": min_dist, "max_dist": max_dist,
            "octave": lvl_ref.astype(np.int32), "angle": pangle}
     return tgt, pts
+
+
+# --------------------------------------------------------------------------
+# Loop-closure burst
+# --------------------------------------------------------------------------
+def synthetic_vocabulary_fast(k: int, L: int, seed: int, flip: float = 0.22):
+    """synthetic_vocabulary for large trees (k=10, L=6: 1,111,110 nodes),
+    vectorised per level: same BFS file order and construction (children
+    are their parent's descriptor with each bit flipped with probability
+    `flip`), leaf weights quantised to 1e-6 so the text form is exact.
+    Returns (parent, is_leaf, desc[n,32], weight) without the root."""
+    rng = np.random.default_rng(seed)
+    root = rng.integers(0, 256, 32, dtype=np.uint8)
+    prev_desc = root[None]
+    prev_ids = np.zeros(1, np.int64)
+    next_id = 1
+    parents, leaves, descs, weights = [], [], [], []
+    thr = int(round(flip * 65536))
+    for depth in range(1, L + 1):
+        n = len(prev_ids) * k
+        desc = np.repeat(prev_desc, k, axis=0)
+        for s in range(0, n, 1 << 17):  # bit flips in chunks (bounded memory)
+            e = min(n, s + (1 << 17))
+            m = rng.integers(0, 65536, (e - s, 256), dtype=np.uint16) < thr
+            desc[s:e] ^= np.packbits(m, axis=1)
+        parents.append(np.repeat(prev_ids, k).astype(np.int32))
+        leaves.append(np.full(n, 1 if depth == L else 0, np.int32))
+        descs.append(desc)
+        if depth == L:
+            weights.append(np.round(rng.uniform(0.5, 5.0, n), 6))
+        else:
+            weights.append(np.zeros(n))
+        prev_desc = desc
+        prev_ids = np.arange(next_id, next_id + n, dtype=np.int64)
+        next_id += n
+    return (np.concatenate(parents), np.concatenate(leaves), np.concatenate(descs),
+            np.concatenate(weights).astype(np.float64))
+
+
+def write_vocabulary_text_fast(path, k, L, scoring, weighting, parent, is_leaf, desc, weight):
+    """DBoW2 text vocabulary (TemplatedVocabulary.h:1359-1448 reads it with
+    stream extraction, so fixed-width space-padded fields are the same
+    file to the loader): one line per node, no trailing newline.  Weights
+    must be multiples of 1e-6 (written with 6 decimals, read back exactly
+    as the nearest double by both loaders)."""
+    n = len(parent)
+    cols = []
+
+    def digits(v, width):  # right-aligned decimal, space padded, then a space
+        v = np.asarray(v, np.int64)
+        out = np.full((len(v), width + 1), ord(" "), np.uint8)
+        rem = v.copy()
+        for c in range(width - 1, -1, -1):
+            d = (rem % 10).astype(np.uint8) + ord("0")
+            show = (rem > 0) | (c == width - 1)
+            out[:, c] = np.where(show, d, ord(" "))
+            rem //= 10
+        return out
+
+    cols.append(digits(parent, 8))
+    cols.append(digits(is_leaf, 1))
+    for j in range(32):
+        cols.append(digits(desc[:, j], 3))
+    w6 = np.round(np.asarray(weight) * 1e6).astype(np.int64)
+    ip, fp = w6 // 1000000, w6 % 1000000
+    wi = digits(ip, 3)[:, :3]
+    dot = np.full((n, 1), ord("."), np.uint8)
+    frac = np.zeros((n, 6), np.uint8)
+    rem = fp.copy()
+    for c in range(5, -1, -1):
+        frac[:, c] = (rem % 10).astype(np.uint8) + ord("0")
+        rem //= 10
+    nl = np.full((n, 1), ord("\n"), np.uint8)
+    rows = np.concatenate(cols + [wi, dot, frac, nl], axis=1)
+    with open(path, "wb") as f:
+        f.write(f"{k} {L} {scoring} {weighting}\n".encode())
+        f.write(rows.tobytes()[:-1])  # no trailing newline
+
+
+def _rot(rng, max_angle):
+    a = rng.uniform(-max_angle, max_angle, 3)
+    cx, cy, cz = np.cos(a)
+    sx, sy, sz = np.sin(a)
+    return (np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]]) @ np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]]) @
+            np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]]))
+
+
+def level_sigma2(nlevels: int = 8, scale: float = 1.2) -> np.ndarray:
+    """mvLevelSigma2 of the extractor (ORBextractor.cpp:412-425, float chain)."""
+    s = np.ones(nlevels, np.float32)
+    for i in range(1, nlevels):
+        s[i] = np.float32(s[i - 1] * np.float32(scale))
+    return (s * s).astype(np.float32)
+
+
+def loop_burst_scene(n_queries: int, n_cand: int, leaves: np.ndarray, n_kp: int = 1000, inlier_frac=0.4,
+                     outlier_frac=0.0, mp_frac: float = 0.9, seed: int = 0x100B, fix_scale: bool = False,
+                     noise_px: float = 0.4):
+    """Keyframes for LoopClosing::ComputeSim3 bursts: query q has a current
+    keyframe (index q) and n_cand loop candidates (index n_queries +
+    q*n_cand + c).  A candidate shares round(inlier_frac * n_kp) keypoints
+    with its current keyframe -- same MapPoint under a known Sim3 S12 (X1 =
+    s R X2 + t in the two camera frames, plus pixel-level noise),
+    descriptors a few bits apart, angles rotated by 10 deg -- and the rest
+    are unrelated, except round(outlier_frac * n_kp) more that copy a
+    current-keyframe descriptor (they match) but carry an unrelated MapPoint
+    (geometric outliers, the "rest outliers" of the burst config).
+    inlier_frac / outlier_frac are scalars or one value per candidate slot.
+    Descriptors start near random vocabulary leaves (so they spread over
+    the tree); keypoint octaves follow the extractor's per-level quotas;
+    mp_frac of the keypoints carry a MapPoint.  Returns a dict of arrays."""
+    rng = np.random.default_rng(seed)
+    K = np.array([517.3, 516.5, 318.6, 255.3], np.float32)
+    sig2 = level_sigma2()
+    quota = np.array([217, 181, 151, 126, 105, 87, 73, 60], np.float64)
+    fracs = np.broadcast_to(np.asarray(inlier_frac, np.float64), (n_cand,))
+    ofracs = np.broadcast_to(np.asarray(outlier_frac, np.float64), (n_cand,))
+    n_kf = n_queries * (1 + n_cand)
+    desc = np.zeros((n_kf, n_kp, 32), np.uint8)
+    angle = np.zeros((n_kf, n_kp), np.float32)
+    octave = np.zeros((n_kf, n_kp), np.int32)
+    valid = np.zeros((n_kf, n_kp), np.uint8)
+    mp = np.zeros((n_kf, n_kp, 3), np.float32)
+    Tcw = np.zeros((n_kf, 12), np.float32)
+    truth = []
+
+    def jitter(d, p):
+        bits = np.unpackbits(d, axis=-1)
+        m = (rng.random(bits.shape) < p).astype(np.uint8)
+        return np.packbits(bits ^ m, axis=-1)
+
+    def cam_points(m):
+        z = rng.uniform(2.0, 12.0, m)
+        u = rng.uniform(10, 630, m)
+        v = rng.uniform(10, 470, m)
+        return np.stack([(u - K[2]) / K[0] * z, (v - K[3]) / K[1] * z, z], 1)
+
+    def fresh(kf):
+        desc[kf] = jitter(leaves[rng.integers(0, len(leaves), n_kp)], 0.08)
+        angle[kf] = rng.uniform(0, 360, n_kp).astype(np.float32)
+        octave[kf] = rng.choice(8, n_kp, p=quota / quota.sum())
+        valid[kf] = rng.random(n_kp) < mp_frac
+        return cam_points(n_kp)
+
+    def pose(kf, Xc):
+        R, t = _rot(rng, 0.4), rng.uniform(-2, 2, 3)
+        Tcw[kf, :9] = R.astype(np.float32).ravel()
+        Tcw[kf, 9:] = t.astype(np.float32)
+        mp[kf] = ((Xc - t) @ R).astype(np.float32)  # R^T (Xc - t)
+
+    for q in range(n_queries):
+        X1c = fresh(q)
+        pose(q, X1c)
+        for c in range(n_cand):
+            kf = n_queries + q * n_cand + c
+            X2c = fresh(kf)
+            s = 1.0 if fix_scale else float(rng.uniform(0.7, 1.4))
+            R12, t12 = _rot(rng, 0.3), rng.uniform(-0.5, 0.5, 3)
+            cand1 = np.nonzero(valid[q])[0]
+            ns = min(int(round(fracs[c] * n_kp)), len(cand1))
+            no = min(int(round(ofracs[c] * n_kp)), len(cand1) - ns)
+            pick = rng.choice(cand1, ns + no, replace=False)
+            slots = rng.choice(n_kp, ns + no, replace=False)
+            # geometric outliers: matching descriptors, unrelated MapPoints
+            osrc, odst = pick[ns:], slots[ns:]
+            desc[kf, odst] = jitter(desc[q, osrc], 0.03)
+            angle[kf, odst] = np.mod(angle[q, osrc] - np.float32(10.0), np.float32(360.0)).astype(np.float32)
+            octave[kf, odst] = octave[q, osrc]
+            valid[kf, odst] = 1
+            src, dst = pick[:ns], slots[:ns]
+            Y = ((X1c[src] - t12) @ R12) / s  # X2 = R^T (X1 - t) / s
+            Y[:, :2] += rng.normal(scale=noise_px, size=(ns, 2)) / K[:2] * Y[:, 2:3]
+            ok = Y[:, 2] > 0.5
+            src, dst, Y = src[ok], dst[ok], Y[ok]
+            X2c[dst] = Y
+            desc[kf, dst] = jitter(desc[q, src], 0.03)
+            angle[kf, dst] = np.mod(angle[q, src] - np.float32(10.0), np.float32(360.0)).astype(np.float32)
+            octave[kf, dst] = octave[q, src]
+            valid[kf, dst] = 1
+            pose(kf, X2c)
+            truth.append({"s": s, "R": R12, "t": t12, "src": src, "dst": dst, "outlier_src": osrc,
+                          "outlier_dst": odst})
+    return {"desc": desc, "angle": angle, "octave": octave, "valid": valid, "mp_world": mp, "Tcw": Tcw, "K": K,
+            "sigma2": sig2, "n_queries": n_queries, "n_cand": n_cand, "truth": truth}
