@@ -7,22 +7,34 @@ GPU, inputs already resident in HBM:
   * ORBextractor::operator() on all B frames (pyramid -> FAST cells ->
     octree -> angle/blur/rBRIEF), and
   * ORBmatcher(0.9, true).SearchForInitialization(F_{t-1}, F_t, window 100)
-    for the B consecutive pairs (the first pair uses the previous step's
-    last frame), the reference's map-free matcher (Tracking.cpp:768-769).
+    for the B consecutive pairs, the reference's map-free matcher
+    (Tracking.cpp:768-769).
 value = frames processed by all ranks / max-over-ranks wall time.
 
-Multi-GPU (launched by torch.distributed.run): every rank owns an independent
-frame stream (weak scaling, no collective on the data path); one barrier
-before/after the timed region and an all-reduce(MAX) of the elapsed time.
+The frames are ONE stream (shard.py): at step s rank r owns
+global frames [(s*N + r)*B, +B) -- contiguous chunks; the chunk-boundary
+frame's keypoints/descriptors go to rank r+1 (RCCL send/recv) so the (t-1, t)
+pair across ranks is matched; every step's outputs are gathered to rank 0
+(send/recv, overlapped with the next step).  Both are inside the timed
+region.  The frames come from a pool of 4 steps per rank rendered up front
+(a fresh batch every step, > the 256 MB MALL).
 
-Also reported (Measurement):
+Also reported:
   * roofline: the pyramid pass (the HBM-bound stage named by BASELINE.json),
     algorithmic bytes = sum_{l>=1} |P_{l-1}| + |P_l| per frame, divided by the
     pyramid launches' summed duration from HIP events recorded on the launch
     stream during the timed region; traffic = PMC-measured HBM bytes from
     profiles/ when a matching summary exists;
-  * cpu_baseline: the oracle (CPU restatement, oracle/liborbref.so) on the
-    host cores, rank 0 at N=1 only, on a bounded sample.
+  * cpu_baseline: the oracle (a scalar C++ restatement, oracle/liborbref.so --
+    NOT the reference's SIMD OpenCV code) on the host cores, rank 0 at N=1
+    only, on a bounded sample;
+  * single_frame: the drop-in path (orbgpu_extract = ORBextractor::operator():
+    host image in, host keypoints/descriptors out, PCIe included), batch 1;
+  * other_geometries: the 1241x376 / 2000-feature mono stream with its own
+    pyramid roofline, and KITTI / EuRoC stereo pairs/s (extract L+R batched +
+    Frame::ComputeStereoMatches).
+--config loopburst runs SURVEY config 5 instead (LoopClosing::ComputeSim3
+bursts: SearchByBoW(KF, KF) + Sim3Solver RANSAC) and reports KF pairs/s.
 """
 from __future__ import annotations
 
@@ -40,22 +52,27 @@ sys.path[:0] = [str(ROOT / "orb-slam2-annotation_amd"), str(ROOT / "oracle")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-PYR_KERNEL_LABEL = {
-    "stream": "pyramid_stream_kernel (one frame per block; source rows staged through LDS per 4-row step)",
-    "frame": "pyramid_frame_kernel (one frame per block; per-lane buffer-load windows)",
-    "band": "pyramid_kernel (frame bands, all levels in LDS)",
-}
 METRIC = "frames/sec ORB extract+match (1000 feat, 640×480 mono) at 1/2/4/8 GPU; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PYR_KERNEL = "pyramid_stream_kernel (one frame per block; source rows staged through LDS per 4-row step)"
+POOL_STEPS = 4
 
 CONFIGS = {
     # name: (width, height, nfeatures, description)
     "mono640": (640, 480, 1000, "synthetic 640x480 mono stream, 1000 feat, 8 levels x1.2, FAST 20/7 "
                                 "(TUM1.yaml params), extract + SearchForInitialization(t-1,t)"),
-    "kitti": (1241, 376, 2000, "synthetic 1241x376 stream, 2000 feat (KITTI00-02.yaml params), "
+    "kitti": (1241, 376, 2000, "synthetic 1241x376 mono stream, 2000 feat (KITTI00-02.yaml params), "
                                "extract + SearchForInitialization(t-1,t)"),
-    "euroc": (752, 480, 1200, "synthetic 752x480 stream, 1200 feat (EuRoC.yaml params), "
+    "euroc": (752, 480, 1200, "synthetic 752x480 mono stream, 1200 feat (EuRoC.yaml params), "
                               "extract + SearchForInitialization(t-1,t)"),
+    "loopburst": (None, None, 1000, "LoopClosing::ComputeSim3 bursts: 100 queries x 5 candidate keyframes "
+                                    "(500 KF pairs, 1000 keypoints each, 40% true correspondences under a "
+                                    "known Sim3, the rest geometric outliers), SearchByBoW(KF,KF) over a "
+                                    "k=10 L=6 DBoW2 vocabulary + Sim3Solver(0.99,20,300) round-robin iterate(5)"),
+}
+STEREO = {  # width, height, nfeatures, Camera.bf, synthetic baseline px
+    "kitti": (1241, 376, 2000, 0.54 * 718.856, 30.0),   # Examples/Stereo/KITTI00-02.yaml
+    "euroc": (752, 480, 1200, 47.90639384423901, 18.0),  # Examples/Stereo/EuRoC.yaml
 }
 
 
@@ -68,6 +85,7 @@ def parse():
     ap.add_argument("--config", default="mono640", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip single_frame / other_geometries")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -90,9 +108,109 @@ def aggregate(elapsed: float, frames_local: int, device=None):
     return float(t.item()), int(n.item())
 
 
-def rank_seed(rank: int) -> int:
-    """Each rank renders its own independent synthetic stream (weak scaling)."""
-    return 0x0B5E + 1009 * rank
+def _barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+class StreamBench:
+    """Extract + SearchForInitialization over one sharded frame stream."""
+
+    def __init__(self, W, H, NF, B, rank, world, dev, stream):
+        import orbgpu
+        import shard
+        import synth
+        self.W, self.H, self.NF, self.B, self.rank, self.world = W, H, NF, B, rank, world
+        self.dev, self.stream = dev, stream
+        self.pitch = (W + 15) // 16 * 16
+        self.ex = orbgpu.Extractor(nfeatures=NF, width=W, height=H, max_batch=B)
+        cap = self.cap = self.ex.max_keypoints
+        # pool: this rank's chunks of POOL_STEPS steps of the global stream
+        self.pool = [synth.torch_stream(B, W, H, device=dev, pitch=self.pitch, bounded=True,
+                                        t0=shard.chunk_frames(s, rank, world, B)[0]) for s in range(POOL_STEPS)]
+        # slot 0 = the frame before this chunk (boundary exchange), slots 1..B this chunk
+        self.sets = []
+        for _ in range(2):  # two output sets: the gather of step k overlaps step k+1
+            kps_all = torch.zeros((B + 1, cap, 7), dtype=torch.float32, device=dev)
+            desc_all = torch.zeros((B + 1, cap, 32), dtype=torch.uint8, device=dev)
+            counts_all = torch.zeros(B + 1, dtype=torch.int32, device=dev)
+            m12 = torch.zeros((B, cap), dtype=torch.int32, device=dev)
+            nmatch = torch.zeros(B, dtype=torch.int32, device=dev)
+            self.sets.append((kps_all, desc_all, counts_all, m12, nmatch))
+        k0, d0, c0 = self.sets[0][0], self.sets[0][1], self.sets[0][2]
+        self.bx = shard.BoundaryExchange(rank, world, [k0[0], d0[0], c0[0:1]])
+        self.gather = shard.OwnerGather(rank, world, [k0[1:], d0[1:], c0[1:], self.sets[0][3], self.sets[0][4]])
+        self.flags = orbgpu.MATCH_CHECK_ORI
+        self.step_no = 0
+
+    def step(self, ev=None):
+        import orbgpu
+        B, st = self.B, self.stream
+        si = self.step_no % 2
+        kps_all, desc_all, counts_all, m12, nmatch = self.sets[si]
+        self.gather.finish(si)  # the set's previous transfer is done before it is rewritten
+        frames = self.pool[self.step_no % POOL_STEPS]
+        self.ex.extract_batch(frames, kps_all[1:], desc_all[1:], counts_all[1:], stream=st, row_step=self.pitch,
+                              frame_step=self.pitch * self.H)
+        prev = self.bx.exchange([kps_all[B], desc_all[B], counts_all[B:B + 1]])
+        kps_all[0].copy_(prev[0])
+        desc_all[0].copy_(prev[1])
+        counts_all[0:1].copy_(prev[2])
+        if ev is not None:
+            ev[0].record(st)
+        orbgpu.search_for_initialization_batch(self.W, self.H, kps_all[:-1], desc_all[:-1], counts_all[:-1],
+                                               kps_all[1:], desc_all[1:], counts_all[1:], m12, nmatch,
+                                               flags=self.flags, stream=st)
+        if ev is not None:
+            ev[1].record(st)
+        self.gather.start(si, [kps_all[1:], desc_all[1:], counts_all[1:], m12, nmatch])
+        self.step_no += 1
+
+    def run(self, warmup, steps):
+        for _ in range(warmup):
+            self.step()
+        self.gather.finish()
+        torch.cuda.synchronize(self.dev)
+        self.ex.sync(self.stream)
+        self.ex.profile(True)
+        self.ex.stage_times(reset=True)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        _barrier(self.world)
+        torch.cuda.synchronize(self.dev)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            self.step(evs[i])
+        self.gather.finish()
+        torch.cuda.synchronize(self.dev)
+        elapsed = time.perf_counter() - t0
+        elapsed, frames_total = aggregate(elapsed, self.B * steps, device=self.dev)
+        _barrier(self.world)
+        self.ex.sync(self.stream)
+        stage_ms, nb = self.ex.stage_times(reset=True)
+        self.ex.profile(False)
+        per_step = {k: v / max(nb, 1) for k, v in stage_ms.items()}
+        per_step["match"] = sum(a.elapsed_time(b) for a, b in evs) / steps
+        pyr_bytes = pyramid_bytes_per_frame(self.ex.level_sizes) * self.B
+        pyr_s = per_step["pyramid"] / 1e3
+        achieved = pyr_bytes / pyr_s / 1e9 if pyr_s > 0 else None
+        last = self.sets[(self.step_no - 1) % 2]
+        return {"fps": frames_total / elapsed, "elapsed": elapsed, "per_step": per_step, "pyr_bytes": pyr_bytes,
+                "achieved": achieved, "keypoints": float(last[2][1:].float().mean().item()),
+                "matches": float(last[4].float().mean().item())}
+
+    def parity_frame0(self):
+        """pool frame 0 of this rank against the oracle (untimed)."""
+        import orbgpu
+        import orbref
+        try:
+            ex1 = orbgpu.Extractor(nfeatures=self.NF, width=self.W, height=self.H, max_batch=1)
+            f0 = self.pool[0][0, :, :self.W].cpu().numpy()
+            kg, dg = ex1.extract(f0)
+            kr, dr = orbref.Extractor(nfeatures=self.NF).extract(f0)
+            return bool(len(kg) == len(kr) and kg.tobytes() == kr.tobytes() and np.array_equal(dg, dr))
+        except Exception as e:  # report, never hide
+            return f"error: {e}"
 
 
 def cpu_baseline(frames_np, W, H, nf, seconds):
@@ -113,12 +231,10 @@ def cpu_baseline(frames_np, W, H, nf, seconds):
             n += 1
         out.append(n)
 
-    # single thread (the reference's own per-frame mode)
     t0 = time.perf_counter()
     res1 = []
     run(iter(range(10 ** 9)), t0 + seconds / 3, res1)
     fps1 = res1[0] / (time.perf_counter() - t0)
-    # all host cores granted to this process (16 on a one-GPU box)
     threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1, 16))
     res = []
     t0 = time.perf_counter()
@@ -130,14 +246,218 @@ def cpu_baseline(frames_np, W, H, nf, seconds):
         t.join()
     fpsN = sum(res) / (time.perf_counter() - t0)
     return {"value": round(fpsN, 2), "unit": "frames/s", "cores": threads, "kind": "port",
-            "single_thread_value": round(fps1, 2),
+            "single_thread_value": round(fps1, 2), "single_thread_ms_per_frame": round(1e3 / fps1, 2),
+            "note": "scalar C++ restatement of the reference's arithmetic (oracle/orbref.cpp: full corner score on "
+                    "every pixel, no SIMD); the reference itself uses OpenCV 2.4's SSE FAST/resize/blur and would "
+                    "be faster per core, so the GPU/CPU ratio overstates the gap",
             "sample": f"oracle extract+match on {len(frames_np)} distinct synthetic {W}x{H} frames, "
                       f"~{seconds:.0f}s bounded ({res1[0]} frames on 1 thread, {sum(res)} on {threads})"}
 
 
+def single_frame(W, H, NF, frame_np, reps=200):
+    """orbgpu_extract latency: the ORBextractor::operator() drop-in path of
+    Frame's constructor (host image -> pinned staging -> H2D, extraction,
+    one D2H of keypoints + descriptors, one sync)."""
+    import orbgpu
+    ex = orbgpu.Extractor(nfeatures=NF, width=W, height=H, max_batch=1)
+    for _ in range(10):
+        ex.extract(frame_np)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ex.extract(frame_np)
+        ts.append(time.perf_counter() - t0)
+    ts = np.array(ts) * 1e3
+    return {"median_ms": round(float(np.median(ts)), 4), "mean_ms": round(float(ts.mean()), 4),
+            "p90_ms": round(float(np.percentile(ts, 90)), 4), "reps": reps,
+            "path": "orbgpu_extract: host image in, host cv::KeyPoint-layout keypoints + N x 32 descriptors out, "
+                    "PCIe copies included, batch 1"}
+
+
+def stereo_throughput(name, dev, pairs=128, steps=10, warmup=2):
+    """KITTI / EuRoC stereo: extract L+R batched + Frame::ComputeStereoMatches."""
+    import orbgpu
+    import synth
+    W, H, NF, BF, BASE = STEREO[name]
+    pitch = (W + 15) // 16 * 16
+    base = synth.base_texture(0x5E7)
+    distinct = 16
+    host = np.zeros((2 * distinct, H, pitch), np.uint8)
+    for i in range(distinct):
+        host[2 * i, :, :W] = synth.render_frame(base, i, W, H, 11)
+        host[2 * i + 1, :, :W] = synth.render_frame(base, i, W, H, 12, BASE)
+    reps = (pairs + distinct - 1) // distinct
+    imgs = torch.from_numpy(np.concatenate([host] * reps)[: 2 * pairs]).to(dev).contiguous()
+    ex = orbgpu.Extractor(nfeatures=NF, width=W, height=H, max_batch=2 * pairs)
+    cap = ex.max_keypoints
+    kps = torch.zeros((2 * pairs, cap, 7), dtype=torch.float32, device=dev)
+    desc = torch.zeros((2 * pairs, cap, 32), dtype=torch.uint8, device=dev)
+    counts = torch.zeros(2 * pairs, dtype=torch.int32, device=dev)
+    ur = torch.zeros((pairs, cap), dtype=torch.float32, device=dev)
+    dp = torch.zeros((pairs, cap), dtype=torch.float32, device=dev)
+    st = torch.cuda.current_stream(dev)
+
+    def step():
+        ex.extract_batch(imgs, kps, desc, counts, stream=st)
+        orbgpu.stereo_matches_batch(ex, imgs, pairs, kps, desc, counts, BF, 0.0, ur, dp, stream=st)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    n = counts.cpu().numpy()
+    urh = ur.cpu().numpy()
+    depth = float(np.mean([(urh[p, : n[2 * p]] >= 0).mean() for p in range(pairs)]))
+    return {"pairs_per_s": round(pairs * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 3),
+            "pairs_per_step": pairs, "width": W, "height": H, "nfeatures": NF,
+            "keypoints_per_frame": round(float(n.mean()), 1), "left_keypoints_with_depth": round(depth, 3),
+            "workload": f"synthetic rectified {W}x{H} pairs (16 distinct, tiled), extract L+R in one batch + "
+                        f"ComputeStereoMatches (bf {BF:.3f})"}
+
+
+def traffic_for(path, config, batch):
+    p = Path(path)
+    if not p.exists():
+        return None
+    try:
+        tj = json.loads(p.read_text())
+        if tj.get("config") == config and tj.get("batch") == batch:
+            return tj.get("pyramid_hbm_bytes_per_step")
+    except Exception:
+        return None
+    return None
+
+
+def run_loopburst(args, rank, world, dev):
+    """SURVEY §8d config 5 on the GPU; KF pairs/s."""
+    import bow
+    import loop
+    import synth
+    nq_total, nc = 100, 5
+    t_set = time.perf_counter()
+    p, l, d, w = synth.synthetic_vocabulary_fast(10, 6, 0x70C)
+    vpath = Path(os.environ.get("TMPDIR", "/tmp")) / f"orbgpu_voc_k10_L6_{os.getpid()}.txt"
+    synth.write_vocabulary_text_fast(vpath, 10, 6, 0, 0, p, l, d, w)
+    t_load = time.perf_counter()
+    voc = bow.Vocabulary.load_text(str(vpath))
+    t_load = time.perf_counter() - t_load
+    vpath.unlink()
+    my_q = list(range(rank, nq_total, world))  # queries round-robin over ranks
+    scene = synth.loop_burst_scene(nq_total, nc, d[l == 1], n_kp=1000, inlier_frac=0.4, outlier_frac=0.6, seed=55)
+    kf_ids = []
+    for q in my_q:
+        kf_ids += [q] + [nq_total + q * nc + c for c in range(nc)]
+    sel = np.array(kf_ids)
+    kfs = loop.Keyframes(scene["desc"][sel], scene["angle"][sel], scene["octave"][sel], scene["valid"][sel],
+                         scene["mp_world"][sel], scene["Tcw"][sel], scene["K"], scene["sigma2"], device=dev)
+    st = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize(dev)
+    t_bow = time.perf_counter()
+    kfs.compute_bow(voc, stream=st)
+    torch.cuda.synchronize(dev)
+    t_bow = time.perf_counter() - t_bow
+    queries = [(j * (1 + nc), [j * (1 + nc) + 1 + c for c in range(nc)], 1000 + q) for j, q in enumerate(my_q)]
+    lb = loop.LoopBurst(kfs, queries)
+    setup_s = time.perf_counter() - t_set
+    for _ in range(args.warmup):
+        lb.step(st)
+    torch.cuda.synchronize(dev)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    _barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(st)
+        lb.search_by_bow(st)
+        ev[i][1].record(st)
+        lb.setup(st)
+        ev[i][2].record(st)
+        lb.compute_sim3(st)
+        ev[i][3].record(st)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    elapsed, pairs_total = aggregate(elapsed, len(my_q) * nc * args.steps, device=dev)
+    stage = {k: sum(e[j].elapsed_time(e[j + 1]) for e in ev) / args.steps
+             for j, k in enumerate(["search_by_bow", "sim3_setup", "compute_sim3"])}
+    res = lb.query_results()
+    states = lb.candidate_states()
+    if rank != 0:
+        return None
+    # algorithmic bytes of SearchByBoW per pair: both frames' descriptors,
+    # angles, MapPoint flags and FeatureVector CSR read once, matches written
+    n_kp = 1000
+    sbb_bytes = 2 * n_kp * (32 + 4 + 1 + 4 + 4) + n_kp * 4
+    dominant = max(stage, key=stage.get)
+    npairs = len(my_q) * nc
+    kern_bytes = {"search_by_bow": sbb_bytes * npairs,
+                  "sim3_setup": npairs * n_kp * (4 + 2 * (12 + 1 + 4)) + npairs * 300 * 36,
+                  "compute_sim3": sum(max(s.n, 0) for s in states) * 36}
+    achieved = kern_bytes[dominant] / (stage[dominant] / 1e3) / 1e9
+    line = {
+        "metric": "KF pairs/s LoopClosing::ComputeSim3 burst (SearchByBoW(KF,KF) + Sim3Solver RANSAC)",
+        "value": round(pairs_total / elapsed, 1), "unit": "KF pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8/f32/f64", "data": "synthetic",
+        "config": {"workload": CONFIGS["loopburst"][3], "config": "loopburst", "queries": nq_total,
+                   "candidates_per_query": nc, "kf_pairs_per_step": npairs * world,
+                   "parallelism": f"queries round-robin x{world}"},
+        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "note": "latency-bound (sequential per-node merge walks / per-query RANSAC chain); the HBM "
+                             "fraction is reported for the record"},
+        "stages_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
+        "queries_matched": int(sum(r.matched >= 0 for r in res)),
+        "mean_round_of_match": round(float(np.mean([r.round for r in res if r.matched >= 0] or [0])), 2),
+        "ransac_iterations_per_step": int(sum(r.hypotheses for r in res)),
+        "mean_searchbybow_matches": round(float(lb.nmatches.float().mean().item()), 1),
+        "setup_s": {"total": round(setup_s, 2), "vocabulary_text_load": round(t_load, 2),
+                    "keyframe_bow_transform": round(t_bow, 4)},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = loopburst_cpu_baseline(scene, p, l, d, w, nc, args.cpu_seconds)
+    return line
+
+
+def loopburst_cpu_baseline(scene, p, l, d, w, nc, seconds):
+    """The oracle pipeline (oracle/loop_ref.py + bow_ref.py: Python/numpy
+    SearchByBoW, C++ Sim3 iterate) on one thread over whole queries."""
+    import bow_ref
+    import loop_ref
+    avoc = loop_ref.ArrayVocabulary(10, 6, 0, 0, p, l, d, w)
+    nq = scene["n_queries"]
+    t0 = time.perf_counter()
+    pairs = 0
+    q = 0
+    while time.perf_counter() - t0 < seconds and q < nq:
+        cur = q
+        fv1 = avoc.transform(scene["desc"][cur], 4)[3]
+        solvers = []
+        for c in range(nc):
+            kf = nq + q * nc + c
+            fv2 = avoc.transform(scene["desc"][kf], 4)[3]
+            nm, m12 = bow_ref.search_by_bow(1, fv1, scene["desc"][cur], scene["angle"][cur], scene["valid"][cur],
+                                            fv2, scene["desc"][kf], scene["angle"][kf], scene["valid"][kf],
+                                            nnratio=0.75, check_ori=True)
+            corr = loop_ref.sim3_setup(m12, scene["valid"][cur], scene["valid"][kf], scene["mp_world"][cur],
+                                       scene["mp_world"][kf], scene["Tcw"][cur], scene["Tcw"][kf],
+                                       scene["octave"][cur], scene["octave"][kf], scene["sigma2"])
+            solvers.append(loop_ref.Sim3SolverRef(corr, scene["K"], scene["K"], False) if nm >= 20 else None)
+            pairs += 1
+        loop_ref.compute_sim3(solvers, 1000 + q)
+        q += 1
+    el = time.perf_counter() - t0
+    return {"value": round(pairs / el, 2), "unit": "KF pairs/s", "cores": 1, "kind": "port",
+            "note": "Python/numpy SearchByBoW + C++ Sim3 iterate restatement (oracle/); the reference's C++ "
+                    "SearchByBoW would be faster per core",
+            "sample": f"{q} queries ({pairs} KF pairs, BoW transform of their keyframes included) in {el:.1f}s"}
+
+
 def main():
     args = parse()
-    W, H, NF, desc_cfg = CONFIGS[args.config]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -146,127 +466,85 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
-    import orbgpu
-    import synth
-
-    B = args.batch
-    pitch = (W + 15) // 16 * 16
-    ex = orbgpu.Extractor(nfeatures=NF, width=W, height=H, max_batch=B)
-    cap = ex.max_keypoints
-    frames = synth.torch_stream(B, W, H, seed=rank_seed(rank), device=dev, pitch=pitch)
-    # frame slots 0..B: slot 0 holds the previous step's last frame, slots
-    # 1..B this step's frames, so all B (t-1, t) pairs are one matcher launch
-    kps_all = torch.zeros((B + 1, cap, 7), dtype=torch.float32, device=dev)
-    desc_all = torch.zeros((B + 1, cap, 32), dtype=torch.uint8, device=dev)
-    counts_all = torch.zeros(B + 1, dtype=torch.int32, device=dev)
-    kps, desc, counts = kps_all[1:], desc_all[1:], counts_all[1:]
-    m12 = torch.zeros((B, cap), dtype=torch.int32, device=dev)
-    nmatch = torch.zeros(B, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    flags = orbgpu.MATCH_CHECK_ORI
-
-    def step(ev=None):
-        ex.extract_batch(frames, kps, desc, counts, stream=stream, row_step=pitch, frame_step=pitch * H)
-        if ev is not None:
-            ev[0].record(stream)
-        orbgpu.search_for_initialization_batch(W, H, kps_all[:-1], desc_all[:-1], counts_all[:-1], kps_all[1:],
-                                               desc_all[1:], counts_all[1:], m12, nmatch, flags=flags, stream=stream)
-        if ev is not None:
-            ev[1].record(stream)
-        kps_all[0].copy_(kps_all[B])
-        desc_all[0].copy_(desc_all[B])
-        counts_all[0].copy_(counts_all[B])
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    ex.sync(stream)
-
-    # parity spot check of this rank's frame 0 against the oracle (untimed)
-    parity = None
-    if rank == 0:
-        try:
-            import orbref
-            ref = orbref.Extractor(nfeatures=NF)
-            f0 = frames[0, :, :W].cpu().numpy()
-            kr, dr = ref.extract(f0)
-            n0 = int(counts[0].item())
-            kg = orbgpu.keypoints_from_raw(kps[0, :n0].cpu().numpy())
-            parity = bool(n0 == len(kr) and kg.tobytes() == kr.tobytes() and
-                          np.array_equal(desc[0, :n0].cpu().numpy(), dr))
-        except Exception as e:  # report, never hide
-            parity = f"error: {e}"
-
-    ex.profile(True)
-    ex.stage_times(reset=True)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(evs[i])
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    elapsed, frames_total = aggregate(elapsed, B * args.steps, device=dev)
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    ex.sync(stream)
-    stage_ms, nb = ex.stage_times(reset=True)
-    ex.profile(False)
-    match_ms = sum(a.elapsed_time(b) for a, b in evs)
-
-    if rank != 0:
+    if args.config == "loopburst":
+        line = run_loopburst(args, rank, world, dev)
+        if line is not None:
+            print(json.dumps(line), flush=True)
         if world > 1:
             import torch.distributed as dist
             dist.destroy_process_group()
         return
 
-    fps = frames_total / elapsed
-    per_step = {k: v / max(nb, 1) for k, v in stage_ms.items()}
-    per_step["match"] = match_ms / args.steps
-    pyr_bytes = pyramid_bytes_per_frame(ex.level_sizes) * B
-    pyr_s = per_step["pyramid"] / 1e3
-    achieved = pyr_bytes / pyr_s / 1e9 if pyr_s > 0 else None
-    traffic = None
-    tpath = Path(args.traffic_json)
-    if tpath.exists():
-        try:
-            tj = json.loads(tpath.read_text())
-            if tj.get("config") == args.config and tj.get("batch") == B:
-                traffic = tj.get("pyramid_hbm_bytes_per_step")
-        except Exception:
-            traffic = None
+    W, H, NF, desc_cfg = CONFIGS[args.config]
+    B = args.batch
+    stream = torch.cuda.current_stream(dev)
+    sb = StreamBench(W, H, NF, B, rank, world, dev, stream)
+    parity = sb.parity_frame0() if rank == 0 else None
+    r = sb.run(args.warmup, args.steps)
+    if rank != 0:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+    achieved = r["achieved"]
     line = {
         "metric": METRIC,
-        "value": round(fps, 1),
+        "value": round(r["fps"], 1),
         "unit": "frames/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
         "config": {"workload": desc_cfg, "config": args.config, "frames_per_gpu_per_step": B,
-                   "width": W, "height": H, "nfeatures": NF, "parallelism": f"frame-sharded x{world}"},
-        "roofline": {"bound": "hbm", "kernel": PYR_KERNEL_LABEL.get(os.environ.get("ORBGPU_PYR_MODE", "stream"),
-                                                               PYR_KERNEL_LABEL["stream"]),
+                   "width": W, "height": H, "nfeatures": NF,
+                   "parallelism": f"one stream in contiguous per-rank chunks x{world}, boundary frame send/recv, "
+                                  f"per-step gather to rank 0"},
+        "roofline": {"bound": "hbm", "kernel": PYR_KERNEL,
                      "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                     "traffic": traffic, "algorithmic_bytes_per_step": pyr_bytes},
-        "stages_ms_per_step": {k: round(v, 4) for k, v in per_step.items()},
-        "keypoints_per_frame": round(float(counts.float().mean().item()), 1),
-        "matches_per_pair": round(float(nmatch.float().mean().item()), 1),
+                     "traffic": traffic_for(args.traffic_json, args.config, B),
+                     "algorithmic_bytes_per_step": r["pyr_bytes"]},
+        "stages_ms_per_step": {k: round(v, 4) for k, v in r["per_step"].items()},
+        "keypoints_per_frame": round(r["keypoints"], 1),
+        "matches_per_pair": round(r["matches"], 1),
         "parity_frame0_vs_oracle": parity,
     }
+    frame0 = sb.pool[0][0, :, :W].cpu().numpy()
+    if world == 1 and not args.no_extras:
+        line["single_frame"] = single_frame(W, H, NF, frame0)
+        del sb
+        torch.cuda.empty_cache()
+        other = {}
+        kw, kh, knf, _ = CONFIGS["kitti"]
+        kb = StreamBench(kw, kh, knf, 256, 0, 1, dev, stream)
+        kr = kb.run(2, 10)
+        other["mono1241x376"] = {
+            "frames_per_s": round(kr["fps"], 1), "ms_per_step": round(kr["elapsed"] / 10 * 1e3, 3),
+            "frames_per_step": 256, "nfeatures": knf,
+            "pyramid_roofline": {"achieved": round(kr["achieved"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(kr["achieved"] / HBM_PEAK_GBS, 4),
+                                 "algorithmic_bytes_per_step": kr["pyr_bytes"]},
+            "stages_ms_per_step": {k: round(v, 4) for k, v in kr["per_step"].items()},
+            "keypoints_per_frame": round(kr["keypoints"], 1), "matches_per_pair": round(kr["matches"], 1),
+            "workload": CONFIGS["kitti"][3]}
+        del kb
+        torch.cuda.empty_cache()
+        for name in ("kitti", "euroc"):
+            other[f"stereo_{name}"] = stereo_throughput(name, dev)
+            torch.cuda.empty_cache()
+        line["other_geometries"] = other
     if world == 1 and not args.no_cpu_baseline:
-        frames_np = frames[: min(B, 24), :, :W].cpu().numpy()
+        import synth
+        frames_np = np.stack([synth.torch_stream(1, W, H, device=dev, t0=t, bounded=True)[0].cpu().numpy()
+                              for t in range(24)])
         line["cpu_baseline"] = cpu_baseline(frames_np, W, H, NF, args.cpu_seconds)
+        if "single_frame" in line:
+            line["single_frame"]["cpu_oracle_single_thread_ms"] = line["cpu_baseline"]["single_thread_ms_per_frame"]
     print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -148,6 +148,13 @@ struct orbgpu_extractor {
     // host-image path
     uint8_t* d_img = nullptr;
     size_t img_pitch = 0;
+    // one device block [count, err, pad, pad | keypoints(cap) | descriptors(cap)]
+    // mirrored by one pinned host block, so a frame's outputs come back in a
+    // single asynchronous copy
+    uint8_t* d_single = nullptr;
+    uint8_t* h_single = nullptr;  // pinned
+    uint8_t* h_img = nullptr;     // pinned staging of the host image (img_pitch rows)
+    size_t single_bytes = 0, single_desc_off = 0;
     orbgpu_keypoint* d_kps1 = nullptr;
     uint8_t* d_desc1 = nullptr;
     int* d_count1 = nullptr;
@@ -163,9 +170,11 @@ struct orbgpu_extractor {
 
     ~orbgpu_extractor() {
         void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_bands, d_pyr_yrec, d_pyr_ystage, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
-                        d_oct_count, d_err, d_trace, d_img, d_kps1, d_desc1, d_count1};
+                        d_oct_count, d_err, d_trace, d_img, d_single};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
+        if (h_single) (void)hipHostFree(h_single);
+        if (h_img) (void)hipHostFree(h_img);
         if (stream) (void)hipStreamDestroy(stream);
         for (auto& a : ev)
             for (hipEvent_t x : a) (void)hipEventDestroy(x);
@@ -598,18 +607,22 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
     return ORBGPU_OK;
 }
 
+std::string capacity_message(int err) {
+    std::string m = "kernel capacity overflow:";
+    if (err & kErrCellCap) m += " FAST-cell";
+    if (err & kErrNodeCap) m += " octree-nodes";
+    if (err & kErrKeyCap) m += " octree-keys";
+    if (err & kErrSeqCap) m += " octree-seq";
+    return m;
+}
+
 int collect_errors(orbgpu_extractor* e, hipStream_t s) {
     ORB_HIP(hipStreamSynchronize(s));
     int err = 0;
     ORB_HIP(hipMemcpy(&err, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (err) {
         ORB_HIP(hipMemset(e->d_err, 0, sizeof(int)));
-        std::string m = "kernel capacity overflow:";
-        if (err & kErrCellCap) m += " FAST-cell";
-        if (err & kErrNodeCap) m += " octree-nodes";
-        if (err & kErrKeyCap) m += " octree-keys";
-        if (err & kErrSeqCap) m += " octree-seq";
-        return fail(ORBGPU_ERR_CAPACITY, m);
+        return fail(ORBGPU_ERR_CAPACITY, capacity_message(err));
     }
     return ORBGPU_OK;
 }
@@ -663,12 +676,25 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
         (rc = dalloc(&e->d_cell_counts, (size_t)g.total_cells * B)) || (rc = dalloc(&e->d_gkeys, g.cand_frame * B)) ||
         (rc = dalloc(&e->d_gknode, g.cand_frame * B)) || (rc = dalloc(&e->d_oct_out, (size_t)g.slots_frame * B)) ||
         (rc = dalloc(&e->d_oct_count, (size_t)g.nlevels * B)) || (rc = dalloc(&e->d_err, 1)) ||
-        (rc = dalloc(&e->d_img, e->img_pitch * height)) || (rc = dalloc(&e->d_kps1, (size_t)e->max_kps)) ||
-        (rc = dalloc(&e->d_desc1, (size_t)e->max_kps * 32)) || (rc = dalloc(&e->d_count1, 1)) ||
+        (rc = dalloc(&e->d_img, e->img_pitch * height)) ||
         (rc = dalloc(&e->d_pyr_bands, e->pyr_bands.size())) || (rc = dalloc(&e->d_pyr_yrec, e->pyr_yrec.size())) ||
         (rc = dalloc(&e->d_pyr_ystage, e->pyr_ystage.size()))) {
         delete e;
         return rc;
+    }
+    e->single_desc_off = round_up(16 + (size_t)e->max_kps * sizeof(orbgpu_keypoint), 256);
+    e->single_bytes = e->single_desc_off + (size_t)e->max_kps * 32;
+    if ((rc = dalloc(&e->d_single, e->single_bytes))) {
+        delete e;
+        return rc;
+    }
+    e->d_count1 = reinterpret_cast<int*>(e->d_single);
+    e->d_kps1 = reinterpret_cast<orbgpu_keypoint*>(e->d_single + 16);
+    e->d_desc1 = e->d_single + e->single_desc_off;
+    if (hipHostMalloc((void**)&e->h_single, e->single_bytes, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&e->h_img, e->img_pitch * height, hipHostMallocDefault) != hipSuccess) {
+        delete e;
+        return fail(ORBGPU_ERR_HIP, "pinned staging allocation failed");
     }
     if (hipMemcpy(e->d_ptab, ptab.data(), ptab.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(e->d_pyr_bands, e->pyr_bands.data(), e->pyr_bands.size() * sizeof(int4), hipMemcpyHostToDevice) !=
@@ -746,18 +772,26 @@ int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int hei
     if (width != e->W || height != e->H) return fail(ORBGPU_ERR_ARG, "image size differs from the extractor geometry");
     if (step < (size_t)width) return fail(ORBGPU_ERR_ARG, "step < width");
     hipStream_t s = e->stream;
-    ORB_HIP(hipMemcpy2DAsync(e->d_img, e->img_pitch, image, step, width, height, hipMemcpyHostToDevice, s));
+    // the drop-in (Frame constructor) path: host image -> pinned staging ->
+    // one async H2D; extraction; the error word folded into the output
+    // block; one async D2H of the whole block; one synchronisation
+    for (int y = 0; y < height; ++y) std::memcpy(e->h_img + (size_t)y * e->img_pitch, image + (size_t)y * step, width);
+    ORB_HIP(hipMemcpyAsync(e->d_img, e->h_img, e->img_pitch * height, hipMemcpyHostToDevice, s));
     int rc = run_batch(e, e->d_img, 1, e->img_pitch, e->img_pitch * height, e->d_kps1, e->d_desc1, e->d_count1,
                        e->max_kps, s);
     if (rc) return rc;
-    int count = 0;
-    ORB_HIP(hipMemcpyAsync(&count, e->d_count1, sizeof(int), hipMemcpyDeviceToHost, s));
-    rc = collect_errors(e, s);
-    if (rc) return rc;
+    ORB_HIP(hipMemcpyAsync(e->d_single + 4, e->d_err, sizeof(int), hipMemcpyDeviceToDevice, s));
+    ORB_HIP(hipMemsetAsync(e->d_err, 0, sizeof(int), s));
+    ORB_HIP(hipMemcpyAsync(e->h_single, e->d_single, e->single_bytes, hipMemcpyDeviceToHost, s));
+    ORB_HIP(hipStreamSynchronize(s));
+    int count = 0, err = 0;
+    std::memcpy(&count, e->h_single, sizeof(int));
+    std::memcpy(&err, e->h_single + 4, sizeof(int));
+    if (err) return fail(ORBGPU_ERR_CAPACITY, capacity_message(err));
     if (count > capacity) return fail(ORBGPU_ERR_CAPACITY, "keypoint capacity too small");
     if (count > 0) {
-        if (keypoints) ORB_HIP(hipMemcpy(keypoints, e->d_kps1, (size_t)count * sizeof(orbgpu_keypoint), hipMemcpyDeviceToHost));
-        if (descriptors) ORB_HIP(hipMemcpy(descriptors, e->d_desc1, (size_t)count * 32, hipMemcpyDeviceToHost));
+        if (keypoints) std::memcpy(keypoints, e->h_single + 16, (size_t)count * sizeof(orbgpu_keypoint));
+        if (descriptors) std::memcpy(descriptors, e->h_single + e->single_desc_off, (size_t)count * 32);
     }
     *n = count;
     return ORBGPU_OK;

@@ -17,6 +17,8 @@ to the HIP path.
 """
 from __future__ import annotations
 
+import functools
+
 import numpy as np
 
 BASE_SIZE = 2048
@@ -35,6 +37,12 @@ def _upsample(a: np.ndarray, size: int) -> np.ndarray:
 
 
 def base_texture(seed: int = 0x0B5E) -> np.ndarray:
+    """The 2048x2048 scene (cached per seed; callers must not modify it)."""
+    return _base_texture(seed)
+
+
+@functools.lru_cache(maxsize=4)
+def _base_texture(seed: int) -> np.ndarray:
     rng = np.random.default_rng(seed)
     img = np.zeros((BASE_SIZE, BASE_SIZE), np.float64)
     amp = 60.0
@@ -105,12 +113,27 @@ def noise_image(width: int = 640, height: int = 480, seed: int = 7) -> np.ndarra
     return np.random.default_rng(seed).integers(0, 256, (height, width), dtype=np.uint8)
 
 
+TRAJ_PERIOD = 512  # frames of one back-and-forth pass of the benchmark camera
+
+
+def trajectory_t(frame: int) -> int:
+    """Camera parameter of global frame `frame` in benchmark streams: a
+    triangle wave 0..255..0 (period TRAJ_PERIOD), so arbitrarily long streams
+    stay inside the base texture and consecutive frames always move by one
+    step (true (t-1, t) correspondences everywhere)."""
+    h = TRAJ_PERIOD // 2
+    m = frame % TRAJ_PERIOD
+    return m if m < h else TRAJ_PERIOD - 1 - m
+
+
 def torch_stream(n: int, width: int, height: int, seed: int = 0x0B5E, device="cuda", t0: int = 0,
-                 noise_sigma: float = 2.0, pitch: int | None = None, chunk: int = 64):
+                 noise_sigma: float = 2.0, pitch: int | None = None, chunk: int = 64, bounded: bool = False):
     """GPU-rendered version of mono_stream for benchmark batches (same scene
     geometry; bilinear sampling and noise come from torch, so frames are not
     byte-identical to mono_stream -- parity tests use the numpy renderer).
-    Returns a (n, height, pitch) uint8 tensor (pitch >= width, zero padded)."""
+    Frames t0 .. t0+n-1; with bounded=True global frame f is rendered at
+    trajectory_t(f) (long streams).  Returns a (n, height, pitch) uint8
+    tensor (pitch >= width, zero padded)."""
     import torch
 
     pitch = pitch or width
@@ -125,6 +148,9 @@ def torch_stream(n: int, width: int, height: int, seed: int = 0x0B5E, device="cu
     for s in range(0, n, chunk):
         m = min(chunk, n - s)
         t = torch.arange(t0 + s, t0 + s + m, device=device, dtype=torch.float32)
+        if bounded:
+            t = torch.tensor([trajectory_t(int(f)) for f in range(t0 + s, t0 + s + m)], device=device,
+                             dtype=torch.float32)
         th = torch.deg2rad(0.5 * t)[:, None, None]
         c, sn = torch.cos(th), torch.sin(th)
         sx = c * u - sn * v + (BASE_SIZE / 2 + 2.0 * t)[:, None, None]

@@ -1,13 +1,24 @@
-"""Multi-process (world_size 2, gloo on CPU) coverage of bench.py's N>1 path:
-independent per-rank streams, max-over-ranks elapsed time and the whole-job
-frame count.  The data path has no collective (frame-sharded, weak scaling)."""
+"""Multi-process (world_size 2, gloo on CPU) coverage of the N>1 path
+(orb-slam2-annotation_amd/shard.py):
+
+* one frame stream in contiguous per-rank chunks; the chunk-boundary frame's
+  keypoints/descriptors go to the next rank (send/recv) so the (t-1, t) pair
+  across ranks is matched; every step's outputs are gathered to rank 0;
+* the gathered keypoints, descriptors and SearchForInitialization matches
+  equal a single-process run over the same frames (computed with the CPU
+  oracle: the sharding logic is device independent);
+* bench.aggregate: max-over-ranks elapsed time and the whole-job frame count.
+"""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+CAP = 1100
 
 
 def _free_port():
@@ -18,13 +29,17 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _init(rank, world, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _worker(rank, world, port, q):
+    _init(rank, world, port)
     import bench
     elapsed, frames = bench.aggregate(1.0 + rank, 100 * (rank + 1))
     dist.barrier()
-    q.put((rank, elapsed, frames, bench.rank_seed(rank)))
+    q.put((rank, elapsed, frames))
     dist.destroy_process_group()
 
 
@@ -41,9 +56,103 @@ def test_aggregate_two_ranks_gloo():
         assert p.exitcode == 0
     assert [r[1] for r in res] == [2.0, 2.0]        # max over ranks
     assert [r[2] for r in res] == [300, 300]        # whole-job frames
-    assert res[0][3] != res[1][3]                   # independent streams
 
 
 def test_aggregate_single_process_is_identity():
     import bench
     assert bench.aggregate(3.5, 42) == (3.5, 42)
+
+
+def _extract(ex, img):
+    k, d = ex.extract(img)
+    kp = torch.zeros((CAP, 7), dtype=torch.float32)
+    de = torch.zeros((CAP, 32), dtype=torch.uint8)
+    n = len(k)
+    kp[:n] = torch.from_numpy(k.view(np.float32).reshape(n, 7).copy())
+    de[:n] = torch.from_numpy(d.copy())
+    return kp, de, n
+
+
+def _match(kp1, de1, n1, kp2, de2, n2):
+    import orbgpu
+    import orbref
+    m = torch.full((CAP,), -1, dtype=torch.int32)
+    if n1 == 0 or n2 == 0:
+        return m, 0
+    k1 = kp1[:n1].numpy().copy().view(orbgpu.KP_DTYPE).reshape(n1)
+    k2 = kp2[:n2].numpy().copy().view(orbgpu.KP_DTYPE).reshape(n2)
+    nm, m12, _ = orbref.search_for_initialization(k1, de1[:n1].numpy(), k2, de2[:n2].numpy(), 640, 480)
+    m[:n1] = torch.from_numpy(m12)
+    return m, nm
+
+
+def _shard_worker(rank, world, port, steps, B, q):
+    _init(rank, world, port)
+    import orbref
+    import shard
+    import synth
+    frames = synth.mono_stream(steps * world * B)
+    ex = orbref.Extractor()
+    bx = shard.BoundaryExchange(rank, world, [torch.zeros((CAP, 7)), torch.zeros((CAP, 32), dtype=torch.uint8),
+                                              torch.zeros(1, dtype=torch.int32)])
+    tmpl = [torch.zeros((B, CAP, 7)), torch.zeros((B, CAP, 32), dtype=torch.uint8), torch.zeros(B, dtype=torch.int32),
+            torch.zeros((B, CAP), dtype=torch.int32), torch.zeros(B, dtype=torch.int32)]
+    gather = shard.OwnerGather(rank, world, tmpl)
+    out = {}
+    for s in range(steps):
+        ids = list(shard.chunk_frames(s, rank, world, B))
+        kps, desc, cnt = (torch.zeros_like(t) for t in tmpl[:3])
+        for b, f in enumerate(ids):
+            kps[b], desc[b], n = _extract(ex, frames[f])
+            cnt[b] = n
+        prev = bx.exchange([kps[B - 1], desc[B - 1], cnt[B - 1:B]])
+        m12, nm = torch.full((B, CAP), -1, dtype=torch.int32), torch.zeros(B, dtype=torch.int32)
+        for b in range(B):
+            p = (prev[0], prev[1], int(prev[2][0])) if b == 0 else (kps[b - 1], desc[b - 1], int(cnt[b - 1]))
+            m12[b], nm[b] = _match(*p, kps[b], desc[b], int(cnt[b]))
+        sidx = s % 2
+        gather.start(sidx, [kps, desc, cnt, m12, nm])
+        gather.finish(sidx)
+        if rank == 0:
+            chunks = [(0, [kps, desc, cnt, m12, nm])] + [(r + 1, t) for r, t in enumerate(gather.received(sidx))]
+            for r, (k, d, c, m, n) in chunks:
+                for b, f in enumerate(shard.chunk_frames(s, r, world, B)):
+                    cc = int(c[b])
+                    out[f] = (cc, k[b, :cc].numpy().tobytes(), d[b, :cc].numpy().tobytes(), int(n[b]),
+                              m[b, :cc].numpy().tobytes())
+    gather.finish()
+    dist.barrier()
+    if rank == 0:
+        q.put(out)
+    dist.destroy_process_group()
+
+
+def test_sharded_stream_equals_single_process():
+    import orbref
+    import synth
+    world, steps, B = 2, 2, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, steps, B, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    # single process, frames in stream order, (t-1, t) pairs
+    frames = synth.mono_stream(steps * world * B)
+    ex = orbref.Extractor()
+    prev = (torch.zeros((CAP, 7)), torch.zeros((CAP, 32), dtype=torch.uint8), 0)
+    assert sorted(got) == list(range(len(frames)))
+    cross = 0
+    for f in range(len(frames)):
+        k, d, n = _extract(ex, frames[f])
+        m, nm = _match(*prev, k, d, n)
+        g = got[f]
+        assert g[0] == n and g[1] == k[:n].numpy().tobytes() and g[2] == d[:n].numpy().tobytes(), f
+        assert g[3] == nm and g[4] == m[:n].numpy().tobytes(), f
+        cross += f > 0 and f % B == 0 and nm > 0  # pairs that straddle two chunks
+        prev = (k, d, n)
+    assert cross >= 2
