@@ -186,10 +186,13 @@ __global__ __launch_bounds__(kThreads) void compute_sim3_kernel(
     int rf = Q.rng.f, rb = Q.rng.b;        // lane 0's stream indices
     int cur_round = 0, cur_c = 0, cur_j = 0;  // lane 0's schedule cursor
     bool sched_end = false;
+    // windows grow 32, 64, .., kWin: most queries return within a few
+    // hypotheses, so the first windows stay small (less speculative work)
+    int win = 32;
     while (true) {
         if (tid == 0) {  // lay out the next window in the reference's order
             int n = 0;
-            while (n < kWin && !sched_end) {
+            while (n < win && !sched_end) {
                 if (cur_c == nc) {  // next round of `while (nCandidates > 0 && !bMatch)`
                     bool any = false;
                     for (int c = 0; c < nc; ++c) any |= c_live[c] != 0;
@@ -206,7 +209,7 @@ __global__ __launch_bounds__(kThreads) void compute_sim3_kernel(
                     continue;
                 }
                 const int k = min(ipc, c_max[c] - c_sched[c]);  // iterations of this iterate() call
-                for (; cur_j < k && n < kWin; ++cur_j, ++n) {
+                for (; cur_j < k && n < win; ++cur_j, ++n) {
                     // vAvailableIndices = mvAllIndices; 3 x RandomInt + swap-remove (Sim3Solver.cpp:172-183)
                     const int N = c_n[c];
                     int pos[2], val[2], nmod = 0;
@@ -294,6 +297,7 @@ __global__ __launch_bounds__(kThreads) void compute_sim3_kernel(
         }
         __syncthreads();
         if (s_done) break;
+        win = min(2 * win, kWin);
     }
     __syncthreads();
     const int mc = s_matched;

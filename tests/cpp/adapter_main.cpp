@@ -7,9 +7,20 @@
 //   adapter_main empty
 //       operator() on an empty image must return leaving outputs untouched
 //   adapter_main extract <w> <h> <nfeat> <img0.raw> <img1.raw> <out.bin>
-//       extract two frames, SearchForInitialization(F0, F1), write
-//       [n0, kps0 (28 B each), desc0, n1, kps1, desc1, nmatches, matches12,
-//        level-1 pyramid of frame 1]
+//       extract two frames, ORBmatcher(0.9, true).SearchForInitialization(F0, F1),
+//       write [n0, kps0 (28 B each), desc0, n1, kps1, desc1, nmatches,
+//       matches12, level-1 pyramid of frame 1]
+//   adapter_main proj <variant> <in.bin> <out.bin>
+//       ORBmatcher::SearchByProjection, the overload of <variant> (0 local map,
+//       1 Sim3 loop, 2 last frame, 3 keyframe), on the scenario in in.bin
+//   adapter_main bow <in.bin> <out.bin>
+//       ORBmatcher::SearchByBoW(KF, F) and SearchByBoW(KF1, KF2)
+//   adapter_main pnp <in.bin> <out.bin>
+//       PnPsolver as Tracking::Relocalization drives it (Tracking.cpp:1786-1822)
+//   adapter_main sim3 <in.bin> <out.bin>
+//       Sim3Solvers as LoopClosing::ComputeSim3 drives them (LoopClosing.cpp:311-356)
+// The .bin layouts are written / read by tests/test_adapter.py (fixed
+// field order, little-endian, no headers).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -18,15 +29,90 @@
 #include <iterator>
 #include <vector>
 
+#include <map>
+#include <memory>
+#include <set>
+
 #include "orbslam2_amd/ORBextractor.h"
 #include "orbslam2_amd/ORBmatcher.h"
+#include "orbslam2_amd/PnPsolver.h"
+#include "orbslam2_amd/Sim3Solver.h"
 
 namespace {
 
-struct MiniFrame {  // the members of ORB_SLAM2::Frame the matcher reads
-    std::vector<cv::KeyPoint> mvKeysUn;
-    cv::Mat mDescriptors;
+struct MiniKeyFrame;
+
+// The members of ORB_SLAM2::MapPoint the adapters read (MapPoint.h:43-130),
+// plus the two raw-distance accessors INTEGRATION.md adds.
+struct MiniMapPoint {
+    cv::Mat pos = cv::Mat(3, 1, CV_32F), nrm = cv::Mat(3, 1, CV_32F), desc = cv::Mat(1, 32, CV_8U);
+    bool bad = false;
+    int nobs = 1;
+    float min_d = 0.f, max_d = 0.f;
+    bool mbTrackInView = false;
+    float mTrackProjX = 0.f, mTrackProjY = 0.f, mTrackProjXR = 0.f, mTrackViewCos = 0.f;
+    int mnTrackScaleLevel = 0;
+    std::map<const MiniKeyFrame*, int> index;
+    cv::Mat GetWorldPos() { return pos; }
+    cv::Mat GetNormal() { return nrm; }
+    cv::Mat GetDescriptor() { return desc; }
+    bool isBad() { return bad; }
+    int Observations() { return nobs; }
+    float GetMinDistance() { return min_d; }
+    float GetMaxDistance() { return max_d; }
+    int GetIndexInKeyFrame(MiniKeyFrame* kf) {
+        auto it = index.find(kf);
+        return it == index.end() ? -1 : it->second;
+    }
+};
+
+// The members of ORB_SLAM2::Frame the adapters read (Frame.h:100-200).
+struct MiniFrame {
+    int N = 0;
+    std::vector<cv::KeyPoint> mvKeys, mvKeysUn;
+    cv::Mat mDescriptors, mTcw;
+    std::vector<float> mvuRight;
+    std::vector<MiniMapPoint*> mvpMapPoints;
+    std::vector<bool> mvbOutlier;
+    std::map<unsigned int, std::vector<unsigned int>> mFeatVec;
     float mnMinX = 0.f, mnMaxX = 0.f, mnMinY = 0.f, mnMaxY = 0.f;
+    float fx = 0.f, fy = 0.f, cx = 0.f, cy = 0.f, mbf = 0.f, mb = 0.f;
+    int mnScaleLevels = 8;
+    float mfLogScaleFactor = 0.f;
+    std::vector<float> mvScaleFactors, mvLevelSigma2;
+};
+
+// ... and of ORB_SLAM2::KeyFrame (KeyFrame.h:40-230).
+struct MiniKeyFrame : MiniFrame {
+    cv::Mat mK = cv::Mat(3, 3, CV_32F), Rcw = cv::Mat(3, 3, CV_32F), tcw = cv::Mat(3, 1, CV_32F);
+    std::vector<MiniMapPoint*> GetMapPointMatches() { return mvpMapPoints; }
+    cv::Mat GetRotation() { return Rcw; }
+    cv::Mat GetTranslation() { return tcw; }
+};
+
+struct In {
+    std::vector<unsigned char> b;
+    size_t o = 0;
+    template <class T> T get() {
+        T v;
+        std::memcpy(&v, &b.at(o), sizeof(T));
+        o += sizeof(T);
+        return v;
+    }
+    template <class T> std::vector<T> vec(size_t n) {
+        std::vector<T> v(n);
+        if (n) std::memcpy(v.data(), &b.at(o), n * sizeof(T));
+        o += n * sizeof(T);
+        return v;
+    }
+};
+
+struct Out {
+    FILE* f;
+    explicit Out(const char* p) : f(fopen(p, "wb")) {}
+    ~Out() { fclose(f); }
+    template <class T> void put(T v) { fwrite(&v, sizeof(T), 1, f); }
+    template <class T> void vec(const std::vector<T>& v) { if (!v.empty()) fwrite(v.data(), sizeof(T), v.size(), f); }
 };
 
 std::vector<unsigned char> read_file(const char* path) {
@@ -46,9 +132,382 @@ void put_frame(FILE* out, const MiniFrame& F) {
     for (int i = 0; i < n; ++i) fwrite(F.mDescriptors.ptr<unsigned char>(i), 1, 32, out);
 }
 
+// frame header written by test_adapter._frame_blob: n, keypoints (28 B each),
+// descriptors, u_right, bounds, intrinsics, scale tables, Tcw (16)
+void read_frame(In& in, MiniFrame& F) {
+    F.N = in.get<int>();
+    const std::vector<float> kp = in.vec<float>((size_t)F.N * 7);
+    F.mvKeysUn.resize(F.N);
+    for (int i = 0; i < F.N; ++i) {
+        const float* k = &kp[7 * (size_t)i];
+        int oc, cl;
+        std::memcpy(&oc, &k[5], 4);
+        std::memcpy(&cl, &k[6], 4);
+        F.mvKeysUn[i] = cv::KeyPoint(k[0], k[1], k[2], k[3], k[4], oc, cl);
+    }
+    F.mvKeys = F.mvKeysUn;
+    const std::vector<unsigned char> d = in.vec<unsigned char>((size_t)F.N * 32);
+    F.mDescriptors.create(F.N > 0 ? F.N : 1, 32, CV_8U);
+    if (F.N) std::memcpy(F.mDescriptors.data, d.data(), d.size());
+    F.mvuRight = in.vec<float>(F.N);
+    const std::vector<float> g = in.vec<float>(10);  // bounds 4, fx fy cx cy bf b
+    F.mnMinX = g[0]; F.mnMaxX = g[1]; F.mnMinY = g[2]; F.mnMaxY = g[3];
+    F.fx = g[4]; F.fy = g[5]; F.cx = g[6]; F.cy = g[7]; F.mbf = g[8]; F.mb = g[9];
+    F.mnScaleLevels = in.get<int>();
+    F.mfLogScaleFactor = in.get<float>();
+    F.mvScaleFactors = in.vec<float>(F.mnScaleLevels);
+    F.mvLevelSigma2 = in.vec<float>(F.mnScaleLevels);
+    const std::vector<float> T = in.vec<float>(16);
+    F.mTcw = cv::Mat(4, 4, CV_32F);
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) F.mTcw.at<float>(r, c) = T[4 * r + c];
+    F.mvpMapPoints.assign(F.N, nullptr);
+    F.mvbOutlier.assign(F.N, false);
+}
+
+// map points: n, then per point flags (i32: 1 valid/!bad, 2 has observations),
+// pos 3, normal 3, desc 32, min/max distance, track 4, track level
+std::vector<MiniMapPoint*> read_points(In& in, std::vector<std::unique_ptr<MiniMapPoint>>& store) {
+    const int n = in.get<int>();
+    const std::vector<int> flags = in.vec<int>(n);
+    const std::vector<float> pos = in.vec<float>((size_t)n * 3), nrm = in.vec<float>((size_t)n * 3);
+    const std::vector<unsigned char> desc = in.vec<unsigned char>((size_t)n * 32);
+    const std::vector<float> mind = in.vec<float>(n), maxd = in.vec<float>(n), track = in.vec<float>((size_t)n * 4);
+    const std::vector<int> lvl = in.vec<int>(n);
+    std::vector<MiniMapPoint*> out(n);
+    for (int i = 0; i < n; ++i) {
+        store.emplace_back(new MiniMapPoint());
+        MiniMapPoint* p = store.back().get();
+        p->bad = !(flags[i] & 1);
+        p->nobs = (flags[i] & 2) ? 1 : 0;
+        p->mbTrackInView = (flags[i] & 4) != 0;
+        for (int k = 0; k < 3; ++k) {
+            p->pos.at<float>(k) = pos[3 * (size_t)i + k];
+            p->nrm.at<float>(k) = nrm[3 * (size_t)i + k];
+        }
+        std::memcpy(p->desc.data, &desc[32 * (size_t)i], 32);
+        p->min_d = mind[i];
+        p->max_d = maxd[i];
+        p->mTrackProjX = track[4 * (size_t)i];
+        p->mTrackProjY = track[4 * (size_t)i + 1];
+        p->mTrackProjXR = track[4 * (size_t)i + 2];
+        p->mTrackViewCos = track[4 * (size_t)i + 3];
+        p->mnTrackScaleLevel = lvl[i];
+        out[i] = p;
+    }
+    return out;
+}
+
+// occupancy of target keypoints before the call: 0 none, 1 a MapPoint without
+// observations, 2 one with observations (dummies, reported as -3)
+void occupy(In& in, std::vector<MiniMapPoint*>& slots, std::vector<std::unique_ptr<MiniMapPoint>>& store) {
+    const std::vector<unsigned char> occ = in.vec<unsigned char>(slots.size());
+    for (size_t k = 0; k < slots.size(); ++k)
+        if (occ[k]) {
+            store.emplace_back(new MiniMapPoint());
+            store.back()->nobs = occ[k] == 2 ? 1 : 0;
+            slots[k] = store.back().get();
+        }
+}
+
+std::vector<int> encode(const std::vector<MiniMapPoint*>& slots, const std::vector<MiniMapPoint*>& pts) {
+    std::map<const MiniMapPoint*, int> idx;
+    for (size_t i = 0; i < pts.size(); ++i) idx[pts[i]] = (int)i;
+    std::vector<int> out(slots.size());
+    for (size_t k = 0; k < slots.size(); ++k) {
+        if (!slots[k]) out[k] = -1;
+        else if (idx.count(slots[k])) out[k] = idx[slots[k]];
+        else out[k] = -3;
+    }
+    return out;
+}
+
+int run_proj(int variant, const char* inp, const char* outp) {
+    In in{read_file(inp)};
+    std::vector<std::unique_ptr<MiniMapPoint>> store;
+    const float th = in.get<float>(), nnratio = in.get<float>();
+    const int check_ori = in.get<int>(), orb_dist = in.get<int>(), mono = in.get<int>();
+    const std::vector<float> lastT = in.vec<float>(16);
+    MiniKeyFrame T;  // the target, as a Frame (variants 0, 2, 3) or a KeyFrame (1)
+    read_frame(in, T);
+    occupy(in, T.mvpMapPoints, store);
+    std::vector<MiniMapPoint*> pts = read_points(in, store);
+    const std::vector<int> oct = in.vec<int>(pts.size());
+    const std::vector<float> ang = in.vec<float>(pts.size());
+    ORB_SLAM2::ORBmatcher m(nnratio, check_ori != 0);
+    int nm = 0;
+    std::vector<MiniMapPoint*> result;
+    if (variant == 0) {
+        nm = m.SearchByProjection(T, pts, th);
+        result = T.mvpMapPoints;
+    } else if (variant == 1) {
+        std::vector<MiniMapPoint*> vpMatched = T.mvpMapPoints;
+        nm = m.SearchByProjection(&T, T.mTcw, pts, vpMatched, (int)th);
+        result = vpMatched;
+    } else if (variant == 2) {
+        MiniFrame last;  // LastFrame: one keypoint per point, with its MapPoint
+        last.N = (int)pts.size();
+        last.mvKeys.resize(last.N);
+        last.mvKeysUn.resize(last.N);
+        for (int i = 0; i < last.N; ++i) {
+            last.mvKeys[i].octave = oct[i];
+            last.mvKeysUn[i].angle = ang[i];
+        }
+        last.mvpMapPoints.assign(last.N, nullptr);
+        last.mvbOutlier.assign(last.N, false);
+        for (int i = 0; i < last.N; ++i) {
+            if (pts[i]->bad) last.mvbOutlier[i] = true;  // invalid -> outlier (no isBad() test on this path)
+            last.mvpMapPoints[i] = pts[i];
+        }
+        last.mTcw = cv::Mat(4, 4, CV_32F);
+        for (int r = 0; r < 4; ++r)
+            for (int c = 0; c < 4; ++c) last.mTcw.at<float>(r, c) = lastT[4 * r + c];
+        MiniFrame& cur = T;
+        nm = m.SearchByProjection(cur, static_cast<const MiniFrame&>(last), th, mono != 0);
+        result = T.mvpMapPoints;
+    } else {
+        MiniKeyFrame kf;  // the keyframe's MapPoints = the points, its keypoint angles
+        kf.mvpMapPoints = pts;
+        kf.mvKeysUn.resize(pts.size());
+        for (size_t i = 0; i < pts.size(); ++i) kf.mvKeysUn[i].angle = ang[i];
+        std::set<MiniMapPoint*> found;
+        MiniFrame& cur = T;
+        nm = m.SearchByProjection(cur, &kf, found, th, orb_dist);
+        result = T.mvpMapPoints;
+    }
+    Out out(outp);
+    out.put(nm);
+    out.vec(encode(result, pts));
+    return 0;
+}
+
+void read_bow_frame(In& in, MiniKeyFrame& F, std::vector<std::unique_ptr<MiniMapPoint>>& store) {
+    F.N = in.get<int>();
+    const std::vector<unsigned char> d = in.vec<unsigned char>((size_t)F.N * 32);
+    F.mDescriptors.create(F.N > 0 ? F.N : 1, 32, CV_8U);
+    if (F.N) std::memcpy(F.mDescriptors.data, d.data(), d.size());
+    const std::vector<float> ang = in.vec<float>(F.N);
+    const std::vector<unsigned char> mp = in.vec<unsigned char>(F.N);  // 0 none, 1 good, 2 bad
+    F.mvKeys.resize(F.N);
+    F.mvKeysUn.resize(F.N);
+    F.mvpMapPoints.assign(F.N, nullptr);
+    for (int i = 0; i < F.N; ++i) {
+        F.mvKeys[i].angle = F.mvKeysUn[i].angle = ang[i];
+        if (mp[i]) {
+            store.emplace_back(new MiniMapPoint());
+            store.back()->bad = mp[i] == 2;
+            F.mvpMapPoints[i] = store.back().get();
+        }
+    }
+    const int nn = in.get<int>();
+    const std::vector<int> nodes = in.vec<int>(nn), offs = in.vec<int>(nn + 1);
+    const std::vector<int> feats = in.vec<int>(offs.empty() ? 0 : offs.back());
+    for (int j = 0; j < nn; ++j)
+        for (int q = offs[j]; q < offs[j + 1]; ++q) F.mFeatVec[(unsigned)nodes[j]].push_back((unsigned)feats[q]);
+}
+
+int run_bow(const char* inp, const char* outp) {
+    In in{read_file(inp)};
+    std::vector<std::unique_ptr<MiniMapPoint>> store;
+    const float nnratio = in.get<float>();
+    const int check_ori = in.get<int>();
+    MiniKeyFrame A, B;
+    read_bow_frame(in, A, store);
+    read_bow_frame(in, B, store);
+    ORB_SLAM2::ORBmatcher m(nnratio, check_ori != 0);
+    MiniFrame& F = B;
+    std::vector<MiniMapPoint*> vpMatches;
+    const int n1 = m.SearchByBoW(&A, F, vpMatches);  // KF = A, F = B
+    std::vector<MiniMapPoint*> vp12;
+    const int n2 = m.SearchByBoW(&A, &B, vp12);       // KF1 = A, KF2 = B
+    Out out(outp);
+    out.put(n1);
+    out.vec(encode(vpMatches, A.mvpMapPoints));
+    out.put(n2);
+    out.vec(encode(vp12, B.mvpMapPoints));
+    return 0;
+}
+
+// PnP: seed, the frame (keypoints, sigma^2 table, intrinsics), the MapPoint of
+// every keypoint (0 none, 1 good, 2 bad) and its world position.
+int run_pnp(const char* inp, const char* outp) {
+    In in{read_file(inp)};
+    const unsigned seed = in.get<unsigned>();
+    std::vector<std::unique_ptr<MiniMapPoint>> store;
+    MiniKeyFrame F;
+    read_frame(in, F);
+    const std::vector<unsigned char> mp = in.vec<unsigned char>(F.N);
+    const std::vector<float> pos = in.vec<float>((size_t)F.N * 3);
+    std::vector<MiniMapPoint*> vp(F.N, nullptr);
+    for (int i = 0; i < F.N; ++i)
+        if (mp[i]) {
+            store.emplace_back(new MiniMapPoint());
+            store.back()->bad = mp[i] == 2;
+            for (int k = 0; k < 3; ++k) store.back()->pos.at<float>(k) = pos[3 * (size_t)i + k];
+            vp[i] = store.back().get();
+        }
+    orbgpu_srand(seed);
+    // Tracking::Relocalization (Tracking.cpp:1786-1822)
+    ORB_SLAM2::PnPsolver solver(static_cast<const MiniFrame&>(F), vp);
+    solver.SetRansacParameters(0.99, 10, 300, 4, 0.5, 5.991);
+    bool bNoMore = false;
+    std::vector<bool> vbInliers;
+    int nInliers = 0, calls = 0;
+    cv::Mat Tcw;
+    while (!bNoMore && calls < 100) {
+        ++calls;
+        Tcw = solver.iterate(5, bNoMore, vbInliers, nInliers);
+        if (!Tcw.empty()) break;
+    }
+    Out out(outp);
+    out.put((int)!Tcw.empty());
+    out.put(nInliers);
+    out.put(solver.Iterations());
+    out.put(solver.BestInliers());
+    out.put(solver.MinInliers());
+    out.put(solver.MaxIterations());
+    std::vector<float> T(16, 0.f);
+    if (!Tcw.empty())
+        for (int r = 0; r < 4; ++r)
+            for (int c = 0; c < 4; ++c) T[4 * r + c] = Tcw.at<float>(r, c);
+    out.vec(T);
+    std::vector<unsigned char> inl(F.N, 0);
+    for (size_t i = 0; i < vbInliers.size() && i < inl.size(); ++i) inl[i] = vbInliers[i];
+    out.vec(inl);
+    for (int k = 0; k < 5; ++k) out.put(orbgpu_rand());
+    return 0;
+}
+
+// Sim3: seed, fix_scale, n candidates; the current keyframe (pose, K, sigma^2,
+// per slot: MapPoint state, world position, octave); per candidate the same
+// plus vpMatched12 (per KF1 slot: KF2 slot or -1).
+void read_sim3_kf(In& in, MiniKeyFrame& K, std::vector<std::unique_ptr<MiniMapPoint>>& store) {
+    K.N = in.get<int>();
+    const std::vector<float> T = in.vec<float>(12), k4 = in.vec<float>(4), sig = in.vec<float>(8);
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) K.Rcw.at<float>(r, c) = T[3 * r + c];
+        K.tcw.at<float>(r) = T[9 + r];
+    }
+    K.mK = cv::Mat::eye(3, 3, CV_32F);
+    K.mK.at<float>(0, 0) = k4[0];
+    K.mK.at<float>(1, 1) = k4[1];
+    K.mK.at<float>(0, 2) = k4[2];
+    K.mK.at<float>(1, 2) = k4[3];
+    K.mvLevelSigma2 = sig;
+    const std::vector<unsigned char> mp = in.vec<unsigned char>(K.N);
+    const std::vector<float> pos = in.vec<float>((size_t)K.N * 3);
+    const std::vector<int> oct = in.vec<int>(K.N);
+    K.mvKeysUn.resize(K.N);
+    K.mvpMapPoints.assign(K.N, nullptr);
+    for (int i = 0; i < K.N; ++i) {
+        K.mvKeysUn[i].octave = oct[i];
+        if (!mp[i]) continue;
+        store.emplace_back(new MiniMapPoint());
+        MiniMapPoint* p = store.back().get();
+        p->bad = mp[i] == 2;
+        for (int k = 0; k < 3; ++k) p->pos.at<float>(k) = pos[3 * (size_t)i + k];
+        p->index[&K] = i;
+        K.mvpMapPoints[i] = p;
+    }
+}
+
+int run_sim3(const char* inp, const char* outp) {
+    In in{read_file(inp)};
+    const unsigned seed = in.get<unsigned>();
+    const int fix = in.get<int>(), nc = in.get<int>();
+    std::vector<std::unique_ptr<MiniMapPoint>> store;
+    MiniKeyFrame cur;
+    read_sim3_kf(in, cur, store);
+    std::vector<std::unique_ptr<MiniKeyFrame>> cands;
+    std::vector<std::vector<MiniMapPoint*>> matches(nc);
+    for (int c = 0; c < nc; ++c) {
+        cands.emplace_back(new MiniKeyFrame());
+        read_sim3_kf(in, *cands.back(), store);
+        const std::vector<int> m12 = in.vec<int>(cur.N);
+        matches[c].assign(cur.N, nullptr);
+        for (int i = 0; i < cur.N; ++i)
+            if (m12[i] >= 0) matches[c][i] = cands.back()->mvpMapPoints[m12[i]];
+    }
+    orbgpu_srand(seed);
+    // LoopClosing::ComputeSim3 (LoopClosing.cpp:311-356), verification taken to pass
+    std::vector<std::unique_ptr<ORB_SLAM2::Sim3Solver>> solvers;
+    std::vector<bool> discarded(nc, false);
+    int nCandidates = 0;
+    for (int c = 0; c < nc; ++c) {
+        int nm = 0;
+        for (MiniMapPoint* p : matches[c]) nm += p != nullptr;
+        if (nm < 20) {
+            discarded[c] = true;
+            solvers.emplace_back(nullptr);
+            continue;
+        }
+        solvers.emplace_back(new ORB_SLAM2::Sim3Solver(&cur, cands[c].get(), matches[c], fix != 0));
+        solvers.back()->SetRansacParameters(0.99, 20, 300);
+        ++nCandidates;
+    }
+    int matched = -1, round = -1, nInl = 0;
+    std::vector<bool> vbInliers;
+    cv::Mat Scm;
+    for (int r = 0; nCandidates > 0 && matched < 0; ++r) {
+        for (int c = 0; c < nc; ++c) {
+            if (discarded[c]) continue;
+            bool bNoMore;
+            int n;
+            std::vector<bool> inl;
+            cv::Mat S = solvers[c]->iterate(5, bNoMore, inl, n);
+            if (bNoMore) {
+                discarded[c] = true;
+                --nCandidates;
+            }
+            if (!S.empty()) {
+                matched = c;
+                round = r;
+                nInl = n;
+                vbInliers = inl;
+                Scm = S;
+                break;
+            }
+        }
+    }
+    Out out(outp);
+    out.put(matched);
+    out.put(round);
+    out.put(nInl);
+    for (int c = 0; c < nc; ++c) {
+        out.put(solvers[c] ? solvers[c]->Iterations() : -1);
+        out.put(solvers[c] ? solvers[c]->BestInliers() : -1);
+        out.put(solvers[c] ? solvers[c]->Correspondences() : -1);
+    }
+    std::vector<float> R(9, 0.f), t(3, 0.f);
+    float s = 0.f;
+    if (matched >= 0) {
+        const cv::Mat Rm = solvers[matched]->GetEstimatedRotation(), tm = solvers[matched]->GetEstimatedTranslation();
+        for (int i = 0; i < 9; ++i) R[i] = Rm.at<float>(i / 3, i % 3);
+        for (int i = 0; i < 3; ++i) t[i] = tm.at<float>(i);
+        s = solvers[matched]->GetEstimatedScale();
+    }
+    out.vec(R);
+    out.vec(t);
+    out.put(s);
+    std::vector<unsigned char> inl(cur.N, 0);
+    for (size_t i = 0; i < vbInliers.size() && i < inl.size(); ++i) inl[i] = vbInliers[i];
+    out.vec(inl);
+    for (int k = 0; k < 5; ++k) out.put(orbgpu_rand());
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
+    try {
+        if (argc >= 5 && !strcmp(argv[1], "proj")) return run_proj(atoi(argv[2]), argv[3], argv[4]);
+        if (argc >= 4 && !strcmp(argv[1], "bow")) return run_bow(argv[2], argv[3]);
+        if (argc >= 4 && !strcmp(argv[1], "pnp")) return run_pnp(argv[2], argv[3]);
+        if (argc >= 4 && !strcmp(argv[1], "sim3")) return run_sim3(argv[2], argv[3]);
+    } catch (const std::exception& e) {
+        fprintf(stderr, "exception: %s\n", e.what());
+        return 3;
+    }
     if (argc >= 5 && !strcmp(argv[1], "scales")) {
         ORB_SLAM2::ORBextractor ex(atoi(argv[2]), (float)atof(argv[3]), atoi(argv[4]), 20, 7);
         const auto s = ex.GetScaleFactors(), is = ex.GetInverseScaleFactors();
@@ -84,7 +543,8 @@ int main(int argc, char** argv) {
             std::vector<cv::Point2f> prev;
             for (const cv::KeyPoint& k : F[0].mvKeysUn) prev.push_back(k.pt);
             std::vector<int> m12;
-            const int nm = orbslam2_amd::SearchForInitialization(0.9f, true, F[0], F[1], prev, m12, 100);
+            ORB_SLAM2::ORBmatcher matcher(0.9f, true);  // Tracking.cpp:766-769
+            const int nm = matcher.SearchForInitialization(F[0], F[1], prev, m12, 100);
             FILE* out = fopen(argv[7], "wb");
             put_frame(out, F[0]);
             put_frame(out, F[1]);

@@ -13,6 +13,8 @@
 
 #define CV_8U 0
 #define CV_8UC1 0
+#define CV_32F 5
+#define CV_64F 6
 
 namespace cv {
 
@@ -38,21 +40,44 @@ public:
     size_t step = 0;
     unsigned char* data = nullptr;
     Mat() = default;
-    Mat(int r, int c, int /*type*/, void* ext, size_t st = 0)
-        : rows(r), cols(c), step(st ? st : (size_t)c), data(static_cast<unsigned char*>(ext)) {}
-    void create(int r, int c, int /*type*/) {
-        if (r == rows && c == cols && buf_) return;
-        buf_ = std::make_shared<std::vector<unsigned char>>((size_t)r * c);
-        rows = r; cols = c; step = (size_t)c; data = buf_->data();
+    Mat(int r, int c, int t, void* ext, size_t st = 0)
+        : rows(r), cols(c), step(st ? st : (size_t)c * esize(t)), data(static_cast<unsigned char*>(ext)), type_(t) {}
+    Mat(int r, int c, int t) { create(r, c, t); }
+    void create(int r, int c, int t) {
+        if (r == rows && c == cols && t == type_ && buf_) return;
+        buf_ = std::make_shared<std::vector<unsigned char>>((size_t)r * c * esize(t));
+        rows = r; cols = c; type_ = t; step = (size_t)c * esize(t); data = buf_->data();
     }
     void release() { buf_.reset(); rows = cols = 0; step = 0; data = nullptr; }
     bool empty() const { return data == nullptr || rows == 0 || cols == 0; }
-    int type() const { return CV_8UC1; }
+    int type() const { return type_; }
+    Mat clone() const {
+        Mat m(rows, cols, type_);
+        for (int r = 0; r < rows; ++r)
+            for (size_t b = 0; b < (size_t)cols * esize(type_); ++b) m.data[r * m.step + b] = data[r * step + b];
+        return m;
+    }
+    static Mat eye(int r, int c, int t) {
+        Mat m(r, c, t);
+        for (int i = 0; i < r; ++i)
+            for (int j = 0; j < c; ++j) {
+                if (t == CV_32F) m.at<float>(i, j) = i == j ? 1.f : 0.f;
+                else if (t == CV_64F) m.at<double>(i, j) = i == j ? 1.0 : 0.0;
+                else m.at<unsigned char>(i, j) = i == j ? 1 : 0;
+            }
+        return m;
+    }
     template <class T> T* ptr(int r) { return reinterpret_cast<T*>(data + (size_t)r * step); }
     template <class T> const T* ptr(int r) const { return reinterpret_cast<const T*>(data + (size_t)r * step); }
+    template <class T> T& at(int r, int c) { return ptr<T>(r)[c]; }
+    template <class T> const T& at(int r, int c) const { return ptr<T>(r)[c]; }
+    template <class T> T& at(int i) { return rows == 1 ? at<T>(0, i) : at<T>(i, 0); }
+    template <class T> const T& at(int i) const { return rows == 1 ? at<T>(0, i) : at<T>(i, 0); }
 
 private:
+    static size_t esize(int t) { return t == CV_32F ? 4 : t == CV_64F ? 8 : 1; }
     std::shared_ptr<std::vector<unsigned char>> buf_;
+    int type_ = CV_8UC1;
 };
 
 class _InputArray {

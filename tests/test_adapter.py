@@ -85,3 +85,254 @@ def test_adapter_extract_and_match_vs_oracle(exe, tmp_path):
     n_r, m_r, _ = orbref.search_for_initialization(kr0, dr0, kr1, dr1, w, h)
     assert nm == n_r
     np.testing.assert_array_equal(m12, m_r)
+
+
+# ---- ORBmatcher / PnPsolver / Sim3Solver class surfaces (C++) --------------
+# adapter_main drives the header-only classes with mini Frame / KeyFrame /
+# MapPoint types carrying the reference's member names; the outputs are
+# compared with the CPU oracle (proj_ref, bow_ref, pnp_ref, loop_ref) on the
+# same scenario.
+
+F32 = np.float32
+
+
+def _frame_blob(tgt, sigma2=None):
+    """read_frame() layout of adapter_main.cpp"""
+    k = np.ascontiguousarray(tgt["kps"])
+    n = len(k)
+    sf = np.asarray(tgt["scale_factors"], F32)
+    s2 = np.asarray(sigma2 if sigma2 is not None else sf * sf, F32)
+    ur = tgt.get("u_right")
+    ur = np.full(n, -1, F32) if ur is None else np.asarray(ur, F32)
+    g = np.array([tgt[f] for f in ("min_x", "max_x", "min_y", "max_y", "fx", "fy", "cx", "cy", "bf", "b")], F32)
+    T = np.asarray(tgt["Tcw"], F32).reshape(4, 4)
+    return b"".join([struct.pack("<i", n), k.tobytes(), np.ascontiguousarray(tgt["desc"], np.uint8).tobytes(),
+                     ur.tobytes(), g.tobytes(), struct.pack("<if", len(sf), float(tgt["log_scale_factor"])),
+                     sf.tobytes(), s2.tobytes(), T.tobytes()])
+
+
+def _points_blob(p):
+    n = len(p["flags"])
+    z = lambda k, w: np.zeros((n, w), F32) if p.get(k) is None else np.asarray(p[k], F32).reshape(n, w)  # noqa: E731
+    lvl = np.zeros(n, np.int32) if p.get("track_level") is None else np.asarray(p["track_level"], np.int32)
+    return b"".join([struct.pack("<i", n), np.asarray(p["flags"], np.int32).tobytes(), z("pos", 3).tobytes(),
+                     z("normal", 3).tobytes(), np.ascontiguousarray(p["desc"], np.uint8).tobytes(),
+                     z("min_dist", 1).tobytes(), z("max_dist", 1).tobytes(), z("track", 4).tobytes(), lvl.tobytes()])
+
+
+def _run(exe, tmp_path, mode, blob, *args):
+    inp, out = tmp_path / f"{mode}.in", tmp_path / f"{mode}.out"
+    inp.write_bytes(blob)
+    r = subprocess.run([exe, mode, *map(str, args), str(inp), str(out)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return out.read_bytes()
+
+
+PROJ_CASES = [  # variant, th, kwargs, stereo, scale (as tests/test_proj.py)
+    (0, 1.0, dict(nnratio=0.8), False, 1.0),
+    (0, 3.0, dict(nnratio=0.6), True, 1.0),
+    (1, 10.0, dict(), False, 1.7),
+    (2, 15.0, dict(check_ori=True, mono=True), False, 1.0),
+    (2, 7.0, dict(check_ori=False, mono=False), True, 1.0),
+    (3, 10.0, dict(check_ori=True, orb_dist=100), False, 1.0),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant,th,kw,stereo,scale", PROJ_CASES)
+def test_adapter_orbmatcher_search_by_projection(exe, tmp_path, variant, th, kw, stereo, scale):
+    """ORB_SLAM2::ORBmatcher::SearchByProjection (all four overloads) vs oracle/proj_ref.py"""
+    import proj_ref
+    tgt, pts = synth.projection_scenario(700, 400, 20 + variant * 7, stereo=stereo, scale=scale)
+    if variant == 0:
+        fl, tr, lv = proj_ref.is_in_frustum(tgt, pts, 0.5)
+        pts = dict(pts, flags=fl, track=tr, track_level=lv)
+    last = np.asarray(tgt["Tcw"], F32).copy()
+    if variant == 2:
+        last[:3, 3] += np.random.default_rng(3).uniform(-0.2, 0.2, 3).astype(F32)
+        kw = dict(kw, last_Tcw=last)
+    nm_r, m_r = proj_ref.search_by_projection(variant, tgt, pts, th, **kw)
+    blob = b"".join([struct.pack("<ffiii", th, kw.get("nnratio", 0.6), int(kw.get("check_ori", True)),
+                                 int(kw.get("orb_dist", 50)), int(kw.get("mono", True))), last.tobytes(),
+                     _frame_blob(tgt), np.asarray(tgt["occupied"], np.uint8).tobytes(), _points_blob(pts),
+                     np.asarray(pts["octave"], np.int32).tobytes(), np.asarray(pts["angle"], F32).tobytes()])
+    buf = _run(exe, tmp_path, "proj", blob, variant)
+    nm, = struct.unpack_from("<i", buf, 0)
+    got = np.frombuffer(buf, np.int32, len(tgt["kps"]), 4)
+    occ = np.asarray(tgt["occupied"])
+    want = np.where(m_r >= 0, m_r, np.where(m_r == -2, -1, np.where(occ > 0, -3, -1)))
+    assert nm == nm_r
+    np.testing.assert_array_equal(got, want)
+    assert nm_r > 30
+
+
+def _bow_frame_blob(desc, angle, mp_state, fv):
+    nodes = np.array(sorted(fv), np.int32)
+    offs = np.zeros(len(nodes) + 1, np.int32)
+    feats = []
+    for i, k in enumerate(nodes):
+        feats += list(fv[int(k)])
+        offs[i + 1] = len(feats)
+    return b"".join([struct.pack("<i", len(desc)), np.ascontiguousarray(desc, np.uint8).tobytes(),
+                     np.asarray(angle, F32).tobytes(), np.asarray(mp_state, np.uint8).tobytes(),
+                     struct.pack("<i", len(nodes)), nodes.tobytes(), offs.tobytes(),
+                     np.array(feats, np.int32).tobytes()])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nnratio,check_ori", [(0.75, True), (0.6, False)])
+def test_adapter_orbmatcher_search_by_bow(exe, tmp_path, nnratio, check_ori):
+    """ORB_SLAM2::ORBmatcher::SearchByBoW(KF, F) and (KF1, KF2) vs oracle/bow_ref.py"""
+    import bow_ref
+    par, leaf, desc, w = synth.synthetic_vocabulary(8, 4, 5)
+    voc = bow_ref.Vocabulary.from_arrays(8, 4, 0, 0, par, leaf, desc, w)
+    rng = np.random.default_rng(23)
+    n = 900
+    d1, a1, d2, a2 = synth.bow_frame_pair(desc[leaf == 1], n, 0.6, seed=41)
+    fv1, fv2 = voc.transform(d1, 2)[3], voc.transform(d2, 2)[3]
+    s1 = rng.choice([0, 1, 1, 1, 1, 1, 1, 2], n).astype(np.uint8)  # none / good / bad MapPoint
+    s2 = rng.choice([0, 1, 1, 1, 1, 1, 1, 2], n).astype(np.uint8)
+    blob = struct.pack("<fi", nnratio, int(check_ori)) + _bow_frame_blob(d1, a1, s1, fv1) + \
+        _bow_frame_blob(d2, a2, s2, fv2)
+    buf = _run(exe, tmp_path, "bow", blob)
+    n1, = struct.unpack_from("<i", buf, 0)
+    m1 = np.frombuffer(buf, np.int32, n, 4)
+    n2, = struct.unpack_from("<i", buf, 4 + 4 * n)
+    m2 = np.frombuffer(buf, np.int32, n, 8 + 4 * n)
+    r1, mr1 = bow_ref.search_by_bow(0, fv1, d1, a1, s1 == 1, fv2, d2, a2, np.ones(n, bool), nnratio, check_ori)
+    r2, mr2 = bow_ref.search_by_bow(1, fv1, d1, a1, s1 == 1, fv2, d2, a2, s2 == 1, nnratio, check_ori)
+    assert (n1, n2) == (r1, r2) and r1 > 50 and r2 > 50
+    np.testing.assert_array_equal(m1, mr1)  # per F slot: the KF slot whose MapPoint it got
+    np.testing.assert_array_equal(m2, mr2)  # per KF1 slot: the KF2 slot
+
+
+LIBC = None
+
+
+def _libc():
+    global LIBC
+    if LIBC is None:
+        import ctypes
+        LIBC = ctypes.CDLL("libc.so.6")
+    return LIBC
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,n,frac", [(0, 80, 0.6), (5, 200, 0.5)])
+def test_adapter_pnpsolver_relocalization(exe, tmp_path, seed, n, frac):
+    """ORB_SLAM2::PnPsolver driven as Tracking::Relocalization does, vs a
+    sequential oracle replay (oracle/pnp_ref.py) drawing from glibc itself."""
+    import pnp_ref
+    P = synth.pnp_problem(n, frac, seed=77 + seed)
+    table = (F32(1.2) ** (2 * np.arange(8))).astype(F32)
+    octv = np.array([int(np.nonzero(table == s)[0][0]) for s in P["sigma2"]], np.int32)
+    # interleave keypoints without a MapPoint (0) and with a bad one (2)
+    rng = np.random.default_rng(seed)
+    extra = 25
+    N = n + extra
+    slots = np.sort(rng.choice(N, n, replace=False))
+    state = np.zeros(N, np.uint8)
+    state[slots] = 1
+    rest = np.setdiff1d(np.arange(N), slots)
+    state[rest[: extra // 2]] = 2
+    kps = np.zeros(N, orbref.KP_DTYPE)
+    kps["x"][slots], kps["y"][slots] = P["P2"][:, 0], P["P2"][:, 1]
+    kps["octave"][slots] = octv
+    kps["x"][rest], kps["y"][rest] = 100.0, 100.0
+    pos = np.zeros((N, 3), F32)
+    pos[slots] = P["P3w"]
+    pos[rest] = rng.uniform(-1, 1, (len(rest), 3)).astype(F32)
+    fu, fv, uc, vc = P["cam"]
+    tgt = {"kps": kps, "desc": np.zeros((N, 32), np.uint8), "min_x": 0, "max_x": 640, "min_y": 0, "max_y": 480,
+           "fx": fu, "fy": fv, "cx": uc, "cy": vc, "bf": 0, "b": 0, "log_scale_factor": float(np.log(F32(1.2))),
+           "scale_factors": np.sqrt(table).astype(F32), "Tcw": np.eye(4, dtype=F32)}
+    blob = struct.pack("<I", 0) + _frame_blob(tgt, sigma2=table) + state.tobytes() + pos.tobytes()
+    buf = _run(exe, tmp_path, "pnp", blob)
+    found, n_inl, its, best, min_inl, max_its = struct.unpack_from("<6i", buf, 0)
+    T = np.frombuffer(buf, F32, 16, 24).reshape(4, 4)
+    vb = np.frombuffer(buf, np.uint8, N, 88).astype(bool)
+    nxt = list(np.frombuffer(buf, np.int32, 5, 88 + N))
+    # oracle replay (Tracking.cpp:1786-1822 with one solver): the `||` loop
+    L = _libc()
+    L.srand(0)
+    samples = []
+    for _ in range(max(max_its, 5)):
+        avail = list(range(n))
+        tri = []
+        for _ in range(4):
+            r = int((L.rand() / (2147483647 + 1.0)) * len(avail))
+            tri.append(avail[r]); avail[r] = avail[-1]; avail.pop()
+        samples.append(tri)
+    maxerr = (P["sigma2"] * F32(5.991)).astype(F32)
+    o = pnp_ref.ransac_call(P["P3w"], P["P2"], maxerr, P["cam"], min_inl, 0, np.zeros(n, bool), np.array(samples))
+    assert found == o["found"] == 1
+    assert its == o["consumed"]
+    assert np.abs(T[:3, :3] - o["refined_R"]).max() <= 1e-3
+    assert np.abs(T[:3, 3] - o["refined_t"]).max() <= 1e-3 * (1 + np.abs(o["refined_t"]).max())
+    want = np.zeros(N, bool)
+    want[slots[o["refined_mask"]]] = True
+    assert (vb != want).sum() <= max(1, n // 100)
+    assert abs(n_inl - int(o["refined_mask"].sum())) <= max(1, n // 100)
+    assert not vb[rest].any()
+    L.srand(0)
+    for _ in range(4 * o["consumed"]):
+        L.rand()
+    assert nxt == [L.rand() for _ in range(5)]
+
+
+def _sim3_kf_blob(Tcw, K, sig2, state, pos, octv):
+    return b"".join([struct.pack("<i", len(state)), np.asarray(Tcw, F32).tobytes(), np.asarray(K, F32).tobytes(),
+                     np.asarray(sig2, F32).tobytes(), np.asarray(state, np.uint8).tobytes(),
+                     np.asarray(pos, F32).tobytes(), np.asarray(octv, np.int32).tobytes()])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fix_scale", [False, True])
+def test_adapter_sim3solver_compute_sim3(exe, tmp_path, fix_scale):
+    """ORB_SLAM2::Sim3Solver driven as LoopClosing::ComputeSim3 does (round-robin
+    iterate(5) over the candidates) vs oracle/loop_ref.py with glibc draws."""
+    import loop_ref
+    p, l, d, w = synth.synthetic_vocabulary_fast(10, 3, 4)
+    nc = 4
+    sc = synth.loop_burst_scene(1, nc, d[l == 1], n_kp=400, inlier_frac=[0.0, 0.02, 0.3, 0.3],
+                                outlier_frac=[0.0, 0.15, 0.3, 0.3], seed=9 + fix_scale, fix_scale=fix_scale)
+    rng = np.random.default_rng(2)
+    state = np.where(sc["valid"] > 0, np.where(rng.random(sc["valid"].shape) < 0.05, 2, 1), 0).astype(np.uint8)
+    blob = struct.pack("<Iii", 0, int(fix_scale), nc)
+    blob += _sim3_kf_blob(sc["Tcw"][0], sc["K"], sc["sigma2"], state[0], sc["mp_world"][0], sc["octave"][0])
+    m12s, solvers = [], []
+    for c in range(nc):
+        kf = 1 + c
+        tr = sc["truth"][c]
+        m12 = np.full(400, -1, np.int32)
+        m12[np.r_[tr["src"], tr["outlier_src"]]] = np.r_[tr["dst"], tr["outlier_dst"]]
+        m12s.append(m12)
+        blob += _sim3_kf_blob(sc["Tcw"][kf], sc["K"], sc["sigma2"], state[kf], sc["mp_world"][kf],
+                              sc["octave"][kf]) + m12.tobytes()
+        nm = int(((m12 >= 0) & (state[kf][np.maximum(m12, 0)] > 0)).sum())
+        corr = loop_ref.sim3_setup(m12, state[0] == 1, state[kf] == 1, sc["mp_world"][0], sc["mp_world"][kf],
+                                   sc["Tcw"][0], sc["Tcw"][kf], sc["octave"][0], sc["octave"][kf], sc["sigma2"])
+        solvers.append(loop_ref.Sim3SolverRef(corr, sc["K"], sc["K"], fix_scale) if nm >= 20 else None)
+    buf = _run(exe, tmp_path, "sim3", blob)
+    matched, rnd, n_inl = struct.unpack_from("<3i", buf, 0)
+    per = np.frombuffer(buf, np.int32, 3 * nc, 12).reshape(nc, 3)
+    off = 12 + 12 * nc
+    R = np.frombuffer(buf, F32, 9, off).reshape(3, 3)
+    t = np.frombuffer(buf, F32, 3, off + 36)
+    s, = struct.unpack_from("<f", buf, off + 48)
+    vb = np.frombuffer(buf, np.uint8, 400, off + 52).astype(bool)
+    nxt = list(np.frombuffer(buf, np.int32, 5, off + 52 + 400))
+    ref = loop_ref.compute_sim3(solvers, 0)
+    after = [loop_ref.libc().rand() for _ in range(5)]
+    assert (matched, rnd, n_inl) == (ref["matched"], ref["round"], ref["n_inliers"])
+    for c in range(nc):
+        sv = solvers[c]
+        assert tuple(per[c]) == ((sv.iterations, sv.best, sv.N) if sv is not None else (-1, -1, -1)), c
+    assert nxt == after
+    assert matched >= 0
+    pose = solvers[matched].best_pose
+    assert np.abs(R - pose["R12"]).max() < 2e-4 and abs(s - pose["s12"]) < 2e-4
+    assert np.abs(t - pose["t12"]).max() < 2e-4 * (1 + np.abs(pose["t12"]).max())
+    want = np.zeros(400, bool)
+    want[solvers[matched].idx[solvers[matched].best_mask]] = True
+    np.testing.assert_array_equal(vb, want)
