@@ -398,6 +398,8 @@ void split_node(const QNode& p, const std::vector<Cand>& cand, QNode ch[4]) {
     for (int q = 0; q < 4; ++q) ch[q].no_more = ch[q].keys.size() == 1;
 }
 
+int g_tiebreak_mode = 0;
+
 std::vector<int> distribute_octree(const std::vector<Cand>& cand, int minX, int maxX, int minY, int maxY, int N) {
     const int nIni = (int)std::round((float)(maxX - minX) / (float)(maxY - minY));
     const float hX = (float)(maxX - minX) / nIni;
@@ -422,8 +424,17 @@ std::vector<int> distribute_octree(const std::vector<Cand>& cand, int minX, int 
     }
 
     typedef std::pair<int, QNode*> Entry;
-    auto by_size_seq = [](const Entry& a, const Entry& b) {
-        return a.first != b.first ? a.first < b.first : a.second->seq < b.second->seq;
+    // Ties of equal size: the spec (mode 0) orders by creation sequence; the
+    // reference sorts (size, ExtractorNode*) pairs, i.e. by heap address
+    // (ORBextractor.cpp:690).  Modes 1 (reversed sequence) and 2 (this
+    // process's heap addresses of the list nodes) exist only to measure how
+    // often the choice changes the result (tools/h2_tiebreak.py).
+    const int tmode = g_tiebreak_mode;
+    auto by_size_seq = [tmode](const Entry& a, const Entry& b) {
+        if (a.first != b.first) return a.first < b.first;
+        if (tmode == 1) return a.second->seq > b.second->seq;
+        if (tmode == 2) return std::less<const QNode*>()(a.second, b.second);
+        return a.second->seq < b.second->seq;
     };
     auto push_children = [&](QNode ch[4], std::vector<Entry>& expand) {
         int grow = 0;
@@ -500,6 +511,8 @@ struct orbref_extractor {
 };
 
 extern "C" {
+
+void orbref_set_tiebreak(int mode) { g_tiebreak_mode = mode; }
 
 orbref_extractor* orbref_create(int nfeatures, float scale_factor, int nlevels, int ini_th, int min_th) {
     if (nfeatures <= 0 || nlevels <= 0 || !(scale_factor > 1.f)) return nullptr;

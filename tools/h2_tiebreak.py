@@ -1,0 +1,71 @@
+"""H2: how often does DistributeOctTree's tie-break between
+equal-size nodes change the extractor's output?
+
+The reference sorts (size, ExtractorNode*) pairs (src/ORBextractor.cpp:690),
+so ties fall to heap addresses; the spec here breaks them by creation
+sequence.  This runs the CPU oracle over synthetic streams of each geometry
+with three tie-breaks -- 0 creation sequence (spec), 1 reversed sequence,
+2 heap address of the oracle's own list nodes (the reference's mechanism in
+this process) -- and reports the fraction of frames (and keypoints) whose
+output differs from mode 0.
+
+usage: python tools/h2_tiebreak.py [--frames 200] [--json out.json]
+"""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+for p in (ROOT / "orb-slam2-annotation_amd", ROOT / "oracle"):
+    sys.path.insert(0, str(p))
+
+import numpy as np  # noqa: E402
+
+import orbref  # noqa: E402
+import synth  # noqa: E402
+
+GEOMS = {"mono640": (640, 480, 1000), "kitti": (1241, 376, 2000), "euroc": (752, 480, 1200)}
+
+
+def measure(w, h, nf, frames, seed=0x0B5E):
+    imgs = synth.mono_stream(frames, w, h, seed=seed)
+    ex = orbref.Extractor(nfeatures=nf)
+    out = {}
+    base = []
+    L = orbref.lib()
+    for mode in (0, 1, 2):
+        L.orbref_set_tiebreak(mode)
+        res = [ex.extract(im) for im in imgs]
+        if mode == 0:
+            base = res
+            continue
+        frames_diff = kp_diff = kp_total = 0
+        for (k0, d0), (k1, d1) in zip(base, res):
+            kp_total += len(k0)
+            if len(k0) != len(k1) or k0.tobytes() != k1.tobytes() or not np.array_equal(d0, d1):
+                frames_diff += 1
+                a = {(float(x), float(y), int(o)) for x, y, o in zip(k0["x"], k0["y"], k0["octave"])}
+                b = {(float(x), float(y), int(o)) for x, y, o in zip(k1["x"], k1["y"], k1["octave"])}
+                kp_diff += len(a ^ b) // 2 + abs(len(k0) - len(k1))
+        out[{1: "reversed_sequence", 2: "heap_address"}[mode]] = {
+            "frames_changed": frames_diff, "frames": len(imgs), "frame_fraction": frames_diff / len(imgs),
+            "keypoints_changed": kp_diff, "keypoint_fraction": kp_diff / max(kp_total, 1)}
+    L.orbref_set_tiebreak(0)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=200)
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    res = {g: measure(*GEOMS[g], a.frames) for g in GEOMS}
+    txt = json.dumps(res, indent=1)
+    print(txt)
+    if a.json:
+        Path(a.json).write_text(txt)
+
+
+if __name__ == "__main__":
+    main()
