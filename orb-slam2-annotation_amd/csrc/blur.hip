@@ -10,88 +10,23 @@
 // pass); HBM: read + write each level once, 6/63 halo rows re-read from L2.
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
+#include "blur_device.h"
 
 namespace orbgpu {
 
 namespace {
 
 constexpr int kStrip = kBlurStrip;
+using namespace blurdev;
 
 // BORDER_REFLECT_101 for an overshoot of at most n - 1 (<= 6 for the filter
 // taps; the interior strip's unused prefetches go up to 9 rows past a strip
 // and are clamped after reflection)
 __device__ inline int reflect101(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
 
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// Row pass of 4 adjacent columns: packed 16-bit arithmetic, two columns per
-// register.  P[j] = (px[j], px[j+1]) with px[j] = column x0 - 3 + j.  The
-// symmetric sum 18(a+g) + 34(b+f) + 49(c+e) + 55d of 8-bit inputs is at most
-// 255 * 257 = 65535: exact in u16.  Returns the 4 sums as floats (exact).
-__device__ __forceinline__ void row_pass(const uint32_t (&P)[9], f32x2& lo, f32x2& hi) {
-    const u16x2* Q = reinterpret_cast<const u16x2*>(P);
-    const u16x2 k18 = {18, 18}, k34 = {34, 34}, k49 = {49, 49}, k55 = {55, 55};
-    const u16x2 r01 = (Q[0] + Q[6]) * k18 + (Q[1] + Q[5]) * k34 + (Q[2] + Q[4]) * k49 + Q[3] * k55;
-    const u16x2 r23 = (Q[2] + Q[8]) * k18 + (Q[3] + Q[7]) * k34 + (Q[4] + Q[6]) * k49 + Q[5] * k55;
-    lo = f32x2{(float)r01.x, (float)r01.y};
-    hi = f32x2{(float)r23.x, (float)r23.y};
-}
-
-// Column pass over the 7-row window (w[i] = row y - 3 + i), two columns per
-// packed-f32 op.  Every product and partial sum is an integer below 2^24
-// unless the total is (then the result saturates to 255 either way), so the
-// float arithmetic is exact.
-__device__ __forceinline__ f32x2 col_pass(f32x2 w0, f32x2 w1, f32x2 w2, f32x2 w3, f32x2 w4, f32x2 w5, f32x2 w6) {
-    const f32x2 k18 = {18.f, 18.f}, k34 = {34.f, 34.f}, k49 = {49.f, 49.f}, k55 = {55.f, 55.f};
-    f32x2 s = w3 * k55;
-    s = __builtin_elementwise_fma(w2 + w4, k49, s);
-    s = __builtin_elementwise_fma(w1 + w5, k34, s);
-    s = __builtin_elementwise_fma(w0 + w6, k18, s);
-    return s * f32x2{1.f / 65536.f, 1.f / 65536.f};  // exact: power of two
-}
-
-// 8-bit result of one column on the scalar tail (x >= 4*floor(w/4)):
-// FixedPtCastEx rounds half up.  (The vector path, SymmColumnVec_32s8u,
-// rounds half to even: v_cvt_pk_u8_f32 in store_row.)
-__device__ __forceinline__ uint32_t to_u8(float v) {
-    return (uint32_t)fminf(__builtin_floorf(v + 0.5f), 255.f);  // v + 0.5 exact (< 2^8, 16 frac bits)
-}
-
-// 8-bit packing of 4 filtered columns; v_cvt_pk_u8_f32 rounds to nearest
-// even and saturates (the vector path), to_u8 rounds half up (the tail).
-__device__ __forceinline__ uint32_t pack4(f32x2 lo, f32x2 hi, bool simd) {
-    if (simd) {
-        uint32_t packed = __builtin_amdgcn_cvt_pk_u8_f32(lo.x, 0, 0u);
-        packed = __builtin_amdgcn_cvt_pk_u8_f32(lo.y, 1, packed);
-        packed = __builtin_amdgcn_cvt_pk_u8_f32(hi.x, 2, packed);
-        return __builtin_amdgcn_cvt_pk_u8_f32(hi.y, 3, packed);
-    }
-    return to_u8(lo.x) | (to_u8(lo.y) << 8) | (to_u8(hi.x) << 16) | (to_u8(hi.y) << 24);
-}
-
 #ifndef BLUR_PROBE
 #define BLUR_PROBE 0  // diagnostic builds only: bit 0 = no stores in interior strips
 #endif
-
-struct Raw3 {
-    uint32_t a, b, c;  // level columns x0-4 .. x0+7
-};
-
-__device__ __forceinline__ void row_pass_raw(const Raw3& R, f32x2& lo, f32x2& hi) {
-    uint32_t P[9];
-    // bytes of (b:a) / (c:b) as v_perm_b32 sees them: low word 0-3, high word 4-7
-    P[0] = __builtin_amdgcn_perm(R.b, R.a, 0x0c020c01u);
-    P[1] = __builtin_amdgcn_perm(R.b, R.a, 0x0c030c02u);
-    P[2] = __builtin_amdgcn_perm(R.b, R.a, 0x0c040c03u);
-    P[3] = __builtin_amdgcn_perm(R.b, R.a, 0x0c050c04u);
-    P[4] = __builtin_amdgcn_perm(R.c, R.b, 0x0c020c01u);
-    P[5] = __builtin_amdgcn_perm(R.c, R.b, 0x0c030c02u);
-    P[6] = __builtin_amdgcn_perm(R.c, R.b, 0x0c040c03u);
-    P[7] = __builtin_amdgcn_perm(R.c, R.b, 0x0c050c04u);
-    P[8] = __builtin_amdgcn_perm(R.c, R.b, 0x0c060c05u);
-    row_pass(P, lo, hi);
-}
 
 // Interior strip (columns x0-3 .. x0+6 need no reflection): rows [y0, y1)
 // in groups of 7.  Row slot u of a group is consumed and immediately

@@ -3,14 +3,19 @@
 //   computeOrbDescriptor (:110-149) on the blurred level (blur.hip) and the
 //   final keypoint fields (:847-857, :1107-1115).
 //
-// One wave per keypoint slot: the 31x31 unblurred disc and the 37x37
-// blurred neighbourhood are staged in LDS with dword loads; moments by a
-// 64-lane reduction; 256 tests as 4 wave ballots (bit t of the descriptor =
-// test t = lane t%64 of ballot t/64).  sin/cos of the angle use
+// One wave per keypoint slot.  The keypoint's raw 43x43 neighbourhood is
+// staged in LDS once (dword loads); the GaussianBlur of the level
+// (ORBextractor.cpp:1097-1098) is computed for the 37x37 patch rBRIEF reads,
+// right there, with the blur's own arithmetic (blur_device.h) -- the whole
+// blurred levels are never written to or read from HBM.  IC_Angle's disc
+// comes from the same staged patch; moments by a 64-lane reduction; 256 tests
+// as 4 wave ballots (bit t of the descriptor = test t = lane t%64 of ballot
+// t/64).  sin/cos of the angle use
 // the glibc-2.35 sinf/cosf restatement (fp64 polynomial), pinned bit-exact
 // against libm over every float in [0, 6.3].
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
+#include "blur_device.h"
 #include "../../include/orbgpu.h"
 
 #include <algorithm>
@@ -101,7 +106,11 @@ __device__ inline int wave_sum(int v) {
     return v;
 }
 
-constexpr int kBPitch = 40;      // 37-px blurred rows, staged from a 4-aligned column
+constexpr int kBPitch = 40;      // 37-px blurred rows, from a 4-aligned column
+constexpr int kRPitch = 48;      // raw patch rows: columns xb-4 .. xb+43 (12 dwords)
+constexpr int kRawWords = kPatch * (kRPitch / 4);   // 43 rows x 12 dwords
+constexpr int kQuads = kBPitch / 4;                 // 10 output quads per blurred row
+constexpr int kRowTasks = kPatch * kQuads, kColTasks = kBlur * kQuads;
 
 // The 4 waves of a block process different keypoints: stages are ordered
 // with a wave-local LDS fence, never a block barrier.
@@ -111,12 +120,21 @@ __device__ inline void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-__device__ void describe_one(const Geom& g, int f, int slot, int lane, uint8_t* s_blur,
+__device__ inline int reflect101(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
+
+// Per-wave LDS: the raw 43x48 neighbourhood, its row-pass sums (4 floats per
+// quad), and the blurred 37x40 patch.
+struct DescLds {
+    uint8_t raw[kPatch * kRPitch];
+    float4 rows[kPatch * kQuads];
+    uint8_t blur[kBlur * kBPitch];
+};
+
+__device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& S,
                              const uint8_t* __restrict__ img0, size_t row0, size_t frame0,
-                             const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ blur,
-                             const uint32_t* __restrict__ oct_out, const int* __restrict__ oct_count,
-                             orbgpu_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
-                             int* __restrict__ counts, int kp_cap) {
+                             const uint8_t* __restrict__ pyr, const uint32_t* __restrict__ oct_out,
+                             const int* __restrict__ oct_count, orbgpu_keypoint* __restrict__ kps,
+                             uint8_t* __restrict__ desc, int* __restrict__ counts, int kp_cap) {
     int l = 0;
     while (l + 1 < g.nlevels && slot >= g.lv[l + 1].out_offset) ++l;
     const LevelGeom& L = g.lv[l];
@@ -134,63 +152,94 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, uint8_t* 
     const int cx = key_x(key) + kBorder, cy = key_y(key) + kBorder;
     const uint8_t* raw = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
     const size_t rp = l == 0 ? row0 : (size_t)L.pitch;
-    const uint8_t* bl = blur + L.blur_offset + (size_t)f * L.blur_frame_bytes;
 
-    // Every lane issues all of its window loads (disc words and blurred
-    // patch) before any is consumed: one memory round trip per keypoint.
-    // Unblurred 31x31 disc (IC_Angle): 31 rows x 9 aligned dwords from
-    // column xd = (cx - 15) & ~3.  The keypoint is >= 19 px from every border
-    // (cx <= w - 20, cy <= h - 20), so the words end at most 1 byte past the
-    // row, inside the next row of the same frame; those bytes are outside the
-    // disc and masked off below.
+    // 1. Stage the raw neighbourhood: rows cy-21 .. cy+21, columns xb-4 ..
+    // xb+43 (xb = the blurred patch's 4-aligned first column), reflected at
+    // the level border (BORDER_REFLECT_101 of GaussianBlur on the level
+    // clone, ORBextractor.cpp:1097-1098).  Dwords inside the level are one
+    // load each; a dword that crosses the border is assembled from reflected
+    // bytes.  All loads of a lane are issued before any is stored.
+    const int xb = (cx - kBlurR) & ~3, ob = cx - kBlurR - xb, x0 = xb - 4;
+    constexpr int kLoads = (kRawWords + 63) / 64;
+    uint32_t v[kLoads];
+#pragma unroll
+    for (int k = 0; k < kLoads; ++k) {
+        const int idx = min(lane + 64 * k, kRawWords - 1), r = idx / 12, q = idx - r * 12;
+        const uint8_t* row = raw + (size_t)reflect101(cy - kPatchR + r, L.h) * rp;
+        const int col = x0 + 4 * q;
+        if (col >= 0 && col + 3 < L.w) {
+            v[k] = *reinterpret_cast<const uint32_t*>(row + col);
+        } else {
+            uint32_t w = 0;
+            for (int j = 0; j < 4; ++j) w |= (uint32_t)row[reflect101(col + j, L.w)] << (8 * j);
+            v[k] = w;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kLoads; ++k) {
+        const int idx = lane + 64 * k;
+        if (idx < kRawWords) reinterpret_cast<uint32_t*>(S.raw)[idx] = v[k];
+    }
+    wave_sync();
+
+    // 2. Blur (blur_device.h, the arithmetic of blur.hip): row pass of the 43
+    // rows for the 10 output quads, then the column pass of the 37 blurred
+    // rows, rounded per path (quad columns x < 4*floor(w/4): SIMD path).
+    for (int t = lane; t < kRowTasks; t += 64) {
+        const int r = t / kQuads, q = t - r * kQuads;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(S.raw + r * kRPitch) + q;
+        blurdev::Raw3 R3;
+        R3.a = w[0];
+        R3.b = w[1];
+        R3.c = w[2];
+        blurdev::f32x2 lo, hi;
+        blurdev::row_pass_raw(R3, lo, hi);
+        S.rows[t] = make_float4(lo.x, lo.y, hi.x, hi.y);
+    }
+    wave_sync();
+    const int simd_end = L.w & ~3;
+    for (int t = lane; t < kColTasks; t += 64) {
+        const int r = t / kQuads, q = t - r * kQuads;
+        blurdev::f32x2 wl[7], wh[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const float4 x = S.rows[(r + k) * kQuads + q];
+            wl[k] = blurdev::f32x2{x.x, x.y};
+            wh[k] = blurdev::f32x2{x.z, x.w};
+        }
+        const blurdev::f32x2 lo = blurdev::col_pass(wl[0], wl[1], wl[2], wl[3], wl[4], wl[5], wl[6]);
+        const blurdev::f32x2 hi = blurdev::col_pass(wh[0], wh[1], wh[2], wh[3], wh[4], wh[5], wh[6]);
+        reinterpret_cast<uint32_t*>(S.blur + r * kBPitch)[q] = blurdev::pack4(lo, hi, xb + 4 * q < simd_end);
+    }
+
+    // 3. Intensity centroid (IC_Angle, ORBextractor.cpp:79-106) from the raw
+    // patch: disc row v = r - 15 covers window columns c = 4q..4q+3 of the
+    // 4-aligned window at xd = (cx - 15) & ~3, i.e. u = c - od - 15; bytes
+    // with |u| <= umax[|v|] are kept and v_dot4_u32_u8 gives sum(p) and
+    // sum(c * p) of the word.  Integer moments: order-free, exact.
     const int xd = (cx - 15) & ~3, od = cx - 15 - xd;
-    const int xb = (cx - kBlurR) & ~3, ob = cx - kBlurR - xb;
-    const uint8_t* dsrc = raw + (size_t)(cy - 15) * rp + xd;
-    const uint8_t* bsrc = bl + (size_t)(cy - kBlurR) * L.pitch + xb;
-    constexpr int kDiscWords = 31 * 9, kBlurWords = kBlur * 10;
-    constexpr int kDiscLoads = (kDiscWords + 63) / 64, kBlurLoads = (kBlurWords + 63) / 64;
-    uint32_t vd[kDiscLoads], vb[kBlurLoads];
-#pragma unroll
-    for (int k = 0; k < kDiscLoads; ++k) {
-        const int idx = min(lane + 64 * k, kDiscWords - 1), r = idx / 9, q = idx - r * 9;
-        vd[k] = *reinterpret_cast<const uint32_t*>(dsrc + (size_t)r * rp + 4 * q);
-    }
-#pragma unroll
-    for (int k = 0; k < kBlurLoads; ++k) {
-        const int idx = min(lane + 64 * k, kBlurWords - 1), r = idx / 10, q = idx - r * 10;
-        vb[k] = *reinterpret_cast<const uint32_t*>(bsrc + (size_t)r * L.pitch + 4 * q);
-    }
-#pragma unroll
-    for (int k = 0; k < kBlurLoads; ++k) {
-        const int idx = lane + 64 * k, r = idx / 10, q = idx - r * 10;
-        if (idx < kBlurWords) *reinterpret_cast<uint32_t*>(s_blur + r * kBPitch + 4 * q) = vb[k];
-    }
-
-    // Intensity centroid (IC_Angle, ORBextractor.cpp:79-106) straight from
-    // the disc words: a word of row v = r - 15 covers window columns c =
-    // 4q..4q+3, i.e. u = c - od - 15; the bytes with |u| <= umax[|v|] are
-    // kept, and v_dot4_u32_u8 gives sum(p) and sum(c * p) of the word.
-    // Integer moments: order-free, so lane partial sums are exact.
+    const uint8_t* disc = S.raw + (kPatchR - 15) * kRPitch + (xd - x0);
+    constexpr int kDiscWords = 31 * 9, kDiscLoads = (kDiscWords + 63) / 64;
     int m10 = 0, m01 = 0;
 #pragma unroll
     for (int k = 0; k < kDiscLoads; ++k) {
-        const int idx = lane + 64 * k, r = idx / 9, q = idx - r * 9;
-        const int v = r - 15, d = c_umax[abs(v) & 15];
+        const int idx = lane + 64 * k, r = min(idx, kDiscWords - 1) / 9, q = min(idx, kDiscWords - 1) - r * 9;
+        const int vv = r - 15, d = c_umax[abs(vv) & 15];
         const int s0 = min(max(od + 15 - d - 4 * q, 0), 4), e0 = min(max(od + 16 + d - 4 * q, 0), 4);
         const uint32_t mask = e0 > s0 ? (uint32_t)(((1ull << (8 * (e0 - s0))) - 1ull) << (8 * s0)) : 0u;
-        const uint32_t w = idx < kDiscWords ? vd[k] & mask : 0u;
+        const uint32_t w = idx < kDiscWords ? *reinterpret_cast<const uint32_t*>(disc + r * kRPitch + 4 * q) & mask : 0u;
         const uint32_t cols = (uint32_t)(4 * q) * 0x01010101u + 0x03020100u;
         const int sp = (int)__builtin_amdgcn_udot4(w, 0x01010101u, 0u, false);
         const int cp = (int)__builtin_amdgcn_udot4(w, cols, 0u, false);
         m10 += cp - (od + 15) * sp;
-        m01 += v * sp;
+        m01 += vv * sp;
     }
-    wave_sync();
     m10 = wave_sum(m10);
     m01 = wave_sum(m01);
     const float angle = fast_atan2((float)m01, (float)m10);
+    wave_sync();  // blurred patch complete
 
-    // rBRIEF (computeOrbDescriptor, ORBextractor.cpp:110-149)
+    // 4. rBRIEF (computeOrbDescriptor, ORBextractor.cpp:110-149)
     const float ang = __fmul_rn(angle, (float)(M_PI / 180.f));
     float sa, ca;
     glibc_sincosf(ang, &sa, &ca);
@@ -205,7 +254,7 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, uint8_t* 
             const float px = (float)c_pattern[4 * t + 2 * pp], py = (float)c_pattern[4 * t + 2 * pp + 1];
             const int ry = __float2int_rn(__fadd_rn(__fmul_rn(px, b), __fmul_rn(py, a)));
             const int rx = __float2int_rn(__fsub_rn(__fmul_rn(px, a), __fmul_rn(py, b)));
-            val[pp] = s_blur[(kBlurR + ry) * kBPitch + ob + kBlurR + rx];
+            val[pp] = S.blur[(kBlurR + ry) * kBPitch + ob + kBlurR + rx];
         }
         words[rnd] = __ballot(val[0] < val[1]);
     }
@@ -228,37 +277,38 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, uint8_t* 
 
 constexpr int kDescWaves = 4;
 
-// One wave per (frame, slot) item, four items per block (fewer, larger
-// workgroups than one wave per block: the 1-wave form was dispatch-bound).
+// One wave per (frame, slot) item, four items per block.  Blocks are
+// XCD-swizzled so one frame's keypoints (whose neighbourhoods overlap) are
+// described on one XCD and its level rows are fetched into one L2.
 __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int items,
                                                                    const uint8_t* __restrict__ img0, size_t row0,
                                                                    size_t frame0, const uint8_t* __restrict__ pyr,
-                                                                   const uint8_t* __restrict__ blur,
                                                                    const uint32_t* __restrict__ oct_out,
                                                                    const int* __restrict__ oct_count,
                                                                    orbgpu_keypoint* __restrict__ kps,
                                                                    uint8_t* __restrict__ desc,
                                                                    int* __restrict__ counts, int kp_cap) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_blur[kDescWaves][kBlur * kBPitch];
+    __shared__ DescLds s_lds[kDescWaves];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: metadata in SGPRs
-    const int item = blockIdx.x * kDescWaves + wave;
+    const int blk = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
+    const int item = blk * kDescWaves + wave;
     if (item >= items) return;
     const int f = item / g.slots_frame, slot = item - f * g.slots_frame;
-    describe_one(g, f, slot, lane, s_blur[wave], img0, row0, frame0, pyr, blur, oct_out, oct_count,
-                 kps, desc, counts, kp_cap);
+    describe_one(g, f, slot, lane, s_lds[wave], img0, row0, frame0, pyr, oct_out, oct_count, kps, desc, counts,
+                 kp_cap);
 }
 
 }  // namespace
 
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
-                           const uint8_t* pyr, const uint8_t* blur, const uint32_t* oct_out, const int* oct_count,
+                           const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
                            hipStream_t stream) {
     const int items = g.slots_frame * batch;
     const int blocks = (items + kDescWaves - 1) / kDescWaves;
     hipLaunchKernelGGL(describe_kernel, dim3(blocks), dim3(64 * kDescWaves), 0, stream, g, items, img0, row0, frame0,
-                       pyr, blur, oct_out, oct_count, kps, desc, counts, kp_cap);
+                       pyr, oct_out, oct_count, kps, desc, counts, kp_cap);
     return hipGetLastError();
 }
 

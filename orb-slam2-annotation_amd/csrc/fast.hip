@@ -240,8 +240,9 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     T.lb = T.la + g.det_max;
     uint8_t* s_win = ws;
 
-    // one cell per wave; waves of a block take consecutive cells of a frame
-    const int item = blockIdx.x * kCellWaves + wave;
+    // one cell per wave; waves of a block take consecutive cells of a frame;
+    // XCD-swizzled blocks keep a frame's cells (overlapping windows) on one L2
+    const int item = xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * kCellWaves + wave;
     if (item >= ncells_total) return;
     const int f = item / g.total_cells;
     const int gc = item - f * g.total_cells;

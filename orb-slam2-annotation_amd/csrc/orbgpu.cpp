@@ -596,9 +596,10 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
     ORB_HIP(launch_octree(g, batch, e->d_cand, e->d_cell_counts, e->d_gkeys, e->d_gknode, e->d_oct_out,
                           e->d_oct_count, e->d_err, e->kcap, e->ncap, e->d_trace, s));
     if (evs) ORB_HIP(hipEventRecord(evs[3], s));
-    ORB_HIP(launch_blur_levels(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_blur, s));
-    ORB_HIP(launch_describe(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_blur, e->d_oct_out, e->d_oct_count,
-                            kps, desc, counts, kp_cap, s));
+    // GaussianBlur is fused into describe (blur of each keypoint's patch);
+    // whole blurred levels exist only for the debug API
+    ORB_HIP(launch_describe(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_oct_out, e->d_oct_count, kps, desc,
+                            counts, kp_cap, s));
     if (evs) ORB_HIP(hipEventRecord(evs[4], s));
     e->last_img = imgs;
     e->last_row = row_step;
@@ -671,7 +672,7 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
     const Geom& g = e->g;
     const size_t B = (size_t)max_batch;
     e->img_pitch = round_up((size_t)width, 16);
-    if ((rc = dalloc(&e->d_pyr, e->pyr_bytes)) || (rc = dalloc(&e->d_blur, e->blur_bytes)) || (rc = dalloc(&e->d_ptab, ptab.size())) ||
+    if ((rc = dalloc(&e->d_pyr, e->pyr_bytes)) || (rc = dalloc(&e->d_ptab, ptab.size())) ||
         (rc = dalloc(&e->d_cand, g.cand_frame * B)) ||
         (rc = dalloc(&e->d_cell_counts, (size_t)g.total_cells * B)) || (rc = dalloc(&e->d_gkeys, g.cand_frame * B)) ||
         (rc = dalloc(&e->d_gknode, g.cand_frame * B)) || (rc = dalloc(&e->d_oct_out, (size_t)g.slots_frame * B)) ||
@@ -841,6 +842,15 @@ int orbgpu_debug_level_blur(orbgpu_extractor* e, int frame, int level, uint8_t* 
         return fail(ORBGPU_ERR_ARG, "no such frame/level in the last extraction");
     const LevelGeom& v = e->g.lv[level];
     if (dst_step < (size_t)v.w) return fail(ORBGPU_ERR_ARG, "dst_step < level width");
+    ORB_HIP(hipStreamSynchronize(e->stream));
+    // the product path never materialises blurred levels: blur the last
+    // batch's levels on demand (same arithmetic as describe's fused blur)
+    if (!e->d_blur) {
+        int rc = dalloc(&e->d_blur, e->blur_bytes);
+        if (rc) return rc;
+    }
+    ORB_HIP(launch_blur_levels(e->g, e->last_batch, e->last_img, e->last_row, e->last_frame, e->d_pyr, e->d_blur,
+                               e->stream));
     ORB_HIP(hipStreamSynchronize(e->stream));
     ORB_HIP(hipMemcpy2D(dst, dst_step, e->d_blur + v.blur_offset + (size_t)frame * v.blur_frame_bytes, v.pitch, v.w,
                         v.h, hipMemcpyDeviceToHost));

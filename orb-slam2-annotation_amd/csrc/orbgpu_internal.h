@@ -23,6 +23,17 @@ constexpr int kPatch = 2 * kPatchR + 1;  // 43
 constexpr int kBlurR = 18;             // blurred patch radius (13*sqrt2 rounded)
 constexpr int kBlur = 2 * kBlurR + 1;    // 37
 
+// XCD-aware block order: the dispatcher deals blocks round-robin over the 8
+// XCDs (each with its own L2), so blocks b and b+8 share an L2.  Kernels whose
+// consecutive blocks read the same frame's pixels use the remapped index, so
+// one frame's blocks land on one XCD and its level rows are fetched into one
+// L2, not eight.  Bijective for any nwg (MI355X_MICROARCH / cdna guide T1);
+// a pure speed choice, never needed for correctness.
+__device__ inline int xcd_swizzle(int orig, int nwg) {
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
 // Candidate key packing (FAST output, octree input/output):
 //   bits 0..10  x relative to minBorderX (level x - 16)
 //   bits 11..21 y relative to minBorderY

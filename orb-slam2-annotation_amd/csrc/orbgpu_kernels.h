@@ -32,7 +32,7 @@ hipError_t launch_octree(const Geom& g, int batch, const uint32_t* cand, const i
                          int* err, int kcap, int ncap, int* trace, hipStream_t stream);
 
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
-                           const uint8_t* pyr, const uint8_t* blur, const uint32_t* oct_out, const int* oct_count,
+                           const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
                            hipStream_t stream);
 
