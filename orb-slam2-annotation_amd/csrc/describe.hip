@@ -110,7 +110,7 @@ constexpr int kBPitch = 40;      // 37-px blurred rows, from a 4-aligned column
 constexpr int kRPitch = 48;      // raw patch rows: columns xb-4 .. xb+43 (12 dwords)
 constexpr int kRawWords = kPatch * (kRPitch / 4);   // 43 rows x 12 dwords
 constexpr int kQuads = kBPitch / 4;                 // 10 output quads per blurred row
-constexpr int kRowTasks = kPatch * kQuads, kColTasks = kBlur * kQuads;
+constexpr int kColChunks = (kBlur + 6) / 7;         // 6 chunks of <= 7 blurred rows
 
 // The 4 waves of a block process different keypoints: stages are ordered
 // with a wave-local LDS fence, never a block barrier.
@@ -122,11 +122,9 @@ __device__ inline void wave_sync() {
 
 __device__ inline int reflect101(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
 
-// Per-wave LDS: the raw 43x48 neighbourhood, its row-pass sums (4 floats per
-// quad), and the blurred 37x40 patch.
+// Per-wave LDS: the raw 43x48 neighbourhood and the blurred 37x40 patch.
 struct DescLds {
     uint8_t raw[kPatch * kRPitch];
-    float4 rows[kPatch * kQuads];
     uint8_t blur[kBlur * kBPitch];
 };
 
@@ -182,37 +180,7 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
     }
     wave_sync();
 
-    // 2. Blur (blur_device.h, the arithmetic of blur.hip): row pass of the 43
-    // rows for the 10 output quads, then the column pass of the 37 blurred
-    // rows, rounded per path (quad columns x < 4*floor(w/4): SIMD path).
-    for (int t = lane; t < kRowTasks; t += 64) {
-        const int r = t / kQuads, q = t - r * kQuads;
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(S.raw + r * kRPitch) + q;
-        blurdev::Raw3 R3;
-        R3.a = w[0];
-        R3.b = w[1];
-        R3.c = w[2];
-        blurdev::f32x2 lo, hi;
-        blurdev::row_pass_raw(R3, lo, hi);
-        S.rows[t] = make_float4(lo.x, lo.y, hi.x, hi.y);
-    }
-    wave_sync();
-    const int simd_end = L.w & ~3;
-    for (int t = lane; t < kColTasks; t += 64) {
-        const int r = t / kQuads, q = t - r * kQuads;
-        blurdev::f32x2 wl[7], wh[7];
-#pragma unroll
-        for (int k = 0; k < 7; ++k) {
-            const float4 x = S.rows[(r + k) * kQuads + q];
-            wl[k] = blurdev::f32x2{x.x, x.y};
-            wh[k] = blurdev::f32x2{x.z, x.w};
-        }
-        const blurdev::f32x2 lo = blurdev::col_pass(wl[0], wl[1], wl[2], wl[3], wl[4], wl[5], wl[6]);
-        const blurdev::f32x2 hi = blurdev::col_pass(wh[0], wh[1], wh[2], wh[3], wh[4], wh[5], wh[6]);
-        reinterpret_cast<uint32_t*>(S.blur + r * kBPitch)[q] = blurdev::pack4(lo, hi, xb + 4 * q < simd_end);
-    }
-
-    // 3. Intensity centroid (IC_Angle, ORBextractor.cpp:79-106) from the raw
+    // 2. Intensity centroid (IC_Angle, ORBextractor.cpp:79-106) from the raw
     // patch: disc row v = r - 15 covers window columns c = 4q..4q+3 of the
     // 4-aligned window at xd = (cx - 15) & ~3, i.e. u = c - od - 15; bytes
     // with |u| <= umax[|v|] are kept and v_dot4_u32_u8 gives sum(p) and
@@ -233,6 +201,37 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
         const int cp = (int)__builtin_amdgcn_udot4(w, cols, 0u, false);
         m10 += cp - (od + 15) * sp;
         m01 += vv * sp;
+    }
+
+    // 3. Blur (blur_device.h, the arithmetic of blur.hip) of the 37x37 patch:
+    // lane = (output quad q, chunk c of 7 blurred rows); it runs the row pass
+    // of the chunk's 13 raw rows from LDS, slides them through registers for
+    // the column pass and rounds per path (quad columns x < 4*floor(w/4): the
+    // SIMD path).  No intermediate array, no extra wave sync.
+    const int simd_end = L.w & ~3;
+    if (lane < kQuads * kColChunks) {
+        const int q = lane % kQuads, c = lane / kQuads, r0 = c * 7;
+        blurdev::f32x2 wl[13], wh[13];
+#pragma unroll
+        for (int k = 0; k < 13; ++k) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(S.raw + min(r0 + k, kPatch - 1) * kRPitch) + q;
+            blurdev::Raw3 R3;
+            R3.a = w[0];
+            R3.b = w[1];
+            R3.c = w[2];
+            blurdev::row_pass_raw(R3, wl[k], wh[k]);
+        }
+        const bool simd = xb + 4 * q < simd_end;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+            if (r0 + j < kBlur) {
+                const blurdev::f32x2 lo = blurdev::col_pass(wl[j], wl[j + 1], wl[j + 2], wl[j + 3], wl[j + 4], wl[j + 5],
+                                                            wl[j + 6]);
+                const blurdev::f32x2 hi = blurdev::col_pass(wh[j], wh[j + 1], wh[j + 2], wh[j + 3], wh[j + 4], wh[j + 5],
+                                                            wh[j + 6]);
+                reinterpret_cast<uint32_t*>(S.blur + (r0 + j) * kBPitch)[q] = blurdev::pack4(lo, hi, simd);
+            }
+        }
     }
     m10 = wave_sum(m10);
     m01 = wave_sum(m01);
@@ -291,7 +290,11 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
     __shared__ DescLds s_lds[kDescWaves];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: metadata in SGPRs
+#if ORBGPU_DESC_SWIZZLE
     const int blk = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
+#else
+    const int blk = (int)blockIdx.x;
+#endif
     const int item = blk * kDescWaves + wave;
     if (item >= items) return;
     const int f = item / g.slots_frame, slot = item - f * g.slots_frame;

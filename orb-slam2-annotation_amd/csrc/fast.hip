@@ -242,7 +242,11 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
 
     // one cell per wave; waves of a block take consecutive cells of a frame;
     // XCD-swizzled blocks keep a frame's cells (overlapping windows) on one L2
+#if ORBGPU_FAST_SWIZZLE
     const int item = xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * kCellWaves + wave;
+#else
+    const int item = (int)blockIdx.x * kCellWaves + wave;
+#endif
     if (item >= ncells_total) return;
     const int f = item / g.total_cells;
     const int gc = item - f * g.total_cells;

@@ -29,6 +29,12 @@ constexpr int kBlur = 2 * kBlurR + 1;    // 37
 // one frame's blocks land on one XCD and its level rows are fetched into one
 // L2, not eight.  Bijective for any nwg (MI355X_MICROARCH / cdna guide T1);
 // a pure speed choice, never needed for correctness.
+#ifndef ORBGPU_FAST_SWIZZLE
+#define ORBGPU_FAST_SWIZZLE 0  // measured slower for FAST (1.193 vs 1.129 ms per 512 frames)
+#endif
+#ifndef ORBGPU_DESC_SWIZZLE
+#define ORBGPU_DESC_SWIZZLE 1
+#endif
 __device__ inline int xcd_swizzle(int orig, int nwg) {
     const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
