@@ -50,6 +50,37 @@ int orbgpu_init_check_both_batch_device(const orbgpu_match_pts* d_pts, int n, co
                                         int nh, const float* d_f21, int nf, float sigma, float* d_scores_h,
                                         uint8_t* d_inliers_h, float* d_scores_f, uint8_t* d_inliers_f, void* stream);
 
+/* ---------------------------------------------------------------------- */
+/* Model hypotheses (Initialize / FindHomography / FindFundamental)        */
+/* ---------------------------------------------------------------------- */
+/* DUtils::Random::SeedRandOnce(seed) on the orbgpu_rand stream
+ * (Thirdparty/DBoW2/DUtils/Random.cpp:38-45): seeds only on the first call
+ * in the process, as Initialize's SeedRandOnce(0) (Initializer.cpp:102). */
+void orbgpu_seed_rand_once(unsigned int seed);
+
+/* Initialize's minimal sets (Initializer.cpp:96-115): for it < n_iter,
+ * vAvailableIndices = 0..n_matches-1 and 8 x (RandomInt(0, size-1), swap
+ * with back, pop) from the orbgpu_rand stream; sets[8*it + j] = mvSets[it][j]. */
+int orbgpu_init_draw_sets(int n_matches, int n_iter, int* sets);
+
+/* Workspace of orbgpu_init_hypotheses_batch_device (normalised points, T1, T2). */
+size_t orbgpu_init_workspace_bytes(int n1, int n2);
+
+/* Normalize (Initializer.cpp:965-1015) of mvKeys1 (d_kp1: n1 x (x, y)) and
+ * mvKeys2 (d_kp2), then for every iteration it < n_iter the hypotheses of
+ * FindHomography (:160-212: H21 = T2.inv()*ComputeH21(8 pairs)*T1, H12 =
+ * H21.inv()) and FindFundamental (:217-269: F21 = T2.t()*ComputeF21*T1) from
+ * the 8 matches d_sets[8 it ..] (indices into d_pairs: n_matches x (first,
+ * second) = mvMatches12).  d_h21 / d_h12 / d_f21: n_iter x 9 row-major.
+ * d_pts (nullable, 16-byte aligned): the n_matches orbgpu_match_pts the
+ * scorers above read.  The 8-point SVDs are one-sided Jacobi in double --
+ * the reference's cv::SVDecomp is not reproducible bit for bit -- so the
+ * matrices equal the reference's to a tolerance (tests/test_init.py). */
+int orbgpu_init_hypotheses_batch_device(const float* d_kp1, int n1, const float* d_kp2, int n2, const int* d_pairs,
+                                        int n_matches, const int* d_sets, int n_iter, void* d_work,
+                                        orbgpu_match_pts* d_pts, float* d_h21, float* d_h12, float* d_f21,
+                                        void* stream);
+
 /* FindHomography / FindFundamental's selection (Initializer.cpp:207-212,
  * :264-269): *best = the first h with scores[h] greater than every earlier
  * score and than 0; -1 when no score exceeds 0 (the reference keeps score 0

@@ -109,3 +109,116 @@ def select_best(scores) -> int:
         if F(s) > best:
             best, idx = F(s), h
     return idx
+
+
+# ---- model hypotheses (Normalize, ComputeH21/F21, FindHomography/Fundamental)
+# The 8-point SVDs are restated with numpy's LAPACK SVD in double (cv::SVDecomp
+# of the float DLT matrix is not reproducible here): H/F are compared with the
+# GPU to a tolerance, the kept iteration exactly.
+
+def normalize(pts: np.ndarray):
+    """Normalize (Initializer.cpp:965-1015): sequential float sums; returns
+    (normalised (n, 2) float32, T (3, 3) float32)."""
+    pts = np.asarray(pts, F).reshape(-1, 2)
+    n = len(pts)
+    out = np.zeros_like(pts)
+    T = np.eye(3, dtype=F)
+    for ax in range(2):
+        mean = F(0.0)
+        for v in pts[:, ax].tolist():
+            mean = F(mean + F(v))
+        mean = F(mean / F(n))
+        dev = F(0.0)
+        for v in pts[:, ax].tolist():
+            dev = F(dev + F(abs(F(F(v) - mean))))
+        dev = F(dev / F(n))
+        s = F(1.0 / np.float64(dev))
+        out[:, ax] = ((pts[:, ax] - mean) * s).astype(F)
+        T[ax, ax] = s
+        T[ax, 2] = F(-mean * s)
+    return out, T
+
+
+def mul3(a, b):
+    """float 3x3 product with double accumulation (OpenCV's small float gemm)"""
+    a64, b64 = np.asarray(a, F).astype(np.float64), np.asarray(b, F).astype(np.float64)
+    c = np.zeros((3, 3), np.float64)
+    for i in range(3):
+        for j in range(3):
+            c[i, j] = (a64[i, 0] * b64[0, j] + a64[i, 1] * b64[1, j]) + a64[i, 2] * b64[2, j]
+    return c.astype(F)
+
+
+def inv3(m):
+    """cv::Mat::inv() of a 3x3 CV_32F (closed form, double, rounded to float)"""
+    S = np.asarray(m, F).astype(np.float64)
+    d0 = (S[0, 0] * (S[1, 1] * S[2, 2] - S[1, 2] * S[2, 1]) - S[0, 1] * (S[1, 0] * S[2, 2] - S[1, 2] * S[2, 0]) +
+          S[0, 2] * (S[1, 0] * S[2, 1] - S[1, 1] * S[2, 0]))
+    if d0 == 0.0:
+        return np.zeros((3, 3), F)
+    d = 1.0 / d0
+    t = [(S[1, 1] * S[2, 2] - S[1, 2] * S[2, 1]) * d, (S[0, 2] * S[2, 1] - S[0, 1] * S[2, 2]) * d,
+         (S[0, 1] * S[1, 2] - S[0, 2] * S[1, 1]) * d, (S[1, 2] * S[2, 0] - S[1, 0] * S[2, 2]) * d,
+         (S[0, 0] * S[2, 2] - S[0, 2] * S[2, 0]) * d, (S[0, 2] * S[1, 0] - S[0, 0] * S[1, 2]) * d,
+         (S[1, 0] * S[2, 1] - S[1, 1] * S[2, 0]) * d, (S[0, 1] * S[2, 0] - S[0, 0] * S[2, 1]) * d,
+         (S[0, 0] * S[1, 1] - S[0, 1] * S[1, 0]) * d]
+    return np.array(t, np.float64).astype(F).reshape(3, 3)
+
+
+def _null_vector(A):
+    _, _, vt = np.linalg.svd(A.astype(np.float64))
+    return vt[-1].astype(F)
+
+
+def compute_h21(p1, p2):
+    """ComputeH21 (:292-330): the float DLT matrix, vt.row(8)"""
+    u1, v1, u2, v2 = p1[:, 0], p1[:, 1], p2[:, 0], p2[:, 1]
+    A = np.zeros((2 * len(p1), 9), F)
+    A[0::2, 3], A[0::2, 4], A[0::2, 5] = -u1, -v1, -1
+    A[0::2, 6], A[0::2, 7], A[0::2, 8] = v2 * u1, v2 * v1, v2
+    A[1::2, 0], A[1::2, 1], A[1::2, 2] = u1, v1, 1
+    A[1::2, 6], A[1::2, 7], A[1::2, 8] = -u2 * u1, -u2 * v1, -u2
+    return _null_vector(A).reshape(3, 3)
+
+
+def compute_f21(p1, p2):
+    """ComputeF21 (:332-388): vt.row(8) of the float DLT matrix, then the
+    rank-2 projection (w(2) = 0)"""
+    u1, v1, u2, v2 = p1[:, 0], p1[:, 1], p2[:, 0], p2[:, 1]
+    A = np.stack([u2 * u1, u2 * v1, u2, v2 * u1, v2 * v1, v2, u1, v1, np.ones_like(u1)], 1).astype(F)
+    if A.shape[0] < 9:
+        A = np.vstack([A, np.zeros((9 - A.shape[0], 9), F)])
+    Fpre = _null_vector(A).reshape(3, 3)
+    u, w, vt = np.linalg.svd(Fpre.astype(np.float64))
+    w[2] = 0.0
+    return (u @ np.diag(w) @ vt).astype(F)
+
+
+def find_models(kp1, kp2, pairs, sets, sigma=1.0):
+    """Normalize + FindHomography + FindFundamental (:160-269) over the given
+    minimal sets.  Returns dict with H21/H12/F21 per iteration, scores,
+    kept iterations (best_h, best_f) and the score ratio RH (:140)."""
+    pn1, T1 = normalize(kp1)
+    pn2, T2 = normalize(kp2)
+    pairs = np.asarray(pairs).reshape(-1, 2)
+    pts = np.concatenate([np.asarray(kp1, F)[pairs[:, 0]], np.asarray(kp2, F)[pairs[:, 1]]], 1)
+    T2inv, T2t = inv3(T2), T2.T.copy()
+    n_it = len(sets)
+    H21 = np.zeros((n_it, 3, 3), F)
+    H12 = np.zeros((n_it, 3, 3), F)
+    F21 = np.zeros((n_it, 3, 3), F)
+    sh = np.zeros(n_it, F)
+    sf = np.zeros(n_it, F)
+    for it, s in enumerate(sets):
+        a, b = pn1[pairs[s, 0]], pn2[pairs[s, 1]]
+        H21[it] = mul3(mul3(T2inv, compute_h21(a, b)), T1)
+        H12[it] = inv3(H21[it])
+        F21[it] = mul3(mul3(T2t, compute_f21(a, b)), T1)
+        sh[it] = check_homography(pts, H21[it], H12[it], sigma)[0]
+        sf[it] = check_fundamental(pts, F21[it], sigma)[0]
+    bh, bf = select_best(sh), select_best(sf)
+    SH = sh[bh] if bh >= 0 else F(0)
+    SF = sf[bf] if bf >= 0 else F(0)
+    return {"pts": pts, "H21": H21, "H12": H12, "F21": F21, "scores_h": sh, "scores_f": sf, "best_h": bh,
+            "best_f": bf, "RH": F(SH / F(SH + SF)) if SH + SF > 0 else F(0), "T1": T1, "T2": T2, "pn1": pn1,
+            "pn2": pn2}

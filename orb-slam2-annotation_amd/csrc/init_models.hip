@@ -1,0 +1,235 @@
+// init_models.hip -- the model hypotheses of the monocular Initializer
+// (src/Initializer.cpp:55-388) for all RANSAC iterations in two launches
+// (include/orbgpu_init.h, orbgpu_init_hypotheses_batch_device):
+//
+//   init_normalize_kernel  Normalize (:965-1015) of both frames' keypoints:
+//                          one lane per (frame, axis) runs the reference's
+//                          sequential float sums (mean, then mean absolute
+//                          deviation), the block writes the normalised points;
+//                          also the match list (u1, v1, u2, v2) the scorers read.
+//   init_models_kernel     one thread per (iteration, model): the 8 sampled
+//                          normalised pairs, the DLT matrix A in float as
+//                          ComputeH21 (:292-330, 16 x 9) / ComputeF21 (:332-388,
+//                          8 x 9) build it, its right singular vector of the
+//                          smallest singular value (cv::SVDecomp's vt.row(8)) by
+//                          one-sided Jacobi in double, for F the rank-2
+//                          projection (w(2) = 0), then the de-normalisation
+//                          T2inv*Hn*T1 / T2t*Fn*T1 and H12 = H21.inv() with
+//                          OpenCV's float 3x3 products (double accumulation)
+//                          and 3x3 closed-form inverse.
+// The SVDs are restated (OpenCV's Jacobi SVD in float is not reproducible
+// here), so H/F match the oracle to a tolerance; CheckHomography /
+// CheckFundamental (init.hip) then score them bit-exactly.
+#include <hip/hip_runtime.h>
+
+#include "../../include/orbgpu_init.h"
+#include "epnp.h"
+#include "host_common.h"
+
+namespace {
+
+constexpr int kNormThreads = 256;
+
+// Normalize (Initializer.cpp:965-1015).  work layout (floats):
+//   [0, 2 n1)            normalised mvKeys1
+//   [2 n1, 2 n1 + 2 n2)  normalised mvKeys2
+//   then T1 (9), T2 (9)
+__global__ __launch_bounds__(kNormThreads) void init_normalize_kernel(const float* __restrict__ kp1, int n1,
+                                                                      const float* __restrict__ kp2, int n2,
+                                                                      const int* __restrict__ pairs, int nm,
+                                                                      float* __restrict__ work,
+                                                                      float4* __restrict__ pts) {
+    __shared__ float s_mean[4], s_scale[4];
+    const int tid = threadIdx.x;
+    if (tid < 4) {  // lane = (frame, axis): the reference's sequential float sums
+        const int fr = tid >> 1, ax = tid & 1;
+        const float* k = fr ? kp2 : kp1;
+        const int n = fr ? n2 : n1;
+        float mean = 0.f;
+        for (int i = 0; i < n; ++i) mean = __fadd_rn(mean, k[2 * i + ax]);
+        mean = __fdiv_rn(mean, (float)n);
+        float dev = 0.f;
+        for (int i = 0; i < n; ++i) dev = __fadd_rn(dev, fabsf(__fsub_rn(k[2 * i + ax], mean)));
+        dev = __fdiv_rn(dev, (float)n);
+        s_mean[tid] = mean;
+        s_scale[tid] = (float)(1.0 / (double)dev);  // float sX = 1.0/meanDevX
+    }
+    __syncthreads();
+    for (int i = tid; i < n1 + n2; i += kNormThreads) {
+        const int fr = i >= n1, j = fr ? i - n1 : i;
+        const float* k = fr ? kp2 : kp1;
+        const float x = __fmul_rn(__fsub_rn(k[2 * j], s_mean[2 * fr]), s_scale[2 * fr]);
+        const float y = __fmul_rn(__fsub_rn(k[2 * j + 1], s_mean[2 * fr + 1]), s_scale[2 * fr + 1]);
+        work[2 * i] = x;
+        work[2 * i + 1] = y;
+    }
+    if (tid < 2) {  // T = [sX 0 -meanX*sX; 0 sY -meanY*sY; 0 0 1]
+        float* T = work + 2 * (n1 + n2) + 9 * tid;
+        const float sx = s_scale[2 * tid], sy = s_scale[2 * tid + 1];
+        T[0] = sx; T[1] = 0.f; T[2] = __fmul_rn(-s_mean[2 * tid], sx);
+        T[3] = 0.f; T[4] = sy; T[5] = __fmul_rn(-s_mean[2 * tid + 1], sy);
+        T[6] = 0.f; T[7] = 0.f; T[8] = 1.f;
+    }
+    if (pts)
+        for (int m = tid; m < nm; m += kNormThreads) {
+            const int a = pairs[2 * m], b = pairs[2 * m + 1];
+            pts[m] = make_float4(kp1[2 * a], kp1[2 * a + 1], kp2[2 * b], kp2[2 * b + 1]);
+        }
+}
+
+// float 3x3 product with double accumulation (OpenCV gemm on small float Mats)
+__device__ void mul3(const float* a, const float* b, float* c) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            c[3 * i + j] = (float)((double)a[3 * i] * b[j] + (double)a[3 * i + 1] * b[3 + j] +
+                                   (double)a[3 * i + 2] * b[6 + j]);
+}
+
+// cv::Mat::inv() of a 3x3 CV_32F (invert, DECOMP_LU, n == 3 closed form):
+// det in double, cofactors in double times 1/det, rounded to float
+__device__ void inv3(const float* m, float* o) {
+    auto S = [&](int r, int c) { return (double)m[3 * r + c]; };
+    const double d0 = S(0, 0) * (S(1, 1) * S(2, 2) - S(1, 2) * S(2, 1)) -
+                      S(0, 1) * (S(1, 0) * S(2, 2) - S(1, 2) * S(2, 0)) +
+                      S(0, 2) * (S(1, 0) * S(2, 1) - S(1, 1) * S(2, 0));
+    if (d0 == 0.0) {
+        for (int k = 0; k < 9; ++k) o[k] = 0.f;
+        return;
+    }
+    const double d = 1.0 / d0;
+    o[0] = (float)((S(1, 1) * S(2, 2) - S(1, 2) * S(2, 1)) * d);
+    o[1] = (float)((S(0, 2) * S(2, 1) - S(0, 1) * S(2, 2)) * d);
+    o[2] = (float)((S(0, 1) * S(1, 2) - S(0, 2) * S(1, 1)) * d);
+    o[3] = (float)((S(1, 2) * S(2, 0) - S(1, 0) * S(2, 2)) * d);
+    o[4] = (float)((S(0, 0) * S(2, 2) - S(0, 2) * S(2, 0)) * d);
+    o[5] = (float)((S(0, 2) * S(1, 0) - S(0, 0) * S(1, 2)) * d);
+    o[6] = (float)((S(1, 0) * S(2, 1) - S(1, 1) * S(2, 0)) * d);
+    o[7] = (float)((S(0, 1) * S(2, 0) - S(0, 0) * S(2, 1)) * d);
+    o[8] = (float)((S(0, 0) * S(1, 1) - S(0, 1) * S(1, 0)) * d);
+}
+
+// right singular vector of the smallest singular value of the M x 9 matrix
+// `a` (row-major, destroyed), unit norm, as float
+template <int M>
+__device__ void null_vector(double* a, float* out) {
+    double s[9], v[81];
+    orbgpu::epnp::svd_hestenes<M, 9>(a, s, v);
+    int jmin = 0;
+    for (int j = 1; j < 9; ++j)
+        if (s[j] < s[jmin]) jmin = j;
+    for (int k = 0; k < 9; ++k) out[k] = (float)v[k * 9 + jmin];
+}
+
+constexpr int kModelThreads = 64;
+
+__global__ __launch_bounds__(kModelThreads) void init_models_kernel(const float* __restrict__ work, int n1, int n2,
+                                                                    const int* __restrict__ pairs,
+                                                                    const int* __restrict__ sets, int n_iter,
+                                                                    float* __restrict__ h21, float* __restrict__ h12,
+                                                                    float* __restrict__ f21) {
+    const int t = blockIdx.x * kModelThreads + threadIdx.x;
+    if (t >= 2 * n_iter) return;
+    const bool homography = t < n_iter;
+    const int it = homography ? t : t - n_iter;
+    const float* pn1 = work;
+    const float* pn2 = work + 2 * n1;
+    const float* T1 = work + 2 * (n1 + n2);
+    const float* T2 = T1 + 9;
+    float u1[8], v1[8], u2[8], v2[8];
+    for (int j = 0; j < 8; ++j) {  // vPn1i[j] = vPn1[mvMatches12[idx].first], vPn2i likewise
+        const int idx = sets[8 * it + j];
+        const int a = pairs[2 * idx], b = pairs[2 * idx + 1];
+        u1[j] = pn1[2 * a];
+        v1[j] = pn1[2 * a + 1];
+        u2[j] = pn2[2 * b];
+        v2[j] = pn2[2 * b + 1];
+    }
+    if (homography) {
+        // ComputeH21 (:292-330): A (16 x 9, float entries), vt.row(8)
+        double A[16 * 9];
+        for (int i = 0; i < 8; ++i) {
+            double* r0 = A + 18 * i;
+            double* r1 = r0 + 9;
+            r0[0] = 0.0; r0[1] = 0.0; r0[2] = 0.0;
+            r0[3] = -u1[i]; r0[4] = -v1[i]; r0[5] = -1.0;
+            r0[6] = __fmul_rn(v2[i], u1[i]); r0[7] = __fmul_rn(v2[i], v1[i]); r0[8] = v2[i];
+            r1[0] = u1[i]; r1[1] = v1[i]; r1[2] = 1.0;
+            r1[3] = 0.0; r1[4] = 0.0; r1[5] = 0.0;
+            r1[6] = -__fmul_rn(u2[i], u1[i]); r1[7] = -__fmul_rn(u2[i], v1[i]); r1[8] = -u2[i];
+        }
+        float Hn[9], T2inv[9], tmp[9], H[9], Hi[9];
+        null_vector<16>(A, Hn);
+        inv3(T2, T2inv);      // T2.inv()
+        mul3(T2inv, Hn, tmp);  // H21i = T2inv*Hn*T1
+        mul3(tmp, T1, H);
+        inv3(H, Hi);           // H12i = H21i.inv()
+        for (int k = 0; k < 9; ++k) {
+            h21[9 * it + k] = H[k];
+            h12[9 * it + k] = Hi[k];
+        }
+    } else {
+        // ComputeF21 (:332-388): A (8 x 9; a zero 9th row for the square
+        // one-sided Jacobi), Fpre = vt.row(8), then the rank-2 projection
+        double A[9 * 9];
+        for (int i = 0; i < 8; ++i) {
+            double* r = A + 9 * i;
+            r[0] = __fmul_rn(u2[i], u1[i]); r[1] = __fmul_rn(u2[i], v1[i]); r[2] = u2[i];
+            r[3] = __fmul_rn(v2[i], u1[i]); r[4] = __fmul_rn(v2[i], v1[i]); r[5] = v2[i];
+            r[6] = u1[i]; r[7] = v1[i]; r[8] = 1.0;
+        }
+        for (int k = 0; k < 9; ++k) A[72 + k] = 0.0;
+        float Fpre[9];
+        null_vector<9>(A, Fpre);
+        // SVDecomp(Fpre): w(2) = 0; Fn = u*diag(w)*vt = sum of the two largest
+        // singular triples
+        double B[9], s[3], V[9];
+        for (int k = 0; k < 9; ++k) B[k] = Fpre[k];
+        orbgpu::epnp::svd_hestenes<3, 3>(B, s, V);
+        int jmin = 0;
+        for (int j = 1; j < 3; ++j)
+            if (s[j] < s[jmin]) jmin = j;
+        float Fn[9];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) {
+                double acc = 0.0;
+                for (int j = 0; j < 3; ++j)
+                    if (j != jmin) acc += B[3 * r + j] * V[3 * c + j];  // (U_j s_j) v_j^T
+                Fn[3 * r + c] = (float)acc;
+            }
+        float T2t[9], tmp[9], F[9];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) T2t[3 * r + c] = T2[3 * c + r];
+        mul3(T2t, Fn, tmp);  // F21i = T2t*Fn*T1
+        mul3(tmp, T1, F);
+        for (int k = 0; k < 9; ++k) f21[9 * it + k] = F[k];
+    }
+}
+
+}  // namespace
+
+extern "C" size_t orbgpu_init_workspace_bytes(int n1, int n2) {
+    return (size_t)(2 * ((n1 > 0 ? n1 : 0) + (n2 > 0 ? n2 : 0)) + 18) * sizeof(float);
+}
+
+extern "C" int orbgpu_init_hypotheses_batch_device(const float* d_kp1, int n1, const float* d_kp2, int n2,
+                                                   const int* d_pairs, int n_matches, const int* d_sets, int n_iter,
+                                                   void* d_work, orbgpu_match_pts* d_pts, float* d_h21,
+                                                   float* d_h12, float* d_f21, void* stream) {
+    if (n1 <= 0 || n2 <= 0 || n_matches < 8 || n_iter < 0 || !d_kp1 || !d_kp2 || !d_pairs || !d_work ||
+        (n_iter > 0 && (!d_sets || !d_h21 || !d_h12 || !d_f21)))
+        return orbgpu::fail(ORBGPU_ERR_ARG, "invalid argument (needs >= 8 matches and keypoints in both frames)");
+    if ((uintptr_t)d_pts & 15) return orbgpu::fail(ORBGPU_ERR_ARG, "d_pts must be 16-byte aligned");
+    if (int rc = orbgpu::check_device()) return rc;
+    (void)hipGetLastError();
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(init_normalize_kernel, dim3(1), dim3(kNormThreads), 0, s, d_kp1, n1, d_kp2, n2, d_pairs,
+                       n_matches, static_cast<float*>(d_work), reinterpret_cast<float4*>(d_pts));
+    ORB_HIP(hipGetLastError());
+    if (n_iter > 0) {
+        hipLaunchKernelGGL(init_models_kernel, dim3((2 * n_iter + kModelThreads - 1) / kModelThreads),
+                           dim3(kModelThreads), 0, s, static_cast<const float*>(d_work), n1, n2, d_pairs, d_sets,
+                           n_iter, d_h21, d_h12, d_f21);
+        ORB_HIP(hipGetLastError());
+    }
+    return ORBGPU_OK;
+}

@@ -4,9 +4,11 @@
 
 #include <algorithm>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
 
+#include "../../include/orbgpu_init.h"
 #include "../../include/orbgpu_ransac.h"
 #include "host_common.h"
 #include "ransac_kernels.h"
@@ -87,6 +89,28 @@ void orbgpu_rand_get_state(orbgpu_rand_state* out) {
 void orbgpu_rand_set_state(const orbgpu_rand_state* in) {
     std::lock_guard<std::mutex> lk(g_rand_mu);
     g_rand = *in;
+}
+
+void orbgpu_seed_rand_once(unsigned int s) {
+    static std::atomic<bool> seeded{false};
+    bool expect = false;
+    if (seeded.compare_exchange_strong(expect, true)) orbgpu_srand(s);
+}
+
+int orbgpu_init_draw_sets(int n_matches, int n_iter, int* sets) {
+    if (n_matches < 8 || n_iter < 0 || (n_iter > 0 && !sets)) return fail(ORBGPU_ERR_ARG, "invalid argument");
+    std::vector<int> avail;
+    for (int it = 0; it < n_iter; ++it) {
+        avail.resize(n_matches);
+        for (int i = 0; i < n_matches; ++i) avail[i] = i;
+        for (int j = 0; j < 8; ++j) {
+            const int r = orbgpu_random_int(0, (int)avail.size() - 1);
+            sets[8 * it + j] = avail[r];
+            avail[r] = avail.back();
+            avail.pop_back();
+        }
+    }
+    return ORBGPU_OK;
 }
 
 size_t orbgpu_sim3_workspace_bytes(int total_samples) {

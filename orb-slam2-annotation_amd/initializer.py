@@ -105,3 +105,80 @@ def select_best(scores) -> int:
     out = ctypes.c_int(-1)
     orbgpu._check(_lib().orbgpu_init_select_best(s.ctypes.data, s.shape[0], ctypes.byref(out)), "init_select_best")
     return out.value
+
+
+# ---- model hypotheses (Initialize / FindHomography / FindFundamental) -----
+def seed_rand_once(seed: int = 0) -> None:
+    """DUtils::Random::SeedRandOnce(seed) on the orbgpu_rand stream."""
+    _lib2().orbgpu_seed_rand_once(seed & 0x7FFFFFFF)
+
+
+def draw_sets(n_matches: int, n_iter: int = 200) -> np.ndarray:
+    """Initialize's minimal sets (Initializer.cpp:96-115) from the orbgpu_rand stream."""
+    sets = np.zeros((n_iter, 8), np.int32)
+    orbgpu._check(_lib2().orbgpu_init_draw_sets(n_matches, n_iter, sets.ctypes.data), "orbgpu_init_draw_sets")
+    return sets
+
+
+_BOUND2 = False
+
+
+def _lib2():
+    global _BOUND2
+    L = _lib()
+    if not _BOUND2:
+        vp, i = ctypes.c_void_p, ctypes.c_int
+        L.orbgpu_seed_rand_once.argtypes = [ctypes.c_uint]
+        L.orbgpu_init_draw_sets.argtypes = [i, i, vp]
+        L.orbgpu_init_workspace_bytes.argtypes = [i, i]
+        L.orbgpu_init_workspace_bytes.restype = ctypes.c_size_t
+        L.orbgpu_init_hypotheses_batch_device.argtypes = [vp, i, vp, i, vp, i, vp, i, vp, vp, vp, vp, vp, vp]
+        _BOUND2 = True
+    return L
+
+
+def find_models(kp1, kp2, matches12, sigma=1.0, n_iter=200, sets=None, device="cuda", stream=None):
+    """Initializer::Initialize up to the model choice (Initializer.cpp:55-140):
+    mvMatches12 from matches12 (vector<int>), Normalize, the n_iter minimal
+    sets (drawn from the orbgpu_rand stream unless given), every H21/H12/F21
+    hypothesis and its CheckHomography / CheckFundamental score on the GPU,
+    the kept iterations and RH = SH / (SH + SF).  kp1, kp2: (n, 2) keypoint
+    positions (mvKeys1 / mvKeysUn of the current frame)."""
+    import torch
+    m12 = np.asarray(matches12)
+    first = np.nonzero(m12 >= 0)[0]
+    pairs = np.stack([first, m12[first]], 1).astype(np.int32)
+    nm = len(pairs)
+    if sets is None:
+        sets = draw_sets(nm, n_iter)
+    sets = np.ascontiguousarray(sets, np.int32)
+    n_iter = len(sets)
+    dev = torch.device(device)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dt)).to(dev)  # noqa: E731
+    d_kp1, d_kp2 = t(np.asarray(kp1).reshape(-1, 2), np.float32), t(np.asarray(kp2).reshape(-1, 2), np.float32)
+    d_pairs, d_sets = t(pairs, np.int32), t(sets, np.int32)
+    work = torch.zeros(_lib2().orbgpu_init_workspace_bytes(len(d_kp1), len(d_kp2)), dtype=torch.uint8, device=dev)
+    pts = torch.zeros((nm, 4), dtype=torch.float32, device=dev)
+    h21 = torch.zeros((n_iter, 3, 3), dtype=torch.float32, device=dev)
+    h12, f21 = torch.zeros_like(h21), torch.zeros_like(h21)
+    orbgpu._check(_lib2().orbgpu_init_hypotheses_batch_device(
+        d_kp1.data_ptr(), len(d_kp1), d_kp2.data_ptr(), len(d_kp2), d_pairs.data_ptr(), nm, d_sets.data_ptr(), n_iter,
+        work.data_ptr(), pts.data_ptr(), h21.data_ptr(), h12.data_ptr(), f21.data_ptr(), _stream(stream)),
+        "orbgpu_init_hypotheses_batch_device")
+    sh, sf = torch.zeros(n_iter, device=dev), torch.zeros(n_iter, device=dev)
+    ih = torch.zeros((n_iter, nm), dtype=torch.uint8, device=dev)
+    jf = torch.zeros((n_iter, nm), dtype=torch.uint8, device=dev)
+    check_both_batch(pts, h21, h12, f21, sigma, sh, ih, sf, jf, stream)
+    if stream is not None:
+        stream.synchronize()
+    else:
+        torch.cuda.synchronize(dev)
+    shn, sfn = sh.cpu().numpy(), sf.cpu().numpy()
+    bh, bf = select_best(shn), select_best(sfn)
+    SH = np.float32(shn[bh]) if bh >= 0 else np.float32(0)
+    SF = np.float32(sfn[bf]) if bf >= 0 else np.float32(0)
+    return {"pairs": pairs, "sets": sets, "H21": h21.cpu().numpy(), "H12": h12.cpu().numpy(), "F21": f21.cpu().numpy(),
+            "scores_h": shn, "scores_f": sfn, "best_h": bh, "best_f": bf,
+            "inliers_h": ih[bh].cpu().numpy().astype(bool) if bh >= 0 else np.zeros(nm, bool),
+            "inliers_f": jf[bf].cpu().numpy().astype(bool) if bf >= 0 else np.zeros(nm, bool),
+            "RH": np.float32(SH / np.float32(SH + SF)) if SH + SF > 0 else np.float32(0)}

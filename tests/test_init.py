@@ -228,3 +228,86 @@ def test_binding_rejects_host_and_wrong_dtype():
     with pytest.raises(TypeError):  # CPU tensors
         initializer.check_fundamental_batch(tp, torch.zeros((2, 3, 3)), 1.0, torch.zeros(2),
                                             torch.zeros((2, 4), dtype=torch.uint8))
+
+
+# ---- model hypotheses: Normalize + ComputeH21 / ComputeF21 ----------------
+
+def _sets_from_glibc(nm, n_iter=200, seed=0):
+    """Initialize's draws (Initializer.cpp:96-115) with the host glibc rand()"""
+    import ctypes
+    libc = ctypes.CDLL("libc.so.6")
+    libc.srand(seed)
+    out = np.zeros((n_iter, 8), np.int32)
+    for it in range(n_iter):
+        avail = list(range(nm))
+        for j in range(8):
+            r = int((libc.rand() / (2147483647 + 1.0)) * len(avail))
+            out[it, j] = avail[r]
+            avail[r] = avail[-1]
+            avail.pop()
+    return out
+
+
+def _frames(n, planar, seed, extra=40):
+    """keypoints of two frames (with unmatched extras) and vMatches12"""
+    pts, M = _scene(n, planar, seed)
+    rng = np.random.default_rng(seed)
+    kp1 = np.vstack([pts[:, :2], rng.uniform([0, 0], [640, 480], (extra, 2))]).astype(F)
+    kp2 = np.vstack([rng.uniform([0, 0], [640, 480], (extra, 2)), pts[:, 2:]]).astype(F)
+    m12 = np.full(len(kp1), -1, np.int32)
+    m12[:n] = np.arange(n) + extra
+    return kp1, kp2, m12, M
+
+
+def test_draw_sets_match_glibc():
+    import initializer
+    import ransac
+    ransac.srand(0)
+    np.testing.assert_array_equal(initializer.draw_sets(150, 200), _sets_from_glibc(150))
+
+
+def test_oracle_normalize_and_models():
+    kp1, kp2, m12, M = _frames(300, True, 31)
+    pn, T = init_ref.normalize(kp1)
+    assert abs(float(np.abs(pn[:, 0]).mean()) - 1.0) < 1e-4 and abs(float(pn[:, 1].mean())) < 1e-4
+    np.testing.assert_allclose((T @ np.c_[kp1, np.ones(len(kp1))].T).T[:, :2], pn, atol=1e-4)
+    first = np.nonzero(m12 >= 0)[0]
+    pairs = np.stack([first, m12[first]], 1)
+    r = init_ref.find_models(kp1, kp2, pairs, _sets_from_glibc(len(pairs), 50))
+    H = r["H21"][r["best_h"]].astype(np.float64)
+    H = H / H[2, 2]
+    assert np.abs(H - M).max() < 0.05 * np.abs(M).max()
+    assert r["RH"] > 0.4  # planar scene: the homography wins (Initializer.cpp:140)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,planar,seed", [(300, True, 41), (1000, False, 42), (600, True, 43), (120, False, 44)])
+def test_gpu_find_models_vs_oracle(n, planar, seed):
+    """Normalize + the 200 H/F hypotheses on the GPU (init_models.hip) + the
+    bit-exact scorers, against init_ref.find_models: the kept iterations are
+    equal, H/F of every iteration agree to 1e-3 (up to sign: the SVD's null
+    vector sign is arbitrary and both scores are sign invariant), scores to
+    1e-4 relative."""
+    _gpu()
+    import initializer
+    kp1, kp2, m12, _ = _frames(n, planar, seed)
+    first = np.nonzero(m12 >= 0)[0]
+    pairs = np.stack([first, m12[first]], 1)
+    sets = _sets_from_glibc(len(pairs))
+    g = initializer.find_models(kp1, kp2, m12, sets=sets)
+    r = init_ref.find_models(kp1, kp2, pairs, sets)
+    assert g["best_h"] == r["best_h"] and g["best_f"] == r["best_f"]
+
+    def close(a, b, tol):
+        a, b = a.astype(np.float64).reshape(-1, 9), b.astype(np.float64).reshape(-1, 9)
+        sc = np.abs(b).max(1, keepdims=True)
+        return np.minimum(np.abs(a - b), np.abs(a + b)).max(1) / sc[:, 0] < tol
+
+    assert close(g["H21"], r["H21"], 1e-3).mean() > 0.97
+    assert close(g["F21"], r["F21"], 1e-3).mean() > 0.97
+    for k in ("scores_h", "scores_f"):
+        np.testing.assert_allclose(g[k], r[k], rtol=1e-4, atol=1e-3)
+    assert abs(float(g["RH"]) - float(r["RH"])) < 1e-4
+    bh = r["best_h"]
+    ref_inl = init_ref.check_homography(r["pts"], r["H21"][bh], r["H12"][bh])[1]
+    assert (g["inliers_h"] != ref_inl).sum() <= max(1, n // 200)
