@@ -54,7 +54,9 @@ import torch  # noqa: E402
 
 METRIC = "frames/sec ORB extract+match (1000 feat, 640×480 mono) at 1/2/4/8 GPU; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PYR_KERNEL = "pyramid_stream_kernel (one frame per block; source rows staged through LDS per 4-row step)"
+PYR_KERNEL = ("pyramid_tick_kernel (one frame per block; all levels advance together in ticks through LDS rings: "
+              "level 0 read once, levels 1..7 written once, nothing read back)")
+PYR_KERNEL_ID = "pyramid_tick_kernel"
 POOL_STEPS = 4
 
 CONFIGS = {
@@ -325,7 +327,8 @@ def traffic_for(path, config, batch):
         return None
     try:
         tj = json.loads(p.read_text())
-        if tj.get("config") == config and tj.get("batch") == batch:
+        if tj.get("config") == config and tj.get("batch") == batch and \
+                str(tj.get("kernel_name", "")).startswith(PYR_KERNEL_ID):
             return tj.get("pyramid_hbm_bytes_per_step")
     except Exception:
         return None

@@ -31,6 +31,18 @@ int orbgpu_debug_level_blur(orbgpu_extractor* ex, int frame, int level, uint8_t*
  * S, nToExpand, kstop, nkeys, N]). */
 int orbgpu_debug_octree_trace(orbgpu_extractor* ex, int enable, int* out, int cap);
 
+/* CPU run of the fused pyramid pass's plan (pyramid_plan.cpp), no GPU
+ * needed: builds the extractor geometry for these parameters and executes the
+ * kernel's tick schedule on the host -- same LDS ring slots, row records,
+ * per-lane column entries and fixed-point arithmetic -- checking that every
+ * read finds its source row in its slot and that no write of a tick lands in
+ * a slot read during it.  Writes levels 1..nlevels-1 tightly packed (w_l x
+ * h_l each) into out (out_bytes), and, if info != NULL, info[0..7] = {ticks,
+ * rows per chunk, compute waves, producer waves, loads per producer lane,
+ * entries per compute lane, LDS bytes per block, level-0 ring rows}. */
+int orbgpu_debug_pyramid_emulate(int nfeatures, float scale_factor, int nlevels, int width, int height,
+                                 const uint8_t* img, size_t img_step, uint8_t* out, size_t out_bytes, int* info);
+
 #ifdef __cplusplus
 }
 #endif

@@ -131,12 +131,9 @@ struct orbgpu_extractor {
     uint8_t* d_blur = nullptr;
     size_t blur_bytes = 0;
     int4* d_ptab = nullptr;
-    std::vector<int4> pyr_bands;   // host copy of the per-band pyramid records
-    int4* d_pyr_bands = nullptr;
-    std::vector<int2> pyr_yrec;    // per-row (y0, ibeta0 | ibeta1 << 16) of levels >= 1 (frame kernel)
-    int2* d_pyr_yrec = nullptr;
-    std::vector<int> pyr_ystage;   // stream kernel: staged source-row base per (level, step, group)
-    int* d_pyr_ystage = nullptr;
+    PyrPlan pyr_plan;              // fused pyramid pass: row records, tick ranges, per-lane entries
+    int4* d_pyr_ent = nullptr;
+    int2* d_pyr_tab = nullptr;
     uint32_t* d_cand = nullptr;
     int* d_cell_counts = nullptr;
     uint32_t* d_gkeys = nullptr;
@@ -169,7 +166,7 @@ struct orbgpu_extractor {
     int last_batch = 0;
 
     ~orbgpu_extractor() {
-        void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_bands, d_pyr_yrec, d_pyr_ystage, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
+        void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_ent, d_pyr_tab, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
                         d_oct_count, d_err, d_trace, d_img, d_single};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
@@ -183,130 +180,10 @@ struct orbgpu_extractor {
 
 namespace {
 
-// Row bands of the fused pyramid pass (pyramid.hip).  Band s owns rows
-// [ceil(s*h_l/S), ceil((s+1)*h_l/S)) of every level l and computes the rows it
-// owns plus the rows its next level's computed rows read (ytab is monotone,
-// so that is one contiguous range per level).  S is the smallest band count
-// whose two LDS ping-pong buffers fit 80 KiB (two blocks per CU), raised
-// while the batch alone would not fill the chip.
-// two 1024-thread blocks per CU (measured: bigger bands at one block per CU are slower)
 // row pitch of pyramid levels >= 1 in HBM (bytes)
 #ifndef ORBGPU_PYR_PITCH_ALIGN
 #define ORBGPU_PYR_PITCH_ALIGN 16
 #endif
-#ifndef ORBGPU_PYR_LDS_KB
-#define ORBGPU_PYR_LDS_KB 80
-#endif
-constexpr int kPyrLdsBudget = ORBGPU_PYR_LDS_KB * 1024;
-int plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, int max_batch, std::vector<int4>& table) {
-    const int L = g.nlevels;
-    table.clear();
-    if (L < 2) {
-        g.pyr_bands = 1;
-        g.pyr_rec_stride = L;
-        table.assign(L, int4{0, 0, 0, 0});
-        return ORBGPU_OK;
-    }
-    auto plan = [&](int S, std::vector<int4>& t, int& lds_a, int& lds_b, int& lds_y) {
-        t.assign((size_t)S * L, int4{0, 0, 0, 0});
-        lds_a = lds_b = lds_y = 0;
-        for (int s = 0; s < S; ++s) {
-            int4* b = &t[(size_t)s * L];
-            for (int l = 0; l < L; ++l) {
-                const int h = g.lv[l].h;
-                b[l].z = (int)(((long)s * h + S - 1) / S);
-                b[l].w = (int)(((long)(s + 1) * h + S - 1) / S);
-            }
-            b[L - 1].x = b[L - 1].z;
-            b[L - 1].y = b[L - 1].w;
-            for (int l = L - 1; l >= 1; --l) {
-                int lo = b[l].x, hi = b[l].y;
-                int slo = INT32_MAX, shi = INT32_MIN;
-                if (hi > lo) {
-                    const int2* yt = &ytab[(size_t)g.lv[l].ytab_offset];
-                    slo = yt[lo].x & 0xFFFF;
-                    shi = (yt[hi - 1].x >> 16) + 1;
-                }
-                if (l - 1 == 0) {
-                    b[0].x = hi > lo ? slo : 0;
-                    b[0].y = hi > lo ? shi : 0;
-                } else {
-                    const int olo = b[l - 1].z, ohi = b[l - 1].w;
-                    b[l - 1].x = std::min(olo < ohi ? olo : INT32_MAX, slo);
-                    b[l - 1].y = std::max(olo < ohi ? ohi : INT32_MIN, shi);
-                    if (b[l - 1].x >= b[l - 1].y) b[l - 1].x = b[l - 1].y = 0;
-                }
-            }
-            int yrows = 0;
-            for (int l = 0; l + 1 < L; ++l) {
-                const int bytes = (b[l].y - b[l].x) * g.lv[l].lds_pitch;
-                int& dst = (l & 1) ? lds_a : lds_b;
-                dst = std::max(dst, bytes);
-            }
-            for (int l = 1; l < L; ++l) yrows += b[l].y - b[l].x;
-            lds_y = std::max(lds_y, (L + yrows) * 16);
-        }
-    };
-    const int hmin = g.lv[L - 1].h;
-    int S = 1, lds_a = 0, lds_b = 0, lds_y = 0;
-    for (;; ++S) {
-        plan(S, table, lds_a, lds_b, lds_y);
-        if (lds_a + lds_b + lds_y + 96 <= kPyrLdsBudget) break;
-        if (S >= hmin || S >= 256) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid band does not fit in LDS");
-    }
-    while ((long)S * max_batch < 2048 && 2 * S <= hmin / 4 && S < 64) {
-        S *= 2;
-        plan(S, table, lds_a, lds_b, lds_y);
-    }
-    g.pyr_bands = S;
-    g.pyr_lds_a = 16;  // 16 bytes in front of each row buffer: column windows may start at -8
-    g.pyr_lds_b = g.pyr_lds_a + (int)round_up((size_t)lds_a + 16, 16);
-    g.pyr_lds_y = g.pyr_lds_b + (int)round_up((size_t)lds_b + 16, 16);
-    g.pyr_lds_bytes = g.pyr_lds_y + (int)round_up((size_t)lds_y, 16);
-    // Per-band records, copied into LDS by the block together with its
-    // level-0 rows: the L band entries, then for levels 1..L-1 one int4 per
-    // computed row = (LDS offset of source row y0, of y1, ibeta0 << 12,
-    // ibeta1 << 12).  Nothing frame-dependent, so the kernel does no
-    // dependent table reads.
-    int stride = 0;
-    for (int s = 0; s < S; ++s) {
-        int n = L;
-        for (int l = 1; l < L; ++l) n += table[(size_t)s * L + l].y - table[(size_t)s * L + l].x;
-        stride = std::max(stride, n);
-    }
-    std::vector<int4> rec((size_t)S * stride, int4{0, 0, 0, 0});
-    for (int s = 0; s < S; ++s) {
-        const int4* b = &table[(size_t)s * L];
-        int4* r = &rec[(size_t)s * stride];
-        for (int l = 0; l < L; ++l) {
-            r[l] = b[l];
-            // .z = run length of a row group (even), .w unused
-            const int rows = b[l].y - b[l].x, R = l > 0 ? g.lv[l].brgroups : 1;
-            r[l].z = ((rows + R - 1) / R + 1) & ~1;
-            r[l].w = 0;
-        }
-        int off = L;
-        for (int l = 1; l < L; ++l) {
-            const int src_lo = b[l - 1].x, sp = g.lv[l - 1].lds_pitch;
-            const int base = ((l - 1) & 1) ? g.pyr_lds_a : g.pyr_lds_b;
-            const int2* yt = &ytab[(size_t)g.lv[l].ytab_offset];
-            for (int y = b[l].x; y < b[l].y; ++y) {
-                const int2 t = yt[y];
-                r[off++] = int4{base + ((t.x & 0xFFFF) - src_lo) * sp, base + ((t.x >> 16) - src_lo) * sp,
-                                t.y & 0xFFFF, (int)((uint32_t)t.y >> 16)};
-            }
-        }
-    }
-    table.swap(rec);
-    g.pyr_rec_stride = stride;
-    if (stride > pyr_prefetch_rec()) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid band record too long");
-    for (int s = 0; s < S; ++s) {
-        const int4 b0 = table[(size_t)s * stride];
-        if ((long)(b0.y - b0.x) * ((g.lv[0].w + 15) / 16) > pyr_prefetch_uint4())
-            return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid band too tall for the level-0 prefetch");
-    }
-    return ORBGPU_OK;
-}
 
 // ORBextractor ctor arithmetic (ORBextractor.cpp:417-448) + per-level layout.
 int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int2>& ytab) {
@@ -388,11 +265,6 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
         ncap = std::max(ncap, std::max(v.ocap, v.nini));
         // resize tables: ytab rows as built; columns as per-quad tap records
         // for pyramid.hip (3 int4 per quad: (lo, wt) x 4 and the 4 perm selectors)
-        v.lds_pitch = (int)round_up((size_t)v.w, l == 0 ? 16 : 4);
-        if (l == 0) {
-            const uint64_t v4 = ((uint64_t)v.w + 15) / 16;
-            v.quad_magic = v4 < 2 ? 0xFFFFFFFFu : (uint32_t)(((1ull << 32) + v4 - 1) / v4);
-        }
         if (l > 0) {
             const LevelGeom& p = g.lv[l - 1];
             std::vector<int2> xt, yt;
@@ -403,39 +275,13 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
             v.simd_end = vresize_simd_end(v.w);
             const int quads = (v.w + 3) / 4;
             if (quads < 3) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid level narrower than 9 px");
-            // pyramid.hip gives the last quad (the scalar tail) its own threads
+            // pyramid.hip gives the last quad (the scalar tail) its own lanes
             // (or, when w is a multiple of 16, there is no tail at all)
             if (v.simd_end == v.w && v.w % 4 == 0) v.qmain = quads;
             else if (v.simd_end == 4 * (quads - 1)) v.qmain = quads - 1;
             else return fail(ORBGPU_ERR_UNSUPPORTED, "resize tail is not the last quad");
-            // thread layout (pyramid.hip quad_taps): vector quads 1 .. qmain-1
-            // in row groups from thread 0, then one edge wave: lanes 0..31 the
-            // first quad of each row (its column window starts before the
-            // row), lanes 32..63 the scalar-tail quad
-            {
-                const int qv = v.qmain - 1;
-                if (qv < 1) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid level narrower than 9 px");
-                v.quad_magic = (uint32_t)(((1ull << 32) + qv - 1) / qv);
-                const int T = pyr_threads();
-                int R = (T - 64) / qv;
-                while (R > 0 && (int)round_up((size_t)qv * R, 64) + 64 > T) --R;
-                if (R < 1) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid level wider than the block");
-                v.rgroups = R;
-                v.tail_base = (int)round_up((size_t)qv * R, 64);
-            }
-
-            {  // band-kernel layout (pyramid.hip band_taps)
-                const int T = pyr_threads();
-                int R = (T - 64) / v.qmain;
-                while (R > 0 && (int)round_up((size_t)v.qmain * R, 64) + 64 > T) --R;
-                if (R < 1 || R > 64) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid level width outside the band layout");
-                v.brgroups = R;
-                v.bquad_magic = (uint32_t)(((1ull << 32) + v.qmain - 1) / v.qmain);
-                v.btail_base = (int)round_up((size_t)v.qmain * R, 64);
-            }
             if ((size_t)v.pitch * v.h >= (1u << 31)) return fail(ORBGPU_ERR_UNSUPPORTED, "level too large");
             v.ptab_offset = (int)ptab.size();
-            v.dbg_level = l;
             // Column taps per quad for pyramid.hip (3 int4 per quad):
             //   (w0, wt0, wt1, wt2), (wt3, sel0, sel1, sel2), (sel3, 0, 0, 0).
             // The kernel reads the three dwords d0, d1, d2 at byte w0 of the
@@ -445,7 +291,7 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
             // wt_k = (16 ialpha0, 16 ialpha1) so v_dot2_u32_u16 yields
             // 4096 x the exact HResizeLinear sum: its high half is h >> 4,
             // the operand of VResizeLinearVec_32s8u.  w0 may be -4 or -8
-            // (the LDS row buffers have 16 bytes in front).  Holds for every
+            // (the LDS ring rows have 16 bytes in front).  Holds for every
             // scale factor <= 2 (checked here per quad).
             for (int q = 0; q < quads; ++q) {
                 const int lo = xt[4 * q].x & 0xFFFF;
@@ -479,62 +325,11 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
             }
             v.ytab_offset = (int)ytab.size();
             ytab.insert(ytab.end(), yt.begin(), yt.end());
-            // frame-kernel row records: the second source row must be y0 + 1,
-            // or y0 with a zero weight (bottom clamp)
-            v.yrec_offset = (int)e->pyr_yrec.size();
-            for (const int2& t : yt) {
-                const int y0 = t.x & 0xFFFF, y1 = t.x >> 16, b1 = (int)((uint32_t)t.y >> 16);
-                if (!(y1 == y0 + 1 || (y1 == y0 && b1 == 0)))
-                    return fail(ORBGPU_ERR_UNSUPPORTED, "unexpected resize row taps");
-                e->pyr_yrec.push_back(int2{y0, t.y});
-            }
         }
     }
-    g.pyr_yrec_total = (int)e->pyr_yrec.size();
     {
-        const char* m = std::getenv("ORBGPU_PYR_MODE");  // tuning/A-B only: "band" / "frame" select the other kernels
-        g.pyr_mode = (m && std::strcmp(m, "band") == 0) ? 0 : (m && std::strcmp(m, "frame") == 0) ? 1 : 2;
-    }
-    // stream kernel (pyramid.hip): row group g of level l owns rows
-    // [g*run, (g+1)*run); step k covers 4 of them, whose source rows are the
-    // 6 rows from ystage[k][g] of the previous level, staged in LDS.
-    e->pyr_ystage.clear();
-    g.pyr_stage_bytes = 0;
-    for (int l = 1; l < L; ++l) {
-        LevelGeom& v = g.lv[l];
-        const LevelGeom& sv = g.lv[l - 1];
-        const int R = v.rgroups;
-        v.pyr_run = ((v.h + R - 1) / R + 3) & ~3;
-        v.pyr_steps = v.pyr_run / 4;
-        v.ystage_offset = (int)e->pyr_ystage.size();
-        const int2* yr = &e->pyr_yrec[(size_t)v.yrec_offset];
-        for (int k = 0; k < v.pyr_steps; ++k)
-            for (int gr = 0; gr < R; ++gr) {
-                const int o0 = gr * v.pyr_run + 4 * k;
-                if (o0 >= v.h) { e->pyr_ystage.push_back(0); continue; }
-                const int o1 = std::min(o0 + 3, v.h - 1);
-                const int ys = yr[o0].x;
-                if (yr[o1].x + 1 - ys > 5) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid step spans more than 6 source rows");
-                e->pyr_ystage.push_back(ys);
-            }
-        const int lsp = (int)round_up((size_t)sv.w, 16);  // staged row pitch in LDS
-        const int bytes = R * 6 * lsp;
-        if (R * 6 * (lsp / 16) > 2 * pyr_threads())
-            return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid staging exceeds two chunks per thread");
-        g.pyr_stage_bytes = std::max(g.pyr_stage_bytes, bytes);
-    }
-    g.pyr_ystage_total = (int)e->pyr_ystage.size();
-    g.pyr_lds_stage = (int)round_up((size_t)g.pyr_yrec_total * 8 + (size_t)g.pyr_ystage_total * 4, 16);
-    if (g.pyr_mode == 2 && g.pyr_lds_stage + 2 * g.pyr_stage_bytes > 80 * 1024)
-        return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid stream kernel needs more than 80 KiB of LDS");
-    if (g.pyr_mode == 0) {
-        int rc = plan_pyramid_bands(g, ytab, e->max_batch, e->pyr_bands);
+        const int rc = plan_pyramid(g, ytab, ptab, e->max_batch, e->pyr_plan);
         if (rc) return rc;
-    } else {
-        g.pyr_bands = 1;
-        e->pyr_bands.assign(1, int4{0, 0, 0, 0});
-        if ((size_t)g.pyr_yrec_total * sizeof(int2) > 64 * 1024)
-            return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid row records exceed 64 KiB of LDS");
     }
     g.total_cells = cell_base;
     g.cand_frame = cand_off;
@@ -589,7 +384,7 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
         evs = e->ev[e->ev_used++].data();
         ORB_HIP(hipEventRecord(evs[0], s));
     }
-    ORB_HIP(launch_pyramid(g, batch, e->d_pyr_bands, e->d_pyr_yrec, e->d_pyr_ystage, e->d_ptab, imgs, row_step, frame_step, e->d_pyr, s));
+    ORB_HIP(launch_pyramid(g, batch, e->d_pyr_ent, e->d_pyr_tab, imgs, row_step, frame_step, e->d_pyr, s));
     if (evs) ORB_HIP(hipEventRecord(evs[1], s));
     ORB_HIP(launch_fast_cells(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_cand, e->d_cell_counts, e->d_err, s));
     if (evs) ORB_HIP(hipEventRecord(evs[2], s));
@@ -678,8 +473,7 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
         (rc = dalloc(&e->d_gknode, g.cand_frame * B)) || (rc = dalloc(&e->d_oct_out, (size_t)g.slots_frame * B)) ||
         (rc = dalloc(&e->d_oct_count, (size_t)g.nlevels * B)) || (rc = dalloc(&e->d_err, 1)) ||
         (rc = dalloc(&e->d_img, e->img_pitch * height)) ||
-        (rc = dalloc(&e->d_pyr_bands, e->pyr_bands.size())) || (rc = dalloc(&e->d_pyr_yrec, e->pyr_yrec.size())) ||
-        (rc = dalloc(&e->d_pyr_ystage, e->pyr_ystage.size()))) {
+        (rc = dalloc(&e->d_pyr_ent, e->pyr_plan.ent.size())) || (rc = dalloc(&e->d_pyr_tab, e->pyr_plan.tab.size()))) {
         delete e;
         return rc;
     }
@@ -698,12 +492,10 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
         return fail(ORBGPU_ERR_HIP, "pinned staging allocation failed");
     }
     if (hipMemcpy(e->d_ptab, ptab.data(), ptab.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(e->d_pyr_bands, e->pyr_bands.data(), e->pyr_bands.size() * sizeof(int4), hipMemcpyHostToDevice) !=
-            hipSuccess ||
-        (!e->pyr_yrec.empty() && hipMemcpy(e->d_pyr_yrec, e->pyr_yrec.data(), e->pyr_yrec.size() * sizeof(int2),
-                                           hipMemcpyHostToDevice) != hipSuccess) ||
-        (!e->pyr_ystage.empty() && hipMemcpy(e->d_pyr_ystage, e->pyr_ystage.data(), e->pyr_ystage.size() * sizeof(int),
-                                             hipMemcpyHostToDevice) != hipSuccess) ||
+        (!e->pyr_plan.ent.empty() && hipMemcpy(e->d_pyr_ent, e->pyr_plan.ent.data(),
+                                               e->pyr_plan.ent.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess) ||
+        (!e->pyr_plan.tab.empty() && hipMemcpy(e->d_pyr_tab, e->pyr_plan.tab.data(),
+                                               e->pyr_plan.tab.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess) ||
         pyramid_set_lds_limit(g) != hipSuccess ||
         hipMemset(e->d_err, 0, sizeof(int)) != hipSuccess ||
         hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -982,6 +774,43 @@ int orbgpu_debug_level_octree(orbgpu_extractor* e, int frame, int level, int* xy
 }
 
 }  // extern "C"
+
+int orbgpu_debug_pyramid_emulate(int nfeatures, float scale_factor, int nlevels, int width, int height,
+                                 const uint8_t* img, size_t img_step, uint8_t* out, size_t out_bytes, int* info) {
+    if (!img || !out || nfeatures <= 0 || nlevels <= 0 || nlevels > kMaxLevels || !(scale_factor > 1.f) ||
+        width <= 0 || height <= 0 || img_step < (size_t)width)
+        return fail(ORBGPU_ERR_ARG, "invalid emulation arguments");
+    orbgpu_extractor e;  // host geometry only: no device buffers are allocated
+    e.nfeatures = nfeatures;
+    e.scale_factor = scale_factor;
+    e.nlevels = nlevels;
+    e.ini_th = 20;
+    e.min_th = 7;
+    e.W = width;
+    e.H = height;
+    e.max_batch = 1;
+    std::vector<int4> ptab;
+    std::vector<int2> ytab;
+    int rc = build_geometry(&e, ptab, ytab);
+    if (rc) return rc;
+    const Geom& g = e.g;
+    size_t need = 0;
+    for (int l = 1; l < nlevels; ++l) need += (size_t)g.lv[l].w * g.lv[l].h;
+    if (out_bytes < need) return fail(ORBGPU_ERR_CAPACITY, "out_bytes smaller than levels 1..L-1");
+    std::vector<std::vector<uint8_t>> levels;
+    rc = emulate_pyramid(g, ytab, e.pyr_plan, img, img_step, levels);
+    if (rc) return rc;
+    for (int l = 1; l < nlevels; ++l) {
+        std::memcpy(out, levels[(size_t)l].data(), levels[(size_t)l].size());
+        out += levels[(size_t)l].size();
+    }
+    if (info) {
+        const int v[8] = {g.tk_ticks, g.tk_t0, g.tk_cwaves, g.tk_pwaves, g.tk_np, g.tk_e, g.tk_lds_bytes,
+                          g.lv[0].tk_ring_rows};
+        std::memcpy(info, v, sizeof(v));
+    }
+    return ORBGPU_OK;
+}
 
 // Frame::ComputeStereoMatches (Frame.cpp:540-748) over the last extraction.
 int orbgpu_stereo_matches_batch_device(orbgpu_extractor* e, const uint8_t* d_images, size_t row_step,

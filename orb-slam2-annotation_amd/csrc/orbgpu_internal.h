@@ -73,21 +73,13 @@ struct LevelGeom {
     int out_offset;           // slot offset of this level within a frame
     // resize tables (levels >= 1)
     int ytab_offset;
-    // fused pyramid pass (pyramid.hip)
-    int lds_pitch;            // LDS row pitch: w rounded up to 4 (level 0: to 16)
+    // fused pyramid pass (pyramid.hip, plan_pyramid in pyramid_plan.cpp)
     int qmain;                // quads per row on VResizeLinearVec_32s8u's vector path (the rest is the tail quad)
-    int dbg_level;            // = level index (diagnostic builds)
-    uint32_t quad_magic;      // ceil(2^32 / d): i / d = umulhi(i, magic); d = qmain (level 0: ceil(w/16))
     int ptab_offset;          // int4 offset of this level's per-quad column taps (3 int4 per quad)
-    int rgroups;              // row groups of a pyramid block (pyramid.hip quad_taps)
-    int tail_base;            // first thread of the tail quads (a wave boundary)
-    int yrec_offset;          // first row record of this level (pyramid_frame_kernel)
-    int brgroups;             // band kernel: row groups (quads 0..qmain-1 per group)
-    uint32_t bquad_magic;     // band kernel: ceil(2^32 / qmain)
-    int btail_base;           // band kernel: first thread of the tail wave (lane = row group)
-    int pyr_run;              // stream/frame kernels: output rows per row group (a multiple of 4)
-    int pyr_steps;            // stream kernel: 4-row steps per level (pyr_run / 4)
-    int ystage_offset;        // stream kernel: first staged-row base of this level ([step][group])
+    int tk_ring;              // LDS byte offset of the ring holding this level's latest rows (levels 0..L-2)
+    int tk_ring_rows;         // rows in that ring (levels >= 1: row y lives in slot y mod tk_ring_rows; level 0: tk_nc0 * tk_t0)
+    int tk_pitch;             // LDS pitch of the ring rows: w rounded up to 16
+    int tk_rec;               // int2 index of row 0's record in the plan table (levels >= 1)
     // blurred level (all levels, incl. 0): same row pitch as the pyramid
     size_t blur_offset, blur_frame_bytes;
     int blur_tiles_x, blur_tile_base;   // blur work items: 4-column x 64-row strips
@@ -104,15 +96,23 @@ struct Geom {
     int win_pitch, win_rows;  // FAST LDS tile: max over levels of (wCell+9) rounded to 4, (hCell+6)
     int blur_tiles_frame;     // blur tiles per frame over all levels
     int det_max;              // max FAST detection-region pixels of a cell (wCell x hCell)
-    // fused pyramid pass (pyramid.hip): frame bands per frame and LDS layout
-    int pyr_bands;
-    int pyr_lds_a, pyr_lds_b, pyr_lds_y, pyr_lds_bytes;  // odd levels, even levels (incl. 0), y taps
-    int pyr_rec_stride;       // int4s per band record (band entries + per-row source offsets)
-    int pyr_mode;             // 0: band kernel (levels through LDS), 1: frame kernel (levels through L2), 2: stream kernel
-    int pyr_yrec_total;       // row records of all levels >= 1 (frame kernel)
-    int pyr_ystage_total;     // stream kernel: staged-row bases of all levels
-    int pyr_stage_bytes;      // stream kernel: bytes of one staging buffer (max over levels)
-    int pyr_lds_stage;        // stream kernel: LDS offset of the staging buffers (after the row tables)
+    // fused pyramid pass (pyramid.hip): one block per frame walks the frame in
+    // ticks; the plan (pyramid_plan.cpp) fixes every row's tick and LDS slot
+    int tk_t0;                // level-0 rows per chunk (one chunk enters LDS per tick)
+    int tk_k0;                // level-0 chunks
+    int tk_ticks;             // ticks per frame
+    int tk_rs;                // int2 entries per tick in the range table ((L-1) * tk_groups + 1; the last is empty)
+    int tk_groups;            // row groups per level (max)
+    int tk_cwaves, tk_pwaves; // compute waves, producer (level-0 loader) waves
+    int tk_np;                // 16-byte level-0 loads per producer lane per chunk
+    int tk_e;                 // entries (level, quad, group) per compute lane
+    int tk_threads;           // 64 * (tk_cwaves + tk_pwaves)
+    int tk_lds_tab;           // LDS byte offset of the plan table (row records, then ranges)
+    int tk_tab_n;             // int2 entries in the plan table
+    int tk_rng;               // int2 index of the range table within the plan table
+    int tk_lds_bytes;         // LDS per block
+    int tk_nc0;               // level-0 chunk runs in ring 0 (row r: run (r / tk_t0) % tk_nc0, row r % tk_t0 in it)
+    int tk_cstride0;          // bytes per chunk run (tk_t0 rows at the level-0 pitch, padded to whole LDS-DMA pieces)
     LevelGeom lv[kMaxLevels];
 };
 

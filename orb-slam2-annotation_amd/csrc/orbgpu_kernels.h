@@ -1,23 +1,31 @@
 // orbgpu_kernels.h -- host-side launchers of the HIP kernels (one per stage).
 #pragma once
 
+#include <vector>
+
 #include "orbgpu_internal.h"
 
 struct orbgpu_keypoint;
 
 namespace orbgpu {
 
-int pyr_threads();
-int pyr_prefetch_uint4();  // level-0 16-byte chunks a pyramid band may stage
-int pyr_prefetch_rec();    // int4s a band record may hold
-// all pyramid levels 1..L-1 of `batch` frames; recs: int4 [pyr_bands][pyr_rec_stride]
-// per band = (need_lo, need_hi, own_lo, own_hi) rows per level, then one
-// (src0 LDS offset, src1 LDS offset, ibeta0 << 12, ibeta1 << 12) per computed
-// row of levels 1..L-1 (plan_pyramid_bands)
-hipError_t launch_pyramid(const Geom& g, int batch, const int4* recs, const int2* yrec, const int* ystage, const int4* ptab,
-                          const uint8_t* img0, size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream);
+// Fused pyramid pass (pyramid.hip) and its host plan (pyramid_plan.cpp).
+struct PyrPlan {
+    std::vector<int2> tab;  // row records of levels 1..L-1 (LDS offsets of the two source rows, ibeta pair), then per tick the row range of every (level, group)
+    std::vector<int4> ent;  // per compute lane and entry: 6 int4 (pyramid.hip TickEnt)
+};
+// fills g.tk_* and g.lv[l].tk_* and the plan; ORBGPU_ERR_UNSUPPORTED when the
+// geometry does not fit one block (message in orbgpu_last_error)
+int plan_pyramid(Geom& g, const std::vector<int2>& ytab, const std::vector<int4>& ptab, int max_batch, PyrPlan& plan);
+// LDS byte offset of row r of level l in its ring
+int slot_offset(const Geom& g, int l, int r);
+// the kernel's schedule run on the CPU with slot-ownership checks (levels[l]: w_l x h_l, tight)
+int emulate_pyramid(const Geom& g, const std::vector<int2>& ytab, const PyrPlan& plan, const uint8_t* img, size_t row0,
+                    std::vector<std::vector<uint8_t>>& levels);
+// all pyramid levels 1..L-1 of `batch` frames (one block per frame)
+hipError_t launch_pyramid(const Geom& g, int batch, const int4* ents, const int2* tab, const uint8_t* img0,
+                          size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream);
 hipError_t pyramid_set_lds_limit(const Geom& g);
-int pyr_stream_lds_bytes(const Geom& g);
 
 hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                              const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err,

@@ -108,6 +108,7 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_debug_level_blur.argtypes = [vp, i, i, vp, sz]
         L.orbgpu_debug_level_octree.argtypes = [vp, i, i, vp, i]
         L.orbgpu_debug_octree_trace.argtypes = [vp, i, vp, i]
+        L.orbgpu_debug_pyramid_emulate.argtypes = [i, f, i, i, i, vp, sz, vp, sz, vp]
         L.orbgpu_search_for_initialization.argtypes = [GridBounds, vp, vp, i, vp, vp, i, vp, i, f, i, vp,
                                                        ctypes.POINTER(i)]
         # orbgpu_frame.h
@@ -167,6 +168,33 @@ def device_arch() -> str:
     buf = ctypes.create_string_buffer(64)
     _check(lib().orbgpu_device_arch(buf, 64), "orbgpu_device_arch")
     return buf.value.decode()
+
+
+def pyramid_plan_emulate(img: np.ndarray, nfeatures=1000, scale_factor=1.2, nlevels=8):
+    """Levels 1..nlevels-1 of `img` computed on the CPU by the fused pyramid
+    kernel's own plan (orbgpu_debug_pyramid_emulate: same LDS ring slots, row
+    records and per-lane columns, with slot-ownership checks), and the plan's
+    figures.  Needs no GPU."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    # level sizes as ORBextractor computes them (cvRound of float products)
+    sizes, s = [], np.float32(1.0)
+    for l in range(1, nlevels):
+        s = np.float32(s * np.float32(scale_factor))
+        inv = np.float32(np.float32(1.0) / s)
+        sizes.append((int(np.rint(np.float32(h) * inv)), int(np.rint(np.float32(w) * inv))))
+    out = np.zeros(sum(a * b for a, b in sizes) + 64, np.uint8)
+    info = np.zeros(8, np.int32)
+    _check(lib().orbgpu_debug_pyramid_emulate(nfeatures, scale_factor, nlevels, w, h, img.ctypes.data, img.strides[0],
+                                              out.ctypes.data, out.size, info.ctypes.data),
+           "orbgpu_debug_pyramid_emulate")
+    levels, o = [], 0
+    for lh, lw in sizes:
+        levels.append(out[o:o + lw * lh].reshape(lh, lw).copy())
+        o += lw * lh
+    keys = ("ticks", "rows_per_chunk", "compute_waves", "producer_waves", "loads_per_lane", "entries_per_lane",
+            "lds_bytes", "ring0_rows")
+    return levels, dict(zip(keys, (int(v) for v in info)))
 
 
 def _ptr(a) -> int:

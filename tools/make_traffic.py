@@ -17,7 +17,7 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent))
 from pmc_summary import load  # noqa: E402
 
-KERNEL = "pyramid"  # matched as a prefix: pyramid_stream_kernel / pyramid_frame_kernel / pyramid_kernel
+KERNEL = "pyramid"  # matched as a prefix (pyramid_tick_kernel<E, NP>)
 
 
 def main():
@@ -39,6 +39,7 @@ def main():
     write_b = write_kib * 1024.0
     out = {
         "kernel": KERNEL,
+        "kernel_name": kf,
         "config": a.config,
         "batch": a.batch,
         "fetch_size_kib_raw": fetch_kib,

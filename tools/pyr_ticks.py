@@ -1,0 +1,49 @@
+"""Per-tick timeline of pyramid_tick_kernel from a diagnostic build
+(make BUILD=build_stamps LIB=liborbgpu_stamps.so EXTRA=-DPYR_STAMPS=1).
+Run on the GPU box:  ORBGPU_LIBRARY=orb-slam2-annotation_amd/liborbgpu_stamps.so python tools/pyr_ticks.py
+Prints, for blocks 0..63 of a 512-frame batch: block span, compute time per
+tick of wave 0, its barrier wait, the producer's wait for its chunk."""
+import ctypes
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "orb-slam2-annotation_amd")]
+import orbgpu  # noqa: E402
+import synth  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+W, H = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (640, 480)
+torch.cuda.set_device(0)
+frames = synth.torch_stream(B, W, H, bounded=True)
+ex = orbgpu.Extractor(width=W, height=H, max_batch=B, nfeatures=1000 if W == 640 else 2000)
+cap = ex.max_keypoints
+kps = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
+desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+counts = torch.zeros(B, dtype=torch.int32, device="cuda")
+for _ in range(3):
+    ex.extract_batch(frames, kps, desc, counts)
+torch.cuda.synchronize()
+lib = orbgpu.lib()
+st = np.zeros(64 * 160 * 16, np.uint64)
+lib.orbgpu_debug_pyr_stamps.argtypes = [ctypes.c_void_p]
+assert lib.orbgpu_debug_pyr_stamps(st.ctypes.data) == 0
+st = st.reshape(64, 160, 16).astype(np.int64)
+_, info = orbgpu.pyramid_plan_emulate(np.zeros((H, W), np.uint8), 1000, 1.2, 8)
+K = info["ticks"]
+nw = info["compute_waves"]
+print("plan", info)
+start = st[:, :K, 15]
+span = st[:, K - 1, :nw].max(1) - st[:, 0, 15]
+print("block span cycles: mean %.0f min %d max %d" % (span.mean(), span.min(), span.max()))
+done = st[:, :K, :nw] - start[:, :, None]  # each compute wave's finish, relative to wave 0's tick start
+prod = st[:, :K, 14] - start
+print("per compute wave: mean finish within the tick (cycles), over ticks 4..K-8")
+for w in range(nw):
+    print(f"  wave {w:2d}: {done[:, 4:K - 8, w].mean():7.0f}  (max {done[:, 4:K - 8, w].max():6d})")
+print(f"  producer ready: {prod[:, 4:K - 8].mean():7.0f}")
+tick = st[:, 1:K, 15] - st[:, :K - 1, 15]
+print("tick length mean %.0f" % tick[:, 4:K - 8].mean())
