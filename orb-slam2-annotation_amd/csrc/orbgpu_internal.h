@@ -101,15 +101,15 @@ struct Geom {
     int tk_t0;                // level-0 rows per chunk (one chunk enters LDS per tick)
     int tk_k0;                // level-0 chunks
     int tk_ticks;             // ticks per frame
-    int tk_rs;                // int2 entries per tick in the range table ((L-1) * tk_groups + 1; the last is empty)
-    int tk_groups;            // row groups per level (max)
+    int tk_rs;                // ranges per tick (tk_groups + 1; the last is empty)
+    int tk_groups;            // row-group slots per tick (each level's regular groups, then its tail groups)
     int tk_cwaves, tk_pwaves; // compute waves, producer (level-0 loader) waves
     int tk_np;                // 16-byte level-0 loads per producer lane per chunk
     int tk_e;                 // entries (level, quad, group) per compute lane
     int tk_threads;           // 64 * (tk_cwaves + tk_pwaves)
     int tk_lds_tab;           // LDS byte offset of the plan table (row records, then ranges)
     int tk_tab_n;             // int2 entries in the plan table
-    int tk_rng;               // int2 index of the range table within the plan table
+    int tk_rng;               // u32 index of the range table within the plan table (one packed u32 per range)
     int tk_lds_bytes;         // LDS per block
     int tk_nc0;               // level-0 chunk runs in ring 0 (row r: run (r / tk_t0) % tk_nc0, row r % tk_t0 in it)
     int tk_cstride0;          // bytes per chunk run (tk_t0 rows at the level-0 pitch, padded to whole LDS-DMA pieces)

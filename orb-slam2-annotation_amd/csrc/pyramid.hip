@@ -34,6 +34,10 @@ namespace {
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
+#ifndef ORBGPU_PYR_WAVES_EU
+#define ORBGPU_PYR_WAVES_EU 5  // waves per SIMD the register budget is sized for (two 10-11-wave blocks per CU)
+#endif
+
 #ifdef PYR_STAMPS  // diagnostic build only (tools/pyr_ticks.py): per-tick clock stamps of blocks 0..63
 __device__ unsigned long long g_pyr_stamps[64 * 160 * 16];
 __device__ __forceinline__ unsigned long long pyr_clock() {
@@ -41,6 +45,12 @@ __device__ __forceinline__ unsigned long long pyr_clock() {
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     return t;
 }
+// per block (all 512): realtime (100 MHz) at start and end, memtime at start and end, HW_ID, XCC_ID
+__device__ unsigned long long g_pyr_blocks[1024 * 6];
+#define PYR_BLOCK(slot, v)                                                                              \
+    do {                                                                                                \
+        if (threadIdx.x == 0 && blockIdx.x < 1024) g_pyr_blocks[(size_t)blockIdx.x * 6 + (slot)] = (v);  \
+    } while (0)
 #define PYR_STAMP(k, slot)                                                                              \
     do {                                                                                                \
         const unsigned long long t_ = pyr_clock();                                                      \
@@ -49,6 +59,7 @@ __device__ __forceinline__ unsigned long long pyr_clock() {
     } while (0)
 #else
 #define PYR_STAMP(k, slot) ((void)0)
+#define PYR_BLOCK(slot, v) ((void)0)
 #endif
 
 // Column taps of a quad (host: build_geometry, 3 int4 per quad): the byte
@@ -156,14 +167,6 @@ __device__ __forceinline__ TickEnt load_ent(const int4* __restrict__ ent, int f)
     return e;
 }
 
-// The vertical pass of either form: the scalar-tail quad of a level (at most
-// one lane per level) redoes it in FixedPtCast form under a lane mask.
-__device__ __forceinline__ uint32_t vert_any(bool tail, const uint32_t (&a)[4], const uint32_t (&b)[4], uint32_t bp) {
-    uint32_t o = vert_simd(a, b, bp, bp >> 16);
-    if (tail) o = vert_tail(a, b, bp & 0xFFFFu, bp >> 16);
-    return o;
-}
-
 // Both quads' horizontal passes of one source row.
 struct HRow {
     uint32_t a[4], b[4];
@@ -174,8 +177,14 @@ __device__ __forceinline__ void hrow2(HRow& h, const uint8_t* lds, const TickEnt
     hrow(h.b, lds, e.tb, row);
 }
 
-__device__ __forceinline__ uint2 vert2(const TickEnt& e, const HRow& p, const HRow& q, uint32_t bp) {
-    return uint2{vert_any(e.tail & 1, p.a, q.a, bp), vert_any(e.tail & 2, p.b, q.b, bp)};
+// Vertical pass of both quads.  A level's scalar-tail quad (the last quad of
+// a row when w is not a multiple of 16: FixedPtCast form) is always quad B of
+// its oct, and those octs fill waves of their own (plan_pyramid), so TAIL is
+// wave-uniform and no lane evaluates both forms.
+template <bool TAIL>
+__device__ __forceinline__ uint2 vert2(const HRow& p, const HRow& q, uint32_t bp) {
+    return uint2{vert_simd(p.a, q.a, bp, bp >> 16),
+                 TAIL ? vert_tail(p.b, q.b, bp & 0xFFFFu, bp >> 16) : vert_simd(p.b, q.b, bp, bp >> 16)};
 }
 
 // The rows [ra, rb) of one entry at one tick.  rec[y] = (LDS offset / 16 of
@@ -184,6 +193,7 @@ __device__ __forceinline__ uint2 vert2(const TickEnt& e, const HRow& p, const HR
 // rows share source rows (~1.2x downscale), so the last source row's sums stay
 // in registers (~1.2 horizontal passes per output row); two rows per step
 // with the roles of P and Q swapped, so the carried row needs no moves.
+template <bool TAIL>
 __device__ __forceinline__ void tick_rows(const uint8_t* __restrict__ lds, uint8_t* __restrict__ ldsw,
                                           const int2* __restrict__ rec, const TickEnt& e, int ra, int rb, int d,
                                           uint8_t* __restrict__ pyr) {
@@ -200,12 +210,14 @@ __device__ __forceinline__ void tick_rows(const uint8_t* __restrict__ lds, uint8
         const int2 r0 = rec[y], r1 = rec[y + 1];
         const int a0 = (r0.x & 0xFFFF) << 4, a1 = (int)((uint32_t)r0.x >> 16) << 4;
         const int c0 = (r1.x & 0xFFFF) << 4, c1 = (int)((uint32_t)r1.x >> 16) << 4;
-        if (a0 != cur) hrow2(P, lds, e, a0);
+        // the tail wave's lanes belong to different levels: no carried-row
+        // branch there (it would diverge)
+        if (TAIL || a0 != cur) hrow2(P, lds, e, a0);
         hrow2(Q, lds, e, a1);
-        const uint2 o0 = vert2(e, P, Q, (uint32_t)r0.y);
-        if (c0 != a1) hrow2(Q, lds, e, c0);
+        const uint2 o0 = vert2<TAIL>(P, Q, (uint32_t)r0.y);
+        if (TAIL || c0 != a1) hrow2(Q, lds, e, c0);
         hrow2(P, lds, e, c1);
-        const uint2 o1 = vert2(e, Q, P, (uint32_t)r1.y);
+        const uint2 o1 = vert2<TAIL>(Q, P, (uint32_t)r1.y);
         cur = c1;
         *reinterpret_cast<uint2*>(ldsw + d) = o0;
         advance();
@@ -218,22 +230,25 @@ __device__ __forceinline__ void tick_rows(const uint8_t* __restrict__ lds, uint8
     if (y < rb) {
         const int2 r0 = rec[y];
         const int a0 = (r0.x & 0xFFFF) << 4, a1 = (int)((uint32_t)r0.x >> 16) << 4;
-        if (a0 != cur) hrow2(P, lds, e, a0);
+        if (TAIL || a0 != cur) hrow2(P, lds, e, a0);
         hrow2(Q, lds, e, a1);
-        const uint2 o0 = vert2(e, P, Q, (uint32_t)r0.y);
+        const uint2 o0 = vert2<TAIL>(P, Q, (uint32_t)r0.y);
         *reinterpret_cast<uint2*>(ldsw + d) = o0;
         *reinterpret_cast<uint2*>(pyr + hp) = o0;
     }
 }
 
+// One entry at one tick: its row run from the packed range (row ra: 11
+// bits, row count: 5, LDS slot of row ra / 16: 16).
+template <bool TAIL>
 __device__ __forceinline__ void tick_entry(const uint8_t* __restrict__ lds, uint8_t* __restrict__ ldsw,
-                                           const int2* __restrict__ s_tab, const int2* __restrict__ rng,
+                                           const int2* __restrict__ s_tab, const uint32_t* __restrict__ rng,
                                            const TickEnt& e, uint8_t* __restrict__ pyr) {
-    const int2 r = rng[e.rng];
-    const int ra = r.x & 0xFFFF, rb = (int)((uint32_t)r.x >> 16);
-    if (ra >= rb) return;
+    const uint32_t r = rng[e.rng];
+    const int ra = (int)(r & 0x7FFu), n = (int)((r >> 11) & 31u);
+    if (n == 0) return;
     // ldsw + 8o: the entry's column within its ring rows (hoff has it for HBM)
-    tick_rows(lds, ldsw + e.col8, s_tab + e.rec, e, ra, rb, r.y, pyr);
+    tick_rows<TAIL>(lds, ldsw + e.col8, s_tab + e.rec, e, ra, ra + n, (int)(r >> 16) << 4, pyr);
 }
 
 // Producer waves: level-0 chunk c (rows [c T0, c T0 + T0)) -> its run of
@@ -299,7 +314,7 @@ __device__ __forceinline__ void pyr_producer(const Geom& g, const uint8_t* __res
 }
 
 template <int E, int NP>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(E == 1 ? 8 : 4))) void pyramid_tick_kernel(Geom g, const int4* __restrict__ ents,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(ORBGPU_PYR_WAVES_EU))) void pyramid_tick_kernel(Geom g, const int4* __restrict__ ents,
                                                             const int2* __restrict__ tab,
                                                             const uint8_t* __restrict__ img0, size_t row0,
                                                             size_t frame0, uint8_t* __restrict__ pyr) {
@@ -308,6 +323,17 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(E == 1 ? 8
     const int tid = threadIdx.x;
     const int f = blockIdx.x;
     const int nthr = g.tk_threads;
+#ifdef PYR_STAMPS
+    PYR_BLOCK(0, __builtin_amdgcn_s_memrealtime());
+    PYR_BLOCK(2, __builtin_amdgcn_s_memtime());
+    {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        PYR_BLOCK(4, hw);
+        PYR_BLOCK(5, xcc);
+    }
+#endif
     for (int i = tid; i < g.tk_tab_n; i += nthr) s_tab[i] = tab[i];
     const int K = g.tk_ticks;
     const int CL = 64 * g.tk_cwaves;
@@ -320,15 +346,27 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(E == 1 ? 8
 #pragma unroll
     for (int e = 0; e < E; ++e) en[e] = load_ent(ents + (size_t)(e * CL + tid) * 9, f);
     __syncthreads();
-    const int2* rng = s_tab + g.tk_rng;
+    const uint32_t* rng = reinterpret_cast<const uint32_t*>(s_tab) + g.tk_rng;
+    // entries whose quad B is a scalar-tail quad fill whole waves (per entry
+    // slot), so the form is wave-uniform
+    bool tail[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) tail[e] = __builtin_amdgcn_ballot_w64(en[e].tail != 0) != 0;
     for (int k = 0; k < K; ++k) {
         if (tid < 64) PYR_STAMP(k, 15);
 #pragma unroll
-        for (int e = 0; e < E; ++e) tick_entry(s_mem, s_mem, s_tab, rng, en[e], pyr);
+        for (int e = 0; e < E; ++e) {
+            if (tail[e])
+                tick_entry<true>(s_mem, s_mem, s_tab, rng, en[e], pyr);
+            else
+                tick_entry<false>(s_mem, s_mem, s_tab, rng, en[e], pyr);
+        }
         PYR_STAMP(k, tid >> 6);
         rng += g.tk_rs;
         __syncthreads();
     }
+    PYR_BLOCK(1, __builtin_amdgcn_s_memrealtime());
+    PYR_BLOCK(3, __builtin_amdgcn_s_memtime());
 }
 
 template <int E>
@@ -351,7 +389,8 @@ hipError_t launch_e(const Geom& g, int batch, const int4* ents, const int2* tab,
 }  // namespace
 
 #ifdef PYR_STAMPS
-extern "C" int orbgpu_debug_pyr_stamps(unsigned long long* out) {
+extern "C" int orbgpu_debug_pyr_stamps(unsigned long long* out, unsigned long long* blocks) {
+    if (blocks && hipMemcpyFromSymbol(blocks, HIP_SYMBOL(g_pyr_blocks), sizeof(g_pyr_blocks)) != hipSuccess) return -2;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pyr_stamps), sizeof(g_pyr_stamps)) == hipSuccess ? 0 : -2;
 }
 #endif

@@ -35,7 +35,7 @@ namespace {
 #define ORBGPU_PYR_T0 8  // level-0 rows per chunk (per tick)
 #endif
 #ifndef ORBGPU_PYR_LANES
-#define ORBGPU_PYR_LANES 1024  // compute lanes the row-group split may use
+#define ORBGPU_PYR_LANES 576  // compute lanes the row-group split may use (9 waves + the tail wave + the producer: two blocks per CU)
 #endif
 
 inline int round_up(int v, int a) { return (v + a - 1) / a * a; }
@@ -117,15 +117,20 @@ int plan_pyramid(Geom& g, const std::vector<int2>& ytab, const std::vector<int4>
     // beside them).
     const int v4p = (g.lv[0].w + 15) / 16, pwaves = (T0 * v4p + 511) / 512;
     const int lane_budget = std::min(ORBGPU_PYR_LANES, 1024 - 64 * pwaves);
-    std::vector<int> G(L, 1), mx(L, 0), octs(L, 0);
+    std::vector<int> G(L, 1), mx(L, 0), octs(L, 0), tailq(L, 0);
     for (int l = 1; l < L; ++l) {
         for (int k = 0; k < K; ++k) mx[l] = std::max(mx[l], p[k + 1][l] - p[k][l]);
-        octs[l] = ((g.lv[l].w + 3) / 4 + 1) / 2;
+        const int Q = (g.lv[l].w + 3) / 4;
+        tailq[l] = g.lv[l].qmain < Q ? 1 : 0;
+        octs[l] = (Q - tailq[l] + 1) / 2;  // regular octs (the column entries below)
     }
-    auto lanes = [&]() {
-        int n = 0;
-        for (int l = 1; l < L; ++l) n += octs[l] * G[l];
-        return n;
+    auto lanes = [&]() {  // regular octs, then the tail octs from a wave boundary
+        int n = 0, t = 0;
+        for (int l = 1; l < L; ++l) {
+            n += octs[l] * G[l];
+            t += tailq[l];
+        }
+        return round_up(n, 64) + (t ? 64 : 0);
     };
     for (;;) {
         int worst = 1;
@@ -139,10 +144,29 @@ int plan_pyramid(Geom& g, const std::vector<int2>& ytab, const std::vector<int4>
             break;
         }
     }
-    int Gmax = 1;
-    for (int l = 1; l < L; ++l) Gmax = std::max(Gmax, G[l]);
-    g.tk_groups = Gmax;
-    g.tk_rs = (L - 1) * Gmax + 1;
+    // The tail octs (one wave of their own, below) split their level's rows
+    // as finely as that wave allows: about one row per lane per tick.
+    std::vector<int> GT(L, 0);
+    int nt = 0;
+    for (int l = 1; l < L; ++l) nt += (GT[l] = tailq[l] ? std::max(1, mx[l]) : 0);
+    while (nt > 64) {
+        int big = 1;
+        for (int l = 2; l < L; ++l)
+            if (GT[l] > GT[big]) big = l;
+        --GT[big];
+        --nt;
+    }
+    // range slots per tick: level l's regular groups, then its tail groups
+    std::vector<int> base_r(L, 0), base_t(L, 0);
+    int slots = 0;
+    for (int l = 1; l < L; ++l) {
+        base_r[l] = slots;
+        slots += G[l];
+        base_t[l] = slots;
+        slots += GT[l];
+    }
+    g.tk_groups = slots;
+    g.tk_rs = slots + 1;  // + the empty range of idle lanes
 
     // --- producer: LDS-DMA pieces of 16 B (one per lane), at most 8 per lane
     const int v4 = (g.lv[0].w + 15) / 16, items = T0 * v4;
@@ -184,34 +208,55 @@ int plan_pyramid(Geom& g, const std::vector<int2>& ytab, const std::vector<int4>
     // the kernel reads one record past a tick's last row (the second row of a
     // step at an odd end, discarded): it must hold a valid LDS offset
     for (int i = 0; i < 4; ++i) tab.push_back(int2{16 >> 4, 0});
-    g.tk_rng = (int)tab.size();
+    g.tk_rng = (int)tab.size() * 2;  // u32 index of the range table
+    std::vector<uint32_t> rng;
     for (int k = 0; k < K; ++k) {
-        for (int l = 1; l < L; ++l) {
-            const int a = p[k][l], b = p[k + 1][l], per = (b - a + G[l] - 1) / G[l];
-            for (int gi = 0; gi < Gmax; ++gi) {
-                int ra = std::min(a + gi * per, b), rb = std::min(ra + per, b);
-                if (gi >= G[l]) ra = rb = 0;
-                const int d = l + 1 < L ? slot_offset(g, l, ra) : sink;
-                tab.push_back(int2{ra | (rb << 16), d});
+        for (int l = 1; l < L; ++l)
+            for (const int n : {G[l], GT[l]}) {  // split the tick's rows into n contiguous runs
+                const int a = p[k][l], b = p[k + 1][l], per = n ? (b - a + n - 1) / n : 0;
+                for (int gi = 0; gi < n; ++gi) {
+                    const int ra = std::min(a + gi * per, b), rb = std::min(ra + per, b);
+                    const int d = l + 1 < L ? slot_offset(g, l, ra) : sink;
+                    if (ra >= 2048 || rb - ra > 31 || (d >> 4) >= 65536)
+                        return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid range does not fit its packing");
+                    rng.push_back((uint32_t)ra | (uint32_t)(rb - ra) << 11 | (uint32_t)(d >> 4) << 16);
+                }
             }
-        }
-        tab.push_back(int2{0, sink});  // the empty range of idle lanes
+        rng.push_back((uint32_t)(sink >> 4) << 16);  // the empty range of idle lanes
     }
+    // ranges packed one per u32: row ra (11 bits) | row count (5) | LDS slot of row ra / 16 (16)
+    if (rng.size() & 1) rng.push_back(0);
+    for (size_t i = 0; i < rng.size(); i += 2) tab.push_back(int2{(int)rng[i], (int)rng[i + 1]});
     g.tk_tab_n = (int)tab.size();
     g.tk_lds_bytes = g.tk_lds_tab + 8 * g.tk_tab_n;
     if (g.tk_lds_bytes > 160 * 1024) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid plan exceeds 160 KiB of LDS");
 
-    // --- column entries: (level, group, oct) in level order, an oct = quads
-    // 2o and 2o+1 (8 pixels; a level with an odd quad count repeats its last
-    // quad's taps in the missing one, whose bytes land in the row padding).
-    // A wave holds one or two levels; a level's scalar-tail quad stays with
-    // its level (the kernel redoes that quad's vertical pass in the tail form
-    // under a lane mask).
-    struct Ent { int l, gi, o; };
-    std::vector<Ent> ents;
-    for (int l = 1; l < L; ++l)
-        for (int gi = 0; gi < G[l]; ++gi)
-            for (int o = 0; o < octs[l]; ++o) ents.push_back(Ent{l, gi, o});
+    // --- column entries: (level, group, oct) in level order.  An oct is two
+    // adjacent quads (8 pixels), always two real ones: a level with a
+    // scalar-tail quad (the last quad, when w is not a multiple of 16) gets
+    // the tail oct (Q-2, Q-1), whose quad B is the tail, and regular octs
+    // (2o, 2o+1) over quads 0..Q-2; a level without one, over 0..Q-1.  An odd
+    // count ends with the oct (last-1, last), which overlaps its neighbour
+    // (both lanes write the same bytes).  The tail octs go last, from a wave
+    // boundary, so the kernel's vertical-pass form is wave-uniform.
+    struct Ent { int l, gi, qa, qb; };
+    std::vector<Ent> ents, tails;
+    for (int l = 1; l < L; ++l) {
+        const int Q = (g.lv[l].w + 3) / 4;
+        const bool has_tail = g.lv[l].qmain < Q;
+        const int last = has_tail ? Q - 2 : Q - 1;  // last quad of the regular octs
+        for (int gi = 0; gi < G[l]; ++gi) {
+            for (int qa = 0; qa <= last; qa += 2) {
+                const int a = std::min(qa, last - 1);
+                ents.push_back(Ent{l, gi, a, a + 1});
+            }
+        }
+        if (has_tail)
+            for (int gi = 0; gi < GT[l]; ++gi) tails.push_back(Ent{l, -1 - gi, Q - 2, Q - 1});  // gi < 0: tail groups
+    }
+    if (tails.size() > 64) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid: more than 64 scalar-tail columns");
+    while (!tails.empty() && ents.size() % 64 != 0) ents.push_back(Ent{0, 0, 0, 0});  // padding lanes
+    ents.insert(ents.end(), tails.begin(), tails.end());
     const int n = (int)ents.size();
     const int cmax = 1024 - 64 * g.tk_pwaves;
     const int E = n <= cmax ? 1 : 2;
@@ -228,22 +273,29 @@ int plan_pyramid(Geom& g, const std::vector<int2>& ytab, const std::vector<int4>
     for (int i = 0; i < CL * E; ++i) {
         int4* r = &plan.ent[(size_t)i * 9];
         if (i >= n) {
-            r[0] = int4{(L - 1) * Gmax, 0, 0, 0};  // empty range
+            r[0] = int4{slots, 0, 0, 0};  // empty range
             r[1] = int4{sink, -1, 0, 0};
             continue;
         }
         const Ent& en = ents[(size_t)i];
+        if (en.l == 0) {  // padding before the tail wave
+            r[0] = int4{slots, 0, 0, 0};
+            r[1] = int4{sink, -1, 0, 0};
+            continue;
+        }
         const LevelGeom& v = g.lv[en.l];
         const bool last = en.l + 1 == L;
-        const int quads = (v.w + 3) / 4, qa = 2 * en.o, qb = std::min(2 * en.o + 1, quads - 1);
-        const int tail = (qa >= v.qmain ? 1 : 0) | (qb >= v.qmain ? 2 : 0);
-        r[0] = int4{(en.l - 1) * Gmax + en.gi, tail, v.tk_rec, last ? 0 : v.tk_pitch};
+        const int qa = en.qa, qb = en.qb;
+        if (qa < 0 || qb != qa + 1) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid: oct layout");
+        const int tail = qb >= v.qmain ? 2 : 0;  // quad A is never a tail quad
+        const int slot = en.gi >= 0 ? base_r[en.l] + en.gi : base_t[en.l] + (-1 - en.gi);
+        r[0] = int4{slot, tail, v.tk_rec, last ? 0 : v.tk_pitch};
         r[1] = int4{last ? sink : v.tk_ring, last ? -1 : v.tk_ring + v.tk_ring_rows * v.tk_pitch, v.pitch,
                     (int)v.frame_bytes};
-        const uint64_t o = (uint64_t)v.offset + 8u * (uint64_t)en.o;
+        const uint64_t o = (uint64_t)v.offset + 4u * (uint64_t)qa;
         if (o + (uint64_t)v.frame_bytes * (uint64_t)max_batch >= (1ull << 32))
             return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid buffer beyond 4 GiB (32-bit store offsets)");
-        r[2] = int4{(int)(uint32_t)o, 0, 8 * en.o, 0};
+        r[2] = int4{(int)(uint32_t)o, 0, 4 * qa, en.l};
         const int4* ta = &ptab[(size_t)v.ptab_offset + 3 * (size_t)qa];
         const int4* tb = &ptab[(size_t)v.ptab_offset + 3 * (size_t)qb];
         for (int j = 0; j < 3; ++j) {
@@ -314,13 +366,13 @@ int emulate_pyramid(const Geom& g, const std::vector<int2>& ytab, const PyrPlan&
         for (int lane = 0; lane < CL; ++lane)
             for (int e = 0; e < E; ++e) {
                 const int4* r = &plan.ent[((size_t)e * CL + lane) * 9];
-                const int2 rg = tab[g.tk_rng + k * g.tk_rs + r[0].x];
-                const int ra = rg.x & 0xFFFF, rb = (int)((uint32_t)rg.x >> 16);
+                const uint32_t rg = reinterpret_cast<const uint32_t*>(tab)[g.tk_rng + k * g.tk_rs + r[0].x];
+                const int ra = (int)(rg & 0x7FF), rb = ra + (int)((rg >> 11) & 31);
                 if (ra >= rb) continue;
-                const int l = 1 + r[0].x / g.tk_groups;
+                const int l = r[2].w;
                 const LevelGeom& v = g.lv[l];
                 const int q0 = r[2].z / 4;  // quads q0, q0 + 1
-                int d = rg.y;
+                int d = (int)(rg >> 16) << 4;
                 for (int y = ra; y < rb; ++y) {
                     const int2 rec = tab[r[0].z + y];
                     const int offs[2] = {(rec.x & 0xFFFF) << 4, (int)((uint32_t)rec.x >> 16) << 4};

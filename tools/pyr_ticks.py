@@ -29,8 +29,21 @@ for _ in range(3):
 torch.cuda.synchronize()
 lib = orbgpu.lib()
 st = np.zeros(64 * 160 * 16, np.uint64)
-lib.orbgpu_debug_pyr_stamps.argtypes = [ctypes.c_void_p]
-assert lib.orbgpu_debug_pyr_stamps(st.ctypes.data) == 0
+bl = np.zeros(1024 * 6, np.uint64)
+lib.orbgpu_debug_pyr_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+assert lib.orbgpu_debug_pyr_stamps(st.ctypes.data, bl.ctypes.data) == 0
+bl = bl.reshape(1024, 6)[:B].astype(np.int64)
+rt0 = bl[:, 0].min()
+life_us = (bl[:, 1] - bl[:, 0]) / 100.0
+print("block lifetime us: mean %.1f min %.1f max %.1f; kernel span (first start..last end) %.1f us" %
+      (life_us.mean(), life_us.min(), life_us.max(), (bl[:, 1].max() - rt0) / 100.0))
+clk = (bl[:, 3] - bl[:, 2]) / np.maximum(1, bl[:, 1] - bl[:, 0]) * 100.0
+print("in-kernel clock MHz: median %.0f" % np.median(clk))
+starts = np.sort((bl[:, 0] - rt0) / 100.0)
+print("block start times us (every 32nd):", [round(x, 1) for x in starts[::32]])
+cu = (bl[:, 5] & 0xF) * 1000 + ((bl[:, 4] >> 13) & 0x7) * 100 + ((bl[:, 4] >> 8) & 0xF) + ((bl[:, 4] >> 12) & 1) * 16
+u, c = np.unique(cu, return_counts=True)
+print("distinct CUs used:", len(u), "blocks per CU histogram:", np.bincount(c).tolist())
 st = st.reshape(64, 160, 16).astype(np.int64)
 _, info = orbgpu.pyramid_plan_emulate(np.zeros((H, W), np.uint8), 1000, 1.2, 8)
 K = info["ticks"]
