@@ -348,10 +348,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(ORBGPU_PYR
     __syncthreads();
     const uint32_t* rng = reinterpret_cast<const uint32_t*>(s_tab) + g.tk_rng;
     // entries whose quad B is a scalar-tail quad fill whole waves (per entry
-    // slot), so the form is wave-uniform
+    // slot) from lane 0, padded with idle lanes, so lane 0 gives the wave's form
     bool tail[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) tail[e] = __builtin_amdgcn_ballot_w64(en[e].tail != 0) != 0;
+    for (int e = 0; e < E; ++e) tail[e] = __builtin_amdgcn_readfirstlane(en[e].tail) != 0;
     for (int k = 0; k < K; ++k) {
         if (tid < 64) PYR_STAMP(k, 15);
 #pragma unroll
