@@ -18,28 +18,6 @@ namespace orbgpu {
 
 namespace {
 
-#ifndef FAST_PROBE
-#define FAST_PROBE 0  // diagnostic build only (tools/pyr_variants.sh): 1 = per-phase cycle totals
-#endif
-#if FAST_PROBE
-__device__ unsigned long long g_fast_phase[16];
-#define FAST_CNT(i, n) do { if ((FAST_PROBE & 4) && lane == 0) atomicAdd(&g_fast_phase[i], (unsigned long long)(n)); } while (0)
-__device__ __forceinline__ unsigned long long fast_now() {
-    __builtin_amdgcn_sched_barrier(0);
-    unsigned long long t;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#define FAST_T(v) const unsigned long long v = fast_now()
-#define FAST_ACC(i, dt) do { if (lane == 0) atomicAdd(&g_fast_phase[i], (unsigned long long)(dt)); } while (0)
-#else
-#define FAST_T(v) ((void)0)
-#define FAST_ACC(i, dt) ((void)0)
-#define FAST_CNT(i, n) ((void)0)
-#endif
-
-
 __device__ inline bool has_run9(uint32_t m16) {
     uint32_t m = m16 | (m16 << 16);
     uint32_t r = m & (m >> 1);   // runs >= 2
@@ -158,13 +136,6 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
         nb = wave_append(corner, (uint16_t)off, T.lb, nb, lane);
     }
     wave_sync();
-    FAST_CNT(8, 1);
-    FAST_CNT(9, (dh + rstep - 1) / rstep);
-    FAST_CNT(10, (na + 63) / 64);
-    FAST_CNT(11, (nb + 63) / 64);
-    FAST_CNT(12, na);
-    FAST_CNT(13, nb);
-    FAST_CNT(14, dw * dh);
     for (int j = lane; j < nb; j += 64) {
         const int off = T.lb[j];
         const uint8_t* p = T.win + off;
@@ -271,7 +242,6 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
 
     // stage rows: dwords covering [xa, maxX), xa = iniX & ~3 (row pitch and
     // frame base are 16-byte aligned; maxX <= w - 16, so no over-read)
-    FAST_T(t0);
     const int xa = iniX & ~3, ox = iniX - xa;
     const int nd = (maxX - xa + 3) >> 2;
     const uint32_t mnd = (1u << 24) / (uint32_t)nd + 1u;
@@ -293,33 +263,20 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
             if (idx < nd * wh) *reinterpret_cast<uint32_t*>(s_win + r * P + 4 * q) = v[k];
         }
     }
-    FAST_T(t1);
     for (int idx = lane; idx < P * R / 4; idx += 64) reinterpret_cast<uint32_t*>(T.sc)[idx] = 0u;
     wave_sync();
-    FAST_T(t2);
 
     // detection region of cv::FAST on the window: rows [3, wh-3), cols [3, ww-3)
     const int dw = maxX - iniX - 6, dh = wh - 6;
     int total = 0;
     if (dw > 0 && dh > 0) {
         int nb = fast_corners<P>(T, dw, dh, ox, g.ini_th, lane);
-        FAST_T(t3);
         total = nms_emit<P>(T, nb, ox, g.ini_th, lane, iniX, iniY, out, L.cell_cap, err);
-        FAST_T(t4);
-        FAST_ACC(0, t1 - t0);
-        FAST_ACC(1, t2 - t1);
-        FAST_ACC(2, t3 - t2);
-        FAST_ACC(3, t4 - t3);
-        FAST_ACC(4, 1);
         if (total == 0) {  // ORBextractor.cpp:821-825: retry the cell at minThFAST
             for (int j = lane; j < nb; j += 64) T.sc[T.lb[j]] = 0;
             wave_sync();
-            FAST_T(t5);
             nb = fast_corners<P>(T, dw, dh, ox, g.min_th, lane);
             total = nms_emit<P>(T, nb, ox, g.min_th, lane, iniX, iniY, out, L.cell_cap, err);
-            FAST_T(t6);
-            FAST_ACC(5, t6 - t5);
-            FAST_ACC(6, 1);
         }
     }
     if (lane == 0) *cnt_out = min(total, L.cell_cap);
@@ -327,11 +284,6 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
 
 }  // namespace
 
-#if FAST_PROBE
-extern "C" int orbgpu_debug_fast_phases(unsigned long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fast_phase), 16 * sizeof(unsigned long long)) == hipSuccess ? 0 : -2;
-}
-#endif
 
 hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                              const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err,
