@@ -92,25 +92,37 @@ template <int P>
 __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, int lane) {
     // compass pre-test, row-major over the detection region: 32 lanes per
     // row when it fits (two rows per pass), else 64 (dw <= 64: host check).
-    // The tests are lane masks (v_cmp -> SGPR) combined with scalar logic.
     const int lpr = dw > 32 ? 64 : 32;
     const int rsub = lpr == 32 ? lane >> 5 : 0, col = lane & (lpr - 1);
     const int rstep = 64 / lpr;
-    int na = 0;
-    for (int rr = 0; rr < dh; rr += rstep) {
-        const int r = rr + rsub;
-        const int off = (3 + r) * P + 3 + ox + col;
-        const uint8_t* p = T.win + off;  // rows/cols past the region stay inside LDS: masked below
-        const int v = p[0], lo = v - t, hi = v + t;
+    // Two passes per iteration: all ten compass loads are issued before
+    // either pass is evaluated (rows past the region read the rest of the
+    // wave's LDS area and are masked).
+    auto compass = [&](const uint8_t* p, int t) {
+        const int v = p[0];
         const int c0 = p[3 * P], c4 = p[3], c8 = p[-3 * P], c12 = p[-3];
-        typedef unsigned long long u64;
-        const u64 D0 = __ballot(c0 < lo), D4 = __ballot(c4 < lo), D8 = __ballot(c8 < lo), D12 = __ballot(c12 < lo);
-        const u64 B0 = __ballot(c0 > hi), B4 = __ballot(c4 > hi), B8 = __ballot(c8 > hi), B12 = __ballot(c12 > hi);
-        const u64 IN = __ballot((r < dh) & (col < dw));
-        const u64 PASS = IN & ((D0 & D4) | (D4 & D8) | (D8 & D12) | (D12 & D0) | (B0 & B4) | (B4 & B8) |
-                               (B8 & B12) | (B12 & B0));
-        if ((PASS >> lane) & 1ull) T.la[na + __popcll(PASS & ((1ull << lane) - 1ull))] = (uint16_t)off;
-        na += __popcll(PASS);
+        // two adjacent compass points both darker than v - t <=> the smallest
+        // pairwise max is; both brighter than v + t <=> the largest pairwise
+        // min is (VALU min/max instead of eight lane masks combined on the SALU)
+        const int dark = min(min(max(c0, c4), max(c4, c8)), min(max(c8, c12), max(c12, c0)));
+        const int bright = max(max(min(c0, c4), min(c4, c8)), max(min(c8, c12), min(c12, c0)));
+        return (dark < v - t) | (bright > v + t);
+    };
+    auto below = [&](unsigned long long m) {  // set bits of m in lanes below this one
+        return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    };
+    const bool incol = col < dw;
+    int na = 0;
+    for (int rr = 0; rr < dh; rr += 2 * rstep) {
+        const int r0 = rr + rsub, r1 = r0 + rstep;
+        const int off0 = (3 + r0) * P + 3 + ox + col, off1 = off0 + rstep * P;
+        const bool pass0 = incol & (r0 < dh) & compass(T.win + off0, t);
+        const bool pass1 = incol & (r1 < dh) & compass(T.win + off1, t);
+        const unsigned long long m0 = __ballot(pass0), m1 = __ballot(pass1);
+        if (pass0) T.la[na + below(m0)] = (uint16_t)off0;
+        na += __popcll(m0);
+        if (pass1) T.la[na + below(m1)] = (uint16_t)off1;
+        na += __popcll(m1);
     }
     wave_sync();
     const int ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
