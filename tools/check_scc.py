@@ -7,7 +7,8 @@ wrote -- so the select takes a stale SCC from an earlier scalar op
 (reproducer: tools/scc_repro.hip).  This script scans device assembly
 (`hipcc -S --cuda-device-only`) and reports every s_cselect / s_cbranch_scc*
 whose nearest preceding definition of SCC-or-VCC in the same basic block is
-a VALU compare into VCC, unless the SCC the consumer actually reads was set
+a VALU compare into VCC, unless the compare's VCC is read by an instruction before the consumer
+(then the compare has its own user), or the SCC the consumer actually reads was set
 in that block by `s_and_b64 s, vcc, exec` -- the compiler's uniform lowering
 of an earlier compare (a later v_cmp into VCC for another purpose may sit
 in between).  build() runs it over every kernel and fails the build on a
@@ -27,6 +28,19 @@ CONSUMER = re.compile(r"^\s*(s_cselect_b(32|64)|s_cbranch_scc[01])\b")
 LABEL = re.compile(r"^\S+:")
 
 
+def vcc_read(lines, lo, hi):
+    """True when an instruction in lines[lo:hi] reads VCC (v_cndmask, s_and, ...): the compare
+    then feeds that reader, and the SCC consumer's flag comes from an earlier scalar op."""
+    for k in range(lo, hi):
+        ins = lines[k].strip()
+        if ins.startswith(";") or VCC_CMP.match(ins):
+            continue
+        ops = ins.split(None, 1)
+        if len(ops) == 2 and re.search(r"\bvcc\b", ops[1].split(",", 1)[1] if "," in ops[1] else ""):
+            return True
+    return False
+
+
 def scan(lines):
     hits = []
     for i, line in enumerate(lines):
@@ -44,7 +58,7 @@ def scan(lines):
                     hits.append((i + 1, line.strip(), cmp_at + 1, lines[cmp_at].strip()))
                 cmp_at = None
                 break
-            if VCC_CMP.match(prev) and cmp_at is None:
+            if VCC_CMP.match(prev) and cmp_at is None and not vcc_read(lines, j + 1, i):
                 cmp_at = j
         if cmp_at is not None:  # reached the block start: SCC comes from another block
             hits.append((i + 1, line.strip(), cmp_at + 1, lines[cmp_at].strip()))
