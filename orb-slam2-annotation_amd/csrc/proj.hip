@@ -3,7 +3,7 @@
 //
 // One 1024-thread block per call (proj_kernel, below): the target's feature
 // grid in LDS, every point's projection and candidate list built by 15
-// waves in parallel (8 lanes per point), the reference's sequential point
+// waves in parallel (4 lanes per point), the reference's sequential point
 // walk (an assignment hides a keypoint from later points) replayed by one
 // wave from those lists, then the rotation-consistency cull.  Candidate keys (Hamming distance <<
 // 20 | grid position) reproduce the reference's first-best-in-order choice.
@@ -52,6 +52,8 @@ __device__ inline int predict_scale(float max_dist, float dist, const orbgpu_pro
 // one point's search parameters after projection
 struct Query {
     bool ok;
+    int flags;           // the point's ORBGPU_PT_* flags
+    float angle;         // its descriptor angle (rotation-checked variants)
     float u, v, r;       // window centre and half-size
     int min_level, max_level;
     float ur;            // stereo: projected right coordinate (LOCAL, LAST_FRAME)
@@ -97,32 +99,52 @@ __device__ inline CallPose call_pose(const orbgpu_proj_call& C) {
 }
 
 // The reference's per-point projection and window for the call's variant.
-__device__ inline Query make_query(const orbgpu_proj_call& C, const CallPose& cp, int ip) {
+// Every point field the variant reads is loaded up front, independent of the
+// flags, so a point costs one memory latency; sf = the target's scale
+// factors (16 entries, in LDS).
+__device__ inline Query make_query(const orbgpu_proj_call& C, const CallPose& cp, const float* sf, int ip) {
     const orbgpu_proj_target& T = C.target;
     const orbgpu_proj_points& P = C.points;
+    const int variant = C.variant;
     const int fl = P.flags[ip];
+    float X[3] = {0.f, 0.f, 0.f}, tr[4] = {0.f, 0.f, 0.f, 0.f}, Pn[3] = {0.f, 0.f, 0.f};
+    float maxd0 = 0.f, mind0 = 0.f;
+    int lv = 0;
+    if (variant == ORBGPU_PROJ_LOCAL) {
+        for (int k = 0; k < 4; ++k) tr[k] = P.track[4 * ip + k];
+        lv = P.track_level[ip];
+    } else {
+        for (int k = 0; k < 3; ++k) X[k] = P.pos[3 * ip + k];
+        if (variant != ORBGPU_PROJ_LAST_FRAME) {
+            maxd0 = P.max_dist[ip];
+            mind0 = P.min_dist[ip];
+        }
+        if (variant == ORBGPU_PROJ_SIM3)
+            for (int k = 0; k < 3; ++k) Pn[k] = P.normal[3 * ip + k];
+        if (variant == ORBGPU_PROJ_LAST_FRAME) lv = P.octave[ip];
+    }
     Query q{};
+    if (C.check_ori && variant != ORBGPU_PROJ_LOCAL && variant != ORBGPU_PROJ_SIM3) q.angle = P.angle[ip];
+    q.flags = fl;
     q.ok = (fl & ORBGPU_PT_VALID) != 0;
-    if (C.variant == ORBGPU_PROJ_LOCAL) {  // ORBmatcher.cpp:68-91
+    if (variant == ORBGPU_PROJ_LOCAL) {  // ORBmatcher.cpp:68-91
         q.ok = q.ok && (fl & ORBGPU_PT_IN_VIEW);
         if (q.ok) {
-            const int lvl = P.track_level[ip];
-            float r = (double)P.track[4 * ip + 3] > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos: double literal
+            float r = (double)tr[3] > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos: double literal
             if (C.th != 1.0f) r *= C.th;
-            q.u = P.track[4 * ip];
-            q.v = P.track[4 * ip + 1];
-            q.r = r * T.scale_factors[lvl];
-            q.min_level = lvl - 1;
-            q.max_level = lvl;
+            q.u = tr[0];
+            q.v = tr[1];
+            q.r = r * sf[lv & 15];  // track level validated on the host (0..n_levels-1)
+            q.min_level = lv - 1;
+            q.max_level = lv;
             q.stereo = true;
-            q.ur = P.track[4 * ip + 2];
+            q.ur = tr[2];
             q.stereo_r = q.r;
             q.level_lo = -1000;
             q.level_hi = 1000;
         }
-    } else if (C.variant == ORBGPU_PROJ_SIM3) {  // ORBmatcher.cpp:376-420
+    } else if (variant == ORBGPU_PROJ_SIM3) {  // ORBmatcher.cpp:376-420
         if (q.ok) {
-            const float* X = P.pos + 3 * ip;
             float pc[3];
             transform(cp.Rs, X, pc);
             if (pc[2] < 0.0f) q.ok = false;
@@ -134,17 +156,16 @@ __device__ inline Query make_query(const orbgpu_proj_call& C, const CallPose& cp
                 if (!(q.u >= T.min_x && q.u < T.max_x && q.v >= T.min_y && q.v < T.max_y)) q.ok = false;  // IsInImage
             }
             if (q.ok) {
-                const float maxd = 1.2f * P.max_dist[ip], mind = 0.8f * P.min_dist[ip];
+                const float maxd = 1.2f * maxd0, mind = 0.8f * mind0;
                 const float PO[3] = {X[0] - cp.O[0], X[1] - cp.O[1], X[2] - cp.O[2]};
                 const float dist = (float)sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
                 if (dist < mind || dist > maxd) q.ok = false;
                 else {
-                    const float* Pn = P.normal + 3 * ip;
                     const double dot = (double)PO[0] * Pn[0] + (double)PO[1] * Pn[1] + (double)PO[2] * Pn[2];
                     if (dot < 0.5 * dist) q.ok = false;
                     else {
-                        const int lvl = predict_scale(P.max_dist[ip], dist, T);
-                        q.r = C.th * T.scale_factors[lvl];
+                        const int lvl = predict_scale(maxd0, dist, T);
+                        q.r = C.th * sf[lvl];
                         q.min_level = -1;
                         q.max_level = -1;
                         q.stereo = false;
@@ -156,17 +177,16 @@ __device__ inline Query make_query(const orbgpu_proj_call& C, const CallPose& cp
         }
     } else {  // LAST_FRAME (ORBmatcher.cpp:1536-1571), KEYFRAME (:1683-1713)
         if (q.ok) {
-            const float* X = P.pos + 3 * ip;
             float pc[3];
             transform(T.Tcw, X, pc);
             const float invzc = (float)(1.0 / (double)pc[2]);
-            if (C.variant == ORBGPU_PROJ_LAST_FRAME && invzc < 0) q.ok = false;
+            if (variant == ORBGPU_PROJ_LAST_FRAME && invzc < 0) q.ok = false;
             q.u = T.fx * pc[0] * invzc + T.cx;
             q.v = T.fy * pc[1] * invzc + T.cy;
             if (q.u < T.min_x || q.u > T.max_x || q.v < T.min_y || q.v > T.max_y) q.ok = false;
-            if (q.ok && C.variant == ORBGPU_PROJ_LAST_FRAME) {
-                const int o = P.octave[ip];
-                q.r = C.th * T.scale_factors[o];
+            if (q.ok && variant == ORBGPU_PROJ_LAST_FRAME) {
+                const int o = lv;  // source octave validated on the host (0..n_levels-1)
+                q.r = C.th * sf[o & 15];
                 if (cp.forward) { q.min_level = o; q.max_level = -1; }
                 else if (cp.backward) { q.min_level = 0; q.max_level = o; }
                 else { q.min_level = o - 1; q.max_level = o + 1; }
@@ -178,11 +198,11 @@ __device__ inline Query make_query(const orbgpu_proj_call& C, const CallPose& cp
             } else if (q.ok) {
                 const float PO[3] = {X[0] - cp.O[0], X[1] - cp.O[1], X[2] - cp.O[2]};
                 const float dist3D = (float)sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
-                const float maxd = 1.2f * P.max_dist[ip], mind = 0.8f * P.min_dist[ip];
+                const float maxd = 1.2f * maxd0, mind = 0.8f * mind0;
                 if (dist3D < mind || dist3D > maxd) q.ok = false;
                 else {
-                    const int lvl = predict_scale(P.max_dist[ip], dist3D, T);
-                    q.r = C.th * T.scale_factors[lvl];
+                    const int lvl = predict_scale(maxd0, dist3D, T);
+                    q.r = C.th * sf[lvl];
                     q.min_level = lvl - 1;
                     q.max_level = lvl + 1;
                     q.stereo = false;
@@ -203,24 +223,34 @@ __device__ inline int hidden_min(int variant) {
     return (variant == ORBGPU_PROJ_LOCAL || variant == ORBGPU_PROJ_LAST_FRAME) ? 2 : 1;
 }
 
-// The target's feature grid in LDS: keypoint slots sorted by cell, the first
-// sorted position of every cell, and the fields a window test reads, stored
-// in sorted order so a scan touches HBM only for the 32-byte descriptors.
+// The target's feature grid in LDS: the first sorted position of every
+// cell, the fields a window test reads stored by sorted position, the hidden
+// set, and -- for targets of up to kDescLds keypoints -- the descriptors, so a
+// window scan does not touch HBM at all.
 struct Grid {
-    const unsigned* sorted;           // cell << 12 | slot
+    const float4* kp;                 // by sorted position: x, y, u_right (-1 without stereo), slot | octave << 16
     const unsigned short* cell_start;
     const unsigned* hidw;             // hidden-slot bitmap: slot i is bit i & 31 of word i >> 5
-    const float* kx;                  // by sorted position
-    const float* ky;
-    const int* koct;
-    const float* kur;                 // u_right, -1 without stereo
+    const uint4* desc;                // by slot, 2 x 16 bytes (LDS copy or the target's HBM array)
 };
 
+__device__ inline int kp_slot(const float4& k) { return (int)(__float_as_uint(k.w) & 0xFFFu); }
+// octave clamped to int16: exact for every test made on it (the levels it is
+// compared with lie in -2..17, and LOCAL's level equality is between
+// candidates that passed the level window)
+__device__ inline int kp_octave(const float4& k) { return (int)(short)(__float_as_uint(k.w) >> 16); }
+
+// Candidate keys: Hamming distance << 12 | sorted position.  The reference
+// keeps the first best in its candidate order (GetFeaturesInArea's), i.e. the
+// smallest key.
+constexpr unsigned kNoKey = 0xFFFFFFFFu;
+__device__ inline int key_dist(unsigned k) { return (int)(k >> 12); }
+__device__ inline int key_pos(unsigned k) { return (int)(k & 0xFFFu); }
+
 // GetFeaturesInArea (Frame.cpp:379-432) with the variant's candidate
-// filters; G lanes (sub-lane sl) walk the window's candidates in grid order
-// and call visit(key, position) for every candidate that passes, with key =
-// Hamming distance << 20 | sorted position: the reference keeps the first
-// best in its candidate order, i.e. the smallest key.
+// filters: G lanes (sub-lane sl) share the window's candidates, flattened
+// over its column runs (candidate f to lane f % G), and call visit(key) for
+// every candidate that passes.
 template <int G, class Visit>
 __device__ inline void scan_candidates(const orbgpu_proj_call& C, const Query& q, int ip, const Grid& g, float invW,
                                        float invH, int sl, Visit&& visit) {
@@ -229,56 +259,61 @@ __device__ inline void scan_candidates(const orbgpu_proj_call& C, const Query& q
     const int cx1 = min(kGC - 1, (int)ceilf((q.u - T.min_x + q.r) * invW));
     const int cy0 = max(0, (int)floorf((q.v - T.min_y - q.r) * invH));
     const int cy1 = min(kGR - 1, (int)ceilf((q.v - T.min_y + q.r) * invH));
-    if (cx0 >= kGC || cx1 < 0 || cy0 >= kGR || cy1 < 0) return;
+    if (cx0 >= kGC || cx1 < 0 || cy0 >= kGR || cy1 < 0 || cx0 > cx1) return;
     const bool check_levels = q.min_level > 0 || q.max_level >= 0;
-    const unsigned long long* dp = reinterpret_cast<const unsigned long long*>(C.points.desc + 32 * (size_t)ip);
-    const unsigned long long d0 = dp[0], d1 = dp[1], d2 = dp[2], d3 = dp[3];
-    for (int ix = cx0; ix <= cx1; ++ix) {
-        const int s = g.cell_start[ix * kGR + cy0], e = g.cell_start[ix * kGR + cy1 + 1];
-        for (int p = s + sl; p < e; p += G) {
-            const int oct = g.koct[p];
-            if (check_levels) {
-                if (oct < q.min_level) continue;
-                if (q.max_level >= 0 && oct > q.max_level) continue;
-            }
-            if (!(fabsf(g.kx[p] - q.u) < q.r && fabsf(g.ky[p] - q.v) < q.r)) continue;
-            const int idx = (int)(g.sorted[p] & 0xFFFu);
-            if ((g.hidw[idx >> 5] >> (idx & 31)) & 1u) continue;
-            if (C.variant == ORBGPU_PROJ_SIM3 && (oct < q.level_lo || oct > q.level_hi)) continue;
-            const float ur = g.kur[p];
-            if (q.stereo && ur > 0) {
-                const float er = fabsf(q.ur - ur);
-                if (er > q.stereo_r) continue;
-            }
-            const unsigned long long* e8 = reinterpret_cast<const unsigned long long*>(T.desc + 32 * (size_t)idx);
-            const int dist = __popcll(d0 ^ e8[0]) + __popcll(d1 ^ e8[1]) + __popcll(d2 ^ e8[2]) + __popcll(d3 ^ e8[3]);
-            visit(((unsigned long long)dist << 20) | (unsigned)p);
+    const uint4* dp = reinterpret_cast<const uint4*>(C.points.desc + 32 * (size_t)ip);
+    const uint4 pa = dp[0], pb = dp[1];
+    int col = cx0;
+    int ce = g.cell_start[col * kGR + cy1 + 1];
+    int p = g.cell_start[col * kGR + cy0] + sl;
+    while (true) {
+        while (p >= ce && col < cx1) {  // carry into the next column run
+            const int over = p - ce;
+            ++col;
+            ce = g.cell_start[col * kGR + cy1 + 1];
+            p = g.cell_start[col * kGR + cy0] + over;
         }
+        if (p >= ce) break;
+        const int cur = p;
+        p += G;
+        const float4 k = g.kp[cur];
+        const int oct = kp_octave(k), idx = kp_slot(k);
+        if (check_levels) {
+            if (oct < q.min_level) continue;
+            if (q.max_level >= 0 && oct > q.max_level) continue;
+        }
+        if (!(fabsf(k.x - q.u) < q.r && fabsf(k.y - q.v) < q.r)) continue;
+        if ((g.hidw[idx >> 5] >> (idx & 31)) & 1u) continue;
+        if (C.variant == ORBGPU_PROJ_SIM3 && (oct < q.level_lo || oct > q.level_hi)) continue;
+        if (q.stereo && k.z > 0) {
+            const float er = fabsf(q.ur - k.z);
+            if (er > q.stereo_r) continue;
+        }
+        const uint4 ea = g.desc[2 * idx], eb = g.desc[2 * idx + 1];
+        const int dist = __popc(pa.x ^ ea.x) + __popc(pa.y ^ ea.y) + __popc(pa.z ^ ea.z) + __popc(pa.w ^ ea.w) +
+                         __popc(pb.x ^ eb.x) + __popc(pb.y ^ eb.y) + __popc(pb.z ^ eb.z) + __popc(pb.w ^ eb.w);
+        visit(((unsigned)dist << 12) | (unsigned)cur);
     }
 }
 
 // minimum over aligned groups of G lanes
 template <int G>
-__device__ inline unsigned long long gmin64(unsigned long long v) {
+__device__ inline unsigned gmin32(unsigned v) {
 #pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) {
-        const unsigned long long t = __shfl_xor(v, o, 64);
-        v = t < v ? t : v;
-    }
+    for (int o = G / 2; o > 0; o >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, o, 64));
     return v;
 }
 
-// best / second best (smallest keys) over the wave, current occupancy
+// best / second best (smallest keys) over the wave, current hidden set
 __device__ inline void best_two(const orbgpu_proj_call& C, const Query& q, int ip, const Grid& g, float invW,
-                                float invH, int lane, unsigned long long& b1, unsigned long long& b2) {
-    unsigned long long best = ~0ull, best2 = ~0ull;
-    scan_candidates<64>(C, q, ip, g, invW, invH, lane, [&](unsigned long long key) {
-        const bool first = key < best;  // value selects (a branchy update made the compiler spill the pair)
-        best2 = first ? best : (key < best2 ? key : best2);
-        best = first ? key : best;
+                                float invH, int lane, unsigned& b1, unsigned& b2) {
+    unsigned best = kNoKey, best2 = kNoKey;
+    scan_candidates<64>(C, q, ip, g, invW, invH, lane, [&](unsigned key) {
+        best2 = key < best ? best : min(key, best2);
+        best = min(key, best);
     });
-    b1 = gmin64<64>(best);
-    b2 = gmin64<64>(best == b1 ? best2 : best);
+    b1 = gmin32<64>(best);
+    b2 = gmin32<64>(best == b1 ? best2 : best);
 }
 
 // rotation bin of a match (ORBmatcher.cpp:155-163 and the overloads' copies)
@@ -298,16 +333,25 @@ __device__ inline int rot_bin(float src_angle, float kp_angle) {
 
 constexpr int kProjThreads = 1024;       // 16 waves: 15 build candidate lists, 1 resolves
 constexpr int kListK = 4;                // candidates kept per point (smallest keys)
-constexpr int kSub = 8;                  // lanes per point while building lists
-constexpr int kChunk = 240;              // points per list buffer (2 rounds of the 15 list waves)
+constexpr int kSub = 4;                  // lanes per point while building lists (one list entry each)
+constexpr int kChunk = 240;              // points per list buffer (one round of the 15 list waves)
+constexpr int kDescLds = 2048;           // targets up to this size keep their descriptors in LDS
+// dynamic LDS: per keypoint kp (16 B) | angle (4) | first hider (4) | rotHist bins (4) [| descriptor (32)]
+constexpr int kProjDynLds = 28 * kMaxKps > 60 * kDescLds ? 28 * kMaxKps : 60 * kDescLds;
+
+// list entry aux word: slot | rotation bin << 12 | (int8) octave << 17
+__device__ inline int aux_slot(unsigned a) { return (int)(a & 0xFFFu); }
+__device__ inline int aux_bin(unsigned a) { return (int)((a >> 12) & 31u); }
+__device__ inline int aux_octave(unsigned a) { return (int)(signed char)(a >> 17); }
 
 // One block per call.  Phase 1 (all threads): the target's 64x48 feature
-// grid in LDS (AssignFeaturesToGrid, Frame.cpp:241-259) as (cell, slot)
-// keys sorted by a block bitonic sort, so a cell row ix, cells iy0..iy1, is
-// one contiguous run in GetFeaturesInArea's order (ix outer, iy inner,
-// insertion order), and the hidden-slot bitmap.  Phase 2: the reference
-// walks the points in order and an assignment hides a keypoint from later
-// points, so:
+// grid in LDS (AssignFeaturesToGrid, Frame.cpp:241-259): (cell, slot) keys
+// placed by a counting sort over the cells with insertion order restored
+// within each cell, so a cell row ix, cells iy0..iy1, is one contiguous run
+// in GetFeaturesInArea's order (ix outer, iy inner, insertion order); the
+// hidden-slot bitmap; the descriptors when they fit.  Phase 2: the
+// reference walks the points in order and an assignment hides a keypoint
+// from later points, so:
 //   * waves 1..15, kSub lanes per point, project every point of the next
 //     chunk and keep its kListK smallest candidate keys with the candidates'
 //     slot, octave and rotation bin, and its candidate count -- the hidden
@@ -327,17 +371,13 @@ constexpr int kChunk = 240;              // points per list buffer (2 rounds of 
 // rotation-consistency cull (LAST_FRAME, KEYFRAME).
 __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_call* __restrict__ calls, int stride,
                                                             int* __restrict__ match_g, int* __restrict__ nmatches) {
-    __shared__ unsigned int s_sorted[kMaxKps];     // (cell << 12 | slot)
     __shared__ unsigned short s_cell_start[kCells + 1];
     __shared__ unsigned int s_hidw[kMaxKps / 32];  // hidden slots (occupancy >= hidden_min)
-    __shared__ float s_kx[kMaxKps], s_ky[kMaxKps], s_kur[kMaxKps];
-    __shared__ int s_koct[kMaxKps];
-    __shared__ unsigned int s_acc[kMaxKps];        // rotHist entries in push order: slot | bin << 16
-    __shared__ unsigned long long s_list[2][kChunk][kListK];
-    __shared__ unsigned int s_aux[2][kChunk][kListK];  // candidate slot | rotation bin << 12
-    __shared__ int s_loct[2][kChunk][kListK];      // candidate octave
+    __shared__ uint2 s_list[2][kChunk][kListK];    // (key, aux) per list entry
     __shared__ int s_ncand[2][kChunk];             // candidate count | has-observations << 30; -1: no query
     __shared__ int s_hist[kHL];
+    __shared__ float s_sf[16];
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
     const orbgpu_proj_call& C = calls[blockIdx.x];
     const orbgpu_proj_target& T = C.target;
     const orbgpu_proj_points& P = C.points;
@@ -353,63 +393,113 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
         return;
     }
     const int variant = C.variant, hmin = hidden_min(variant), np = P.n;
-    // ---- phase 1: grid (PosInGrid with C round, Frame.cpp:434-443)
+    const bool desc_lds = n <= kDescLds;
+    const int nr = (n + 3) & ~3;
+    float4* s_kp = reinterpret_cast<float4*>(s_dyn);
+    float* s_kang = reinterpret_cast<float*>(s_dyn + 16 * nr);
+    unsigned* s_first = reinterpret_cast<unsigned*>(s_dyn + 20 * nr);  // walk: lowest batch lane hiding a slot
+    unsigned* s_bins = reinterpret_cast<unsigned*>(s_dyn + 24 * nr);   // per slot: rotHist bins holding it
+    uint4* s_desc = reinterpret_cast<uint4*>(s_dyn + 28 * nr);
+    int* s_cnt = reinterpret_cast<int*>(&s_list[0][0][0]);  // phase 1: per-cell counts, then cursors
+    unsigned* s_sorted = s_first;                            // phase 1: (cell << 12 | slot) keys (8n bytes free)
+    // ---- phase 1: grid (PosInGrid with C round, Frame.cpp:434-443) by a counting sort over the cells
     const float invW = (float)kGC / (T.max_x - T.min_x), invH = (float)kGR / (T.max_y - T.min_y);
-    int n2 = 1;
-    while (n2 < n) n2 <<= 1;
-    for (int i = tid; i < n2; i += kProjThreads) {
-        unsigned key = 0xFFFFFFFFu;
+    for (int c = tid; c < kCells; c += kProjThreads) s_cnt[c] = 0;
+    if (const uint8_t* occ = T.occupied) {  // hidden-slot bitmap, 64 slots per ballot
+        for (int i0 = wave * 64; i0 < n; i0 += kProjThreads) {
+            const int i = i0 + lane;
+            const unsigned long long m = __ballot(i < n && occ[i] >= hmin);
+            if (lane == 0) {
+                s_hidw[i0 >> 5] = (unsigned)m;
+                s_hidw[(i0 >> 5) + 1] = (unsigned)(m >> 32);
+            }
+        }
+    } else {
+        for (int w = tid; w < kMaxKps / 32; w += kProjThreads) s_hidw[w] = 0;
+    }
+    if (tid < kHL) s_hist[tid] = 0;
+    if (tid < 16) s_sf[tid] = tid < T.n_levels ? T.scale_factors[tid] : 0.0f;
+    if (desc_lds) {  // the descriptors, 16 bytes per thread and step
+        const uint4* gd = reinterpret_cast<const uint4*>(T.desc);
+        for (int i = tid; i < 2 * n; i += kProjThreads) s_desc[i] = gd[i];
+    }
+    __syncthreads();
+    constexpr int kPer = kMaxKps / kProjThreads;
+    int cell[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+        const int i = tid + r * kProjThreads;
+        cell[r] = -1;
         if (i < n) {
             const int px = (int)roundf((T.kps[i].x - T.min_x) * invW);
             const int py = (int)roundf((T.kps[i].y - T.min_y) * invH);
-            if (px >= 0 && px < kGC && py >= 0 && py < kGR) key = ((unsigned)(px * kGR + py) << 12) | (unsigned)i;
-        }
-        s_sorted[i] = key;
-    }
-    if (tid < kMaxKps / 32) {
-        unsigned w = 0;
-        if (T.occupied)
-            for (int b = 0; b < 32; ++b) {
-                const int i = 32 * tid + b;
-                if (i < n && T.occupied[i] >= hmin) w |= 1u << b;
-            }
-        s_hidw[tid] = w;
-    }
-    if (tid < kHL) s_hist[tid] = 0;
-    for (int size = 2; size <= n2; size <<= 1)  // bitonic sort
-        for (int st = size >> 1; st > 0; st >>= 1) {
-            __syncthreads();
-            for (int i = tid; i < n2 / 2; i += kProjThreads) {
-                const int lo = 2 * i - (i & (st - 1)), hi = lo + st;
-                const bool up = (lo & size) == 0;
-                const unsigned a = s_sorted[lo], b = s_sorted[hi];
-                if ((a > b) == up) {
-                    s_sorted[lo] = b;
-                    s_sorted[hi] = a;
-                }
+            if (px >= 0 && px < kGC && py >= 0 && py < kGR) {
+                cell[r] = px * kGR + py;
+                atomicAdd(&s_cnt[cell[r]], 1);
             }
         }
+    }
     __syncthreads();
-    for (int c = tid; c <= kCells; c += kProjThreads) {  // first sorted position with cell >= c
-        int lo = 0, hi = n;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if ((s_sorted[mid] >> 12) < (unsigned)c) lo = mid + 1; else hi = mid;
+    {  // exclusive scan of the counts: 3 cells per thread, wave scans, wave totals
+        constexpr int kCPT = kCells / kProjThreads;
+        int c3[kCPT], loc = 0;
+#pragma unroll
+        for (int k = 0; k < kCPT; ++k) {
+            c3[k] = s_cnt[kCPT * tid + k];
+            loc += c3[k];
         }
-        s_cell_start[c] = (unsigned short)lo;
+        int v = loc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(v, o, 64);
+            if (lane >= o) v += t;
+        }
+        int* s_wsum = s_ncand[0];  // 16 wave totals (s_ncand is free until the lists)
+        if (lane == 63) s_wsum[wave] = v;
+        __syncthreads();
+        int off = v - loc;
+        for (int w = 0; w < wave; ++w) off += s_wsum[w];
+#pragma unroll
+        for (int k = 0; k < kCPT; ++k) {
+            s_cell_start[kCPT * tid + k] = (unsigned short)off;
+            s_cnt[kCPT * tid + k] = off;
+            off += c3[k];
+        }
+        if (tid == kProjThreads - 1) s_cell_start[kCells] = (unsigned short)off;
     }
-    for (int p = tid; p < n; p += kProjThreads) {  // window-test fields in sorted order
-        const unsigned key = s_sorted[p];
-        if (key == 0xFFFFFFFFu) continue;  // outside the grid: never scanned
-        const int i = (int)(key & 0xFFFu);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kPer; ++r)  // scatter (any order within a cell)
+        if (cell[r] >= 0) s_sorted[atomicAdd(&s_cnt[cell[r]], 1)] = ((unsigned)cell[r] << 12) | (unsigned)(tid + r * kProjThreads);
+    __syncthreads();
+    for (int c = tid; c < kCells; c += kProjThreads) {  // insertion order within each cell
+        const int s0 = s_cell_start[c], e0 = s_cell_start[c + 1];
+        for (int x = s0 + 1; x < e0; ++x) {
+            const unsigned key = s_sorted[x];
+            int y = x - 1;
+            while (y >= s0 && s_sorted[y] > key) {
+                s_sorted[y + 1] = s_sorted[y];
+                --y;
+            }
+            s_sorted[y + 1] = key;
+        }
+    }
+    __syncthreads();
+    const int ngrid = s_cell_start[kCells];
+    for (int p = tid; p < ngrid; p += kProjThreads) {  // window-test fields in sorted order
+        const int i = (int)(s_sorted[p] & 0xFFFu);
         const orbgpu_keypoint kp = T.kps[i];
-        s_kx[p] = kp.x;
-        s_ky[p] = kp.y;
-        s_koct[p] = kp.octave;
-        s_kur[p] = T.u_right ? T.u_right[i] : -1.0f;
+        const unsigned oct = (unsigned)(unsigned short)(short)min(32767, max(-32768, kp.octave));
+        s_kp[p] = make_float4(kp.x, kp.y, T.u_right ? T.u_right[i] : -1.0f, __uint_as_float((unsigned)i | oct << 16));
+        s_kang[p] = kp.angle;
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += kProjThreads) {  // the sort keys are consumed
+        s_first[i] = ~0u;
+        s_bins[i] = 0u;
     }
     PSTAMP(1);
-    const Grid g{s_sorted, s_cell_start, s_hidw, s_kx, s_ky, s_koct, s_kur};
+    const Grid g{s_kp, s_cell_start, s_hidw, desc_lds ? s_desc : reinterpret_cast<const uint4*>(T.desc)};
     const CallPose cp = call_pose(C);
     const bool hist = C.check_ori && (variant == ORBGPU_PROJ_LAST_FRAME || variant == ORBGPU_PROJ_KEYFRAME);
     // list of chunk ch into buffer ch & 1, by waves w0..15 (nw waves), kSub lanes per point
@@ -419,47 +509,51 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
         for (int jb = 0; jb < kChunk; jb += ng) {
             if (ch * kChunk + jb >= np) break;
             const int j = jb + gid, ip = ch * kChunk + j;
+            const bool act = j < kChunk && ip < np;
             Query q{};
-            if (j < kChunk && ip < np) q = make_query(C, cp, ip);
-            unsigned long long top[kListK];
+            if (act) q = make_query(C, cp, s_sf, ip);
+            unsigned top[kListK];
 #pragma unroll
-            for (int k = 0; k < kListK; ++k) top[k] = ~0ull;
+            for (int k = 0; k < kListK; ++k) top[k] = kNoKey;
             int cnt = 0;
             if (q.ok)
-                scan_candidates<kSub>(C, q, ip, g, invW, invH, sl, [&](unsigned long long key) {
+                scan_candidates<kSub>(C, q, ip, g, invW, invH, sl, [&](unsigned key) {
                     ++cnt;
 #pragma unroll
                     for (int k = kListK - 1; k >= 0; --k) {  // insert into the lane's sorted top-K
-                        const unsigned long long prev = k > 0 ? top[k - 1] : 0ull;
+                        const unsigned prev = k > 0 ? top[k - 1] : 0u;
                         if (key < top[k]) top[k] = (k > 0 && key < prev) ? prev : key;
                     }
                 });
 #pragma unroll
             for (int o = kSub / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-            if (!(j < kChunk && ip < np)) continue;
-            // the group's kListK smallest keys: repeatedly take the minimum of the lanes' heads;
-            // the owner records it with its candidate's slot, octave and rotation bin
-            const float pangle = hist ? P.angle[ip] : 0.0f;
+            // the group's kListK smallest keys: every lane ranks its own keys against the group's
+            // (keys are distinct) and writes those of rank < kListK with slot, octave and bin
+            unsigned other[kSub - 1][kListK];
+#pragma unroll
+            for (int o = 1; o < kSub; ++o)
+#pragma unroll
+                for (int k = 0; k < kListK; ++k) other[o - 1][k] = (unsigned)__shfl_xor((int)top[k], o, 64);
+            if (!act) continue;
 #pragma unroll
             for (int k = 0; k < kListK; ++k) {
-                const unsigned long long m = gmin64<kSub>(top[0]);
-                if (m == ~0ull ? sl == 0 : top[0] == m) {
-                    unsigned aux = 0;
-                    int oct = 0;
-                    if (m != ~0ull) {
-                        const int p = (int)(m & 0xFFFFFu), i = (int)(s_sorted[p] & 0xFFFu);
-                        aux = (unsigned)i | (hist ? (unsigned)rot_bin(pangle, T.kps[i].angle) << 12 : 0u);
-                        oct = s_koct[p];
+                if (top[k] == kNoKey) break;
+                int rank = k;
 #pragma unroll
-                        for (int t = 0; t + 1 < kListK; ++t) top[t] = top[t + 1];
-                        top[kListK - 1] = ~0ull;
-                    }
-                    s_list[buf][j][k] = m;
-                    s_aux[buf][j][k] = aux;
-                    s_loct[buf][j][k] = oct;
+                for (int o = 0; o < kSub - 1; ++o)
+#pragma unroll
+                    for (int t = 0; t < kListK; ++t) rank += other[o][t] < top[k] ? 1 : 0;
+                if (rank < kListK) {
+                    const float4 kq = s_kp[key_pos(top[k])];
+                    const int oct = max(-128, min(127, kp_octave(kq)));
+                    const unsigned bin = hist ? (unsigned)rot_bin(q.angle, s_kang[key_pos(top[k])]) : 0u;
+                    s_list[buf][j][rank] = make_uint2(top[k], (unsigned)kp_slot(kq) | bin << 12 | ((unsigned)oct & 0xFFu) << 17);
                 }
             }
-            if (sl == 0) s_ncand[buf][j] = q.ok ? cnt | ((P.flags[ip] & ORBGPU_PT_HAS_OBS) ? (1 << 30) : 0) : -1;
+            if (sl == 0) {
+                for (int k = min(cnt, kListK); k < kListK; ++k) s_list[buf][j][k] = make_uint2(kNoKey, 0u);
+                s_ncand[buf][j] = q.ok ? cnt | ((q.flags & ORBGPU_PT_HAS_OBS) ? (1 << 30) : 0) : -1;
+            }
         }
     };
     __syncthreads();
@@ -473,18 +567,18 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
     const int need = variant == ORBGPU_PROJ_LOCAL ? 2 : 1;
     const float nnratio = C.nnratio;
     const int orb_dist = C.orb_dist;
-    auto accept = [&](unsigned long long b1, unsigned long long b2, int o1, int o2) {
-        const int bestDist = (int)(b1 >> 20);
+    auto accept = [&](unsigned b1, unsigned b2, int o1, int o2) {
+        const int bestDist = key_dist(b1);
         if (variant == ORBGPU_PROJ_LOCAL) {  // ORBmatcher.cpp:133-151
-            const int bestDist2 = b2 == ~0ull ? 256 : (int)(b2 >> 20);
-            const int bestLevel2 = b2 == ~0ull ? -1 : o2;
+            const int bestDist2 = b2 == kNoKey ? 256 : key_dist(b2);
+            const int bestLevel2 = b2 == kNoKey ? -1 : o2;
             return bestDist <= kThHigh && !(o1 == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2);
         }
         if (variant == ORBGPU_PROJ_SIM3) return bestDist <= kThLow;
         if (variant == ORBGPU_PROJ_LAST_FRAME) return bestDist <= kThHigh;
         return bestDist <= orb_dist;
     };
-    int nm = 0, nacc = 0;
+    int nm = 0;
     for (int ch = 0; ch < nchunks; ++ch) {
         if (wave > 0) {
             if (ch + 1 < nchunks) build(ch + 1, 1, kProjThreads / 64 - 1);
@@ -497,19 +591,13 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
                 const int jn = min(64, min(kChunk - b, np - ipb));
                 const int ip = ipb + lane;
                 int nc = -1;
-                unsigned long long kk[kListK];
-                unsigned ka[kListK] = {};
-                int ko[kListK] = {};
+                uint2 e[kListK];
 #pragma unroll
-                for (int k = 0; k < kListK; ++k) kk[k] = ~0ull;
+                for (int k = 0; k < kListK; ++k) e[k] = make_uint2(kNoKey, 0u);
                 if (lane < jn) {
                     nc = s_ncand[buf][b + lane];
 #pragma unroll
-                    for (int k = 0; k < kListK; ++k) {
-                        kk[k] = s_list[buf][b + lane][k];
-                        ka[k] = s_aux[buf][b + lane][k];
-                        ko[k] = s_loct[buf][b + lane][k];
-                    }
+                    for (int k = 0; k < kListK; ++k) e[k] = s_list[buf][b + lane][k];
                 }
                 const bool live = nc > 0;  // a valid point with a non-empty window
                 const bool trunc = (nc & ((1 << 30) - 1)) > kListK;
@@ -517,82 +605,69 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
                 int t = 0;  // lanes below t are committed
                 while (t < jn) {
                     // every pending lane resolves its point against the current hidden set
-                    unsigned long long b1 = ~0ull, b2 = ~0ull;
-                    unsigned x1 = 0, exam[kListK];
-                    int o1 = 0, o2 = 0, nvis = 0;
+                    unsigned b1 = kNoKey, b2 = kNoKey, x1 = 0, x2 = 0, exam[kListK];
+                    int nvis = 0;
 #pragma unroll
                     for (int k = 0; k < kListK; ++k) {
-                        const bool examined = kk[k] != ~0ull && nvis < need;
-                        const unsigned i = ka[k] & 0xFFFu;
+                        const bool examined = e[k].x != kNoKey && nvis < need;
+                        const unsigned i = (unsigned)aux_slot(e[k].y);
                         exam[k] = examined ? i : 0xFFFFFFFFu;
                         const bool vis = examined && !((s_hidw[i >> 5] >> (i & 31)) & 1u);
-                        b2 = vis && nvis == 1 ? kk[k] : b2;
-                        o2 = vis && nvis == 1 ? ko[k] : o2;
-                        b1 = vis && nvis == 0 ? kk[k] : b1;
-                        x1 = vis && nvis == 0 ? ka[k] : x1;
-                        o1 = vis && nvis == 0 ? ko[k] : o1;
+                        b2 = vis && nvis == 1 ? e[k].x : b2;
+                        x2 = vis && nvis == 1 ? e[k].y : x2;
+                        b1 = vis && nvis == 0 ? e[k].x : b1;
+                        x1 = vis && nvis == 0 ? e[k].y : x1;
                         nvis += vis ? 1 : 0;
                     }
                     const bool pend = lane >= t && lane < jn;
                     const bool rescan = pend && live && nvis < need && trunc;
-                    const bool acc = pend && live && !rescan && b1 != ~0ull && accept(b1, b2, o1, o2);
+                    const bool acc = pend && live && !rescan && b1 != kNoKey &&
+                                     accept(b1, b2, aux_octave(x1), aux_octave(x2));
                     const bool hides = acc && hides_on_match;
                     // a lane whose examined entries hold a slot an earlier pending lane hides
+                    // (s_first: the lowest hiding lane per slot, reset right after the test)
+                    const unsigned slot = (unsigned)aux_slot(x1);
+                    if (hides) atomicMin(&s_first[slot], (unsigned)lane);
                     bool conflict = false;
-                    unsigned long long hm = __ballot(hides);
-                    while (hm) {
-                        const int s = __builtin_ctzll(hm);
-                        hm &= hm - 1;
-                        const unsigned hs = (unsigned)__builtin_amdgcn_readlane((int)(x1 & 0xFFFu), s);
-                        bool in = false;
 #pragma unroll
-                        for (int k = 0; k < kListK; ++k) in = in || exam[k] == hs;
-                        conflict = conflict || (lane > s && in);
-                    }
+                    for (int k = 0; k < kListK; ++k)
+                        conflict = conflict || (exam[k] != 0xFFFFFFFFu && s_first[exam[k]] < (unsigned)lane);
+                    if (hides) s_first[slot] = ~0u;
                     const unsigned long long stop = __ballot(pend && (conflict || rescan));
                     const int t0 = stop ? __builtin_ctzll(stop) : jn;
                     // commit the pending lanes below t0
                     const bool com = acc && lane < t0;
-                    const unsigned slot = x1 & 0xFFFu;
                     if (com) {
                         if (hides) atomicOr(&s_hidw[slot >> 5], 1u << (slot & 31));
                         atomicMax(&match[slot], ip);
                     }
-                    const unsigned long long cm = __ballot(com);
-                    if (hist) {
-                        if (com) {
-                            const int r = nacc + __builtin_amdgcn_mbcnt_hi((unsigned)(cm >> 32),
-                                                                           __builtin_amdgcn_mbcnt_lo((unsigned)cm, 0u));
-                            const unsigned bin = x1 >> 12;
-                            if (r < kMaxKps) s_acc[r] = slot | (bin << 16);
-                            atomicAdd(&s_hist[bin], 1);
-                        }
-                        nacc += __popcll(cm);
+                    if (hist && com) {  // rotHist[bin].push_back(slot)
+                        atomicOr(&s_bins[slot], 1u << aux_bin(x1));
+                        atomicAdd(&s_hist[aux_bin(x1)], 1);
                     }
-                    nm += __popcll(cm);
+                    nm += __popcll(__ballot(com));
                     t = t0;
                     if (t0 < jn && !((__ballot(conflict) >> t0) & 1ull)) {
                         // lane t0's truncated list ran out: rescan its window exactly
                         const int ipr = ipb + t0;
                         const int ncr = __builtin_amdgcn_readlane(nc, t0);
-                        const Query q = make_query(C, cp, ipr);
-                        unsigned long long r1, r2;
+                        const Query q = make_query(C, cp, s_sf, ipr);
+                        unsigned r1, r2;
                         best_two(C, q, ipr, g, invW, invH, lane, r1, r2);
-                        if (r1 != ~0ull) {
-                            const int p1 = (int)(r1 & 0xFFFFFu);
-                            const int q1 = s_koct[p1], q2 = r2 != ~0ull ? s_koct[r2 & 0xFFFFFu] : 0;
-                            if (accept(r1, r2, q1, q2)) {
-                                const unsigned sr = s_sorted[p1] & 0xFFFu;
+                        if (r1 != kNoKey) {
+                            const float4 k1 = s_kp[key_pos(r1)];
+                            const int q2 = r2 != kNoKey ? kp_octave(s_kp[key_pos(r2)]) : 0;
+                            if (accept(r1, r2, kp_octave(k1), q2)) {
+                                const unsigned sr = (unsigned)kp_slot(k1);
                                 if (lane == 0) {
                                     if (((ncr >> 30) & 1 ? 2 : 1) >= hmin) atomicOr(&s_hidw[sr >> 5], 1u << (sr & 31));
                                     atomicMax(&match[sr], ipr);
                                     if (hist) {
-                                        const int bin = rot_bin(P.angle[ipr], T.kps[sr].angle);
-                                        if (nacc < kMaxKps) s_acc[nacc] = sr | ((unsigned)bin << 16);
+                                        const int bin = rot_bin(q.angle, s_kang[key_pos(r1)]);
+                                        atomicOr(&s_bins[sr], 1u << bin);
                                         atomicAdd(&s_hist[bin], 1);
                                     }
                                 }
-                                if (hist) ++nacc;
                                 ++nm;
                             }
                         }
@@ -618,22 +693,14 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
         }
         if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
         else if ((float)max3 < 0.1f * (float)max1) ind3 = -1;
-        if (nacc > kMaxKps) {  // more histogram entries than the LDS list holds: rejected
-            if (lane == 0) nmatches[blockIdx.x] = -1;
-            return;
-        }
-        int culled = 0;
-        for (int k = lane; k < nacc; k += 64) {
-            const int b = (int)(s_acc[k] >> 16);
-            if (b != ind1 && b != ind2 && b != ind3) ++culled;
-        }
-        for (int k = lane; k < nacc; k += 64) {  // every entry of a culled bin sets its slot to NULL
-            const int b = (int)(s_acc[k] >> 16);
-            if (b != ind1 && b != ind2 && b != ind3) match[s_acc[k] & 0xFFFFu] = -2;
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) culled += __shfl_xor(culled, o, 64);
-        nm -= culled;
+        unsigned keep = 0;
+        if (ind1 >= 0) keep |= 1u << ind1;
+        if (ind2 >= 0) keep |= 1u << ind2;
+        if (ind3 >= 0) keep |= 1u << ind3;
+        for (int b = 0; b < kHL; ++b)  // every entry of a culled bin is one match less
+            if (!((keep >> b) & 1u)) nm -= s_hist[b];
+        for (int i = lane; i < n; i += 64)  // and sets its slot to NULL
+            if (s_bins[i] & ~keep) match[i] = -2;
     }
     if (lane == 0) nmatches[blockIdx.x] = nm;
 #ifdef PROJ_STAMPS
@@ -694,7 +761,11 @@ int proj_max_keypoints() { return kMaxKps; }
 hipError_t launch_search_by_projection(int ncalls, const orbgpu_proj_call* calls, int stride, int* match,
                                        int* nmatches, hipStream_t stream) {
     if (ncalls <= 0) return hipSuccess;
-    hipLaunchKernelGGL(proj_kernel, dim3(ncalls), dim3(kProjThreads), 0, stream, calls, stride, match, nmatches);
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&proj_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, kProjDynLds);
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(proj_kernel, dim3(ncalls), dim3(kProjThreads), kProjDynLds, stream, calls, stride, match,
+                       nmatches);
     return hipGetLastError();
 }
 

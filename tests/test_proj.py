@@ -80,3 +80,62 @@ def test_gpu_search_by_projection_exact(variant, th, kw, stereo, scale):
         assert nm_g == nm_r, f"seed {seed}"
         np.testing.assert_array_equal(m_g, m_r)
         assert nm_r > 20
+
+
+def _run_both(variant, tgt, pts, th, kw, seed):
+    import proj
+    if variant == 0:
+        fl, tr, lv = proj_ref.is_in_frustum(tgt, pts, 0.5)
+        pts = dict(pts, flags=fl, track=tr, track_level=lv)
+    if variant == 2:
+        rng = np.random.default_rng(seed)
+        last = tgt["Tcw"].copy()
+        last[:3, 3] += rng.uniform(-0.2, 0.2, 3).astype(np.float32)
+        kw = dict(kw, last_Tcw=last)
+    nm_r, m_r = proj_ref.search_by_projection(variant, tgt, pts, th, **kw)
+    nm_g, m_g = proj.search_by_projection(variant, tgt, pts, th, **kw)
+    assert nm_g == nm_r
+    np.testing.assert_array_equal(m_g, m_r)
+    return nm_r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant,th,kw", [(0, 1.0, dict(nnratio=0.8)), (1, 10.0, dict()),
+                                           (2, 15.0, dict(check_ori=True, mono=True)),
+                                           (3, 10.0, dict(check_ori=True, orb_dist=100))])
+def test_gpu_search_by_projection_large_target_exact(variant, th, kw):
+    """A target above the kernel's LDS descriptor budget (2048 keypoints):
+    descriptors are read from HBM instead; same bar."""
+    tgt, pts = synth.projection_scenario(1500, 1200, 40 + variant, stereo=variant in (0, 2))
+    assert len(tgt["kps"]) > 2048
+    assert _run_both(variant, tgt, pts, th, kw, 40) > 100
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_gpu_search_by_projection_crowded_exact(variant):
+    """Many points onto few keypoints: most points compete for the same
+    slots, so the in-order walk's hiding decides nearly every match."""
+    tgt, pts = synth.projection_scenario(900, 40, 60 + variant)
+    keep = np.random.default_rng(7).permutation(len(tgt["kps"]))[:60]
+    tgt = dict(tgt, kps=tgt["kps"][keep], desc=tgt["desc"][keep])
+    for key in ("u_right", "occupied"):
+        if tgt.get(key) is not None:
+            tgt[key] = tgt[key][keep]
+    th = 30.0 if variant else 3.0
+    kw = {1: dict(), 2: dict(check_ori=True, mono=True), 3: dict(check_ori=True, orb_dist=100),
+          0: dict(nnratio=0.9)}[variant]
+    _run_both(variant, tgt, pts, th, kw, 60)
+
+
+@pytest.mark.gpu
+def test_gpu_search_by_projection_empty_inputs():
+    import proj
+    tgt, pts = synth.projection_scenario(200, 50, 9)
+    none = {k: (v[:0] if isinstance(v, np.ndarray) and v.ndim and len(v) == len(pts["flags"]) else v)
+            for k, v in pts.items()}
+    for variant, th, kw in [(1, 10.0, dict()), (3, 10.0, dict(check_ori=True, orb_dist=100))]:
+        nm_r, m_r = proj_ref.search_by_projection(variant, tgt, none, th, **kw)
+        nm_g, m_g = proj.search_by_projection(variant, tgt, none, th, **kw)
+        assert nm_g == nm_r == 0
+        np.testing.assert_array_equal(m_g, m_r)
