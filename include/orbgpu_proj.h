@@ -100,7 +100,9 @@ int orbgpu_is_in_frustum_device(const orbgpu_proj_target* target, int n, const f
  *     -1 : untouched by this call
  *     -2 : set to NULL by the rotation-consistency cull (LAST_FRAME, KEYFRAME)
  * and d_nmatches[c] (the reference's return value; -1 if the target has
- * more than `stride` or 4096 keypoints -- rejected, never truncated). */
+ * more than `stride` or 4096 keypoints -- rejected, never truncated).
+ * Descriptor arrays (target.desc, points.desc) are read as 16-byte vectors:
+ * their device addresses must be 16-byte aligned (hipMalloc's are). */
 int orbgpu_search_by_projection_batch_device(int ncalls, const orbgpu_proj_call* d_calls, int stride, int* d_match,
                                              int* d_nmatches, void* stream);
 /* Host form of one call: every pointer in *call is a host pointer. */
