@@ -11,6 +11,7 @@
  *   Frame::ComputeBoW (levelsup 4)         src/Frame.cpp:452-460
  *   ORBmatcher::SearchByBoW(KF, F)         src/ORBmatcher.cpp:205-348
  *   ORBmatcher::SearchByBoW(KF1, KF2)      src/ORBmatcher.cpp:604-743
+ *   ORBmatcher::SearchForTriangulation     src/ORBmatcher.cpp:755-951 (+ CheckDistEpipolarLine :166-190)
  *
  * Layouts.  A FeatureVector is returned as CSR: node ids ascending
  * (fv_nodes[0..fv_n)), fv_offsets[0..fv_n] into fv_features (feature
@@ -101,6 +102,42 @@ int orbgpu_search_by_bow_batch_device(int mode, int batch, const orbgpu_bow_fram
 /* Host form for one pair (host arrays; match sized as above). */
 int orbgpu_search_by_bow(int mode, const orbgpu_bow_frame* a, const orbgpu_bow_frame* b, float nnratio,
                          int check_ori, int* match, int* nmatches);
+
+/* ---------------------------------------------------------------------- */
+/* SearchForTriangulation (LocalMapping::CreateNewMapPoints,               */
+/* LocalMapping.cpp:355-360)                                               */
+/* ---------------------------------------------------------------------- */
+/* One keyframe pair.  kf1 / kf2: FeatureVector CSR, descriptors,
+ * angle[i] = mvKeysUn[i].angle, valid[i] = 1 when the keyframe has NO
+ * MapPoint at i (GetMapPoint(idx) == NULL: only untracked keypoints are
+ * matched).  kps = mvKeysUn (x, y, octave read), u_right = mvuRight (NULL =
+ * monocular, all -1).  The epipole is computed from Cw1 (pKF1's camera
+ * centre) and pKF2's pose as the reference does (:763-770). */
+typedef struct orbgpu_triangulation_pair {
+    orbgpu_bow_frame kf1, kf2;
+    const orbgpu_keypoint* kps1;
+    const orbgpu_keypoint* kps2;
+    const float* u_right1;
+    const float* u_right2;
+    float F12[9];              /* row-major, F12.at<float>(r, c) = F12[3r + c] */
+    float Cw1[3];              /* pKF1->GetCameraCenter()                     */
+    float T2w[12];             /* pKF2 [R2w | t2w], row-major 3 x 4           */
+    float fx2, fy2, cx2, cy2;  /* pKF2 intrinsics                             */
+    float scale_factors2[16];  /* pKF2->mvScaleFactors                        */
+    float level_sigma2_2[16];  /* pKF2->mvLevelSigma2                         */
+    int only_stereo;           /* bOnlyStereo                                 */
+} orbgpu_triangulation_pair;
+
+/* Batched (pairs and everything they point to on the device).  Pair p
+ * writes d_match12 + p*stride: kf1.n ints, the KF2 keypoint matched to each
+ * KF1 keypoint after the rotation cull, or -1 (vMatchedPairs = the (i, m[i])
+ * with m[i] >= 0 in increasing i); d_nmatches[p] = the return value, -1 for
+ * a pair rejected because a keyframe has more than `stride` features. */
+int orbgpu_search_for_triangulation_batch_device(int batch, const orbgpu_triangulation_pair* d_pairs, int check_ori,
+                                                 int stride, int* d_match12, int* d_nmatches, void* stream);
+/* Host form for one pair (host arrays; match12 sized kf1.n). */
+int orbgpu_search_for_triangulation(const orbgpu_triangulation_pair* pair, int check_ori, int* match12,
+                                    int* nmatches);
 
 #ifdef __cplusplus
 }

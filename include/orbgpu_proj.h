@@ -7,6 +7,11 @@
  *   ORBmatcher::SearchByProjection(F, LastF, th, bMono)  src/ORBmatcher.cpp:1506-1641 (LAST_FRAME)
  *   ORBmatcher::SearchByProjection(F, KF, sAlreadyFound,
  *                                  th, ORBdist)          src/ORBmatcher.cpp:1661-1790 (KEYFRAME)
+ *   ORBmatcher::Fuse(KF, vpMapPoints, th)                src/ORBmatcher.cpp:962-1115  (FUSE)
+ *   ORBmatcher::Fuse(KF, Scw, vpPoints, th, vpReplace)   src/ORBmatcher.cpp:1119-1249 (FUSE_SIM3)
+ *   ORBmatcher::SearchBySim3(KF1, KF2, vpMatches12, s12, R12, t12, th)
+ *                                                        src/ORBmatcher.cpp:1253-1491 (SIM3_DIR x 2
+ *                                                        + the agreement check: orbgpu_search_by_sim3)
  * with Frame::GetFeaturesInArea / AssignFeaturesToGrid (src/Frame.cpp:241-259,
  * :379-443), MapPoint::PredictScale (src/MapPoint.cpp:481-508) and
  * RadiusByViewingCos (ORBmatcher.cpp:157-163).
@@ -16,6 +21,13 @@
  * reference (an assignment hides a keypoint from later points), and the GPU
  * keeps that order: one wave per call walks the points in order with its
  * lanes over the candidate keypoints.
+ *
+ * Fuse and SearchBySim3 have no such dependency inside the search: each
+ * point's best keypoint depends only on the geometry and the descriptors.
+ * Those variants return one result PER POINT; what the reference then does
+ * with it (MapPoint::Replace, AddObservation, the agreement of the two
+ * SearchBySim3 directions) stays with the caller, in the reference's order
+ * (include/orbslam2_amd/ORBmatcher.h does exactly that).
  */
 #ifndef ORBGPU_PROJ_H
 #define ORBGPU_PROJ_H
@@ -33,7 +45,17 @@ enum {
     ORBGPU_PROJ_LOCAL = 0,      /* SearchByProjection(F, vpMapPoints, th)          */
     ORBGPU_PROJ_SIM3 = 1,       /* SearchByProjection(KF, Scw, vpPoints, vpMatched) */
     ORBGPU_PROJ_LAST_FRAME = 2, /* SearchByProjection(F, LastF, th, bMono)          */
-    ORBGPU_PROJ_KEYFRAME = 3    /* SearchByProjection(F, KF, sAlreadyFound, th, d)  */
+    ORBGPU_PROJ_KEYFRAME = 3,   /* SearchByProjection(F, KF, sAlreadyFound, th, d)  */
+    /* per-point variants (the output row is indexed by point, see below) */
+    ORBGPU_PROJ_FUSE = 4,       /* Fuse(pKF, vpMapPoints, th): target Tcw = the keyframe's pose,
+                                   u_right = mvuRight (chi-square 7.8 / 5.99 test), points need
+                                   pos, normal, min_dist, max_dist, desc                     */
+    ORBGPU_PROJ_FUSE_SIM3 = 5,  /* Fuse(pKF, Scw, vpPoints, th, ...): target Tcw = Scw         */
+    ORBGPU_PROJ_SIM3_DIR = 6    /* one direction of SearchBySim3: last_Tcw = the points' own
+                                   keyframe pose [R1w|t1w], target Tcw = [sR21|t21], target
+                                   fx..cy = pKF1's (the reference projects both ways with
+                                   pKF1's intrinsics, ORBmatcher.cpp:1257-1260); points need
+                                   pos, min_dist, max_dist, desc                            */
 };
 
 /* Point flags */
@@ -95,18 +117,44 @@ int orbgpu_is_in_frustum_device(const orbgpu_proj_target* target, int n, const f
                                 int* d_flags, float* d_track, int* d_track_level, void* stream);
 
 /* Batched projection matching; d_calls and everything they point to on the
- * device.  Call c writes d_match + c*stride (one int per target keypoint):
+ * device.  Call c writes d_match + c*stride, for variants 0..3 one int per
+ * target keypoint:
  *   >= 0 : the point index assigned to that keypoint by this call
  *     -1 : untouched by this call
  *     -2 : set to NULL by the rotation-consistency cull (LAST_FRAME, KEYFRAME)
  * and d_nmatches[c] (the reference's return value; -1 if the target has
  * more than `stride` or 4096 keypoints -- rejected, never truncated).
+ * For the per-point variants (FUSE, FUSE_SIM3, SIM3_DIR) one int per POINT:
+ * the target keypoint with the smallest Hamming distance in the point's
+ * window (first in GetFeaturesInArea order on ties) when that distance is
+ * <= TH_LOW (Fuse) / TH_HIGH (SearchBySim3), else -1; d_nmatches[c] = the
+ * number of such points (-1: more than `stride` points or 4096 keypoints).
  * Descriptor arrays (target.desc, points.desc) are read as 16-byte vectors:
  * their device addresses must be 16-byte aligned (hipMalloc's are). */
 int orbgpu_search_by_projection_batch_device(int ncalls, const orbgpu_proj_call* d_calls, int stride, int* d_match,
                                              int* d_nmatches, void* stream);
-/* Host form of one call: every pointer in *call is a host pointer. */
+/* Host form of one call: every pointer in *call is a host pointer; match
+ * holds target.n ints (points.n for the per-point variants). */
 int orbgpu_search_by_projection(const orbgpu_proj_call* call, int* match, int* nmatches);
+
+/* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
+ * (ORBmatcher.cpp:1253-1491): both directions in one launch, then the
+ * agreement check.  kf1/kf2: Tcw = each keyframe's pose, mvKeysUn,
+ * descriptors, bounds, scale pyramid (fx..cy are taken from kf1 for both
+ * directions, as the reference does).  pts1/pts2: GetMapPointMatches() of
+ * each keyframe, one entry per keypoint; flags VALID = non-NULL, !isBad() and
+ * not already matched (vbAlreadyMatched1 / vbAlreadyMatched2, :1282-1296).
+ * R12 row-major.  match12[i1] (kf1.n ints) = the KF2 keypoint whose MapPoint
+ * becomes vpMatches12[i1], or -1; *nfound = the return value. */
+typedef struct orbgpu_sim3_search {
+    orbgpu_proj_target kf1, kf2;
+    orbgpu_proj_points pts1, pts2;
+    float s12;
+    float R12[9];
+    float t12[3];
+    float th;
+} orbgpu_sim3_search;
+int orbgpu_search_by_sim3(const orbgpu_sim3_search* search, int* match12, int* nfound);
 
 #ifdef __cplusplus
 }

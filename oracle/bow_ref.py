@@ -208,3 +208,83 @@ def search_by_bow(mode, fvA, descA, angA, validA, fvB, descB, angB, validB, nnra
                 match[idx] = -1
                 nm -= 1
     return nm, np.array(match, np.int32)
+
+
+def search_for_triangulation(fv1, fv2, P, check_ori=True, only_stereo=False):
+    """ORBmatcher::SearchForTriangulation (M:755-951) with
+    CheckDistEpipolarLine (M:166-190).  fv: dict node -> [features]; P: the
+    pair's arrays (synth.triangulation_scenario layout; valid = the keyframe
+    has no MapPoint at that keypoint).  Returns (nmatches, match12[n1])."""
+    HL, TH_LOW = 30, 50
+    f32, f64 = np.float32, np.float64
+    factor = f32(HL) / f32(360.0)
+    k1, k2, F = P["kps1"], P["kps2"], np.asarray(P["F12"], np.float32).reshape(3, 3)
+    T, Cw = np.asarray(P["T2w"], np.float32).reshape(3, 4), np.asarray(P["Cw1"], np.float32)
+    C2 = [f32(f32(f64(T[r, 0]) * f64(Cw[0]) + f64(T[r, 1]) * f64(Cw[1]) + f64(T[r, 2]) * f64(Cw[2])) + T[r, 3])
+          for r in range(3)]
+    invz = f32(f32(1.0) / C2[2])
+    ex = f32(f32(f32(f32(P["fx2"]) * C2[0]) * invz) + f32(P["cx2"]))
+    ey = f32(f32(f32(f32(P["fy2"]) * C2[1]) * invz) + f32(P["cy2"]))
+    uR1, uR2 = P.get("u_right1"), P.get("u_right2")
+    sf, s2 = [f32(x) for x in P["scale_factors2"]], [f32(x) for x in P["level_sigma2_2"]]
+    n1 = len(k1)
+    match = [-1] * n1
+    matched2 = [False] * len(k2)
+    hist = [[] for _ in range(HL)]
+    nm = 0
+    for node in sorted(set(fv1) & set(fv2)):
+        for i1 in fv1[node]:
+            if not P["valid1"][i1]:
+                continue
+            st1 = uR1 is not None and f32(uR1[i1]) >= 0
+            if only_stereo and not st1:
+                continue
+            x1, y1 = f32(k1["x"][i1]), f32(k1["y"][i1])
+            a = f32(f32(f32(x1 * F[0, 0]) + f32(y1 * F[1, 0])) + F[2, 0])
+            b = f32(f32(f32(x1 * F[0, 1]) + f32(y1 * F[1, 1])) + F[2, 1])
+            c = f32(f32(f32(x1 * F[0, 2]) + f32(y1 * F[1, 2])) + F[2, 2])
+            best, bidx = TH_LOW, -1
+            for i2 in fv2[node]:
+                if matched2[i2] or not P["valid2"][i2]:
+                    continue
+                st2 = uR2 is not None and f32(uR2[i2]) >= 0
+                if only_stereo and not st2:
+                    continue
+                d = _dist(P["desc1"][i1], P["desc2"][i2])
+                if d > TH_LOW or d > best:
+                    continue
+                x2, y2, o2 = f32(k2["x"][i2]), f32(k2["y"][i2]), int(k2["octave"][i2])
+                if not st1 and not st2:
+                    dx, dy = f32(ex - x2), f32(ey - y2)
+                    if f32(f32(dx * dx) + f32(dy * dy)) < f32(f32(100) * sf[o2]):
+                        continue
+                num = f32(f32(f32(a * x2) + f32(b * y2)) + c)
+                den = f32(f32(a * a) + f32(b * b))
+                if den == f32(0):
+                    continue
+                dsqr = f32(f32(num * num) / den)
+                if f64(dsqr) < 3.84 * f64(s2[o2]):
+                    best, bidx = d, i2
+            if bidx < 0:
+                continue
+            match[i1] = bidx
+            matched2[bidx] = True
+            nm += 1
+            if check_ori:
+                rot = f32(f32(k1["angle"][i1]) - f32(k2["angle"][bidx]))
+                if rot < 0.0:
+                    rot = f32(rot + f32(360.0))
+                vv = float(f32(rot * factor))
+                bb = int(math.copysign(math.floor(abs(vv) + 0.5), vv))
+                if bb == HL:
+                    bb = 0
+                hist[bb].append(i1)
+    if check_ori:
+        i1_, i2_, i3_ = _three_maxima(hist)
+        for i in range(HL):
+            if i in (i1_, i2_, i3_):
+                continue
+            for idx in hist[i]:
+                match[idx] = -1
+                nm -= 1
+    return nm, np.array(match, np.int32)

@@ -305,3 +305,113 @@ def search_by_projection(variant, tgt, pts, th, nnratio=0.6, check_ori=True, orb
                 match[slot] = -2
                 nm -= 1
     return nm, np.array(match, np.int32)
+
+
+FUSE, FUSE_SIM3, SIM3_DIR = 4, 5, 6
+
+
+def radius_search(variant, tgt, pts, th, last_Tcw=None):
+    """The per-point searches: Fuse(pKF, vpMapPoints, th) (M:962-1115, FUSE),
+    Fuse(pKF, Scw, vpPoints, th, vpReplace) (M:1119-1249, FUSE_SIM3) and one
+    direction of SearchBySim3 (M:1305-1387, SIM3_DIR: last_Tcw = the points'
+    own keyframe pose, tgt Tcw = [sR|t], tgt fx..cy = pKF1's).  Returns
+    (count, best) with best[i] = the target keypoint of point i when its
+    distance is <= TH_LOW (Fuse) / TH_HIGH (SearchBySim3), else -1."""
+    k = tgt["kps"]
+    grid = Grid(tgt)
+    uR = tgt.get("u_right")
+    T = np.asarray(tgt["Tcw"], np.float32).reshape(4, 4)
+    sf = [f32(s) for s in tgt["scale_factors"]]
+    isig = [f32(f32(1.0) / f32(s * s)) for s in sf]  # mvInvLevelSigma2 = 1/(s*s)
+    if variant == FUSE_SIM3:  # M:1129-1133
+        scw = norm3(T[0, :3])
+        P = np.zeros((4, 4), np.float32)
+        P[:3, :3] = (T[:3, :3] / scw).astype(np.float32)
+        P[:3, 3] = (T[:3, 3] / scw).astype(np.float32)
+        O = camera_center(P)
+    elif variant == FUSE:
+        P, O = T, camera_center(T)  # pKF->GetCameraCenter()
+    else:
+        L = np.asarray(last_Tcw, np.float32).reshape(4, 4)
+    limit = TH_HIGH if variant == SIM3_DIR else TH_LOW
+    n = len(pts["flags"])
+    best_out = np.full(n, -1, np.int32)
+    for ip in range(n):
+        if not int(pts["flags"][ip]) & VALID:
+            continue
+        X = pts["pos"][ip]
+        if variant == SIM3_DIR:
+            pc = transform(T, transform(L, X))  # sR21*(R1w*X + t1w) + t21
+        else:
+            pc = transform(P, X)
+        if pc[2] < f32(0.0):
+            continue
+        invz = f32(f32(1) / pc[2])
+        u = f32(f32(f32(tgt["fx"]) * f32(pc[0] * invz)) + f32(tgt["cx"]))
+        v = f32(f32(f32(tgt["fy"]) * f32(pc[1] * invz)) + f32(tgt["cy"]))
+        if not (u >= f32(tgt["min_x"]) and u < f32(tgt["max_x"]) and v >= f32(tgt["min_y"]) and
+                v < f32(tgt["max_y"])):  # KeyFrame::IsInImage
+            continue
+        ur = f32(u - f32(f32(tgt["bf"]) * invz))
+        maxd = f32(f32(1.2) * f32(pts["max_dist"][ip]))
+        mind = f32(f32(0.8) * f32(pts["min_dist"][ip]))
+        if variant == SIM3_DIR:
+            dist = norm3(pc)  # cv::norm(p3Dc2)
+        else:
+            PO = [f32(f32(X[j]) - O[j]) for j in range(3)]
+            dist = norm3(PO)
+        if dist < mind or dist > maxd:
+            continue
+        if variant != SIM3_DIR:  # viewing angle < 60 deg
+            Pn = pts["normal"][ip]
+            dot = f64(PO[0]) * f64(Pn[0]) + f64(PO[1]) * f64(Pn[1]) + f64(PO[2]) * f64(Pn[2])
+            if dot < 0.5 * f64(dist):
+                continue
+        lvl = predict_scale(pts["max_dist"][ip], dist, tgt)
+        rad = f32(f32(th) * sf[lvl])
+        cands = grid.area(u, v, rad)
+        best, best_i = 1 << 30, -1
+        for i in cands:
+            o = int(k["octave"][i])
+            if o < lvl - 1 or o > lvl:
+                continue
+            if variant == FUSE:  # M:1053-1078
+                ex = f32(u - f32(k["x"][i]))
+                ey = f32(v - f32(k["y"][i]))
+                e2 = f32(f32(ex * ex) + f32(ey * ey))
+                if uR is not None and f32(uR[i]) >= f32(0):
+                    er = f32(ur - f32(uR[i]))
+                    if f64(f32(f32(e2 + f32(er * er)) * isig[o & 15])) > 7.8:
+                        continue
+                elif f64(f32(e2 * isig[o & 15])) > 5.99:
+                    continue
+            d = _hamming(pts["desc"][ip], tgt["desc"][i])
+            if d < best:
+                best, best_i = d, i
+        if best_i >= 0 and best <= limit:
+            best_out[ip] = best_i
+    return int((best_out >= 0).sum()), best_out
+
+
+def search_by_sim3(kf1, kf2, pts1, pts2, s12, R12, t12, th):
+    """ORBmatcher::SearchBySim3 (M:1253-1491): both directions + agreement.
+    pts1/pts2 one entry per keypoint of kf1/kf2, VALID = non-NULL, !isBad,
+    not already matched.  Returns (nfound, match12[n1]) = KF2 keypoint or -1."""
+    R12 = np.asarray(R12, np.float32).reshape(3, 3)
+    t12 = np.asarray(t12, np.float32).reshape(3)
+    s12 = f32(s12)
+    sR12 = np.array([[f32(f64(R12[i, j]) * f64(s12)) for j in range(3)] for i in range(3)], np.float32)
+    inv = 1.0 / f64(s12)
+    sR21 = np.array([[f32(f64(R12[j, i]) * inv) for j in range(3)] for i in range(3)], np.float32)
+    t21 = np.array([-dotd3(sR21[i], t12) for i in range(3)], np.float32)
+    S21, S12 = np.eye(4, dtype=np.float32), np.eye(4, dtype=np.float32)
+    S21[:3, :3], S21[:3, 3] = sR21, t21
+    S12[:3, :3], S12[:3, 3] = sR12, t12
+    intr = {f: kf1[f] for f in ("fx", "fy", "cx", "cy")}
+    _, m1 = radius_search(SIM3_DIR, dict(kf2, Tcw=S21, **intr), pts1, th, last_Tcw=kf1["Tcw"])
+    _, m2 = radius_search(SIM3_DIR, dict(kf1, Tcw=S12, **intr), pts2, th, last_Tcw=kf2["Tcw"])
+    out = np.full(len(kf1["kps"]), -1, np.int32)
+    for i1, i2 in enumerate(m1):
+        if i2 >= 0 and m2[i2] == i1:
+            out[i1] = i2
+    return int((out >= 0).sum()), out

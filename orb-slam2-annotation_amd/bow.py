@@ -114,6 +114,48 @@ def search_by_bow(mode, fvA, descA, angA, validA, fvB, descB, angB, validB, nnra
     return nm.value, match[:nout]
 
 
+
+class TriangulationPair(ctypes.Structure):
+    _fields_ = [("kf1", BowFrame), ("kf2", BowFrame), ("kps1", ctypes.c_void_p), ("kps2", ctypes.c_void_p),
+                ("u_right1", ctypes.c_void_p), ("u_right2", ctypes.c_void_p), ("F12", ctypes.c_float * 9),
+                ("Cw1", ctypes.c_float * 3), ("T2w", ctypes.c_float * 12), ("fx2", ctypes.c_float),
+                ("fy2", ctypes.c_float), ("cx2", ctypes.c_float), ("cy2", ctypes.c_float),
+                ("scale_factors2", ctypes.c_float * 16), ("level_sigma2_2", ctypes.c_float * 16),
+                ("only_stereo", ctypes.c_int)]
+
+
+def search_for_triangulation(fv1, fv2, P, check_ori=True, only_stereo=False):
+    """ORBmatcher(0.6, checkOri).SearchForTriangulation on the GPU:
+    (nmatches, match12[n1]); P in synth.triangulation_scenario's layout."""
+    keep = []
+    T = TriangulationPair()
+    T.kf1 = _frame(fv1, P["desc1"], P["kps1"]["angle"], P["valid1"], keep)
+    T.kf2 = _frame(fv2, P["desc2"], P["kps2"]["angle"], P["valid2"], keep)
+    for name in ("kps1", "kps2"):
+        k = np.ascontiguousarray(P[name], orbgpu.KP_DTYPE)
+        keep.append(k)
+        setattr(T, name, k.ctypes.data)
+    for name in ("u_right1", "u_right2"):
+        if P.get(name) is not None:
+            a = np.ascontiguousarray(P[name], np.float32)
+            keep.append(a)
+            setattr(T, name, a.ctypes.data)
+    T.F12[:] = [float(x) for x in np.asarray(P["F12"], np.float32).reshape(9)]
+    T.Cw1[:] = [float(x) for x in np.asarray(P["Cw1"], np.float32).reshape(3)]
+    T.T2w[:] = [float(x) for x in np.asarray(P["T2w"], np.float32).reshape(12)]
+    T.fx2, T.fy2, T.cx2, T.cy2 = (float(P[k]) for k in ("fx2", "fy2", "cx2", "cy2"))
+    T.scale_factors2[:len(P["scale_factors2"])] = [float(x) for x in P["scale_factors2"]]
+    T.level_sigma2_2[:len(P["level_sigma2_2"])] = [float(x) for x in P["level_sigma2_2"]]
+    T.only_stereo = int(only_stereo)
+    n1 = T.kf1.n
+    match = np.zeros(max(n1, 1), np.int32)
+    nm = ctypes.c_int()
+    L = orbgpu.lib()
+    L.orbgpu_search_for_triangulation.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    orbgpu._check(L.orbgpu_search_for_triangulation(ctypes.byref(T), int(check_ori), match.ctypes.data,
+                                                    ctypes.byref(nm)), "orbgpu_search_for_triangulation")
+    return nm.value, match[:n1]
+
 # --------------------------------------------------------------------------
 # Batched, HBM-resident forms (torch tensors on the GPU)
 # --------------------------------------------------------------------------

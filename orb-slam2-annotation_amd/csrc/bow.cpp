@@ -312,4 +312,82 @@ int orbgpu_search_by_bow(int mode, const orbgpu_bow_frame* a, const orbgpu_bow_f
     return ORBGPU_OK;
 }
 
+int orbgpu_search_for_triangulation_batch_device(int batch, const orbgpu_triangulation_pair* d_pairs, int check_ori,
+                                                 int stride, int* d_match12, int* d_nmatches, void* stream) {
+    if (batch < 0 || stride <= 0 || stride > bow_max_stride() ||
+        (batch > 0 && (!d_pairs || !d_match12 || !d_nmatches)))
+        return fail(ORBGPU_ERR_ARG, "invalid argument (stride must be 1..4096)");
+    int rc = check_device();
+    if (rc) return rc;
+    ORB_HIP(launch_search_for_triangulation(batch, d_pairs, check_ori, stride, d_match12, d_nmatches,
+                                            (hipStream_t)stream));
+    return ORBGPU_OK;
+}
+
+int orbgpu_search_for_triangulation(const orbgpu_triangulation_pair* pair, int check_ori, int* match12,
+                                    int* nmatches) {
+    if (!pair || !match12 || !nmatches) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    const orbgpu_triangulation_pair& P = *pair;
+    const orbgpu_bow_frame* src[2] = {&P.kf1, &P.kf2};
+    for (const orbgpu_bow_frame* f : src) {
+        if (f->n < 0 || f->n > bow_max_stride() || f->fv_n < 0)
+            return fail(ORBGPU_ERR_ARG, "keyframe sizes out of range (<= 4096 features)");
+        if (f->n > 0 && (!f->desc || !f->angle || !f->valid))
+            return fail(ORBGPU_ERR_ARG, "missing descriptors / angles / valid flags");
+        if (f->fv_n > 0 && (!f->fv_nodes || !f->fv_offsets || !f->fv_features))
+            return fail(ORBGPU_ERR_ARG, "missing FeatureVector");
+    }
+    if ((P.kf1.n > 0 && !P.kps1) || (P.kf2.n > 0 && !P.kps2)) return fail(ORBGPU_ERR_ARG, "missing keypoints");
+    int rc = check_device();
+    if (rc) return rc;
+    std::vector<void*> allocs;
+    auto cleanup = [&]() {
+        for (void* p : allocs) (void)hipFree(p);
+    };
+    bool ok = true;
+    auto up = [&](const void* src_, size_t bytes) -> void* {
+        void* d = nullptr;
+        if (hipMalloc(&d, std::max<size_t>(bytes, 4)) != hipSuccess) {
+            ok = false;
+            return nullptr;
+        }
+        allocs.push_back(d);
+        if (src_ && bytes && hipMemcpy(d, src_, bytes, hipMemcpyHostToDevice) != hipSuccess) ok = false;
+        return d;
+    };
+    orbgpu_triangulation_pair d = P;
+    orbgpu_bow_frame* dst[2] = {&d.kf1, &d.kf2};
+    for (int i = 0; i < 2; ++i) {
+        const orbgpu_bow_frame& s = *src[i];
+        orbgpu_bow_frame& f = *dst[i];
+        f.fv_nodes = (const int*)up(s.fv_nodes, 4 * (size_t)s.fv_n);
+        f.fv_offsets = (const int*)up(s.fv_offsets, 4 * (size_t)(s.fv_n + 1));
+        const int nfeat = s.fv_n ? s.fv_offsets[s.fv_n] : 0;
+        f.fv_features = (const int*)up(s.fv_features, 4 * (size_t)nfeat);
+        f.desc = (const uint8_t*)up(s.desc, 32 * (size_t)s.n);
+        f.angle = (const float*)up(s.angle, 4 * (size_t)s.n);
+        f.valid = (const uint8_t*)up(s.valid, (size_t)s.n);
+    }
+    d.kps1 = (const orbgpu_keypoint*)up(P.kps1, sizeof(orbgpu_keypoint) * (size_t)P.kf1.n);
+    d.kps2 = (const orbgpu_keypoint*)up(P.kps2, sizeof(orbgpu_keypoint) * (size_t)P.kf2.n);
+    d.u_right1 = P.u_right1 ? (const float*)up(P.u_right1, 4 * (size_t)P.kf1.n) : nullptr;
+    d.u_right2 = P.u_right2 ? (const float*)up(P.u_right2, 4 * (size_t)P.kf2.n) : nullptr;
+    const int stride = std::max(std::max(P.kf1.n, P.kf2.n), 1);
+    orbgpu_triangulation_pair* dP = (orbgpu_triangulation_pair*)up(&d, sizeof(d));
+    int* dm = (int*)up(nullptr, 4 * (size_t)stride);
+    int* dn = (int*)up(nullptr, 4);
+    if (!ok) {
+        cleanup();
+        return fail(ORBGPU_ERR_HIP, "upload failed");
+    }
+    rc = orbgpu_search_for_triangulation_batch_device(1, dP, check_ori, stride, dm, dn, nullptr);
+    ok = !rc && hipDeviceSynchronize() == hipSuccess &&
+         (P.kf1.n == 0 || hipMemcpy(match12, dm, 4 * (size_t)P.kf1.n, hipMemcpyDeviceToHost) == hipSuccess) &&
+         hipMemcpy(nmatches, dn, 4, hipMemcpyDeviceToHost) == hipSuccess;
+    cleanup();
+    if (rc) return rc;
+    if (!ok) return fail(ORBGPU_ERR_HIP, "SearchForTriangulation failed");
+    return ORBGPU_OK;
+}
+
 }  // extern "C"

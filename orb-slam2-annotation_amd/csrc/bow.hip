@@ -19,6 +19,12 @@
 //                          and one lane walks one common node sequentially
 //                          (ORBmatcher.cpp:205-348, :604-743); the rotation
 //                          histogram, ComputeThreeMaxima and the cull follow.
+//   triangulation_kernel   ORBmatcher::SearchForTriangulation (ORBmatcher.cpp:
+//                          755-951) in the same shape: one block per keyframe
+//                          pair, one lane per common node, the reference's
+//                          inner loop (TH_LOW gate, last passing candidate
+//                          among equal distances, epipole distance for
+//                          monocular pairs, CheckDistEpipolarLine :166-190).
 #include "../../include/orbgpu_bow.h"
 #include "bow_kernels.h"
 
@@ -330,6 +336,129 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
     if (threadIdx.x == 0) nmatches[blockIdx.x] = s_cnt;
 }
 
+// ComputeThreeMaxima (ORBmatcher.cpp:1792-1833) over s_hist into s_ind[3]
+__device__ inline void three_maxima(const int* s_hist, int* s_ind) {
+    int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+    for (int i = 0; i < kHL; ++i) {
+        const int s = s_hist[i];
+        if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+        else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+        else if (s > max3) { max3 = s; ind3 = i; }
+    }
+    if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+    else if ((float)max3 < 0.1f * (float)max1) ind3 = -1;
+    s_ind[0] = ind1;
+    s_ind[1] = ind2;
+    s_ind[2] = ind3;
+}
+
+__global__ __launch_bounds__(256) void triangulation_kernel(const orbgpu_triangulation_pair* __restrict__ pairs,
+                                                            int check_ori, int stride, int* __restrict__ match_g,
+                                                            int* __restrict__ nmatches) {
+    __shared__ unsigned int s_used[kMaxStride / 32];  // vbMatched2
+    __shared__ signed char s_bin[kMaxStride];
+    __shared__ int s_hist[kHL];
+    __shared__ int s_ind[3];
+    __shared__ int s_cnt;
+    __shared__ float s_e[2];  // epipole (ex, ey)
+    const orbgpu_triangulation_pair& P = pairs[blockIdx.x];
+    const orbgpu_bow_frame& A = P.kf1;
+    const orbgpu_bow_frame& B = P.kf2;
+    int* match = match_g + (size_t)blockIdx.x * stride;
+    if (A.n > stride || B.n > stride) {  // rejected, never truncated
+        if (threadIdx.x == 0) nmatches[blockIdx.x] = -1;
+        return;
+    }
+    for (int i = threadIdx.x; i < A.n; i += blockDim.x) {
+        match[i] = -1;
+        s_bin[i] = -1;
+    }
+    for (int i = threadIdx.x; i < kMaxStride / 32; i += blockDim.x) s_used[i] = 0;
+    if (threadIdx.x < kHL) s_hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+        s_cnt = 0;
+        // C2 = R2w*Cw + t2w (cv::Mat product accumulated in double), epipole (:763-770)
+        float C2[3];
+        for (int r = 0; r < 3; ++r)
+            C2[r] = (float)((double)P.T2w[4 * r] * P.Cw1[0] + (double)P.T2w[4 * r + 1] * P.Cw1[1] +
+                            (double)P.T2w[4 * r + 2] * P.Cw1[2]) + P.T2w[4 * r + 3];
+        const float invz = 1.0f / C2[2];
+        s_e[0] = P.fx2 * C2[0] * invz + P.cx2;
+        s_e[1] = P.fy2 * C2[1] * invz + P.cy2;
+    }
+    __syncthreads();
+    const float ex = s_e[0], ey = s_e[1];
+    const float* F = P.F12;
+    const float factor = (float)kHL / 360.0f;
+    for (int a = threadIdx.x; a < A.fv_n; a += blockDim.x) {
+        const int b = find_node(B.fv_nodes, B.fv_n, A.fv_nodes[a]);
+        if (b < 0) continue;
+        const int a0 = A.fv_offsets[a], a1 = A.fv_offsets[a + 1];
+        const int b0 = B.fv_offsets[b], b1 = B.fv_offsets[b + 1];
+        for (int ia_ = a0; ia_ < a1; ++ia_) {
+            const int idx1 = A.fv_features[ia_];
+            if (!A.valid[idx1]) continue;  // pKF1 already has a MapPoint there
+            const bool stereo1 = P.u_right1 && P.u_right1[idx1] >= 0.0f;
+            if (P.only_stereo && !stereo1) continue;
+            const orbgpu_keypoint kp1 = P.kps1[idx1];
+            // epipolar line of kp1 in KF2 (CheckDistEpipolarLine), the same for every candidate
+            const float la = kp1.x * F[0] + kp1.y * F[3] + F[6];
+            const float lb = kp1.x * F[1] + kp1.y * F[4] + F[7];
+            const float lc = kp1.x * F[2] + kp1.y * F[5] + F[8];
+            const float den = la * la + lb * lb;
+            const uint8_t* d1 = A.desc + 32 * (size_t)idx1;
+            int bestDist = kThLow, bestIdx2 = -1;
+            for (int ib_ = b0; ib_ < b1; ++ib_) {
+                const int idx2 = B.fv_features[ib_];
+                if (((s_used[idx2 >> 5] >> (idx2 & 31)) & 1u) || !B.valid[idx2]) continue;
+                const bool stereo2 = P.u_right2 && P.u_right2[idx2] >= 0.0f;
+                if (P.only_stereo && !stereo2) continue;
+                const int dist = hamming32(d1, B.desc + 32 * (size_t)idx2);
+                if (dist > kThLow || dist > bestDist) continue;
+                const orbgpu_keypoint kp2 = P.kps2[idx2];
+                if (!stereo1 && !stereo2) {  // too close to the epipole: the point is too close to KF1
+                    const float dx = ex - kp2.x, dy = ey - kp2.y;
+                    if (dx * dx + dy * dy < 100 * P.scale_factors2[kp2.octave & 15]) continue;
+                }
+                if (den == 0.0f) continue;
+                const float num = la * kp2.x + lb * kp2.y + lc;
+                const float dsqr = num * num / den;
+                if ((double)dsqr < 3.84 * (double)P.level_sigma2_2[kp2.octave & 15]) {
+                    bestIdx2 = idx2;
+                    bestDist = dist;
+                }
+            }
+            if (bestIdx2 < 0) continue;
+            match[idx1] = bestIdx2;
+            atomicOr(&s_used[bestIdx2 >> 5], 1u << (bestIdx2 & 31));
+            if (check_ori) {
+                float rot = A.angle[idx1] - B.angle[bestIdx2];
+                if (rot < 0.0f) rot += 360.0f;
+                int bin = (int)roundf(rot * factor);
+                if (bin == kHL) bin = 0;
+                s_bin[idx1] = (signed char)bin;
+                atomicAdd(&s_hist[bin], 1);
+            }
+        }
+    }
+    __syncthreads();
+    if (check_ori && threadIdx.x == 0) three_maxima(s_hist, s_ind);
+    __syncthreads();
+    int cnt = 0;
+    for (int i = threadIdx.x; i < A.n; i += blockDim.x) {
+        if (match[i] < 0) continue;
+        const int bin = s_bin[i];
+        if (check_ori && bin != s_ind[0] && bin != s_ind[1] && bin != s_ind[2]) {
+            match[i] = -1;
+            continue;
+        }
+        ++cnt;
+    }
+    atomicAdd(&s_cnt, cnt);
+    __syncthreads();
+    if (threadIdx.x == 0) nmatches[blockIdx.x] = s_cnt;
+}
+
 }  // namespace
 
 int bow_max_stride() { return kMaxStride; }
@@ -353,6 +482,14 @@ hipError_t launch_search_by_bow(int mode, int batch, const orbgpu_bow_frame* a, 
     if (batch <= 0) return hipSuccess;
     hipLaunchKernelGGL(search_by_bow_kernel, dim3(batch), dim3(256), 0, stream, mode, a, b, nnratio, check_ori,
                        stride, match, nmatches);
+    return hipGetLastError();
+}
+
+hipError_t launch_search_for_triangulation(int batch, const orbgpu_triangulation_pair* pairs, int check_ori, int stride,
+                                          int* match, int* nmatches, hipStream_t stream) {
+    if (batch <= 0) return hipSuccess;
+    hipLaunchKernelGGL(triangulation_kernel, dim3(batch), dim3(256), 0, stream, pairs, check_ori, stride, match,
+                       nmatches);
     return hipGetLastError();
 }
 

@@ -27,4 +27,7 @@ hipError_t launch_search_by_bow(int mode, int batch, const orbgpu_bow_frame* a, 
                                 float nnratio, int check_ori, int stride, int* match, int* nmatches,
                                 hipStream_t stream);
 
+hipError_t launch_search_for_triangulation(int batch, const orbgpu_triangulation_pair* pairs, int check_ori, int stride,
+                                          int* match, int* nmatches, hipStream_t stream);
+
 }  // namespace orbgpu

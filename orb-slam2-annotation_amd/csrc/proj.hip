@@ -1,5 +1,7 @@
 // proj.hip -- the projection matchers (include/orbgpu_proj.h):
-// Frame::isInFrustum and the four ORBmatcher::SearchByProjection overloads.
+// Frame::isInFrustum, the four ORBmatcher::SearchByProjection overloads and
+// the per-point radius searches of ORBmatcher::Fuse (both overloads) and
+// SearchBySim3 (one direction per call).
 //
 // One 1024-thread block per call (proj_kernel, below): the target's feature
 // grid in LDS, every point's projection and candidate list built by 15
@@ -59,8 +61,13 @@ struct Query {
     float ur;            // stereo: projected right coordinate (LOCAL, LAST_FRAME)
     float stereo_r;      // stereo tolerance
     bool stereo;
-    int level_lo, level_hi;  // SIM3: keypoint level window applied after the area query
+    bool chi2;               // FUSE: the reprojection chi-square test (ORBmatcher.cpp:1053-1078)
+    int level_lo, level_hi;  // SIM3 / FUSE* / SIM3_DIR: keypoint level window applied after the area query
 };
+
+// variants that report one result per point (best keypoint in the window,
+// no hidden set, no sequential walk)
+__device__ inline bool per_point(int variant) { return variant >= ORBGPU_PROJ_FUSE; }
 
 // Per-call pose quantities shared by every point of the call.
 struct CallPose {
@@ -73,7 +80,7 @@ __device__ inline CallPose call_pose(const orbgpu_proj_call& C) {
     CallPose cp{};
     const orbgpu_proj_target& T = C.target;
     const float* Tcw = T.Tcw;
-    if (C.variant == ORBGPU_PROJ_SIM3) {  // ORBmatcher.cpp:361-371
+    if (C.variant == ORBGPU_PROJ_SIM3 || C.variant == ORBGPU_PROJ_FUSE_SIM3) {  // ORBmatcher.cpp:361-371, :1129-1133
         const float row0[3] = {Tcw[0], Tcw[1], Tcw[2]};
         const float scw = (float)sqrt((double)row0[0] * row0[0] + (double)row0[1] * row0[1] + (double)row0[2] * row0[2]);
         for (int i = 0; i < 3; ++i) {
@@ -81,6 +88,8 @@ __device__ inline CallPose call_pose(const orbgpu_proj_call& C) {
             cp.Rs[4 * i + 3] = Tcw[4 * i + 3] / scw;
         }
         camera_center(cp.Rs, cp.O);
+    } else if (C.variant == ORBGPU_PROJ_FUSE) {  // pKF->GetCameraCenter() (KeyFrame::SetPose: Ow = -Rcw^T tcw)
+        camera_center(Tcw, cp.O);
     } else if (C.variant == ORBGPU_PROJ_LAST_FRAME || C.variant == ORBGPU_PROJ_KEYFRAME) {
         float twc[3];
         camera_center(Tcw, twc);  // twc = -Rcw^T tcw (= Ow)
@@ -119,12 +128,14 @@ __device__ inline Query make_query(const orbgpu_proj_call& C, const CallPose& cp
             maxd0 = P.max_dist[ip];
             mind0 = P.min_dist[ip];
         }
-        if (variant == ORBGPU_PROJ_SIM3)
+        if (variant == ORBGPU_PROJ_SIM3 || variant == ORBGPU_PROJ_FUSE || variant == ORBGPU_PROJ_FUSE_SIM3)
             for (int k = 0; k < 3; ++k) Pn[k] = P.normal[3 * ip + k];
         if (variant == ORBGPU_PROJ_LAST_FRAME) lv = P.octave[ip];
     }
     Query q{};
-    if (C.check_ori && variant != ORBGPU_PROJ_LOCAL && variant != ORBGPU_PROJ_SIM3) q.angle = P.angle[ip];
+    if (C.check_ori && (variant == ORBGPU_PROJ_LAST_FRAME || variant == ORBGPU_PROJ_KEYFRAME)) q.angle = P.angle[ip];
+    q.level_lo = -1000;
+    q.level_hi = 1000;
     q.flags = fl;
     q.ok = (fl & ORBGPU_PT_VALID) != 0;
     if (variant == ORBGPU_PROJ_LOCAL) {  // ORBmatcher.cpp:68-91
@@ -143,10 +154,12 @@ __device__ inline Query make_query(const orbgpu_proj_call& C, const CallPose& cp
             q.level_lo = -1000;
             q.level_hi = 1000;
         }
-    } else if (variant == ORBGPU_PROJ_SIM3) {  // ORBmatcher.cpp:376-420
+    } else if (variant == ORBGPU_PROJ_SIM3 || variant == ORBGPU_PROJ_FUSE || variant == ORBGPU_PROJ_FUSE_SIM3) {
+        // SIM3: ORBmatcher.cpp:376-420; FUSE: :987-1030 (Rcw, tcw of the keyframe,
+        // then the same tests); FUSE_SIM3: :1149-1198 (the scale removed as in SIM3)
         if (q.ok) {
             float pc[3];
-            transform(cp.Rs, X, pc);
+            transform(variant == ORBGPU_PROJ_FUSE ? T.Tcw : cp.Rs, X, pc);
             if (pc[2] < 0.0f) q.ok = false;
             else {
                 const float invz = 1 / pc[2];
@@ -154,6 +167,7 @@ __device__ inline Query make_query(const orbgpu_proj_call& C, const CallPose& cp
                 q.u = T.fx * x + T.cx;
                 q.v = T.fy * y + T.cy;
                 if (!(q.u >= T.min_x && q.u < T.max_x && q.v >= T.min_y && q.v < T.max_y)) q.ok = false;  // IsInImage
+                q.ur = q.u - T.bf * invz;  // FUSE (:1008)
             }
             if (q.ok) {
                 const float maxd = 1.2f * maxd0, mind = 0.8f * mind0;
@@ -169,9 +183,37 @@ __device__ inline Query make_query(const orbgpu_proj_call& C, const CallPose& cp
                         q.min_level = -1;
                         q.max_level = -1;
                         q.stereo = false;
+                        q.chi2 = variant == ORBGPU_PROJ_FUSE;
                         q.level_lo = lvl - 1;
                         q.level_hi = lvl;
                     }
+                }
+            }
+        }
+    } else if (variant == ORBGPU_PROJ_SIM3_DIR) {  // SearchBySim3, one direction (ORBmatcher.cpp:1305-1387)
+        if (q.ok) {
+            float pc1[3], pc[3];
+            transform(C.last_Tcw, X, pc1);  // the points' own keyframe: R1w*p3Dw + t1w
+            transform(T.Tcw, pc1, pc);      // the similarity: sR21*p3Dc1 + t21
+            if (pc[2] < 0.0f) q.ok = false;
+            else {
+                const float invz = 1 / pc[2];
+                const float x = pc[0] * invz, y = pc[1] * invz;
+                q.u = T.fx * x + T.cx;
+                q.v = T.fy * y + T.cy;
+                if (!(q.u >= T.min_x && q.u < T.max_x && q.v >= T.min_y && q.v < T.max_y)) q.ok = false;
+            }
+            if (q.ok) {
+                const float maxd = 1.2f * maxd0, mind = 0.8f * mind0;
+                const float dist = (float)sqrt((double)pc[0] * pc[0] + (double)pc[1] * pc[1] + (double)pc[2] * pc[2]);
+                if (dist < mind || dist > maxd) q.ok = false;
+                else {
+                    const int lvl = predict_scale(maxd0, dist, T);
+                    q.r = C.th * sf[lvl];
+                    q.min_level = -1;
+                    q.max_level = -1;
+                    q.level_lo = lvl - 1;
+                    q.level_hi = lvl;
                 }
             }
         }
@@ -232,6 +274,7 @@ struct Grid {
     const unsigned short* cell_start;
     const unsigned* hidw;             // hidden-slot bitmap: slot i is bit i & 31 of word i >> 5
     const uint4* desc;                // by slot, 2 x 16 bytes (LDS copy or the target's HBM array)
+    const float* isig;                // mvInvLevelSigma2 by octave (FUSE's chi-square test)
 };
 
 __device__ inline int kp_slot(const float4& k) { return (int)(__float_as_uint(k.w) & 0xFFFu); }
@@ -284,10 +327,21 @@ __device__ inline void scan_candidates(const orbgpu_proj_call& C, const Query& q
         }
         if (!(fabsf(k.x - q.u) < q.r && fabsf(k.y - q.v) < q.r)) continue;
         if ((g.hidw[idx >> 5] >> (idx & 31)) & 1u) continue;
-        if (C.variant == ORBGPU_PROJ_SIM3 && (oct < q.level_lo || oct > q.level_hi)) continue;
+        if (oct < q.level_lo || oct > q.level_hi) continue;
         if (q.stereo && k.z > 0) {
             const float er = fabsf(q.ur - k.z);
             if (er > q.stereo_r) continue;
+        }
+        if (q.chi2) {  // Fuse: e2 * mvInvLevelSigma2[kpLevel] against 7.8 (stereo) / 5.99 (double literals)
+            const float ex = q.u - k.x, ey = q.v - k.y;
+            float e2 = ex * ex + ey * ey;
+            double lim = 5.99;
+            if (k.z >= 0.0f) {
+                const float er = q.ur - k.z;
+                e2 = e2 + er * er;
+                lim = 7.8;
+            }
+            if ((double)(e2 * g.isig[oct & 15]) > lim) continue;
         }
         const uint4 ea = g.desc[2 * idx], eb = g.desc[2 * idx + 1];
         const int dist = __popc(pa.x ^ ea.x) + __popc(pa.y ^ ea.y) + __popc(pa.z ^ ea.z) + __popc(pa.w ^ ea.w) +
@@ -376,7 +430,8 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
     __shared__ uint2 s_list[2][kChunk][kListK];    // (key, aux) per list entry
     __shared__ int s_ncand[2][kChunk];             // candidate count | has-observations << 30; -1: no query
     __shared__ int s_hist[kHL];
-    __shared__ float s_sf[16];
+    __shared__ float s_sf[16], s_isig[16];
+    __shared__ int s_nm;  // per-point variants: accepted points
     extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
     const orbgpu_proj_call& C = calls[blockIdx.x];
     const orbgpu_proj_target& T = C.target;
@@ -388,11 +443,14 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
 #endif
     PSTAMP(0);
     const int n = T.n;
-    if (n > stride || n > kMaxKps) {
+    const int variant = C.variant, np = P.n;
+    const bool perpoint = per_point(variant);
+    // the output row holds one entry per target keypoint (per point for the per-point variants)
+    if (n > kMaxKps || (perpoint ? np : n) > stride) {
         if (tid == 0) nmatches[blockIdx.x] = -1;
         return;
     }
-    const int variant = C.variant, hmin = hidden_min(variant), np = P.n;
+    const int hmin = perpoint ? 3 : hidden_min(variant);  // per-point variants hide nothing
     const bool desc_lds = n <= kDescLds;
     const int nr = (n + 3) & ~3;
     float4* s_kp = reinterpret_cast<float4*>(s_dyn);
@@ -405,7 +463,7 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
     // ---- phase 1: grid (PosInGrid with C round, Frame.cpp:434-443) by a counting sort over the cells
     const float invW = (float)kGC / (T.max_x - T.min_x), invH = (float)kGR / (T.max_y - T.min_y);
     for (int c = tid; c < kCells; c += kProjThreads) s_cnt[c] = 0;
-    if (const uint8_t* occ = T.occupied) {  // hidden-slot bitmap, 64 slots per ballot
+    if (const uint8_t* occ = perpoint ? nullptr : T.occupied) {  // hidden-slot bitmap, 64 slots per ballot
         for (int i0 = wave * 64; i0 < n; i0 += kProjThreads) {
             const int i = i0 + lane;
             const unsigned long long m = __ballot(i < n && occ[i] >= hmin);
@@ -418,7 +476,12 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
         for (int w = tid; w < kMaxKps / 32; w += kProjThreads) s_hidw[w] = 0;
     }
     if (tid < kHL) s_hist[tid] = 0;
-    if (tid < 16) s_sf[tid] = tid < T.n_levels ? T.scale_factors[tid] : 0.0f;
+    if (tid < 16) {
+        const float sfl = tid < T.n_levels ? T.scale_factors[tid] : 0.0f;
+        s_sf[tid] = sfl;
+        s_isig[tid] = 1.0f / (sfl * sfl);  // mvInvLevelSigma2 = 1 / (s * s) (ORBextractor.cpp:428-433)
+    }
+    if (tid == 0) s_nm = 0;
     if (desc_lds) {  // the descriptors, 16 bytes per thread and step
         const uint4* gd = reinterpret_cast<const uint4*>(T.desc);
         for (int i = tid; i < 2 * n; i += kProjThreads) s_desc[i] = gd[i];
@@ -499,7 +562,8 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
         s_bins[i] = 0u;
     }
     PSTAMP(1);
-    const Grid g{s_kp, s_cell_start, s_hidw, desc_lds ? s_desc : reinterpret_cast<const uint4*>(T.desc)};
+    const Grid g{s_kp, s_cell_start, s_hidw, desc_lds ? s_desc : reinterpret_cast<const uint4*>(T.desc), s_isig};
+    const int pp_max = variant == ORBGPU_PROJ_SIM3_DIR ? kThHigh : kThLow;  // per-point acceptance
     const CallPose cp = call_pose(C);
     const bool hist = C.check_ori && (variant == ORBGPU_PROJ_LAST_FRAME || variant == ORBGPU_PROJ_KEYFRAME);
     // list of chunk ch into buffer ch & 1, by waves w0..15 (nw waves), kSub lanes per point
@@ -543,14 +607,22 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
                 for (int o = 0; o < kSub - 1; ++o)
 #pragma unroll
                     for (int t = 0; t < kListK; ++t) rank += other[o][t] < top[k] ? 1 : 0;
-                if (rank < kListK) {
+                if (perpoint) {  // the group minimum = the reference's first best in window order
+                    if (rank == 0) {
+                        const bool okd = key_dist(top[k]) <= pp_max;
+                        match[ip] = okd ? kp_slot(s_kp[key_pos(top[k])]) : -1;
+                        if (okd) atomicAdd(&s_nm, 1);
+                    }
+                } else if (rank < kListK) {
                     const float4 kq = s_kp[key_pos(top[k])];
                     const int oct = max(-128, min(127, kp_octave(kq)));
                     const unsigned bin = hist ? (unsigned)rot_bin(q.angle, s_kang[key_pos(top[k])]) : 0u;
                     s_list[buf][j][rank] = make_uint2(top[k], (unsigned)kp_slot(kq) | bin << 12 | ((unsigned)oct & 0xFFu) << 17);
                 }
             }
-            if (sl == 0) {
+            if (perpoint) {
+                if (sl == 0 && cnt == 0) match[ip] = -1;  // no query or an empty window
+            } else if (sl == 0) {
                 for (int k = min(cnt, kListK); k < kListK; ++k) s_list[buf][j][k] = make_uint2(kNoKey, 0u);
                 s_ncand[buf][j] = q.ok ? cnt | ((q.flags & ORBGPU_PT_HAS_OBS) ? (1 << 30) : 0) : -1;
             }
@@ -558,6 +630,12 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
     };
     __syncthreads();
     const int nchunks = (np + kChunk - 1) / kChunk;
+    if (perpoint) {  // Fuse / SearchBySim3: independent points, every wave builds
+        for (int ch = 0; ch < nchunks; ++ch) build(ch, 0, kProjThreads / 64);
+        __syncthreads();
+        if (tid == 0) nmatches[blockIdx.x] = s_nm;
+        return;
+    }
     if (nchunks > 0) build(0, 0, kProjThreads / 64);
     if (wave == 0)  // matches start NULL; wave 0 owns every later write of match[]
         for (int i = lane; i < n; i += 64) match[i] = -1;

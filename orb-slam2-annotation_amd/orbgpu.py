@@ -151,6 +151,7 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_is_in_frustum_device.argtypes = [vp, i, vp, vp, vp, vp, f, vp, vp, vp, vp]
         L.orbgpu_search_by_projection_batch_device.argtypes = [i, vp, i, vp, vp, vp]
         L.orbgpu_search_by_projection.argtypes = [vp, vp, vp]
+        L.orbgpu_search_by_sim3.argtypes = [vp, vp, vp]
         _LIB = L
     return _LIB
 

@@ -1,6 +1,8 @@
 """Host-side mirror of the projection matchers over include/orbgpu_proj.h:
-``is_in_frustum`` (Frame::isInFrustum) and ``search_by_projection`` (the
-four ORBmatcher::SearchByProjection overloads)."""
+``is_in_frustum`` (Frame::isInFrustum), ``search_by_projection`` (the four
+ORBmatcher::SearchByProjection overloads), ``radius_search`` (the per-point
+searches of ORBmatcher::Fuse, both overloads, and of one SearchBySim3
+direction) and ``search_by_sim3`` (ORBmatcher::SearchBySim3)."""
 from __future__ import annotations
 
 import ctypes
@@ -10,6 +12,7 @@ import numpy as np
 import orbgpu
 
 LOCAL, SIM3, LAST_FRAME, KEYFRAME = 0, 1, 2, 3
+FUSE, FUSE_SIM3, SIM3_DIR = 4, 5, 6
 VALID, HAS_OBS, IN_VIEW = 1, 2, 4
 vp = ctypes.c_void_p
 
@@ -85,12 +88,39 @@ def search_by_projection(variant, tgt, pts, th, nnratio=0.6, check_ori=True, orb
         C.last_Tcw[:] = [float(v) for v in np.asarray(last_Tcw, np.float32).reshape(16)]
     C.target = _target(tgt, keep)
     C.points = _points(pts, keep)
-    n = C.target.n
+    n = C.points.n if variant >= FUSE else C.target.n  # per-point variants: one entry per point
     match = np.zeros(max(n, 1), np.int32)
     nm = ctypes.c_int()
     orbgpu._check(orbgpu.lib().orbgpu_search_by_projection(ctypes.byref(C), match.ctypes.data, ctypes.byref(nm)),
                   "orbgpu_search_by_projection")
     return nm.value, match[:n]
+
+
+def radius_search(variant, tgt, pts, th, last_Tcw=None):
+    """FUSE / FUSE_SIM3 / SIM3_DIR: (count, best keypoint per point or -1)."""
+    return search_by_projection(variant, tgt, pts, th, last_Tcw=last_Tcw)
+
+
+class Sim3Search(ctypes.Structure):
+    _fields_ = [("kf1", Target), ("kf2", Target), ("pts1", Points), ("pts2", Points), ("s12", ctypes.c_float),
+                ("R12", ctypes.c_float * 9), ("t12", ctypes.c_float * 3), ("th", ctypes.c_float)]
+
+
+def search_by_sim3(kf1, kf2, pts1, pts2, s12, R12, t12, th):
+    """ORBmatcher::SearchBySim3: (nfound, match12[n1] = KF2 keypoint or -1)."""
+    keep = []
+    S = Sim3Search()
+    S.kf1, S.kf2 = _target(kf1, keep), _target(kf2, keep)
+    S.pts1, S.pts2 = _points(pts1, keep), _points(pts2, keep)
+    S.s12, S.th = float(s12), float(th)
+    S.R12[:] = [float(v) for v in np.asarray(R12, np.float32).reshape(9)]
+    S.t12[:] = [float(v) for v in np.asarray(t12, np.float32).reshape(3)]
+    n1 = S.kf1.n
+    match = np.zeros(max(n1, 1), np.int32)
+    nf = ctypes.c_int()
+    orbgpu._check(orbgpu.lib().orbgpu_search_by_sim3(ctypes.byref(S), match.ctypes.data, ctypes.byref(nf)),
+                  "orbgpu_search_by_sim3")
+    return nf.value, match[:n1]
 
 
 def is_in_frustum(tgt, pts, cos_limit):

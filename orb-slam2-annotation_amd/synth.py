@@ -378,6 +378,182 @@ def projection_scenario(n_points: int, n_distractors: int, seed: int, stereo: bo
     return tgt, pts
 
 
+
+def _kf_target(kps, desc, T, rng, stereo=False):
+    """a keyframe dict in the layout of proj.py / proj_ref.py"""
+    fx, fy, cx, cy = 517.3, 516.5, 318.6, 255.3
+    sf = (np.float32(1.2) ** np.arange(8)).astype(np.float32)
+    kp_arr = np.zeros(len(kps), dtype=[("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                                       ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+    for o, k in enumerate(kps):
+        kp_arr[o] = k
+    return {"kps": kp_arr, "desc": np.array(desc, np.uint8).reshape(-1, 32),
+            "u_right": np.where(rng.uniform(size=len(kp_arr)) < 0.5, kp_arr["x"] - rng.uniform(5, 40, len(kp_arr)),
+                                -1.0).astype(np.float32) if stereo else None,
+            "occupied": None, "min_x": 0.0, "max_x": 640.0, "min_y": 0.0, "max_y": 480.0, "fx": fx, "fy": fy,
+            "cx": cx, "cy": cy, "bf": 40.0, "b": 0.08, "n_levels": 8,
+            "log_scale_factor": float(np.log(np.float32(1.2))), "scale_factors": sf,
+            "Tcw": np.asarray(T, np.float32)}
+
+
+def sim3_search_scenario(n_points: int, n_distractors: int, seed: int, s12: float = 1.15,
+                         already: float = 0.15, bad: float = 0.05):
+    """Two keyframes of a loop (ORBmatcher::SearchBySim3): world points seen by
+    KF1 (map 1) and, through the similarity S12 = [s12 R12 | t12] (camera 2 ->
+    camera 1), by KF2 in its own map.  Every keypoint carries a MapPoint
+    entry (one per keypoint; distractor keypoints have none); `already` of
+    the common points are marked as matched in both (vbAlreadyMatched1/2)
+    and `bad` as isBad().  Returns (kf1, kf2, pts1, pts2, s12, R12, t12)."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = 517.3, 516.5, 318.6, 255.3
+    sf = (np.float32(1.2) ** np.arange(8)).astype(np.float32)
+    T1 = _pose(rng)
+    R12 = _rot(rng, 0.2)
+    t12 = rng.uniform(-0.3, 0.3, 3)
+    z = rng.uniform(1.5, 8.0, n_points)
+    u = rng.uniform(-20, 660, n_points)
+    v = rng.uniform(-20, 500, n_points)
+    pc1 = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], 1)
+    X1 = (pc1 - T1[:3, 3]) @ T1[:3, :3]
+    pc2 = ((pc1 - t12) @ R12) / s12  # p3Dc1 = s12 R12 p3Dc2 + t12
+    T2 = _pose(rng)
+    X2 = (pc2 - T2[:3, 3]) @ T2[:3, :3]
+    pdesc = rng.integers(0, 256, (n_points, 32), dtype=np.uint8)
+    lvl_ref = rng.integers(0, 8, n_points)
+    common = rng.uniform(size=n_points) < 0.6
+
+    def view(pc, X, only):
+        kps, desc, owner = [], [], []
+        d = np.linalg.norm(pc, axis=1)
+        maxd = (d * rng.uniform(0.9, 1.1, n_points) * sf[lvl_ref]).astype(np.float32)
+        for i in range(n_points):
+            if only is not None and not only[i]:
+                continue
+            if pc[i, 2] <= 0:
+                continue
+            uu, vv = fx * pc[i, 0] / pc[i, 2] + cx, fy * pc[i, 1] / pc[i, 2] + cy
+            if not (0 <= uu < 640 and 0 <= vv < 480):
+                continue
+            lv = int(np.clip(np.ceil(np.log(maxd[i] / d[i]) / np.log(1.2)), 0, 7)) + int(rng.integers(-1, 2))
+            lv = int(np.clip(lv, 0, 7))
+            bits = np.unpackbits(pdesc[i])
+            bits ^= (rng.uniform(size=256) < 0.06).astype(np.uint8)
+            kps.append((uu + rng.normal(scale=0.7), vv + rng.normal(scale=0.7), 31 * sf[lv], rng.uniform(0, 360),
+                        0.0, lv, -1))
+            desc.append(np.packbits(bits))
+            owner.append(i)
+        for _ in range(n_distractors):
+            j = int(rng.integers(0, n_points))
+            bits = np.unpackbits(pdesc[j])
+            bits ^= (rng.uniform(size=256) < 0.25).astype(np.uint8)
+            lv = int(rng.integers(0, 8))
+            kps.append((rng.uniform(0, 639), rng.uniform(0, 479), 31 * sf[lv], rng.uniform(0, 360), 0.0, lv, -1))
+            desc.append(np.packbits(bits))
+            owner.append(-1)
+        order = rng.permutation(len(kps))
+        kps = [kps[o] for o in order]
+        desc = [desc[o] for o in order]
+        owner = np.array(owner, np.int64)[order]
+        n = len(kps)
+        pts = {"flags": np.zeros(n, np.int32), "pos": np.zeros((n, 3), np.float32),
+               "desc": np.zeros((n, 32), np.uint8), "min_dist": np.zeros(n, np.float32),
+               "max_dist": np.zeros(n, np.float32), "normal": np.zeros((n, 3), np.float32)}
+        for k_, i in enumerate(owner):
+            if i < 0:
+                continue
+            pts["flags"][k_] = 1 if rng.uniform() >= bad else 0
+            pts["pos"][k_] = X[i]
+            pts["desc"][k_] = pdesc[i]
+            pts["max_dist"][k_] = maxd[i]
+            pts["min_dist"][k_] = maxd[i] / sf[7]
+        return kps, desc, owner, pts
+
+    k1, d1, own1, pts1 = view(pc1, X1, None)
+    k2, d2, own2, pts2 = view(pc2, X2, common)
+    # vbAlreadyMatched1/2: some common points matched before the call (SearchByBoW)
+    where2 = {int(i): k_ for k_, i in enumerate(own2) if i >= 0}
+    for k_, i in enumerate(own1):
+        if i >= 0 and int(i) in where2 and rng.uniform() < already:
+            pts1["flags"][k_] = 0
+            pts2["flags"][where2[int(i)]] = 0
+    kf1 = _kf_target(k1, d1, T1, rng)
+    kf2 = _kf_target(k2, d2, T2, rng)
+    return kf1, kf2, pts1, pts2, np.float32(s12), R12.astype(np.float32), t12.astype(np.float32)
+
+
+def triangulation_scenario(voc_desc_leaves: np.ndarray, n_points: int, seed: int, n_distractors: int = 200,
+                           tracked: float = 0.3, stereo: bool = False):
+    """Two neighbouring keyframes for LocalMapping::CreateNewMapPoints ->
+    ORBmatcher::SearchForTriangulation: world points projected into both
+    (descriptors near vocabulary leaves, so the direct-index nodes agree),
+    `tracked` of the keypoints already carry a MapPoint (skipped), F12 from
+    the poses as LocalMapping::ComputeF12 forms it (LocalMapping.cpp:697-713).
+    Returns a dict of the pair's host arrays."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = 517.3, 516.5, 318.6, 255.3
+    K = np.array([[fx, 0, cx], [0, fy, cy], [0, 0, 1]])
+    sf = (np.float32(1.2) ** np.arange(8)).astype(np.float32)
+    T1 = _pose(rng, 0.1, 0.1)
+    T2 = T1.copy()
+    T2[:3, :3] = _rot(rng, 0.08) @ T1[:3, :3]
+    T2[:3, 3] = T1[:3, 3] + rng.uniform(-0.4, 0.4, 3)
+    z = rng.uniform(2.0, 10.0, n_points)
+    u = rng.uniform(0, 640, n_points)
+    v = rng.uniform(0, 480, n_points)
+    pc1 = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], 1)
+    Xw = (pc1 - T1[:3, 3]) @ T1[:3, :3]
+    pc2 = Xw @ T2[:3, :3].T + T2[:3, 3]
+    base = voc_desc_leaves[rng.integers(0, len(voc_desc_leaves), n_points)]
+
+    def jitter(d, p):
+        bits = np.unpackbits(d, axis=1)
+        return np.packbits(bits ^ (rng.uniform(size=bits.shape) < p).astype(np.uint8), axis=1)
+
+    def frame(pc, only):
+        kps, desc, ang = [], [], []
+        for i in range(n_points):
+            if only is not None and not only[i]:
+                continue
+            if pc[i, 2] <= 0:
+                continue
+            uu, vv = fx * pc[i, 0] / pc[i, 2] + cx, fy * pc[i, 1] / pc[i, 2] + cy
+            if not (0 <= uu < 640 and 0 <= vv < 480):
+                continue
+            lv = int(rng.integers(0, 8))
+            kps.append((uu + rng.normal(scale=0.6), vv + rng.normal(scale=0.6), 31 * sf[lv], 0.0, 0.0, lv, -1))
+            desc.append(jitter(base[i:i + 1], 0.03)[0])
+            ang.append(float(i * 37 % 360))
+        for _ in range(n_distractors):
+            lv = int(rng.integers(0, 8))
+            kps.append((rng.uniform(0, 639), rng.uniform(0, 479), 31 * sf[lv], 0.0, 0.0, lv, -1))
+            desc.append(jitter(base[int(rng.integers(0, n_points)):][:1], 0.15)[0])
+            ang.append(rng.uniform(0, 360))
+        order = rng.permutation(len(kps))
+        k = np.zeros(len(kps), dtype=[("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+        for o, j in enumerate(order):
+            k[o] = kps[j]
+        k["angle"] = (np.array(ang)[order] + rng.normal(scale=1.0, size=len(order))) % 360.0
+        return k, np.array(desc, np.uint8)[order]
+
+    k1, d1 = frame(pc1, None)
+    k2, d2 = frame(pc2, rng.uniform(size=n_points) < 0.8)
+    # F12 = K1^-T [t12]x R12 K2^-1 (ComputeF12), with R12 = R1w R2w^T, t12 = -R12 t2w + t1w
+    R12 = T1[:3, :3] @ T2[:3, :3].T
+    t12 = -R12 @ T2[:3, 3] + T1[:3, 3]
+    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]])
+    F12 = (np.linalg.inv(K).T @ tx @ R12 @ np.linalg.inv(K)).astype(np.float32)
+    Cw1 = (-T1[:3, :3].T @ T1[:3, 3]).astype(np.float32)
+    sig2 = (sf * sf).astype(np.float32)
+    ur = lambda k: (np.where(rng.uniform(size=len(k)) < 0.5, k["x"] - rng.uniform(5, 40, len(k)), -1.0)  # noqa: E731
+                    .astype(np.float32) if stereo else None)
+    return {"kps1": k1, "kps2": k2, "desc1": d1, "desc2": d2,
+            "valid1": (rng.uniform(size=len(k1)) >= tracked).astype(np.uint8),
+            "valid2": (rng.uniform(size=len(k2)) >= tracked).astype(np.uint8),
+            "u_right1": ur(k1), "u_right2": ur(k2), "F12": F12, "Cw1": Cw1,
+            "T2w": T2[:3, :].astype(np.float32), "fx2": fx, "fy2": fy, "cx2": cx, "cy2": cy,
+            "scale_factors2": sf, "level_sigma2_2": sig2}
+
 # --------------------------------------------------------------------------
 # Loop-closure burst (SURVEY.md section 8d, config 5)
 # --------------------------------------------------------------------------

@@ -7,8 +7,9 @@ wrote -- so the select takes a stale SCC from an earlier scalar op
 (reproducer: tools/scc_repro.hip).  This script scans device assembly
 (`hipcc -S --cuda-device-only`) and reports every s_cselect / s_cbranch_scc*
 whose nearest preceding definition of SCC-or-VCC in the same basic block is
-a VALU compare into VCC, unless the compare's VCC is read by an instruction before the consumer
-(then the compare has its own user), or the SCC the consumer actually reads was set
+a VALU compare into VCC, unless the compare's VCC is read by an instruction before the consumer,
+or after it before VCC is redefined in the same block (then the compare has its own user and the
+consumer's SCC comes from an earlier scalar op), or the SCC the consumer actually reads was set
 in that block by `s_and_b64 s, vcc, exec` -- the compiler's uniform lowering
 of an earlier compare (a later v_cmp into VCC for another purpose may sit
 in between).  build() runs it over every kernel and fails the build on a
@@ -41,6 +42,28 @@ def vcc_read(lines, lo, hi):
     return False
 
 
+def vcc_read_after(lines, i):
+    """True when VCC (as left by the compare) is read after the consumer at line i, before it is
+    redefined or the basic block ends."""
+    for k in range(i + 1, min(len(lines), i + 60)):
+        ins = lines[k].strip()
+        if LABEL.match(ins) or ins.startswith("s_cbranch") or ins.startswith("s_branch"):
+            return False
+        if ins.startswith(";") or not ins:
+            continue
+        if VCC_CMP.match(ins):
+            return False
+        ops = ins.split(None, 1)
+        if len(ops) < 2:
+            continue
+        args = [a.strip() for a in ops[1].split(",")]
+        if "vcc" in args[1:]:
+            return True
+        if args[0] == "vcc":
+            return False
+    return False
+
+
 def scan(lines):
     hits = []
     for i, line in enumerate(lines):
@@ -58,7 +81,8 @@ def scan(lines):
                     hits.append((i + 1, line.strip(), cmp_at + 1, lines[cmp_at].strip()))
                 cmp_at = None
                 break
-            if VCC_CMP.match(prev) and cmp_at is None and not vcc_read(lines, j + 1, i):
+            if VCC_CMP.match(prev) and cmp_at is None and not vcc_read(lines, j + 1, i) and \
+                    not vcc_read_after(lines, i):
                 cmp_at = j
         if cmp_at is not None:  # reached the block start: SCC comes from another block
             hits.append((i + 1, line.strip(), cmp_at + 1, lines[cmp_at].strip()))
