@@ -19,6 +19,15 @@
 //   SearchByBoW(KeyFrame*, KeyFrame*, vector<MapPoint*>&)           :105, .cpp:604-743
 //   SearchForInitialization(Frame&, Frame&, vector<Point2f>&, vector<int>&, windowSize)
 //                                                                  :108, .cpp:474-590
+//   SearchForTriangulation(KF1, KF2, F12, vMatchedPairs, bOnlyStereo)
+//                                                                  :111, .cpp:755-951
+//   SearchBySim3(KF1, KF2, vpMatches12, s12, R12, t12, th)         :116, .cpp:1253-1491
+//   Fuse(KF, vpMapPoints, th = 3.0)                                :119, .cpp:962-1115
+//   Fuse(KF, Scw, vpPoints, th, vpReplacePoint)                    :122, .cpp:1119-1249
+// Fuse's searches run on the GPU, one result per MapPoint; the MapPoint
+// updates (Replace / AddObservation / AddMapPoint) are then made here, on the
+// host, in the reference's point order with the reference's live checks, so
+// a point affected by an earlier point's update behaves as in the loop.
 // The Frame / KeyFrame / MapPoint parameters are template parameters, so the
 // header needs none of the reference's own headers: the members read are
 // the reference's (mvKeysUn, mDescriptors, mFeatVec, mvpMapPoints, mTcw,
@@ -52,6 +61,8 @@
 #include <stdexcept>
 #include <string>
 #include <vector>
+
+#include <utility>
 
 #include "../orbgpu.h"
 #include "../orbgpu_bow.h"
@@ -374,6 +385,183 @@ public:
         return nmatches;
     }
 
+    // ---- SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
+    // LocalMapping::CreateNewMapPoints (LocalMapping.cpp:355-360)
+    template <class KeyFrameT>
+    int SearchForTriangulation(KeyFrameT* pKF1, KeyFrameT* pKF2, cv::Mat F12,
+                               std::vector<std::pair<size_t, size_t> >& vMatchedPairs, const bool bOnlyStereo) {
+        using namespace orbslam2_amd::detail;
+        BowBuf a, b;
+        const int n1 = (int)pKF1->mvKeysUn.size(), n2 = (int)pKF2->mvKeysUn.size();
+        a.set(pKF1->mFeatVec, pKF1->mDescriptors, n1);
+        b.set(pKF2->mFeatVec, pKF2->mDescriptors, n2);
+        for (int i = 0; i < n1; ++i) {
+            a.angle[i] = pKF1->mvKeysUn[i].angle;
+            a.valid[i] = pKF1->GetMapPoint(i) ? 0 : 1;  // only keypoints without a MapPoint (:808-813)
+        }
+        for (int i = 0; i < n2; ++i) {
+            b.angle[i] = pKF2->mvKeysUn[i].angle;
+            b.valid[i] = pKF2->GetMapPoint(i) ? 0 : 1;
+        }
+        std::vector<orbgpu_keypoint> k1, k2;
+        pack_keys(pKF1->mvKeysUn, k1);
+        pack_keys(pKF2->mvKeysUn, k2);
+        if (k1.empty()) k1.resize(1);
+        if (k2.empty()) k2.resize(1);
+        orbgpu_triangulation_pair P;
+        std::memset(&P, 0, sizeof(P));
+        P.kf1 = a.frame();
+        P.kf2 = b.frame();
+        P.kps1 = k1.data();
+        P.kps2 = k2.data();
+        P.u_right1 = (int)pKF1->mvuRight.size() >= n1 && n1 ? pKF1->mvuRight.data() : nullptr;
+        P.u_right2 = (int)pKF2->mvuRight.size() >= n2 && n2 ? pKF2->mvuRight.data() : nullptr;
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) P.F12[3 * r + c] = F12.template at<float>(r, c);
+        const cv::Mat Cw = pKF1->GetCameraCenter(), R2w = pKF2->GetRotation(), t2w = pKF2->GetTranslation();
+        for (int r = 0; r < 3; ++r) {
+            P.Cw1[r] = Cw.template at<float>(r);
+            for (int c = 0; c < 3; ++c) P.T2w[4 * r + c] = R2w.template at<float>(r, c);
+            P.T2w[4 * r + 3] = t2w.template at<float>(r);
+        }
+        P.fx2 = pKF2->fx;
+        P.fy2 = pKF2->fy;
+        P.cx2 = pKF2->cx;
+        P.cy2 = pKF2->cy;
+        for (int l = 0; l < (int)pKF2->mvScaleFactors.size() && l < 16; ++l) P.scale_factors2[l] = pKF2->mvScaleFactors[l];
+        for (int l = 0; l < (int)pKF2->mvLevelSigma2.size() && l < 16; ++l) P.level_sigma2_2[l] = pKF2->mvLevelSigma2[l];
+        P.only_stereo = bOnlyStereo ? 1 : 0;
+        std::vector<int> m12(n1 > 0 ? n1 : 1);
+        int nm = 0;
+        check(orbgpu_search_for_triangulation(&P, mbCheckOrientation ? 1 : 0, m12.data(), &nm));
+        vMatchedPairs.clear();
+        vMatchedPairs.reserve(nm);
+        for (int i = 0; i < n1; ++i)
+            if (m12[i] >= 0) vMatchedPairs.push_back(std::make_pair((size_t)i, (size_t)m12[i]));
+        return nm;
+    }
+
+    // ---- SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) ---------
+    // LoopClosing::ComputeSim3 (LoopClosing.cpp:386)
+    template <class KeyFrameT, class MapPointT>
+    int SearchBySim3(KeyFrameT* pKF1, KeyFrameT* pKF2, std::vector<MapPointT*>& vpMatches12, const float& s12,
+                     const cv::Mat& R12, const cv::Mat& t12, const float th) {
+        using namespace orbslam2_amd::detail;
+        const std::vector<MapPointT*> vp1 = pKF1->GetMapPointMatches(), vp2 = pKF2->GetMapPointMatches();
+        const int N1 = (int)vp1.size(), N2 = (int)vp2.size();
+        std::vector<char> already1(N1, 0), already2(N2, 0);  // vbAlreadyMatched1/2 (:1282-1296)
+        for (int i = 0; i < N1; ++i)
+            if (MapPointT* pMP = vpMatches12[i]) {
+                already1[i] = 1;
+                const int idx2 = pMP->GetIndexInKeyFrame(pKF2);
+                if (idx2 >= 0 && idx2 < N2) already2[idx2] = 1;
+            }
+        TargetBuf t1, t2;
+        keyframe_target(*pKF1, t1);
+        keyframe_target(*pKF2, t2);
+        PointBuf p1(N1), p2(N2);
+        for (int i = 0; i < N1; ++i) {
+            MapPointT* p = vp1[i];
+            if (!p || already1[i] || p->isBad()) continue;
+            p1.flags[i] = ORBGPU_PT_VALID;
+            p1.fill(i, p);
+        }
+        for (int i = 0; i < N2; ++i) {
+            MapPointT* p = vp2[i];
+            if (!p || already2[i] || p->isBad()) continue;
+            p2.flags[i] = ORBGPU_PT_VALID;
+            p2.fill(i, p);
+        }
+        orbgpu_sim3_search S;
+        std::memset(&S, 0, sizeof(S));
+        S.kf1 = attach_target(t1);
+        S.kf2 = attach_target(t2);
+        p1.attach(S.pts1);
+        p2.attach(S.pts2);
+        S.s12 = s12;
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c) S.R12[3 * r + c] = R12.template at<float>(r, c);
+            S.t12[r] = t12.template at<float>(r);
+        }
+        S.th = th;
+        std::vector<int> m12(N1 > 0 ? N1 : 1);
+        int nfound = 0;
+        check(orbgpu_search_by_sim3(&S, m12.data(), &nfound));
+        for (int i = 0; i < N1; ++i)
+            if (m12[i] >= 0) vpMatches12[i] = vp2[m12[i]];
+        return nfound;
+    }
+
+    // ---- Fuse(pKF, vpMapPoints, th): LocalMapping::SearchInNeighbors -------
+    template <class KeyFrameT, class MapPointT>
+    int Fuse(KeyFrameT* pKF, const std::vector<MapPointT*>& vpMapPoints, const float th = 3.0) {
+        using namespace orbslam2_amd::detail;
+        TargetBuf tb;
+        keyframe_target(*pKF, tb);
+        const int np = (int)vpMapPoints.size();
+        PointBuf pb(np);
+        for (int i = 0; i < np; ++i) {
+            MapPointT* p = vpMapPoints[i];
+            if (!p || p->isBad() || p->IsInKeyFrame(pKF)) continue;
+            pb.flags[i] = ORBGPU_PT_VALID;
+            pb.fill(i, p);
+            normal(p, &pb.normal[3 * (size_t)i]);
+        }
+        const std::vector<int> best = per_point(ORBGPU_PROJ_FUSE, th, tb, pb);
+        int nFused = 0;
+        for (int i = 0; i < np; ++i) {  // the reference's updates, in its order (:1091-1111)
+            MapPointT* pMP = vpMapPoints[i];
+            if (!pMP || pMP->isBad() || pMP->IsInKeyFrame(pKF) || best[i] < 0) continue;
+            MapPointT* pMPinKF = pKF->GetMapPoint(best[i]);
+            if (pMPinKF) {
+                if (!pMPinKF->isBad()) {
+                    if (pMPinKF->Observations() > pMP->Observations()) pMP->Replace(pMPinKF);
+                    else pMPinKF->Replace(pMP);
+                }
+            } else {
+                pMP->AddObservation(pKF, best[i]);
+                pKF->AddMapPoint(pMP, best[i]);
+            }
+            nFused++;
+        }
+        return nFused;
+    }
+
+    // ---- Fuse(pKF, Scw, vpPoints, th, vpReplacePoint): LoopClosing::SearchAndFuse
+    template <class KeyFrameT, class MapPointT>
+    int Fuse(KeyFrameT* pKF, cv::Mat Scw, const std::vector<MapPointT*>& vpPoints, float th,
+             std::vector<MapPointT*>& vpReplacePoint) {
+        using namespace orbslam2_amd::detail;
+        TargetBuf tb;
+        keyframe_target(*pKF, tb);
+        mat4(Scw, tb.t.Tcw);
+        const std::set<MapPointT*> spAlreadyFound = pKF->GetMapPoints();
+        const int np = (int)vpPoints.size();
+        PointBuf pb(np);
+        for (int i = 0; i < np; ++i) {
+            MapPointT* p = vpPoints[i];
+            if (p->isBad() || spAlreadyFound.count(p)) continue;
+            pb.flags[i] = ORBGPU_PT_VALID;
+            pb.fill(i, p);
+            normal(p, &pb.normal[3 * (size_t)i]);
+        }
+        const std::vector<int> best = per_point(ORBGPU_PROJ_FUSE_SIM3, th, tb, pb);
+        int nFused = 0;
+        for (int i = 0; i < np; ++i) {  // :1228-1245
+            MapPointT* pMP = vpPoints[i];
+            if (pMP->isBad() || spAlreadyFound.count(pMP) || best[i] < 0) continue;
+            MapPointT* pMPinKF = pKF->GetMapPoint(best[i]);
+            if (pMPinKF) {
+                if (!pMPinKF->isBad()) vpReplacePoint[i] = pMPinKF;
+            } else {
+                pMP->AddObservation(pKF, best[i]);
+                pKF->AddMapPoint(pMP, best[i]);
+            }
+            nFused++;
+        }
+        return nFused;
+    }
+
     // Extension (not in the reference): the annotated tree's rotation-bin
     // factor 1/HISTO_LENGTH in SearchForInitialization.
     bool mbAnnotatedHisto = false;
@@ -447,6 +635,48 @@ private:
             if (F.mvpMapPoints[k]) tb.occ[k] = F.mvpMapPoints[k]->Observations() > 0 ? 2 : 1;
             if (k < (int)F.mvuRight.size()) tb.ur[k] = F.mvuRight[k];
         }
+    }
+
+    // a KeyFrame as a projection target: mvKeysUn, descriptors, mvuRight,
+    // pose [GetRotation() | GetTranslation()]
+    template <class KeyFrameT>
+    static void keyframe_target(KeyFrameT& KF, TargetBuf& tb) {
+        using namespace orbslam2_amd::detail;
+        const int n = (int)KF.mvKeysUn.size();
+        fill_target(KF, n, tb.t);
+        pack_keys(KF.mvKeysUn, tb.kps);
+        pack_desc(KF.mDescriptors, (size_t)n, tb.desc);
+        tb.occ.assign(n > 0 ? n : 1, 0);
+        tb.ur.assign(n > 0 ? n : 1, -1.f);
+        for (int k = 0; k < n && k < (int)KF.mvuRight.size(); ++k) tb.ur[k] = KF.mvuRight[k];
+        const cv::Mat R = KF.GetRotation(), t = KF.GetTranslation();
+        for (int i = 0; i < 16; ++i) tb.t.Tcw[i] = (i == 15) ? 1.f : 0.f;
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c) tb.t.Tcw[4 * r + c] = R.template at<float>(r, c);
+            tb.t.Tcw[4 * r + 3] = t.template at<float>(r);
+        }
+    }
+
+    static orbgpu_proj_target attach_target(TargetBuf& tb) {
+        orbgpu_proj_target t = tb.t;
+        if (tb.kps.empty()) tb.kps.resize(1);
+        if (tb.desc.empty()) tb.desc.assign(32, 0);
+        t.kps = tb.kps.data();
+        t.desc = tb.desc.data();
+        t.occupied = nullptr;
+        t.u_right = tb.ur.data();
+        return t;
+    }
+
+    // one per-point search (FUSE / FUSE_SIM3): best keypoint per point or -1
+    std::vector<int> per_point(int variant, float th, TargetBuf& tb, PointBuf& pb) const {
+        orbgpu_proj_call c = make_call(variant, th, tb);
+        c.target.occupied = nullptr;
+        pb.attach(c.points);
+        std::vector<int> best(pb.flags.empty() ? 1 : pb.flags.size());
+        run(c, best);
+        best.resize(pb.flags.size());
+        return best;
     }
 
     orbgpu_proj_call make_call(int variant, float th, TargetBuf& tb) const {

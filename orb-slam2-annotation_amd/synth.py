@@ -403,7 +403,10 @@ def sim3_search_scenario(n_points: int, n_distractors: int, seed: int, s12: floa
     camera 1), by KF2 in its own map.  Every keypoint carries a MapPoint
     entry (one per keypoint; distractor keypoints have none); `already` of
     the common points are marked as matched in both (vbAlreadyMatched1/2)
-    and `bad` as isBad().  Returns (kf1, kf2, pts1, pts2, s12, R12, t12)."""
+    and `bad` as isBad().  pts*["flags"] are the oracle's (VALID = non-NULL,
+    good, not already matched); pts*["null"] / ["bad"] and pts1["pre"] (the
+    KF2 slot already matched to each KF1 slot, or -1) describe the same state
+    for the C++ class.  Returns (kf1, kf2, pts1, pts2, s12, R12, t12)."""
     rng = np.random.default_rng(seed)
     fx, fy, cx, cy = 517.3, 516.5, 318.6, 255.3
     sf = (np.float32(1.2) ** np.arange(8)).astype(np.float32)
@@ -458,10 +461,14 @@ def sim3_search_scenario(n_points: int, n_distractors: int, seed: int, s12: floa
         pts = {"flags": np.zeros(n, np.int32), "pos": np.zeros((n, 3), np.float32),
                "desc": np.zeros((n, 32), np.uint8), "min_dist": np.zeros(n, np.float32),
                "max_dist": np.zeros(n, np.float32), "normal": np.zeros((n, 3), np.float32)}
+        pts["null"] = owner < 0
+        pts["bad"] = np.zeros(n, bool)
+        pts["pre"] = np.full(n, -1, np.int32)
         for k_, i in enumerate(owner):
             if i < 0:
                 continue
-            pts["flags"][k_] = 1 if rng.uniform() >= bad else 0
+            pts["bad"][k_] = rng.uniform() < bad
+            pts["flags"][k_] = 0 if pts["bad"][k_] else 1
             pts["pos"][k_] = X[i]
             pts["desc"][k_] = pdesc[i]
             pts["max_dist"][k_] = maxd[i]
@@ -476,6 +483,7 @@ def sim3_search_scenario(n_points: int, n_distractors: int, seed: int, s12: floa
         if i >= 0 and int(i) in where2 and rng.uniform() < already:
             pts1["flags"][k_] = 0
             pts2["flags"][where2[int(i)]] = 0
+            pts1["pre"][k_] = where2[int(i)]  # vpMatches12[k_] = KF2's MapPoint at that slot
     kf1 = _kf_target(k1, d1, T1, rng)
     kf2 = _kf_target(k2, d2, T2, rng)
     return kf1, kf2, pts1, pts2, np.float32(s12), R12.astype(np.float32), t12.astype(np.float32)

@@ -19,6 +19,13 @@
 //       PnPsolver as Tracking::Relocalization drives it (Tracking.cpp:1786-1822)
 //   adapter_main sim3 <in.bin> <out.bin>
 //       Sim3Solvers as LoopClosing::ComputeSim3 drives them (LoopClosing.cpp:311-356)
+//   adapter_main fuse <4|5> <in.bin> <out.bin>
+//       ORBmatcher::Fuse(KF, vpMapPoints, th) (4, LocalMapping::SearchInNeighbors) or
+//       Fuse(KF, Scw, vpPoints, th, vpReplacePoint) (5, LoopClosing::SearchAndFuse)
+//   adapter_main sim3search <in.bin> <out.bin>
+//       ORBmatcher::SearchBySim3 (LoopClosing.cpp:386)
+//   adapter_main tri <in.bin> <out.bin>
+//       ORBmatcher::SearchForTriangulation (LocalMapping.cpp:355-360)
 // The .bin layouts are written / read by tests/test_adapter.py (fixed
 // field order, little-endian, no headers).
 #include <cstdio>
@@ -53,6 +60,7 @@ struct MiniMapPoint {
     float mTrackProjX = 0.f, mTrackProjY = 0.f, mTrackProjXR = 0.f, mTrackViewCos = 0.f;
     int mnTrackScaleLevel = 0;
     std::map<const MiniKeyFrame*, int> index;
+    int id = -1;  // the test's label of this MapPoint
     cv::Mat GetWorldPos() { return pos; }
     cv::Mat GetNormal() { return nrm; }
     cv::Mat GetDescriptor() { return desc; }
@@ -64,6 +72,9 @@ struct MiniMapPoint {
         auto it = index.find(kf);
         return it == index.end() ? -1 : it->second;
     }
+    bool IsInKeyFrame(MiniKeyFrame* kf) { return index.count(kf) != 0; }
+    inline void AddObservation(MiniKeyFrame* kf, size_t idx);
+    inline void Replace(MiniMapPoint* p);  // MapPoint::Replace (MapPoint.cpp:191-238), map bookkeeping only
 };
 
 // The members of ORB_SLAM2::Frame the adapters read (Frame.h:100-200).
@@ -85,10 +96,48 @@ struct MiniFrame {
 // ... and of ORB_SLAM2::KeyFrame (KeyFrame.h:40-230).
 struct MiniKeyFrame : MiniFrame {
     cv::Mat mK = cv::Mat(3, 3, CV_32F), Rcw = cv::Mat(3, 3, CV_32F), tcw = cv::Mat(3, 1, CV_32F);
+    cv::Mat Ow = cv::Mat(3, 1, CV_32F);
     std::vector<MiniMapPoint*> GetMapPointMatches() { return mvpMapPoints; }
     cv::Mat GetRotation() { return Rcw; }
     cv::Mat GetTranslation() { return tcw; }
+    cv::Mat GetCameraCenter() { return Ow; }
+    MiniMapPoint* GetMapPoint(size_t idx) { return mvpMapPoints[idx]; }
+    void AddMapPoint(MiniMapPoint* p, size_t idx) { mvpMapPoints[idx] = p; }
+    std::set<MiniMapPoint*> GetMapPoints() {  // KeyFrame::GetMapPoints: the good ones
+        std::set<MiniMapPoint*> s;
+        for (MiniMapPoint* p : mvpMapPoints)
+            if (p && !p->isBad()) s.insert(p);
+        return s;
+    }
+    void pose_from_Tcw() {
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c) Rcw.at<float>(r, c) = mTcw.at<float>(r, c);
+            tcw.at<float>(r) = mTcw.at<float>(r, 3);
+        }
+    }
 };
+
+void MiniMapPoint::AddObservation(MiniKeyFrame* kf, size_t idx) {
+    if (index.count(kf)) return;
+    index[kf] = (int)idx;
+    ++nobs;
+}
+
+void MiniMapPoint::Replace(MiniMapPoint* p) {
+    if (p == this) return;
+    for (auto& o : index) {
+        MiniKeyFrame* kf = const_cast<MiniKeyFrame*>(o.first);
+        if (!p->IsInKeyFrame(kf)) {
+            kf->mvpMapPoints[o.second] = p;  // ReplaceMapPointMatch
+            p->AddObservation(kf, o.second);
+        } else {
+            kf->mvpMapPoints[o.second] = nullptr;  // EraseMapPointMatch
+        }
+    }
+    index.clear();
+    nobs = 0;
+    bad = true;
+}
 
 struct In {
     std::vector<unsigned char> b;
@@ -496,6 +545,133 @@ int run_sim3(const char* inp, const char* outp) {
     return 0;
 }
 
+int label(const MiniMapPoint* p) { return p ? p->id : -1; }
+
+// Fuse: th, the keyframe (read_frame layout; Tcw = its pose), Scw (16), per
+// keyframe slot its MapPoint (0 none, 1 good, 2 bad) and observation count,
+// the points (read_points layout), per point its observation count and
+// whether it is already in the keyframe (at no slot of this test).
+// Output: nFused, per keyframe slot the final MapPoint label (points i, slot
+// dummies 100000 + slot, -1 NULL), per point bad flag, vpReplacePoint labels.
+int run_fuse(int variant, const char* inp, const char* outp) {
+    In in{read_file(inp)};
+    std::vector<std::unique_ptr<MiniMapPoint>> store;
+    const float th = in.get<float>();
+    MiniKeyFrame KF;
+    read_frame(in, KF);
+    KF.pose_from_Tcw();
+    const std::vector<float> S = in.vec<float>(16);
+    cv::Mat Scw(4, 4, CV_32F);
+    for (int i = 0; i < 16; ++i) Scw.at<float>(i / 4, i % 4) = S[i];
+    const std::vector<unsigned char> slot = in.vec<unsigned char>(KF.N);
+    const std::vector<int> slot_obs = in.vec<int>(KF.N);
+    for (int k = 0; k < KF.N; ++k)
+        if (slot[k]) {
+            store.emplace_back(new MiniMapPoint());
+            MiniMapPoint* d = store.back().get();
+            d->bad = slot[k] == 2;
+            d->id = 100000 + k;
+            d->index[&KF] = k;
+            d->nobs = slot_obs[k];
+            KF.mvpMapPoints[k] = d;
+        }
+    std::vector<MiniMapPoint*> pts = read_points(in, store);
+    const std::vector<int> pobs = in.vec<int>(pts.size());
+    const std::vector<unsigned char> inkf = in.vec<unsigned char>(pts.size());
+    MiniKeyFrame other;  // where "already in the keyframe" points are observed (a slot outside the test)
+    for (size_t i = 0; i < pts.size(); ++i) {
+        pts[i]->id = (int)i;
+        pts[i]->nobs = pobs[i];
+        if (inkf[i]) pts[i]->index[&KF] = -1;
+    }
+    ORB_SLAM2::ORBmatcher m;
+    std::vector<MiniMapPoint*> repl(pts.size(), nullptr);
+    const int nf = variant == 4 ? m.Fuse(&KF, pts, th) : m.Fuse(&KF, Scw, pts, th, repl);
+    Out out(outp);
+    out.put(nf);
+    for (int k = 0; k < KF.N; ++k) out.put(label(KF.mvpMapPoints[k]));
+    for (MiniMapPoint* p : pts) out.put((int)p->bad);
+    for (MiniMapPoint* p : repl) out.put(label(p));
+    return 0;
+}
+
+// SearchBySim3: th, s12, R12 (9), t12 (3), KF1 and KF2 (read_frame layout,
+// Tcw = pose), their MapPoints (read_points layout, one per slot, flags bit 0
+// = exists and good, bit 3 = NULL), then vpMatches12 before the call (per KF1
+// slot: the KF2 slot whose MapPoint it holds, or -1).  Output: nfound, then
+// vpMatches12 as KF2 slots.
+int run_sim3search(const char* inp, const char* outp) {
+    In in{read_file(inp)};
+    std::vector<std::unique_ptr<MiniMapPoint>> store;
+    const float th = in.get<float>(), s12 = in.get<float>();
+    const std::vector<float> R = in.vec<float>(9), t = in.vec<float>(3);
+    MiniKeyFrame K1, K2;
+    read_frame(in, K1);
+    read_frame(in, K2);
+    K1.pose_from_Tcw();
+    K2.pose_from_Tcw();
+    std::vector<MiniMapPoint*> p1 = read_points(in, store), p2 = read_points(in, store);
+    const std::vector<int> null1 = in.vec<int>(p1.size()), null2 = in.vec<int>(p2.size());
+    for (size_t i = 0; i < p1.size(); ++i) K1.mvpMapPoints[i] = null1[i] ? nullptr : p1[i];
+    for (size_t i = 0; i < p2.size(); ++i) {
+        K2.mvpMapPoints[i] = null2[i] ? nullptr : p2[i];
+        p2[i]->index[&K2] = (int)i;
+    }
+    const std::vector<int> pre = in.vec<int>(p1.size());
+    std::vector<MiniMapPoint*> vpMatches12(p1.size(), nullptr);
+    for (size_t i = 0; i < p1.size(); ++i)
+        if (pre[i] >= 0) vpMatches12[i] = p2[pre[i]];
+    cv::Mat R12(3, 3, CV_32F), t12(3, 1, CV_32F);
+    for (int i = 0; i < 9; ++i) R12.at<float>(i / 3, i % 3) = R[i];
+    for (int i = 0; i < 3; ++i) t12.at<float>(i) = t[i];
+    ORB_SLAM2::ORBmatcher m;
+    const int nf = m.SearchBySim3(&K1, &K2, vpMatches12, s12, R12, t12, th);
+    Out out(outp);
+    out.put(nf);
+    for (MiniMapPoint* p : vpMatches12) out.put(p ? p->GetIndexInKeyFrame(&K2) : -1);
+    return 0;
+}
+
+// SearchForTriangulation: check_ori, only_stereo, F12 (9), Cw1 (3), then per
+// keyframe: read_frame layout (Tcw = pose), MapPoint presence per slot,
+// FeatureVector CSR.  Output: nmatches, vMatchedPairs (count, pairs).
+int run_tri(const char* inp, const char* outp) {
+    In in{read_file(inp)};
+    std::vector<std::unique_ptr<MiniMapPoint>> store;
+    const int check_ori = in.get<int>(), only_stereo = in.get<int>();
+    const std::vector<float> F = in.vec<float>(9), Cw = in.vec<float>(3);
+    MiniKeyFrame K[2];
+    for (int k = 0; k < 2; ++k) {
+        read_frame(in, K[k]);
+        K[k].pose_from_Tcw();
+        const std::vector<unsigned char> has = in.vec<unsigned char>(K[k].N);
+        for (int i = 0; i < K[k].N; ++i)
+            if (has[i]) {
+                store.emplace_back(new MiniMapPoint());
+                K[k].mvpMapPoints[i] = store.back().get();
+            }
+        const int nn = in.get<int>();
+        const std::vector<int> nodes = in.vec<int>(nn), offs = in.vec<int>(nn + 1);
+        const std::vector<int> feats = in.vec<int>(offs.empty() ? 0 : offs.back());
+        for (int j = 0; j < nn; ++j)
+            for (int q = offs[j]; q < offs[j + 1]; ++q) K[k].mFeatVec[(unsigned)nodes[j]].push_back((unsigned)feats[q]);
+    }
+    for (int i = 0; i < 3; ++i) K[0].Ow.at<float>(i) = Cw[i];
+    cv::Mat F12(3, 3, CV_32F);
+    for (int i = 0; i < 9; ++i) F12.at<float>(i / 3, i % 3) = F[i];
+    ORB_SLAM2::ORBmatcher m(0.6f, check_ori != 0);
+    std::vector<std::pair<size_t, size_t> > pairs;
+    const int nm = m.SearchForTriangulation(&K[0], &K[1], F12, pairs, only_stereo != 0);
+    Out out(outp);
+    out.put(nm);
+    out.put((int)pairs.size());
+    for (auto& pr : pairs) {
+        out.put((int)pr.first);
+        out.put((int)pr.second);
+    }
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -504,6 +680,9 @@ int main(int argc, char** argv) {
         if (argc >= 4 && !strcmp(argv[1], "bow")) return run_bow(argv[2], argv[3]);
         if (argc >= 4 && !strcmp(argv[1], "pnp")) return run_pnp(argv[2], argv[3]);
         if (argc >= 4 && !strcmp(argv[1], "sim3")) return run_sim3(argv[2], argv[3]);
+        if (argc >= 5 && !strcmp(argv[1], "fuse")) return run_fuse(atoi(argv[2]), argv[3], argv[4]);
+        if (argc >= 4 && !strcmp(argv[1], "sim3search")) return run_sim3search(argv[2], argv[3]);
+        if (argc >= 4 && !strcmp(argv[1], "tri")) return run_tri(argv[2], argv[3]);
     } catch (const std::exception& e) {
         fprintf(stderr, "exception: %s\n", e.what());
         return 3;

@@ -336,3 +336,156 @@ def test_adapter_sim3solver_compute_sim3(exe, tmp_path, fix_scale):
     want = np.zeros(400, bool)
     want[solvers[matched].idx[solvers[matched].best_mask]] = True
     np.testing.assert_array_equal(vb, want)
+
+
+# ---- Fuse / SearchBySim3 / SearchForTriangulation (LocalMapping, LoopClosing)
+def _fuse_replay(variant, best, slot_state, slot_obs, bad0, pobs, inkf):
+    """The reference's MapPoint updates after the per-point searches
+    (ORBmatcher.cpp:1091-1111, :1228-1245) over the adapter test's map model
+    (MapPoint::Replace moves the keyframe observation and marks the old point
+    bad).  Labels: point i, slot dummy 100000 + k, -1 NULL."""
+    n_kp, n_pts = len(slot_state), len(best)
+    owner = [100000 + k if slot_state[k] else -1 for k in range(n_kp)]
+    bad = {i: bool(bad0[i]) for i in range(n_pts)}
+    bad.update({100000 + k: slot_state[k] == 2 for k in range(n_kp)})
+    nobs = {i: int(pobs[i]) for i in range(n_pts)}
+    nobs.update({100000 + k: int(slot_obs[k]) for k in range(n_kp)})
+    where = {100000 + k: k for k in range(n_kp) if slot_state[k]}  # the keyframe slot of a point in it
+    in_kf = {i for i in range(n_pts) if inkf[i]}
+    found = {owner[k] for k in range(n_kp) if owner[k] != -1 and not bad[owner[k]]}
+    repl = [-1] * n_pts
+
+    def add(p, k):
+        if p in where or p in in_kf:
+            return
+        where[p] = k
+        nobs[p] += 1
+
+    def replace(a, b):  # a->Replace(b)
+        if a == b:
+            return
+        if a in where:
+            k = where.pop(a)
+            if b not in where and b not in in_kf:
+                owner[k] = b
+                add(b, k)
+            else:
+                owner[k] = -1
+        bad[a] = True
+        nobs[a] = 0
+
+    nf = 0
+    for i in range(n_pts):
+        if variant == 4:
+            if bad[i] or i in where or i in in_kf or best[i] < 0:
+                continue
+        elif bad[i] or i in found or best[i] < 0:
+            continue
+        pin = owner[best[i]]
+        if pin != -1:
+            if not bad[pin]:
+                if variant == 5:
+                    repl[i] = pin
+                elif nobs[pin] > nobs[i]:
+                    replace(i, pin)
+                else:
+                    replace(pin, i)
+        else:
+            add(i, best[i])
+            owner[best[i]] = i
+        nf += 1
+    return nf, owner, [int(bad[i]) for i in range(n_pts)], repl
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant,th,stereo,scale", [(4, 3.0, True, 1.0), (4, 6.0, False, 1.0), (5, 4.0, False, 1.7)])
+def test_adapter_orbmatcher_fuse(exe, tmp_path, variant, th, stereo, scale):
+    """ORB_SLAM2::ORBmatcher::Fuse (both overloads): GPU searches + the host
+    replay of the reference's updates, vs oracle/proj_ref.py + the replay"""
+    import proj_ref
+    tgt, pts = synth.projection_scenario(700, 400, 50 + variant, stereo=stereo, scale=scale)
+    rng = np.random.default_rng(variant)
+    n_kp, n_pts = len(tgt["kps"]), len(pts["flags"])
+    slot_state = np.where(rng.uniform(size=n_kp) < 0.3, rng.choice([1, 1, 1, 2], n_kp), 0).astype(np.uint8)
+    slot_obs = rng.integers(1, 6, n_kp).astype(np.int32)
+    pobs = rng.integers(1, 6, n_pts).astype(np.int32)
+    inkf = (rng.uniform(size=n_pts) < (0.05 if variant == 4 else 0.0)).astype(np.uint8)
+    bad0 = (np.asarray(pts["flags"]) & 1) == 0
+    pose = np.asarray(tgt["Tcw"], F32)
+    if variant == 5:  # Scw = the scenario's Sim3; the keyframe's own pose is not read
+        kf_tgt, Scw = dict(tgt, Tcw=np.eye(4, dtype=F32)), pose
+        oracle_pts = dict(pts, flags=(~bad0).astype(np.int32))
+    else:
+        kf_tgt, Scw = tgt, np.eye(4, dtype=F32)
+        oracle_pts = dict(pts, flags=((~bad0) & (inkf == 0)).astype(np.int32))
+    _, best = proj_ref.radius_search(variant, tgt, oracle_pts, th)
+    nf_r, owner_r, bad_r, repl_r = _fuse_replay(variant, best, slot_state, slot_obs, bad0, pobs, inkf)
+    blob = b"".join([struct.pack("<f", th), _frame_blob(kf_tgt), Scw.tobytes(), slot_state.tobytes(),
+                     slot_obs.tobytes(), _points_blob(dict(pts, flags=np.where(bad0, 0, 1))), pobs.tobytes(),
+                     inkf.tobytes()])
+    buf = _run(exe, tmp_path, "fuse", blob, variant)
+    got = np.frombuffer(buf, np.int32)
+    assert got[0] == nf_r > 50
+    np.testing.assert_array_equal(got[1:1 + n_kp], owner_r)
+    np.testing.assert_array_equal(got[1 + n_kp:1 + n_kp + n_pts], bad_r)
+    np.testing.assert_array_equal(got[1 + n_kp + n_pts:], repl_r)
+    assert any(o != -1 and o < 100000 for o in owner_r)  # some AddMapPoint happened
+    if variant == 4:
+        assert sum(bad_r) > bad0.sum()  # and some Replace
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,s12", [(60, 1.0), (61, 1.1)])
+def test_adapter_orbmatcher_search_by_sim3(exe, tmp_path, seed, s12):
+    """ORB_SLAM2::ORBmatcher::SearchBySim3 vs oracle/proj_ref.py"""
+    import proj_ref
+    kf1, kf2, p1, p2, s, R, t = synth.sim3_search_scenario(600, 250, seed, s12=s12)
+    nf_r, m_r = proj_ref.search_by_sim3(kf1, kf2, p1, p2, s, R, t, 7.5)
+
+    def cpp_pts(p):  # exists-and-good flags for the class (already-matched entries are ordinary MapPoints)
+        return dict(p, flags=((~p["null"]) & (~p["bad"])).astype(np.int32))
+    blob = b"".join([struct.pack("<ff", 7.5, float(s)), np.asarray(R, F32).tobytes(), np.asarray(t, F32).tobytes(),
+                     _frame_blob(kf1), _frame_blob(kf2), _points_blob(cpp_pts(p1)), _points_blob(cpp_pts(p2)),
+                     p1["null"].astype(np.int32).tobytes(), p2["null"].astype(np.int32).tobytes(),
+                     p1["pre"].astype(np.int32).tobytes()])
+    buf = _run(exe, tmp_path, "sim3search", blob)
+    got = np.frombuffer(buf, np.int32)
+    want = np.where(p1["pre"] >= 0, p1["pre"], m_r)
+    assert got[0] == nf_r > 20
+    np.testing.assert_array_equal(got[1:], want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,check_ori,stereo", [(2, True, False), (3, False, True)])
+def test_adapter_orbmatcher_search_for_triangulation(exe, tmp_path, seed, check_ori, stereo):
+    """ORB_SLAM2::ORBmatcher::SearchForTriangulation vs oracle/bow_ref.py"""
+    import bow_ref
+    par, leaf, desc, w = synth.synthetic_vocabulary(6, 4, 30 + seed)
+    voc = bow_ref.Vocabulary.from_arrays(6, 4, 0, 0, par, leaf, desc, w)
+    P = synth.triangulation_scenario(desc[leaf == 1], 500, seed, stereo=stereo)
+    fv1, fv2 = voc.transform(P["desc1"], 2)[3], voc.transform(P["desc2"], 2)[3]
+    nm_r, m_r = bow_ref.search_for_triangulation(fv1, fv2, P, check_ori, False)
+    sf, s2 = P["scale_factors2"], P["level_sigma2_2"]
+    T2 = np.eye(4, dtype=F32)
+    T2[:3, :] = P["T2w"]
+
+    def kf(i, T):
+        g = {"min_x": 0.0, "max_x": 640.0, "min_y": 0.0, "max_y": 480.0, "fx": P["fx2"], "fy": P["fy2"],
+             "cx": P["cx2"], "cy": P["cy2"], "bf": 0.0, "b": 0.0, "log_scale_factor": float(np.log(F32(1.2)))}
+        t = dict(g, kps=P[f"kps{i}"], desc=P[f"desc{i}"], u_right=P[f"u_right{i}"], scale_factors=sf, Tcw=T)
+        nodes = np.array(sorted((fv1, fv2)[i - 1]), np.int32)
+        offs = np.zeros(len(nodes) + 1, np.int32)
+        feats = []
+        for j, k in enumerate(nodes):
+            feats += list((fv1, fv2)[i - 1][int(k)])
+            offs[j + 1] = len(feats)
+        return b"".join([_frame_blob(t, s2), (1 - P[f"valid{i}"]).astype(np.uint8).tobytes(),
+                         struct.pack("<i", len(nodes)), nodes.tobytes(), offs.tobytes(),
+                         np.array(feats, np.int32).tobytes()])
+    blob = b"".join([struct.pack("<ii", int(check_ori), 0), np.asarray(P["F12"], F32).tobytes(),
+                     np.asarray(P["Cw1"], F32).tobytes(), kf(1, np.eye(4, dtype=F32)), kf(2, T2)])
+    buf = _run(exe, tmp_path, "tri", blob)
+    got = np.frombuffer(buf, np.int32)
+    pairs = [(i, int(m_r[i])) for i in range(len(m_r)) if m_r[i] >= 0]
+    assert got[0] == nm_r > 30 and got[1] == len(pairs)
+    np.testing.assert_array_equal(got[2:].reshape(-1, 2), np.array(pairs, np.int32).reshape(-1, 2))
