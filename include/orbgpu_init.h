@@ -11,8 +11,8 @@
  * inlier flags are bit-identical to the reference's loop.  Choosing the best
  * iteration (first strict maximum over score 0) is
  * orbgpu_init_select_best, the reference's `if(currentScore>score)`.
- * The 8-point solvers ComputeH21 / ComputeF21 (:292-388, cv::SVDecomp) stay
- * on the host.
+ * The model hypotheses (Normalize, ComputeH21 / ComputeF21) and the motion
+ * recovery (ReconstructH / ReconstructF) are declared further below.
  */
 #ifndef ORBGPU_INIT_H
 #define ORBGPU_INIT_H
@@ -86,6 +86,38 @@ int orbgpu_init_hypotheses_batch_device(const float* d_kp1, int n1, const float*
  * score and than 0; -1 when no score exceeds 0 (the reference keeps score 0
  * and an all-false inlier vector).  Host arrays. */
 int orbgpu_init_select_best(const float* scores, int nhyp, int* best);
+
+/* ---------------------------------------------------------------------- */
+/* Motion and structure (ReconstructH / ReconstructF)                      */
+/* ---------------------------------------------------------------------- */
+#define ORBGPU_INIT_MODEL_H 0
+#define ORBGPU_INIT_MODEL_F 1
+
+typedef struct orbgpu_init_reconstruction {
+    int ok;             /* the reference's return value                              */
+    int best;           /* the hypothesis the decision looked at, or -1              */
+    int n_hyp;          /* 8 (H), 4 (F), 0 when ReconstructH stops at d1/d2, d2/d3   */
+    int n_good[8];      /* CheckRT's nGood per hypothesis                            */
+    float parallax[8];  /* CheckRT's parallax (degrees) per hypothesis               */
+    float R21[9];       /* hypothesis `best`: rotation (row-major) ...               */
+    float t21[3];       /* ... and unit translation                                  */
+} orbgpu_init_reconstruction;
+
+/* Initializer::ReconstructH (model H, M21 = H21) / ReconstructF (model F,
+ * M21 = F21) (src/Initializer.cpp:596-963) with CheckRT (:1017-1118),
+ * Triangulate and DecomposeE: the 8 / 4 motion hypotheses on the host,
+ * CheckRT of every hypothesis over every inlier match on the GPU (one block
+ * per hypothesis), then the reference's choice.  kp1 / kp2: n1 / n2 x (x, y)
+ * (mvKeys1 / mvKeys2), pairs: n_matches x (first, second) = mvMatches12,
+ * inliers: vbMatchesInliers (0/1), K row-major, sigma = mSigma.  Host
+ * arrays.  p3d (n1 x 3) and triangulated (n1) receive vP3D and
+ * vbTriangulated when out->ok (zeros otherwise).  n_matches <= 16384.
+ * The SVDs are Jacobi in double (OpenCV's float Jacobi is not reproducible):
+ * equal to the reference within the tolerance of tests/test_init.py. */
+int orbgpu_init_reconstruct(int model, const float* kp1, int n1, const float* kp2, int n2, const int* pairs,
+                            int n_matches, const unsigned char* inliers, const float* M21, const float* K,
+                            float sigma, float min_parallax, int min_triangulated, orbgpu_init_reconstruction* out,
+                            float* p3d, unsigned char* triangulated);
 
 #ifdef __cplusplus
 }

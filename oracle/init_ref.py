@@ -222,3 +222,169 @@ def find_models(kp1, kp2, pairs, sets, sigma=1.0):
     return {"pts": pts, "H21": H21, "H12": H12, "F21": F21, "scores_h": sh, "scores_f": sf, "best_h": bh,
             "best_f": bf, "RH": F(SH / F(SH + SF)) if SH + SF > 0 else F(0), "T1": T1, "T2": T2, "pn1": pn1,
             "pn2": pn2}
+
+
+# ---- ReconstructH / ReconstructF (Initializer.cpp:596-963, CheckRT :1017-1118) ----
+def _det3(m):
+    S = np.asarray(m, F).astype(np.float64)
+    return (S[0, 0] * (S[1, 1] * S[2, 2] - S[1, 2] * S[2, 1]) - S[0, 1] * (S[1, 0] * S[2, 2] - S[1, 2] * S[2, 0]) +
+            S[0, 2] * (S[1, 0] * S[2, 1] - S[1, 1] * S[2, 0]))
+
+
+def _svd3(M):
+    """cv::SVD::compute of a 3x3 float Mat: (w, U, Vt) as floats (LAPACK in
+    double; sign conventions only reorder the hypotheses)"""
+    u, w, vt = np.linalg.svd(np.asarray(M, F).astype(np.float64))
+    return w.astype(F), u.astype(F), vt.astype(F)
+
+
+def _unit(t):
+    t = np.asarray(t, F)
+    nrm = np.sqrt(np.sum(t.astype(np.float64) ** 2))
+    return (t.astype(np.float64) * (1.0 / nrm)).astype(F)
+
+
+def _gemv(A, x):
+    A64, x64 = np.asarray(A, F).astype(np.float64), np.asarray(x, F).astype(np.float64)
+    return np.array([(A64[i, 0] * x64[0] + A64[i, 1] * x64[1]) + A64[i, 2] * x64[2] for i in range(3)]).astype(F)
+
+
+def homography_hypotheses(H21, K):
+    """ReconstructH's eight (R, t) (:700-850), or [] when d1/d2 or d2/d3 < 1.00001"""
+    A = mul3(mul3(inv3(K), H21), K)
+    w, U, Vt = _svd3(A)
+    s = F(_det3(U) * _det3(Vt))
+    d1, d2, d3 = w
+    if float(F(d1 / d2)) < 1.00001 or float(F(d2 / d3)) < 1.00001:
+        return []
+    aux1 = F(np.sqrt(F(F(d1 * d1 - d2 * d2) / F(d1 * d1 - d3 * d3))))
+    aux3 = F(np.sqrt(F(F(d2 * d2 - d3 * d3) / F(d1 * d1 - d3 * d3))))
+    x1, x3 = [aux1, aux1, -aux1, -aux1], [aux3, -aux3, aux3, -aux3]
+    ast = F(F(np.sqrt(F(F(d1 * d1 - d2 * d2) * F(d2 * d2 - d3 * d3)))) / F(F(d1 + d3) * d2))
+    cth = F(F(F(d2 * d2) + F(d1 * d3)) / F(F(d1 + d3) * d2))
+    asp = F(F(np.sqrt(F(F(d1 * d1 - d2 * d2) * F(d2 * d2 - d3 * d3)))) / F(F(d1 - d3) * d2))
+    cph = F(F(F(d1 * d3) - F(d2 * d2)) / F(F(d1 - d3) * d2))
+    st, sp = [ast, -ast, -ast, ast], [asp, -asp, -asp, asp]
+    out = []
+    for pas in range(2):
+        for i in range(4):
+            Rp = np.eye(3, dtype=F)
+            if pas == 0:
+                Rp[0, 0], Rp[0, 2], Rp[2, 0], Rp[2, 2] = cth, -st[i], st[i], cth
+                tp = np.array([x1[i], 0, -x3[i]], F) * F(d1 - d3)
+            else:
+                Rp[0, 0], Rp[0, 2], Rp[1, 1], Rp[2, 0], Rp[2, 2] = cph, sp[i], -1, sp[i], -cph
+                tp = np.array([x1[i], 0, x3[i]], F) * F(d1 + d3)
+            URp = (U.astype(np.float64) @ Rp.astype(np.float64) * float(s)).astype(F)
+            out.append((mul3(URp, Vt), _unit(_gemv(U, tp.astype(F)))))
+    return out
+
+
+def fundamental_hypotheses(F21, K):
+    """DecomposeE (:1120-1150) of E21 = K^T F21 K; ReconstructF's order
+    (R1, t), (R2, t), (R1, -t), (R2, -t)"""
+    E = mul3(mul3(np.asarray(K, F).T.copy(), F21), K)
+    w, U, Vt = _svd3(E)
+    t = _unit(U[:, 2])
+    W = np.array([[0, -1, 0], [1, 0, 0], [0, 0, 1]], F)
+    R1 = mul3(mul3(U, W), Vt)
+    if _det3(R1) < 0:
+        R1 = -R1
+    R2 = mul3(mul3(U, W.T.copy()), Vt)
+    if _det3(R2) < 0:
+        R2 = -R2
+    return [(R1, t), (R2, t), (R1, -t), (R2, -t)]
+
+
+def check_rt(R, t, pts, inliers, K, th2):
+    """CheckRT (:1017-1118) for one hypothesis: (nGood, parallax, counted[n],
+    good[n], p3d (n, 3)) per match (the reference indexes the last three by
+    the match's first keypoint)."""
+    K = np.asarray(K, F)
+    fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+    Rt = np.concatenate([np.asarray(R, F), np.asarray(t, F).reshape(3, 1)], 1)
+    P2 = (K.astype(np.float64) @ Rt.astype(np.float64)).astype(F)
+    O2 = (-(np.asarray(R, F).T.astype(np.float64) @ np.asarray(t, F).astype(np.float64))).astype(F)
+    P1 = np.zeros((3, 4), F)
+    P1[:, :3] = K
+    n = len(pts)
+    counted, good = np.zeros(n, bool), np.zeros(n, bool)
+    p3d = np.zeros((n, 3), F)
+    cosv = []
+    for m in range(n):
+        if not inliers[m]:
+            continue
+        u1, v1, u2, v2 = (F(x) for x in pts[m])
+        A = np.stack([u1 * P1[2] - P1[0], v1 * P1[2] - P1[1], u2 * P2[2] - P2[0], v2 * P2[2] - P2[1]]).astype(F)
+        _, _, vt = np.linalg.svd(A.astype(np.float64))
+        x = vt[3].astype(F)
+        X = (x[:3] / x[3]).astype(F)
+        if not np.all(np.isfinite(X)):
+            continue
+        d1 = F(np.sqrt(np.sum(X.astype(np.float64) ** 2)))
+        n2 = (X - O2).astype(F)
+        d2 = F(np.sqrt(np.sum(n2.astype(np.float64) ** 2)))
+        cp = F(float(np.dot(X.astype(np.float64), n2.astype(np.float64))) / float(F(d1 * d2)))
+        if X[2] <= 0 and float(cp) < 0.99998:
+            continue
+        Xc2 = (_gemv(R, X) + np.asarray(t, F)).astype(F)
+        if Xc2[2] <= 0 and float(cp) < 0.99998:
+            continue
+        iz1 = F(F(1.0) / X[2])
+        im1x, im1y = F(F(fx * X[0]) * iz1 + cx), F(F(fy * X[1]) * iz1 + cy)
+        if F(F((im1x - u1) * (im1x - u1)) + F((im1y - v1) * (im1y - v1))) > th2:
+            continue
+        iz2 = F(F(1.0) / Xc2[2])
+        im2x, im2y = F(F(fx * Xc2[0]) * iz2 + cx), F(F(fy * Xc2[1]) * iz2 + cy)
+        if F(F((im2x - u2) * (im2x - u2)) + F((im2y - v2) * (im2y - v2))) > th2:
+            continue
+        cosv.append(cp)
+        counted[m] = True
+        p3d[m] = X
+        good[m] = float(cp) < 0.99998
+    ng = int(counted.sum())
+    if ng:
+        cosv.sort()
+        par = F(float(F(np.arccos(cosv[min(50, ng - 1)]) * F(180))) / np.pi)
+    else:
+        par = F(0)
+    return ng, par, counted, good, p3d
+
+
+def reconstruct(model, kp1, kp2, pairs, inliers, M21, K, sigma=1.0, min_parallax=1.0, min_triangulated=50):
+    """ReconstructH (model 0) / ReconstructF (model 1): dict with ok, best,
+    hyps [(R, t)], n_good, parallax, R21, t21, p3d (n1, 3), triangulated (n1)."""
+    pairs = np.asarray(pairs).reshape(-1, 2)
+    pts = np.concatenate([np.asarray(kp1, F)[pairs[:, 0]], np.asarray(kp2, F)[pairs[:, 1]]], 1)
+    N = int(np.sum(np.asarray(inliers) != 0))
+    hy = homography_hypotheses(M21, K) if model == 0 else fundamental_hypotheses(M21, K)
+    th2 = F(4.0 * float(F(F(sigma) * F(sigma))))
+    res = [check_rt(R, t, pts, inliers, K, th2) for R, t in hy]
+    ng = [r[0] for r in res]
+    par = [r[1] for r in res]
+    best, ok = -1, False
+    if model == 0 and hy:
+        bg, sbg, bp = 0, 0, F(-1)
+        for i in range(len(hy)):
+            if ng[i] > bg:
+                sbg, bg, best, bp = bg, ng[i], i, par[i]
+            elif ng[i] > sbg:
+                sbg = ng[i]
+        ok = sbg < 0.75 * bg and bp >= min_parallax and bg > min_triangulated and bg > 0.9 * N
+    elif model == 1:
+        mg = max(ng)
+        nmin = max(int(0.9 * N), min_triangulated)
+        nsim = sum(1 for g in ng if g > 0.7 * mg)
+        if not (mg < nmin or nsim > 1):
+            best = ng.index(mg)
+            ok = par[best] > min_parallax
+    n1 = len(kp1)
+    p3d, tri = np.zeros((n1, 3), F), np.zeros(n1, bool)
+    if ok:
+        _, _, counted, good, P = res[best]
+        for m in np.nonzero(counted)[0]:
+            p3d[pairs[m, 0]] = P[m]
+            tri[pairs[m, 0]] = good[m]
+    return {"ok": bool(ok), "best": best, "hyps": hy, "n_good": ng, "parallax": par,
+            "R21": hy[best][0] if best >= 0 else None, "t21": hy[best][1] if best >= 0 else None,
+            "p3d": p3d, "triangulated": tri}

@@ -1,0 +1,467 @@
+// init_reconstruct.hip -- Initializer::ReconstructH / ReconstructF
+// (src/Initializer.cpp:596-963) with CheckRT (:1017-1118), Triangulate
+// (:930-945) and DecomposeE (:1120-1150) (include/orbgpu_init.h,
+// orbgpu_init_reconstruct).
+//
+// The motion hypotheses are a handful of 3x3 decompositions per call and
+// are built on the host (8 for a homography, 4 for an essential matrix);
+// CheckRT -- a 4x4 linear triangulation plus the depth, parallax and
+// reprojection tests for every inlier match under every hypothesis -- is
+// the data-parallel part and runs on the GPU: one 256-thread block per
+// hypothesis, lanes over matches.  The block also counts nGood and finds
+// the parallax the reference reads after sorting (the min(50, nGood-1)-th
+// smallest cosine) by an order-statistic walk over the cosines kept in LDS.
+//
+// OpenCV's SVDs (cv::SVD::compute of float Mats, Jacobi in float) are not
+// reproducible bit for bit: the 3x3 decompositions and each match's 4x4
+// null vector are computed by one-sided Jacobi in double and rounded to
+// float where the reference holds floats.  Every other operation follows
+// the reference's float expression order.  Sign conventions of the SVD only
+// reorder the hypothesis set, the kept motion is the
+// same.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../../include/orbgpu_init.h"
+#include "epnp.h"
+#include "host_common.h"
+
+namespace orbgpu {
+
+namespace {
+
+constexpr int kRecThreads = 256;
+constexpr int kRecMaxMatches = 16384;  // LDS: one u32 cosine key per match
+
+struct RecHyp {
+    float R[9], t[3];
+    float P2[12];  // K*[R|t]
+    float O2[3];   // -R^T t
+};
+
+__device__ inline float dotd3f(const float* a, const float* x) {  // cv::Mat product, double accumulation
+    return (float)((double)a[0] * x[0] + (double)a[1] * x[1] + (double)a[2] * x[2]);
+}
+
+// float -> u32 key with the float order (no NaN expected)
+__device__ inline unsigned ord_key(float f) {
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ inline float key_float(unsigned k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+__global__ __launch_bounds__(kRecThreads) void check_rt_kernel(const float4* __restrict__ pts,
+                                                               const unsigned char* __restrict__ inl, int n,
+                                                               const RecHyp* __restrict__ hyps, float fx, float fy,
+                                                               float cx, float cy, float th2,
+                                                               int* __restrict__ n_good, float* __restrict__ parallax,
+                                                               unsigned char* __restrict__ good,
+                                                               float* __restrict__ p3d) {
+    extern __shared__ unsigned s_key[];  // cosine keys of the counted matches, ~0u elsewhere
+    __shared__ int s_cnt;
+    const int h = blockIdx.x, tid = threadIdx.x;
+    const RecHyp H = hyps[h];
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+    int cnt = 0;
+    for (int m = tid; m < n; m += kRecThreads) {
+        unsigned key = ~0u;
+        unsigned char gflag = 0;
+        float X[3] = {0.f, 0.f, 0.f};
+        if (inl[m]) {
+            const float4 p = pts[m];  // (kp1.x, kp1.y, kp2.x, kp2.y)
+            // Triangulate (:930-945): A rows = x * P.row(2) - P.row(0), ...; P1 = [K|0]
+            double A[16];
+            const float P1r0[4] = {fx, 0.f, cx, 0.f}, P1r1[4] = {0.f, fy, cy, 0.f}, P1r2[4] = {0.f, 0.f, 1.f, 0.f};
+            for (int c = 0; c < 4; ++c) {
+                A[c] = (double)(p.x * P1r2[c] - P1r0[c]);
+                A[4 + c] = (double)(p.y * P1r2[c] - P1r1[c]);
+                A[8 + c] = (double)(p.z * H.P2[8 + c] - H.P2[c]);
+                A[12 + c] = (double)(p.w * H.P2[8 + c] - H.P2[4 + c]);
+            }
+            double s[4], v[16];
+            epnp::svd_hestenes<4, 4>(A, s, v);
+            int jmin = 0;
+            for (int j = 1; j < 4; ++j)
+                if (s[j] < s[jmin]) jmin = j;
+            const float w3 = (float)v[12 + jmin];  // x3D = vt.row(3).t(); rowRange(0,3) / x3D(3)
+            for (int k = 0; k < 3; ++k) X[k] = (float)v[4 * k + jmin] / w3;
+            bool ok = isfinite(X[0]) && isfinite(X[1]) && isfinite(X[2]);
+            float cosPar = 0.f;
+            if (ok) {
+                const float dist1 = (float)sqrt((double)X[0] * X[0] + (double)X[1] * X[1] + (double)X[2] * X[2]);
+                const float n2[3] = {X[0] - H.O2[0], X[1] - H.O2[1], X[2] - H.O2[2]};
+                const float dist2 = (float)sqrt((double)n2[0] * n2[0] + (double)n2[1] * n2[1] + (double)n2[2] * n2[2]);
+                const double dot = (double)X[0] * n2[0] + (double)X[1] * n2[1] + (double)X[2] * n2[2];
+                cosPar = (float)(dot / (double)(dist1 * dist2));
+                if (X[2] <= 0.f && (double)cosPar < 0.99998) ok = false;
+                float Xc2[3];
+                for (int r = 0; r < 3; ++r) Xc2[r] = dotd3f(H.R + 3 * r, X) + H.t[r];
+                if (ok && Xc2[2] <= 0.f && (double)cosPar < 0.99998) ok = false;
+                if (ok) {
+                    const float invZ1 = 1.0f / X[2];
+                    const float im1x = fx * X[0] * invZ1 + cx, im1y = fy * X[1] * invZ1 + cy;
+                    const float e1 = (im1x - p.x) * (im1x - p.x) + (im1y - p.y) * (im1y - p.y);
+                    if (e1 > th2) ok = false;
+                }
+                if (ok) {
+                    const float invZ2 = 1.0f / Xc2[2];
+                    const float im2x = fx * Xc2[0] * invZ2 + cx, im2y = fy * Xc2[1] * invZ2 + cy;
+                    const float e2 = (im2x - p.z) * (im2x - p.z) + (im2y - p.w) * (im2y - p.w);
+                    if (e2 > th2) ok = false;
+                }
+            }
+            if (ok) {
+                key = min(ord_key(cosPar), 0xFFFFFFFEu);  // ~0u marks a match CheckRT did not count
+                gflag = (double)cosPar < 0.99998 ? 1 : 0;
+                ++cnt;
+            } else {
+                X[0] = X[1] = X[2] = 0.f;
+            }
+        }
+        s_key[m] = key;
+        good[(size_t)h * n + m] = key != ~0u ? (unsigned char)(gflag | 2) : 0;  // bit 1: counted in nGood
+        float* o = p3d + 3 * ((size_t)h * n + m);
+        o[0] = X[0];
+        o[1] = X[1];
+        o[2] = X[2];
+    }
+    atomicAdd(&s_cnt, cnt);
+    __syncthreads();
+    if (tid >= 64) return;
+    // wave 0: the k-th smallest cosine, k = min(50, nGood - 1) (:1102-1110), walking the distinct values
+    const int ng = s_cnt;
+    float par = 0.f;
+    if (ng > 0) {
+        const int k = min(50, ng - 1);
+        unsigned last = 0u;
+        int below = 0;  // keys < current value
+        bool first = true;
+        unsigned val = 0u;
+        while (true) {
+            unsigned mn = ~0u;
+            for (int m = tid; m < n; m += 64) {
+                const unsigned kk = s_key[m];
+                if (kk != ~0u && (first || kk > last)) mn = min(mn, kk);
+            }
+            for (int o = 32; o > 0; o >>= 1) mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
+            if (mn == ~0u) break;  // unreachable: ng keys are present
+            int eq = 0;
+            for (int m = tid; m < n; m += 64) eq += s_key[m] == mn ? 1 : 0;
+            for (int o = 32; o > 0; o >>= 1) eq += __shfl_xor(eq, o, 64);
+            if (below + eq > k) {
+                val = mn;
+                break;
+            }
+            below += eq;
+            last = mn;
+            first = false;
+        }
+        // parallax = acos(c) * 180 / CV_PI (float acos, float * int, then the double division)
+        par = (float)((double)(acosf(key_float(val)) * 180) / 3.14159265358979323846);
+    }
+    if (tid == 0) {
+        n_good[h] = ng;
+        parallax[h] = par;
+    }
+}
+
+// ---- host: the 3x3 decompositions ------------------------------------------------
+void mul3h(const float* a, const float* b, float* c) {  // float gemm, double accumulation
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            c[3 * i + j] = (float)((double)a[3 * i] * b[j] + (double)a[3 * i + 1] * b[3 + j] +
+                                   (double)a[3 * i + 2] * b[6 + j]);
+}
+
+void inv3h(const float* m, float* o) {  // cv::Mat::inv() of a 3x3 CV_32F (closed form, double)
+    auto S = [&](int r, int c) { return (double)m[3 * r + c]; };
+    const double d0 = S(0, 0) * (S(1, 1) * S(2, 2) - S(1, 2) * S(2, 1)) -
+                      S(0, 1) * (S(1, 0) * S(2, 2) - S(1, 2) * S(2, 0)) +
+                      S(0, 2) * (S(1, 0) * S(2, 1) - S(1, 1) * S(2, 0));
+    if (d0 == 0.0) {
+        for (int k = 0; k < 9; ++k) o[k] = 0.f;
+        return;
+    }
+    const double d = 1.0 / d0;
+    o[0] = (float)((S(1, 1) * S(2, 2) - S(1, 2) * S(2, 1)) * d);
+    o[1] = (float)((S(0, 2) * S(2, 1) - S(0, 1) * S(2, 2)) * d);
+    o[2] = (float)((S(0, 1) * S(1, 2) - S(0, 2) * S(1, 1)) * d);
+    o[3] = (float)((S(1, 2) * S(2, 0) - S(1, 0) * S(2, 2)) * d);
+    o[4] = (float)((S(0, 0) * S(2, 2) - S(0, 2) * S(2, 0)) * d);
+    o[5] = (float)((S(0, 2) * S(1, 0) - S(0, 0) * S(1, 2)) * d);
+    o[6] = (float)((S(1, 0) * S(2, 1) - S(1, 1) * S(2, 0)) * d);
+    o[7] = (float)((S(0, 1) * S(2, 0) - S(0, 0) * S(2, 1)) * d);
+    o[8] = (float)((S(0, 0) * S(1, 1) - S(0, 1) * S(1, 0)) * d);
+}
+
+double det3(const float* m) {  // cv::determinant of a 3x3 CV_32F (double)
+    auto S = [&](int r, int c) { return (double)m[3 * r + c]; };
+    return S(0, 0) * (S(1, 1) * S(2, 2) - S(1, 2) * S(2, 1)) - S(0, 1) * (S(1, 0) * S(2, 2) - S(1, 2) * S(2, 0)) +
+           S(0, 2) * (S(1, 0) * S(2, 1) - S(1, 1) * S(2, 0));
+}
+
+// cv::SVD::compute of a 3x3 float matrix: w descending, U and Vt as floats.
+// Jacobi on the columns in double; U's third column completes a right-handed
+// basis when sigma3 is ~0 (E: rank 2), any consistent choice only reorders
+// the reference's hypothesis set.
+void svd3(const float* M, float* w, float* U, float* Vt) {
+    double a[9], s[3], v[9];
+    for (int k = 0; k < 9; ++k) a[k] = M[k];
+    epnp::svd_hestenes<3, 3>(a, s, v);
+    int o[3] = {0, 1, 2};
+    std::sort(o, o + 3, [&](int x, int y) { return s[x] > s[y]; });
+    double u[3][3], vv[3][3];
+    for (int j = 0; j < 3; ++j) {
+        for (int k = 0; k < 3; ++k) vv[j][k] = v[3 * k + o[j]];
+        for (int k = 0; k < 3; ++k) u[j][k] = s[o[j]] > 0 ? a[3 * k + o[j]] / s[o[j]] : 0.0;
+    }
+    if (!(s[o[2]] > 1e-9 * s[o[0]])) {  // u3 = u1 x u2
+        u[2][0] = u[0][1] * u[1][2] - u[0][2] * u[1][1];
+        u[2][1] = u[0][2] * u[1][0] - u[0][0] * u[1][2];
+        u[2][2] = u[0][0] * u[1][1] - u[0][1] * u[1][0];
+    }
+    for (int j = 0; j < 3; ++j) {
+        w[j] = (float)s[o[j]];
+        for (int k = 0; k < 3; ++k) {
+            U[3 * k + j] = (float)u[j][k];
+            Vt[3 * j + k] = (float)vv[j][k];
+        }
+    }
+}
+
+void scale_norm(float* t) {  // t = t / cv::norm(t): double norm, alpha = 1/norm
+    const double nrm = std::sqrt((double)t[0] * t[0] + (double)t[1] * t[1] + (double)t[2] * t[2]);
+    const double al = 1.0 / nrm;
+    for (int k = 0; k < 3; ++k) t[k] = (float)((double)t[k] * al);
+}
+
+// ReconstructH's eight (R, t) (:707-850); false when d1/d2 or d2/d3 < 1.00001
+bool homography_hyps(const float* H21, const float* K, std::vector<RecHyp>& hy) {
+    float invK[9], tmp[9], A[9], U[9], w[3], Vt[9];
+    inv3h(K, invK);
+    mul3h(invK, H21, tmp);
+    mul3h(tmp, K, A);
+    svd3(A, w, U, Vt);
+    const float s = (float)(det3(U) * det3(Vt));
+    const float d1 = w[0], d2 = w[1], d3 = w[2];
+    if ((double)(d1 / d2) < 1.00001 || (double)(d2 / d3) < 1.00001) return false;
+    const float aux1 = std::sqrt((d1 * d1 - d2 * d2) / (d1 * d1 - d3 * d3));
+    const float aux3 = std::sqrt((d2 * d2 - d3 * d3) / (d1 * d1 - d3 * d3));
+    const float x1[4] = {aux1, aux1, -aux1, -aux1}, x3[4] = {aux3, -aux3, aux3, -aux3};
+    const float aux_st = std::sqrt((d1 * d1 - d2 * d2) * (d2 * d2 - d3 * d3)) / ((d1 + d3) * d2);
+    const float cth = (d2 * d2 + d1 * d3) / ((d1 + d3) * d2);
+    const float st[4] = {aux_st, -aux_st, -aux_st, aux_st};
+    const float aux_sp = std::sqrt((d1 * d1 - d2 * d2) * (d2 * d2 - d3 * d3)) / ((d1 - d3) * d2);
+    const float cph = (d1 * d3 - d2 * d2) / ((d1 - d3) * d2);
+    const float sp[4] = {aux_sp, -aux_sp, -aux_sp, aux_sp};
+    for (int pass = 0; pass < 2; ++pass)
+        for (int i = 0; i < 4; ++i) {
+            float Rp[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+            float tp[3];
+            if (pass == 0) {  // d' = d2 (:734-782)
+                Rp[0] = cth; Rp[2] = -st[i]; Rp[6] = st[i]; Rp[8] = cth;
+                tp[0] = x1[i]; tp[1] = 0; tp[2] = -x3[i];
+                for (float& x : tp) x *= d1 - d3;
+            } else {  // d' = -d2 (:786-836)
+                Rp[0] = cph; Rp[2] = sp[i]; Rp[4] = -1; Rp[6] = sp[i]; Rp[8] = -cph;
+                tp[0] = x1[i]; tp[1] = 0; tp[2] = x3[i];
+                for (float& x : tp) x *= d1 + d3;
+            }
+            RecHyp hh{};
+            float sU[9], URp[9];
+            for (int r = 0; r < 3; ++r)  // s*U*Rp: one gemm with alpha = s
+                for (int c = 0; c < 3; ++c)
+                    URp[3 * r + c] = (float)(((double)U[3 * r] * Rp[c] + (double)U[3 * r + 1] * Rp[3 + c] +
+                                              (double)U[3 * r + 2] * Rp[6 + c]) * (double)s);
+            (void)sU;
+            mul3h(URp, Vt, hh.R);
+            for (int r = 0; r < 3; ++r)
+                hh.t[r] = (float)((double)U[3 * r] * tp[0] + (double)U[3 * r + 1] * tp[1] + (double)U[3 * r + 2] * tp[2]);
+            scale_norm(hh.t);
+            hy.push_back(hh);
+        }
+    return true;
+}
+
+// DecomposeE (:1120-1150) and ReconstructF's four (R, t) in its order:
+// (R1, t), (R2, t), (R1, -t), (R2, -t)
+void fundamental_hyps(const float* F21, const float* K, std::vector<RecHyp>& hy) {
+    float Kt[9], tmp[9], E[9], U[9], w[3], Vt[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) Kt[3 * r + c] = K[3 * c + r];
+    mul3h(Kt, F21, tmp);
+    mul3h(tmp, K, E);
+    svd3(E, w, U, Vt);
+    float t[3] = {U[2], U[5], U[8]};
+    scale_norm(t);
+    const float W[9] = {0, -1, 0, 1, 0, 0, 0, 0, 1}, Wt[9] = {0, 1, 0, -1, 0, 0, 0, 0, 1};
+    float uw[9], R1[9], R2[9];
+    mul3h(U, W, uw);
+    mul3h(uw, Vt, R1);
+    if (det3(R1) < 0)
+        for (float& x : R1) x = -x;
+    mul3h(U, Wt, uw);
+    mul3h(uw, Vt, R2);
+    if (det3(R2) < 0)
+        for (float& x : R2) x = -x;
+    const float* Rs[4] = {R1, R2, R1, R2};
+    for (int i = 0; i < 4; ++i) {
+        RecHyp hh{};
+        std::memcpy(hh.R, Rs[i], sizeof(hh.R));
+        for (int k = 0; k < 3; ++k) hh.t[k] = i < 2 ? t[k] : -t[k];
+        hy.push_back(hh);
+    }
+}
+
+}  // namespace
+
+}  // namespace orbgpu
+
+using namespace orbgpu;
+
+extern "C" int orbgpu_init_reconstruct(int model, const float* kp1, int n1, const float* kp2, int n2,
+                                       const int* pairs, int n_matches, const unsigned char* inliers,
+                                       const float* M21, const float* K, float sigma, float min_parallax,
+                                       int min_triangulated, orbgpu_init_reconstruction* out, float* p3d,
+                                       unsigned char* triangulated) {
+    if (!out || (model != ORBGPU_INIT_MODEL_H && model != ORBGPU_INIT_MODEL_F) || n1 < 0 || n2 < 0 ||
+        n_matches < 0 || !M21 || !K || (n_matches > 0 && (!pairs || !inliers || !kp1 || !kp2)))
+        return fail(ORBGPU_ERR_ARG, "invalid argument");
+    if (n_matches > kRecMaxMatches) return fail(ORBGPU_ERR_CAPACITY, "more than 16384 matches");
+    for (int i = 0; i < n_matches; ++i)
+        if (pairs[2 * i] < 0 || pairs[2 * i] >= n1 || pairs[2 * i + 1] < 0 || pairs[2 * i + 1] >= n2)
+            return fail(ORBGPU_ERR_ARG, "match index out of range");
+    std::memset(out, 0, sizeof(*out));
+    out->best = -1;
+    if (p3d) std::memset(p3d, 0, sizeof(float) * 3 * (size_t)n1);
+    if (triangulated) std::memset(triangulated, 0, (size_t)n1);
+    int N = 0;
+    for (int i = 0; i < n_matches; ++i) N += inliers[i] ? 1 : 0;
+    std::vector<RecHyp> hy;
+    if (model == ORBGPU_INIT_MODEL_H) {
+        if (!homography_hyps(M21, K, hy)) return ORBGPU_OK;  // ok = 0 (:703-706)
+    } else {
+        fundamental_hyps(M21, K, hy);
+    }
+    const int nh = (int)hy.size();
+    out->n_hyp = nh;
+    const float fx = K[0], fy = K[4], cx = K[2], cy = K[5];
+    for (RecHyp& h : hy) {  // P2 = K*[R|t] (:1042-1045), O2 = -R^T t (:1047)
+        float Rt[12];
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c) Rt[4 * r + c] = h.R[3 * r + c];
+            Rt[4 * r + 3] = h.t[r];
+        }
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 4; ++c)
+                h.P2[4 * r + c] = (float)((double)K[3 * r] * Rt[c] + (double)K[3 * r + 1] * Rt[4 + c] +
+                                          (double)K[3 * r + 2] * Rt[8 + c]);
+        for (int j = 0; j < 3; ++j)
+            h.O2[j] = -(float)((double)h.R[j] * h.t[0] + (double)h.R[3 + j] * h.t[1] + (double)h.R[6 + j] * h.t[2]);
+    }
+    int rc = check_device();
+    if (rc) return rc;
+    const int n = std::max(n_matches, 1);
+    std::vector<float> pts(4 * (size_t)n, 0.f);
+    for (int i = 0; i < n_matches; ++i) {
+        const int a = pairs[2 * i], b = pairs[2 * i + 1];
+        pts[4 * i] = kp1[2 * a];
+        pts[4 * i + 1] = kp1[2 * a + 1];
+        pts[4 * i + 2] = kp2[2 * b];
+        pts[4 * i + 3] = kp2[2 * b + 1];
+    }
+    std::vector<unsigned char> inl(n, 0);
+    if (n_matches) std::memcpy(inl.data(), inliers, n_matches);
+    const float mSigma2 = sigma * sigma;
+    const float th2 = (float)(4.0 * mSigma2);
+    void *d_pts = nullptr, *d_inl = nullptr, *d_h = nullptr, *d_ng = nullptr, *d_par = nullptr, *d_good = nullptr,
+         *d_p3 = nullptr;
+    auto cleanup = [&]() {
+        for (void* p : {d_pts, d_inl, d_h, d_ng, d_par, d_good, d_p3})
+            if (p) (void)hipFree(p);
+    };
+    const size_t nhn = (size_t)nh * n;
+    if (hipMalloc(&d_pts, pts.size() * 4) != hipSuccess || hipMalloc(&d_inl, n) != hipSuccess ||
+        hipMalloc(&d_h, sizeof(RecHyp) * nh) != hipSuccess || hipMalloc(&d_ng, 4 * nh) != hipSuccess ||
+        hipMalloc(&d_par, 4 * nh) != hipSuccess || hipMalloc(&d_good, nhn) != hipSuccess ||
+        hipMalloc(&d_p3, 12 * nhn) != hipSuccess) {
+        cleanup();
+        return fail(ORBGPU_ERR_HIP, "allocation failed");
+    }
+    std::vector<int> ng(nh);
+    std::vector<float> par(nh);
+    std::vector<unsigned char> good(nhn);
+    std::vector<float> P3(3 * nhn);
+    bool ok = hipMemcpy(d_pts, pts.data(), pts.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d_inl, inl.data(), n, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d_h, hy.data(), sizeof(RecHyp) * nh, hipMemcpyHostToDevice) == hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL(check_rt_kernel, dim3(nh), dim3(kRecThreads), 4 * (size_t)n, nullptr,
+                           (const float4*)d_pts, (const unsigned char*)d_inl, n_matches, (const RecHyp*)d_h, fx, fy,
+                           cx, cy, th2, (int*)d_ng, (float*)d_par, (unsigned char*)d_good, (float*)d_p3);
+        ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+             hipMemcpy(ng.data(), d_ng, 4 * nh, hipMemcpyDeviceToHost) == hipSuccess &&
+             hipMemcpy(par.data(), d_par, 4 * nh, hipMemcpyDeviceToHost) == hipSuccess &&
+             hipMemcpy(good.data(), d_good, nhn, hipMemcpyDeviceToHost) == hipSuccess &&
+             hipMemcpy(P3.data(), d_p3, 12 * nhn, hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    cleanup();
+    if (!ok) return fail(ORBGPU_ERR_HIP, "CheckRT failed");
+    for (int i = 0; i < nh; ++i) {
+        out->n_good[i] = ng[i];
+        out->parallax[i] = par[i];
+    }
+    int best = -1;
+    if (model == ORBGPU_INIT_MODEL_H) {  // :853-910
+        int bestGood = 0, secondBestGood = 0;
+        float bestParallax = -1;
+        for (int i = 0; i < nh; ++i) {
+            if (ng[i] > bestGood) {
+                secondBestGood = bestGood;
+                bestGood = ng[i];
+                best = i;
+                bestParallax = par[i];
+            } else if (ng[i] > secondBestGood) {
+                secondBestGood = ng[i];
+            }
+        }
+        out->ok = secondBestGood < 0.75 * bestGood && bestParallax >= min_parallax && bestGood > min_triangulated &&
+                  bestGood > 0.9 * N;
+    } else {  // :620-690
+        const int maxGood = std::max(ng[0], std::max(ng[1], std::max(ng[2], ng[3])));
+        const int nMinGood = std::max(static_cast<int>(0.9 * N), min_triangulated);
+        int nsimilar = 0;
+        for (int i = 0; i < 4; ++i) nsimilar += ng[i] > 0.7 * maxGood ? 1 : 0;
+        if (!(maxGood < nMinGood || nsimilar > 1)) {
+            for (int i = 0; i < 4; ++i)
+                if (maxGood == ng[i]) {  // the first hypothesis reaching maxGood decides
+                    best = i;
+                    out->ok = par[i] > min_parallax;
+                    break;
+                }
+        }
+    }
+    out->best = best;
+    if (best >= 0) {
+        std::memcpy(out->R21, hy[best].R, sizeof(out->R21));
+        std::memcpy(out->t21, hy[best].t, sizeof(out->t21));
+    }
+    if (out->ok) {
+        for (int i = 0; i < n_matches; ++i) {
+            const unsigned char g = good[(size_t)best * n + i];
+            if (!(g & 2)) continue;  // counted by CheckRT: vP3D[first] written
+            const int a = pairs[2 * i];
+            if (p3d)
+                for (int k = 0; k < 3; ++k) p3d[3 * a + k] = P3[3 * ((size_t)best * n + i) + k];
+            if (triangulated) triangulated[a] = g & 1;
+        }
+    }
+    return ORBGPU_OK;
+}

@@ -8,6 +8,9 @@ ABI in include/orbgpu_init.h (csrc/init.hip).
 * ``check_both_batch`` -- both of the above in one launch.
 * ``select_best`` -- FindHomography / FindFundamental's kept iteration
   (:207-212, :264-269): first strict maximum above 0, or -1.
+* ``find_models`` -- Initialize up to the model choice (hypotheses + scores).
+* ``reconstruct`` -- ReconstructH / ReconstructF (:596-963): motion
+  hypotheses, CheckRT of each over the inliers on the GPU, the choice.
 
 Inputs are device tensors (torch, on the GPU); the matches are
 (u1, v1, u2, v2) = (mvKeys1[first].pt, mvKeys2[second].pt) rows.
@@ -182,3 +185,48 @@ def find_models(kp1, kp2, matches12, sigma=1.0, n_iter=200, sets=None, device="c
             "inliers_h": ih[bh].cpu().numpy().astype(bool) if bh >= 0 else np.zeros(nm, bool),
             "inliers_f": jf[bf].cpu().numpy().astype(bool) if bf >= 0 else np.zeros(nm, bool),
             "RH": np.float32(SH / np.float32(SH + SF)) if SH + SF > 0 else np.float32(0)}
+
+
+class Reconstruction(ctypes.Structure):
+    _fields_ = [("ok", ctypes.c_int), ("best", ctypes.c_int), ("n_hyp", ctypes.c_int),
+                ("n_good", ctypes.c_int * 8), ("parallax", ctypes.c_float * 8), ("R21", ctypes.c_float * 9),
+                ("t21", ctypes.c_float * 3)]
+
+
+MODEL_H, MODEL_F = 0, 1
+
+
+def reconstruct(model, kp1, kp2, matches12, inliers, M21, K, sigma=1.0, min_parallax=1.0, min_triangulated=50):
+    """Initializer::ReconstructH (model 0, M21 = H21) / ReconstructF (model 1,
+    M21 = F21).  kp1, kp2: (n, 2) keypoint positions; matches12: vector<int>
+    (mvMatches12 = the (i, m[i]) with m[i] >= 0); inliers: vbMatchesInliers
+    over those pairs.  Returns a dict: ok, best, n_good, parallax, R21, t21,
+    p3d (n1, 3), triangulated (n1)."""
+    L = _lib()
+    L.orbgpu_init_reconstruct.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_float,
+                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    m12 = np.asarray(matches12)
+    first = np.nonzero(m12 >= 0)[0]
+    pairs = np.ascontiguousarray(np.stack([first, m12[first]], 1), np.int32)
+    k1 = np.ascontiguousarray(np.asarray(kp1, np.float32).reshape(-1, 2))
+    k2 = np.ascontiguousarray(np.asarray(kp2, np.float32).reshape(-1, 2))
+    inl = np.ascontiguousarray(np.asarray(inliers).astype(np.uint8))
+    if len(inl) != len(pairs):
+        raise ValueError("inliers must hold one flag per match")
+    M = np.ascontiguousarray(np.asarray(M21, np.float32).reshape(9))
+    Km = np.ascontiguousarray(np.asarray(K, np.float32).reshape(9))
+    out = Reconstruction()
+    p3d = np.zeros((max(len(k1), 1), 3), np.float32)
+    tri = np.zeros(max(len(k1), 1), np.uint8)
+    orbgpu._check(L.orbgpu_init_reconstruct(int(model), k1.ctypes.data, len(k1), k2.ctypes.data, len(k2),
+                                            pairs.ctypes.data, len(pairs), inl.ctypes.data, M.ctypes.data,
+                                            Km.ctypes.data, float(sigma), float(min_parallax),
+                                            int(min_triangulated), ctypes.byref(out), p3d.ctypes.data,
+                                            tri.ctypes.data), "orbgpu_init_reconstruct")
+    nh = out.n_hyp
+    return {"ok": bool(out.ok), "best": out.best, "n_good": list(out.n_good[:nh]),
+            "parallax": np.array(out.parallax[:nh], np.float32),
+            "R21": np.array(out.R21, np.float32).reshape(3, 3), "t21": np.array(out.t21, np.float32),
+            "p3d": p3d[:len(k1)], "triangulated": tri[:len(k1)].astype(bool)}

@@ -311,3 +311,113 @@ def test_gpu_find_models_vs_oracle(n, planar, seed):
     bh = r["best_h"]
     ref_inl = init_ref.check_homography(r["pts"], r["H21"][bh], r["H12"][bh])[1]
     assert (g["inliers_h"] != ref_inl).sum() <= max(1, n // 200)
+
+
+# ---- ReconstructH / ReconstructF (Initializer.cpp:596-963) ----------------
+_A = 0.05
+_R_TRUE = np.array([[np.cos(_A), 0, np.sin(_A)], [0, 1, 0], [-np.sin(_A), 0, np.cos(_A)]])
+
+
+def _recon_scene(kind, n, seed):
+    """two views with the exact model and its inliers: "ground" (plane y = 1.5
+    seen with a lateral move: ReconstructH accepts), "tilted" (a tilted plane:
+    the classic two-fold homography ambiguity, ReconstructH refuses), "general"
+    (3-D points, ReconstructF accepts).  Returns kp1, kp2, m12, pairs, M, inl, t."""
+    rng = np.random.default_rng(seed)
+    if kind == "ground":
+        X = np.c_[rng.uniform(-4, 4, n), np.full(n, 1.5), rng.uniform(2, 20, n)]
+        t, nrm, d = np.array([0.6, 0.0, 0.0]), np.array([0, 1.0, 0]), 1.5
+    elif kind == "tilted":
+        x = rng.uniform(-2, 2, n)
+        X = np.c_[x, rng.uniform(-1.5, 1.5, n), 5.0 + 0.4 * x]
+        t, nrm, d = np.array([0.5, 0.05, 0.1]), np.array([-0.4, 0, 1.0]), 5.0
+    else:
+        X = np.c_[rng.uniform(-2, 2, n), rng.uniform(-1.5, 1.5, n), rng.uniform(3, 8, n)]
+        t = np.array([0.5, 0.05, 0.1])
+    x1, x2 = (K @ X.T).T, (K @ (_R_TRUE @ X.T + t[:, None])).T
+    p1 = (x1[:, :2] / x1[:, 2:]).astype(F)
+    p2 = (x2[:, :2] / x2[:, 2:] + rng.normal(0, 0.5, (n, 2))).astype(F)
+    keep = np.all((p1 >= 0) & (p1 < [640, 480]) & (p2 >= 0) & (p2 < [640, 480]), 1)
+    p1, p2 = p1[keep], p2[keep]
+    m = len(p1)
+    Ki = np.linalg.inv(K)
+    if kind == "general":
+        tx = np.array([[0, -t[2], t[1]], [t[2], 0, -t[0]], [-t[1], t[0], 0]])
+        M = Ki.T @ tx @ _R_TRUE @ Ki
+        M = (M / np.linalg.norm(M)).astype(F)
+        inl = init_ref.check_fundamental(np.c_[p1, p2], M)[1]
+    else:
+        M = K @ (_R_TRUE + np.outer(t, nrm) / d) @ Ki
+        M = (M / M[2, 2]).astype(F)
+        inl = init_ref.check_homography(np.c_[p1, p2], M, init_ref.inv3(M))[1]
+    # frame 2's keypoints in another order, plus unmatched extras in both frames
+    perm = rng.permutation(m)
+    kp1 = np.vstack([p1, rng.uniform([0, 0], [640, 480], (30, 2))]).astype(F)
+    kp2 = np.vstack([rng.uniform([0, 0], [640, 480], (30, 2)), p2[perm]]).astype(F)
+    m12 = np.full(len(kp1), -1, np.int32)
+    m12[perm] = np.arange(m) + 30
+    first = np.nonzero(m12 >= 0)[0]
+    pairs = np.stack([first, m12[first]], 1)
+    return kp1, kp2, m12, pairs, M, np.asarray(inl, bool), t
+
+
+def _rot_angle(Ra, Rb):
+    c = (np.trace(np.asarray(Ra, np.float64) @ np.asarray(Rb, np.float64).T) - 1) / 2
+    return np.degrees(np.arccos(np.clip(c, -1, 1)))
+
+
+@pytest.mark.parametrize("kind", ["ground", "general"])
+def test_oracle_reconstruct_recovers_motion(kind):
+    kp1, kp2, m12, pairs, M, inl, t = _recon_scene(kind, 500, 71)
+    r = init_ref.reconstruct(0 if kind == "ground" else 1, kp1, kp2, pairs, inl, M, K.astype(F))
+    assert r["ok"]
+    assert _rot_angle(r["R21"], _R_TRUE) < 0.5
+    assert np.dot(r["t21"], t / np.linalg.norm(t)) > 0.99
+    assert r["triangulated"].sum() > 0.5 * inl.sum()
+    k1, k2, _, pr, Mt, it, _ = _recon_scene("tilted", 500, 71)
+    assert not init_ref.reconstruct(0, k1, k2, pr, it, Mt, K.astype(F))["ok"]  # two hypotheses explain every inlier
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n,seed", [("ground", 500, 71), ("general", 500, 72), ("general", 1500, 73),
+                                         ("tilted", 500, 74), ("ground", 1200, 75)])
+def test_gpu_reconstruct_vs_oracle(kind, n, seed):
+    """ReconstructH / ReconstructF: hypotheses on the host, CheckRT on the GPU.
+    Tolerance (the SVDs are Jacobi in double on both sides, OpenCV's float
+    Jacobi is not reproducible): same decision and kept motion (R21, t21 to
+    1e-4), per-hypothesis nGood as multisets within 0.5 % + 2, the kept
+    hypothesis's parallax to 1e-3 relative, triangulated flags >= 99 % equal
+    and the 3-D points to 1e-3 relative where both triangulate."""
+    _gpu()
+    import initializer
+    kp1, kp2, m12, pairs, M, inl, _ = _recon_scene(kind, n, seed)
+    model = 0 if kind != "general" else 1
+    r = init_ref.reconstruct(model, kp1, kp2, pairs, inl, M, K.astype(F))
+    g = initializer.reconstruct(model, kp1, kp2, m12, inl, M, K.astype(F))
+    assert g["ok"] == r["ok"] == (kind != "tilted")
+    for a, b in zip(sorted(g["n_good"]), sorted(r["n_good"])):
+        assert abs(a - b) <= 2 + 0.005 * b
+    if r["ok"]:
+        np.testing.assert_allclose(g["R21"], r["R21"], atol=1e-4)
+        np.testing.assert_allclose(g["t21"], r["t21"], atol=1e-4)
+        pg, pr = float(g["parallax"][g["best"]]), float(r["parallax"][r["best"]])
+        assert abs(pg - pr) <= 1e-3 * pr
+        assert (g["triangulated"] == r["triangulated"]).mean() >= 0.99
+        both = g["triangulated"] & r["triangulated"]
+        assert both.sum() > 100
+        np.testing.assert_allclose(g["p3d"][both], r["p3d"][both], rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_gpu_reconstruct_degenerate():
+    """no inliers: CheckRT counts nothing, both models refuse"""
+    _gpu()
+    import initializer
+    kp1, kp2, m12, pairs, M, inl, _ = _recon_scene("general", 300, 76)
+    none = np.zeros_like(inl)
+    Mh = _recon_scene("ground", 300, 76)[4]
+    for model, Mm in ((0, Mh), (1, M)):
+        r = init_ref.reconstruct(model, kp1, kp2, pairs, none, Mm, K.astype(F))
+        g = initializer.reconstruct(model, kp1, kp2, m12, none, Mm, K.astype(F))
+        assert g["ok"] is False and r["ok"] is False
+        assert all(x == 0 for x in g["n_good"]) and g["n_good"] == r["n_good"]
