@@ -80,7 +80,8 @@ struct CellTiles {
     const uint8_t* win;  // staged window, pitch P, column c <-> level x = xa + c
     uint8_t* sc;         // FAST arc strength of corners, 0 elsewhere
     uint16_t* la;        // tile offsets passing the compass pre-test
-    uint16_t* lb;        // tile offsets of corners (row-major order)
+    uint16_t* lb;        // tile offsets of corners (row-major order); the same buffer as la: the
+                         // corner list is compacted in place behind the survivors being read
 };
 
 // FAST at threshold t on the cell's detection region: returns the number
@@ -214,13 +215,13 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     const int R = g.win_rows;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: metadata in SGPRs
-    const size_t per_wave = ((size_t)2 * P * R + 4 * (size_t)g.det_max + 15) & ~(size_t)15;
+    const size_t per_wave = ((size_t)2 * P * R + 2 * (size_t)g.det_max + 15) & ~(size_t)15;
     uint8_t* ws = smem + wave * per_wave;
     CellTiles T;
     T.win = ws;
     T.sc = ws + P * R;
     T.la = reinterpret_cast<uint16_t*>(ws + 2 * P * R);
-    T.lb = T.la + g.det_max;
+    T.lb = T.la;  // in-place: iteration `base` writes below base + 64 after reading la[base .. base + 64)
     uint8_t* s_win = ws;
 
     // one cell per wave; waves of a block take consecutive cells of a frame;
@@ -301,7 +302,7 @@ hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size
                              const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err,
                              hipStream_t stream) {
     const int items = g.total_cells * batch;
-    const size_t per_wave = ((size_t)2 * g.win_pitch * g.win_rows + 4 * (size_t)g.det_max + 15) & ~(size_t)15;
+    const size_t per_wave = ((size_t)2 * g.win_pitch * g.win_rows + 2 * (size_t)g.det_max + 15) & ~(size_t)15;
     dim3 grid((items + kCellWaves - 1) / kCellWaves);
     const size_t lds = per_wave * kCellWaves;
 #define ORBGPU_FAST_CASE(PP)                                                                                        \
