@@ -211,24 +211,31 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
     const int simd_end = L.w & ~3;
     if (lane < kQuads * kColChunks) {
         const int q = lane % kQuads, c = lane / kQuads, r0 = c * 7;
-        blurdev::f32x2 wl[13], wh[13];
-#pragma unroll
-        for (int k = 0; k < 13; ++k) {
+        // the 7 row sums the next output row needs, slid one row per output row
+        // (28 live registers instead of all 13 rows' 52)
+        blurdev::f32x2 wl[7], wh[7];
+        auto row = [&](int k, blurdev::f32x2& lo, blurdev::f32x2& hi) {
             const uint32_t* w = reinterpret_cast<const uint32_t*>(S.raw + min(r0 + k, kPatch - 1) * kRPitch) + q;
             blurdev::Raw3 R3;
             R3.a = w[0];
             R3.b = w[1];
             R3.c = w[2];
-            blurdev::row_pass_raw(R3, wl[k], wh[k]);
-        }
+            blurdev::row_pass_raw(R3, lo, hi);
+        };
+#pragma unroll
+        for (int k = 0; k < 6; ++k) row(k, wl[k + 1], wh[k + 1]);
         const bool simd = xb + 4 * q < simd_end;
 #pragma unroll
         for (int j = 0; j < 7; ++j) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                wl[k] = wl[k + 1];
+                wh[k] = wh[k + 1];
+            }
+            row(j + 6, wl[6], wh[6]);
             if (r0 + j < kBlur) {
-                const blurdev::f32x2 lo = blurdev::col_pass(wl[j], wl[j + 1], wl[j + 2], wl[j + 3], wl[j + 4], wl[j + 5],
-                                                            wl[j + 6]);
-                const blurdev::f32x2 hi = blurdev::col_pass(wh[j], wh[j + 1], wh[j + 2], wh[j + 3], wh[j + 4], wh[j + 5],
-                                                            wh[j + 6]);
+                const blurdev::f32x2 lo = blurdev::col_pass(wl[0], wl[1], wl[2], wl[3], wl[4], wl[5], wl[6]);
+                const blurdev::f32x2 hi = blurdev::col_pass(wh[0], wh[1], wh[2], wh[3], wh[4], wh[5], wh[6]);
                 reinterpret_cast<uint32_t*>(S.blur + (r0 + j) * kBPitch)[q] = blurdev::pack4(lo, hi, simd);
             }
         }
