@@ -10,6 +10,11 @@ GPU, inputs already resident in HBM:
     for the B consecutive pairs, the reference's map-free matcher
     (Tracking.cpp:768-769).
 value = frames processed by all ranks / max-over-ranks wall time.
+The matcher runs on a second HIP stream one step behind: step k-1's
+SearchForInitialization starts when step k's pyramid pass (which fills every
+CU) is done and overlaps step k's FAST / octree / describe (the extractor's
+stage-event hook, orbgpu_extractor_set_stage_event); the last step's match is
+issued before the timed region closes, so all K steps' work is inside it.
 
 The frames are ONE stream (shard.py): at step s rank r owns
 global frames [(s*N + r)*B, +B) -- contiguous chunks; the chunk-boundary
@@ -145,13 +150,44 @@ class StreamBench:
         self.gather = shard.OwnerGather(rank, world, [k0[1:], d0[1:], c0[1:], self.sets[0][3], self.sets[0][4]])
         self.flags = orbgpu.MATCH_CHECK_ORI
         self.step_no = 0
+        # The matcher runs on its own stream, one step behind: SearchForInitialization of
+        # step k-1 (a few hundred latency-bound blocks) starts once step k's pyramid pass --
+        # which wants every CU -- is done, and overlaps step k's FAST / octree / describe.
+        # The two output sets keep step k+1's extraction off the buffers step k-1's match
+        # reads (it waits for that match).  run() flushes the last match inside the timed
+        # region.
+        self.mstream = torch.cuda.Stream(dev)
+        self.ev_pyr = torch.cuda.Event()
+        self.ex.set_stage_event("pyramid", self.ev_pyr)
+        self.ev_ext = [torch.cuda.Event() for _ in range(2)]
+        self.ev_match = [None, None]
+        self.pending = None  # (set index, timing events) of the step whose match is not issued yet
+
+    def _match(self, si, after, ev=None):
+        import orbgpu
+        kps_all, desc_all, counts_all, m12, nmatch = self.sets[si]
+        ms = self.mstream
+        ms.wait_event(after)
+        if ev is not None:
+            ev[0].record(ms)
+        orbgpu.search_for_initialization_batch(self.W, self.H, kps_all[:-1], desc_all[:-1], counts_all[:-1],
+                                               kps_all[1:], desc_all[1:], counts_all[1:], m12, nmatch,
+                                               flags=self.flags, stream=ms)
+        if ev is not None:
+            ev[1].record(ms)
+        em = torch.cuda.Event()
+        em.record(ms)
+        self.ev_match[si] = em
+        with torch.cuda.stream(ms):  # the gather (RCCL send/recv) is ordered after the match
+            self.gather.start(si, [kps_all[1:], desc_all[1:], counts_all[1:], m12, nmatch])
 
     def step(self, ev=None):
-        import orbgpu
         B, st = self.B, self.stream
         si = self.step_no % 2
         kps_all, desc_all, counts_all, m12, nmatch = self.sets[si]
         self.gather.finish(si)  # the set's previous transfer is done before it is rewritten
+        if self.ev_match[si] is not None:  # ... and the match that read it (step k-2)
+            st.wait_event(self.ev_match[si])
         frames = self.pool[self.step_no % POOL_STEPS]
         self.ex.extract_batch(frames, kps_all[1:], desc_all[1:], counts_all[1:], stream=st, row_step=self.pitch,
                               frame_step=self.pitch * self.H)
@@ -159,19 +195,23 @@ class StreamBench:
         kps_all[0].copy_(prev[0])
         desc_all[0].copy_(prev[1])
         counts_all[0:1].copy_(prev[2])
-        if ev is not None:
-            ev[0].record(st)
-        orbgpu.search_for_initialization_batch(self.W, self.H, kps_all[:-1], desc_all[:-1], counts_all[:-1],
-                                               kps_all[1:], desc_all[1:], counts_all[1:], m12, nmatch,
-                                               flags=self.flags, stream=st)
-        if ev is not None:
-            ev[1].record(st)
-        self.gather.start(si, [kps_all[1:], desc_all[1:], counts_all[1:], m12, nmatch])
+        self.ev_ext[si].record(st)
+        if self.pending is not None:  # step k-1's match, after step k's pyramid pass
+            self._match(*self.pending[:1], self.ev_pyr, self.pending[1])
+        self.pending = (si, ev)
         self.step_no += 1
+
+    def flush(self):
+        """issue the match of the last extracted step"""
+        if self.pending is not None:
+            si, ev = self.pending
+            self._match(si, self.ev_ext[si], ev)
+            self.pending = None
 
     def run(self, warmup, steps):
         for _ in range(warmup):
             self.step()
+        self.flush()
         self.gather.finish()
         torch.cuda.synchronize(self.dev)
         self.ex.sync(self.stream)
@@ -183,6 +223,7 @@ class StreamBench:
         t0 = time.perf_counter()
         for i in range(steps):
             self.step(evs[i])
+        self.flush()
         self.gather.finish()
         torch.cuda.synchronize(self.dev)
         elapsed = time.perf_counter() - t0

@@ -107,6 +107,15 @@ int orbgpu_extractor_sync(orbgpu_extractor* ex, void* stream);
 int orbgpu_extractor_profile(orbgpu_extractor* ex, int enable);
 int orbgpu_extractor_stage_times(orbgpu_extractor* ex, float* ms4, int* nbatches, int reset);
 
+/* Pipelining hook (no reference equivalent): after every later batch
+ * extraction the extractor records `event` (a hipEvent_t, or NULL to clear)
+ * on its stream right after the launch group `stage` (0 pyramid, 1 FAST
+ * cells, 2 octree, 3 describe), so a caller can start dependent or
+ * independent work on another stream at that point, e.g. the previous
+ * batch's matching once the pyramid pass (which wants the whole chip) is
+ * done. */
+int orbgpu_extractor_set_stage_event(orbgpu_extractor* ex, int stage, void* event);
+
 /* mvImagePyramid[level] of frame `frame` of the last extraction, copied to
  * host (ORBextractor.h:85; read by Frame::ComputeStereoMatches). */
 int orbgpu_extractor_copy_level(orbgpu_extractor* ex, int frame, int level, uint8_t* dst,

@@ -158,6 +158,7 @@ struct orbgpu_extractor {
     hipStream_t stream = nullptr;
     // stage timing
     bool profile = false;
+    hipEvent_t stage_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // orbgpu_extractor_set_stage_event
     std::vector<std::array<hipEvent_t, 5>> ev;
     size_t ev_used = 0;
     // last extraction (for copy_level)
@@ -386,16 +387,20 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
     }
     ORB_HIP(launch_pyramid(g, batch, e->d_pyr_ent, e->d_pyr_tab, imgs, row_step, frame_step, e->d_pyr, s));
     if (evs) ORB_HIP(hipEventRecord(evs[1], s));
+    if (e->stage_ev[0]) ORB_HIP(hipEventRecord(e->stage_ev[0], s));
     ORB_HIP(launch_fast_cells(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_cand, e->d_cell_counts, e->d_err, s));
     if (evs) ORB_HIP(hipEventRecord(evs[2], s));
+    if (e->stage_ev[1]) ORB_HIP(hipEventRecord(e->stage_ev[1], s));
     ORB_HIP(launch_octree(g, batch, e->d_cand, e->d_cell_counts, e->d_gkeys, e->d_gknode, e->d_oct_out,
                           e->d_oct_count, e->d_err, e->kcap, e->ncap, e->d_trace, s));
     if (evs) ORB_HIP(hipEventRecord(evs[3], s));
+    if (e->stage_ev[2]) ORB_HIP(hipEventRecord(e->stage_ev[2], s));
     // GaussianBlur is fused into describe (blur of each keypoint's patch);
     // whole blurred levels exist only for the debug API
     ORB_HIP(launch_describe(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_oct_out, e->d_oct_count, kps, desc,
                             counts, kp_cap, s));
     if (evs) ORB_HIP(hipEventRecord(evs[4], s));
+    if (e->stage_ev[3]) ORB_HIP(hipEventRecord(e->stage_ev[3], s));
     e->last_img = imgs;
     e->last_row = row_step;
     e->last_frame = frame_step;
@@ -593,6 +598,12 @@ int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int hei
 int orbgpu_extractor_profile(orbgpu_extractor* e, int enable) {
     if (!e) return fail(ORBGPU_ERR_ARG, "NULL extractor");
     e->profile = enable != 0;
+    return ORBGPU_OK;
+}
+
+int orbgpu_extractor_set_stage_event(orbgpu_extractor* e, int stage, void* event) {
+    if (!e || stage < 0 || stage > 3) return fail(ORBGPU_ERR_ARG, "invalid argument");
+    e->stage_ev[stage] = (hipEvent_t)event;
     return ORBGPU_OK;
 }
 

@@ -100,6 +100,7 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_extractor_sync.argtypes = [vp, vp]
         L.orbgpu_extractor_profile.argtypes = [vp, i]
         L.orbgpu_extractor_stage_times.argtypes = [vp, vp, ctypes.POINTER(i), i]
+        L.orbgpu_extractor_set_stage_event.argtypes = [vp, i, vp]
         L.orbgpu_extractor_copy_level.argtypes = [vp, i, i, vp, sz]
         L.orbgpu_hamming_pairs_device.argtypes = [vp, vp, i, vp, vp]
         L.orbgpu_search_for_initialization_batch_device.argtypes = [
@@ -275,6 +276,15 @@ class Extractor:
 
     def profile(self, enable: bool = True):
         _check(lib().orbgpu_extractor_profile(self.h, int(enable)), "profile")
+
+    def set_stage_event(self, stage: str, event=None):
+        """record `event` (a torch.cuda.Event, or None to clear) on the extraction
+        stream right after `stage` (one of STAGES) of every later batch"""
+        ptr = None
+        if event is not None:
+            event.record()  # torch creates the HIP event lazily; make sure it exists
+            ptr = event.cuda_event
+        _check(lib().orbgpu_extractor_set_stage_event(self.h, self.STAGES.index(stage), ptr), "set_stage_event")
 
     def stage_times(self, reset: bool = True):
         """(dict stage -> summed ms, number of extractions) since last reset."""

@@ -562,6 +562,61 @@ def triangulation_scenario(voc_desc_leaves: np.ndarray, n_points: int, seed: int
             "T2w": T2[:3, :].astype(np.float32), "fx2": fx, "fy2": fy, "cx2": cx, "cy2": cy,
             "scale_factors2": sf, "level_sigma2_2": sig2}
 
+
+def mapping_scenario(n_points: int, seed: int, stereo: bool = False, outliers: float = 0.15,
+                     baseline: float = 0.4):
+    """Two keyframes for LocalMapping::CreateNewMapPoints: world points seen
+    by both (pixel noise, octaves from the distance), matched pairs (idx1,
+    idx2) with `outliers` of them pointing at a wrong keypoint; stereo
+    keyframes carry mvuRight / mvDepth for about half of the keypoints.
+    Returns (kf1, kf2, pairs, scale_factor) in proj/mapping_ref layouts."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = 517.3, 516.5, 318.6, 255.3, 40.0
+    sf = (np.float32(1.2) ** np.arange(8)).astype(np.float32)
+    T1 = _pose(rng, 0.1, 0.2)
+    T2 = T1.copy()
+    T2[:3, :3] = _rot(rng, 0.05) @ T1[:3, :3]
+    T2[:3, 3] = T1[:3, 3] + rng.uniform(-baseline, baseline, 3)
+    z = rng.uniform(1.5, 12.0, n_points)
+    u = rng.uniform(0, 640, n_points)
+    v = rng.uniform(0, 480, n_points)
+    pc1 = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], 1)
+    Xw = (pc1 - T1[:3, 3]) @ T1[:3, :3]
+    pc2 = Xw @ T2[:3, :3].T + T2[:3, 3]
+
+    def kf(T, pc):
+        kp = np.zeros(n_points, dtype=[("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                                       ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+        kp["x"] = fx * pc[:, 0] / pc[:, 2] + cx + rng.normal(0, 0.6, n_points)
+        kp["y"] = fy * pc[:, 1] / pc[:, 2] + cy + rng.normal(0, 0.6, n_points)
+        kp["octave"] = np.clip(np.log(pc[:, 2] / 1.5) / np.log(1.2) * 0.5 + rng.integers(-1, 2, n_points), 0, 7)
+        kp["size"] = 31 * sf[kp["octave"]]
+        kp["class_id"] = -1
+        d = {"Tcw": T[:3, :].astype(np.float32), "Ow": (-T[:3, :3].T @ T[:3, 3]).astype(np.float32),
+             "fx": fx, "fy": fy, "cx": cx, "cy": cy, "invfx": float(np.float32(1) / np.float32(fx)),
+             "invfy": float(np.float32(1) / np.float32(fy)), "bf": bf, "b": bf / fx, "kps_un": kp, "kps": kp,
+             "u_right": None, "depth": None, "scale_factors": sf, "level_sigma2": (sf * sf).astype(np.float32)}
+        if stereo:
+            has = rng.uniform(size=n_points) < 0.5
+            depth = np.where(has, pc[:, 2] * (1 + rng.normal(0, 0.002, n_points)), -1.0).astype(np.float32)
+            d["depth"] = depth
+            d["u_right"] = np.where(has, kp["x"] - bf / np.where(has, depth, 1.0), -1.0).astype(np.float32)
+        return d
+
+    k1, k2 = kf(T1, pc1), kf(T2, pc2)
+    order2 = rng.permutation(n_points)  # kf2's keypoints in another order
+    for key in ("kps_un", "u_right", "depth"):
+        if k2[key] is not None:
+            k2[key] = k2[key][order2]
+    k2["kps"] = k2["kps_un"]
+    inv2 = np.argsort(order2)
+    idx1 = rng.permutation(n_points)[: int(0.8 * n_points)]
+    idx2 = inv2[idx1]
+    bad = rng.uniform(size=len(idx1)) < outliers
+    idx2 = np.where(bad, rng.integers(0, n_points, len(idx1)), idx2)
+    pairs = np.stack([idx1, idx2], 1).astype(np.int32)
+    return k1, k2, pairs, 1.2
+
 # --------------------------------------------------------------------------
 # Loop-closure burst (SURVEY.md section 8d, config 5)
 # --------------------------------------------------------------------------
