@@ -339,9 +339,9 @@ __global__ __launch_bounds__(kThreads) void octree_kernel(Geom g, const uint32_t
                                                           uint16_t* __restrict__ gknode,
                                                           uint32_t* __restrict__ oct_out,
                                                           int* __restrict__ oct_count, int* __restrict__ err,
-                                                          int kcap, int ncap, int* __restrict__ trace) {
+                                                          int kcap, int ncap, int* __restrict__ trace, int level0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int l = blockIdx.x, f = blockIdx.y;
+    const int l = level0 + (int)blockIdx.x, f = blockIdx.y;
     const int tid = threadIdx.x;
     const LevelGeom& L = g.lv[l];
     const int ncells = L.ncols * L.nrows;
@@ -401,12 +401,18 @@ size_t octree_lds_bytes(const Geom& g, int kcap, int ncap) {
 
 hipError_t launch_octree(const Geom& g, int batch, const uint32_t* cand, const int* cell_counts,
                          uint32_t* gkeys, uint16_t* gknode, uint32_t* oct_out, int* oct_count,
-                         int* err, int kcap, int ncap, int* trace, hipStream_t stream) {
-    const size_t lds = octree_lds_bytes(g, kcap, ncap);
-    dim3 grid(g.nlevels, batch);
-    hipLaunchKernelGGL(octree_kernel, grid, dim3(kThreads), lds, stream, g, cand, cell_counts, gkeys, gknode,
-                       oct_out, oct_count, err, kcap, ncap, trace);
-    return hipGetLastError();
+                         int* err, const OctreeGroup* groups, int ngroups, int* trace, hipStream_t stream) {
+    // one launch per level group: the LDS (and so the workgroups per CU) sized for the group's levels
+    for (int i = 0; i < ngroups; ++i) {
+        const OctreeGroup& G = groups[i];
+        if (G.nlev <= 0) continue;
+        const size_t lds = octree_lds_bytes(g, G.kcap, G.ncap);
+        hipLaunchKernelGGL(octree_kernel, dim3(G.nlev, batch), dim3(kThreads), lds, stream, g, cand, cell_counts,
+                           gkeys, gknode, oct_out, oct_count, err, G.kcap, G.ncap, trace, G.level0);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace orbgpu

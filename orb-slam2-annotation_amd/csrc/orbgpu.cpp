@@ -125,6 +125,7 @@ struct orbgpu_extractor {
     std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
     int W = 0, H = 0, max_batch = 0, max_kps = 0;
     int kcap = 0, ncap = 0;
+    OctreeGroup oct_groups[2] = {};  // the octree launches (big levels / small levels)
     // device buffers
     uint8_t* d_pyr = nullptr;
     size_t pyr_bytes = 0;
@@ -369,6 +370,18 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     const size_t fixed = octree_lds_bytes(g, 0, e->ncap);
     const long budget = 65536 - (long)fixed - 64;
     e->kcap = budget > 0 ? (int)(budget / 6) & ~63 : 0;
+    // Two octree launches: levels 0..1 with the 64 KiB budget (two workgroups per CU), the
+    // smaller levels with node arrays for their own feature counts and keys in LDS up to
+    // 2048 (about 28 KiB: five workgroups per CU); a level with more candidates takes the
+    // same HBM-scratch path as an oversized big level.
+    const int split = std::min(2, L);
+    int ncap_b = 0;
+    for (int l = split; l < L; ++l) ncap_b = std::max(ncap_b, std::max(g.lv[l].ocap, g.lv[l].nini));
+    ncap_b = (int)round_up((size_t)std::max(ncap_b, 1), 16);
+    const long budget_b = std::min<long>(65536, (long)octree_lds_bytes(g, 2048, ncap_b)) -
+                          (long)octree_lds_bytes(g, 0, ncap_b) - 64;
+    e->oct_groups[0] = OctreeGroup{0, split, e->kcap, e->ncap};
+    e->oct_groups[1] = OctreeGroup{split, L - split, budget_b > 0 ? (int)(budget_b / 6) & ~63 : 0, ncap_b};
     return ORBGPU_OK;
 }
 
@@ -392,7 +405,7 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
     if (evs) ORB_HIP(hipEventRecord(evs[2], s));
     if (e->stage_ev[1]) ORB_HIP(hipEventRecord(e->stage_ev[1], s));
     ORB_HIP(launch_octree(g, batch, e->d_cand, e->d_cell_counts, e->d_gkeys, e->d_gknode, e->d_oct_out,
-                          e->d_oct_count, e->d_err, e->kcap, e->ncap, e->d_trace, s));
+                          e->d_oct_count, e->d_err, e->oct_groups, 2, e->d_trace, s));
     if (evs) ORB_HIP(hipEventRecord(evs[3], s));
     if (e->stage_ev[2]) ORB_HIP(hipEventRecord(e->stage_ev[2], s));
     // GaussianBlur is fused into describe (blur of each keypoint's patch);

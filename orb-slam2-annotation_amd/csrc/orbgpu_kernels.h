@@ -35,9 +35,14 @@ hipError_t launch_blur_levels(const Geom& g, int batch, const uint8_t* img0, siz
                               const uint8_t* pyr, uint8_t* blur, hipStream_t stream);
 
 size_t octree_lds_bytes(const Geom& g, int kcap, int ncap);
+// levels [level0, level0 + nlev) in one launch: node arrays for ncap nodes,
+// keys in LDS up to kcap (more: the HBM scratch path)
+struct OctreeGroup {
+    int level0, nlev, kcap, ncap;
+};
 hipError_t launch_octree(const Geom& g, int batch, const uint32_t* cand, const int* cell_counts,
                          uint32_t* gkeys, uint16_t* gknode, uint32_t* oct_out, int* oct_count,
-                         int* err, int kcap, int ncap, int* trace, hipStream_t stream);
+                         int* err, const OctreeGroup* groups, int ngroups, int* trace, hipStream_t stream);
 
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                            const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
