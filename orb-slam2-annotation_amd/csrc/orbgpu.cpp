@@ -370,7 +370,7 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     const size_t fixed = octree_lds_bytes(g, 0, e->ncap);
     const long budget = 65536 - (long)fixed - 64;
     e->kcap = budget > 0 ? (int)(budget / 6) & ~63 : 0;
-    // Two octree launches: levels 0..1 with the 64 KiB budget (two workgroups per CU), the
+    // Two octree launches: levels 0..1 (below), the
     // smaller levels with node arrays for their own feature counts and keys in LDS up to
     // 2048 (about 28 KiB: five workgroups per CU); a level with more candidates takes the
     // same HBM-scratch path as an oversized big level.
@@ -380,7 +380,10 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     ncap_b = (int)round_up((size_t)std::max(ncap_b, 1), 16);
     const long budget_b = std::min<long>(65536, (long)octree_lds_bytes(g, 2048, ncap_b)) -
                           (long)octree_lds_bytes(g, 0, ncap_b) - 64;
-    e->oct_groups[0] = OctreeGroup{0, split, e->kcap, e->ncap};
+    // levels 0..1: keys in LDS up to 4096 (about 40 KiB, four workgroups per CU)
+    const long budget_a = std::min<long>(65536, (long)octree_lds_bytes(g, 4096, e->ncap)) -
+                          (long)octree_lds_bytes(g, 0, e->ncap) - 64;
+    e->oct_groups[0] = OctreeGroup{0, split, budget_a > 0 ? (int)(budget_a / 6) & ~63 : 0, e->ncap};
     e->oct_groups[1] = OctreeGroup{split, L - split, budget_b > 0 ? (int)(budget_b / 6) & ~63 : 0, ncap_b};
     return ORBGPU_OK;
 }
