@@ -12,6 +12,10 @@
  *   ORBmatcher::SearchByBoW(KF, F)         src/ORBmatcher.cpp:205-348
  *   ORBmatcher::SearchByBoW(KF1, KF2)      src/ORBmatcher.cpp:604-743
  *   ORBmatcher::SearchForTriangulation     src/ORBmatcher.cpp:755-951 (+ CheckDistEpipolarLine :166-190)
+ *   TemplatedVocabulary::score / the scoring loops of KeyFrameDatabase::
+ *   DetectLoopCandidates / DetectRelocalizationCandidates
+ *                                          TemplatedVocabulary.h:1222-1227, ScoringObject.cpp:23-313,
+ *                                          src/KeyFrameDatabase.cpp:96-330
  *
  * Layouts.  A FeatureVector is returned as CSR: node ids ascending
  * (fv_nodes[0..fv_n)), fv_offsets[0..fv_n] into fv_features (feature
@@ -102,6 +106,27 @@ int orbgpu_search_by_bow_batch_device(int mode, int batch, const orbgpu_bow_fram
 /* Host form for one pair (host arrays; match sized as above). */
 int orbgpu_search_by_bow(int mode, const orbgpu_bow_frame* a, const orbgpu_bow_frame* b, float nnratio,
                          int check_ori, int* match, int* nmatches);
+
+/* ---------------------------------------------------------------------- */
+/* Keyframe database scoring                                               */
+/* ---------------------------------------------------------------------- */
+/* One query BowVector (q_words ascending, q_values) against nkf keyframes'
+ * BowVectors (CSR: keyframe k's words db_words[db_offsets[k] ..
+ * db_offsets[k+1]) ascending, values in db_values).  Per keyframe: the
+ * number of words it shares with the query (KeyFrameDatabase's
+ * mnLoopWords / mnRelocWords over the inverted file, KeyFrameDatabase.cpp:
+ * 107-125, 250-262) and TemplatedVocabulary::score(query, kf) for the
+ * vocabulary's scoring type (0 L1 .. 5 DOT_PRODUCT; ScoringObject.cpp
+ * 23-313), summed in the reference's word order (bit-exact; KL uses the
+ * device log).  The candidate selection (0.8 * max common words, minScore,
+ * covisibility groups) stays with the caller. */
+int orbgpu_bow_score_batch_device(int scoring, const int* d_q_words, const double* d_q_values, int nq, int nkf,
+                                  const int* d_db_offsets, const int* d_db_words, const double* d_db_values,
+                                  int* d_common, double* d_scores, void* stream);
+/* Host form (host arrays). */
+int orbgpu_bow_score(int scoring, const int* q_words, const double* q_values, int nq, int nkf,
+                     const int* db_offsets, const int* db_words, const double* db_values, int* common,
+                     double* scores);
 
 /* ---------------------------------------------------------------------- */
 /* SearchForTriangulation (LocalMapping::CreateNewMapPoints,               */

@@ -288,3 +288,52 @@ def search_for_triangulation(fv1, fv2, P, check_ori=True, only_stereo=False):
                 match[idx] = -1
                 nm -= 1
     return nm, np.array(match, np.int32)
+
+
+LOG_EPS = math.log(2.220446049250313080847e-16)  # GeneralScoring::LOG_EPS = log(DBL_EPSILON)
+
+
+def bow_score(scoring, v1: dict, v2: dict):
+    """TemplatedVocabulary::score(v1, v2) (ScoringObject.cpp:23-313): the merge
+    walk in ascending word order, double sum in that order.  v: dict word ->
+    value.  Returns (score, common words)."""
+    a, b = sorted(v1.items()), sorted(v2.items())
+    i = j = 0
+    s, nc = 0.0, 0
+    while i < len(a) and j < len(b):
+        (wa, vi), (wb, wi) = a[i], b[j]
+        if wa == wb:
+            nc += 1
+            if scoring == 0:
+                s += abs(vi - wi) - abs(vi) - abs(wi)
+            elif scoring in (1, 5):
+                s += vi * wi
+            elif scoring == 2:
+                if vi + wi != 0.0:
+                    s += vi * wi / (vi + wi)
+            elif scoring == 3:
+                if vi != 0 and wi != 0:
+                    s += vi * math.log(vi / wi)
+            else:
+                s += math.sqrt(vi * wi)
+            i += 1
+            j += 1
+        elif wa < wb:
+            if scoring == 3:
+                s += vi * (math.log(vi) - LOG_EPS)
+            i += 1
+        else:
+            j += 1
+    if scoring == 3:
+        for _, vi in a[i:]:
+            if vi != 0:
+                s += vi * (math.log(vi) - LOG_EPS)
+    if scoring == 0:
+        s = -s / 2.0
+    elif scoring == 1:
+        s = 1.0 if s >= 1 else 1.0 - math.sqrt(1.0 - s)
+    elif scoring == 2:
+        s = 2.0 * s
+    if scoring == 3:  # common words of the whole vectors
+        nc = len(set(v1) & set(v2))
+    return s, nc

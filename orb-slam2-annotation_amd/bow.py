@@ -156,6 +156,32 @@ def search_for_triangulation(fv1, fv2, P, check_ori=True, only_stereo=False):
                                                     ctypes.byref(nm)), "orbgpu_search_for_triangulation")
     return nm.value, match[:n1]
 
+
+def bow_score(scoring, query: dict, db: list):
+    """TemplatedVocabulary::score(query, kf) and the common-word count for every
+    keyframe BowVector in `db` (dicts word -> value) on the GPU:
+    (common (nkf,) int32, scores (nkf,) float64)."""
+    qw = np.array(sorted(query), np.int32)
+    qv = np.array([query[int(w)] for w in qw], np.float64)
+    off = np.zeros(len(db) + 1, np.int32)
+    words, vals = [], []
+    for k, v in enumerate(db):
+        ws = sorted(v)
+        words += ws
+        vals += [v[w] for w in ws]
+        off[k + 1] = len(words)
+    dw, dv = np.array(words, np.int32), np.array(vals, np.float64)
+    common = np.zeros(max(len(db), 1), np.int32)
+    scores = np.zeros(max(len(db), 1), np.float64)
+    L = orbgpu.lib()
+    vp = ctypes.c_void_p
+    L.orbgpu_bow_score.argtypes = [ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, vp]
+    orbgpu._check(L.orbgpu_bow_score(int(scoring), qw.ctypes.data, qv.ctypes.data, len(qw), len(db),
+                                     off.ctypes.data, dw.ctypes.data if len(dw) else None,
+                                     dv.ctypes.data if len(dv) else None, common.ctypes.data, scores.ctypes.data),
+                  "orbgpu_bow_score")
+    return common[:len(db)], scores[:len(db)]
+
 # --------------------------------------------------------------------------
 # Batched, HBM-resident forms (torch tensors on the GPU)
 # --------------------------------------------------------------------------

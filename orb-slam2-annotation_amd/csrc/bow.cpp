@@ -390,4 +390,64 @@ int orbgpu_search_for_triangulation(const orbgpu_triangulation_pair* pair, int c
     return ORBGPU_OK;
 }
 
+int orbgpu_bow_score_batch_device(int scoring, const int* d_q_words, const double* d_q_values, int nq, int nkf,
+                                  const int* d_db_offsets, const int* d_db_words, const double* d_db_values,
+                                  int* d_common, double* d_scores, void* stream) {
+    if (scoring < 0 || scoring > 5 || nq < 0 || nkf < 0 ||
+        (nkf > 0 && (!d_db_offsets || !d_common || !d_scores)) || (nq > 0 && (!d_q_words || !d_q_values)))
+        return fail(ORBGPU_ERR_ARG, "invalid argument");
+    int rc = check_device();
+    if (rc) return rc;
+    ORB_HIP(launch_bow_db_score(scoring, d_q_words, d_q_values, nq, nkf, d_db_offsets, d_db_words, d_db_values,
+                                d_common, d_scores, (hipStream_t)stream));
+    return ORBGPU_OK;
+}
+
+int orbgpu_bow_score(int scoring, const int* q_words, const double* q_values, int nq, int nkf,
+                     const int* db_offsets, const int* db_words, const double* db_values, int* common,
+                     double* scores) {
+    if (scoring < 0 || scoring > 5 || nq < 0 || nkf < 0 || (nkf > 0 && (!db_offsets || !common || !scores)) ||
+        (nq > 0 && (!q_words || !q_values)))
+        return fail(ORBGPU_ERR_ARG, "invalid argument");
+    if (nkf == 0) return ORBGPU_OK;
+    const size_t ndb = (size_t)db_offsets[nkf];
+    if (ndb > 0 && (!db_words || !db_values)) return fail(ORBGPU_ERR_ARG, "missing keyframe words");
+    int rc = check_device();
+    if (rc) return rc;
+    std::vector<void*> allocs;
+    bool ok = true;
+    auto up = [&](const void* src, size_t bytes) -> void* {
+        void* d = nullptr;
+        if (hipMalloc(&d, std::max<size_t>(bytes, 8)) != hipSuccess) {
+            ok = false;
+            return nullptr;
+        }
+        allocs.push_back(d);
+        if (src && bytes && hipMemcpy(d, src, bytes, hipMemcpyHostToDevice) != hipSuccess) ok = false;
+        return d;
+    };
+    const int* dqw = (const int*)up(q_words, 4 * (size_t)nq);
+    const double* dqv = (const double*)up(q_values, 8 * (size_t)nq);
+    const int* doff = (const int*)up(db_offsets, 4 * (size_t)(nkf + 1));
+    const int* dw = (const int*)up(db_words, 4 * ndb);
+    const double* dv = (const double*)up(db_values, 8 * ndb);
+    int* dc = (int*)up(nullptr, 4 * (size_t)nkf);
+    double* ds = (double*)up(nullptr, 8 * (size_t)nkf);
+    auto cleanup = [&]() {
+        for (void* p : allocs) (void)hipFree(p);
+    };
+    if (!ok) {
+        cleanup();
+        return fail(ORBGPU_ERR_HIP, "upload failed");
+    }
+    rc = orbgpu_bow_score_batch_device(scoring, dqw, dqv, nq, nkf, doff, dw, dv, dc, ds, nullptr);
+    ok = !rc && hipDeviceSynchronize() == hipSuccess &&
+         hipMemcpy(common, dc, 4 * (size_t)nkf, hipMemcpyDeviceToHost) == hipSuccess &&
+         hipMemcpy(scores, ds, 8 * (size_t)nkf, hipMemcpyDeviceToHost) == hipSuccess;
+    cleanup();
+    if (rc) return rc;
+    if (!ok) return fail(ORBGPU_ERR_HIP, "bow score failed");
+    return ORBGPU_OK;
+}
+
 }  // extern "C"

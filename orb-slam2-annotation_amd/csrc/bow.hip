@@ -459,6 +459,66 @@ __global__ __launch_bounds__(256) void triangulation_kernel(const orbgpu_triangu
     if (threadIdx.x == 0) nmatches[blockIdx.x] = s_cnt;
 }
 
+// DBoW2 GeneralScoring::score (ScoringObject.cpp:23-313) of the query
+// BowVector against keyframe k's, one thread per keyframe: the reference's
+// merge walk in ascending word order (lower_bound skips == stepping), the
+// double sum in that order; plus the number of common words (the mnLoopWords /
+// mnRelocWords counts of KeyFrameDatabase.cpp:107-125, 250-262).
+__global__ __launch_bounds__(256) void bow_db_score_kernel(int scoring, const int* __restrict__ qw,
+                                                           const double* __restrict__ qv, int nq, int nkf,
+                                                           const int* __restrict__ off, const int* __restrict__ dw,
+                                                           const double* __restrict__ dv, int* __restrict__ common,
+                                                           double* __restrict__ score) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= nkf) return;
+    const double LOG_EPS = log(2.220446049250313080847e-16);  // log(DBL_EPSILON)
+    int i = 0, j = off[k];
+    const int je = off[k + 1];
+    double s = 0.0;
+    int nc = 0;
+    while (i < nq && j < je) {
+        const int a = qw[i], b = dw[j];
+        const double vi = qv[i], wi = dv[j];
+        if (a == b) {
+            ++nc;
+            switch (scoring) {
+                case 0: s += fabs(vi - wi) - fabs(vi) - fabs(wi); break;     // L1
+                case 1: case 5: s += vi * wi; break;                         // L2, dot product
+                case 2: if (vi + wi != 0.0) s += vi * wi / (vi + wi); break; // chi-square
+                case 3: if (vi != 0 && wi != 0) s += vi * log(vi / wi); break;  // KL
+                default: s += sqrt(vi * wi); break;                          // Bhattacharyya
+            }
+            ++i;
+            ++j;
+        } else if (a < b) {
+            if (scoring == 3) s += vi * (log(vi) - LOG_EPS);  // KL walks every query word
+            ++i;
+        } else {
+            ++j;
+        }
+    }
+    if (scoring == 3)
+        for (; i < nq; ++i)
+            if (qv[i] != 0) s += qv[i] * (log(qv[i]) - LOG_EPS);
+    if (scoring == 0) s = -s / 2.0;
+    else if (scoring == 1) s = s >= 1 ? 1.0 : 1.0 - sqrt(1.0 - s);
+    else if (scoring == 2) s = 2. * s;
+    // common words count every query word once (the inverted-file loop visits each
+    // (word, keyframe) entry once)
+    if (scoring == 3) {  // the KL walk advanced i past non-common words too: count separately
+        nc = 0;
+        int ii = 0, jj = off[k];
+        while (ii < nq && jj < je) {
+            const int a = qw[ii], b = dw[jj];
+            if (a == b) { ++nc; ++ii; ++jj; }
+            else if (a < b) ++ii;
+            else ++jj;
+        }
+    }
+    common[k] = nc;
+    score[k] = s;
+}
+
 }  // namespace
 
 int bow_max_stride() { return kMaxStride; }
@@ -482,6 +542,14 @@ hipError_t launch_search_by_bow(int mode, int batch, const orbgpu_bow_frame* a, 
     if (batch <= 0) return hipSuccess;
     hipLaunchKernelGGL(search_by_bow_kernel, dim3(batch), dim3(256), 0, stream, mode, a, b, nnratio, check_ori,
                        stride, match, nmatches);
+    return hipGetLastError();
+}
+
+hipError_t launch_bow_db_score(int scoring, const int* qw, const double* qv, int nq, int nkf, const int* off,
+                               const int* dw, const double* dv, int* common, double* score, hipStream_t stream) {
+    if (nkf <= 0) return hipSuccess;
+    hipLaunchKernelGGL(bow_db_score_kernel, dim3((nkf + 255) / 256), dim3(256), 0, stream, scoring, qw, qv, nq, nkf,
+                       off, dw, dv, common, score);
     return hipGetLastError();
 }
 

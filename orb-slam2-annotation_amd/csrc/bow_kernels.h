@@ -27,6 +27,8 @@ hipError_t launch_search_by_bow(int mode, int batch, const orbgpu_bow_frame* a, 
                                 float nnratio, int check_ori, int stride, int* match, int* nmatches,
                                 hipStream_t stream);
 
+hipError_t launch_bow_db_score(int scoring, const int* qw, const double* qv, int nq, int nkf, const int* off,
+                               const int* dw, const double* dv, int* common, double* score, hipStream_t stream);
 hipError_t launch_search_for_triangulation(int batch, const orbgpu_triangulation_pair* pairs, int check_ori, int stride,
                                           int* match, int* nmatches, hipStream_t stream);
 

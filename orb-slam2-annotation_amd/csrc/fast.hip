@@ -202,29 +202,20 @@ __device__ int nms_emit(const CellTiles& T, int nb, int ox, int t, int lane, int
 }
 
 constexpr int kCellWaves = 4;  // cells (one per wave) in flight per block
-
-// window pitch of a level's cells: wCell + 6 columns plus up to 3 of alignment, rounded to
-// an instantiated pitch (40, 48, ..., 72)
-inline int fast_pitch(const LevelGeom& L) {
-    const int p = (L.wcell + 9 + 3) & ~3;
-    return p <= 40 ? 40 : (p + 7) & ~7;
-}
 constexpr int kStageLoads = 8;  // window dwords per lane in flight
 
 template <int P>
-// One launch covers the cells [c0, c0 + ncg) of every frame (a group of
-// levels that share the window pitch P, rows R and list size det_max).
-__global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int ncells_total, int c0, int ncg, int R,
-                                                                     int det_max,
+__global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int ncells_total,
                                                                      const uint8_t* __restrict__ img0, size_t row0,
                                                                      size_t frame0, const uint8_t* __restrict__ pyr,
                                                                      uint32_t* __restrict__ cand,
                                                                      int* __restrict__ cell_counts,
                                                                      int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int R = g.win_rows;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: metadata in SGPRs
-    const size_t per_wave = ((size_t)2 * P * R + 2 * (size_t)det_max + 15) & ~(size_t)15;
+    const size_t per_wave = ((size_t)2 * P * R + 2 * (size_t)g.det_max + 15) & ~(size_t)15;
     uint8_t* ws = smem + wave * per_wave;
     CellTiles T;
     T.win = ws;
@@ -241,8 +232,8 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     const int item = (int)blockIdx.x * kCellWaves + wave;
 #endif
     if (item >= ncells_total) return;
-    const int f = item / ncg;
-    const int gc = c0 + (item - f * ncg);
+    const int f = item / g.total_cells;
+    const int gc = item - f * g.total_cells;
     int l = 0;
     while (l + 1 < g.nlevels && gc >= g.lv[l + 1].cell_base) ++l;
     const LevelGeom& L = g.lv[l];
@@ -310,44 +301,26 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
 hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                              const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err,
                              hipStream_t stream) {
-    // levels in groups of equal window pitch (the ring offsets are compile-time): a narrower
-    // window for the levels that allow it means less LDS per wave and more waves per CU
-    int l = 0;
-    while (l < g.nlevels) {
-        const int P = fast_pitch(g.lv[l]);
-        int l1 = l + 1;
-        while (l1 < g.nlevels && fast_pitch(g.lv[l1]) == P) ++l1;
-        int R = 0, det = 0;
-        for (int k = l; k < l1; ++k) {
-            R = std::max(R, g.lv[k].hcell + 6);
-            det = std::max(det, (g.lv[k].wcell * g.lv[k].hcell + 7) & ~7);
-        }
-        const int c0 = g.lv[l].cell_base;
-        const int ncg = (l1 < g.nlevels ? g.lv[l1].cell_base : g.total_cells) - c0;
-        const int items = ncg * batch;
-        const size_t per_wave = ((size_t)2 * P * R + 2 * (size_t)det + 15) & ~(size_t)15;
-        dim3 grid((items + kCellWaves - 1) / kCellWaves);
-        const size_t lds = per_wave * kCellWaves;
+    const int items = g.total_cells * batch;
+    const size_t per_wave = ((size_t)2 * g.win_pitch * g.win_rows + 2 * (size_t)g.det_max + 15) & ~(size_t)15;
+    dim3 grid((items + kCellWaves - 1) / kCellWaves);
+    const size_t lds = per_wave * kCellWaves;
 #define ORBGPU_FAST_CASE(PP)                                                                                        \
     case PP:                                                                                                        \
-        hipLaunchKernelGGL(fast_cells_kernel<PP>, grid, dim3(64 * kCellWaves), lds, stream, g, items, c0, ncg, R, \
-                           det, img0, row0, frame0, pyr, cand, cell_counts, err);                                  \
+        hipLaunchKernelGGL(fast_cells_kernel<PP>, grid, dim3(64 * kCellWaves), lds, stream, g, items, img0, row0, \
+                           frame0, pyr, cand, cell_counts, err);                                                   \
         break;
-        switch (P) {
-            ORBGPU_FAST_CASE(40)
-            ORBGPU_FAST_CASE(48)
-            ORBGPU_FAST_CASE(56)
-            ORBGPU_FAST_CASE(64)
-            ORBGPU_FAST_CASE(72)
-            default:
-                return hipErrorInvalidValue;
-        }
-#undef ORBGPU_FAST_CASE
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        l = l1;
+    switch (g.win_pitch) {
+        ORBGPU_FAST_CASE(40)
+        ORBGPU_FAST_CASE(48)
+        ORBGPU_FAST_CASE(56)
+        ORBGPU_FAST_CASE(64)
+        ORBGPU_FAST_CASE(72)
+        default:
+            return hipErrorInvalidValue;
     }
-    return hipSuccess;
+#undef ORBGPU_FAST_CASE
+    return hipGetLastError();
 }
 
 }  // namespace orbgpu

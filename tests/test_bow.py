@@ -121,3 +121,46 @@ def test_gpu_search_by_bow_bit_exact(mode, nnratio, check_ori, invalid):
         assert nm_g == nm_r
         np.testing.assert_array_equal(m_g, m_r)
         assert nm_r > 20
+
+
+# ---- keyframe database scoring (KeyFrameDatabase::Detect*Candidates) ------
+def _bow_db(scoring, weighting, n_kf, seed):
+    par, leaf, desc, w = synth.synthetic_vocabulary(6, 4, 60 + seed)
+    voc = bow_ref.Vocabulary.from_arrays(6, 4, scoring, weighting, par, leaf, desc, w)
+    rng = np.random.default_rng(seed)
+    leaves = desc[leaf == 1]
+    base = leaves[rng.integers(0, len(leaves), 400)]
+    db = []
+    for k in range(n_kf):  # keyframes re-observe a drifting subset of a common scene
+        pick = rng.choice(400, 250, replace=False) if k % 3 else rng.choice(400, 150, replace=False)
+        d = base[pick] ^ (rng.uniform(size=(len(pick), 32)) < 0.02).astype(np.uint8) * np.uint8(1)
+        db.append(voc.transform(d, 2)[4])
+    q = voc.transform(base[rng.choice(400, 300, replace=False)], 2)[4]
+    return q, db
+
+
+@pytest.mark.parametrize("scoring", [0, 1, 2, 3, 4, 5])
+def test_oracle_bow_score_properties(scoring):
+    q, db = _bow_db(scoring, 0, 3, 1)
+    s_self, nc_self = bow_ref.bow_score(scoring, q, q)
+    assert nc_self == len(q)
+    if scoring in (0, 1, 4):  # normalised scores: identical vectors score 1
+        assert abs(s_self - 1.0) < 1e-7  # L2: 1 - sqrt(1 - s) amplifies the rounding of s
+    s, nc = bow_ref.bow_score(scoring, q, db[0])
+    assert 0 < nc < len(q)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scoring,weighting", [(0, 0), (1, 0), (2, 1), (3, 0), (4, 2), (5, 3)])
+def test_gpu_bow_score_vs_oracle(scoring, weighting):
+    """scores bit-exact (KL: the device log, to 1e-12 relative), common-word counts exact"""
+    import bow
+    q, db = _bow_db(scoring, weighting, 300, 2)
+    db += [{}, dict(q)]  # an empty keyframe and the query itself
+    common, scores = bow.bow_score(scoring, q, db)
+    ref = [bow_ref.bow_score(scoring, q, v) for v in db]
+    np.testing.assert_array_equal(common, [r[1] for r in ref])
+    if scoring == 3:
+        np.testing.assert_allclose(scores, [r[0] for r in ref], rtol=1e-12, atol=1e-12)
+    else:
+        np.testing.assert_array_equal(scores.view(np.uint64), np.array([r[0] for r in ref]).view(np.uint64))
