@@ -119,6 +119,18 @@ int orbgpu_init_reconstruct(int model, const float* kp1, int n1, const float* kp
                             float sigma, float min_parallax, int min_triangulated, orbgpu_init_reconstruction* out,
                             float* p3d, unsigned char* triangulated);
 
+/* Initializer::Initialize (src/Initializer.cpp:55-157) in one host call:
+ * mvMatches12 from matches12 (n1 ints, -1 = unmatched), SeedRandOnce(0) and
+ * the `iterations` minimal sets from the orbgpu_rand stream, every H / F
+ * hypothesis and its score on the GPU, the kept iterations, RH = SH/(SH+SF)
+ * and ReconstructH (RH > 0.40) or ReconstructF with minParallax 1.0 and
+ * minTriangulated 50.  kp1 = the reference frame's mvKeysUn (n1 x (x, y)),
+ * kp2 = the current frame's.  `out` as orbgpu_init_reconstruct; *rh = RH,
+ * *model = the model reconstructed.  p3d / triangulated: n1 entries. */
+int orbgpu_init_initialize(const float* kp1, int n1, const float* kp2, int n2, const int* matches12, const float* K,
+                           float sigma, int iterations, orbgpu_init_reconstruction* out, float* rh, int* model,
+                           float* p3d, unsigned char* triangulated);
+
 #ifdef __cplusplus
 }
 #endif

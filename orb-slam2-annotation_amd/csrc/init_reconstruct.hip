@@ -465,3 +465,85 @@ extern "C" int orbgpu_init_reconstruct(int model, const float* kp1, int n1, cons
     }
     return ORBGPU_OK;
 }
+
+extern "C" int orbgpu_init_initialize(const float* kp1, int n1, const float* kp2, int n2, const int* matches12,
+                                      const float* K, float sigma, int iterations, orbgpu_init_reconstruction* out,
+                                      float* rh, int* model, float* p3d, unsigned char* triangulated) {
+    if (!kp1 || !kp2 || !matches12 || !K || !out || !rh || !model || n1 < 0 || n2 < 0 || iterations <= 0)
+        return fail(ORBGPU_ERR_ARG, "invalid argument");
+    std::vector<int> pairs;  // mvMatches12 (:59-72)
+    for (int i = 0; i < n1; ++i)
+        if (matches12[i] >= 0) {
+            if (matches12[i] >= n2) return fail(ORBGPU_ERR_ARG, "match index out of range");
+            pairs.push_back(i);
+            pairs.push_back(matches12[i]);
+        }
+    const int N = (int)pairs.size() / 2;
+    if (N < 8) return fail(ORBGPU_ERR_ARG, "fewer than 8 matches (the reference's draws need 8)");
+    orbgpu_seed_rand_once(0);  // :102
+    std::vector<int> sets(8 * (size_t)iterations);
+    int rc = orbgpu_init_draw_sets(N, iterations, sets.data());
+    if (rc) return rc;
+    rc = check_device();
+    if (rc) return rc;
+    const size_t work_b = orbgpu_init_workspace_bytes(n1, n2);
+    void *d_kp1 = nullptr, *d_kp2 = nullptr, *d_pairs = nullptr, *d_sets = nullptr, *d_work = nullptr,
+         *d_pts = nullptr, *d_h21 = nullptr, *d_h12 = nullptr, *d_f21 = nullptr, *d_sh = nullptr, *d_sf = nullptr,
+         *d_ih = nullptr, *d_if = nullptr;
+    void** all[] = {&d_kp1, &d_kp2, &d_pairs, &d_sets, &d_work, &d_pts, &d_h21, &d_h12, &d_f21, &d_sh, &d_sf,
+                    &d_ih, &d_if};
+    const size_t sizes[] = {8 * (size_t)std::max(n1, 1), 8 * (size_t)std::max(n2, 1), 8 * (size_t)N,
+                            4 * sets.size(), std::max<size_t>(work_b, 16), 16 * (size_t)N,
+                            36 * (size_t)iterations, 36 * (size_t)iterations, 36 * (size_t)iterations,
+                            4 * (size_t)iterations, 4 * (size_t)iterations, (size_t)iterations * N,
+                            (size_t)iterations * N};
+    auto cleanup = [&]() {
+        for (void** p : all)
+            if (*p) (void)hipFree(*p);
+    };
+    bool ok = true;
+    for (size_t i = 0; i < sizeof(all) / sizeof(all[0]); ++i) ok = ok && hipMalloc(all[i], sizes[i]) == hipSuccess;
+    ok = ok && hipMemcpy(d_kp1, kp1, 8 * (size_t)n1, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(d_kp2, kp2, 8 * (size_t)n2, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(d_pairs, pairs.data(), 8 * (size_t)N, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(d_sets, sets.data(), 4 * sets.size(), hipMemcpyHostToDevice) == hipSuccess;
+    if (!ok) {
+        cleanup();
+        return fail(ORBGPU_ERR_HIP, "allocation / upload failed");
+    }
+    // FindHomography / FindFundamental (:160-269): every iteration's hypotheses and scores
+    rc = orbgpu_init_hypotheses_batch_device((const float*)d_kp1, n1, (const float*)d_kp2, n2, (const int*)d_pairs, N,
+                                             (const int*)d_sets, iterations, d_work, (orbgpu_match_pts*)d_pts,
+                                             (float*)d_h21, (float*)d_h12, (float*)d_f21, nullptr);
+    if (!rc)
+        rc = orbgpu_init_check_both_batch_device((const orbgpu_match_pts*)d_pts, N, (const float*)d_h21,
+                                                 (const float*)d_h12, iterations, (const float*)d_f21, iterations,
+                                                 sigma, (float*)d_sh, (uint8_t*)d_ih, (float*)d_sf, (uint8_t*)d_if,
+                                                 nullptr);
+    std::vector<float> sh(iterations), sf(iterations);
+    if (!rc && (hipDeviceSynchronize() != hipSuccess ||
+                hipMemcpy(sh.data(), d_sh, 4 * (size_t)iterations, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(sf.data(), d_sf, 4 * (size_t)iterations, hipMemcpyDeviceToHost) != hipSuccess))
+        rc = fail(ORBGPU_ERR_HIP, "model scoring failed");
+    int bh = -1, bf = -1;
+    if (!rc) rc = orbgpu_init_select_best(sh.data(), iterations, &bh);
+    if (!rc) rc = orbgpu_init_select_best(sf.data(), iterations, &bf);
+    const float SH = bh >= 0 ? sh[bh] : 0.f, SF = bf >= 0 ? sf[bf] : 0.f;
+    const float RH = SH / (SH + SF);  // :140 (NaN when both are 0: ReconstructF, as the reference)
+    const bool useH = RH > 0.40;
+    float M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    std::vector<unsigned char> inl(N, 0);
+    const int best = useH ? bh : bf;
+    if (!rc && best >= 0 &&
+        (hipMemcpy(M, (float*)(useH ? d_h21 : d_f21) + 9 * (size_t)best, 36, hipMemcpyDeviceToHost) != hipSuccess ||
+         hipMemcpy(inl.data(), (uint8_t*)(useH ? d_ih : d_if) + (size_t)best * N, N, hipMemcpyDeviceToHost) !=
+             hipSuccess))
+        rc = fail(ORBGPU_ERR_HIP, "model read-back failed");
+    cleanup();
+    if (rc) return rc;
+    *rh = RH;
+    *model = useH ? ORBGPU_INIT_MODEL_H : ORBGPU_INIT_MODEL_F;
+    // (no kept iteration: the reference reconstructs from an empty H/F with no inliers -> false)
+    return orbgpu_init_reconstruct(*model, kp1, n1, kp2, n2, pairs.data(), N, inl.data(), M, K, sigma, 1.0f, 50, out,
+                                   p3d, triangulated);
+}

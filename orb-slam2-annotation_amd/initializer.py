@@ -230,3 +230,33 @@ def reconstruct(model, kp1, kp2, matches12, inliers, M21, K, sigma=1.0, min_para
             "parallax": np.array(out.parallax[:nh], np.float32),
             "R21": np.array(out.R21, np.float32).reshape(3, 3), "t21": np.array(out.t21, np.float32),
             "p3d": p3d[:len(k1)], "triangulated": tri[:len(k1)].astype(bool)}
+
+
+def initialize(kp1, kp2, matches12, K, sigma=1.0, iterations=200):
+    """Initializer(ReferenceFrame, sigma, iterations).Initialize(CurrentFrame,
+    vMatches12, ...) (Initializer.cpp:55-157) in one call: draws from the
+    orbgpu_rand stream after SeedRandOnce(0), hypotheses + scores + the
+    reconstruction on the GPU.  Returns a dict: ok, model (0 H / 1 F), RH,
+    R21, t21, p3d (n1, 3), triangulated (n1), n_good, parallax."""
+    L = _lib()
+    vp = ctypes.c_void_p
+    L.orbgpu_init_initialize.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, vp, vp, ctypes.c_float, ctypes.c_int,
+                                         vp, vp, vp, vp, vp]
+    k1 = np.ascontiguousarray(np.asarray(kp1, np.float32).reshape(-1, 2))
+    k2 = np.ascontiguousarray(np.asarray(kp2, np.float32).reshape(-1, 2))
+    m12 = np.ascontiguousarray(np.asarray(matches12, np.int32))
+    Km = np.ascontiguousarray(np.asarray(K, np.float32).reshape(9))
+    out = Reconstruction()
+    rh = ctypes.c_float()
+    model = ctypes.c_int()
+    p3d = np.zeros((max(len(k1), 1), 3), np.float32)
+    tri = np.zeros(max(len(k1), 1), np.uint8)
+    orbgpu._check(L.orbgpu_init_initialize(k1.ctypes.data, len(k1), k2.ctypes.data, len(k2), m12.ctypes.data,
+                                           Km.ctypes.data, float(sigma), int(iterations), ctypes.byref(out),
+                                           ctypes.byref(rh), ctypes.byref(model), p3d.ctypes.data, tri.ctypes.data),
+                  "orbgpu_init_initialize")
+    nh = out.n_hyp
+    return {"ok": bool(out.ok), "model": model.value, "RH": np.float32(rh.value),
+            "R21": np.array(out.R21, np.float32).reshape(3, 3), "t21": np.array(out.t21, np.float32),
+            "p3d": p3d[:len(k1)], "triangulated": tri[:len(k1)].astype(bool), "n_good": list(out.n_good[:nh]),
+            "parallax": np.array(out.parallax[:nh], np.float32)}

@@ -24,6 +24,9 @@
 //       Fuse(KF, Scw, vpPoints, th, vpReplacePoint) (5, LoopClosing::SearchAndFuse)
 //   adapter_main sim3search <in.bin> <out.bin>
 //       ORBmatcher::SearchBySim3 (LoopClosing.cpp:386)
+//   adapter_main init <in.bin> <out.bin>
+//       Initializer(F1, 1.0, 200).Initialize(F2, vMatches12, ...) as
+//       Tracking::MonocularInitialization drives it (Tracking.cpp:755-820)
 //   adapter_main tri <in.bin> <out.bin>
 //       ORBmatcher::SearchForTriangulation (LocalMapping.cpp:355-360)
 // The .bin layouts are written / read by tests/test_adapter.py (fixed
@@ -41,6 +44,7 @@
 #include <set>
 
 #include "orbslam2_amd/ORBextractor.h"
+#include "orbslam2_amd/Initializer.h"
 #include "orbslam2_amd/ORBmatcher.h"
 #include "orbslam2_amd/PnPsolver.h"
 #include "orbslam2_amd/Sim3Solver.h"
@@ -80,6 +84,7 @@ struct MiniMapPoint {
 // The members of ORB_SLAM2::Frame the adapters read (Frame.h:100-200).
 struct MiniFrame {
     int N = 0;
+    cv::Mat mK;
     std::vector<cv::KeyPoint> mvKeys, mvKeysUn;
     cv::Mat mDescriptors, mTcw;
     std::vector<float> mvuRight;
@@ -672,6 +677,50 @@ int run_tri(const char* inp, const char* outp) {
     return 0;
 }
 
+// Initializer: K (9 floats), n1, kp1 (x, y), n2, kp2 (x, y), vMatches12 (n1 ints).
+// Output: ok, model, RH, R21 (9), t21 (3), then n1 x (x, y, z) and n1 triangulated bytes.
+int run_init(const char* inp, const char* outp) {
+    In in{read_file(inp)};
+    const std::vector<float> K = in.vec<float>(9);
+    MiniFrame F1, F2;
+    for (MiniFrame* F : {&F1, &F2}) {
+        F->N = in.get<int>();
+        const std::vector<float> xy = in.vec<float>(2 * (size_t)F->N);
+        F->mvKeysUn.resize(F->N);
+        for (int i = 0; i < F->N; ++i) F->mvKeysUn[i] = cv::KeyPoint(xy[2 * i], xy[2 * i + 1], 7.f);
+        F->mK = cv::Mat(3, 3, CV_32F);
+        for (int i = 0; i < 9; ++i) F->mK.at<float>(i / 3, i % 3) = K[i];
+    }
+    const std::vector<int> m12 = in.vec<int>(F1.N);
+    orbgpu_srand(1);  // a fresh process stream: SeedRandOnce(0) below seeds it (glibc: seed 0 == 1)
+    ORB_SLAM2::Initializer ini(F1, 1.0, 200);
+    cv::Mat R21, t21;
+    std::vector<cv::Point3f> vP3D;
+    std::vector<bool> vbTri;
+    const bool ok = ini.Initialize(F2, m12, R21, t21, vP3D, vbTri);
+    Out out(outp);
+    out.put((int)ok);
+    out.put(ini.mModel);
+    out.put(ini.mRH);
+    std::vector<float> R(9, 0.f), t(3, 0.f), P(3 * (size_t)F1.N, 0.f);
+    std::vector<unsigned char> tri(F1.N, 0);
+    if (ok) {
+        for (int i = 0; i < 9; ++i) R[i] = R21.at<float>(i / 3, i % 3);
+        for (int i = 0; i < 3; ++i) t[i] = t21.at<float>(i);
+        for (int i = 0; i < F1.N; ++i) {
+            P[3 * i] = vP3D[i].x;
+            P[3 * i + 1] = vP3D[i].y;
+            P[3 * i + 2] = vP3D[i].z;
+            tri[i] = vbTri[i];
+        }
+    }
+    out.vec(R);
+    out.vec(t);
+    out.vec(P);
+    out.vec(tri);
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -683,6 +732,7 @@ int main(int argc, char** argv) {
         if (argc >= 5 && !strcmp(argv[1], "fuse")) return run_fuse(atoi(argv[2]), argv[3], argv[4]);
         if (argc >= 4 && !strcmp(argv[1], "sim3search")) return run_sim3search(argv[2], argv[3]);
         if (argc >= 4 && !strcmp(argv[1], "tri")) return run_tri(argv[2], argv[3]);
+        if (argc >= 4 && !strcmp(argv[1], "init")) return run_init(argv[2], argv[3]);
     } catch (const std::exception& e) {
         fprintf(stderr, "exception: %s\n", e.what());
         return 3;

@@ -24,6 +24,12 @@ struct Point2f {
     Point2f(float x_, float y_) : x(x_), y(y_) {}
 };
 
+struct Point3f {
+    float x = 0.f, y = 0.f, z = 0.f;
+    Point3f() = default;
+    Point3f(float x_, float y_, float z_) : x(x_), y(y_), z(z_) {}
+};
+
 struct KeyPoint {
     Point2f pt;
     float size = 0.f, angle = -1.f, response = 0.f;

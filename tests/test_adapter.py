@@ -489,3 +489,24 @@ def test_adapter_orbmatcher_search_for_triangulation(exe, tmp_path, seed, check_
     pairs = [(i, int(m_r[i])) for i in range(len(m_r)) if m_r[i] >= 0]
     assert got[0] == nm_r > 30 and got[1] == len(pairs)
     np.testing.assert_array_equal(got[2:].reshape(-1, 2), np.array(pairs, np.int32).reshape(-1, 2))
+
+
+@pytest.mark.gpu
+def test_adapter_initializer_monocular_initialization(exe, tmp_path):
+    """ORB_SLAM2::Initializer(F1, 1.0, 200).Initialize(F2, ...) in a fresh
+    process (SeedRandOnce(0) seeds the stream) vs the oracle pipeline"""
+    import test_init as ti
+    kp1, kp2, m12, pairs, M, inl, _ = ti._recon_scene("general", 600, 82)
+    K = ti.K.astype(F32)
+    blob = b"".join([K.tobytes(), struct.pack("<i", len(kp1)), np.asarray(kp1, F32).tobytes(),
+                     struct.pack("<i", len(kp2)), np.asarray(kp2, F32).tobytes(), np.asarray(m12, np.int32).tobytes()])
+    buf = _run(exe, tmp_path, "init", blob)
+    ok, model = struct.unpack_from("<ii", buf, 0)
+    rh, = struct.unpack_from("<f", buf, 8)
+    R = np.frombuffer(buf, F32, 9, 12).reshape(3, 3)
+    t = np.frombuffer(buf, F32, 3, 48)
+    r = ti._oracle_initialize(kp1, kp2, m12, K)
+    assert ok == int(r["ok"]) == 1 and model == r["model"] == 1
+    assert abs(rh - float(r["RH"])) < 1e-3
+    np.testing.assert_allclose(R, r["R21"], atol=2e-3)
+    np.testing.assert_allclose(t, r["t21"], atol=2e-3)

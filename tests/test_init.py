@@ -421,3 +421,39 @@ def test_gpu_reconstruct_degenerate():
         g = initializer.reconstruct(model, kp1, kp2, m12, none, Mm, K.astype(F))
         assert g["ok"] is False and r["ok"] is False
         assert all(x == 0 for x in g["n_good"]) and g["n_good"] == r["n_good"]
+
+
+# ---- Initializer::Initialize end to end (Initializer.cpp:55-157) ------------
+def _oracle_initialize(kp1, kp2, m12, K_, iterations=200):
+    first = np.nonzero(m12 >= 0)[0]
+    pairs = np.stack([first, m12[first]], 1)
+    r = init_ref.find_models(kp1, kp2, pairs, _sets_from_glibc(len(pairs), iterations))
+    useH = float(r["RH"]) > 0.40
+    if useH:
+        M = r["H21"][r["best_h"]]
+        inl = init_ref.check_homography(r["pts"], M, r["H12"][r["best_h"]])[1]
+    else:
+        M = r["F21"][r["best_f"]]
+        inl = init_ref.check_fundamental(r["pts"], M)[1]
+    rec = init_ref.reconstruct(0 if useH else 1, kp1, kp2, pairs, np.asarray(inl, bool), M, K_)
+    return dict(rec, model=0 if useH else 1, RH=r["RH"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n,seed", [("ground", 600, 81), ("general", 600, 82)])
+def test_gpu_initialize_vs_oracle(kind, n, seed):
+    """the whole Initialize: the kept model and decision equal, R21 / t21 to
+    2e-3 (the hypotheses are Jacobi vs LAPACK SVDs of the same DLT: section 5d)"""
+    _gpu()
+    import initializer
+    import ransac
+    kp1, kp2, m12, pairs, M, inl, _ = _recon_scene(kind, n, seed)
+    ransac.srand(0)  # the process stream as SeedRandOnce(0) leaves it
+    g = initializer.initialize(kp1, kp2, m12, K.astype(F))
+    r = _oracle_initialize(kp1, kp2, m12, K.astype(F))
+    assert g["model"] == r["model"] == (0 if kind == "ground" else 1)
+    assert abs(float(g["RH"]) - float(r["RH"])) < 1e-3
+    assert g["ok"] == r["ok"] is True
+    np.testing.assert_allclose(g["R21"], r["R21"], atol=2e-3)
+    np.testing.assert_allclose(g["t21"], r["t21"], atol=2e-3)
+    assert (g["triangulated"] == r["triangulated"]).mean() > 0.98
