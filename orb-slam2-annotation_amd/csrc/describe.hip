@@ -27,9 +27,18 @@ namespace {
 __constant__ signed char c_pattern[1024] = {
 #include "bit_pattern_31.inc"
 };
-// umax of the 31-px disc (ORBextractor.cpp:456-471); checked against the
-// construction on the host at extractor creation.
-__constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+// umax of the 31-px disc (ORBextractor.cpp:456-471; the oracle builds it the
+// reference's way), packed 4 bits per entry so a per-lane lookup is a shift,
+// not a memory load
+constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+constexpr unsigned long long pack_umax() {
+    unsigned long long k = 0;
+    for (int i = 0; i < 16; ++i) k |= (unsigned long long)kUmax[i] << (4 * i);
+    return k;
+}
+constexpr unsigned long long kUmaxPacked = pack_umax();
+static_assert(kUmaxPacked == 0x3689abcddeeeffffull, "umax packing");
+__device__ inline int umax_of(int v) { return (int)((kUmaxPacked >> (4 * (v & 15))) & 15ull); }
 
 // OpenCV 2.4 fastAtan2 (mathfuncs.cpp); explicit _rn ops: never contracted.
 __device__ inline float fast_atan2(float y, float x) {
@@ -192,7 +201,7 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
 #pragma unroll
     for (int k = 0; k < kDiscLoads; ++k) {
         const int idx = lane + 64 * k, r = min(idx, kDiscWords - 1) / 9, q = min(idx, kDiscWords - 1) - r * 9;
-        const int vv = r - 15, d = c_umax[abs(vv) & 15];
+        const int vv = r - 15, d = umax_of(abs(vv));
         const int s0 = min(max(od + 15 - d - 4 * q, 0), 4), e0 = min(max(od + 16 + d - 4 * q, 0), 4);
         const uint32_t mask = e0 > s0 ? (uint32_t)(((1ull << (8 * (e0 - s0))) - 1ull) << (8 * s0)) : 0u;
         const uint32_t w = idx < kDiscWords ? *reinterpret_cast<const uint32_t*>(disc + r * kRPitch + 4 * q) & mask : 0u;
