@@ -65,19 +65,22 @@ struct Raw3 {
     uint32_t a, b, c;  // level columns x0-4 .. x0+7
 };
 
+// Row pass of the 4 columns x0..x0+3 from the three raw words around them:
+// per column the 7 taps are two 4-byte windows cut out by v_alignbyte_b32,
+// [x-3, x] against (18, 34, 49, 55) and [x+1, x+4) against (49, 34, 18, 0),
+// summed exactly by two v_dot4_u32_u8 (at most 255 * 257 = 65535).
 __device__ __forceinline__ void row_pass_raw(const Raw3& R, f32x2& lo, f32x2& hi) {
-    uint32_t P[9];
-    // bytes of (b:a) / (c:b) as v_perm_b32 sees them: low word 0-3, high word 4-7
-    P[0] = __builtin_amdgcn_perm(R.b, R.a, 0x0c020c01u);
-    P[1] = __builtin_amdgcn_perm(R.b, R.a, 0x0c030c02u);
-    P[2] = __builtin_amdgcn_perm(R.b, R.a, 0x0c040c03u);
-    P[3] = __builtin_amdgcn_perm(R.b, R.a, 0x0c050c04u);
-    P[4] = __builtin_amdgcn_perm(R.c, R.b, 0x0c020c01u);
-    P[5] = __builtin_amdgcn_perm(R.c, R.b, 0x0c030c02u);
-    P[6] = __builtin_amdgcn_perm(R.c, R.b, 0x0c040c03u);
-    P[7] = __builtin_amdgcn_perm(R.c, R.b, 0x0c050c04u);
-    P[8] = __builtin_amdgcn_perm(R.c, R.b, 0x0c060c05u);
-    row_pass(P, lo, hi);
+    constexpr uint32_t K1 = 18u | 34u << 8 | 49u << 16 | 55u << 24;  // taps x-3 .. x
+    constexpr uint32_t K2 = 49u | 34u << 8 | 18u << 16;              // taps x+1 .. x+3
+    const uint32_t w10 = __builtin_amdgcn_alignbyte(R.b, R.a, 1), w20 = __builtin_amdgcn_alignbyte(R.c, R.b, 1);
+    const uint32_t w11 = __builtin_amdgcn_alignbyte(R.b, R.a, 2), w21 = __builtin_amdgcn_alignbyte(R.c, R.b, 2);
+    const uint32_t w12 = __builtin_amdgcn_alignbyte(R.b, R.a, 3), w22 = __builtin_amdgcn_alignbyte(R.c, R.b, 3);
+    const uint32_t s0 = __builtin_amdgcn_udot4(w20, K2, __builtin_amdgcn_udot4(w10, K1, 0u, false), false);
+    const uint32_t s1 = __builtin_amdgcn_udot4(w21, K2, __builtin_amdgcn_udot4(w11, K1, 0u, false), false);
+    const uint32_t s2 = __builtin_amdgcn_udot4(w22, K2, __builtin_amdgcn_udot4(w12, K1, 0u, false), false);
+    const uint32_t s3 = __builtin_amdgcn_udot4(R.c, K2, __builtin_amdgcn_udot4(R.b, K1, 0u, false), false);
+    lo = f32x2{(float)s0, (float)s1};
+    hi = f32x2{(float)s2, (float)s3};
 }
 
 }  // namespace blurdev
