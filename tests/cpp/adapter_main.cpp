@@ -27,6 +27,9 @@
 //   adapter_main init <in.bin> <out.bin>
 //       Initializer(F1, 1.0, 200).Initialize(F2, vMatches12, ...) as
 //       Tracking::MonocularInitialization drives it (Tracking.cpp:755-820)
+//   adapter_main kfdb <in.bin> <out.bin>
+//       KeyFrameDatabase::add + DetectLoopCandidates / DetectRelocalizationCandidates
+//       (LoopClosing::DetectLoop, Tracking::Relocalization)
 //   adapter_main tri <in.bin> <out.bin>
 //       ORBmatcher::SearchForTriangulation (LocalMapping.cpp:355-360)
 // The .bin layouts are written / read by tests/test_adapter.py (fixed
@@ -45,6 +48,7 @@
 
 #include "orbslam2_amd/ORBextractor.h"
 #include "orbslam2_amd/Initializer.h"
+#include "orbslam2_amd/KeyFrameDatabase.h"
 #include "orbslam2_amd/ORBmatcher.h"
 #include "orbslam2_amd/PnPsolver.h"
 #include "orbslam2_amd/Sim3Solver.h"
@@ -721,6 +725,88 @@ int run_init(const char* inp, const char* outp) {
     return 0;
 }
 
+// The KeyFrame / Frame fields KeyFrameDatabase reads (KeyFrame.h:120-200).
+struct DbKeyFrame {
+    long unsigned int mnId = 0;
+    std::map<unsigned int, double> mBowVec;
+    long unsigned int mnLoopQuery = 0, mnRelocQuery = 0;
+    int mnLoopWords = 0, mnRelocWords = 0;
+    float mLoopScore = 0.f, mRelocScore = 0.f;
+    std::set<DbKeyFrame*> connected;
+    std::vector<DbKeyFrame*> covis;
+    std::set<DbKeyFrame*> GetConnectedKeyFrames() { return connected; }
+    std::vector<DbKeyFrame*> GetBestCovisibilityKeyFrames(int n) {
+        return std::vector<DbKeyFrame*>(covis.begin(), covis.begin() + std::min<size_t>(n, covis.size()));
+    }
+};
+struct DbFrame {
+    long unsigned int mnId = 0;
+    std::map<unsigned int, double> mBowVec;
+};
+struct DbVoc {
+    size_t n;
+    int scoring;
+    size_t size() const { return n; }
+    int getScoringType() const { return scoring; }
+};
+class KeyFrameDatabase : public orbslam2_amd::KeyFrameDatabaseT<DbKeyFrame, DbFrame> {
+public:
+    explicit KeyFrameDatabase(const DbVoc& voc) : KeyFrameDatabaseT(voc) {}
+};
+
+// kfdb: scoring, n_words, nkf; per keyframe: id, nbow, words, values, nconn, conn idx,
+// ncov, covis idx; then the queries: nq x (kind (0 loop, 1 reloc), loop: kf index +
+// minScore; reloc: frame id, nbow, words, values).  Output per query: n, candidate indices.
+int run_kfdb(const char* inp, const char* outp) {
+    In in{read_file(inp)};
+    const int scoring = in.get<int>(), nwords = in.get<int>(), nkf = in.get<int>();
+    std::vector<std::unique_ptr<DbKeyFrame>> kfs;
+    std::vector<std::vector<int>> conn(nkf), cov(nkf);
+    for (int k = 0; k < nkf; ++k) {
+        kfs.emplace_back(new DbKeyFrame());
+        DbKeyFrame* K = kfs.back().get();
+        K->mnId = in.get<unsigned>();
+        const int nb = in.get<int>();
+        const std::vector<int> w = in.vec<int>(nb);
+        const std::vector<double> v = in.vec<double>(nb);
+        for (int i = 0; i < nb; ++i) K->mBowVec[(unsigned)w[i]] = v[i];
+        conn[k] = in.vec<int>(in.get<int>());
+        cov[k] = in.vec<int>(in.get<int>());
+    }
+    std::map<const DbKeyFrame*, int> index;
+    for (int k = 0; k < nkf; ++k) {
+        index[kfs[k].get()] = k;
+        for (int c : conn[k]) kfs[k]->connected.insert(kfs[c].get());
+        for (int c : cov[k]) kfs[k]->covis.push_back(kfs[c].get());
+    }
+    KeyFrameDatabase db(DbVoc{(size_t)nwords, scoring});
+    for (auto& k : kfs) db.add(k.get());
+    Out out(outp);
+    const int nq = in.get<int>();
+    for (int q = 0; q < nq; ++q) {
+        const int kind = in.get<int>();
+        std::vector<DbKeyFrame*> cands;
+        if (kind == 0) {
+            const int k = in.get<int>();
+            const float minScore = in.get<float>();
+            db.erase(kfs[k].get());  // LoopClosing::DetectLoop adds the current keyframe after the query
+            cands = db.DetectLoopCandidates(kfs[k].get(), minScore);
+            db.add(kfs[k].get());
+        } else {
+            DbFrame F;
+            F.mnId = in.get<unsigned>();
+            const int nb = in.get<int>();
+            const std::vector<int> w = in.vec<int>(nb);
+            const std::vector<double> v = in.vec<double>(nb);
+            for (int i = 0; i < nb; ++i) F.mBowVec[(unsigned)w[i]] = v[i];
+            cands = db.DetectRelocalizationCandidates(&F);
+        }
+        out.put((int)cands.size());
+        for (DbKeyFrame* c : cands) out.put(index[c]);
+    }
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -733,6 +819,7 @@ int main(int argc, char** argv) {
         if (argc >= 4 && !strcmp(argv[1], "sim3search")) return run_sim3search(argv[2], argv[3]);
         if (argc >= 4 && !strcmp(argv[1], "tri")) return run_tri(argv[2], argv[3]);
         if (argc >= 4 && !strcmp(argv[1], "init")) return run_init(argv[2], argv[3]);
+        if (argc >= 4 && !strcmp(argv[1], "kfdb")) return run_kfdb(argv[2], argv[3]);
     } catch (const std::exception& e) {
         fprintf(stderr, "exception: %s\n", e.what());
         return 3;

@@ -510,3 +510,76 @@ def test_adapter_initializer_monocular_initialization(exe, tmp_path):
     assert abs(rh - float(r["RH"])) < 1e-3
     np.testing.assert_allclose(R, r["R21"], atol=2e-3)
     np.testing.assert_allclose(t, r["t21"], atol=2e-3)
+
+
+def _kfdb_scene(scoring=0, n_kf=120, seed=5):
+    """keyframes along a looping path over 1200 landmarks (keyframe k sees
+    landmarks [10k, 10k + 250) mod 1200), BowVectors from a synthetic
+    vocabulary; covisibility = path neighbours"""
+    import bow_ref
+    par, leaf, desc, w = synth.synthetic_vocabulary(6, 4, 77)
+    voc = bow_ref.Vocabulary.from_arrays(6, 4, scoring, 0, par, leaf, desc, w)
+    rng = np.random.default_rng(seed)
+    leaves = desc[leaf == 1]
+    lm = leaves[rng.integers(0, len(leaves), 1200)]
+
+    def observe(ids):
+        d = lm[ids] ^ (rng.uniform(size=(len(ids), 32)) < 0.03).astype(np.uint8)
+        return voc.transform(d, 2)[4]
+    kfs = []
+    for k in range(n_kf):
+        ids = (10 * k + np.arange(250)) % 1200
+        ids = ids[rng.uniform(size=250) < 0.85]
+        near = [j for j in sorted(range(max(0, k - 6), min(n_kf, k + 7)), key=lambda j: (abs(j - k), j)) if j != k]
+        kfs.append({"id": k + 1, "bow": observe(ids), "connected": set(near),
+                    "best_covis": near[:10], "loop_query": 0, "loop_words": 0, "loop_score": np.float32(0),
+                    "reloc_query": 0, "reloc_words": 0, "reloc_score": np.float32(0)})
+    frame_bow = observe((500 + np.arange(250)) % 1200)
+    return voc, kfs, frame_bow
+
+
+def _bow_blob(bow):
+    ws = np.array(sorted(bow), np.int32)
+    return struct.pack("<i", len(ws)) + ws.tobytes() + np.array([bow[int(x)] for x in ws], np.float64).tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scoring", [0, 1])
+def test_adapter_keyframe_database(exe, tmp_path, scoring):
+    """orbslam2_amd::KeyFrameDatabaseT (GPU scores) vs oracle/kfdb_ref.py:
+    DetectLoopCandidates for two query keyframes, DetectRelocalizationCandidates
+    for one frame -- candidate lists equal, in order"""
+    import kfdb_ref
+    voc, kfs, fbow = _kfdb_scene(scoring)
+    db = kfdb_ref.KeyFrameDatabase(voc.n_words, scoring)
+    for i in range(len(kfs)):
+        db.add(kfs, i)
+    queries = [(0, 118, 0.01), (0, 60, 0.02), (1, 1000, fbow)]
+    want = []
+    for kind, a, b in queries:
+        if kind == 0:  # the query keyframe is not in the database yet (LoopClosing::DetectLoop)
+            db.erase(kfs, a)
+            want.append(db.detect_loop(kfs, a, b))
+            db.inv = [lst for lst in db.inv]
+            for w in sorted(kfs[a]["bow"]):
+                db.inv[w].append(a)
+        else:
+            want.append(db.detect_reloc(kfs, b, a))
+    parts = [struct.pack("<iii", scoring, voc.n_words + 1, len(kfs))]
+    for k in kfs:
+        conn = np.array(sorted(k["connected"]), np.int32)
+        cov = np.array(k["best_covis"], np.int32)
+        parts += [struct.pack("<I", k["id"]), _bow_blob(k["bow"]), struct.pack("<i", len(conn)), conn.tobytes(),
+                  struct.pack("<i", len(cov)), cov.tobytes()]
+    parts.append(struct.pack("<i", len(queries)))
+    for kind, a, b in queries:
+        parts.append(struct.pack("<iif", 0, a, b) if kind == 0 else struct.pack("<iI", 1, a) + _bow_blob(b))
+    buf = _run(exe, tmp_path, "kfdb", b"".join(parts))
+    got, o = [], 0
+    for _ in queries:
+        n, = struct.unpack_from("<i", buf, o)
+        got.append(list(np.frombuffer(buf, np.int32, n, o + 4)))
+        o += 4 + 4 * n
+    assert got == want
+    assert len(want[0]) >= 1 and min(want[0]) < 10  # the loop back to the first keyframes is found
+    assert len(want[2]) >= 1
