@@ -30,6 +30,9 @@
 //   adapter_main kfdb <in.bin> <out.bin>
 //       KeyFrameDatabase::add + DetectLoopCandidates / DetectRelocalizationCandidates
 //       (LoopClosing::DetectLoop, Tracking::Relocalization)
+//   adapter_main voc <vocab.txt> <in.bin> <out.bin>
+//       ORBVocabulary::loadFromTextFile, transform of two descriptor sets (as
+//       Frame::ComputeBoW, levelsup 4), score of the two BowVectors
 //   adapter_main tri <in.bin> <out.bin>
 //       ORBmatcher::SearchForTriangulation (LocalMapping.cpp:355-360)
 // The .bin layouts are written / read by tests/test_adapter.py (fixed
@@ -49,6 +52,7 @@
 #include "orbslam2_amd/ORBextractor.h"
 #include "orbslam2_amd/Initializer.h"
 #include "orbslam2_amd/KeyFrameDatabase.h"
+#include "orbslam2_amd/ORBVocabulary.h"
 #include "orbslam2_amd/ORBmatcher.h"
 #include "orbslam2_amd/PnPsolver.h"
 #include "orbslam2_amd/Sim3Solver.h"
@@ -807,6 +811,47 @@ int run_kfdb(const char* inp, const char* outp) {
     return 0;
 }
 
+// voc: in = levelsup, n1, desc1 (n1 x 32), n2, desc2.  Output: size, scoring, then per
+// set: nb, (word, value) pairs, nf, (node, count, features...) ; then score(v1, v2).
+int run_voc(const char* vocp, const char* inp, const char* outp) {
+    orbslam2_amd::ORBVocabulary voc;
+    if (!voc.loadFromTextFile(vocp)) {
+        fprintf(stderr, "load failed\n");
+        return 4;
+    }
+    In in{read_file(inp)};
+    const int levelsup = in.get<int>();
+    Out out(outp);
+    out.put((int)voc.size());
+    out.put(voc.getScoringType());
+    std::map<unsigned int, double> bv[2];
+    for (int s = 0; s < 2; ++s) {
+        const int n = in.get<int>();
+        const std::vector<unsigned char> d = in.vec<unsigned char>(32 * (size_t)n);
+        std::vector<cv::Mat> feats;
+        for (int i = 0; i < n; ++i) {
+            cv::Mat row(1, 32, CV_8U);
+            std::memcpy(row.data, &d[32 * (size_t)i], 32);
+            feats.push_back(row);
+        }
+        std::map<unsigned int, std::vector<unsigned int>> fv;
+        voc.transform(feats, bv[s], fv, levelsup);
+        out.put((int)bv[s].size());
+        for (auto& kv : bv[s]) {
+            out.put((int)kv.first);
+            out.put(kv.second);
+        }
+        out.put((int)fv.size());
+        for (auto& kv : fv) {
+            out.put((int)kv.first);
+            out.put((int)kv.second.size());
+            for (unsigned int f : kv.second) out.put((int)f);
+        }
+    }
+    out.put(voc.score(bv[0], bv[1]));
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -820,6 +865,7 @@ int main(int argc, char** argv) {
         if (argc >= 4 && !strcmp(argv[1], "tri")) return run_tri(argv[2], argv[3]);
         if (argc >= 4 && !strcmp(argv[1], "init")) return run_init(argv[2], argv[3]);
         if (argc >= 4 && !strcmp(argv[1], "kfdb")) return run_kfdb(argv[2], argv[3]);
+        if (argc >= 5 && !strcmp(argv[1], "voc")) return run_voc(argv[2], argv[3], argv[4]);
     } catch (const std::exception& e) {
         fprintf(stderr, "exception: %s\n", e.what());
         return 3;

@@ -583,3 +583,51 @@ def test_adapter_keyframe_database(exe, tmp_path, scoring):
     assert got == want
     assert len(want[0]) >= 1 and min(want[0]) < 10  # the loop back to the first keyframes is found
     assert len(want[2]) >= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scoring,weighting", [(0, 0), (1, 1)])
+def test_adapter_orb_vocabulary(exe, tmp_path, scoring, weighting):
+    """orbslam2_amd::ORBVocabulary: loadFromTextFile, transform (Frame::ComputeBoW,
+    levelsup 4) and score vs oracle/bow_ref.py -- bit-exact"""
+    import bow_ref
+    par, leaf, desc, w = synth.synthetic_vocabulary(6, 5, 91)
+    vp = tmp_path / "voc.txt"
+    synth.write_vocabulary_text(vp, 6, 5, scoring, weighting, par, leaf, desc, w)
+    ref = bow_ref.Vocabulary.load_text(vp)
+    rng = np.random.default_rng(4)
+    leaves = desc[leaf == 1]
+    d1 = leaves[rng.integers(0, len(leaves), 500)] ^ (rng.uniform(size=(500, 32)) < 0.04).astype(np.uint8)
+    d2 = np.vstack([d1[:300], rng.integers(0, 256, (200, 32), dtype=np.uint8)])
+    blob = struct.pack("<ii", 4, len(d1)) + d1.tobytes() + struct.pack("<i", len(d2)) + d2.tobytes()
+    inp, out = tmp_path / "voc.in", tmp_path / "voc.out"
+    inp.write_bytes(blob)
+    r = subprocess.run([exe, "voc", str(vp), str(inp), str(out)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    buf = out.read_bytes()
+    size, sc = struct.unpack_from("<ii", buf, 0)
+    assert size == ref.n_words and sc == scoring
+    o = 8
+    bows = []
+    for d in (d1, d2):
+        _, _, _, rfv, rbow = ref.transform(d, 4)
+        nb, = struct.unpack_from("<i", buf, o)
+        o += 4
+        got = {}
+        for _ in range(nb):
+            wd, = struct.unpack_from("<i", buf, o)
+            val, = struct.unpack_from("<d", buf, o + 4)
+            got[wd] = val
+            o += 12
+        assert got == rbow  # ids and double weights bit-exact
+        nf, = struct.unpack_from("<i", buf, o)
+        o += 4
+        gfv = {}
+        for _ in range(nf):
+            node, cnt = struct.unpack_from("<ii", buf, o)
+            gfv[node] = list(np.frombuffer(buf, np.int32, cnt, o + 8))
+            o += 8 + 4 * cnt
+        assert gfv == {k: list(v) for k, v in rfv.items()}
+        bows.append(rbow)
+    s, = struct.unpack_from("<d", buf, o)
+    assert s == bow_ref.bow_score(scoring, bows[0], bows[1])[0]
