@@ -261,6 +261,28 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     // all of a lane's loads are issued before any is consumed, so the
     // window costs one memory round trip, not one per row group
     const uint8_t* wbase = base + (size_t)iniY * pitch + xa;
+    if constexpr (P % 16 == 0) {
+        // 16-byte chunks (P a multiple of 16: a row's chunks stay inside its LDS row; the
+        // last chunk reads at most 12 bytes past maxX, still inside the level row since
+        // maxX <= w - 16); one load per lane for ~64 of a window's ~115 chunks
+        const int nc = (maxX - xa + 15) >> 4;
+        const uint32_t mnc = (1u << 24) / (uint32_t)nc + 1u;
+        for (int b0 = 0; b0 < nc * wh; b0 += 64 * 2) {
+            uint4 v[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int idx = min(b0 + lane + 64 * k, nc * wh - 1);
+                const int r = fast_div(idx, mnc), q = idx - r * nc;
+                v[k] = *reinterpret_cast<const uint4*>(wbase + (size_t)r * pitch + 16 * q);
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int idx = b0 + lane + 64 * k;
+                const int r = fast_div(idx, mnc), q = idx - r * nc;
+                if (idx < nc * wh) *reinterpret_cast<uint4*>(s_win + r * P + 16 * q) = v[k];
+            }
+        }
+    } else
     for (int b0 = 0; b0 < nd * wh; b0 += 64 * kStageLoads) {
         uint32_t v[kStageLoads];
 #pragma unroll
@@ -276,7 +298,10 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
             if (idx < nd * wh) *reinterpret_cast<uint32_t*>(s_win + r * P + 4 * q) = v[k];
         }
     }
-    for (int idx = lane; idx < P * R / 4; idx += 64) reinterpret_cast<uint32_t*>(T.sc)[idx] = 0u;
+    // (T.sc is 16-byte aligned when P * R is: then 16-byte stores, else dwords)
+    const int nz16 = (P * R) % 16 == 0 ? P * R / 16 : 0;
+    for (int idx = lane; idx < nz16; idx += 64) reinterpret_cast<uint4*>(T.sc)[idx] = make_uint4(0u, 0u, 0u, 0u);
+    for (int idx = nz16 * 4 + lane; idx < P * R / 4; idx += 64) reinterpret_cast<uint32_t*>(T.sc)[idx] = 0u;
     wave_sync();
 
     // detection region of cv::FAST on the window: rows [3, wh-3), cols [3, ww-3)
