@@ -132,7 +132,7 @@ __device__ inline void wave_sync() {
 __device__ inline int reflect101(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
 
 // Per-wave LDS: the raw 43x48 neighbourhood and the blurred 37x40 patch.
-struct DescLds {
+struct alignas(16) DescLds {
     uint8_t raw[kPatch * kRPitch];
     uint8_t blur[kBlur * kBPitch];
 };
@@ -167,6 +167,23 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
     // load each; a dword that crosses the border is assembled from reflected
     // bytes.  All loads of a lane are issued before any is stored.
     const int xb = (cx - kBlurR) & ~3, ob = cx - kBlurR - xb, x0 = xb - 4;
+    // a neighbourhood entirely inside the level (wave-uniform; most keypoints): three
+    // 16-byte chunks per row, two loads per lane, no reflection
+    if (x0 >= 0 && x0 + kRPitch <= L.w && cy - kPatchR >= 0 && cy + kPatchR < L.h) {
+        constexpr int kChunks = kPatch * (kRPitch / 16);  // 129
+        const uint8_t* top = raw + (size_t)(cy - kPatchR) * rp + x0;
+        uint4 c[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int idx = min(lane + 64 * k, kChunks - 1), r = idx / 3, q = idx - 3 * r;
+            c[k] = *reinterpret_cast<const uint4*>(top + (size_t)r * rp + 16 * q);
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int idx = lane + 64 * k, r = idx / 3, q = idx - 3 * r;
+            if (idx < kChunks) *reinterpret_cast<uint4*>(S.raw + r * kRPitch + 16 * q) = c[k];
+        }
+    } else {
     constexpr int kLoads = (kRawWords + 63) / 64;
     uint32_t v[kLoads];
 #pragma unroll
@@ -186,6 +203,7 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
     for (int k = 0; k < kLoads; ++k) {
         const int idx = lane + 64 * k;
         if (idx < kRawWords) reinterpret_cast<uint32_t*>(S.raw)[idx] = v[k];
+    }
     }
     wave_sync();
 
