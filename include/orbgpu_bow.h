@@ -48,6 +48,16 @@ typedef struct orbgpu_vocabulary_info {
  * zero-descriptor, zero-weight node under the root.  ORBGPU_ERR_ARG for a
  * header outside the reference's accepted ranges. */
 int orbgpu_vocabulary_load_text(const char* path, orbgpu_vocabulary** out);
+/* loadFromBinaryFile semantics (TemplatedVocabulary.h:1477-1522; the format
+ * saveToBinaryFile writes, :1527-1548): weights are the file's floats; the
+ * reference's `while(!f.eof())` loop processes the last record twice, so the
+ * last node appears twice under its parent (the copy never wins the strict
+ * minimum of transform's descent) and, when it is a leaf, adds one word; the
+ * node table holds nb_nodes + 1 entries.  ORBGPU_ERR_ARG for a short header,
+ * k/L/scoring/weighting outside the text loader's ranges, records under 41
+ * bytes, more records than nb_nodes or a parent that is not an earlier node
+ * (the reference's undefined behaviour in those cases). */
+int orbgpu_vocabulary_load_binary(const char* path, orbgpu_vocabulary** out);
 /* From node arrays in file order: node i+1 has parent[i], is_leaf[i],
  * desc[32*i..], weight[i] (the root, node 0, is implicit). */
 int orbgpu_vocabulary_create(int k, int L, int scoring, int weighting, int n_nodes_without_root,

@@ -7,6 +7,7 @@
 //
 // The members ORB-SLAM2 calls:
 //   bool loadFromTextFile(const std::string&)          TemplatedVocabulary.h:1362   (System.cc)
+//   bool loadFromBinaryFile(const std::string&)        :1478 (the binary form of the same tree)
 //   void transform(features, BowVector&, FeatureVector&, levelsup) const   :1151 (Frame/KeyFrame::ComputeBoW)
 //   double score(const BowVector&, const BowVector&) const                 :1222 (LoopClosing, KeyFrameDatabase)
 //   unsigned size() const, ScoringType getScoringType() const              (KeyFrameDatabase)
@@ -45,6 +46,17 @@ public:
     bool loadFromTextFile(const std::string& filename) {
         orbgpu_vocabulary* v = nullptr;
         if (orbgpu_vocabulary_load_text(filename.c_str(), &v) != ORBGPU_OK) return false;
+        if (mVoc) orbgpu_vocabulary_destroy(mVoc);
+        mVoc = v;
+        return orbgpu_vocabulary_get_info(mVoc, &mInfo) == ORBGPU_OK;
+    }
+
+    // TemplatedVocabulary::loadFromBinaryFile (TemplatedVocabulary.h:1478); the
+    // reference returns true for any file it opens, this false when the file
+    // cannot be read or is malformed (include/orbgpu_bow.h)
+    bool loadFromBinaryFile(const std::string& filename) {
+        orbgpu_vocabulary* v = nullptr;
+        if (orbgpu_vocabulary_load_binary(filename.c_str(), &v) != ORBGPU_OK) return false;
         if (mVoc) orbgpu_vocabulary_destroy(mVoc);
         mVoc = v;
         return orbgpu_vocabulary_get_info(mVoc, &mInfo) == ORBGPU_OK;

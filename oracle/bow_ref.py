@@ -69,6 +69,39 @@ class Vocabulary:
             v._add(pid, leaf, d, w)
         return v
 
+    @classmethod
+    def load_binary(cls, path):
+        """loadFromBinaryFile (T:1477-1522): header u32 nb_nodes, u32 size_node,
+        int k, L, scoring, weighting; records (int parent, 32 desc bytes, float
+        weight, bool leaf at byte 40).  The `while(!f.eof())` loop runs once
+        more after the last full record on a 0-byte read, so the persistent
+        buffer's record is processed again (a short read overwrites only its
+        prefix); m_nodes has nb_nodes + 1 entries, the ones no record reaches
+        stay default (parent 0, unattached)."""
+        data = open(path, "rb").read()
+        nb_nodes, size_node = (int(x) for x in np.frombuffer(data[:8], "<u4"))
+        k, L, n1, n2 = (int(x) for x in np.frombuffer(data[8:24], "<i4"))
+        v = cls(k, L, n1, n2)
+        buf = bytearray(size_node)
+        pos = 24
+        while True:
+            chunk = data[pos:pos + size_node]
+            pos += len(chunk)
+            buf[:len(chunk)] = chunk
+            pid = int(np.frombuffer(bytes(buf[0:4]), "<i4")[0])
+            w = float(np.frombuffer(bytes(buf[36:40]), "<f4")[0])
+            v._add(pid, 1 if buf[40] else 0, np.frombuffer(bytes(buf[4:36]), np.uint8).copy(), w)
+            if len(chunk) < size_node:  # the read that hit the end of the file sets eof
+                break
+        assert len(v.parent) <= nb_nodes + 1, "more records than nb_nodes (undefined in the reference)"
+        while len(v.parent) < nb_nodes + 1:  # default Node()s, not attached to any parent
+            v.parent.append(0)
+            v.children.append([])
+            v.desc.append(np.zeros(32, np.uint8))
+            v.weight.append(0.0)
+            v.word_id.append(0)
+        return v
+
     def transform_one(self, f, levelsup):
         """transform(feature, word, weight, nid, levelsup) (T:1242-1283)."""
         nid_level = self.L - levelsup

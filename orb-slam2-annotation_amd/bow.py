@@ -37,6 +37,14 @@ class Vocabulary:
         return cls(h)
 
     @classmethod
+    def load_binary(cls, path: str) -> "Vocabulary":
+        """TemplatedVocabulary::loadFromBinaryFile (TemplatedVocabulary.h:1478)."""
+        h = ctypes.c_void_p()
+        orbgpu._check(orbgpu.lib().orbgpu_vocabulary_load_binary(str(path).encode(), ctypes.byref(h)),
+                      "orbgpu_vocabulary_load_binary")
+        return cls(h)
+
+    @classmethod
     def from_arrays(cls, k, L, scoring, weighting, parent, is_leaf, desc, weight) -> "Vocabulary":
         parent = np.ascontiguousarray(parent, np.int32)
         is_leaf = np.ascontiguousarray(is_leaf, np.int32)

@@ -138,6 +138,54 @@ int orbgpu_vocabulary_load_text(const char* path, orbgpu_vocabulary** out) {
     return finish(nodes, k, L, n1, n2, n_words, out);
 }
 
+int orbgpu_vocabulary_load_binary(const char* path, orbgpu_vocabulary** out) {
+    if (!path || !out) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    *out = nullptr;
+    // TemplatedVocabulary::loadFromBinaryFile (TemplatedVocabulary.h:1477-1522):
+    // header u32 nb_nodes (root included), u32 size_node, int k, int L, int
+    // scoring, int weighting; then records of size_node bytes: int parent,
+    // 32 descriptor bytes, float weight, bool isLeaf (saveToBinaryFile, :1527-1548).
+    std::ifstream f(path, std::ios::in | std::ios::binary);
+    if (!f.is_open()) return fail(ORBGPU_ERR_ARG, std::string("cannot open ") + path);
+    uint32_t nb_nodes = 0, size_node = 0;
+    int32_t hdr[4] = {0, 0, 0, 0};
+    f.read(reinterpret_cast<char*>(&nb_nodes), 4);
+    f.read(reinterpret_cast<char*>(&size_node), 4);
+    f.read(reinterpret_cast<char*>(hdr), 16);
+    if (!f) return fail(ORBGPU_ERR_ARG, "vocabulary file shorter than the binary header");
+    const int k = hdr[0], L = hdr[1], scoring = hdr[2], weighting = hdr[3];
+    if (k < 0 || k > 20 || L < 1 || L > 10 || scoring < 0 || scoring > 5 || weighting < 0 || weighting > 3)
+        return fail(ORBGPU_ERR_ARG, "vocabulary header out of range (not a DBoW2 binary vocabulary)");
+    if (size_node < 41) return fail(ORBGPU_ERR_ARG, "binary vocabulary record smaller than 41 bytes");
+    if (nb_nodes > (1u << 26)) return fail(ORBGPU_ERR_ARG, "binary vocabulary node count out of range");
+    // m_nodes.resize(nb_nodes + 1); nodes past the records stay default and unattached
+    std::vector<HostNode> nodes((size_t)nb_nodes + 1);
+    // The record buffer persists across iterations, as the reference's: its
+    // `while (!f.eof())` loop runs once more after the last full record, on a
+    // read of 0 bytes, and so processes that record a second time (a short
+    // final read overwrites only its prefix).  A file with no record at all
+    // processes the buffer as allocated -- uninitialised there, zeros here.
+    std::vector<char> buf(size_node, 0);
+    int n_words = 0;
+    size_t nid = 1;
+    while (!f.eof()) {
+        f.read(buf.data(), size_node);
+        if (nid >= nodes.size()) return fail(ORBGPU_ERR_ARG, "binary vocabulary holds more records than nb_nodes");
+        int32_t pid;
+        float w;
+        std::memcpy(&pid, buf.data(), 4);
+        std::memcpy(nodes[nid].desc, buf.data() + 4, 32);
+        std::memcpy(&w, buf.data() + 36, 4);
+        if (pid < 0 || (size_t)pid >= nid) return fail(ORBGPU_ERR_ARG, "vocabulary node with an invalid parent");
+        nodes[nid].parent = pid;
+        nodes[pid].children.push_back((int)nid);
+        nodes[nid].weight = (double)w;
+        if (buf[40]) nodes[nid].word_id = n_words++;
+        ++nid;
+    }
+    return finish(nodes, k, L, scoring, weighting, n_words, out);
+}
+
 int orbgpu_vocabulary_create(int k, int L, int scoring, int weighting, int n, const int* parent, const int* is_leaf,
                              const uint8_t* desc, const double* weight, orbgpu_vocabulary** out) {
     if (!out || n < 0 || (n > 0 && (!parent || !is_leaf || !desc || !weight)))

@@ -140,6 +140,7 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_pnp_ransac_batch.argtypes = [i, vp, i, vp, vp, vp, i, vp, vp, vp, vp]
         # orbgpu_bow.h
         L.orbgpu_vocabulary_load_text.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
+        L.orbgpu_vocabulary_load_binary.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
         L.orbgpu_vocabulary_create.argtypes = [i, i, i, i, i, vp, vp, vp, vp, ctypes.POINTER(vp)]
         L.orbgpu_vocabulary_destroy.argtypes = [vp]
         L.orbgpu_vocabulary_get_info.argtypes = [vp, vp]

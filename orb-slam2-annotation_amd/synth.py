@@ -269,6 +269,24 @@ def write_vocabulary_text(path, k, L, scoring, weighting, parent, is_leaf, desc,
         f.write("\n".join(lines) + ("\n" if trailing_newline else ""))
 
 
+def write_vocabulary_binary(path, k, L, scoring, weighting, parent, is_leaf, desc, weight):
+    """DBoW2 binary vocabulary as saveToBinaryFile writes it
+    (TemplatedVocabulary.h:1527-1548): u32 nb_nodes (root included), u32
+    size_node = 41, int k, L, scoring, weighting, then per node after the root
+    int parent, 32 descriptor bytes, float weight, bool isLeaf."""
+    n = len(parent)
+    rec = np.zeros(n, dtype=np.dtype([("parent", "<i4"), ("desc", "u1", 32), ("weight", "<f4"), ("leaf", "u1")]))
+    rec["parent"] = np.asarray(parent, np.int32)
+    rec["desc"] = np.asarray(desc, np.uint8)
+    rec["weight"] = np.asarray(weight, np.float64).astype(np.float32)
+    rec["leaf"] = (np.asarray(is_leaf) > 0).astype(np.uint8)
+    assert rec.dtype.itemsize == 41
+    with open(path, "wb") as f:
+        f.write(np.array([n + 1, 41], "<u4").tobytes())
+        f.write(np.array([k, L, scoring, weighting], "<i4").tobytes())
+        f.write(rec.tobytes())
+
+
 def bow_frame_pair(voc_desc_leaves: np.ndarray, n: int, shared: float, seed: int, flip: float = 0.04):
     """Two frames' descriptors for SearchByBoW: frame-2 feature j for
     j < shared*n is frame-1 feature perm[j] with a few bits flipped (true

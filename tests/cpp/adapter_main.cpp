@@ -30,7 +30,7 @@
 //   adapter_main kfdb <in.bin> <out.bin>
 //       KeyFrameDatabase::add + DetectLoopCandidates / DetectRelocalizationCandidates
 //       (LoopClosing::DetectLoop, Tracking::Relocalization)
-//   adapter_main voc <vocab.txt> <in.bin> <out.bin>
+//   adapter_main voc <vocab.txt|vocab.bin> <in.bin> <out.bin>   (.bin: loadFromBinaryFile)
 //       ORBVocabulary::loadFromTextFile, transform of two descriptor sets (as
 //       Frame::ComputeBoW, levelsup 4), score of the two BowVectors
 //   adapter_main tri <in.bin> <out.bin>
@@ -815,7 +815,9 @@ int run_kfdb(const char* inp, const char* outp) {
 // set: nb, (word, value) pairs, nf, (node, count, features...) ; then score(v1, v2).
 int run_voc(const char* vocp, const char* inp, const char* outp) {
     orbslam2_amd::ORBVocabulary voc;
-    if (!voc.loadFromTextFile(vocp)) {
+    const std::string vps(vocp);
+    const bool binary = vps.size() > 4 && vps.compare(vps.size() - 4, 4, ".bin") == 0;
+    if (!(binary ? voc.loadFromBinaryFile(vps) : voc.loadFromTextFile(vps))) {
         fprintf(stderr, "load failed\n");
         return 4;
     }

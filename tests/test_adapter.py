@@ -586,15 +586,19 @@ def test_adapter_keyframe_database(exe, tmp_path, scoring):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("scoring,weighting", [(0, 0), (1, 1)])
-def test_adapter_orb_vocabulary(exe, tmp_path, scoring, weighting):
-    """orbslam2_amd::ORBVocabulary: loadFromTextFile, transform (Frame::ComputeBoW,
-    levelsup 4) and score vs oracle/bow_ref.py -- bit-exact"""
+@pytest.mark.parametrize("scoring,weighting,fmt", [(0, 0, "txt"), (1, 1, "txt"), (2, 0, "bin")])
+def test_adapter_orb_vocabulary(exe, tmp_path, scoring, weighting, fmt):
+    """orbslam2_amd::ORBVocabulary: loadFromTextFile / loadFromBinaryFile,
+    transform (Frame::ComputeBoW, levelsup 4) and score vs oracle/bow_ref.py -- bit-exact"""
     import bow_ref
     par, leaf, desc, w = synth.synthetic_vocabulary(6, 5, 91)
-    vp = tmp_path / "voc.txt"
-    synth.write_vocabulary_text(vp, 6, 5, scoring, weighting, par, leaf, desc, w)
-    ref = bow_ref.Vocabulary.load_text(vp)
+    vp = tmp_path / f"voc.{fmt}"
+    if fmt == "bin":
+        synth.write_vocabulary_binary(vp, 6, 5, scoring, weighting, par, leaf, desc, w)
+        ref = bow_ref.Vocabulary.load_binary(vp)
+    else:
+        synth.write_vocabulary_text(vp, 6, 5, scoring, weighting, par, leaf, desc, w)
+        ref = bow_ref.Vocabulary.load_text(vp)
     rng = np.random.default_rng(4)
     leaves = desc[leaf == 1]
     d1 = leaves[rng.integers(0, len(leaves), 500)] ^ (rng.uniform(size=(500, 32)) < 0.04).astype(np.uint8)

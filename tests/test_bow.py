@@ -33,6 +33,35 @@ def test_oracle_loader_roundtrip_and_trailing_newline(tmp_path):
     assert v2.weight[-1] == 0.0 and not v2.desc[-1].any() and v2.n_words == v.n_words
 
 
+def test_oracle_binary_loader_last_record_twice(tmp_path):
+    """loadFromBinaryFile (TemplatedVocabulary.h:1477-1522): the eof loop
+    processes the last record a second time; weights are the file's floats."""
+    par, leaf, desc, w = _voc_arrays(3, 3, 1)
+    p = tmp_path / "voc.bin"
+    synth.write_vocabulary_binary(p, 3, 3, 2, 1, par, leaf, desc, w)
+    v = bow_ref.Vocabulary.load_binary(p)
+    ref = bow_ref.Vocabulary.from_arrays(3, 3, 2, 1, par, leaf, desc, np.float32(w).astype(np.float64))
+    n = len(ref.parent)
+    assert (v.k, v.L, v.scoring, v.weighting) == (3, 3, 2, 1)
+    assert len(v.parent) == n + 1 and v.parent[:n] == ref.parent and v.weight[:n] == ref.weight
+    assert v.parent[n] == ref.parent[n - 1] and v.children[ref.parent[n - 1]][-2:] == [n - 1, n]
+    assert np.array_equal(v.desc[n], ref.desc[n - 1]) and v.n_words == ref.n_words + 1 == 28
+    # the duplicate never wins the strict minimum: words of the text-format tree
+    feats = np.random.default_rng(3).integers(0, 256, (200, 32), dtype=np.uint8)
+    feats[:50] = desc[len(par) - 1]
+    assert v.transform(feats, 1)[:3] == ref.transform(feats, 1)[:3]
+    # a file cut inside the last record: its prefix overwrites the previous record's
+    raw = open(p, "rb").read()
+    p2 = tmp_path / "cut.bin"
+    open(p2, "wb").write(raw[:-20])
+    v2 = bow_ref.Vocabulary.load_binary(p2)
+    # 21 bytes of the last record: parent + 17 descriptor bytes, the rest from the one before
+    assert len(v2.parent) == n + 1 and v2.parent[n - 1] == ref.parent[n - 1]
+    assert np.array_equal(v2.desc[n - 1][:17], ref.desc[n - 1][:17])
+    assert np.array_equal(v2.desc[n - 1][17:], ref.desc[n - 2][17:]) and v2.weight[n - 1] == ref.weight[n - 2]
+    assert v2.parent[n] == 0 and all(n not in c for c in v2.children)  # m_nodes[nb_nodes]: default, unattached
+
+
 def test_oracle_transform_structure():
     par, leaf, desc, w = _voc_arrays(5, 4, 2)
     v = bow_ref.Vocabulary.from_arrays(5, 4, 0, 0, par, leaf, desc, w)
@@ -98,6 +127,42 @@ def test_gpu_vocabulary_text_loader(tmp_path):
         np.testing.assert_array_equal(gw, rw)
         np.testing.assert_array_equal(gn, rn)
         np.testing.assert_array_equal(gwt, np.array(rwt))
+
+
+@pytest.mark.gpu
+def test_gpu_vocabulary_binary_loader(tmp_path):
+    import bow
+    import orbgpu
+    par, leaf, desc, w = _voc_arrays(5, 4, 9)
+    for scoring, weighting in ((0, 0), (1, 3), (5, 1)):
+        p = tmp_path / f"v{scoring}{weighting}.bin"
+        synth.write_vocabulary_binary(p, 5, 4, scoring, weighting, par, leaf, desc, w)
+        gv = bow.Vocabulary.load_binary(p)
+        ref = bow_ref.Vocabulary.load_binary(p)
+        info = gv.info()
+        assert (info.k, info.L, info.scoring, info.weighting) == (5, 4, scoring, weighting)
+        assert info.n_nodes == len(ref.parent) == len(par) + 2 and info.n_words == ref.n_words
+        feats = np.random.default_rng(scoring).integers(0, 256, (500, 32), dtype=np.uint8)
+        feats[:200] = desc[leaf == 1][np.random.default_rng(1).integers(0, int(leaf.sum()), 200)]
+        feats[200:230] = desc[len(par) - 1]  # the twice-read last leaf
+        words, nodes, weights, fv, bowv = gv.transform(feats, 2)
+        rw, rn, rwt, rfv, rbow = ref.transform(feats, 2)
+        np.testing.assert_array_equal(words, rw)
+        np.testing.assert_array_equal(nodes, rn)
+        np.testing.assert_array_equal(weights, np.array(rwt))
+        assert list(fv) == list(rfv) and all(np.array_equal(fv[n_], rfv[n_]) for n_ in fv)
+        assert list(bowv) == list(rbow)
+        np.testing.assert_array_equal(np.array(list(bowv.values())), np.array(list(rbow.values())))
+    # malformed files fail loudly (the reference reads garbage there)
+    raw = open(tmp_path / "v00.bin", "rb").read()
+    bad = {"short": raw[:20], "ksize": raw[:8] + np.array([25, 4, 0, 0], "<i4").tobytes() + raw[24:],
+           "recsize": raw[:4] + np.array([40], "<u4").tobytes() + raw[8:],
+           "count": np.array([5], "<u4").tobytes() + raw[4:]}
+    for name, data in bad.items():
+        q = tmp_path / f"bad_{name}.bin"
+        open(q, "wb").write(data)
+        with pytest.raises(orbgpu.OrbGpuError):
+            bow.Vocabulary.load_binary(q)
 
 
 @pytest.mark.gpu
