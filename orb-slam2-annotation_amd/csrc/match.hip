@@ -94,7 +94,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     __shared__ float s_px[kMaxK0], s_py[kMaxK0], s_ang1[kMaxK0];  // F1: vbPrevMatched, angle
     __shared__ uint32_t s_top[kMaxK0][kTopK];
     __shared__ int s_ncand[kMaxK0];          // candidates in the window (-1: window off the grid)
-    __shared__ signed char s_bin[kMaxK0];    // rotation bin pushed for i1, or -1
+    __shared__ short s_cj[kMaxK0];           // F2 index i1 was matched to when the loop reached it, or -1
     __shared__ int s_hist[kHL];
     __shared__ int s_nm;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     }
     for (int i = tid; i < n10; i += kMatchThreads) {
         s_m12[i] = -1;
-        s_bin[i] = -1;
+        s_cj[i] = -1;
         s_px[i] = prev ? prev[2 * i] : K1[i].x;
         s_py[i] = prev ? prev[2 * i + 1] : K1[i].y;
         s_ang1[i] = K1[i].angle;
@@ -195,86 +195,119 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     }
     __syncthreads();
 
-    // phase 2: the sequential query loop (wave 0; wave-uniform control)
+    // phase 2: the sequential query loop (wave 0; wave-uniform control).  The
+    // lists of 64 queries at a time are read into lanes and taken from there
+    // with readlane, so a query costs one LDS round trip (vMatchedDistance of
+    // its listed candidates) plus the commit; the rotation bins are computed
+    // after the loop from the F2 index each query was matched to when the
+    // loop reached it (the reference pushes i1 into rotHist at that moment,
+    // and a later steal does not remove it), in parallel.
     if (wave == 0) {
-        const float factor =
-            (flags & ORBGPU_MATCH_ANNOTATED_HISTO) ? __fdiv_rn(1.0f, (float)kHL) : __fdiv_rn((float)kHL, 360.0f);
-        for (int i1 = 0; i1 < n10; ++i1) {
-            const int ncand = s_ncand[i1];
-            if (ncand <= 0) continue;  // window off the grid, or no candidate in it
-            uint32_t best = 0xFFFFFFFFu;
-            int best2 = 0x7FFFFFFF;
-            bool have2 = false;
-            const int nk = min(ncand, kTopK);
-            for (int k = 0; k < nk; ++k) {
-                const uint32_t key = s_top[i1][k];
-                const int dist = key_dist(key), j = key_j(key);
-                if (s_mdist[j] <= dist) continue;
-                if (best == 0xFFFFFFFFu) {
-                    best = key;
-                } else {
-                    best2 = dist;
-                    have2 = true;
-                    break;
-                }
+        for (int base = 0; base < n10; base += 64) {
+            const int qi = base + lane;
+            int l_nc = 0;
+            uint32_t l_top[kTopK];
+#pragma unroll
+            for (int k = 0; k < kTopK; ++k) l_top[k] = 0xFFFFFFFFu;
+            if (qi < n10) {
+                l_nc = s_ncand[qi];
+#pragma unroll
+                for (int k = 0; k < kTopK; ++k) l_top[k] = s_top[qi][k];
             }
-            if (!have2 && ncand > kTopK) {
-                // the list ran out: exact re-scan against the live state
-                const float x = s_px[i1], y = s_py[i1];
-                int cx0, cx1, cy0, cy1;
-                cell_range(x, y, cx0, cx1, cy0, cy1);
-                const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D1 + (size_t)i1 * 32);
-                const unsigned long long q0 = d[0], q1 = d[1], q2 = d[2], q3 = d[3];
-                unsigned long long lbest = ~0ull;
-                int second = 0x7FFFFFFF;
-                for (int j = lane; j < n20; j += 64) {
-                    int cell;
-                    if (!in_window(j, x, y, cx0, cx1, cy0, cy1, cell)) continue;
-                    const int dist = __popcll(q0 ^ s_d2[j][0]) + __popcll(q1 ^ s_d2[j][1]) +
-                                     __popcll(q2 ^ s_d2[j][2]) + __popcll(q3 ^ s_d2[j][3]);
-                    if (s_mdist[j] <= dist) continue;
-                    const unsigned long long key = ((unsigned long long)dist << 32) | ((unsigned)cell << 16) | (unsigned)j;
-                    if (key < lbest) {
-                        if (lbest != ~0ull) second = min(second, (int)(lbest >> 32));
-                        lbest = key;
+            const int cnt = min(64, n10 - base);
+            for (int u = 0; u < cnt; ++u) {
+                const int i1 = base + u;
+                const int ncand = __builtin_amdgcn_readlane(l_nc, u);
+                if (ncand <= 0) continue;  // window off the grid, or no candidate in it
+                uint32_t key[kTopK];
+                int md[kTopK];
+#pragma unroll
+                for (int k = 0; k < kTopK; ++k) key[k] = __builtin_amdgcn_readlane(l_top[k], u);
+#pragma unroll
+                for (int k = 0; k < kTopK; ++k) md[k] = key[k] != 0xFFFFFFFFu ? s_mdist[key_j(key[k])] : 0;
+                uint32_t best = 0xFFFFFFFFu;
+                int best2 = 0x7FFFFFFF;
+                bool have2 = false;
+                const int nk = min(ncand, kTopK);
+#pragma unroll
+                for (int k = 0; k < kTopK; ++k) {
+                    if (k >= nk || have2) continue;
+                    const int dist = key_dist(key[k]);
+                    if (md[k] <= dist) continue;
+                    if (best == 0xFFFFFFFFu) {
+                        best = key[k];
                     } else {
-                        second = min(second, dist);
+                        best2 = dist;
+                        have2 = true;
                     }
                 }
-                const unsigned long long wbest = wave_min_u64(lbest);
-                const int contrib = lbest == wbest ? second : (lbest == ~0ull ? 0x7FFFFFFF : (int)(lbest >> 32));
-                best2 = wave_min_i(contrib);
-                best = wbest == ~0ull ? 0xFFFFFFFFu
-                                      : cand_key((int)(wbest >> 32), (int)((wbest >> 16) & 0xFFFF), (int)(wbest & 0xFFFF));
-            }
-            if (best == 0xFFFFFFFFu) continue;  // no usable candidate
-            const int bestDist = key_dist(best);
-            const int bidx = key_j(best);
-            if (bestDist <= kThLow && (float)bestDist < __fmul_rn((float)best2, nnratio)) {
-                if (lane == 0) {
-                    const int prev21 = s_m21[bidx];
-                    if (prev21 >= 0) s_m12[prev21] = -1;
-                    s_m12[i1] = bidx;
-                    s_m21[bidx] = i1;
-                    s_mdist[bidx] = bestDist;
-                    if (flags & ORBGPU_MATCH_CHECK_ORI) {
-                        float rot = __fsub_rn(s_ang1[i1], K2[bidx].angle);
-                        if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
-                        int bin = (int)roundf(__fmul_rn(rot, factor));
-                        if (bin == kHL) bin = 0;
-                        s_bin[i1] = (signed char)bin;
-                        s_hist[bin] += 1;
+                if (!have2 && ncand > kTopK) {
+                    // the list ran out: exact re-scan against the live state
+                    const float x = s_px[i1], y = s_py[i1];
+                    int cx0, cx1, cy0, cy1;
+                    cell_range(x, y, cx0, cx1, cy0, cy1);
+                    const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D1 + (size_t)i1 * 32);
+                    const unsigned long long q0 = d[0], q1 = d[1], q2 = d[2], q3 = d[3];
+                    unsigned long long lbest = ~0ull;
+                    int second = 0x7FFFFFFF;
+                    for (int j = lane; j < n20; j += 64) {
+                        int cell;
+                        if (!in_window(j, x, y, cx0, cx1, cy0, cy1, cell)) continue;
+                        const int dist = __popcll(q0 ^ s_d2[j][0]) + __popcll(q1 ^ s_d2[j][1]) +
+                                         __popcll(q2 ^ s_d2[j][2]) + __popcll(q3 ^ s_d2[j][3]);
+                        if (s_mdist[j] <= dist) continue;
+                        const unsigned long long k64 = ((unsigned long long)dist << 32) | ((unsigned)cell << 16) | (unsigned)j;
+                        if (k64 < lbest) {
+                            if (lbest != ~0ull) second = min(second, (int)(lbest >> 32));
+                            lbest = k64;
+                        } else {
+                            second = min(second, dist);
+                        }
                     }
+                    const unsigned long long wbest = wave_min_u64(lbest);
+                    const int contrib = lbest == wbest ? second : (lbest == ~0ull ? 0x7FFFFFFF : (int)(lbest >> 32));
+                    best2 = wave_min_i(contrib);
+                    best = wbest == ~0ull ? 0xFFFFFFFFu
+                                          : cand_key((int)(wbest >> 32), (int)((wbest >> 16) & 0xFFFF), (int)(wbest & 0xFFFF));
                 }
-                // wave-local LDS ordering for the next query's reads
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                if (best == 0xFFFFFFFFu) continue;  // no usable candidate
+                const int bestDist = key_dist(best);
+                const int bidx = key_j(best);
+                if (bestDist <= kThLow && (float)bestDist < __fmul_rn((float)best2, nnratio)) {
+                    if (lane == 0) {
+                        const int prev21 = s_m21[bidx];
+                        if (prev21 >= 0) s_m12[prev21] = -1;
+                        s_m12[i1] = bidx;
+                        s_m21[bidx] = i1;
+                        s_mdist[bidx] = bestDist;
+                        s_cj[i1] = (short)bidx;
+                    }
+                    // wave-local LDS ordering for the next query's reads
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                }
             }
         }
     }
     __syncthreads();
     if (flags & ORBGPU_MATCH_CHECK_ORI) {
+        // rotHist (ORBmatcher.cpp:541-552): one entry per query matched when the loop reached it
+        const float factor =
+            (flags & ORBGPU_MATCH_ANNOTATED_HISTO) ? __fdiv_rn(1.0f, (float)kHL) : __fdiv_rn((float)kHL, 360.0f);
+        for (int i = tid; i < n10; i += kMatchThreads) {
+            const int j = s_cj[i];
+            int bin = -1;
+            if (j >= 0) {
+                float rot = __fsub_rn(s_ang1[i], K2[j].angle);
+                if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+                bin = (int)roundf(__fmul_rn(rot, factor));
+                if (bin == kHL) bin = 0;
+                atomicAdd(&s_hist[bin], 1);
+            }
+            s_cj[i] = (short)bin;
+        }
+        __syncthreads();
         // ComputeThreeMaxima (ORBmatcher.cpp:1792-1833), then cull other bins
         int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
         for (int i = 0; i < kHL; ++i) {
@@ -286,7 +319,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
         if ((float)max2 < __fmul_rn(0.1f, (float)max1)) { ind2 = -1; ind3 = -1; }
         else if ((float)max3 < __fmul_rn(0.1f, (float)max1)) ind3 = -1;
         for (int i = tid; i < n10; i += kMatchThreads) {
-            const int bin = s_bin[i];
+            const int bin = s_cj[i];
             if (bin >= 0 && bin != ind1 && bin != ind2 && bin != ind3) s_m12[i] = -1;
         }
         __syncthreads();
