@@ -817,3 +817,31 @@ def loop_burst_scene(n_queries: int, n_cand: int, leaves: np.ndarray, n_kp: int 
                           "outlier_dst": odst})
     return {"desc": desc, "angle": angle, "octave": octave, "valid": valid, "mp_world": mp, "Tcw": Tcw, "K": K,
             "sigma2": sig2, "n_queries": n_queries, "n_cand": n_cand, "truth": truth}
+
+
+def mappoint_scenario(n_points: int, seed: int, max_obs: int = 40, bad_frac: float = 0.15, flip: float = 0.06):
+    """Points with CSR observations for ComputeDistinctiveDescriptors /
+    UpdateNormalAndDepth: each point's descriptors are noisy copies of one
+    base descriptor (a few outliers); camera centres around the point; sizes
+    0, 1, 2 and up to max_obs observations; some keyframes bad."""
+    rng = np.random.default_rng(seed)
+    counts = rng.integers(0, max_obs + 1, n_points)
+    counts[: min(n_points, 4)] = [0, 1, 2, 3][: min(n_points, 4)]
+    off = np.zeros(n_points + 1, np.int32)
+    off[1:] = np.cumsum(counts)
+    n_obs = int(off[-1])
+    base = rng.integers(0, 256, (n_points, 32), dtype=np.uint8)
+    owner = np.repeat(np.arange(n_points), counts)
+    bits = (rng.uniform(size=(n_obs, 256)) < flip).astype(np.uint8)
+    desc = base[owner] ^ np.packbits(bits, axis=1)
+    outl = rng.uniform(size=n_obs) < 0.1
+    desc[outl] = rng.integers(0, 256, (int(outl.sum()), 32), dtype=np.uint8)
+    valid = (rng.uniform(size=n_obs) >= bad_frac).astype(np.uint8)
+    pos = rng.normal(0, 5, (n_points, 3)).astype(np.float32)
+    obs_Ow = (pos[owner] + rng.normal(0, 3, (n_obs, 3))).astype(np.float32)
+    ref_Ow = (pos + rng.normal(0, 3, (n_points, 3))).astype(np.float32)
+    sf = (1.2 ** np.arange(8)).astype(np.float32)
+    level_scale = sf[rng.integers(0, 8, n_points)]
+    max_scale = np.full(n_points, sf[7], np.float32)
+    return dict(offsets=off, desc=desc, valid=valid, pos=pos, obs_Ow=obs_Ow, ref_Ow=ref_Ow,
+                level_scale=level_scale, max_scale=max_scale)
