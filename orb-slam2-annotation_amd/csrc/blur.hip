@@ -24,10 +24,6 @@ using namespace blurdev;
 // and are clamped after reflection)
 __device__ inline int reflect101(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
 
-#ifndef BLUR_PROBE
-#define BLUR_PROBE 0  // diagnostic builds only: bit 0 = no stores in interior strips
-#endif
-
 // Interior strip (columns x0-3 .. x0+6 need no reflection): rows [y0, y1)
 // in groups of 7.  Row slot u of a group is consumed and immediately
 // refilled with the row 7 ahead, so 7 rows of loads are in flight and the
@@ -42,15 +38,9 @@ __device__ __forceinline__ void blur_strip_interior(const uint8_t* __restrict__ 
         const int r = min(reflect101(yy, H), H - 1);
         const uint8_t* row = base + __umul24((uint32_t)r, sp);
         Raw3 R;
-#if BLUR_PROBE & 2
-        R.a = (uint32_t)(uintptr_t)row * 0x9E3779B1u;  // timing probe: no loads
-        R.b = R.a ^ 0x5bd1e995u;
-        R.c = R.a + 0x1b873593u;
-#else
         R.a = *reinterpret_cast<const uint32_t*>(row - 4);
         R.b = *reinterpret_cast<const uint32_t*>(row);
         R.c = *reinterpret_cast<const uint32_t*>(row + 4);
-#endif
         return R;
     };
     f32x2 wl[7], wh[7];  // row-pass window: slot (y - y0 + i) % 7 holds row y - 3 + i
@@ -68,11 +58,7 @@ __device__ __forceinline__ void blur_strip_interior(const uint8_t* __restrict__ 
                                       wl[(u + 5) % 7], wl[(u + 6) % 7]);
             const f32x2 hi = col_pass(wh[u % 7], wh[(u + 1) % 7], wh[(u + 2) % 7], wh[(u + 3) % 7], wh[(u + 4) % 7],
                                       wh[(u + 5) % 7], wh[(u + 6) % 7]);
-#if BLUR_PROBE & 1
-            if (y + u < y1 && pack4(lo, hi, simd) == 0x12345678u) *reinterpret_cast<uint32_t*>(dst) = 0;  // timing probe: no stores
-#else
             if (y + u < y1) *reinterpret_cast<uint32_t*>(dst + __umul24((uint32_t)(y + u), dp) + x0) = pack4(lo, hi, simd);
-#endif
         }
     }
 }
@@ -110,10 +96,7 @@ __device__ __noinline__ void blur_strip_edge(const uint8_t* __restrict__ src, ui
 // Walking down the strip it keeps the last 7 row-pass results (as floats)
 // in registers -- the window rotates statically (the row loop is unrolled
 // by 7) -- so every input row is read once per strip (+6 halo rows).
-#ifndef BLUR_WAVES_PER_EU
-#define BLUR_WAVES_PER_EU 1
-#endif
-__global__ __launch_bounds__(256, BLUR_WAVES_PER_EU) void blur_levels_kernel(Geom g, int items_frame, int items_total,
+__global__ __launch_bounds__(256) void blur_levels_kernel(Geom g, int items_frame, int items_total,
                                                           const uint8_t* __restrict__ img0, size_t row0,
                                                           size_t frame0, const uint8_t* __restrict__ pyr,
                                                           uint8_t* __restrict__ blur) {
