@@ -96,18 +96,34 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
     const int lpr = dw > 32 ? 64 : 32;
     const int rsub = lpr == 32 ? lane >> 5 : 0, col = lane & (lpr - 1);
     const int rstep = 64 / lpr;
-    // Two passes per iteration: all ten compass loads are issued before
-    // either pass is evaluated (rows past the region read the rest of the
-    // wave's LDS area and are masked).
-    auto compass = [&](const uint8_t* p, int t) {
-        const int v = p[0];
-        const int c0 = p[3 * P], c4 = p[3], c8 = p[-3 * P], c12 = p[-3];
-        // two adjacent compass points both darker than v - t <=> the smallest
-        // pairwise max is; both brighter than v + t <=> the largest pairwise
-        // min is (VALU min/max instead of eight lane masks combined on the SALU)
-        const int dark = min(min(max(c0, c4), max(c4, c8)), min(max(c8, c12), max(c12, c0)));
-        const int bright = max(max(min(c0, c4), min(c4, c8)), max(min(c8, c12), min(c12, c0)));
-        return (dark < v - t) | (bright > v + t);
+    // Two passes per iteration, evaluated together: the lane's two pixels
+    // (rows r0 and r1 of one column) are the two halves of packed u16 values,
+    // so every min/max/subtract below is one packed op for both (rows past
+    // the region read the rest of the wave's LDS area and are masked).
+    //   two adjacent compass points both darker than v - t <=> the smallest
+    //   pairwise max is; both brighter than v + t <=> the largest pairwise min
+    //   is; dark < v - t <=> sat(v - dark) > t, bright > v + t <=> sat(bright - v) > t
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    auto compass2 = [&](const uint8_t* p, const uint8_t* q, int t, bool& pass0, bool& pass1) {
+        auto ld = [&](int o) {
+            u16x2 r;
+            r.x = p[o];
+            r.y = q[o];
+            return r;
+        };
+        const u16x2 v = ld(0), c0 = ld(3 * P), c4 = ld(3), c8 = ld(-3 * P), c12 = ld(-3);
+        const u16x2 dark = __builtin_elementwise_min(
+            __builtin_elementwise_min(__builtin_elementwise_max(c0, c4), __builtin_elementwise_max(c4, c8)),
+            __builtin_elementwise_min(__builtin_elementwise_max(c8, c12), __builtin_elementwise_max(c12, c0)));
+        const u16x2 bright = __builtin_elementwise_max(
+            __builtin_elementwise_max(__builtin_elementwise_min(c0, c4), __builtin_elementwise_min(c4, c8)),
+            __builtin_elementwise_max(__builtin_elementwise_min(c8, c12), __builtin_elementwise_min(c12, c0)));
+        const u16x2 x = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, dark),
+                                                  __builtin_elementwise_sub_sat(bright, v));
+        const u16x2 tt = {(unsigned short)t, (unsigned short)t};
+        const u16x2 y = __builtin_elementwise_sub_sat(x, tt);  // nonzero <=> passes
+        pass0 = y.x != 0;
+        pass1 = y.y != 0;
     };
     auto below = [&](unsigned long long m) {  // set bits of m in lanes below this one
         return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -117,8 +133,10 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
     for (int rr = 0; rr < dh; rr += 2 * rstep) {
         const int r0 = rr + rsub, r1 = r0 + rstep;
         const int off0 = (3 + r0) * P + 3 + ox + col, off1 = off0 + rstep * P;
-        const bool pass0 = incol & (r0 < dh) & compass(T.win + off0, t);
-        const bool pass1 = incol & (r1 < dh) & compass(T.win + off1, t);
+        bool c0, c1;
+        compass2(T.win + off0, T.win + off1, t, c0, c1);
+        const bool pass0 = incol & (r0 < dh) & c0;
+        const bool pass1 = incol & (r1 < dh) & c1;
         const unsigned long long m0 = __ballot(pass0), m1 = __ballot(pass1);
         if (pass0) T.la[na + below(m0)] = (uint16_t)off0;
         na += __popcll(m0);
