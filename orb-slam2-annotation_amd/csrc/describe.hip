@@ -287,7 +287,8 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
             const float px = (float)c_pattern[4 * t + 2 * pp], py = (float)c_pattern[4 * t + 2 * pp + 1];
             const int ry = __float2int_rn(__fadd_rn(__fmul_rn(px, b), __fmul_rn(py, a)));
             const int rx = __float2int_rn(__fsub_rn(__fmul_rn(px, a), __fmul_rn(py, b)));
-            val[pp] = S.blur[(kBlurR + ry) * kBPitch + ob + kBlurR + rx];
+            // |ry|, |rx| <= 18: a 24-bit multiply-add (full rate), not v_mul_lo_u32
+            val[pp] = S.blur[__umul24((uint32_t)(kBlurR + ry), (uint32_t)kBPitch) + (uint32_t)(ob + kBlurR + rx)];
         }
         words[rnd] = __ballot(val[0] < val[1]);
     }
