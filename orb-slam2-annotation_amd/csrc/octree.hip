@@ -22,6 +22,7 @@
 // identical to the oracle.
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
+#include <algorithm>
 
 namespace orbgpu {
 
@@ -339,9 +340,17 @@ __global__ __launch_bounds__(kThreads) void octree_kernel(Geom g, const uint32_t
                                                           uint16_t* __restrict__ gknode,
                                                           uint32_t* __restrict__ oct_out,
                                                           int* __restrict__ oct_count, int* __restrict__ err,
-                                                          int kcap, int ncap, int* __restrict__ trace, int level0) {
+                                                          int* __restrict__ trace, OctreeGroup A, OctreeGroup B,
+                                                          int batch) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int l = level0 + (int)blockIdx.x, f = blockIdx.y;
+    // linear block index: group A's (frame, level) blocks first, then group B's, so B's
+    // short workgroups fill the slots of A's finished ones inside one launch
+    const int id = (int)blockIdx.x, na = A.nlev * batch;
+    const bool inA = id < na;
+    const OctreeGroup& G = inA ? A : B;
+    const int j = inA ? id : id - na;
+    const int f = j / G.nlev, l = G.level0 + (j - f * G.nlev);
+    const int kcap = G.kcap, ncap = G.ncap;
     const int tid = threadIdx.x;
     const LevelGeom& L = g.lv[l];
     const int ncells = L.ncols * L.nrows;
@@ -402,13 +411,24 @@ size_t octree_lds_bytes(const Geom& g, int kcap, int ncap) {
 hipError_t launch_octree(const Geom& g, int batch, const uint32_t* cand, const int* cell_counts,
                          uint32_t* gkeys, uint16_t* gknode, uint32_t* oct_out, int* oct_count,
                          int* err, const OctreeGroup* groups, int ngroups, int* trace, hipStream_t stream) {
+    // both level groups in one launch, LDS sized for the larger group: group B's short
+    // workgroups start as group A's finish instead of after the last of them (two
+    // launches: 0.278 ms per 512 frames, one: 0.184 ms)
+    if (ngroups == 2 && groups[0].nlev > 0 && groups[1].nlev > 0) {
+        const size_t lds = std::max(octree_lds_bytes(g, groups[0].kcap, groups[0].ncap),
+                                    octree_lds_bytes(g, groups[1].kcap, groups[1].ncap));
+        hipLaunchKernelGGL(octree_kernel, dim3((groups[0].nlev + groups[1].nlev) * batch), dim3(kThreads), lds,
+                           stream, g, cand, cell_counts, gkeys, gknode, oct_out, oct_count, err, trace, groups[0],
+                           groups[1], batch);
+        return hipGetLastError();
+    }
     // one launch per level group: the LDS (and so the workgroups per CU) sized for the group's levels
     for (int i = 0; i < ngroups; ++i) {
         const OctreeGroup& G = groups[i];
         if (G.nlev <= 0) continue;
         const size_t lds = octree_lds_bytes(g, G.kcap, G.ncap);
-        hipLaunchKernelGGL(octree_kernel, dim3(G.nlev, batch), dim3(kThreads), lds, stream, g, cand, cell_counts,
-                           gkeys, gknode, oct_out, oct_count, err, G.kcap, G.ncap, trace, G.level0);
+        hipLaunchKernelGGL(octree_kernel, dim3(G.nlev * batch), dim3(kThreads), lds, stream, g, cand, cell_counts,
+                           gkeys, gknode, oct_out, oct_count, err, trace, G, OctreeGroup{0, 0, 0, 0}, batch);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
