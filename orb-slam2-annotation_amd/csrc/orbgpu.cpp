@@ -143,6 +143,8 @@ struct orbgpu_extractor {
     int* d_oct_count = nullptr;
     int* d_err = nullptr;
     int* d_trace = nullptr;  // optional octree pass trace (debug API)
+    int* d_stereo_sad = nullptr;  // ComputeStereoMatches: accepted SAD per left keypoint (pairs x cap)
+    size_t stereo_sad_n = 0;
     // host-image path
     uint8_t* d_img = nullptr;
     size_t img_pitch = 0;
@@ -169,7 +171,7 @@ struct orbgpu_extractor {
 
     ~orbgpu_extractor() {
         void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_ent, d_pyr_tab, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
-                        d_oct_count, d_err, d_trace, d_img, d_single};
+                        d_oct_count, d_err, d_trace, d_stereo_sad, d_img, d_single};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
         if (h_single) (void)hipHostFree(h_single);
@@ -877,6 +879,15 @@ int orbgpu_stereo_matches_batch_device(orbgpu_extractor* e, const uint8_t* d_ima
     a.rr = (int)std::ceil(2.0f * e->scale[g.nlevels - 1]) + 1;
     a.uright = d_uright;
     a.depth = d_depth;
+    const size_t nsad = (size_t)npairs * kp_capacity;
+    if (nsad > e->stereo_sad_n) {
+        if (e->d_stereo_sad) ORB_HIP(hipFree(e->d_stereo_sad));
+        e->d_stereo_sad = nullptr;
+        e->stereo_sad_n = 0;
+        ORB_HIP(hipMalloc((void**)&e->d_stereo_sad, nsad * sizeof(int)));
+        e->stereo_sad_n = nsad;
+    }
+    a.sad = e->d_stereo_sad;
     if (stereo_lds_bytes(kp_capacity, g.lv[0].h) > 160 * 1024)
         return fail(ORBGPU_ERR_UNSUPPORTED, "stereo LDS tables exceed 160 KiB");
     ORB_HIP(launch_stereo(a, npairs, reinterpret_cast<hipStream_t>(stream)));

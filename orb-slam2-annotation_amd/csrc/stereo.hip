@@ -2,7 +2,9 @@
 // of rectified stereo pairs extracted by one orbgpu_extractor (left = frame
 // 2p, right = frame 2p+1 of the last batch extraction).
 //
-// One 1024-thread block per pair:
+// S 1024-thread blocks per pair (S chosen so the launch fills every CU; a
+// pair's left keypoints are dealt to its S blocks, wave w of block b taking
+// iL = 16 b + w + 16 S k):
 //  A. the right keypoints go to LDS with their row band [minr, maxr]
 //     (Frame.cpp:562-576: r = 2 * scale[octave], ceil/floor of y +- r) and
 //     are bucketed by floor(y) (CSR over the image rows);
@@ -13,16 +15,19 @@
 //     SAD search over 11 shifts on the keypoint's pyramid level (:656-691):
 //     lanes = (shift, window row) pairs, per-shift sums reduced in LDS;
 //     parabola fit, disparity and depth (:697-729) on lane 0;
-//  C. the median cut (:734-747): the (M/2)-th smallest SAD of the accepted
+//  C. (stereo_median_kernel, one block per pair, after all S blocks) the
+//     median cut (:734-747): the (M/2)-th smallest SAD of the accepted
 //     matches by a two-pass 8-bit radix select in LDS, then every match with
 //     SAD >= 1.5f*1.4f*median is reset to -1.
-// Results stay in LDS until C, so each output is written once.
+// A and B write uRight/depth and the accepted SAD (scratch) once per left
+// keypoint; C rewrites the rejected ones.
 //
 // Spec decisions where the reference is undefined: row-band
 // rows outside the image are skipped; a SAD window that would leave the
 // level makes the keypoint unmatched; no accepted match -> no cut.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "../../include/orbgpu.h"
@@ -46,23 +51,20 @@ __device__ __forceinline__ uint8_t px(const StereoArgs& a, int frame, int lvl, i
     return a.lvl_base[lvl][(size_t)frame * a.lvl_frame[lvl] + (size_t)y * a.lvl_pitch[lvl] + x];
 }
 
-__global__ __launch_bounds__(kStThreads) void stereo_kernel(StereoArgs a) {
+__global__ __launch_bounds__(kStThreads) void stereo_kernel(StereoArgs a, int S) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_mem[];
-    const int p = blockIdx.x;
+    const int p = blockIdx.x / S, sub = blockIdx.x - p * S;
     const int fl = 2 * p, fr = 2 * p + 1;
     const int N = a.counts[fl], Nr = a.counts[fr];
     const int H = a.lvl_h[0];
     const int cap = a.cap;
     // LDS carve (host: stereo_lds_bytes)
     float4* s_r = reinterpret_cast<float4*>(s_mem);                     // x, y, minr, maxr << 8 | octave (as int bits)
-    float* s_ur = reinterpret_cast<float*>(s_r + cap);                   // uRight
-    float* s_dp = s_ur + cap;                                            // depth
-    int* s_sad = reinterpret_cast<int*>(s_dp + cap);                     // accepted SAD or -1
-    int* s_cnt = s_sad + cap;                                            // H + 1 row starts
+    int* s_cnt = reinterpret_cast<int*>(s_r + cap);                      // H + 1 row starts
     int* s_cur = s_cnt + (H + 1);                                        // H fill cursors
     uint16_t* s_ent = reinterpret_cast<uint16_t*>(s_cur + H);            // cap entries
     int* s_scr = reinterpret_cast<int*>(s_ent + ((cap + 1) & ~1));      // per wave 128 SAD partials
-    int* s_hist = s_scr + kStWaves * 128;                                // 256 bins + 4 scalars
+    int* s_wsum = s_scr + kStWaves * 128;                                // row-scan wave totals
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const orbgpu_keypoint* kl = a.kps + (size_t)fl * cap;
     const orbgpu_keypoint* kr = a.kps + (size_t)fr * cap;
@@ -70,12 +72,17 @@ __global__ __launch_bounds__(kStThreads) void stereo_kernel(StereoArgs a) {
     const uint8_t* dr = a.desc + (size_t)fr * cap * 32;
 
     // A. right keypoints, row bands, buckets
+    float* g_ur = a.uright + (size_t)p * cap;
+    float* g_dp = a.depth + (size_t)p * cap;
+    int* g_sad = a.sad + (size_t)p * cap;
+    const int first = sub * kStWaves, stride = S * kStWaves;  // this block's left keypoints
     for (int i = tid; i <= H; i += kStThreads) s_cnt[i] = 0;
-    for (int i = tid; i < N; i += kStThreads) {
-        s_ur[i] = -1.f;
-        s_dp[i] = -1.f;
-        s_sad[i] = -1;
-    }
+    for (int i = first + wave; i < N; i += stride)
+        if (lane == 0) {
+            g_ur[i] = -1.f;
+            g_dp[i] = -1.f;
+            g_sad[i] = -1;
+        }
     __syncthreads();
     for (int i = tid; i < Nr; i += kStThreads) {
         const orbgpu_keypoint k = kr[i];
@@ -87,16 +94,38 @@ __global__ __launch_bounds__(kStThreads) void stereo_kernel(StereoArgs a) {
         atomicAdd(&s_cnt[row], 1);
     }
     __syncthreads();
-    if (tid == 0) {  // exclusive scan over the rows (H <= a few thousand; one pass)
-        int acc = 0;
-        for (int i = 0; i < H; ++i) {
-            const int c = s_cnt[i];
-            s_cnt[i] = acc;
-            s_cur[i] = acc;
-            acc += c;
+    // exclusive scan over the rows, 1024 rows per pass (wave scans + wave totals)
+    int carry = 0;
+    for (int base = 0; base < H; base += kStThreads) {
+        const int i = base + tid;
+        const int x = i < H ? s_cnt[i] : 0;
+        int v = x;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(v, o, 64);
+            if (lane >= o) v += y;
         }
-        s_cnt[H] = acc;
+        if (lane == 63) s_wsum[wave] = v;
+        __syncthreads();
+        if (tid == 0) {
+            int acc = 0;
+            for (int w = 0; w < kStWaves; ++w) {
+                const int t = s_wsum[w];
+                s_wsum[w] = acc;
+                acc += t;
+            }
+            s_wsum[kStWaves] = acc;
+        }
+        __syncthreads();
+        const int ex = carry + s_wsum[wave] + v - x;
+        if (i < H) {
+            s_cnt[i] = ex;
+            s_cur[i] = ex;
+        }
+        carry += s_wsum[kStWaves];
+        __syncthreads();
     }
+    if (tid == 0) s_cnt[H] = carry;
     __syncthreads();
     for (int i = tid; i < Nr; i += kStThreads) {
         const int row = min(max((int)s_r[i].y, 0), H - 1);
@@ -106,7 +135,7 @@ __global__ __launch_bounds__(kStThreads) void stereo_kernel(StereoArgs a) {
 
     // B. one wave per left keypoint
     int* scr = s_scr + wave * 128;
-    for (int iL = wave; iL < N; iL += kStWaves) {
+    for (int iL = first + wave; iL < N; iL += stride) {
         const orbgpu_keypoint k = kl[iL];
         const int lvl = k.octave;
         const float vL = k.y, uL = k.x;
@@ -196,74 +225,79 @@ __global__ __launch_bounds__(kStThreads) void stereo_kernel(StereoArgs a) {
                             disparity = 0.01f;
                             bestuR = (float)__dsub_rn((double)uL, 0.01);
                         }
-                        s_dp[iL] = __fdiv_rn(a.bf, disparity);
-                        s_ur[iL] = bestuR;
-                        s_sad[iL] = bestSad;
+                        g_dp[iL] = __fdiv_rn(a.bf, disparity);
+                        g_ur[iL] = bestuR;
+                        g_sad[iL] = bestSad;
                     }
                 }
             }
         }
     }
-    __syncthreads();
+}
 
-    // C. median cut: (M/2)-th smallest accepted SAD (< 2^16), radix select
-    int* s_tot = s_hist + 256;
-    for (int i = tid; i < 256; i += kStThreads) s_hist[i] = 0;
+// C. median cut (Frame.cpp:734-747) of pair p: (M/2)-th smallest accepted SAD
+// (< 2^16) by a two-pass 8-bit radix select, then every accepted match with
+// SAD >= 1.5f*1.4f*median is reset to -1.
+constexpr int kMedThreads = 256;
+
+__global__ __launch_bounds__(kMedThreads) void stereo_median_kernel(StereoArgs a) {
+    __shared__ int s_hist[256];
+    __shared__ int s_tot[4];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int N = a.counts[2 * p], cap = a.cap;
+    const int* sad = a.sad + (size_t)p * cap;
+    s_hist[tid] = 0;
     if (tid == 0) s_tot[0] = 0;
     __syncthreads();
-    for (int i = tid; i < N; i += kStThreads)
-        if (s_sad[i] >= 0) {
-            atomicAdd(&s_hist[(s_sad[i] >> 8) & 0xFF], 1);
-            atomicAdd(&s_tot[0], 1);
+    int m = 0;
+    for (int i = tid; i < N; i += kMedThreads)
+        if (sad[i] >= 0) {
+            atomicAdd(&s_hist[(sad[i] >> 8) & 0xFF], 1);
+            ++m;
         }
+    atomicAdd(&s_tot[0], m);
     __syncthreads();
     const int M = s_tot[0];
-    if (M > 0) {
-        if (tid == 0) {
-            int k = M / 2, acc = 0, b = 0;
-            for (; b < 256; ++b) {
-                if (acc + s_hist[b] > k) break;
-                acc += s_hist[b];
-            }
-            s_tot[1] = b;
-            s_tot[2] = k - acc;
+    if (M == 0) return;
+    if (tid == 0) {
+        int k = M / 2, acc = 0, b = 0;
+        for (; b < 256; ++b) {
+            if (acc + s_hist[b] > k) break;
+            acc += s_hist[b];
         }
-        __syncthreads();
-        const int hb = s_tot[1];
-        for (int i = tid; i < 256; i += kStThreads) s_hist[i] = 0;
-        __syncthreads();
-        for (int i = tid; i < N; i += kStThreads)
-            if (s_sad[i] >= 0 && ((s_sad[i] >> 8) & 0xFF) == hb) atomicAdd(&s_hist[s_sad[i] & 0xFF], 1);
-        __syncthreads();
-        if (tid == 0) {
-            int k = s_tot[2], acc = 0, b = 0;
-            for (; b < 256; ++b) {
-                if (acc + s_hist[b] > k) break;
-                acc += s_hist[b];
-            }
-            s_tot[3] = (hb << 8) | b;
+        s_tot[1] = b;
+        s_tot[2] = k - acc;
+    }
+    __syncthreads();
+    const int hb = s_tot[1];
+    s_hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < N; i += kMedThreads)
+        if (sad[i] >= 0 && ((sad[i] >> 8) & 0xFF) == hb) atomicAdd(&s_hist[sad[i] & 0xFF], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int k = s_tot[2], acc = 0, b = 0;
+        for (; b < 256; ++b) {
+            if (acc + s_hist[b] > k) break;
+            acc += s_hist[b];
         }
-        __syncthreads();
-        const float median = (float)s_tot[3];
-        const float th = __fmul_rn(1.5f * 1.4f, median);
-        for (int i = tid; i < N; i += kStThreads)
-            if (s_sad[i] >= 0 && !((float)s_sad[i] < th)) {
-                s_ur[i] = -1.f;
-                s_dp[i] = -1.f;
-            }
-        __syncthreads();
+        s_tot[3] = (hb << 8) | b;
     }
-    for (int i = tid; i < N; i += kStThreads) {
-        a.uright[(size_t)p * cap + i] = s_ur[i];
-        a.depth[(size_t)p * cap + i] = s_dp[i];
-    }
+    __syncthreads();
+    const float median = (float)s_tot[3];
+    const float th = __fmul_rn(1.5f * 1.4f, median);
+    for (int i = tid; i < N; i += kMedThreads)
+        if (sad[i] >= 0 && !((float)sad[i] < th)) {
+            a.uright[(size_t)p * cap + i] = -1.f;
+            a.depth[(size_t)p * cap + i] = -1.f;
+        }
 }
 
 }  // namespace
 
 size_t stereo_lds_bytes(int cap, int H) {
-    return (size_t)cap * 16 + (size_t)cap * 12 + (size_t)(2 * H + 1) * 4 + (size_t)((cap + 1) & ~1) * 2 +
-           (size_t)kStWaves * 128 * 4 + (256 + 4) * 4;
+    return (size_t)cap * 16 + (size_t)(2 * H + 1) * 4 + (size_t)((cap + 1) & ~1) * 2 + (size_t)kStWaves * 128 * 4 +
+           (kStWaves + 4) * 4;
 }
 
 hipError_t launch_stereo(const StereoArgs& a, int npairs, hipStream_t stream) {
@@ -272,7 +306,14 @@ hipError_t launch_stereo(const StereoArgs& a, int npairs, hipStream_t stream) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stereo_kernel),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(stereo_kernel, dim3(npairs), dim3(kStThreads), lds, stream, a);
+    // blocks per pair: at least two 1024-thread blocks per CU over the launch
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int S = std::min(8, std::max(1, (2 * ncu + npairs - 1) / npairs));
+    hipLaunchKernelGGL(stereo_kernel, dim3(npairs * S), dim3(kStThreads), lds, stream, a, S);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(stereo_median_kernel, dim3(npairs), dim3(kMedThreads), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -26,6 +26,7 @@ struct StereoArgs {
     int rr;        // rows scanned either side of vL: ceil(2 * max scale) + 1
     float* uright; // pair p: + p * cap
     float* depth;
+    int* sad;      // scratch: accepted SAD per left keypoint or -1 (pair p: + p * cap)
 };
 
 size_t stereo_lds_bytes(int cap, int H);
