@@ -270,10 +270,19 @@ __global__ __launch_bounds__(kThreads) void compute_sim3_kernel(
             const size_t o = (size_t)(c0 + c) * stride;
             const int N = c_n[c];
             int cnt = 0;
-            for (int i = lane; i < N; i += 64) {
-                const bool in = is_inlier(s_hyp[h], K1, K2, ws.X1 + 3 * (o + i), ws.X2 + 3 * (o + i), ws.e1[o + i],
-                                          ws.e2[o + i]);
-                cnt += __popcll(__ballot(in));
+            // four correspondences per lane in flight (one wave per SIMD here: the
+            // test's loads and FP64 chains are latency bound, so independent work
+            // is what hides them); indices past N are clamped and masked
+            for (int i0 = lane; i0 < N; i0 += 256) {
+                bool in[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = min(i0 + 64 * u, N - 1);
+                    in[u] = is_inlier(s_hyp[h], K1, K2, ws.X1 + 3 * (o + i), ws.X2 + 3 * (o + i), ws.e1[o + i],
+                                      ws.e2[o + i]);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) cnt += __popcll(__ballot(in[u] && i0 + 64 * u < N));
             }
             if (lane == 0) s_cnt[h] = cnt;
         }
