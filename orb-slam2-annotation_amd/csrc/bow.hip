@@ -265,23 +265,38 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
         for (int ia_ = a0; ia_ < a1; ++ia_) {
             const int ia = A.fv_features[ia_];
             if (!A.valid[ia]) continue;
-            const uint8_t* da = A.desc + 32 * (size_t)ia;
+            const ulonglong4 qa = *reinterpret_cast<const ulonglong4*>(A.desc + 32 * (size_t)ia);
             int best1 = 256, best2 = 256, bidx = -1;
-            for (int ib_ = b0; ib_ < b1; ++ib_) {
-                const int ib = B.fv_features[ib_];
-                if (mode == ORBGPU_BOW_KF_F) {
-                    if (match[ib] >= 0) continue;
-                } else {
-                    if ((s_used[ib >> 5] >> (ib & 31)) & 1u) continue;
-                    if (!B.valid[ib]) continue;
+            // the node's B features four at a time: their indices, skip flags and
+            // descriptors are loaded together (one memory round trip per four
+            // instead of a dependent chain per feature), then compared in the
+            // reference's order.  The skip state (match[] / vbMatched2) only
+            // changes after this loop, and only in this lane (nodes partition B).
+            for (int base = b0; base < b1; base += 4) {
+                int ibs[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) ibs[u] = B.fv_features[min(base + u, b1 - 1)];
+                bool skip[4];
+                ulonglong4 qb[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int ib = ibs[u];
+                    skip[u] = mode == ORBGPU_BOW_KF_F ? match[ib] >= 0
+                                                      : (((s_used[ib >> 5] >> (ib & 31)) & 1u) || !B.valid[ib]);
+                    qb[u] = *reinterpret_cast<const ulonglong4*>(B.desc + 32 * (size_t)ib);
                 }
-                const int dist = hamming32(da, B.desc + 32 * (size_t)ib);
-                if (dist < best1) {
-                    best2 = best1;
-                    best1 = dist;
-                    bidx = ib;
-                } else if (dist < best2) {
-                    best2 = dist;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (base + u >= b1 || skip[u]) continue;
+                    const int dist = __popcll(qa.x ^ qb[u].x) + __popcll(qa.y ^ qb[u].y) +
+                                     __popcll(qa.z ^ qb[u].z) + __popcll(qa.w ^ qb[u].w);
+                    if (dist < best1) {
+                        best2 = best1;
+                        best1 = dist;
+                        bidx = ibs[u];
+                    } else if (dist < best2) {
+                        best2 = dist;
+                    }
                 }
             }
             const bool pass = mode == ORBGPU_BOW_KF_F ? best1 <= kThLow : best1 < kThLow;
