@@ -35,12 +35,6 @@ namespace {
 constexpr int kMaxStride = 4096;
 constexpr int kHL = 30, kThLow = 50;
 
-__device__ inline int hamming32(const uint8_t* a, const uint8_t* b) {
-    const unsigned long long* x = reinterpret_cast<const unsigned long long*>(a);
-    const unsigned long long* y = reinterpret_cast<const unsigned long long*>(b);
-    return __popcll(x[0] ^ y[0]) + __popcll(x[1] ^ y[1]) + __popcll(x[2] ^ y[2]) + __popcll(x[3] ^ y[3]);
-}
-
 __global__ __launch_bounds__(256) void bow_transform_kernel(VocabDev V, int batch, const uint8_t* __restrict__ desc,
                                                             const int* __restrict__ counts, int stride, int levelsup,
                                                             int* __restrict__ word, int* __restrict__ node,
@@ -421,14 +415,32 @@ __global__ __launch_bounds__(256) void triangulation_kernel(const orbgpu_triangu
             const float lb = kp1.x * F[1] + kp1.y * F[4] + F[7];
             const float lc = kp1.x * F[2] + kp1.y * F[5] + F[8];
             const float den = la * la + lb * lb;
-            const uint8_t* d1 = A.desc + 32 * (size_t)idx1;
+            const ulonglong4 q1 = *reinterpret_cast<const ulonglong4*>(A.desc + 32 * (size_t)idx1);
             int bestDist = kThLow, bestIdx2 = -1;
-            for (int ib_ = b0; ib_ < b1; ++ib_) {
-                const int idx2 = B.fv_features[ib_];
-                if (((s_used[idx2 >> 5] >> (idx2 & 31)) & 1u) || !B.valid[idx2]) continue;
-                const bool stereo2 = P.u_right2 && P.u_right2[idx2] >= 0.0f;
+            // four candidates per memory round trip (as in search_by_bow_kernel), then
+            // the reference's tests in candidate order; vbMatched2 only changes after
+            // this loop, in this lane
+            for (int base = b0; base < b1; base += 4) {
+              int ids[4];
+              bool st2[4], skip[4];
+              ulonglong4 q2[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) ids[u] = B.fv_features[min(base + u, b1 - 1)];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                  const int id = ids[u];
+                  st2[u] = P.u_right2 && P.u_right2[id] >= 0.0f;
+                  skip[u] = ((s_used[id >> 5] >> (id & 31)) & 1u) || !B.valid[id];
+                  q2[u] = *reinterpret_cast<const ulonglong4*>(B.desc + 32 * (size_t)id);
+              }
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const int idx2 = ids[u];
+                if (base + u >= b1 || skip[u]) continue;
+                const bool stereo2 = st2[u];
                 if (P.only_stereo && !stereo2) continue;
-                const int dist = hamming32(d1, B.desc + 32 * (size_t)idx2);
+                const int dist = __popcll(q1.x ^ q2[u].x) + __popcll(q1.y ^ q2[u].y) + __popcll(q1.z ^ q2[u].z) +
+                                 __popcll(q1.w ^ q2[u].w);
                 if (dist > kThLow || dist > bestDist) continue;
                 const orbgpu_keypoint kp2 = P.kps2[idx2];
                 if (!stereo1 && !stereo2) {  // too close to the epipole: the point is too close to KF1
@@ -442,6 +454,7 @@ __global__ __launch_bounds__(256) void triangulation_kernel(const orbgpu_triangu
                     bestIdx2 = idx2;
                     bestDist = dist;
                 }
+              }
             }
             if (bestIdx2 < 0) continue;
             match[idx1] = bestIdx2;
