@@ -13,10 +13,16 @@ value = frames processed by all ranks / max-over-ranks wall time.
 The matcher runs on a second HIP stream one step behind: step k-1's
 SearchForInitialization starts when step k's FAST pass is done (never during
 the pyramid pass, which fills every CU) and overlaps step k's octree /
-describe (measured: after pyramid 196.9k, after FAST 198.2k, after octree
-194.5k frames/s; the extractor's
-stage-event hook, orbgpu_extractor_set_stage_event); the last step's match is
-issued before the timed region closes, so all K steps' work is inside it.
+describe (the extractor's stage-event hook, orbgpu_extractor_set_stage_event);
+the last step's match is issued before the timed region closes, so all K
+steps' work is inside it.
+
+Ranks.  `python3 bench.py --gpus N` with N > 1 and no WORLD_SIZE in the
+environment starts `python -m torch.distributed.run --nproc-per-node N`
+on this same command line as a CHILD process (the parent never touches the
+GPU) and exits with its status; under torchrun (the driver's own N > 1 form)
+each rank reads RANK / LOCAL_RANK / WORLD_SIZE and checks WORLD_SIZE == N.
+One process per GPU, RCCL ("nccl") process group.
 
 The frames are ONE stream (shard.py): at step s rank r owns
 global frames [(s*N + r)*B, +B) -- contiguous chunks; the chunk-boundary
@@ -25,6 +31,14 @@ pair across ranks is matched; every step's outputs are gathered to rank 0
 (send/recv, overlapped with the next step).  Both are inside the timed
 region.  The frames come from a pool of 4 steps per rank rendered up front
 (a fresh batch every step, > the 256 MB MALL).
+
+Stereo (--config euroc_stereo / kitti_stereo, and the `stereo_euroc_sharded`
+leg of the default line at every N): the unit is the L/R pair one stereo
+Frame is built from (src/Frame.cpp:84-98): each rank extracts the L and R
+images of its contiguous chunk of pairs in one batch and runs
+Frame::ComputeStereoMatches on them; the pair never straddles ranks, there is
+no cross-pair dependency, and every step's keypoints / descriptors / uRight /
+depth are gathered to rank 0.
 
 Also reported:
   * roofline: the pyramid pass (the HBM-bound stage named by BASELINE.json),
@@ -35,19 +49,29 @@ Also reported:
   * cpu_baseline: the oracle (a scalar C++ restatement, oracle/liborbref.so --
     NOT the reference's SIMD OpenCV code) on the host cores, rank 0 at N=1
     only, on a bounded sample;
-  * single_frame: the drop-in path (orbgpu_extract = ORBextractor::operator():
-    host image in, host keypoints/descriptors out, PCIe included), batch 1;
+  * single_frame / drop_in: the drop-in C++ classes timed as Tracking calls
+    them (tests/cpp/adapter_main --time);
   * other_geometries: the 1241x376 / 2000-feature mono stream with its own
-    pyramid roofline, and KITTI / EuRoC stereo pairs/s (extract L+R batched +
-    Frame::ComputeStereoMatches).
---config loopburst runs SURVEY config 5 instead (LoopClosing::ComputeSim3
-bursts: SearchByBoW(KF, KF) + Sim3Solver RANSAC) and reports KF pairs/s.
+    pyramid roofline, and KITTI / EuRoC stereo pairs/s;
+  * loop_burst: SURVEY config 5 (LoopClosing::ComputeSim3 bursts) on the
+    bench mix and two harder mixes, queries round-robin over the ranks.
+--config loopburst runs config 5 alone as the headline.
+
+--cpu-dry-run ENGINE.py (tests only): the same launcher, rank logic,
+sharding and gather over gloo on the CPU, with ENGINE.py providing the
+orbgpu surface (tests/dryrun_orbgpu.py wraps the CPU oracle as the checker);
+--dump DIR makes rank 0 write the gathered outputs of every step.
 """
 from __future__ import annotations
 
 import argparse
+import contextlib
+import importlib.util
 import json
 import os
+import socket
+import struct
+import subprocess
 import sys
 import threading
 import time
@@ -74,34 +98,125 @@ CONFIGS = {
                                "extract + SearchForInitialization(t-1,t)"),
     "euroc": (752, 480, 1200, "synthetic 752x480 mono stream, 1200 feat (EuRoC.yaml params), "
                               "extract + SearchForInitialization(t-1,t)"),
+    "euroc_stereo": (752, 480, 1200, "synthetic rectified 752x480 stereo stream, 1200 feat (EuRoC.yaml params), "
+                                     "per pair: extract L+R + Frame::ComputeStereoMatches, pairs sharded "
+                                     "per rank in contiguous chunks"),
+    "kitti_stereo": (1241, 376, 2000, "synthetic rectified 1241x376 stereo stream, 2000 feat (KITTI00-02.yaml), "
+                                      "per pair: extract L+R + Frame::ComputeStereoMatches, pairs sharded per "
+                                      "rank in contiguous chunks"),
     "loopburst": (None, None, 1000, "LoopClosing::ComputeSim3 bursts: 100 queries x 5 candidate keyframes "
                                     "(500 KF pairs, 1000 keypoints each, 40% true correspondences under a "
                                     "known Sim3, the rest geometric outliers), SearchByBoW(KF,KF) over a "
                                     "k=10 L=6 DBoW2 vocabulary + Sim3Solver(0.99,20,300) round-robin iterate(5)"),
 }
-STEREO = {  # width, height, nfeatures, Camera.bf, synthetic baseline px
-    "kitti": (1241, 376, 2000, 0.54 * 718.856, 30.0),   # Examples/Stereo/KITTI00-02.yaml
-    "euroc": (752, 480, 1200, 47.90639384423901, 18.0),  # Examples/Stereo/EuRoC.yaml
+STEREO = {  # config -> (Camera.bf, synthetic baseline px)
+    "kitti_stereo": (0.54 * 718.856, 30.0),           # Examples/Stereo/KITTI00-02.yaml
+    "euroc_stereo": (47.90639384423901, 18.0),        # Examples/Stereo/EuRoC.yaml
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=512, help="frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="frames (stereo: pairs) per GPU per step (default 512 mono640, 256 kitti, 128 stereo)")
     ap.add_argument("--config", default="mono640", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="bounded CPU-baseline budget per config")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip single_frame / other_geometries")
+    ap.add_argument("--no-extras", action="store_true", help="headline only (no extra legs)")
     ap.add_argument("--match-after", default="fast_cells", choices=["pyramid", "fast_cells", "octree"],
                     help="extraction stage of step k after which step k-1's match starts")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
-    return ap.parse_args()
+    ap.add_argument("--cpu-dry-run", default=None, metavar="ENGINE.py",
+                    help="tests only: gloo on the CPU with ENGINE.py standing in for orbgpu")
+    ap.add_argument("--dump", default=None, metavar="DIR", help="rank 0 writes every step's gathered outputs")
+    return ap.parse_args(argv)
 
 
 MATCH_AFTER = ["fast_cells"]  # set from --match-after
+
+
+# ---------------------------------------------------------------------------
+# launcher: one process per GPU
+# ---------------------------------------------------------------------------
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(n: int, argv) -> int:
+    """Run this command line under torchrun with n ranks as a child process
+    (never exec: the parent has not touched the GPU, but a child is the
+    pattern the GPU box allows everywhere) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(Path(__file__).resolve())] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+class _NullStream:
+    """CPU stand-in for a HIP stream (dry run)."""
+    cuda_stream = None
+
+    def wait_event(self, ev):
+        pass
+
+
+class _NullEvent:
+    def record(self, stream=None):
+        pass
+
+    def elapsed_time(self, other):
+        return 0.0
+
+
+class Dev:
+    """The rank's device: a GPU (HIP streams / events) or, for --cpu-dry-run,
+    the CPU with no-op streams and events."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.cuda = device.type == "cuda"
+
+    def stream(self, priority=0):
+        return torch.cuda.Stream(self.device, priority=priority) if self.cuda else _NullStream()
+
+    def current_stream(self):
+        return torch.cuda.current_stream(self.device) if self.cuda else _NullStream()
+
+    def event(self, timing=False):
+        return torch.cuda.Event(enable_timing=timing) if self.cuda else _NullEvent()
+
+    def synchronize(self):
+        if self.cuda:
+            torch.cuda.synchronize(self.device)
+
+    def use_stream(self, s):
+        return torch.cuda.stream(s) if self.cuda else contextlib.nullcontext()
+
+    def empty_cache(self):
+        if self.cuda:
+            torch.cuda.empty_cache()
+
+
+def load_engine(path):
+    """orbgpu (the HIP library; raises when liborbgpu.so or the GPU is
+    missing), or the dry-run stand-in a test names."""
+    if path is None:
+        import orbgpu
+        orbgpu.lib()
+        return orbgpu
+    spec = importlib.util.spec_from_file_location("orbgpu_dryrun_engine", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
 
 
 def pyramid_bytes_per_frame(level_sizes):
@@ -128,21 +243,48 @@ def _barrier(world):
         dist.barrier()
 
 
+class _Dumper:
+    """rank 0: collects gathered outputs per global unit (frame or pair)."""
+
+    def __init__(self, path, name):
+        self.path, self.name, self.rows = path, name, {}
+
+    def add(self, unit, **arrays):
+        self.rows[int(unit)] = {k: np.asarray(v) for k, v in arrays.items()}
+
+    def write(self):
+        if not self.path:
+            return
+        Path(self.path).mkdir(parents=True, exist_ok=True)
+        units = sorted(self.rows)
+        keys = sorted(self.rows[units[0]]) if units else []
+        out = {"units": np.array(units, np.int64)}
+        for k in keys:
+            out[k] = np.stack([self.rows[u][k] for u in units])
+        np.savez(Path(self.path) / f"{self.name}.npz", **out)
+
+
+# ---------------------------------------------------------------------------
+# mono stream: extract + SearchForInitialization(t-1, t)
+# ---------------------------------------------------------------------------
+
 class StreamBench:
     """Extract + SearchForInitialization over one sharded frame stream."""
 
-    def __init__(self, W, H, NF, B, rank, world, dev, stream):
-        import orbgpu
+    def __init__(self, og, D: Dev, W, H, NF, B, rank, world, stream, dump=None):
         import shard
         import synth
+        self.og, self.D = og, D
         self.W, self.H, self.NF, self.B, self.rank, self.world = W, H, NF, B, rank, world
+        dev = D.device
         self.dev, self.stream = dev, stream
         self.pitch = (W + 15) // 16 * 16
-        self.ex = orbgpu.Extractor(nfeatures=NF, width=W, height=H, max_batch=B)
+        self.ex = og.Extractor(nfeatures=NF, width=W, height=H, max_batch=B)
         cap = self.cap = self.ex.max_keypoints
         # pool: this rank's chunks of POOL_STEPS steps of the global stream
-        self.pool = [synth.torch_stream(B, W, H, device=dev, pitch=self.pitch, bounded=True,
-                                        t0=shard.chunk_frames(s, rank, world, B)[0]) for s in range(POOL_STEPS)]
+        self.pool_t0 = [shard.chunk_frames(s, rank, world, B)[0] for s in range(POOL_STEPS)]
+        self.pool = [synth.torch_stream(B, W, H, device=dev, pitch=self.pitch, bounded=True, t0=t0)
+                     for t0 in self.pool_t0]
         # slot 0 = the frame before this chunk (boundary exchange), slots 1..B this chunk
         self.sets = []
         for _ in range(2):  # two output sets: the gather of step k overlaps step k+1
@@ -155,37 +297,38 @@ class StreamBench:
         k0, d0, c0 = self.sets[0][0], self.sets[0][1], self.sets[0][2]
         self.bx = shard.BoundaryExchange(rank, world, [k0[0], d0[0], c0[0:1]])
         self.gather = shard.OwnerGather(rank, world, [k0[1:], d0[1:], c0[1:], self.sets[0][3], self.sets[0][4]])
-        self.flags = orbgpu.MATCH_CHECK_ORI
+        self.flags = og.MATCH_CHECK_ORI
         self.step_no = 0
+        self.dump = _Dumper(dump, f"mono_{W}x{H}") if (dump and rank == 0) else None
+        self.dump_all = bool(dump)
         # The matcher runs on its own stream, one step behind: SearchForInitialization of
         # step k-1 (a few hundred latency-bound blocks) starts once step k's FAST pass is
         # done (--match-after; never during the pyramid pass, which wants every CU).
         # The two output sets keep step k+1's extraction off the buffers step k-1's match
         # reads (it waits for that match).  run() flushes the last match inside the timed
         # region.
-        self.mstream = torch.cuda.Stream(dev)
-        self.ev_pyr = torch.cuda.Event()
+        self.mstream = D.stream()
+        self.ev_pyr = D.event()
         self.ex.set_stage_event(MATCH_AFTER[0], self.ev_pyr)
-        self.ev_ext = [torch.cuda.Event() for _ in range(2)]
+        self.ev_ext = [D.event() for _ in range(2)]
         self.ev_match = [None, None]
         self.pending = None  # (set index, timing events) of the step whose match is not issued yet
 
     def _match(self, si, after, ev=None):
-        import orbgpu
         kps_all, desc_all, counts_all, m12, nmatch = self.sets[si]
         ms = self.mstream
         ms.wait_event(after)
         if ev is not None:
             ev[0].record(ms)
-        orbgpu.search_for_initialization_batch(self.W, self.H, kps_all[:-1], desc_all[:-1], counts_all[:-1],
-                                               kps_all[1:], desc_all[1:], counts_all[1:], m12, nmatch,
-                                               flags=self.flags, stream=ms)
+        self.og.search_for_initialization_batch(self.W, self.H, kps_all[:-1], desc_all[:-1], counts_all[:-1],
+                                                kps_all[1:], desc_all[1:], counts_all[1:], m12, nmatch,
+                                                flags=self.flags, stream=ms)
         if ev is not None:
             ev[1].record(ms)
-        em = torch.cuda.Event()
+        em = self.D.event()
         em.record(ms)
         self.ev_match[si] = em
-        with torch.cuda.stream(ms):  # the gather (RCCL send/recv) is ordered after the match
+        with self.D.use_stream(ms):  # the gather (RCCL send/recv) is ordered after the match
             self.gather.start(si, [kps_all[1:], desc_all[1:], counts_all[1:], m12, nmatch])
 
     def step(self, ev=None):
@@ -195,18 +338,35 @@ class StreamBench:
         self.gather.finish(si)  # the set's previous transfer is done before it is rewritten
         if self.ev_match[si] is not None:  # ... and the match that read it (step k-2)
             st.wait_event(self.ev_match[si])
-        frames = self.pool[self.step_no % POOL_STEPS]
+        pidx = self.step_no % POOL_STEPS
+        frames = self.pool[pidx]
         self.ex.extract_batch(frames, kps_all[1:], desc_all[1:], counts_all[1:], stream=st, row_step=self.pitch,
                               frame_step=self.pitch * self.H)
-        prev = self.bx.exchange([kps_all[B], desc_all[B], counts_all[B:B + 1]])
-        kps_all[0].copy_(prev[0])
-        desc_all[0].copy_(prev[1])
-        counts_all[0:1].copy_(prev[2])
+        with self.D.use_stream(st):
+            prev = self.bx.exchange([kps_all[B], desc_all[B], counts_all[B:B + 1]])
+            kps_all[0].copy_(prev[0])
+            desc_all[0].copy_(prev[1])
+            counts_all[0:1].copy_(prev[2])
         self.ev_ext[si].record(st)
-        if self.pending is not None:  # step k-1's match, after step k's pyramid pass
+        if self.pending is not None:  # step k-1's match, after step k's FAST pass
             self._match(*self.pending[:1], self.ev_pyr, self.pending[1])
         self.pending = (si, ev)
+        if self.dump_all:  # test mode: finish the step and record what rank 0 received
+            self.flush()
+            self.gather.finish()
+            if self.dump is not None:
+                self._record(si, pidx)
         self.step_no += 1
+
+    def _record(self, si, pidx):
+        import shard
+        own = [t.cpu() for t in (self.sets[si][0][1:], self.sets[si][1][1:], self.sets[si][2][1:],
+                                 self.sets[si][3], self.sets[si][4])]
+        chunks = [(0, own)] + [(r + 1, [t.cpu() for t in ts]) for r, ts in enumerate(self.gather.received(si))]
+        for r, (k, d, c, m, n) in chunks:
+            for b, f in enumerate(shard.chunk_frames(pidx, r, self.world, self.B)):
+                cc = int(c[b])
+                self.dump.add(f, count=cc, kps=k[b].numpy(), desc=d[b].numpy(), nmatch=int(n[b]), m12=m[b].numpy())
 
     def flush(self):
         """issue the match of the last extracted step"""
@@ -216,29 +376,32 @@ class StreamBench:
             self.pending = None
 
     def run(self, warmup, steps):
+        D = self.D
         for _ in range(warmup):
             self.step()
         self.flush()
         self.gather.finish()
-        torch.cuda.synchronize(self.dev)
+        D.synchronize()
         self.ex.sync(self.stream)
         self.ex.profile(True)
         self.ex.stage_times(reset=True)
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        evs = [(D.event(True), D.event(True)) for _ in range(steps)]
         _barrier(self.world)
-        torch.cuda.synchronize(self.dev)
+        D.synchronize()
         t0 = time.perf_counter()
         for i in range(steps):
             self.step(evs[i])
         self.flush()
         self.gather.finish()
-        torch.cuda.synchronize(self.dev)
+        D.synchronize()
         elapsed = time.perf_counter() - t0
         elapsed, frames_total = aggregate(elapsed, self.B * steps, device=self.dev)
         _barrier(self.world)
         self.ex.sync(self.stream)
         stage_ms, nb = self.ex.stage_times(reset=True)
         self.ex.profile(False)
+        if self.dump is not None:
+            self.dump.write()
         per_step = {k: v / max(nb, 1) for k, v in stage_ms.items()}
         per_step["match"] = sum(a.elapsed_time(b) for a, b in evs) / steps
         pyr_bytes = pyramid_bytes_per_frame(self.ex.level_sizes) * self.B
@@ -247,7 +410,7 @@ class StreamBench:
         last = self.sets[(self.step_no - 1) % 2]
         return {"fps": frames_total / elapsed, "elapsed": elapsed, "per_step": per_step, "pyr_bytes": pyr_bytes,
                 "achieved": achieved, "keypoints": float(last[2][1:].float().mean().item()),
-                "matches": float(last[4].float().mean().item())}
+                "matches": float(last[4].float().mean().item()), "frames_total": frames_total}
 
     def parity_frame0(self):
         """pool frame 0 of this rank against the oracle (untimed)."""
@@ -263,110 +426,525 @@ class StreamBench:
             return f"error: {e}"
 
 
-def cpu_baseline(frames_np, W, H, nf, seconds):
-    """Oracle extract + match on host cores: one extractor per thread."""
+# ---------------------------------------------------------------------------
+# stereo stream: per pair extract L+R + ComputeStereoMatches, sharded by pair
+# ---------------------------------------------------------------------------
+
+class StereoBench:
+    """Stereo Frames (src/Frame.cpp:66-127) over one sharded pair stream: at
+    step s rank r owns pairs [(s*N + r)*P, +P); the L and R images of its
+    pairs are extracted in one batch (frames 2p, 2p+1) and
+    Frame::ComputeStereoMatches runs on them; outputs go to rank 0."""
+
+    def __init__(self, og, D: Dev, config, P, rank, world, stream, dump=None):
+        import shard
+        import synth
+        W, H, NF, _ = CONFIGS[config]
+        self.bf, base_px = STEREO[config]
+        self.og, self.D, self.config = og, D, config
+        self.W, self.H, self.NF, self.P, self.rank, self.world = W, H, NF, P, rank, world
+        dev = D.device
+        self.dev, self.stream = dev, stream
+        self.pitch = (W + 15) // 16 * 16
+        self.ex = og.Extractor(nfeatures=NF, width=W, height=H, max_batch=2 * P)
+        cap = self.cap = self.ex.max_keypoints
+        self.pool = [synth.torch_stereo_stream(P, W, H, base_px, device=dev, pitch=self.pitch,
+                                               t0=shard.chunk_frames(s, rank, world, P)[0])
+                     for s in range(POOL_STEPS)]
+        self.sets = []
+        for _ in range(2):
+            self.sets.append((torch.zeros((2 * P, cap, 7), dtype=torch.float32, device=dev),
+                              torch.zeros((2 * P, cap, 32), dtype=torch.uint8, device=dev),
+                              torch.zeros(2 * P, dtype=torch.int32, device=dev),
+                              torch.zeros((P, cap), dtype=torch.float32, device=dev),
+                              torch.zeros((P, cap), dtype=torch.float32, device=dev)))
+        self.gather = shard.OwnerGather(rank, world, list(self.sets[0]))
+        self.ev_done = [None, None]
+        self.step_no = 0
+        self.dump = _Dumper(dump, f"stereo_{W}x{H}") if (dump and rank == 0) else None
+        self.dump_all = bool(dump)
+
+    def step(self):
+        st = self.stream
+        si = self.step_no % 2
+        kps, desc, counts, ur, dp = self.sets[si]
+        self.gather.finish(si)
+        pidx = self.step_no % POOL_STEPS
+        imgs = self.pool[pidx]
+        self.ex.extract_batch(imgs, kps, desc, counts, stream=st, row_step=self.pitch, frame_step=self.pitch * self.H)
+        self.og.stereo_matches_batch(self.ex, imgs, self.P, kps, desc, counts, self.bf, 0.0, ur, dp, stream=st,
+                                     row_step=self.pitch, frame_step=self.pitch * self.H)
+        with self.D.use_stream(st):
+            self.gather.start(si, [kps, desc, counts, ur, dp])
+        if self.dump_all:
+            self.gather.finish()
+            if self.dump is not None:
+                self._record(si, pidx)
+        self.step_no += 1
+
+    def _record(self, si, pidx):
+        import shard
+        own = [t.cpu() for t in self.sets[si]]
+        chunks = [(0, own)] + [(r + 1, [t.cpu() for t in ts]) for r, ts in enumerate(self.gather.received(si))]
+        for r, (k, d, c, u, z) in chunks:
+            for p, pair in enumerate(shard.chunk_frames(pidx, r, self.world, self.P)):
+                self.dump.add(pair, count=c[2 * p:2 * p + 2].numpy(), kps=k[2 * p:2 * p + 2].numpy(),
+                              desc=d[2 * p:2 * p + 2].numpy(), uright=u[p].numpy(), depth=z[p].numpy())
+
+    def run(self, warmup, steps):
+        D = self.D
+        for _ in range(warmup):
+            self.step()
+        self.gather.finish()
+        D.synchronize()
+        _barrier(self.world)
+        D.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step()
+        self.gather.finish()
+        D.synchronize()
+        elapsed = time.perf_counter() - t0
+        elapsed, pairs_total = aggregate(elapsed, self.P * steps, device=self.dev)
+        _barrier(self.world)
+        if self.dump is not None:
+            self.dump.write()
+        kps, desc, counts, ur, dp = self.sets[(self.step_no - 1) % 2]
+        n = counts.cpu().numpy()
+        urh = ur.cpu().numpy()
+        with_depth = float(np.mean([(urh[p, :n[2 * p]] >= 0).mean() if n[2 * p] else 0.0 for p in range(self.P)]))
+        return {"pairs_per_s": pairs_total / elapsed, "elapsed": elapsed, "pairs_total": pairs_total,
+                "keypoints_per_frame": float(n.mean()), "left_keypoints_with_depth": with_depth}
+
+    def summary(self, r, steps):
+        return {"pairs_per_s": round(r["pairs_per_s"], 1), "ms_per_step": round(r["elapsed"] / steps * 1e3, 3),
+                "pairs_per_gpu_per_step": self.P, "n_gpus": self.world, "width": self.W, "height": self.H,
+                "nfeatures": self.NF, "keypoints_per_frame": round(r["keypoints_per_frame"], 1),
+                "left_keypoints_with_depth": round(r["left_keypoints_with_depth"], 3),
+                "workload": CONFIGS[self.config][3] + f" (bf {self.bf:.3f})",
+                "parallelism": f"contiguous pair chunks x{self.world}, L/R of a pair on one rank, "
+                               f"per-step gather to rank 0"}
+
+
+# ---------------------------------------------------------------------------
+# CPU baselines (oracle on the host cores; rank 0 at N=1 only)
+# ---------------------------------------------------------------------------
+
+def cpu_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(avail, share) if share > 0 else avail
+    return {"cpu_model": model, "host_cpus": os.cpu_count(), "cpus_available_to_process": avail,
+            "threads_used": max(1, threads)}
+
+
+def _timed_threads(fn, threads, seconds):
+    """fn(j, stop_at, out) per thread; returns (units, elapsed)."""
+    res = []
+    t0 = time.perf_counter()
+    stop = t0 + seconds
+    ths = [threading.Thread(target=fn, args=(j, stop, res)) for j in range(threads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    return sum(res), time.perf_counter() - t0
+
+
+def cpu_baseline_mono(frames_np, W, H, nf, seconds, info):
+    """Oracle extract + match (t-1, t) on host cores: one extractor per thread."""
     import orbref
 
-    def run(idx_iter, stop_at, out):
+    def run(j, stop_at, out, step=1):
         ex = orbref.Extractor(nfeatures=nf)
         prev = None
         n = 0
-        for i in idx_iter:
-            if time.perf_counter() > stop_at:
-                break
+        i = j
+        while time.perf_counter() < stop_at:
             k, d = ex.extract(frames_np[i % len(frames_np)])
             if prev is not None:
                 orbref.search_for_initialization(prev[0], prev[1], k, d, W, H)
             prev = (k, d)
             n += 1
+            i += step
         out.append(n)
 
-    t0 = time.perf_counter()
-    res1 = []
-    run(iter(range(10 ** 9)), t0 + seconds / 3, res1)
-    fps1 = res1[0] / (time.perf_counter() - t0)
-    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1, 16))
-    res = []
-    t0 = time.perf_counter()
-    stop = t0 + 2 * seconds / 3
-    ths = [threading.Thread(target=run, args=(iter(range(j, 10 ** 9, threads)), stop, res)) for j in range(threads)]
-    for t in ths:
-        t.start()
-    for t in ths:
-        t.join()
-    fpsN = sum(res) / (time.perf_counter() - t0)
-    return {"value": round(fpsN, 2), "unit": "frames/s", "cores": threads, "kind": "port",
-            "single_thread_value": round(fps1, 2), "single_thread_ms_per_frame": round(1e3 / fps1, 2),
+    n1, e1 = _timed_threads(run, 1, seconds / 3)
+    T = info["threads_used"]
+    nN, eN = _timed_threads(lambda j, s, o: run(j, s, o, T), T, 2 * seconds / 3)
+    return {"value": round(nN / eN, 2), "unit": "frames/s", "cores": T, "kind": "port",
+            "single_thread_value": round(n1 / e1, 2), "single_thread_ms_per_frame": round(1e3 * e1 / max(n1, 1), 2),
+            "cpu_model": info["cpu_model"], "host_cpus": info["host_cpus"],
+            "cpus_available_to_process": info["cpus_available_to_process"],
             "note": "scalar C++ restatement of the reference's arithmetic (oracle/orbref.cpp: full corner score on "
                     "every pixel, no SIMD); the reference itself uses OpenCV 2.4's SSE FAST/resize/blur and would "
-                    "be faster per core, so the GPU/CPU ratio overstates the gap",
+                    "be faster per core. cores = the process's CPU share on the GPU box (all CPUs it may use)",
             "sample": f"oracle extract+match on {len(frames_np)} distinct synthetic {W}x{H} frames, "
-                      f"~{seconds:.0f}s bounded ({res1[0]} frames on 1 thread, {sum(res)} on {threads})"}
+                      f"~{seconds:.0f}s bounded ({n1} frames on 1 thread, {nN} on {T})"}
 
 
-def single_frame(W, H, NF, frame_np, reps=200):
-    """orbgpu_extract latency: the ORBextractor::operator() drop-in path of
-    Frame's constructor (host image -> pinned staging -> H2D, extraction,
-    one D2H of keypoints + descriptors, one sync)."""
-    import orbgpu
-    ex = orbgpu.Extractor(nfeatures=NF, width=W, height=H, max_batch=1)
-    for _ in range(10):
-        ex.extract(frame_np)
-    ts = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        ex.extract(frame_np)
-        ts.append(time.perf_counter() - t0)
-    ts = np.array(ts) * 1e3
-    return {"median_ms": round(float(np.median(ts)), 4), "mean_ms": round(float(ts.mean()), 4),
-            "p90_ms": round(float(np.percentile(ts, 90)), 4), "reps": reps,
-            "path": "orbgpu_extract: host image in, host cv::KeyPoint-layout keypoints + N x 32 descriptors out, "
-                    "PCIe copies included, batch 1"}
-
-
-def stereo_throughput(name, dev, pairs=128, steps=10, warmup=2):
-    """KITTI / EuRoC stereo: extract L+R batched + Frame::ComputeStereoMatches."""
-    import orbgpu
+def cpu_baseline_stereo(config, seconds, info):
+    """Oracle stereo Frame (extract L, R + ComputeStereoMatches, C++) on host cores."""
+    import orbref
     import synth
-    W, H, NF, BF, BASE = STEREO[name]
-    pitch = (W + 15) // 16 * 16
-    base = synth.base_texture(0x5E7)
-    distinct = 16
-    host = np.zeros((2 * distinct, H, pitch), np.uint8)
-    for i in range(distinct):
-        host[2 * i, :, :W] = synth.render_frame(base, i, W, H, 11)
-        host[2 * i + 1, :, :W] = synth.render_frame(base, i, W, H, 12, BASE)
-    reps = (pairs + distinct - 1) // distinct
-    imgs = torch.from_numpy(np.concatenate([host] * reps)[: 2 * pairs]).to(dev).contiguous()
-    ex = orbgpu.Extractor(nfeatures=NF, width=W, height=H, max_batch=2 * pairs)
-    cap = ex.max_keypoints
-    kps = torch.zeros((2 * pairs, cap, 7), dtype=torch.float32, device=dev)
-    desc = torch.zeros((2 * pairs, cap, 32), dtype=torch.uint8, device=dev)
-    counts = torch.zeros(2 * pairs, dtype=torch.int32, device=dev)
-    ur = torch.zeros((pairs, cap), dtype=torch.float32, device=dev)
-    dp = torch.zeros((pairs, cap), dtype=torch.float32, device=dev)
-    st = torch.cuda.current_stream(dev)
+    W, H, NF, _ = CONFIGS[config]
+    bf, base_px = STEREO[config]
+    pairs = synth.stereo_stream(4, W, H, 0x5E7, base_px)
 
-    def step():
-        ex.extract_batch(imgs, kps, desc, counts, stream=st)
-        orbgpu.stereo_matches_batch(ex, imgs, pairs, kps, desc, counts, BF, 0.0, ur, dp, stream=st)
+    def run(j, stop_at, out, step=1):
+        ex = [orbref.Extractor(nfeatures=NF), orbref.Extractor(nfeatures=NF)]
+        n, i = 0, j
+        while time.perf_counter() < stop_at:
+            lr = pairs[i % len(pairs)]
+            orbref.stereo_frame(ex[0], ex[1], lr[0], lr[1], bf)
+            n += 1
+            i += step
+        out.append(n)
 
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    torch.cuda.synchronize(dev)
-    el = time.perf_counter() - t0
-    n = counts.cpu().numpy()
-    urh = ur.cpu().numpy()
-    depth = float(np.mean([(urh[p, : n[2 * p]] >= 0).mean() for p in range(pairs)]))
-    return {"pairs_per_s": round(pairs * steps / el, 1), "ms_per_step": round(el / steps * 1e3, 3),
-            "pairs_per_step": pairs, "width": W, "height": H, "nfeatures": NF,
-            "keypoints_per_frame": round(float(n.mean()), 1), "left_keypoints_with_depth": round(depth, 3),
-            "workload": f"synthetic rectified {W}x{H} pairs (16 distinct, tiled), extract L+R in one batch + "
-                        f"ComputeStereoMatches (bf {BF:.3f})"}
+    n1, e1 = _timed_threads(run, 1, seconds / 3)
+    T = info["threads_used"]
+    nN, eN = _timed_threads(lambda j, s, o: run(j, s, o, T), T, 2 * seconds / 3)
+    return {"value": round(nN / eN, 2), "unit": "pairs/s", "cores": T, "kind": "port",
+            "single_thread_value": round(n1 / e1, 2), "single_thread_ms_per_pair": round(1e3 * e1 / max(n1, 1), 2),
+            "sample": f"oracle stereo Frame (extract L + R, ComputeStereoMatches; oracle/orbref.cpp) on 4 synthetic "
+                      f"{W}x{H} pairs, ~{seconds:.0f}s bounded ({n1} pairs on 1 thread, {nN} on {T})"}
+
+
+def cpu_baseline_mono_geometry(config, seconds, info):
+    W, H, NF, _ = CONFIGS[config]
+    import synth
+    frames = synth.mono_stream(6, W, H)
+    r = cpu_baseline_mono(frames, W, H, NF, seconds, info)
+    return {k: r[k] for k in ("value", "unit", "cores", "kind", "single_thread_value", "single_thread_ms_per_frame",
+                              "sample")}
+
+
+# ---------------------------------------------------------------------------
+# drop-in latency (the C++ classes, as Tracking calls them)
+# ---------------------------------------------------------------------------
+
+class DropIn:
+    """The drop-in C++ classes timed as the reference's threads call them:
+    tests/cpp/adapter_main (the include/orbslam2_amd/ headers over
+    liborbgpu.so) with ADAPTER_REPS / ADAPTER_TIME_LOG, at per-frame sizes:
+      * ORBextractor::operator() on a 640x480 frame (Frame::ExtractORB), with
+        and without the mvImagePyramid host copy;
+      * ORBmatcher::SearchForInitialization (Tracking.cpp:769);
+      * the stereo Frame (two extractors on two threads + ComputeStereoMatches
+        on their HBM pyramids) at 752x480 / 1200 features;
+      * ORBmatcher::SearchByProjection(F, localMPs, th) (Tracking.cpp:1560,
+        ~2000 local MapPoints) and (F, LastFrame) (:1152);
+      * ORBmatcher::SearchByBoW(KF, F) (:990) and (KF1, KF2) (LoopClosing:311);
+      * PnPsolver::iterate(5) of a fresh solver (Relocalization, :1822);
+      * Initializer::Initialize (MonocularInitialization, :790).
+    The scenarios come from synth.py (FeatureVectors and isInFrustum flags
+    from the GPU library itself)."""
+
+    def __init__(self, workdir: Path, reps: int = 60):
+        self.dir, self.reps = workdir, reps
+        self.scen = {}
+
+    def _run(self, *args, timeout=300):
+        exe = ROOT / "tests" / "cpp" / "adapter_main"
+        env = dict(os.environ, ADAPTER_REPS=str(self.reps), ADAPTER_TIME_LOG=str(self.dir / "times.jsonl"))
+        r = subprocess.run([str(exe), *map(str, args)], capture_output=True, text=True, timeout=timeout, env=env)
+        if r.returncode != 0:
+            raise RuntimeError(f"adapter_main {args[0]}: rc {r.returncode}: {r.stderr[-400:]}")
+
+    def run(self):
+        sys.path.insert(0, str(ROOT))
+        import bow
+        import proj
+        import synth
+        from tools import adapter_io as aio
+        d = self.dir
+        d.mkdir(parents=True, exist_ok=True)
+        (d / "times.jsonl").unlink(missing_ok=True)
+        # extraction + SearchForInitialization (640x480, 1000 features)
+        fr = synth.mono_stream(2, 640, 480)
+        self.scen["mono"] = fr
+        for k in range(2):
+            (d / f"f{k}.raw").write_bytes(fr[k].tobytes())
+        self._run("extract", 640, 480, 1000, d / "f0.raw", d / "f1.raw", d / "extract.out")
+        # stereo Frame (EuRoC geometry)
+        bf = float(np.float32(STEREO["euroc_stereo"][0]))
+        st = synth.stereo_stream(1, 752, 480, 0x5E7, STEREO["euroc_stereo"][1])[0]
+        self.scen["stereo"] = (st, bf)
+        (d / "l.raw").write_bytes(st[0].tobytes())
+        (d / "r.raw").write_bytes(st[1].tobytes())
+        self._run("stereo", 752, 480, 1200, repr(bf), d / "l.raw", d / "r.raw", d / "stereo.out")
+        # SearchByProjection: local map (LOCAL, th 1 as Tracking with a recent relocalisation off)
+        tgt, pts = synth.projection_scenario(2000, 600, 91)
+        fl, tr, lv = proj.is_in_frustum(tgt, pts, 0.5)
+        pts_l = dict(pts, flags=fl, track=tr, track_level=lv)
+        self.scen["proj_local"] = (tgt, pts_l)
+        (d / "proj0.in").write_bytes(aio.proj_blob(1.0, dict(nnratio=0.8), tgt, pts_l, tgt["Tcw"]))
+        self._run("proj", 0, d / "proj0.in", d / "proj0.out")
+        tgt2, pts2 = synth.projection_scenario(1000, 400, 92)
+        last = np.asarray(tgt2["Tcw"], np.float32).copy()
+        last[:3, 3] += np.float32(0.05)
+        self.scen["proj_last"] = (tgt2, pts2, last)
+        (d / "proj2.in").write_bytes(aio.proj_blob(15.0, dict(check_ori=True, mono=True), tgt2, pts2, last))
+        self._run("proj", 2, d / "proj2.in", d / "proj2.out")
+        # SearchByBoW: 1000-feature frames over a k=10, L=5 vocabulary (GPU transform, levelsup 4)
+        par, leaf, vdesc, w = synth.synthetic_vocabulary_fast(10, 5, 7)
+        voc = bow.Vocabulary.from_arrays(10, 5, 0, 0, par, leaf, vdesc, w)
+        d1, a1, d2, a2 = synth.bow_frame_pair(vdesc[leaf == 1], 1000, 0.6, seed=41)
+        fv1, fv2 = voc.transform(d1, 4)[3], voc.transform(d2, 4)[3]
+        rng = np.random.default_rng(23)
+        s1 = rng.choice([0, 1, 1, 1, 1, 1, 1, 2], 1000).astype(np.uint8)
+        s2 = rng.choice([0, 1, 1, 1, 1, 1, 1, 2], 1000).astype(np.uint8)
+        self.scen["bow"] = (par, leaf, vdesc, w, d1, a1, s1, d2, a2, s2)
+        (d / "bow.in").write_bytes(aio.bow_blob(0.7, True, (d1, a1, s1, fv1), (d2, a2, s2, fv2)))
+        self._run("bow", d / "bow.in", d / "bow.out")
+        # PnPsolver: 300 correspondences, half inliers (Relocalization's SearchByBoW output size)
+        P = synth.pnp_problem(300, 0.5, seed=80)
+        self.scen["pnp"] = P
+        blob, _, _ = aio.pnp_frame(P, seed=1)
+        (d / "pnp.in").write_bytes(struct.pack("<I", 0) + blob)
+        self._run("pnp", d / "pnp.in", d / "pnp.out")
+        # Initializer: 1000 matches
+        kp1, kp2, m12 = aio.init_scene(1000, 3)
+        self.scen["init"] = (kp1, kp2, m12)
+        (d / "init.in").write_bytes(aio.init_blob(aio.K_TUM, kp1, kp2, m12))
+        self._run("init", d / "init.in", d / "init.out")
+        out = {}
+        for line in (d / "times.jsonl").read_text().splitlines():
+            r = json.loads(line)
+            out[r.pop("op")] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items()}
+        return out
+
+    def cpu_oracle(self, ops):
+        """Single-thread time of the oracle doing the same call on the same
+        scenario (C++ oracle where it exists, else the numpy/Python one)."""
+        import orbref
+        res = {}
+
+        def t(fn, n=3):
+            ts = []
+            for _ in range(n):
+                t0 = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t0)
+            return round(1e6 * float(np.median(ts)), 1)
+
+        fr = self.scen["mono"]
+        ex = orbref.Extractor(1000)
+        k0, d0 = ex.extract(fr[0])
+        k1, d1 = ex.extract(fr[1])
+        res["ORBextractor::operator()"] = (t(lambda: ex.extract(fr[1])), "C++ oracle (scalar)")
+        res["ORBmatcher::SearchForInitialization"] = (
+            t(lambda: orbref.search_for_initialization(k0, d0, k1, d1, 640, 480)), "C++ oracle")
+        st, bf = self.scen["stereo"]
+        eL, eR = orbref.Extractor(1200), orbref.Extractor(1200)
+        kl, dl, kr, dr, _, _ = orbref.stereo_frame(eL, eR, st[0], st[1], bf)
+        res["stereo Frame: ORBextractor L || R + ComputeStereoMatches"] = (
+            t(lambda: orbref.stereo_frame(eL, eR, st[0], st[1], bf)), "C++ oracle, L and R sequential")
+        res["ComputeStereoMatches"] = (t(lambda: orbref.stereo_matches(eL, eR, kl, dl, kr, dr, bf)), "C++ oracle")
+        import proj_ref
+        tgt, pts = self.scen["proj_local"]
+        res["ORBmatcher::SearchByProjection(F, vpLocalMapPoints, th)"] = (
+            t(lambda: proj_ref.search_by_projection(0, tgt, pts, 1.0, nnratio=0.8), 1), "Python oracle")
+        tgt2, pts2, last = self.scen["proj_last"]
+        res["ORBmatcher::SearchByProjection(F, LastFrame, th, bMono)"] = (
+            t(lambda: proj_ref.search_by_projection(2, tgt2, pts2, 15.0, check_ori=True, mono=True, last_Tcw=last),
+              1), "Python oracle")
+        import bow_ref
+        par, leaf, vdesc, w, d1_, a1, s1, d2_, a2, s2 = self.scen["bow"]
+        cv = orbref.Vocabulary(10, 5, par, leaf, vdesc, w)
+        res["ORBmatcher::SearchByBoW(KF1, KF2)"] = (
+            t(lambda: orbref.search_by_bow_kf_kf(cv, d1_, a1, s1 == 1, d2_, a2, s2 == 1, 0.7)),
+            "C++ oracle (includes the two BoW transforms)")
+        bv = bow_ref.Vocabulary.from_arrays(10, 5, 0, 0, par, leaf, vdesc, w)
+        f1, f2 = bv.transform(d1_, 4)[3], bv.transform(d2_, 4)[3]
+        res["ORBmatcher::SearchByBoW(KF, F)"] = (
+            t(lambda: bow_ref.search_by_bow(0, f1, d1_, a1, s1 == 1, f2, d2_, a2, np.ones(1000, bool), 0.7, True), 1),
+            "Python oracle")
+        import pnp_ref
+        P = self.scen["pnp"]
+        maxerr = (P["sigma2"] * np.float32(5.991)).astype(np.float32)
+        rng = np.random.default_rng(0)
+        smp = np.array([rng.choice(len(P["P2"]), 4, replace=False) for _ in range(5)])
+        res["PnPsolver::iterate(5)"] = (
+            t(lambda: pnp_ref.ransac_call(P["P3w"], P["P2"], maxerr, P["cam"], 150, 0, np.zeros(len(P["P2"]), bool),
+                                          smp), 1), "numpy oracle, 5 hypotheses")
+        return {op: {"cpu_oracle_single_thread_us": v[0], "cpu_oracle_kind": v[1]} for op, v in res.items()
+                if op in ops}
+
+
+def drop_in_latency(with_cpu=True):
+    import tempfile
+    with tempfile.TemporaryDirectory(prefix="orbgpu_dropin_") as td:
+        di = DropIn(Path(td))
+        try:
+            ops = di.run()
+        except Exception as e:  # report, never hide
+            return {"error": str(e)}
+        if with_cpu:
+            try:
+                for op, v in di.cpu_oracle(ops).items():
+                    ops[op].update(v)
+            except Exception as e:
+                ops["cpu_oracle_error"] = str(e)
+    return {"unit": "us per call (wall, steady_clock around the class member call, median of repetitions)",
+            "path": "tests/cpp/adapter_main: include/orbslam2_amd/*.h over liborbgpu.so, host inputs and outputs, "
+                    "per-thread stream / arena / pinned staging (no hipMalloc, hipFree or device-wide sync per call)",
+            "ops": ops}
+
+
+# ---------------------------------------------------------------------------
+# loop burst (SURVEY config 5)
+# ---------------------------------------------------------------------------
+
+LOOP_MIXES = {
+    # name: (inlier fractions per candidate slot, outlier fractions, fixed scale, description)
+    "bench": (0.4, 0.6, False, "40% true correspondences, the rest geometric outliers"),
+    "several_rounds": ([0.0, 0.0, 0.03, 0.4, 0.4], [0.0, 0.08, 0.05, 0.5, 0.5], False,
+                       "unrelated / false loop / weak / two true loops with 50% outliers"),
+    "false_loops": (0.0, [0.0, 0.06, 0.08, 0.1, 0.05], False,
+                    "false loops only: every solver runs to its maximum iterations, no Sim3 returned"),
+}
+
+
+class LoopLeg:
+    """ComputeSim3 bursts (src/LoopClosing.cpp:273-356): 100 queries x 5
+    candidates per mix, queries round-robin over the ranks."""
+
+    def __init__(self, rank, world, dev, nq_total=100, nc=5):
+        import bow
+        import synth
+        self.rank, self.world, self.dev, self.nq, self.nc = rank, world, dev, nq_total, nc
+        t_set = time.perf_counter()
+        self.voc_arrays = synth.synthetic_vocabulary_fast(10, 6, 0x70C)
+        p, l, d, w = self.voc_arrays
+        vpath = Path(os.environ.get("TMPDIR", "/tmp")) / f"orbgpu_voc_k10_L6_{os.getpid()}.txt"
+        synth.write_vocabulary_text_fast(vpath, 10, 6, 0, 0, p, l, d, w)
+        t_load = time.perf_counter()
+        self.voc = bow.Vocabulary.load_text(str(vpath))
+        self.t_load = time.perf_counter() - t_load
+        vpath.unlink()
+        self.t_voc = time.perf_counter() - t_set
+        self.scenes = {}
+
+    def scene(self, mix):
+        import synth
+        if mix not in self.scenes:
+            fr, ofr, fix, _ = LOOP_MIXES[mix]
+            p, l, d, w = self.voc_arrays
+            seed = {"bench": 55, "several_rounds": 56, "false_loops": 57}[mix]
+            self.scenes[mix] = synth.loop_burst_scene(self.nq, self.nc, d[l == 1], n_kp=1000, inlier_frac=fr,
+                                                      outlier_frac=ofr, seed=seed, fix_scale=fix)
+        return self.scenes[mix]
+
+    def run(self, mix, steps, warmup):
+        import loop
+        nq, nc, dev = self.nq, self.nc, self.dev
+        scene = self.scene(mix)
+        fix = LOOP_MIXES[mix][2]
+        my_q = list(range(self.rank, nq, self.world))
+        kf_ids = []
+        for q in my_q:
+            kf_ids += [q] + [nq + q * nc + c for c in range(nc)]
+        sel = np.array(kf_ids)
+        kfs = loop.Keyframes(scene["desc"][sel], scene["angle"][sel], scene["octave"][sel], scene["valid"][sel],
+                             scene["mp_world"][sel], scene["Tcw"][sel], scene["K"], scene["sigma2"], device=dev)
+        st = torch.cuda.current_stream(dev)
+        kfs.compute_bow(self.voc, stream=st)
+        queries = [(j * (1 + nc), [j * (1 + nc) + 1 + c for c in range(nc)], 1000 + q) for j, q in enumerate(my_q)]
+        lb = loop.LoopBurst(kfs, queries, fix_scale=fix)
+        for _ in range(warmup):
+            lb.step(st)
+        torch.cuda.synchronize(dev)
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+        _barrier(self.world)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            ev[i][0].record(st)
+            lb.search_by_bow(st)
+            ev[i][1].record(st)
+            lb.setup(st)
+            ev[i][2].record(st)
+            lb.compute_sim3(st)
+            ev[i][3].record(st)
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        elapsed, pairs_total = aggregate(elapsed, len(my_q) * nc * steps, device=dev)
+        stage = {k: sum(e[j].elapsed_time(e[j + 1]) for e in ev) / steps
+                 for j, k in enumerate(["search_by_bow", "sim3_setup", "compute_sim3"])}
+        res = lb.query_results()
+        states = lb.candidate_states()
+        n_kp = 1000
+        npairs = len(my_q) * nc
+        sbb_bytes = 2 * n_kp * (32 + 4 + 1 + 4 + 4) + n_kp * 4
+        kern_bytes = {"search_by_bow": sbb_bytes * npairs,
+                      "sim3_setup": npairs * n_kp * (4 + 2 * (12 + 1 + 4)) + npairs * 300 * 36,
+                      "compute_sim3": sum(max(s.n, 0) for s in states) * 36}
+        dominant = max(stage, key=stage.get)
+        achieved = kern_bytes[dominant] / (stage[dominant] / 1e3) / 1e9
+        return {"kf_pairs_per_s": round(pairs_total / elapsed, 1), "ms_per_step": round(elapsed / steps * 1e3, 4),
+                "kf_pairs_per_step": pairs_total // steps, "mix": LOOP_MIXES[mix][3],
+                "stages_ms_per_step_rank0": {k: round(v, 4) for k, v in stage.items()},
+                "dominant_kernel": dominant,
+                "dominant_hbm_frac": round(achieved / HBM_PEAK_GBS, 5),
+                "queries_matched_rank0": int(sum(r.matched >= 0 for r in res)),
+                "mean_round_of_match_rank0": round(float(np.mean([r.round for r in res if r.matched >= 0] or [0])), 2),
+                "ransac_iterations_per_step_rank0": int(sum(r.hypotheses for r in res)),
+                "mean_searchbybow_matches": round(float(lb.nmatches.float().mean().item()), 1)}
+
+    def cpu_baseline(self, mix, seconds, info):
+        """The oracle pipeline in C++ (oracle/liborbref.so: DBoW2 transform,
+        SearchByBoW(KF,KF), Sim3Solver set-up and the round-robin iterate(5)
+        with host glibc rand()) over whole queries, 1 thread and all threads."""
+        import orbref
+        scene = self.scene(mix)
+        p, l, d, w = self.voc_arrays
+        voc = orbref.Vocabulary(10, 6, p, l, d, w)
+        nq, nc = self.nq, self.nc
+        fix = LOOP_MIXES[mix][2]
+
+        def run(j, stop_at, out, step=1):
+            n, q = 0, j
+            while time.perf_counter() < stop_at:
+                qq = q % nq
+                orbref.compute_sim3_query(voc, scene, qq, [nq + qq * nc + c for c in range(nc)], 1000 + qq, fix)
+                n += nc
+                q += step
+            out.append(n)
+
+        n1, e1 = _timed_threads(run, 1, seconds / 3)
+        T = info["threads_used"]
+        nN, eN = _timed_threads(lambda j, s, o: run(j, s, o, T), T, 2 * seconds / 3)
+        return {"value": round(nN / eN, 2), "unit": "KF pairs/s", "cores": T, "kind": "port",
+                "single_thread_value": round(n1 / e1, 2),
+                "sample": f"C++ oracle ComputeSim3 queries (BoW transform of the query and its {nc} candidates, "
+                          f"SearchByBoW(KF,KF), Sim3Solver set-up, round-robin iterate(5)), ~{seconds:.0f}s bounded "
+                          f"({n1} KF pairs on 1 thread, {nN} on {T}); rand() is process-global in glibc, so the "
+                          f"threads' draws interleave (timing only)"}
+
+
+def run_loop_leg(args, rank, world, dev, mixes, info=None):
+    leg = LoopLeg(rank, world, dev)
+    out = {"vocabulary": "k=10 L=6 (1,111,111 nodes), DBoW2 text format, loaded by orbgpu_vocabulary_load_text",
+           "setup_s": round(leg.t_voc, 2), "vocabulary_text_load_s": round(leg.t_load, 2)}
+    steps, warm = max(5, min(args.steps, 20)), 2
+    for mix in mixes:
+        out[mix] = leg.run(mix, steps, warm)
+    if info is not None:
+        for mix in mixes:
+            out[mix]["cpu_baseline"] = leg.cpu_baseline(mix, args.cpu_seconds / 2, info)
+    return out, leg
 
 
 def traffic_for(path, config, batch):
@@ -383,178 +961,84 @@ def traffic_for(path, config, batch):
     return None
 
 
-def run_loopburst(args, rank, world, dev):
-    """SURVEY §8d config 5 on the GPU; KF pairs/s."""
-    import bow
-    import loop
-    import synth
-    nq_total, nc = 100, 5
-    t_set = time.perf_counter()
-    p, l, d, w = synth.synthetic_vocabulary_fast(10, 6, 0x70C)
-    vpath = Path(os.environ.get("TMPDIR", "/tmp")) / f"orbgpu_voc_k10_L6_{os.getpid()}.txt"
-    synth.write_vocabulary_text_fast(vpath, 10, 6, 0, 0, p, l, d, w)
-    t_load = time.perf_counter()
-    voc = bow.Vocabulary.load_text(str(vpath))
-    t_load = time.perf_counter() - t_load
-    vpath.unlink()
-    my_q = list(range(rank, nq_total, world))  # queries round-robin over ranks
-    scene = synth.loop_burst_scene(nq_total, nc, d[l == 1], n_kp=1000, inlier_frac=0.4, outlier_frac=0.6, seed=55)
-    kf_ids = []
-    for q in my_q:
-        kf_ids += [q] + [nq_total + q * nc + c for c in range(nc)]
-    sel = np.array(kf_ids)
-    kfs = loop.Keyframes(scene["desc"][sel], scene["angle"][sel], scene["octave"][sel], scene["valid"][sel],
-                         scene["mp_world"][sel], scene["Tcw"][sel], scene["K"], scene["sigma2"], device=dev)
-    st = torch.cuda.current_stream(dev)
-    torch.cuda.synchronize(dev)
-    t_bow = time.perf_counter()
-    kfs.compute_bow(voc, stream=st)
-    torch.cuda.synchronize(dev)
-    t_bow = time.perf_counter() - t_bow
-    queries = [(j * (1 + nc), [j * (1 + nc) + 1 + c for c in range(nc)], 1000 + q) for j, q in enumerate(my_q)]
-    lb = loop.LoopBurst(kfs, queries)
-    setup_s = time.perf_counter() - t_set
-    for _ in range(args.warmup):
-        lb.step(st)
-    torch.cuda.synchronize(dev)
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
-    _barrier(world)
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(st)
-        lb.search_by_bow(st)
-        ev[i][1].record(st)
-        lb.setup(st)
-        ev[i][2].record(st)
-        lb.compute_sim3(st)
-        ev[i][3].record(st)
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    elapsed, pairs_total = aggregate(elapsed, len(my_q) * nc * args.steps, device=dev)
-    stage = {k: sum(e[j].elapsed_time(e[j + 1]) for e in ev) / args.steps
-             for j, k in enumerate(["search_by_bow", "sim3_setup", "compute_sim3"])}
-    res = lb.query_results()
-    states = lb.candidate_states()
+def common_line(args, world):
+    return {"n_gpus": world, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "data": "synthetic"}
+
+
+def main_loopburst(args, rank, world, dev):
+    info = cpu_info() if (world == 1 and not args.no_cpu_baseline and rank == 0) else None
+    legs, _ = run_loop_leg(args, rank, world, dev, ["bench", "several_rounds", "false_loops"], info)
     if rank != 0:
         return None
-    # algorithmic bytes of SearchByBoW per pair: both frames' descriptors,
-    # angles, MapPoint flags and FeatureVector CSR read once, matches written
-    n_kp = 1000
-    sbb_bytes = 2 * n_kp * (32 + 4 + 1 + 4 + 4) + n_kp * 4
-    dominant = max(stage, key=stage.get)
-    npairs = len(my_q) * nc
-    kern_bytes = {"search_by_bow": sbb_bytes * npairs,
-                  "sim3_setup": npairs * n_kp * (4 + 2 * (12 + 1 + 4)) + npairs * 300 * 36,
-                  "compute_sim3": sum(max(s.n, 0) for s in states) * 36}
-    achieved = kern_bytes[dominant] / (stage[dominant] / 1e3) / 1e9
-    line = {
-        "metric": "KF pairs/s LoopClosing::ComputeSim3 burst (SearchByBoW(KF,KF) + Sim3Solver RANSAC)",
-        "value": round(pairs_total / elapsed, 1), "unit": "KF pairs/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u8/f32/f64", "data": "synthetic",
-        "config": {"workload": CONFIGS["loopburst"][3], "config": "loopburst", "queries": nq_total,
-                   "candidates_per_query": nc, "kf_pairs_per_step": npairs * world,
-                   "parallelism": f"queries round-robin x{world}"},
-        "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                     "note": "latency-bound (sequential per-node merge walks / per-query RANSAC chain); the HBM "
-                             "fraction is reported for the record"},
-        "stages_ms_per_step": {k: round(v, 4) for k, v in stage.items()},
-        "queries_matched": int(sum(r.matched >= 0 for r in res)),
-        "mean_round_of_match": round(float(np.mean([r.round for r in res if r.matched >= 0] or [0])), 2),
-        "ransac_iterations_per_step": int(sum(r.hypotheses for r in res)),
-        "mean_searchbybow_matches": round(float(lb.nmatches.float().mean().item()), 1),
-        "setup_s": {"total": round(setup_s, 2), "vocabulary_text_load": round(t_load, 2),
-                    "keyframe_bow_transform": round(t_bow, 4)},
-    }
-    if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = loopburst_cpu_baseline(scene, p, l, d, w, nc, args.cpu_seconds)
+    b = legs["bench"]
+    line = {"metric": "KF pairs/s LoopClosing::ComputeSim3 burst (SearchByBoW(KF,KF) + Sim3Solver RANSAC)",
+            "value": b["kf_pairs_per_s"], "unit": "KF pairs/s", **common_line(args, world),
+            "ms_per_step": b["ms_per_step"], "dtype": "u8/f32/f64",
+            "config": {"workload": CONFIGS["loopburst"][3], "config": "loopburst", "queries": 100,
+                       "candidates_per_query": 5, "kf_pairs_per_step": b["kf_pairs_per_step"],
+                       "parallelism": f"queries round-robin x{world}"},
+            "roofline": {"bound": "hbm", "kernel": b["dominant_kernel"], "frac": b["dominant_hbm_frac"],
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
+                         "note": "latency-bound (sequential per-node merge walks / per-query RANSAC chain)"},
+            "mixes": legs}
+    if "cpu_baseline" in b:
+        line["cpu_baseline"] = b["cpu_baseline"]
     return line
 
 
-def loopburst_cpu_baseline(scene, p, l, d, w, nc, seconds):
-    """The oracle pipeline (oracle/loop_ref.py + bow_ref.py: Python/numpy
-    SearchByBoW, C++ Sim3 iterate) on one thread over whole queries."""
-    import bow_ref
-    import loop_ref
-    avoc = loop_ref.ArrayVocabulary(10, 6, 0, 0, p, l, d, w)
-    nq = scene["n_queries"]
-    t0 = time.perf_counter()
-    pairs = 0
-    q = 0
-    while time.perf_counter() - t0 < seconds and q < nq:
-        cur = q
-        fv1 = avoc.transform(scene["desc"][cur], 4)[3]
-        solvers = []
-        for c in range(nc):
-            kf = nq + q * nc + c
-            fv2 = avoc.transform(scene["desc"][kf], 4)[3]
-            nm, m12 = bow_ref.search_by_bow(1, fv1, scene["desc"][cur], scene["angle"][cur], scene["valid"][cur],
-                                            fv2, scene["desc"][kf], scene["angle"][kf], scene["valid"][kf],
-                                            nnratio=0.75, check_ori=True)
-            corr = loop_ref.sim3_setup(m12, scene["valid"][cur], scene["valid"][kf], scene["mp_world"][cur],
-                                       scene["mp_world"][kf], scene["Tcw"][cur], scene["Tcw"][kf],
-                                       scene["octave"][cur], scene["octave"][kf], scene["sigma2"])
-            solvers.append(loop_ref.Sim3SolverRef(corr, scene["K"], scene["K"], False) if nm >= 20 else None)
-            pairs += 1
-        loop_ref.compute_sim3(solvers, 1000 + q)
-        q += 1
-    el = time.perf_counter() - t0
-    return {"value": round(pairs / el, 2), "unit": "KF pairs/s", "cores": 1, "kind": "port",
-            "note": "Python/numpy SearchByBoW + C++ Sim3 iterate restatement (oracle/); the reference's C++ "
-                    "SearchByBoW would be faster per core",
-            "sample": f"{q} queries ({pairs} KF pairs, BoW transform of their keyframes included) in {el:.1f}s"}
-
-
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
-    if args.config == "loopburst":
-        line = run_loopburst(args, rank, world, dev)
-        if line is not None:
-            print(json.dumps(line), flush=True)
-        if world > 1:
-            import torch.distributed as dist
-            dist.destroy_process_group()
-        return
-
-    W, H, NF, desc_cfg = CONFIGS[args.config]
-    B = args.batch
-    MATCH_AFTER[0] = args.match_after
-    # extraction on a high-priority stream (the matcher's stream has the default, lower
-    # priority): when both have work ready, the extraction's workgroups dispatch first
-    stream = torch.cuda.Stream(dev, priority=-1)
-    torch.cuda.set_stream(stream)
-    sb = StreamBench(W, H, NF, B, rank, world, dev, stream)
-    parity = sb.parity_frame0() if rank == 0 else None
+def main_stereo(args, og, D, rank, world, stream):
+    P = args.batch or 128
+    sb = StereoBench(og, D, args.config, P, rank, world, stream, dump=args.dump)
     r = sb.run(args.warmup, args.steps)
     if rank != 0:
-        if world > 1:
-            import torch.distributed as dist
-            dist.destroy_process_group()
-        return
+        return None
+    W, H, NF, desc = CONFIGS[args.config]
+    line = {"metric": f"pairs/sec stereo Frame (extract L+R + ComputeStereoMatches, {W}x{H}, {NF} feat)",
+            "value": round(r["pairs_per_s"], 1), "unit": "pairs/s", **common_line(args, world),
+            "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 3), "dtype": "u8",
+            "config": {"workload": desc, "config": args.config, "pairs_per_gpu_per_step": P, "width": W, "height": H,
+                       "nfeatures": NF, "parallelism": sb.summary(r, args.steps)["parallelism"]},
+            "keypoints_per_frame": round(r["keypoints_per_frame"], 1),
+            "left_keypoints_with_depth": round(r["left_keypoints_with_depth"], 3)}
+    if D.cuda and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_stereo(args.config, args.cpu_seconds, cpu_info())
+    return line
+
+
+def main_mono(args, og, D, rank, world, stream):
+    W, H, NF, desc_cfg = CONFIGS[args.config]
+    B = args.batch or (512 if args.config == "mono640" else 256)
+    MATCH_AFTER[0] = args.match_after
+    sb = StreamBench(og, D, W, H, NF, B, rank, world, stream, dump=args.dump)
+    parity = sb.parity_frame0() if (rank == 0 and D.cuda) else None
+    r = sb.run(args.warmup, args.steps)
+    frame0 = sb.pool[0][0, :, :W].cpu().numpy() if rank == 0 else None
+    del sb
+    D.empty_cache()
+    extras = {}
+    if not args.no_extras and D.cuda:
+        # config 4: EuRoC stereo sharded over all ranks (every N)
+        esb = StereoBench(og, D, "euroc_stereo", 128, rank, world, stream)
+        er = esb.run(2, 10)
+        extras["stereo_euroc_sharded"] = esb.summary(er, 10)
+        del esb
+        D.empty_cache()
+        # config 5: loop-closure bursts, queries round-robin over all ranks
+        info = cpu_info() if (world == 1 and not args.no_cpu_baseline and rank == 0) else None
+        loop_legs, _ = run_loop_leg(args, rank, world, D.device, ["bench", "several_rounds", "false_loops"], info)
+        extras["loop_burst"] = loop_legs
+        D.empty_cache()
+    if rank != 0:
+        return None
     achieved = r["achieved"]
     line = {
         "metric": METRIC,
         "value": round(r["fps"], 1),
         "unit": "frames/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
+        **common_line(args, world),
         "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic",
         "config": {"workload": desc_cfg, "config": args.config, "frames_per_gpu_per_step": B,
                    "width": W, "height": H, "nfeatures": NF,
                    "parallelism": f"one stream in contiguous per-rank chunks x{world}, boundary frame send/recv, "
@@ -568,19 +1052,25 @@ def main():
         "keypoints_per_frame": round(r["keypoints"], 1),
         "matches_per_pair": round(r["matches"], 1),
         "parity_frame0_vs_oracle": parity,
+        "world_size_checked": world,
     }
-    frame0 = sb.pool[0][0, :, :W].cpu().numpy()
-    if world == 1 and not args.no_extras:
-        line["single_frame"] = single_frame(W, H, NF, frame0)
-        del sb
-        torch.cuda.empty_cache()
+    tr = line["roofline"]["traffic"]
+    if tr and r["per_step"].get("pyramid"):
+        line["roofline"]["traffic_frac"] = round(tr / (r["per_step"]["pyramid"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+    line.update(extras)
+    if world == 1 and not args.no_extras and D.cuda:
+        line["drop_in"] = drop_in_latency(with_cpu=not args.no_cpu_baseline)
+        ex_op = line["drop_in"].get("ops", {}).get("ORBextractor::operator()")
+        if ex_op:
+            line["single_frame"] = {"median_ms": round(ex_op["median_us"] / 1e3, 4),
+                                    "path": "ORB_SLAM2::ORBextractor::operator() (C++ drop-in class, 640x480, host "
+                                            "image in, keypoints + descriptors out, no host pyramid copy)"}
         other = {}
-        kw, kh, knf, _ = CONFIGS["kitti"]
-        kb = StreamBench(kw, kh, knf, 256, 0, 1, dev, stream)
+        kb = StreamBench(og, D, *CONFIGS["kitti"][:3], 256, 0, 1, stream)
         kr = kb.run(2, 10)
         other["mono1241x376"] = {
             "frames_per_s": round(kr["fps"], 1), "ms_per_step": round(kr["elapsed"] / 10 * 1e3, 3),
-            "frames_per_step": 256, "nfeatures": knf,
+            "frames_per_step": 256, "nfeatures": CONFIGS["kitti"][2],
             "pyramid_roofline": {"achieved": round(kr["achieved"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": round(kr["achieved"] / HBM_PEAK_GBS, 4),
                                  "algorithmic_bytes_per_step": kr["pyr_bytes"]},
@@ -588,19 +1078,70 @@ def main():
             "keypoints_per_frame": round(kr["keypoints"], 1), "matches_per_pair": round(kr["matches"], 1),
             "workload": CONFIGS["kitti"][3]}
         del kb
-        torch.cuda.empty_cache()
-        for name in ("kitti", "euroc"):
-            other[f"stereo_{name}"] = stereo_throughput(name, dev)
-            torch.cuda.empty_cache()
+        D.empty_cache()
+        ksb = StereoBench(og, D, "kitti_stereo", 128, 0, 1, stream)
+        other["stereo_kitti"] = ksb.summary(ksb.run(2, 10), 10)
+        del ksb
+        D.empty_cache()
         line["other_geometries"] = other
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and D.cuda:
         import synth
-        frames_np = np.stack([synth.torch_stream(1, W, H, device=dev, t0=t, bounded=True)[0].cpu().numpy()
+        info = cpu_info()
+        frames_np = np.stack([synth.torch_stream(1, W, H, device=D.device, t0=t, bounded=True)[0].cpu().numpy()
                               for t in range(24)])
-        line["cpu_baseline"] = cpu_baseline(frames_np, W, H, NF, args.cpu_seconds)
-        if "single_frame" in line:
-            line["single_frame"]["cpu_oracle_single_thread_ms"] = line["cpu_baseline"]["single_thread_ms_per_frame"]
-    print(json.dumps(line), flush=True)
+        line["cpu_baseline"] = cpu_baseline_mono(frames_np, W, H, NF, args.cpu_seconds, info)
+        if "other_geometries" in line:
+            og_ = line["other_geometries"]
+            og_["mono1241x376"]["cpu_baseline"] = cpu_baseline_mono_geometry("kitti", args.cpu_seconds / 2, info)
+            og_["stereo_kitti"]["cpu_baseline"] = cpu_baseline_stereo("kitti_stereo", args.cpu_seconds / 2, info)
+        if "stereo_euroc_sharded" in line:
+            line["stereo_euroc_sharded"]["cpu_baseline"] = cpu_baseline_stereo("euroc_stereo", args.cpu_seconds / 2,
+                                                                               info)
+    return line
+
+
+def main():
+    argv = sys.argv[1:]
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args.gpus, argv))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    dry = args.cpu_dry_run is not None
+    og = load_engine(args.cpu_dry_run)
+    if dry:
+        device = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    D = Dev(device)
+    if world > 1:
+        import torch.distributed as dist
+        if dry:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+    if args.config == "loopburst":
+        if dry:
+            raise SystemExit("--cpu-dry-run covers the frame and pair streams, not loopburst")
+        line = main_loopburst(args, rank, world, device)
+    else:
+        # extraction on a high-priority stream (the matcher's stream has the default, lower
+        # priority): when both have work ready, the extraction's workgroups dispatch first
+        stream = D.stream(priority=-1)
+        if D.cuda:
+            torch.cuda.set_stream(stream)
+        if args.config in STEREO:
+            line = main_stereo(args, og, D, rank, world, stream)
+        else:
+            line = main_mono(args, og, D, rank, world, stream)
+    if line is not None:
+        line["world_size_checked"] = world
+        print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -47,6 +47,12 @@ public:
         const std::vector<cv::KeyPoint>& k2 = CurrentFrame.mvKeysUn;
         const int n1 = (int)mvKeys1.size(), n2 = (int)k2.size();
         if ((int)vMatches12.size() != n1) throw std::invalid_argument("vMatches12 must have one entry per reference keypoint");
+        // Fewer than 8 matches: the reference's 8-point draws would index an empty vector
+        // (Initializer.cpp:104-115; Tracking only calls with >= 100 matches).  Return false with
+        // R21 / t21 / vP3D untouched rather than throw out of the tracking thread.
+        int nmatched = 0;
+        for (int i = 0; i < n1; ++i) nmatched += vMatches12[i] >= 0;
+        if (nmatched < 8) return false;
         std::vector<float> p1(2 * (size_t)n1), p2(2 * (size_t)n2);
         for (int i = 0; i < n1; ++i) {
             p1[2 * i] = mvKeys1[i].pt.x;

@@ -7,11 +7,16 @@
 // so Frame.cpp / Tracking.cpp compile unchanged against it.  Differences:
 //  * the GPU handle is created on the first frame (its geometry is fixed by
 //    the frame size) and re-created if the size changes;
-//  * mvImagePyramid[l] is a tight w_l x h_l copy of the level (the
-//    reference's is a view into a bordered buffer; the border was never
-//    read outside ORBextractor.cpp).  SetCopyPyramid(false) skips the copy
-//    for callers that do not read it (only stereo matching does,
-//    Frame.cpp:621-760);
+//  * the pyramid stays in HBM: mvImagePyramid is filled only when the host
+//    copy is asked for (SetCopyPyramid(true), or -DORBGPU_HOST_PYRAMID=1 to
+//    make that the default).  Its only reader in the reference is the stereo
+//    Frame's ComputeStereoMatches (Frame.cpp:547-676), which the build
+//    replaces with ORB_SLAM2::ComputeStereoMatchesGPU (StereoMatcher.h) on
+//    the two extractors' HBM pyramids; a copy is then
+//    8 blocking device-to-host level copies per frame for nothing.  When
+//    copied, level l is a tight w_l x h_l copy (the reference's is a view
+//    into a bordered buffer whose border is never read outside
+//    ORBextractor.cpp);
 //  * failures throw std::runtime_error carrying orbgpu_last_error() (the
 //    reference asserts).
 //
@@ -32,6 +37,10 @@
 #include <vector>
 
 #include "../orbgpu.h"
+
+#ifndef ORBGPU_HOST_PYRAMID
+#define ORBGPU_HOST_PYRAMID 0
+#endif
 
 namespace ORB_SLAM2 {
 
@@ -110,7 +119,7 @@ public:
 
     // adapter-only
     void SetCopyPyramid(bool on) { copy_pyramid_ = on; }
-    orbgpu_extractor* handle() { return ex_; }
+    orbgpu_extractor* handle() { return ex_; }  // the last frame's pyramid lives here (HBM)
 
     std::vector<cv::Mat> mvImagePyramid;
 
@@ -140,7 +149,7 @@ private:
     orbgpu_extractor_info info_{};
     std::vector<orbgpu_keypoint> kp_buf_;
     std::vector<unsigned char> desc_buf_;
-    bool copy_pyramid_ = true;
+    bool copy_pyramid_ = ORBGPU_HOST_PYRAMID != 0;
 };
 
 }  // namespace ORB_SLAM2

@@ -636,6 +636,12 @@ int orbref_level_size(const orbref_extractor* e, int l, int* w, int* h) {
     return 0;
 }
 
+const uint8_t* orbref_level_ptr(const orbref_extractor* e, int l, int* w, int* h) {
+    if (!e || l < 0 || l >= (int)e->pyr.size()) return nullptr;
+    *w = e->lw[l]; *h = e->lh[l];
+    return e->pyr[l].data();
+}
+
 int orbref_level_copy(const orbref_extractor* e, int l, uint8_t* dst) {
     if (!e || l < 0 || l >= (int)e->pyr.size()) return -1;
     std::memcpy(dst, e->pyr[l].data(), e->pyr[l].size());

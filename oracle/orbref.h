@@ -55,6 +55,8 @@ int orbref_extract(orbref_extractor* ex, const uint8_t* img, int width, int heig
 /* Accessors for the state the last orbref_extract() left behind. */
 int orbref_level_count(const orbref_extractor* ex);
 int orbref_level_size(const orbref_extractor* ex, int level, int* w, int* h);
+/* level `level` of mvImagePyramid in place (tight rows, step = w) */
+const uint8_t* orbref_level_ptr(const orbref_extractor* ex, int level, int* w, int* h);
 /* copies level `level` of mvImagePyramid (tight rows, w*h bytes) */
 int orbref_level_copy(const orbref_extractor* ex, int level, uint8_t* dst);
 /* FAST candidates of a level in vToDistributeKeys order, coordinates
@@ -109,6 +111,30 @@ int orbref_sim3_ransac(int n, const float* X1, const float* X2, const float* max
                        const float* K1, const float* K2, int fix_scale, int min_inliers, int best_inliers, int n_hyp,
                        const int* samples, int* out_ints, float* out_T12, float* out_R12, float* out_t12,
                        float* out_s12, uint8_t* inliers);
+
+/* --- stereo (stereo_ref.cpp) -------------------------------------------- */
+/* Frame::ComputeStereoMatches (Frame.cpp:540-748) over the keypoints and the
+ * pyramids the two extractors' last orbref_extract calls left (the left and
+ * right ORBextractor of a stereo Frame).  Same spec as oracle/stereo_ref.py.
+ * uright / depth: float[nL]. */
+void orbref_stereo_matches(const orbref_extractor* exL, const orbref_extractor* exR, const orbref_kp* kpsL,
+                           const uint8_t* descL, int nL, const orbref_kp* kpsR, const uint8_t* descR, int nR,
+                           float bf, float min_z, float* uright, float* depth);
+
+/* --- loop closure (loop_ref.cpp) ------------------------------------------ */
+typedef struct orbref_vocabulary orbref_vocabulary;
+orbref_vocabulary* orbref_vocabulary_create(int k, int L, int n, const int32_t* parent, const int32_t* is_leaf,
+                                            const uint8_t* desc, const double* weight);
+void orbref_vocabulary_destroy(orbref_vocabulary* voc);
+void orbref_vocabulary_transform(const orbref_vocabulary* voc, const uint8_t* desc, int n, int levelsup,
+                                 int* words, int* nodes, double* weights);
+int orbref_search_by_bow_kf_kf(const orbref_vocabulary* voc, const uint8_t* d1, const float* a1, const uint8_t* v1,
+                               int n1, const uint8_t* d2, const float* a2, const uint8_t* v2, int n2,
+                               float nnratio, int check_ori, int* match);
+int orbref_compute_sim3_query(const orbref_vocabulary* voc, int n_kp, const uint8_t* desc, const float* angle,
+                              const int32_t* octave, const uint8_t* valid, const float* mp_world, const float* Tcw,
+                              const float* K, const float* sigma2, int cur, const int* cands, int n_cand,
+                              unsigned seed, int fix_scale, int* out, int* nmatches);
 
 #ifdef __cplusplus
 }

@@ -60,6 +60,16 @@ def lib() -> ctypes.CDLL:
         L.orbref_ic_angle.argtypes = [vp, sz, i, i]
         L.orbref_sim3_ransac.argtypes = [i, vp, vp, vp, vp, vp, vp, i, i, i, i, vp, vp, vp, vp, vp, vp, vp]
         L.orbref_search_for_initialization.argtypes = [vp, vp, i, vp, vp, i, f, f, f, f, vp, i, f, i, i, vp]
+        L.orbref_level_ptr.restype = vp
+        L.orbref_level_ptr.argtypes = [vp, i, ctypes.POINTER(i), ctypes.POINTER(i)]
+        L.orbref_stereo_matches.argtypes = [vp, vp, vp, vp, i, vp, vp, i, f, f, vp, vp]
+        L.orbref_vocabulary_create.restype = vp
+        L.orbref_vocabulary_create.argtypes = [i, i, i, vp, vp, vp, vp]
+        L.orbref_vocabulary_destroy.argtypes = [vp]
+        L.orbref_vocabulary_transform.argtypes = [vp, vp, i, i, vp, vp, vp]
+        L.orbref_search_by_bow_kf_kf.argtypes = [vp, vp, vp, vp, i, vp, vp, vp, i, f, i, vp]
+        L.orbref_compute_sim3_query.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, i, ctypes.c_uint, i,
+                                                vp, vp]
         _LIB = L
     return _LIB
 
@@ -192,3 +202,81 @@ def sim3_ransac(X1, X2, maxerr1, maxerr2, K1, K2, fix_scale, min_inliers, best_i
                              int(best_inliers), len(smp), _p(smp), _p(ints), _p(T), _p(R), _p(t), _p(sc), _p(inl))
     return {"found": int(ints[0]), "consumed": int(ints[1]), "best_inliers": int(ints[2]), "best_hyp": int(ints[3]),
             "T12": T.reshape(4, 4), "R12": R.reshape(3, 3), "t12": t, "s12": float(sc[0]), "inliers": inl[:n]}
+
+
+def stereo_matches(exL: Extractor, exR: Extractor, kpsL, descL, kpsR, descR, bf, min_z=0.0):
+    """Frame::ComputeStereoMatches (oracle/stereo_ref.cpp) on the keypoints
+    and pyramids of the two extractors' last extract() calls."""
+    kpsL = np.ascontiguousarray(kpsL, KP_DTYPE)
+    kpsR = np.ascontiguousarray(kpsR, KP_DTYPE)
+    descL = np.ascontiguousarray(descL, np.uint8)
+    descR = np.ascontiguousarray(descR, np.uint8)
+    ur = np.zeros(max(len(kpsL), 1), np.float32)
+    dp = np.zeros(max(len(kpsL), 1), np.float32)
+    lib().orbref_stereo_matches(exL.h, exR.h, _p(kpsL), _p(descL), len(kpsL), _p(kpsR), _p(descR), len(kpsR),
+                                float(bf), float(min_z), _p(ur), _p(dp))
+    return ur[:len(kpsL)], dp[:len(kpsL)]
+
+
+def stereo_frame(exL: Extractor, exR: Extractor, left, right, bf, min_z=0.0):
+    """A stereo Frame's hot path (Frame.cpp:84-98): extract L and R with their
+    own extractors, then ComputeStereoMatches.  Returns (kpsL, descL, kpsR,
+    descR, uright, depth)."""
+    kl, dl = exL.extract(left)
+    kr, dr = exR.extract(right)
+    ur, dp = stereo_matches(exL, exR, kl, dl, kr, dr, bf, min_z)
+    return kl, dl, kr, dr, ur, dp
+
+
+class Vocabulary:
+    """DBoW2 tree from synth.synthetic_vocabulary* arrays (oracle/loop_ref.cpp)."""
+
+    def __init__(self, k, L, parent, is_leaf, desc, weight):
+        self._keep = [np.ascontiguousarray(parent, np.int32), np.ascontiguousarray(is_leaf, np.int32),
+                      np.ascontiguousarray(desc, np.uint8), np.ascontiguousarray(weight, np.float64)]
+        self.h = lib().orbref_vocabulary_create(k, L, len(self._keep[0]), *[_p(a) for a in self._keep])
+        self._keep = None
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orbref_vocabulary_destroy(self.h)
+            self.h = None
+
+    def transform(self, desc, levelsup=4):
+        desc = np.ascontiguousarray(desc, np.uint8)
+        n = len(desc)
+        words, nodes = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        weights = np.zeros(n, np.float64)
+        lib().orbref_vocabulary_transform(self.h, _p(desc), n, levelsup, _p(words), _p(nodes), _p(weights))
+        return words, nodes, weights
+
+
+def search_by_bow_kf_kf(voc: Vocabulary, d1, a1, v1, d2, a2, v2, nnratio=0.75, check_ori=True):
+    """SearchByBoW(KF1, KF2) with both FeatureVectors from voc (levelsup 4)."""
+    arrs = [np.ascontiguousarray(d1, np.uint8), np.ascontiguousarray(a1, np.float32),
+            np.ascontiguousarray(v1, np.uint8), np.ascontiguousarray(d2, np.uint8),
+            np.ascontiguousarray(a2, np.float32), np.ascontiguousarray(v2, np.uint8)]
+    m = np.zeros(len(arrs[0]), np.int32)
+    n = lib().orbref_search_by_bow_kf_kf(voc.h, _p(arrs[0]), _p(arrs[1]), _p(arrs[2]), len(arrs[0]), _p(arrs[3]),
+                                         _p(arrs[4]), _p(arrs[5]), len(arrs[3]), float(nnratio), int(check_ori),
+                                         _p(m))
+    return n, m
+
+
+_SCENE_KEYS = (("desc", np.uint8), ("angle", np.float32), ("octave", np.int32), ("valid", np.uint8),
+               ("mp_world", np.float32), ("Tcw", np.float32), ("K", np.float32), ("sigma2", np.float32))
+
+
+def compute_sim3_query(voc: Vocabulary, scene, cur, cands, seed, fix_scale=False):
+    """One ComputeSim3 call in C++ (oracle/loop_ref.cpp) on a
+    synth.loop_burst_scene.  Returns (matched, round, n_inliers, hypotheses,
+    nmatches per candidate)."""
+    c = scene.get("_c")
+    if c is None:
+        c = scene["_c"] = [np.ascontiguousarray(scene[k], t) for k, t in _SCENE_KEYS]
+    cd = np.ascontiguousarray(cands, np.int32)
+    out = np.zeros(4, np.int32)
+    nm = np.zeros(len(cd), np.int32)
+    lib().orbref_compute_sim3_query(voc.h, c[0].shape[1], *[_p(a) for a in c], int(cur), _p(cd), len(cd),
+                                    int(seed) & 0xFFFFFFFF, int(fix_scale), _p(out), _p(nm))
+    return int(out[0]), int(out[1]), int(out[2]), int(out[3]), nm

@@ -14,6 +14,7 @@
 #include "../../include/orbgpu_bow.h"
 #include "bow_kernels.h"
 #include "host_common.h"
+#include "host_ctx.h"
 
 using namespace orbgpu;
 
@@ -245,47 +246,51 @@ int orbgpu_bow_transform(const orbgpu_vocabulary* voc, int n, const uint8_t* des
     int rc = check_device();
     if (rc) return rc;
     const int s = std::max(n, 1);
-    uint8_t* dd = nullptr;
-    int *dc = nullptr, *dw = nullptr, *dn = nullptr, *dfn = nullptr, *dfo = nullptr, *dff = nullptr, *dfc = nullptr,
-        *dbw = nullptr, *dbc = nullptr;
-    double *dwt = nullptr, *dbv = nullptr;
-    auto cleanup = [&]() {
-        void* ptrs[] = {dd, dc, dw, dn, dfn, dfo, dff, dfc, dbw, dbc, dwt, dbv};
-        for (void* p : ptrs)
-            if (p) (void)hipFree(p);
-    };
-    bool ok = hipMalloc((void**)&dd, 32 * (size_t)s) == hipSuccess && hipMalloc((void**)&dc, 4) == hipSuccess &&
-              hipMalloc((void**)&dw, 4 * (size_t)s) == hipSuccess && hipMalloc((void**)&dn, 4 * (size_t)s) == hipSuccess &&
-              hipMalloc((void**)&dfn, 4 * (size_t)s) == hipSuccess &&
-              hipMalloc((void**)&dfo, 4 * (size_t)(s + 1)) == hipSuccess &&
-              hipMalloc((void**)&dff, 4 * (size_t)s) == hipSuccess && hipMalloc((void**)&dfc, 4) == hipSuccess &&
-              hipMalloc((void**)&dbw, 4 * (size_t)s) == hipSuccess && hipMalloc((void**)&dbc, 4) == hipSuccess &&
-              hipMalloc((void**)&dwt, 8 * (size_t)s) == hipSuccess && hipMalloc((void**)&dbv, 8 * (size_t)s) == hipSuccess;
-    if (!ok) {
-        cleanup();
-        return fail(ORBGPU_ERR_HIP, "device allocation failed");
-    }
-    ok = (n == 0 || hipMemcpy(dd, desc, 32 * (size_t)n, hipMemcpyHostToDevice) == hipSuccess) &&
-         hipMemcpy(dc, &n, 4, hipMemcpyHostToDevice) == hipSuccess;
-    if (ok) rc = orbgpu_bow_transform_batch_device(voc, 1, dd, dc, s, levelsup, dw, dn, dwt, dfn, dfo, dff, dfc, dbw,
-                                                   dbv, dbc, nullptr);
-    if (!ok || rc) {
-        cleanup();
-        return rc ? rc : fail(ORBGPU_ERR_HIP, "upload failed");
-    }
+    HostCtx* ctx;
+    if ((rc = host_ctx(&ctx))) return rc;
+    HostCall call(*ctx);
+    const uint8_t* dd;
+    const int* dc;
+    int *dw, *dn, *dfn, *dfo, *dff, *dfc, *dbw, *dbc;
+    double *dwt, *dbv;
+    rc = call.run([&](HostCall& A) {
+        dd = A.inout(desc, 32 * (size_t)n, 32 * (size_t)s);
+        dc = A.in(&n, 1);
+        dfc = A.out<int>(1);
+        dbc = A.out<int>(1);
+        dw = A.out<int>(s);
+        dn = A.out<int>(s);
+        dwt = A.out<double>(s);
+        dff = A.out<int>(s);
+        dfn = A.out<int>(s);
+        dfo = A.out<int>(s + 1);
+        dbw = A.out<int>(s);
+        dbv = A.out<double>(s);
+    });
+    if (rc) return rc;
+    rc = orbgpu_bow_transform_batch_device(voc, 1, dd, dc, s, levelsup, dw, dn, dwt, dfn, dfo, dff, dfc, dbw, dbv,
+                                           dbc, ctx->stream);
+    if (rc) return rc;
     int nf = 0, nb = 0;
-    ok = hipDeviceSynchronize() == hipSuccess && hipMemcpy(&nf, dfc, 4, hipMemcpyDeviceToHost) == hipSuccess &&
-         hipMemcpy(&nb, dbc, 4, hipMemcpyDeviceToHost) == hipSuccess &&
-         (n == 0 || (hipMemcpy(word, dw, 4 * (size_t)n, hipMemcpyDeviceToHost) == hipSuccess &&
-                     hipMemcpy(node, dn, 4 * (size_t)n, hipMemcpyDeviceToHost) == hipSuccess &&
-                     hipMemcpy(weight, dwt, 8 * (size_t)n, hipMemcpyDeviceToHost) == hipSuccess &&
-                     hipMemcpy(fv_features, dff, 4 * (size_t)n, hipMemcpyDeviceToHost) == hipSuccess)) &&
-         hipMemcpy(fv_nodes, dfn, 4 * (size_t)std::max(nf, 0), hipMemcpyDeviceToHost) == hipSuccess &&
-         hipMemcpy(fv_offsets, dfo, 4 * (size_t)(nf + 1), hipMemcpyDeviceToHost) == hipSuccess &&
-         hipMemcpy(bow_words, dbw, 4 * (size_t)std::max(nb, 0), hipMemcpyDeviceToHost) == hipSuccess &&
-         hipMemcpy(bow_values, dbv, 8 * (size_t)std::max(nb, 0), hipMemcpyDeviceToHost) == hipSuccess;
-    cleanup();
-    if (!ok) return fail(ORBGPU_ERR_HIP, "transform failed");
+    std::vector<int> fvn(s), fvo(s + 1), bw(s);
+    std::vector<double> bv(s);
+    call.fetch(dfc, &nf, 4);
+    call.fetch(dbc, &nb, 4);
+    call.fetch(dw, word, 4 * (size_t)n);
+    call.fetch(dn, node, 4 * (size_t)n);
+    call.fetch(dwt, weight, 8 * (size_t)n);
+    call.fetch(dff, fv_features, 4 * (size_t)n);
+    call.fetch(dfn, fvn.data(), 4 * (size_t)s);
+    call.fetch(dfo, fvo.data(), 4 * (size_t)(s + 1));
+    call.fetch(dbw, bw.data(), 4 * (size_t)s);
+    call.fetch(dbv, bv.data(), 8 * (size_t)s);
+    if ((rc = call.finish())) return rc;
+    nf = std::max(nf, 0);
+    nb = std::max(nb, 0);
+    std::memcpy(fv_nodes, fvn.data(), 4 * (size_t)nf);
+    std::memcpy(fv_offsets, fvo.data(), 4 * (size_t)(nf + 1));
+    std::memcpy(bow_words, bw.data(), 4 * (size_t)nb);
+    std::memcpy(bow_values, bv.data(), 8 * (size_t)nb);
     *fv_n = nf;
     *bow_n = nb;
     return ORBGPU_OK;
@@ -311,53 +316,38 @@ int orbgpu_search_by_bow(int mode, const orbgpu_bow_frame* a, const orbgpu_bow_f
         return fail(ORBGPU_ERR_ARG, "frame sizes out of range (<= 4096 features)");
     int rc = check_device();
     if (rc) return rc;
-    std::vector<void*> allocs;
-    auto cleanup = [&]() {
-        for (void* p : allocs) (void)hipFree(p);
-    };
-    auto up = [&](const void* src, size_t bytes) -> void* {
-        void* d = nullptr;
-        if (hipMalloc(&d, std::max<size_t>(bytes, 4)) != hipSuccess) return nullptr;
-        allocs.push_back(d);
-        if (src && bytes && hipMemcpy(d, src, bytes, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
-        return d;
-    };
-    orbgpu_bow_frame fr[2];
+    HostCtx* ctx;
+    if ((rc = host_ctx(&ctx))) return rc;
+    HostCall call(*ctx);
     const orbgpu_bow_frame* src[2] = {a, b};
-    for (int i = 0; i < 2; ++i) {
-        const orbgpu_bow_frame& s = *src[i];
-        fr[i] = s;
-        fr[i].fv_nodes = (const int*)up(s.fv_nodes, 4 * (size_t)s.fv_n);
-        fr[i].fv_offsets = (const int*)up(s.fv_offsets, 4 * (size_t)(s.fv_n + 1));
-        const int nfeat = s.fv_n ? s.fv_offsets[s.fv_n] : 0;
-        fr[i].fv_features = (const int*)up(s.fv_features, 4 * (size_t)nfeat);
-        fr[i].desc = (const uint8_t*)up(s.desc, 32 * (size_t)s.n);
-        fr[i].angle = (const float*)up(s.angle, 4 * (size_t)s.n);
-        fr[i].valid = (const uint8_t*)up(s.valid, (size_t)s.n);
-        if (!fr[i].fv_nodes || !fr[i].fv_offsets || !fr[i].fv_features || !fr[i].desc || !fr[i].angle ||
-            !fr[i].valid) {
-            cleanup();
-            return fail(ORBGPU_ERR_HIP, "upload failed");
-        }
-    }
     const int stride = std::max(std::max(a->n, b->n), 1);
-    orbgpu_bow_frame* dA = (orbgpu_bow_frame*)up(&fr[0], sizeof(fr[0]));
-    orbgpu_bow_frame* dB = (orbgpu_bow_frame*)up(&fr[1], sizeof(fr[1]));
-    int* dm = (int*)up(nullptr, 4 * (size_t)stride);
-    int* dn = (int*)up(nullptr, 4);
-    if (!dA || !dB || !dm || !dn) {
-        cleanup();
-        return fail(ORBGPU_ERR_HIP, "allocation failed");
-    }
-    rc = orbgpu_search_by_bow_batch_device(mode, 1, dA, dB, nnratio, check_ori, stride, dm, dn, nullptr);
-    const int nout = mode == ORBGPU_BOW_KF_F ? b->n : a->n;
-    const bool ok = !rc && hipDeviceSynchronize() == hipSuccess &&
-                    (nout == 0 || hipMemcpy(match, dm, 4 * (size_t)nout, hipMemcpyDeviceToHost) == hipSuccess) &&
-                    hipMemcpy(nmatches, dn, 4, hipMemcpyDeviceToHost) == hipSuccess;
-    cleanup();
+    const orbgpu_bow_frame *dA, *dB;
+    int *dm, *dn;
+    rc = call.run([&](HostCall& A) {
+        orbgpu_bow_frame fr[2];
+        for (int i = 0; i < 2; ++i) {
+            const orbgpu_bow_frame& s = *src[i];
+            fr[i] = s;
+            fr[i].fv_nodes = A.inout(s.fv_nodes, (size_t)s.fv_n);
+            fr[i].fv_offsets = A.inout(s.fv_offsets, (size_t)(s.fv_n + 1));
+            const int nfeat = s.fv_n ? s.fv_offsets[s.fv_n] : 0;
+            fr[i].fv_features = A.inout(s.fv_features, (size_t)nfeat);
+            fr[i].desc = A.inout(s.desc, 32 * (size_t)s.n);
+            fr[i].angle = A.inout(s.angle, (size_t)s.n);
+            fr[i].valid = A.inout(s.valid, (size_t)s.n);
+        }
+        dA = A.in(&fr[0], 1);
+        dB = A.in(&fr[1], 1);
+        dm = A.out<int>((size_t)stride);
+        dn = A.out<int>(1);
+    });
     if (rc) return rc;
-    if (!ok) return fail(ORBGPU_ERR_HIP, "SearchByBoW failed");
-    return ORBGPU_OK;
+    rc = orbgpu_search_by_bow_batch_device(mode, 1, dA, dB, nnratio, check_ori, stride, dm, dn, ctx->stream);
+    if (rc) return rc;
+    const int nout = mode == ORBGPU_BOW_KF_F ? b->n : a->n;
+    call.fetch(dm, match, 4 * (size_t)nout);
+    call.fetch(dn, nmatches, 4);
+    return call.finish();
 }
 
 int orbgpu_search_for_triangulation_batch_device(int batch, const orbgpu_triangulation_pair* d_pairs, int check_ori,
@@ -388,54 +378,40 @@ int orbgpu_search_for_triangulation(const orbgpu_triangulation_pair* pair, int c
     if ((P.kf1.n > 0 && !P.kps1) || (P.kf2.n > 0 && !P.kps2)) return fail(ORBGPU_ERR_ARG, "missing keypoints");
     int rc = check_device();
     if (rc) return rc;
-    std::vector<void*> allocs;
-    auto cleanup = [&]() {
-        for (void* p : allocs) (void)hipFree(p);
-    };
-    bool ok = true;
-    auto up = [&](const void* src_, size_t bytes) -> void* {
-        void* d = nullptr;
-        if (hipMalloc(&d, std::max<size_t>(bytes, 4)) != hipSuccess) {
-            ok = false;
-            return nullptr;
-        }
-        allocs.push_back(d);
-        if (src_ && bytes && hipMemcpy(d, src_, bytes, hipMemcpyHostToDevice) != hipSuccess) ok = false;
-        return d;
-    };
-    orbgpu_triangulation_pair d = P;
-    orbgpu_bow_frame* dst[2] = {&d.kf1, &d.kf2};
-    for (int i = 0; i < 2; ++i) {
-        const orbgpu_bow_frame& s = *src[i];
-        orbgpu_bow_frame& f = *dst[i];
-        f.fv_nodes = (const int*)up(s.fv_nodes, 4 * (size_t)s.fv_n);
-        f.fv_offsets = (const int*)up(s.fv_offsets, 4 * (size_t)(s.fv_n + 1));
-        const int nfeat = s.fv_n ? s.fv_offsets[s.fv_n] : 0;
-        f.fv_features = (const int*)up(s.fv_features, 4 * (size_t)nfeat);
-        f.desc = (const uint8_t*)up(s.desc, 32 * (size_t)s.n);
-        f.angle = (const float*)up(s.angle, 4 * (size_t)s.n);
-        f.valid = (const uint8_t*)up(s.valid, (size_t)s.n);
-    }
-    d.kps1 = (const orbgpu_keypoint*)up(P.kps1, sizeof(orbgpu_keypoint) * (size_t)P.kf1.n);
-    d.kps2 = (const orbgpu_keypoint*)up(P.kps2, sizeof(orbgpu_keypoint) * (size_t)P.kf2.n);
-    d.u_right1 = P.u_right1 ? (const float*)up(P.u_right1, 4 * (size_t)P.kf1.n) : nullptr;
-    d.u_right2 = P.u_right2 ? (const float*)up(P.u_right2, 4 * (size_t)P.kf2.n) : nullptr;
+    HostCtx* ctx;
+    if ((rc = host_ctx(&ctx))) return rc;
+    HostCall call(*ctx);
     const int stride = std::max(std::max(P.kf1.n, P.kf2.n), 1);
-    orbgpu_triangulation_pair* dP = (orbgpu_triangulation_pair*)up(&d, sizeof(d));
-    int* dm = (int*)up(nullptr, 4 * (size_t)stride);
-    int* dn = (int*)up(nullptr, 4);
-    if (!ok) {
-        cleanup();
-        return fail(ORBGPU_ERR_HIP, "upload failed");
-    }
-    rc = orbgpu_search_for_triangulation_batch_device(1, dP, check_ori, stride, dm, dn, nullptr);
-    ok = !rc && hipDeviceSynchronize() == hipSuccess &&
-         (P.kf1.n == 0 || hipMemcpy(match12, dm, 4 * (size_t)P.kf1.n, hipMemcpyDeviceToHost) == hipSuccess) &&
-         hipMemcpy(nmatches, dn, 4, hipMemcpyDeviceToHost) == hipSuccess;
-    cleanup();
+    const orbgpu_triangulation_pair* dP;
+    int *dm, *dn;
+    rc = call.run([&](HostCall& A) {
+        orbgpu_triangulation_pair d = P;
+        orbgpu_bow_frame* dst[2] = {&d.kf1, &d.kf2};
+        for (int i = 0; i < 2; ++i) {
+            const orbgpu_bow_frame& s = *src[i];
+            orbgpu_bow_frame& f = *dst[i];
+            f.fv_nodes = A.inout(s.fv_nodes, (size_t)s.fv_n);
+            f.fv_offsets = A.inout(s.fv_offsets, (size_t)(s.fv_n + 1));
+            const int nfeat = s.fv_n ? s.fv_offsets[s.fv_n] : 0;
+            f.fv_features = A.inout(s.fv_features, (size_t)nfeat);
+            f.desc = A.inout(s.desc, 32 * (size_t)s.n);
+            f.angle = A.inout(s.angle, (size_t)s.n);
+            f.valid = A.inout(s.valid, (size_t)s.n);
+        }
+        d.kps1 = A.inout(P.kps1, (size_t)P.kf1.n);
+        d.kps2 = A.inout(P.kps2, (size_t)P.kf2.n);
+        d.u_right1 = A.in(P.u_right1, (size_t)P.kf1.n);
+        d.u_right2 = A.in(P.u_right2, (size_t)P.kf2.n);
+        dP = A.in(&d, 1);
+        dm = A.out<int>((size_t)stride);
+        dn = A.out<int>(1);
+    });
     if (rc) return rc;
-    if (!ok) return fail(ORBGPU_ERR_HIP, "SearchForTriangulation failed");
-    return ORBGPU_OK;
+    rc = orbgpu_search_for_triangulation_batch_device(1, dP, check_ori, stride, dm, dn, ctx->stream);
+    if (rc) return rc;
+    call.fetch(dm, match12, 4 * (size_t)P.kf1.n);
+    call.fetch(dn, nmatches, 4);
+    return call.finish();
 }
 
 int orbgpu_bow_score_batch_device(int scoring, const int* d_q_words, const double* d_q_values, int nq, int nkf,
@@ -462,40 +438,28 @@ int orbgpu_bow_score(int scoring, const int* q_words, const double* q_values, in
     if (ndb > 0 && (!db_words || !db_values)) return fail(ORBGPU_ERR_ARG, "missing keyframe words");
     int rc = check_device();
     if (rc) return rc;
-    std::vector<void*> allocs;
-    bool ok = true;
-    auto up = [&](const void* src, size_t bytes) -> void* {
-        void* d = nullptr;
-        if (hipMalloc(&d, std::max<size_t>(bytes, 8)) != hipSuccess) {
-            ok = false;
-            return nullptr;
-        }
-        allocs.push_back(d);
-        if (src && bytes && hipMemcpy(d, src, bytes, hipMemcpyHostToDevice) != hipSuccess) ok = false;
-        return d;
-    };
-    const int* dqw = (const int*)up(q_words, 4 * (size_t)nq);
-    const double* dqv = (const double*)up(q_values, 8 * (size_t)nq);
-    const int* doff = (const int*)up(db_offsets, 4 * (size_t)(nkf + 1));
-    const int* dw = (const int*)up(db_words, 4 * ndb);
-    const double* dv = (const double*)up(db_values, 8 * ndb);
-    int* dc = (int*)up(nullptr, 4 * (size_t)nkf);
-    double* ds = (double*)up(nullptr, 8 * (size_t)nkf);
-    auto cleanup = [&]() {
-        for (void* p : allocs) (void)hipFree(p);
-    };
-    if (!ok) {
-        cleanup();
-        return fail(ORBGPU_ERR_HIP, "upload failed");
-    }
-    rc = orbgpu_bow_score_batch_device(scoring, dqw, dqv, nq, nkf, doff, dw, dv, dc, ds, nullptr);
-    ok = !rc && hipDeviceSynchronize() == hipSuccess &&
-         hipMemcpy(common, dc, 4 * (size_t)nkf, hipMemcpyDeviceToHost) == hipSuccess &&
-         hipMemcpy(scores, ds, 8 * (size_t)nkf, hipMemcpyDeviceToHost) == hipSuccess;
-    cleanup();
+    HostCtx* ctx;
+    if ((rc = host_ctx(&ctx))) return rc;
+    HostCall call(*ctx);
+    const int *dqw, *doff, *dw;
+    const double *dqv, *dv;
+    int* dc;
+    double* ds;
+    rc = call.run([&](HostCall& A) {
+        dqw = A.inout(q_words, (size_t)nq);
+        dqv = A.inout(q_values, (size_t)nq);
+        doff = A.in(db_offsets, (size_t)(nkf + 1));
+        dw = A.inout(db_words, ndb);
+        dv = A.inout(db_values, ndb);
+        dc = A.out<int>((size_t)nkf);
+        ds = A.out<double>((size_t)nkf);
+    });
     if (rc) return rc;
-    if (!ok) return fail(ORBGPU_ERR_HIP, "bow score failed");
-    return ORBGPU_OK;
+    rc = orbgpu_bow_score_batch_device(scoring, dqw, dqv, nq, nkf, doff, dw, dv, dc, ds, ctx->stream);
+    if (rc) return rc;
+    call.fetch(dc, common, 4 * (size_t)nkf);
+    call.fetch(ds, scores, 8 * (size_t)nkf);
+    return call.finish();
 }
 
 }  // extern "C"

@@ -29,6 +29,7 @@
 #include "../../include/orbgpu_init.h"
 #include "epnp.h"
 #include "host_common.h"
+#include "host_ctx.h"
 
 namespace orbgpu {
 
@@ -381,39 +382,38 @@ extern "C" int orbgpu_init_reconstruct(int model, const float* kp1, int n1, cons
     if (n_matches) std::memcpy(inl.data(), inliers, n_matches);
     const float mSigma2 = sigma * sigma;
     const float th2 = (float)(4.0 * mSigma2);
-    void *d_pts = nullptr, *d_inl = nullptr, *d_h = nullptr, *d_ng = nullptr, *d_par = nullptr, *d_good = nullptr,
-         *d_p3 = nullptr;
-    auto cleanup = [&]() {
-        for (void* p : {d_pts, d_inl, d_h, d_ng, d_par, d_good, d_p3})
-            if (p) (void)hipFree(p);
-    };
     const size_t nhn = (size_t)nh * n;
-    if (hipMalloc(&d_pts, pts.size() * 4) != hipSuccess || hipMalloc(&d_inl, n) != hipSuccess ||
-        hipMalloc(&d_h, sizeof(RecHyp) * nh) != hipSuccess || hipMalloc(&d_ng, 4 * nh) != hipSuccess ||
-        hipMalloc(&d_par, 4 * nh) != hipSuccess || hipMalloc(&d_good, nhn) != hipSuccess ||
-        hipMalloc(&d_p3, 12 * nhn) != hipSuccess) {
-        cleanup();
-        return fail(ORBGPU_ERR_HIP, "allocation failed");
-    }
+    HostCtx* ctx;
+    if ((rc = host_ctx(&ctx))) return rc;
+    HostCall call(*ctx);
+    const float4* d_pts;
+    const unsigned char* d_inl;
+    const RecHyp* d_h;
+    int* d_ng;
+    float *d_par, *d_p3;
+    unsigned char* d_good;
+    rc = call.run([&](HostCall& A) {
+        d_pts = reinterpret_cast<const float4*>(A.in(pts.data(), pts.size()));
+        d_inl = A.in(inl.data(), (size_t)n);
+        d_h = A.in(hy.data(), (size_t)nh);
+        d_ng = A.out<int>((size_t)nh);
+        d_par = A.out<float>((size_t)nh);
+        d_good = A.out<unsigned char>(nhn);
+        d_p3 = A.out<float>(3 * nhn);
+    });
+    if (rc) return rc;
     std::vector<int> ng(nh);
     std::vector<float> par(nh);
     std::vector<unsigned char> good(nhn);
     std::vector<float> P3(3 * nhn);
-    bool ok = hipMemcpy(d_pts, pts.data(), pts.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-              hipMemcpy(d_inl, inl.data(), n, hipMemcpyHostToDevice) == hipSuccess &&
-              hipMemcpy(d_h, hy.data(), sizeof(RecHyp) * nh, hipMemcpyHostToDevice) == hipSuccess;
-    if (ok) {
-        hipLaunchKernelGGL(check_rt_kernel, dim3(nh), dim3(kRecThreads), 4 * (size_t)n, nullptr,
-                           (const float4*)d_pts, (const unsigned char*)d_inl, n_matches, (const RecHyp*)d_h, fx, fy,
-                           cx, cy, th2, (int*)d_ng, (float*)d_par, (unsigned char*)d_good, (float*)d_p3);
-        ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
-             hipMemcpy(ng.data(), d_ng, 4 * nh, hipMemcpyDeviceToHost) == hipSuccess &&
-             hipMemcpy(par.data(), d_par, 4 * nh, hipMemcpyDeviceToHost) == hipSuccess &&
-             hipMemcpy(good.data(), d_good, nhn, hipMemcpyDeviceToHost) == hipSuccess &&
-             hipMemcpy(P3.data(), d_p3, 12 * nhn, hipMemcpyDeviceToHost) == hipSuccess;
-    }
-    cleanup();
-    if (!ok) return fail(ORBGPU_ERR_HIP, "CheckRT failed");
+    hipLaunchKernelGGL(check_rt_kernel, dim3(nh), dim3(kRecThreads), 4 * (size_t)n, ctx->stream, d_pts, d_inl,
+                       n_matches, d_h, fx, fy, cx, cy, th2, d_ng, d_par, d_good, d_p3);
+    ORB_HIP(hipGetLastError());
+    call.fetch(d_ng, ng.data(), 4 * (size_t)nh);
+    call.fetch(d_par, par.data(), 4 * (size_t)nh);
+    call.fetch(d_good, good.data(), nhn);
+    call.fetch(d_p3, P3.data(), 12 * nhn);
+    if ((rc = call.finish())) return rc;
     for (int i = 0; i < nh; ++i) {
         out->n_good[i] = ng[i];
         out->parallax[i] = par[i];
@@ -487,60 +487,57 @@ extern "C" int orbgpu_init_initialize(const float* kp1, int n1, const float* kp2
     rc = check_device();
     if (rc) return rc;
     const size_t work_b = orbgpu_init_workspace_bytes(n1, n2);
-    void *d_kp1 = nullptr, *d_kp2 = nullptr, *d_pairs = nullptr, *d_sets = nullptr, *d_work = nullptr,
-         *d_pts = nullptr, *d_h21 = nullptr, *d_h12 = nullptr, *d_f21 = nullptr, *d_sh = nullptr, *d_sf = nullptr,
-         *d_ih = nullptr, *d_if = nullptr;
-    void** all[] = {&d_kp1, &d_kp2, &d_pairs, &d_sets, &d_work, &d_pts, &d_h21, &d_h12, &d_f21, &d_sh, &d_sf,
-                    &d_ih, &d_if};
-    const size_t sizes[] = {8 * (size_t)std::max(n1, 1), 8 * (size_t)std::max(n2, 1), 8 * (size_t)N,
-                            4 * sets.size(), std::max<size_t>(work_b, 16), 16 * (size_t)N,
-                            36 * (size_t)iterations, 36 * (size_t)iterations, 36 * (size_t)iterations,
-                            4 * (size_t)iterations, 4 * (size_t)iterations, (size_t)iterations * N,
-                            (size_t)iterations * N};
-    auto cleanup = [&]() {
-        for (void** p : all)
-            if (*p) (void)hipFree(*p);
-    };
-    bool ok = true;
-    for (size_t i = 0; i < sizeof(all) / sizeof(all[0]); ++i) ok = ok && hipMalloc(all[i], sizes[i]) == hipSuccess;
-    ok = ok && hipMemcpy(d_kp1, kp1, 8 * (size_t)n1, hipMemcpyHostToDevice) == hipSuccess &&
-         hipMemcpy(d_kp2, kp2, 8 * (size_t)n2, hipMemcpyHostToDevice) == hipSuccess &&
-         hipMemcpy(d_pairs, pairs.data(), 8 * (size_t)N, hipMemcpyHostToDevice) == hipSuccess &&
-         hipMemcpy(d_sets, sets.data(), 4 * sets.size(), hipMemcpyHostToDevice) == hipSuccess;
-    if (!ok) {
-        cleanup();
-        return fail(ORBGPU_ERR_HIP, "allocation / upload failed");
-    }
+    HostCtx* ctx;
+    if ((rc = host_ctx(&ctx))) return rc;
+    HostCall call(*ctx);
+    const float *d_kp1, *d_kp2;
+    const int *d_pairs, *d_sets;
+    void* d_work;
+    orbgpu_match_pts* d_pts;
+    float *d_h21, *d_h12, *d_f21, *d_sh, *d_sf;
+    uint8_t *d_ih, *d_if;
+    const size_t it = (size_t)iterations;
+    rc = call.run([&](HostCall& A) {
+        d_kp1 = A.inout(kp1, 2 * (size_t)n1, 2 * (size_t)std::max(n1, 1));
+        d_kp2 = A.inout(kp2, 2 * (size_t)n2, 2 * (size_t)std::max(n2, 1));
+        d_pairs = A.in(pairs.data(), 2 * (size_t)N);
+        d_sets = A.in(sets.data(), sets.size());
+        d_work = A.out<uint8_t>(std::max<size_t>(work_b, 16));
+        d_pts = A.out<orbgpu_match_pts>((size_t)N);
+        d_h21 = A.out<float>(9 * it);
+        d_h12 = A.out<float>(9 * it);
+        d_f21 = A.out<float>(9 * it);
+        d_sh = A.out<float>(it);
+        d_sf = A.out<float>(it);
+        d_ih = A.out<uint8_t>(it * N);
+        d_if = A.out<uint8_t>(it * N);
+    });
+    if (rc) return rc;
     // FindHomography / FindFundamental (:160-269): every iteration's hypotheses and scores
-    rc = orbgpu_init_hypotheses_batch_device((const float*)d_kp1, n1, (const float*)d_kp2, n2, (const int*)d_pairs, N,
-                                             (const int*)d_sets, iterations, d_work, (orbgpu_match_pts*)d_pts,
-                                             (float*)d_h21, (float*)d_h12, (float*)d_f21, nullptr);
+    rc = orbgpu_init_hypotheses_batch_device(d_kp1, n1, d_kp2, n2, d_pairs, N, d_sets, iterations, d_work, d_pts,
+                                             d_h21, d_h12, d_f21, ctx->stream);
     if (!rc)
-        rc = orbgpu_init_check_both_batch_device((const orbgpu_match_pts*)d_pts, N, (const float*)d_h21,
-                                                 (const float*)d_h12, iterations, (const float*)d_f21, iterations,
-                                                 sigma, (float*)d_sh, (uint8_t*)d_ih, (float*)d_sf, (uint8_t*)d_if,
-                                                 nullptr);
+        rc = orbgpu_init_check_both_batch_device(d_pts, N, d_h21, d_h12, iterations, d_f21, iterations, sigma, d_sh,
+                                                 d_ih, d_sf, d_if, ctx->stream);
+    if (rc) return rc;
     std::vector<float> sh(iterations), sf(iterations);
-    if (!rc && (hipDeviceSynchronize() != hipSuccess ||
-                hipMemcpy(sh.data(), d_sh, 4 * (size_t)iterations, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(sf.data(), d_sf, 4 * (size_t)iterations, hipMemcpyDeviceToHost) != hipSuccess))
-        rc = fail(ORBGPU_ERR_HIP, "model scoring failed");
+    call.fetch(d_sh, sh.data(), 4 * it);
+    call.fetch(d_sf, sf.data(), 4 * it);
+    if ((rc = call.finish())) return rc;
     int bh = -1, bf = -1;
-    if (!rc) rc = orbgpu_init_select_best(sh.data(), iterations, &bh);
-    if (!rc) rc = orbgpu_init_select_best(sf.data(), iterations, &bf);
+    if ((rc = orbgpu_init_select_best(sh.data(), iterations, &bh))) return rc;
+    if ((rc = orbgpu_init_select_best(sf.data(), iterations, &bf))) return rc;
     const float SH = bh >= 0 ? sh[bh] : 0.f, SF = bf >= 0 ? sf[bf] : 0.f;
     const float RH = SH / (SH + SF);  // :140 (NaN when both are 0: ReconstructF, as the reference)
     const bool useH = RH > 0.40;
     float M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     std::vector<unsigned char> inl(N, 0);
     const int best = useH ? bh : bf;
-    if (!rc && best >= 0 &&
-        (hipMemcpy(M, (float*)(useH ? d_h21 : d_f21) + 9 * (size_t)best, 36, hipMemcpyDeviceToHost) != hipSuccess ||
-         hipMemcpy(inl.data(), (uint8_t*)(useH ? d_ih : d_if) + (size_t)best * N, N, hipMemcpyDeviceToHost) !=
-             hipSuccess))
-        rc = fail(ORBGPU_ERR_HIP, "model read-back failed");
-    cleanup();
-    if (rc) return rc;
+    if (best >= 0) {  // the kept model and its inlier flags (a second, small read-back)
+        call.fetch((useH ? d_h21 : d_f21) + 9 * (size_t)best, M, 36);
+        call.fetch((useH ? d_ih : d_if) + (size_t)best * N, inl.data(), (size_t)N);
+        if ((rc = call.finish())) return rc;
+    }
     *rh = RH;
     *model = useH ? ORBGPU_INIT_MODEL_H : ORBGPU_INIT_MODEL_F;
     // (no kept iteration: the reference reconstructs from an empty H/F with no inliers -> false)

@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -28,6 +29,7 @@
 #include "orbgpu_kernels.h"
 #include "stereo_kernels.h"
 #include "host_common.h"
+#include "host_ctx.h"
 
 using namespace orbgpu;
 
@@ -41,13 +43,17 @@ int fail(int code, const std::string& msg) {
 }
 
 int check_device() {
+    // the arch check once per device and thread (the host-form calls run it on every call)
+    static thread_local int checked_dev = -1;
     int dev = 0, n = 0;
+    if (checked_dev >= 0 && hipGetDevice(&dev) == hipSuccess && dev == checked_dev) return ORBGPU_OK;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(ORBGPU_ERR_NO_DEVICE, "no HIP device visible");
     ORB_HIP(hipGetDevice(&dev));
     hipDeviceProp_t p;
     ORB_HIP(hipGetDeviceProperties(&p, dev));
     if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
         return fail(ORBGPU_ERR_NO_DEVICE, std::string("device is ") + p.gcnArchName + ", this build targets gfx950");
+    checked_dev = dev;
     return ORBGPU_OK;
 }
 
@@ -143,8 +149,15 @@ struct orbgpu_extractor {
     int* d_oct_count = nullptr;
     int* d_err = nullptr;
     int* d_trace = nullptr;  // optional octree pass trace (debug API)
-    int* d_stereo_sad = nullptr;  // ComputeStereoMatches: accepted SAD per left keypoint (pairs x cap)
-    size_t stereo_sad_n = 0;
+    // ComputeStereoMatches: accepted SAD per left keypoint (pairs x cap), one scratch per
+    // stream the batch form was called on (calls on different streams never share one)
+    struct SadScratch {
+        hipStream_t stream;
+        int* d;
+        size_t n;
+    };
+    std::vector<SadScratch> stereo_sad;
+    std::mutex stereo_mu;
     // host-image path
     uint8_t* d_img = nullptr;
     size_t img_pitch = 0;
@@ -171,9 +184,10 @@ struct orbgpu_extractor {
 
     ~orbgpu_extractor() {
         void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_ent, d_pyr_tab, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
-                        d_oct_count, d_err, d_trace, d_stereo_sad, d_img, d_single};
+                        d_oct_count, d_err, d_trace, d_img, d_single};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
+        for (auto& sc : stereo_sad) (void)hipFree(sc.d);
         if (h_single) (void)hipHostFree(h_single);
         if (h_img) (void)hipHostFree(h_img);
         if (stream) (void)hipStreamDestroy(stream);
@@ -705,41 +719,32 @@ int orbgpu_search_for_initialization(orbgpu_grid_bounds bd, const orbgpu_keypoin
     if (n1 < 0 || n2 < 0 || !matches12 || !nmatches) return fail(ORBGPU_ERR_ARG, "invalid argument");
     int rc = check_device();
     if (rc) return rc;
+    HostCtx* ctx;
+    if ((rc = host_ctx(&ctx))) return rc;
     const size_t n1c = std::max(n1, 1), n2c = std::max(n2, 1);
-    orbgpu_keypoint *dk1 = nullptr, *dk2 = nullptr;
-    uint8_t *dd1 = nullptr, *dd2 = nullptr;
-    int *dn = nullptr, *dm = nullptr;
-    float* dp = nullptr;
-    auto cleanup = [&]() {
-        void* ptrs[] = {dk1, dk2, dd1, dd2, dn, dm, dp};
-        for (void* p : ptrs)
-            if (p) (void)hipFree(p);
-    };
-    if (hipMalloc((void**)&dk1, n1c * sizeof(orbgpu_keypoint)) != hipSuccess ||
-        hipMalloc((void**)&dk2, n2c * sizeof(orbgpu_keypoint)) != hipSuccess ||
-        hipMalloc((void**)&dd1, n1c * 32) != hipSuccess || hipMalloc((void**)&dd2, n2c * 32) != hipSuccess ||
-        hipMalloc((void**)&dn, 3 * sizeof(int)) != hipSuccess || hipMalloc((void**)&dm, n1c * sizeof(int)) != hipSuccess ||
-        (prev_xy && hipMalloc((void**)&dp, n1c * 2 * sizeof(float)) != hipSuccess)) {
-        cleanup();
-        return fail(ORBGPU_ERR_HIP, "device allocation failed");
-    }
-    const int ns[2] = {n1, n2};
-    bool ok = hipMemcpy(dk1, kps1, (size_t)n1 * sizeof(orbgpu_keypoint), hipMemcpyHostToDevice) == hipSuccess &&
-              hipMemcpy(dk2, kps2, (size_t)n2 * sizeof(orbgpu_keypoint), hipMemcpyHostToDevice) == hipSuccess &&
-              hipMemcpy(dd1, desc1, (size_t)n1 * 32, hipMemcpyHostToDevice) == hipSuccess &&
-              hipMemcpy(dd2, desc2, (size_t)n2 * 32, hipMemcpyHostToDevice) == hipSuccess &&
-              hipMemcpy(dn, ns, 2 * sizeof(int), hipMemcpyHostToDevice) == hipSuccess &&
-              (!prev_xy || hipMemcpy(dp, prev_xy, (size_t)n1 * 2 * sizeof(float), hipMemcpyHostToDevice) == hipSuccess);
-    if (!ok) { cleanup(); return fail(ORBGPU_ERR_HIP, "upload failed"); }
+    const int ns[3] = {n1, n2, 0};
+    const orbgpu_keypoint *dk1, *dk2;
+    const uint8_t *dd1, *dd2;
+    int *dn, *dm;
+    float* dp;
+    HostCall call(*ctx);
+    rc = call.run([&](HostCall& A) {
+        dk1 = A.inout(kps1, (size_t)n1, n1c);
+        dk2 = A.inout(kps2, (size_t)n2, n2c);
+        dd1 = A.inout(desc1, 32 * (size_t)n1, 32 * n1c);
+        dd2 = A.inout(desc2, 32 * (size_t)n2, 32 * n2c);
+        dn = A.inout(ns, 3);
+        dm = A.out<int>(n1c);
+        dp = prev_xy ? A.inout(prev_xy, 2 * (size_t)n1, 2 * n1c) : nullptr;
+    });
+    if (rc) return rc;
     rc = orbgpu_search_for_initialization_batch_device(1, bd, dk1, dd1, dn, n1c, dk2, dd2, dn + 1, n2c, dp,
-                                                       window, nnratio, flags, dm, dn + 2, nullptr);
-    if (rc) { cleanup(); return rc; }
-    ok = hipDeviceSynchronize() == hipSuccess &&
-         hipMemcpy(matches12, dm, (size_t)n1 * sizeof(int), hipMemcpyDeviceToHost) == hipSuccess &&
-         hipMemcpy(nmatches, dn + 2, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess &&
-         (!prev_xy || hipMemcpy(prev_xy, dp, (size_t)n1 * 2 * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess);
-    cleanup();
-    if (!ok) return fail(ORBGPU_ERR_HIP, "matcher failed");
+                                                       window, nnratio, flags, dm, dn + 2, ctx->stream);
+    if (rc) return rc;
+    call.fetch(dm, matches12, (size_t)n1 * sizeof(int));
+    call.fetch(dn + 2, nmatches, sizeof(int));
+    if (prev_xy) call.fetch(dp, prev_xy, (size_t)n1 * 2 * sizeof(float));
+    if ((rc = call.finish())) return rc;
     if (*nmatches < 0) {
         *nmatches = 0;
         return fail(ORBGPU_ERR_CAPACITY, "matcher: more than 1024 level-0 keypoints in a frame");
@@ -841,6 +846,42 @@ int orbgpu_debug_pyramid_emulate(int nfeatures, float scale_factor, int nlevels,
     return ORBGPU_OK;
 }
 
+namespace {
+
+// StereoArgs common to both entry points: level sizes and scales, thresholds,
+// and the level bases of the left / right image of pair 0 (lb0 / rb0: level 0
+// from the caller's image pointers, levels >= 1 from the extractors' pyramids)
+void stereo_args(const orbgpu_extractor* left, const orbgpu_extractor* right, int lframe, int rframe,
+                 const uint8_t* l0, const uint8_t* r0, size_t row_step, size_t pair_step0, int cap, float bf,
+                 float min_z, StereoArgs& a) {
+    const Geom& g = left->g;
+    std::memset(&a, 0, sizeof(a));
+    for (int l = 0; l < g.nlevels; ++l) {
+        if (l == 0) {
+            a.lvl_base[0] = l0;
+            a.lvl_base_r[0] = r0;
+            a.lvl_pair[0] = pair_step0;
+            a.lvl_pitch[0] = (int)row_step;
+        } else {
+            a.lvl_base[l] = left->d_pyr + g.lv[l].offset + (size_t)lframe * g.lv[l].frame_bytes;
+            a.lvl_base_r[l] = right->d_pyr + g.lv[l].offset + (size_t)rframe * g.lv[l].frame_bytes;
+            a.lvl_pair[l] = 2 * g.lv[l].frame_bytes;
+            a.lvl_pitch[l] = g.lv[l].pitch;
+        }
+        a.lvl_w[l] = g.lv[l].w;
+        a.lvl_h[l] = g.lv[l].h;
+        a.scale[l] = left->scale[l];
+        a.inv_scale[l] = left->inv_scale[l];
+    }
+    a.cap = cap;
+    a.bf = bf;
+    a.max_d = bf / min_z;  // +inf for min_z = 0, as the reference (Frame.cpp:581)
+    a.th_orb = (100 + 50) / 2;
+    a.rr = (int)std::ceil(2.0f * left->scale[g.nlevels - 1]) + 1;
+}
+
+}  // namespace
+
 // Frame::ComputeStereoMatches (Frame.cpp:540-748) over the last extraction.
 int orbgpu_stereo_matches_batch_device(orbgpu_extractor* e, const uint8_t* d_images, size_t row_step,
                                        size_t frame_step, int npairs, const orbgpu_keypoint* d_kps,
@@ -852,44 +893,96 @@ int orbgpu_stereo_matches_batch_device(orbgpu_extractor* e, const uint8_t* d_ima
     if (kp_capacity < e->max_kps || kp_capacity > 65535)
         return fail(ORBGPU_ERR_ARG, "kp_capacity must be >= max_keypoints and < 65536");
     const Geom& g = e->g;
+    if (stereo_lds_bytes(kp_capacity, g.lv[0].h) > 160 * 1024)
+        return fail(ORBGPU_ERR_UNSUPPORTED, "stereo LDS tables exceed 160 KiB");
     StereoArgs a;
-    std::memset(&a, 0, sizeof(a));
-    for (int l = 0; l < g.nlevels; ++l) {
-        if (l == 0) {
-            a.lvl_base[0] = d_images;
-            a.lvl_frame[0] = frame_step;
-            a.lvl_pitch[0] = (int)row_step;
-        } else {
-            a.lvl_base[l] = e->d_pyr + g.lv[l].offset;
-            a.lvl_frame[l] = g.lv[l].frame_bytes;
-            a.lvl_pitch[l] = g.lv[l].pitch;
-        }
-        a.lvl_w[l] = g.lv[l].w;
-        a.lvl_h[l] = g.lv[l].h;
-        a.scale[l] = e->scale[l];
-        a.inv_scale[l] = e->inv_scale[l];
-    }
+    stereo_args(e, e, 0, 1, d_images, d_images + frame_step, row_step, 2 * frame_step, kp_capacity, bf, min_z, a);
     a.kps = d_kps;
     a.desc = d_desc;
     a.counts = d_counts;
-    a.cap = kp_capacity;
-    a.bf = bf;
-    a.max_d = bf / min_z;  // +inf for min_z = 0, as the reference (Frame.cpp:581)
-    a.th_orb = (100 + 50) / 2;
-    a.rr = (int)std::ceil(2.0f * e->scale[g.nlevels - 1]) + 1;
     a.uright = d_uright;
     a.depth = d_depth;
     const size_t nsad = (size_t)npairs * kp_capacity;
-    if (nsad > e->stereo_sad_n) {
-        if (e->d_stereo_sad) ORB_HIP(hipFree(e->d_stereo_sad));
-        e->d_stereo_sad = nullptr;
-        e->stereo_sad_n = 0;
-        ORB_HIP(hipMalloc((void**)&e->d_stereo_sad, nsad * sizeof(int)));
-        e->stereo_sad_n = nsad;
+    const hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+    {
+        std::lock_guard<std::mutex> lk(e->stereo_mu);
+        orbgpu_extractor::SadScratch* sc = nullptr;
+        for (auto& x : e->stereo_sad)
+            if (x.stream == hs) sc = &x;
+        if (!sc) {
+            e->stereo_sad.push_back({hs, nullptr, 0});
+            sc = &e->stereo_sad.back();
+        }
+        if (nsad > sc->n) {
+            if (sc->d) ORB_HIP(hipFree(sc->d));
+            sc->d = nullptr;
+            sc->n = 0;
+            ORB_HIP(hipMalloc((void**)&sc->d, nsad * sizeof(int)));
+            sc->n = nsad;
+        }
+        a.sad = sc->d;
     }
-    a.sad = e->d_stereo_sad;
-    if (stereo_lds_bytes(kp_capacity, g.lv[0].h) > 160 * 1024)
-        return fail(ORBGPU_ERR_UNSUPPORTED, "stereo LDS tables exceed 160 KiB");
-    ORB_HIP(launch_stereo(a, npairs, reinterpret_cast<hipStream_t>(stream)));
+    ORB_HIP(launch_stereo(a, npairs, hs));
     return ORBGPU_OK;
+}
+
+// ComputeStereoMatches of a stereo Frame built by two extractors
+// (Frame.cpp:84-98): the pyramids of their last orbgpu_extract calls, read in
+// place in HBM; keypoints / descriptors from the host.
+int orbgpu_stereo_matches_pair(orbgpu_extractor* left, orbgpu_extractor* right, const orbgpu_keypoint* kps_l,
+                               const uint8_t* desc_l, int n_l, const orbgpu_keypoint* kps_r, const uint8_t* desc_r,
+                               int n_r, float bf, float min_z, float* uright, float* depth) {
+    if (!left || !right || n_l < 0 || n_r < 0 || (n_l > 0 && (!kps_l || !desc_l || !uright || !depth)) ||
+        (n_r > 0 && (!kps_r || !desc_r)))
+        return fail(ORBGPU_ERR_ARG, "invalid argument");
+    if (left->W != right->W || left->H != right->H || left->nlevels != right->nlevels ||
+        left->scale_factor != right->scale_factor)
+        return fail(ORBGPU_ERR_ARG, "left and right extractors differ in geometry");
+    if (!left->last_img || !right->last_img || left->last_batch < 1 || right->last_batch < 1)
+        return fail(ORBGPU_ERR_ARG, "both extractors need an extraction first");
+    if (left->last_row != right->last_row) return fail(ORBGPU_ERR_ARG, "level-0 row steps differ");
+    // frame capacity a multiple of 64, so the staged L and R arrays are contiguous (28 * 64 and
+    // 32 * 64 bytes are multiples of the arena's 256-byte granule): frame f at + f * cap
+    const int cap = (std::max(std::max(n_l, n_r), 1) + 63) / 64 * 64;
+    if (cap > 65535) return fail(ORBGPU_ERR_ARG, "more than 65535 keypoints");
+    if (stereo_lds_bytes(cap, left->g.lv[0].h) > 160 * 1024)
+        return fail(ORBGPU_ERR_UNSUPPORTED, "stereo LDS tables exceed 160 KiB");
+    if (n_l == 0) return ORBGPU_OK;
+    int rc = check_device();
+    if (rc) return rc;
+    HostCtx* ctx;
+    if ((rc = host_ctx(&ctx))) return rc;
+    // the pyramids were written on the extractors' streams (orbgpu_extract returned after
+    // synchronising them), so the thread's stream may read them directly
+    HostCall call(*ctx);
+    orbgpu_keypoint *dk, *dk_r;
+    uint8_t *dd, *dd_r;
+    int* dn;
+    float *du, *dz;
+    int* ds;
+    const int counts[2] = {n_l, n_r};
+    rc = call.run([&](HostCall& A) {
+        dk = A.inout(kps_l, (size_t)n_l, (size_t)cap);
+        dk_r = A.inout(kps_r, (size_t)n_r, (size_t)cap);
+        dd = A.inout(desc_l, 32 * (size_t)n_l, 32 * (size_t)cap);
+        dd_r = A.inout(desc_r, 32 * (size_t)n_r, 32 * (size_t)cap);
+        dn = A.in(counts, 2);
+        du = A.out<float>((size_t)cap);
+        dz = A.out<float>((size_t)cap);
+        ds = A.out<int>((size_t)cap);
+    });
+    if (rc) return rc;
+    if (dk_r != dk + cap || dd_r != dd + 32 * (size_t)cap) return fail(ORBGPU_ERR_ARG, "internal: staging layout");
+    StereoArgs a;
+    stereo_args(left, right, 0, 0, left->last_img, right->last_img, left->last_row, 0, cap, bf, min_z, a);
+    a.kps = dk;
+    a.desc = dd;
+    a.counts = dn;
+    a.uright = du;
+    a.depth = dz;
+    a.sad = ds;
+    ORB_HIP(launch_stereo(a, 1, ctx->stream));
+    call.fetch(du, uright, 4 * (size_t)n_l);
+    call.fetch(dz, depth, 4 * (size_t)n_l);
+    return call.finish();
 }

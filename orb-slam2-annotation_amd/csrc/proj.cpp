@@ -7,59 +7,31 @@
 
 #include "../../include/orbgpu_proj.h"
 #include "host_common.h"
+#include "host_ctx.h"
 #include "proj_kernels.h"
 
 using namespace orbgpu;
 
 namespace {
 
-struct DeviceArena {  // uploads a call's host arrays; frees them on destruction
-    std::vector<void*> ptrs;
-    bool ok = true;
-    ~DeviceArena() {
-        for (void* p : ptrs) (void)hipFree(p);
-    }
-    template <class T>
-    const T* up(const T* src, size_t count) {
-        if (!src) return nullptr;
-        void* d = nullptr;
-        if (hipMalloc(&d, std::max<size_t>(count * sizeof(T), 4)) != hipSuccess) {
-            ok = false;
-            return nullptr;
-        }
-        ptrs.push_back(d);
-        if (count && hipMemcpy(d, src, count * sizeof(T), hipMemcpyHostToDevice) != hipSuccess) ok = false;
-        return static_cast<const T*>(d);
-    }
-    void* alloc(size_t bytes) {
-        void* d = nullptr;
-        if (hipMalloc(&d, std::max<size_t>(bytes, 4)) != hipSuccess) {
-            ok = false;
-            return nullptr;
-        }
-        ptrs.push_back(d);
-        return d;
-    }
-};
-
 // the call's host arrays uploaded into A; d = the call with device pointers
-void upload_call(DeviceArena& A, const orbgpu_proj_call& c, orbgpu_proj_call& d) {
+void upload_call(HostCall& A, const orbgpu_proj_call& c, orbgpu_proj_call& d) {
     const size_t n = (size_t)c.target.n, m = (size_t)c.points.n;
     d = c;
-    d.target.kps = A.up(c.target.kps, n);
-    d.target.desc = A.up(c.target.desc, 32 * n);
-    d.target.u_right = A.up(c.target.u_right, n);
-    d.target.occupied = A.up(c.target.occupied, n);
-    d.points.flags = A.up(c.points.flags, m);
-    d.points.pos = A.up(c.points.pos, 3 * m);
-    d.points.normal = A.up(c.points.normal, 3 * m);
-    d.points.desc = A.up(c.points.desc, 32 * m);
-    d.points.min_dist = A.up(c.points.min_dist, m);
-    d.points.max_dist = A.up(c.points.max_dist, m);
-    d.points.octave = A.up(c.points.octave, m);
-    d.points.angle = A.up(c.points.angle, m);
-    d.points.track = A.up(c.points.track, 4 * m);
-    d.points.track_level = A.up(c.points.track_level, m);
+    d.target.kps = A.in(c.target.kps, n);
+    d.target.desc = A.in(c.target.desc, 32 * n);
+    d.target.u_right = A.in(c.target.u_right, n);
+    d.target.occupied = A.in(c.target.occupied, n);
+    d.points.flags = A.in(c.points.flags, m);
+    d.points.pos = A.in(c.points.pos, 3 * m);
+    d.points.normal = A.in(c.points.normal, 3 * m);
+    d.points.desc = A.in(c.points.desc, 32 * m);
+    d.points.min_dist = A.in(c.points.min_dist, m);
+    d.points.max_dist = A.in(c.points.max_dist, m);
+    d.points.octave = A.in(c.points.octave, m);
+    d.points.angle = A.in(c.points.angle, m);
+    d.points.track = A.in(c.points.track, 4 * m);
+    d.points.track_level = A.in(c.points.track_level, m);
 }
 
 // argument checks of one host call (orbgpu_search_by_projection)
@@ -135,19 +107,24 @@ int orbgpu_search_by_projection(const orbgpu_proj_call* call, int* match, int* n
     if (rc) return rc;
     // one output entry per target keypoint, or per point for the per-point variants
     const int nout = c.variant >= ORBGPU_PROJ_FUSE ? c.points.n : c.target.n;
-    DeviceArena A;
-    orbgpu_proj_call d;
-    upload_call(A, c, d);
-    const orbgpu_proj_call* dc = A.up(&d, 1);
-    int* dm = static_cast<int*>(A.alloc(4 * (size_t)std::max(nout, 1)));
-    int* dn = static_cast<int*>(A.alloc(4));
-    if (!A.ok) return fail(ORBGPU_ERR_HIP, "upload failed");
-    rc = orbgpu_search_by_projection_batch_device(1, dc, std::max(nout, 1), dm, dn, nullptr);
+    HostCtx* ctx;
+    if ((rc = host_ctx(&ctx))) return rc;
+    HostCall hc(*ctx);
+    const orbgpu_proj_call* dc;
+    int *dm, *dn;
+    rc = hc.run([&](HostCall& A) {
+        orbgpu_proj_call d;
+        upload_call(A, c, d);
+        dc = A.in(&d, 1);
+        dm = A.out<int>((size_t)std::max(nout, 1));
+        dn = A.out<int>(1);
+    });
     if (rc) return rc;
-    if (hipDeviceSynchronize() != hipSuccess ||
-        (nout && hipMemcpy(match, dm, 4 * (size_t)nout, hipMemcpyDeviceToHost) != hipSuccess) ||
-        hipMemcpy(nmatches, dn, 4, hipMemcpyDeviceToHost) != hipSuccess)
-        return fail(ORBGPU_ERR_HIP, "SearchByProjection failed");
+    rc = orbgpu_search_by_projection_batch_device(1, dc, std::max(nout, 1), dm, dn, ctx->stream);
+    if (rc) return rc;
+    hc.fetch(dm, match, 4 * (size_t)nout);
+    hc.fetch(dn, nmatches, 4);
+    if ((rc = hc.finish())) return rc;
     if (*nmatches < 0) return fail(ORBGPU_ERR_CAPACITY, "call rejected by the kernel");
     return ORBGPU_OK;
 }
@@ -198,22 +175,27 @@ int orbgpu_search_by_sim3(const orbgpu_sim3_search* search, int* match12, int* n
     int rc = check_device();
     if (rc) return rc;
     const int stride = std::max(1, std::max(n1, n2));
-    DeviceArena A;
-    orbgpu_proj_call d[2];
-    upload_call(A, c[0], d[0]);
-    upload_call(A, c[1], d[1]);
-    const orbgpu_proj_call* dc = A.up(d, 2);
-    int* dm = static_cast<int*>(A.alloc(2 * 4 * (size_t)stride));
-    int* dn = static_cast<int*>(A.alloc(8));
-    if (!A.ok) return fail(ORBGPU_ERR_HIP, "upload failed");
-    rc = orbgpu_search_by_projection_batch_device(2, dc, stride, dm, dn, nullptr);
+    HostCtx* ctx;
+    if ((rc = host_ctx(&ctx))) return rc;
+    HostCall call(*ctx);
+    const orbgpu_proj_call* dc;
+    int *dm, *dn;
+    rc = call.run([&](HostCall& A) {
+        orbgpu_proj_call d[2];
+        upload_call(A, c[0], d[0]);
+        upload_call(A, c[1], d[1]);
+        dc = A.in(d, 2);
+        dm = A.out<int>(2 * (size_t)stride);
+        dn = A.out<int>(2);
+    });
+    if (rc) return rc;
+    rc = orbgpu_search_by_projection_batch_device(2, dc, stride, dm, dn, ctx->stream);
     if (rc) return rc;
     std::vector<int> m(2 * (size_t)stride);
     int nn[2];
-    if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(m.data(), dm, m.size() * 4, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(nn, dn, 8, hipMemcpyDeviceToHost) != hipSuccess)
-        return fail(ORBGPU_ERR_HIP, "SearchBySim3 failed");
+    call.fetch(dm, m.data(), m.size() * 4);
+    call.fetch(dn, nn, 8);
+    if ((rc = call.finish())) return rc;
     if (nn[0] < 0 || nn[1] < 0) return fail(ORBGPU_ERR_CAPACITY, "call rejected by the kernel");
     const int* v1 = m.data();            // vnMatch1
     const int* v2 = m.data() + stride;   // vnMatch2

@@ -11,6 +11,7 @@
 #include "../../include/orbgpu_init.h"
 #include "../../include/orbgpu_ransac.h"
 #include "host_common.h"
+#include "host_ctx.h"
 #include "ransac_kernels.h"
 
 using namespace orbgpu;
@@ -154,50 +155,33 @@ int orbgpu_sim3_ransac_batch(int batch, const orbgpu_sim3_problem* problems, int
     int max_hyp = 0;
     for (int b = 0; b < batch; ++b) max_hyp = std::max(max_hyp, problems[b].n_hyp);
     const size_t np = (size_t)(total_points > 0 ? total_points : 1), ns = (size_t)(total_samples > 0 ? total_samples : 1);
-    orbgpu_sim3_problem* dp = nullptr;
-    float *dx1 = nullptr, *dx2 = nullptr, *de1 = nullptr, *de2 = nullptr;
-    int* ds = nullptr;
-    orbgpu_sim3_result* dr = nullptr;
-    uint8_t* di = nullptr;
-    void* dw = nullptr;
-    auto cleanup = [&]() {
-        void* ptrs[] = {dp, dx1, dx2, de1, de2, ds, dr, di, dw};
-        for (void* p : ptrs)
-            if (p) (void)hipFree(p);
-    };
-    bool ok = hipMalloc((void**)&dp, sizeof(*dp) * batch) == hipSuccess &&
-              hipMalloc((void**)&dx1, 12 * np) == hipSuccess && hipMalloc((void**)&dx2, 12 * np) == hipSuccess &&
-              hipMalloc((void**)&de1, 4 * np) == hipSuccess && hipMalloc((void**)&de2, 4 * np) == hipSuccess &&
-              hipMalloc((void**)&ds, 12 * ns) == hipSuccess && hipMalloc((void**)&dr, sizeof(*dr) * batch) == hipSuccess &&
-              hipMalloc((void**)&di, np) == hipSuccess &&
-              hipMalloc(&dw, orbgpu_sim3_workspace_bytes(total_samples)) == hipSuccess;
-    if (!ok) {
-        cleanup();
-        return fail(ORBGPU_ERR_HIP, "device allocation failed");
-    }
-    ok = hipMemcpy(dp, problems, sizeof(*dp) * batch, hipMemcpyHostToDevice) == hipSuccess &&
-         (total_points == 0 ||
-          (hipMemcpy(dx1, X1, 12 * (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
-           hipMemcpy(dx2, X2, 12 * (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
-           hipMemcpy(de1, maxerr1, 4 * (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
-           hipMemcpy(de2, maxerr2, 4 * (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
-           hipMemcpy(di, inliers, (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess)) &&
-         (total_samples == 0 || hipMemcpy(ds, samples, 12 * (size_t)total_samples, hipMemcpyHostToDevice) == hipSuccess);
-    if (!ok) {
-        cleanup();
-        return fail(ORBGPU_ERR_HIP, "upload failed");
-    }
-    rc = orbgpu_sim3_ransac_batch_device(batch, dp, max_hyp, dx1, dx2, de1, de2, ds, dw, dr, di, nullptr);
-    if (rc) {
-        cleanup();
-        return rc;
-    }
-    ok = hipDeviceSynchronize() == hipSuccess &&
-         hipMemcpy(results, dr, sizeof(*dr) * batch, hipMemcpyDeviceToHost) == hipSuccess &&
-         (total_points == 0 || hipMemcpy(inliers, di, (size_t)total_points, hipMemcpyDeviceToHost) == hipSuccess);
-    cleanup();
-    if (!ok) return fail(ORBGPU_ERR_HIP, "Sim3 RANSAC failed");
-    return ORBGPU_OK;
+    const size_t tp = (size_t)total_points, ts = (size_t)total_samples;
+    HostCtx* ctx;
+    if ((rc = host_ctx(&ctx))) return rc;
+    HostCall call(*ctx);
+    const orbgpu_sim3_problem* dp;
+    const float *dx1, *dx2, *de1, *de2;
+    const int* ds;
+    orbgpu_sim3_result* dr;
+    uint8_t* di;
+    void* dw;
+    rc = call.run([&](HostCall& A) {
+        dp = A.in(problems, (size_t)batch);
+        dx1 = A.inout(X1, 3 * tp, 3 * np);
+        dx2 = A.inout(X2, 3 * tp, 3 * np);
+        de1 = A.inout(maxerr1, tp, np);
+        de2 = A.inout(maxerr2, tp, np);
+        ds = A.inout(samples, 3 * ts, 3 * ns);
+        di = A.inout(inliers, tp, np);
+        dr = A.out<orbgpu_sim3_result>((size_t)batch);
+        dw = A.out<uint8_t>(orbgpu_sim3_workspace_bytes(total_samples));
+    });
+    if (rc) return rc;
+    rc = orbgpu_sim3_ransac_batch_device(batch, dp, max_hyp, dx1, dx2, de1, de2, ds, dw, dr, di, ctx->stream);
+    if (rc) return rc;
+    call.fetch(dr, results, sizeof(*dr) * batch);
+    call.fetch(di, inliers, tp);
+    return call.finish();
 }
 
 size_t orbgpu_pnp_workspace_bytes(int total_points, int total_samples) {
@@ -245,53 +229,35 @@ int orbgpu_pnp_ransac_batch(int batch, const orbgpu_pnp_problem* problems, int t
     int max_hyp = 0;
     for (int b = 0; b < batch; ++b) max_hyp = std::max(max_hyp, problems[b].n_hyp);
     const size_t np = (size_t)(total_points > 0 ? total_points : 1), ns = (size_t)(total_samples > 0 ? total_samples : 1);
-    orbgpu_pnp_problem* dp = nullptr;
-    float *d3 = nullptr, *d2 = nullptr, *de = nullptr;
-    int* ds = nullptr;
-    orbgpu_pnp_result* dr = nullptr;
-    uint8_t *dbm = nullptr, *drm = nullptr;
-    void* dw = nullptr;
-    auto cleanup = [&]() {
-        void* ptrs[] = {dp, d3, d2, de, ds, dr, dbm, drm, dw};
-        for (void* p : ptrs)
-            if (p) (void)hipFree(p);
-    };
-    bool ok = hipMalloc((void**)&dp, sizeof(*dp) * batch) == hipSuccess &&
-              hipMalloc((void**)&d3, 12 * np) == hipSuccess && hipMalloc((void**)&d2, 8 * np) == hipSuccess &&
-              hipMalloc((void**)&de, 4 * np) == hipSuccess && hipMalloc((void**)&ds, 16 * ns) == hipSuccess &&
-              hipMalloc((void**)&dr, sizeof(*dr) * batch) == hipSuccess && hipMalloc((void**)&dbm, np) == hipSuccess &&
-              hipMalloc((void**)&drm, np) == hipSuccess &&
-              hipMalloc(&dw, orbgpu_pnp_workspace_bytes(total_points, total_samples)) == hipSuccess;
-    if (!ok) {
-        cleanup();
-        return fail(ORBGPU_ERR_HIP, "device allocation failed");
-    }
-    ok = hipMemcpy(dp, problems, sizeof(*dp) * batch, hipMemcpyHostToDevice) == hipSuccess &&
-         (total_points == 0 ||
-          (hipMemcpy(d3, P3w, 12 * (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
-           hipMemcpy(d2, P2, 8 * (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
-           hipMemcpy(de, maxerr, 4 * (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
-           hipMemcpy(dbm, best_mask, (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess &&
-           hipMemcpy(drm, refined_mask, (size_t)total_points, hipMemcpyHostToDevice) == hipSuccess)) &&
-         (total_samples == 0 || hipMemcpy(ds, samples, 16 * (size_t)total_samples, hipMemcpyHostToDevice) == hipSuccess);
-    if (!ok) {
-        cleanup();
-        return fail(ORBGPU_ERR_HIP, "upload failed");
-    }
+    const size_t tp = (size_t)total_points, ts = (size_t)total_samples;
+    HostCtx* ctx;
+    if ((rc = host_ctx(&ctx))) return rc;
+    HostCall call(*ctx);
+    const orbgpu_pnp_problem* dp;
+    const float *d3, *d2, *de;
+    const int* ds;
+    orbgpu_pnp_result* dr;
+    uint8_t *dbm, *drm;
+    void* dw;
+    rc = call.run([&](HostCall& A) {
+        dp = A.in(problems, (size_t)batch);
+        d3 = A.inout(P3w, 3 * tp, 3 * np);
+        d2 = A.inout(P2, 2 * tp, 2 * np);
+        de = A.inout(maxerr, tp, np);
+        ds = A.inout(samples, 4 * ts, 4 * ns);
+        dbm = A.inout(best_mask, tp, np);
+        drm = A.inout(refined_mask, tp, np);
+        dr = A.out<orbgpu_pnp_result>((size_t)batch);
+        dw = A.out<uint8_t>(orbgpu_pnp_workspace_bytes(total_points, total_samples));
+    });
+    if (rc) return rc;
     rc = orbgpu_pnp_ransac_batch_device(batch, dp, max_hyp, total_points, total_samples, d3, d2, de, ds, dw, dr, dbm,
-                                        drm, nullptr);
-    if (rc) {
-        cleanup();
-        return rc;
-    }
-    ok = hipDeviceSynchronize() == hipSuccess &&
-         hipMemcpy(results, dr, sizeof(*dr) * batch, hipMemcpyDeviceToHost) == hipSuccess &&
-         (total_points == 0 ||
-          (hipMemcpy(best_mask, dbm, (size_t)total_points, hipMemcpyDeviceToHost) == hipSuccess &&
-           hipMemcpy(refined_mask, drm, (size_t)total_points, hipMemcpyDeviceToHost) == hipSuccess));
-    cleanup();
-    if (!ok) return fail(ORBGPU_ERR_HIP, "PnP RANSAC failed");
-    return ORBGPU_OK;
+                                        drm, ctx->stream);
+    if (rc) return rc;
+    call.fetch(dr, results, sizeof(*dr) * batch);
+    call.fetch(dbm, best_mask, tp);
+    call.fetch(drm, refined_mask, tp);
+    return call.finish();
 }
 
 }  // extern "C"

@@ -1,6 +1,7 @@
 // stereo.hip -- Frame::ComputeStereoMatches (Frame.cpp:540-748) for batches
 // of rectified stereo pairs extracted by one orbgpu_extractor (left = frame
-// 2p, right = frame 2p+1 of the last batch extraction).
+// 2p, right = frame 2p+1 of the last batch extraction), or for one pair
+// extracted by two extractors (the stereo Frame's mpORBextractorLeft/Right).
 //
 // S 1024-thread blocks per pair (S chosen so the launch fills every CU; a
 // pair's left keypoints are dealt to its S blocks, wave w of block b taking
@@ -47,8 +48,10 @@ __device__ __forceinline__ int wave_min(int v) {
     return v;
 }
 
-__device__ __forceinline__ uint8_t px(const StereoArgs& a, int frame, int lvl, int y, int x) {
-    return a.lvl_base[lvl][(size_t)frame * a.lvl_frame[lvl] + (size_t)y * a.lvl_pitch[lvl] + x];
+// pixel (x, y) of level lvl of pair p's left (right = false) or right image
+__device__ __forceinline__ uint8_t px(const StereoArgs& a, int p, bool right, int lvl, int y, int x) {
+    const uint8_t* b = right ? a.lvl_base_r[lvl] : a.lvl_base[lvl];
+    return b[(size_t)p * a.lvl_pair[lvl] + (size_t)y * a.lvl_pitch[lvl] + x];
 }
 
 __global__ __launch_bounds__(kStThreads) void stereo_kernel(StereoArgs a, int S) {
@@ -180,16 +183,16 @@ __global__ __launch_bounds__(kStThreads) void stereo_kernel(StereoArgs a, int S)
         const float iniu = __fadd_rn(sr, 0.0f), endu = __fadd_rn(sr, 11.0f);   // scaleduR0 + L - w, + L + w + 1
         if (iniu < 0.f || endu >= (float)lw) continue;                            // :668-671
         if (ir - 10 < 0) continue;                                                 // spec: IR inside the level
-        const int cL = px(a, fl, lvl, iv, iu);
+        const int cL = px(a, p, false, lvl, iv, iu);
         for (int c = lane; c < 121; c += 64) {
             const int inc = c / 11 - 5, rr = c - (c / 11) * 11;
             const int y = iv - 5 + rr;
-            const int cR = px(a, fr, lvl, iv, ir + inc);
+            const int cR = px(a, p, true, lvl, iv, ir + inc);
             int s = 0;
 #pragma unroll
             for (int col = 0; col < 11; ++col) {
-                const int l = (int)px(a, fl, lvl, y, iu - 5 + col) - cL;
-                const int rv = (int)px(a, fr, lvl, y, ir + inc - 5 + col) - cR;
+                const int l = (int)px(a, p, false, lvl, y, iu - 5 + col) - cL;
+                const int rv = (int)px(a, p, true, lvl, y, ir + inc - 5 + col) - cR;
                 s += abs(l - rv);
             }
             scr[c] = s;

@@ -11,9 +11,12 @@
 namespace orbgpu {
 
 struct StereoArgs {
-    // pyramid level l of frame f: lvl_base[l] + f * lvl_frame[l], row pitch lvl_pitch[l]
+    // pyramid level l of pair p: left image at lvl_base[l] + p * lvl_pair[l], right image at
+    // lvl_base_r[l] + p * lvl_pair[l], row pitch lvl_pitch[l] (one extractor's batch: right =
+    // left + one frame, pair = two frames; two extractors' single frames: p = 0)
     const uint8_t* lvl_base[kMaxLevels];
-    size_t lvl_frame[kMaxLevels];
+    const uint8_t* lvl_base_r[kMaxLevels];
+    size_t lvl_pair[kMaxLevels];
     int lvl_pitch[kMaxLevels], lvl_w[kMaxLevels], lvl_h[kMaxLevels];
     float scale[kMaxLevels], inv_scale[kMaxLevels];  // mvScaleFactors, mvInvScaleFactors
     const orbgpu_keypoint* kps;  // extraction outputs: frame f at + f * cap

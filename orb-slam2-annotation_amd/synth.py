@@ -127,23 +127,27 @@ def trajectory_t(frame: int) -> int:
 
 
 def torch_stream(n: int, width: int, height: int, seed: int = 0x0B5E, device="cuda", t0: int = 0,
-                 noise_sigma: float = 2.0, pitch: int | None = None, chunk: int = 64, bounded: bool = False):
+                 noise_sigma: float = 2.0, pitch: int | None = None, chunk: int = 64, bounded: bool = False,
+                 baseline_px: float = 0.0, noise_seed: int | None = None):
     """GPU-rendered version of mono_stream for benchmark batches (same scene
     geometry; bilinear sampling and noise come from torch, so frames are not
     byte-identical to mono_stream -- parity tests use the numpy renderer).
     Frames t0 .. t0+n-1; with bounded=True global frame f is rendered at
-    trajectory_t(f) (long streams).  Returns a (n, height, pitch) uint8
-    tensor (pitch >= width, zero padded)."""
+    trajectory_t(f) (long streams).  baseline_px shifts the virtual camera
+    horizontally (right images of stereo pairs); noise_seed (default seed)
+    seeds the sensor noise only.  Returns a (n, height,
+    pitch) uint8 tensor (pitch >= width, zero padded).  Deterministic on a
+    given device type for the same arguments."""
     import torch
 
     pitch = pitch or width
     base = torch.from_numpy(base_texture(seed)).to(device=device, dtype=torch.float32)[None, None]
     out = torch.zeros((n, height, pitch), dtype=torch.uint8, device=device)
     gen = torch.Generator(device=device)
-    gen.manual_seed(seed * 7919 + t0)
+    gen.manual_seed((seed if noise_seed is None else noise_seed) * 7919 + t0)
     v, u = torch.meshgrid(torch.arange(height, device=device, dtype=torch.float32),
                           torch.arange(width, device=device, dtype=torch.float32), indexing="ij")
-    u = u - (width - 1) / 2.0
+    u = u - (width - 1) / 2.0 + baseline_px
     v = v - (height - 1) / 2.0
     for s in range(0, n, chunk):
         m = min(chunk, n - s)
@@ -161,6 +165,22 @@ def torch_stream(n: int, width: int, height: int, seed: int = 0x0B5E, device="cu
         img = img + noise_sigma * torch.randn(img.shape, generator=gen, device=device)
         out[s:s + m, :, :width] = img.round().clamp(0, 255).to(torch.uint8)
     return out
+
+
+def torch_stereo_stream(n_pairs: int, width: int, height: int, baseline_px: float, seed: int = 0x5E7,
+                        device="cuda", t0: int = 0, pitch: int | None = None):
+    """Rectified stereo pairs t0 .. t0+n_pairs-1 of a bounded camera path
+    (torch_stream geometry): a (2*n_pairs, height, pitch) uint8 tensor with
+    the left image of pair p at 2p and the right one (camera shifted by
+    baseline_px) at 2p+1 -- the layout orbgpu_stereo_matches_batch_device
+    reads.  Deterministic for the same (n_pairs, t0, seed) on a device type."""
+    import torch
+
+    pitch = pitch or width
+    left = torch_stream(n_pairs, width, height, seed, device, t0, pitch=pitch, bounded=True)
+    right = torch_stream(n_pairs, width, height, seed, device, t0, pitch=pitch, bounded=True,
+                         baseline_px=baseline_px, noise_seed=seed + 1)
+    return torch.stack([left, right], dim=1).reshape(2 * n_pairs, height, pitch).contiguous()
 
 
 def sim3_problem(n: int, inlier_frac: float, seed: int, fix_scale: bool = False, noise_px: float = 0.5):

@@ -35,6 +35,17 @@
 //       Frame::ComputeBoW, levelsup 4), score of the two BowVectors
 //   adapter_main tri <in.bin> <out.bin>
 //       ORBmatcher::SearchForTriangulation (LocalMapping.cpp:355-360)
+//   adapter_main stereo <w> <h> <nfeat> <bf> <left.raw> <right.raw> <out.bin>
+//       the stereo Frame (Frame.cpp:84-98): two ORBextractor objects on two
+//       threads, then ComputeStereoMatchesGPU (StereoMatcher.h) on their HBM
+//       pyramids; writes both frames' keypoints / descriptors, mvuRight, mvDepth
+//
+// Timing (bench.py's drop_in section): with ADAPTER_REPS=<n> and
+// ADAPTER_TIME_LOG=<file> the extract, stereo, proj, bow, pnp and init modes
+// repeat their drop-in call n times (state restored between repetitions,
+// untimed) and append one JSON line per call to the log: the median / p90 /
+// min of the per-call wall time, steady_clock around the class member call
+// exactly as Tracking / Frame make it.
 // The .bin layouts are written / read by tests/test_adapter.py (fixed
 // field order, little-endian, no headers).
 #include <cstdio>
@@ -45,9 +56,12 @@
 #include <iterator>
 #include <vector>
 
+#include <algorithm>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <set>
+#include <thread>
 
 #include "orbslam2_amd/ORBextractor.h"
 #include "orbslam2_amd/Initializer.h"
@@ -56,8 +70,44 @@
 #include "orbslam2_amd/ORBmatcher.h"
 #include "orbslam2_amd/PnPsolver.h"
 #include "orbslam2_amd/Sim3Solver.h"
+#include "orbslam2_amd/StereoMatcher.h"
 
 namespace {
+
+// ---- drop-in timing (ADAPTER_REPS / ADAPTER_TIME_LOG) ----------------------
+int reps() {
+    const char* r = std::getenv("ADAPTER_REPS");
+    return r ? std::max(1, std::atoi(r)) : 1;
+}
+
+void log_times(const char* op, std::vector<double> us, const char* note = "") {
+    const char* path = std::getenv("ADAPTER_TIME_LOG");
+    if (!path || us.empty()) return;
+    std::sort(us.begin(), us.end());
+    const double med = us[us.size() / 2], p90 = us[std::min(us.size() - 1, us.size() * 9 / 10)];
+    FILE* f = std::fopen(path, "a");
+    if (!f) return;
+    std::fprintf(f, "{\"op\": \"%s\", \"median_us\": %.2f, \"p90_us\": %.2f, \"min_us\": %.2f, \"reps\": %zu, "
+                    "\"note\": \"%s\"}\n", op, med, p90, us.front(), us.size(), note);
+    std::fclose(f);
+}
+
+// run setup() (untimed) then body() reps() times; log body's wall time
+template <class Setup, class Body>
+void timed(const char* op, Setup setup, Body body, const char* note = "") {
+    const int n = reps();
+    if (n <= 1 || !std::getenv("ADAPTER_TIME_LOG")) return;
+    std::vector<double> us;
+    for (int r = 0; r < n; ++r) {
+        setup();
+        const auto t0 = std::chrono::steady_clock::now();
+        body();
+        const auto t1 = std::chrono::steady_clock::now();
+        us.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+    }
+    log_times(op, us, note);
+}
+
 
 struct MiniKeyFrame;
 
@@ -299,9 +349,12 @@ int run_proj(int variant, const char* inp, const char* outp) {
     ORB_SLAM2::ORBmatcher m(nnratio, check_ori != 0);
     int nm = 0;
     std::vector<MiniMapPoint*> result;
+    const std::vector<MiniMapPoint*> slots0 = T.mvpMapPoints;
     if (variant == 0) {
         nm = m.SearchByProjection(T, pts, th);
         result = T.mvpMapPoints;
+        timed("ORBmatcher::SearchByProjection(F, vpLocalMapPoints, th)", [&] { T.mvpMapPoints = slots0; },
+              [&] { m.SearchByProjection(T, pts, th); }, "Tracking::SearchLocalPoints, Tracking.cpp:1560");
     } else if (variant == 1) {
         std::vector<MiniMapPoint*> vpMatched = T.mvpMapPoints;
         nm = m.SearchByProjection(&T, T.mTcw, pts, vpMatched, (int)th);
@@ -327,6 +380,9 @@ int run_proj(int variant, const char* inp, const char* outp) {
         MiniFrame& cur = T;
         nm = m.SearchByProjection(cur, static_cast<const MiniFrame&>(last), th, mono != 0);
         result = T.mvpMapPoints;
+        timed("ORBmatcher::SearchByProjection(F, LastFrame, th, bMono)", [&] { T.mvpMapPoints = slots0; },
+              [&] { m.SearchByProjection(cur, static_cast<const MiniFrame&>(last), th, mono != 0); },
+              "Tracking::TrackWithMotionModel, Tracking.cpp:1152");
     } else {
         MiniKeyFrame kf;  // the keyframe's MapPoints = the points, its keypoint angles
         kf.mvpMapPoints = pts;
@@ -382,6 +438,14 @@ int run_bow(const char* inp, const char* outp) {
     const int n1 = m.SearchByBoW(&A, F, vpMatches);  // KF = A, F = B
     std::vector<MiniMapPoint*> vp12;
     const int n2 = m.SearchByBoW(&A, &B, vp12);       // KF1 = A, KF2 = B
+    timed("ORBmatcher::SearchByBoW(KF, F)", [] {}, [&] {
+        std::vector<MiniMapPoint*> v;
+        m.SearchByBoW(&A, F, v);
+    }, "Tracking::TrackReferenceKeyFrame, Tracking.cpp:990");
+    timed("ORBmatcher::SearchByBoW(KF1, KF2)", [] {}, [&] {
+        std::vector<MiniMapPoint*> v;
+        m.SearchByBoW(&A, &B, v);
+    }, "LoopClosing::ComputeSim3, LoopClosing.cpp:311");
     Out out(outp);
     out.put(n1);
     out.vec(encode(vpMatches, A.mvpMapPoints));
@@ -420,6 +484,21 @@ int run_pnp(const char* inp, const char* outp) {
         ++calls;
         Tcw = solver.iterate(5, bNoMore, vbInliers, nInliers);
         if (!Tcw.empty()) break;
+    }
+    {
+        std::unique_ptr<ORB_SLAM2::PnPsolver> sv;
+        timed("PnPsolver::iterate(5)", [&] {
+            orbgpu_srand(seed);
+            sv.reset(new ORB_SLAM2::PnPsolver(static_cast<const MiniFrame&>(F), vp));
+            sv->SetRansacParameters(0.99, 10, 300, 4, 0.5, 5.991);
+        }, [&] {
+            bool nm = false;
+            std::vector<bool> v;
+            int ni = 0;
+            sv->iterate(5, nm, v, ni);
+        }, "Tracking::Relocalization, Tracking.cpp:1822 (first call of a fresh solver)");
+        orbgpu_srand(seed);  // the stream the output below reports continues from the loop above
+        for (int c = 0; c < 4 * solver.Iterations(); ++c) orbgpu_rand();
     }
     Out out(outp);
     out.put((int)!Tcw.empty());
@@ -706,6 +785,18 @@ int run_init(const char* inp, const char* outp) {
     std::vector<cv::Point3f> vP3D;
     std::vector<bool> vbTri;
     const bool ok = ini.Initialize(F2, m12, R21, t21, vP3D, vbTri);
+    {
+        std::unique_ptr<ORB_SLAM2::Initializer> iv;
+        timed("Initializer::Initialize", [&] {
+            orbgpu_srand(1);
+            iv.reset(new ORB_SLAM2::Initializer(F1, 1.0, 200));
+        }, [&] {
+            cv::Mat R, t;
+            std::vector<cv::Point3f> P;
+            std::vector<bool> tri;
+            iv->Initialize(F2, m12, R, t, P, tri);
+        }, "Tracking::MonocularInitialization, Tracking.cpp:790");
+    }
     Out out(outp);
     out.put((int)ok);
     out.put(ini.mModel);
@@ -897,6 +988,7 @@ int main(int argc, char** argv) {
         }
         try {
             ORB_SLAM2::ORBextractor ex(nf, 1.2f, 8, 20, 7);
+            ex.SetCopyPyramid(true);  // this mode writes mvImagePyramid[1] for the test
             MiniFrame F[2];
             for (int f = 0; f < 2; ++f) {
                 cv::Mat img(h, w, CV_8UC1, im[f].data(), (size_t)w);
@@ -909,6 +1001,23 @@ int main(int argc, char** argv) {
             std::vector<int> m12;
             ORB_SLAM2::ORBmatcher matcher(0.9f, true);  // Tracking.cpp:766-769
             const int nm = matcher.SearchForInitialization(F[0], F[1], prev, m12, 100);
+            {
+                ORB_SLAM2::ORBextractor tx(nf, 1.2f, 8, 20, 7);  // default: pyramid stays in HBM
+                cv::Mat img(h, w, CV_8UC1, im[1].data(), (size_t)w);
+                std::vector<cv::KeyPoint> k;
+                cv::Mat d;
+                tx(img, cv::Mat(), k, d);  // first frame builds the handle (untimed)
+                timed("ORBextractor::operator()", [] {}, [&] { tx(img, cv::Mat(), k, d); },
+                      "Frame::ExtractORB, Frame.cpp:259-265; no host pyramid copy");
+                tx.SetCopyPyramid(true);
+                timed("ORBextractor::operator() + mvImagePyramid host copy", [] {}, [&] { tx(img, cv::Mat(), k, d); },
+                      "ORBGPU_HOST_PYRAMID=1 form");
+                std::vector<cv::Point2f> pv;
+                std::vector<int> mm;
+                timed("ORBmatcher::SearchForInitialization", [&] { pv = prev; },
+                      [&] { matcher.SearchForInitialization(F[0], F[1], pv, mm, 100); },
+                      "Tracking::MonocularInitialization, Tracking.cpp:769");
+            }
             FILE* out = fopen(argv[7], "wb");
             put_frame(out, F[0]);
             put_frame(out, F[1]);
@@ -919,6 +1028,57 @@ int main(int argc, char** argv) {
             fwrite(&lw, 4, 1, out);
             fwrite(&lh, 4, 1, out);
             for (int y = 0; y < lh; ++y) fwrite(L1.ptr<unsigned char>(y), 1, (size_t)lw, out);
+            fclose(out);
+        } catch (const std::exception& e) {
+            fprintf(stderr, "exception: %s\n", e.what());
+            return 3;
+        }
+        return 0;
+    }
+    if (argc >= 9 && !strcmp(argv[1], "stereo")) {
+        const int w = atoi(argv[2]), h = atoi(argv[3]), nf = atoi(argv[4]);
+        const float bf = (float)atof(argv[5]);
+        std::vector<unsigned char> im[2] = {read_file(argv[6]), read_file(argv[7])};
+        if (im[0].size() != (size_t)w * h || im[1].size() != (size_t)w * h) {
+            fprintf(stderr, "bad image size\n");
+            return 2;
+        }
+        try {
+            // Frame.cpp:66-127: mpORBextractorLeft / Right, ExtractORB(0 / 1) on two threads
+            ORB_SLAM2::ORBextractor exL(nf, 1.2f, 8, 20, 7), exR(nf, 1.2f, 8, 20, 7);
+            cv::Mat imL(h, w, CV_8UC1, im[0].data(), (size_t)w), imR(h, w, CV_8UC1, im[1].data(), (size_t)w);
+            std::vector<cv::KeyPoint> kL, kR;
+            cv::Mat dL, dR;
+            std::vector<float> uR, dep;
+            auto frame = [&] {
+                std::thread tl([&] { exL(imL, cv::Mat(), kL, dL); });
+                std::thread tr([&] { exR(imR, cv::Mat(), kR, dR); });
+                tl.join();
+                tr.join();
+                ORB_SLAM2::ComputeStereoMatchesGPU(&exL, &exR, kL, dL, kR, dR, bf, 0.0f, uR, dep);
+            };
+            frame();
+            timed("stereo Frame: ORBextractor L || R + ComputeStereoMatches", [] {}, frame,
+                  "Frame.cpp:84-98 (two extraction threads, then the GPU stereo match)");
+            timed("ComputeStereoMatches", [] {}, [&] {
+                ORB_SLAM2::ComputeStereoMatchesGPU(&exL, &exR, kL, dL, kR, dR, bf, 0.0f, uR, dep);
+            }, "Frame.cpp:540-748 on the HBM pyramids");
+            FILE* out = fopen(argv[8], "wb");
+            for (int f = 0; f < 2; ++f) {
+                const std::vector<cv::KeyPoint>& k = f ? kR : kL;
+                const cv::Mat& d = f ? dR : dL;
+                const int n = (int)k.size();
+                fwrite(&n, 4, 1, out);
+                for (const cv::KeyPoint& q : k) {
+                    const float v[5] = {q.pt.x, q.pt.y, q.size, q.angle, q.response};
+                    fwrite(v, 4, 5, out);
+                    fwrite(&q.octave, 4, 1, out);
+                    fwrite(&q.class_id, 4, 1, out);
+                }
+                for (int i = 0; i < n; ++i) fwrite(d.ptr<unsigned char>(i), 1, 32, out);
+            }
+            fwrite(uR.data(), 4, uR.size(), out);
+            fwrite(dep.data(), 4, dep.size(), out);
             fclose(out);
         } catch (const std::exception& e) {
             fprintf(stderr, "exception: %s\n", e.what());

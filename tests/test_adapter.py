@@ -96,28 +96,9 @@ def test_adapter_extract_and_match_vs_oracle(exe, tmp_path):
 F32 = np.float32
 
 
-def _frame_blob(tgt, sigma2=None):
-    """read_frame() layout of adapter_main.cpp"""
-    k = np.ascontiguousarray(tgt["kps"])
-    n = len(k)
-    sf = np.asarray(tgt["scale_factors"], F32)
-    s2 = np.asarray(sigma2 if sigma2 is not None else sf * sf, F32)
-    ur = tgt.get("u_right")
-    ur = np.full(n, -1, F32) if ur is None else np.asarray(ur, F32)
-    g = np.array([tgt[f] for f in ("min_x", "max_x", "min_y", "max_y", "fx", "fy", "cx", "cy", "bf", "b")], F32)
-    T = np.asarray(tgt["Tcw"], F32).reshape(4, 4)
-    return b"".join([struct.pack("<i", n), k.tobytes(), np.ascontiguousarray(tgt["desc"], np.uint8).tobytes(),
-                     ur.tobytes(), g.tobytes(), struct.pack("<if", len(sf), float(tgt["log_scale_factor"])),
-                     sf.tobytes(), s2.tobytes(), T.tobytes()])
-
-
-def _points_blob(p):
-    n = len(p["flags"])
-    z = lambda k, w: np.zeros((n, w), F32) if p.get(k) is None else np.asarray(p[k], F32).reshape(n, w)  # noqa: E731
-    lvl = np.zeros(n, np.int32) if p.get("track_level") is None else np.asarray(p["track_level"], np.int32)
-    return b"".join([struct.pack("<i", n), np.asarray(p["flags"], np.int32).tobytes(), z("pos", 3).tobytes(),
-                     z("normal", 3).tobytes(), np.ascontiguousarray(p["desc"], np.uint8).tobytes(),
-                     z("min_dist", 1).tobytes(), z("max_dist", 1).tobytes(), z("track", 4).tobytes(), lvl.tobytes()])
+from tools.adapter_io import bow_frame_blob as _bow_frame_blob  # noqa: E402
+from tools.adapter_io import frame_blob as _frame_blob  # noqa: E402
+from tools.adapter_io import points_blob as _points_blob  # noqa: E402
 
 
 def _run(exe, tmp_path, mode, blob, *args):
@@ -164,19 +145,6 @@ def test_adapter_orbmatcher_search_by_projection(exe, tmp_path, variant, th, kw,
     assert nm == nm_r
     np.testing.assert_array_equal(got, want)
     assert nm_r > 30
-
-
-def _bow_frame_blob(desc, angle, mp_state, fv):
-    nodes = np.array(sorted(fv), np.int32)
-    offs = np.zeros(len(nodes) + 1, np.int32)
-    feats = []
-    for i, k in enumerate(nodes):
-        feats += list(fv[int(k)])
-        offs[i + 1] = len(feats)
-    return b"".join([struct.pack("<i", len(desc)), np.ascontiguousarray(desc, np.uint8).tobytes(),
-                     np.asarray(angle, F32).tobytes(), np.asarray(mp_state, np.uint8).tobytes(),
-                     struct.pack("<i", len(nodes)), nodes.tobytes(), offs.tobytes(),
-                     np.array(feats, np.int32).tobytes()])
 
 
 @pytest.mark.gpu
@@ -635,3 +603,45 @@ def test_adapter_orb_vocabulary(exe, tmp_path, scoring, weighting, fmt):
         bows.append(rbow)
     s, = struct.unpack_from("<d", buf, o)
     assert s == bow_ref.bow_score(scoring, bows[0], bows[1])[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,nf,bf,base", [(752, 480, 1200, 47.90639384423901, 18.0),
+                                            (1241, 376, 2000, 0.54 * 718.856, 30.0)])
+def test_adapter_stereo_frame_vs_oracle(exe, tmp_path, w, h, nf, bf, base):
+    """The stereo Frame through the drop-in classes: two ORBextractor objects
+    on two threads, then ComputeStereoMatchesGPU on their HBM pyramids
+    (StereoMatcher.h, orbgpu_stereo_matches_pair) vs the oracle stereo Frame
+    (two oracle extractors + oracle/stereo_ref.cpp), bit-exact"""
+    pair = synth.stereo_stream(1, w, h, 0x5E7, base)[0]
+    (tmp_path / "l.raw").write_bytes(pair[0].tobytes())
+    (tmp_path / "r.raw").write_bytes(pair[1].tobytes())
+    out = tmp_path / "st.bin"
+    r = subprocess.run([exe, "stereo", str(w), str(h), str(nf), repr(float(np.float32(bf))), str(tmp_path / "l.raw"),
+                        str(tmp_path / "r.raw"), str(out)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    buf = out.read_bytes()
+    kl, dl, off = _read_frame(buf, 0)
+    kr, dr, off = _read_frame(buf, off)
+    ur = np.frombuffer(buf, np.float32, len(kl), off)
+    dp = np.frombuffer(buf, np.float32, len(kl), off + 4 * len(kl))
+    exL, exR = orbref.Extractor(nf), orbref.Extractor(nf)
+    rk = orbref.stereo_frame(exL, exR, pair[0], pair[1], np.float32(bf))
+    assert kl.tobytes() == rk[0].tobytes() and np.array_equal(dl, rk[1])
+    assert kr.tobytes() == rk[2].tobytes() and np.array_equal(dr, rk[3])
+    assert ur.tobytes() == rk[4].tobytes() and dp.tobytes() == rk[5].tobytes()
+    assert (ur >= 0).mean() > 0.3
+
+
+def test_adapter_initializer_fewer_than_8_matches_returns_false(exe, tmp_path):
+    """Initialize with < 8 matches returns false (no throw out of Tracking's
+    thread; the reference's draws would index an empty vector).  Needs no GPU:
+    the check runs before any device call."""
+    kp = np.random.default_rng(0).uniform(0, 400, (20, 2)).astype(F32)
+    m12 = np.full(20, -1, np.int32)
+    m12[:7] = np.arange(7)
+    blob = b"".join([np.eye(3, dtype=F32).tobytes(), struct.pack("<i", 20), kp.tobytes(), struct.pack("<i", 20),
+                     kp.tobytes(), m12.tobytes()])
+    buf = _run(exe, tmp_path, "init", blob)
+    ok, = struct.unpack_from("<i", buf, 0)
+    assert ok == 0

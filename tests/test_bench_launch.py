@@ -1,0 +1,117 @@
+"""bench.py's multi-rank path end to end on the CPU:
+
+`python bench.py --gpus 2 --cpu-dry-run tests/dryrun_orbgpu.py ...` goes
+through the same launcher a driver's `bench.py --gpus N` uses (no
+WORLD_SIZE -> a torchrun child with N ranks, gloo here instead of RCCL), the
+same per-rank chunking, boundary exchange and gather to rank 0 as the GPU
+run, with the CPU oracle standing in for the kernels.  Rank 0 dumps what it
+gathered; the test recomputes the whole stream in one process and requires
+equality:
+
+* mono: every frame's keypoints / descriptors and SearchForInitialization
+  (t-1, t) matches, including the pairs that straddle two ranks' chunks and
+  two steps;
+* stereo (EuRoC geometry): every pair's L/R keypoints, descriptors and the
+  ComputeStereoMatches uRight / depth, pairs on both sides of a chunk
+  boundary;
+* the JSON line reports n_gpus == world_size_checked == 2.
+"""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+ENGINE = ROOT / "tests" / "dryrun_orbgpu.py"
+
+
+def _run_bench(tmp_path, *args, timeout=420):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.pop("LOCAL_RANK", None)
+    env["OMP_NUM_THREADS"] = "2"
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--cpu-dry-run", str(ENGINE), "--dump",
+           str(tmp_path), "--no-cpu-baseline", "--no-extras", *args]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=str(ROOT))
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-3000:]
+    return json.loads(lines[0])
+
+
+def test_gpus_flag_rejects_mismatched_world_size():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--cpu-dry-run", str(ENGINE)],
+                         capture_output=True, text=True, timeout=120, env=env, cwd=str(ROOT))
+    assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr
+
+
+def test_mono_stream_two_ranks_equals_single_process(tmp_path):
+    import orbref
+    import shard
+    import synth
+    import torch
+    world, B, steps = 2, 2, 2
+    line = _run_bench(tmp_path, "--config", "mono640", "--batch", str(B), "--steps", str(steps), "--warmup", "0")
+    assert line["n_gpus"] == 2 and line["world_size_checked"] == 2
+    assert line["config"]["frames_per_gpu_per_step"] == B
+    got = np.load(tmp_path / "mono_640x480.npz")
+    n_frames = world * B * steps
+    assert list(got["units"]) == list(range(n_frames))
+    frames = {}
+    for s in range(steps):
+        for r in range(world):
+            ids = shard.chunk_frames(s, r, world, B)
+            imgs = synth.torch_stream(B, 640, 480, device="cpu", pitch=640, bounded=True, t0=ids[0])
+            for b, f in enumerate(ids):
+                frames[f] = imgs[b].numpy()
+    ex = orbref.Extractor(1000)
+    prev = None
+    cross = 0
+    for f in range(n_frames):
+        k, d = ex.extract(frames[f])
+        n = len(k)
+        assert got["count"][f] == n, f
+        assert got["kps"][f][:n].tobytes() == k.tobytes(), f
+        assert np.array_equal(got["desc"][f][:n], d), f
+        if prev is None:
+            nm, m12 = 0, np.full(n, -1, np.int32)
+        else:
+            nm, m12, _ = orbref.search_for_initialization(prev[0], prev[1], k, d, 640, 480)
+        assert got["nmatch"][f] == nm, f
+        if prev is not None:
+            assert np.array_equal(got["m12"][f][:len(prev[0])], m12), f
+        cross += f % B == 0 and f > 0 and nm > 0
+        prev = (k, d)
+    assert cross == n_frames // B - 1  # every chunk's first frame matched against another rank's / step's last
+
+
+def test_stereo_pairs_two_ranks_equal_single_process(tmp_path):
+    import orbref
+    import shard
+    import synth
+    world, P = 2, 2
+    line = _run_bench(tmp_path, "--config", "euroc_stereo", "--batch", str(P), "--steps", "1", "--warmup", "0")
+    assert line["n_gpus"] == 2 and line["world_size_checked"] == 2 and line["unit"] == "pairs/s"
+    got = np.load(tmp_path / "stereo_752x480.npz")
+    assert list(got["units"]) == list(range(world * P))
+    exL, exR = orbref.Extractor(1200), orbref.Extractor(1200)
+    for r in range(world):
+        ids = shard.chunk_frames(0, r, world, P)
+        imgs = synth.torch_stereo_stream(P, 752, 480, 18.0, device="cpu", t0=ids[0], pitch=752)
+        for p, pair in enumerate(ids):
+            kl, dl, kr, dr, ur, dp = orbref.stereo_frame(exL, exR, imgs[2 * p].numpy(), imgs[2 * p + 1].numpy(),
+                                                         47.90639384423901)
+            c = got["count"][pair]
+            assert (c[0], c[1]) == (len(kl), len(kr)), pair
+            assert got["kps"][pair][0][:len(kl)].tobytes() == kl.tobytes()
+            assert got["kps"][pair][1][:len(kr)].tobytes() == kr.tobytes()
+            assert np.array_equal(got["desc"][pair][1][:len(kr)], dr)
+            assert got["uright"][pair][:len(kl)].tobytes() == ur.tobytes()
+            assert got["depth"][pair][:len(kl)].tobytes() == dp.tobytes()
+            assert (ur >= 0).sum() > 0.3 * len(kl)  # a real stereo scene
