@@ -14,6 +14,9 @@
  *            F = /root/reference/ORB-SLAM2/src/Frame.cpp.
  */
 #include "orbref.h"
+#include "octree_faithful.h"
+
+thread_local h2::Heap* h2::g_heap = nullptr;
 
 #include <algorithm>
 #include <cfloat>
@@ -400,7 +403,36 @@ void split_node(const QNode& p, const std::vector<Cand>& cand, QNode ch[4]) {
 
 int g_tiebreak_mode = 0;
 
+std::vector<int> distribute_octree_faithful(const std::vector<Cand>& cand, int minX, int maxX, int minY, int maxY,
+                                           int N, bool model) {
+    // modes 3 / 4 / 5: the reference's allocation pattern (octree_faithful.h)
+    std::vector<h2::KP28> keys(cand.size());
+    for (size_t k = 0; k < cand.size(); ++k)
+        keys[k] = h2::KP28{(float)cand[k].x, (float)cand[k].y, 7.f, -1.f, (float)cand[k].score, 0, (int)k};
+    h2::Heap heap;
+    heap.model = model;
+    h2::g_heap = &heap;
+    std::vector<int> kept = h2::distribute(keys, minX, maxX, minY, maxY, N);
+    h2::g_heap = nullptr;
+    return kept;
+}
+
 std::vector<int> distribute_octree(const std::vector<Cand>& cand, int minX, int maxX, int minY, int maxY, int N) {
+    if (g_tiebreak_mode >= 3) {
+        if (g_tiebreak_mode == 4) {  // perturb the heap first: the same sizes, a different free-list state
+            static thread_local unsigned s = 12345;
+            std::vector<void*> held;
+            for (int i = 0; i < 64; ++i) {
+                s = s * 1103515245u + 12345u;
+                held.push_back(std::malloc(((s >> 16) % 12 == 0) ? 72 + 16 : 28 * (1 + (s >> 20) % 64)));
+            }
+            for (size_t i = 0; i < held.size(); i += 2) std::free(held[i]);
+            std::vector<int> kept = distribute_octree_faithful(cand, minX, maxX, minY, maxY, N, false);
+            for (size_t i = 1; i < held.size(); i += 2) std::free(held[i]);
+            return kept;
+        }
+        return distribute_octree_faithful(cand, minX, maxX, minY, maxY, N, g_tiebreak_mode == 5);
+    }
     const int nIni = (int)std::round((float)(maxX - minX) / (float)(maxY - minY));
     const float hX = (float)(maxX - minX) / nIni;
     std::list<QNode> nodes;

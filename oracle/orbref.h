@@ -41,9 +41,12 @@ orbref_extractor* orbref_create(int nfeatures, float scale_factor, int nlevels,
                                 int ini_th_fast, int min_th_fast);
 void orbref_destroy(orbref_extractor* ex);
 /* DistributeOctTree tie-break among equal-size nodes: 0 = creation sequence
- * (the spec, default), 1 = reversed sequence, 2 = heap address of the list
- * node (what the reference's sort of (size, ExtractorNode*) does).  For the
- * H2 measurement only (tools/h2_tiebreak.py); process-global. */
+ * (the spec, default), 1 = reversed sequence, 2 = heap address of the
+ * oracle's own list node, 3 = heap address under the REFERENCE'S allocation
+ * pattern (octree_faithful.h: ExtractorNode layout, reserve / copy / erase
+ * sequence) in this process's glibc heap, 4 = the same after a heap
+ * perturbation, 5 = the same pattern under a deterministic glibc model.  For
+ * the H2 measurement only (tools/h2_tiebreak.py); process-global. */
 void orbref_set_tiebreak(int mode);
 
 /* ORBextractor::operator()  (ORBextractor.cpp:1053-1117).

@@ -1,0 +1,491 @@
+// epnp_wave.h -- EPnP (PnPsolver::compute_pose and helpers,
+// src/PnPsolver.cpp:423-1080) for a GROUP of G lanes working together
+// (G = 16: four minimal-set hypotheses per wave; G = 64: Refine over all
+// inliers on one wave).  Same spec as the one-thread epnp.h (control points,
+// sign normalisation, canonical null space, three beta approximations each
+// refined by 5 Gauss-Newton steps with the reference's qr_solve, the
+// minimum-error choice); what changes is who computes what:
+//   * every per-correspondence loop (centroid, covariance, M^T M, the camera
+//     centroid and ABt of compute_R_and_t, the reprojection error) is split
+//     over the group's lanes and reduced with xor shuffles;
+//   * M^T M is assembled from 40 group sums (its 3x3 blocks are fu^2,
+//     fv^2, fu, fv multiples of sums of alpha_k alpha_l weighted by 1,
+//     (uc - u), (vc - v) and their squares) and its eigenvectors come from a
+//     one-sided Jacobi with the 12 rows on 12 lanes (lane r also carries
+//     row r of V); a column pair's three dot products are group reductions;
+//   * the dense 3x3 / 6xk pieces run redundantly on every lane (identical
+//     inputs, identical results, no broadcast needed); L (6x10) and the four
+//     null-space vectors live in the group's LDS scratch.
+// Reduction order differs from the sequential sums of epnp.h, so results
+// agree with the oracle to the pose tolerance of tests/test_pnp.py, like
+// epnp.h does.  (Round 2: one thread per hypothesis, 512 VGPRs and 2.9 KB of
+// scratch per thread, 2.2 ms per 16-solver batch.)
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "epnp.h"
+
+namespace orbgpu {
+namespace epnp {
+
+// per-group LDS scratch (doubles)
+constexpr int kWaveScratch = 144 + 48 + 60;
+
+template <int G>
+__device__ __forceinline__ double gsum(double x) {
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+// LDS writes of the group visible to its other lanes (one wave: in-order LDS,
+// so a counter wait and a wave barrier suffice; no block barrier, so a single
+// wave of a larger block can run this)
+#define EPNP_GROUP_SYNC()                          \
+    do {                                           \
+        __builtin_amdgcn_s_waitcnt(0xC07F);        \
+        __builtin_amdgcn_wave_barrier();           \
+    } while (0)
+
+// canonicalize_null_space (epnp.h) for k null vectors held as ut4[c] = ut row
+// 11 - c, on one lane, with its small matrices in LDS (scr: >= 80 doubles) so
+// they cost no registers
+__device__ inline void canonicalize_null_space4(double* ut4, int k, double* scr) {
+    double* A = scr;       // k x 2k  (row stride 8)
+    double* B = scr + 32;  // 12 x k  (row stride 4)
+    for (int i = 0; i < k; ++i)  // [W^T V | I]
+        for (int j = 0; j < k; ++j) {
+            double acc = 0.0;
+            for (int r = 0; r < 12; ++r) acc += null_w(r, i) * ut4[12 * j + r];
+            A[8 * i + j] = acc;
+            A[8 * i + k + j] = i == j ? 1.0 : 0.0;
+        }
+    for (int c = 0; c < k; ++c) {  // Gauss-Jordan with partial pivoting
+        int p = c;
+        for (int r = c + 1; r < k; ++r)
+            if (fabs(A[8 * r + c]) > fabs(A[8 * p + c])) p = r;
+        if (A[8 * p + c] == 0.0) return;  // degenerate: keep the eigenvectors
+        if (p != c)
+            for (int j = 0; j < 2 * k; ++j) {
+                const double tmp = A[8 * c + j];
+                A[8 * c + j] = A[8 * p + j];
+                A[8 * p + j] = tmp;
+            }
+        const double inv = 1.0 / A[8 * c + c];
+        for (int j = 0; j < 2 * k; ++j) A[8 * c + j] *= inv;
+        for (int r = 0; r < k; ++r)
+            if (r != c) {
+                const double f = A[8 * r + c];
+                for (int j = 0; j < 2 * k; ++j) A[8 * r + j] -= f * A[8 * c + j];
+            }
+    }
+    for (int r = 0; r < 12; ++r)
+        for (int c = 0; c < k; ++c) {
+            double acc = 0.0;
+            for (int j = 0; j < k; ++j) acc += ut4[12 * j + r] * A[8 * j + k + c];
+            B[4 * r + c] = acc;
+        }
+    for (int c = 0; c < k; ++c) {  // modified Gram-Schmidt, columns in order
+        for (int j = 0; j < c; ++j) {
+            double d = 0.0;
+            for (int r = 0; r < 12; ++r) d += B[4 * r + j] * B[4 * r + c];
+            for (int r = 0; r < 12; ++r) B[4 * r + c] -= d * B[4 * r + j];
+        }
+        double nrm = 0.0;
+        for (int r = 0; r < 12; ++r) nrm += B[4 * r + c] * B[4 * r + c];
+        nrm = sqrt(nrm);
+        for (int r = 0; r < 12; ++r) B[4 * r + c] /= nrm;
+    }
+    for (int c = 0; c < k; ++c)
+        for (int r = 0; r < 12; ++r) ut4[12 * c + r] = B[4 * r + c];
+}
+
+// r = the lane's index in its group; lds = the group's kWaveScratch doubles.
+// Every lane of the group returns the same pose and error.
+template <int G, class Src>
+__device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& out, int r, double* lds) {
+    const int n = src.count();
+    double* s_mtm = lds;        // 12 x 12
+    double* s_ut4 = lds + 144;  // 4 x 12: null vectors, ut row 11 - c
+    double* s_L = lds + 192;    // 6 x 10
+    double cws[4][3];
+    // choose_control_points (:423-455)
+    {
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+        for (int i = r; i < n; i += G) {
+            double pw[3], u, v;
+            src.get(i, pw, u, v);
+            a0 += pw[0];
+            a1 += pw[1];
+            a2 += pw[2];
+        }
+        cws[0][0] = gsum<G>(a0) / n;
+        cws[0][1] = gsum<G>(a1) / n;
+        cws[0][2] = gsum<G>(a2) / n;
+    }
+    {
+        double c[6] = {0, 0, 0, 0, 0, 0};  // xx xy xz yy yz zz
+        for (int i = r; i < n; i += G) {
+            double pw[3], u, v;
+            src.get(i, pw, u, v);
+            const double d0 = pw[0] - cws[0][0], d1 = pw[1] - cws[0][1], d2 = pw[2] - cws[0][2];
+            c[0] += d0 * d0;
+            c[1] += d0 * d1;
+            c[2] += d0 * d2;
+            c[3] += d1 * d1;
+            c[4] += d1 * d2;
+            c[5] += d2 * d2;
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) c[k] = gsum<G>(c[k]);
+        double c3[9] = {c[0], c[1], c[2], c[1], c[3], c[4], c[2], c[4], c[5]};
+        double dc[3], uct[9];
+        sym_eig_desc<3>(c3, dc, uct);
+        for (int i = 0; i < 3; ++i) {  // spec: largest-magnitude component positive
+            int m = 0;
+            for (int j = 1; j < 3; ++j)
+                if (fabs(uct[3 * i + j]) > fabs(uct[3 * i + m])) m = j;
+            if (uct[3 * i + m] < 0)
+                for (int j = 0; j < 3; ++j) uct[3 * i + j] = -uct[3 * i + j];
+        }
+        for (int i = 1; i < 4; ++i) {
+            const double k = sqrt(dc[i - 1] / n);
+            for (int j = 0; j < 3; ++j) cws[i][j] = cws[0][j] + k * uct[3 * (i - 1) + j];
+        }
+    }
+    // compute_barycentric_coordinates (:457-481): CC_inv = pinv(CC)
+    double ci[9];
+    {
+        double cc[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 1; j < 4; ++j) cc[3 * i + j - 1] = cws[j][i] - cws[0][i];
+        double s[3], v[9];
+        svd_hestenes<3, 3>(cc, s, v);
+        const double thr = fmax(fmax(s[0], s[1]), s[2]) * 2.220446049250313e-16 * 3;
+        for (int rr = 0; rr < 3; ++rr)
+            for (int c = 0; c < 3; ++c) {
+                double acc = 0.0;
+                for (int j = 0; j < 3; ++j)
+                    if (s[j] > thr) acc += v[rr * 3 + j] * cc[c * 3 + j] / (s[j] * s[j]);
+                ci[rr * 3 + c] = acc;
+            }
+    }
+    auto alphas = [&](const double* pw, double* a) {
+        for (int j = 0; j < 3; ++j)
+            a[1 + j] = ci[3 * j] * (pw[0] - cws[0][0]) + ci[3 * j + 1] * (pw[1] - cws[0][1]) +
+                       ci[3 * j + 2] * (pw[2] - cws[0][2]);
+        a[0] = 1.0f - a[1] - a[2] - a[3];
+    };
+    // M^T M (fill_M :483-497, cvMulTransposed): per (k <= l) sums of a_k a_l times
+    // 1, (uc - u), (vc - v), (uc - u)^2 + (vc - v)^2
+    {
+        double S1[10], S2[10], S3[10], S4[10];
+#pragma unroll
+        for (int q = 0; q < 10; ++q) S1[q] = S2[q] = S3[q] = S4[q] = 0.0;
+        for (int i = r; i < n; i += G) {
+            double pw[3], u, v, a[4];
+            src.get(i, pw, u, v);
+            alphas(pw, a);
+            const double du = cam.uc - u, dv = cam.vc - v, dd = du * du + dv * dv;
+            int q = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int l = k; l < 4; ++l, ++q) {
+                    const double aa = a[k] * a[l];
+                    S1[q] += aa;
+                    S2[q] += aa * du;
+                    S3[q] += aa * dv;
+                    S4[q] += aa * dd;
+                }
+        }
+#pragma unroll
+        for (int q = 0; q < 10; ++q) {
+            S1[q] = gsum<G>(S1[q]);
+            S2[q] = gsum<G>(S2[q]);
+            S3[q] = gsum<G>(S3[q]);
+            S4[q] = gsum<G>(S4[q]);
+        }
+        if (r == 0) {
+            const double fu = cam.fu, fv = cam.fv;
+            int q = 0;
+            for (int k = 0; k < 4; ++k)
+                for (int l = k; l < 4; ++l, ++q) {
+                    const double blk[9] = {fu * fu * S1[q], 0.0, fu * S2[q], 0.0, fv * fv * S1[q], fv * S3[q],
+                                           fu * S2[q], fv * S3[q], S4[q]};
+                    for (int i = 0; i < 3; ++i)
+                        for (int j = 0; j < 3; ++j) {
+                            s_mtm[(3 * k + i) * 12 + 3 * l + j] = blk[3 * i + j];
+                            s_mtm[(3 * l + j) * 12 + 3 * k + i] = blk[3 * i + j];
+                        }
+                }
+        }
+    }
+    EPNP_GROUP_SYNC();
+    // eigenvectors of M^T M: one-sided Jacobi on the symmetric PSD matrix, rows on lanes
+    {
+        double a[12], v[12];
+#pragma unroll
+        for (int c = 0; c < 12; ++c) {
+            a[c] = r < 12 ? s_mtm[r * 12 + c] : 0.0;
+            v[c] = (r == c) ? 1.0 : 0.0;
+        }
+        for (int sweep = 0; sweep < 60; ++sweep) {
+            bool rotated = false;
+#pragma unroll
+            for (int p = 0; p < 11; ++p)
+#pragma unroll
+                for (int q = p + 1; q < 12; ++q) {
+                    const double alpha = gsum<G>(a[p] * a[p]);
+                    const double beta = gsum<G>(a[q] * a[q]);
+                    const double gamma = gsum<G>(a[p] * a[q]);
+                    double c = 1.0, sn = 0.0;
+                    if (!(fabs(gamma) <= 1e-15 * sqrt(alpha * beta) || gamma == 0.0)) {
+                        rotated = true;
+                        const double zeta = (beta - alpha) / (2.0 * gamma);
+                        const double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                        c = 1.0 / sqrt(1.0 + t * t);
+                        sn = c * t;
+                    }
+                    const double x = a[p], y = a[q];
+                    a[p] = c * x - sn * y;
+                    a[q] = sn * x + c * y;
+                    const double vx = v[p], vy = v[q];
+                    v[p] = c * vx - sn * vy;
+                    v[q] = sn * vx + c * vy;
+                }
+            if (!__any(rotated)) break;  // wave-uniform: converged groups rotate by the identity
+        }
+        double lam[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) lam[j] = sqrt(gsum<G>(a[j] * a[j]));
+        // descending order, stable (sym_eig_desc's insertion sort); the four last ranks
+        // are the null-space vectors: rank 11 - c -> ut4[c]
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            int rank = 0;
+#pragma unroll
+            for (int i = 0; i < 12; ++i) rank += (lam[i] > lam[j]) || (i < j && lam[i] == lam[j]);
+            if (rank >= 8 && r < 12) s_ut4[12 * (11 - rank) + r] = v[j];
+        }
+    }
+    EPNP_GROUP_SYNC();
+    {
+        const int k = 12 - 2 * n;
+        if (k > 0 && r == 0) canonicalize_null_space4(s_ut4, k < 4 ? k : 4, s_mtm);  // M^T M is consumed
+    }
+    EPNP_GROUP_SYNC();
+    // compute_L_6x10 (:863-898), compute_rho (:900-908)
+    double rho[6];
+    if (r == 0) {
+        double dv[4][6][3];
+        for (int i = 0; i < 4; ++i) {
+            const double* vv = s_ut4 + 12 * i;
+            int a = 0, b = 1;
+            for (int j = 0; j < 6; ++j) {
+                for (int k = 0; k < 3; ++k) dv[i][j][k] = vv[3 * a + k] - vv[3 * b + k];
+                if (++b > 3) {
+                    ++a;
+                    b = a + 1;
+                }
+            }
+        }
+        for (int i = 0; i < 6; ++i) {
+            double* row = s_L + 10 * i;
+            row[0] = dot3(dv[0][i], dv[0][i]);
+            row[1] = 2.0f * dot3(dv[0][i], dv[1][i]);
+            row[2] = dot3(dv[1][i], dv[1][i]);
+            row[3] = 2.0f * dot3(dv[0][i], dv[2][i]);
+            row[4] = 2.0f * dot3(dv[1][i], dv[2][i]);
+            row[5] = dot3(dv[2][i], dv[2][i]);
+            row[6] = 2.0f * dot3(dv[0][i], dv[3][i]);
+            row[7] = 2.0f * dot3(dv[1][i], dv[3][i]);
+            row[8] = 2.0f * dot3(dv[2][i], dv[3][i]);
+            row[9] = dot3(dv[3][i], dv[3][i]);
+        }
+    }
+    rho[0] = dist2(cws[0], cws[1]);
+    rho[1] = dist2(cws[0], cws[2]);
+    rho[2] = dist2(cws[0], cws[3]);
+    rho[3] = dist2(cws[1], cws[2]);
+    rho[4] = dist2(cws[1], cws[3]);
+    rho[5] = dist2(cws[2], cws[3]);
+    EPNP_GROUP_SYNC();
+    const double* L = s_L;
+    auto gauss_newton = [&](double* betas) {  // :942-963 + compute_A_and_b_gauss_newton :910-940
+        for (int it = 0; it < 5; ++it) {
+            double A[24], b[6], x[4];
+            for (int i = 0; i < 6; ++i) {
+                const double* rr = L + 10 * i;
+                double* a = A + 4 * i;
+                a[0] = 2 * rr[0] * betas[0] + rr[1] * betas[1] + rr[3] * betas[2] + rr[6] * betas[3];
+                a[1] = rr[1] * betas[0] + 2 * rr[2] * betas[1] + rr[4] * betas[2] + rr[7] * betas[3];
+                a[2] = rr[3] * betas[0] + rr[4] * betas[1] + 2 * rr[5] * betas[2] + rr[8] * betas[3];
+                a[3] = rr[6] * betas[0] + rr[7] * betas[1] + rr[8] * betas[2] + 2 * rr[9] * betas[3];
+                b[i] = rho[i] - (rr[0] * betas[0] * betas[0] + rr[1] * betas[0] * betas[1] +
+                                 rr[2] * betas[1] * betas[1] + rr[3] * betas[0] * betas[2] +
+                                 rr[4] * betas[1] * betas[2] + rr[5] * betas[2] * betas[2] +
+                                 rr[6] * betas[0] * betas[3] + rr[7] * betas[1] * betas[3] +
+                                 rr[8] * betas[2] * betas[3] + rr[9] * betas[3] * betas[3]);
+            }
+            qr_solve_6x4(A, b, x);
+            for (int i = 0; i < 4; ++i) betas[i] += x[i];
+        }
+    };
+    // compute_R_and_t (:735-745) with the per-correspondence sums over the group
+    auto r_and_t = [&](const double* betas, Pose& P) -> double {
+        double ccs[4][3];
+        for (int i = 0; i < 4; ++i) ccs[i][0] = ccs[i][1] = ccs[i][2] = 0.0f;
+        for (int i = 0; i < 4; ++i) {
+            const double* vv = s_ut4 + 12 * i;
+            for (int j = 0; j < 4; ++j)
+                for (int k = 0; k < 3; ++k) ccs[j][k] += betas[i] * vv[3 * j + k];
+        }
+        auto pc_of = [&](const double* pw, double* pc) {
+            double a[4];
+            alphas(pw, a);
+            for (int j = 0; j < 3; ++j)
+                pc[j] = a[0] * ccs[0][j] + a[1] * ccs[1][j] + a[2] * ccs[2][j] + a[3] * ccs[3][j];
+        };
+        {  // solve_for_sign (:715-733): the sign of point 0's depth
+            double pw[3], u, v, pc[3];
+            src.get(0, pw, u, v);
+            pc_of(pw, pc);
+            if (pc[2] < 0.0)
+                for (int i = 0; i < 4; ++i)
+                    for (int j = 0; j < 3; ++j) ccs[i][j] = -ccs[i][j];
+        }
+        double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
+        for (int i = r; i < n; i += G) {
+            double pw[3], u, v, pc[3];
+            src.get(i, pw, u, v);
+            pc_of(pw, pc);
+            for (int j = 0; j < 3; ++j) {
+                pc0[j] += pc[j];
+                pw0[j] += pw[j];
+            }
+        }
+        for (int j = 0; j < 3; ++j) {
+            pc0[j] = gsum<G>(pc0[j]) / n;
+            pw0[j] = gsum<G>(pw0[j]) / n;
+        }
+        double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i = r; i < n; i += G) {
+            double pw[3], u, v, pc[3];
+            src.get(i, pw, u, v);
+            pc_of(pw, pc);
+            for (int j = 0; j < 3; ++j) {
+                abt[3 * j] += (pc[j] - pc0[j]) * (pw[0] - pw0[0]);
+                abt[3 * j + 1] += (pc[j] - pc0[j]) * (pw[1] - pw0[1]);
+                abt[3 * j + 2] += (pc[j] - pc0[j]) * (pw[2] - pw0[2]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 9; ++k) abt[k] = gsum<G>(abt[k]);
+        double s[3], vv[9];
+        svd_hestenes<3, 3>(abt, s, vv);  // abt columns = U_j s_j
+        double U[9];
+        for (int rr = 0; rr < 3; ++rr)
+            for (int c = 0; c < 3; ++c) U[rr * 3 + c] = s[c] > 0.0 ? abt[rr * 3 + c] / s[c] : 0.0;
+        double* R = P.R;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) R[3 * i + j] = dot3(U + 3 * i, vv + 3 * j);
+        const double det = R[0] * R[4] * R[8] + R[1] * R[5] * R[6] + R[2] * R[3] * R[7] - R[2] * R[4] * R[6] -
+                           R[1] * R[3] * R[8] - R[0] * R[5] * R[7];
+        if (det < 0) {
+            R[6] = -R[6];
+            R[7] = -R[7];
+            R[8] = -R[8];
+        }
+        P.t[0] = pc0[0] - dot3(R, pw0);
+        P.t[1] = pc0[1] - dot3(R + 3, pw0);
+        P.t[2] = pc0[2] - dot3(R + 6, pw0);
+        double sum2 = 0.0;
+        for (int i = r; i < n; i += G) {
+            double pw[3], u, v;
+            src.get(i, pw, u, v);
+            const double Xc = dot3(R, pw) + P.t[0], Yc = dot3(R + 3, pw) + P.t[1];
+            const double inv_Zc = 1.0 / (dot3(R + 6, pw) + P.t[2]);
+            const double ue = cam.uc + cam.fu * Xc * inv_Zc, ve = cam.vc + cam.fv * Yc * inv_Zc;
+            sum2 += sqrt((u - ue) * (u - ue) + (v - ve) * (v - ve));
+        }
+        return gsum<G>(sum2) / n;
+    };
+    double best_err;
+    auto keep = [&](double e, const Pose& P, bool first) {  // N = 1; err[2] < err[N] -> 2; err[3] < err[N] -> 3
+        if (first || e < best_err) {
+            best_err = e;
+            out = P;
+        }
+    };
+    {  // find_betas_approx_1 (:747-781)
+        double l[24], b4[4], B[4];
+        for (int i = 0; i < 6; ++i) {
+            l[4 * i] = L[10 * i];
+            l[4 * i + 1] = L[10 * i + 1];
+            l[4 * i + 2] = L[10 * i + 3];
+            l[4 * i + 3] = L[10 * i + 6];
+        }
+        svd_solve<6, 4>(l, rho, b4);
+        if (b4[0] < 0) {
+            B[0] = sqrt(-b4[0]);
+            B[1] = -b4[1] / B[0];
+            B[2] = -b4[2] / B[0];
+            B[3] = -b4[3] / B[0];
+        } else {
+            B[0] = sqrt(b4[0]);
+            B[1] = b4[1] / B[0];
+            B[2] = b4[2] / B[0];
+            B[3] = b4[3] / B[0];
+        }
+        gauss_newton(B);
+        Pose P;
+        const double e = r_and_t(B, P);
+        keep(e, P, true);
+    }
+    {  // find_betas_approx_2 (:783-815)
+        double l[18], b3[3], B[4];
+        for (int i = 0; i < 6; ++i)
+            for (int k = 0; k < 3; ++k) l[3 * i + k] = L[10 * i + k];
+        svd_solve<6, 3>(l, rho, b3);
+        if (b3[0] < 0) {
+            B[0] = sqrt(-b3[0]);
+            B[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0;
+        } else {
+            B[0] = sqrt(b3[0]);
+            B[1] = (b3[2] > 0) ? sqrt(b3[2]) : 0.0;
+        }
+        if (b3[1] < 0) B[0] = -B[0];
+        B[2] = 0.0;
+        B[3] = 0.0;
+        gauss_newton(B);
+        Pose P;
+        const double e = r_and_t(B, P);
+        keep(e, P, false);
+    }
+    {  // find_betas_approx_3 (:817-851)
+        double l[30], b5[5], B[4];
+        for (int i = 0; i < 6; ++i)
+            for (int k = 0; k < 5; ++k) l[5 * i + k] = L[10 * i + k];
+        svd_solve<6, 5>(l, rho, b5);
+        if (b5[0] < 0) {
+            B[0] = sqrt(-b5[0]);
+            B[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;
+        } else {
+            B[0] = sqrt(b5[0]);
+            B[1] = (b5[2] > 0) ? sqrt(b5[2]) : 0.0;
+        }
+        if (b5[1] < 0) B[0] = -B[0];
+        B[2] = b5[3] / B[0];
+        B[3] = 0.0;
+        gauss_newton(B);
+        Pose P;
+        const double e = r_and_t(B, P);
+        keep(e, P, false);
+    }
+    return best_err;
+}
+
+}  // namespace epnp
+}  // namespace orbgpu

@@ -7,16 +7,24 @@
 //                          sequential float sums (mean, then mean absolute
 //                          deviation), the block writes the normalised points;
 //                          also the match list (u1, v1, u2, v2) the scorers read.
-//   init_models_kernel     one thread per (iteration, model): the 8 sampled
-//                          normalised pairs, the DLT matrix A in float as
-//                          ComputeH21 (:292-330, 16 x 9) / ComputeF21 (:332-388,
-//                          8 x 9) build it, its right singular vector of the
-//                          smallest singular value (cv::SVDecomp's vt.row(8)) by
-//                          one-sided Jacobi in double, for F the rank-2
-//                          projection (w(2) = 0), then the de-normalisation
-//                          T2inv*Hn*T1 / T2t*Fn*T1 and H12 = H21.inv() with
-//                          OpenCV's float 3x3 products (double accumulation)
-//                          and 3x3 closed-form inverse.
+//   init_models_kernel     16 lanes per (iteration, model), four hypotheses
+//                          per wave: lane r builds row r of the DLT matrix A in
+//                          float as ComputeH21 (:292-330, 16 x 9) /
+//                          ComputeF21 (:332-388, 8 x 9 + zero rows) build it;
+//                          its right singular vector of the smallest singular
+//                          value (cv::SVDecomp's vt.row(8)) by one-sided
+//                          (Hestenes) Jacobi in double with the rows on the
+//                          lanes -- each column pair's three dot products are
+//                          16-lane xor reductions, lane r < 9 carries row r of
+//                          V, converged groups rotate by the identity until
+//                          the whole wave has converged; then the group's
+//                          lane 0 does, for F, the rank-2 projection
+//                          (w(2) = 0), the de-normalisation T2inv*Hn*T1 /
+//                          T2t*Fn*T1 and H12 = H21.inv() with OpenCV's float
+//                          3x3 products (double accumulation) and 3x3
+//                          closed-form inverse.  (Round 2 ran one thread per
+//                          hypothesis with the 16 x 9 and 9 x 9 doubles in
+//                          scratch: 5.1 ms per 200 + 200 hypotheses.)
 // The SVDs are restated (OpenCV's Jacobi SVD in float is not reproducible
 // here), so H/F match the oracle to a tolerance; CheckHomography /
 // CheckFundamental (init.hip) then score them bit-exactly.
@@ -108,59 +116,109 @@ __device__ void inv3(const float* m, float* o) {
     o[8] = (float)((S(0, 0) * S(1, 1) - S(0, 1) * S(1, 0)) * d);
 }
 
-// right singular vector of the smallest singular value of the M x 9 matrix
-// `a` (row-major, destroyed), unit norm, as float
-template <int M>
-__device__ void null_vector(double* a, float* out) {
-    double s[9], v[81];
-    orbgpu::epnp::svd_hestenes<M, 9>(a, s, v);
-    int jmin = 0;
-    for (int j = 1; j < 9; ++j)
-        if (s[j] < s[jmin]) jmin = j;
-    for (int k = 0; k < 9; ++k) out[k] = (float)v[k * 9 + jmin];
-}
+constexpr int kModelThreads = 64;  // one wave = four hypotheses of 16 lanes
+constexpr int kGroups = kModelThreads / 16;
 
-constexpr int kModelThreads = 64;
+__device__ __forceinline__ double group_sum(double x) {  // over the lane's 16-lane group
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
 
 __global__ __launch_bounds__(kModelThreads) void init_models_kernel(const float* __restrict__ work, int n1, int n2,
                                                                     const int* __restrict__ pairs,
                                                                     const int* __restrict__ sets, int n_iter,
                                                                     float* __restrict__ h21, float* __restrict__ h12,
                                                                     float* __restrict__ f21) {
-    const int t = blockIdx.x * kModelThreads + threadIdx.x;
-    if (t >= 2 * n_iter) return;
+    __shared__ double s_null[kGroups][9];
+    const int lane = threadIdx.x, g = lane >> 4, r = lane & 15;
+    const int t_raw = blockIdx.x * kGroups + g;
+    const bool valid = t_raw < 2 * n_iter;
+    const int t = valid ? t_raw : 2 * n_iter - 1;  // idle groups mirror a real one and store nothing
     const bool homography = t < n_iter;
     const int it = homography ? t : t - n_iter;
     const float* pn1 = work;
     const float* pn2 = work + 2 * n1;
     const float* T1 = work + 2 * (n1 + n2);
     const float* T2 = T1 + 9;
-    float u1[8], v1[8], u2[8], v2[8];
-    for (int j = 0; j < 8; ++j) {  // vPn1i[j] = vPn1[mvMatches12[idx].first], vPn2i likewise
-        const int idx = sets[8 * it + j];
-        const int a = pairs[2 * idx], b = pairs[2 * idx + 1];
-        u1[j] = pn1[2 * a];
-        v1[j] = pn1[2 * a + 1];
-        u2[j] = pn2[2 * b];
-        v2[j] = pn2[2 * b + 1];
-    }
-    if (homography) {
-        // ComputeH21 (:292-330): A (16 x 9, float entries), vt.row(8)
-        double A[16 * 9];
-        for (int i = 0; i < 8; ++i) {
-            double* r0 = A + 18 * i;
-            double* r1 = r0 + 9;
-            r0[0] = 0.0; r0[1] = 0.0; r0[2] = 0.0;
-            r0[3] = -u1[i]; r0[4] = -v1[i]; r0[5] = -1.0;
-            r0[6] = __fmul_rn(v2[i], u1[i]); r0[7] = __fmul_rn(v2[i], v1[i]); r0[8] = v2[i];
-            r1[0] = u1[i]; r1[1] = v1[i]; r1[2] = 1.0;
-            r1[3] = 0.0; r1[4] = 0.0; r1[5] = 0.0;
-            r1[6] = -__fmul_rn(u2[i], u1[i]); r1[7] = -__fmul_rn(u2[i], v1[i]); r1[8] = -u2[i];
+    // row r of A (float entries as the reference computes them, held in double)
+    double a[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) a[k] = 0.0;
+    {
+        const int i = homography ? (r >> 1) : r;  // the pair this row comes from
+        if (i < 8) {
+            const int idx = sets[8 * it + i];
+            const int pa = pairs[2 * idx], pb = pairs[2 * idx + 1];
+            const float u1 = pn1[2 * pa], v1 = pn1[2 * pa + 1], u2 = pn2[2 * pb], v2 = pn2[2 * pb + 1];
+            if (homography) {
+                if ((r & 1) == 0) {  // [0 0 0 -u1 -v1 -1 v2*u1 v2*v1 v2]
+                    a[3] = -u1; a[4] = -v1; a[5] = -1.0;
+                    a[6] = __fmul_rn(v2, u1); a[7] = __fmul_rn(v2, v1); a[8] = v2;
+                } else {             // [u1 v1 1 0 0 0 -u2*u1 -u2*v1 -u2]
+                    a[0] = u1; a[1] = v1; a[2] = 1.0;
+                    a[6] = -__fmul_rn(u2, u1); a[7] = -__fmul_rn(u2, v1); a[8] = -u2;
+                }
+            } else {  // [u2*u1 u2*v1 u2 v2*u1 v2*v1 v2 u1 v1 1]
+                a[0] = __fmul_rn(u2, u1); a[1] = __fmul_rn(u2, v1); a[2] = u2;
+                a[3] = __fmul_rn(v2, u1); a[4] = __fmul_rn(v2, v1); a[5] = v2;
+                a[6] = u1; a[7] = v1; a[8] = 1.0;
+            }
         }
-        float Hn[9], T2inv[9], tmp[9], H[9], Hi[9];
-        null_vector<16>(A, Hn);
-        inv3(T2, T2inv);      // T2.inv()
-        mul3(T2inv, Hn, tmp);  // H21i = T2inv*Hn*T1
+    }
+    double v[9];  // row r of V (lanes r < 9)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) v[k] = (r == k) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        bool rotated = false;
+#pragma unroll
+        for (int p = 0; p < 8; ++p)
+#pragma unroll
+            for (int q = p + 1; q < 9; ++q) {
+                const double alpha = group_sum(a[p] * a[p]);
+                const double beta = group_sum(a[q] * a[q]);
+                const double gamma = group_sum(a[p] * a[q]);
+                double c = 1.0, sn = 0.0;
+                if (!(fabs(gamma) <= 1e-15 * sqrt(alpha * beta) || gamma == 0.0)) {
+                    rotated = true;
+                    const double zeta = (beta - alpha) / (2.0 * gamma);
+                    const double tt = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                    c = 1.0 / sqrt(1.0 + tt * tt);
+                    sn = c * tt;
+                }
+                const double x = a[p], y = a[q];
+                a[p] = c * x - sn * y;
+                a[q] = sn * x + c * y;
+                const double vx = v[p], vy = v[q];
+                v[p] = c * vx - sn * vy;
+                v[q] = sn * vx + c * vy;
+            }
+        if (!__any(rotated)) break;
+    }
+    // singular values = column norms; the first smallest decides vt.row(8)
+    int jmin = 0;
+    double smin = 0.0;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        const double sj = sqrt(group_sum(a[j] * a[j]));
+        if (j == 0 || sj < smin) {
+            smin = sj;
+            jmin = j;
+        }
+    }
+    double vj = v[0];
+#pragma unroll
+    for (int j = 1; j < 9; ++j)
+        if (jmin == j) vj = v[j];
+    if (r < 9) s_null[g][r] = vj;
+    __syncthreads();
+    if (r != 0 || !valid) return;
+    float nv[9];
+    for (int k = 0; k < 9; ++k) nv[k] = (float)s_null[g][k];
+    if (homography) {
+        float T2inv[9], tmp[9], H[9], Hi[9];
+        inv3(T2, T2inv);       // T2.inv()
+        mul3(T2inv, nv, tmp);  // H21i = T2inv*Hn*T1
         mul3(tmp, T1, H);
         inv3(H, Hi);           // H12i = H21i.inv()
         for (int k = 0; k < 9; ++k) {
@@ -168,37 +226,25 @@ __global__ __launch_bounds__(kModelThreads) void init_models_kernel(const float*
             h12[9 * it + k] = Hi[k];
         }
     } else {
-        // ComputeF21 (:332-388): A (8 x 9; a zero 9th row for the square
-        // one-sided Jacobi), Fpre = vt.row(8), then the rank-2 projection
-        double A[9 * 9];
-        for (int i = 0; i < 8; ++i) {
-            double* r = A + 9 * i;
-            r[0] = __fmul_rn(u2[i], u1[i]); r[1] = __fmul_rn(u2[i], v1[i]); r[2] = u2[i];
-            r[3] = __fmul_rn(v2[i], u1[i]); r[4] = __fmul_rn(v2[i], v1[i]); r[5] = v2[i];
-            r[6] = u1[i]; r[7] = v1[i]; r[8] = 1.0;
-        }
-        for (int k = 0; k < 9; ++k) A[72 + k] = 0.0;
-        float Fpre[9];
-        null_vector<9>(A, Fpre);
         // SVDecomp(Fpre): w(2) = 0; Fn = u*diag(w)*vt = sum of the two largest
         // singular triples
-        double B[9], s[3], V[9];
-        for (int k = 0; k < 9; ++k) B[k] = Fpre[k];
-        orbgpu::epnp::svd_hestenes<3, 3>(B, s, V);
-        int jmin = 0;
+        double B[9], sv[3], V[9];
+        for (int k = 0; k < 9; ++k) B[k] = nv[k];
+        orbgpu::epnp::svd_hestenes<3, 3>(B, sv, V);
+        int jm = 0;
         for (int j = 1; j < 3; ++j)
-            if (s[j] < s[jmin]) jmin = j;
+            if (sv[j] < sv[jm]) jm = j;
         float Fn[9];
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) {
+        for (int rr = 0; rr < 3; ++rr)
+            for (int cc = 0; cc < 3; ++cc) {
                 double acc = 0.0;
                 for (int j = 0; j < 3; ++j)
-                    if (j != jmin) acc += B[3 * r + j] * V[3 * c + j];  // (U_j s_j) v_j^T
-                Fn[3 * r + c] = (float)acc;
+                    if (j != jm) acc += B[3 * rr + j] * V[3 * cc + j];  // (U_j s_j) v_j^T
+                Fn[3 * rr + cc] = (float)acc;
             }
         float T2t[9], tmp[9], F[9];
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) T2t[3 * r + c] = T2[3 * c + r];
+        for (int rr = 0; rr < 3; ++rr)
+            for (int cc = 0; cc < 3; ++cc) T2t[3 * rr + cc] = T2[3 * cc + rr];
         mul3(T2t, Fn, tmp);  // F21i = T2t*Fn*T1
         mul3(tmp, T1, F);
         for (int k = 0; k < 9; ++k) f21[9 * it + k] = F[k];
@@ -226,8 +272,7 @@ extern "C" int orbgpu_init_hypotheses_batch_device(const float* d_kp1, int n1, c
                        n_matches, static_cast<float*>(d_work), reinterpret_cast<float4*>(d_pts));
     ORB_HIP(hipGetLastError());
     if (n_iter > 0) {
-        hipLaunchKernelGGL(init_models_kernel, dim3((2 * n_iter + kModelThreads - 1) / kModelThreads),
-                           dim3(kModelThreads), 0, s, static_cast<const float*>(d_work), n1, n2, d_pairs, d_sets,
+        hipLaunchKernelGGL(init_models_kernel, dim3((2 * n_iter + kGroups - 1) / kGroups), dim3(kModelThreads), 0, s, static_cast<const float*>(d_work), n1, n2, d_pairs, d_sets,
                            n_iter, d_h21, d_h12, d_f21);
         ORB_HIP(hipGetLastError());
     }

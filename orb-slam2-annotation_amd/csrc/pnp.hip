@@ -1,15 +1,17 @@
 // pnp.hip -- PnPsolver's RANSAC loop (src/PnPsolver.cpp:203-349) for a batch
 // of solvers (one per relocalisation candidate keyframe), in two launches:
-//   1  pnp_hyp_kernel: one thread per hypothesis runs EPnP (epnp.h) on its
-//      minimal set of 4 correspondences -- speculative, all n_hyp of every
-//      solver;
+//   1  pnp_hyp_kernel: 16 lanes per hypothesis (four per wave) run EPnP
+//      (epnp_wave.h) on its minimal set of 4 correspondences -- speculative,
+//      all n_hyp of every solver;
 //   2  pnp_score_kernel, one 256-thread block per solver, chunks of 64
 //      hypotheses: the waves score them (CheckInliers :352-386, lanes over
 //      correspondences, ballot + popcount), then the whole block replays the
 //      reference's loop body in iteration order: a hypothesis with
 //      inliers >= minInliers becomes the best if it beats it (its mask is
 //      written by all threads), and Refine() (:303-349: EPnP over all best
-//      inliers, then CheckInliers) runs on one lane; the first refinement
+//      inliers, then CheckInliers) runs on wave 0 (the inlier list by an
+//      ordered ballot compaction, EPnP with the correspondences over the 64
+//      lanes); the first refinement
 //      with more than minInliers inliers ends the call.  Refine() of an
 //      unchanged best is deterministic, so it is evaluated once per best.
 // Parity with the CPU oracle is to a stated pose tolerance
@@ -17,6 +19,7 @@
 // methods and the null space of a minimal set is only defined up to a basis.
 #include "../../include/orbgpu_ransac.h"
 #include "epnp.h"
+#include "epnp_wave.h"
 #include "ransac_kernels.h"
 
 namespace orbgpu {
@@ -92,16 +95,20 @@ __device__ inline void pose_to_tcw(const HypPose& H, float* T) {  // Rcw/tcw con
 __global__ __launch_bounds__(64) void pnp_hyp_kernel(const orbgpu_pnp_problem* __restrict__ probs,
                                                      const float* __restrict__ P3g, const float* __restrict__ P2g,
                                                      const int* __restrict__ samples, HypPose* __restrict__ hyps) {
+    __shared__ double s_ep[4][epnp::kWaveScratch];
     const orbgpu_pnp_problem& P = probs[blockIdx.y];
-    const int h = blockIdx.x * 64 + threadIdx.x;
-    if (h >= P.n_hyp) return;
+    const int lane = threadIdx.x, g = lane >> 4, r = lane & 15;
+    const int h = blockIdx.x * 4 + g;
+    if (h >= P.n_hyp) return;  // the whole 16-lane group leaves together
     const size_t slot = (size_t)P.sample_offset + h;
     SampleSrc src{P3g + 3 * (size_t)P.offset, P2g + 2 * (size_t)P.offset, samples + 4 * slot};
     epnp::Pose pose;
-    epnp::compute_pose(src, camera_of(P), pose);
-    HypPose& out = hyps[slot];
-    for (int k = 0; k < 9; ++k) out.R[k] = pose.R[k];
-    for (int k = 0; k < 3; ++k) out.t[k] = pose.t[k];
+    epnp::compute_pose_group<16>(src, camera_of(P), pose, r, s_ep[g]);
+    if (r == 0) {
+        HypPose& out = hyps[slot];
+        for (int k = 0; k < 9; ++k) out.R[k] = pose.R[k];
+        for (int k = 0; k < 3; ++k) out.t[k] = pose.t[k];
+    }
 }
 
 __global__ __launch_bounds__(kThreads) void pnp_score_kernel(const orbgpu_pnp_problem* __restrict__ probs,
@@ -116,6 +123,7 @@ __global__ __launch_bounds__(kThreads) void pnp_score_kernel(const orbgpu_pnp_pr
     __shared__ int s_cnt[kChunk];
     __shared__ int s_state[6];  // best, best_hyp, found, consumed, refine_tried, refined_inliers
     __shared__ HypPose s_ref;
+    __shared__ double s_ep[epnp::kWaveScratch];
     const orbgpu_pnp_problem P = probs[blockIdx.x];
     const HypPose* HP = hyps + P.sample_offset;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -158,15 +166,25 @@ __global__ __launch_bounds__(kThreads) void pnp_score_kernel(const orbgpu_pnp_pr
                 __syncthreads();
             }
             if (!s_state[4]) {  // Refine() with the current best inliers
-                if (tid == 0) {
-                    int m = 0;
-                    for (int i = 0; i < P.n; ++i)
-                        if (BM[i]) list[m++] = i;
+                if (wave == 0) {
+                    int m = 0;  // the best inliers in index order (ordered ballot compaction)
+                    for (int b0 = 0; b0 < P.n; b0 += 64) {
+                        const int i = b0 + lane;
+                        const bool in = i < P.n && BM[i];
+                        const unsigned long long bal = __ballot(in);
+                        if (in) list[m + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u))] = i;
+                        m += __popcll(bal);
+                    }
+                    __builtin_amdgcn_s_waitcnt(0);  // the list is in memory before any lane reads it
+                    __builtin_amdgcn_wave_barrier();
                     ListSrc src{P3, P2, list, m};
                     epnp::Pose pose;
-                    if (m > 0) epnp::compute_pose(src, cam, pose);
-                    for (int k = 0; k < 9; ++k) s_ref.R[k] = m > 0 ? pose.R[k] : 0.0;
-                    for (int k = 0; k < 3; ++k) s_ref.t[k] = m > 0 ? pose.t[k] : 0.0;
+                    if (m > 0) epnp::compute_pose_group<64>(src, cam, pose, lane, s_ep);
+                    if (lane == 0) {
+                        for (int k = 0; k < 9; ++k) s_ref.R[k] = m > 0 ? pose.R[k] : 0.0;
+                        for (int k = 0; k < 3; ++k) s_ref.t[k] = m > 0 ? pose.t[k] : 0.0;
+                    }
                 }
                 __syncthreads();
                 int cnt = 0;
@@ -216,7 +234,7 @@ hipError_t launch_pnp_ransac(int batch, const orbgpu_pnp_problem* probs, int max
                              hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
     if (max_hyp > 0)
-        hipLaunchKernelGGL(pnp_hyp_kernel, dim3((max_hyp + 63) / 64, batch), dim3(64), 0, stream, probs, P3, P2,
+        hipLaunchKernelGGL(pnp_hyp_kernel, dim3((max_hyp + 3) / 4, batch), dim3(64), 0, stream, probs, P3, P2,
                            samples, static_cast<HypPose*>(hyps));
     hipLaunchKernelGGL(pnp_score_kernel, dim3(batch), dim3(kThreads), 0, stream, probs,
                        static_cast<const HypPose*>(hyps), P3, P2, maxerr, lists, results, best_mask, refined_mask);

@@ -4,10 +4,17 @@ equal-size nodes change the extractor's output?
 The reference sorts (size, ExtractorNode*) pairs (src/ORBextractor.cpp:690),
 so ties fall to heap addresses; the spec here breaks them by creation
 sequence.  This runs the CPU oracle over synthetic streams of each geometry
-with three tie-breaks -- 0 creation sequence (spec), 1 reversed sequence,
-2 heap address of the oracle's own list nodes (the reference's mechanism in
-this process) -- and reports the fraction of frames (and keypoints) whose
-output differs from mode 0.
+with these tie-breaks (oracle/orbref.h orbref_set_tiebreak):
+  0 creation sequence (the spec),
+  1 reversed sequence,
+  2 heap address of the oracle's own list nodes,
+  3 heap address under the REFERENCE'S allocation pattern (ExtractorNode
+    layout, reserve / push_front copy / erase order: oracle/octree_faithful.h)
+    in this process's glibc heap -- the reference's mechanism,
+  4 mode 3 after a perturbation of the heap's free lists,
+  5 mode 3's allocation sequence under a deterministic glibc model,
+and reports, for every pair of modes, the fraction of frames (and
+keypoints) whose output differs.
 
 usage: python tools/h2_tiebreak.py [--frames 200] [--json out.json]
 """
@@ -28,30 +35,36 @@ import synth  # noqa: E402
 GEOMS = {"mono640": (640, 480, 1000), "kitti": (1241, 376, 2000), "euroc": (752, 480, 1200)}
 
 
+MODES = {0: "creation_sequence", 1: "reversed_sequence", 2: "heap_address_oracle_nodes",
+         3: "heap_address_reference_allocations", 4: "heap_address_reference_allocations_perturbed",
+         5: "reference_allocations_glibc_model"}
+
+
+def _diff(base, res):
+    frames_diff = kp_diff = kp_total = 0
+    for (k0, d0), (k1, d1) in zip(base, res):
+        kp_total += len(k0)
+        if len(k0) != len(k1) or k0.tobytes() != k1.tobytes() or not np.array_equal(d0, d1):
+            frames_diff += 1
+            a = {(float(x), float(y), int(o)) for x, y, o in zip(k0["x"], k0["y"], k0["octave"])}
+            b = {(float(x), float(y), int(o)) for x, y, o in zip(k1["x"], k1["y"], k1["octave"])}
+            kp_diff += len(a ^ b) // 2 + abs(len(k0) - len(k1))
+    return {"frames_changed": frames_diff, "frames": len(base), "frame_fraction": round(frames_diff / len(base), 4),
+            "keypoints_changed": kp_diff, "keypoint_fraction": round(kp_diff / max(kp_total, 1), 5)}
+
+
 def measure(w, h, nf, frames, seed=0x0B5E):
     imgs = synth.mono_stream(frames, w, h, seed=seed)
     ex = orbref.Extractor(nfeatures=nf)
-    out = {}
-    base = []
     L = orbref.lib()
-    for mode in (0, 1, 2):
+    res = {}
+    for mode in MODES:
         L.orbref_set_tiebreak(mode)
-        res = [ex.extract(im) for im in imgs]
-        if mode == 0:
-            base = res
-            continue
-        frames_diff = kp_diff = kp_total = 0
-        for (k0, d0), (k1, d1) in zip(base, res):
-            kp_total += len(k0)
-            if len(k0) != len(k1) or k0.tobytes() != k1.tobytes() or not np.array_equal(d0, d1):
-                frames_diff += 1
-                a = {(float(x), float(y), int(o)) for x, y, o in zip(k0["x"], k0["y"], k0["octave"])}
-                b = {(float(x), float(y), int(o)) for x, y, o in zip(k1["x"], k1["y"], k1["octave"])}
-                kp_diff += len(a ^ b) // 2 + abs(len(k0) - len(k1))
-        out[{1: "reversed_sequence", 2: "heap_address"}[mode]] = {
-            "frames_changed": frames_diff, "frames": len(imgs), "frame_fraction": frames_diff / len(imgs),
-            "keypoints_changed": kp_diff, "keypoint_fraction": kp_diff / max(kp_total, 1)}
+        res[mode] = [ex.extract(im) for im in imgs]
     L.orbref_set_tiebreak(0)
+    out = {}
+    for a, b in [(0, 1), (0, 2), (0, 3), (0, 4), (0, 5), (3, 4), (3, 5), (4, 5)]:
+        out[f"{MODES[a]}__vs__{MODES[b]}"] = _diff(res[a], res[b])
     return out
 
 
