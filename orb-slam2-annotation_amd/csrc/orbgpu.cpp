@@ -141,6 +141,8 @@ struct orbgpu_extractor {
     PyrPlan pyr_plan;              // fused pyramid pass: row records, tick ranges, per-lane entries
     int4* d_pyr_ent = nullptr;
     int2* d_pyr_tab = nullptr;
+    int2* d_xtab = nullptr;  // level-by-level pyramid (small batches): column / row taps per level
+    int2* d_ytab = nullptr;
     uint32_t* d_cand = nullptr;
     int* d_cell_counts = nullptr;
     uint32_t* d_gkeys = nullptr;
@@ -183,7 +185,7 @@ struct orbgpu_extractor {
     int last_batch = 0;
 
     ~orbgpu_extractor() {
-        void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_ent, d_pyr_tab, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
+        void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_ent, d_pyr_tab, d_xtab, d_ytab, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
                         d_oct_count, d_err, d_trace, d_img, d_single};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
@@ -204,7 +206,7 @@ namespace {
 #endif
 
 // ORBextractor ctor arithmetic (ORBextractor.cpp:417-448) + per-level layout.
-int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int2>& ytab) {
+int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int2>& ytab, std::vector<int2>* xtab) {
     const int L = e->nlevels;
     e->scale.assign(L, 1.f);
     e->sigma2.assign(L, 1.f);
@@ -240,6 +242,7 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     int cell_base = 0, out_off = 0, max_cells = 0, ncap = 0;
     ptab.clear();
     ytab.clear();
+    if (xtab) xtab->clear();
     for (int l = 0; l < L; ++l) {
         LevelGeom& v = g.lv[l];
         v.w = cv_round((float)e->W * e->inv_scale[l]);
@@ -343,6 +346,10 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
             }
             v.ytab_offset = (int)ytab.size();
             ytab.insert(ytab.end(), yt.begin(), yt.end());
+            if (xtab) {
+                v.xtab_offset = (int)xtab->size();
+                xtab->insert(xtab->end(), xt.begin(), xt.end());
+            }
         }
     }
     {
@@ -404,6 +411,15 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     return ORBGPU_OK;
 }
 
+// batches up to this size take the level-by-level pyramid (ORBGPU_PYR_LEVELS_MAX_BATCH overrides)
+int pyr_levels_max_batch() {
+    static const int v = [] {
+        const char* s = std::getenv("ORBGPU_PYR_LEVELS_MAX_BATCH");
+        return s ? std::atoi(s) : 8;
+    }();
+    return v;
+}
+
 int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_step, size_t frame_step,
               orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap, hipStream_t s) {
     const Geom& g = e->g;
@@ -417,7 +433,11 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
         evs = e->ev[e->ev_used++].data();
         ORB_HIP(hipEventRecord(evs[0], s));
     }
-    ORB_HIP(launch_pyramid(g, batch, e->d_pyr_ent, e->d_pyr_tab, imgs, row_step, frame_step, e->d_pyr, s));
+    // the tick pipeline is one block per frame: a few frames go level by level over the chip
+    if (batch <= pyr_levels_max_batch())
+        ORB_HIP(launch_pyramid_levels(g, batch, e->d_xtab, e->d_ytab, imgs, row_step, frame_step, e->d_pyr, s));
+    else
+        ORB_HIP(launch_pyramid(g, batch, e->d_pyr_ent, e->d_pyr_tab, imgs, row_step, frame_step, e->d_pyr, s));
     if (evs) ORB_HIP(hipEventRecord(evs[1], s));
     if (e->stage_ev[0]) ORB_HIP(hipEventRecord(e->stage_ev[0], s));
     ORB_HIP(launch_fast_cells(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_cand, e->d_cell_counts, e->d_err, s));
@@ -498,8 +518,8 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
     e->H = height;
     e->max_batch = max_batch;
     std::vector<int4> ptab;
-    std::vector<int2> ytab;
-    rc = build_geometry(e, ptab, ytab);
+    std::vector<int2> ytab, xtab;
+    rc = build_geometry(e, ptab, ytab, &xtab);
     if (rc) { delete e; return rc; }
     const Geom& g = e->g;
     const size_t B = (size_t)max_batch;
@@ -510,7 +530,8 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
         (rc = dalloc(&e->d_gknode, g.cand_frame * B)) || (rc = dalloc(&e->d_oct_out, (size_t)g.slots_frame * B)) ||
         (rc = dalloc(&e->d_oct_count, (size_t)g.nlevels * B)) || (rc = dalloc(&e->d_err, 1)) ||
         (rc = dalloc(&e->d_img, e->img_pitch * height)) ||
-        (rc = dalloc(&e->d_pyr_ent, e->pyr_plan.ent.size())) || (rc = dalloc(&e->d_pyr_tab, e->pyr_plan.tab.size()))) {
+        (rc = dalloc(&e->d_pyr_ent, e->pyr_plan.ent.size())) || (rc = dalloc(&e->d_pyr_tab, e->pyr_plan.tab.size())) ||
+        (rc = dalloc(&e->d_xtab, xtab.size())) || (rc = dalloc(&e->d_ytab, ytab.size()))) {
         delete e;
         return rc;
     }
@@ -529,6 +550,8 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
         return fail(ORBGPU_ERR_HIP, "pinned staging allocation failed");
     }
     if (hipMemcpy(e->d_ptab, ptab.data(), ptab.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess ||
+        (!xtab.empty() && hipMemcpy(e->d_xtab, xtab.data(), xtab.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess) ||
+        (!ytab.empty() && hipMemcpy(e->d_ytab, ytab.data(), ytab.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess) ||
         (!e->pyr_plan.ent.empty() && hipMemcpy(e->d_pyr_ent, e->pyr_plan.ent.data(),
                                                e->pyr_plan.ent.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess) ||
         (!e->pyr_plan.tab.empty() && hipMemcpy(e->d_pyr_tab, e->pyr_plan.tab.data(),
@@ -825,7 +848,7 @@ int orbgpu_debug_pyramid_emulate(int nfeatures, float scale_factor, int nlevels,
     e.max_batch = 1;
     std::vector<int4> ptab;
     std::vector<int2> ytab;
-    int rc = build_geometry(&e, ptab, ytab);
+    int rc = build_geometry(&e, ptab, ytab, nullptr);
     if (rc) return rc;
     const Geom& g = e.g;
     size_t need = 0;

@@ -55,6 +55,7 @@ struct LevelGeom {
     int w, h;                 // level size (ComputePyramid, ORBextractor.cpp:1128)
     int pitch;                // row pitch in the pyramid buffer (levels >= 1)
     int simd_end;             // resize: VResizeLinearVec_32s8u coverage
+    int xtab_offset;          // resize column taps (per output column) in the level-by-level tables
     size_t frame_bytes;       // bytes per frame of this level in the pyramid buffer
     size_t offset;            // byte offset of this level's region (levels >= 1)
     float scale;              // mvScaleFactor[l]

@@ -23,6 +23,9 @@ int slot_offset(const Geom& g, int l, int r);
 int emulate_pyramid(const Geom& g, const std::vector<int2>& ytab, const PyrPlan& plan, const uint8_t* img, size_t row0,
                     std::vector<std::vector<uint8_t>>& levels);
 // all pyramid levels 1..L-1 of `batch` frames (one block per frame)
+// level-by-level pyramid for small batches (xtab / ytab: build_resize_tables per level)
+hipError_t launch_pyramid_levels(const Geom& g, int batch, const int2* xtab, const int2* ytab, const uint8_t* img0,
+                                 size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream);
 hipError_t launch_pyramid(const Geom& g, int batch, const int4* ents, const int2* tab, const uint8_t* img0,
                           size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream);
 hipError_t pyramid_set_lds_limit(const Geom& g);

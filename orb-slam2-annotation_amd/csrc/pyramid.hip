@@ -395,6 +395,63 @@ extern "C" int orbgpu_debug_pyr_stamps(unsigned long long* out, unsigned long lo
 }
 #endif
 
+// ---- small batches (the drop-in Frame path): level by level over the whole chip ----
+// The tick kernel runs one block per frame, so a single frame is 66 serial
+// ticks on one CU.  For a few frames each level is instead one launch of
+// quads over every row of every frame (level l-1 read from HBM/L2 in place),
+// with the same arithmetic: exact Q11 horizontal sums, then
+// VResizeLinearVec_32s8u for x < simd_end and FixedPtCast<int,uchar,22> on the
+// tail.  Tables: xt[x] = (sx0 | sx1 << 16, a0 | a1 << 16) and
+// yt[y] = (y0 | y1 << 16, b0 | b1 << 16) as build_resize_tables makes them.
+constexpr int kLevelThreads = 64;
+
+__global__ __launch_bounds__(kLevelThreads) void pyramid_level_kernel(const uint8_t* __restrict__ src, int spitch,
+                                                                       size_t sframe, uint8_t* __restrict__ dst,
+                                                                       int dpitch, size_t dframe, int dw,
+                                                                       int simd_end, const int2* __restrict__ xt,
+                                                                       const int2* __restrict__ yt) {
+    const int q = blockIdx.x * kLevelThreads + threadIdx.x;
+    const int y = blockIdx.y, f = blockIdx.z;
+    if (4 * q >= dw) return;
+    const int2 ty = yt[y];
+    const uint32_t b0 = (uint32_t)ty.y & 0xFFFFu, b1 = (uint32_t)ty.y >> 16;
+    const uint8_t* r0 = src + (size_t)f * sframe + (size_t)(ty.x & 0xFFFF) * spitch;
+    const uint8_t* r1 = src + (size_t)f * sframe + (size_t)((uint32_t)ty.x >> 16) * spitch;
+    uint32_t out = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int x = 4 * q + k;
+        if (x >= dw) break;
+        const int2 tx = xt[x];
+        const int sx0 = tx.x & 0xFFFF, sx1 = (int)((uint32_t)tx.x >> 16);
+        const uint32_t a0 = (uint32_t)tx.y & 0xFFFFu, a1 = (uint32_t)tx.y >> 16;
+        const uint32_t h0 = r0[sx0] * a0 + r0[sx1] * a1, h1 = r1[sx0] * a0 + r1[sx1] * a1;
+        const uint32_t v = x < simd_end ? ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2u) >> 2
+                                        : (h0 * b0 + h1 * b1 + (1u << 21)) >> 22;
+        out |= v << (8 * k);
+    }
+    // the level pitch is a multiple of 16 >= dw: the quad's dword lies inside the row
+    *reinterpret_cast<uint32_t*>(dst + (size_t)f * dframe + (size_t)y * dpitch + 4 * q) = out;
+}
+
+hipError_t launch_pyramid_levels(const Geom& g, int batch, const int2* xtab, const int2* ytab, const uint8_t* img0,
+                                 size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream) {
+    for (int l = 1; l < g.nlevels; ++l) {
+        const LevelGeom& v = g.lv[l];
+        const LevelGeom& p = g.lv[l - 1];
+        const uint8_t* src = l == 1 ? img0 : pyr + p.offset;
+        const int spitch = l == 1 ? (int)row0 : p.pitch;
+        const size_t sframe = l == 1 ? frame0 : p.frame_bytes;
+        const int quads = (v.w + 3) / 4;
+        hipLaunchKernelGGL(pyramid_level_kernel, dim3((quads + kLevelThreads - 1) / kLevelThreads, v.h, batch),
+                           dim3(kLevelThreads), 0, stream, src, spitch, sframe, pyr + v.offset, v.pitch,
+                           v.frame_bytes, v.w, v.simd_end, xtab + v.xtab_offset, ytab + v.ytab_offset);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 hipError_t launch_pyramid(const Geom& g, int batch, const int4* ents, const int2* tab, const uint8_t* img0,
                           size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream) {
     if (g.nlevels < 2) return hipSuccess;
