@@ -697,9 +697,10 @@ class DropIn:
         self.scen["proj_last"] = (tgt2, pts2, last)
         (d / "proj2.in").write_bytes(aio.proj_blob(15.0, dict(check_ori=True, mono=True), tgt2, pts2, last))
         self._run("proj", 2, d / "proj2.in", d / "proj2.out")
-        # SearchByBoW: 1000-feature frames over a k=10, L=5 vocabulary (GPU transform, levelsup 4)
-        par, leaf, vdesc, w = synth.synthetic_vocabulary_fast(10, 5, 7)
-        voc = bow.Vocabulary.from_arrays(10, 5, 0, 0, par, leaf, vdesc, w)
+        # SearchByBoW: 1000-feature frames over a k=10, L=6 vocabulary (ORBvoc.txt's shape; GPU
+        # transform, levelsup 4: the FeatureVector nodes are the 100 level-2 nodes)
+        par, leaf, vdesc, w = synth.synthetic_vocabulary_fast(10, 6, 7)
+        voc = bow.Vocabulary.from_arrays(10, 6, 0, 0, par, leaf, vdesc, w)
         d1, a1, d2, a2 = synth.bow_frame_pair(vdesc[leaf == 1], 1000, 0.6, seed=41)
         fv1, fv2 = voc.transform(d1, 4)[3], voc.transform(d2, 4)[3]
         rng = np.random.default_rng(23)
@@ -762,12 +763,13 @@ class DropIn:
               1), "Python oracle")
         import bow_ref
         par, leaf, vdesc, w, d1_, a1, s1, d2_, a2, s2 = self.scen["bow"]
-        cv = orbref.Vocabulary(10, 5, par, leaf, vdesc, w)
+        cv = orbref.Vocabulary(10, 6, par, leaf, vdesc, w)
         res["ORBmatcher::SearchByBoW(KF1, KF2)"] = (
             t(lambda: orbref.search_by_bow_kf_kf(cv, d1_, a1, s1 == 1, d2_, a2, s2 == 1, 0.7)),
             "C++ oracle (includes the two BoW transforms)")
-        bv = bow_ref.Vocabulary.from_arrays(10, 5, 0, 0, par, leaf, vdesc, w)
-        f1, f2 = bv.transform(d1_, 4)[3], bv.transform(d2_, 4)[3]
+        import loop_ref
+        av = loop_ref.ArrayVocabulary(10, 6, 0, 0, par, leaf, vdesc, w)
+        f1, f2 = av.transform(d1_, 4)[3], av.transform(d2_, 4)[3]
         res["ORBmatcher::SearchByBoW(KF, F)"] = (
             t(lambda: bow_ref.search_by_bow(0, f1, d1_, a1, s1 == 1, f2, d2_, a2, np.ones(1000, bool), 0.7, True), 1),
             "Python oracle")

@@ -120,6 +120,11 @@ int orbgpu_extractor_set_stage_event(orbgpu_extractor* ex, int stage, void* even
  * host (ORBextractor.h:85; read by Frame::ComputeStereoMatches). */
 int orbgpu_extractor_copy_level(orbgpu_extractor* ex, int frame, int level, uint8_t* dst,
                                 size_t dst_step);
+/* All levels of frame `frame` of the last extraction at once (the host
+ * mvImagePyramid of ORBextractor): dst[l] / dst_step[l] for l < nlevels.
+ * One pinned staging copy per level on the extractor's stream and one
+ * synchronisation. */
+int orbgpu_extractor_copy_levels(orbgpu_extractor* ex, int frame, uint8_t* const* dst, const size_t* dst_step);
 
 /* ---------------------------------------------------------------------- */
 /* ORBmatcher                                                              */

@@ -103,10 +103,14 @@ public:
         }
         if (copy_pyramid_) {
             mvImagePyramid.resize((size_t)nlevels);
+            std::vector<uint8_t*> dst((size_t)nlevels);
+            std::vector<size_t> step((size_t)nlevels);
             for (int l = 0; l < nlevels; ++l) {
                 mvImagePyramid[l].create(info_.level_height[l], info_.level_width[l], CV_8U);
-                check(orbgpu_extractor_copy_level(ex_, 0, l, mvImagePyramid[l].data, mvImagePyramid[l].step));
+                dst[l] = mvImagePyramid[l].data;
+                step[l] = mvImagePyramid[l].step;
             }
+            check(orbgpu_extractor_copy_levels(ex_, 0, dst.data(), step.data()));
         }
     }
 

@@ -7,7 +7,7 @@
 // minimum-error choice); what changes is who computes what:
 //   * every per-correspondence loop (centroid, covariance, M^T M, the camera
 //     centroid and ABt of compute_R_and_t, the reprojection error) is split
-//     over the group's lanes and reduced with xor shuffles;
+//     over the group's lanes and reduced on DPP (group_sum.h);
 //   * M^T M is assembled from 40 group sums (its 3x3 blocks are fu^2,
 //     fv^2, fu, fv multiples of sums of alpha_k alpha_l weighted by 1,
 //     (uc - u), (vc - v) and their squares) and its eigenvectors come from a
@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include "epnp.h"
+#include "group_sum.h"
 
 namespace orbgpu {
 namespace epnp {
@@ -34,9 +35,7 @@ constexpr int kWaveScratch = 144 + 48 + 60;
 
 template <int G>
 __device__ __forceinline__ double gsum(double x) {
-#pragma unroll
-    for (int o = G / 2; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
-    return x;
+    return group_sum_dpp<G>(x);
 }
 
 // LDS writes of the group visible to its other lanes (one wave: in-order LDS,

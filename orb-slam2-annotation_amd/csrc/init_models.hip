@@ -15,7 +15,7 @@
 //                          value (cv::SVDecomp's vt.row(8)) by one-sided
 //                          (Hestenes) Jacobi in double with the rows on the
 //                          lanes -- each column pair's three dot products are
-//                          16-lane xor reductions, lane r < 9 carries row r of
+//                          16-lane DPP reductions, lane r < 9 carries row r of
 //                          V, converged groups rotate by the identity until
 //                          the whole wave has converged; then the group's
 //                          lane 0 does, for F, the rank-2 projection
@@ -32,6 +32,7 @@
 
 #include "../../include/orbgpu_init.h"
 #include "epnp.h"
+#include "group_sum.h"
 #include "host_common.h"
 
 namespace {
@@ -119,10 +120,8 @@ __device__ void inv3(const float* m, float* o) {
 constexpr int kModelThreads = 64;  // one wave = four hypotheses of 16 lanes
 constexpr int kGroups = kModelThreads / 16;
 
-__device__ __forceinline__ double group_sum(double x) {  // over the lane's 16-lane group
-#pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
-    return x;
+__device__ __forceinline__ double group_sum(double x) {  // over the lane's 16-lane group (DPP)
+    return orbgpu::row16_sum(x);
 }
 
 __global__ __launch_bounds__(kModelThreads) void init_models_kernel(const float* __restrict__ work, int n1, int n2,

@@ -169,6 +169,7 @@ struct orbgpu_extractor {
     uint8_t* d_single = nullptr;
     uint8_t* h_single = nullptr;  // pinned
     uint8_t* h_img = nullptr;     // pinned staging of the host image (img_pitch rows)
+    uint8_t* h_levels = nullptr;  // pinned staging of one frame's pyramid (copy_levels), on first use
     size_t single_bytes = 0, single_desc_off = 0;
     orbgpu_keypoint* d_kps1 = nullptr;
     uint8_t* d_desc1 = nullptr;
@@ -192,6 +193,7 @@ struct orbgpu_extractor {
         for (auto& sc : stereo_sad) (void)hipFree(sc.d);
         if (h_single) (void)hipHostFree(h_single);
         if (h_img) (void)hipHostFree(h_img);
+        if (h_levels) (void)hipHostFree(h_levels);
         if (stream) (void)hipStreamDestroy(stream);
         for (auto& a : ev)
             for (hipEvent_t x : a) (void)hipEventDestroy(x);
@@ -691,6 +693,39 @@ int orbgpu_extractor_copy_level(orbgpu_extractor* e, int frame, int level, uint8
     const size_t pitch = level == 0 ? e->last_row : (size_t)v.pitch;
     ORB_HIP(hipStreamSynchronize(e->stream));
     ORB_HIP(hipMemcpy2D(dst, dst_step, src, pitch, v.w, v.h, hipMemcpyDeviceToHost));
+    return ORBGPU_OK;
+}
+
+// mvImagePyramid of one frame: every level into pinned staging with one async
+// copy each on the extractor's stream, one synchronisation, then host copies
+// into the caller's rows (a pageable 2-D copy per level costs ~1 ms)
+int orbgpu_extractor_copy_levels(orbgpu_extractor* e, int frame, uint8_t* const* dst, const size_t* dst_step) {
+    if (!e || !dst || !dst_step) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    if (!e->last_img || frame < 0 || frame >= e->last_batch)
+        return fail(ORBGPU_ERR_ARG, "no such frame in the last extraction");
+    size_t total = 0, off[kMaxLevels];
+    for (int l = 0; l < e->nlevels; ++l) {
+        const LevelGeom& v = e->g.lv[l];
+        if (!dst[l] || dst_step[l] < (size_t)v.w) return fail(ORBGPU_ERR_ARG, "bad destination of a level");
+        off[l] = total;
+        total += round_up((size_t)v.pitch * v.h, 256);
+    }
+    if (!e->h_levels) ORB_HIP(hipHostMalloc((void**)&e->h_levels, total, hipHostMallocDefault));
+    for (int l = 0; l < e->nlevels; ++l) {
+        const LevelGeom& v = e->g.lv[l];
+        if (l == 0)
+            ORB_HIP(hipMemcpy2DAsync(e->h_levels, (size_t)v.pitch, e->last_img + (size_t)frame * e->last_frame,
+                                     e->last_row, v.w, v.h, hipMemcpyDeviceToHost, e->stream));
+        else
+            ORB_HIP(hipMemcpyAsync(e->h_levels + off[l], e->d_pyr + v.offset + (size_t)frame * v.frame_bytes,
+                                   (size_t)v.pitch * v.h, hipMemcpyDeviceToHost, e->stream));
+    }
+    ORB_HIP(hipStreamSynchronize(e->stream));
+    for (int l = 0; l < e->nlevels; ++l) {
+        const LevelGeom& v = e->g.lv[l];
+        for (int y = 0; y < v.h; ++y)
+            std::memcpy(dst[l] + (size_t)y * dst_step[l], e->h_levels + off[l] + (size_t)y * v.pitch, (size_t)v.w);
+    }
     return ORBGPU_OK;
 }
 
