@@ -176,7 +176,7 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const int idx = min(lane + 64 * k, kChunks - 1), r = idx / 3, q = idx - 3 * r;
-            c[k] = *reinterpret_cast<const uint4*>(top + (size_t)r * rp + 16 * q);
+            c[k] = load16_a4(top + (size_t)r * rp + 16 * q);
         }
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -321,8 +321,14 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
                                                                    const int* __restrict__ oct_count,
                                                                    orbgpu_keypoint* __restrict__ kps,
                                                                    uint8_t* __restrict__ desc,
-                                                                   int* __restrict__ counts, int kp_cap) {
+                                                                   int* __restrict__ counts, int kp_cap,
+                                                                   int* __restrict__ err_word,
+                                                                   int* __restrict__ err_copy) {
     __shared__ DescLds s_lds[kDescWaves];
+    // single-frame path: the error word of this extraction (FAST / octree ran
+    // before on the stream) moves into the output block and is cleared, so
+    // the host needs no extra copy and memset launches
+    if (err_copy && blockIdx.x == 0 && threadIdx.x == 0) *err_copy = atomicExch(err_word, 0);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: metadata in SGPRs
 #if ORBGPU_DESC_SWIZZLE
@@ -342,11 +348,11 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                            const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
-                           hipStream_t stream) {
+                           hipStream_t stream, int* err_word, int* err_copy) {
     const int items = g.slots_frame * batch;
     const int blocks = (items + kDescWaves - 1) / kDescWaves;
     hipLaunchKernelGGL(describe_kernel, dim3(blocks), dim3(64 * kDescWaves), 0, stream, g, items, img0, row0, frame0,
-                       pyr, oct_out, oct_count, kps, desc, counts, kp_cap);
+                       pyr, oct_out, oct_count, kps, desc, counts, kp_cap, err_word, err_copy);
     return hipGetLastError();
 }
 

@@ -20,6 +20,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "jacobi_group.h"
+
 namespace orbgpu {
 namespace epnp {
 
@@ -86,6 +88,9 @@ template <int M, int N>
 __host__ __device__ void svd_hestenes(double* a, double* s, double* v) {
     for (int i = 0; i < N; ++i)
         for (int j = 0; j < N; ++j) v[i * N + j] = i == j ? 1.0 : 0.0;
+    double fro = 0.0;  // numerically null columns take no rotation (jacobi_group.h)
+    for (int k = 0; k < M * N; ++k) fro += a[k] * a[k];
+    const double negl = kJacobiNegl * fro;
     for (int sweep = 0; sweep < 60; ++sweep) {
         bool rotated = false;
         for (int p = 0; p < N - 1; ++p)
@@ -96,11 +101,9 @@ __host__ __device__ void svd_hestenes(double* a, double* s, double* v) {
                     beta += a[k * N + q] * a[k * N + q];
                     gamma += a[k * N + p] * a[k * N + q];
                 }
-                if (fabs(gamma) <= 1e-15 * sqrt(alpha * beta) || gamma == 0.0) continue;
+                double c, sn;
+                if (!jacobi_rotation(alpha, beta, gamma, negl, c, sn)) continue;
                 rotated = true;
-                const double zeta = (beta - alpha) / (2.0 * gamma);
-                const double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-                const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
                 for (int k = 0; k < M; ++k) {
                     const double x = a[k * N + p], y = a[k * N + q];
                     a[k * N + p] = c * x - sn * y;

@@ -12,7 +12,9 @@
 //     fv^2, fu, fv multiples of sums of alpha_k alpha_l weighted by 1,
 //     (uc - u), (vc - v) and their squares) and its eigenvectors come from a
 //     one-sided Jacobi with the 12 rows on 12 lanes (lane r also carries
-//     row r of V); a column pair's three dot products are group reductions;
+//     row r of V; jacobi_group.h: round-robin order, six disjoint column
+//     pairs per round, null columns skipped); a column pair's three dot
+//     products are group reductions;
 //   * the dense 3x3 / 6xk pieces run redundantly on every lane (identical
 //     inputs, identical results, no broadcast needed); L (6x10) and the four
 //     null-space vectors live in the group's LDS scratch.
@@ -26,9 +28,21 @@
 
 #include "epnp.h"
 #include "group_sum.h"
+#include "jacobi_group.h"
 
 namespace orbgpu {
 namespace epnp {
+
+// EPNP_STAMPS (diagnostic build only, tools/epnp_stamps.py): lane 0 of a
+// chosen group records s_memtime at each phase boundary
+#ifdef EPNP_STAMPS
+#define EPNP_T(k)                                                        \
+    do {                                                                 \
+        if (stamps && r == 0) stamps[k] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define EPNP_T(k) ((void)stamps)
+#endif
 
 // per-group LDS scratch (doubles)
 constexpr int kWaveScratch = 144 + 48 + 60;
@@ -103,8 +117,10 @@ __device__ inline void canonicalize_null_space4(double* ut4, int k, double* scr)
 // r = the lane's index in its group; lds = the group's kWaveScratch doubles.
 // Every lane of the group returns the same pose and error.
 template <int G, class Src>
-__device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& out, int r, double* lds) {
+__device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& out, int r, double* lds,
+                                     unsigned long long* stamps = nullptr) {
     const int n = src.count();
+    EPNP_T(0);
     double* s_mtm = lds;        // 12 x 12
     double* s_ut4 = lds + 144;  // 4 x 12: null vectors, ut row 11 - c
     double* s_L = lds + 192;    // 6 x 10
@@ -153,6 +169,7 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
             for (int j = 0; j < 3; ++j) cws[i][j] = cws[0][j] + k * uct[3 * (i - 1) + j];
         }
     }
+    EPNP_T(1);
     // compute_barycentric_coordinates (:457-481): CC_inv = pinv(CC)
     double ci[9];
     {
@@ -176,6 +193,7 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
                        ci[3 * j + 2] * (pw[2] - cws[0][2]);
         a[0] = 1.0f - a[1] - a[2] - a[3];
     };
+    EPNP_T(2);
     // M^T M (fill_M :483-497, cvMulTransposed): per (k <= l) sums of a_k a_l times
     // 1, (uc - u), (vc - v), (uc - u)^2 + (vc - v)^2
     {
@@ -222,6 +240,7 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
         }
     }
     EPNP_GROUP_SYNC();
+    EPNP_T(3);
     // eigenvectors of M^T M: one-sided Jacobi on the symmetric PSD matrix, rows on lanes
     {
         double a[12], v[12];
@@ -230,32 +249,7 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
             a[c] = r < 12 ? s_mtm[r * 12 + c] : 0.0;
             v[c] = (r == c) ? 1.0 : 0.0;
         }
-        for (int sweep = 0; sweep < 60; ++sweep) {
-            bool rotated = false;
-#pragma unroll
-            for (int p = 0; p < 11; ++p)
-#pragma unroll
-                for (int q = p + 1; q < 12; ++q) {
-                    const double alpha = gsum<G>(a[p] * a[p]);
-                    const double beta = gsum<G>(a[q] * a[q]);
-                    const double gamma = gsum<G>(a[p] * a[q]);
-                    double c = 1.0, sn = 0.0;
-                    if (!(fabs(gamma) <= 1e-15 * sqrt(alpha * beta) || gamma == 0.0)) {
-                        rotated = true;
-                        const double zeta = (beta - alpha) / (2.0 * gamma);
-                        const double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-                        c = 1.0 / sqrt(1.0 + t * t);
-                        sn = c * t;
-                    }
-                    const double x = a[p], y = a[q];
-                    a[p] = c * x - sn * y;
-                    a[q] = sn * x + c * y;
-                    const double vx = v[p], vy = v[q];
-                    v[p] = c * vx - sn * vy;
-                    v[q] = sn * vx + c * vy;
-                }
-            if (!__any(rotated)) break;  // wave-uniform: converged groups rotate by the identity
-        }
+        hestenes_group<12, G>(a, v);
         double lam[12];
 #pragma unroll
         for (int j = 0; j < 12; ++j) lam[j] = sqrt(gsum<G>(a[j] * a[j]));
@@ -270,11 +264,13 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
         }
     }
     EPNP_GROUP_SYNC();
+    EPNP_T(4);
     {
         const int k = 12 - 2 * n;
         if (k > 0 && r == 0) canonicalize_null_space4(s_ut4, k < 4 ? k : 4, s_mtm);  // M^T M is consumed
     }
     EPNP_GROUP_SYNC();
+    EPNP_T(5);
     // compute_L_6x10 (:863-898), compute_rho (:900-908)
     double rho[6];
     if (r == 0) {
@@ -311,6 +307,7 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
     rho[4] = dist2(cws[1], cws[3]);
     rho[5] = dist2(cws[2], cws[3]);
     EPNP_GROUP_SYNC();
+    EPNP_T(6);
     const double* L = s_L;
     auto gauss_newton = [&](double* betas) {  // :942-963 + compute_A_and_b_gauss_newton :910-940
         for (int it = 0; it < 5; ++it) {
@@ -427,6 +424,7 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
             l[4 * i + 3] = L[10 * i + 6];
         }
         svd_solve<6, 4>(l, rho, b4);
+        EPNP_T(7);
         if (b4[0] < 0) {
             B[0] = sqrt(-b4[0]);
             B[1] = -b4[1] / B[0];
@@ -439,15 +437,18 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
             B[3] = b4[3] / B[0];
         }
         gauss_newton(B);
+        EPNP_T(8);
         Pose P;
         const double e = r_and_t(B, P);
         keep(e, P, true);
     }
+    EPNP_T(9);
     {  // find_betas_approx_2 (:783-815)
         double l[18], b3[3], B[4];
         for (int i = 0; i < 6; ++i)
             for (int k = 0; k < 3; ++k) l[3 * i + k] = L[10 * i + k];
         svd_solve<6, 3>(l, rho, b3);
+        EPNP_T(10);
         if (b3[0] < 0) {
             B[0] = sqrt(-b3[0]);
             B[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0;
@@ -459,15 +460,18 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
         B[2] = 0.0;
         B[3] = 0.0;
         gauss_newton(B);
+        EPNP_T(11);
         Pose P;
         const double e = r_and_t(B, P);
         keep(e, P, false);
     }
+    EPNP_T(12);
     {  // find_betas_approx_3 (:817-851)
         double l[30], b5[5], B[4];
         for (int i = 0; i < 6; ++i)
             for (int k = 0; k < 5; ++k) l[5 * i + k] = L[10 * i + k];
         svd_solve<6, 5>(l, rho, b5);
+        EPNP_T(13);
         if (b5[0] < 0) {
             B[0] = sqrt(-b5[0]);
             B[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;
@@ -479,10 +483,12 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
         B[2] = b5[3] / B[0];
         B[3] = 0.0;
         gauss_newton(B);
+        EPNP_T(14);
         Pose P;
         const double e = r_and_t(B, P);
         keep(e, P, false);
     }
+    EPNP_T(15);
     return best_err;
 }
 

@@ -294,7 +294,7 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
             for (int k = 0; k < 2; ++k) {
                 const int idx = min(b0 + lane + 64 * k, nc * wh - 1);
                 const int r = fast_div(idx, mnc), q = idx - r * nc;
-                v[k] = *reinterpret_cast<const uint4*>(wbase + (size_t)r * pitch + 16 * q);
+                v[k] = load16_a4(wbase + (size_t)r * pitch + 16 * q);
             }
 #pragma unroll
             for (int k = 0; k < 2; ++k) {

@@ -14,10 +14,10 @@
 //                          its right singular vector of the smallest singular
 //                          value (cv::SVDecomp's vt.row(8)) by one-sided
 //                          (Hestenes) Jacobi in double with the rows on the
-//                          lanes -- each column pair's three dot products are
+//                          lanes (jacobi_group.h: round-robin pair order,
 //                          16-lane DPP reductions, lane r < 9 carries row r of
-//                          V, converged groups rotate by the identity until
-//                          the whole wave has converged; then the group's
+//                          V, numerically null columns take no rotation --
+//                          the 8 x 9 F system always has one); then the group's
 //                          lane 0 does, for F, the rank-2 projection
 //                          (w(2) = 0), the de-normalisation T2inv*Hn*T1 /
 //                          T2t*Fn*T1 and H12 = H21.inv() with OpenCV's float
@@ -33,11 +33,13 @@
 #include "../../include/orbgpu_init.h"
 #include "epnp.h"
 #include "group_sum.h"
+#include "jacobi_group.h"
 #include "host_common.h"
 
 namespace {
 
 constexpr int kNormThreads = 256;
+constexpr int kNormChunk = 2048;  // keypoints per frame staged in LDS at a time (2 x 16 KB)
 
 // Normalize (Initializer.cpp:965-1015).  work layout (floats):
 //   [0, 2 n1)            normalised mvKeys1
@@ -49,19 +51,39 @@ __global__ __launch_bounds__(kNormThreads) void init_normalize_kernel(const floa
                                                                       float* __restrict__ work,
                                                                       float4* __restrict__ pts) {
     __shared__ float s_mean[4], s_scale[4];
+    __shared__ float2 s_kp[2][kNormChunk];
     const int tid = threadIdx.x;
-    if (tid < 4) {  // lane = (frame, axis): the reference's sequential float sums
-        const int fr = tid >> 1, ax = tid & 1;
-        const float* k = fr ? kp2 : kp1;
-        const int n = fr ? n2 : n1;
-        float mean = 0.f;
-        for (int i = 0; i < n; ++i) mean = __fadd_rn(mean, k[2 * i + ax]);
-        mean = __fdiv_rn(mean, (float)n);
-        float dev = 0.f;
-        for (int i = 0; i < n; ++i) dev = __fadd_rn(dev, fabsf(__fsub_rn(k[2 * i + ax], mean)));
-        dev = __fdiv_rn(dev, (float)n);
+    // lane = (frame, axis) runs the reference's sequential float sums (mean,
+    // then mean absolute deviation) over LDS; the block stages the keypoints
+    // chunk by chunk with coalesced loads (a lane walking them in HBM paid one
+    // dependent memory round trip per keypoint: 177 us for 2 x 2000)
+    const int fr = (tid >> 1) & 1, ax = tid & 1;
+    const int n = fr ? n2 : n1;
+    const int nmax = n1 > n2 ? n1 : n2;
+    float mean = 0.f, acc = 0.f;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int base = 0; base < nmax; base += kNormChunk) {
+            __syncthreads();  // the previous chunk is consumed
+            for (int i = tid; i < 2 * kNormChunk; i += kNormThreads) {
+                const int f = i / kNormChunk, j = i - f * kNormChunk, idx = base + j;
+                if (idx < (f ? n2 : n1)) s_kp[f][j] = reinterpret_cast<const float2*>(f ? kp2 : kp1)[idx];
+            }
+            __syncthreads();
+            if (tid < 4) {
+                const int cnt = min(kNormChunk, n - base);
+                const float* col = reinterpret_cast<const float*>(s_kp[fr]) + ax;
+                if (pass == 0)
+                    for (int i = 0; i < cnt; ++i) acc = __fadd_rn(acc, col[2 * i]);
+                else
+                    for (int i = 0; i < cnt; ++i) acc = __fadd_rn(acc, fabsf(__fsub_rn(col[2 * i], mean)));
+            }
+        }
+        if (pass == 0) mean = __fdiv_rn(acc, (float)n);
+        acc = pass == 0 ? 0.f : __fdiv_rn(acc, (float)n);
+    }
+    if (tid < 4) {
         s_mean[tid] = mean;
-        s_scale[tid] = (float)(1.0 / (double)dev);  // float sX = 1.0/meanDevX
+        s_scale[tid] = (float)(1.0 / (double)acc);  // float sX = 1.0/meanDevX
     }
     __syncthreads();
     for (int i = tid; i < n1 + n2; i += kNormThreads) {
@@ -168,32 +190,7 @@ __global__ __launch_bounds__(kModelThreads) void init_models_kernel(const float*
     double v[9];  // row r of V (lanes r < 9)
 #pragma unroll
     for (int k = 0; k < 9; ++k) v[k] = (r == k) ? 1.0 : 0.0;
-    for (int sweep = 0; sweep < 60; ++sweep) {
-        bool rotated = false;
-#pragma unroll
-        for (int p = 0; p < 8; ++p)
-#pragma unroll
-            for (int q = p + 1; q < 9; ++q) {
-                const double alpha = group_sum(a[p] * a[p]);
-                const double beta = group_sum(a[q] * a[q]);
-                const double gamma = group_sum(a[p] * a[q]);
-                double c = 1.0, sn = 0.0;
-                if (!(fabs(gamma) <= 1e-15 * sqrt(alpha * beta) || gamma == 0.0)) {
-                    rotated = true;
-                    const double zeta = (beta - alpha) / (2.0 * gamma);
-                    const double tt = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-                    c = 1.0 / sqrt(1.0 + tt * tt);
-                    sn = c * tt;
-                }
-                const double x = a[p], y = a[q];
-                a[p] = c * x - sn * y;
-                a[q] = sn * x + c * y;
-                const double vx = v[p], vy = v[q];
-                v[p] = c * vx - sn * vy;
-                v[q] = sn * vx + c * vy;
-            }
-        if (!__any(rotated)) break;
-    }
+    orbgpu::hestenes_group<9, 16>(a, v);
     // singular values = column norms; the first smallest decides vt.row(8)
     int jmin = 0;
     double smin = 0.0;
@@ -264,6 +261,8 @@ extern "C" int orbgpu_init_hypotheses_batch_device(const float* d_kp1, int n1, c
         (n_iter > 0 && (!d_sets || !d_h21 || !d_h12 || !d_f21)))
         return orbgpu::fail(ORBGPU_ERR_ARG, "invalid argument (needs >= 8 matches and keypoints in both frames)");
     if ((uintptr_t)d_pts & 15) return orbgpu::fail(ORBGPU_ERR_ARG, "d_pts must be 16-byte aligned");
+    if (((uintptr_t)d_kp1 | (uintptr_t)d_kp2) & 7)
+        return orbgpu::fail(ORBGPU_ERR_ARG, "d_kp1 / d_kp2 must be 8-byte aligned (x, y float pairs)");
     if (int rc = orbgpu::check_device()) return rc;
     (void)hipGetLastError();
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);

@@ -69,15 +69,25 @@ __device__ inline int key_dist(uint32_t key) { return (int)(key >> (12 + kKeyJBi
 __device__ inline int key_j(uint32_t key) { return (int)(key & kKeyJMask); }
 
 // Two phases per frame pair (one 256-thread block):
-//  1 parallel, one thread per F1 query: scan the level-0 F2 keypoints (same
-//    j for every lane: LDS broadcasts), keep the kTopK smallest (dist, grid
-//    order) keys of the candidates in the query's window, and their count;
-//  2 sequential, wave 0: the reference's query loop (ORBmatcher.cpp:510-563)
-//    over those lists -- a candidate is skipped when vMatchedDistance[i2] <=
-//    dist (state of the loop so far); best = first kept key, bestDist2 = the
-//    next kept key's dist.  A list is exact while it holds all candidates or
-//    both values are found inside it; otherwise the query is re-scanned by
-//    the whole wave against the live state (rare).
+//  1 parallel, one thread per F1 query: the F2 level-0 keypoints of the
+//    query's window, walked through a cell CSR of F2 (the window's 64x48
+//    grid columns are contiguous runs, so a query visits only the keypoints
+//    of its cells -- ~60 instead of all n20), keep the kTopK smallest
+//    (dist, grid order) keys and the candidate count;
+//  2 wave 0: the reference's query loop (ORBmatcher.cpp:510-563) over those
+//    lists against the live vMatchedDistance -- a candidate is skipped when
+//    vMatchedDistance[i2] <= dist; best = the first kept key, bestDist2 =
+//    the next kept key's dist.  64 consecutive queries are resolved at once,
+//    one per lane, against the state before the batch; a lane's outcome can
+//    only change through a match committed by an EARLIER lane of the batch
+//    to an F2 keypoint the lane depends on (vMatchedDistance only decreases,
+//    so a skipped entry stays skipped): its best when it matches, its best
+//    and second when it fails the ratio test, none when it fails TH_LOW or
+//    has no candidate.  The lanes before the first such dependence commit
+//    together (their F2 keypoints are distinct), the loop resumes at that
+//    lane.  A list that runs out is exact when its last key bounds
+//    bestDist2 from below far enough for the ratio test; otherwise the
+//    query is re-scanned by the whole wave against the live state (rare).
 template <int kMaxK0>
 __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     float minX, float maxX, float minY, float maxY, const orbgpu_keypoint* __restrict__ kps1,
@@ -85,6 +95,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     const orbgpu_keypoint* __restrict__ kps2, const uint8_t* __restrict__ desc2, const int* __restrict__ n2p,
     size_t stride2, float* __restrict__ prev_xy, int window, float nnratio, int flags, int* __restrict__ matches12,
     int* __restrict__ nmatches_out) {
+    constexpr int kCells = kGC * kGR;
     __shared__ float s_x[kMaxK0], s_y[kMaxK0];
     __shared__ int s_cell[kMaxK0];           // grid cell ix*48+iy, or -1 when not in the grid
     __shared__ int s_mdist[kMaxK0];          // vMatchedDistance
@@ -95,6 +106,10 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     __shared__ uint32_t s_top[kMaxK0][kTopK];
     __shared__ int s_ncand[kMaxK0];          // candidates in the window (-1: window off the grid)
     __shared__ short s_cj[kMaxK0];           // F2 index i1 was matched to when the loop reached it, or -1
+    __shared__ unsigned short s_cidx[kMaxK0];  // F2 level-0 indices grouped by cell
+    __shared__ int s_claim[kMaxK0];          // phase 2: first lane of the batch claiming an F2 keypoint, or 64
+    __shared__ int s_cend[kCells];           // cell CSR: end of each cell's run in s_cidx
+    __shared__ int s_wsum[kMatchThreads / 64];
     __shared__ int s_hist[kHL];
     __shared__ int s_nm;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -121,15 +136,20 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     // grid inverses (Frame.cpp:221-224)
     const float invW = __fdiv_rn((float)kGC, __fsub_rn(maxX, minX));
     const float invH = __fdiv_rn((float)kGR, __fsub_rn(maxY, minY));
+    for (int c = tid; c < kCells; c += kMatchThreads) s_cend[c] = 0;
+    __syncthreads();
     for (int j = tid; j < n20; j += kMatchThreads) {
         const float x = K2[j].x, y = K2[j].y;
         s_x[j] = x;
         s_y[j] = y;
         const int px = (int)roundf(__fmul_rn(__fsub_rn(x, minX), invW));
         const int py = (int)roundf(__fmul_rn(__fsub_rn(y, minY), invH));
-        s_cell[j] = (px < 0 || px >= kGC || py < 0 || py >= kGR) ? -1 : px * kGR + py;
+        const int cell = (px < 0 || px >= kGC || py < 0 || py >= kGR) ? -1 : px * kGR + py;
+        s_cell[j] = cell;
+        if (cell >= 0) atomicAdd(&s_cend[cell], 1);
         s_mdist[j] = 0x7FFFFFFF;
         s_m21[j] = -1;
+        s_claim[j] = 64;
         const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D2 + (size_t)j * 32);
 #pragma unroll
         for (int q = 0; q < 4; ++q) s_d2[j][q] = d[q];
@@ -144,6 +164,34 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     if (tid < kHL) s_hist[tid] = 0;
     if (tid == 0) s_nm = 0;
     __syncthreads();
+    {  // exclusive scan of the cell counts: thread t owns cells [12 t, 12 t + 12)
+        constexpr int kPer = kCells / kMatchThreads;
+        static_assert(kCells % kMatchThreads == 0, "cells per thread");
+        int loc[kPer], run = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            loc[k] = run;
+            run += s_cend[kPer * tid + k];
+        }
+        int incl = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += t;
+        }
+        if (lane == 63) s_wsum[wave] = incl;
+        __syncthreads();
+        int base = incl - run;
+        for (int w = 0; w < wave; ++w) base += s_wsum[w];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) s_cend[kPer * tid + k] = base + loc[k];  // cell start
+        __syncthreads();
+        for (int j = tid; j < n20; j += kMatchThreads) {
+            const int cell = s_cell[j];
+            if (cell >= 0) s_cidx[atomicAdd(&s_cend[cell], 1)] = (unsigned short)j;  // start -> end
+        }
+        __syncthreads();
+    }
 
     const float r = (float)window;
     // GetFeaturesInArea's cell range (Frame.cpp:385-395) for a query at (x, y)
@@ -174,19 +222,23 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
             ncand = 0;
             const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D1 + (size_t)i1 * 32);
             const unsigned long long q0 = d[0], q1 = d[1], q2 = d[2], q3 = d[3];
-            for (int j = 0; j < n20; ++j) {
-                int cell;
-                if (!in_window(j, x, y, cx0, cx1, cy0, cy1, cell)) continue;
-                const int dist = __popcll(q0 ^ s_d2[j][0]) + __popcll(q1 ^ s_d2[j][1]) +
-                                 __popcll(q2 ^ s_d2[j][2]) + __popcll(q3 ^ s_d2[j][3]);
-                uint32_t key = cand_key(dist, cell, j);
+            for (int ix = cx0; ix <= cx1; ++ix) {
+                const int c0 = ix * kGR + cy0;
+                const int lo = c0 > 0 ? s_cend[c0 - 1] : 0, hi = s_cend[ix * kGR + cy1];
+                for (int p = lo; p < hi; ++p) {
+                    const int j = s_cidx[p];
+                    if (!(fabsf(__fsub_rn(s_x[j], x)) < r && fabsf(__fsub_rn(s_y[j], y)) < r)) continue;
+                    const int dist = __popcll(q0 ^ s_d2[j][0]) + __popcll(q1 ^ s_d2[j][1]) +
+                                     __popcll(q2 ^ s_d2[j][2]) + __popcll(q3 ^ s_d2[j][3]);
+                    uint32_t key = cand_key(dist, s_cell[j], j);
 #pragma unroll
-                for (int k = 0; k < kTopK; ++k) {  // sorted insert
-                    const uint32_t lo = min(key, top[k]);
-                    key = max(key, top[k]);
-                    top[k] = lo;
+                    for (int k = 0; k < kTopK; ++k) {  // sorted insert
+                        const uint32_t lo_k = min(key, top[k]);
+                        key = max(key, top[k]);
+                        top[k] = lo_k;
+                    }
+                    ++ncand;
                 }
-                ++ncand;
             }
         }
 #pragma unroll
@@ -195,98 +247,114 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     }
     __syncthreads();
 
-    // phase 2: the sequential query loop (wave 0; wave-uniform control).  The
-    // lists of 64 queries at a time are read into lanes and taken from there
-    // with readlane, so a query costs one LDS round trip (vMatchedDistance of
-    // its listed candidates) plus the commit; the rotation bins are computed
-    // after the loop from the F2 index each query was matched to when the
-    // loop reached it (the reference pushes i1 into rotHist at that moment,
-    // and a later steal does not remove it), in parallel.
+    // phase 2 (wave 0, wave-uniform control): batches of 64 queries
     if (wave == 0) {
-        for (int base = 0; base < n10; base += 64) {
-            const int qi = base + lane;
-            int l_nc = 0;
-            uint32_t l_top[kTopK];
+        auto lds_sync = [] {  // this wave's LDS writes visible to its other lanes
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        };
+        int cur = 0;
+        while (cur < n10) {
+            const int i1 = cur + lane;
+            const bool act = i1 < n10;
+            const int nc = act ? s_ncand[i1] : 0;
+            uint32_t key[kTopK];
+            int md[kTopK];
 #pragma unroll
-            for (int k = 0; k < kTopK; ++k) l_top[k] = 0xFFFFFFFFu;
-            if (qi < n10) {
-                l_nc = s_ncand[qi];
+            for (int k = 0; k < kTopK; ++k) key[k] = act ? s_top[i1][k] : 0xFFFFFFFFu;
 #pragma unroll
-                for (int k = 0; k < kTopK; ++k) l_top[k] = s_top[qi][k];
+            for (int k = 0; k < kTopK; ++k) md[k] = key[k] != 0xFFFFFFFFu ? s_mdist[key_j(key[k])] : 0;
+            const int nk = min(nc, kTopK);
+            uint32_t best = 0xFFFFFFFFu, second = 0xFFFFFFFFu;
+#pragma unroll
+            for (int k = 0; k < kTopK; ++k) {
+                if (k >= nk || second != 0xFFFFFFFFu) continue;
+                if (md[k] <= key_dist(key[k])) continue;  // vMatchedDistance[i2] <= dist
+                if (best == 0xFFFFFFFFu) best = key[k]; else second = key[k];
             }
-            const int cnt = min(64, n10 - base);
-            for (int u = 0; u < cnt; ++u) {
-                const int i1 = base + u;
-                const int ncand = __builtin_amdgcn_readlane(l_nc, u);
-                if (ncand <= 0) continue;  // window off the grid, or no candidate in it
-                uint32_t key[kTopK];
-                int md[kTopK];
-#pragma unroll
-                for (int k = 0; k < kTopK; ++k) key[k] = __builtin_amdgcn_readlane(l_top[k], u);
-#pragma unroll
-                for (int k = 0; k < kTopK; ++k) md[k] = key[k] != 0xFFFFFFFFu ? s_mdist[key_j(key[k])] : 0;
-                uint32_t best = 0xFFFFFFFFu;
-                int best2 = 0x7FFFFFFF;
-                bool have2 = false;
-                const int nk = min(ncand, kTopK);
-#pragma unroll
-                for (int k = 0; k < kTopK; ++k) {
-                    if (k >= nk || have2) continue;
-                    const int dist = key_dist(key[k]);
-                    if (md[k] <= dist) continue;
-                    if (best == 0xFFFFFFFFu) {
-                        best = key[k];
+            // 0 no match, 1 match, 2 needs the exact re-scan
+            int state = 0;
+            if (nc > 0) {
+                if (best == 0xFFFFFFFFu) {
+                    state = nc > kTopK ? 2 : 0;
+                } else {
+                    const int bd = key_dist(best);
+                    if (bd > kThLow) state = 0;
+                    else if (second != 0xFFFFFFFFu) state = (float)bd < __fmul_rn((float)key_dist(second), nnratio) ? 1 : 0;
+                    else if (nc <= kTopK) state = (float)bd < __fmul_rn((float)0x7FFFFFFF, nnratio) ? 1 : 0;
+                    // bestDist2 >= the last listed key's dist: enough when it passes the ratio test
+                    else state = (float)bd < __fmul_rn((float)key_dist(key[kTopK - 1]), nnratio) ? 1 : 2;
+                }
+            }
+            const int claim = state == 1 ? key_j(best) : -1;
+            if (claim >= 0) atomicMin(&s_claim[claim], lane);
+            lds_sync();
+            // F2 keypoints this lane's outcome depends on (see above)
+            int dep0 = -1, dep1 = -1;
+            if (state == 1) {
+                dep0 = claim;
+            } else if (state == 0 && best != 0xFFFFFFFFu && key_dist(best) <= kThLow) {
+                dep0 = key_j(best);  // failed the ratio test: best and second decide it
+                dep1 = second != 0xFFFFFFFFu ? key_j(second) : -1;
+            }
+            const bool dep = (dep0 >= 0 && s_claim[dep0] < lane) || (dep1 >= 0 && s_claim[dep1] < lane);
+            const unsigned long long stop = __ballot(act && (dep || state == 2));
+            const int ncommit = stop ? (int)__builtin_ctzll(stop) : min(64, n10 - cur);
+            if (lane < ncommit && state == 1) {  // distinct F2 keypoints: no ordering among these lanes
+                const int prev21 = s_m21[claim];
+                if (prev21 >= 0) s_m12[prev21] = -1;  // a match of an earlier batch is taken over
+                s_m12[i1] = claim;
+                s_m21[claim] = i1;
+                s_mdist[claim] = key_dist(best);
+                s_cj[i1] = (short)claim;
+            }
+            if (claim >= 0) s_claim[claim] = 64;
+            lds_sync();
+            if (ncommit > 0) {
+                cur += ncommit;
+                continue;
+            }
+            // the batch's first query needs the exact re-scan against the live state
+            {
+                const int q = cur;
+                const float x = s_px[q], y = s_py[q];
+                int cx0, cx1, cy0, cy1;
+                cell_range(x, y, cx0, cx1, cy0, cy1);
+                const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D1 + (size_t)q * 32);
+                const unsigned long long q0 = d[0], q1 = d[1], q2 = d[2], q3 = d[3];
+                unsigned long long lbest = ~0ull;
+                int second2 = 0x7FFFFFFF;
+                for (int j = lane; j < n20; j += 64) {
+                    int cell;
+                    if (!in_window(j, x, y, cx0, cx1, cy0, cy1, cell)) continue;
+                    const int dist = __popcll(q0 ^ s_d2[j][0]) + __popcll(q1 ^ s_d2[j][1]) +
+                                     __popcll(q2 ^ s_d2[j][2]) + __popcll(q3 ^ s_d2[j][3]);
+                    if (s_mdist[j] <= dist) continue;
+                    const unsigned long long k64 = ((unsigned long long)dist << 32) | ((unsigned)cell << 16) | (unsigned)j;
+                    if (k64 < lbest) {
+                        if (lbest != ~0ull) second2 = min(second2, (int)(lbest >> 32));
+                        lbest = k64;
                     } else {
-                        best2 = dist;
-                        have2 = true;
+                        second2 = min(second2, dist);
                     }
                 }
-                if (!have2 && ncand > kTopK) {
-                    // the list ran out: exact re-scan against the live state
-                    const float x = s_px[i1], y = s_py[i1];
-                    int cx0, cx1, cy0, cy1;
-                    cell_range(x, y, cx0, cx1, cy0, cy1);
-                    const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D1 + (size_t)i1 * 32);
-                    const unsigned long long q0 = d[0], q1 = d[1], q2 = d[2], q3 = d[3];
-                    unsigned long long lbest = ~0ull;
-                    int second = 0x7FFFFFFF;
-                    for (int j = lane; j < n20; j += 64) {
-                        int cell;
-                        if (!in_window(j, x, y, cx0, cx1, cy0, cy1, cell)) continue;
-                        const int dist = __popcll(q0 ^ s_d2[j][0]) + __popcll(q1 ^ s_d2[j][1]) +
-                                         __popcll(q2 ^ s_d2[j][2]) + __popcll(q3 ^ s_d2[j][3]);
-                        if (s_mdist[j] <= dist) continue;
-                        const unsigned long long k64 = ((unsigned long long)dist << 32) | ((unsigned)cell << 16) | (unsigned)j;
-                        if (k64 < lbest) {
-                            if (lbest != ~0ull) second = min(second, (int)(lbest >> 32));
-                            lbest = k64;
-                        } else {
-                            second = min(second, dist);
-                        }
-                    }
-                    const unsigned long long wbest = wave_min_u64(lbest);
-                    const int contrib = lbest == wbest ? second : (lbest == ~0ull ? 0x7FFFFFFF : (int)(lbest >> 32));
-                    best2 = wave_min_i(contrib);
-                    best = wbest == ~0ull ? 0xFFFFFFFFu
-                                          : cand_key((int)(wbest >> 32), (int)((wbest >> 16) & 0xFFFF), (int)(wbest & 0xFFFF));
-                }
-                if (best == 0xFFFFFFFFu) continue;  // no usable candidate
-                const int bestDist = key_dist(best);
-                const int bidx = key_j(best);
-                if (bestDist <= kThLow && (float)bestDist < __fmul_rn((float)best2, nnratio)) {
-                    if (lane == 0) {
+                const unsigned long long wbest = wave_min_u64(lbest);
+                const int contrib = lbest == wbest ? second2 : (lbest == ~0ull ? 0x7FFFFFFF : (int)(lbest >> 32));
+                const int best2 = wave_min_i(contrib);
+                if (wbest != ~0ull) {
+                    const int bestDist = (int)(wbest >> 32), bidx = (int)(wbest & 0xFFFF);
+                    if (bestDist <= kThLow && (float)bestDist < __fmul_rn((float)best2, nnratio) && lane == 0) {
                         const int prev21 = s_m21[bidx];
                         if (prev21 >= 0) s_m12[prev21] = -1;
-                        s_m12[i1] = bidx;
-                        s_m21[bidx] = i1;
+                        s_m12[q] = bidx;
+                        s_m21[bidx] = q;
                         s_mdist[bidx] = bestDist;
-                        s_cj[i1] = (short)bidx;
+                        s_cj[q] = (short)bidx;
                     }
-                    // wave-local LDS ordering for the next query's reads
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 }
+                lds_sync();
+                cur += 1;
             }
         }
     }

@@ -28,7 +28,9 @@ namespace orbgpu {
 
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 256;       // large batches: 4 workgroups per CU (LDS-bound)
+constexpr int kThreadsSmall = 1024;  // a few frames: one workgroup per (frame, level) on its own CU
+constexpr int kSmallBatch = 8;       // batches up to this size take kThreadsSmall
 
 struct ONode {
     uint32_t r0;   // x0 | y0 << 16
@@ -68,8 +70,9 @@ __device__ inline int wave_incl_scan(int v) {
 }
 
 // In-place exclusive scan of a[0..n) in LDS by the whole block; returns total.
+template <int NT>
 __device__ int block_scan(int* a, int n, int* s_tmp) {
-    const int per = (n + kThreads - 1) / kThreads;
+    const int per = (n + NT - 1) / NT;
     const int beg = min(n, (int)threadIdx.x * per), end = min(n, beg + per);
     int sum = 0;
     for (int i = beg; i < end; ++i) sum += a[i];
@@ -79,7 +82,7 @@ __device__ int block_scan(int* a, int n, int* s_tmp) {
     __syncthreads();
     int off = 0, total = 0;
 #pragma unroll
-    for (int w = 0; w < kThreads / 64; ++w) {
+    for (int w = 0; w < NT / 64; ++w) {
         const int t = s_tmp[w];
         if (w < wave) off += t;
         total += t;
@@ -113,7 +116,7 @@ __device__ inline int pow2ceil(int v) {
     return p;
 }
 
-template <bool LDS>
+template <int NT, bool LDS>
 __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int nk, int ncells, int ncap, int ncap2,
                             const uint32_t* __restrict__ cand, uint32_t* __restrict__ out,
                             int* __restrict__ oct_count, int* __restrict__ err, int* __restrict__ trace,
@@ -131,10 +134,10 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
     }
 
     // 2. roots (:545-587): keys -> root index (int)(x / hX)
-    for (int i = tid; i < nini; i += kThreads) s_aux0[i] = 0;
+    for (int i = tid; i < nini; i += NT) s_aux0[i] = 0;
     __syncthreads();
     const uint32_t* cbase = cand + (size_t)f * g.cand_frame + L.cand_offset;
-    for (int k = tid; k < nk; k += kThreads) {
+    for (int k = tid; k < nk; k += NT) {
         int lo = 0, hi = ncells - 1;  // last cell with cellofs <= k
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
@@ -151,10 +154,10 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
     // non-empty roots keep their order; empty ones are erased.  Computed by
     // thread r (no single-lane loop: see tools/check_scc.py for the ROCm 7.2
     // miscompile a uniform-address select in such a loop triggered).
-    for (int r = tid; r < nini; r += kThreads) s_aux1[r] = s_aux0[r] > 0 ? 1 : 0;
+    for (int r = tid; r < nini; r += NT) s_aux1[r] = s_aux0[r] > 0 ? 1 : 0;
     __syncthreads();
-    const int nroots = block_scan(s_aux1, nini, s_tmp);
-    for (int r = tid; r < nini; r += kThreads) {
+    const int nroots = block_scan<NT>(s_aux1, nini, s_tmp);
+    for (int r = tid; r < nini; r += NT) {
         const int c = s_aux0[r];
         const int pos = s_aux1[r];
         if (c > 0) {
@@ -169,7 +172,7 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
         s_aux1[r] = c > 0 ? pos : -1;
     }
     __syncthreads();
-    for (int k = tid; k < nk; k += kThreads) ks.set_node(k, s_aux1[ks.node(k)]);
+    for (int k = tid; k < nk; k += NT) ks.set_node(k, s_aux1[ks.node(k)]);
     __syncthreads();
 
     // 3. passes.  The pass state (list size, buffer, phase, next seq) is kept
@@ -180,9 +183,9 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
         ONode* old = cur ? s_node1 : s_node0;
         ONode* nw = cur ? s_node0 : s_node1;
         // quadrant histogram of every node with > 1 key
-        for (int i = tid; i < nL * 4; i += kThreads) s_qc[i] = 0;
+        for (int i = tid; i < nL * 4; i += NT) s_qc[i] = 0;
         __syncthreads();
-        for (int k = tid; k < nk; k += kThreads) {
+        for (int k = tid; k < nk; k += NT) {
             const int i = ks.node(k);
             const ONode nd = old[i];
             if (nd.cnt > 1) atomicAdd(&s_qc[i * 4 + node_quad(nd, ks.key(k))], 1u);
@@ -191,7 +194,7 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
         // processing order and push bases
         int C;  // children pushed this pass
         if (!inner) {
-            for (int i = tid; i < nL; i += kThreads) {
+            for (int i = tid; i < nL; i += NT) {
                 const bool div = old[i].cnt > 1;
                 int nch = 0;
 #pragma unroll
@@ -200,23 +203,23 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
                 s_flag[i] = div;
             }
             __syncthreads();
-            C = block_scan(s_aux0, nL, s_tmp);  // aux0 = push base (list order)
+            C = block_scan<NT>(s_aux0, nL, s_tmp);  // aux0 = push base (list order)
         } else {
             // compact the nodes with > 1 key, sort descending by (cnt, seq)
-            for (int i = tid; i < nL; i += kThreads) s_aux1[i] = old[i].cnt > 1;
+            for (int i = tid; i < nL; i += NT) s_aux1[i] = old[i].cnt > 1;
             __syncthreads();
-            const int m = block_scan(s_aux1, nL, s_tmp);
+            const int m = block_scan<NT>(s_aux1, nL, s_tmp);
             const int P = pow2ceil(max(m, 1));
-            for (int i = tid; i < P; i += kThreads) s_sortk[i] = 0ull;
+            for (int i = tid; i < P; i += NT) s_sortk[i] = 0ull;
             __syncthreads();
-            for (int i = tid; i < nL; i += kThreads)
+            for (int i = tid; i < nL; i += NT)
                 if (old[i].cnt > 1)
                     s_sortk[s_aux1[i]] = ((unsigned long long)min(old[i].cnt, 0xFFFFFFu) << 40) |
                                          ((unsigned long long)(old[i].seq & 0xFFFFFFFu) << 12) | (unsigned)i;
             __syncthreads();
             for (int k = 2; k <= P; k <<= 1)
                 for (int j = k >> 1; j > 0; j >>= 1) {
-                    for (int i = tid; i < P; i += kThreads) {
+                    for (int i = tid; i < P; i += NT) {
                         const int ixj = i ^ j;
                         if (ixj > i) {
                             const unsigned long long a = s_sortk[i], b = s_sortk[ixj];
@@ -227,28 +230,28 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
                     __syncthreads();
                 }
             // rank r -> (nch - 1); inclusive scan; first r reaching N
-            for (int r = tid; r < m; r += kThreads) {
+            for (int r = tid; r < m; r += NT) {
                 const int i = (int)(s_sortk[r] & 0xFFF);
                 int nch = 0;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) nch += s_qc[i * 4 + q] > 0;
                 s_aux1[r] = nch - 1;
             }
-            if (tid == 0) s_misc[8] = m - 1;
+            if (tid == 0) s_misc[24] = m - 1;
             __syncthreads();
-            block_scan(s_aux1, m, s_tmp);  // exclusive prefix of (nch-1)
-            for (int r = tid; r < m; r += kThreads) {
+            block_scan<NT>(s_aux1, m, s_tmp);  // exclusive prefix of (nch-1)
+            for (int r = tid; r < m; r += NT) {
                 const int i = (int)(s_sortk[r] & 0xFFF);
                 int nch = 0;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) nch += s_qc[i * 4 + q] > 0;
-                if (nL + s_aux1[r] + nch - 1 >= N) atomicMin(&s_misc[8], r);
+                if (nL + s_aux1[r] + nch - 1 >= N) atomicMin(&s_misc[24], r);
             }
-            for (int i = tid; i < nL; i += kThreads) { s_flag[i] = 0; s_aux0[i] = 0; }
+            for (int i = tid; i < nL; i += NT) { s_flag[i] = 0; s_aux0[i] = 0; }
             __syncthreads();
-            const int kstop = s_misc[8];
+            const int kstop = s_misc[24];
             // push bases over ranks 0..kstop, scattered to node index
-            for (int r = tid; r < m; r += kThreads) {
+            for (int r = tid; r < m; r += NT) {
                 const int i = (int)(s_sortk[r] & 0xFFF);
                 int nch = 0;
 #pragma unroll
@@ -256,8 +259,8 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
                 s_aux1[r] = r <= kstop ? nch : 0;
             }
             __syncthreads();
-            C = block_scan(s_aux1, m, s_tmp);
-            for (int r = tid; r <= kstop && r < m; r += kThreads) {
+            C = block_scan<NT>(s_aux1, m, s_tmp);
+            for (int r = tid; r <= kstop && r < m; r += NT) {
                 const int i = (int)(s_sortk[r] & 0xFFF);
                 s_aux0[i] = s_aux1[r];
                 s_flag[i] = 1;
@@ -265,17 +268,17 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
             __syncthreads();
         }
         // survivors keep their order after the C pushed children
-        for (int i = tid; i < nL; i += kThreads) s_aux1[i] = s_flag[i] ? 0 : 1;
+        for (int i = tid; i < nL; i += NT) s_aux1[i] = s_flag[i] ? 0 : 1;
         __syncthreads();
-        const int S = block_scan(s_aux1, nL, s_tmp);
+        const int S = block_scan<NT>(s_aux1, nL, s_tmp);
         const int nNew = C + S;
         if (nNew > ncap || nseq + C > 0x0FFFFFFF) {
             if (tid == 0) { atomicOr(err, nNew > ncap ? kErrNodeCap : kErrSeqCap); oct_count[f * g.nlevels + l] = 0; }
             return;
         }
-        if (tid == 0) s_misc[9] = 0;
+        if (tid == 0) s_misc[25] = 0;
         __syncthreads();
-        for (int i = tid; i < nL; i += kThreads) {
+        for (int i = tid; i < nL; i += NT) {
             const ONode nd = old[i];
             if (s_flag[i]) {
                 int p = s_aux0[i];
@@ -289,7 +292,7 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
                         ch.seq = (uint32_t)(nseq + p);
                         nw[pos] = ch;
                         s_qc[i * 4 + q] = (uint32_t)pos;
-                        if (c > 1) atomicAdd(&s_misc[9], 1);
+                        if (c > 1) atomicAdd(&s_misc[25], 1);
                         ++p;
                     }
                 }
@@ -300,41 +303,42 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
             }
         }
         __syncthreads();
-        for (int k = tid; k < nk; k += kThreads) {
+        for (int k = tid; k < nk; k += NT) {
             const int i = ks.node(k);
             ks.set_node(k, s_flag[i] ? (int)s_qc[i * 4 + node_quad(old[i], ks.key(k))] : s_aux1[i]);
         }
         __syncthreads();
         if (tid == 0 && trace && f == 0 && guard < 60) {
             int* t = trace + l * 512 + 2 + guard * 8;
-            t[0] = inner; t[1] = nL; t[2] = C; t[3] = S; t[4] = s_misc[9]; t[5] = s_misc[8]; t[6] = nk; t[7] = N;
+            t[0] = inner; t[1] = nL; t[2] = C; t[3] = S; t[4] = s_misc[25]; t[5] = s_misc[24]; t[6] = nk; t[7] = N;
             trace[l * 512] = guard + 1;
         }
-        const int nexp = s_misc[9];  // children with > 1 key (nToExpand)
+        const int nexp = s_misc[25];  // children with > 1 key (nToExpand)
         const bool done = nNew >= N || nNew == nL;  // :673 / :740
         if (!inner && nNew + nexp * 3 > N) inner = true;  // :678
         nseq += C;
         cur ^= 1;
         nL = nNew;
-        __syncthreads();  // s_misc[9] is reset by the next pass
+        __syncthreads();  // s_misc[25] is reset by the next pass
         if (done) break;
     }
 
     // 4. best key per node (max response, first in candidate order)
-    for (int i = tid; i < nL; i += kThreads) s_qc[i] = 0;
+    for (int i = tid; i < nL; i += NT) s_qc[i] = 0;
     __syncthreads();
-    for (int k = tid; k < nk; k += kThreads)
+    for (int k = tid; k < nk; k += NT)
         atomicMax(&s_qc[ks.node(k)], ((uint32_t)key_s(ks.key(k)) << 24) | (0xFFFFFFu - (uint32_t)k));
     __syncthreads();
     if (nL > L.ocap) {
         if (tid == 0) { atomicOr(err, kErrNodeCap); oct_count[f * g.nlevels + l] = 0; }
         return;
     }
-    for (int i = tid; i < nL; i += kThreads) out[i] = ks.key((int)(0xFFFFFFu - (s_qc[i] & 0xFFFFFFu)));
+    for (int i = tid; i < nL; i += NT) out[i] = ks.key((int)(0xFFFFFFu - (s_qc[i] & 0xFFFFFFu)));
     if (tid == 0) oct_count[f * g.nlevels + l] = nL;
 }
 
-__global__ __launch_bounds__(kThreads) void octree_kernel(Geom g, const uint32_t* __restrict__ cand,
+template <int NT>
+__global__ __launch_bounds__(NT) void octree_kernel(Geom g, const uint32_t* __restrict__ cand,
                                                           const int* __restrict__ cell_counts,
                                                           uint32_t* __restrict__ gkeys,
                                                           uint16_t* __restrict__ gknode,
@@ -357,7 +361,7 @@ __global__ __launch_bounds__(kThreads) void octree_kernel(Geom g, const uint32_t
     const int ncap2 = pow2ceil(ncap);
 
     // LDS carve (byte offsets must match octree_lds_bytes)
-    const size_t o_sortk = 64;
+    const size_t o_sortk = 128;
     const size_t o_node0 = o_sortk + (size_t)ncap2 * 8;
     const size_t o_node1 = o_node0 + (size_t)ncap * 16;
     const size_t o_qc = o_node1 + (size_t)ncap * 16;
@@ -376,23 +380,23 @@ __global__ __launch_bounds__(kThreads) void octree_kernel(Geom g, const uint32_t
     int* s_aux1 = reinterpret_cast<int*>(smem + o_aux1);
     uint8_t* s_flag = smem + o_flag;
     int* s_cellofs = reinterpret_cast<int*>(smem + o_cell);
-    int* s_tmp = s_misc;  // [0..3] scan scratch, [4..] scalars
+    int* s_tmp = s_misc;  // [0..15] scan scratch (a wave total each), [24..25] scalars
 
     // 1. candidate order: cells row-major, within a cell FAST order (:797-838)
     const int* cc = cell_counts + (size_t)f * g.total_cells + L.cell_base;
-    for (int i = tid; i < ncells; i += kThreads) s_cellofs[i] = cc[i];
+    for (int i = tid; i < ncells; i += NT) s_cellofs[i] = cc[i];
     if (tid == 0) s_cellofs[ncells] = 0;
     __syncthreads();
-    const int nk = block_scan(s_cellofs, ncells + 1, s_tmp);
+    const int nk = block_scan<NT>(s_cellofs, ncells + 1, s_tmp);
     uint32_t* out = oct_out + (size_t)f * g.slots_frame + L.out_offset;
     if (nk <= kcap) {
         KeyStore<true> ks{reinterpret_cast<uint32_t*>(smem + o_keys), reinterpret_cast<uint16_t*>(smem + o_knode)};
-        octree_body<true>(g, L, l, f, nk, ncells, ncap, ncap2, cand, out, oct_count, err, trace, ks, s_misc, s_sortk,
+        octree_body<NT, true>(g, L, l, f, nk, ncells, ncap, ncap2, cand, out, oct_count, err, trace, ks, s_misc, s_sortk,
                           s_node0, s_node1, s_qc, s_aux0, s_aux1, s_flag, s_cellofs);
     } else {  // too many candidates for LDS: the same algorithm on an HBM scratch region
         KeyStore<false> ks{gkeys + (size_t)f * g.cand_frame + L.cand_offset,
                            gknode + (size_t)f * g.cand_frame + L.cand_offset};
-        octree_body<false>(g, L, l, f, nk, ncells, ncap, ncap2, cand, out, oct_count, err, trace, ks, s_misc, s_sortk,
+        octree_body<NT, false>(g, L, l, f, nk, ncells, ncap, ncap2, cand, out, oct_count, err, trace, ks, s_misc, s_sortk,
                            s_node0, s_node1, s_qc, s_aux0, s_aux1, s_flag, s_cellofs);
     }
 }
@@ -403,7 +407,7 @@ size_t octree_lds_bytes(const Geom& g, int kcap, int ncap) {
     auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
     int ncap2 = 1;
     while (ncap2 < ncap) ncap2 <<= 1;
-    return r16(16 * 4) + r16((size_t)ncap2 * 8) + 2 * r16((size_t)ncap * 16) + r16((size_t)ncap * 16) +
+    return r16(32 * 4) + r16((size_t)ncap2 * 8) + 2 * r16((size_t)ncap * 16) + r16((size_t)ncap * 16) +
            2 * r16((size_t)ncap * 4) + r16((size_t)ncap) + r16((size_t)(g.max_cells_level + 1) * 4) +
            r16((size_t)kcap * 4) + r16((size_t)kcap * 2);
 }
@@ -414,10 +418,15 @@ hipError_t launch_octree(const Geom& g, int batch, const uint32_t* cand, const i
     // both level groups in one launch, LDS sized for the larger group: group B's short
     // workgroups start as group A's finish instead of after the last of them (two
     // launches: 0.278 ms per 512 frames, one: 0.184 ms)
+    // a few frames leave most CUs idle: then every (frame, level) workgroup
+    // gets 1024 threads, so its key sweeps, scans and sorts take a quarter of the steps
+    const bool small = batch <= kSmallBatch;
+    auto kernel = small ? &octree_kernel<kThreadsSmall> : &octree_kernel<kThreads>;
+    const int nt = small ? kThreadsSmall : kThreads;
     if (ngroups == 2 && groups[0].nlev > 0 && groups[1].nlev > 0) {
         const size_t lds = std::max(octree_lds_bytes(g, groups[0].kcap, groups[0].ncap),
                                     octree_lds_bytes(g, groups[1].kcap, groups[1].ncap));
-        hipLaunchKernelGGL(octree_kernel, dim3((groups[0].nlev + groups[1].nlev) * batch), dim3(kThreads), lds,
+        hipLaunchKernelGGL(kernel, dim3((groups[0].nlev + groups[1].nlev) * batch), dim3(nt), lds,
                            stream, g, cand, cell_counts, gkeys, gknode, oct_out, oct_count, err, trace, groups[0],
                            groups[1], batch);
         return hipGetLastError();
@@ -427,7 +436,7 @@ hipError_t launch_octree(const Geom& g, int batch, const uint32_t* cand, const i
         const OctreeGroup& G = groups[i];
         if (G.nlev <= 0) continue;
         const size_t lds = octree_lds_bytes(g, G.kcap, G.ncap);
-        hipLaunchKernelGGL(octree_kernel, dim3(G.nlev * batch), dim3(kThreads), lds, stream, g, cand, cell_counts,
+        hipLaunchKernelGGL(kernel, dim3(G.nlev * batch), dim3(nt), lds, stream, g, cand, cell_counts,
                            gkeys, gknode, oct_out, oct_count, err, trace, G, OctreeGroup{0, 0, 0, 0}, batch);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

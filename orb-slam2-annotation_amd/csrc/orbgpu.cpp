@@ -143,6 +143,7 @@ struct orbgpu_extractor {
     int2* d_pyr_tab = nullptr;
     int2* d_xtab = nullptr;  // level-by-level pyramid (small batches): column / row taps per level
     int2* d_ytab = nullptr;
+    int4* d_band = nullptr;  // banded pyramid (small batches): per band and level row ranges
     uint32_t* d_cand = nullptr;
     int* d_cell_counts = nullptr;
     uint32_t* d_gkeys = nullptr;
@@ -186,7 +187,7 @@ struct orbgpu_extractor {
     int last_batch = 0;
 
     ~orbgpu_extractor() {
-        void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_ent, d_pyr_tab, d_xtab, d_ytab, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
+        void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_ent, d_pyr_tab, d_xtab, d_ytab, d_band, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
                         d_oct_count, d_err, d_trace, d_img, d_single};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
@@ -422,8 +423,17 @@ int pyr_levels_max_batch() {
     return v;
 }
 
+// ORBGPU_PYR_BANDS=0 selects the level-by-level launches (A/B and parity checks)
+bool pyr_bands_off() {
+    static const bool v = [] {
+        const char* s = std::getenv("ORBGPU_PYR_BANDS");
+        return s && std::atoi(s) == 0;
+    }();
+    return v;
+}
+
 int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_step, size_t frame_step,
-              orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap, hipStream_t s) {
+              orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap, hipStream_t s, int* err_copy = nullptr) {
     const Geom& g = e->g;
     hipEvent_t* evs = nullptr;
     if (e->profile) {
@@ -435,8 +445,11 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
         evs = e->ev[e->ev_used++].data();
         ORB_HIP(hipEventRecord(evs[0], s));
     }
-    // the tick pipeline is one block per frame: a few frames go level by level over the chip
-    if (batch <= pyr_levels_max_batch())
+    // the tick pipeline is one block per frame: a few frames go in row bands
+    // over the chip (one launch), or level by level when no band plan fits
+    if (batch <= pyr_levels_max_batch() && g.bd_nb > 0 && !pyr_bands_off())
+        ORB_HIP(launch_pyramid_bands(g, batch, e->d_band, e->d_xtab, e->d_ytab, imgs, row_step, frame_step, e->d_pyr, s));
+    else if (batch <= pyr_levels_max_batch())
         ORB_HIP(launch_pyramid_levels(g, batch, e->d_xtab, e->d_ytab, imgs, row_step, frame_step, e->d_pyr, s));
     else
         ORB_HIP(launch_pyramid(g, batch, e->d_pyr_ent, e->d_pyr_tab, imgs, row_step, frame_step, e->d_pyr, s));
@@ -452,7 +465,7 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
     // GaussianBlur is fused into describe (blur of each keypoint's patch);
     // whole blurred levels exist only for the debug API
     ORB_HIP(launch_describe(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_oct_out, e->d_oct_count, kps, desc,
-                            counts, kp_cap, s));
+                            counts, kp_cap, s, err_copy ? e->d_err : nullptr, err_copy));
     if (evs) ORB_HIP(hipEventRecord(evs[4], s));
     if (e->stage_ev[3]) ORB_HIP(hipEventRecord(e->stage_ev[3], s));
     e->last_img = imgs;
@@ -523,6 +536,8 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
     std::vector<int2> ytab, xtab;
     rc = build_geometry(e, ptab, ytab, &xtab);
     if (rc) { delete e; return rc; }
+    std::vector<int4> bands;
+    plan_pyramid_bands(e->g, ytab, bands);
     const Geom& g = e->g;
     const size_t B = (size_t)max_batch;
     e->img_pitch = round_up((size_t)width, 16);
@@ -533,7 +548,8 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
         (rc = dalloc(&e->d_oct_count, (size_t)g.nlevels * B)) || (rc = dalloc(&e->d_err, 1)) ||
         (rc = dalloc(&e->d_img, e->img_pitch * height)) ||
         (rc = dalloc(&e->d_pyr_ent, e->pyr_plan.ent.size())) || (rc = dalloc(&e->d_pyr_tab, e->pyr_plan.tab.size())) ||
-        (rc = dalloc(&e->d_xtab, xtab.size())) || (rc = dalloc(&e->d_ytab, ytab.size()))) {
+        (rc = dalloc(&e->d_xtab, xtab.size())) || (rc = dalloc(&e->d_ytab, ytab.size())) ||
+        (rc = dalloc(&e->d_band, std::max<size_t>(bands.size(), 1)))) {
         delete e;
         return rc;
     }
@@ -554,6 +570,7 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
     if (hipMemcpy(e->d_ptab, ptab.data(), ptab.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess ||
         (!xtab.empty() && hipMemcpy(e->d_xtab, xtab.data(), xtab.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess) ||
         (!ytab.empty() && hipMemcpy(e->d_ytab, ytab.data(), ytab.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess) ||
+        (!bands.empty() && hipMemcpy(e->d_band, bands.data(), bands.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess) ||
         (!e->pyr_plan.ent.empty() && hipMemcpy(e->d_pyr_ent, e->pyr_plan.ent.data(),
                                                e->pyr_plan.ent.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess) ||
         (!e->pyr_plan.tab.empty() && hipMemcpy(e->d_pyr_tab, e->pyr_plan.tab.data(),
@@ -632,11 +649,10 @@ int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int hei
     // block; one async D2H of the whole block; one synchronisation
     for (int y = 0; y < height; ++y) std::memcpy(e->h_img + (size_t)y * e->img_pitch, image + (size_t)y * step, width);
     ORB_HIP(hipMemcpyAsync(e->d_img, e->h_img, e->img_pitch * height, hipMemcpyHostToDevice, s));
+    // describe moves the error word into the output block and clears it
     int rc = run_batch(e, e->d_img, 1, e->img_pitch, e->img_pitch * height, e->d_kps1, e->d_desc1, e->d_count1,
-                       e->max_kps, s);
+                       e->max_kps, s, reinterpret_cast<int*>(e->d_single + 4));
     if (rc) return rc;
-    ORB_HIP(hipMemcpyAsync(e->d_single + 4, e->d_err, sizeof(int), hipMemcpyDeviceToDevice, s));
-    ORB_HIP(hipMemsetAsync(e->d_err, 0, sizeof(int), s));
     ORB_HIP(hipMemcpyAsync(e->h_single, e->d_single, e->single_bytes, hipMemcpyDeviceToHost, s));
     ORB_HIP(hipStreamSynchronize(s));
     int count = 0, err = 0;

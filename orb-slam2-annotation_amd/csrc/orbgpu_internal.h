@@ -40,6 +40,15 @@ __device__ inline int xcd_swizzle(int orig, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
+// 16 bytes read from a 4-byte-aligned address (level rows staged from a
+// dword-aligned column): declaring the alignment keeps the dwordx4 load
+// well-defined instead of promising the 16 bytes of uint4.
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ inline uint4 load16_a4(const uint8_t* p) {
+    const u32x4_a4 v = *reinterpret_cast<const u32x4_a4*>(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // Candidate key packing (FAST output, octree input/output):
 //   bits 0..10  x relative to minBorderX (level x - 16)
 //   bits 11..21 y relative to minBorderY
@@ -81,6 +90,10 @@ struct LevelGeom {
     int tk_ring_rows;         // rows in that ring (levels >= 1: row y lives in slot y mod tk_ring_rows; level 0: tk_nc0 * tk_t0)
     int tk_pitch;             // LDS pitch of the ring rows: w rounded up to 16
     int tk_rec;               // int2 index of row 0's record in the plan table (levels >= 1)
+    // banded pyramid pass (small batches, pyramid.hip pyramid_band_kernel):
+    // this level's rows of a band live in LDS at bd_lds_off with pitch bd_pitch
+    // (levels 0..L-2)
+    int bd_lds_off, bd_pitch;
     // blurred level (all levels, incl. 0): same row pitch as the pyramid
     size_t blur_offset, blur_frame_bytes;
     int blur_tiles_x, blur_tile_base;   // blur work items: 4-column x 64-row strips
@@ -114,6 +127,10 @@ struct Geom {
     int tk_lds_bytes;         // LDS per block
     int tk_nc0;               // level-0 chunk runs in ring 0 (row r: run (r / tk_t0) % tk_nc0, row r % tk_t0 in it)
     int tk_cstride0;          // bytes per chunk run (tk_t0 rows at the level-0 pitch, padded to whole LDS-DMA pieces)
+    // banded pyramid pass (plan_pyramid_bands): bd_nb row bands per frame, one
+    // block each; 0 when the geometry does not fit (the level-by-level launches run)
+    int bd_nb;
+    int bd_lds_bytes;
     LevelGeom lv[kMaxLevels];
 };
 

@@ -26,6 +26,13 @@ int emulate_pyramid(const Geom& g, const std::vector<int2>& ytab, const PyrPlan&
 // level-by-level pyramid for small batches (xtab / ytab: build_resize_tables per level)
 hipError_t launch_pyramid_levels(const Geom& g, int batch, const int2* xtab, const int2* ytab, const uint8_t* img0,
                                  size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream);
+// banded pyramid for small batches: g.bd_nb blocks per frame, every level of a
+// row band in one launch (bands: per band and level (need_lo, need_hi,
+// own_lo, own_hi) rows; level 0: the staged rows).  Fills g.bd_* and
+// g.lv[l].bd_*; bd_nb = 0 when no band count fits the LDS budget.
+void plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, std::vector<int4>& bands);
+hipError_t launch_pyramid_bands(const Geom& g, int batch, const int4* bands, const int2* xtab, const int2* ytab,
+                                const uint8_t* img0, size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream);
 hipError_t launch_pyramid(const Geom& g, int batch, const int4* ents, const int2* tab, const uint8_t* img0,
                           size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream);
 hipError_t pyramid_set_lds_limit(const Geom& g);
@@ -50,7 +57,7 @@ hipError_t launch_octree(const Geom& g, int batch, const uint32_t* cand, const i
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                            const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
-                           hipStream_t stream);
+                           hipStream_t stream, int* err_word = nullptr, int* err_copy = nullptr);
 
 hipError_t launch_match_init(int batch, float minX, float maxX, float minY, float maxY,
                              const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,

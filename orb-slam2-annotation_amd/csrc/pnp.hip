@@ -1,11 +1,11 @@
 // pnp.hip -- PnPsolver's RANSAC loop (src/PnPsolver.cpp:203-349) for a batch
 // of solvers (one per relocalisation candidate keyframe), in two launches:
 //   1  pnp_hyp_kernel: 16 lanes per hypothesis (four per wave) run EPnP
-//      (epnp_wave.h) on its minimal set of 4 correspondences -- speculative,
-//      all n_hyp of every solver;
-//   2  pnp_score_kernel, one 256-thread block per solver, chunks of 64
-//      hypotheses: the waves score them (CheckInliers :352-386, lanes over
-//      correspondences, ballot + popcount), then the whole block replays the
+//      (epnp_wave.h) on its minimal set of 4 correspondences and score it
+//      (CheckInliers :352-386, the group's lanes over the correspondences)
+//      -- speculative, all n_hyp of every solver;
+//   2  pnp_score_kernel, one 256-thread block per solver, chunks of 256
+//      hypothesis counts in LDS: the whole block replays the
 //      reference's loop body in iteration order: a hypothesis with
 //      inliers >= minInliers becomes the best if it beats it (its mask is
 //      written by all threads), and Refine() (:303-349: EPnP over all best
@@ -27,10 +27,24 @@ namespace orbgpu {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kChunk = 64;
+
+#ifdef EPNP_STAMPS  // diagnostic build only (tools/epnp_stamps.py)
+// [0]: EPnP phases of block (0, 0) group 0 of pnp_hyp_kernel; [1]: the first
+// Refine of solver 0; [2]: pnp_score_kernel phases of solver 0
+__device__ unsigned long long g_epnp_stamps[3][32];
+#define SCORE_T(k)                                                                      \
+    do {                                                                                \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_epnp_stamps[2][k] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define SCORE_T(k) ((void)0)
+#endif
+constexpr int kChunk = 256;  // hypothesis counts staged in LDS at a time
 
 struct HypPose {
     double R[9], t[3];
+    int inliers;  // CheckInliers count, by the group that solved it
+    int pad;
 };
 
 struct SampleSrc {  // the minimal set of one hypothesis
@@ -94,7 +108,8 @@ __device__ inline void pose_to_tcw(const HypPose& H, float* T) {  // Rcw/tcw con
 
 __global__ __launch_bounds__(64) void pnp_hyp_kernel(const orbgpu_pnp_problem* __restrict__ probs,
                                                      const float* __restrict__ P3g, const float* __restrict__ P2g,
-                                                     const int* __restrict__ samples, HypPose* __restrict__ hyps) {
+                                                     const float* __restrict__ errg, const int* __restrict__ samples,
+                                                     HypPose* __restrict__ hyps) {
     __shared__ double s_ep[4][epnp::kWaveScratch];
     const orbgpu_pnp_problem& P = probs[blockIdx.y];
     const int lane = threadIdx.x, g = lane >> 4, r = lane & 15;
@@ -102,13 +117,32 @@ __global__ __launch_bounds__(64) void pnp_hyp_kernel(const orbgpu_pnp_problem* _
     if (h >= P.n_hyp) return;  // the whole 16-lane group leaves together
     const size_t slot = (size_t)P.sample_offset + h;
     SampleSrc src{P3g + 3 * (size_t)P.offset, P2g + 2 * (size_t)P.offset, samples + 4 * slot};
+    const epnp::Camera cam = camera_of(P);
     epnp::Pose pose;
-    epnp::compute_pose_group<16>(src, camera_of(P), pose, r, s_ep[g]);
-    if (r == 0) {
-        HypPose& out = hyps[slot];
-        for (int k = 0; k < 9; ++k) out.R[k] = pose.R[k];
-        for (int k = 0; k < 3; ++k) out.t[k] = pose.t[k];
-    }
+#ifdef EPNP_STAMPS
+    unsigned long long* st = (blockIdx.x == 0 && blockIdx.y == 0 && g == 0) ? g_epnp_stamps[0] : nullptr;
+#else
+    unsigned long long* st = nullptr;
+#endif
+    epnp::compute_pose_group<16>(src, cam, pose, r, s_ep[g], st);
+    HypPose H;
+    for (int k = 0; k < 9; ++k) H.R[k] = pose.R[k];
+    for (int k = 0; k < 3; ++k) H.t[k] = pose.t[k];
+    // CheckInliers (:352-386) of this hypothesis by the same group: every
+    // hypothesis of the batch is scored here, in parallel, so the replay in
+    // pnp_score_kernel only reads the counts
+    const float* P3 = P3g + 3 * (size_t)P.offset;
+    const float* P2 = P2g + 2 * (size_t)P.offset;
+    const float* E = errg + P.offset;
+    int cnt = 0;
+    for (int i = r; i < P.n; i += 16) cnt += pnp_inlier(H, cam, P3 + 3 * i, P2 + 2 * i, E[i]);
+    cnt += __shfl_xor(cnt, 1, 16);
+    cnt += __shfl_xor(cnt, 2, 16);
+    cnt += __shfl_xor(cnt, 4, 16);
+    cnt += __shfl_xor(cnt, 8, 16);
+    H.inliers = cnt;
+    H.pad = 0;
+    if (r == 0) hyps[slot] = H;
 }
 
 __global__ __launch_bounds__(kThreads) void pnp_score_kernel(const orbgpu_pnp_problem* __restrict__ probs,
@@ -142,14 +176,10 @@ __global__ __launch_bounds__(kThreads) void pnp_score_kernel(const orbgpu_pnp_pr
         s_state[5] = 0;
     }
     __syncthreads();
+    SCORE_T(0);
     for (int base = 0; base < P.n_hyp && !s_state[2]; base += kChunk) {
         const int nh = min(kChunk, P.n_hyp - base);
-        for (int h = wave; h < nh; h += kThreads / 64) {
-            const HypPose& H = HP[base + h];
-            int cnt = 0;
-            for (int i = lane; i < P.n; i += 64) cnt += __popcll(__ballot(pnp_inlier(H, cam, P3 + 3 * i, P2 + 2 * i, E[i])));
-            if (lane == 0) s_cnt[h] = cnt;
-        }
+        for (int h = tid; h < nh; h += kThreads) s_cnt[h] = HP[base + h].inliers;  // scored by pnp_hyp_kernel
         __syncthreads();
         for (int h = 0; h < nh; ++h) {  // block-uniform replay of the loop body (:224-299)
             const int c = s_cnt[h];
@@ -158,6 +188,7 @@ __global__ __launch_bounds__(kThreads) void pnp_score_kernel(const orbgpu_pnp_pr
                 const HypPose& H = HP[base + h];
                 for (int i = tid; i < P.n; i += kThreads) BM[i] = pnp_inlier(H, cam, P3 + 3 * i, P2 + 2 * i, E[i]);
                 __syncthreads();
+                SCORE_T(1);
                 if (tid == 0) {
                     s_state[0] = c;
                     s_state[1] = base + h;
@@ -178,15 +209,22 @@ __global__ __launch_bounds__(kThreads) void pnp_score_kernel(const orbgpu_pnp_pr
                     }
                     __builtin_amdgcn_s_waitcnt(0);  // the list is in memory before any lane reads it
                     __builtin_amdgcn_wave_barrier();
+                    SCORE_T(2);
                     ListSrc src{P3, P2, list, m};
                     epnp::Pose pose;
-                    if (m > 0) epnp::compute_pose_group<64>(src, cam, pose, lane, s_ep);
+#ifdef EPNP_STAMPS
+                    unsigned long long* st = (blockIdx.x == 0 && !s_state[3]) ? g_epnp_stamps[1] : nullptr;
+#else
+                    unsigned long long* st = nullptr;
+#endif
+                    if (m > 0) epnp::compute_pose_group<64>(src, cam, pose, lane, s_ep, st);
                     if (lane == 0) {
                         for (int k = 0; k < 9; ++k) s_ref.R[k] = m > 0 ? pose.R[k] : 0.0;
                         for (int k = 0; k < 3; ++k) s_ref.t[k] = m > 0 ? pose.t[k] : 0.0;
                     }
                 }
                 __syncthreads();
+                SCORE_T(3);
                 int cnt = 0;
                 for (int i = tid; i < P.n; i += kThreads) {
                     const bool in = pnp_inlier(s_ref, cam, P3 + 3 * i, P2 + 2 * i, E[i]);
@@ -212,6 +250,7 @@ __global__ __launch_bounds__(kThreads) void pnp_score_kernel(const orbgpu_pnp_pr
         }
         __syncthreads();
     }
+    SCORE_T(4);
     if (tid == 0) {
         orbgpu_pnp_result& R = results[blockIdx.x];
         R.found = s_state[2];
@@ -228,6 +267,12 @@ __global__ __launch_bounds__(kThreads) void pnp_score_kernel(const orbgpu_pnp_pr
 
 size_t pnp_hyp_bytes() { return sizeof(HypPose); }
 
+#ifdef EPNP_STAMPS
+extern "C" int orbgpu_debug_epnp_stamps(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_epnp_stamps), sizeof(g_epnp_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif
+
 hipError_t launch_pnp_ransac(int batch, const orbgpu_pnp_problem* probs, int max_hyp, const float* P3,
                              const float* P2, const float* maxerr, const int* samples, void* hyps, int* lists,
                              orbgpu_pnp_result* results, uint8_t* best_mask, uint8_t* refined_mask,
@@ -235,7 +280,7 @@ hipError_t launch_pnp_ransac(int batch, const orbgpu_pnp_problem* probs, int max
     if (batch <= 0) return hipSuccess;
     if (max_hyp > 0)
         hipLaunchKernelGGL(pnp_hyp_kernel, dim3((max_hyp + 3) / 4, batch), dim3(64), 0, stream, probs, P3, P2,
-                           samples, static_cast<HypPose*>(hyps));
+                           maxerr, samples, static_cast<HypPose*>(hyps));
     hipLaunchKernelGGL(pnp_score_kernel, dim3(batch), dim3(kThreads), 0, stream, probs,
                        static_cast<const HypPose*>(hyps), P3, P2, maxerr, lists, results, best_mask, refined_mask);
     return hipGetLastError();

@@ -25,6 +25,8 @@
 // the exact horizontal sum, whose high half is the (h >> 4) of the vertical
 // pass.
 // The vertical pass is four SDWA/op_sel instructions per pixel.
+#include <algorithm>
+
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
 
@@ -452,6 +454,101 @@ hipError_t launch_pyramid_levels(const Geom& g, int batch, const int2* xtab, con
     return hipSuccess;
 }
 
+// ---- small batches, one launch: row bands with every level in LDS ----
+// The level-by-level launches cost a dependent launch each (7 x ~4.4 us at
+// one 640x480 frame, measured, for ~1 us of work each).  Here g.bd_nb blocks
+// per frame each own a band of rows of every level and compute all levels of
+// it in one launch: level 0's rows the band needs are staged in LDS, then
+// level l is computed from level l-1's LDS rows into LDS (levels < L-1) and
+// its OWN rows are written to HBM.  A band needs, at level l, its own rows
+// plus the source rows of the rows it needs at level l+1 (plan_pyramid_bands:
+// a few rows of halo per level, recomputed by the neighbouring band with the
+// same arithmetic, so the written rows are exactly the level kernel's).
+constexpr int kBandThreads = 256;
+constexpr int kBandMaxLds = 96 * 1024;
+
+__device__ __forceinline__ uint32_t resize_quad(const uint8_t* r0, const uint8_t* r1, int x0, int dw, int simd_end,
+                                                const int2* __restrict__ xt, uint32_t b0, uint32_t b1) {
+    uint32_t out = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int x = x0 + k;
+        if (x >= dw) break;
+        const int2 tx = xt[x];
+        const int sx0 = tx.x & 0xFFFF, sx1 = (int)((uint32_t)tx.x >> 16);
+        const uint32_t a0 = (uint32_t)tx.y & 0xFFFFu, a1 = (uint32_t)tx.y >> 16;
+        const uint32_t h0 = r0[sx0] * a0 + r0[sx1] * a1, h1 = r1[sx0] * a0 + r1[sx1] * a1;
+        const uint32_t v = x < simd_end ? ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2u) >> 2
+                                        : (h0 * b0 + h1 * b1 + (1u << 21)) >> 22;
+        out |= v << (8 * k);
+    }
+    return out;
+}
+
+__global__ __launch_bounds__(kBandThreads) void pyramid_band_kernel(const Geom g, const int4* __restrict__ bands,
+                                                                     const int2* __restrict__ xtab,
+                                                                     const int2* __restrict__ ytab,
+                                                                     const uint8_t* __restrict__ img0, size_t row0,
+                                                                     size_t frame0, uint8_t* __restrict__ pyr) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_rows[];
+    const int L = g.nlevels, tid = threadIdx.x, f = blockIdx.y;
+    const int4* B = bands + (size_t)blockIdx.x * L;
+    {  // stage level 0's rows [B[0].x, B[0].y)
+        const LevelGeom& v = g.lv[0];
+        const int4 r = B[0];
+        const uint8_t* src = img0 + (size_t)f * frame0;
+        uint8_t* dst = s_rows + v.bd_lds_off;
+        if ((((uintptr_t)src | row0) & 3) == 0) {
+            const int words = (v.w + 3) >> 2, n = (r.y - r.x) * words;
+            for (int i = tid; i < n; i += kBandThreads) {
+                const int y = i / words, c = i - y * words;
+                // the last word of a row may end past w: inside the row when the step is a multiple of 4
+                // and the row is not the image's last; the last row is read bytewise
+                const uint8_t* p = src + (size_t)(r.x + y) * row0 + 4 * c;
+                uint32_t w;
+                if (4 * c + 4 <= v.w) {
+                    w = *reinterpret_cast<const uint32_t*>(p);
+                } else {
+                    w = 0;
+                    for (int k = 0; 4 * c + k < v.w; ++k) w |= (uint32_t)p[k] << (8 * k);
+                }
+                *reinterpret_cast<uint32_t*>(dst + y * v.bd_pitch + 4 * c) = w;
+            }
+        } else {
+            const int n = (r.y - r.x) * v.w;
+            for (int i = tid; i < n; i += kBandThreads) {
+                const int y = i / v.w, c = i - y * v.w;
+                dst[y * v.bd_pitch + c] = src[(size_t)(r.x + y) * row0 + c];
+            }
+        }
+    }
+    __syncthreads();
+    for (int l = 1; l < L; ++l) {
+        const LevelGeom& v = g.lv[l];
+        const LevelGeom& p = g.lv[l - 1];
+        const int4 r = B[l];
+        const int src_lo = B[l - 1].x;
+        const uint8_t* srow = s_rows + p.bd_lds_off;
+        uint8_t* drow = s_rows + v.bd_lds_off;
+        const bool keep = l + 1 < L;
+        const int quads = (v.w + 3) >> 2, n = (r.y - r.x) * quads;
+        const int2* xt = xtab + v.xtab_offset;
+        const int2* yt = ytab + v.ytab_offset;
+        uint8_t* out = pyr + v.offset + (size_t)f * v.frame_bytes;
+        for (int i = tid; i < n; i += kBandThreads) {
+            const int yy = i / quads, q = i - yy * quads, y = r.x + yy;
+            const int2 ty = yt[y];
+            const uint8_t* r0 = srow + ((ty.x & 0xFFFF) - src_lo) * p.bd_pitch;
+            const uint8_t* r1 = srow + ((int)((uint32_t)ty.x >> 16) - src_lo) * p.bd_pitch;
+            const uint32_t o = resize_quad(r0, r1, 4 * q, v.w, v.simd_end, xt, (uint32_t)ty.y & 0xFFFFu,
+                                           (uint32_t)ty.y >> 16);
+            if (keep) *reinterpret_cast<uint32_t*>(drow + yy * v.bd_pitch + 4 * q) = o;
+            if (y >= r.z && y < r.w) *reinterpret_cast<uint32_t*>(out + (size_t)y * v.pitch + 4 * q) = o;
+        }
+        __syncthreads();
+    }
+}
+
 hipError_t launch_pyramid(const Geom& g, int batch, const int4* ents, const int2* tab, const uint8_t* img0,
                           size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream) {
     if (g.nlevels < 2) return hipSuccess;
@@ -461,8 +558,76 @@ hipError_t launch_pyramid(const Geom& g, int batch, const int4* ents, const int2
 
 hipError_t pyramid_set_lds_limit(const Geom& g) {
     if (g.nlevels < 2) return hipSuccess;
+    if (g.bd_nb > 0) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&pyramid_band_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kBandMaxLds);
+        if (e != hipSuccess) return e;
+    }
     return g.tk_e == 1 ? launch_e<1>(g, 0, nullptr, nullptr, nullptr, 0, 0, nullptr, nullptr, true)
                        : launch_e<2>(g, 0, nullptr, nullptr, nullptr, 0, 0, nullptr, nullptr, true);
+}
+
+void plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, std::vector<int4>& bands) {
+    const int L = g.nlevels;
+    g.bd_nb = 0;
+    g.bd_lds_bytes = 0;
+    bands.clear();
+    if (L < 2) return;
+    auto src_rows = [&](int l, int lo, int hi) {  // level l-1 rows read by level-l rows [lo, hi)
+        const int2* yt = ytab.data() + g.lv[l].ytab_offset;
+        return int2{yt[lo].x & 0xFFFF, (int)((uint32_t)yt[hi - 1].x >> 16) + 1};
+    };
+    // the most bands (smallest halo share) whose rows fit the LDS budget; at
+    // least one own row per band at every level
+    for (int nb : {32, 24, 16, 8}) {
+        bool ok = true;
+        for (int l = 1; l < L; ++l) ok = ok && g.lv[l].h >= nb;
+        if (!ok) continue;
+        std::vector<int4> b((size_t)nb * L);
+        std::vector<int> cap(L, 0);
+        for (int k = 0; k < nb; ++k) {
+            int4* B = b.data() + (size_t)k * L;
+            for (int l = 1; l < L; ++l) {
+                const int h = g.lv[l].h;
+                B[l] = int4{0, 0, (int)((long)k * h / nb), (int)((long)(k + 1) * h / nb)};
+            }
+            B[L - 1].x = B[L - 1].z;
+            B[L - 1].y = B[L - 1].w;
+            for (int l = L - 1; l >= 1; --l) {
+                const int2 s = src_rows(l, B[l].x, B[l].y);
+                if (l == 1) {
+                    B[0] = int4{s.x, s.y, 0, 0};
+                } else {
+                    B[l - 1].x = std::min(B[l - 1].z, s.x);
+                    B[l - 1].y = std::max(B[l - 1].w, s.y);
+                }
+            }
+            for (int l = 0; l + 1 < L; ++l) cap[l] = std::max(cap[l], B[l].y - B[l].x);
+        }
+        int off = 0;
+        for (int l = 0; l + 1 < L; ++l) {
+            LevelGeom& v = g.lv[l];
+            v.bd_pitch = (v.w + 15) & ~15;
+            v.bd_lds_off = off;
+            off += cap[l] * v.bd_pitch;
+        }
+        if (off > kBandMaxLds) continue;
+        g.lv[L - 1].bd_pitch = 0;
+        g.lv[L - 1].bd_lds_off = 0;
+        g.bd_nb = nb;
+        g.bd_lds_bytes = off;
+        bands = std::move(b);
+        return;
+    }
+}
+
+hipError_t launch_pyramid_bands(const Geom& g, int batch, const int4* bands, const int2* xtab, const int2* ytab,
+                                const uint8_t* img0, size_t row0, size_t frame0, uint8_t* pyr, hipStream_t stream) {
+    if (g.nlevels < 2 || batch <= 0) return hipSuccess;
+    if (g.bd_nb <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pyramid_band_kernel, dim3(g.bd_nb, batch), dim3(kBandThreads), (size_t)g.bd_lds_bytes, stream,
+                       g, bands, xtab, ytab, img0, row0, frame0, pyr);
+    return hipGetLastError();
 }
 
 }  // namespace orbgpu

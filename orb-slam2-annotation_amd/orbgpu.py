@@ -286,6 +286,10 @@ class Extractor:
             event.record()  # torch creates the HIP event lazily; make sure it exists
             ptr = event.cuda_event
         _check(lib().orbgpu_extractor_set_stage_event(self.h, self.STAGES.index(stage), ptr), "set_stage_event")
+        # the library keeps the raw hipEvent_t: hold the owner so it outlives the registration
+        if not hasattr(self, "_stage_events"):
+            self._stage_events = {}
+        self._stage_events[stage] = event
 
     def stage_times(self, reset: bool = True):
         """(dict stage -> summed ms, number of extractions) since last reset."""
