@@ -102,7 +102,7 @@ __host__ __device__ void svd_hestenes(double* a, double* s, double* v) {
                     gamma += a[k * N + p] * a[k * N + q];
                 }
                 double c, sn;
-                if (!jacobi_rotation(alpha, beta, gamma, negl, c, sn)) continue;
+                if (!jacobi_rot(alpha, beta, gamma, negl, c, sn)) continue;
                 rotated = true;
                 for (int k = 0; k < M; ++k) {
                     const double x = a[k * N + p], y = a[k * N + q];

@@ -26,6 +26,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "epnp.h"
 #include "group_sum.h"
 #include "jacobi_group.h"
@@ -249,7 +251,12 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
             a[c] = r < 12 ? s_mtm[r * 12 + c] : 0.0;
             v[c] = (r == c) ? 1.0 : 0.0;
         }
-        hestenes_group<12, G>(a, v);
+        const int sweeps = hestenes_group<12, G>(a, v);
+#ifdef EPNP_STAMPS
+        if (stamps && r == 0) stamps[16] = (unsigned long long)sweeps;
+#else
+        (void)sweeps;
+#endif
         double lam[12];
 #pragma unroll
         for (int j = 0; j < 12; ++j) lam[j] = sqrt(gsum<G>(a[j] * a[j]));
@@ -329,8 +336,15 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
             for (int i = 0; i < 4; ++i) betas[i] += x[i];
         }
     };
-    // compute_R_and_t (:735-745) with the per-correspondence sums over the group
-    auto r_and_t = [&](const double* betas, Pose& P) -> double {
+    // compute_R_and_t (:735-745): per-correspondence sums over the group
+    // (Serial = false) or over all correspondences on the calling lane
+    // (Serial = true: the minimal sets, one beta approximation per lane)
+    // Mode 0: the group's lanes (stride G, group reductions); 1: the calling
+    // lane alone; 2: the lane's 16-lane row (stride 16, row reductions)
+    auto r_and_t_impl = [&](const double* betas, Pose& P, auto mode_tag) -> double {
+        constexpr int Mode = decltype(mode_tag)::value;
+        const int i0 = Mode == 0 ? r : Mode == 1 ? 0 : (r & 15), di = Mode == 0 ? G : Mode == 1 ? 1 : 16;
+        auto red = [&](double x) { return Mode == 0 ? gsum<G>(x) : Mode == 1 ? x : gsum<16>(x); };
         double ccs[4][3];
         for (int i = 0; i < 4; ++i) ccs[i][0] = ccs[i][1] = ccs[i][2] = 0.0f;
         for (int i = 0; i < 4; ++i) {
@@ -353,7 +367,7 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
                     for (int j = 0; j < 3; ++j) ccs[i][j] = -ccs[i][j];
         }
         double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
-        for (int i = r; i < n; i += G) {
+        for (int i = i0; i < n; i += di) {
             double pw[3], u, v, pc[3];
             src.get(i, pw, u, v);
             pc_of(pw, pc);
@@ -363,11 +377,11 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
             }
         }
         for (int j = 0; j < 3; ++j) {
-            pc0[j] = gsum<G>(pc0[j]) / n;
-            pw0[j] = gsum<G>(pw0[j]) / n;
+            pc0[j] = red(pc0[j]) / n;
+            pw0[j] = red(pw0[j]) / n;
         }
         double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        for (int i = r; i < n; i += G) {
+        for (int i = i0; i < n; i += di) {
             double pw[3], u, v, pc[3];
             src.get(i, pw, u, v);
             pc_of(pw, pc);
@@ -378,7 +392,7 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
             }
         }
 #pragma unroll
-        for (int k = 0; k < 9; ++k) abt[k] = gsum<G>(abt[k]);
+        for (int k = 0; k < 9; ++k) abt[k] = red(abt[k]);
         double s[3], vv[9];
         svd_hestenes<3, 3>(abt, s, vv);  // abt columns = U_j s_j
         double U[9];
@@ -398,7 +412,7 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
         P.t[1] = pc0[1] - dot3(R + 3, pw0);
         P.t[2] = pc0[2] - dot3(R + 6, pw0);
         double sum2 = 0.0;
-        for (int i = r; i < n; i += G) {
+        for (int i = i0; i < n; i += di) {
             double pw[3], u, v;
             src.get(i, pw, u, v);
             const double Xc = dot3(R, pw) + P.t[0], Yc = dot3(R + 3, pw) + P.t[1];
@@ -406,8 +420,9 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
             const double ue = cam.uc + cam.fu * Xc * inv_Zc, ve = cam.vc + cam.fv * Yc * inv_Zc;
             sum2 += sqrt((u - ue) * (u - ue) + (v - ve) * (v - ve));
         }
-        return gsum<G>(sum2) / n;
+        return red(sum2) / n;
     };
+    auto r_and_t = [&](const double* betas, Pose& P) { return r_and_t_impl(betas, P, std::integral_constant<int, 0>{}); };
     double best_err;
     auto keep = [&](double e, const Pose& P, bool first) {  // N = 1; err[2] < err[N] -> 2; err[3] < err[N] -> 3
         if (first || e < best_err) {
@@ -415,6 +430,79 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
             out = P;
         }
     };
+    if constexpr (G == 16 || G == 64) {
+        // The three beta approximations side by side: on lanes 0, 1, 2 of a
+        // 16-lane group (minimal sets: compute_R_and_t over the n
+        // correspondences on the lane), or on rows 0, 1, 2 of the wave
+        // (Refine: compute_R_and_t with the row's 16 lanes over all
+        // correspondences); the other lanes / row repeat the third.  Then the
+        // reference's choice (1, then 2 or 3 if strictly better, in order).
+        // The 6 x 4 / 6 x 3 systems of approximations 1 and 2 are solved as
+        // 6 x 5 with zero columns: the Jacobi skips every pair with a zero
+        // column and the pseudo-inverse gives them zero, so the solution is
+        // bit for bit the smaller system's.
+        const int ap = min(G == 16 ? r : (r >> 4), 2);
+        double l[30], b5[5], B[4];
+        for (int i = 0; i < 6; ++i) {
+            const double* Lr = L + 10 * i;
+            l[5 * i] = Lr[0];
+            l[5 * i + 1] = Lr[1];
+            l[5 * i + 2] = ap == 0 ? Lr[3] : Lr[2];
+            l[5 * i + 3] = ap == 0 ? Lr[6] : ap == 1 ? 0.0 : Lr[3];
+            l[5 * i + 4] = ap == 2 ? Lr[4] : 0.0;
+        }
+        svd_solve<6, 5>(l, rho, b5);
+        if (ap == 0) {  // find_betas_approx_1 (:747-781)
+            if (b5[0] < 0) {
+                B[0] = sqrt(-b5[0]);
+                B[1] = -b5[1] / B[0];
+                B[2] = -b5[2] / B[0];
+                B[3] = -b5[3] / B[0];
+            } else {
+                B[0] = sqrt(b5[0]);
+                B[1] = b5[1] / B[0];
+                B[2] = b5[2] / B[0];
+                B[3] = b5[3] / B[0];
+            }
+        } else {  // find_betas_approx_2 (:783-815) / _3 (:817-851)
+            if (b5[0] < 0) {
+                B[0] = sqrt(-b5[0]);
+                B[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;
+            } else {
+                B[0] = sqrt(b5[0]);
+                B[1] = (b5[2] > 0) ? sqrt(b5[2]) : 0.0;
+            }
+            if (b5[1] < 0) B[0] = -B[0];
+            B[2] = ap == 2 ? b5[3] / B[0] : 0.0;
+            B[3] = 0.0;
+        }
+        EPNP_T(7);
+        gauss_newton(B);
+        EPNP_T(8);
+        Pose P;
+        double e;
+        if constexpr (G == 16)
+            e = r_and_t_impl(B, P, std::integral_constant<int, 1>{});
+        else
+            e = r_and_t_impl(B, P, std::integral_constant<int, 2>{});
+        EPNP_T(15);
+        const int base = G == 16 ? ((int)(threadIdx.x & 63) & ~15) : 0, step = G == 16 ? 1 : 16;
+        const double e0 = __shfl(e, base, 64), e1 = __shfl(e, base + step, 64), e2 = __shfl(e, base + 2 * step, 64);
+        int pick = 0;
+        double best = e0;
+        if (e1 < best) {
+            best = e1;
+            pick = 1;
+        }
+        if (e2 < best) {
+            best = e2;
+            pick = 2;
+        }
+        const int src_lane = base + pick * step;
+        for (int k = 0; k < 9; ++k) out.R[k] = __shfl(P.R[k], src_lane, 64);
+        for (int k = 0; k < 3; ++k) out.t[k] = __shfl(P.t[k], src_lane, 64);
+        return best;
+    } else {
     {  // find_betas_approx_1 (:747-781)
         double l[24], b4[4], B[4];
         for (int i = 0; i < 6; ++i) {
@@ -490,6 +578,7 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
     }
     EPNP_T(15);
     return best_err;
+    }
 }
 
 }  // namespace epnp

@@ -70,12 +70,30 @@ __global__ __launch_bounds__(kNormThreads) void init_normalize_kernel(const floa
             }
             __syncthreads();
             if (tid < 4) {
+                // 32 keypoints per step: their LDS reads issued ahead of the dependent adds
                 const int cnt = min(kNormChunk, n - base);
+                const float* colv = reinterpret_cast<const float*>(s_kp[fr]) + ax;
+                int i = 0;
+                if (pass == 0) {
+                    for (; i + 32 <= cnt; i += 32) {
+                        float v[32];
+#pragma unroll
+                        for (int k = 0; k < 32; ++k) v[k] = colv[2 * (i + k)];
+#pragma unroll
+                        for (int k = 0; k < 32; ++k) acc = __fadd_rn(acc, v[k]);
+                    }
+                } else {
+                    for (; i + 32 <= cnt; i += 32) {
+                        float v[32];
+#pragma unroll
+                        for (int k = 0; k < 32; ++k) v[k] = colv[2 * (i + k)];
+#pragma unroll
+                        for (int k = 0; k < 32; ++k) acc = __fadd_rn(acc, fabsf(__fsub_rn(v[k], mean)));
+                    }
+                }
                 const float* col = reinterpret_cast<const float*>(s_kp[fr]) + ax;
-                if (pass == 0)
-                    for (int i = 0; i < cnt; ++i) acc = __fadd_rn(acc, col[2 * i]);
-                else
-                    for (int i = 0; i < cnt; ++i) acc = __fadd_rn(acc, fabsf(__fsub_rn(col[2 * i], mean)));
+                for (; i < cnt; ++i)
+                    acc = pass == 0 ? __fadd_rn(acc, col[2 * i]) : __fadd_rn(acc, fabsf(__fsub_rn(col[2 * i], mean)));
             }
         }
         if (pass == 0) mean = __fdiv_rn(acc, (float)n);

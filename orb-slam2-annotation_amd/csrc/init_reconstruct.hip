@@ -7,10 +7,12 @@
 // are built on the host (8 for a homography, 4 for an essential matrix);
 // CheckRT -- a 4x4 linear triangulation plus the depth, parallax and
 // reprojection tests for every inlier match under every hypothesis -- is
-// the data-parallel part and runs on the GPU: one 256-thread block per
-// hypothesis, lanes over matches.  The block also counts nGood and finds
-// the parallax the reference reads after sorting (the min(50, nGood-1)-th
-// smallest cosine) by an order-statistic walk over the cosines kept in LDS.
+// the data-parallel part and runs on the GPU: one thread per (match,
+// hypothesis) over the whole chip (check_rt_kernel), then one block per
+// hypothesis counts nGood and finds the parallax the reference reads after
+// sorting (the min(50, nGood-1)-th smallest cosine) by a radix select
+// (rt_parallax_kernel).  (Round 2 ran one block per hypothesis with an
+// order-statistic walk: 177 us for 8 hypotheses x 1000 matches.)
 //
 // OpenCV's SVDs (cv::SVD::compute of float Mats, Jacobi in float) are not
 // reproducible bit for bit: the 3x3 decompositions and each match's 4x4
@@ -61,17 +63,12 @@ __global__ __launch_bounds__(kRecThreads) void check_rt_kernel(const float4* __r
                                                                const unsigned char* __restrict__ inl, int n,
                                                                const RecHyp* __restrict__ hyps, float fx, float fy,
                                                                float cx, float cy, float th2,
-                                                               int* __restrict__ n_good, float* __restrict__ parallax,
                                                                unsigned char* __restrict__ good,
-                                                               float* __restrict__ p3d) {
-    extern __shared__ unsigned s_key[];  // cosine keys of the counted matches, ~0u elsewhere
-    __shared__ int s_cnt;
-    const int h = blockIdx.x, tid = threadIdx.x;
+                                                               float* __restrict__ p3d,
+                                                               unsigned* __restrict__ keys) {
+    const int h = blockIdx.y, m = blockIdx.x * kRecThreads + threadIdx.x;
     const RecHyp H = hyps[h];
-    if (tid == 0) s_cnt = 0;
-    __syncthreads();
-    int cnt = 0;
-    for (int m = tid; m < n; m += kRecThreads) {
+    if (m < n) {
         unsigned key = ~0u;
         unsigned char gflag = 0;
         float X[3] = {0.f, 0.f, 0.f};
@@ -121,55 +118,97 @@ __global__ __launch_bounds__(kRecThreads) void check_rt_kernel(const float4* __r
             if (ok) {
                 key = min(ord_key(cosPar), 0xFFFFFFFEu);  // ~0u marks a match CheckRT did not count
                 gflag = (double)cosPar < 0.99998 ? 1 : 0;
-                ++cnt;
             } else {
                 X[0] = X[1] = X[2] = 0.f;
             }
         }
-        s_key[m] = key;
+        keys[(size_t)h * n + m] = key;
         good[(size_t)h * n + m] = key != ~0u ? (unsigned char)(gflag | 2) : 0;  // bit 1: counted in nGood
         float* o = p3d + 3 * ((size_t)h * n + m);
         o[0] = X[0];
         o[1] = X[1];
         o[2] = X[2];
     }
-    atomicAdd(&s_cnt, cnt);
+}
+
+// nGood and the parallax of one hypothesis (:1102-1110): the count of the
+// counted matches and the k-th smallest of their cosines, k = min(50,
+// nGood - 1) -- vCosParallax[k] after the reference's sort -- by a radix
+// select (four 8-bit histogram passes in LDS) over the keys check_rt_kernel
+// wrote; matches it did not count carry ~0u, above every counted key, so they
+// never reach rank k < nGood
+constexpr int kSelThreads = 1024;
+__global__ __launch_bounds__(kSelThreads) void rt_parallax_kernel(const unsigned* __restrict__ keys, int n,
+                                                                  int* __restrict__ n_good,
+                                                                  float* __restrict__ parallax) {
+    __shared__ int s_hist[256];
+    __shared__ int s_wsum[kSelThreads / 64];
+    __shared__ unsigned s_prefix;
+    __shared__ int s_k;
+    const int h = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const unsigned* K = keys + (size_t)h * n;
+    int cnt = 0;
+    for (int m = tid; m < n; m += kSelThreads) cnt += K[m] != ~0u;
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if (lane == 0) s_wsum[wave] = cnt;
     __syncthreads();
-    if (tid >= 64) return;
-    // wave 0: the k-th smallest cosine, k = min(50, nGood - 1) (:1102-1110), walking the distinct values
-    const int ng = s_cnt;
-    float par = 0.f;
-    if (ng > 0) {
-        const int k = min(50, ng - 1);
-        unsigned last = 0u;
-        int below = 0;  // keys < current value
-        bool first = true;
-        unsigned val = 0u;
-        while (true) {
-            unsigned mn = ~0u;
-            for (int m = tid; m < n; m += 64) {
-                const unsigned kk = s_key[m];
-                if (kk != ~0u && (first || kk > last)) mn = min(mn, kk);
-            }
-            for (int o = 32; o > 0; o >>= 1) mn = min(mn, (unsigned)__shfl_xor((int)mn, o, 64));
-            if (mn == ~0u) break;  // unreachable: ng keys are present
-            int eq = 0;
-            for (int m = tid; m < n; m += 64) eq += s_key[m] == mn ? 1 : 0;
-            for (int o = 32; o > 0; o >>= 1) eq += __shfl_xor(eq, o, 64);
-            if (below + eq > k) {
-                val = mn;
-                break;
-            }
-            below += eq;
-            last = mn;
-            first = false;
+    int ng = 0;
+    for (int w = 0; w < kSelThreads / 64; ++w) ng += s_wsum[w];
+    if (ng == 0) {
+        if (tid == 0) {
+            n_good[h] = 0;
+            parallax[h] = 0.f;
         }
-        // parallax = acos(c) * 180 / CV_PI (float acos, float * int, then the double division)
-        par = (float)((double)(acosf(key_float(val)) * 180) / 3.14159265358979323846);
+        return;
     }
     if (tid == 0) {
+        s_prefix = 0u;
+        s_k = min(50, ng - 1);
+    }
+    unsigned mask = 0u;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        if (tid < 256) s_hist[tid] = 0;
+        __syncthreads();
+        const unsigned prefix = s_prefix;
+        for (int m = tid; m < n; m += kSelThreads) {
+            const unsigned key = K[m];
+            if ((key & mask) == prefix) atomicAdd(&s_hist[(key >> shift) & 255u], 1);
+        }
+        __syncthreads();
+        if (wave == 0) {  // the bin holding rank k: lane owns bins 4 lane .. 4 lane + 3
+            int c[4], sum = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                c[q] = s_hist[4 * lane + q];
+                sum += c[q];
+            }
+            int incl = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += t;
+            }
+            const int k = s_k;
+            int below = incl - sum;
+            if (below <= k && k < incl) {  // exactly one lane
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (k < below + c[q]) {
+                        s_prefix = prefix | ((unsigned)(4 * lane + q) << shift);
+                        s_k = k - below;
+                        break;
+                    }
+                    below += c[q];
+                }
+            }
+        }
+        mask |= 255u << shift;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        // parallax = acos(c) * 180 / CV_PI (float acos, float * int, then the double division)
         n_good[h] = ng;
-        parallax[h] = par;
+        parallax[h] = (float)((double)(acosf(key_float(s_prefix)) * 180) / 3.14159265358979323846);
     }
 }
 
@@ -392,6 +431,7 @@ extern "C" int orbgpu_init_reconstruct(int model, const float* kp1, int n1, cons
     int* d_ng;
     float *d_par, *d_p3;
     unsigned char* d_good;
+    unsigned* d_key;
     rc = call.run([&](HostCall& A) {
         d_pts = reinterpret_cast<const float4*>(A.in(pts.data(), pts.size()));
         d_inl = A.in(inl.data(), (size_t)n);
@@ -400,14 +440,22 @@ extern "C" int orbgpu_init_reconstruct(int model, const float* kp1, int n1, cons
         d_par = A.out<float>((size_t)nh);
         d_good = A.out<unsigned char>(nhn);
         d_p3 = A.out<float>(3 * nhn);
+        d_key = A.out<unsigned>(nhn);  // scratch: the cosine keys between the two kernels
     });
     if (rc) return rc;
     std::vector<int> ng(nh);
     std::vector<float> par(nh);
     std::vector<unsigned char> good(nhn);
     std::vector<float> P3(3 * nhn);
-    hipLaunchKernelGGL(check_rt_kernel, dim3(nh), dim3(kRecThreads), 4 * (size_t)n, ctx->stream, d_pts, d_inl,
-                       n_matches, d_h, fx, fy, cx, cy, th2, d_ng, d_par, d_good, d_p3);
+    // one match per thread over every (match block, hypothesis): a few
+    // hypotheses x ~1000 matches is far below one wave per SIMD otherwise
+    if (n_matches > 0) {
+        hipLaunchKernelGGL(check_rt_kernel, dim3((n_matches + kRecThreads - 1) / kRecThreads, nh), dim3(kRecThreads),
+                           0, ctx->stream, d_pts, d_inl, n_matches, d_h, fx, fy, cx, cy, th2, d_good, d_p3, d_key);
+        ORB_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(rt_parallax_kernel, dim3(nh), dim3(kSelThreads), 0, ctx->stream, d_key, n_matches, d_ng,
+                       d_par);
     ORB_HIP(hipGetLastError());
     call.fetch(d_ng, ng.data(), 4 * (size_t)nh);
     call.fetch(d_par, par.data(), 4 * (size_t)nh);

@@ -22,7 +22,9 @@
 //     stays O(1e-15) after every rotation, and the sweep loop ran to its cap
 //     of 60 (measured: 779 us for the 400 models of one Initialize).
 // The relative test itself is the usual |gamma| <= 1e-15 sqrt(alpha beta),
-// evaluated squared (no sqrt on the chain).
+// evaluated squared (no sqrt on the chain); the column norms are carried
+// through the rotations, and the rotation parameters use the hardware
+// reciprocal estimates with Newton steps.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -55,47 +57,124 @@ __host__ __device__ constexpr int jacobi_col(int pos, int k, int M) {
     return pos == 0 ? 0 : (pos - 1 + k) % (M - 1) + 1;
 }
 
+// 1/x and 1/sqrt(x) from the hardware estimates (v_rcp_f64, v_rsq_f64) and
+// two Newton steps each: full double accuracy for the finite positive
+// arguments of a rotation, at a fraction of the IEEE div / sqrt sequences
+__device__ __forceinline__ double rcp_nr(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return fma(r, fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ double rsq_nr(double x) {
+    double r = __builtin_amdgcn_rsq(x);
+    r = fma(0.5 * r, fma(-x * r, r, 1.0), r);
+    return fma(0.5 * r, fma(-x * r, r, 1.0), r);
+}
+
+// the rotation of jacobi_rotation with t = tan(theta) too (for the norm
+// update).  t itself is computed in single precision (v_rcp_f32 /
+// v_sqrt_f32 on the float-rounded zeta): an angle off by ~1e-7 relative
+// leaves a residual cosine of ~1e-7 times the old one, which the next sweep
+// removes, while c = 1/sqrt(1 + t^2) (double, Newton-refined) and s = c t
+// keep every rotation orthogonal to double precision, so V stays
+// orthonormal and the converged singular vectors are as accurate as with an
+// exact angle.  |zeta| beyond float range gives t = 0 (an angle below 1e-19).
+__device__ __forceinline__ bool jacobi_rotation_fast(double alpha, double beta, double gamma, double negl, double& c,
+                                                     double& s, double& t) {
+    c = 1.0;
+    s = 0.0;
+    t = 0.0;
+    if (gamma == 0.0 || gamma * gamma <= kJacobiTol2 * alpha * beta || alpha <= negl || beta <= negl) return false;
+    const float zeta = (float)(beta - alpha) * __builtin_amdgcn_rcpf((float)(2.0 * gamma));
+    const float root = __builtin_amdgcn_sqrtf(fmaf(zeta, zeta, 1.0f));
+    const float tf = copysignf(__builtin_amdgcn_rcpf(fabsf(zeta) + root), zeta);
+    t = zeta == 0.0f ? 1.0 : (double)tf;
+    c = rsq_nr(fma(t, t, 1.0));
+    s = c * t;
+    return true;
+}
+
+// the rotation the sequential Jacobis (epnp.h) use: IEEE on the host, the
+// fast reciprocals on the device (HIP host/device overloading)
+__host__ inline bool jacobi_rot(double alpha, double beta, double gamma, double negl, double& c, double& s) {
+    return jacobi_rotation(alpha, beta, gamma, negl, c, s);
+}
+__device__ inline bool jacobi_rot(double alpha, double beta, double gamma, double negl, double& c, double& s) {
+    double t;
+    return jacobi_rotation_fast(alpha, beta, gamma, negl, c, s, t);
+}
+
+// returns the number of sweeps run.  The squared column norms are kept
+// current through the rotations (alpha' = alpha - t gamma, beta' = beta + t
+// gamma) and recomputed from the columns at the start of every sweep, so a
+// pair costs one group reduction (its dot product) instead of three.  The
+// circle method moves the COLUMNS, not the pairing: every round pairs
+// positions (i, M-1-i), then positions 1..M-1 rotate left by one (after M-1
+// rounds every column is back in place), so the round body has static
+// register indices and stays a loop (a fully unrolled sweep of 66 pairs
+// inflated register pressure until the kernel spilled).  An odd NC gets a
+// zero column, which every test skips.
 template <int NC, int G>
-__device__ __forceinline__ void hestenes_group(double (&a)[NC], double (&v)[NC], int max_sweeps = 60) {
+__device__ __forceinline__ int hestenes_group(double (&a_in)[NC], double (&v_in)[NC], int max_sweeps = 60) {
     constexpr int M = NC + (NC & 1);
     constexpr int P = M / 2;
+    double a[M], v[M], nrm[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        a[j] = j < NC ? a_in[j] : 0.0;
+        v[j] = j < NC ? v_in[j] : 0.0;
+    }
     double fro = 0.0;
 #pragma unroll
     for (int j = 0; j < NC; ++j) fro += a[j] * a[j];
     const double negl = kJacobiNegl * group_sum_dpp<G>(fro);
-    for (int sweep = 0; sweep < max_sweeps; ++sweep) {
+    int sweep = 0;
+    while (sweep < max_sweeps) {
+        ++sweep;
         bool rotated = false;
 #pragma unroll
+        for (int j = 0; j < M; ++j) nrm[j] = group_sum_dpp<G>(a[j] * a[j]);
+#pragma unroll 1
         for (int k = 0; k < M - 1; ++k) {
-            double al[P], be[P], ga[P], cs[P], sn[P];
+            double ga[P], cs[P], sn[P], tn[P];
+#pragma unroll
+            for (int i = 0; i < P; ++i) ga[i] = group_sum_dpp<G>(a[i] * a[M - 1 - i]);
 #pragma unroll
             for (int i = 0; i < P; ++i) {
-                const int p = jacobi_col(i, k, M), q = jacobi_col(M - 1 - i, k, M);
-                if (p >= NC || q >= NC) continue;
-                al[i] = group_sum_dpp<G>(a[p] * a[p]);
-                be[i] = group_sum_dpp<G>(a[q] * a[q]);
-                ga[i] = group_sum_dpp<G>(a[p] * a[q]);
+                rotated |= jacobi_rotation_fast(nrm[i], nrm[M - 1 - i], ga[i], negl, cs[i], sn[i], tn[i]);
+                nrm[i] = fma(-tn[i], ga[i], nrm[i]);
+                nrm[M - 1 - i] = fma(tn[i], ga[i], nrm[M - 1 - i]);
             }
 #pragma unroll
             for (int i = 0; i < P; ++i) {
-                const int p = jacobi_col(i, k, M), q = jacobi_col(M - 1 - i, k, M);
-                if (p >= NC || q >= NC) continue;
-                rotated |= jacobi_rotation(al[i], be[i], ga[i], negl, cs[i], sn[i]);
-            }
-#pragma unroll
-            for (int i = 0; i < P; ++i) {
-                const int p = jacobi_col(i, k, M), q = jacobi_col(M - 1 - i, k, M);
-                if (p >= NC || q >= NC) continue;
-                const double x = a[p], y = a[q];
-                a[p] = cs[i] * x - sn[i] * y;
+                const int q = M - 1 - i;
+                const double x = a[i], y = a[q];
+                a[i] = cs[i] * x - sn[i] * y;
                 a[q] = sn[i] * x + cs[i] * y;
-                const double vx = v[p], vy = v[q];
-                v[p] = cs[i] * vx - sn[i] * vy;
+                const double vx = v[i], vy = v[q];
+                v[i] = cs[i] * vx - sn[i] * vy;
                 v[q] = sn[i] * vx + cs[i] * vy;
             }
+            // positions 1..M-1 rotate left by one
+            const double a1 = a[1], v1 = v[1], n1 = nrm[1];
+#pragma unroll
+            for (int j = 1; j < M - 1; ++j) {
+                a[j] = a[j + 1];
+                v[j] = v[j + 1];
+                nrm[j] = nrm[j + 1];
+            }
+            a[M - 1] = a1;
+            v[M - 1] = v1;
+            nrm[M - 1] = n1;
         }
         if (!__any(rotated)) break;  // wave-uniform: converged groups rotate by the identity
     }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        a_in[j] = a[j];
+        v_in[j] = v[j];
+    }
+    return sweep;
 }
 
 }  // namespace orbgpu

@@ -464,19 +464,22 @@ hipError_t launch_pyramid_levels(const Geom& g, int batch, const int2* xtab, con
 // plus the source rows of the rows it needs at level l+1 (plan_pyramid_bands:
 // a few rows of halo per level, recomputed by the neighbouring band with the
 // same arithmetic, so the written rows are exactly the level kernel's).
-constexpr int kBandThreads = 256;
+constexpr int kBandThreads = 1024;  // 16 waves per CU: the per-level loads of one wave hide behind the others
 constexpr int kBandMaxLds = 96 * 1024;
+constexpr int kBandStage = 4;       // level-0 words per thread per staging round, all loads issued first
 
 __device__ __forceinline__ uint32_t resize_quad(const uint8_t* r0, const uint8_t* r1, int x0, int dw, int simd_end,
                                                 const int2* __restrict__ xt, uint32_t b0, uint32_t b1) {
+    int2 tx[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tx[k] = xt[min(x0 + k, dw - 1)];
     uint32_t out = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int x = x0 + k;
         if (x >= dw) break;
-        const int2 tx = xt[x];
-        const int sx0 = tx.x & 0xFFFF, sx1 = (int)((uint32_t)tx.x >> 16);
-        const uint32_t a0 = (uint32_t)tx.y & 0xFFFFu, a1 = (uint32_t)tx.y >> 16;
+        const int sx0 = tx[k].x & 0xFFFF, sx1 = (int)((uint32_t)tx[k].x >> 16);
+        const uint32_t a0 = (uint32_t)tx[k].y & 0xFFFFu, a1 = (uint32_t)tx[k].y >> 16;
         const uint32_t h0 = r0[sx0] * a0 + r0[sx1] * a1, h1 = r1[sx0] * a0 + r1[sx1] * a1;
         const uint32_t v = x < simd_end ? ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2u) >> 2
                                         : (h0 * b0 + h1 * b1 + (1u << 21)) >> 22;
@@ -499,21 +502,26 @@ __global__ __launch_bounds__(kBandThreads) void pyramid_band_kernel(const Geom g
         const uint8_t* src = img0 + (size_t)f * frame0;
         uint8_t* dst = s_rows + v.bd_lds_off;
         if ((((uintptr_t)src | row0) & 3) == 0) {
-            const int words = (v.w + 3) >> 2, n = (r.y - r.x) * words;
-            for (int i = tid; i < n; i += kBandThreads) {
-                const int y = i / words, c = i - y * words;
-                // the last word of a row may end past w: inside the row when the step is a multiple of 4
-                // and the row is not the image's last; the last row is read bytewise
-                const uint8_t* p = src + (size_t)(r.x + y) * row0 + 4 * c;
-                uint32_t w;
-                if (4 * c + 4 <= v.w) {
-                    w = *reinterpret_cast<const uint32_t*>(p);
-                } else {
-                    w = 0;
-                    for (int k = 0; 4 * c + k < v.w; ++k) w |= (uint32_t)p[k] << (8 * k);
+            // whole words inside the row; the row's last partial word bytewise
+            const int words = v.w >> 2, n = (r.y - r.x) * words;
+            for (int i0 = 0; i0 < n; i0 += kBandThreads * kBandStage) {
+                uint32_t w[kBandStage];
+#pragma unroll
+                for (int k = 0; k < kBandStage; ++k) {
+                    const int i = min(i0 + k * kBandThreads + tid, n - 1), y = i / words, c = i - y * words;
+                    w[k] = *reinterpret_cast<const uint32_t*>(src + (size_t)(r.x + y) * row0 + 4 * c);
                 }
-                *reinterpret_cast<uint32_t*>(dst + y * v.bd_pitch + 4 * c) = w;
+#pragma unroll
+                for (int k = 0; k < kBandStage; ++k) {
+                    const int i = i0 + k * kBandThreads + tid, y = i / words, c = i - y * words;
+                    if (i < n) *reinterpret_cast<uint32_t*>(dst + y * v.bd_pitch + 4 * c) = w[k];
+                }
             }
+            const int tail = v.w & 3;
+            if (tail)
+                for (int y = tid; y < r.y - r.x; y += kBandThreads)
+                    for (int k = 0; k < tail; ++k)
+                        dst[y * v.bd_pitch + 4 * words + k] = src[(size_t)(r.x + y) * row0 + 4 * words + k];
         } else {
             const int n = (r.y - r.x) * v.w;
             for (int i = tid; i < n; i += kBandThreads) {

@@ -42,7 +42,7 @@ names = ["start", "control pts", "pinv(CC)", "M^T M", "Jacobi 12x12", "canonical
          "svd_solve 6x5", "gauss-newton 3", "r_and_t 3 / end"]
 for row, title in ((0, "hypothesis (G=16, n=4)"), (1, "Refine (G=64)")):
     s = st[row]
-    print(f"== {title}: total {s[15] - s[0]} cycles")
+    print(f"== {title}: total {s[15] - s[0]} cycles, Jacobi sweeps {s[16]}")
     for k in range(1, 16):
         if s[k] and s[k - 1]:
             print(f"  {names[k]:18s} {s[k] - s[k - 1]:8d}")

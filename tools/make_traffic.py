@@ -17,7 +17,7 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent))
 from pmc_summary import load  # noqa: E402
 
-KERNEL = "pyramid"  # matched as a prefix (pyramid_tick_kernel<E, NP>)
+KERNEL = "pyramid_tick"  # matched as a prefix (pyramid_tick_kernel<E, NP>)
 
 
 def main():
