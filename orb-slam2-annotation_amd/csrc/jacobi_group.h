@@ -78,17 +78,25 @@ __device__ __forceinline__ double rsq_nr(double x) {
 // removes, while c = 1/sqrt(1 + t^2) (double, Newton-refined) and s = c t
 // keep every rotation orthogonal to double precision, so V stays
 // orthonormal and the converged singular vectors are as accurate as with an
-// exact angle.  |zeta| beyond float range gives t = 0 (an angle below 1e-19).
+// exact angle.  |zeta| >= 1e18 takes t = gamma / (beta - alpha) in double.
 __device__ __forceinline__ bool jacobi_rotation_fast(double alpha, double beta, double gamma, double negl, double& c,
                                                      double& s, double& t) {
     c = 1.0;
     s = 0.0;
     t = 0.0;
     if (gamma == 0.0 || gamma * gamma <= kJacobiTol2 * alpha * beta || alpha <= negl || beta <= negl) return false;
-    const float zeta = (float)(beta - alpha) * __builtin_amdgcn_rcpf((float)(2.0 * gamma));
-    const float root = __builtin_amdgcn_sqrtf(fmaf(zeta, zeta, 1.0f));
-    const float tf = copysignf(__builtin_amdgcn_rcpf(fabsf(zeta) + root), zeta);
-    t = zeta == 0.0f ? 1.0 : (double)tf;
+    const double dba = beta - alpha;
+    const float zeta = (float)dba * __builtin_amdgcn_rcpf((float)(2.0 * gamma));
+    if (fabsf(zeta) < 1e18f) {
+        const float root = __builtin_amdgcn_sqrtf(fmaf(zeta, zeta, 1.0f));
+        const float tf = copysignf(__builtin_amdgcn_rcpf(fabsf(zeta) + root), zeta);
+        t = zeta == 0.0f ? 1.0 : (double)tf;
+    } else {
+        // zeta^2 beyond float range (or 2 gamma below it): t = 1/(2 zeta) to
+        // double precision; a zero t here would leave the pair unrotated and
+        // the sweep loop running to its cap
+        t = dba == 0.0 ? 1.0 : gamma * rcp_nr(dba);
+    }
     c = rsq_nr(fma(t, t, 1.0));
     s = c * t;
     return true;
