@@ -226,19 +226,40 @@ __device__ inline int find_node(const int* nodes, int n, int key) {
     return -1;
 }
 
-// B-side staging (kStage): the candidate frame's descriptors, FeatureVector
-// feature list and valid flags, and the match state, are copied to LDS with
-// coalesced loads first, so the node walks' inner loop (the reference's
-// sequential candidate scan) costs LDS round trips instead of dependent HBM
-// ones (the lane-per-node walk is latency bound: round 2 measured 136 us for
-// one 1000-feature pair, most of it in chained global loads).  Used when
-// `stride` features fit the budget; larger frames take the global form.
+// Staging (kStage): kStage >= 1 copies the candidate frame's descriptors,
+// FeatureVector feature list and valid flags, and the match state, to LDS
+// with coalesced loads first; kStage == 2 also the query frame's.  The node
+// walks then cost LDS round trips instead of dependent HBM ones (the walk is
+// latency bound: round 2 measured 136 us for one 1000-feature pair, most of
+// it in chained global loads).  The level is the largest whose bytes for
+// `stride` features fit the budget.
 constexpr int kBowStageMaxLds = 96 * 1024;
-__host__ __device__ inline size_t bow_stage_bytes(int stride) {
-    return (size_t)stride * (32 + 4 + 1 + 4) + 64;
+__host__ __device__ inline size_t bow_stage_bytes(int stride, int level) {
+    return level == 0 ? 0
+                      : (size_t)stride * (32 + 4 + 1 + 4 + 4) + (level == 2 ? (size_t)stride * (32 + 4 + 1) : 0) + 128;
 }
 
-template <bool kStage>
+// block-wide copy of n elements with kBatch loads per thread issued before
+// any store (a plain copy loop waits for each load: one memory latency per
+// iteration)
+template <class T, int kBatch = 8>
+__device__ __forceinline__ void stage_copy(T* __restrict__ dst, const T* __restrict__ src, int n) {
+    for (int base = threadIdx.x; base < n; base += kBatch * blockDim.x) {
+        T v[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const int i = base + k * (int)blockDim.x;
+            v[k] = src[i < n ? i : n - 1];
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const int i = base + k * (int)blockDim.x;
+            if (i < n) dst[i] = v[k];
+        }
+    }
+}
+
+template <int kStage>
 __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbgpu_bow_frame* __restrict__ A_,
                                                             const orbgpu_bow_frame* __restrict__ B_, float nnratio,
                                                             int check_ori, int stride, int* __restrict__ match_g,
@@ -248,6 +269,7 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
     __shared__ int s_hist[kHL];
     __shared__ int s_ind[3];
     __shared__ int s_cnt;
+    __shared__ int s_npairs;
     extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
     const orbgpu_bow_frame A = A_[blockIdx.x], B = B_[blockIdx.x];
     const int nout = mode == ORBGPU_BOW_KF_F ? B.n : A.n;
@@ -256,94 +278,139 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
         if (threadIdx.x == 0) nmatches[blockIdx.x] = -1;
         return;
     }
-    // LDS carve (kStage): descB[stride] (32 B), fvfB[stride], match[stride], validB[stride]
+    // LDS carve: descB[stride] (32 B) | descA[stride] (level 2) | fvfB | fvfA (2) | match | common-node pairs |
+    // validB | validA (2)
     ulonglong4* s_descB = reinterpret_cast<ulonglong4*>(s_dyn);
-    int* s_fvfB = reinterpret_cast<int*>(s_dyn + (size_t)stride * 32);
-    int* s_match = s_fvfB + stride;
-    unsigned char* s_validB = reinterpret_cast<unsigned char*>(s_match + stride);
+    ulonglong4* s_descA = s_descB + (kStage == 2 ? stride : 0);
+    int* s_fvfB = reinterpret_cast<int*>(s_descA + (kStage == 2 ? stride : 0));
+    int* s_fvfA = s_fvfB + stride;
+    int* s_match = s_fvfA + (kStage == 2 ? stride : 0);
+    int* s_pairs = s_match + stride;
+    unsigned char* s_validB = reinterpret_cast<unsigned char*>(s_pairs + stride);
+    unsigned char* s_validA = s_validB + stride;
     int* match = kStage ? s_match : match_out;
     for (int i = threadIdx.x; i < nout; i += blockDim.x) {
         match[i] = -1;
         s_bin[i] = -1;
     }
-    if constexpr (kStage) {
-        const uint4* gd = reinterpret_cast<const uint4*>(B.desc);
-        uint4* sd = reinterpret_cast<uint4*>(s_descB);
-        for (int i = threadIdx.x; i < 2 * B.n; i += blockDim.x) sd[i] = gd[i];
-        for (int i = threadIdx.x; i < B.n; i += blockDim.x) {
-            s_fvfB[i] = B.fv_features[i];
-            s_validB[i] = B.valid[i];
-        }
+    if constexpr (kStage >= 1) {
+        stage_copy(reinterpret_cast<uint4*>(s_descB), reinterpret_cast<const uint4*>(B.desc), 2 * B.n);
+        stage_copy(s_fvfB, B.fv_features, B.n);
+        stage_copy(s_validB, B.valid, B.n);
+    }
+    if constexpr (kStage == 2) {
+        stage_copy(reinterpret_cast<uint4*>(s_descA), reinterpret_cast<const uint4*>(A.desc), 2 * A.n);
+        stage_copy(s_fvfA, A.fv_features, A.n);
+        stage_copy(s_validA, A.valid, A.n);
     }
     for (int i = threadIdx.x; i < kMaxStride / 32; i += blockDim.x) s_used[i] = 0;
     if (threadIdx.x < kHL) s_hist[threadIdx.x] = 0;
-    if (threadIdx.x == 0) s_cnt = 0;
+    if (threadIdx.x == 0) {
+        s_cnt = 0;
+        s_npairs = 0;
+    }
     __syncthreads();
+    if constexpr (kStage >= 1) {
+        // the common direct-index nodes, found by every thread at once (one
+        // binary search each) instead of by each row before its node
+        for (int a = threadIdx.x; a < A.fv_n; a += blockDim.x) {
+            const int b = find_node(B.fv_nodes, B.fv_n, A.fv_nodes[a]);
+            if (b >= 0) s_pairs[atomicAdd(&s_npairs, 1)] = a | (b << 16);
+        }
+        __syncthreads();
+    }
+    auto fvfA = [&](int k) { return kStage == 2 ? s_fvfA[k] : A.fv_features[k]; };
+    auto validA = [&](int i) { return kStage == 2 ? s_validA[i] != 0 : A.valid[i] != 0; };
+    auto descA = [&](int i) {
+        return kStage == 2 ? s_descA[i] : *reinterpret_cast<const ulonglong4*>(A.desc + 32 * (size_t)i);
+    };
     auto fvfB = [&](int k) { return kStage ? s_fvfB[k] : B.fv_features[k]; };
     auto descB = [&](int i) { return kStage ? s_descB[i] : *reinterpret_cast<const ulonglong4*>(B.desc + 32 * (size_t)i); };
     auto validB = [&](int i) { return kStage ? s_validB[i] != 0 : B.valid[i] != 0; };
+    auto sync_match = [&] {  // lane 0's match / vbMatched2 update visible to its row before the next A feature
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
     const float factor = (float)kHL / 360.0f;
-    for (int a = threadIdx.x; a < A.fv_n; a += blockDim.x) {
-        const int b = find_node(B.fv_nodes, B.fv_n, A.fv_nodes[a]);
-        if (b < 0) continue;
+    // One common direct-index node per 8-lane row (32 rows per block).  The
+    // node's A features are taken in the reference's order (the match state
+    // they leave feeds the next one); for each, the row's lanes scan the
+    // node's B features (lane r: positions r, r + 8, ...) and the row
+    // reduces (dist << 16 | position) -- the reference keeps the FIRST
+    // minimum in node order -- and the second smallest distance of the
+    // multiset (bestDist2: an equal second minimum counts).  A lane per node
+    // (round 2) ran a whole skewed node serially.
+    constexpr int kRow = 8;
+    const int r16 = threadIdx.x & (kRow - 1), row = threadIdx.x / kRow, nrows = blockDim.x / kRow;
+    const int nwork = kStage >= 1 ? s_npairs : A.fv_n;  // nodes are independent: any order
+    for (int w = row; w < nwork; w += nrows) {
+        int a, b;
+        if constexpr (kStage >= 1) {
+            a = s_pairs[w] & 0xFFFF;
+            b = s_pairs[w] >> 16;
+        } else {
+            a = w;
+            b = find_node(B.fv_nodes, B.fv_n, A.fv_nodes[a]);
+            if (b < 0) continue;
+        }
         const int a0 = A.fv_offsets[a], a1 = A.fv_offsets[a + 1];
-        const int b0 = B.fv_offsets[b], b1 = B.fv_offsets[b + 1];
+        const int b0 = B.fv_offsets[b], nb = B.fv_offsets[b + 1] - b0;
         for (int ia_ = a0; ia_ < a1; ++ia_) {
-            const int ia = A.fv_features[ia_];
-            if (!A.valid[ia]) continue;
-            const ulonglong4 qa = *reinterpret_cast<const ulonglong4*>(A.desc + 32 * (size_t)ia);
-            int best1 = 256, best2 = 256, bidx = -1;
-            // the node's B features four at a time: their indices, skip flags and
-            // descriptors are loaded together (one memory round trip per four
-            // instead of a dependent chain per feature), then compared in the
-            // reference's order.  The skip state (match[] / vbMatched2) only
-            // changes after this loop, and only in this lane (nodes partition B).
-            for (int base = b0; base < b1; base += 4) {
-                int ibs[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) ibs[u] = fvfB(min(base + u, b1 - 1));
-                bool skip[4];
-                ulonglong4 qb[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int ib = ibs[u];
-                    skip[u] = mode == ORBGPU_BOW_KF_F ? match[ib] >= 0
-                                                      : (((s_used[ib >> 5] >> (ib & 31)) & 1u) || !validB(ib));
-                    qb[u] = descB(ib);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (base + u >= b1 || skip[u]) continue;
-                    const int dist = __popcll(qa.x ^ qb[u].x) + __popcll(qa.y ^ qb[u].y) +
-                                     __popcll(qa.z ^ qb[u].z) + __popcll(qa.w ^ qb[u].w);
-                    if (dist < best1) {
-                        best2 = best1;
-                        best1 = dist;
-                        bidx = ibs[u];
-                    } else if (dist < best2) {
-                        best2 = dist;
-                    }
+            const int ia = fvfA(ia_);
+            if (!validA(ia)) continue;
+            const ulonglong4 qa = descA(ia);
+            uint32_t k1 = 0xFFFFFFFFu;  // (dist << 16 | position) of the lane's first minimum
+            uint32_t d2 = 0xFFFFu;      // the lane's second smallest distance
+            for (int j = r16; j < nb; j += kRow) {
+                const int ib = fvfB(b0 + j);
+                const bool skip = mode == ORBGPU_BOW_KF_F ? match[ib] >= 0
+                                                          : (((s_used[ib >> 5] >> (ib & 31)) & 1u) || !validB(ib));
+                if (skip) continue;
+                const ulonglong4 qb = descB(ib);
+                const uint32_t dist = __popcll(qa.x ^ qb.x) + __popcll(qa.y ^ qb.y) + __popcll(qa.z ^ qb.z) +
+                                      __popcll(qa.w ^ qb.w);
+                const uint32_t key = (dist << 16) | (uint32_t)j;
+                if (key < k1) {
+                    d2 = min(d2, k1 >> 16);
+                    k1 = key;
+                } else {
+                    d2 = min(d2, dist);
                 }
             }
+            // row reduction: xor 1, 2, 4 within the row's lanes
+#pragma unroll
+            for (int o = 1; o < kRow; o <<= 1) {
+                const uint32_t ok1 = (uint32_t)__shfl_xor((int)k1, o, kRow);
+                const uint32_t od2 = (uint32_t)__shfl_xor((int)d2, o, kRow);
+                d2 = min(min(d2, od2), max(k1 >> 16, ok1 >> 16));
+                k1 = min(k1, ok1);
+            }
+            const int best1 = k1 == 0xFFFFFFFFu ? 256 : (int)(k1 >> 16);
+            const int best2 = d2 >= 256u ? 256 : (int)d2;
             const bool pass = mode == ORBGPU_BOW_KF_F ? best1 <= kThLow : best1 < kThLow;
-            if (!pass || !((float)best1 < nnratio * (float)best2)) continue;
-            int out;
-            if (mode == ORBGPU_BOW_KF_F) {
-                match[bidx] = ia;
-                out = bidx;
-            } else {
-                match[ia] = bidx;
-                atomicOr(&s_used[bidx >> 5], 1u << (bidx & 31));
-                out = ia;
+            if (!pass || !((float)best1 < nnratio * (float)best2)) continue;  // row-uniform
+            const int bidx = fvfB(b0 + (int)(k1 & 0xFFFFu));
+            if (r16 == 0) {
+                int out;
+                if (mode == ORBGPU_BOW_KF_F) {
+                    match[bidx] = ia;
+                    out = bidx;
+                } else {
+                    match[ia] = bidx;
+                    atomicOr(&s_used[bidx >> 5], 1u << (bidx & 31));
+                    out = ia;
+                }
+                if (check_ori) {
+                    float rot = A.angle[ia] - B.angle[bidx];
+                    if (rot < 0.0f) rot += 360.0f;
+                    int bin = (int)roundf(rot * factor);
+                    if (bin == kHL) bin = 0;
+                    s_bin[out] = (signed char)bin;
+                    atomicAdd(&s_hist[bin], 1);
+                }
             }
-            if (check_ori) {
-                float rot = A.angle[ia] - B.angle[bidx];
-                if (rot < 0.0f) rot += 360.0f;
-                int bin = (int)roundf(rot * factor);
-                if (bin == kHL) bin = 0;
-                s_bin[out] = (signed char)bin;
-                atomicAdd(&s_hist[bin], 1);
-            }
+            sync_match();
         }
     }
     __syncthreads();
@@ -600,17 +667,24 @@ hipError_t launch_search_by_bow(int mode, int batch, const orbgpu_bow_frame* a, 
                                 float nnratio, int check_ori, int stride, int* match, int* nmatches,
                                 hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
-    const size_t lds = bow_stage_bytes(stride);
-    if (lds <= (size_t)kBowStageMaxLds) {
-        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&search_by_bow_kernel<true>),
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, kBowStageMaxLds);
-        if (attr != hipSuccess) return attr;
-        hipLaunchKernelGGL(search_by_bow_kernel<true>, dim3(batch), dim3(256), lds, stream, mode, a, b, nnratio,
+    static const hipError_t attr = [] {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&search_by_bow_kernel<1>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kBowStageMaxLds);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void*>(&search_by_bow_kernel<2>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kBowStageMaxLds);
+        return e;
+    }();
+    if (attr != hipSuccess) return attr;
+    if (bow_stage_bytes(stride, 2) <= (size_t)kBowStageMaxLds)
+        hipLaunchKernelGGL(search_by_bow_kernel<2>, dim3(batch), dim3(256), bow_stage_bytes(stride, 2), stream, mode,
+                           a, b, nnratio, check_ori, stride, match, nmatches);
+    else if (bow_stage_bytes(stride, 1) <= (size_t)kBowStageMaxLds)
+        hipLaunchKernelGGL(search_by_bow_kernel<1>, dim3(batch), dim3(256), bow_stage_bytes(stride, 1), stream, mode,
+                           a, b, nnratio, check_ori, stride, match, nmatches);
+    else
+        hipLaunchKernelGGL(search_by_bow_kernel<0>, dim3(batch), dim3(256), 0, stream, mode, a, b, nnratio,
                            check_ori, stride, match, nmatches);
-    } else {
-        hipLaunchKernelGGL(search_by_bow_kernel<false>, dim3(batch), dim3(256), 0, stream, mode, a, b, nnratio,
-                           check_ori, stride, match, nmatches);
-    }
     return hipGetLastError();
 }
 

@@ -54,6 +54,13 @@ __device__ __forceinline__ double gsum(double x) {
     return group_sum_dpp<G>(x);
 }
 
+// maximum over the lane's 16-lane row
+__device__ __forceinline__ double gmax16(double x) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) x = fmax(x, __shfl_xor(x, o, 16));
+    return x;
+}
+
 // LDS writes of the group visible to its other lanes (one wave: in-order LDS,
 // so a counter wait and a wave barrier suffice; no block barrier, so a single
 // wave of a larger block can run this)
@@ -196,6 +203,103 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
         a[0] = 1.0f - a[1] - a[2] - a[3];
     };
     EPNP_T(2);
+    // Minimal sets (n = 4, G = 16): M is 8 x 12, so null(M) -- the span of
+    // the four smallest eigenvectors of M^T M -- is at least 4-dimensional,
+    // and the canonical basis of the spec (Gram-Schmidt of V (W^T V)^-1, V any
+    // basis, canonicalize_null_space) is the Gram-Schmidt of the unique N
+    // with M N = 0 and W^T N = I.  So N comes from one 12 x 12 solve, [M; W^T]
+    // N = [0; I], by Gauss-Jordan with the rows on the group's lanes (pivot
+    // = the row with the largest |entry| in the column, found by a row
+    // reduction; the pivot row broadcast by shuffles), instead of the 12 x 12
+    // eigen-decomposition: the same vectors up to rounding, for ~40x fewer
+    // instructions.  A group whose system is (near-)singular (M of rank < 8:
+    // degenerate points) makes the wave take the eigen path below.
+    bool need_eig = true;
+    if constexpr (G == 16) {
+        if (n == 4) {
+            double row[16];  // 12 coefficients | 4 right-hand sides
+#pragma unroll
+            for (int j = 0; j < 16; ++j) row[j] = 0.0;
+            if (r < 8) {  // fill_M (:483-497): rows 2i, 2i+1 of correspondence i
+                double pw[3], u, v, a[4];
+                src.get(r >> 1, pw, u, v);
+                alphas(pw, a);
+                const bool second = r & 1;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    row[3 * j] = second ? 0.0 : a[j] * cam.fu;
+                    row[3 * j + 1] = second ? a[j] * cam.fv : 0.0;
+                    row[3 * j + 2] = second ? a[j] * (cam.vc - v) : a[j] * (cam.uc - u);
+                }
+            } else if (r < 12) {  // W^T row c, right-hand side e_c
+#pragma unroll
+                for (int j = 0; j < 12; ++j) row[j] = null_w(j, r - 8);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) row[12 + c] = (r - 8) == c ? 1.0 : 0.0;
+            }
+            double amax = 0.0;
+#pragma unroll
+            for (int j = 0; j < 12; ++j) amax = fmax(amax, fabs(row[j]));
+            const double scale = gmax16(amax);
+            const int g0 = (int)(threadIdx.x & 63) & ~15;
+            bool used = r >= 12, degenerate = false;
+            int my_col = -1;
+#pragma unroll
+            for (int k = 0; k < 12; ++k) {
+                // pivot: the unused row with the largest |row[k]| (ties: lowest lane)
+                const double av = used ? -1.0 : fabs(row[k]);
+                double best = av;
+                int bl = r;
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    const double ob = __shfl_xor(best, o, 16);
+                    const int ol = __shfl_xor(bl, o, 16);
+                    if (ob > best || (ob == best && ol < bl)) {
+                        best = ob;
+                        bl = ol;
+                    }
+                }
+                degenerate |= !(best > 1e-12 * scale);
+                double prow[16];
+#pragma unroll
+                for (int j = k; j < 16; ++j) prow[j] = __shfl(row[j], g0 + bl, 64);
+                if (r == bl) {
+                    used = true;
+                    my_col = k;
+                } else if (r < 12) {
+                    const double f = row[k] / prow[k];
+#pragma unroll
+                    for (int j = k; j < 16; ++j) row[j] = fma(-f, prow[j], row[j]);
+                }
+            }
+            // the pivot row of column k holds x_k: N[k][c] = rhs[c] / diag
+            double nv[4];
+            double dk = 1.0;
+#pragma unroll
+            for (int k = 0; k < 12; ++k)
+                if (my_col == k) dk = row[k];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) nv[c] = my_col >= 0 ? row[12 + c] / dk : 0.0;
+            // modified Gram-Schmidt over the columns, in order (row order is a permutation: sums are order-free
+            // up to rounding)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+#pragma unroll
+                for (int j = 0; j < c; ++j) {
+                    const double d = gsum<16>(nv[j] * nv[c]);
+                    nv[c] = fma(-d, nv[j], nv[c]);
+                }
+                const double nrm = sqrt(gsum<16>(nv[c] * nv[c]));
+                nv[c] = nv[c] / nrm;
+            }
+            if (my_col >= 0)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) s_ut4[12 * c + my_col] = nv[c];
+            need_eig = __any(degenerate);
+            EPNP_GROUP_SYNC();
+        }
+    }
+    if (need_eig) {
     // M^T M (fill_M :483-497, cvMulTransposed): per (k <= l) sums of a_k a_l times
     // 1, (uc - u), (vc - v), (uc - u)^2 + (vc - v)^2
     {
@@ -277,6 +381,7 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
         if (k > 0 && r == 0) canonicalize_null_space4(s_ut4, k < 4 ? k : 4, s_mtm);  // M^T M is consumed
     }
     EPNP_GROUP_SYNC();
+    }  // need_eig
     EPNP_T(5);
     // compute_L_6x10 (:863-898), compute_rho (:900-908)
     double rho[6];

@@ -195,15 +195,19 @@ __device__ int nms_emit(const CellTiles& T, int nb, int ox, int t, int lane, int
             off = T.lb[j];
             const uint8_t* q = T.sc + off;
             s = q[0];
-            keep = true;
+            // all eight neighbours loaded and tested without short-circuit
+            // branches (one basic block: the loads issue together)
+            int v[8];
+            int k = 0;
 #pragma unroll
             for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
-                for (int dx = -1; dx <= 1; ++dx) {
-                    if (dx == 0 && dy == 0) continue;
-                    const int v = q[dy * P + dx];
-                    keep = keep && (s - 1 > (v >= t1 ? v - 1 : 0));
-                }
+                for (int dx = -1; dx <= 1; ++dx)
+                    if (dx != 0 || dy != 0) v[k++] = q[dy * P + dx];
+            int vmax = 0;
+#pragma unroll
+            for (int m = 0; m < 8; ++m) vmax = max(vmax, v[m] >= t1 ? v[m] - 1 : 0);
+            keep = s - 1 > vmax;
         }
         const unsigned long long m = __ballot(keep);
         if (keep) {

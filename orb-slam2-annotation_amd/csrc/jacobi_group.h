@@ -81,25 +81,24 @@ __device__ __forceinline__ double rsq_nr(double x) {
 // exact angle.  |zeta| >= 1e18 takes t = gamma / (beta - alpha) in double.
 __device__ __forceinline__ bool jacobi_rotation_fast(double alpha, double beta, double gamma, double negl, double& c,
                                                      double& s, double& t) {
-    c = 1.0;
-    s = 0.0;
-    t = 0.0;
-    if (gamma == 0.0 || gamma * gamma <= kJacobiTol2 * alpha * beta || alpha <= negl || beta <= negl) return false;
+    // branch-free (every value computed, the identity selected at the end):
+    // a round's pairs are then one basic block and their chains interleave
+    const bool skip = gamma == 0.0 || gamma * gamma <= kJacobiTol2 * alpha * beta || alpha <= negl || beta <= negl;
     const double dba = beta - alpha;
     const float zeta = (float)dba * __builtin_amdgcn_rcpf((float)(2.0 * gamma));
-    if (fabsf(zeta) < 1e18f) {
-        const float root = __builtin_amdgcn_sqrtf(fmaf(zeta, zeta, 1.0f));
-        const float tf = copysignf(__builtin_amdgcn_rcpf(fabsf(zeta) + root), zeta);
-        t = zeta == 0.0f ? 1.0 : (double)tf;
-    } else {
-        // zeta^2 beyond float range (or 2 gamma below it): t = 1/(2 zeta) to
-        // double precision; a zero t here would leave the pair unrotated and
-        // the sweep loop running to its cap
-        t = dba == 0.0 ? 1.0 : gamma * rcp_nr(dba);
-    }
-    c = rsq_nr(fma(t, t, 1.0));
-    s = c * t;
-    return true;
+    const float root = __builtin_amdgcn_sqrtf(fmaf(zeta, zeta, 1.0f));
+    const float tf = copysignf(__builtin_amdgcn_rcpf(fabsf(zeta) + root), zeta);
+    const double t_small = zeta == 0.0f ? 1.0 : (double)tf;
+    // zeta^2 beyond float range (or 2 gamma below it): t = 1/(2 zeta) in
+    // double; a zero t there would leave the pair unrotated and the sweep
+    // loop running to its cap
+    const double t_big = dba == 0.0 ? 1.0 : gamma * rcp_nr(dba);
+    const double tt = fabsf(zeta) < 1e18f ? t_small : t_big;
+    const double cc = rsq_nr(fma(tt, tt, 1.0));
+    t = skip ? 0.0 : tt;
+    c = skip ? 1.0 : cc;
+    s = skip ? 0.0 : cc * tt;
+    return !skip;
 }
 
 // the rotation the sequential Jacobis (epnp.h) use: IEEE on the host, the
@@ -154,14 +153,14 @@ __device__ __forceinline__ int hestenes_group(double (&a_in)[NC], double (&v_in)
                 nrm[M - 1 - i] = fma(tn[i], ga[i], nrm[M - 1 - i]);
             }
 #pragma unroll
-            for (int i = 0; i < P; ++i) {
+            for (int i = 0; i < P; ++i) {  // explicit FMAs: two instructions per updated value
                 const int q = M - 1 - i;
                 const double x = a[i], y = a[q];
-                a[i] = cs[i] * x - sn[i] * y;
-                a[q] = sn[i] * x + cs[i] * y;
+                a[i] = fma(cs[i], x, -sn[i] * y);
+                a[q] = fma(sn[i], x, cs[i] * y);
                 const double vx = v[i], vy = v[q];
-                v[i] = cs[i] * vx - sn[i] * vy;
-                v[q] = sn[i] * vx + cs[i] * vy;
+                v[i] = fma(cs[i], vx, -sn[i] * vy);
+                v[q] = fma(sn[i], vx, cs[i] * vy);
             }
             // positions 1..M-1 rotate left by one
             const double a1 = a[1], v1 = v[1], n1 = nrm[1];
