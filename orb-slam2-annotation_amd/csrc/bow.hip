@@ -233,10 +233,13 @@ __device__ inline int find_node(const int* nodes, int n, int key) {
 // latency bound: round 2 measured 136 us for one 1000-feature pair, most of
 // it in chained global loads).  The level is the largest whose bytes for
 // `stride` features fit the budget.
-constexpr int kBowStageMaxLds = 96 * 1024;
+constexpr int kBowStageMaxLds = 128 * 1024;
 __host__ __device__ inline size_t bow_stage_bytes(int stride, int level) {
+    // per feature: descB 32, fvfB 4, match 4, common-node record 16, B node id 4, validB 1 (+ descA 32,
+    // fvfA 4, validA 1 at level 2)
     return level == 0 ? 0
-                      : (size_t)stride * (32 + 4 + 1 + 4 + 4) + (level == 2 ? (size_t)stride * (32 + 4 + 1) : 0) + 128;
+                      : (size_t)stride * (32 + 4 + 4 + 16 + 4 + 1) + (level == 2 ? (size_t)stride * (32 + 4 + 1) : 0) +
+                            128;
 }
 
 // block-wide copy of n elements with kBatch loads per thread issued before
@@ -278,15 +281,16 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
         if (threadIdx.x == 0) nmatches[blockIdx.x] = -1;
         return;
     }
-    // LDS carve: descB[stride] (32 B) | descA[stride] (level 2) | fvfB | fvfA (2) | match | common-node pairs |
-    // validB | validA (2)
+    // LDS carve: descB[stride] (32 B) | descA[stride] (level 2) | common-node records (16 B) | fvfB | fvfA (2) |
+    // match | B node ids | validB | validA (2)
     ulonglong4* s_descB = reinterpret_cast<ulonglong4*>(s_dyn);
     ulonglong4* s_descA = s_descB + (kStage == 2 ? stride : 0);
-    int* s_fvfB = reinterpret_cast<int*>(s_descA + (kStage == 2 ? stride : 0));
+    int4* s_pairs = reinterpret_cast<int4*>(s_descA + (kStage == 2 ? stride : 0));  // (a0, na, b0, nb)
+    int* s_fvfB = reinterpret_cast<int*>(s_pairs + stride);
     int* s_fvfA = s_fvfB + stride;
     int* s_match = s_fvfA + (kStage == 2 ? stride : 0);
-    int* s_pairs = s_match + stride;
-    unsigned char* s_validB = reinterpret_cast<unsigned char*>(s_pairs + stride);
+    int* s_nodesB = s_match + stride;
+    unsigned char* s_validB = reinterpret_cast<unsigned char*>(s_nodesB + stride);
     unsigned char* s_validA = s_validB + stride;
     int* match = kStage ? s_match : match_out;
     for (int i = threadIdx.x; i < nout; i += blockDim.x) {
@@ -294,14 +298,53 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
         s_bin[i] = -1;
     }
     if constexpr (kStage >= 1) {
-        stage_copy(reinterpret_cast<uint4*>(s_descB), reinterpret_cast<const uint4*>(B.desc), 2 * B.n);
-        stage_copy(s_fvfB, B.fv_features, B.n);
-        stage_copy(s_validB, B.valid, B.n);
-    }
-    if constexpr (kStage == 2) {
-        stage_copy(reinterpret_cast<uint4*>(s_descA), reinterpret_cast<const uint4*>(A.desc), 2 * A.n);
-        stage_copy(s_fvfA, A.fv_features, A.n);
-        stage_copy(s_validA, A.valid, A.n);
+        // every staged array's loads of a round issued before its stores (one memory latency per round)
+        const uint4* gdB = reinterpret_cast<const uint4*>(B.desc);
+        const uint4* gdA = reinterpret_cast<const uint4*>(A.desc);
+        uint4* sdB = reinterpret_cast<uint4*>(s_descB);
+        uint4* sdA = reinterpret_cast<uint4*>(s_descA);
+        const int nA = kStage == 2 ? A.n : 0;
+        const int nmax = max(max(B.n, nA), B.fv_n);
+        for (int base = threadIdx.x; base < nmax; base += 2 * blockDim.x) {
+            uint4 db[4], da[4];
+            int fb[2], fa[2], nd[2];
+            unsigned char vb[2], va[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {  // clamped indices; an empty array is never read
+                const int i = base + k * (int)blockDim.x;
+                const int ib = min(i, B.n - 1), ia = min(i, nA - 1);
+                if (B.n > 0) {
+                    db[2 * k] = gdB[2 * ib];
+                    db[2 * k + 1] = gdB[2 * ib + 1];
+                    fb[k] = B.fv_features[ib];
+                    vb[k] = B.valid[ib];
+                }
+                if (B.fv_n > 0) nd[k] = B.fv_nodes[min(i, B.fv_n - 1)];
+                if (kStage == 2 && nA > 0) {
+                    da[2 * k] = gdA[2 * ia];
+                    da[2 * k + 1] = gdA[2 * ia + 1];
+                    fa[k] = A.fv_features[ia];
+                    va[k] = A.valid[ia];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int i = base + k * (int)blockDim.x;
+                if (i < B.n) {
+                    sdB[2 * i] = db[2 * k];
+                    sdB[2 * i + 1] = db[2 * k + 1];
+                    s_fvfB[i] = fb[k];
+                    s_validB[i] = vb[k];
+                }
+                if (i < B.fv_n) s_nodesB[i] = nd[k];
+                if (kStage == 2 && i < nA) {
+                    sdA[2 * i] = da[2 * k];
+                    sdA[2 * i + 1] = da[2 * k + 1];
+                    s_fvfA[i] = fa[k];
+                    s_validA[i] = va[k];
+                }
+            }
+        }
     }
     for (int i = threadIdx.x; i < kMaxStride / 32; i += blockDim.x) s_used[i] = 0;
     if (threadIdx.x < kHL) s_hist[threadIdx.x] = 0;
@@ -311,11 +354,15 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
     }
     __syncthreads();
     if constexpr (kStage >= 1) {
-        // the common direct-index nodes, found by every thread at once (one
-        // binary search each) instead of by each row before its node
+        // the common direct-index nodes and their feature ranges, found by
+        // every thread at once (one binary search each, over B's node ids in
+        // LDS) instead of by each row before its node
         for (int a = threadIdx.x; a < A.fv_n; a += blockDim.x) {
-            const int b = find_node(B.fv_nodes, B.fv_n, A.fv_nodes[a]);
-            if (b >= 0) s_pairs[atomicAdd(&s_npairs, 1)] = a | (b << 16);
+            const int b = find_node(s_nodesB, B.fv_n, A.fv_nodes[a]);
+            if (b >= 0) {
+                const int a0 = A.fv_offsets[a], b0 = B.fv_offsets[b];
+                s_pairs[atomicAdd(&s_npairs, 1)] = make_int4(a0, A.fv_offsets[a + 1] - a0, b0, B.fv_offsets[b + 1] - b0);
+            }
         }
         __syncthreads();
     }
@@ -342,20 +389,102 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
     // multiset (bestDist2: an equal second minimum counts).  A lane per node
     // (round 2) ran a whole skewed node serially.
     constexpr int kRow = 8;
+    constexpr int kRegC = 4;  // candidates per lane held in registers (nodes of up to 32 B features)
     const int r16 = threadIdx.x & (kRow - 1), row = threadIdx.x / kRow, nrows = blockDim.x / kRow;
     const int nwork = kStage >= 1 ? s_npairs : A.fv_n;  // nodes are independent: any order
     for (int w = row; w < nwork; w += nrows) {
-        int a, b;
+        int a0, a1, b0, nb;
         if constexpr (kStage >= 1) {
-            a = s_pairs[w] & 0xFFFF;
-            b = s_pairs[w] >> 16;
+            const int4 pr = s_pairs[w];
+            a0 = pr.x;
+            a1 = pr.x + pr.y;
+            b0 = pr.z;
+            nb = pr.w;
         } else {
-            a = w;
-            b = find_node(B.fv_nodes, B.fv_n, A.fv_nodes[a]);
+            const int b = find_node(B.fv_nodes, B.fv_n, A.fv_nodes[w]);
             if (b < 0) continue;
+            a0 = A.fv_offsets[w];
+            a1 = A.fv_offsets[w + 1];
+            b0 = B.fv_offsets[b];
+            nb = B.fv_offsets[b + 1] - b0;
         }
-        const int a0 = A.fv_offsets[a], a1 = A.fv_offsets[a + 1];
-        const int b0 = B.fv_offsets[b], nb = B.fv_offsets[b + 1] - b0;
+        if (nb <= kRow * kRegC) {
+            // The node's B features are the same for all of its A features:
+            // the row loads them once into registers (lane r: positions r, r +
+            // 8, ...) with their skip flags, and keeps the flags current
+            // itself (nodes partition B, so only this row changes them: a
+            // match clears the matched candidate in its owner lane).  An A
+            // feature then costs its own loads, the distances and the row
+            // reduction, with no LDS round trip per candidate.
+            ulonglong4 cd[kRegC];
+            bool ok[kRegC];
+#pragma unroll
+            for (int c = 0; c < kRegC; ++c) {
+                const int j = r16 + kRow * c;
+                ok[c] = false;
+                if (j < nb) {
+                    const int ib = fvfB(b0 + j);
+                    cd[c] = descB(ib);
+                    ok[c] = mode == ORBGPU_BOW_KF_F ? match[ib] < 0
+                                                    : !(((s_used[ib >> 5] >> (ib & 31)) & 1u) || !validB(ib));
+                }
+            }
+            for (int ia_ = a0; ia_ < a1; ++ia_) {
+                const int ia = fvfA(ia_);
+                if (!validA(ia)) continue;
+                const ulonglong4 qa = descA(ia);
+                uint32_t k1 = 0xFFFFFFFFu, d2 = 0xFFFFu;
+#pragma unroll
+                for (int c = 0; c < kRegC; ++c) {
+                    if (!ok[c]) continue;
+                    const uint32_t dist = __popcll(qa.x ^ cd[c].x) + __popcll(qa.y ^ cd[c].y) +
+                                          __popcll(qa.z ^ cd[c].z) + __popcll(qa.w ^ cd[c].w);
+                    const uint32_t key = (dist << 16) | (uint32_t)(r16 + kRow * c);
+                    if (key < k1) {
+                        d2 = min(d2, k1 >> 16);
+                        k1 = key;
+                    } else {
+                        d2 = min(d2, dist);
+                    }
+                }
+#pragma unroll
+                for (int o = 1; o < kRow; o <<= 1) {
+                    const uint32_t ok1 = (uint32_t)__shfl_xor((int)k1, o, kRow);
+                    const uint32_t od2 = (uint32_t)__shfl_xor((int)d2, o, kRow);
+                    d2 = min(min(d2, od2), max(k1 >> 16, ok1 >> 16));
+                    k1 = min(k1, ok1);
+                }
+                const int best1 = k1 == 0xFFFFFFFFu ? 256 : (int)(k1 >> 16);
+                const int best2 = d2 >= 256u ? 256 : (int)d2;
+                const bool pass = mode == ORBGPU_BOW_KF_F ? best1 <= kThLow : best1 < kThLow;
+                if (!pass || !((float)best1 < nnratio * (float)best2)) continue;  // row-uniform
+                const int pos = (int)(k1 & 0xFFFFu);
+#pragma unroll
+                for (int c = 0; c < kRegC; ++c)
+                    if (r16 + kRow * c == pos) ok[c] = false;  // matched: skipped by later A features
+                if (r16 == 0) {
+                    const int bidx = fvfB(b0 + pos);
+                    int out;
+                    if (mode == ORBGPU_BOW_KF_F) {
+                        match[bidx] = ia;
+                        out = bidx;
+                    } else {
+                        match[ia] = bidx;
+                        atomicOr(&s_used[bidx >> 5], 1u << (bidx & 31));
+                        out = ia;
+                    }
+                    if (check_ori) {
+                        float rot = A.angle[ia] - B.angle[bidx];
+                        if (rot < 0.0f) rot += 360.0f;
+                        int bin = (int)roundf(rot * factor);
+                        if (bin == kHL) bin = 0;
+                        s_bin[out] = (signed char)bin;
+                        atomicAdd(&s_hist[bin], 1);
+                    }
+                }
+            }
+            continue;
+        }
         for (int ia_ = a0; ia_ < a1; ++ia_) {
             const int ia = fvfA(ia_);
             if (!validA(ia)) continue;

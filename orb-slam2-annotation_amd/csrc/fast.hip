@@ -129,15 +129,17 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
         return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     };
     const bool incol = col < dw;
+    // per-lane offset of row rsub; the row step rr * P is wave-uniform (a
+    // scalar multiply), so a pass costs one vector add for its address
+    const int lane_off = (3 + rsub) * P + 3 + ox + col;
     int na = 0;
     for (int rr = 0; rr < dh; rr += 2 * rstep) {
-        const int r0 = rr + rsub, r1 = r0 + rstep;
-        const int off0 = (3 + r0) * P + 3 + ox + col, off1 = off0 + rstep * P;
+        const int off0 = lane_off + rr * P, off1 = off0 + rstep * P;
         bool c0, c1;
         compass2(T.win + off0, T.win + off1, t, c0, c1);
-        const bool pass0 = incol & (r0 < dh) & c0;
-        const bool pass1 = incol & (r1 < dh) & c1;
-        const unsigned long long m0 = __ballot(pass0), m1 = __ballot(pass1);
+        const bool pass0 = incol & (rsub < dh - rr) & c0;
+        const bool pass1 = incol & (rsub + rstep < dh - rr) & c1;
+        const unsigned long long m0 = __builtin_amdgcn_ballot_w64(pass0), m1 = __builtin_amdgcn_ballot_w64(pass1);
         if (pass0) T.la[na + below(m0)] = (uint16_t)off0;
         na += __popcll(m0);
         if (pass1) T.la[na + below(m1)] = (uint16_t)off1;
