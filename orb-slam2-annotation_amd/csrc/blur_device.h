@@ -34,12 +34,15 @@ __device__ __forceinline__ void row_pass(const uint32_t (&P)[9], f32x2& lo, f32x
 // unless the total is (then the result saturates to 255 either way), so the
 // float arithmetic is exact.
 __device__ __forceinline__ f32x2 col_pass(f32x2 w0, f32x2 w1, f32x2 w2, f32x2 w3, f32x2 w4, f32x2 w5, f32x2 w6) {
-    const f32x2 k18 = {18.f, 18.f}, k34 = {34.f, 34.f}, k49 = {49.f, 49.f}, k55 = {55.f, 55.f};
+    // the taps carry the 1/65536 of the two passes' fixed-point scale: every
+    // term is an integer below 2^24 times 2^-16, so the sums are still exact
+    constexpr float kS = 1.f / 65536.f;
+    const f32x2 k18 = {18.f * kS, 18.f * kS}, k34 = {34.f * kS, 34.f * kS}, k49 = {49.f * kS, 49.f * kS},
+                k55 = {55.f * kS, 55.f * kS};
     f32x2 s = w3 * k55;
     s = __builtin_elementwise_fma(w2 + w4, k49, s);
     s = __builtin_elementwise_fma(w1 + w5, k34, s);
-    s = __builtin_elementwise_fma(w0 + w6, k18, s);
-    return s * f32x2{1.f / 65536.f, 1.f / 65536.f};  // exact: power of two
+    return __builtin_elementwise_fma(w0 + w6, k18, s);
 }
 
 // 8-bit result of one column on the scalar tail (x >= 4*floor(w/4)):

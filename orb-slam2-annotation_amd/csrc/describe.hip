@@ -16,6 +16,7 @@
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
 #include "blur_device.h"
+#include "group_sum.h"
 #include "../../include/orbgpu.h"
 
 #include <algorithm>
@@ -24,21 +25,56 @@ namespace orbgpu {
 
 namespace {
 
-__constant__ signed char c_pattern[1024] = {
+constexpr signed char kPattern[1024] = {
 #include "bit_pattern_31.inc"
 };
-// umax of the 31-px disc (ORBextractor.cpp:456-471; the oracle builds it the
-// reference's way), packed 4 bits per entry so a per-lane lookup is a shift,
-// not a memory load
-constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
-constexpr unsigned long long pack_umax() {
-    unsigned long long k = 0;
-    for (int i = 0; i < 16; ++i) k |= (unsigned long long)kUmax[i] << (4 * i);
-    return k;
+// the pattern as floats, one float4 (x0, y0, x1, y1) per test: a lane's test
+// is one 16-byte load, no per-coordinate conversions
+struct PatternF { float4 t[256]; };
+constexpr PatternF make_pattern_f() {
+    PatternF p{};
+    for (int i = 0; i < 256; ++i)
+        p.t[i] = float4{(float)kPattern[4 * i], (float)kPattern[4 * i + 1], (float)kPattern[4 * i + 2],
+                        (float)kPattern[4 * i + 3]};
+    return p;
 }
-constexpr unsigned long long kUmaxPacked = pack_umax();
-static_assert(kUmaxPacked == 0x3689abcddeeeffffull, "umax packing");
-__device__ inline int umax_of(int v) { return (int)((kUmaxPacked >> (4 * (v & 15))) & 15ull); }
+__constant__ PatternF c_pattern = make_pattern_f();
+
+// umax of the 31-px disc (ORBextractor.cpp:456-471; the oracle builds it the
+// reference's way)
+constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+
+constexpr int kRPitchC = 48;  // = kRPitch (raw patch row pitch), needed by the table below
+constexpr int kDiscWords = 31 * 9, kDiscLoads = (kDiscWords + 63) / 64;
+// IC_Angle's disc as staged-patch words.  Disc row v = r - 15 (r < 31)
+// covers the 4-aligned window columns c = 4q .. 4q+3 (q < 9) starting at
+// xd = (cx - 15) & ~3, so byte b of word (r, q) is u = 4q + b - od - 15
+// (od = cx - 15 - xd) and it is in the disc iff |u| <= umax[|v|].  Per
+// (od, word): byte weights 1, c and v + 15 of the bytes in the disc (0
+// outside), so Σp, Σc·p and Σ(v+15)·p are three v_dot4 accumulations, and
+// the word's LDS offset from the disc's top-left word.  Words past the disc
+// (idx >= 279) weigh 0.
+struct DiscWord { uint32_t m1, mc, mv, off; };
+struct DiscLut { DiscWord w[4][kDiscLoads * 64]; };
+constexpr DiscLut make_disc_lut() {
+    DiscLut L{};
+    for (int od = 0; od < 4; ++od)
+        for (int idx = 0; idx < kDiscWords; ++idx) {
+            const int r = idx / 9, q = idx % 9, v = r - 15, d = kUmax[v < 0 ? -v : v];
+            DiscWord e{0u, 0u, 0u, (uint32_t)(r * kRPitchC + 4 * q)};
+            for (int b = 0; b < 4; ++b) {
+                const int u = 4 * q + b - od - 15;
+                if (u >= -d && u <= d) {
+                    e.m1 |= 1u << (8 * b);
+                    e.mc |= (uint32_t)(4 * q + b) << (8 * b);
+                    e.mv |= (uint32_t)(v + 15) << (8 * b);
+                }
+            }
+            L.w[od][idx] = e;
+        }
+    return L;
+}
+__constant__ DiscLut c_disc = make_disc_lut();
 
 // OpenCV 2.4 fastAtan2 (mathfuncs.cpp); explicit _rn ops: never contracted.
 __device__ inline float fast_atan2(float y, float x) {
@@ -109,14 +145,24 @@ __device__ inline void glibc_sincosf(float y, float* sinp, float* cosp) {
     *cosp = sc_poly(xs, x2, p, n ^ 1);
 }
 
-__device__ inline int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+// wave total of an unsigned int, wave-uniform: 16-lane row sums on DPP
+// (quad xor 1, xor 2, half mirror, mirror: full-rate VALU moves), then the
+// four row totals read into scalars (integer: order-free, exact)
+__device__ inline uint32_t wave_total(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppXor1, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppXor2, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppHalfMirror, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppMirror, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 
+#ifndef ORBGPU_DESC_HALO
+#define ORBGPU_DESC_HALO 1
+#endif
+
 constexpr int kBPitch = 40;      // 37-px blurred rows, from a 4-aligned column
-constexpr int kRPitch = 48;      // raw patch rows: columns xb-4 .. xb+43 (12 dwords)
+constexpr int kRPitch = kRPitchC;  // raw patch rows: columns xb-4 .. xb+43 (12 dwords)
 constexpr int kRawWords = kPatch * (kRPitch / 4);   // 43 rows x 12 dwords
 constexpr int kQuads = kBPitch / 4;                 // 10 output quads per blurred row
 constexpr int kColChunks = (kBlur + 6) / 7;         // 6 chunks of <= 7 blurred rows
@@ -208,27 +254,25 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
     wave_sync();
 
     // 2. Intensity centroid (IC_Angle, ORBextractor.cpp:79-106) from the raw
-    // patch: disc row v = r - 15 covers window columns c = 4q..4q+3 of the
-    // 4-aligned window at xd = (cx - 15) & ~3, i.e. u = c - od - 15; bytes
-    // with |u| <= umax[|v|] are kept and v_dot4_u32_u8 gives sum(p) and
-    // sum(c * p) of the word.  Integer moments: order-free, exact.
+    // patch: per disc word (c_disc: offset and byte weights for this od)
+    // three v_dot4_u32_u8 accumulate Σp, Σc·p and Σ(v+15)·p; then
+    // m10 = Σc·p - (od+15)Σp, m01 = Σ(v+15)·p - 15Σp.  Integer moments:
+    // order-free, exact.
     const int xd = (cx - 15) & ~3, od = cx - 15 - xd;
     const uint8_t* disc = S.raw + (kPatchR - 15) * kRPitch + (xd - x0);
-    constexpr int kDiscWords = 31 * 9, kDiscLoads = (kDiscWords + 63) / 64;
-    int m10 = 0, m01 = 0;
+    uint32_t sp = 0u, cp = 0u, vp = 0u;
 #pragma unroll
     for (int k = 0; k < kDiscLoads; ++k) {
-        const int idx = lane + 64 * k, r = min(idx, kDiscWords - 1) / 9, q = min(idx, kDiscWords - 1) - r * 9;
-        const int vv = r - 15, d = umax_of(abs(vv));
-        const int s0 = min(max(od + 15 - d - 4 * q, 0), 4), e0 = min(max(od + 16 + d - 4 * q, 0), 4);
-        const uint32_t mask = e0 > s0 ? (uint32_t)(((1ull << (8 * (e0 - s0))) - 1ull) << (8 * s0)) : 0u;
-        const uint32_t w = idx < kDiscWords ? *reinterpret_cast<const uint32_t*>(disc + r * kRPitch + 4 * q) & mask : 0u;
-        const uint32_t cols = (uint32_t)(4 * q) * 0x01010101u + 0x03020100u;
-        const int sp = (int)__builtin_amdgcn_udot4(w, 0x01010101u, 0u, false);
-        const int cp = (int)__builtin_amdgcn_udot4(w, cols, 0u, false);
-        m10 += cp - (od + 15) * sp;
-        m01 += vv * sp;
+        const DiscWord e = c_disc.w[od][lane + 64 * k];
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(disc + e.off);
+        sp = __builtin_amdgcn_udot4(w, e.m1, sp, false);
+        cp = __builtin_amdgcn_udot4(w, e.mc, cp, false);
+        vp = __builtin_amdgcn_udot4(w, e.mv, vp, false);
     }
+    // wave totals now (scalars): the blur below then has every VGPR
+    const uint32_t tp = wave_total(sp);
+    const int m10 = (int)(wave_total(cp) - (uint32_t)(od + 15) * tp);
+    const int m01 = (int)(wave_total(vp) - 15u * tp);
 
     // 3. Blur (blur_device.h, the arithmetic of blur.hip) of the 37x37 patch:
     // lane = (output quad q, chunk c of 7 blurred rows); it runs the row pass
@@ -236,6 +280,50 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
     // the column pass and rounds per path (quad columns x < 4*floor(w/4): the
     // SIMD path).  No intermediate array, no extra wave sync.
     const int simd_end = L.w & ~3;
+#if ORBGPU_DESC_HALO
+    // lane = (quad q, chunk c) with c fastest, so the chunk below a lane's is
+    // the next lane: a lane runs the row pass of its chunk's first 8 raw rows
+    // (7c .. 7c+7) and takes the 5 halo rows 7c+8 .. 7c+12 from lane + 1
+    // (its rows 1..5) by whole-wave DPP shifts -- 8 row passes per 7 output
+    // rows instead of 13.  Chunk 5 (rows 35..42) needs no halo: it outputs
+    // rows 35 and 36 only.  All 64 lanes run the passes (lanes 60..63 repeat
+    // quad 9 and store nothing), so every DPP source lane is active.
+    {
+        const int qq = lane / kColChunks, c = lane - qq * kColChunks;
+        const int q = min(qq, kQuads - 1), r0 = c * 7;
+        const bool simd = xb + 4 * q < simd_end, store = qq < kQuads;
+        auto row = [&](int k, blurdev::f32x2& lo, blurdev::f32x2& hi) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(S.raw + (r0 + k) * kRPitch) + q;
+            blurdev::Raw3 R3;
+            R3.a = w[0];
+            R3.b = w[1];
+            R3.c = w[2];
+            blurdev::row_pass_raw(R3, lo, hi);
+        };
+        auto from_next = [](blurdev::f32x2 v) {  // the value of lane + 1 (DPP wave_shl:1)
+            return blurdev::f32x2{
+                __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.x), 0x130, 0xF, 0xF, false)),
+                __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.y), 0x130, 0xF, 0xF, false))};
+        };
+        blurdev::f32x2 wl[13], wh[13];  // local rows 0..12 (8..12 from lane + 1)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) row(k, wl[k], wh[k]);
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+            if (j >= 2) {  // halo row 6 + j = next lane's row j - 1, fetched just before its first use
+                wl[6 + j] = from_next(wl[j - 1]);
+                wh[6 + j] = from_next(wh[j - 1]);
+            }
+            if (store && r0 + j < kBlur) {
+                const blurdev::f32x2 lo =
+                    blurdev::col_pass(wl[j], wl[j + 1], wl[j + 2], wl[j + 3], wl[j + 4], wl[j + 5], wl[j + 6]);
+                const blurdev::f32x2 hi =
+                    blurdev::col_pass(wh[j], wh[j + 1], wh[j + 2], wh[j + 3], wh[j + 4], wh[j + 5], wh[j + 6]);
+                reinterpret_cast<uint32_t*>(S.blur + (r0 + j) * kBPitch)[q] = blurdev::pack4(lo, hi, simd);
+            }
+        }
+    }
+#else
     if (lane < kQuads * kColChunks) {
         const int q = lane % kQuads, c = lane / kQuads, r0 = c * 7;
         // the 7 row sums the next output row needs, slid one row per output row
@@ -267,8 +355,7 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
             }
         }
     }
-    m10 = wave_sum(m10);
-    m01 = wave_sum(m01);
+#endif
     const float angle = fast_atan2((float)m01, (float)m10);
     wave_sync();  // blurred patch complete
 
@@ -278,17 +365,18 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
     glibc_sincosf(ang, &sa, &ca);
     const float a = ca, b = sa;
     unsigned long long words[4];
+    // the patch centre in LDS; |ry|, |rx| <= 18: one signed 24-bit multiply-add per point
+    const uint8_t* centre = S.blur + kBlurR * kBPitch + kBlurR + ob;
 #pragma unroll
     for (int rnd = 0; rnd < 4; ++rnd) {
-        const int t = rnd * 64 + lane;
+        const float4 pt = c_pattern.t[rnd * 64 + lane];
         int val[2];
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) {
-            const float px = (float)c_pattern[4 * t + 2 * pp], py = (float)c_pattern[4 * t + 2 * pp + 1];
+            const float px = pp ? pt.z : pt.x, py = pp ? pt.w : pt.y;
             const int ry = __float2int_rn(__fadd_rn(__fmul_rn(px, b), __fmul_rn(py, a)));
             const int rx = __float2int_rn(__fsub_rn(__fmul_rn(px, a), __fmul_rn(py, b)));
-            // |ry|, |rx| <= 18: a 24-bit multiply-add (full rate), not v_mul_lo_u32
-            val[pp] = S.blur[__umul24((uint32_t)(kBlurR + ry), (uint32_t)kBPitch) + (uint32_t)(ob + kBlurR + rx)];
+            val[pp] = centre[__mul24(ry, kBPitch) + rx];
         }
         words[rnd] = __ballot(val[0] < val[1]);
     }
