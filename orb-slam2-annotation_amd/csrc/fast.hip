@@ -18,45 +18,6 @@ namespace orbgpu {
 
 namespace {
 
-__device__ inline bool has_run9(uint32_t m16) {
-    uint32_t m = m16 | (m16 << 16);
-    uint32_t r = m & (m >> 1);   // runs >= 2
-    r &= r >> 2;                 // >= 4
-    r &= r >> 4;                 // >= 8
-    r &= m >> 8;                 // >= 9
-    return r != 0;
-}
-
-// acc = 2 * acc + (a < b): the compare's VCC lane bit is the carry-in of
-// v_addc (2 VALU per ring bit instead of compare, select, shift-or)
-__device__ __forceinline__ void shift_in_lt(uint32_t& acc, int a, int b) {
-    asm("v_cmp_lt_i32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc" : "+v"(acc) : "v"(a), "v"(b) : "vcc");
-}
-
-// arc strength: max over the 16 arcs of 9 of max(min d, -max d), d = v - ring
-__device__ inline int arc_strength(const int d[16]) {
-    int mn2[16], mx2[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        mn2[k] = min(d[k], d[(k + 1) & 15]);
-        mx2[k] = max(d[k], d[(k + 1) & 15]);
-    }
-    int mn4[16], mx4[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
-    }
-    int best = -1000;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-        const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-        best = max(best, max(mn9, -mx9));
-    }
-    return best;
-}
-
 // q = n / d for n < 65536, 0 < d < 256 via one multiply (m = ceil(2^24/d))
 __device__ inline int fast_div(int n, uint32_t m) { return (int)(((uint32_t)n * m) >> 24); }
 
@@ -87,8 +48,8 @@ struct CellTiles {
 // FAST at threshold t on the cell's detection region: returns the number
 // of corners, their tile offsets in lb[] (row-major) and scores in sc[].
 // Stages are separated by wave compaction so each runs on dense lanes:
-// compass pre-test on every pixel -> 16-pixel contiguity test on survivors
-// -> arc strength on corners.
+// compass pre-test on every pixel -> arc strength of the survivors, two per
+// lane in packed 16-bit arithmetic (the corner test is s >= t + 1).
 template <int P>
 __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, int lane) {
     // compass pre-test, row-major over the detection region: 32 lanes per
@@ -146,37 +107,59 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
         na += __popcll(m1);
     }
     wave_sync();
+    // Survivors -> corners, two per lane (list entries base + lane and
+    // base + 64 + lane, one per 16-bit half): the arc strength of both pixels
+    // in packed 16-bit arithmetic (d = v - ring in [-255, 255]); corner at t
+    // <=> s >= t + 1.  Corners are compacted in list order (the low halves'
+    // entries precede the high halves') behind the survivors being read, and
+    // their scores go to the score tile.
+    typedef short i16x2 __attribute__((ext_vector_type(2)));
     const int ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
     const int ring_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
     int nb = 0;
-    for (int base = 0; base < na; base += 64) {
-        const int j = base + lane;
-        bool corner = false;
-        int off = 0;
-        if (j < na) {
-            off = T.la[j];
-            const uint8_t* p = T.win + off;
-            const int v = p[0], lo = v - t, hi = v + t;
-            uint32_t dark = 0, bright = 0;  // ring bits, position 0 ends in bit 15 (runs are order-free)
+    for (int base = 0; base < na; base += 128) {
+        const int j0 = base + lane, j1 = j0 + 64;
+        const int off0 = T.la[min(j0, na - 1)], off1 = T.la[min(j1, na - 1)];  // clamped: real pixels
+        // ring reads from the circle's top-left corner: every read is the base
+        // register plus a non-negative immediate (the empty asm keeps the
+        // compiler from folding the bias back into per-read adds)
+        int a0 = off0 - (3 * P + 3), a1 = off1 - (3 * P + 3);
+        asm volatile("" : "+v"(a0), "+v"(a1));
+        const uint8_t* p0 = T.win + a0;
+        const uint8_t* p1 = T.win + a1;
+        const i16x2 v = {(short)p0[3 * P + 3], (short)p1[3 * P + 3]};
+        i16x2 d[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int q = p[ring_dy[k] * P + ring_dx[k]];
-                shift_in_lt(dark, q, lo);
-                shift_in_lt(bright, hi, q);
-            }
-            corner = has_run9(dark) || has_run9(bright);
+        for (int k = 0; k < 16; ++k) {
+            const int o = (ring_dy[k] + 3) * P + ring_dx[k] + 3;
+            d[k] = v - i16x2{(short)p0[o], (short)p1[o]};
         }
-        nb = wave_append(corner, (uint16_t)off, T.lb, nb, lane);
-    }
-    wave_sync();
-    for (int j = lane; j < nb; j += 64) {
-        const int off = T.lb[j];
-        const uint8_t* p = T.win + off;
-        const int v = p[0];
-        int d[16];
+        i16x2 mn2[16], mx2[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) d[k] = v - p[ring_dy[k] * P + ring_dx[k]];
-        T.sc[off] = (uint8_t)min(arc_strength(d), 255);  // >= t + 1 for a corner
+        for (int k = 0; k < 16; ++k) {
+            mn2[k] = __builtin_elementwise_min(d[k], d[(k + 1) & 15]);
+            mx2[k] = __builtin_elementwise_max(d[k], d[(k + 1) & 15]);
+        }
+        i16x2 mn4[16], mx4[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            mn4[k] = __builtin_elementwise_min(mn2[k], mn2[(k + 2) & 15]);
+            mx4[k] = __builtin_elementwise_max(mx2[k], mx2[(k + 2) & 15]);
+        }
+        i16x2 bp = {-1000, -1000}, bn = {1000, 1000};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            bp = __builtin_elementwise_max(
+                bp, __builtin_elementwise_min(__builtin_elementwise_min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]));
+            bn = __builtin_elementwise_min(
+                bn, __builtin_elementwise_max(__builtin_elementwise_max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]));
+        }
+        const i16x2 sc = __builtin_elementwise_max(bp, -bn);  // arc strength (cornerScore + 1)
+        const bool c0 = (j0 < na) & (sc.x > t), c1 = (j1 < na) & (sc.y > t);
+        if (c0) T.sc[off0] = (uint8_t)sc.x;
+        if (c1) T.sc[off1] = (uint8_t)sc.y;
+        nb = wave_append(c0, (uint16_t)off0, T.lb, nb, lane);
+        nb = wave_append(c1, (uint16_t)off1, T.lb, nb, lane);
     }
     wave_sync();
     return nb;
@@ -195,17 +178,19 @@ __device__ int nms_emit(const CellTiles& T, int nb, int ox, int t, int lane, int
         int s = 0, off = 0;
         if (j < nb) {
             off = T.lb[j];
-            const uint8_t* q = T.sc + off;
-            s = q[0];
+            int a = off - (P + 1);  // the 3x3 block's top-left: non-negative read offsets
+            asm volatile("" : "+v"(a));
+            const uint8_t* q = T.sc + a;
+            s = q[P + 1];
             // all eight neighbours loaded and tested without short-circuit
             // branches (one basic block: the loads issue together)
             int v[8];
             int k = 0;
 #pragma unroll
-            for (int dy = -1; dy <= 1; ++dy)
+            for (int dy = 0; dy <= 2; ++dy)
 #pragma unroll
-                for (int dx = -1; dx <= 1; ++dx)
-                    if (dx != 0 || dy != 0) v[k++] = q[dy * P + dx];
+                for (int dx = 0; dx <= 2; ++dx)
+                    if (dx != 1 || dy != 1) v[k++] = q[dy * P + dx];
             int vmax = 0;
 #pragma unroll
             for (int m = 0; m < 8; ++m) vmax = max(vmax, v[m] >= t1 ? v[m] - 1 : 0);
