@@ -157,10 +157,6 @@ __device__ inline uint32_t wave_total(uint32_t v) {
            (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 
-#ifndef ORBGPU_DESC_HALO
-#define ORBGPU_DESC_HALO 1
-#endif
-
 constexpr int kBPitch = 40;      // 37-px blurred rows, from a 4-aligned column
 constexpr int kRPitch = kRPitchC;  // raw patch rows: columns xb-4 .. xb+43 (12 dwords)
 constexpr int kRawWords = kPatch * (kRPitch / 4);   // 43 rows x 12 dwords
@@ -275,13 +271,12 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
     const int m01 = (int)(wave_total(vp) - 15u * tp);
 
     // 3. Blur (blur_device.h, the arithmetic of blur.hip) of the 37x37 patch:
-    // lane = (output quad q, chunk c of 7 blurred rows); it runs the row pass
-    // of the chunk's 13 raw rows from LDS, slides them through registers for
-    // the column pass and rounds per path (quad columns x < 4*floor(w/4): the
-    // SIMD path).  No intermediate array, no extra wave sync.
+    // lane = (output quad q, chunk c of 7 blurred rows); row passes from the
+    // raw patch in LDS, the column pass in registers, rounding per path (quad
+    // columns x < 4*floor(w/4): the SIMD path).  No intermediate array, no
+    // extra wave sync.
     const int simd_end = L.w & ~3;
-#if ORBGPU_DESC_HALO
-    // lane = (quad q, chunk c) with c fastest, so the chunk below a lane's is
+    // c is the fastest lane index, so the chunk below a lane's is
     // the next lane: a lane runs the row pass of its chunk's first 8 raw rows
     // (7c .. 7c+7) and takes the 5 halo rows 7c+8 .. 7c+12 from lane + 1
     // (its rows 1..5) by whole-wave DPP shifts -- 8 row passes per 7 output
@@ -323,39 +318,6 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
             }
         }
     }
-#else
-    if (lane < kQuads * kColChunks) {
-        const int q = lane % kQuads, c = lane / kQuads, r0 = c * 7;
-        // the 7 row sums the next output row needs, slid one row per output row
-        // (28 live registers instead of all 13 rows' 52)
-        blurdev::f32x2 wl[7], wh[7];
-        auto row = [&](int k, blurdev::f32x2& lo, blurdev::f32x2& hi) {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(S.raw + min(r0 + k, kPatch - 1) * kRPitch) + q;
-            blurdev::Raw3 R3;
-            R3.a = w[0];
-            R3.b = w[1];
-            R3.c = w[2];
-            blurdev::row_pass_raw(R3, lo, hi);
-        };
-#pragma unroll
-        for (int k = 0; k < 6; ++k) row(k, wl[k + 1], wh[k + 1]);
-        const bool simd = xb + 4 * q < simd_end;
-#pragma unroll
-        for (int j = 0; j < 7; ++j) {
-#pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                wl[k] = wl[k + 1];
-                wh[k] = wh[k + 1];
-            }
-            row(j + 6, wl[6], wh[6]);
-            if (r0 + j < kBlur) {
-                const blurdev::f32x2 lo = blurdev::col_pass(wl[0], wl[1], wl[2], wl[3], wl[4], wl[5], wl[6]);
-                const blurdev::f32x2 hi = blurdev::col_pass(wh[0], wh[1], wh[2], wh[3], wh[4], wh[5], wh[6]);
-                reinterpret_cast<uint32_t*>(S.blur + (r0 + j) * kBPitch)[q] = blurdev::pack4(lo, hi, simd);
-            }
-        }
-    }
-#endif
     const float angle = fast_atan2((float)m01, (float)m10);
     wave_sync();  // blurred patch complete
 
@@ -365,8 +327,14 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
     glibc_sincosf(ang, &sa, &ca);
     const float a = ca, b = sa;
     unsigned long long words[4];
-    // the patch centre in LDS; |ry|, |rx| <= 18: one signed 24-bit multiply-add per point
-    const uint8_t* centre = S.blur + kBlurR * kBPitch + kBlurR + ob;
+    // cvRound of the rotated offsets by the float magic-number add: r + 1.5*2^23
+    // rounds r to an integer half-to-even (the magic is even, |r| <= 19), and
+    // the sum's bits are 0x4B400000 + round(r), whose low 24 bits 0x400000 +
+    // round(r) feed one v_mad_u32_u24: ry_bits * 40 + rx_bits - kBias is the
+    // blurred-patch offset from the centre
+    constexpr float kMagic = 12582912.f;
+    constexpr uint32_t kBias = 0x400000u * (uint32_t)kBPitch + 0x4B400000u;
+    const uint32_t cb = (uint32_t)(kBlurR * kBPitch + kBlurR + ob) - kBias;  // wave-uniform
 #pragma unroll
     for (int rnd = 0; rnd < 4; ++rnd) {
         const float4 pt = c_pattern.t[rnd * 64 + lane];
@@ -374,9 +342,10 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) {
             const float px = pp ? pt.z : pt.x, py = pp ? pt.w : pt.y;
-            const int ry = __float2int_rn(__fadd_rn(__fmul_rn(px, b), __fmul_rn(py, a)));
-            const int rx = __float2int_rn(__fsub_rn(__fmul_rn(px, a), __fmul_rn(py, b)));
-            val[pp] = centre[__mul24(ry, kBPitch) + rx];
+            const float fy = __fadd_rn(__fmul_rn(px, b), __fmul_rn(py, a));
+            const float fx = __fsub_rn(__fmul_rn(px, a), __fmul_rn(py, b));
+            const uint32_t iy = __float_as_uint(__fadd_rn(fy, kMagic)), ix = __float_as_uint(__fadd_rn(fx, kMagic));
+            val[pp] = S.blur[(int)(__umul24(iy, (uint32_t)kBPitch) + ix + cb)];
         }
         words[rnd] = __ballot(val[0] < val[1]);
     }

@@ -108,14 +108,23 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
     }
     wave_sync();
     // Survivors -> corners, two per lane (list entries base + lane and
-    // base + 64 + lane, one per 16-bit half): the arc strength of both pixels
-    // in packed 16-bit arithmetic (d = v - ring in [-255, 255]); corner at t
-    // <=> s >= t + 1.  Corners are compacted in list order (the low halves'
+    // base + 64 + lane, one per 16-bit half).  With d = v - ring, the arc
+    // strength max over arcs of max(min d, -max d) is
+    //   s = max(v - min_k max9_k(ring), max_k min9_k(ring) - v)
+    // (max9_k / min9_k over the 9-arc starting at ring position k); corner at
+    // t <=> s >= t + 1.  The ring bytes of both pixels sit in the two halves
+    // of a register as f16 denormals (order-preserving bit patterns; the
+    // kernel keeps f16 denormals, and minimum/maximum only select), so every
+    // 3-way min/max is one v_pk_minimum3_f16 / v_pk_maximum3_f16: a 9-arc is
+    // three 3-runs.  Corners are compacted in list order (the low halves'
     // entries precede the high halves') behind the survivors being read, and
     // their scores go to the score tile.
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     typedef short i16x2 __attribute__((ext_vector_type(2)));
     const int ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
     const int ring_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+    auto max3 = [](h2 x, h2 y, h2 z) { return __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z); };
+    auto min3 = [](h2 x, h2 y, h2 z) { return __builtin_elementwise_minimum(__builtin_elementwise_minimum(x, y), z); };
     int nb = 0;
     for (int base = 0; base < na; base += 128) {
         const int j0 = base + lane, j1 = j0 + 64;
@@ -127,34 +136,32 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
         asm volatile("" : "+v"(a0), "+v"(a1));
         const uint8_t* p0 = T.win + a0;
         const uint8_t* p1 = T.win + a1;
-        const i16x2 v = {(short)p0[3 * P + 3], (short)p1[3 * P + 3]};
-        i16x2 d[16];
+        auto pair = [&](int o) { return (uint32_t)p0[o] | ((uint32_t)p1[o] << 16); };
+        const uint32_t vv = pair(3 * P + 3);
+        h2 r[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) r[k] = __builtin_bit_cast(h2, pair((ring_dy[k] + 3) * P + ring_dx[k] + 3));
+        h2 hi3[16], lo3[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            const int o = (ring_dy[k] + 3) * P + ring_dx[k] + 3;
-            d[k] = v - i16x2{(short)p0[o], (short)p1[o]};
+            hi3[k] = max3(r[k], r[(k + 1) & 15], r[(k + 2) & 15]);
+            lo3[k] = min3(r[k], r[(k + 1) & 15], r[(k + 2) & 15]);
         }
-        i16x2 mn2[16], mx2[16];
+        h2 hi9[16], lo9[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            mn2[k] = __builtin_elementwise_min(d[k], d[(k + 1) & 15]);
-            mx2[k] = __builtin_elementwise_max(d[k], d[(k + 1) & 15]);
+            hi9[k] = max3(hi3[k], hi3[(k + 3) & 15], hi3[(k + 6) & 15]);
+            lo9[k] = min3(lo3[k], lo3[(k + 3) & 15], lo3[(k + 6) & 15]);
         }
-        i16x2 mn4[16], mx4[16];
+        h2 A = min3(hi9[0], hi9[1], hi9[2]), B = max3(lo9[0], lo9[1], lo9[2]);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            mn4[k] = __builtin_elementwise_min(mn2[k], mn2[(k + 2) & 15]);
-            mx4[k] = __builtin_elementwise_max(mx2[k], mx2[(k + 2) & 15]);
+        for (int k = 3; k < 16; k += 2) {
+            A = k + 1 < 16 ? min3(A, hi9[k], hi9[k + 1]) : __builtin_elementwise_minimum(A, hi9[k]);
+            B = k + 1 < 16 ? max3(B, lo9[k], lo9[k + 1]) : __builtin_elementwise_maximum(B, lo9[k]);
         }
-        i16x2 bp = {-1000, -1000}, bn = {1000, 1000};
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            bp = __builtin_elementwise_max(
-                bp, __builtin_elementwise_min(__builtin_elementwise_min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]));
-            bn = __builtin_elementwise_min(
-                bn, __builtin_elementwise_max(__builtin_elementwise_max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]));
-        }
-        const i16x2 sc = __builtin_elementwise_max(bp, -bn);  // arc strength (cornerScore + 1)
+        const i16x2 v = __builtin_bit_cast(i16x2, vv), ia = __builtin_bit_cast(i16x2, A),
+                    ib = __builtin_bit_cast(i16x2, B);
+        const i16x2 sc = __builtin_elementwise_max(v - ia, ib - v);  // arc strength (cornerScore + 1)
         const bool c0 = (j0 < na) & (sc.x > t), c1 = (j1 < na) & (sc.y > t);
         if (c0) T.sc[off0] = (uint8_t)sc.x;
         if (c1) T.sc[off1] = (uint8_t)sc.y;
