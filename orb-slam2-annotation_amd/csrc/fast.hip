@@ -72,13 +72,26 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
             r.y = q[o];
             return r;
         };
-        const u16x2 v = ld(0), c0 = ld(3 * P), c4 = ld(3), c8 = ld(-3 * P), c12 = ld(-3);
-        const u16x2 dark = __builtin_elementwise_min(
-            __builtin_elementwise_min(__builtin_elementwise_max(c0, c4), __builtin_elementwise_max(c4, c8)),
-            __builtin_elementwise_min(__builtin_elementwise_max(c8, c12), __builtin_elementwise_max(c12, c0)));
-        const u16x2 bright = __builtin_elementwise_max(
-            __builtin_elementwise_max(__builtin_elementwise_min(c0, c4), __builtin_elementwise_min(c4, c8)),
-            __builtin_elementwise_max(__builtin_elementwise_min(c8, c12), __builtin_elementwise_min(c12, c0)));
+        // (the min/max run on the bytes as f16 denormal pairs, order-preserving
+        // bit patterns: the 3-way steps are v_pk_minimum3 / maximum3_f16)
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        auto h = [](u16x2 x) { return __builtin_bit_cast(h2, x); };
+        const u16x2 v = ld(0);
+        const h2 c0 = h(ld(3 * P)), c4 = h(ld(3)), c8 = h(ld(-3 * P)), c12 = h(ld(-3));
+        const u16x2 dark = __builtin_bit_cast(
+            u16x2, __builtin_elementwise_minimum(
+                       __builtin_elementwise_minimum(
+                           __builtin_elementwise_minimum(__builtin_elementwise_maximum(c0, c4),
+                                                         __builtin_elementwise_maximum(c4, c8)),
+                           __builtin_elementwise_maximum(c8, c12)),
+                       __builtin_elementwise_maximum(c12, c0)));
+        const u16x2 bright = __builtin_bit_cast(
+            u16x2, __builtin_elementwise_maximum(
+                       __builtin_elementwise_maximum(
+                           __builtin_elementwise_maximum(__builtin_elementwise_minimum(c0, c4),
+                                                         __builtin_elementwise_minimum(c4, c8)),
+                           __builtin_elementwise_minimum(c8, c12)),
+                       __builtin_elementwise_minimum(c12, c0)));
         const u16x2 x = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, dark),
                                                   __builtin_elementwise_sub_sat(bright, v));
         const u16x2 tt = {(unsigned short)t, (unsigned short)t};
