@@ -37,12 +37,27 @@ __device__ inline int wave_append(bool pred, uint16_t v, uint16_t* list, int n, 
     return n + __popcll(m);
 }
 
+// na + the number of set bits of m in lanes below this one
+__device__ __forceinline__ int append_pos(unsigned long long m, int na) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)na));
+}
+
+// a where this lane's bit of the mask m (scalar registers) is set, else b:
+// one v_cndmask on the mask as it is (a bool built from it would be turned
+// back into a vector value and compared again)
+__device__ __forceinline__ int lane_select(unsigned long long m, int a, int b) {
+    int r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+    return r;
+}
+
 struct CellTiles {
     const uint8_t* win;  // staged window, pitch P, column c <-> level x = xa + c
     uint8_t* sc;         // FAST arc strength of corners, 0 elsewhere
     uint16_t* la;        // tile offsets passing the compass pre-test
     uint16_t* lb;        // tile offsets of corners (row-major order); the same buffer as la: the
                          // corner list is compacted in place behind the survivors being read
+    int dump;            // list index past the longest list: the compass's non-survivor lanes store there
 };
 
 // FAST at threshold t on the cell's detection region: returns the number
@@ -65,7 +80,7 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
     //   pairwise max is; both brighter than v + t <=> the largest pairwise min
     //   is; dark < v - t <=> sat(v - dark) > t, bright > v + t <=> sat(bright - v) > t
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-    auto compass2 = [&](const uint8_t* p, const uint8_t* q, int t, bool& pass0, bool& pass1) {
+    auto compass2 = [&](const uint8_t* p, const uint8_t* q, int t) -> uint32_t {
         auto ld = [&](int o) {
             u16x2 r;
             r.x = p[o];
@@ -95,28 +110,28 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
         const u16x2 x = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, dark),
                                                   __builtin_elementwise_sub_sat(bright, v));
         const u16x2 tt = {(unsigned short)t, (unsigned short)t};
-        const u16x2 y = __builtin_elementwise_sub_sat(x, tt);  // nonzero <=> passes
-        pass0 = y.x != 0;
-        pass1 = y.y != 0;
+        return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x, tt));  // a half nonzero <=> its pixel passes
     };
-    auto below = [&](unsigned long long m) {  // set bits of m in lanes below this one
-        return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    };
-    const bool incol = col < dw;
-    // per-lane offset of row rsub; the row step rr * P is wave-uniform (a
-    // scalar multiply), so a pass costs one vector add for its address
+    // Lane masks are formed in scalar registers: the compass results by
+    // v_cmp straight into a mask, the column and row ranges as wave-uniform
+    // masks (rows rr + rsub are in range for every lane while 2+ rows remain,
+    // only the rsub = 0 half on the last row).  Every lane stores: a survivor
+    // at its compacted position, the others into the dump slot past the list.
+    const unsigned long long colmask = __builtin_amdgcn_ballot_w64(col < dw);
+    const unsigned long long sub0 = lpr == 32 ? 0xFFFFFFFFull : ~0ull;  // lanes of row rsub = 0
     const int lane_off = (3 + rsub) * P + 3 + ox + col;
     int na = 0;
     for (int rr = 0; rr < dh; rr += 2 * rstep) {
         const int off0 = lane_off + rr * P, off1 = off0 + rstep * P;
-        bool c0, c1;
-        compass2(T.win + off0, T.win + off1, t, c0, c1);
-        const bool pass0 = incol & (rsub < dh - rr) & c0;
-        const bool pass1 = incol & (rsub + rstep < dh - rr) & c1;
-        const unsigned long long m0 = __builtin_amdgcn_ballot_w64(pass0), m1 = __builtin_amdgcn_ballot_w64(pass1);
-        if (pass0) T.la[na + below(m0)] = (uint16_t)off0;
+        const uint32_t y = compass2(T.win + off0, T.win + off1, t);
+        const int rem = dh - rr;  // rows left, >= 1
+        const unsigned long long rows0 = rem >= 2 ? ~0ull : sub0;
+        const unsigned long long rows1 = rem > rstep + 1 ? ~0ull : (rem > rstep ? sub0 : 0ull);
+        const unsigned long long m0 = __builtin_amdgcn_uicmp(y & 0xFFFFu, 0u, 33 /* ne */) & colmask & rows0;
+        const unsigned long long m1 = __builtin_amdgcn_uicmp(y, 0x10000u, 35 /* uge */) & colmask & rows1;
+        T.la[lane_select(m0, append_pos(m0, na), T.dump)] = (uint16_t)off0;
         na += __popcll(m0);
-        if (pass1) T.la[na + below(m1)] = (uint16_t)off1;
+        T.la[lane_select(m1, append_pos(m1, na), T.dump)] = (uint16_t)off1;
         na += __popcll(m1);
     }
     wave_sync();
@@ -190,7 +205,6 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
 template <int P>
 __device__ int nms_emit(const CellTiles& T, int nb, int ox, int t, int lane, int iniX, int iniY,
                         uint32_t* out, int cap, int* err) {
-    const int t1 = t + 1;
     int total = 0;
     for (int base = 0; base < nb; base += 64) {
         const int j = base + lane;
@@ -202,8 +216,11 @@ __device__ int nms_emit(const CellTiles& T, int nb, int ox, int t, int lane, int
             asm volatile("" : "+v"(a));
             const uint8_t* q = T.sc + a;
             s = q[P + 1];
-            // all eight neighbours loaded and tested without short-circuit
-            // branches (one basic block: the loads issue together)
+            // all eight neighbours loaded without short-circuit branches (one
+            // basic block: the loads issue together).  The tile holds 0 or a
+            // score >= t + 1 (this pass's corners only), so cv::FAST's neighbour
+            // term (v >= t + 1 ? v - 1 : 0) is max(v - 1, 0), and
+            // s - 1 > max over the neighbours  <=>  s > max(vmax, 1)
             int v[8];
             int k = 0;
 #pragma unroll
@@ -211,10 +228,8 @@ __device__ int nms_emit(const CellTiles& T, int nb, int ox, int t, int lane, int
 #pragma unroll
                 for (int dx = 0; dx <= 2; ++dx)
                     if (dx != 1 || dy != 1) v[k++] = q[dy * P + dx];
-            int vmax = 0;
-#pragma unroll
-            for (int m = 0; m < 8; ++m) vmax = max(vmax, v[m] >= t1 ? v[m] - 1 : 0);
-            keep = s - 1 > vmax;
+            const int vmax = max(max(max(max(v[0], v[1]), max(v[2], v[3])), max(max(v[4], v[5]), max(v[6], v[7]))), 1);
+            keep = s > vmax;
         }
         const unsigned long long m = __ballot(keep);
         if (keep) {
@@ -247,13 +262,14 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     const int R = g.win_rows;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: metadata in SGPRs
-    const size_t per_wave = ((size_t)2 * P * R + 2 * (size_t)g.det_max + 15) & ~(size_t)15;
+    const size_t per_wave = ((size_t)2 * P * R + 2 * ((size_t)g.det_max + 1) + 15) & ~(size_t)15;
     uint8_t* ws = smem + wave * per_wave;
     CellTiles T;
     T.win = ws;
     T.sc = ws + P * R;
     T.la = reinterpret_cast<uint16_t*>(ws + 2 * P * R);
-    T.lb = T.la;  // in-place: iteration `base` writes below base + 64 after reading la[base .. base + 64)
+    T.lb = T.la;
+    T.dump = g.det_max;  // in-place: iteration `base` writes below base + 64 after reading la[base .. base + 64)
     uint8_t* s_win = ws;
 
     // one cell per wave; waves of a block take consecutive cells of a frame;
@@ -359,7 +375,7 @@ hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size
                              const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err,
                              hipStream_t stream) {
     const int items = g.total_cells * batch;
-    const size_t per_wave = ((size_t)2 * g.win_pitch * g.win_rows + 2 * (size_t)g.det_max + 15) & ~(size_t)15;
+    const size_t per_wave = ((size_t)2 * g.win_pitch * g.win_rows + 2 * ((size_t)g.det_max + 1) + 15) & ~(size_t)15;
     dim3 grid((items + kCellWaves - 1) / kCellWaves);
     const size_t lds = per_wave * kCellWaves;
 #define ORBGPU_FAST_CASE(PP)                                                                                        \
