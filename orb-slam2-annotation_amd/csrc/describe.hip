@@ -179,15 +179,18 @@ struct alignas(16) DescLds {
     uint8_t blur[kBlur * kBPitch];
 };
 
-__device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& S,
-                             const uint8_t* __restrict__ img0, size_t row0, size_t frame0,
-                             const uint8_t* __restrict__ pyr, const uint32_t* __restrict__ oct_out,
-                             const int* __restrict__ oct_count, orbgpu_keypoint* __restrict__ kps,
-                             uint8_t* __restrict__ desc, int* __restrict__ counts, int kp_cap) {
+// A keypoint slot of a frame: its level, index within the level and output
+// position; false when the slot is past the level's octree count.
+struct KeyRef {
+    int l, i, before, cx, cy;
+    uint32_t key;
+};
+
+__device__ bool key_ref(const Geom& g, int f, int slot, int lane, const uint32_t* __restrict__ oct_out,
+                        const int* __restrict__ oct_count, int* __restrict__ counts, KeyRef& K) {
     int l = 0;
     while (l + 1 < g.nlevels && slot >= g.lv[l + 1].out_offset) ++l;
-    const LevelGeom& L = g.lv[l];
-    const int i = slot - L.out_offset;
+    const int i = slot - g.lv[l].out_offset;
     const int* oc = oct_count + (size_t)f * g.nlevels;
     int before = 0, total = 0;
     for (int ll = 0; ll < g.nlevels; ++ll) {
@@ -196,9 +199,23 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
         if (ll < l) before += c;
     }
     if (slot == 0 && lane == 0) counts[f] = total;
-    if (i >= oc[l]) return;
-    const uint32_t key = oct_out[(size_t)f * g.slots_frame + slot];
-    const int cx = key_x(key) + kBorder, cy = key_y(key) + kBorder;
+    if (i >= oc[l]) return false;
+    K.l = l;
+    K.i = i;
+    K.before = before;
+    K.key = oct_out[(size_t)f * g.slots_frame + slot];
+    K.cx = key_x(K.key) + kBorder;
+    K.cy = key_y(K.key) + kBorder;
+    return true;
+}
+
+// Stage the neighbourhood, IC_Angle's moments, the blurred patch into S.blur;
+// returns (m10, m01), wave-uniform.
+__device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, DescLds& S,
+                               const uint8_t* __restrict__ img0, size_t row0, size_t frame0,
+                               const uint8_t* __restrict__ pyr) {
+    const int l = K.l, cx = K.cx, cy = K.cy;
+    const LevelGeom& L = g.lv[l];
     const uint8_t* raw = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
     const size_t rp = l == 0 ? row0 : (size_t)L.pitch;
 
@@ -208,17 +225,20 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
     // clone, ORBextractor.cpp:1097-1098).  Dwords inside the level are one
     // load each; a dword that crosses the border is assembled from reflected
     // bytes.  All loads of a lane are issued before any is stored.
-    const int xb = (cx - kBlurR) & ~3, ob = cx - kBlurR - xb, x0 = xb - 4;
+    const int xb = (cx - kBlurR) & ~3, x0 = xb - 4;
     // a neighbourhood entirely inside the level (wave-uniform; most keypoints): three
     // 16-byte chunks per row, two loads per lane, no reflection
     if (x0 >= 0 && x0 + kRPitch <= L.w && cy - kPatchR >= 0 && cy + kPatchR < L.h) {
         constexpr int kChunks = kPatch * (kRPitch / 16);  // 129
         const uint8_t* top = raw + (size_t)(cy - kPatchR) * rp + x0;
         uint4 c[3];
+        // r = idx / 3 by a 24-bit multiply (exact for idx < 4096), row offsets
+        // by 24-bit multiplies (rp < 2^24: launcher check)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const int idx = min(lane + 64 * k, kChunks - 1), r = idx / 3, q = idx - 3 * r;
-            c[k] = load16_a4(top + (size_t)r * rp + 16 * q);
+            const int idx = min(lane + 64 * k, kChunks - 1), r = (int)(__umul24((uint32_t)idx, 21846u) >> 16),
+                      q = idx - 3 * r;
+            c[k] = load16_a4(top + __umul24((uint32_t)r, (uint32_t)rp) + 16 * q);
         }
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -318,14 +338,16 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
             }
         }
     }
-    const float angle = fast_atan2((float)m01, (float)m10);
-    wave_sync();  // blurred patch complete
+    return int2{m10, m01};
+}
 
-    // 4. rBRIEF (computeOrbDescriptor, ORBextractor.cpp:110-149)
-    const float ang = __fmul_rn(angle, (float)(M_PI / 180.f));
-    float sa, ca;
-    glibc_sincosf(ang, &sa, &ca);
-    const float a = ca, b = sa;
+// rBRIEF (computeOrbDescriptor, ORBextractor.cpp:110-149) on the blurred
+// patch with the keypoint's rotation, and the output record.
+__device__ void describe_tests(const Geom& g, int f, const KeyRef& K, int lane, const DescLds& S, float4 rot,
+                               orbgpu_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int kp_cap) {
+    const LevelGeom& L = g.lv[K.l];
+    const int ob = K.cx - kBlurR - ((K.cx - kBlurR) & ~3);
+    const float angle = rot.x, a = rot.y, b = rot.z;
     unsigned long long words[4];
     // cvRound of the rotated offsets by the float magic-number add: r + 1.5*2^23
     // rounds r to an integer half-to-even (the magic is even, |r| <= 19), and
@@ -350,23 +372,26 @@ __device__ void describe_one(const Geom& g, int f, int slot, int lane, DescLds& 
         words[rnd] = __ballot(val[0] < val[1]);
     }
 
-    const size_t o = (size_t)f * kp_cap + before + i;
+    const size_t o = (size_t)f * kp_cap + K.before + K.i;
     if (lane < 4) reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = words[lane];
     if (lane == 0) {
         orbgpu_keypoint kp;
-        const float fx = (float)cx, fy = (float)cy;
-        kp.x = l == 0 ? fx : __fmul_rn(fx, L.scale);
-        kp.y = l == 0 ? fy : __fmul_rn(fy, L.scale);
+        const float fx = (float)K.cx, fy = (float)K.cy;
+        kp.x = K.l == 0 ? fx : __fmul_rn(fx, L.scale);
+        kp.y = K.l == 0 ? fy : __fmul_rn(fy, L.scale);
         kp.size = (float)L.size_i;
         kp.angle = angle;
-        kp.response = (float)key_s(key);
-        kp.octave = l;
+        kp.response = (float)key_s(K.key);
+        kp.octave = K.l;
         kp.class_id = -1;
         kps[o] = kp;
     }
 }
 
-constexpr int kDescWaves = 4;
+#ifndef ORBGPU_DESC_WAVES
+#define ORBGPU_DESC_WAVES 4
+#endif
+constexpr int kDescWaves = ORBGPU_DESC_WAVES;  // keypoints (waves) per block
 
 // One wave per (frame, slot) item, four items per block.  Blocks are
 // XCD-swizzled so one frame's keypoints (whose neighbourhoods overlap) are
@@ -394,10 +419,19 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
     const int blk = (int)blockIdx.x;
 #endif
     const int item = blk * kDescWaves + wave;
-    if (item >= items) return;
     const int f = item / g.slots_frame, slot = item - f * g.slots_frame;
-    describe_one(g, f, slot, lane, s_lds[wave], img0, row0, frame0, pyr, oct_out, oct_count, kps, desc, counts,
-                 kp_cap);
+    KeyRef K;
+    const bool valid = item < items && key_ref(g, f, slot, lane, oct_out, oct_count, counts, K);
+    if (!valid) return;
+    const int2 m = describe_patch(g, f, K, lane, s_lds[wave], img0, row0, frame0, pyr);
+    // the orientation: a serial chain on wave-uniform values, run by the
+    // whole wave (measured: sharing it across the block's waves through LDS
+    // and two barriers made the kernel slower, 0.574 -> 0.593 ms)
+    const float angle = fast_atan2((float)m.y, (float)m.x);
+    float sa, ca;
+    glibc_sincosf(__fmul_rn(angle, (float)(M_PI / 180.f)), &sa, &ca);
+    wave_sync();  // blurred patch complete
+    describe_tests(g, f, K, lane, s_lds[wave], float4{angle, ca, sa, 0.f}, kps, desc, kp_cap);
 }
 
 }  // namespace
@@ -407,6 +441,7 @@ hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
                            hipStream_t stream, int* err_word, int* err_copy) {
     const int items = g.slots_frame * batch;
+    if (row0 >= (1u << 24)) return hipErrorInvalidValue;  // row offsets by 24-bit multiplies
     const int blocks = (items + kDescWaves - 1) / kDescWaves;
     hipLaunchKernelGGL(describe_kernel, dim3(blocks), dim3(64 * kDescWaves), 0, stream, g, items, img0, row0, frame0,
                        pyr, oct_out, oct_count, kps, desc, counts, kp_cap, err_word, err_copy);

@@ -18,8 +18,12 @@ namespace orbgpu {
 
 namespace {
 
-// q = n / d for n < 65536, 0 < d < 256 via one multiply (m = ceil(2^24/d))
-__device__ inline int fast_div(int n, uint32_t m) { return (int)(((uint32_t)n * m) >> 24); }
+// q = n / d via one full-rate v_mul_u32_u24 (not the quarter-rate
+// v_mul_lo_u32): m = floor(2^23 / d) + 1 < 2^24 for every d >= 1 (a cell
+// clipped at the level's right edge can be one chunk wide), exact while
+// n < 2^23 / d and n * m < 2^32 -- here n < 512, d <= 5
+__host__ __device__ constexpr uint32_t fast_div_m(uint32_t d) { return (1u << 23) / d + 1u; }
+__device__ inline int fast_div(int n, uint32_t m) { return (int)(__umul24((uint32_t)n, m) >> 23); }
 
 // The waves of a block work on different cells, so stages are ordered with
 // a wave-local LDS fence, never a block barrier.
@@ -117,7 +121,7 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
     // masks (rows rr + rsub are in range for every lane while 2+ rows remain,
     // only the rsub = 0 half on the last row).  Every lane stores: a survivor
     // at its compacted position, the others into the dump slot past the list.
-    const unsigned long long colmask = __builtin_amdgcn_ballot_w64(col < dw);
+    const unsigned long long colmask = __builtin_amdgcn_uicmp((uint32_t)col, (uint32_t)dw, 36 /* ult */);
     const unsigned long long sub0 = lpr == 32 ? 0xFFFFFFFFull : ~0ull;  // lanes of row rsub = 0
     const int lane_off = (3 + rsub) * P + 3 + ox + col;
     int na = 0;
@@ -299,13 +303,13 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     const int maxY = min(iniY + L.hcell + 6, L.max_by), maxX = min(iniX + L.wcell + 6, L.max_bx);
     const int wh = maxY - iniY;
     const uint8_t* base = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
-    const size_t pitch = l == 0 ? row0 : (size_t)L.pitch;
+    const uint32_t pitch = l == 0 ? (uint32_t)row0 : (uint32_t)L.pitch;  // < 2^24 (launcher check)
 
     // stage rows: dwords covering [xa, maxX), xa = iniX & ~3 (row pitch and
     // frame base are 16-byte aligned; maxX <= w - 16, so no over-read)
     const int xa = iniX & ~3, ox = iniX - xa;
     const int nd = (maxX - xa + 3) >> 2;
-    const uint32_t mnd = (1u << 24) / (uint32_t)nd + 1u;
+    const uint32_t mnd = fast_div_m((uint32_t)nd);
     // all of a lane's loads are issued before any is consumed, so the
     // window costs one memory round trip, not one per row group
     const uint8_t* wbase = base + (size_t)iniY * pitch + xa;
@@ -314,19 +318,19 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
         // last chunk reads at most 12 bytes past maxX, still inside the level row since
         // maxX <= w - 16); one load per lane for ~64 of a window's ~115 chunks
         const int nc = (maxX - xa + 15) >> 4;
-        const uint32_t mnc = (1u << 24) / (uint32_t)nc + 1u;
+        const uint32_t mnc = fast_div_m((uint32_t)nc);
         for (int b0 = 0; b0 < nc * wh; b0 += 64 * 2) {
             uint4 v[2];
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
                 const int idx = min(b0 + lane + 64 * k, nc * wh - 1);
-                const int r = fast_div(idx, mnc), q = idx - r * nc;
-                v[k] = load16_a4(wbase + (size_t)r * pitch + 16 * q);
+                const int r = fast_div(idx, mnc), q = idx - (int)__umul24((uint32_t)r, (uint32_t)nc);
+                v[k] = load16_a4(wbase + __umul24((uint32_t)r, pitch) + 16 * q);
             }
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
                 const int idx = b0 + lane + 64 * k;
-                const int r = fast_div(idx, mnc), q = idx - r * nc;
+                const int r = fast_div(idx, mnc), q = idx - (int)__umul24((uint32_t)r, (uint32_t)nc);
                 if (idx < nc * wh) *reinterpret_cast<uint4*>(s_win + r * P + 16 * q) = v[k];
             }
         }
@@ -336,13 +340,13 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
 #pragma unroll
         for (int k = 0; k < kStageLoads; ++k) {  // unconditional (clamped) loads: no waits between them
             const int idx = min(b0 + lane + 64 * k, nd * wh - 1);
-            const int r = fast_div(idx, mnd), q = idx - r * nd;
-            v[k] = *reinterpret_cast<const uint32_t*>(wbase + (size_t)r * pitch + 4 * q);
+            const int r = fast_div(idx, mnd), q = idx - (int)__umul24((uint32_t)r, (uint32_t)nd);
+            v[k] = *reinterpret_cast<const uint32_t*>(wbase + __umul24((uint32_t)r, pitch) + 4 * q);
         }
 #pragma unroll
         for (int k = 0; k < kStageLoads; ++k) {
             const int idx = b0 + lane + 64 * k;
-            const int r = fast_div(idx, mnd), q = idx - r * nd;
+            const int r = fast_div(idx, mnd), q = idx - (int)__umul24((uint32_t)r, (uint32_t)nd);
             if (idx < nd * wh) *reinterpret_cast<uint32_t*>(s_win + r * P + 4 * q) = v[k];
         }
     }
@@ -375,6 +379,7 @@ hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size
                              const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err,
                              hipStream_t stream) {
     const int items = g.total_cells * batch;
+    if (row0 >= (1u << 24)) return hipErrorInvalidValue;  // row offsets by 24-bit multiplies
     const size_t per_wave = ((size_t)2 * g.win_pitch * g.win_rows + 2 * ((size_t)g.det_max + 1) + 15) & ~(size_t)15;
     dim3 grid((items + kCellWaves - 1) / kCellWaves);
     const size_t lds = per_wave * kCellWaves;
