@@ -41,11 +41,6 @@ __device__ inline int wave_append(bool pred, uint16_t v, uint16_t* list, int n, 
     return n + __popcll(m);
 }
 
-// na + the number of set bits of m in lanes below this one
-__device__ __forceinline__ int append_pos(unsigned long long m, int na) {
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)na));
-}
-
 // a where this lane's bit of the mask m (scalar registers) is set, else b:
 // one v_cndmask on the mask as it is (a bool built from it would be turned
 // back into a vector value and compared again)
@@ -64,6 +59,68 @@ struct CellTiles {
     int dump;            // list index past the longest list: the compass's non-survivor lanes store there
 };
 
+// Compass pre-test, row-major over the detection region: LPR = 32 lanes
+// per row when it fits (two rows per pass), else 64 (dw <= 64: host check).
+// Two passes per iteration, evaluated together: the lane's two pixels (rows
+// r and r + 64 / LPR of one column) are the two halves of packed u16 values,
+// so every min/max/subtract below is one packed op for both (rows past the
+// region read the rest of the wave's LDS area and are masked).
+//   two adjacent compass points both darker than v - t <=> the smallest
+//   pairwise max is; both brighter than v + t <=> the largest pairwise min
+//   is; dark < v - t <=> sat(v - dark) > t, bright > v + t <=> sat(bright - v) > t
+// Returns the number of survivors, listed (tile offsets, row-major) in T.la.
+template <int P, int LPR>
+__device__ int compass_pass(const CellTiles& T, int dw, int dh, int ox, int t, int lane) {
+    constexpr int kStep = 64 / LPR;  // rows between a lane's two pixels
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    auto compass2 = [&](const uint8_t* p) -> uint32_t {
+        auto ld = [&](int o) {
+            u16x2 r;
+            r.x = p[o];
+            r.y = p[kStep * P + o];
+            return r;
+        };
+        // Every pair of adjacent compass points is one of {c0, c8} with one of
+        // {c4, c12} (a 4-cycle), so the smallest pairwise max is
+        // max(min(c0, c8), min(c4, c12)) and the largest pairwise min is
+        // min(max(c0, c8), max(c4, c12)): three ops each
+        const u16x2 v = ld(0), c0 = ld(3 * P), c4 = ld(3), c8 = ld(-3 * P), c12 = ld(-3);
+        const u16x2 dark = __builtin_elementwise_max(__builtin_elementwise_min(c0, c8), __builtin_elementwise_min(c4, c12));
+        const u16x2 bright =
+            __builtin_elementwise_min(__builtin_elementwise_max(c0, c8), __builtin_elementwise_max(c4, c12));
+        const u16x2 x = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, dark),
+                                                  __builtin_elementwise_sub_sat(bright, v));
+        const u16x2 tt = {(unsigned short)t, (unsigned short)t};
+        return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x, tt));  // a half nonzero <=> its pixel passes
+    };
+    auto below = [](unsigned long long m) {  // set bits of m in lanes below this one
+        return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    };
+    // Lane masks are formed in scalar registers: the compass results by
+    // v_cmp straight into a mask, the column and row ranges as wave-uniform
+    // masks (rows r + rsub are in range for every lane while 2+ rows remain,
+    // only the rsub = 0 half on the last row).  Every lane stores: a survivor
+    // at its compacted position, the others into the dump slot past the list.
+    const int rsub = LPR == 32 ? lane >> 5 : 0, col = lane & (LPR - 1);
+    const unsigned long long colmask = __builtin_amdgcn_uicmp((uint32_t)col, (uint32_t)dw, 36 /* ult */);
+    constexpr unsigned long long sub0 = LPR == 32 ? 0xFFFFFFFFull : ~0ull;  // lanes of row rsub = 0
+    int o = (3 + rsub) * P + 3 + ox + col;  // tile offset of the lane's first pixel
+    int na = 0;
+    for (int rr = 0; rr < dh; rr += 2 * kStep, o += 2 * kStep * P) {
+        const uint32_t y = compass2(T.win + o);
+        const int rem = dh - rr;  // rows left, >= 1
+        const unsigned long long rows0 = rem >= 2 ? ~0ull : sub0;
+        const unsigned long long rows1 = rem > kStep + 1 ? ~0ull : (rem > kStep ? sub0 : 0ull);
+        const unsigned long long m0 = __builtin_amdgcn_uicmp(y & 0xFFFFu, 0u, 33 /* ne */) & colmask & rows0;
+        const unsigned long long m1 = __builtin_amdgcn_uicmp(y, 0x10000u, 35 /* uge */) & colmask & rows1;
+        T.la[na + lane_select(m0, below(m0), T.dump - na)] = (uint16_t)o;
+        na += __popcll(m0);
+        T.la[na + lane_select(m1, below(m1), T.dump - na)] = (uint16_t)(o + kStep * P);
+        na += __popcll(m1);
+    }
+    return na;
+}
+
 // FAST at threshold t on the cell's detection region: returns the number
 // of corners, their tile offsets in lb[] (row-major) and scores in sc[].
 // Stages are separated by wave compaction so each runs on dense lanes:
@@ -71,73 +128,7 @@ struct CellTiles {
 // lane in packed 16-bit arithmetic (the corner test is s >= t + 1).
 template <int P>
 __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, int lane) {
-    // compass pre-test, row-major over the detection region: 32 lanes per
-    // row when it fits (two rows per pass), else 64 (dw <= 64: host check).
-    const int lpr = dw > 32 ? 64 : 32;
-    const int rsub = lpr == 32 ? lane >> 5 : 0, col = lane & (lpr - 1);
-    const int rstep = 64 / lpr;
-    // Two passes per iteration, evaluated together: the lane's two pixels
-    // (rows r0 and r1 of one column) are the two halves of packed u16 values,
-    // so every min/max/subtract below is one packed op for both (rows past
-    // the region read the rest of the wave's LDS area and are masked).
-    //   two adjacent compass points both darker than v - t <=> the smallest
-    //   pairwise max is; both brighter than v + t <=> the largest pairwise min
-    //   is; dark < v - t <=> sat(v - dark) > t, bright > v + t <=> sat(bright - v) > t
-    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-    auto compass2 = [&](const uint8_t* p, const uint8_t* q, int t) -> uint32_t {
-        auto ld = [&](int o) {
-            u16x2 r;
-            r.x = p[o];
-            r.y = q[o];
-            return r;
-        };
-        // (the min/max run on the bytes as f16 denormal pairs, order-preserving
-        // bit patterns: the 3-way steps are v_pk_minimum3 / maximum3_f16)
-        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-        auto h = [](u16x2 x) { return __builtin_bit_cast(h2, x); };
-        const u16x2 v = ld(0);
-        const h2 c0 = h(ld(3 * P)), c4 = h(ld(3)), c8 = h(ld(-3 * P)), c12 = h(ld(-3));
-        const u16x2 dark = __builtin_bit_cast(
-            u16x2, __builtin_elementwise_minimum(
-                       __builtin_elementwise_minimum(
-                           __builtin_elementwise_minimum(__builtin_elementwise_maximum(c0, c4),
-                                                         __builtin_elementwise_maximum(c4, c8)),
-                           __builtin_elementwise_maximum(c8, c12)),
-                       __builtin_elementwise_maximum(c12, c0)));
-        const u16x2 bright = __builtin_bit_cast(
-            u16x2, __builtin_elementwise_maximum(
-                       __builtin_elementwise_maximum(
-                           __builtin_elementwise_maximum(__builtin_elementwise_minimum(c0, c4),
-                                                         __builtin_elementwise_minimum(c4, c8)),
-                           __builtin_elementwise_minimum(c8, c12)),
-                       __builtin_elementwise_minimum(c12, c0)));
-        const u16x2 x = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, dark),
-                                                  __builtin_elementwise_sub_sat(bright, v));
-        const u16x2 tt = {(unsigned short)t, (unsigned short)t};
-        return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x, tt));  // a half nonzero <=> its pixel passes
-    };
-    // Lane masks are formed in scalar registers: the compass results by
-    // v_cmp straight into a mask, the column and row ranges as wave-uniform
-    // masks (rows rr + rsub are in range for every lane while 2+ rows remain,
-    // only the rsub = 0 half on the last row).  Every lane stores: a survivor
-    // at its compacted position, the others into the dump slot past the list.
-    const unsigned long long colmask = __builtin_amdgcn_uicmp((uint32_t)col, (uint32_t)dw, 36 /* ult */);
-    const unsigned long long sub0 = lpr == 32 ? 0xFFFFFFFFull : ~0ull;  // lanes of row rsub = 0
-    const int lane_off = (3 + rsub) * P + 3 + ox + col;
-    int na = 0;
-    for (int rr = 0; rr < dh; rr += 2 * rstep) {
-        const int off0 = lane_off + rr * P, off1 = off0 + rstep * P;
-        const uint32_t y = compass2(T.win + off0, T.win + off1, t);
-        const int rem = dh - rr;  // rows left, >= 1
-        const unsigned long long rows0 = rem >= 2 ? ~0ull : sub0;
-        const unsigned long long rows1 = rem > rstep + 1 ? ~0ull : (rem > rstep ? sub0 : 0ull);
-        const unsigned long long m0 = __builtin_amdgcn_uicmp(y & 0xFFFFu, 0u, 33 /* ne */) & colmask & rows0;
-        const unsigned long long m1 = __builtin_amdgcn_uicmp(y, 0x10000u, 35 /* uge */) & colmask & rows1;
-        T.la[lane_select(m0, append_pos(m0, na), T.dump)] = (uint16_t)off0;
-        na += __popcll(m0);
-        T.la[lane_select(m1, append_pos(m1, na), T.dump)] = (uint16_t)off1;
-        na += __popcll(m1);
-    }
+    const int na = dw > 32 ? compass_pass<P, 64>(T, dw, dh, ox, t, lane) : compass_pass<P, 32>(T, dw, dh, ox, t, lane);
     wave_sync();
     // Survivors -> corners, two per lane (list entries base + lane and
     // base + 64 + lane, one per 16-bit half).  With d = v - ring, the arc
