@@ -116,6 +116,22 @@ __device__ inline int pow2ceil(int v) {
     return p;
 }
 
+// Diagnostic build (-DOCT_STAMPS): thread 0 of frame 0's workgroups records
+// s_memtime at phase boundaries into the debug trace (ints 384.. of the
+// level's 512-int record, 64-bit stamps); tools/octree_trace.py prints them.
+#ifdef OCT_STAMPS
+#define OCT_T(k)                                                                                      \
+    do {                                                                                              \
+        if (trace && f == 0 && threadIdx.x == 0 && (k) < 64) {                                        \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();                              \
+            trace[l * 512 + 384 + 2 * (k)] = (int)(t_ & 0xFFFFFFFFu);                               \
+            trace[l * 512 + 385 + 2 * (k)] = (int)(t_ >> 32);                                        \
+        }                                                                                             \
+    } while (0)
+#else
+#define OCT_T(k) ((void)0)
+#endif
+
 template <int NT, bool LDS>
 __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int nk, int ncells, int ncap, int ncap2,
                             const uint32_t* __restrict__ cand, uint32_t* __restrict__ out,
@@ -133,24 +149,43 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
         return;
     }
 
-    // 2. roots (:545-587): keys -> root index (int)(x / hX)
+    // 2. roots (:545-587): keys -> root index (int)(x / hX).  The keys are
+    // gathered from the FAST cell slots in candidate order: first every cell
+    // writes its index over its key range (the node array as a key -> cell
+    // map), then each thread loads its keys four at a time, all four loads in
+    // flight before any is used (measured: the per-key binary search over
+    // the cell offsets and one dependent load per key made this phase a
+    // quarter of the workgroup's time).
     for (int i = tid; i < nini; i += NT) s_aux0[i] = 0;
-    __syncthreads();
-    const uint32_t* cbase = cand + (size_t)f * g.cand_frame + L.cand_offset;
-    for (int k = tid; k < nk; k += NT) {
-        int lo = 0, hi = ncells - 1;  // last cell with cellofs <= k
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_cellofs[mid] <= k) lo = mid; else hi = mid - 1;
-        }
-        const uint32_t key = cbase[(size_t)lo * L.cell_cap + (k - s_cellofs[lo])];
-        ks.set_key(k, key);
-        int r = (int)__fdiv_rn((float)key_x(key), L.hx);
-        r = min(r, nini - 1);
-        ks.set_node(k, r);
-        atomicAdd(&s_aux0[r], 1);
+    for (int c = tid; c < ncells; c += NT) {
+        const int b = s_cellofs[c], e = s_cellofs[c + 1];
+        for (int k = b; k < e; ++k) ks.set_node(k, c);
     }
     __syncthreads();
+    const uint32_t* cbase = cand + (size_t)f * g.cand_frame + L.cand_offset;
+    constexpr int kGather = 4;
+    for (int k0 = tid; k0 < nk; k0 += kGather * NT) {
+        uint32_t key[kGather];
+#pragma unroll
+        for (int u = 0; u < kGather; ++u) {
+            const int k = min(k0 + u * NT, nk - 1);
+            const int c = ks.node(k);
+            key[u] = cbase[(size_t)c * L.cell_cap + (k - s_cellofs[c])];
+        }
+#pragma unroll
+        for (int u = 0; u < kGather; ++u) {
+            const int k = k0 + u * NT;
+            if (k < nk) {
+                ks.set_key(k, key[u]);
+                int r = (int)__fdiv_rn((float)key_x(key[u]), L.hx);
+                r = min(r, nini - 1);
+                ks.set_node(k, r);
+                atomicAdd(&s_aux0[r], 1);
+            }
+        }
+    }
+    __syncthreads();
+    OCT_T(1);
     // non-empty roots keep their order; empty ones are erased.  Computed by
     // thread r (no single-lane loop: see tools/check_scc.py for the ROCm 7.2
     // miscompile a uniform-address select in such a loop triggered).
@@ -175,6 +210,7 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
     for (int k = tid; k < nk; k += NT) ks.set_node(k, s_aux1[ks.node(k)]);
     __syncthreads();
 
+    OCT_T(2);
     // 3. passes.  The pass state (list size, buffer, phase, next seq) is kept
     // in registers: every thread derives it from the same block-scan totals.
     int nL = nroots, cur = 0, nseq = nini;
@@ -182,8 +218,12 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
     for (int guard = 0; guard < 4096; ++guard) {
         ONode* old = cur ? s_node1 : s_node0;
         ONode* nw = cur ? s_node0 : s_node1;
-        // quadrant histogram of every node with > 1 key
+        // quadrant histogram of every node with > 1 key; the counter of
+        // children with > 1 key alternates between two slots, so this pass
+        // resets its own while the previous pass's may still be read
+        int* s_nexp = s_misc + 25 + (guard & 1);
         for (int i = tid; i < nL * 4; i += NT) s_qc[i] = 0;
+        if (tid == 0) *s_nexp = 0;
         __syncthreads();
         for (int k = tid; k < nk; k += NT) {
             const int i = ks.node(k);
@@ -191,44 +231,74 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
             if (nd.cnt > 1) atomicAdd(&s_qc[i * 4 + node_quad(nd, ks.key(k))], 1u);
         }
         __syncthreads();
+        OCT_T(3 + 4 * guard);
         // processing order and push bases
-        int C;  // children pushed this pass
+        int C, S;  // children pushed this pass, surviving nodes
         if (!inner) {
+            // one scan of (children << 16 | survives): push bases and survivor
+            // positions together (C <= 4 nL and S <= nL stay below 2^16)
             for (int i = tid; i < nL; i += NT) {
                 const bool div = old[i].cnt > 1;
                 int nch = 0;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) nch += s_qc[i * 4 + q] > 0;
-                s_aux0[i] = div ? nch : 0;
+                s_aux0[i] = div ? nch << 16 : 1;
                 s_flag[i] = div;
             }
             __syncthreads();
-            C = block_scan<NT>(s_aux0, nL, s_tmp);  // aux0 = push base (list order)
+            const int tot = block_scan<NT>(s_aux0, nL, s_tmp);
+            C = tot >> 16;
+            S = tot & 0xFFFF;
         } else {
             // compact the nodes with > 1 key, sort descending by (cnt, seq)
             for (int i = tid; i < nL; i += NT) s_aux1[i] = old[i].cnt > 1;
             __syncthreads();
             const int m = block_scan<NT>(s_aux1, nL, s_tmp);
             const int P = pow2ceil(max(m, 1));
-            for (int i = tid; i < P; i += NT) s_sortk[i] = 0ull;
-            __syncthreads();
+            constexpr int kRankPer = 2;  // up to 2 keys per thread: rank sort, else bitonic
+            const bool by_rank = m <= kRankPer * NT;
             for (int i = tid; i < nL; i += NT)
                 if (old[i].cnt > 1)
                     s_sortk[s_aux1[i]] = ((unsigned long long)min(old[i].cnt, 0xFFFFFFu) << 40) |
                                          ((unsigned long long)(old[i].seq & 0xFFFFFFFu) << 12) | (unsigned)i;
+            if (!by_rank)
+                for (int i = m + tid; i < P; i += NT) s_sortk[i] = 0ull;
             __syncthreads();
-            for (int k = 2; k <= P; k <<= 1)
-                for (int j = k >> 1; j > 0; j >>= 1) {
-                    for (int i = tid; i < P; i += NT) {
-                        const int ixj = i ^ j;
-                        if (ixj > i) {
-                            const unsigned long long a = s_sortk[i], b = s_sortk[ixj];
-                            const bool desc = (i & k) == 0;
-                            if (desc ? (a < b) : (a > b)) { s_sortk[i] = b; s_sortk[ixj] = a; }
-                        }
-                    }
-                    __syncthreads();
+            if (by_rank) {
+                // descending order by rank = the number of larger keys (the keys
+                // are distinct: they end in the node index); every thread reads
+                // the same key per step (LDS broadcast), no barrier per step
+                unsigned long long mine[kRankPer];
+                int rank[kRankPer];
+#pragma unroll
+                for (int u = 0; u < kRankPer; ++u) {
+                    mine[u] = s_sortk[min(tid + u * NT, max(m - 1, 0))];
+                    rank[u] = 0;
                 }
+                for (int j = 0; j < m; ++j) {
+                    const unsigned long long kj = s_sortk[j];
+#pragma unroll
+                    for (int u = 0; u < kRankPer; ++u) rank[u] += kj > mine[u];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < kRankPer; ++u)
+                    if (tid + u * NT < m) s_sortk[rank[u]] = mine[u];
+                __syncthreads();
+            } else {
+                for (int k = 2; k <= P; k <<= 1)
+                    for (int j = k >> 1; j > 0; j >>= 1) {
+                        for (int i = tid; i < P; i += NT) {
+                            const int ixj = i ^ j;
+                            if (ixj > i) {
+                                const unsigned long long a = s_sortk[i], b = s_sortk[ixj];
+                                const bool desc = (i & k) == 0;
+                                if (desc ? (a < b) : (a > b)) { s_sortk[i] = b; s_sortk[ixj] = a; }
+                            }
+                        }
+                        __syncthreads();
+                    }
+            }
             // rank r -> (nch - 1); inclusive scan; first r reaching N
             for (int r = tid; r < m; r += NT) {
                 const int i = (int)(s_sortk[r] & 0xFFF);
@@ -267,21 +337,22 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
             }
             __syncthreads();
         }
-        // survivors keep their order after the C pushed children
-        for (int i = tid; i < nL; i += NT) s_aux1[i] = s_flag[i] ? 0 : 1;
-        __syncthreads();
-        const int S = block_scan<NT>(s_aux1, nL, s_tmp);
+        OCT_T(4 + 4 * guard);
+        if (inner) {  // survivors keep their order after the C pushed children
+            for (int i = tid; i < nL; i += NT) s_aux1[i] = s_flag[i] ? 0 : 1;
+            __syncthreads();
+            S = block_scan<NT>(s_aux1, nL, s_tmp);
+        }
         const int nNew = C + S;
         if (nNew > ncap || nseq + C > 0x0FFFFFFF) {
             if (tid == 0) { atomicOr(err, nNew > ncap ? kErrNodeCap : kErrSeqCap); oct_count[f * g.nlevels + l] = 0; }
             return;
         }
-        if (tid == 0) s_misc[25] = 0;
-        __syncthreads();
         for (int i = tid; i < nL; i += NT) {
             const ONode nd = old[i];
+            const int pk = s_aux0[i];  // main pass: packed prefix; inner pass: push base
             if (s_flag[i]) {
-                int p = s_aux0[i];
+                int p = inner ? pk : pk >> 16;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const uint32_t c = s_qc[i * 4 + q];
@@ -292,34 +363,37 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
                         ch.seq = (uint32_t)(nseq + p);
                         nw[pos] = ch;
                         s_qc[i * 4 + q] = (uint32_t)pos;
-                        if (c > 1) atomicAdd(&s_misc[25], 1);
+                        if (c > 1) atomicAdd(s_nexp, 1);
                         ++p;
                     }
                 }
             } else {
-                const int pos = C + s_aux1[i];
+                const int pos = C + (inner ? s_aux1[i] : (pk & 0xFFFF));
                 nw[pos] = nd;
                 s_aux1[i] = pos;
             }
         }
         __syncthreads();
+        OCT_T(5 + 4 * guard);
         for (int k = tid; k < nk; k += NT) {
             const int i = ks.node(k);
             ks.set_node(k, s_flag[i] ? (int)s_qc[i * 4 + node_quad(old[i], ks.key(k))] : s_aux1[i]);
         }
         __syncthreads();
-        if (tid == 0 && trace && f == 0 && guard < 60) {
+        OCT_T(6 + 4 * guard);
+        if (tid == 0 && trace && f == 0 && guard < 47) {  // below the stamp region (ints 384..)
             int* t = trace + l * 512 + 2 + guard * 8;
-            t[0] = inner; t[1] = nL; t[2] = C; t[3] = S; t[4] = s_misc[25]; t[5] = s_misc[24]; t[6] = nk; t[7] = N;
+            t[0] = inner; t[1] = nL; t[2] = C; t[3] = S; t[4] = *s_nexp; t[5] = s_misc[24]; t[6] = nk; t[7] = N;
             trace[l * 512] = guard + 1;
         }
-        const int nexp = s_misc[25];  // children with > 1 key (nToExpand)
+        const int nexp = *s_nexp;  // children with > 1 key (nToExpand)
         const bool done = nNew >= N || nNew == nL;  // :673 / :740
         if (!inner && nNew + nexp * 3 > N) inner = true;  // :678
         nseq += C;
         cur ^= 1;
         nL = nNew;
-        __syncthreads();  // s_misc[25] is reset by the next pass
+        // no barrier here: the next pass first writes s_qc (last read by the
+        // remap above, before its barrier) and the other nexp slot
         if (done) break;
     }
 
@@ -335,6 +409,7 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
     }
     for (int i = tid; i < nL; i += NT) out[i] = ks.key((int)(0xFFFFFFu - (s_qc[i] & 0xFFFFFFu)));
     if (tid == 0) oct_count[f * g.nlevels + l] = nL;
+    OCT_T(63);
 }
 
 template <int NT>
@@ -359,6 +434,7 @@ __global__ __launch_bounds__(NT) void octree_kernel(Geom g, const uint32_t* __re
     const LevelGeom& L = g.lv[l];
     const int ncells = L.ncols * L.nrows;
     const int ncap2 = pow2ceil(ncap);
+    OCT_T(0);
 
     // LDS carve (byte offsets must match octree_lds_bytes)
     const size_t o_sortk = 128;
