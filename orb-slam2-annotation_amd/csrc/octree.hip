@@ -152,18 +152,20 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
     // 2. roots (:545-587): keys -> root index (int)(x / hX).  The keys are
     // gathered from the FAST cell slots in candidate order: first every cell
     // writes its index over its key range (the node array as a key -> cell
-    // map), then each thread loads its keys four at a time, all four loads in
+    // map), then each thread loads its keys eight at a time, all eight loads in
     // flight before any is used (measured: the per-key binary search over
     // the cell offsets and one dependent load per key made this phase a
     // quarter of the workgroup's time).
     for (int i = tid; i < nini; i += NT) s_aux0[i] = 0;
+    OCT_T(60);
     for (int c = tid; c < ncells; c += NT) {
         const int b = s_cellofs[c], e = s_cellofs[c + 1];
         for (int k = b; k < e; ++k) ks.set_node(k, c);
     }
     __syncthreads();
+    OCT_T(61);
     const uint32_t* cbase = cand + (size_t)f * g.cand_frame + L.cand_offset;
-    constexpr int kGather = 4;
+    constexpr int kGather = 8;
     for (int k0 = tid; k0 < nk; k0 += kGather * NT) {
         uint32_t key[kGather];
 #pragma unroll

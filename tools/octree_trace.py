@@ -29,7 +29,8 @@ for l, rows in enumerate(ex.octree_trace()):
     print(f"level {l}: {len(rows)} passes (inner, nL, C, S, nexp, kstop, nk, N)")
     for r in rows:
         print("   ", [int(v) for v in r])
-    # phase stamps (OCT_STAMPS build): 0 start, 1 keys, 2 roots, 3+4p hist, 4+4p order, 5+4p nodes, 6+4p remap, 63 end
+    # phase stamps (OCT_STAMPS build): 0 start, 60 cell offsets, 61 key->cell map, 1 keys, 2 roots,
+    # 3+4p hist, 4+4p order, 5+4p nodes, 6+4p remap, 63 end
     st = raw[l * 512 + 384: l * 512 + 512].view(np.uint32).astype(np.uint64)
     t = st[0::2] | (st[1::2] << np.uint64(32))
     if t[0]:
