@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 
 #include "../../include/orbgpu.h"
@@ -303,18 +304,39 @@ size_t stereo_lds_bytes(int cap, int H) {
            (kStWaves + 4) * 4;
 }
 
+// blocks per pair at most (ORBGPU_STEREO_SPLIT_MAX overrides): a single pair
+// (the stereo Frame's call) is dealt to this many blocks, whose waves then
+// take about 1200 / (16 S) left keypoints each
+int stereo_split_max() {
+    static const int v = [] {
+        const char* s = std::getenv("ORBGPU_STEREO_SPLIT_MAX");
+        const int x = s ? std::atoi(s) : 32;
+        return std::max(1, std::min(x, 256));
+    }();
+    return v;
+}
+
 hipError_t launch_stereo(const StereoArgs& a, int npairs, hipStream_t stream) {
     if (npairs <= 0) return hipSuccess;
     const size_t lds = stereo_lds_bytes(a.cap, a.lvl_h[0]);
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stereo_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
+    // per-process state (the drop-in calls this per frame): the kernel's LDS
+    // attribute only grows, the CU count is read once
+    static thread_local size_t lds_set = 0;
+    if (lds > lds_set) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stereo_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        lds_set = lds;
+    }
+    static const int ncu = [] {
+        int dev = 0, n = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return n;
+    }();
     // blocks per pair: at least two 1024-thread blocks per CU over the launch
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const int S = std::min(8, std::max(1, (2 * ncu + npairs - 1) / npairs));
+    const int S = std::min(stereo_split_max(), std::max(1, (2 * ncu + npairs - 1) / npairs));
     hipLaunchKernelGGL(stereo_kernel, dim3(npairs * S), dim3(kStThreads), lds, stream, a, S);
-    e = hipGetLastError();
+    const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(stereo_median_kernel, dim3(npairs), dim3(kMedThreads), 0, stream, a);
     return hipGetLastError();
