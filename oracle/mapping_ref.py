@@ -27,8 +27,12 @@ def _rowdot_t(T, r, x):
     return F(D(T[r, 0]) * D(x[0]) + D(T[r, 1]) * D(x[1]) + D(T[r, 2]) * D(x[2]) + D(T[r, 3]))
 
 
-def _norm(v):
-    return F(math.sqrt(D(v[0]) * D(v[0]) + D(v[1]) * D(v[1]) + D(v[2]) * D(v[2])))
+def _norm_d(v):  # cv::norm: double
+    return math.sqrt(D(v[0]) * D(v[0]) + D(v[1]) * D(v[1]) + D(v[2]) * D(v[2]))
+
+
+def _norm(v):  # float dist = cv::norm(...)
+    return F(_norm_d(v))
 
 
 def _unproject(K, i):
@@ -70,7 +74,7 @@ def triangulate_matches(kf1, kf2, pairs, scale_factor):
         xn2 = [F(F(F(kp2["x"]) - F(B["cx"])) * F(B["invfx"])), F(F(F(kp2["y"]) - F(B["cy"])) * F(B["invfy"])), F(1)]
         r1, r2 = _rwc(A["Tcw"], xn1), _rwc(B["Tcw"], xn2)
         dot = D(r1[0]) * D(r2[0]) + D(r1[1]) * D(r2[1]) + D(r1[2]) * D(r2[2])
-        cos_rays = F(dot / D(F(_norm(r1) * _norm(r2))))
+        cos_rays = F(dot / (_norm_d(r1) * _norm_d(r2)))  # LocalMapping.cpp:410, all double
         cs = F(cos_rays + F(1))
         cs1 = cs2 = cs
         if st1:

@@ -37,9 +37,12 @@ __device__ inline void rwc_mul(const float* T, const float* v, float* out) {
         out[j] = (float)((double)T[j] * v[0] + (double)T[4 + j] * v[1] + (double)T[8 + j] * v[2]);
 }
 
-__device__ inline float norm3f(const float* v) {
-    return (float)sqrt((double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2]);
+// cv::norm of a 3x1 CV_32F Mat: the double square root of the double sum
+__device__ inline double norm3d(const float* v) {
+    return sqrt((double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2]);
 }
+// ... assigned to a float (float dist = cv::norm(...))
+__device__ inline float norm3f(const float* v) { return (float)norm3d(v); }
 
 // KeyFrame::UnprojectStereo (KeyFrame.cpp:747-775): Twc * (x, y, z) of the raw keypoint
 __device__ inline bool unproject_stereo(const orbgpu_mapping_kf& K, int i, float* X) {
@@ -88,7 +91,9 @@ __global__ __launch_bounds__(kMapThreads) void triangulate_kernel(const orbgpu_m
     rwc_mul(A.Tcw, xn1, ray1);
     rwc_mul(B.Tcw, xn2, ray2);
     const double dot = (double)ray1[0] * ray2[0] + (double)ray1[1] * ray2[1] + (double)ray1[2] * ray2[2];
-    const float cosRays = (float)(dot / (double)(norm3f(ray1) * norm3f(ray2)));
+    // ray1.dot(ray2) / (cv::norm(ray1) * cv::norm(ray2)): dot, norms and their
+    // product in double, the quotient assigned to the float (LocalMapping.cpp:410)
+    const float cosRays = (float)(dot / (norm3d(ray1) * norm3d(ray2)));
     float cosStereo = cosRays + 1;
     float cosStereo1 = cosStereo, cosStereo2 = cosStereo;
     if (st1) cosStereo1 = cosf(2 * atan2f(A.b / 2, A.depth[idx1]));
