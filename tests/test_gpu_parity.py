@@ -104,6 +104,21 @@ def test_extract_stereo_geometries(w, h, nf):
         _assert_same_kps(kg, dg, kr, dr)
 
 
+@pytest.mark.parametrize("w,h,nf", [(1241, 376, 4000), (640, 480, 2500)])
+def test_extract_many_features(w, h, nf):
+    """Large feature budgets (the KITTI initialisation extractor uses 2 x
+    nFeatures, Tracking.cpp:149): the octree's inner pass orders several
+    hundred level-0 nodes (rank sort up to 512, bitonic above) and the
+    level-0 candidate lists approach the in-LDS key capacity."""
+    og = _gpu()
+    ex = og.Extractor(nfeatures=nf, width=w, height=h)
+    ref = orbref.Extractor(nfeatures=nf)
+    for img in synth.mono_stream(2, w, h, seed=0x0B5E + nf):
+        kg, dg = ex.extract(img)
+        kr, dr = ref.extract(img)
+        _assert_same_kps(kg, dg, kr, dr)
+
+
 @pytest.mark.parametrize("w,h,nf", [(640, 480, 1000), (1241, 376, 2000), (752, 480, 1200)])
 def test_pyramid_paths_agree(w, h, nf):
     """The two device pyramid passes: batches up to 8 frames take the banded
