@@ -7,13 +7,13 @@
 //                        order-preserving compaction (ballot prefix sums),
 //                        camera-frame points Rcw*Xw + tcw with
 //                        double-accumulated products, truncated error bounds.
-//   compute_sim3_kernel  one 256-thread block per query.  Lane 0 lays out
+//   compute_sim3_kernel  one 512-thread block per query.  Lane 0 lays out
 //                        the reference's hypothesis order -- rounds of
 //                        iterate(5) over the live candidates, 3 RandomInt
 //                        swap-remove draws per hypothesis from the query's
 //                        glibc stream -- for a window of 256 hypotheses; every
 //                        thread solves one of them (Horn, sim3_device.h), the
-//                        4 waves score them (lanes over correspondences,
+//                        8 waves score them (lanes over correspondences,
 //                        ballot + popcount), and lane 0 replays the acceptance
 //                        in stream order (best on >=, return on > minInliers).
 //                        The first return ends the query; hypotheses past it
@@ -29,7 +29,11 @@ namespace {
 
 using namespace sim3dev;
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 256;       // sim3_setup_kernel
+#ifndef ORBGPU_SIM3_THREADS
+#define ORBGPU_SIM3_THREADS 512
+#endif
+constexpr int kQThreads = ORBGPU_SIM3_THREADS;  // compute_sim3_kernel: 8 scoring waves, 2 per SIMD
 constexpr int kWin = 256;  // hypotheses solved and scored per window
 constexpr int kMaxC = ORBGPU_LOOP_MAX_CANDIDATES;
 
@@ -117,8 +121,9 @@ __global__ __launch_bounds__(kThreads) void sim3_setup_kernel(const orbgpu_sim3_
     if (tid == 0) n_corr[c] = base;
 }
 
-// glibc random_r TYPE_3 step (csrc/ransac.cpp restates the same generator)
-__device__ inline int32_t rand_next(int32_t* r, int& f, int& b) {
+// glibc random_r TYPE_3 step (csrc/ransac.cpp restates the same generator):
+// returns the raw sum written into the state; rand() is raw >> 1
+__device__ inline uint32_t rand_next_raw(int32_t* r, int& f, int& b) {
     const uint32_t val = (uint32_t)r[f] + (uint32_t)r[b];
     r[f] = (int32_t)val;
     if (++f >= 31) {
@@ -127,7 +132,7 @@ __device__ inline int32_t rand_next(int32_t* r, int& f, int& b) {
     } else if (++b >= 31) {
         b = 0;
     }
-    return (int32_t)(val >> 1);
+    return val;
 }
 
 // DUtils::Random::RandomInt(0, d-1)
@@ -135,7 +140,7 @@ __device__ inline int random_below(int32_t v, int d) {
     return (int)(((double)v / ((double)2147483647 + 1.0)) * d);
 }
 
-__global__ __launch_bounds__(kThreads) void compute_sim3_kernel(
+__global__ __launch_bounds__(kQThreads) void compute_sim3_kernel(
     const orbgpu_compute_sim3_query* __restrict__ queries, const orbgpu_sim3_candidate* __restrict__ cands,
     const orbgpu_loop_keyframe* __restrict__ kfs, int stride, Workspace ws, const int* __restrict__ n_corr,
     orbgpu_sim3_ransac_params prm, orbgpu_compute_sim3_result* __restrict__ results,
@@ -146,6 +151,10 @@ __global__ __launch_bounds__(kThreads) void compute_sim3_kernel(
     __shared__ int c_n[kMaxC], c_max[kMaxC], c_its[kMaxC], c_best[kMaxC], c_sched[kMaxC];
     __shared__ unsigned char c_live[kMaxC];  // still scheduled (not discarded)
     __shared__ int32_t s_r[31];
+    // the stream at the current window's start and the raw values its layout
+    // drew: the state after exactly the consumed draws is rebuilt from these
+    // (the last 31 raw values are the generator's whole state)
+    __shared__ int32_t s_snap[31], s_gen[3 * kWin];
     __shared__ int s_nslots, s_done, s_matched, s_round, s_total;
     const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const orbgpu_compute_sim3_query Q = queries[q];
@@ -184,6 +193,7 @@ __global__ __launch_bounds__(kThreads) void compute_sim3_kernel(
     }
     __syncthreads();
     int rf = Q.rng.f, rb = Q.rng.b;        // lane 0's stream indices
+    int snap_f = rf, snap_b = rb, snap_total = 0;  // lane 0: the current window's start
     int cur_round = 0, cur_c = 0, cur_j = 0;  // lane 0's schedule cursor
     bool sched_end = false;
     // windows grow 32, 64, .., kWin: most queries return within a few
@@ -191,6 +201,10 @@ __global__ __launch_bounds__(kThreads) void compute_sim3_kernel(
     int win = 32;
     while (true) {
         if (tid == 0) {  // lay out the next window in the reference's order
+            for (int k = 0; k < 31; ++k) s_snap[k] = s_r[k];
+            snap_f = rf;
+            snap_b = rb;
+            snap_total = s_total;
             int n = 0;
             while (n < win && !sched_end) {
                 if (cur_c == nc) {  // next round of `while (nCandidates > 0 && !bMatch)`
@@ -215,7 +229,9 @@ __global__ __launch_bounds__(kThreads) void compute_sim3_kernel(
                     int pos[2], val[2], nmod = 0;
                     for (int d = 0; d < 3; ++d) {
                         const int size = N - d;
-                        const int r = random_below(rand_next(s_r, rf, rb), size);
+                        const uint32_t raw = rand_next_raw(s_r, rf, rb);
+                        s_gen[3 * n + d] = (int32_t)raw;
+                        const int r = random_below((int32_t)(raw >> 1), size);
                         int idx = r;  // vAvailableIndices[r] after the earlier swaps
                         for (int m = nmod - 1; m >= 0; --m)
                             if (pos[m] == r) {
@@ -262,7 +278,7 @@ __global__ __launch_bounds__(kThreads) void compute_sim3_kernel(
             compute_sim3(A, B, prm.fix_scale != 0, s_hyp[tid]);
         }
         __syncthreads();
-        for (int h = wave; h < ns; h += kThreads / 64) {  // CheckInliers
+        for (int h = wave; h < ns; h += kQThreads / 64) {  // CheckInliers
             const int c = s_slot_c[h];
             const orbgpu_sim3_candidate cd = cands[c0 + c];
             const float* K1 = kfs[cd.kf1].K;
@@ -315,7 +331,7 @@ __global__ __launch_bounds__(kThreads) void compute_sim3_kernel(
         const float* K1 = kfs[cd.kf1].K;
         const float* K2 = kfs[cd.kf2].K;
         const size_t o = (size_t)(c0 + mc) * stride;
-        for (int i = tid; i < c_n[mc]; i += kThreads)
+        for (int i = tid; i < c_n[mc]; i += kQThreads)
             inliers[o + i] = is_inlier(s_best[mc], K1, K2, ws.X1 + 3 * (o + i), ws.X2 + 3 * (o + i), ws.e1[o + i],
                                        ws.e2[o + i]) ? 1 : 0;
     }
@@ -353,14 +369,14 @@ __global__ __launch_bounds__(kThreads) void compute_sim3_kernel(
             for (int k = 0; k < 3; ++k) R.t12[k] = 0.f;
             R.s12 = 0.f;
         }
-        // the stream after exactly the consumed draws
-        int32_t r[31];
-        for (int k = 0; k < 31; ++k) r[k] = Q.rng.r[k];
-        int f = Q.rng.f, b = Q.rng.b;
-        for (int k = 0; k < 3 * s_total; ++k) (void)rand_next(r, f, b);
-        for (int k = 0; k < 31; ++k) R.rng_after.r[k] = r[k];
-        R.rng_after.f = f;
-        R.rng_after.b = b;
+        // the stream after exactly the consumed draws: the last window's start
+        // state with its first K raw values written at slots snap_f, snap_f+1, ..
+        // (mod 31), and both indices advanced by K
+        const int K = 3 * (s_total - snap_total);
+        for (int k = 0; k < 31; ++k) R.rng_after.r[k] = s_snap[k];
+        for (int j = max(0, K - 31); j < K; ++j) R.rng_after.r[(snap_f + j) % 31] = s_gen[j];
+        R.rng_after.f = (snap_f + K) % 31;
+        R.rng_after.b = (snap_b + K) % 31;
     }
 }
 
@@ -412,7 +428,7 @@ int orbgpu_compute_sim3_batch_device(int n_queries, const orbgpu_compute_sim3_qu
     if (n_queries == 0) return ORBGPU_OK;
     if (int rc = check_device()) return rc;
     (void)hipGetLastError();
-    hipLaunchKernelGGL(compute_sim3_kernel, dim3(n_queries), dim3(kThreads), 0, (hipStream_t)stream, d_queries,
+    hipLaunchKernelGGL(compute_sim3_kernel, dim3(n_queries), dim3(kQThreads), 0, (hipStream_t)stream, d_queries,
                        d_cands, d_kfs, match_stride, carve(const_cast<void*>(d_workspace), n_cand, match_stride), d_n_corr,
                        params, d_results, d_cand_states, d_inliers);
     ORB_HIP(hipGetLastError());
