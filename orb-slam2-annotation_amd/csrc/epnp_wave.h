@@ -31,6 +31,7 @@
 #include "epnp.h"
 #include "group_sum.h"
 #include "jacobi_group.h"
+#include "jacobi_lds.h"
 
 namespace orbgpu {
 namespace epnp {
@@ -123,11 +124,13 @@ __device__ inline void canonicalize_null_space4(double* ut4, int k, double* scr)
         for (int r = 0; r < 12; ++r) ut4[12 * c + r] = B[4 * r + c];
 }
 
-// r = the lane's index in its group; lds = the group's kWaveScratch doubles.
-// Every lane of the group returns the same pose and error.
+// r = the lane's index in its group; lds = the group's kWaveScratch doubles;
+// jac (G = 64 only, optional): JacobiLds<12, 12>::kDoubles of LDS for the
+// wave-parallel 12 x 12 decomposition.  Every lane of the group returns the
+// same pose and error.
 template <int G, class Src>
 __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& out, int r, double* lds,
-                                     unsigned long long* stamps = nullptr) {
+                                     unsigned long long* stamps = nullptr, double* jac = nullptr) {
     const int n = src.count();
     EPNP_T(0);
     double* s_mtm = lds;        // 12 x 12
@@ -347,15 +350,43 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
     }
     EPNP_GROUP_SYNC();
     EPNP_T(3);
-    // eigenvectors of M^T M: one-sided Jacobi on the symmetric PSD matrix, rows on lanes
-    {
+    // eigenvectors of M^T M: one-sided Jacobi on the symmetric PSD matrix
+    if (G == 64 && jac != nullptr) {
+        // a whole wave on one matrix (Refine): the six disjoint pairs of a
+        // round on six 8-lane groups, A and V in LDS (jacobi_lds.h)
+        using J = JacobiLds<12, 12>;
+        double* A = jac;
+        double* V = jac + J::M * J::NRP;
+        double* nrm = V + J::M * J::NVP;
+        J::init(A, V, r, [&](int rr, int c) { return s_mtm[rr * 12 + c]; });
+        const int sweeps = J::run(A, V, nrm, r);
+#ifdef EPNP_STAMPS
+        if (stamps && r == 0) stamps[16] = (unsigned long long)sweeps;
+#else
+        (void)sweeps;
+#endif
+        double lam[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) lam[j] = sqrt(nrm[j]);
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            int rank = 0;
+#pragma unroll
+            for (int i = 0; i < 12; ++i) rank += (lam[i] > lam[j]) || (i < j && lam[i] == lam[j]);
+            if (rank >= 8 && r < 12) s_ut4[12 * (11 - rank) + r] = V[j * J::NVP + r];
+        }
+    } else {  // rows on lanes (jacobi_group.h)
         double a[12], v[12];
 #pragma unroll
         for (int c = 0; c < 12; ++c) {
             a[c] = r < 12 ? s_mtm[r * 12 + c] : 0.0;
             v[c] = (r == c) ? 1.0 : 0.0;
         }
-        const int sweeps = hestenes_group<12, G>(a, v);
+        // the rows sit on lanes 0..11 and every other lane holds zeros, so
+        // the 16-lane row sum IS the group sum (the cross-row terms add +0):
+        // a wave-wide group (Refine, G = 64) runs its sweeps on DPP row sums
+        // alone instead of two ds_bpermute round trips per reduction
+        const int sweeps = hestenes_group<12, (G > 16 ? 16 : G)>(a, v);
 #ifdef EPNP_STAMPS
         if (stamps && r == 0) stamps[16] = (unsigned long long)sweeps;
 #else

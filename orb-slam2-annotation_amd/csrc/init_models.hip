@@ -7,24 +7,25 @@
 //                          sequential float sums (mean, then mean absolute
 //                          deviation), the block writes the normalised points;
 //                          also the match list (u1, v1, u2, v2) the scorers read.
-//   init_models_kernel     16 lanes per (iteration, model), four hypotheses
-//                          per wave: lane r builds row r of the DLT matrix A in
-//                          float as ComputeH21 (:292-330, 16 x 9) /
-//                          ComputeF21 (:332-388, 8 x 9 + zero rows) build it;
-//                          its right singular vector of the smallest singular
-//                          value (cv::SVDecomp's vt.row(8)) by one-sided
-//                          (Hestenes) Jacobi in double with the rows on the
-//                          lanes (jacobi_group.h: round-robin pair order,
-//                          16-lane DPP reductions, lane r < 9 carries row r of
-//                          V, numerically null columns take no rotation --
-//                          the 8 x 9 F system always has one); then the group's
-//                          lane 0 does, for F, the rank-2 projection
+//   init_models_kernel     one wave per (iteration, model): lanes 0..15 build
+//                          the rows of the DLT matrix A in float as ComputeH21
+//                          (:292-330, 16 x 9) / ComputeF21 (:332-388, 8 x 9 +
+//                          zero rows) build it, in LDS; its right singular
+//                          vector of the smallest singular value
+//                          (cv::SVDecomp's vt.row(8)) by one-sided (Hestenes)
+//                          Jacobi in double with the five disjoint column
+//                          pairs of each round-robin round on five 8-lane
+//                          groups (jacobi_lds.h; numerically null columns take
+//                          no rotation -- the 8 x 9 F system always has one);
+//                          then lane 0 does, for F, the rank-2 projection
 //                          (w(2) = 0), the de-normalisation T2inv*Hn*T1 /
 //                          T2t*Fn*T1 and H12 = H21.inv() with OpenCV's float
 //                          3x3 products (double accumulation) and 3x3
 //                          closed-form inverse.  (Round 2 ran one thread per
 //                          hypothesis with the 16 x 9 and 9 x 9 doubles in
-//                          scratch: 5.1 ms per 200 + 200 hypotheses.)
+//                          scratch: 5.1 ms per 200 + 200 hypotheses; round 3
+//                          first ran 16 lanes per model with the rows on the
+//                          lanes, jacobi_group.h: 92 us.)
 // The SVDs are restated (OpenCV's Jacobi SVD in float is not reproducible
 // here), so H/F match the oracle to a tolerance; CheckHomography /
 // CheckFundamental (init.hip) then score them bit-exactly.
@@ -34,6 +35,7 @@
 #include "epnp.h"
 #include "group_sum.h"
 #include "jacobi_group.h"
+#include "jacobi_lds.h"
 #include "host_common.h"
 
 namespace {
@@ -157,34 +159,36 @@ __device__ void inv3(const float* m, float* o) {
     o[8] = (float)((S(0, 0) * S(1, 1) - S(0, 1) * S(1, 0)) * d);
 }
 
-constexpr int kModelThreads = 64;  // one wave = four hypotheses of 16 lanes
-constexpr int kGroups = kModelThreads / 16;
+constexpr int kModelThreads = 64;  // one wave per hypothesis
 
-__device__ __forceinline__ double group_sum(double x) {  // over the lane's 16-lane group (DPP)
-    return orbgpu::row16_sum(x);
-}
+using ModelJacobi = orbgpu::JacobiLds<9, 16>;  // 9 columns, up to 16 rows (H: 16, F: 8 + zero rows)
 
 __global__ __launch_bounds__(kModelThreads) void init_models_kernel(const float* __restrict__ work, int n1, int n2,
                                                                     const int* __restrict__ pairs,
                                                                     const int* __restrict__ sets, int n_iter,
                                                                     float* __restrict__ h21, float* __restrict__ h12,
                                                                     float* __restrict__ f21) {
-    __shared__ double s_null[kGroups][9];
-    const int lane = threadIdx.x, g = lane >> 4, r = lane & 15;
-    const int t_raw = blockIdx.x * kGroups + g;
-    const bool valid = t_raw < 2 * n_iter;
-    const int t = valid ? t_raw : 2 * n_iter - 1;  // idle groups mirror a real one and store nothing
+    __shared__ double s_jac[ModelJacobi::kDoubles];
+    const int lane = threadIdx.x;
+    const int t = blockIdx.x;  // grid = 2 n_iter: H of every iteration, then F
+    const bool valid = t < 2 * n_iter;
     const bool homography = t < n_iter;
     const int it = homography ? t : t - n_iter;
     const float* pn1 = work;
     const float* pn2 = work + 2 * n1;
     const float* T1 = work + 2 * (n1 + n2);
     const float* T2 = T1 + 9;
-    // row r of A (float entries as the reference computes them, held in double)
-    double a[9];
+    double* A = s_jac;
+    double* V = s_jac + ModelJacobi::M * ModelJacobi::NRP;
+    double* nrm = V + ModelJacobi::M * ModelJacobi::NVP;
+    ModelJacobi::init(A, V, lane, [](int, int) { return 0.0; });
+    // lane r < 16 writes row r of A (float entries as the reference computes
+    // them, held in double)
+    if (valid && lane < 16) {
+        const int r = lane;
+        double a[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) a[k] = 0.0;
-    {
+        for (int k = 0; k < 9; ++k) a[k] = 0.0;
         const int i = homography ? (r >> 1) : r;  // the pair this row comes from
         if (i < 8) {
             const int idx = sets[8 * it + i];
@@ -204,31 +208,24 @@ __global__ __launch_bounds__(kModelThreads) void init_models_kernel(const float*
                 a[6] = u1; a[7] = v1; a[8] = 1.0;
             }
         }
-    }
-    double v[9];  // row r of V (lanes r < 9)
 #pragma unroll
-    for (int k = 0; k < 9; ++k) v[k] = (r == k) ? 1.0 : 0.0;
-    orbgpu::hestenes_group<9, 16>(a, v);
+        for (int k = 0; k < 9; ++k) A[k * ModelJacobi::NRP + r] = a[k];
+    }
+    ModelJacobi::sync();
+    ModelJacobi::run(A, V, nrm, lane);
     // singular values = column norms; the first smallest decides vt.row(8)
+    if (lane != 0 || !valid) return;
     int jmin = 0;
     double smin = 0.0;
-#pragma unroll
     for (int j = 0; j < 9; ++j) {
-        const double sj = sqrt(group_sum(a[j] * a[j]));
+        const double sj = sqrt(nrm[j]);
         if (j == 0 || sj < smin) {
             smin = sj;
             jmin = j;
         }
     }
-    double vj = v[0];
-#pragma unroll
-    for (int j = 1; j < 9; ++j)
-        if (jmin == j) vj = v[j];
-    if (r < 9) s_null[g][r] = vj;
-    __syncthreads();
-    if (r != 0 || !valid) return;
     float nv[9];
-    for (int k = 0; k < 9; ++k) nv[k] = (float)s_null[g][k];
+    for (int k = 0; k < 9; ++k) nv[k] = (float)V[jmin * ModelJacobi::NVP + k];
     if (homography) {
         float T2inv[9], tmp[9], H[9], Hi[9];
         inv3(T2, T2inv);       // T2.inv()
@@ -288,7 +285,7 @@ extern "C" int orbgpu_init_hypotheses_batch_device(const float* d_kp1, int n1, c
                        n_matches, static_cast<float*>(d_work), reinterpret_cast<float4*>(d_pts));
     ORB_HIP(hipGetLastError());
     if (n_iter > 0) {
-        hipLaunchKernelGGL(init_models_kernel, dim3((2 * n_iter + kGroups - 1) / kGroups), dim3(kModelThreads), 0, s, static_cast<const float*>(d_work), n1, n2, d_pairs, d_sets,
+        hipLaunchKernelGGL(init_models_kernel, dim3(2 * n_iter), dim3(kModelThreads), 0, s, static_cast<const float*>(d_work), n1, n2, d_pairs, d_sets,
                            n_iter, d_h21, d_h12, d_f21);
         ORB_HIP(hipGetLastError());
     }

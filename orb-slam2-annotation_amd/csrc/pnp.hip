@@ -158,6 +158,7 @@ __global__ __launch_bounds__(kThreads) void pnp_score_kernel(const orbgpu_pnp_pr
     __shared__ int s_state[6];  // best, best_hyp, found, consumed, refine_tried, refined_inliers
     __shared__ HypPose s_ref;
     __shared__ double s_ep[epnp::kWaveScratch];
+    __shared__ double s_jac[JacobiLds<12, 12>::kDoubles];
     const orbgpu_pnp_problem P = probs[blockIdx.x];
     const HypPose* HP = hyps + P.sample_offset;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -217,7 +218,7 @@ __global__ __launch_bounds__(kThreads) void pnp_score_kernel(const orbgpu_pnp_pr
 #else
                     unsigned long long* st = nullptr;
 #endif
-                    if (m > 0) epnp::compute_pose_group<64>(src, cam, pose, lane, s_ep, st);
+                    if (m > 0) epnp::compute_pose_group<64>(src, cam, pose, lane, s_ep, st, s_jac);
                     if (lane == 0) {
                         for (int k = 0; k < 9; ++k) s_ref.R[k] = m > 0 ? pose.R[k] : 0.0;
                         for (int k = 0; k < 3; ++k) s_ref.t[k] = m > 0 ? pose.t[k] : 0.0;
