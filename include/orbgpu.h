@@ -152,9 +152,12 @@ typedef struct orbgpu_grid_bounds {
  * d_prev_xy (nullable): float2 per F1 keypoint at + b*stride1*2, read and
  * updated (vbPrevMatched); NULL means vbPrevMatched = F1 positions.
  * d_matches12: int per F1 keypoint at + b*stride1; d_nmatches[b].
- * Capacity: up to 1024 level-0 keypoints per frame (pairs above 512 run in
- * a second, larger-LDS pass).  A pair with more reports d_nmatches[b] = -1
- * and all its matches12 = -1; the status is per pair, nothing global. */
+ * Capacity: up to 2048 level-0 keypoints per frame (pairs above 512 run in
+ * a second, larger-LDS pass, pairs above 1024 in a third one that reads F2's
+ * descriptors from HBM; a pass is launched only when stride1 or stride2
+ * exceeds the previous pass's limit).  A pair with more reports
+ * d_nmatches[b] = -1 and all its matches12 = -1; the status is per pair,
+ * nothing global. */
 int orbgpu_search_for_initialization_batch_device(
     int batch, orbgpu_grid_bounds bounds,
     const orbgpu_keypoint* d_kps1, const uint8_t* d_desc1, const int* d_n1, size_t stride1,
@@ -163,7 +166,7 @@ int orbgpu_search_for_initialization_batch_device(
     int* d_matches12, int* d_nmatches, void* stream);
 
 /* Host-pointer convenience form for one pair; returns nmatches in *n.
- * ORBGPU_ERR_CAPACITY (and *nmatches = 0) for more than 1024 level-0
+ * ORBGPU_ERR_CAPACITY (and *nmatches = 0) for more than 2048 level-0
  * keypoints in either frame. */
 int orbgpu_search_for_initialization(orbgpu_grid_bounds bounds,
                                      const orbgpu_keypoint* kps1, const uint8_t* desc1, int n1,

@@ -22,12 +22,17 @@ namespace orbgpu {
 
 namespace {
 
-// Level-0 keypoints per frame held in LDS.  The 512 variant (45 KB of LDS)
-// covers nfeatures <= 2350; pairs above it are handed to the 1024 variant
-// (89 KB: the 2x-features initialisation extractor of KITTI mono,
-// Tracking.cpp:149, has ~870 at level 0); above 1024 a pair reports -1.
-constexpr int kMaxK0Small = 512, kMaxK0Large = 1024;
+// Level-0 keypoints per frame held in LDS.  The 512 variant covers
+// nfeatures <= 2350; pairs above it are handed to the 1024 variant (the
+// 2x-features initialisation extractor of KITTI mono, Tracking.cpp:149, has
+// ~870 at level 0), pairs above that to the 2048 variant (F2's descriptors
+// read from HBM instead of LDS: 68 B of LDS per keypoint; initialisation
+// extractors up to ~9,400 features); above 2048 a pair reports -1.  A
+// variant is launched only when a frame's keypoint capacity can exceed the
+// previous one's limit.
+constexpr int kMaxK0Small = 512, kMaxK0Large = 1024, kMaxK0Huge = 2048;
 constexpr int kNeedLarge = -2;  // nmatches sentinel: the pair waits for the large variant
+constexpr int kNeedHuge = -3;   // ... for the huge variant
 constexpr int kGC = 64, kGR = 48, kHL = 30, kThLow = 50;
 
 __device__ inline unsigned long long wave_min_u64(unsigned long long v) {
@@ -59,8 +64,8 @@ constexpr int kMatchThreads = 256;
 constexpr int kTopK = 4;  // best candidate keys kept per query by the parallel phase
 
 // (dist, grid order) of a candidate as one ordered key: dist <= 256 (9 bits),
-// cell = ix * 48 + iy < 3072 (12 bits), level-0 index < 1024 (10 bits)
-constexpr int kKeyJBits = 10;
+// cell = ix * 48 + iy < 3072 (12 bits), level-0 index < 2048 (11 bits)
+constexpr int kKeyJBits = 11;
 constexpr uint32_t kKeyJMask = (1u << kKeyJBits) - 1;
 __device__ inline uint32_t cand_key(int dist, int cell, int j) {
     return ((uint32_t)dist << (12 + kKeyJBits)) | ((uint32_t)cell << kKeyJBits) | (uint32_t)j;
@@ -100,7 +105,8 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     __shared__ int s_cell[kMaxK0];           // grid cell ix*48+iy, or -1 when not in the grid
     __shared__ int s_mdist[kMaxK0];          // vMatchedDistance
     __shared__ int s_m21[kMaxK0];            // vnMatches21
-    __shared__ unsigned long long s_d2[kMaxK0][4];
+    constexpr bool kDescHbm = kMaxK0 > kMaxK0Large;  // F2's descriptors stay in HBM (L2-resident)
+    __shared__ unsigned long long s_d2[kDescHbm ? 1 : kMaxK0][4];
     __shared__ int s_m12[kMaxK0];            // vnMatches12 for F1 level-0
     __shared__ float s_px[kMaxK0], s_py[kMaxK0], s_ang1[kMaxK0];  // F1: vbPrevMatched, angle
     __shared__ uint32_t s_top[kMaxK0][kTopK];
@@ -122,17 +128,25 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     const int n1 = n1p[b], n2 = n2p[b];
     int* M12 = matches12 + (size_t)b * stride1;
     float* prev = prev_xy ? prev_xy + (size_t)b * stride1 * 2 : nullptr;
-    const bool large = kMaxK0 == kMaxK0Large;
-    // the large variant only takes the pairs the small one handed over
-    if (large && nmatches_out[b] != kNeedLarge) return;
+    // a larger variant only takes the pairs the previous one handed over
+    if (kMaxK0 == kMaxK0Large && nmatches_out[b] != kNeedLarge) return;
+    if (kMaxK0 == kMaxK0Huge && nmatches_out[b] != kNeedHuge) return;
     const int n10 = level0_count(K1, n1), n20 = level0_count(K2, n2);
     if (n10 > kMaxK0 || n20 > kMaxK0) {
-        // per-pair status: kNeedLarge (retried by the large variant) or -1
-        // (capacity exceeded); no match is reported for the pair
+        // per-pair status: retried by the next variant, or -1 (capacity
+        // exceeded); no match is reported for the pair
         for (int i = tid; i < n1; i += kMatchThreads) M12[i] = -1;
-        if (tid == 0) nmatches_out[b] = large ? -1 : kNeedLarge;
+        if (tid == 0)
+            nmatches_out[b] = kMaxK0 == kMaxK0Small ? kNeedLarge : kMaxK0 == kMaxK0Large ? kNeedHuge : -1;
         return;
     }
+    const unsigned long long* D2q = reinterpret_cast<const unsigned long long*>(D2);
+    auto d2 = [&](int j, int q) -> unsigned long long {
+        if constexpr (kDescHbm)
+            return D2q[4 * j + q];
+        else
+            return s_d2[j][q];
+    };
     // grid inverses (Frame.cpp:221-224)
     const float invW = __fdiv_rn((float)kGC, __fsub_rn(maxX, minX));
     const float invH = __fdiv_rn((float)kGR, __fsub_rn(maxY, minY));
@@ -150,9 +164,11 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
         s_mdist[j] = 0x7FFFFFFF;
         s_m21[j] = -1;
         s_claim[j] = 64;
-        const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D2 + (size_t)j * 32);
+        if (!kDescHbm) {
+            const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D2 + (size_t)j * 32);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s_d2[j][q] = d[q];
+            for (int q = 0; q < 4; ++q) s_d2[j][q] = d[q];
+        }
     }
     for (int i = tid; i < n10; i += kMatchThreads) {
         s_m12[i] = -1;
@@ -228,8 +244,8 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
                 for (int p = lo; p < hi; ++p) {
                     const int j = s_cidx[p];
                     if (!(fabsf(__fsub_rn(s_x[j], x)) < r && fabsf(__fsub_rn(s_y[j], y)) < r)) continue;
-                    const int dist = __popcll(q0 ^ s_d2[j][0]) + __popcll(q1 ^ s_d2[j][1]) +
-                                     __popcll(q2 ^ s_d2[j][2]) + __popcll(q3 ^ s_d2[j][3]);
+                    const int dist = __popcll(q0 ^ d2(j, 0)) + __popcll(q1 ^ d2(j, 1)) +
+                                     __popcll(q2 ^ d2(j, 2)) + __popcll(q3 ^ d2(j, 3));
                     uint32_t key = cand_key(dist, s_cell[j], j);
 #pragma unroll
                     for (int k = 0; k < kTopK; ++k) {  // sorted insert
@@ -328,8 +344,8 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
                 for (int j = lane; j < n20; j += 64) {
                     int cell;
                     if (!in_window(j, x, y, cx0, cx1, cy0, cy1, cell)) continue;
-                    const int dist = __popcll(q0 ^ s_d2[j][0]) + __popcll(q1 ^ s_d2[j][1]) +
-                                     __popcll(q2 ^ s_d2[j][2]) + __popcll(q3 ^ s_d2[j][3]);
+                    const int dist = __popcll(q0 ^ d2(j, 0)) + __popcll(q1 ^ d2(j, 1)) +
+                                     __popcll(q2 ^ d2(j, 2)) + __popcll(q3 ^ d2(j, 3));
                     if (s_mdist[j] <= dist) continue;
                     const unsigned long long k64 = ((unsigned long long)dist << 32) | ((unsigned)cell << 16) | (unsigned)j;
                     if (k64 < lbest) {
@@ -431,14 +447,21 @@ hipError_t launch_match_init(int batch, float minX, float maxX, float minY, floa
                              const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2, size_t stride2,
                              float* prev_xy, int window, float nnratio, int flags,
                              int* matches12, int* nmatches, hipStream_t stream) {
-    // small variant for every pair, then the large one for the pairs it
-    // handed over (a no-op block per pair otherwise)
+    // small variant for every pair, then the larger ones for the pairs handed
+    // over (a no-op block per other pair); a larger variant is launched only
+    // when a frame's capacity (stride) can exceed the previous limit
+    const size_t cap = stride1 > stride2 ? stride1 : stride2;
     hipLaunchKernelGGL(match_init_kernel<kMaxK0Small>, dim3(batch), dim3(kMatchThreads), 0, stream, minX, maxX, minY,
                        maxY, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags,
                        matches12, nmatches);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || cap <= (size_t)kMaxK0Small) return e;
     hipLaunchKernelGGL(match_init_kernel<kMaxK0Large>, dim3(batch), dim3(kMatchThreads), 0, stream, minX, maxX, minY,
+                       maxY, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags,
+                       matches12, nmatches);
+    e = hipGetLastError();
+    if (e != hipSuccess || cap <= (size_t)kMaxK0Large) return e;
+    hipLaunchKernelGGL(match_init_kernel<kMaxK0Huge>, dim3(batch), dim3(kMatchThreads), 0, stream, minX, maxX, minY,
                        maxY, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags,
                        matches12, nmatches);
     return hipGetLastError();

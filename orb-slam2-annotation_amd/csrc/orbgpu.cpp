@@ -821,7 +821,7 @@ int orbgpu_search_for_initialization(orbgpu_grid_bounds bd, const orbgpu_keypoin
     if ((rc = call.finish())) return rc;
     if (*nmatches < 0) {
         *nmatches = 0;
-        return fail(ORBGPU_ERR_CAPACITY, "matcher: more than 1024 level-0 keypoints in a frame");
+        return fail(ORBGPU_ERR_CAPACITY, "matcher: more than 2048 level-0 keypoints in a frame");
     }
     return ORBGPU_OK;
 }

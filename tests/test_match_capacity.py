@@ -1,9 +1,10 @@
 """SearchForInitialization capacity: the 2x-features
 initialisation extractor (Tracking.cpp:149: mpIniORBextractor with
 2*nFeatures) puts ~870 keypoints on level 0 of a KITTI 1241x376 frame, above
-the 512 the small LDS variant holds.  Such pairs run in the 1024 variant and
-stay bit-exact against the oracle; above 1024 the status is per pair
-(nmatches = -1), never a process-global flag.  Also: DescriptorDistance over
+the 512 the small LDS variant holds.  Such pairs run in the 1024 variant
+(above that: the 2048 variant, F2's descriptors from HBM) and stay bit-exact
+against the oracle; above 2048 the status is per pair (nmatches = -1), never
+a process-global flag.  Also: DescriptorDistance over
 HBM pairs (orbgpu_hamming_pairs_device) against numpy popcounts."""
 import numpy as np
 import pytest
@@ -66,33 +67,45 @@ def _crowded(n, seed):
 
 
 def test_batch_mixed_capacity_is_per_pair(mono_frames):
-    """pair 0 normal, pair 1 in the 1024 variant, pair 2 over capacity: each
-    gets its own status; a single-pair call afterwards is unaffected."""
+    """pair 0 normal, pair 1 in the 1024 variant, pair 2 in the 2048 variant,
+    pair 3 over capacity: each gets its own status; a single-pair call
+    afterwards is unaffected."""
     og = _gpu()
     ref = orbref.Extractor()
     f0, f1 = ref.extract(mono_frames[0]), ref.extract(mono_frames[1])
     mid1, mid2 = _crowded(800, 1), _crowded(800, 2)
-    big1, big2 = _crowded(1100, 3), _crowded(1100, 4)
-    cap = 1100
-    K1, D1, N1 = _pack([f0, mid1, big1], cap)
-    K2, D2, N2 = _pack([f1, mid2, big2], cap)
-    m12 = torch.full((3, cap), -7, dtype=torch.int32, device="cuda")
-    nm = torch.full((3,), 99, dtype=torch.int32, device="cuda")
+    big1, big2 = _crowded(1900, 3), _crowded(2040, 4)
+    # big2 re-observes big1: jittered positions, a few flipped descriptor bits
+    rng = np.random.default_rng(7)
+    big2[0][:1900]["x"] = big1[0]["x"] + rng.uniform(-3, 3, 1900).astype(np.float32)
+    big2[0][:1900]["y"] = big1[0]["y"] + rng.uniform(-3, 3, 1900).astype(np.float32)
+    big2[1][:1900] = big1[1] ^ (rng.random((1900, 32)) < 0.03).astype(np.uint8) << rng.integers(0, 8, (1900, 32)).astype(np.uint8)
+    over1, over2 = _crowded(2100, 5), _crowded(900, 6)
+    cap = 2100
+    K1, D1, N1 = _pack([f0, mid1, big1, over1], cap)
+    K2, D2, N2 = _pack([f1, mid2, big2, over2], cap)
+    m12 = torch.full((4, cap), -7, dtype=torch.int32, device="cuda")
+    nm = torch.full((4,), 99, dtype=torch.int32, device="cuda")
     og.search_for_initialization_batch(640, 480, K1, D1, N1, K2, D2, N2, m12, nm)
     torch.cuda.synchronize()
     nm, m12 = nm.cpu().numpy(), m12.cpu().numpy()
-    for b, (a, c) in enumerate([(f0, f1), (mid1, mid2)]):
+    for b, (a, c) in enumerate([(f0, f1), (mid1, mid2), (big1, big2)]):
         n_r, m_r, _ = orbref.search_for_initialization(a[0], a[1], c[0], c[1], 640, 480)
         assert nm[b] == n_r, b
         np.testing.assert_array_equal(m12[b, :len(a[0])], m_r)
-    assert nm[2] == -1
-    assert (m12[2, :1100] == -1).all()
-    # the next single-pair call sees no stale error
+    assert nm[2] > 0
+    assert nm[3] == -1
+    assert (m12[3, :2100] == -1).all()
+    # the next single-pair calls see no stale error; the host form takes the 2048 variant too
     n_r, m_r, _ = orbref.search_for_initialization(f0[0], f0[1], f1[0], f1[1], 640, 480)
     n_g, m_g, _ = og.search_for_initialization(f0[0], f0[1], f1[0], f1[1], 640, 480)
     assert n_g == n_r and np.array_equal(m_g, m_r)
+    n_r, m_r, p_r = orbref.search_for_initialization(big1[0], big1[1], big2[0], big2[1], 640, 480)
+    n_g, m_g, p_g = og.search_for_initialization(big1[0], big1[1], big2[0], big2[1], 640, 480)
+    assert n_g == n_r and np.array_equal(m_g, m_r)
+    np.testing.assert_array_equal(p_g.view(np.uint32), p_r.view(np.uint32))
     with pytest.raises(og.OrbGpuError) as ei:
-        og.search_for_initialization(big1[0], big1[1], big2[0], big2[1], 640, 480)
+        og.search_for_initialization(over1[0], over1[1], over2[0], over2[1], 640, 480)
     assert ei.value.code == og.ERR_CAPACITY
 
 
