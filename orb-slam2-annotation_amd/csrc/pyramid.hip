@@ -277,6 +277,23 @@ __device__ __forceinline__ void pyr_issue(const uint8_t* __restrict__ fb, size_t
     }
 }
 
+// Two frames share each CU (two blocks), and the hardware issues by wave
+// priority, then age: the older block's waves win every contended slot, so
+// it finishes first (measured: 114 us vs 170 us for the two blocks of a CU,
+// tools/pyr_ticks.py) and the younger one then runs alone, leaving the CU
+// half used.  A priority that decreases with the tick index (3 at the
+// start, 0 at the end) lets a block that is behind win over
+// one that is ahead, so the two progress together.  The phases shrink
+// towards the end (ticks [0, K/2), [K/2, 3K/4), [3K/4, 7K/8), [7K/8, K)):
+// within a phase age decides again, so the last phase bounds how far apart
+// the two blocks can finish.
+__device__ __forceinline__ void prio_by_progress(int k, int K) {
+    if (k == 0) __builtin_amdgcn_s_setprio(3);
+    else if (k == K / 2) __builtin_amdgcn_s_setprio(2);
+    else if (k == (3 * K) / 4) __builtin_amdgcn_s_setprio(1);
+    else if (k == (7 * K) / 8) __builtin_amdgcn_s_setprio(0);
+}
+
 template <int NP>
 __device__ __forceinline__ void pyr_producer(const Geom& g, const uint8_t* __restrict__ fb, size_t row0, int p,
                                              int P, uint8_t* s_mem) {
@@ -305,6 +322,7 @@ __device__ __forceinline__ void pyr_producer(const Geom& g, const uint8_t* __res
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's share of the plan-table copy
     __builtin_amdgcn_s_barrier();
     for (int k = 0; k < K; ++k) {
+        prio_by_progress(k, K);
         // chunk k+1 lands before the barrier that ends tick k; chunk k+2 stays
         // in flight; chunk k+3 is issued as tick k+1 starts (plan_pyramid
         // sizes ring 0 for the two chunks written during a tick)
@@ -355,6 +373,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(ORBGPU_PYR
 #pragma unroll
     for (int e = 0; e < E; ++e) tail[e] = __builtin_amdgcn_readfirstlane(en[e].tail) != 0;
     for (int k = 0; k < K; ++k) {
+        prio_by_progress(k, K);
         if (tid < 64) PYR_STAMP(k, 15);
 #pragma unroll
         for (int e = 0; e < E; ++e) {

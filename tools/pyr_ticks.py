@@ -60,3 +60,11 @@ for w in range(nw):
 print(f"  producer ready: {prod[:, 4:K - 8].mean():7.0f}")
 tick = st[:, 1:K, 15] - st[:, :K - 1, 15]
 print("tick length mean %.0f" % tick[:, 4:K - 8].mean())
+# per-XCD block lifetime and clock (all blocks of the batch)
+xcc = bl[:, 5] & 0xF
+for x in np.unique(xcc):
+    m = xcc == x
+    print("xcc %d: blocks %3d lifetime us mean %.1f min %.1f max %.1f  clock MHz mean %.0f min %.0f max %.0f" %
+          (x, m.sum(), life_us[m].mean(), life_us[m].min(), life_us[m].max(), clk[m].mean(), clk[m].min(), clk[m].max()))
+cyc = bl[:, 3] - bl[:, 2]
+print("block cycles (all blocks): mean %.0f min %d max %d" % (cyc.mean(), cyc.min(), cyc.max()))
