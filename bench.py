@@ -753,15 +753,14 @@ class DropIn:
         res["stereo Frame: ORBextractor L || R + ComputeStereoMatches"] = (
             t(lambda: orbref.stereo_frame(eL, eR, st[0], st[1], bf)), "C++ oracle, L and R sequential")
         res["ComputeStereoMatches"] = (t(lambda: orbref.stereo_matches(eL, eR, kl, dl, kr, dr, bf)), "C++ oracle")
-        import proj_ref
         tgt, pts = self.scen["proj_local"]
         res["ORBmatcher::SearchByProjection(F, vpLocalMapPoints, th)"] = (
-            t(lambda: proj_ref.search_by_projection(0, tgt, pts, 1.0, nnratio=0.8), 1), "Python oracle")
+            t(lambda: orbref.search_by_projection(0, tgt, pts, 1.0, nnratio=0.8), 5),
+            "C++ oracle (oracle/proj_ref.cpp, equal to proj_ref.py)")
         tgt2, pts2, last = self.scen["proj_last"]
         res["ORBmatcher::SearchByProjection(F, LastFrame, th, bMono)"] = (
-            t(lambda: proj_ref.search_by_projection(2, tgt2, pts2, 15.0, check_ori=True, mono=True, last_Tcw=last),
-              1), "Python oracle")
-        import bow_ref
+            t(lambda: orbref.search_by_projection(2, tgt2, pts2, 15.0, check_ori=True, mono=True, last_Tcw=last),
+              5), "C++ oracle (oracle/proj_ref.cpp, equal to proj_ref.py)")
         par, leaf, vdesc, w, d1_, a1, s1, d2_, a2, s2 = self.scen["bow"]
         cv = orbref.Vocabulary(10, 6, par, leaf, vdesc, w)
         res["ORBmatcher::SearchByBoW(KF1, KF2)"] = (
@@ -771,16 +770,19 @@ class DropIn:
         av = loop_ref.ArrayVocabulary(10, 6, 0, 0, par, leaf, vdesc, w)
         f1, f2 = av.transform(d1_, 4)[3], av.transform(d2_, 4)[3]
         res["ORBmatcher::SearchByBoW(KF, F)"] = (
-            t(lambda: bow_ref.search_by_bow(0, f1, d1_, a1, s1 == 1, f2, d2_, a2, np.ones(1000, bool), 0.7, True), 1),
-            "Python oracle")
-        import pnp_ref
+            t(lambda: orbref.search_by_bow_kf_f(f1, d1_, a1, s1 == 1, f2, d2_, a2, 0.7, True), 5),
+            "C++ oracle (oracle/loop_ref.cpp, FeatureVectors given as in TrackReferenceKeyFrame)")
         P = self.scen["pnp"]
         maxerr = (P["sigma2"] * np.float32(5.991)).astype(np.float32)
         rng = np.random.default_rng(0)
-        smp = np.array([rng.choice(len(P["P2"]), 4, replace=False) for _ in range(5)])
+        # a fresh solver's iterate(5) runs hypotheses until the first Refine
+        # that passes (the || loop condition, up to mRansacMaxIts = 300)
+        smp = np.array([rng.choice(len(P["P2"]), 4, replace=False) for _ in range(300)], np.int32)
+        o = orbref.pnp_ransac_call(P["P3w"], P["P2"], maxerr, P["cam"], 150, 0, smp)
         res["PnPsolver::iterate(5)"] = (
-            t(lambda: pnp_ref.ransac_call(P["P3w"], P["P2"], maxerr, P["cam"], 150, 0, np.zeros(len(P["P2"]), bool),
-                                          smp), 1), "numpy oracle, 5 hypotheses")
+            t(lambda: orbref.pnp_ransac_call(P["P3w"], P["P2"], maxerr, P["cam"], 150, 0, smp), 5),
+            f"C++ oracle (oracle/pnp_ref.cpp, equal to pnp_ref.py): {o['consumed']} hypotheses + Refine until "
+            f"the first pass, found={o['found']}")
         return {op: {"cpu_oracle_single_thread_us": v[0], "cpu_oracle_kind": v[1]} for op, v in res.items()
                 if op in ops}
 

@@ -151,6 +151,59 @@ int search_by_bow_kf_kf(const FeatVec& fv1, const uint8_t* d1, const float* a1, 
     return nm;
 }
 
+// SearchByBoW(KF, F) (M:205-348): the KeyFrame's features (side A, valid =
+// it has a MapPoint that is not bad) against the Frame's (side B); a Frame
+// keypoint already matched is skipped; match: int[nB] = the A feature
+int search_by_bow_kf_f(const FeatVec& fva, const uint8_t* da, const float* aa, const uint8_t* va,
+                       const FeatVec& fvb, const uint8_t* db, const float* ab, int nb, float nnratio,
+                       bool check_ori, int* match) {
+    const int HL = 30, TH_LOW = 50;
+    const float factor = (float)HL / 360.0f;
+    for (int i = 0; i < nb; ++i) match[i] = -1;
+    std::vector<std::vector<int>> hist(HL);
+    int nm = 0;
+    auto ia_it = fva.begin(), ib_it = fvb.begin();
+    while (ia_it != fva.end() && ib_it != fvb.end()) {
+        if (ia_it->first == ib_it->first) {
+            for (int ia : ia_it->second) {
+                if (!va[ia]) continue;
+                int b1 = 256, b2 = 256, bidx = -1;
+                for (int ib : ib_it->second) {
+                    if (match[ib] >= 0) continue;
+                    const int d = hamming32(da + 32 * ia, db + 32 * ib);
+                    if (d < b1) { b2 = b1; b1 = d; bidx = ib; }
+                    else if (d < b2) b2 = d;
+                }
+                if (b1 <= TH_LOW && (float)b1 < nnratio * (float)b2) {
+                    match[bidx] = ia;
+                    if (check_ori) {
+                        float rot = aa[ia] - ab[bidx];
+                        if (rot < 0.0f) rot += 360.0f;
+                        int bin = (int)std::round(rot * factor);
+                        if (bin == HL) bin = 0;
+                        hist[bin].push_back(bidx);
+                    }
+                    ++nm;
+                }
+            }
+            ++ia_it; ++ib_it;
+        } else if (ia_it->first < ib_it->first) {
+            ia_it = fva.lower_bound(ib_it->first);
+        } else {
+            ib_it = fvb.lower_bound(ia_it->first);
+        }
+    }
+    if (check_ori) {
+        int i1, i2, i3;
+        three_maxima(hist, i1, i2, i3);
+        for (int i = 0; i < HL; ++i) {
+            if (i == i1 || i == i2 || i == i3) continue;
+            for (int idx : hist[i]) { match[idx] = -1; --nm; }
+        }
+    }
+    return nm;
+}
+
 // float 3x3 * float 3-vector, double accumulation, rounded to float
 void gemv_f32(const float* R, const float* X, float* out) {
     for (int r = 0; r < 3; ++r)
@@ -239,6 +292,20 @@ int orbref_search_by_bow_kf_kf(const orbref_vocabulary* h, const uint8_t* d1, co
     transform(h->v, d1, n1, 4, nullptr, nullptr, nullptr, &f1);
     transform(h->v, d2, n2, 4, nullptr, nullptr, nullptr, &f2);
     return search_by_bow_kf_kf(f1, d1, a1, v1, n1, f2, d2, a2, v2, n2, nnratio, check_ori != 0, match);
+}
+
+/* SearchByBoW(KF, F) on given FeatureVectors (Frame::ComputeBoW /
+ * KeyFrame::ComputeBoW already run, as Tracking::TrackReferenceKeyFrame calls
+ * it), each as a CSR: nodes[k] ascending, its features feats[start[k] ..
+ * start[k+1]) in FeatureVector order. */
+int orbref_search_by_bow_kf_f(const int* nodes_a, const int* start_a, const int* feats_a, int nn_a,
+                              const uint8_t* da, const float* aa, const uint8_t* va, const int* nodes_b,
+                              const int* start_b, const int* feats_b, int nn_b, const uint8_t* db, const float* ab,
+                              int nb, float nnratio, int check_ori, int* match) {
+    FeatVec fa, fb;
+    for (int k = 0; k < nn_a; ++k) fa[nodes_a[k]].assign(feats_a + start_a[k], feats_a + start_a[k + 1]);
+    for (int k = 0; k < nn_b; ++k) fb[nodes_b[k]].assign(feats_b + start_b[k], feats_b + start_b[k + 1]);
+    return search_by_bow_kf_f(fa, da, aa, va, fb, db, ab, nb, nnratio, check_ori != 0, match);
 }
 
 /* One ComputeSim3 call (LC:273-356) for keyframe `cur` and candidates

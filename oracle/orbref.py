@@ -68,6 +68,10 @@ def lib() -> ctypes.CDLL:
         L.orbref_vocabulary_destroy.argtypes = [vp]
         L.orbref_vocabulary_transform.argtypes = [vp, vp, i, i, vp, vp, vp]
         L.orbref_search_by_bow_kf_kf.argtypes = [vp, vp, vp, vp, i, vp, vp, vp, i, f, i, vp]
+        L.orbref_search_by_bow_kf_f.argtypes = [vp, vp, vp, i, vp, vp, vp, vp, vp, vp, i, vp, vp, i, f, i, vp]
+        L.orbref_pnp_ransac_call.argtypes = [vp, vp, vp, i, vp, i, i, vp, i, vp, vp]
+        L.orbref_search_by_projection.argtypes = [i, vp, vp, i, vp, vp, vp, vp, vp, vp, i, vp, vp, vp, vp, vp, vp,
+                                                  vp, vp, f, f, i, i, vp]
         L.orbref_compute_sim3_query.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, i, ctypes.c_uint, i,
                                                 vp, vp]
         _LIB = L
@@ -261,6 +265,86 @@ def search_by_bow_kf_kf(voc: Vocabulary, d1, a1, v1, d2, a2, v2, nnratio=0.75, c
                                          _p(arrs[4]), _p(arrs[5]), len(arrs[3]), float(nnratio), int(check_ori),
                                          _p(m))
     return n, m
+
+
+def pnp_ransac_call(P3w, P2, maxerr, cam, min_inliers, best_inliers, samples):
+    """pnp_ref.ransac_call in C++ (oracle/pnp_ref.cpp): the iterate loop body
+    over the given 4-tuples with Refine.  Returns dict(found, consumed,
+    best_inliers, best_hyp, refined_inliers, best_R, best_t, refined_R,
+    refined_t)."""
+    P3 = np.ascontiguousarray(P3w, np.float32)
+    P2 = np.ascontiguousarray(P2, np.float32)
+    E = np.ascontiguousarray(maxerr, np.float32)
+    cam = np.ascontiguousarray(np.asarray(cam, np.float64))
+    smp = np.ascontiguousarray(samples, np.int32).reshape(-1, 4)
+    oi = np.zeros(5, np.int32)
+    op = np.zeros(24, np.float64)
+    lib().orbref_pnp_ransac_call(_p(P3), _p(P2), _p(E), len(P2), _p(cam), int(min_inliers), int(best_inliers),
+                                 _p(smp), len(smp), _p(oi), _p(op))
+    return {"found": int(oi[0]), "consumed": int(oi[1]), "best_inliers": int(oi[2]), "best_hyp": int(oi[3]),
+            "refined_inliers": int(oi[4]), "best_R": op[:9].reshape(3, 3), "best_t": op[9:12],
+            "refined_R": op[12:21].reshape(3, 3), "refined_t": op[21:24]}
+
+
+def _fv_csr(fv):
+    nodes = np.array(sorted(fv), np.int32)
+    start = np.zeros(len(nodes) + 1, np.int32)
+    feats = []
+    for k, nd in enumerate(nodes):
+        feats.extend(fv[int(nd)])
+        start[k + 1] = len(feats)
+    return nodes, start, np.array(feats, np.int32)
+
+
+def search_by_bow_kf_f(fvA, descA, angA, validA, fvB, descB, angB, nnratio=0.6, check_ori=True):
+    """SearchByBoW(KF, F) (mode 0 of bow_ref.search_by_bow) in C++ on given
+    FeatureVectors (dict node -> [features]); returns (nmatches, match[nB])."""
+    na, sa, fa = _fv_csr(fvA)
+    nb_, sb, fb = _fv_csr(fvB)
+    arrs = [np.ascontiguousarray(descA, np.uint8), np.ascontiguousarray(angA, np.float32),
+            np.ascontiguousarray(validA, np.uint8), np.ascontiguousarray(descB, np.uint8),
+            np.ascontiguousarray(angB, np.float32)]
+    m = np.zeros(len(arrs[3]), np.int32)
+    n = lib().orbref_search_by_bow_kf_f(_p(na), _p(sa), _p(fa), len(na), _p(arrs[0]), _p(arrs[1]), _p(arrs[2]),
+                                        _p(nb_), _p(sb), _p(fb), len(nb_), _p(arrs[3]), _p(arrs[4]), len(arrs[3]),
+                                        float(nnratio), int(check_ori), _p(m))
+    return n, m
+
+
+def search_by_projection(variant, tgt, pts, th, nnratio=0.6, check_ori=True, mono=True, last_Tcw=None):
+    """SearchByProjection for variant 0 (LOCAL: F, vpLocalMapPoints, th) and 2
+    (LAST_FRAME: F, LastFrame, th, bMono) in C++ (proj_ref.cpp), with the
+    dict layout of proj_ref.py; returns (nmatches, match)."""
+    k = np.ascontiguousarray(tgt["kps"]).view(KP_DTYPE)
+    n = len(k)
+    f32, i32 = np.float32, np.int32
+    npts = len(pts["flags"])
+    A = dict(
+        desc=np.ascontiguousarray(tgt["desc"], np.uint8),
+        ur=None if tgt.get("u_right") is None else np.ascontiguousarray(tgt["u_right"], f32),
+        occ=None if tgt.get("occupied") is None else np.ascontiguousarray(tgt["occupied"], np.uint8),
+        bounds=np.array([tgt["min_x"], tgt["max_x"], tgt["min_y"], tgt["max_y"]], f32),
+        cam=np.array([tgt["fx"], tgt["fy"], tgt["cx"], tgt["cy"], tgt["bf"], tgt["b"]], f32),
+        sf=np.ascontiguousarray(tgt["scale_factors"], f32),
+        T=np.ascontiguousarray(np.asarray(tgt["Tcw"], f32).reshape(16)),
+        flags=np.ascontiguousarray(pts["flags"], i32),
+        pos=np.ascontiguousarray(pts["pos"], f32),
+        pdesc=np.ascontiguousarray(pts["desc"], np.uint8),
+        track=np.ascontiguousarray(pts["track"], f32) if "track" in pts else np.zeros((npts, 4), f32),
+        tl=np.ascontiguousarray(pts["track_level"], i32) if "track_level" in pts else np.zeros(npts, i32),
+        oct=np.ascontiguousarray(pts["octave"], i32),
+        ang=np.ascontiguousarray(pts["angle"], f32),
+        last=np.ascontiguousarray(np.asarray(last_Tcw if last_Tcw is not None else tgt["Tcw"], f32).reshape(16)))
+    m = np.zeros(n, np.int32)
+    kk = np.ascontiguousarray(k)
+    nm = lib().orbref_search_by_projection(
+        int(variant), _p(kk), _p(A["desc"]), n, _p(A["ur"]) if A["ur"] is not None else None,
+        _p(A["occ"]) if A["occ"] is not None else None, _p(A["bounds"]), _p(A["cam"]), _p(A["sf"]), _p(A["T"]),
+        npts, _p(A["flags"]), _p(A["pos"]), _p(A["pdesc"]), _p(A["track"]), _p(A["tl"]), _p(A["oct"]),
+        _p(A["ang"]), _p(A["last"]), float(th), float(nnratio), int(check_ori), int(mono), _p(m))
+    if nm < 0:
+        raise ValueError(f"variant {variant} not in the C++ oracle")
+    return nm, m
 
 
 _SCENE_KEYS = (("desc", np.uint8), ("angle", np.float32), ("octave", np.int32), ("valid", np.uint8),

@@ -46,8 +46,10 @@ def test_oracle_recovers_baseline_disparity():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,h,nf,baseline", [(640, 480, 1000, 24.0), (1241, 376, 2000, 30.0), (752, 480, 1200, 18.0)])
-def test_gpu_stereo_matches_vs_oracle(w, h, nf, baseline):
+@pytest.mark.parametrize("w,h,nf,baseline,bf", [(640, 480, 1000, 24.0, 40.0),
+                                                (1241, 376, 2000, 30.0, 0.54 * 718.856),  # KITTI00-02.yaml Camera.bf
+                                                (752, 480, 1200, 18.0, 47.90639384423901)])  # EuRoC.yaml Camera.bf
+def test_gpu_stereo_matches_vs_oracle(w, h, nf, baseline, bf):
     torch = pytest.importorskip("torch")
     import orbgpu
     if not torch.cuda.is_available():
@@ -68,7 +70,6 @@ def test_gpu_stereo_matches_vs_oracle(w, h, nf, baseline):
     counts = torch.zeros(B, dtype=torch.int32, device=dev)
     ur = torch.full((len(pairs), cap), -7.0, dtype=torch.float32, device=dev)
     dp = torch.full((len(pairs), cap), -7.0, dtype=torch.float32, device=dev)
-    bf = 0.54 * 718.856  # KITTI00-02.yaml Camera.bf
     ex.extract_batch(imgs, kps, desc, counts)
     orbgpu.stereo_matches_batch(ex, imgs, len(pairs), kps, desc, counts, bf, 0.0, ur, dp)
     ex.sync()
