@@ -235,11 +235,11 @@ __device__ inline int find_node(const int* nodes, int n, int key) {
 // `stride` features fit the budget.
 constexpr int kBowStageMaxLds = 128 * 1024;
 __host__ __device__ inline size_t bow_stage_bytes(int stride, int level) {
-    // per feature: descB 32, fvfB 4, match 4, common-node record 16, B node id 4, validB 1 (+ descA 32,
-    // fvfA 4, validA 1 at level 2)
+    // per feature: descB 32, fvfB 4, match 4, common-node record 16, B node id 4, angleB 4, validB 1 (+ descA
+    // 32, fvfA 4, angleA 4, validA 1 at level 2)
     return level == 0 ? 0
-                      : (size_t)stride * (32 + 4 + 4 + 16 + 4 + 1) + (level == 2 ? (size_t)stride * (32 + 4 + 1) : 0) +
-                            128;
+                      : (size_t)stride * (32 + 4 + 4 + 16 + 4 + 4 + 1) +
+                            (level == 2 ? (size_t)stride * (32 + 4 + 4 + 1) : 0) + 128;
 }
 
 // block-wide copy of n elements with kBatch loads per thread issued before
@@ -262,8 +262,40 @@ __device__ __forceinline__ void stage_copy(T* __restrict__ dst, const T* __restr
     }
 }
 
+// (first minimum key, second smallest distance) over the lane's 8-lane row:
+// three DPP exchanges (quad xor 1, xor 2, then the other quad of the half
+// row), all within the row, so a row-uniform branch leaves no source lane
+// disabled; min / max are order-free, so every pattern gives the same result.
+// (ds_bpermute here cost ~100 cycles per exchange on the sequential walk.)
+template <int Ctrl>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, Ctrl, 0xF, 0xF, false);
+}
+__device__ __forceinline__ void row8_best2(uint32_t& k1, uint32_t& d2) {
+    auto step = [&](uint32_t ok1, uint32_t od2) {
+        d2 = min(min(d2, od2), max(k1 >> 16, ok1 >> 16));
+        k1 = min(k1, ok1);
+    };
+    step(dpp_u32<0xB1>(k1), dpp_u32<0xB1>(d2));    // quad_perm [1,0,3,2]
+    step(dpp_u32<0x4E>(k1), dpp_u32<0x4E>(d2));    // quad_perm [2,3,0,1]
+    step(dpp_u32<0x141>(k1), dpp_u32<0x141>(d2));  // row_half_mirror
+}
+
+#ifdef BOW_STAMPS  // diagnostic build only: phase stamps of block 0 (tools/bow_stamps.py)
+__device__ unsigned long long g_bow_stamps[32];
+#define BOW_T(k)                                                                                 \
+    do {                                                                                         \
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0)                                          \
+            g_bow_stamps[(k) < 4 ? (k) : (k) + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define BOW_T(k) ((void)0)
+#endif
+
+constexpr int kBowThreads = 1024;  // 128 rows of 8 lanes: ~one common node per row for a 1000-feature pair
+
 template <int kStage>
-__global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbgpu_bow_frame* __restrict__ A_,
+__global__ __launch_bounds__(kBowThreads) void search_by_bow_kernel(int mode, const orbgpu_bow_frame* __restrict__ A_,
                                                             const orbgpu_bow_frame* __restrict__ B_, float nnratio,
                                                             int check_ori, int stride, int* __restrict__ match_g,
                                                             int* __restrict__ nmatches) {
@@ -274,6 +306,7 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
     __shared__ int s_cnt;
     __shared__ int s_npairs;
     extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+    BOW_T(0);
     const orbgpu_bow_frame A = A_[blockIdx.x], B = B_[blockIdx.x];
     const int nout = mode == ORBGPU_BOW_KF_F ? B.n : A.n;
     int* match_out = match_g + (size_t)blockIdx.x * stride;
@@ -281,8 +314,14 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
         if (threadIdx.x == 0) nmatches[blockIdx.x] = -1;
         return;
     }
+    if (A.n == 0 || B.n == 0 || A.fv_n == 0 || B.fv_n == 0) {  // no common node: nothing matches
+        for (int i = threadIdx.x; i < nout; i += blockDim.x) match_out[i] = -1;
+        if (threadIdx.x == 0) nmatches[blockIdx.x] = 0;
+        return;
+    }
     // LDS carve: descB[stride] (32 B) | descA[stride] (level 2) | common-node records (16 B) | fvfB | fvfA (2) |
-    // match | B node ids | validB | validA (2)
+    // match | B node ids | angleB | angleA (2) | validB | validA (2).  The angles are staged too: a match's
+    // rotation bin read them from HBM inside the sequential node walk (two dependent global loads per match)
     ulonglong4* s_descB = reinterpret_cast<ulonglong4*>(s_dyn);
     ulonglong4* s_descA = s_descB + (kStage == 2 ? stride : 0);
     int4* s_pairs = reinterpret_cast<int4*>(s_descA + (kStage == 2 ? stride : 0));  // (a0, na, b0, nb)
@@ -290,7 +329,9 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
     int* s_fvfA = s_fvfB + stride;
     int* s_match = s_fvfA + (kStage == 2 ? stride : 0);
     int* s_nodesB = s_match + stride;
-    unsigned char* s_validB = reinterpret_cast<unsigned char*>(s_nodesB + stride);
+    float* s_angB = reinterpret_cast<float*>(s_nodesB + stride);
+    float* s_angA = s_angB + stride;
+    unsigned char* s_validB = reinterpret_cast<unsigned char*>(s_angA + (kStage == 2 ? stride : 0));
     unsigned char* s_validA = s_validB + stride;
     int* match = kStage ? s_match : match_out;
     for (int i = threadIdx.x; i < nout; i += blockDim.x) {
@@ -299,41 +340,47 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
     }
     if constexpr (kStage >= 1) {
         // every staged array's loads of a round issued before its stores (one memory latency per round)
-        const uint4* gdB = reinterpret_cast<const uint4*>(B.desc);
-        const uint4* gdA = reinterpret_cast<const uint4*>(A.desc);
-        uint4* sdB = reinterpret_cast<uint4*>(s_descB);
-        uint4* sdA = reinterpret_cast<uint4*>(s_descA);
+        // native vectors (HIP's uint4 is a union wrapper, and arrays of it
+        // were kept in scratch memory)
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+        const v4u* gdB = reinterpret_cast<const v4u*>(B.desc);
+        const v4u* gdA = reinterpret_cast<const v4u*>(A.desc);
+        v4u* sdB = reinterpret_cast<v4u*>(s_descB);
+        v4u* sdA = reinterpret_cast<v4u*>(s_descA);
         const int nA = kStage == 2 ? A.n : 0;
         const int nmax = max(max(B.n, nA), B.fv_n);
-        for (int base = threadIdx.x; base < nmax; base += 2 * blockDim.x) {
-            uint4 db[4], da[4];
-            int fb[2], fa[2], nd[2];
-            unsigned char vb[2], va[2];
+        constexpr int kR = 2;  // elements per thread per round: up to 2048 features in one round trip
+        for (int base = threadIdx.x; base < nmax; base += kR * blockDim.x) {
+            v4u db[2 * kR], da[2 * kR];
+            int fb[kR], fa[kR], nd[kR];
+            float gb[kR], ga[kR];
+            unsigned char vb[kR], va[kR];
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {  // clamped indices; an empty array is never read
+            for (int k = 0; k < kR; ++k) {  // clamped indices (every array is non-empty here)
                 const int i = base + k * (int)blockDim.x;
                 const int ib = min(i, B.n - 1), ia = min(i, nA - 1);
-                if (B.n > 0) {
-                    db[2 * k] = gdB[2 * ib];
-                    db[2 * k + 1] = gdB[2 * ib + 1];
-                    fb[k] = B.fv_features[ib];
-                    vb[k] = B.valid[ib];
-                }
-                if (B.fv_n > 0) nd[k] = B.fv_nodes[min(i, B.fv_n - 1)];
-                if (kStage == 2 && nA > 0) {
+                db[2 * k] = gdB[2 * ib];
+                db[2 * k + 1] = gdB[2 * ib + 1];
+                fb[k] = B.fv_features[ib];
+                gb[k] = check_ori ? B.angle[ib] : 0.f;  // angles may be absent without the orientation check
+                vb[k] = B.valid[ib];
+                nd[k] = B.fv_nodes[min(i, B.fv_n - 1)];
+                if (kStage == 2) {
                     da[2 * k] = gdA[2 * ia];
                     da[2 * k + 1] = gdA[2 * ia + 1];
                     fa[k] = A.fv_features[ia];
+                    ga[k] = check_ori ? A.angle[ia] : 0.f;
                     va[k] = A.valid[ia];
                 }
             }
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < kR; ++k) {
                 const int i = base + k * (int)blockDim.x;
                 if (i < B.n) {
                     sdB[2 * i] = db[2 * k];
                     sdB[2 * i + 1] = db[2 * k + 1];
                     s_fvfB[i] = fb[k];
+                    s_angB[i] = gb[k];
                     s_validB[i] = vb[k];
                 }
                 if (i < B.fv_n) s_nodesB[i] = nd[k];
@@ -341,6 +388,7 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
                     sdA[2 * i] = da[2 * k];
                     sdA[2 * i + 1] = da[2 * k + 1];
                     s_fvfA[i] = fa[k];
+                    s_angA[i] = ga[k];
                     s_validA[i] = va[k];
                 }
             }
@@ -353,6 +401,7 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
         s_npairs = 0;
     }
     __syncthreads();
+    BOW_T(1);
     if constexpr (kStage >= 1) {
         // the common direct-index nodes and their feature ranges, found by
         // every thread at once (one binary search each, over B's node ids in
@@ -366,6 +415,7 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
         }
         __syncthreads();
     }
+    BOW_T(2);
     auto fvfA = [&](int k) { return kStage == 2 ? s_fvfA[k] : A.fv_features[k]; };
     auto validA = [&](int i) { return kStage == 2 ? s_validA[i] != 0 : A.valid[i] != 0; };
     auto descA = [&](int i) {
@@ -374,6 +424,8 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
     auto fvfB = [&](int k) { return kStage ? s_fvfB[k] : B.fv_features[k]; };
     auto descB = [&](int i) { return kStage ? s_descB[i] : *reinterpret_cast<const ulonglong4*>(B.desc + 32 * (size_t)i); };
     auto validB = [&](int i) { return kStage ? s_validB[i] != 0 : B.valid[i] != 0; };
+    auto angA = [&](int i) { return kStage == 2 ? s_angA[i] : A.angle[i]; };
+    auto angB = [&](int i) { return kStage ? s_angB[i] : B.angle[i]; };
     auto sync_match = [&] {  // lane 0's match / vbMatched2 update visible to its row before the next A feature
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
@@ -421,13 +473,10 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
 #pragma unroll
             for (int c = 0; c < kRegC; ++c) {
                 const int j = r16 + kRow * c;
-                ok[c] = false;
-                if (j < nb) {
-                    const int ib = fvfB(b0 + j);
-                    cd[c] = descB(ib);
-                    ok[c] = mode == ORBGPU_BOW_KF_F ? match[ib] < 0
-                                                    : !(((s_used[ib >> 5] >> (ib & 31)) & 1u) || !validB(ib));
-                }
+                const int ib = fvfB(b0 + min(j, nb - 1));  // clamped: every slot loaded, unused ones flagged off
+                cd[c] = descB(ib);
+                ok[c] = j < nb && (mode == ORBGPU_BOW_KF_F ? match[ib] < 0
+                                                           : !(((s_used[ib >> 5] >> (ib & 31)) & 1u) || !validB(ib)));
             }
             for (int ia_ = a0; ia_ < a1; ++ia_) {
                 const int ia = fvfA(ia_);
@@ -435,25 +484,17 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
                 const ulonglong4 qa = descA(ia);
                 uint32_t k1 = 0xFFFFFFFFu, d2 = 0xFFFFu;
 #pragma unroll
-                for (int c = 0; c < kRegC; ++c) {
-                    if (!ok[c]) continue;
+                for (int c = 0; c < kRegC; ++c) {  // predicated: cd[] stays in registers
+                    if (c > 0 && !__any(r16 + kRow * c < nb)) break;  // no row of the wave has slot c
                     const uint32_t dist = __popcll(qa.x ^ cd[c].x) + __popcll(qa.y ^ cd[c].y) +
                                           __popcll(qa.z ^ cd[c].z) + __popcll(qa.w ^ cd[c].w);
-                    const uint32_t key = (dist << 16) | (uint32_t)(r16 + kRow * c);
-                    if (key < k1) {
-                        d2 = min(d2, k1 >> 16);
-                        k1 = key;
-                    } else {
-                        d2 = min(d2, dist);
-                    }
+                    const uint32_t key = ok[c] ? ((dist << 16) | (uint32_t)(r16 + kRow * c)) : 0xFFFFFFFFu;
+                    const uint32_t dm = ok[c] ? dist : 0xFFFFu;
+                    const bool lt = key < k1;
+                    d2 = min(d2, lt ? (k1 >> 16) : dm);
+                    k1 = lt ? key : k1;
                 }
-#pragma unroll
-                for (int o = 1; o < kRow; o <<= 1) {
-                    const uint32_t ok1 = (uint32_t)__shfl_xor((int)k1, o, kRow);
-                    const uint32_t od2 = (uint32_t)__shfl_xor((int)d2, o, kRow);
-                    d2 = min(min(d2, od2), max(k1 >> 16, ok1 >> 16));
-                    k1 = min(k1, ok1);
-                }
+                row8_best2(k1, d2);
                 const int best1 = k1 == 0xFFFFFFFFu ? 256 : (int)(k1 >> 16);
                 const int best2 = d2 >= 256u ? 256 : (int)d2;
                 const bool pass = mode == ORBGPU_BOW_KF_F ? best1 <= kThLow : best1 < kThLow;
@@ -474,7 +515,7 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
                         out = ia;
                     }
                     if (check_ori) {
-                        float rot = A.angle[ia] - B.angle[bidx];
+                        float rot = angA(ia) - angB(bidx);
                         if (rot < 0.0f) rot += 360.0f;
                         int bin = (int)roundf(rot * factor);
                         if (bin == kHL) bin = 0;
@@ -507,14 +548,7 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
                     d2 = min(d2, dist);
                 }
             }
-            // row reduction: xor 1, 2, 4 within the row's lanes
-#pragma unroll
-            for (int o = 1; o < kRow; o <<= 1) {
-                const uint32_t ok1 = (uint32_t)__shfl_xor((int)k1, o, kRow);
-                const uint32_t od2 = (uint32_t)__shfl_xor((int)d2, o, kRow);
-                d2 = min(min(d2, od2), max(k1 >> 16, ok1 >> 16));
-                k1 = min(k1, ok1);
-            }
+            row8_best2(k1, d2);  // row reduction within the row's 8 lanes
             const int best1 = k1 == 0xFFFFFFFFu ? 256 : (int)(k1 >> 16);
             const int best2 = d2 >= 256u ? 256 : (int)d2;
             const bool pass = mode == ORBGPU_BOW_KF_F ? best1 <= kThLow : best1 < kThLow;
@@ -531,7 +565,7 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
                     out = ia;
                 }
                 if (check_ori) {
-                    float rot = A.angle[ia] - B.angle[bidx];
+                    float rot = angA(ia) - angB(bidx);
                     if (rot < 0.0f) rot += 360.0f;
                     int bin = (int)roundf(rot * factor);
                     if (bin == kHL) bin = 0;
@@ -542,7 +576,9 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
             sync_match();
         }
     }
+    BOW_T(8);  // slots 8..11: each wave's end of the node walk
     __syncthreads();
+    BOW_T(3);
     if (check_ori && threadIdx.x == 0) {  // ComputeThreeMaxima (ORBmatcher.cpp:1792-1833)
         int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
         for (int i = 0; i < kHL; ++i) {
@@ -568,10 +604,21 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(int mode, const orbg
         }
         match_out[i] = m;
     }
-    atomicAdd(&s_cnt, cnt);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&s_cnt, cnt);  // one LDS atomic per wave, not per thread
     __syncthreads();
     if (threadIdx.x == 0) nmatches[blockIdx.x] = s_cnt;
+#ifdef BOW_STAMPS
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_bow_stamps[30] = __builtin_amdgcn_s_memtime();
+#endif
 }
+
+#ifdef BOW_STAMPS
+extern "C" int orbgpu_debug_bow_stamps(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bow_stamps), sizeof(g_bow_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 // ComputeThreeMaxima (ORBmatcher.cpp:1792-1833) over s_hist into s_ind[3]
 __device__ inline void three_maxima(const int* s_hist, int* s_ind) {
@@ -806,13 +853,13 @@ hipError_t launch_search_by_bow(int mode, int batch, const orbgpu_bow_frame* a, 
     }();
     if (attr != hipSuccess) return attr;
     if (bow_stage_bytes(stride, 2) <= (size_t)kBowStageMaxLds)
-        hipLaunchKernelGGL(search_by_bow_kernel<2>, dim3(batch), dim3(256), bow_stage_bytes(stride, 2), stream, mode,
+        hipLaunchKernelGGL(search_by_bow_kernel<2>, dim3(batch), dim3(kBowThreads), bow_stage_bytes(stride, 2), stream, mode,
                            a, b, nnratio, check_ori, stride, match, nmatches);
     else if (bow_stage_bytes(stride, 1) <= (size_t)kBowStageMaxLds)
-        hipLaunchKernelGGL(search_by_bow_kernel<1>, dim3(batch), dim3(256), bow_stage_bytes(stride, 1), stream, mode,
+        hipLaunchKernelGGL(search_by_bow_kernel<1>, dim3(batch), dim3(kBowThreads), bow_stage_bytes(stride, 1), stream, mode,
                            a, b, nnratio, check_ori, stride, match, nmatches);
     else
-        hipLaunchKernelGGL(search_by_bow_kernel<0>, dim3(batch), dim3(256), 0, stream, mode, a, b, nnratio,
+        hipLaunchKernelGGL(search_by_bow_kernel<0>, dim3(batch), dim3(kBowThreads), 0, stream, mode, a, b, nnratio,
                            check_ori, stride, match, nmatches);
     return hipGetLastError();
 }

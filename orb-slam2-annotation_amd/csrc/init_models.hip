@@ -66,9 +66,24 @@ __global__ __launch_bounds__(kNormThreads) void init_normalize_kernel(const floa
     for (int pass = 0; pass < 2; ++pass) {
         for (int base = 0; base < nmax; base += kNormChunk) {
             __syncthreads();  // the previous chunk is consumed
-            for (int i = tid; i < 2 * kNormChunk; i += kNormThreads) {
-                const int f = i / kNormChunk, j = i - f * kNormChunk, idx = base + j;
-                if (idx < (f ? n2 : n1)) s_kp[f][j] = reinterpret_cast<const float2*>(f ? kp2 : kp1)[idx];
+            // eight loads per thread in flight before any store (a copy loop
+            // waited one memory latency per element)
+            for (int i0 = tid; i0 < 2 * kNormChunk; i0 += 8 * kNormThreads) {
+                float2 v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int i = i0 + k * kNormThreads;
+                    const int f = i / kNormChunk, j = i - f * kNormChunk, idx = base + j;
+                    const int nf = f ? n2 : n1;
+                    v[k] = (i < 2 * kNormChunk && idx < nf) ? reinterpret_cast<const float2*>(f ? kp2 : kp1)[idx]
+                                                            : make_float2(0.f, 0.f);
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int i = i0 + k * kNormThreads;
+                    const int f = i / kNormChunk, j = i - f * kNormChunk;
+                    if (i < 2 * kNormChunk && base + j < (f ? n2 : n1)) s_kp[f][j] = v[k];
+                }
             }
             __syncthreads();
             if (tid < 4) {
@@ -106,11 +121,15 @@ __global__ __launch_bounds__(kNormThreads) void init_normalize_kernel(const floa
         s_scale[tid] = (float)(1.0 / (double)acc);  // float sX = 1.0/meanDevX
     }
     __syncthreads();
+    // the normalised points: from the staged keypoints when each frame fit
+    // one chunk (still in LDS), else re-read
+    const bool staged = nmax <= kNormChunk;
     for (int i = tid; i < n1 + n2; i += kNormThreads) {
         const int fr = i >= n1, j = fr ? i - n1 : i;
         const float* k = fr ? kp2 : kp1;
-        const float x = __fmul_rn(__fsub_rn(k[2 * j], s_mean[2 * fr]), s_scale[2 * fr]);
-        const float y = __fmul_rn(__fsub_rn(k[2 * j + 1], s_mean[2 * fr + 1]), s_scale[2 * fr + 1]);
+        const float2 p = staged ? s_kp[fr][j] : make_float2(k[2 * j], k[2 * j + 1]);
+        const float x = __fmul_rn(__fsub_rn(p.x, s_mean[2 * fr]), s_scale[2 * fr]);
+        const float y = __fmul_rn(__fsub_rn(p.y, s_mean[2 * fr + 1]), s_scale[2 * fr + 1]);
         work[2 * i] = x;
         work[2 * i + 1] = y;
     }
@@ -124,7 +143,9 @@ __global__ __launch_bounds__(kNormThreads) void init_normalize_kernel(const floa
     if (pts)
         for (int m = tid; m < nm; m += kNormThreads) {
             const int a = pairs[2 * m], b = pairs[2 * m + 1];
-            pts[m] = make_float4(kp1[2 * a], kp1[2 * a + 1], kp2[2 * b], kp2[2 * b + 1]);
+            const float2 p1 = staged ? s_kp[0][a] : make_float2(kp1[2 * a], kp1[2 * a + 1]);
+            const float2 p2 = staged ? s_kp[1][b] : make_float2(kp2[2 * b], kp2[2 * b + 1]);
+            pts[m] = make_float4(p1.x, p1.y, p2.x, p2.y);
         }
 }
 

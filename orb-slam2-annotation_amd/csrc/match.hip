@@ -50,16 +50,6 @@ __device__ inline int wave_min_i(int v) {
     return v;
 }
 
-// number of leading octave-0 keypoints
-__device__ int level0_count(const orbgpu_keypoint* k, int n) {
-    int lo = 0, hi = n;  // first index with octave != 0
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (k[mid].octave == 0) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-}
-
 constexpr int kMatchThreads = 256;
 constexpr int kTopK = 4;  // best candidate keys kept per query by the parallel phase
 
@@ -131,7 +121,41 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     // a larger variant only takes the pairs the previous one handed over
     if (kMaxK0 == kMaxK0Large && nmatches_out[b] != kNeedLarge) return;
     if (kMaxK0 == kMaxK0Huge && nmatches_out[b] != kNeedHuge) return;
-    const int n10 = level0_count(K1, n1), n20 = level0_count(K2, n2);
+    // level-0 counts (the leading octave-0 run of each list, extractor order)
+    // counted by the whole block, four loads per thread in flight (a binary
+    // search was ten dependent global loads on every thread's path)
+    __shared__ int s_l0[2];
+    if (tid < 2) s_l0[tid] = 0;
+    __syncthreads();
+    {
+        int c1 = 0, c2 = 0;
+        const int nmax = max(n1, n2);
+        for (int base = tid; base < nmax; base += 4 * kMatchThreads) {
+            int o1[4], o2[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = base + k * kMatchThreads;
+                o1[k] = i < n1 ? K1[i].octave : 1;
+                o2[k] = i < n2 ? K2[i].octave : 1;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                c1 += o1[k] == 0;
+                c2 += o2[k] == 0;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            c1 += __shfl_xor(c1, o, 64);
+            c2 += __shfl_xor(c2, o, 64);
+        }
+        if (lane == 0) {
+            atomicAdd(&s_l0[0], c1);
+            atomicAdd(&s_l0[1], c2);
+        }
+    }
+    __syncthreads();
+    const int n10 = s_l0[0], n20 = s_l0[1];
     if (n10 > kMaxK0 || n20 > kMaxK0) {
         // per-pair status: retried by the next variant, or -1 (capacity
         // exceeded); no match is reported for the pair
@@ -446,11 +470,13 @@ hipError_t launch_match_init(int batch, float minX, float maxX, float minY, floa
                              const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,
                              const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2, size_t stride2,
                              float* prev_xy, int window, float nnratio, int flags,
-                             int* matches12, int* nmatches, hipStream_t stream) {
+                             int* matches12, int* nmatches, hipStream_t stream, size_t level0_bound) {
     // small variant for every pair, then the larger ones for the pairs handed
     // over (a no-op block per other pair); a larger variant is launched only
-    // when a frame's capacity (stride) can exceed the previous limit
-    const size_t cap = stride1 > stride2 ? stride1 : stride2;
+    // when a frame's level-0 keypoints can exceed the previous limit: bounded
+    // by its capacity (stride), or by level0_bound when the caller knows it
+    // (the host form counts them)
+    const size_t cap = level0_bound ? level0_bound : (stride1 > stride2 ? stride1 : stride2);
     hipLaunchKernelGGL(match_init_kernel<kMaxK0Small>, dim3(batch), dim3(kMatchThreads), 0, stream, minX, maxX, minY,
                        maxY, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags,
                        matches12, nmatches);

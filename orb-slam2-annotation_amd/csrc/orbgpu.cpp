@@ -812,9 +812,19 @@ int orbgpu_search_for_initialization(orbgpu_grid_bounds bd, const orbgpu_keypoin
         dp = prev_xy ? A.inout(prev_xy, 2 * (size_t)n1, 2 * n1c) : nullptr;
     });
     if (rc) return rc;
-    rc = orbgpu_search_for_initialization_batch_device(1, bd, dk1, dd1, dn, n1c, dk2, dd2, dn + 1, n2c, dp,
-                                                       window, nnratio, flags, dm, dn + 2, ctx->stream);
-    if (rc) return rc;
+    // the number of level-0 keypoints bounds which matcher variants can be
+    // needed, so a 1000-feature frame (~220 at level 0) takes one launch, not
+    // one per variant (all octave-0 entries are counted: an upper bound of the
+    // leading run the kernel uses, whatever the order)
+    auto level0 = [](const orbgpu_keypoint* k, int n) {
+        int c = 0;
+        for (int i = 0; i < n; ++i) c += k[i].octave == 0;
+        return c;
+    };
+    const size_t n0 = (size_t)std::max(std::max(level0(kps1, n1), level0(kps2, n2)), 1);
+    if (!(bd.max_x > bd.min_x) || !(bd.max_y > bd.min_y)) return fail(ORBGPU_ERR_ARG, "invalid argument");
+    ORB_HIP(launch_match_init(1, bd.min_x, bd.max_x, bd.min_y, bd.max_y, dk1, dd1, dn, n1c, dk2, dd2, dn + 1, n2c, dp,
+                              window, nnratio, flags, dm, dn + 2, ctx->stream, n0));
     call.fetch(dm, matches12, (size_t)n1 * sizeof(int));
     call.fetch(dn + 2, nmatches, sizeof(int));
     if (prev_xy) call.fetch(dp, prev_xy, (size_t)n1 * 2 * sizeof(float));
