@@ -40,7 +40,9 @@ __host__ __device__ void sym_eig_desc(double* a, double* w, double* ut) {
             for (int j = i + 1; j < N; ++j) off += a[i * N + j] * a[i * N + j];
         }
         if (off <= 1e-32 * diag || off == 0.0) break;
+#pragma unroll
         for (int p = 0; p < N - 1; ++p)
+#pragma unroll
             for (int q = p + 1; q < N; ++q) {
                 const double apq = a[p * N + q];
                 if (fabs(apq) < 1e-300) continue;
@@ -64,21 +66,23 @@ __host__ __device__ void sym_eig_desc(double* a, double* w, double* ut) {
                 }
             }
     }
-    int order[N];
-    for (int i = 0; i < N; ++i) order[i] = i;
-    for (int i = 1; i < N; ++i) {  // insertion sort by descending eigenvalue
-        const int o = order[i];
-        int j = i - 1;
-        while (j >= 0 && a[order[j] * N + order[j]] < a[o * N + o]) {
-            order[j + 1] = order[j];
-            --j;
-        }
-        order[j + 1] = o;
-    }
-    for (int r = 0; r < N; ++r) {
-        const int c = order[r];
-        w[r] = a[c * N + c];
-        for (int k = 0; k < N; ++k) ut[r * N + k] = v[k * N + c];
+    // descending by eigenvalue, stable (the order of an insertion sort that
+    // moves an entry before strictly smaller ones): column c goes to rank
+    // #{j : w_j > w_c} + #{j < c : w_j == w_c}; selected with constant
+    // indices only (a dynamic order[] put a, v, w and ut in scratch memory)
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+        int rank = 0;
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            rank += (a[j * N + j] > a[c * N + c]) || (j < c && a[j * N + j] == a[c * N + c]);
+#pragma unroll
+        for (int r = 0; r < N; ++r)
+            if (rank == r) {
+                w[r] = a[c * N + c];
+#pragma unroll
+                for (int k = 0; k < N; ++k) ut[r * N + k] = v[k * N + c];
+            }
     }
 }
 
@@ -93,9 +97,13 @@ __host__ __device__ void svd_hestenes(double* a, double* s, double* v) {
     const double negl = kJacobiNegl * fro;
     for (int sweep = 0; sweep < 60; ++sweep) {
         bool rotated = false;
+        // fully unrolled (device): constant indices keep a and v in registers
+#pragma unroll
         for (int p = 0; p < N - 1; ++p)
+#pragma unroll
             for (int q = p + 1; q < N; ++q) {
                 double alpha = 0.0, beta = 0.0, gamma = 0.0;
+#pragma unroll
                 for (int k = 0; k < M; ++k) {
                     alpha += a[k * N + p] * a[k * N + p];
                     beta += a[k * N + q] * a[k * N + q];
@@ -104,11 +112,13 @@ __host__ __device__ void svd_hestenes(double* a, double* s, double* v) {
                 double c, sn;
                 if (!jacobi_rot(alpha, beta, gamma, negl, c, sn)) continue;
                 rotated = true;
+#pragma unroll
                 for (int k = 0; k < M; ++k) {
                     const double x = a[k * N + p], y = a[k * N + q];
                     a[k * N + p] = c * x - sn * y;
                     a[k * N + q] = sn * x + c * y;
                 }
+#pragma unroll
                 for (int k = 0; k < N; ++k) {
                     const double x = v[k * N + p], y = v[k * N + q];
                     v[k * N + p] = c * x - sn * y;

@@ -76,7 +76,7 @@ struct CallPose {
     bool forward, backward;
 };
 
-__device__ inline CallPose call_pose(const orbgpu_proj_call& C) {
+__device__ __forceinline__ CallPose call_pose(const orbgpu_proj_call& C) {
     CallPose cp{};
     const orbgpu_proj_target& T = C.target;
     const float* Tcw = T.Tcw;
@@ -111,7 +111,7 @@ __device__ inline CallPose call_pose(const orbgpu_proj_call& C) {
 // Every point field the variant reads is loaded up front, independent of the
 // flags, so a point costs one memory latency; sf = the target's scale
 // factors (16 entries, in LDS).
-__device__ inline Query make_query(const orbgpu_proj_call& C, const CallPose& cp, const float* sf, int ip) {
+__device__ __forceinline__ Query make_query(const orbgpu_proj_call& C, const CallPose& cp, const float* sf, int ip) {
     const orbgpu_proj_target& T = C.target;
     const orbgpu_proj_points& P = C.points;
     const int variant = C.variant;
@@ -295,7 +295,7 @@ __device__ inline int key_pos(unsigned k) { return (int)(k & 0xFFFu); }
 // over its column runs (candidate f to lane f % G), and call visit(key) for
 // every candidate that passes.
 template <int G, class Visit>
-__device__ inline void scan_candidates(const orbgpu_proj_call& C, const Query& q, int ip, const Grid& g, float invW,
+__device__ __forceinline__ void scan_candidates(const orbgpu_proj_call& C, const Query& q, int ip, const Grid& g, float invW,
                                        float invH, int sl, Visit&& visit) {
     const orbgpu_proj_target& T = C.target;
     const int cx0 = max(0, (int)floorf((q.u - T.min_x - q.r) * invW));

@@ -41,23 +41,30 @@ __device__ __forceinline__ void dominant_eigvec4(const float Nf[16], double v_ou
             for (int j = i + 1; j < 4; ++j) off += a[i][j] * a[i][j];
         }
         if (off <= 1e-30 * (diag + 1e-300)) break;
+        // fully unrolled: every a[][] / v[][] index is a constant, so the
+        // matrices stay in registers (a loop over (p, q) put them in scratch)
+#pragma unroll
         for (int p = 0; p < 3; ++p)
+#pragma unroll
             for (int q = p + 1; q < 4; ++q) {
                 const double apq = a[p][q];
                 if (apq == 0.0) continue;
                 const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
                 const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
                 const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+#pragma unroll
                 for (int k = 0; k < 4; ++k) {  // A <- J^T A J
                     const double akp = a[k][p], akq = a[k][q];
                     a[k][p] = c * akp - s * akq;
                     a[k][q] = s * akp + c * akq;
                 }
+#pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const double apk = a[p][k], aqk = a[q][k];
                     a[p][k] = c * apk - s * aqk;
                     a[q][k] = s * apk + c * aqk;
                 }
+#pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const double vkp = v[k][p], vkq = v[k][q];
                     v[k][p] = c * vkp - s * vkq;
@@ -66,9 +73,15 @@ __device__ __forceinline__ void dominant_eigvec4(const float Nf[16], double v_ou
             }
     }
     int best = 0;
+    double dbest = a[0][0];
+#pragma unroll
     for (int i = 1; i < 4; ++i)
-        if (a[i][i] > a[best][best]) best = i;
-    for (int k = 0; k < 4; ++k) v_out[k] = v[k][best];
+        if (a[i][i] > dbest) {
+            best = i;
+            dbest = a[i][i];
+        }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v_out[k] = best == 0 ? v[k][0] : best == 1 ? v[k][1] : best == 2 ? v[k][2] : v[k][3];
 }
 
 // ComputeSim3 (Sim3Solver.cpp:225-327); P1[k], P2[k] = point k (xyz)
