@@ -360,6 +360,63 @@ void fundamental_hyps(const float* F21, const float* K, std::vector<RecHyp>& hy)
     }
 }
 
+// FindHomography / FindFundamental's choice of the kept iteration for both
+// models (`if (currentScore > score)` from score = 0: the first maximum among
+// scores > 0, NaN never kept; Initializer.cpp:160-269), then the kept models
+// and their inlier flags packed for ONE read-back: out = {bh, bf, SH bits, SF
+// bits, H21[9], F21[9], inliersH[N], inliersF[N]} (zeros for -1).
+struct PickKey {
+    float v;
+    int i;
+};
+__device__ inline PickKey pick_better(PickKey a, PickKey b) {
+    return (b.v > a.v || (b.v == a.v && b.i >= 0 && (a.i < 0 || b.i < a.i))) ? b : a;
+}
+__global__ __launch_bounds__(256) void init_pick_kernel(const float* __restrict__ sh, const float* __restrict__ sf,
+                                                        int it, const float* __restrict__ h21,
+                                                        const float* __restrict__ f21, const uint8_t* __restrict__ ih,
+                                                        const uint8_t* __restrict__ iff, int N,
+                                                        uint8_t* __restrict__ out) {
+    __shared__ PickKey s_k[2][4];
+    __shared__ int s_best[2];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int m = 0; m < 2; ++m) {
+        const float* sc = m ? sf : sh;
+        PickKey k{0.f, -1};
+        for (int h = tid; h < it; h += 256) {
+            const float v = sc[h];
+            if (v > k.v) k = PickKey{v, h};  // strided ascending: the thread's first maximum
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const PickKey q{__shfl_xor(k.v, o, 64), __shfl_xor(k.i, o, 64)};
+            k = pick_better(k, q);
+        }
+        if (lane == 0) s_k[m][wave] = k;
+    }
+    __syncthreads();
+    if (tid < 2) {
+        PickKey k = s_k[tid][0];
+        for (int w = 1; w < 4; ++w) k = pick_better(k, s_k[tid][w]);
+        s_best[tid] = k.i;
+        int* hdr = reinterpret_cast<int*>(out);
+        hdr[tid] = k.i;
+        hdr[2 + tid] = __float_as_int(k.i >= 0 ? k.v : 0.f);
+    }
+    __syncthreads();
+    const int bh = s_best[0], bf = s_best[1];
+    float* mo = reinterpret_cast<float*>(out + 16);
+    if (tid < 18) {
+        const int m = tid / 9, k = tid - 9 * m, b = m ? bf : bh;
+        mo[tid] = b >= 0 ? (m ? f21 : h21)[9 * (size_t)b + k] : 0.f;
+    }
+    uint8_t* fl = out + 16 + 72;
+    for (int i = tid; i < 2 * N; i += 256) {
+        const int m = i >= N, j = m ? i - N : i, b = m ? bf : bh;
+        fl[i] = b >= 0 ? (m ? iff : ih)[(size_t)b * N + j] : 0;
+    }
+}
+
 }  // namespace
 
 }  // namespace orbgpu
@@ -543,8 +600,9 @@ extern "C" int orbgpu_init_initialize(const float* kp1, int n1, const float* kp2
     void* d_work;
     orbgpu_match_pts* d_pts;
     float *d_h21, *d_h12, *d_f21, *d_sh, *d_sf;
-    uint8_t *d_ih, *d_if;
+    uint8_t *d_ih, *d_if, *d_pick;
     const size_t it = (size_t)iterations;
+    const size_t pick_b = 16 + 72 + 2 * (size_t)N;  // init_pick_kernel's packed read-back
     rc = call.run([&](HostCall& A) {
         d_kp1 = A.inout(kp1, 2 * (size_t)n1, 2 * (size_t)std::max(n1, 1));
         d_kp2 = A.inout(kp2, 2 * (size_t)n2, 2 * (size_t)std::max(n2, 1));
@@ -559,6 +617,7 @@ extern "C" int orbgpu_init_initialize(const float* kp1, int n1, const float* kp2
         d_sf = A.out<float>(it);
         d_ih = A.out<uint8_t>(it * N);
         d_if = A.out<uint8_t>(it * N);
+        d_pick = A.out<uint8_t>(pick_b);
     });
     if (rc) return rc;
     // FindHomography / FindFundamental (:160-269): every iteration's hypotheses and scores
@@ -568,24 +627,28 @@ extern "C" int orbgpu_init_initialize(const float* kp1, int n1, const float* kp2
         rc = orbgpu_init_check_both_batch_device(d_pts, N, d_h21, d_h12, iterations, d_f21, iterations, sigma, d_sh,
                                                  d_ih, d_sf, d_if, ctx->stream);
     if (rc) return rc;
-    std::vector<float> sh(iterations), sf(iterations);
-    call.fetch(d_sh, sh.data(), 4 * it);
-    call.fetch(d_sf, sf.data(), 4 * it);
+    // the kept iteration of both models, their matrices and inlier flags in
+    // one read-back (init_pick_kernel; the host chose between them after a
+    // first read-back of all scores before)
+    hipLaunchKernelGGL(init_pick_kernel, dim3(1), dim3(256), 0, ctx->stream, d_sh, d_sf, iterations, d_h21, d_f21,
+                       d_ih, d_if, N, d_pick);
+    ORB_HIP(hipGetLastError());
+    std::vector<uint8_t> pick(pick_b);
+    call.fetch(d_pick, pick.data(), pick_b);
     if ((rc = call.finish())) return rc;
-    int bh = -1, bf = -1;
-    if ((rc = orbgpu_init_select_best(sh.data(), iterations, &bh))) return rc;
-    if ((rc = orbgpu_init_select_best(sf.data(), iterations, &bf))) return rc;
-    const float SH = bh >= 0 ? sh[bh] : 0.f, SF = bf >= 0 ? sf[bf] : 0.f;
+    int hdr[4];
+    std::memcpy(hdr, pick.data(), 16);
+    const int bh = hdr[0], bf = hdr[1];
+    float SH, SF;
+    std::memcpy(&SH, &hdr[2], 4);
+    std::memcpy(&SF, &hdr[3], 4);
     const float RH = SH / (SH + SF);  // :140 (NaN when both are 0: ReconstructF, as the reference)
     const bool useH = RH > 0.40;
-    float M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    std::vector<unsigned char> inl(N, 0);
+    float M[9];
+    std::memcpy(M, pick.data() + 16 + (useH ? 0 : 36), 36);
+    std::vector<unsigned char> inl(pick.begin() + 16 + 72 + (useH ? 0 : N), pick.begin() + 16 + 72 + (useH ? N : 2 * N));
     const int best = useH ? bh : bf;
-    if (best >= 0) {  // the kept model and its inlier flags (a second, small read-back)
-        call.fetch((useH ? d_h21 : d_f21) + 9 * (size_t)best, M, 36);
-        call.fetch((useH ? d_ih : d_if) + (size_t)best * N, inl.data(), (size_t)N);
-        if ((rc = call.finish())) return rc;
-    }
+    (void)best;
     *rh = RH;
     *model = useH ? ORBGPU_INIT_MODEL_H : ORBGPU_INIT_MODEL_F;
     // (no kept iteration: the reference reconstructs from an empty H/F with no inliers -> false)
