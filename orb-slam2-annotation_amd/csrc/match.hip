@@ -83,6 +83,16 @@ __device__ inline int key_j(uint32_t key) { return (int)(key & kKeyJMask); }
 //    lane.  A list that runs out is exact when its last key bounds
 //    bestDist2 from below far enough for the ratio test; otherwise the
 //    query is re-scanned by the whole wave against the live state (rare).
+#ifdef MATCH_STAMPS  // diagnostic build only: phase stamps of block 0 (tools/match_stamps.py)
+__device__ unsigned long long g_match_stamps[16];
+#define MSTAMP(k)                                                                              \
+    do {                                                                                       \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_match_stamps[k] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define MSTAMP(k) ((void)0)
+#endif
+
 template <int kMaxK0>
 __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     float minX, float maxX, float minY, float maxY, const orbgpu_keypoint* __restrict__ kps1,
@@ -96,7 +106,10 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     __shared__ int s_mdist[kMaxK0];          // vMatchedDistance
     __shared__ int s_m21[kMaxK0];            // vnMatches21
     constexpr bool kDescHbm = kMaxK0 > kMaxK0Large;  // F2's descriptors stay in HBM (L2-resident)
-    __shared__ unsigned long long s_d2[kDescHbm ? 1 : kMaxK0][4];
+    // F2's descriptors as four planes (word q of keypoint j at s_d2[q][j]): a
+    // 32-byte row per keypoint put every lane's 8-byte read of a random j on
+    // the same 4 of the 32 banks (16-way conflicts on every candidate)
+    __shared__ unsigned long long s_d2[4][kDescHbm ? 1 : kMaxK0];
     __shared__ int s_m12[kMaxK0];            // vnMatches12 for F1 level-0
     __shared__ float s_px[kMaxK0], s_py[kMaxK0], s_ang1[kMaxK0];  // F1: vbPrevMatched, angle
     __shared__ uint32_t s_top[kMaxK0][kTopK];
@@ -111,6 +124,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.x;
+    MSTAMP(0);
     const orbgpu_keypoint* K1 = kps1 + (size_t)b * stride1;
     const orbgpu_keypoint* K2 = kps2 + (size_t)b * stride2;
     const uint8_t* D1 = desc1 + (size_t)b * stride1 * 32;
@@ -155,6 +169,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
         }
     }
     __syncthreads();
+    MSTAMP(1);
     const int n10 = s_l0[0], n20 = s_l0[1];
     if (n10 > kMaxK0 || n20 > kMaxK0) {
         // per-pair status: retried by the next variant, or -1 (capacity
@@ -169,13 +184,14 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
         if constexpr (kDescHbm)
             return D2q[4 * j + q];
         else
-            return s_d2[j][q];
+            return s_d2[q][j];
     };
     // grid inverses (Frame.cpp:221-224)
     const float invW = __fdiv_rn((float)kGC, __fsub_rn(maxX, minX));
     const float invH = __fdiv_rn((float)kGR, __fsub_rn(maxY, minY));
     for (int c = tid; c < kCells; c += kMatchThreads) s_cend[c] = 0;
     __syncthreads();
+    MSTAMP(2);
     for (int j = tid; j < n20; j += kMatchThreads) {
         const float x = K2[j].x, y = K2[j].y;
         s_x[j] = x;
@@ -191,7 +207,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
         if (!kDescHbm) {
             const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D2 + (size_t)j * 32);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) s_d2[j][q] = d[q];
+            for (int q = 0; q < 4; ++q) s_d2[q][j] = d[q];
         }
     }
     for (int i = tid; i < n10; i += kMatchThreads) {
@@ -204,6 +220,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     if (tid < kHL) s_hist[tid] = 0;
     if (tid == 0) s_nm = 0;
     __syncthreads();
+    MSTAMP(3);
     {  // exclusive scan of the cell counts: thread t owns cells [12 t, 12 t + 12)
         constexpr int kPer = kCells / kMatchThreads;
         static_assert(kCells % kMatchThreads == 0, "cells per thread");
@@ -231,6 +248,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
             if (cell >= 0) s_cidx[atomicAdd(&s_cend[cell], 1)] = (unsigned short)j;  // start -> end
         }
         __syncthreads();
+    MSTAMP(4);
     }
 
     const float r = (float)window;
@@ -286,6 +304,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
         s_ncand[i1] = ncand;
     }
     __syncthreads();
+    MSTAMP(5);
 
     // phase 2 (wave 0, wave-uniform control): batches of 64 queries
     if (wave == 0) {
@@ -399,6 +418,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
         }
     }
     __syncthreads();
+    MSTAMP(6);
     if (flags & ORBGPU_MATCH_CHECK_ORI) {
         // rotHist (ORBmatcher.cpp:541-552): one entry per query matched when the loop reached it
         const float factor =
@@ -446,6 +466,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     if (lane == 0) atomicAdd(&s_nm, nmatches);
     __syncthreads();
     if (tid == 0) nmatches_out[b] = s_nm;
+    MSTAMP(8);
 }
 
 __global__ __launch_bounds__(256) void hamming_pairs_kernel(const uint8_t* __restrict__ a,
@@ -459,6 +480,12 @@ __global__ __launch_bounds__(256) void hamming_pairs_kernel(const uint8_t* __res
 }
 
 }  // namespace
+
+#ifdef MATCH_STAMPS
+extern "C" int orbgpu_debug_match_stamps(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_match_stamps), sizeof(g_match_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 hipError_t launch_hamming_pairs(const uint8_t* a, const uint8_t* b, int n, int* dist, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
