@@ -14,6 +14,8 @@
 // GetFeaturesInArea order (cell ix outer, iy inner, index) -- and a second
 // reduction for bestDist2.  The rotation histogram, ComputeThreeMaxima and
 // the cull run on the same wave.
+#include <type_traits>
+
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
 #include "../../include/orbgpu.h"
@@ -50,7 +52,7 @@ __device__ inline int wave_min_i(int v) {
     return v;
 }
 
-constexpr int kMatchThreads = 256;
+constexpr int kMatchThreads = 1024;
 constexpr int kTopK = 4;  // best candidate keys kept per query by the parallel phase
 
 // (dist, grid order) of a candidate as one ordered key: dist <= 256 (9 bits),
@@ -268,19 +270,36 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
         return fabsf(__fsub_rn(s_x[j], x)) < r && fabsf(__fsub_rn(s_y[j], y)) < r;
     };
 
-    // phase 1: per-query candidate lists (no dependence on the match state)
-    for (int i1 = tid; i1 < n10; i1 += kMatchThreads) {
-        const float x = s_px[i1], y = s_py[i1];
-        int cx0, cx1, cy0, cy1;
+    // phase 1: per-query candidate lists (no dependence on the match state).
+    // Four lanes per query (an aligned quad): lane sl walks the window's grid
+    // columns cx0 + sl, cx0 + sl + 4, ..., keeping its own sorted top-4 and
+    // count; the quad then merges by rank through DPP quad permutations (keys
+    // are distinct: they carry the keypoint index).  The walk is a chain of
+    // dependent LDS reads; one lane per query on four waves ran ~20 columns
+    // and ~30 candidates in series (73 k cycles per 1000-feature pair,
+    // tools/match_stamps.py); the 1024-thread block runs a pair's ~220
+    // queries in one pass of 16 waves, each lane a quarter of a window.
+    constexpr int kSub = 4;
+    auto quad = [](uint32_t v, auto ctrl) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, decltype(ctrl)::value, 0xF, 0xF, false);
+    };
+    using QX1 = std::integral_constant<int, 0xB1>;  // quad_perm [1,0,3,2]
+    using QX2 = std::integral_constant<int, 0x4E>;  // quad_perm [2,3,0,1]
+    using QX3 = std::integral_constant<int, 0x1B>;  // quad_perm [3,2,1,0]
+    for (int qbase = 0; qbase < n10; qbase += kMatchThreads / kSub) {
+        const int i1 = qbase + tid / kSub, sl = tid % kSub;
+        const bool act = i1 < n10;
         int ncand = -1;
         uint32_t top[kTopK];
 #pragma unroll
         for (int k = 0; k < kTopK; ++k) top[k] = 0xFFFFFFFFu;
-        if (cell_range(x, y, cx0, cx1, cy0, cy1)) {
+        const float x = act ? s_px[i1] : 0.f, y = act ? s_py[i1] : 0.f;
+        int cx0, cx1, cy0, cy1;
+        if (act && cell_range(x, y, cx0, cx1, cy0, cy1)) {
             ncand = 0;
             const unsigned long long* d = reinterpret_cast<const unsigned long long*>(D1 + (size_t)i1 * 32);
             const unsigned long long q0 = d[0], q1 = d[1], q2 = d[2], q3 = d[3];
-            for (int ix = cx0; ix <= cx1; ++ix) {
+            for (int ix = cx0 + sl; ix <= cx1; ix += kSub) {
                 const int c0 = ix * kGR + cy0;
                 const int lo = c0 > 0 ? s_cend[c0 - 1] : 0, hi = s_cend[ix * kGR + cy1];
                 for (int p = lo; p < hi; ++p) {
@@ -299,9 +318,32 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
                 }
             }
         }
+        // quad merge (every lane takes part: DPP reads its quad's lanes)
+        uint32_t o1[kTopK], o2[kTopK], o3[kTopK];
 #pragma unroll
-        for (int k = 0; k < kTopK; ++k) s_top[i1][k] = top[k];
-        s_ncand[i1] = ncand;
+        for (int k = 0; k < kTopK; ++k) {
+            o1[k] = quad(top[k], QX1{});
+            o2[k] = quad(top[k], QX2{});
+            o3[k] = quad(top[k], QX3{});
+        }
+        int tot = ncand;  // -1 on all four lanes when the window is off the grid
+        tot += (int)quad((uint32_t)tot, QX1{});
+        tot += (int)quad((uint32_t)tot, QX2{});
+        if (act) {
+            if (sl == 0) {
+#pragma unroll
+                for (int k = 0; k < kTopK; ++k) s_top[i1][k] = 0xFFFFFFFFu;
+                s_ncand[i1] = ncand < 0 ? -1 : tot;
+            }
+#pragma unroll
+            for (int k = 0; k < kTopK; ++k) {
+                if (top[k] == 0xFFFFFFFFu) continue;
+                int rank = k;
+#pragma unroll
+                for (int t = 0; t < kTopK; ++t) rank += (o1[t] < top[k]) + (o2[t] < top[k]) + (o3[t] < top[k]);
+                if (rank < kTopK) s_top[i1][rank] = top[k];
+            }
+        }
     }
     __syncthreads();
     MSTAMP(5);
