@@ -13,6 +13,10 @@ for s in sorted(d.glob("*.s")):
         if pat not in name:
             continue
         get = lambda k: (re.search(rf"\.{k}:\s+(\d+)", body) or [None, "?"])[1]  # noqa: E731
+        # static LDS lives in the kernel descriptor (.amdhsa_group_segment_fixed_size)
+        km = re.search(r"\.amdhsa_kernel " + re.escape(name) + r"\n(.*?)\.end_amdhsa_kernel", txt, re.S)
+        lds = (re.search(r"\.amdhsa_group_segment_fixed_size (\d+)", km.group(1)) if km else None)
+        lds = lds.group(1) if lds else "?"
         print(f"{s.stem:18s} {name[:70]:70s} vgpr={get('vgpr_count'):>4} agpr={get('agpr_count'):>3} "
               f"sgpr={get('sgpr_count'):>3} scratch={get('private_segment_fixed_size'):>5} "
-              f"lds={get('group_segment_fixed_size'):>6}")
+              f"lds={lds:>6} (static; dynamic LDS is set at launch)")
