@@ -482,9 +482,18 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
         s_isig[tid] = 1.0f / (sfl * sfl);  // mvInvLevelSigma2 = 1 / (s * s) (ORBextractor.cpp:428-433)
     }
     if (tid == 0) s_nm = 0;
-    if (desc_lds) {  // the descriptors, 16 bytes per thread and step
-        const uint4* gd = reinterpret_cast<const uint4*>(T.desc);
-        for (int i = tid; i < 2 * n; i += kProjThreads) s_desc[i] = gd[i];
+    if (desc_lds) {  // the descriptors, 16 bytes per piece, four pieces per thread in flight before any store
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));  // (arrays of HIP's uint4 land in scratch)
+        const v4u* gd = reinterpret_cast<const v4u*>(T.desc);
+        v4u* sd = reinterpret_cast<v4u*>(s_desc);
+        for (int i0 = tid; i0 < 2 * n; i0 += 4 * kProjThreads) {
+            v4u v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = gd[min(i0 + k * kProjThreads, 2 * n - 1)];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (i0 + k * kProjThreads < 2 * n) sd[i0 + k * kProjThreads] = v[k];
+        }
     }
     __syncthreads();
     constexpr int kPer = kMaxKps / kProjThreads;
