@@ -587,7 +587,52 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
             l[5 * i + 3] = ap == 0 ? Lr[6] : ap == 1 ? 0.0 : Lr[3];
             l[5 * i + 4] = ap == 2 ? Lr[4] : 0.0;
         }
-        svd_solve<6, 5>(l, rho, b5);
+        if (G == 64 && jac != nullptr) {
+            // Refine: each row's 6 x 5 solve on its own 12 lanes (three 4-lane
+            // column pairs per round-robin round, jacobi_lds.h), A and V in
+            // LDS -- rows 0..2 in the 12 x 12 decomposition's area, row 3 (a
+            // duplicate of approximation 3) in the consumed M^T M area; on one
+            // lane each the sequential Jacobi took ~55 k cycles
+            using JB = JacobiLds<5, 6, 4, 16>;
+            static_assert(3 * JB::kDoubles <= JacobiLds<12, 12>::kDoubles && JB::kDoubles <= 144, "LDS areas");
+            const int grp = r >> 4;
+            double* JA = grp < 3 ? jac + grp * JB::kDoubles : lds;
+            double* JV = JA + JB::M * JB::NRP;
+            double* jn = JV + JB::M * JB::NVP;
+            JB::init(JA, JV, r, [](int, int) { return 0.0; });
+            // l[] into A with constant indices only (a dynamically indexed l went to scratch)
+#pragma unroll
+            for (int e = 0; e < 30; ++e)
+                if ((e & 15) == (r & 15)) JA[(e % 5) * JB::NRP + e / 5] = l[e];
+            JB::sync();
+            JB::run(JA, JV, jn, r);
+            double sv[5], smax = 0.0, y[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                sv[j] = sqrt(jn[j]);
+                smax = fmax(smax, sv[j]);
+            }
+            const double thr = smax * 2.220446049250313e-16 * 6;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {  // y = Sigma^+ U^T rho, U_j = a_j / s_j (svd_solve's pinv)
+                double d = 0.0;
+                if (sv[j] > thr) {
+#pragma unroll
+                    for (int rr = 0; rr < 6; ++rr) d += JA[j * JB::NRP + rr] * rho[rr];
+                    d /= sv[j] * sv[j];
+                }
+                y[j] = d;
+            }
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                double acc = 0.0;
+#pragma unroll
+                for (int j = 0; j < 5; ++j) acc += JV[j * JB::NVP + i] * y[j];
+                b5[i] = acc;
+            }
+        } else {
+            svd_solve<6, 5>(l, rho, b5);
+        }
         if (ap == 0) {  // find_betas_approx_1 (:747-781)
             if (b5[0] < 0) {
                 B[0] = sqrt(-b5[0]);

@@ -40,15 +40,27 @@ __device__ __forceinline__ double oct_sum(double x) {
     return x;
 }
 
-template <int NC, int NR>
+// LP lanes per column pair (8 or 4); one problem per GW-lane group of the
+// wave (GW = 64: the whole wave, or 16: four independent problems per wave,
+// each on its own LDS matrices).
+template <int LP>
+__device__ __forceinline__ double lp_sum(double x) {
+    static_assert(LP == 4 || LP == 8, "4 or 8 lanes per pair");
+    if constexpr (LP == 8) return oct_sum(x);
+    x += dpp_f64<kDppXor1>(x);
+    x += dpp_f64<kDppXor2>(x);
+    return x;
+}
+
+template <int NC, int NR, int LP = 8, int GW = 64>
 struct JacobiLds {
-    static_assert(NC >= 2 && NC <= 16, "at most 8 column pairs: 8 lanes per pair on one wave");
     static constexpr int M = NC + (NC & 1);  // positions of the circle method
     static constexpr int P = M / 2;          // pairs per round
-    static constexpr int RA = (NR + 7) / 8;  // rows of A per lane
-    static constexpr int RV = (NC + 7) / 8;  // rows of V per lane
-    static constexpr int NRP = 8 * RA;       // column stride of A
-    static constexpr int NVP = 8 * RV;       // column stride of V
+    static_assert(NC >= 2 && P * LP <= GW, "every column pair of a round needs its own LP lanes in the group");
+    static constexpr int RA = (NR + LP - 1) / LP;  // rows of A per lane
+    static constexpr int RV = (NC + LP - 1) / LP;  // rows of V per lane
+    static constexpr int NRP = LP * RA;            // column stride of A
+    static constexpr int NVP = LP * RV;            // column stride of V
     static constexpr int kDoubles = M * NRP + M * NVP + M;
 
     // the wave's LDS writes visible to its later reads (one wave, no block
@@ -58,14 +70,15 @@ struct JacobiLds {
         __builtin_amdgcn_wave_barrier();
     }
 
-    // A <- the NR x NC matrix a(r, c), V <- I (every lane of the wave calls)
+    // A <- the NR x NC matrix a(r, c), V <- I (every lane of the group calls)
     template <class F>
     static __device__ void init(double* A, double* V, int lane, F a) {
-        for (int idx = lane; idx < M * NRP; idx += 64) {
+        lane %= GW;
+        for (int idx = lane; idx < M * NRP; idx += GW) {
             const int c = idx / NRP, r = idx - c * NRP;
             A[idx] = (r < NR && c < NC) ? a(r, c) : 0.0;
         }
-        for (int idx = lane; idx < M * NVP; idx += 64) {
+        for (int idx = lane; idx < M * NVP; idx += GW) {
             const int c = idx / NVP, r = idx - c * NVP;
             V[idx] = (r == c && c < NC) ? 1.0 : 0.0;
         }
@@ -73,13 +86,14 @@ struct JacobiLds {
     }
 
     // returns the number of sweeps run
-    static __device__ int run(double* A, double* V, double* nrm, int lane, int max_sweeps = 60) {
-        const int pair = lane >> 3, s = lane & 7;
-        const bool active = pair < P;
-        const int i = active ? pair : 0;  // idle lanes shadow pair 0 and never store
+    // `store` false: the group computes but never writes (a duplicate problem)
+    static __device__ int run(double* A, double* V, double* nrm, int lane, int max_sweeps = 60, bool store = true) {
+        const int lg = lane % GW, pair = lg / LP, s = lg % LP;
+        const bool active = pair < P && store;
+        const int i = pair < P ? pair : 0;  // idle lanes shadow pair 0 and never store
         double fro = 0.0;
-        for (int idx = lane; idx < M * NRP; idx += 64) fro += A[idx] * A[idx];
-        const double negl = kJacobiNegl * group_sum_dpp<64>(fro);
+        for (int idx = lg; idx < M * NRP; idx += GW) fro += A[idx] * A[idx];
+        const double negl = kJacobiNegl * group_sum_dpp<GW>(fro);
         int sweep = 0;
         while (sweep < max_sweeps) {
             ++sweep;
@@ -89,12 +103,12 @@ struct JacobiLds {
                 double np = 0.0, nq = 0.0;
 #pragma unroll
                 for (int k = 0; k < RA; ++k) {
-                    const double x = A[p * NRP + s + 8 * k], y = A[q * NRP + s + 8 * k];
+                    const double x = A[p * NRP + s + LP * k], y = A[q * NRP + s + LP * k];
                     np += x * x;
                     nq += y * y;
                 }
-                np = oct_sum(np);
-                nq = oct_sum(nq);
+                np = lp_sum<LP>(np);
+                nq = lp_sum<LP>(nq);
                 if (active && s == 0) {
                     nrm[p] = np;
                     nrm[q] = nq;
@@ -111,19 +125,19 @@ struct JacobiLds {
                 double ap[RA], aq[RA], vp[RV], vq[RV];
 #pragma unroll
                 for (int j = 0; j < RA; ++j) {
-                    ap[j] = Ap[8 * j];
-                    aq[j] = Aq[8 * j];
+                    ap[j] = Ap[LP * j];
+                    aq[j] = Aq[LP * j];
                 }
 #pragma unroll
                 for (int j = 0; j < RV; ++j) {
-                    vp[j] = Vp[8 * j];
-                    vq[j] = Vq[8 * j];
+                    vp[j] = Vp[LP * j];
+                    vq[j] = Vq[LP * j];
                 }
                 const double alpha = nrm[p], beta = nrm[q];
                 double g = ap[0] * aq[0];
 #pragma unroll
                 for (int j = 1; j < RA; ++j) g = fma(ap[j], aq[j], g);
-                g = oct_sum(g);
+                g = lp_sum<LP>(g);
                 double c, sn, t;
                 rotated |= jacobi_rotation_fast(alpha, beta, g, negl, c, sn, t);
 #pragma unroll
@@ -141,13 +155,13 @@ struct JacobiLds {
                 if (active) {
 #pragma unroll
                     for (int j = 0; j < RA; ++j) {
-                        Ap[8 * j] = ap[j];
-                        Aq[8 * j] = aq[j];
+                        Ap[LP * j] = ap[j];
+                        Aq[LP * j] = aq[j];
                     }
 #pragma unroll
                     for (int j = 0; j < RV; ++j) {
-                        Vp[8 * j] = vp[j];
-                        Vq[8 * j] = vq[j];
+                        Vp[LP * j] = vp[j];
+                        Vq[LP * j] = vq[j];
                     }
                     if (s == 0) {
                         nrm[p] = fma(-t, g, alpha);
@@ -163,12 +177,12 @@ struct JacobiLds {
             double np = 0.0, nq = 0.0;
 #pragma unroll
             for (int k = 0; k < RA; ++k) {
-                const double x = A[p * NRP + s + 8 * k], y = A[q * NRP + s + 8 * k];
+                const double x = A[p * NRP + s + LP * k], y = A[q * NRP + s + LP * k];
                 np += x * x;
                 nq += y * y;
             }
-            np = oct_sum(np);
-            nq = oct_sum(nq);
+            np = lp_sum<LP>(np);
+            nq = lp_sum<LP>(nq);
             if (active && s == 0) {
                 nrm[p] = np;
                 nrm[q] = nq;
