@@ -37,7 +37,7 @@ namespace {
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
 #ifndef ORBGPU_PYR_WAVES_EU
-#define ORBGPU_PYR_WAVES_EU 5  // waves per SIMD the register budget is sized for (two 10-11-wave blocks per CU)
+#define ORBGPU_PYR_WAVES_EU 4  // register budget hint: 4 measured 0.6-1.4 % faster than 5 (two 10-wave blocks per CU either way, 65-66 VGPRs)
 #endif
 
 #ifdef PYR_STAMPS  // diagnostic build only (tools/pyr_ticks.py): per-tick clock stamps of blocks 0..63
