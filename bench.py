@@ -530,7 +530,46 @@ class StereoBench:
 # CPU baselines (oracle on the host cores; rank 0 at N=1 only)
 # ---------------------------------------------------------------------------
 
+def _cgroup_cpu_quota():
+    """CPUs granted by the cgroup CPU controller (cpu.max of cgroup v2, or
+    cpu.cfs_quota_us / cpu.cfs_period_us of v1) on this process's cgroup
+    path, or None when no quota is set or readable."""
+    paths = []
+    try:
+        for line in open("/proc/self/cgroup"):
+            parts = line.strip().split(":", 2)
+            if len(parts) == 3 and (parts[1] == "" or "cpu" in parts[1].split(",")):
+                paths.append((parts[1] == "", parts[2]))
+    except OSError:
+        pass
+    for v2, rel in paths + [(True, "/"), (False, "/")]:
+        root = "/sys/fs/cgroup" if v2 else "/sys/fs/cgroup/cpu"
+        rel = rel.lstrip("/")
+        # walk up from the process's own cgroup: a limit set on an ancestor applies
+        while True:
+            d = os.path.join(root, rel)
+            try:
+                if v2:
+                    q, per = open(os.path.join(d, "cpu.max")).read().split()[:2]
+                    if q != "max":
+                        return float(q) / float(per), os.path.join(d, "cpu.max")
+                else:
+                    q = int(open(os.path.join(d, "cpu.cfs_quota_us")).read())
+                    per = int(open(os.path.join(d, "cpu.cfs_period_us")).read())
+                    if q > 0:
+                        return q / per, os.path.join(d, "cpu.cfs_quota_us")
+            except (OSError, ValueError):
+                pass
+            if not rel:
+                break
+            rel = os.path.dirname(rel)
+    return None
+
+
 def cpu_info():
+    """The CPU share the all-core baseline runs on: the cgroup CPU quota when
+    one is set (rounded down, at least 1), else the affinity mask; both are
+    reported, with OMP_NUM_THREADS (the box's documented share) beside them."""
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -543,10 +582,17 @@ def cpu_info():
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    threads = min(avail, share) if share > 0 else avail
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    quota = _cgroup_cpu_quota()
+    if quota is not None:
+        threads, source = max(1, min(avail, int(quota[0]))), f"cgroup CPU quota ({quota[1]})"
+    elif omp > 0:
+        threads, source = min(avail, omp), "OMP_NUM_THREADS (no cgroup CPU quota readable)"
+    else:
+        threads, source = avail, "affinity mask (no cgroup CPU quota, no OMP_NUM_THREADS)"
     return {"cpu_model": model, "host_cpus": os.cpu_count(), "cpus_available_to_process": avail,
-            "threads_used": max(1, threads)}
+            "cgroup_cpu_quota": None if quota is None else round(quota[0], 2), "omp_num_threads": omp or None,
+            "threads_used": max(1, threads), "threads_source": source}
 
 
 def _timed_threads(fn, threads, seconds):
@@ -587,9 +633,13 @@ def cpu_baseline_mono(frames_np, W, H, nf, seconds, info):
             "single_thread_value": round(n1 / e1, 2), "single_thread_ms_per_frame": round(1e3 * e1 / max(n1, 1), 2),
             "cpu_model": info["cpu_model"], "host_cpus": info["host_cpus"],
             "cpus_available_to_process": info["cpus_available_to_process"],
+            "cgroup_cpu_quota": info["cgroup_cpu_quota"], "omp_num_threads": info["omp_num_threads"],
+            "threads_used": T, "threads_source": info["threads_source"],
             "note": "scalar C++ restatement of the reference's arithmetic (oracle/orbref.cpp: full corner score on "
                     "every pixel, no SIMD); the reference itself uses OpenCV 2.4's SSE FAST/resize/blur and would "
-                    "be faster per core. cores = the process's CPU share on the GPU box (all CPUs it may use)",
+                    "be faster per core. cores = threads_used: the cgroup CPU quota when one is set, else "
+                    "OMP_NUM_THREADS, else the affinity mask (threads_source says which); the reference's own "
+                    "timing mode is single_thread_value (mono_tum.cc:79-120, one thread per sequence)",
             "sample": f"oracle extract+match on {len(frames_np)} distinct synthetic {W}x{H} frames, "
                       f"~{seconds:.0f}s bounded ({n1} frames on 1 thread, {nN} on {T})"}
 

@@ -43,6 +43,13 @@ int orbgpu_debug_octree_trace(orbgpu_extractor* ex, int enable, int* out, int ca
 int orbgpu_debug_pyramid_emulate(int nfeatures, float scale_factor, int nlevels, int width, int height,
                                  const uint8_t* img, size_t img_step, uint8_t* out, size_t out_bytes, int* info);
 
+/* PnPsolver::qr_solve (PnPsolver.cpp:955-1047) as the GPU's EPnP runs it
+ * (csrc/epnp.h qr_solve_6x4), on n independent 6 x 4 systems in HBM: A (n x
+ * 24 doubles, row-major), b (n x 6), X (n x 4, read as the initial x: a
+ * singular system leaves it untouched, as the reference does).  Asynchronous
+ * on `stream`. */
+int orbgpu_debug_qr_solve_6x4_device(const double* A, const double* b, double* X, int n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

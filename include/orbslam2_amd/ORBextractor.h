@@ -4,19 +4,22 @@
 // include/orbgpu.h.  Header-only; link liborbgpu.so.
 //
 // Same class name, constructor, operator() and accessors as the reference,
-// so Frame.cpp / Tracking.cpp compile unchanged against it.  Differences:
+// so Frame.cpp / Tracking.cpp compile unchanged against it -- the stereo
+// Frame's ComputeStereoMatches included.  Differences:
 //  * the GPU handle is created on the first frame (its geometry is fixed by
 //    the frame size) and re-created if the size changes;
-//  * the pyramid stays in HBM: mvImagePyramid is filled only when the host
-//    copy is asked for (SetCopyPyramid(true), or -DORBGPU_HOST_PYRAMID=1 to
-//    make that the default).  Its only reader in the reference is the stereo
-//    Frame's ComputeStereoMatches (Frame.cpp:547-676), which the build
-//    replaces with ORB_SLAM2::ComputeStereoMatchesGPU (StereoMatcher.h) on
-//    the two extractors' HBM pyramids; a copy is then
-//    8 blocking device-to-host level copies per frame for nothing.  When
-//    copied, level l is a tight w_l x h_l copy (the reference's is a view
-//    into a bordered buffer whose border is never read outside
-//    ORBextractor.cpp);
+//  * the pyramid stays in HBM.  mvImagePyramid is a HostPyramid: a
+//    std::vector<cv::Mat> of nlevels entries (as ORBextractor.cpp:435 sizes
+//    it) whose element access copies the last frame's levels from HBM on the
+//    first read after each extraction.  An unmodified stereo Frame.cpp
+//    (Frame.cpp:547-676, its only reader) therefore works as it is, paying one
+//    device-to-host copy of the levels per frame; the build's
+//    ORB_SLAM2::ComputeStereoMatchesGPU (StereoMatcher.h)
+//    reads the HBM pyramids in place and never triggers the copy.
+//    SetCopyPyramid(true) (or -DORBGPU_HOST_PYRAMID=1) copies eagerly after
+//    every frame instead.  Level l is a tight w_l x h_l copy (the
+//    reference's is a view into a bordered buffer whose border is never read
+//    outside ORBextractor.cpp);
 //  * failures throw std::runtime_error carrying orbgpu_last_error() (the
 //    reference asserts).
 //
@@ -44,6 +47,58 @@
 
 namespace ORB_SLAM2 {
 
+// ORBextractor::mvImagePyramid (ORBextractor.h:85): the levels of the last
+// extracted frame, copied from HBM when first read.  Element access
+// (operator[], at, data, begin/end) fills every level at once (one pinned
+// staging copy per level, one synchronisation); size()/empty() do not.
+class HostPyramid : public std::vector<cv::Mat> {
+    using Base = std::vector<cv::Mat>;
+
+public:
+    cv::Mat& operator[](size_t l) { fill(); return Base::operator[](l); }
+    const cv::Mat& operator[](size_t l) const { fill(); return Base::operator[](l); }
+    cv::Mat& at(size_t l) { fill(); return Base::at(l); }
+    const cv::Mat& at(size_t l) const { fill(); return Base::at(l); }
+    cv::Mat* data() { fill(); return Base::data(); }
+    const cv::Mat* data() const { fill(); return Base::data(); }
+    Base::iterator begin() { fill(); return Base::begin(); }
+    Base::iterator end() { fill(); return Base::end(); }
+    Base::const_iterator begin() const { fill(); return Base::begin(); }
+    Base::const_iterator end() const { fill(); return Base::end(); }
+
+    // number of device-to-host level copies so far (adapter tests)
+    long copies() const { return copies_; }
+
+private:
+    friend class ORBextractor;
+    // a new frame is in HBM: the host levels are stale until read
+    void mark(orbgpu_extractor* ex, const orbgpu_extractor_info* info) {
+        ex_ = ex;
+        info_ = info;
+        stale_ = true;
+    }
+    void fill() const {
+        if (!stale_) return;
+        stale_ = false;  // a failed copy is not retried silently
+        Base& v = const_cast<HostPyramid&>(*this);
+        const int L = (int)v.size();
+        std::vector<uint8_t*> dst((size_t)L);
+        std::vector<size_t> step((size_t)L);
+        for (int l = 0; l < L; ++l) {
+            v[(size_t)l].create(info_->level_height[l], info_->level_width[l], CV_8U);
+            dst[(size_t)l] = v[(size_t)l].data;
+            step[(size_t)l] = v[(size_t)l].step;
+        }
+        if (orbgpu_extractor_copy_levels(ex_, 0, dst.data(), step.data()) != ORBGPU_OK)
+            throw std::runtime_error(std::string("orbgpu: mvImagePyramid copy: ") + orbgpu_last_error());
+        ++copies_;
+    }
+    orbgpu_extractor* ex_ = nullptr;
+    const orbgpu_extractor_info* info_ = nullptr;
+    mutable bool stale_ = false;
+    mutable long copies_ = 0;
+};
+
 class ORBextractor {
 public:
     enum { HARRIS_SCORE = 0, FAST_SCORE = 1 };
@@ -64,6 +119,7 @@ public:
         }
         mvInvScaleFactor.resize(nlevels);
         mvInvLevelSigma2.resize(nlevels);
+        mvImagePyramid.resize((size_t)nlevels);  // ORBextractor.cpp:435
         for (int i = 0; i < nlevels; i++) {
             mvInvScaleFactor[i] = 1.0f / mvScaleFactor[i];
             mvInvLevelSigma2[i] = 1.0f / mvLevelSigma2[i];
@@ -101,17 +157,8 @@ public:
             cv::Mat d = _descriptors.getMat();
             for (int i = 0; i < n; ++i) std::memcpy(d.ptr<unsigned char>(i), &desc_buf_[(size_t)i * 32], 32);
         }
-        if (copy_pyramid_) {
-            mvImagePyramid.resize((size_t)nlevels);
-            std::vector<uint8_t*> dst((size_t)nlevels);
-            std::vector<size_t> step((size_t)nlevels);
-            for (int l = 0; l < nlevels; ++l) {
-                mvImagePyramid[l].create(info_.level_height[l], info_.level_width[l], CV_8U);
-                dst[l] = mvImagePyramid[l].data;
-                step[l] = mvImagePyramid[l].step;
-            }
-            check(orbgpu_extractor_copy_levels(ex_, 0, dst.data(), step.data()));
-        }
+        mvImagePyramid.mark(ex_, &info_);
+        if (copy_pyramid_) mvImagePyramid.fill();
     }
 
     int inline GetLevels() { return nlevels; }
@@ -125,7 +172,7 @@ public:
     void SetCopyPyramid(bool on) { copy_pyramid_ = on; }
     orbgpu_extractor* handle() { return ex_; }  // the last frame's pyramid lives here (HBM)
 
-    std::vector<cv::Mat> mvImagePyramid;
+    HostPyramid mvImagePyramid;
 
 protected:
     int nfeatures;

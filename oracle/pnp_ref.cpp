@@ -98,20 +98,28 @@ void sym_eig_desc(const std::vector<double>& A, int n, std::vector<double>& w, s
     }
 }
 
-// PnPsolver::qr_solve (:1003-1070), 6 x 4
+// PnPsolver::qr_solve (PnPsolver.cpp:955-1047), 6 x 4.  The eta scan is the
+// reference's pointer loop (:975-980): it starts at |A[k][k]| and for
+// i = k+1 .. nr-1 reads row i-1 (the pointer advances after the read), so the
+// last row never takes part; the column is scaled by *= inv_eta with
+// inv_eta = 1./eta (:987-990).  Singular (eta == 0, :982-985): return with X
+// untouched.
 void qr_solve(double A[6][4], double b[6], double X[4]) {
     const int nr = 6, nc = 4;
     double A1[4], A2[4];
     for (int k = 0; k < nc; ++k) {
-        double eta = 0;
-        for (int i = k; i < nr; ++i) eta = std::max(eta, std::fabs(A[i][k]));
-        if (eta == 0) {
-            for (int i = 0; i < nc; ++i) X[i] = 0;
-            return;
+        double eta = std::fabs(A[k][k]);
+        for (int i = k + 1; i < nr; ++i) {
+            const double elt = std::fabs(A[i - 1][k]);
+            if (eta < elt) eta = elt;
         }
-        for (int i = k; i < nr; ++i) A[i][k] /= eta;
+        if (eta == 0) return;
+        const double inv_eta = 1. / eta;
         double sum = 0;
-        for (int i = k; i < nr; ++i) sum += A[i][k] * A[i][k];
+        for (int i = k; i < nr; ++i) {
+            A[i][k] *= inv_eta;
+            sum += A[i][k] * A[i][k];
+        }
         double sigma = std::sqrt(sum);
         if (A[k][k] < 0) sigma = -sigma;
         A[k][k] += sigma;
@@ -267,8 +275,9 @@ Pose compute_pose(const std::vector<double>& pws, const std::vector<double>& us,
         for (int c = 0; c < 3; ++c) rho[j] += (cws[pa[j]][c] - cws[pb[j]][c]) * (cws[pa[j]][c] - cws[pb[j]][c]);
     }
     auto gauss_newton = [&](double* B) {
+        double X[4] = {0, 0, 0, 0};  // gauss_newton's x: kept by a singular qr_solve
         for (int it = 0; it < 5; ++it) {
-            double A[6][4], bb[6], X[4];
+            double A[6][4], bb[6];
             for (int i = 0; i < 6; ++i) {
                 const double* r = L[i];
                 A[i][0] = 2 * r[0] * B[0] + r[1] * B[1] + r[3] * B[2] + r[6] * B[3];
@@ -466,3 +475,13 @@ void orbref_pnp_ransac_call(const float* P3, const float* P2, const float* maxer
 }
 
 }  // extern "C"
+
+// qr_solve on its own (tests: the eta-scan case, tests/test_pnp.py)
+extern "C" void orbref_qr_solve_6x4(const double* A, const double* b, double* X) {
+    double a[6][4], bb[6];
+    for (int i = 0; i < 6; ++i) {
+        for (int j = 0; j < 4; ++j) a[i][j] = A[i * 4 + j];
+        bb[i] = b[i];
+    }
+    qr_solve(a, bb, X);
+}

@@ -20,34 +20,57 @@ def _sym_eig_desc(a):
     return w[order], v[:, order].T
 
 
-def _qr_solve(A, b):
-    """PnPsolver::qr_solve (P:1003-1070), Householder QR least squares."""
+def _qr_solve(A, b, X=None):
+    """PnPsolver::qr_solve (P:955-1047), Householder QR least squares, letter
+    for letter: the eta scan starts at |A[k,k]| and covers rows k .. nr-2 (the
+    pointer loop P:975-980 reads before it advances, so the last row never
+    takes part); the column is scaled by `*= inv_eta`, inv_eta = 1./eta
+    (P:987-990); a zero eta returns with X untouched (P:982-985)."""
     A = A.copy()
     b = b.copy()
     nr, nc = A.shape
+    X = np.zeros(nc) if X is None else X.copy()
     A1 = np.zeros(nc)
     A2 = np.zeros(nc)
     for k in range(nc):
-        eta = np.abs(A[k:, k]).max()
+        eta = abs(A[k, k])
+        for i in range(k + 1, nr):
+            elt = abs(A[i - 1, k])
+            if eta < elt:
+                eta = elt
         if eta == 0:
-            return np.zeros(nc)
-        A[k:, k] /= eta
-        sigma = np.sqrt((A[k:, k] ** 2).sum())
+            return X
+        inv_eta = 1.0 / eta
+        s = 0.0
+        for i in range(k, nr):
+            A[i, k] *= inv_eta
+            s += A[i, k] * A[i, k]
+        sigma = np.sqrt(s)
         if A[k, k] < 0:
             sigma = -sigma
         A[k, k] += sigma
         A1[k] = sigma * A[k, k]
         A2[k] = -eta * sigma
         for j in range(k + 1, nc):
-            tau = (A[k:, k] * A[k:, j]).sum() / A1[k]
-            A[k:, j] -= tau * A[k:, k]
+            t = 0.0
+            for i in range(k, nr):
+                t += A[i, k] * A[i, j]
+            tau = t / A1[k]
+            for i in range(k, nr):
+                A[i, j] -= tau * A[i, k]
     for j in range(nc):
-        tau = (A[j:, j] * b[j:]).sum() / A1[j]
-        b[j:] -= tau * A[j:, j]
-    X = np.zeros(nc)
+        tau = 0.0
+        for i in range(j, nr):
+            tau += A[i, j] * b[i]
+        tau /= A1[j]
+        for i in range(j, nr):
+            b[i] -= tau * A[i, j]
     X[nc - 1] = b[nc - 1] / A2[nc - 1]
     for i in range(nc - 2, -1, -1):
-        X[i] = (b[i] - (A[i, i + 1:] * X[i + 1:]).sum()) / A2[i]
+        s = 0.0
+        for j in range(i + 1, nc):
+            s += A[i, j] * X[j]
+        X[i] = (b[i] - s) / A2[i]
     return X
 
 
@@ -114,6 +137,7 @@ def compute_pose(pws, us, cam):
     rho = np.array([((cws[a] - cws[b]) ** 2).sum() for (a, b) in pairs])
 
     def gauss_newton(betas):  # P:942-963, compute_A_and_b_gauss_newton P:910-940
+        x = np.zeros(4)  # gauss_newton's x, kept by a singular qr_solve
         for _ in range(5):
             A = np.zeros((6, 4))
             bb = np.zeros(6)
@@ -126,7 +150,8 @@ def compute_pose(pws, us, cam):
                         r[6] * b0 + r[7] * b1 + r[8] * b2 + 2 * r[9] * b3]
                 bb[i] = rho[i] - (r[0] * b0 * b0 + r[1] * b0 * b1 + r[2] * b1 * b1 + r[3] * b0 * b2 + r[4] * b1 * b2 +
                                   r[5] * b2 * b2 + r[6] * b0 * b3 + r[7] * b1 * b3 + r[8] * b2 * b3 + r[9] * b3 * b3)
-            betas = betas + _qr_solve(A, bb)
+            x = _qr_solve(A, bb, x)
+            betas = betas + x
         return betas
 
     def r_and_t(betas):  # compute_R_and_t (P:735-745)

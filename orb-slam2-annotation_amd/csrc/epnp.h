@@ -164,17 +164,22 @@ __host__ __device__ inline double dist2(const double* p, const double* q) {
     return (p[0] - q[0]) * (p[0] - q[0]) + (p[1] - q[1]) * (p[1] - q[1]) + (p[2] - q[2]) * (p[2] - q[2]);
 }
 
-// PnPsolver::qr_solve (PnPsolver.cpp:1003-1070), 6 x 4, A and b destroyed
+// PnPsolver::qr_solve (PnPsolver.cpp:955-1047), 6 x 4, A and b destroyed.
+// The eta scan is the reference's pointer loop (:975-980): it starts at
+// |A[k][k]| and, for i = k+1 .. nr-1, reads the row BEFORE advancing, so it
+// covers rows k .. nr-2 and never the last row.  A zero eta is the
+// reference's singular return (:982-985): X is left as it is (the caller's
+// x persists across the Gauss-Newton iterations, as gauss_newton's does).
 __host__ __device__ inline void qr_solve_6x4(double* A, double* b, double* X) {
     constexpr int nr = 6, nc = 4;
     double A1[nc], A2[nc];
     for (int k = 0; k < nc; ++k) {
         double eta = fabs(A[k * nc + k]);
-        for (int i = k + 1; i < nr; ++i) eta = fmax(eta, fabs(A[i * nc + k]));
-        if (eta == 0.0) {  // singular: the reference returns with X untouched
-            for (int i = 0; i < nc; ++i) X[i] = 0.0;
-            return;
+        for (int i = k + 1; i < nr; ++i) {
+            const double elt = fabs(A[(i - 1) * nc + k]);
+            if (eta < elt) eta = elt;
         }
+        if (eta == 0.0) return;
         double sum = 0.0;
         const double inv_eta = 1.0 / eta;
         for (int i = k; i < nr; ++i) {
@@ -405,8 +410,9 @@ __host__ __device__ double compute_pose(const Src& src, const Camera& cam, Pose&
         rho[5] = dist2(cws[2], cws[3]);
     }
     auto gauss_newton = [&](double* betas) {  // :942-963 + compute_A_and_b_gauss_newton :910-940
+        double x[4] = {0.0, 0.0, 0.0, 0.0};  // gauss_newton's x: kept by a singular qr_solve
         for (int it = 0; it < 5; ++it) {
-            double A[24], b[6], x[4];
+            double A[24], b[6];
             for (int i = 0; i < 6; ++i) {
                 const double* r = L + 10 * i;
                 double* a = A + 4 * i;

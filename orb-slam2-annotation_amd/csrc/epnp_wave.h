@@ -453,8 +453,9 @@ __device__ double compute_pose_group(const Src& src, const Camera& cam, Pose& ou
     EPNP_T(6);
     const double* L = s_L;
     auto gauss_newton = [&](double* betas) {  // :942-963 + compute_A_and_b_gauss_newton :910-940
+        double x[4] = {0.0, 0.0, 0.0, 0.0};  // gauss_newton's x: kept by a singular qr_solve
         for (int it = 0; it < 5; ++it) {
-            double A[24], b[6], x[4];
+            double A[24], b[6];
             for (int i = 0; i < 6; ++i) {
                 const double* rr = L + 10 * i;
                 double* a = A + 4 * i;

@@ -64,10 +64,13 @@ struct JacobiLds {
     static constexpr int kDoubles = M * NRP + M * NVP + M;
 
     // the wave's LDS writes visible to its later reads (one wave, no block
-    // barrier: the stores retired, then a compiler scheduling barrier)
+    // barrier): release/acquire workgroup fences around the wave barrier so
+    // the compiler cannot move or reuse LDS loads across it (the intrinsics
+    // alone are IntrNoMem), then the stores retired
     static __device__ __forceinline__ void sync() {
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
 
     // A <- the NR x NC matrix a(r, c), V <- I (every lane of the group calls)

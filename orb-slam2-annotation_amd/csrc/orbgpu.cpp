@@ -392,6 +392,10 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     e->max_kps = out_off;
     e->ncap = (int)round_up((size_t)ncap, 16);
     if (e->ncap > 4096) return fail(ORBGPU_ERR_UNSUPPORTED, "more than 4092 features per level");
+    // octree.hip's main pass scans (children << 16 | survives) in one int:
+    // C <= 4 * nodes must stay below 2^15 and S <= nodes below 2^16
+    static_assert(4 * 4096 < (1 << 15), "octree packed scan bound");
+    if (4 * e->ncap >= (1 << 15)) return fail(ORBGPU_ERR_UNSUPPORTED, "octree node capacity exceeds the packed scan");
     // keys in LDS up to a 64 KiB workgroup budget; larger levels use HBM scratch
     const size_t fixed = octree_lds_bytes(g, 0, e->ncap);
     const long budget = 65536 - (long)fixed - 64;

@@ -264,9 +264,32 @@ __global__ __launch_bounds__(kThreads) void pnp_score_kernel(const orbgpu_pnp_pr
     }
 }
 
+// qr_solve_6x4 on its own, one thread per problem (debug ABI, tests)
+__global__ void qr_solve_kernel(const double* A, const double* b, double* X, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double a[24], bb[6], x[4];
+    for (int k = 0; k < 24; ++k) a[k] = A[(size_t)i * 24 + k];
+    for (int k = 0; k < 6; ++k) bb[k] = b[(size_t)i * 6 + k];
+    for (int k = 0; k < 4; ++k) x[k] = X[(size_t)i * 4 + k];
+    epnp::qr_solve_6x4(a, bb, x);
+    for (int k = 0; k < 4; ++k) X[(size_t)i * 4 + k] = x[k];
+}
+
 }  // namespace
 
 size_t pnp_hyp_bytes() { return sizeof(HypPose); }
+
+}  // namespace orbgpu
+
+extern "C" int orbgpu_debug_qr_solve_6x4_device(const double* A, const double* b, double* X, int n, void* stream) {
+    if (n <= 0) return 0;
+    if (!A || !b || !X) return -1;
+    hipLaunchKernelGGL(orbgpu::qr_solve_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, A, b, X, n);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+namespace orbgpu {
 
 #ifdef EPNP_STAMPS
 extern "C" int orbgpu_debug_epnp_stamps(unsigned long long* out) {

@@ -1079,6 +1079,26 @@ int main(int argc, char** argv) {
             }
             fwrite(uR.data(), 4, uR.size(), out);
             fwrite(dep.data(), 4, dep.size(), out);
+            // An unmodified stereo Frame.cpp reads the extractors' host pyramids
+            // (Frame.cpp:547 `mvImagePyramid[0].rows`, :657/:670/:676 the octave
+            // levels): the GPU stereo path above never copied them, the first
+            // read copies every level of the last frame once.
+            const long c0[2] = {exL.mvImagePyramid.copies(), exR.mvImagePyramid.copies()};
+            const int n_rows = exL.mvImagePyramid[0].rows;  // Frame.cpp:547
+            fwrite(c0, 8, 2, out);
+            fwrite(&n_rows, 4, 1, out);
+            for (ORB_SLAM2::ORBextractor* e : {&exL, &exR}) {
+                const int L = (int)e->mvImagePyramid.size();
+                fwrite(&L, 4, 1, out);
+                for (int l = 0; l < L; ++l) {
+                    const cv::Mat& M = e->mvImagePyramid[l];
+                    const int wh[2] = {M.cols, M.rows};
+                    fwrite(wh, 4, 2, out);
+                    for (int y = 0; y < M.rows; ++y) fwrite(M.ptr<unsigned char>(y), 1, (size_t)M.cols, out);
+                }
+            }
+            const long c1[2] = {exL.mvImagePyramid.copies(), exR.mvImagePyramid.copies()};
+            fwrite(c1, 8, 2, out);
             fclose(out);
         } catch (const std::exception& e) {
             fprintf(stderr, "exception: %s\n", e.what());

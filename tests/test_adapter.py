@@ -631,6 +631,24 @@ def test_adapter_stereo_frame_vs_oracle(exe, tmp_path, w, h, nf, bf, base):
     assert kr.tobytes() == rk[2].tobytes() and np.array_equal(dr, rk[3])
     assert ur.tobytes() == rk[4].tobytes() and dp.tobytes() == rk[5].tobytes()
     assert (ur >= 0).mean() > 0.3
+    # an unmodified stereo Frame.cpp reads mvImagePyramid (Frame.cpp:547-676):
+    # no copy was made for the GPU stereo path, the first read copies the
+    # levels once per extractor, and they are the oracle's pyramid bit for bit
+    off += 8 * len(kl)
+    c0 = np.frombuffer(buf, np.int64, 2, off)
+    n_rows, = struct.unpack_from("<i", buf, off + 16)
+    off += 20
+    assert list(c0) == [0, 0] and n_rows == h
+    for ex in (exL, exR):
+        nlev, = struct.unpack_from("<i", buf, off)
+        off += 4
+        assert nlev == 8
+        for lv in range(nlev):
+            lw, lh = struct.unpack_from("<ii", buf, off)
+            got = np.frombuffer(buf, np.uint8, lw * lh, off + 8).reshape(lh, lw)
+            off += 8 + lw * lh
+            np.testing.assert_array_equal(got, ex.level(lv))
+    assert list(np.frombuffer(buf, np.int64, 2, off)) == [1, 1]
 
 
 def test_adapter_initializer_fewer_than_8_matches_returns_false(exe, tmp_path):

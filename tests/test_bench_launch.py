@@ -111,6 +111,7 @@ def test_stereo_pairs_two_ranks_equal_single_process(tmp_path):
             assert (c[0], c[1]) == (len(kl), len(kr)), pair
             assert got["kps"][pair][0][:len(kl)].tobytes() == kl.tobytes()
             assert got["kps"][pair][1][:len(kr)].tobytes() == kr.tobytes()
+            assert np.array_equal(got["desc"][pair][0][:len(kl)], dl)
             assert np.array_equal(got["desc"][pair][1][:len(kr)], dr)
             assert got["uright"][pair][:len(kl)].tobytes() == ur.tobytes()
             assert got["depth"][pair][:len(kl)].tobytes() == dp.tobytes()

@@ -32,6 +32,105 @@ def test_qr_solve_restatement_is_least_squares():
         np.testing.assert_allclose(pnp_ref._qr_solve(A, b), np.linalg.lstsq(A, b, rcond=None)[0], atol=1e-9)
 
 
+def _qr_cases():
+    """6 x 4 systems whose LAST row holds a column's largest magnitude: the
+    reference's eta scan (PnPsolver.cpp:975-980) never reads the last row, so
+    eta -- and the rounding of every later step -- differs from a scan over
+    all rows; plus a system the reference calls singular (rows k .. nr-2 of
+    column 0 zero, the last row not): it returns with X untouched."""
+    rng = np.random.default_rng(7)
+    cases = []
+    for t in range(32):
+        A = rng.normal(size=(6, 4))
+        A[5, t % 4] = 40.0 * (1 + rng.random())  # last row: the column maximum
+        cases.append((A, rng.normal(size=6)))
+    A = rng.normal(size=(6, 4))
+    A[:5, 0] = 0.0
+    cases.append((A, rng.normal(size=6)))
+    return cases
+
+
+def _qr_all_rows(A, b):
+    """the same Householder QR with eta over ALL rows and a division (the
+    pre-round-4 restatement): what the letter-faithful scan must differ from"""
+    A = A.copy()
+    b = b.copy()
+    nr, nc = A.shape
+    A1, A2 = np.zeros(nc), np.zeros(nc)
+    for k in range(nc):
+        eta = np.abs(A[k:, k]).max()
+        A[k:, k] /= eta
+        sigma = np.sqrt((A[k:, k] ** 2).sum())
+        sigma = -sigma if A[k, k] < 0 else sigma
+        A[k, k] += sigma
+        A1[k], A2[k] = sigma * A[k, k], -eta * sigma
+        for j in range(k + 1, nc):
+            tau = (A[k:, k] * A[k:, j]).sum() / A1[k]
+            A[k:, j] -= tau * A[k:, k]
+    for j in range(nc):
+        b[j:] -= (A[j:, j] * b[j:]).sum() / A1[j] * A[j:, j]
+    X = np.zeros(nc)
+    X[nc - 1] = b[nc - 1] / A2[nc - 1]
+    for i in range(nc - 2, -1, -1):
+        X[i] = (b[i] - (A[i, i + 1:] * X[i + 1:]).sum()) / A2[i]
+    return X
+
+
+def _qr_cpp(A, b, X0):
+    import ctypes
+    import orbref
+    L = orbref.lib()
+    f = L.orbref_qr_solve_6x4
+    f.argtypes = [ctypes.c_void_p] * 3
+    A = np.ascontiguousarray(A, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    X = np.array(X0, np.float64)
+    f(A.ctypes.data, b.ctypes.data, X.ctypes.data)
+    return X
+
+
+def test_qr_solve_eta_scan_is_the_references():
+    """oracle/pnp_ref.py == oracle/pnp_ref.cpp bit for bit on the eta-scan
+    cases; the last-row-maximum systems differ in rounding from an all-rows
+    scan on some systems (the scan is observable), and the singular case
+    leaves X as it was."""
+    cases = _qr_cases()
+    X0 = np.array([0.25, -1.5, 3.0, 7.0])
+    differ = 0
+    for A, b in cases[:-1]:
+        xp = pnp_ref._qr_solve(A, b, X0)
+        xc = _qr_cpp(A, b, X0)
+        assert xp.tobytes() == xc.tobytes()
+        np.testing.assert_allclose(xp, np.linalg.lstsq(A, b, rcond=None)[0], rtol=1e-9, atol=1e-9)
+        differ += xp.tobytes() != _qr_all_rows(A, b).tobytes()
+    assert differ > 0
+    A, b = cases[-1]
+    assert pnp_ref._qr_solve(A, b, X0).tobytes() == X0.tobytes()
+    assert _qr_cpp(A, b, X0).tobytes() == X0.tobytes()
+
+
+@pytest.mark.gpu
+def test_gpu_qr_solve_eta_scan_equals_oracle():
+    """csrc/epnp.h qr_solve_6x4 (the EPnP Gauss-Newton solve on the GPU) on
+    the same cases, through orbgpu_debug_qr_solve_6x4_device: bit-identical
+    to the oracle, the singular case leaving X untouched"""
+    import ctypes
+    import orbgpu
+    import torch
+    cases = _qr_cases()
+    X0 = np.array([0.25, -1.5, 3.0, 7.0])
+    A = torch.tensor(np.stack([a.reshape(-1) for a, _ in cases]), dtype=torch.float64, device="cuda")
+    b = torch.tensor(np.stack([bb for _, bb in cases]), dtype=torch.float64, device="cuda")
+    X = torch.tensor(np.tile(X0, (len(cases), 1)), dtype=torch.float64, device="cuda")
+    f = orbgpu.lib().orbgpu_debug_qr_solve_6x4_device
+    f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p]
+    assert f(A.data_ptr(), b.data_ptr(), X.data_ptr(), len(cases), None) == 0
+    torch.cuda.synchronize()
+    got = X.cpu().numpy()
+    for i, (a, bb) in enumerate(cases):
+        assert got[i].tobytes() == pnp_ref._qr_solve(a, bb, X0).tobytes(), i
+
+
 def test_epnp_minimal_sets_mostly_accurate():
     """EPnP on 4 noise-free points is approximate (three beta linearisations +
     5 Gauss-Newton steps); with the canonical null-space basis most minimal
