@@ -128,6 +128,13 @@ def parse(argv=None):
     ap.add_argument("--no-extras", action="store_true", help="headline only (no extra legs)")
     ap.add_argument("--match-after", default="fast_cells", choices=["pyramid", "fast_cells", "octree"],
                     help="extraction stage of step k after which step k-1's match starts")
+    ap.add_argument("--deliver", default="host", choices=["host", "gpu0"],
+                    help="where each step's outputs go (shard.Delivery): host = every rank copies its trimmed "
+                         "outputs over its own PCIe link to pinned host memory (the Tracking thread's side); "
+                         "gpu0 = counts then used rows sent to rank 0's HBM")
+    ap.add_argument("--feed", default="hbm", choices=["hbm", "host"],
+                    help="headline input: frames resident in HBM (default) or copied from pinned host memory "
+                         "every step (the host_fed leg of the default line)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     ap.add_argument("--cpu-dry-run", default=None, metavar="ENGINE.py",
                     help="tests only: gloo on the CPU with ENGINE.py standing in for orbgpu")
@@ -237,6 +244,23 @@ def aggregate(elapsed: float, frames_local: int, device=None):
     return float(t.item()), int(n.item())
 
 
+def gather_delivery_stats(rep, world, device=None):
+    """per-rank delivery numbers -> rank 0: the bytes every rank moved per
+    step and the owner waits, max over ranks (no-op at N = 1)"""
+    import torch.distributed as dist
+    keys = ["bytes_per_step", "recv_bytes_per_step", "owner_wait_ms_per_step", "delivery_latency_ms"]
+    if not (dist.is_available() and dist.is_initialized()) or world == 1:
+        return {**rep, "per_rank": [{k: rep[k] for k in keys}]}
+    t = torch.tensor([float(rep[k]) for k in keys], dtype=torch.float64, device=device)
+    allt = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(allt, t)
+    per = [{k: (int(v) if "bytes" in k else round(float(v), 4)) for k, v in zip(keys, x.tolist())} for x in allt]
+    out = {"mode": rep["mode"], "per_rank": per}
+    for k in keys:
+        out[k + "_max"] = max(p[k] for p in per)
+    return out
+
+
 def _barrier(world):
     if world > 1:
         import torch.distributed as dist
@@ -271,10 +295,11 @@ class _Dumper:
 class StreamBench:
     """Extract + SearchForInitialization over one sharded frame stream."""
 
-    def __init__(self, og, D: Dev, W, H, NF, B, rank, world, stream, dump=None):
+    def __init__(self, og, D: Dev, W, H, NF, B, rank, world, stream, dump=None, deliver="host", feed="hbm"):
         import shard
         import synth
         self.og, self.D = og, D
+        self.deliver, self.feed = deliver, feed
         self.W, self.H, self.NF, self.B, self.rank, self.world = W, H, NF, B, rank, world
         dev = D.device
         self.dev, self.stream = dev, stream
@@ -285,6 +310,17 @@ class StreamBench:
         self.pool_t0 = [shard.chunk_frames(s, rank, world, B)[0] for s in range(POOL_STEPS)]
         self.pool = [synth.torch_stream(B, W, H, device=dev, pitch=self.pitch, bounded=True, t0=t0)
                      for t0 in self.pool_t0]
+        if feed == "host":
+            # host-fed stream (TrackMonocular's images arrive from host memory,
+            # mono_tum.cc:79-90): the pool lives in pinned host memory; every step's B
+            # frames are copied into one of two HBM input buffers on a copy stream, the
+            # next step's copy overlapping this step's extraction
+            self.pool = [p.cpu().pin_memory() if D.cuda else p.cpu() for p in self.pool]
+            self.inbuf = [torch.empty_like(self.pool[0], device=dev) for _ in range(2)]
+            self.h2d = D.stream()
+            self.ev_h2d = [D.event() for _ in range(2)]
+            self.h2d_time = []  # (start, end) timing events per copy in the timed region
+            self.h2d_issued = -1
         # slot 0 = the frame before this chunk (boundary exchange), slots 1..B this chunk
         self.sets = []
         for _ in range(2):  # two output sets: the gather of step k overlaps step k+1
@@ -296,10 +332,23 @@ class StreamBench:
             self.sets.append((kps_all, desc_all, counts_all, m12, nmatch))
         k0, d0, c0 = self.sets[0][0], self.sets[0][1], self.sets[0][2]
         self.bx = shard.BoundaryExchange(rank, world, [k0[0], d0[0], c0[0:1]])
-        self.gather = shard.OwnerGather(rank, world, [k0[1:], d0[1:], c0[1:], self.sets[0][3], self.sets[0][4]])
+        # every step's keypoints, descriptors (trimmed to the counts) and m12 rows (trimmed to the
+        # matched-against frames' counts) plus counts / match counts go to the Tracking owner
+        # (shard.Delivery: "host" over each rank's own PCIe link, or "gpu0" to rank 0's HBM)
+        group = None
+        if deliver == "gpu0" and world > 1:
+            import torch.distributed as dist
+            group = dist.new_group(list(range(world)))
+        self.delivery = shard.Delivery(deliver, rank, world, dev,
+                                       [shard.RowSpec("kps", 0), shard.RowSpec("desc", 0), shard.RowSpec("m12", 1)],
+                                       B, cap, [k0[1:], d0[1:], self.sets[0][3]], 3 * B, group=group,
+                                       packer=getattr(og, "pack_rows", None))
         self.flags = og.MATCH_CHECK_ORI
         self.step_no = 0
-        self.dump = _Dumper(dump, f"mono_{W}x{H}") if (dump and rank == 0) else None
+        # dumps (tests): host mode -- every rank its own delivered frames; gpu0 -- rank 0 all ranks'
+        per_rank = deliver == "host" and world > 1
+        self.dump = (_Dumper(dump, f"mono_{W}x{H}" + (f"_rank{rank}" if per_rank else ""))
+                     if (dump and (rank == 0 or per_rank)) else None)
         self.dump_all = bool(dump)
         # The matcher runs on its own stream, one step behind: SearchForInitialization of
         # step k-1 (a few hundred latency-bound blocks) starts once step k's FAST pass is
@@ -313,6 +362,8 @@ class StreamBench:
         self.ev_ext = [D.event() for _ in range(2)]
         self.ev_match = [None, None]
         self.pending = None  # (set index, timing events) of the step whose match is not issued yet
+        self.timing_h2d = False
+        self.dslot = [0, 0]  # delivery ring slot of each output set's last step
 
     def _match(self, si, after, ev=None):
         kps_all, desc_all, counts_all, m12, nmatch = self.sets[si]
@@ -325,21 +376,22 @@ class StreamBench:
                                                 flags=self.flags, stream=ms)
         if ev is not None:
             ev[1].record(ms)
+        # delivery (packing on this stream, after the match; the copies or sends on the
+        # delivery thread's own stream)
+        self.dslot[si] = self.delivery.start([kps_all[1:], desc_all[1:], m12], [counts_all[1:], counts_all[:-1], nmatch],
+                                             [counts_all[1:], counts_all[:-1]], stream=None if not self.D.cuda else ms)
         em = self.D.event()
-        em.record(ms)
+        em.record(ms)  # the next extraction into this set waits for the match and the packing
         self.ev_match[si] = em
-        with self.D.use_stream(ms):  # the gather (RCCL send/recv) is ordered after the match
-            self.gather.start(si, [kps_all[1:], desc_all[1:], counts_all[1:], m12, nmatch])
 
     def step(self, ev=None):
         B, st = self.B, self.stream
         si = self.step_no % 2
         kps_all, desc_all, counts_all, m12, nmatch = self.sets[si]
-        self.gather.finish(si)  # the set's previous transfer is done before it is rewritten
         if self.ev_match[si] is not None:  # ... and the match that read it (step k-2)
             st.wait_event(self.ev_match[si])
         pidx = self.step_no % POOL_STEPS
-        frames = self.pool[pidx]
+        frames = self.pool[pidx] if self.feed == "hbm" else self._fed(self.step_no)
         self.ex.extract_batch(frames, kps_all[1:], desc_all[1:], counts_all[1:], stream=st, row_step=self.pitch,
                               frame_step=self.pitch * self.H)
         with self.D.use_stream(st):
@@ -351,22 +403,64 @@ class StreamBench:
         if self.pending is not None:  # step k-1's match, after step k's FAST pass
             self._match(*self.pending[:1], self.ev_pyr, self.pending[1])
         self.pending = (si, ev)
-        if self.dump_all:  # test mode: finish the step and record what rank 0 received
+        if self.dump_all:  # test mode: finish the step and record what was delivered
             self.flush()
-            self.gather.finish()
+            self.delivery.finish()
             if self.dump is not None:
                 self._record(si, pidx)
         self.step_no += 1
 
+    def _issue_h2d(self, k):
+        """copy step k's frames from pinned host memory into input buffer k % 2 on
+        the copy stream, after the extraction that last read that buffer (step k-2)"""
+        b = k % 2
+        h = self.h2d
+        if self.ev_ext[b] is not None and k >= 2:
+            h.wait_event(self.ev_ext[b])
+        timed = self.timing_h2d
+        if timed:
+            e0, e1 = self.D.event(True), self.D.event(True)
+            e0.record(h)
+        with self.D.use_stream(h):
+            self.inbuf[b].copy_(self.pool[k % POOL_STEPS], non_blocking=True)
+        if timed:
+            e1.record(h)
+            self.h2d_time.append((e0, e1))
+        self.ev_h2d[b].record(h)
+        self.h2d_issued = k
+
+    def _fed(self, k):
+        """input buffer of step k (its copy issued, the next step's copy issued behind it)"""
+        if self.h2d_issued < k:
+            self._issue_h2d(k)
+        self.stream.wait_event(self.ev_h2d[k % 2])
+        self._issue_h2d(k + 1)  # prefetch: overlaps this step's extraction
+        return self.inbuf[k % 2]
+
     def _record(self, si, pidx):
         import shard
-        own = [t.cpu() for t in (self.sets[si][0][1:], self.sets[si][1][1:], self.sets[si][2][1:],
-                                 self.sets[si][3], self.sets[si][4])]
-        chunks = [(0, own)] + [(r + 1, [t.cpu() for t in ts]) for r, ts in enumerate(self.gather.received(si))]
+        B, cap = self.B, self.cap
+
+        def unpack(rows, small):
+            sm = small.cpu().numpy()
+            c, cp, nm = sm[:B], sm[B:2 * B], sm[2 * B:]
+            k = shard.unpack_rows(rows[0].cpu().numpy(), c, cap)
+            d = shard.unpack_rows(rows[1].cpu().numpy(), c, cap)
+            m = shard.unpack_rows(rows[2].cpu().numpy(), cp, cap)
+            return k, d, c, m, nm
+
+        ds = self.dslot[si]
+        if self.deliver == "host":
+            rows, small = self.delivery.host_rows(ds)
+            chunks = [(self.rank, unpack([r for r, _ in rows], small))]
+        else:
+            own = [t.cpu().numpy() for t in (self.sets[si][0][1:], self.sets[si][1][1:], self.sets[si][2][1:],
+                                             self.sets[si][3], self.sets[si][4])]
+            chunks = [(0, own)] + [(r + 1, unpack(rows, small))
+                                   for r, (rows, small) in enumerate(self.delivery.received(ds))]
         for r, (k, d, c, m, n) in chunks:
             for b, f in enumerate(shard.chunk_frames(pidx, r, self.world, self.B)):
-                cc = int(c[b])
-                self.dump.add(f, count=cc, kps=k[b].numpy(), desc=d[b].numpy(), nmatch=int(n[b]), m12=m[b].numpy())
+                self.dump.add(f, count=int(c[b]), kps=k[b], desc=d[b], nmatch=int(n[b]), m12=m[b])
 
     def flush(self):
         """issue the match of the last extracted step"""
@@ -380,10 +474,12 @@ class StreamBench:
         for _ in range(warmup):
             self.step()
         self.flush()
-        self.gather.finish()
+        self.delivery.finish()
         D.synchronize()
+        self.delivery.reset_stats()
         self.ex.sync(self.stream)
         self.ex.profile(True)
+        self.timing_h2d, self.h2d_time = True, []
         self.ex.stage_times(reset=True)
         evs = [(D.event(True), D.event(True)) for _ in range(steps)]
         _barrier(self.world)
@@ -392,10 +488,13 @@ class StreamBench:
         for i in range(steps):
             self.step(evs[i])
         self.flush()
-        self.gather.finish()
+        self.delivery.finish()
         D.synchronize()
         elapsed = time.perf_counter() - t0
+        self.timing_h2d = False
+        delivery = self.delivery.report(steps)
         elapsed, frames_total = aggregate(elapsed, self.B * steps, device=self.dev)
+        delivery = gather_delivery_stats(delivery, self.world, self.dev)
         _barrier(self.world)
         self.ex.sync(self.stream)
         stage_ms, nb = self.ex.stage_times(reset=True)
@@ -408,9 +507,19 @@ class StreamBench:
         pyr_s = per_step["pyramid"] / 1e3
         achieved = pyr_bytes / pyr_s / 1e9 if pyr_s > 0 else None
         last = self.sets[(self.step_no - 1) % 2]
+        h2d = None
+        if self.feed == "host" and self.h2d_time:
+            ms = [a.elapsed_time(b) for a, b in self.h2d_time]  # the copies issued inside the timed region
+            nbytes = self.inbuf[0].numel()
+            h2d = {"bytes_per_step": int(nbytes), "ms_per_copy_mean": round(float(np.mean(ms)), 4),
+                   "gb_per_s": round(nbytes / (float(np.mean(ms)) / 1e3) / 1e9, 2), "copies": len(ms)}
         return {"fps": frames_total / elapsed, "elapsed": elapsed, "per_step": per_step, "pyr_bytes": pyr_bytes,
                 "achieved": achieved, "keypoints": float(last[2][1:].float().mean().item()),
-                "matches": float(last[4].float().mean().item()), "frames_total": frames_total}
+                "matches": float(last[4].float().mean().item()), "frames_total": frames_total,
+                "delivery": delivery, "h2d": h2d}
+
+    def close(self):
+        self.delivery.close()
 
     def parity_frame0(self):
         """pool frame 0 of this rank against the oracle (untimed)."""
@@ -1064,13 +1173,31 @@ def main_mono(args, og, D, rank, world, stream):
     W, H, NF, desc_cfg = CONFIGS[args.config]
     B = args.batch or (512 if args.config == "mono640" else 256)
     MATCH_AFTER[0] = args.match_after
-    sb = StreamBench(og, D, W, H, NF, B, rank, world, stream, dump=args.dump)
+    sb = StreamBench(og, D, W, H, NF, B, rank, world, stream, dump=args.dump, deliver=args.deliver, feed=args.feed)
     parity = sb.parity_frame0() if (rank == 0 and D.cuda) else None
     r = sb.run(args.warmup, args.steps)
-    frame0 = sb.pool[0][0, :, :W].cpu().numpy() if rank == 0 else None
+    sb.close()
     del sb
     D.empty_cache()
     extras = {}
+    if not args.no_extras and D.cuda and args.feed == "hbm":
+        # host-fed leg: the same stream with every step's frames copied from pinned host
+        # memory (double-buffered H2D on a copy stream, overlapped with extraction) and the
+        # outputs delivered to host memory, as TrackMonocular consumes them
+        hb = StreamBench(og, D, W, H, NF, B, rank, world, stream, deliver="host", feed="host")
+        hr = hb.run(2, max(10, args.steps))
+        hb.close()
+        del hb
+        D.empty_cache()
+        h2d_ms = hr["h2d"]["ms_per_copy_mean"] if hr["h2d"] else None
+        compute_ms = r["elapsed"] / args.steps * 1e3
+        extras["host_fed"] = {
+            "frames_per_s": round(hr["fps"], 1), "ms_per_step": round(hr["elapsed"] / max(10, args.steps) * 1e3, 3),
+            "frames_per_gpu_per_step": B, "h2d": hr["h2d"], "delivery": hr["delivery"],
+            "hbm_resident_ms_per_step": round(compute_ms, 3),
+            "bound": ("pcie_h2d" if h2d_ms and h2d_ms > compute_ms else "kernels"),
+            "workload": desc_cfg + "; frames copied from pinned host memory every step (H2D on a copy stream, "
+                                   "double-buffered), outputs delivered to pinned host memory"}
     if not args.no_extras and D.cuda:
         # config 4: EuRoC stereo sharded over all ranks (every N)
         esb = StereoBench(og, D, "euroc_stereo", 128, rank, world, stream)
@@ -1096,7 +1223,8 @@ def main_mono(args, og, D, rank, world, stream):
         "config": {"workload": desc_cfg, "config": args.config, "frames_per_gpu_per_step": B,
                    "width": W, "height": H, "nfeatures": NF,
                    "parallelism": f"one stream in contiguous per-rank chunks x{world}, boundary frame send/recv, "
-                                  f"per-step gather to rank 0"},
+                                  + ("per-rank delivery of trimmed outputs to pinned host memory"
+                                     if args.deliver == "host" else "per-step counts-first gather to rank 0")},
         "roofline": {"bound": "hbm", "kernel": PYR_KERNEL,
                      "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
@@ -1107,7 +1235,12 @@ def main_mono(args, og, D, rank, world, stream):
         "matches_per_pair": round(r["matches"], 1),
         "parity_frame0_vs_oracle": parity,
         "world_size_checked": world,
+        "input": "frames resident in HBM" if args.feed == "hbm" else
+                 "frames copied from pinned host memory every step (double-buffered H2D)",
+        "delivery": r["delivery"],
     }
+    if r.get("h2d"):
+        line["h2d"] = r["h2d"]
     tr = line["roofline"]["traffic"]
     if tr and r["per_step"].get("pyramid"):
         line["roofline"]["traffic_frac"] = round(tr / (r["per_step"]["pyramid"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
@@ -1120,8 +1253,9 @@ def main_mono(args, og, D, rank, world, stream):
                                     "path": "ORB_SLAM2::ORBextractor::operator() (C++ drop-in class, 640x480, host "
                                             "image in, keypoints + descriptors out, no host pyramid copy)"}
         other = {}
-        kb = StreamBench(og, D, *CONFIGS["kitti"][:3], 256, 0, 1, stream)
+        kb = StreamBench(og, D, *CONFIGS["kitti"][:3], 256, 0, 1, stream, deliver=args.deliver)
         kr = kb.run(2, 10)
+        kb.close()
         other["mono1241x376"] = {
             "frames_per_s": round(kr["fps"], 1), "ms_per_step": round(kr["elapsed"] / 10 * 1e3, 3),
             "frames_per_step": 256, "nfeatures": CONFIGS["kitti"][2],

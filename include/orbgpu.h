@@ -137,6 +137,22 @@ int orbgpu_extractor_copy_levels(orbgpu_extractor* ex, int frame, uint8_t* const
  * descriptor pairs resident in HBM: d_dist[i] = popcount(a_i xor b_i). */
 int orbgpu_hamming_pairs_device(const uint8_t* d_a, const uint8_t* d_b, int n, int* d_dist, void* stream);
 
+/* Delivery of a batch's outputs to the host thread that consumes them (the
+ * Tracking thread reads one Frame's mvKeys / mDescriptors,
+ * src/Tracking.cpp:280-317): the B frames' rows -- `rows` holds B x cap rows
+ * of row_bytes each (a multiple of 4), frame b's first counts[b] rows used --
+ * packed back to back into `packed` (frame b at sum_{b' < b} counts[b']), so
+ * a single copy of sum(counts) rows moves only used data.  Up to four
+ * tensors per call (keypoints, descriptors, matches, ...), each with its own
+ * counts (device pointers); asynchronous on `stream`. */
+typedef struct orbgpu_pack_desc {
+    const uint8_t* rows;
+    uint8_t* packed;
+    const int* counts;
+    int row_bytes;
+} orbgpu_pack_desc;
+int orbgpu_pack_rows_device(int batch, int cap, int ntensors, const orbgpu_pack_desc* descs, void* stream);
+
 /* Frame image bounds of the 64x48 feature grid: Frame::mnMinX, mnMaxX,
  * mnMinY, mnMaxY (Frame.cpp:505-530; [0,cols]x[0,rows] without distortion). */
 typedef struct orbgpu_grid_bounds {

@@ -188,18 +188,22 @@ struct KeyRef {
 
 __device__ bool key_ref(const Geom& g, int f, int slot, int lane, const uint32_t* __restrict__ oct_out,
                         const int* __restrict__ oct_count, int* __restrict__ counts, KeyRef& K) {
-    int l = 0;
-    while (l + 1 < g.nlevels && slot >= g.lv[l + 1].out_offset) ++l;
-    const int i = slot - g.lv[l].out_offset;
-    const int* oc = oct_count + (size_t)f * g.nlevels;
-    int before = 0, total = 0;
-    for (int ll = 0; ll < g.nlevels; ++ll) {
-        const int c = oc[ll];
-        total += c;
-        if (ll < l) before += c;
-    }
-    if (slot == 0 && lane == 0) counts[f] = total;
-    if (i >= oc[l]) return false;
+    // level and index of the slot: one scalar load; the frame's per-level
+    // counts on lanes 0..15 (each 16-lane row holds them all), prefix sums by
+    // DPP row shifts, the values this slot needs read out of lane l / 15
+    const uint32_t se = g.slot_tab[slot];
+    const int l = (int)(se & 15u), i = (int)(se >> 4);
+    const int ll = lane & 15;
+    const int c = ll < g.nlevels ? oct_count[(size_t)f * kOcStride + ll] : 0;
+    int sc = c;
+    sc += __builtin_amdgcn_update_dpp(0, sc, 0x111, 0xF, 0xF, true);  // row_shr:1
+    sc += __builtin_amdgcn_update_dpp(0, sc, 0x112, 0xF, 0xF, true);  // row_shr:2
+    sc += __builtin_amdgcn_update_dpp(0, sc, 0x114, 0xF, 0xF, true);  // row_shr:4
+    sc += __builtin_amdgcn_update_dpp(0, sc, 0x118, 0xF, 0xF, true);  // row_shr:8
+    const int mine = __builtin_amdgcn_readlane(c, l);
+    const int before = __builtin_amdgcn_readlane(sc, l) - mine;
+    if (slot == 0 && lane == 0) counts[f] = __builtin_amdgcn_readlane(sc, 15);
+    if (i >= mine) return false;
     K.l = l;
     K.i = i;
     K.before = before;
@@ -388,6 +392,16 @@ __device__ void describe_tests(const Geom& g, int f, const KeyRef& K, int lane, 
     }
 }
 
+// Diagnostic build (-DDESC_STAMPS): every 64th item's wave adds its phase
+// durations (s_memtime cycles) to g_desc_stamps[phase], and [15] counts the
+// sampled waves; tools/extract_stamps.py prints the per-wave means.
+#ifdef DESC_STAMPS
+__device__ unsigned long long g_desc_stamps[16];
+#define DSTAMP(k) (stamp_on ? (ts[k] = __builtin_amdgcn_s_memtime()) : 0ull)
+#else
+#define DSTAMP(k) ((void)0)
+#endif
+
 #ifndef ORBGPU_DESC_WAVES
 #define ORBGPU_DESC_WAVES 4
 #endif
@@ -419,11 +433,18 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
     const int blk = (int)blockIdx.x;
 #endif
     const int item = blk * kDescWaves + wave;
+#ifdef DESC_STAMPS
+    const bool stamp_on = (item & 63) == 0;
+    unsigned long long ts[8] = {};
+#endif
+    DSTAMP(0);
     const int f = item / g.slots_frame, slot = item - f * g.slots_frame;
     KeyRef K;
     const bool valid = item < items && key_ref(g, f, slot, lane, oct_out, oct_count, counts, K);
     if (!valid) return;
+    DSTAMP(1);
     const int2 m = describe_patch(g, f, K, lane, s_lds[wave], img0, row0, frame0, pyr);
+    DSTAMP(2);
     // the orientation: a serial chain on wave-uniform values, run by the
     // whole wave (measured: sharing it across the block's waves through LDS
     // and two barriers made the kernel slower, 0.574 -> 0.593 ms)
@@ -431,10 +452,29 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
     float sa, ca;
     glibc_sincosf(__fmul_rn(angle, (float)(M_PI / 180.f)), &sa, &ca);
     wave_sync();  // blurred patch complete
+    DSTAMP(3);
     describe_tests(g, f, K, lane, s_lds[wave], float4{angle, ca, sa, 0.f}, kps, desc, kp_cap);
+#ifdef DESC_STAMPS
+    DSTAMP(4);
+    if (stamp_on && lane == 0) {
+        for (int k = 1; k <= 4; ++k) atomicAdd(&g_desc_stamps[k - 1], ts[k] - ts[k - 1]);
+        atomicAdd(&g_desc_stamps[15], 1ull);
+    }
+#endif
 }
 
 }  // namespace
+
+#ifdef DESC_STAMPS
+extern "C" int orbgpu_debug_desc_stamps(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_desc_stamps), sizeof(g_desc_stamps)) != hipSuccess) return -2;
+    if (reset) {
+        unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_desc_stamps), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
 
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                            const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,

@@ -127,9 +127,16 @@ __device__ int compass_pass(const CellTiles& T, int dw, int dh, int ox, int t, i
 // compass pre-test on every pixel -> arc strength of the survivors, two per
 // lane in packed 16-bit arithmetic (the corner test is s >= t + 1).
 template <int P>
-__device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, int lane) {
+__device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, int lane,
+                            unsigned long long* stamp = nullptr) {
     const int na = dw > 32 ? compass_pass<P, 64>(T, dw, dh, ox, t, lane) : compass_pass<P, 32>(T, dw, dh, ox, t, lane);
     wave_sync();
+#ifdef FAST_STAMPS
+    if (stamp) {
+        stamp[0] = __builtin_amdgcn_s_memtime();
+        stamp[1] = (unsigned long long)na;
+    }
+#endif
     // Survivors -> corners, two per lane (list entries base + lane and
     // base + 64 + lane, one per 16-bit half).  With d = v - ring, the arc
     // strength max over arcs of max(min d, -max d) is
@@ -240,6 +247,17 @@ __device__ int nms_emit(const CellTiles& T, int nb, int ox, int t, int lane, int
     return total;
 }
 
+// Diagnostic build (-DFAST_STAMPS): every 16th cell's wave adds its phase
+// durations (s_memtime cycles) to g_fast_stamps[phase] and its survivor /
+// corner counts to [8] / [9]; [15] counts the sampled waves
+// (tools/extract_stamps.py).
+#ifdef FAST_STAMPS
+__device__ unsigned long long g_fast_stamps[16];
+#define FSTAMP(k) (stamp_on ? (ts[k] = __builtin_amdgcn_s_memtime()) : 0ull)
+#else
+#define FSTAMP(k) ((void)0)
+#endif
+
 #ifndef ORBGPU_FAST_CELL_WAVES
 #define ORBGPU_FAST_CELL_WAVES 1
 #endif
@@ -275,13 +293,18 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     const int item = (int)blockIdx.x * kCellWaves + wave;
 #endif
     if (item >= ncells_total) return;
+#ifdef FAST_STAMPS
+    const bool stamp_on = (item & 15) == 0;
+    unsigned long long ts[8] = {};
+#endif
+    FSTAMP(0);
     const int f = item / g.total_cells;
     const int gc = item - f * g.total_cells;
-    int l = 0;
-    while (l + 1 < g.nlevels && gc >= g.lv[l + 1].cell_base) ++l;
+    // level and cell coordinates of the frame's cell gc: one scalar load
+    const uint32_t ce = g.cell_tab[gc];
+    const int l = (int)(ce & 15u), ci = (int)((ce >> 4) & 0x3FFFu), cj = (int)(ce >> 18);
     const LevelGeom& L = g.lv[l];
-    const int c = gc - L.cell_base;
-    const int ci = c / L.ncols, cj = c - ci * L.ncols;
+    const int c = ci * L.ncols + cj;
     int* cnt_out = cell_counts + (size_t)f * g.total_cells + gc;
     uint32_t* out = cand + (size_t)f * g.cand_frame + L.cand_offset + (size_t)c * L.cell_cap;
 
@@ -346,14 +369,31 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     for (int idx = lane; idx < nz16; idx += 64) reinterpret_cast<uint4*>(T.sc)[idx] = make_uint4(0u, 0u, 0u, 0u);
     for (int idx = nz16 * 4 + lane; idx < P * R / 4; idx += 64) reinterpret_cast<uint32_t*>(T.sc)[idx] = 0u;
     wave_sync();
+    FSTAMP(1);
 
     // detection region of cv::FAST on the window: rows [3, wh-3), cols [3, ww-3)
     const int dw = maxX - iniX - 6, dh = wh - 6;
     int total = 0;
+#ifdef FAST_STAMPS
+    int st_nb = 0, st_retry = 0;
+    unsigned long long cst[2] = {0, 0};
+#endif
     if (dw > 0 && dh > 0) {
+#ifdef FAST_STAMPS
+        int nb = fast_corners<P>(T, dw, dh, ox, g.ini_th, lane, stamp_on ? cst : nullptr);
+#else
         int nb = fast_corners<P>(T, dw, dh, ox, g.ini_th, lane);
+#endif
+        FSTAMP(2);
         total = nms_emit<P>(T, nb, ox, g.ini_th, lane, iniX, iniY, out, L.cell_cap, err);
+        FSTAMP(3);
+#ifdef FAST_STAMPS
+        st_nb = nb;
+#endif
         if (total == 0) {  // ORBextractor.cpp:821-825: retry the cell at minThFAST
+#ifdef FAST_STAMPS
+            st_retry = 1;
+#endif
             for (int j = lane; j < nb; j += 64) T.sc[T.lb[j]] = 0;
             wave_sync();
             nb = fast_corners<P>(T, dw, dh, ox, g.min_th, lane);
@@ -361,9 +401,35 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
         }
     }
     if (lane == 0) *cnt_out = min(total, L.cell_cap);
+#ifdef FAST_STAMPS
+    FSTAMP(4);
+    if (stamp_on && lane == 0) {
+        if (dw > 0 && dh > 0) {
+            for (int k = 1; k <= 4; ++k) atomicAdd(&g_fast_stamps[k - 1], ts[k] - ts[k - 1]);
+            atomicAdd(&g_fast_stamps[6], cst[0] - ts[1]);  // compass part of fast_corners
+            atomicAdd(&g_fast_stamps[8], cst[1]);          // compass survivors
+        } else
+            atomicAdd(&g_fast_stamps[4], ts[4] - ts[0]);
+        atomicAdd(&g_fast_stamps[5], ts[1] - ts[0]);
+        atomicAdd(&g_fast_stamps[9], (unsigned long long)st_nb);
+        atomicAdd(&g_fast_stamps[10], (unsigned long long)st_retry);
+        atomicAdd(&g_fast_stamps[15], 1ull);
+    }
+#endif
 }
 
 }  // namespace
+
+#ifdef FAST_STAMPS
+extern "C" int orbgpu_debug_fast_stamps(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fast_stamps), sizeof(g_fast_stamps)) != hipSuccess) return -2;
+    if (reset) {
+        unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_fast_stamps), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
 
 
 hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,

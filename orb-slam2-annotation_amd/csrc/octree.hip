@@ -145,7 +145,7 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
     const int N = L.nfeat;
     const int nini = L.nini;
     if (nini > ncap) {
-        if (tid == 0) { atomicOr(err, kErrNodeCap); oct_count[f * g.nlevels + l] = 0; }
+        if (tid == 0) { atomicOr(err, kErrNodeCap); oct_count[f * kOcStride + l] = 0; }
         return;
     }
 
@@ -347,7 +347,7 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
         }
         const int nNew = C + S;
         if (nNew > ncap || nseq + C > 0x0FFFFFFF) {
-            if (tid == 0) { atomicOr(err, nNew > ncap ? kErrNodeCap : kErrSeqCap); oct_count[f * g.nlevels + l] = 0; }
+            if (tid == 0) { atomicOr(err, nNew > ncap ? kErrNodeCap : kErrSeqCap); oct_count[f * kOcStride + l] = 0; }
             return;
         }
         for (int i = tid; i < nL; i += NT) {
@@ -406,11 +406,11 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
         atomicMax(&s_qc[ks.node(k)], ((uint32_t)key_s(ks.key(k)) << 24) | (0xFFFFFFu - (uint32_t)k));
     __syncthreads();
     if (nL > L.ocap) {
-        if (tid == 0) { atomicOr(err, kErrNodeCap); oct_count[f * g.nlevels + l] = 0; }
+        if (tid == 0) { atomicOr(err, kErrNodeCap); oct_count[f * kOcStride + l] = 0; }
         return;
     }
     for (int i = tid; i < nL; i += NT) out[i] = ks.key((int)(0xFFFFFFu - (s_qc[i] & 0xFFFFFFu)));
-    if (tid == 0) oct_count[f * g.nlevels + l] = nL;
+    if (tid == 0) oct_count[f * kOcStride + l] = nL;
     OCT_T(63);
 }
 

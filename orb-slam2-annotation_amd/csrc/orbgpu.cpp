@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <array>
 #include <cmath>
 #include <cstdint>
@@ -149,6 +150,7 @@ struct orbgpu_extractor {
     uint32_t* d_gkeys = nullptr;
     uint16_t* d_gknode = nullptr;
     uint32_t* d_oct_out = nullptr;
+    uint32_t* d_tab = nullptr;     // cell_tab then slot_tab (Geom)
     int* d_oct_count = nullptr;
     int* d_err = nullptr;
     int* d_trace = nullptr;  // optional octree pass trace (debug API)
@@ -188,7 +190,7 @@ struct orbgpu_extractor {
 
     ~orbgpu_extractor() {
         void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_ent, d_pyr_tab, d_xtab, d_ytab, d_band, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
-                        d_oct_count, d_err, d_trace, d_img, d_single};
+                        d_oct_count, d_err, d_trace, d_img, d_single, d_tab};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
         for (auto& sc : stereo_sad) (void)hipFree(sc.d);
@@ -362,6 +364,10 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     g.total_cells = cell_base;
     g.cand_frame = cand_off;
     g.slots_frame = out_off;
+    for (int l = 0; l < kMaxLevels; ++l) {
+        g.lvl_cell_base[l] = l < L ? g.lv[l].cell_base : INT_MAX;
+        g.lvl_out_offset[l] = l < L ? g.lv[l].out_offset : INT_MAX;
+    }
     g.max_cells_level = max_cells;
     size_t blur_off = 0;
     int tiles = 0;
@@ -549,13 +555,29 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
         (rc = dalloc(&e->d_cand, g.cand_frame * B)) ||
         (rc = dalloc(&e->d_cell_counts, (size_t)g.total_cells * B)) || (rc = dalloc(&e->d_gkeys, g.cand_frame * B)) ||
         (rc = dalloc(&e->d_gknode, g.cand_frame * B)) || (rc = dalloc(&e->d_oct_out, (size_t)g.slots_frame * B)) ||
-        (rc = dalloc(&e->d_oct_count, (size_t)g.nlevels * B)) || (rc = dalloc(&e->d_err, 1)) ||
+        (rc = dalloc(&e->d_oct_count, (size_t)kOcStride * B)) || (rc = dalloc(&e->d_err, 1)) ||
         (rc = dalloc(&e->d_img, e->img_pitch * height)) ||
         (rc = dalloc(&e->d_pyr_ent, e->pyr_plan.ent.size())) || (rc = dalloc(&e->d_pyr_tab, e->pyr_plan.tab.size())) ||
         (rc = dalloc(&e->d_xtab, xtab.size())) || (rc = dalloc(&e->d_ytab, ytab.size())) ||
-        (rc = dalloc(&e->d_band, std::max<size_t>(bands.size(), 1)))) {
+        (rc = dalloc(&e->d_band, std::max<size_t>(bands.size(), 1))) ||
+        (rc = dalloc(&e->d_tab, (size_t)g.total_cells + g.slots_frame))) {
         delete e;
         return rc;
+    }
+    {  // per-cell / per-slot lookup tables (Geom::cell_tab, slot_tab)
+        std::vector<uint32_t> tab((size_t)g.total_cells + g.slots_frame);
+        for (int l = 0; l < g.nlevels; ++l) {
+            const LevelGeom& v = g.lv[l];
+            for (int c = 0; c < v.ncols * v.nrows; ++c)
+                tab[(size_t)v.cell_base + c] = (uint32_t)l | (uint32_t)(c / v.ncols) << 4 | (uint32_t)(c % v.ncols) << 18;
+            for (int i = 0; i < v.ocap; ++i) tab[(size_t)g.total_cells + v.out_offset + i] = (uint32_t)l | (uint32_t)i << 4;
+        }
+        if (hipMemcpy(e->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            delete e;
+            return fail(ORBGPU_ERR_HIP, "table upload failed");
+        }
+        e->g.cell_tab = e->d_tab;
+        e->g.slot_tab = e->d_tab + g.total_cells;
     }
     e->single_desc_off = round_up(16 + (size_t)e->max_kps * sizeof(orbgpu_keypoint), 256);
     e->single_bytes = e->single_desc_off + (size_t)e->max_kps * 32;
@@ -777,6 +799,17 @@ int orbgpu_hamming_pairs_device(const uint8_t* a, const uint8_t* b, int n, int* 
     return ORBGPU_OK;
 }
 
+int orbgpu_pack_rows_device(int batch, int cap, int ntensors, const orbgpu_pack_desc* d, void* stream) {
+    if (batch < 0 || cap < 0 || ntensors < 0 || ntensors > 4 || (ntensors > 0 && !d))
+        return fail(ORBGPU_ERR_ARG, "invalid argument");
+    for (int t = 0; t < ntensors; ++t)
+        if (!d[t].rows || !d[t].packed || !d[t].counts || d[t].row_bytes <= 0 || (d[t].row_bytes & 3) ||
+            (((uintptr_t)d[t].rows | (uintptr_t)d[t].packed) & 3))
+            return fail(ORBGPU_ERR_ARG, "pack: rows must be 4-byte multiples at 4-byte aligned addresses");
+    ORB_HIP(launch_pack_rows(batch, cap, ntensors, d, (hipStream_t)stream));
+    return ORBGPU_OK;
+}
+
 int orbgpu_search_for_initialization_batch_device(int batch, orbgpu_grid_bounds bd, const orbgpu_keypoint* kps1,
                                                   const uint8_t* desc1, const int* n1, size_t stride1,
                                                   const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2,
@@ -885,7 +918,7 @@ int orbgpu_debug_level_octree(orbgpu_extractor* e, int frame, int level, int* xy
     const LevelGeom& v = g.lv[level];
     int n = 0;
     ORB_HIP(hipDeviceSynchronize());
-    ORB_HIP(hipMemcpy(&n, e->d_oct_count + (size_t)frame * g.nlevels + level, sizeof(int), hipMemcpyDeviceToHost));
+    ORB_HIP(hipMemcpy(&n, e->d_oct_count + (size_t)frame * kOcStride + level, sizeof(int), hipMemcpyDeviceToHost));
     std::vector<uint32_t> keys(std::max(n, 1));
     ORB_HIP(hipMemcpy(keys.data(), e->d_oct_out + (size_t)frame * g.slots_frame + v.out_offset,
                       (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost));

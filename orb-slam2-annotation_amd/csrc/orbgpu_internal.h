@@ -11,6 +11,9 @@
 namespace orbgpu {
 
 constexpr int kMaxLevels = 16;
+// per-frame stride of the octree's per-level counts (oct_count): one 64-byte
+// record per frame, so a wave loads all of a frame's counts in one scalar load
+constexpr int kOcStride = kMaxLevels;
 constexpr int kEdge = 19;              // EDGE_THRESHOLD (ORBextractor.cpp:76)
 constexpr int kBorder = kEdge - 3;     // minBorderX/Y (ORBextractor.cpp:781)
 #ifndef ORBGPU_BLUR_STRIP
@@ -60,6 +63,15 @@ __host__ __device__ inline int key_x(uint32_t k) { return (int)(k & 0x7FF); }
 __host__ __device__ inline int key_y(uint32_t k) { return (int)((k >> 11) & 0x7FF); }
 __host__ __device__ inline int key_s(uint32_t k) { return (int)(k >> 22); }
 
+// level of index `i` given a packed table of level start indices (entry 0 is
+// 0, entries past the last level INT_MAX): compares only, wave-uniform
+__host__ __device__ inline int level_of(const int (&base)[kMaxLevels], int i) {
+    int l = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxLevels; ++k) l += i >= base[k];
+    return l;
+}
+
 struct LevelGeom {
     int w, h;                 // level size (ComputePyramid, ORBextractor.cpp:1128)
     int pitch;                // row pitch in the pyramid buffer (levels >= 1)
@@ -101,6 +113,17 @@ struct LevelGeom {
 
 struct Geom {
     int nlevels;
+    // level lookup tables, packed so one scalar load brings a whole table and the
+    // level of an index is a count of compares (no dependent loads per level):
+    // entry l = lv[l].cell_base / lv[l].out_offset, INT_MAX past the last level
+    int lvl_cell_base[kMaxLevels];
+    int lvl_out_offset[kMaxLevels];
+    // per-index lookup tables in HBM (built once per geometry), one scalar load
+    // per wave: cell_tab[gc] = level | ci << 4 | cj << 18 for the frame's cell gc
+    // (FAST), slot_tab[slot] = level | i << 4 for octree output slot `slot`
+    // (describe)
+    const uint32_t* cell_tab;
+    const uint32_t* slot_tab;
     int width, height;
     int ini_th, min_th;
     int total_cells;          // cells per frame over all levels

@@ -6,6 +6,7 @@
 #include "orbgpu_internal.h"
 
 struct orbgpu_keypoint;
+struct orbgpu_pack_desc;
 
 namespace orbgpu {
 
@@ -66,6 +67,7 @@ hipError_t launch_match_init(int batch, float minX, float maxX, float minY, floa
                              int* matches12, int* nmatches, hipStream_t stream, size_t level0_bound = 0);
 
 hipError_t launch_hamming_pairs(const uint8_t* a, const uint8_t* b, int n, int* dist, hipStream_t stream);
+hipError_t launch_pack_rows(int batch, int cap, int ntensors, const ::orbgpu_pack_desc* d, hipStream_t stream);
 
 // error bits written to the device error word
 enum : int {

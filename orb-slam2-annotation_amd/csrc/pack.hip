@@ -1,0 +1,54 @@
+// pack.hip -- a batch's per-frame outputs trimmed to their counts and packed
+// back to back, for delivery to the Tracking thread that consumes them
+// (src/Tracking.cpp:280-317 reads one Frame's mvKeys / mDescriptors; the
+// batch path keeps B frames x capacity rows in HBM).  One launch packs up to
+// four row tensors (keypoints, descriptors, matches, ...): block (b, t) copies
+// frame b's counts[t][b] rows of tensor t to the offset sum_{b' < b}
+// counts[t][b'] -- a block-wide sum over the preceding frames' counts, then a
+// dword copy (every row size here is a multiple of 4 bytes).  HBM-bound:
+// each used row is read once and written once.
+#include "../../include/orbgpu.h"
+#include "orbgpu_internal.h"
+#include "orbgpu_kernels.h"
+
+namespace orbgpu {
+
+namespace {
+
+constexpr int kPackThreads = 256;
+
+__global__ __launch_bounds__(kPackThreads) void pack_rows_kernel(orbgpu_pack_desc d0, orbgpu_pack_desc d1,
+                                                                 orbgpu_pack_desc d2, orbgpu_pack_desc d3, int cap) {
+    const int t = blockIdx.y;
+    const orbgpu_pack_desc& D = t == 0 ? d0 : t == 1 ? d1 : t == 2 ? d2 : d3;
+    const int b = blockIdx.x;
+    __shared__ int s_part[kPackThreads / 64];
+    // offset of frame b: the counts of frames 0 .. b-1 (B <= a few thousand)
+    int part = 0;
+    for (int j = threadIdx.x; j < b; j += kPackThreads) part += D.counts[j];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = part;
+    __syncthreads();
+    int off = 0;
+#pragma unroll
+    for (int w = 0; w < kPackThreads / 64; ++w) off += s_part[w];
+    const int n = min(max(D.counts[b], 0), cap);
+    const int words = D.row_bytes >> 2;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(D.rows + (size_t)b * cap * D.row_bytes);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(D.packed + (size_t)off * D.row_bytes);
+    const int total = n * words;
+    for (int k = threadIdx.x; k < total; k += kPackThreads) dst[k] = src[k];
+}
+
+}  // namespace
+
+hipError_t launch_pack_rows(int batch, int cap, int ntensors, const orbgpu_pack_desc* d, hipStream_t stream) {
+    if (batch <= 0 || ntensors <= 0) return hipSuccess;
+    const orbgpu_pack_desc z{};
+    hipLaunchKernelGGL(pack_rows_kernel, dim3(batch, ntensors), dim3(kPackThreads), 0, stream, d[0],
+                       ntensors > 1 ? d[1] : z, ntensors > 2 ? d[2] : z, ntensors > 3 ? d[3] : z, cap);
+    return hipGetLastError();
+}
+
+}  // namespace orbgpu

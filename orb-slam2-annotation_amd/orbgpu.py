@@ -45,6 +45,12 @@ class GridBounds(ctypes.Structure):
                 ("min_y", ctypes.c_float), ("max_y", ctypes.c_float)]
 
 
+class PackDesc(ctypes.Structure):
+    """orbgpu_pack_desc (include/orbgpu.h)"""
+    _fields_ = [("rows", ctypes.c_void_p), ("packed", ctypes.c_void_p), ("counts", ctypes.c_void_p),
+                ("row_bytes", ctypes.c_int)]
+
+
 class Camera(ctypes.Structure):
     """orbgpu_camera: mK (fx, fy, cx, cy) and mDistCoef (k1, k2, p1, p2[, k3])."""
     _fields_ = [("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
@@ -103,6 +109,7 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_extractor_set_stage_event.argtypes = [vp, i, vp]
         L.orbgpu_extractor_copy_level.argtypes = [vp, i, i, vp, sz]
         L.orbgpu_hamming_pairs_device.argtypes = [vp, vp, i, vp, vp]
+        L.orbgpu_pack_rows_device.argtypes = [i, i, i, ctypes.POINTER(PackDesc), vp]
         L.orbgpu_search_for_initialization_batch_device.argtypes = [
             i, GridBounds, vp, vp, vp, sz, vp, vp, vp, sz, vp, i, f, i, vp, vp, vp]
         L.orbgpu_debug_level_candidates.argtypes = [vp, i, i, vp, i]
@@ -386,6 +393,23 @@ def hamming_pairs(a, b, out, stream=None):
     """DescriptorDistance over n pairs of device descriptors (n, 32) uint8."""
     _check(lib().orbgpu_hamming_pairs_device(_ptr(a), _ptr(b), a.shape[0], _ptr(out), _stream_ptr(stream)),
            "orbgpu_hamming_pairs_device")
+
+
+def pack_rows(batch: int, cap: int, items, stream=None) -> None:
+    """orbgpu_pack_rows_device: items = [(rows (batch, cap, ...) tensor,
+    packed tensor with >= batch * cap rows, counts int32 (batch,) tensor)];
+    frame b's first counts[b] rows land at sum_{b' < b} counts[b'] of
+    packed (asynchronous on `stream`)."""
+    import torch
+    descs = (PackDesc * len(items))()
+    for d, (rows, packed, counts) in zip(descs, items):
+        assert rows.is_contiguous() and packed.is_contiguous() and counts.is_contiguous()
+        assert counts.dtype == torch.int32 and counts.numel() >= batch and rows.shape[1] == cap
+        rb = rows[0, 0].numel() * rows.element_size()
+        assert packed[0].numel() * packed.element_size() == rb and packed.shape[0] >= batch * cap
+        d.rows, d.packed, d.counts, d.row_bytes = rows.data_ptr(), packed.data_ptr(), counts.data_ptr(), rb
+    _check(lib().orbgpu_pack_rows_device(batch, cap, len(items), descs, _stream_ptr(stream)),
+           "orbgpu_pack_rows_device")
 
 
 def stereo_matches_batch(ex: "Extractor", images, npairs, kps, desc, counts, bf, min_z, uright, depth,

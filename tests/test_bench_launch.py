@@ -51,16 +51,36 @@ def test_gpus_flag_rejects_mismatched_world_size():
     assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr
 
 
-def test_mono_stream_two_ranks_equals_single_process(tmp_path):
+def _merge_rank_dumps(tmp_path, name, world):
+    parts = [np.load(tmp_path / f"{name}_rank{r}.npz") for r in range(world)]
+    units = np.concatenate([p["units"] for p in parts])
+    order = np.argsort(units)
+    return {k: np.concatenate([p[k] for p in parts])[order] for k in parts[0].files}
+
+
+@pytest.mark.parametrize("deliver", ["host", "gpu0"])
+def test_mono_stream_two_ranks_equals_single_process(tmp_path, deliver):
+    """both delivery modes (shard.Delivery): host -- each rank's trimmed
+    outputs in its own host memory (merged here from the per-rank dumps);
+    gpu0 -- counts first, then the used rows, received by rank 0"""
     import orbref
     import shard
     import synth
     import torch
     world, B, steps = 2, 2, 2
-    line = _run_bench(tmp_path, "--config", "mono640", "--batch", str(B), "--steps", str(steps), "--warmup", "0")
+    line = _run_bench(tmp_path, "--config", "mono640", "--batch", str(B), "--steps", str(steps), "--warmup", "0",
+                      "--deliver", deliver)
     assert line["n_gpus"] == 2 and line["world_size_checked"] == 2
     assert line["config"]["frames_per_gpu_per_step"] == B
-    got = np.load(tmp_path / "mono_640x480.npz")
+    dl = line["delivery"]
+    assert dl["mode"] == deliver and len(dl["per_rank"]) == 2
+    if deliver == "host":  # every rank moves its own outputs
+        assert all(p["bytes_per_step"] > 0 for p in dl["per_rank"])
+        got = _merge_rank_dumps(tmp_path, "mono_640x480", world)
+    else:  # rank 1 sends, rank 0 receives exactly that
+        assert dl["per_rank"][1]["bytes_per_step"] > 0 and dl["per_rank"][0]["bytes_per_step"] == 0
+        assert dl["per_rank"][0]["recv_bytes_per_step"] + 4 * 3 * B == dl["per_rank"][1]["bytes_per_step"]
+        got = np.load(tmp_path / "mono_640x480.npz")
     n_frames = world * B * steps
     assert list(got["units"]) == list(range(n_frames))
     frames = {}
@@ -116,3 +136,41 @@ def test_stereo_pairs_two_ranks_equal_single_process(tmp_path):
             assert got["uright"][pair][:len(kl)].tobytes() == ur.tobytes()
             assert got["depth"][pair][:len(kl)].tobytes() == dp.tobytes()
             assert (ur >= 0).sum() > 0.3 * len(kl)  # a real stereo scene
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("deliver", ["host", "gpu0"])
+def test_gpu_host_fed_stream_frames_equal_oracle(tmp_path, deliver):
+    """The host-fed path on the GPU (bench.py --feed host: frames copied from
+    pinned host memory through the double-buffered H2D stream) with each
+    delivery mode: every delivered frame's keypoints, descriptors and matches
+    equal the CPU oracle on the same frames."""
+    import orbref
+    import synth
+    import torch
+    B, steps = 3, 2
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--feed", "host", "--deliver", deliver, "--batch", str(B),
+           "--steps", str(steps), "--warmup", "0", "--dump", str(tmp_path), "--no-cpu-baseline", "--no-extras"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(ROOT))
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    line = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["h2d"]["bytes_per_step"] == B * 480 * 640 and line["delivery"]["mode"] == deliver
+    got = np.load(tmp_path / "mono_640x480.npz")
+    assert list(got["units"]) == list(range(B * steps))
+    ex = orbref.Extractor(1000)
+    prev = None
+    for s in range(steps):
+        imgs = synth.torch_stream(B, 640, 480, device="cuda", pitch=640, bounded=True, t0=s * B).cpu()
+        for b in range(B):
+            f = s * B + b
+            k, d = ex.extract(imgs[b].numpy())
+            n = len(k)
+            assert got["count"][f] == n and got["kps"][f][:n].tobytes() == k.tobytes(), f
+            assert np.array_equal(got["desc"][f][:n], d), f
+            if prev is not None:
+                nm, m12, _ = orbref.search_for_initialization(prev[0], prev[1], k, d, 640, 480)
+                assert got["nmatch"][f] == nm and np.array_equal(got["m12"][f][:len(prev[0])], m12), f
+            prev = (k, d)

@@ -125,3 +125,37 @@ def test_hamming_pairs_device(n):
     np.testing.assert_array_equal(out.cpu().numpy()[:n], want)
     for i in range(min(n, 50)):
         assert want[i] == orbref.descriptor_distance(a[i], b[i])
+
+
+@pytest.mark.gpu
+def test_pack_rows_device_equals_host_unpack():
+    """orbgpu_pack_rows_device (the delivery of a batch's trimmed outputs):
+    frame b's first counts[b] rows of each tensor at the exclusive prefix sum
+    of the counts, for keypoint (28 B), descriptor (32 B) and match (4 B) rows,
+    ragged counts including empty frames and full-capacity frames."""
+    import torch
+    import orbgpu
+    import shard
+    rng = np.random.default_rng(5)
+    B, cap = 37, 130
+    counts = rng.integers(0, cap + 1, B).astype(np.int32)
+    counts[[0, 7, 8]] = 0
+    counts[[3, 36]] = cap
+    kps = torch.tensor(rng.standard_normal((B, cap, 7)).astype(np.float32), device="cuda")
+    desc = torch.tensor(rng.integers(0, 256, (B, cap, 32)).astype(np.uint8), device="cuda")
+    m12 = torch.tensor(rng.integers(-2, 500, (B, cap)).astype(np.int32), device="cuda")
+    c = torch.tensor(counts, device="cuda")
+    c2 = torch.tensor(counts[::-1].copy(), device="cuda")
+    pk = torch.zeros((B * cap, 7), dtype=torch.float32, device="cuda")
+    pd = torch.zeros((B * cap, 32), dtype=torch.uint8, device="cuda")
+    pm = torch.zeros(B * cap, dtype=torch.int32, device="cuda")
+    orbgpu.pack_rows(B, cap, [(kps, pk, c), (desc, pd, c), (m12, pm, c2)])
+    torch.cuda.synchronize()
+    for rows, packed, cnt in ((kps, pk, counts), (desc, pd, counts), (m12, pm, counts[::-1])):
+        n = int(cnt.sum())
+        back = shard.unpack_rows(packed[:n].cpu().numpy(), cnt, cap)
+        ref = rows.cpu().numpy().copy()
+        for b in range(B):
+            ref[b, cnt[b]:] = 0
+        assert np.array_equal(back, ref)
+        assert not packed[n:].cpu().numpy().any()  # nothing written past the used rows
