@@ -810,7 +810,7 @@ class DropIn:
     The scenarios come from synth.py (FeatureVectors and isInFrustum flags
     from the GPU library itself)."""
 
-    def __init__(self, workdir: Path, reps: int = 60):
+    def __init__(self, workdir: Path, reps: int = 100):
         self.dir, self.reps = workdir, reps
         self.scen = {}
 

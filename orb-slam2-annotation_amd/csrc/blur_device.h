@@ -68,10 +68,29 @@ struct Raw3 {
     uint32_t a, b, c;  // level columns x0-4 .. x0+7
 };
 
-// Row pass of the 4 columns x0..x0+3 from the three raw words around them:
-// per column the 7 taps are two 4-byte windows cut out by v_alignbyte_b32,
-// [x-3, x] against (18, 34, 49, 55) and [x+1, x+4) against (49, 34, 18, 0),
-// summed exactly by two v_dot4_u32_u8 (at most 255 * 257 = 65535).
+// Row pass of the 4 columns x0..x0+3 from the three raw words around them,
+// with no byte shuffling: column x0 + m takes its 7 taps from the words as
+// they are, against the kernel shifted by m bytes -- m = 0: a[1..3] b[0..3];
+// m = 1: a[2..3] b c[0]; m = 2: a[3] b c[0..1]; m = 3: b c[0..2] -- ten
+// v_dot4_u32_u8 in all (2 + 3 + 3 + 2), exact (at most 255 * 257 = 65535).
+__device__ __forceinline__ void row_pass_raw_shifted(const Raw3& R, f32x2& lo, f32x2& hi) {
+    constexpr uint32_t A0 = 0u | 18u << 8 | 34u << 16 | 49u << 24, B0 = 55u | 49u << 8 | 34u << 16 | 18u << 24;
+    constexpr uint32_t A1 = 18u << 16 | 34u << 24, B1 = 49u | 55u << 8 | 49u << 16 | 34u << 24, C1 = 18u;
+    constexpr uint32_t A2 = 18u << 24, B2 = 34u | 49u << 8 | 55u << 16 | 49u << 24, C2 = 34u | 18u << 8;
+    constexpr uint32_t B3 = 18u | 34u << 8 | 49u << 16 | 55u << 24, C3 = 49u | 34u << 8 | 18u << 16;
+    const uint32_t s0 = __builtin_amdgcn_udot4(R.b, B0, __builtin_amdgcn_udot4(R.a, A0, 0u, false), false);
+    const uint32_t s1 = __builtin_amdgcn_udot4(
+        R.c, C1, __builtin_amdgcn_udot4(R.b, B1, __builtin_amdgcn_udot4(R.a, A1, 0u, false), false), false);
+    const uint32_t s2 = __builtin_amdgcn_udot4(
+        R.c, C2, __builtin_amdgcn_udot4(R.b, B2, __builtin_amdgcn_udot4(R.a, A2, 0u, false), false), false);
+    const uint32_t s3 = __builtin_amdgcn_udot4(R.c, C3, __builtin_amdgcn_udot4(R.b, B3, 0u, false), false);
+    lo = f32x2{(float)s0, (float)s1};
+    hi = f32x2{(float)s2, (float)s3};
+}
+
+// The same sums with the windows cut out by v_alignbyte_b32 ([x-3, x]
+// against (18, 34, 49, 55), [x+1, x+4) against (49, 34, 18, 0)): the form
+// blur.hip's whole-level pass uses.
 __device__ __forceinline__ void row_pass_raw(const Raw3& R, f32x2& lo, f32x2& hi) {
     constexpr uint32_t K1 = 18u | 34u << 8 | 49u << 16 | 55u << 24;  // taps x-3 .. x
     constexpr uint32_t K2 = 49u | 34u << 8 | 18u << 16;              // taps x+1 .. x+3

@@ -28,13 +28,14 @@ namespace {
 constexpr signed char kPattern[1024] = {
 #include "bit_pattern_31.inc"
 };
-// the pattern as floats, one float4 (x0, y0, x1, y1) per test: a lane's test
-// is one 16-byte load, no per-coordinate conversions
+// the pattern as floats, one float4 (x0, x1, y0, y1) per test: a lane's test
+// is one 16-byte load, no per-coordinate conversions, and the two points'
+// x and y coordinates are already the packed pairs the rotation uses
 struct PatternF { float4 t[256]; };
 constexpr PatternF make_pattern_f() {
     PatternF p{};
     for (int i = 0; i < 256; ++i)
-        p.t[i] = float4{(float)kPattern[4 * i], (float)kPattern[4 * i + 1], (float)kPattern[4 * i + 2],
+        p.t[i] = float4{(float)kPattern[4 * i], (float)kPattern[4 * i + 2], (float)kPattern[4 * i + 1],
                         (float)kPattern[4 * i + 3]};
     return p;
 }
@@ -173,10 +174,16 @@ __device__ inline void wave_sync() {
 
 __device__ inline int reflect101(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
 
-// Per-wave LDS: the raw 43x48 neighbourhood and the blurred 37x40 patch.
+#ifndef ORBGPU_DESC_PAIR
+#define ORBGPU_DESC_PAIR 0
+#endif
+constexpr int kKeysPerWave = ORBGPU_DESC_PAIR ? 2 : 1;
+
+// Per-wave LDS: the raw 43x48 neighbourhood (re-staged per keypoint) and one
+// blurred 37x40 patch per keypoint of the wave.
 struct alignas(16) DescLds {
     uint8_t raw[kPatch * kRPitch];
-    uint8_t blur[kBlur * kBPitch];
+    uint8_t blur[kKeysPerWave][kBlur * kBPitch];
 };
 
 // A keypoint slot of a frame: its level, index within the level and output
@@ -215,7 +222,7 @@ __device__ bool key_ref(const Geom& g, int f, int slot, int lane, const uint32_t
 
 // Stage the neighbourhood, IC_Angle's moments, the blurred patch into S.blur;
 // returns (m10, m01), wave-uniform.
-__device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, DescLds& S,
+__device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, DescLds& S, uint8_t* blur_out,
                                const uint8_t* __restrict__ img0, size_t row0, size_t frame0,
                                const uint8_t* __restrict__ pyr) {
     const int l = K.l, cx = K.cx, cy = K.cy;
@@ -317,7 +324,7 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
             R3.a = w[0];
             R3.b = w[1];
             R3.c = w[2];
-            blurdev::row_pass_raw(R3, lo, hi);
+            blurdev::row_pass_raw_shifted(R3, lo, hi);
         };
         auto from_next = [](blurdev::f32x2 v) {  // the value of lane + 1 (DPP wave_shl:1)
             return blurdev::f32x2{
@@ -338,7 +345,7 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
                     blurdev::col_pass(wl[j], wl[j + 1], wl[j + 2], wl[j + 3], wl[j + 4], wl[j + 5], wl[j + 6]);
                 const blurdev::f32x2 hi =
                     blurdev::col_pass(wh[j], wh[j + 1], wh[j + 2], wh[j + 3], wh[j + 4], wh[j + 5], wh[j + 6]);
-                reinterpret_cast<uint32_t*>(S.blur + (r0 + j) * kBPitch)[q] = blurdev::pack4(lo, hi, simd);
+                reinterpret_cast<uint32_t*>(blur_out + (r0 + j) * kBPitch)[q] = blurdev::pack4(lo, hi, simd);
             }
         }
     }
@@ -347,7 +354,7 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
 
 // rBRIEF (computeOrbDescriptor, ORBextractor.cpp:110-149) on the blurred
 // patch with the keypoint's rotation, and the output record.
-__device__ void describe_tests(const Geom& g, int f, const KeyRef& K, int lane, const DescLds& S, float4 rot,
+__device__ void describe_tests(const Geom& g, int f, const KeyRef& K, int lane, const uint8_t* blur, float4 rot,
                                orbgpu_keypoint* __restrict__ kps, uint8_t* __restrict__ desc, int kp_cap) {
     const LevelGeom& L = g.lv[K.l];
     const int ob = K.cx - kBlurR - ((K.cx - kBlurR) & ~3);
@@ -361,17 +368,23 @@ __device__ void describe_tests(const Geom& g, int f, const KeyRef& K, int lane, 
     constexpr float kMagic = 12582912.f;
     constexpr uint32_t kBias = 0x400000u * (uint32_t)kBPitch + 0x4B400000u;
     const uint32_t cb = (uint32_t)(kBlurR * kBPitch + kBlurR + ob) - kBias;  // wave-uniform
+    // both points of a test at once on packed f32 pairs: every product and sum
+    // is one IEEE single operation per component, as the reference's scalar
+    // float code (no contraction: -ffp-contract=off)
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 va = {a, a}, vb = {b, b}, vm = {kMagic, kMagic};
 #pragma unroll
     for (int rnd = 0; rnd < 4; ++rnd) {
         const float4 pt = c_pattern.t[rnd * 64 + lane];
+        const f2 px = {pt.x, pt.y}, py = {pt.z, pt.w};  // (x0, x1), (y0, y1)
+        const f2 fy = px * vb + py * va;                 // x*b + y*a
+        const f2 fx = px * va - py * vb;                 // x*a - y*b
+        const f2 my = fy + vm, mx = fx + vm;
         int val[2];
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) {
-            const float px = pp ? pt.z : pt.x, py = pp ? pt.w : pt.y;
-            const float fy = __fadd_rn(__fmul_rn(px, b), __fmul_rn(py, a));
-            const float fx = __fsub_rn(__fmul_rn(px, a), __fmul_rn(py, b));
-            const uint32_t iy = __float_as_uint(__fadd_rn(fy, kMagic)), ix = __float_as_uint(__fadd_rn(fx, kMagic));
-            val[pp] = S.blur[(int)(__umul24(iy, (uint32_t)kBPitch) + ix + cb)];
+            const uint32_t iy = __float_as_uint(pp ? my.y : my.x), ix = __float_as_uint(pp ? mx.y : mx.x);
+            val[pp] = blur[(int)(__umul24(iy, (uint32_t)kBPitch) + ix + cb)];
         }
         words[rnd] = __ballot(val[0] < val[1]);
     }
@@ -432,28 +445,66 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
 #else
     const int blk = (int)blockIdx.x;
 #endif
-    const int item = blk * kDescWaves + wave;
+    const int item = blk * kDescWaves + wave;  // the wave's keypoint slots: kKeysPerWave consecutive ones
 #ifdef DESC_STAMPS
     const bool stamp_on = (item & 63) == 0;
     unsigned long long ts[8] = {};
 #endif
     DSTAMP(0);
-    const int f = item / g.slots_frame, slot = item - f * g.slots_frame;
-    KeyRef K;
-    const bool valid = item < items && key_ref(g, f, slot, lane, oct_out, oct_count, counts, K);
-    if (!valid) return;
+    const int per_frame = (g.slots_frame + kKeysPerWave - 1) / kKeysPerWave;
+    const int f = item / per_frame, slot0 = (item - f * per_frame) * kKeysPerWave;
+    if (item >= items) return;
+    KeyRef K[kKeysPerWave];
+    bool valid[kKeysPerWave];
+    int nvalid = 0;
+#pragma unroll
+    for (int k = 0; k < kKeysPerWave; ++k) {
+        valid[k] = slot0 + k < g.slots_frame && key_ref(g, f, slot0 + k, lane, oct_out, oct_count, counts, K[k]);
+        nvalid += valid[k];
+    }
+    if (nvalid == 0) return;
     DSTAMP(1);
-    const int2 m = describe_patch(g, f, K, lane, s_lds[wave], img0, row0, frame0, pyr);
+    // Each keypoint in turn: raw neighbourhood -> moments -> its blurred patch
+    // (the raw buffer is re-staged, so a wave sync before the next keypoint's
+    // staging); then ONE orientation chain for all of them (lane k computes
+    // keypoint k's: the same instructions as for one), then the tests.
+    // (a rolled loop: one copy of the staging / blur code, so the register
+    // budget is the one-keypoint kernel's)
+    int mx = 0, my = 0;
+#pragma unroll 1
+    for (int k = 0; k < kKeysPerWave; ++k) {
+        const bool vk = k == 0 ? valid[0] : valid[kKeysPerWave - 1];
+        if (!vk) continue;
+        KeyRef Kk = K[0];
+        if (k != 0) Kk = K[kKeysPerWave - 1];
+        if (k > 0) wave_sync();  // the previous keypoint's blur has read the raw buffer
+        int lane_k = lane;
+        asm volatile("" : "+v"(lane_k));  // per iteration: no lane-derived invariant is hoisted out (VGPRs 82 -> 50)
+        const int2 mm = describe_patch(g, f, Kk, lane_k, s_lds[wave], s_lds[wave].blur[k], img0, row0, frame0, pyr);
+        if (lane == k) {
+            mx = mm.x;
+            my = mm.y;
+        }
+    }
     DSTAMP(2);
-    // the orientation: a serial chain on wave-uniform values, run by the
-    // whole wave (measured: sharing it across the block's waves through LDS
-    // and two barriers made the kernel slower, 0.574 -> 0.593 ms)
-    const float angle = fast_atan2((float)m.y, (float)m.x);
+    // the orientation: fastAtan2 + sincosf on lane k for keypoint k (a serial
+    // chain; measured in round 3: sharing it across a block's waves through LDS
+    // and barriers was slower, 0.574 -> 0.593 ms -- within a wave it is free)
+    const float ang = fast_atan2((float)my, (float)mx);
     float sa, ca;
-    glibc_sincosf(__fmul_rn(angle, (float)(M_PI / 180.f)), &sa, &ca);
-    wave_sync();  // blurred patch complete
+    glibc_sincosf(__fmul_rn(ang, (float)(M_PI / 180.f)), &sa, &ca);
+    wave_sync();  // blurred patches complete
     DSTAMP(3);
-    describe_tests(g, f, K, lane, s_lds[wave], float4{angle, ca, sa, 0.f}, kps, desc, kp_cap);
+#pragma unroll 1
+    for (int k = 0; k < kKeysPerWave; ++k) {
+        if (!(k == 0 ? valid[0] : valid[kKeysPerWave - 1])) continue;
+        KeyRef Kk = K[0];
+        if (k != 0) Kk = K[kKeysPerWave - 1];
+        const float a_k = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ang), k));
+        const float c_k = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), k));
+        const float s_k = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), k));
+        describe_tests(g, f, Kk, lane, s_lds[wave].blur[k], float4{a_k, c_k, s_k, 0.f}, kps, desc, kp_cap);
+    }
 #ifdef DESC_STAMPS
     DSTAMP(4);
     if (stamp_on && lane == 0) {
@@ -480,7 +531,7 @@ hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t
                            const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
                            hipStream_t stream, int* err_word, int* err_copy) {
-    const int items = g.slots_frame * batch;
+    const int items = (g.slots_frame + kKeysPerWave - 1) / kKeysPerWave * batch;  // waves
     if (row0 >= (1u << 24)) return hipErrorInvalidValue;  // row offsets by 24-bit multiplies
     const int blocks = (items + kDescWaves - 1) / kDescWaves;
     hipLaunchKernelGGL(describe_kernel, dim3(blocks), dim3(64 * kDescWaves), 0, stream, g, items, img0, row0, frame0,

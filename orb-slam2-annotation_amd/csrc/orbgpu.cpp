@@ -673,8 +673,16 @@ int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int hei
     // the drop-in (Frame constructor) path: host image -> pinned staging ->
     // one async H2D; extraction; the error word folded into the output
     // block; one async D2H of the whole block; one synchronisation
-    for (int y = 0; y < height; ++y) std::memcpy(e->h_img + (size_t)y * e->img_pitch, image + (size_t)y * step, width);
-    ORB_HIP(hipMemcpyAsync(e->d_img, e->h_img, e->img_pitch * height, hipMemcpyHostToDevice, s));
+    // (in four row bands: the DMA of band i overlaps the host copy of band i+1)
+    constexpr int kBands = 4;
+    for (int b = 0; b < kBands; ++b) {
+        const int y0 = height * b / kBands, y1 = height * (b + 1) / kBands;
+        if (y1 <= y0) continue;
+        for (int y = y0; y < y1; ++y)
+            std::memcpy(e->h_img + (size_t)y * e->img_pitch, image + (size_t)y * step, width);
+        ORB_HIP(hipMemcpyAsync(e->d_img + (size_t)y0 * e->img_pitch, e->h_img + (size_t)y0 * e->img_pitch,
+                               e->img_pitch * (size_t)(y1 - y0), hipMemcpyHostToDevice, s));
+    }
     // describe moves the error word into the output block and clears it
     int rc = run_batch(e, e->d_img, 1, e->img_pitch, e->img_pitch * height, e->d_kps1, e->d_desc1, e->d_count1,
                        e->max_kps, s, reinterpret_cast<int*>(e->d_single + 4));

@@ -175,11 +175,21 @@ int plan_pyramid(Geom& g, const std::vector<int2>& ytab, const std::vector<int4>
     g.tk_nc0 = NC;
     g.tk_cstride0 = 16 * 64 * g.tk_pwaves * g.tk_np;  // >= T0 rows at the level-0 pitch
 
-    // --- LDS layout: 16 B pad | ring 0 | ring 1 | ... | ring L-2 | 16 B pad | sink | plan table
+    // --- LDS layout: 16 B pad | ring 0 | ring 1 | ... | ring L-2 | 16 B pad | sink | plan table.
+    // Ring rows of levels >= 1 get an odd number of 16-byte units per row
+    // (ORBGPU_PYR_STAGGER): consecutive rows then start 4, 12, 20 or 28
+    // banks apart instead of on the same bank, so lanes of one instruction
+    // that read different rows of a ring at nearby columns (different row
+    // groups / levels in one wave) do not pile onto the same banks.  Level 0
+    // keeps 16 * v4: its LDS-DMA pieces land contiguously.
+#ifndef ORBGPU_PYR_STAGGER
+#define ORBGPU_PYR_STAGGER 1
+#endif
     int off = 16;
     for (int l = 0; l + 1 < L; ++l) {
         LevelGeom& v = g.lv[l];
         v.tk_pitch = round_up(v.w, 16);
+        if (ORBGPU_PYR_STAGGER && l > 0 && (v.tk_pitch / 16) % 2 == 0) v.tk_pitch += 16;
         v.tk_ring = off;
         v.tk_ring_rows = C[l];
         off += l == 0 ? NC * g.tk_cstride0 : C[l] * v.tk_pitch;

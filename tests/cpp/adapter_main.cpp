@@ -85,10 +85,12 @@ void log_times(const char* op, std::vector<double> us, const char* note = "") {
     if (!path || us.empty()) return;
     std::sort(us.begin(), us.end());
     const double med = us[us.size() / 2], p90 = us[std::min(us.size() - 1, us.size() * 9 / 10)];
+    const double p99 = us[std::min(us.size() - 1, us.size() * 99 / 100)];
     FILE* f = std::fopen(path, "a");
     if (!f) return;
-    std::fprintf(f, "{\"op\": \"%s\", \"median_us\": %.2f, \"p90_us\": %.2f, \"min_us\": %.2f, \"reps\": %zu, "
-                    "\"note\": \"%s\"}\n", op, med, p90, us.front(), us.size(), note);
+    std::fprintf(f, "{\"op\": \"%s\", \"median_us\": %.2f, \"p90_us\": %.2f, \"p99_us\": %.2f, \"min_us\": %.2f, "
+                    "\"max_us\": %.2f, \"reps\": %zu, \"note\": \"%s\"}\n",
+                 op, med, p90, p99, us.front(), us.back(), us.size(), note);
     std::fclose(f);
 }
 
@@ -97,6 +99,12 @@ template <class Setup, class Body>
 void timed(const char* op, Setup setup, Body body, const char* note = "") {
     const int n = reps();
     if (n <= 1 || !std::getenv("ADAPTER_TIME_LOG")) return;
+    // untimed warm-up repetitions first: first-use growth (staging arenas,
+    // pinned mirrors, code-object loads) stays out of the distribution
+    for (int r = 0; r < std::max(3, n / 10); ++r) {
+        setup();
+        body();
+    }
     std::vector<double> us;
     for (int r = 0; r < n; ++r) {
         setup();

@@ -1,0 +1,25 @@
+# A/B of the product library against variants (liborbgpu_<name>.so): extraction
+# parity of each, then alternated bench lines (no extras / CPU legs), then the
+# LDS / instruction PMC pass of each.  usage: bash tools/gpu_r4_ab.sh <tag> <variant>...
+set -e
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+tag=$1; shift
+L=$GRAFT_REPO_ROOT/orb-slam2-annotation_amd
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py > gpurun_out/${tag}_par_base.log 2>&1
+for v in "$@"; do
+  ORBGPU_LIBRARY=$L/liborbgpu_$v.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py > gpurun_out/${tag}_par_$v.log 2>&1
+done
+for rep in 1 2; do
+  timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-extras --deliver gpu0 > gpurun_out/${tag}_base_$rep.log 2>&1
+  for v in "$@"; do
+    ORBGPU_LIBRARY=$L/liborbgpu_$v.so timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-extras --deliver gpu0 > gpurun_out/${tag}_${v}_$rep.log 2>&1
+  done
+done
+B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extras --deliver gpu0"
+timeout -k 10 120 rocprofv3 --pmc SQ_BUSY_CU_CYCLES SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAVES --output-format csv -d gpurun_out/${tag}_pmc_base -o q -- $B > gpurun_out/${tag}_pmc_base.log 2>&1
+for v in "$@"; do
+  ORBGPU_LIBRARY=$L/liborbgpu_$v.so timeout -k 10 120 rocprofv3 --pmc SQ_BUSY_CU_CYCLES SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAVES --output-format csv -d gpurun_out/${tag}_pmc_$v -o q -- $B > gpurun_out/${tag}_pmc_$v.log 2>&1
+done
+echo ABDONE

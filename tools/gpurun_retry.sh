@@ -5,12 +5,14 @@
 # that ran, whatever its result, is never repeated.
 # usage: tools/gpurun_retry.sh <timeout> '<command>'
 t=$1; shift
-for i in 1 2 3 4; do
-  /usr/local/graft/bin/gpurun --timeout "$t" -- "$@"
-  rc=$?
+for i in 1 2 3 4 5 6; do
+  /usr/local/graft/bin/gpurun --timeout "$t" -- "$@" 2>&1 | tee /tmp/gpurun_retry_last.log
+  rc=${PIPESTATUS[0]}
   st=$(python3 -c "import json;print(json.load(open('gpurun_out/.last_call.json')).get('status',''))" 2>/dev/null)
   if [ "$st" != "transient" ] && [ $rc -ne 3 ]; then exit $rc; fi
-  echo "[gpurun_retry] transient (attempt $i), retrying in 60 s"
-  sleep 60
+  # honour the client's back-off ("retry in Ns") when it gives one
+  wait=$(python3 -c "import re;m=re.findall(r'retry in (\d+)s',open('/tmp/gpurun_retry_last.log').read());print(int(m[-1])+15 if m else 240)" 2>/dev/null || echo 240)
+  echo "[gpurun_retry] transient (attempt $i), retrying in $wait s"
+  sleep $wait
 done
 exit $rc
