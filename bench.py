@@ -128,7 +128,7 @@ def parse(argv=None):
     ap.add_argument("--no-extras", action="store_true", help="headline only (no extra legs)")
     ap.add_argument("--match-after", default="fast_cells", choices=["pyramid", "fast_cells", "octree"],
                     help="extraction stage of step k after which step k-1's match starts")
-    ap.add_argument("--deliver", default="host", choices=["host", "gpu0"],
+    ap.add_argument("--deliver", default="gpu0", choices=["host", "gpu0"],
                     help="where each step's outputs go (shard.Delivery): host = every rank copies its trimmed "
                          "outputs over its own PCIe link to pinned host memory (the Tracking thread's side); "
                          "gpu0 = counts then used rows sent to rank 0's HBM")

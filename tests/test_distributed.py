@@ -156,3 +156,63 @@ def test_sharded_stream_equals_single_process():
         cross += f > 0 and f % B == 0 and nm > 0  # pairs that straddle two chunks
         prev = (k, d, n)
     assert cross >= 2
+
+
+def test_pack_rows_torch_path_matches_unpack():
+    """shard.pack_rows (the torch packing used where the engine has no HIP
+    packer: the CPU dry run) puts frame b's first counts[b] rows at the
+    exclusive prefix sum of the counts; shard.unpack_rows inverts it.  Ragged
+    counts, empty and full frames, rows of keypoint (7 f32), descriptor
+    (32 u8) and match (i32) shape."""
+    import shard
+    rng = np.random.default_rng(11)
+    B, cap = 9, 17
+    counts = rng.integers(0, cap + 1, B).astype(np.int32)
+    counts[[1, 4]] = 0
+    counts[7] = cap
+    for shape, dt in (((7,), torch.float32), ((32,), torch.uint8), ((), torch.int32)):
+        rows = torch.from_numpy(rng.integers(0, 200, (B, cap, *shape)).astype(np.float32)).to(dt)
+        out = torch.zeros((B * cap + 1, *shape), dtype=dt)
+        shard.pack_rows(rows, torch.from_numpy(counts), out)
+        n = int(counts.sum())
+        back = shard.unpack_rows(out[:n].numpy(), counts, cap)
+        ref = rows.numpy().copy()
+        for b in range(B):
+            ref[b, counts[b]:] = 0
+        assert np.array_equal(back, ref)
+        assert np.array_equal(shard.pack_offsets(torch.from_numpy(counts)).numpy(),
+                              np.concatenate([[0], np.cumsum(counts)[:-1]]))
+
+
+def test_delivery_host_mode_single_process_round_trip():
+    """shard.Delivery in host mode on the CPU (world 1): the ring of slots,
+    back-pressure and the delivered rows / counts of every step."""
+    import shard
+    rng = np.random.default_rng(12)
+    B, cap, steps = 4, 10, 7
+    tmpl = [torch.zeros((B, cap, 7)), torch.zeros((B, cap, 32), dtype=torch.uint8),
+            torch.zeros((B, cap), dtype=torch.int32)]
+    d = shard.Delivery("host", 0, 1, torch.device("cpu"),
+                       [shard.RowSpec("kps", 0), shard.RowSpec("desc", 0), shard.RowSpec("m12", 1)],
+                       B, cap, tmpl, 3 * B, sets=3)
+    for s in range(steps):
+        c = torch.from_numpy(rng.integers(0, cap + 1, B).astype(np.int32))
+        cp = torch.from_numpy(rng.integers(0, cap + 1, B).astype(np.int32))
+        nm = torch.from_numpy(rng.integers(0, 5, B).astype(np.int32))
+        k = torch.randn(B, cap, 7)
+        de = torch.from_numpy(rng.integers(0, 255, (B, cap, 32)).astype(np.uint8))
+        m = torch.from_numpy(rng.integers(-1, 50, (B, cap)).astype(np.int32))
+        si = d.start([k, de, m], [c, cp, nm], [c, cp])
+        d.finish(si)
+        rows, small = d.host_rows(si)
+        assert np.array_equal(small.numpy(), np.concatenate([c.numpy(), cp.numpy(), nm.numpy()]))
+        for (h, n), t, cnt in zip(rows, (k, de, m), (c, c, cp)):
+            assert n == int(cnt.sum())
+            back = shard.unpack_rows(h[:n].numpy(), cnt.numpy(), cap)
+            ref = t.numpy().copy()
+            for b in range(B):
+                ref[b, int(cnt[b]):] = 0
+            assert np.array_equal(back, ref)
+    rep = d.report(steps)
+    assert rep["mode"] == "host" and rep["bytes_per_step"] > 0
+    d.close()
