@@ -54,13 +54,15 @@ __device__ __forceinline__ uint32_t to_u8(float v) {
 
 // 8-bit packing of 4 filtered columns; v_cvt_pk_u8_f32 rounds to nearest
 // even and saturates (the vector path), to_u8 rounds half up (the tail).
+__device__ __forceinline__ uint32_t pack4_simd(f32x2 lo, f32x2 hi) {
+    uint32_t packed = __builtin_amdgcn_cvt_pk_u8_f32(lo.x, 0, 0u);
+    packed = __builtin_amdgcn_cvt_pk_u8_f32(lo.y, 1, packed);
+    packed = __builtin_amdgcn_cvt_pk_u8_f32(hi.x, 2, packed);
+    return __builtin_amdgcn_cvt_pk_u8_f32(hi.y, 3, packed);
+}
+
 __device__ __forceinline__ uint32_t pack4(f32x2 lo, f32x2 hi, bool simd) {
-    if (simd) {
-        uint32_t packed = __builtin_amdgcn_cvt_pk_u8_f32(lo.x, 0, 0u);
-        packed = __builtin_amdgcn_cvt_pk_u8_f32(lo.y, 1, packed);
-        packed = __builtin_amdgcn_cvt_pk_u8_f32(hi.x, 2, packed);
-        return __builtin_amdgcn_cvt_pk_u8_f32(hi.y, 3, packed);
-    }
+    if (simd) return pack4_simd(lo, hi);
     return to_u8(lo.x) | (to_u8(lo.y) << 8) | (to_u8(hi.x) << 16) | (to_u8(hi.y) << 24);
 }
 

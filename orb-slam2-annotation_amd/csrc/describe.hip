@@ -20,6 +20,7 @@
 #include "../../include/orbgpu.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace orbgpu {
 
@@ -45,7 +46,15 @@ __constant__ PatternF c_pattern = make_pattern_f();
 // reference's way)
 constexpr int kUmax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 
-constexpr int kRPitchC = 48;  // = kRPitch (raw patch row pitch), needed by the table below
+// raw patch row pitch (bytes; the staged rows are 48 columns wide).  A/B:
+// 52 spreads the row pass's six row chunks over distinct LDS banks (48: the
+// chunk stride 84 dwords = 20 mod 32 banks, 2-way conflicts)
+#ifndef ORBGPU_DESC_RPITCH
+#define ORBGPU_DESC_RPITCH 48
+#endif
+constexpr int kRPitchC = ORBGPU_DESC_RPITCH;  // = kRPitch, needed by the table below
+constexpr int kRWidth = 48;                   // staged columns per row: xb-4 .. xb+43
+static_assert(kRPitchC % 4 == 0 && kRPitchC >= kRWidth, "raw pitch");
 constexpr int kDiscWords = 31 * 9, kDiscLoads = (kDiscWords + 63) / 64;
 // IC_Angle's disc as staged-patch words.  Disc row v = r - 15 (r < 31)
 // covers the 4-aligned window columns c = 4q .. 4q+3 (q < 9) starting at
@@ -160,7 +169,7 @@ __device__ inline uint32_t wave_total(uint32_t v) {
 
 constexpr int kBPitch = 40;      // 37-px blurred rows, from a 4-aligned column
 constexpr int kRPitch = kRPitchC;  // raw patch rows: columns xb-4 .. xb+43 (12 dwords)
-constexpr int kRawWords = kPatch * (kRPitch / 4);   // 43 rows x 12 dwords
+constexpr int kRawWords = kPatch * (kRWidth / 4);   // 43 rows x 12 dwords
 constexpr int kQuads = kBPitch / 4;                 // 10 output quads per blurred row
 constexpr int kColChunks = (kBlur + 6) / 7;         // 6 chunks of <= 7 blurred rows
 
@@ -174,10 +183,13 @@ __device__ inline void wave_sync() {
 
 __device__ inline int reflect101(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
 
-#ifndef ORBGPU_DESC_PAIR
-#define ORBGPU_DESC_PAIR 0
+// keypoints per wave (1, 2 or 4): the wave stages and blurs them one after
+// the other, then runs ONE orientation chain for all (lane k: keypoint k)
+#ifndef ORBGPU_DESC_KEYS
+#define ORBGPU_DESC_KEYS 1
 #endif
-constexpr int kKeysPerWave = ORBGPU_DESC_PAIR ? 2 : 1;
+constexpr int kKeysPerWave = ORBGPU_DESC_KEYS;
+static_assert(kKeysPerWave == 1 || kKeysPerWave == 2 || kKeysPerWave == 4, "ORBGPU_DESC_KEYS: 1, 2 or 4");
 
 // Per-wave LDS: the raw 43x48 neighbourhood (re-staged per keypoint) and one
 // blurred 37x40 patch per keypoint of the wave.
@@ -239,8 +251,8 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
     const int xb = (cx - kBlurR) & ~3, x0 = xb - 4;
     // a neighbourhood entirely inside the level (wave-uniform; most keypoints): three
     // 16-byte chunks per row, two loads per lane, no reflection
-    if (x0 >= 0 && x0 + kRPitch <= L.w && cy - kPatchR >= 0 && cy + kPatchR < L.h) {
-        constexpr int kChunks = kPatch * (kRPitch / 16);  // 129
+    if (x0 >= 0 && x0 + kRWidth <= L.w && cy - kPatchR >= 0 && cy + kPatchR < L.h) {
+        constexpr int kChunks = kPatch * (kRWidth / 16);  // 129
         const uint8_t* top = raw + (size_t)(cy - kPatchR) * rp + x0;
         uint4 c[3];
         // r = idx / 3 by a 24-bit multiply (exact for idx < 4096), row offsets
@@ -254,7 +266,17 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const int idx = lane + 64 * k, r = idx / 3, q = idx - 3 * r;
-            if (idx < kChunks) *reinterpret_cast<uint4*>(S.raw + r * kRPitch + 16 * q) = c[k];
+            if (idx < kChunks) {
+                if constexpr (kRPitch % 16 == 0) {
+                    *reinterpret_cast<uint4*>(S.raw + r * kRPitch + 16 * q) = c[k];
+                } else {
+                    uint32_t* d = reinterpret_cast<uint32_t*>(S.raw + r * kRPitch + 16 * q);
+                    d[0] = c[k].x;
+                    d[1] = c[k].y;
+                    d[2] = c[k].z;
+                    d[3] = c[k].w;
+                }
+            }
         }
     } else {
     constexpr int kLoads = (kRawWords + 63) / 64;
@@ -274,8 +296,8 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
     }
 #pragma unroll
     for (int k = 0; k < kLoads; ++k) {
-        const int idx = lane + 64 * k;
-        if (idx < kRawWords) reinterpret_cast<uint32_t*>(S.raw)[idx] = v[k];
+        const int idx = lane + 64 * k, r = idx / 12, q = idx - r * 12;
+        if (idx < kRawWords) reinterpret_cast<uint32_t*>(S.raw)[r * (kRPitch / 4) + q] = v[k];
     }
     }
     wave_sync();
@@ -314,7 +336,11 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
     // rows instead of 13.  Chunk 5 (rows 35..42) needs no halo: it outputs
     // rows 35 and 36 only.  All 64 lanes run the passes (lanes 60..63 repeat
     // quad 9 and store nothing), so every DPP source lane is active.
-    {
+    // A patch whose every quad is on the SIMD path (xb + 36 < simd_end: all
+    // but the keypoints at a level's right edge) takes a copy of the passes
+    // that packs with v_cvt_pk_u8_f32 alone: with a per-lane path choice the
+    // compiler evaluates both roundings and selects (16 VALU per output row).
+    auto passes = [&](auto all_simd) {
         const int qq = lane / kColChunks, c = lane - qq * kColChunks;
         const int q = min(qq, kQuads - 1), r0 = c * 7;
         const bool simd = xb + 4 * q < simd_end, store = qq < kQuads;
@@ -345,10 +371,15 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
                     blurdev::col_pass(wl[j], wl[j + 1], wl[j + 2], wl[j + 3], wl[j + 4], wl[j + 5], wl[j + 6]);
                 const blurdev::f32x2 hi =
                     blurdev::col_pass(wh[j], wh[j + 1], wh[j + 2], wh[j + 3], wh[j + 4], wh[j + 5], wh[j + 6]);
-                reinterpret_cast<uint32_t*>(blur_out + (r0 + j) * kBPitch)[q] = blurdev::pack4(lo, hi, simd);
+                reinterpret_cast<uint32_t*>(blur_out + (r0 + j) * kBPitch)[q] =
+                    all_simd ? blurdev::pack4_simd(lo, hi) : blurdev::pack4(lo, hi, simd);
             }
         }
-    }
+    };
+    if (xb + 4 * (kQuads - 1) < simd_end)
+        passes(std::true_type{});
+    else
+        passes(std::false_type{});
     return int2{m10, m01};
 }
 
@@ -470,18 +501,36 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
     // keypoint k's: the same instructions as for one), then the tests.
     // (a rolled loop: one copy of the staging / blur code, so the register
     // budget is the one-keypoint kernel's)
+    // keypoint k of the wave in a rolled loop (k wave-uniform: the selects
+    // below are scalar)
+    auto key_at = [&](int k, KeyRef& Kk) {
+        int l = K[0].l, i = K[0].i, before = K[0].before, cx = K[0].cx, cy = K[0].cy;
+        uint32_t key = K[0].key;
+        bool v = valid[0];
+#pragma unroll
+        for (int j = 1; j < kKeysPerWave; ++j) {
+            const bool h = k == j;
+            l = h ? K[j].l : l;
+            i = h ? K[j].i : i;
+            before = h ? K[j].before : before;
+            cx = h ? K[j].cx : cx;
+            cy = h ? K[j].cy : cy;
+            key = h ? K[j].key : key;
+            v = h ? valid[j] : v;
+        }
+        Kk = KeyRef{l, i, before, cx, cy, key};
+        return v;
+    };
     int mx = 0, my = 0;
 #pragma unroll 1
     for (int k = 0; k < kKeysPerWave; ++k) {
-        const bool vk = k == 0 ? valid[0] : valid[kKeysPerWave - 1];
-        if (!vk) continue;
-        KeyRef Kk = K[0];
-        if (k != 0) Kk = K[kKeysPerWave - 1];
+        KeyRef Kk;
+        if (!key_at(k, Kk)) continue;
         if (k > 0) wave_sync();  // the previous keypoint's blur has read the raw buffer
         int lane_k = lane;
         asm volatile("" : "+v"(lane_k));  // per iteration: no lane-derived invariant is hoisted out (VGPRs 82 -> 50)
         const int2 mm = describe_patch(g, f, Kk, lane_k, s_lds[wave], s_lds[wave].blur[k], img0, row0, frame0, pyr);
-        if (lane == k) {
+        if (kKeysPerWave == 1 || lane == k) {  // one keypoint: wave-uniform moments, uniform branches below
             mx = mm.x;
             my = mm.y;
         }
@@ -497,9 +546,8 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
     DSTAMP(3);
 #pragma unroll 1
     for (int k = 0; k < kKeysPerWave; ++k) {
-        if (!(k == 0 ? valid[0] : valid[kKeysPerWave - 1])) continue;
-        KeyRef Kk = K[0];
-        if (k != 0) Kk = K[kKeysPerWave - 1];
+        KeyRef Kk;
+        if (!key_at(k, Kk)) continue;
         const float a_k = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ang), k));
         const float c_k = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ca), k));
         const float s_k = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sa), k));

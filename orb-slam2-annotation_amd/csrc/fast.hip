@@ -57,12 +57,7 @@ struct CellTiles {
     uint16_t* lb;        // tile offsets of corners (row-major order); the same buffer as la: the
                          // corner list is compacted in place behind the survivors being read
     int dump;            // list index past the longest list: the compass's non-survivor lanes store there
-    int* counter;        // the wave's LDS append counter (ORBGPU_FAST_APPEND)
 };
-
-#ifndef ORBGPU_FAST_APPEND
-#define ORBGPU_FAST_APPEND 0
-#endif
 
 // Compass pre-test, row-major over the detection region: LPR = 32 lanes
 // per row when it fits (two rows per pass), else 64 (dw <= 64: host check).
@@ -107,24 +102,6 @@ __device__ int compass_pass(const CellTiles& T, int dw, int dh, int ox, int t, i
     // only the rsub = 0 half on the last row).  Every lane stores: a survivor
     // at its compacted position, the others into the dump slot past the list.
     const int rsub = LPR == 32 ? lane >> 5 : 0, col = lane & (LPR - 1);
-#if ORBGPU_FAST_APPEND
-    // ds_append compaction: the lanes that pass take consecutive list slots
-    // from the wave's LDS counter in lane order (DS_APPEND returns the counter
-    // plus the number of active lanes below), one instruction per mask
-    typedef __attribute__((address_space(3))) int lds_int;
-    lds_int* counter = (lds_int*)(uintptr_t)(uint32_t)(uintptr_t)T.counter;
-    const bool col_ok = col < dw;
-    int o = (3 + rsub) * P + 3 + ox + col;
-    for (int rr = 0; rr < dh; rr += 2 * kStep, o += 2 * kStep * P) {
-        const uint32_t y = compass2(T.win + o);
-        const int r0 = rr + rsub;  // rows of the lane's two pixels
-        if (col_ok && (y & 0xFFFFu) != 0u && r0 < dh) T.la[__builtin_amdgcn_ds_append(counter)] = (uint16_t)o;
-        if (col_ok && y >= 0x10000u && r0 + kStep < dh)
-            T.la[__builtin_amdgcn_ds_append(counter)] = (uint16_t)(o + kStep * P);
-    }
-    wave_sync();
-    return *T.counter;
-#else
     const unsigned long long colmask = __builtin_amdgcn_uicmp((uint32_t)col, (uint32_t)dw, 36 /* ult */);
     constexpr unsigned long long sub0 = LPR == 32 ? 0xFFFFFFFFull : ~0ull;  // lanes of row rsub = 0
     int o = (3 + rsub) * P + 3 + ox + col;  // tile offset of the lane's first pixel
@@ -142,7 +119,6 @@ __device__ int compass_pass(const CellTiles& T, int dw, int dh, int ox, int t, i
         na += __popcll(m1);
     }
     return na;
-#endif
 }
 
 // FAST at threshold t on the cell's detection region: returns the number
@@ -153,10 +129,6 @@ __device__ int compass_pass(const CellTiles& T, int dw, int dh, int ox, int t, i
 template <int P>
 __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, int lane,
                             unsigned long long* stamp = nullptr) {
-#if ORBGPU_FAST_APPEND
-    if (lane == 0) *T.counter = 0;
-    wave_sync();
-#endif
     const int na = dw > 32 ? compass_pass<P, 64>(T, dw, dh, ox, t, lane) : compass_pass<P, 32>(T, dw, dh, ox, t, lane);
     wave_sync();
 #ifdef FAST_STAMPS
@@ -303,7 +275,7 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     const int R = g.win_rows;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: metadata in SGPRs
-    const size_t per_wave = (((size_t)2 * P * R + 2 * ((size_t)g.det_max + 1) + 15) & ~(size_t)15) + 16;
+    const size_t per_wave = (((size_t)2 * P * R + 2 * ((size_t)g.det_max + 1) + 15) & ~(size_t)15);
     uint8_t* ws = smem + wave * per_wave;
     CellTiles T;
     T.win = ws;
@@ -311,7 +283,6 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     T.la = reinterpret_cast<uint16_t*>(ws + 2 * P * R);
     T.lb = T.la;
     T.dump = g.det_max;  // in-place: iteration `base` writes below base + 64 after reading la[base .. base + 64)
-    T.counter = reinterpret_cast<int*>(ws + per_wave - 16);
     uint8_t* s_win = ws;
 
     // one cell per wave; waves of a block take consecutive cells of a frame;
@@ -467,7 +438,7 @@ hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size
     const int items = g.total_cells * batch;
     if (row0 >= (1u << 24)) return hipErrorInvalidValue;  // row offsets by 24-bit multiplies
     const size_t per_wave =
-        (((size_t)2 * g.win_pitch * g.win_rows + 2 * ((size_t)g.det_max + 1) + 15) & ~(size_t)15) + 16;
+        (((size_t)2 * g.win_pitch * g.win_rows + 2 * ((size_t)g.det_max + 1) + 15) & ~(size_t)15);
     dim3 grid((items + kCellWaves - 1) / kCellWaves);
     const size_t lds = per_wave * kCellWaves;
 #define ORBGPU_FAST_CASE(PP)                                                                                        \

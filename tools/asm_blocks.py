@@ -1,32 +1,60 @@
-"""Per-basic-block instruction counts of one kernel in a .s file
-(usage: asm_blocks.py file.s kernel_substring)."""
+#!/usr/bin/env python3
+"""Per-basic-block instruction counts of one kernel in a device .s file
+(hipcc -S --cuda-device-only): VALU / SALU / LDS / VMEM / SMEM per block and
+the block's most frequent VALU opcodes -- to attribute a kernel's
+SQ_INSTS_VALU per launch to its phases.
+
+usage: asm_blocks.py FILE.s KERNEL_SUBSTRING [--top N]
+"""
+import collections
+import re
 import sys
 
-lines = open(sys.argv[1]).read().splitlines()
-key = sys.argv[2]
-start = next(i for i, l in enumerate(lines) if key in l and l.endswith(":") or (key in l and ": ;" in l))
-end = next(i for i in range(start, len(lines)) if lines[i].startswith(".Lfunc_end"))
-blocks = [{"name": "entry", "v": 0, "s": 0, "ds": 0, "vm": 0, "line": start + 1, "loop": ""}]
-for i in range(start + 1, end):
-    l = lines[i]
-    t = l.strip()
-    if l.startswith(".LBB") or t.startswith("; %bb."):
-        blocks.append({"name": l.split()[0] if l.startswith(".LBB") else t.split()[1], "v": 0, "s": 0, "ds": 0,
-                       "vm": 0, "line": i + 1, "loop": "LOOP" if "Loop" in l else ""})
-        continue
-    b = blocks[-1]
-    if t.startswith("v_"):
-        b["v"] += 1
-    elif t.startswith("s_"):
-        b["s"] += 1
-    elif t.startswith("ds_"):
-        b["ds"] += 1
-    elif t.startswith(("global_", "buffer_", "flat_")):
-        b["vm"] += 1
-tot = {"v": 0, "s": 0, "ds": 0}
-for b in blocks:
-    for k in tot:
-        tot[k] += b[k]
-    if b["v"] + b["ds"] + b["vm"] >= int(sys.argv[3] if len(sys.argv) > 3 else 6):
-        print(f'{b["name"]:12s} line {b["line"]:5d} valu {b["v"]:4d} salu {b["s"]:3d} ds {b["ds"]:3d} vmem {b["vm"]:3d} {b["loop"]}')
-print("total", tot)
+
+def main():
+    path, name = sys.argv[1], sys.argv[2]
+    top = int(sys.argv[sys.argv.index("--top") + 1]) if "--top" in sys.argv else 6
+    s = open(path).read()
+    m = re.search(r"^(\S*%s\S*):" % re.escape(name), s, re.M)
+    if not m:
+        sys.exit("kernel not found")
+    end = s.index(".Lfunc_end", m.end())
+    blocks, cur = [], ["entry", []]
+    for raw in s[m.end():end].splitlines():
+        l = raw.split(";")[0].strip()
+        if not l or l.startswith("."):
+            if re.match(r"^\.LBB\S*:", raw.strip()):
+                blocks.append(cur)
+                cur = [raw.strip().rstrip(":"), []]
+            continue
+        cur[1].append(l)
+        if l.startswith(("s_cbranch", "s_branch")):  # fall-through: a block of its own
+            blocks.append(cur)
+            cur = [cur[0].split("+")[0] + "+", []]
+    blocks.append(cur)
+    tot = collections.Counter()
+    for lab, ins in blocks:
+        c = collections.Counter()
+        ops = collections.Counter()
+        for l in ins:
+            op = l.split()[0]
+            if op.startswith("v_"):
+                c["valu"] += 1
+                ops[op] += 1
+            elif op.startswith("s_"):
+                k = "smem" if op.startswith(("s_load", "s_buffer_load")) else "salu"
+                c[k] += 1
+            elif op.startswith("ds_"):
+                c["lds"] += 1
+            elif op.startswith(("global_", "buffer_", "flat_")):
+                c["vmem"] += 1
+        tot.update(c)
+        tail = ins[-1].split()[0] if ins else ""
+        print("%-14s valu %4d salu %4d lds %3d vmem %3d smem %3d  end %-22s %s" % (
+            lab, c["valu"], c["salu"], c["lds"], c["vmem"], c["smem"], tail,
+            " ".join("%s:%d" % kv for kv in ops.most_common(top))))
+    print("total", dict(tot))
+
+
+if __name__ == "__main__":
+    main()

@@ -23,3 +23,7 @@ for v in "$@"; do
   ORBGPU_LIBRARY=$L/liborbgpu_$v.so timeout -k 10 120 rocprofv3 --pmc SQ_BUSY_CU_CYCLES SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAVES --output-format csv -d gpurun_out/${tag}_pmc_$v -o q -- $B > gpurun_out/${tag}_pmc_$v.log 2>&1
 done
 echo ABDONE
+if [ -f tools/split_probe.py ]; then
+  timeout -k 10 300 python3 -u tools/split_probe.py > gpurun_out/${tag}_split.log 2>&1 || echo "split probe rc $?"
+fi
+echo SPLITDONE

@@ -1,37 +1,76 @@
-"""Probe: one 512-frame extraction vs the same frames as 2 x 256 (or 4 x 128)
-sub-batches on separate streams (kernel tails and the octree's short level
-workgroups filled by the other sub-batch).  Prints ms per 512 frames."""
-import sys, time
-sys.path.insert(0, "orb-slam2-annotation_amd")
-import torch
-import orbgpu, synth
+#!/usr/bin/env python3
+"""Probe: does splitting a step's batch into parts on their own streams, each
+part started once the previous part has passed a stage, beat one batch on
+one stream?  The extraction stages have different limits (pyramid: HBM;
+FAST and describe: VALU issue; octree: latency), so parts offset by a stage
+overlap unlike kernels.  Extraction only (no match), frames resident in HBM.
 
-W, H, NF, B = 640, 480, 1000, 512
-dev = torch.device("cuda:0")
-pitch = (W + 15) // 16 * 16
-frames = synth.torch_stream(B, W, H, device=dev, pitch=pitch, bounded=True)
-for nsplit in (1, 2, 4, 1, 2):
-    sb = B // nsplit
-    exs = [orbgpu.Extractor(nfeatures=NF, width=W, height=H, max_batch=sb) for _ in range(nsplit)]
-    cap = exs[0].max_keypoints
-    sts = [torch.cuda.Stream(dev, priority=-1) for _ in range(nsplit)]
-    outs = [(torch.zeros((sb, cap, 7), dtype=torch.float32, device=dev),
-             torch.zeros((sb, cap, 32), dtype=torch.uint8, device=dev),
-             torch.zeros(sb, dtype=torch.int32, device=dev)) for _ in range(nsplit)]
+usage: split_probe.py [--batch 512] [--steps 20] [--warmup 3]
+prints one JSON line per configuration.
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
 
-    def run():
-        for i in range(nsplit):
-            exs[i].extract_batch(frames[i * sb:(i + 1) * sb], *outs[i], stream=sts[i], row_step=pitch,
-                                 frame_step=pitch * H)
-    for _ in range(3):
-        run()
-    torch.cuda.synchronize()
-    n = 30
-    t0 = time.perf_counter()
-    for _ in range(n):
-        run()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / n * 1e3
-    for i in range(nsplit):
-        exs[i].sync(sts[i])
-    print(f"split {nsplit}: {dt:.3f} ms per {B} frames, {B / dt * 1e3:.0f} frames/s, kp {outs[0][2].float().mean().item():.1f}", flush=True)
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "orb-slam2-annotation_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    import orbgpu as og
+    import synth
+    W, H, NF, B = 640, 480, 1000, a.batch
+    frames = synth.torch_stream(B, W, H, device="cuda", pitch=W, bounded=True, t0=0)
+
+    def run(parts, stage):
+        n = B // parts
+        exs = [og.Extractor(nfeatures=NF, width=W, height=H, max_batch=n) for _ in range(parts)]
+        cap = exs[0].max_keypoints
+        streams = [torch.cuda.Stream() for _ in range(parts)]
+        outs = [(torch.zeros((n, cap, 7), dtype=torch.float32, device="cuda"),
+                 torch.zeros((n, cap, 32), dtype=torch.uint8, device="cuda"),
+                 torch.zeros(n, dtype=torch.int32, device="cuda")) for _ in range(parts)]
+        evs = [torch.cuda.Event() for _ in range(parts)]
+        if parts > 1:
+            for e, ev in zip(exs, evs):
+                e.set_stage_event(stage, ev)
+        started = [False]
+
+        def step():
+            for i in range(parts):
+                prev = (i - 1) % parts
+                if parts > 1 and (i > 0 or started[0]):
+                    streams[i].wait_event(evs[prev])  # part i-1 (of this or the last step) passed the stage
+                exs[i].extract_batch(frames[i * n:(i + 1) * n], *outs[i], stream=streams[i], row_step=W,
+                                     frame_step=W * H)
+            started[0] = True
+
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        kp = float(sum(o[2].float().sum().item() for o in outs)) / B
+        for e in exs:
+            e.close()
+        return {"parts": parts, "offset_stage": stage if parts > 1 else None, "frames_per_s": round(B * a.steps / dt, 1),
+                "ms_per_step": round(1e3 * dt / a.steps, 4), "keypoints_per_frame": round(kp, 1)}
+
+    configs = [(1, None), (2, "pyramid"), (2, "fast_cells"), (2, "octree"), (4, "pyramid"), (4, "fast_cells"), (1, None)]
+    for parts, stage in configs:
+        print(json.dumps(run(parts, stage)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
