@@ -135,6 +135,10 @@ def parse(argv=None):
     ap.add_argument("--feed", default="hbm", choices=["hbm", "host"],
                     help="headline input: frames resident in HBM (default) or copied from pinned host memory "
                          "every step (the host_fed leg of the default line)")
+    ap.add_argument("--parts", type=int, default=1,
+                    help="headline step as this many sub-batches on their own streams, each started once the "
+                         "previous one has passed --part-stage (1: one extraction of the whole batch)")
+    ap.add_argument("--part-stage", default="pyramid", choices=["pyramid", "fast_cells", "octree"])
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     ap.add_argument("--cpu-dry-run", default=None, metavar="ENGINE.py",
                     help="tests only: gloo on the CPU with ENGINE.py standing in for orbgpu")
@@ -295,7 +299,8 @@ class _Dumper:
 class StreamBench:
     """Extract + SearchForInitialization over one sharded frame stream."""
 
-    def __init__(self, og, D: Dev, W, H, NF, B, rank, world, stream, dump=None, deliver="host", feed="hbm"):
+    def __init__(self, og, D: Dev, W, H, NF, B, rank, world, stream, dump=None, deliver="host", feed="hbm",
+                 parts=1, part_stage="pyramid"):
         import shard
         import synth
         self.og, self.D = og, D
@@ -304,7 +309,16 @@ class StreamBench:
         dev = D.device
         self.dev, self.stream = dev, stream
         self.pitch = (W + 15) // 16 * 16
-        self.ex = og.Extractor(nfeatures=NF, width=W, height=H, max_batch=B)
+        # --parts P: the step's B frames as P sub-batches, each on an extractor and a stream
+        # of its own; sub-batch i starts once sub-batch i-1 has passed `part_stage` (the
+        # first one after the previous step's last), so stages with different limits
+        # overlap (P = 1: one extraction of B frames on `stream`)
+        if B % parts:
+            raise SystemExit(f"--parts {parts} does not divide the batch {B}")
+        self.parts, self.part_n = parts, B // parts
+        self.exs = [og.Extractor(nfeatures=NF, width=W, height=H, max_batch=self.part_n) for _ in range(parts)]
+        self.ex = self.exs[0]
+        self.pstreams = [stream] + [D.stream(priority=-1) for _ in range(parts - 1)]
         cap = self.cap = self.ex.max_keypoints
         # pool: this rank's chunks of POOL_STEPS steps of the global stream
         self.pool_t0 = [shard.chunk_frames(s, rank, world, B)[0] for s in range(POOL_STEPS)]
@@ -358,7 +372,16 @@ class StreamBench:
         # region.
         self.mstream = D.stream()
         self.ev_pyr = D.event()
-        self.ex.set_stage_event(MATCH_AFTER[0], self.ev_pyr)
+        self.exs[-1].set_stage_event(MATCH_AFTER[0], self.ev_pyr)  # the step's last sub-batch
+        self.ev_part = [None] * parts
+        self.ev_part_done = [D.event() for _ in range(parts)]
+        if parts > 1:
+            for i, e in enumerate(self.exs):
+                if i == parts - 1 and part_stage == MATCH_AFTER[0]:
+                    self.ev_part[i] = self.ev_pyr  # one event per (extractor, stage)
+                else:
+                    self.ev_part[i] = D.event()
+                    e.set_stage_event(part_stage, self.ev_part[i])
         self.ev_ext = [D.event() for _ in range(2)]
         self.ev_match = [None, None]
         self.pending = None  # (set index, timing events) of the step whose match is not issued yet
@@ -392,8 +415,18 @@ class StreamBench:
             st.wait_event(self.ev_match[si])
         pidx = self.step_no % POOL_STEPS
         frames = self.pool[pidx] if self.feed == "hbm" else self._fed(self.step_no)
-        self.ex.extract_batch(frames, kps_all[1:], desc_all[1:], counts_all[1:], stream=st, row_step=self.pitch,
-                              frame_step=self.pitch * self.H)
+        n = self.part_n
+        for i, (e, ps) in enumerate(zip(self.exs, self.pstreams)):
+            if i > 0 and self.ev_match[si] is not None:
+                ps.wait_event(self.ev_match[si])
+            if self.parts > 1 and (i > 0 or self.step_no > 0):
+                ps.wait_event(self.ev_part[i - 1])  # i = 0: the previous step's last sub-batch
+            lo, hi = i * n, (i + 1) * n
+            e.extract_batch(frames[lo:hi], kps_all[1 + lo:1 + hi], desc_all[1 + lo:1 + hi], counts_all[1 + lo:1 + hi],
+                            stream=ps, row_step=self.pitch, frame_step=self.pitch * self.H)
+        for i in range(1, self.parts):  # the rest of the step (exchange, match) after every sub-batch
+            self.ev_part_done[i].record(self.pstreams[i])
+            st.wait_event(self.ev_part_done[i])
         with self.D.use_stream(st):
             prev = self.bx.exchange([kps_all[B], desc_all[B], counts_all[B:B + 1]])
             kps_all[0].copy_(prev[0])
@@ -433,7 +466,8 @@ class StreamBench:
         """input buffer of step k (its copy issued, the next step's copy issued behind it)"""
         if self.h2d_issued < k:
             self._issue_h2d(k)
-        self.stream.wait_event(self.ev_h2d[k % 2])
+        for ps in self.pstreams:
+            ps.wait_event(self.ev_h2d[k % 2])
         self._issue_h2d(k + 1)  # prefetch: overlaps this step's extraction
         return self.inbuf[k % 2]
 
@@ -477,10 +511,11 @@ class StreamBench:
         self.delivery.finish()
         D.synchronize()
         self.delivery.reset_stats()
-        self.ex.sync(self.stream)
-        self.ex.profile(True)
+        for e, ps in zip(self.exs, self.pstreams):
+            e.sync(ps)
+            e.profile(True)
+            e.stage_times(reset=True)
         self.timing_h2d, self.h2d_time = True, []
-        self.ex.stage_times(reset=True)
         evs = [(D.event(True), D.event(True)) for _ in range(steps)]
         _barrier(self.world)
         D.synchronize()
@@ -496,9 +531,15 @@ class StreamBench:
         elapsed, frames_total = aggregate(elapsed, self.B * steps, device=self.dev)
         delivery = gather_delivery_stats(delivery, self.world, self.dev)
         _barrier(self.world)
-        self.ex.sync(self.stream)
-        stage_ms, nb = self.ex.stage_times(reset=True)
-        self.ex.profile(False)
+        # stage times summed over the sub-batches (per launch: a stage's duration on its
+        # stream; with P > 1 sub-batches overlap, so the sum exceeds the step)
+        stage_ms, nb = {}, 0
+        for e, ps in zip(self.exs, self.pstreams):
+            e.sync(ps)
+            ms_i, nb = e.stage_times(reset=True)
+            e.profile(False)
+            for k, v in ms_i.items():
+                stage_ms[k] = stage_ms.get(k, 0.0) + v
         if self.dump is not None:
             self.dump.write()
         per_step = {k: v / max(nb, 1) for k, v in stage_ms.items()}
@@ -1173,7 +1214,8 @@ def main_mono(args, og, D, rank, world, stream):
     W, H, NF, desc_cfg = CONFIGS[args.config]
     B = args.batch or (512 if args.config == "mono640" else 256)
     MATCH_AFTER[0] = args.match_after
-    sb = StreamBench(og, D, W, H, NF, B, rank, world, stream, dump=args.dump, deliver=args.deliver, feed=args.feed)
+    sb = StreamBench(og, D, W, H, NF, B, rank, world, stream, dump=args.dump, deliver=args.deliver, feed=args.feed,
+                     parts=args.parts, part_stage=args.part_stage)
     parity = sb.parity_frame0() if (rank == 0 and D.cuda) else None
     r = sb.run(args.warmup, args.steps)
     sb.close()
@@ -1222,6 +1264,8 @@ def main_mono(args, og, D, rank, world, stream):
         "dtype": "u8",
         "config": {"workload": desc_cfg, "config": args.config, "frames_per_gpu_per_step": B,
                    "width": W, "height": H, "nfeatures": NF,
+                   "sub_batches": {"parts": args.parts, "frames_each": B // args.parts,
+                                   "next_starts_after": args.part_stage if args.parts > 1 else None},
                    "parallelism": f"one stream in contiguous per-rank chunks x{world}, boundary frame send/recv, "
                                   + ("per-rank delivery of trimmed outputs to pinned host memory"
                                      if args.deliver == "host" else "per-step counts-first gather to rank 0")},

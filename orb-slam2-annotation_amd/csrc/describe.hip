@@ -255,27 +255,32 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
         constexpr int kChunks = kPatch * (kRWidth / 16);  // 129
         const uint8_t* top = raw + (size_t)(cy - kPatchR) * rp + x0;
         uint4 c[3];
+        uint32_t loff[3];
+        // the dump for lanes past the patch: the wave's last blurred patch,
+        // written only after this staging (earlier keypoints' patches are final)
+        constexpr uint32_t kDump =
+            (uint32_t)((offsetof(DescLds, blur) + (kKeysPerWave - 1) * kBlur * kBPitch + 15) & ~size_t(15));
         // r = idx / 3 by a 24-bit multiply (exact for idx < 4096), row offsets
-        // by 24-bit multiplies (rp < 2^24: launcher check)
+        // by 24-bit multiplies (rp < 2^24: launcher check), unsigned 32-bit
+        // offsets (no sign extension); lanes past the patch load its last row
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const int idx = min(lane + 64 * k, kChunks - 1), r = (int)(__umul24((uint32_t)idx, 21846u) >> 16),
-                      q = idx - 3 * r;
-            c[k] = load16_a4(top + __umul24((uint32_t)r, (uint32_t)rp) + 16 * q);
+            const uint32_t idx = (uint32_t)(lane + 64 * k), r = __umul24(idx, 21846u) >> 16, q = idx - 3u * r;
+            loff[k] = idx < (uint32_t)kChunks ? __umul24(r, (uint32_t)kRPitch) + 16u * q : kDump;
+            c[k] = load16_a4(top + (__umul24(min(r, (uint32_t)kPatch - 1u), (uint32_t)rp) + 16u * q));
         }
+        // unconditional stores (lanes past the patch write into kDump): no
+        // branch the loads could be sunk into
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const int idx = lane + 64 * k, r = idx / 3, q = idx - 3 * r;
-            if (idx < kChunks) {
-                if constexpr (kRPitch % 16 == 0) {
-                    *reinterpret_cast<uint4*>(S.raw + r * kRPitch + 16 * q) = c[k];
-                } else {
-                    uint32_t* d = reinterpret_cast<uint32_t*>(S.raw + r * kRPitch + 16 * q);
-                    d[0] = c[k].x;
-                    d[1] = c[k].y;
-                    d[2] = c[k].z;
-                    d[3] = c[k].w;
-                }
+            if constexpr (kRPitch % 16 == 0) {
+                *reinterpret_cast<uint4*>(S.raw + loff[k]) = c[k];
+            } else {
+                uint32_t* d = reinterpret_cast<uint32_t*>(S.raw + loff[k]);
+                d[0] = c[k].x;
+                d[1] = c[k].y;
+                d[2] = c[k].z;
+                d[3] = c[k].w;
             }
         }
     } else {
@@ -319,9 +324,10 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
         vp = __builtin_amdgcn_udot4(w, e.mv, vp, false);
     }
     // wave totals now (scalars): the blur below then has every VGPR
-    const uint32_t tp = wave_total(sp);
-    const int m10 = (int)(wave_total(cp) - (uint32_t)(od + 15) * tp);
-    const int m01 = (int)(wave_total(vp) - 15u * tp);
+    // (the per-lane combinations first: two wave totals instead of three;
+    // modulo-2^32 sums, exact since the totals fit)
+    const int m10 = (int)wave_total(cp - (uint32_t)(od + 15) * sp);
+    const int m01 = (int)wave_total(vp - 15u * sp);
 
     // 3. Blur (blur_device.h, the arithmetic of blur.hip) of the 37x37 patch:
     // lane = (output quad q, chunk c of 7 blurred rows); row passes from the
@@ -341,11 +347,15 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
     // that packs with v_cvt_pk_u8_f32 alone: with a per-lane path choice the
     // compiler evaluates both roundings and selects (16 VALU per output row).
     auto passes = [&](auto all_simd) {
-        const int qq = lane / kColChunks, c = lane - qq * kColChunks;
+        // lane / 6 by a 24-bit multiply (exact for lane < 64); LDS offsets as
+        // 24-bit products (no quarter-rate v_mul_lo_u32 / v_mad_u64_u32)
+        const int qq = (int)(__umul24((uint32_t)lane, 10923u) >> 16), c = lane - qq * kColChunks;
         const int q = min(qq, kQuads - 1), r0 = c * 7;
         const bool simd = xb + 4 * q < simd_end, store = qq < kQuads;
+        const uint32_t raw0 = __umul24((uint32_t)r0, (uint32_t)kRPitch) + 4u * (uint32_t)q;
+        const uint32_t out0 = __umul24((uint32_t)r0, (uint32_t)kBPitch) + 4u * (uint32_t)q;
         auto row = [&](int k, blurdev::f32x2& lo, blurdev::f32x2& hi) {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(S.raw + (r0 + k) * kRPitch) + q;
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(S.raw + raw0 + k * kRPitch);
             blurdev::Raw3 R3;
             R3.a = w[0];
             R3.b = w[1];
@@ -371,7 +381,7 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
                     blurdev::col_pass(wl[j], wl[j + 1], wl[j + 2], wl[j + 3], wl[j + 4], wl[j + 5], wl[j + 6]);
                 const blurdev::f32x2 hi =
                     blurdev::col_pass(wh[j], wh[j + 1], wh[j + 2], wh[j + 3], wh[j + 4], wh[j + 5], wh[j + 6]);
-                reinterpret_cast<uint32_t*>(blur_out + (r0 + j) * kBPitch)[q] =
+                *reinterpret_cast<uint32_t*>(blur_out + out0 + j * kBPitch) =
                     all_simd ? blurdev::pack4_simd(lo, hi) : blurdev::pack4(lo, hi, simd);
             }
         }
@@ -421,8 +431,14 @@ __device__ void describe_tests(const Geom& g, int f, const KeyRef& K, int lane, 
     }
 
     const size_t o = (size_t)f * kp_cap + K.before + K.i;
-    if (lane < 4) reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = words[lane];
     if (lane == 0) {
+        // the four ballot words (scalars) from lane 0 as two 16-byte stores: 8
+        // moves, where selecting words[lane] on lanes 0..3 took 17 VALU
+        uint4* d = reinterpret_cast<uint4*>(desc + o * 32);
+        d[0] = make_uint4((uint32_t)words[0], (uint32_t)(words[0] >> 32), (uint32_t)words[1],
+                          (uint32_t)(words[1] >> 32));
+        d[1] = make_uint4((uint32_t)words[2], (uint32_t)(words[2] >> 32), (uint32_t)words[3],
+                          (uint32_t)(words[3] >> 32));
         orbgpu_keypoint kp;
         const float fx = (float)K.cx, fy = (float)K.cy;
         kp.x = K.l == 0 ? fx : __fmul_rn(fx, L.scale);

@@ -23,7 +23,18 @@ namespace {
 // clipped at the level's right edge can be one chunk wide), exact while
 // n < 2^23 / d and n * m < 2^32 -- here n < 512, d <= 5
 __host__ __device__ constexpr uint32_t fast_div_m(uint32_t d) { return (1u << 23) / d + 1u; }
-__device__ inline int fast_div(int n, uint32_t m) { return (int)(__umul24((uint32_t)n, m) >> 23); }
+// (both operands masked to 24 bits, so the product is one v_mul_u32_u24 even
+// with m in a scalar register)
+__device__ inline uint32_t fast_div(uint32_t n, uint32_t m) { return __umul24(n & 0xFFFFFFu, m & 0xFFFFFFu) >> 23; }
+// m for the divisors the staging uses (chunks or dwords per window row, <= 24),
+// a scalar table load instead of a VALU integer division
+struct DivTab { uint32_t m[25]; };
+constexpr DivTab make_div_tab() {
+    DivTab t{};
+    for (int d = 1; d < 25; ++d) t.m[d] = fast_div_m((uint32_t)d);
+    return t;
+}
+__constant__ DivTab c_div = make_div_tab();
 
 // The waves of a block work on different cells, so stages are ordered with
 // a wave-local LDS fence, never a block barrier.
@@ -323,45 +334,45 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     // frame base are 16-byte aligned; maxX <= w - 16, so no over-read)
     const int xa = iniX & ~3, ox = iniX - xa;
     const int nd = (maxX - xa + 3) >> 2;
-    const uint32_t mnd = fast_div_m((uint32_t)nd);
     // all of a lane's loads are issued before any is consumed, so the
-    // window costs one memory round trip, not one per row group
+    // window costs one memory round trip, not one per row group; (row,
+    // column) of an index by one 24-bit multiply, computed once for the load
+    // (row clamped into the window) and the store
     const uint8_t* wbase = base + (size_t)iniY * pitch + xa;
     if constexpr (P % 16 == 0) {
         // 16-byte chunks (P a multiple of 16: a row's chunks stay inside its LDS row; the
         // last chunk reads at most 12 bytes past maxX, still inside the level row since
         // maxX <= w - 16); one load per lane for ~64 of a window's ~115 chunks
-        const int nc = (maxX - xa + 15) >> 4;
-        const uint32_t mnc = fast_div_m((uint32_t)nc);
-        for (int b0 = 0; b0 < nc * wh; b0 += 64 * 2) {
+        const uint32_t nc = (uint32_t)(maxX - xa + 15) >> 4, total = nc * (uint32_t)wh;
+        const uint32_t mnc = c_div.m[nc];
+        for (uint32_t b0 = 0; b0 < total; b0 += 64 * 2) {
             uint4 v[2];
+            uint32_t loff[2];
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
-                const int idx = min(b0 + lane + 64 * k, nc * wh - 1);
-                const int r = fast_div(idx, mnc), q = idx - (int)__umul24((uint32_t)r, (uint32_t)nc);
-                v[k] = load16_a4(wbase + __umul24((uint32_t)r, pitch) + 16 * q);
+                const uint32_t idx = b0 + (uint32_t)(lane + 64 * k), r = fast_div(idx, mnc), q = idx - __umul24(r, nc);
+                loff[k] = idx < total ? __umul24(r, (uint32_t)P) + 16u * q : (uint32_t)(P * R);
+                v[k] = load16_a4(wbase + (__umul24(min(r, (uint32_t)wh - 1u), pitch) + 16u * q));
+            }
+            // unconditional stores (lanes past the window write into the score
+            // tile, zeroed below): no branch the loads could be sunk into
+#pragma unroll
+            for (int k = 0; k < 2; ++k) *reinterpret_cast<uint4*>(s_win + loff[k]) = v[k];
+        }
+    } else {
+        const uint32_t total = (uint32_t)(nd * wh), mnd = c_div.m[nd];
+        for (uint32_t b0 = 0; b0 < total; b0 += 64 * kStageLoads) {
+            uint32_t v[kStageLoads];
+            uint32_t loff[kStageLoads];
+#pragma unroll
+            for (int k = 0; k < kStageLoads; ++k) {  // unconditional (row-clamped) loads: no waits between them
+                const uint32_t idx = b0 + (uint32_t)(lane + 64 * k), r = fast_div(idx, mnd),
+                               q = idx - __umul24(r, (uint32_t)nd);
+                loff[k] = idx < total ? __umul24(r, (uint32_t)P) + 4u * q : (uint32_t)(P * R);
+                v[k] = *reinterpret_cast<const uint32_t*>(wbase + (__umul24(min(r, (uint32_t)wh - 1u), pitch) + 4u * q));
             }
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const int idx = b0 + lane + 64 * k;
-                const int r = fast_div(idx, mnc), q = idx - (int)__umul24((uint32_t)r, (uint32_t)nc);
-                if (idx < nc * wh) *reinterpret_cast<uint4*>(s_win + r * P + 16 * q) = v[k];
-            }
-        }
-    } else
-    for (int b0 = 0; b0 < nd * wh; b0 += 64 * kStageLoads) {
-        uint32_t v[kStageLoads];
-#pragma unroll
-        for (int k = 0; k < kStageLoads; ++k) {  // unconditional (clamped) loads: no waits between them
-            const int idx = min(b0 + lane + 64 * k, nd * wh - 1);
-            const int r = fast_div(idx, mnd), q = idx - (int)__umul24((uint32_t)r, (uint32_t)nd);
-            v[k] = *reinterpret_cast<const uint32_t*>(wbase + __umul24((uint32_t)r, pitch) + 4 * q);
-        }
-#pragma unroll
-        for (int k = 0; k < kStageLoads; ++k) {
-            const int idx = b0 + lane + 64 * k;
-            const int r = fast_div(idx, mnd), q = idx - (int)__umul24((uint32_t)r, (uint32_t)nd);
-            if (idx < nd * wh) *reinterpret_cast<uint32_t*>(s_win + r * P + 4 * q) = v[k];
+            for (int k = 0; k < kStageLoads; ++k) *reinterpret_cast<uint32_t*>(s_win + loff[k]) = v[k];
         }
     }
     // (T.sc is 16-byte aligned when P * R is: then 16-byte stores, else dwords)

@@ -678,8 +678,11 @@ int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int hei
     for (int b = 0; b < kBands; ++b) {
         const int y0 = height * b / kBands, y1 = height * (b + 1) / kBands;
         if (y1 <= y0) continue;
-        for (int y = y0; y < y1; ++y)
-            std::memcpy(e->h_img + (size_t)y * e->img_pitch, image + (size_t)y * step, width);
+        if (step == e->img_pitch)  // a continuous cv::Mat of a 16-multiple width: one copy per band
+            std::memcpy(e->h_img + (size_t)y0 * step, image + (size_t)y0 * step, step * (size_t)(y1 - y0));
+        else
+            for (int y = y0; y < y1; ++y)
+                std::memcpy(e->h_img + (size_t)y * e->img_pitch, image + (size_t)y * step, width);
         ORB_HIP(hipMemcpyAsync(e->d_img + (size_t)y0 * e->img_pitch, e->h_img + (size_t)y0 * e->img_pitch,
                                e->img_pitch * (size_t)(y1 - y0), hipMemcpyHostToDevice, s));
     }

@@ -1,11 +1,11 @@
 #!/bin/bash
 # Local wrapper around the gpurun client: re-submits ONLY when the call never
 # ran (gpurun status "transient": no box / box lost while being prepared --
-# nothing executed, nothing charged), up to 4 times with a pause.  Any call
+# nothing executed, nothing charged), up to GPURUN_RETRIES (12) times with a pause.  Any call
 # that ran, whatever its result, is never repeated.
 # usage: tools/gpurun_retry.sh <timeout> '<command>'
 t=$1; shift
-for i in 1 2 3 4 5 6; do
+for i in $(seq 1 ${GPURUN_RETRIES:-12}); do
   /usr/local/graft/bin/gpurun --timeout "$t" -- "$@" 2>&1 | tee /tmp/gpurun_retry_last.log
   rc=${PIPESTATUS[0]}
   st=$(python3 -c "import json;print(json.load(open('gpurun_out/.last_call.json')).get('status',''))" 2>/dev/null)
