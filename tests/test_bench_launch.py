@@ -58,20 +58,22 @@ def _merge_rank_dumps(tmp_path, name, world):
     return {k: np.concatenate([p[k] for p in parts])[order] for k in parts[0].files}
 
 
-@pytest.mark.parametrize("deliver", ["host", "gpu0"])
-def test_mono_stream_two_ranks_equals_single_process(tmp_path, deliver):
+@pytest.mark.parametrize("deliver,parts", [("host", 1), ("gpu0", 1), ("gpu0", 2)])
+def test_mono_stream_two_ranks_equals_single_process(tmp_path, deliver, parts):
     """both delivery modes (shard.Delivery): host -- each rank's trimmed
     outputs in its own host memory (merged here from the per-rank dumps);
-    gpu0 -- counts first, then the used rows, received by rank 0"""
+    gpu0 -- counts first, then the used rows, received by rank 0; and the
+    step as two sub-batches (--parts 2: each on its own extractor and stream)"""
     import orbref
     import shard
     import synth
     import torch
-    world, B, steps = 2, 2, 2
+    world, B, steps = 2, 2 * parts, 2
     line = _run_bench(tmp_path, "--config", "mono640", "--batch", str(B), "--steps", str(steps), "--warmup", "0",
-                      "--deliver", deliver)
+                      "--deliver", deliver, "--parts", str(parts))
     assert line["n_gpus"] == 2 and line["world_size_checked"] == 2
     assert line["config"]["frames_per_gpu_per_step"] == B
+    assert line["config"]["sub_batches"]["parts"] == parts
     dl = line["delivery"]
     assert dl["mode"] == deliver and len(dl["per_rank"]) == 2
     if deliver == "host":  # every rank moves its own outputs
