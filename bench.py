@@ -140,6 +140,8 @@ def parse(argv=None):
                     help="headline step as this many sub-batches on their own streams, each started once the "
                          "previous one has passed --part-stage (1: one extraction of the whole batch)")
     ap.add_argument("--part-stage", default="pyramid", choices=["pyramid", "fast_cells", "octree"])
+    ap.add_argument("--match-priority", type=int, default=0, choices=[0, -1],
+                    help="matcher stream priority (0: default, below the extraction streams; -1: high)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     ap.add_argument("--cpu-dry-run", default=None, metavar="ENGINE.py",
                     help="tests only: gloo on the CPU with ENGINE.py standing in for orbgpu")
@@ -148,6 +150,7 @@ def parse(argv=None):
 
 
 MATCH_AFTER = ["fast_cells"]  # set from --match-after
+MATCH_PRIORITY = [0]  # set from --match-priority (0: default, -1: high, as the extraction streams)
 
 
 # ---------------------------------------------------------------------------
@@ -371,14 +374,16 @@ class StreamBench:
         # The two output sets keep step k+1's extraction off the buffers step k-1's match
         # reads (it waits for that match).  run() flushes the last match inside the timed
         # region.
-        self.mstream = D.stream()
+        self.mstream = D.stream(priority=MATCH_PRIORITY[0])
         self.ev_pyr = D.event()
-        self.exs[-1].set_stage_event(MATCH_AFTER[0], self.ev_pyr)  # the step's last sub-batch
+        # the previous step's match starts once the first sub-batch has passed
+        # MATCH_AFTER: the next step's extraction into its output set waits for it
+        self.exs[0].set_stage_event(MATCH_AFTER[0], self.ev_pyr)
         self.ev_part = [None] * parts
         self.ev_part_done = [D.event() for _ in range(parts)]
         if parts > 1:
             for i, e in enumerate(self.exs):
-                if i == parts - 1 and part_stage == MATCH_AFTER[0]:
+                if i == 0 and part_stage == MATCH_AFTER[0]:
                     self.ev_part[i] = self.ev_pyr  # one event per (extractor, stage)
                 else:
                     self.ev_part[i] = D.event()
@@ -1215,6 +1220,7 @@ def main_mono(args, og, D, rank, world, stream):
     W, H, NF, desc_cfg = CONFIGS[args.config]
     B = args.batch or (512 if args.config == "mono640" else 256)
     MATCH_AFTER[0] = args.match_after
+    MATCH_PRIORITY[0] = args.match_priority
     sb = StreamBench(og, D, W, H, NF, B, rank, world, stream, dump=args.dump, deliver=args.deliver, feed=args.feed,
                      parts=args.parts, part_stage=args.part_stage)
     parity = sb.parity_frame0() if (rank == 0 and D.cuda) else None

@@ -433,6 +433,17 @@ int pyr_levels_max_batch() {
     return v;
 }
 
+// the single-frame path moves the frame in and the results out by kernels over
+// PCIe (a copy kernel reading pinned memory; describe writing the results into
+// pinned memory) -- ORBGPU_SINGLE_ZEROCOPY=0 selects copy-engine transfers
+bool single_zero_copy() {
+    static const bool v = [] {
+        const char* s = std::getenv("ORBGPU_SINGLE_ZEROCOPY");
+        return !(s && std::atoi(s) == 0);
+    }();
+    return v;
+}
+
 // ORBGPU_PYR_BANDS=0 selects the level-by-level launches (A/B and parity checks)
 bool pyr_bands_off() {
     static const bool v = [] {
@@ -670,6 +681,24 @@ int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int hei
     if (width != e->W || height != e->H) return fail(ORBGPU_ERR_ARG, "image size differs from the extractor geometry");
     if (step < (size_t)width) return fail(ORBGPU_ERR_ARG, "step < width");
     hipStream_t s = e->stream;
+    if (single_zero_copy()) {
+        // the drop-in (Frame constructor) path without copy-engine transfers:
+        // host image -> pinned staging (one memcpy for a continuous image) ->
+        // a copy kernel into HBM; extraction with describe writing keypoints,
+        // descriptors, the count and the error word straight into the pinned
+        // output block; one synchronisation
+        if (step == e->img_pitch)
+            std::memcpy(e->h_img, image, step * (size_t)height);
+        else
+            for (int y = 0; y < height; ++y)
+                std::memcpy(e->h_img + (size_t)y * e->img_pitch, image + (size_t)y * step, width);
+        ORB_HIP(launch_copy16(e->d_img, e->h_img, e->img_pitch * (size_t)height, s));
+        int rc = run_batch(e, e->d_img, 1, e->img_pitch, e->img_pitch * height,
+                           reinterpret_cast<orbgpu_keypoint*>(e->h_single + 16), e->h_single + e->single_desc_off,
+                           reinterpret_cast<int*>(e->h_single), e->max_kps, s, reinterpret_cast<int*>(e->h_single + 4));
+        if (rc) return rc;
+        ORB_HIP(hipStreamSynchronize(s));
+    } else {
     // the drop-in (Frame constructor) path: host image -> pinned staging ->
     // one async H2D; extraction; the error word folded into the output
     // block; one async D2H of the whole block; one synchronisation
@@ -692,6 +721,7 @@ int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int hei
     if (rc) return rc;
     ORB_HIP(hipMemcpyAsync(e->h_single, e->d_single, e->single_bytes, hipMemcpyDeviceToHost, s));
     ORB_HIP(hipStreamSynchronize(s));
+    }
     int count = 0, err = 0;
     std::memcpy(&count, e->h_single, sizeof(int));
     std::memcpy(&err, e->h_single + 4, sizeof(int));

@@ -68,6 +68,9 @@ hipError_t launch_match_init(int batch, float minX, float maxX, float minY, floa
 
 hipError_t launch_hamming_pairs(const uint8_t* a, const uint8_t* b, int n, int* dist, hipStream_t stream);
 hipError_t launch_pack_rows(int batch, int cap, int ntensors, const ::orbgpu_pack_desc* d, hipStream_t stream);
+// nbytes (a multiple of 16, both pointers 16-byte aligned) from src to dst by a kernel;
+// src may be pinned host memory
+hipError_t launch_copy16(void* dst, const void* src, size_t nbytes, hipStream_t stream);
 
 // error bits written to the device error word
 enum : int {

@@ -41,7 +41,26 @@ __global__ __launch_bounds__(kPackThreads) void pack_rows_kernel(orbgpu_pack_des
     for (int k = threadIdx.x; k < total; k += kPackThreads) dst[k] = src[k];
 }
 
+// The single-frame upload: the frame's rows from pinned host memory to HBM
+// by a kernel (16 bytes per thread, reads over PCIe), so the drop-in path
+// has no copy-engine transfer and no copy-engine / compute-queue handoff
+// (each cost ~8 us per transfer on the box, tools/dropin_timeline.py).
+__global__ __launch_bounds__(256) void copy16_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src, int n16) {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) dst[i] = src[i];
+}
+
 }  // namespace
+
+hipError_t launch_copy16(void* dst, const void* src, size_t nbytes, hipStream_t stream) {
+    if (nbytes % 16 || ((uintptr_t)dst & 15) || ((uintptr_t)src & 15) || nbytes / 16 > (size_t)INT32_MAX)
+        return hipErrorInvalidValue;
+    const int n16 = (int)(nbytes / 16);
+    if (n16 == 0) return hipSuccess;
+    const int blocks = (n16 + 255) / 256;
+    hipLaunchKernelGGL(copy16_kernel, dim3(blocks), dim3(256), 0, stream, reinterpret_cast<uint4*>(dst),
+                       reinterpret_cast<const uint4*>(src), n16);
+    return hipGetLastError();
+}
 
 hipError_t launch_pack_rows(int batch, int cap, int ntensors, const orbgpu_pack_desc* d, hipStream_t stream) {
     if (batch <= 0 || ntensors <= 0) return hipSuccess;

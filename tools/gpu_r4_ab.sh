@@ -27,9 +27,9 @@ for rep in 1 2; do
     ORBGPU_LIBRARY=$L/liborbgpu_$v.so timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-extras --deliver gpu0 > gpurun_out/${tag}_${v}_$rep.log 2>&1
   done
 done
-for pp in "2 pyramid" "2 fast_cells" "4 pyramid"; do
+for pp in "2 fast_cells 0" "2 fast_cells -1" "1 pyramid -1" "2 pyramid -1"; do
   set -- $pp
-  timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-extras --deliver gpu0 --parts $1 --part-stage $2 > gpurun_out/${tag}_parts$1_$2.log 2>&1 || echo "parts $pp rc $?"
+  timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-extras --deliver gpu0 --parts $1 --part-stage $2 --match-priority $3 > gpurun_out/${tag}_parts$1_$2_m$3.log 2>&1 || echo "parts $pp rc $?"
 done
 set -- $ok
 B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extras --deliver gpu0"

@@ -16,6 +16,7 @@ for k in range(2): open('$D/f%d.raw' % k, 'wb').write(fr[k].tobytes())
 "
 X="tests/cpp/adapter_main extract 640 480 1000 $D/f0.raw $D/f1.raw $D/x.out"
 ADAPTER_REPS=200 ADAPTER_TIME_LOG=$D/times.jsonl timeout -k 10 120 $X > $D/run.log 2>&1
+ORBGPU_SINGLE_ZEROCOPY=0 ADAPTER_REPS=200 ADAPTER_TIME_LOG=$D/times_sdma.jsonl timeout -k 10 120 $X > $D/run_sdma.log 2>&1
 ADAPTER_REPS=200 ADAPTER_TIME_LOG=$D/times_traced.jsonl timeout -k 10 180 rocprofv3 --kernel-trace --memory-copy-trace \
   --output-format csv -d $D/prof -o t -- $X > $D/prof.log 2>&1
 echo DROPIN_DONE
