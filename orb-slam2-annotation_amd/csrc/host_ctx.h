@@ -10,18 +10,32 @@
 // mirror, uploads them with ONE async copy, launches on the thread's stream,
 // reads the outputs back with ONE async copy and waits on that stream only.
 // No hipMalloc / hipFree / hipDeviceSynchronize per call, so the threads do
-// not serialise against each other or against a batch stream.
+// not serialise against each other or against a batch stream.  The two copies
+// are kernels (launch_copy16: reads or writes of the pinned mirror over PCIe)
+// rather than copy-engine transfers, whose hand-off to and from the compute
+// queue cost ~8 us each on the box (ORBGPU_HOST_ZEROCOPY=0: copy engine).
 #pragma once
 
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
 #include "host_common.h"
+#include "orbgpu_kernels.h"
 
 namespace orbgpu {
+
+// transfers of the host-form calls by copy kernels (default) or the copy engine
+inline bool host_copy_kernels() {
+    static const bool v = [] {
+        const char* s = std::getenv("ORBGPU_HOST_ZEROCOPY");
+        return !(s && std::atoi(s) == 0);
+    }();
+    return v;
+}
 
 struct HostCtx {
     hipStream_t stream = nullptr;
@@ -54,8 +68,12 @@ class HostCall {
         off_ = 0;
         stage(*this);
         used_ = off_;
-        if (used_)
-            ORB_HIP(hipMemcpyAsync(c_.dev, c_.pin, used_, hipMemcpyHostToDevice, c_.stream));
+        if (used_) {  // used_ is a multiple of 256 (take)
+            if (host_copy_kernels())
+                ORB_HIP(launch_copy16(c_.dev, c_.pin, used_, c_.stream));
+            else
+                ORB_HIP(hipMemcpyAsync(c_.dev, c_.pin, used_, hipMemcpyHostToDevice, c_.stream));
+        }
         return ORBGPU_OK;
     }
 
@@ -94,7 +112,15 @@ class HostCall {
             lo = f.off < lo ? f.off : lo;
             hi = f.off + f.bytes > hi ? f.off + f.bytes : hi;
         }
-        if (hi > lo) ORB_HIP(hipMemcpyAsync(c_.pin + lo, c_.dev + lo, hi - lo, hipMemcpyDeviceToHost, c_.stream));
+        if (hi > lo) {
+            // the span widened to 16-byte bounds stays inside the arena (its slots are
+            // 256-byte multiples); the extra bytes only overwrite staging copies
+            const size_t lo16 = lo & ~size_t(15), hi16 = (hi + 15) & ~size_t(15);
+            if (host_copy_kernels())
+                ORB_HIP(launch_copy16(c_.pin + lo16, c_.dev + lo16, hi16 - lo16, c_.stream));
+            else
+                ORB_HIP(hipMemcpyAsync(c_.pin + lo, c_.dev + lo, hi - lo, hipMemcpyDeviceToHost, c_.stream));
+        }
         ORB_HIP(hipStreamSynchronize(c_.stream));
         for (auto& f : fetches_) std::memcpy(f.dst, c_.pin + f.off, f.bytes);
         fetches_.clear();

@@ -794,20 +794,29 @@ int orbgpu_extractor_copy_levels(orbgpu_extractor* e, int frame, uint8_t* const*
         total += round_up((size_t)v.pitch * v.h, 256);
     }
     if (!e->h_levels) ORB_HIP(hipHostMalloc((void**)&e->h_levels, total, hipHostMallocDefault));
-    for (int l = 0; l < e->nlevels; ++l) {
-        const LevelGeom& v = e->g.lv[l];
-        if (l == 0)
-            ORB_HIP(hipMemcpy2DAsync(e->h_levels, (size_t)v.pitch, e->last_img + (size_t)frame * e->last_frame,
-                                     e->last_row, v.w, v.h, hipMemcpyDeviceToHost, e->stream));
-        else
-            ORB_HIP(hipMemcpyAsync(e->h_levels + off[l], e->d_pyr + v.offset + (size_t)frame * v.frame_bytes,
-                                   (size_t)v.pitch * v.h, hipMemcpyDeviceToHost, e->stream));
+    // level 0 of the last single-frame call is still in the pinned upload
+    // staging (zero-copy path); other levels (and level 0 otherwise) come back
+    // by one copy kernel writing the pinned staging (no copy-engine transfers)
+    const bool l0_host = single_zero_copy() && e->last_img == e->d_img && e->last_batch == 1;
+    if (!l0_host)
+        ORB_HIP(hipMemcpy2DAsync(e->h_levels, (size_t)e->g.lv[0].pitch, e->last_img + (size_t)frame * e->last_frame,
+                                 e->last_row, e->g.lv[0].w, e->g.lv[0].h, hipMemcpyDeviceToHost, e->stream));
+    if (e->nlevels > 1) {
+        CopyList16 L{};
+        L.n = 0;
+        for (int l = 1; l < e->nlevels && L.n < kCopyList; ++l) {
+            const LevelGeom& v = e->g.lv[l];
+            L.d[L.n++] = CopyDesc16{e->d_pyr + v.offset + (size_t)frame * v.frame_bytes, e->h_levels + off[l],
+                                    (size_t)v.pitch * v.h};
+        }
+        ORB_HIP(launch_copy16_list(L, e->stream));
     }
     ORB_HIP(hipStreamSynchronize(e->stream));
     for (int l = 0; l < e->nlevels; ++l) {
         const LevelGeom& v = e->g.lv[l];
-        for (int y = 0; y < v.h; ++y)
-            std::memcpy(dst[l] + (size_t)y * dst_step[l], e->h_levels + off[l] + (size_t)y * v.pitch, (size_t)v.w);
+        const uint8_t* src = l == 0 && l0_host ? e->h_img : e->h_levels + off[l];
+        const size_t sp = l == 0 && l0_host ? e->img_pitch : (size_t)v.pitch;
+        for (int y = 0; y < v.h; ++y) std::memcpy(dst[l] + (size_t)y * dst_step[l], src + (size_t)y * sp, (size_t)v.w);
     }
     return ORBGPU_OK;
 }

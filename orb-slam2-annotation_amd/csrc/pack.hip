@@ -11,6 +11,8 @@
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
 
+#include <algorithm>
+
 namespace orbgpu {
 
 namespace {
@@ -49,7 +51,32 @@ __global__ __launch_bounds__(256) void copy16_kernel(uint4* __restrict__ dst, co
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) dst[i] = src[i];
 }
 
+// up to kCopyList such copies in one launch (blockIdx.y = the copy)
+__global__ __launch_bounds__(256) void copy16_list_kernel(CopyList16 L) {
+    const CopyDesc16& d = L.d[blockIdx.y];
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(d.src);
+    uint4* __restrict__ dst = reinterpret_cast<uint4*>(d.dst);
+    const int n16 = (int)(d.bytes / 16);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) dst[i] = src[i];
+}
+
 }  // namespace
+
+hipError_t launch_copy16_list(const CopyList16& L, hipStream_t stream) {
+    if (L.n <= 0) return hipSuccess;
+    if (L.n > kCopyList) return hipErrorInvalidValue;
+    size_t most = 0;
+    for (int i = 0; i < L.n; ++i) {
+        const CopyDesc16& d = L.d[i];
+        if (d.bytes % 16 || ((uintptr_t)d.src & 15) || ((uintptr_t)d.dst & 15) || d.bytes / 16 > (size_t)INT32_MAX)
+            return hipErrorInvalidValue;
+        most = d.bytes > most ? d.bytes : most;
+    }
+    const int blocks = (int)std::min<size_t>((most / 16 + 255) / 256, 1024);
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(copy16_list_kernel, dim3(blocks, L.n), dim3(256), 0, stream, L);
+    return hipGetLastError();
+}
 
 hipError_t launch_copy16(void* dst, const void* src, size_t nbytes, hipStream_t stream) {
     if (nbytes % 16 || ((uintptr_t)dst & 15) || ((uintptr_t)src & 15) || nbytes / 16 > (size_t)INT32_MAX)

@@ -12,4 +12,5 @@ import bench  # noqa: E402
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
 with tempfile.TemporaryDirectory(prefix="orbgpu_dropin_") as td:
     ops = bench.DropIn(Path(td), reps=reps).run()
-print(json.dumps({k: v["median_us"] for k, v in ops.items()}, indent=1))
+print(json.dumps({k: ({f: v.get(f) for f in ("median_us", "p90_us", "p99_us", "max_us")} if isinstance(v, dict) else v)
+                  for k, v in ops.items()}, indent=1))
