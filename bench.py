@@ -323,6 +323,10 @@ class StreamBench:
         self.exs = [og.Extractor(nfeatures=NF, width=W, height=H, max_batch=self.part_n) for _ in range(parts)]
         self.ex = self.exs[0]
         self.pstreams = [stream] + [D.stream(priority=-1) for _ in range(parts - 1)]
+        # the step's tail (boundary exchange, the event the matcher waits for) on a stream of
+        # its own when the step is split: the next step's first sub-batch then waits only for
+        # the stage event, not for this step's last sub-batch to finish
+        self.tstream = D.stream(priority=-1) if parts > 1 else stream
         cap = self.cap = self.ex.max_keypoints
         # pool: this rank's chunks of POOL_STEPS steps of the global stream
         self.pool_t0 = [shard.chunk_frames(s, rank, world, B)[0] for s in range(POOL_STEPS)]
@@ -398,6 +402,8 @@ class StreamBench:
         kps_all, desc_all, counts_all, m12, nmatch = self.sets[si]
         ms = self.mstream
         ms.wait_event(after)
+        if after is not self.ev_ext[si]:
+            ms.wait_event(self.ev_ext[si])  # its step's tail (on its own stream when the step is split)
         if ev is not None:
             ev[0].record(ms)
         self.og.search_for_initialization_batch(self.W, self.H, kps_all[:-1], desc_all[:-1], counts_all[:-1],
@@ -430,15 +436,17 @@ class StreamBench:
             lo, hi = i * n, (i + 1) * n
             e.extract_batch(frames[lo:hi], kps_all[1 + lo:1 + hi], desc_all[1 + lo:1 + hi], counts_all[1 + lo:1 + hi],
                             stream=ps, row_step=self.pitch, frame_step=self.pitch * self.H)
-        for i in range(1, self.parts):  # the rest of the step (exchange, match) after every sub-batch
-            self.ev_part_done[i].record(self.pstreams[i])
-            st.wait_event(self.ev_part_done[i])
-        with self.D.use_stream(st):
+        ts = self.tstream
+        if self.parts > 1:  # the rest of the step (exchange, match) after every sub-batch
+            for i in range(self.parts):
+                self.ev_part_done[i].record(self.pstreams[i])
+                ts.wait_event(self.ev_part_done[i])
+        with self.D.use_stream(ts):
             prev = self.bx.exchange([kps_all[B], desc_all[B], counts_all[B:B + 1]])
             kps_all[0].copy_(prev[0])
             desc_all[0].copy_(prev[1])
             counts_all[0:1].copy_(prev[2])
-        self.ev_ext[si].record(st)
+        self.ev_ext[si].record(ts)
         if self.pending is not None:  # step k-1's match, after step k's FAST pass
             self._match(*self.pending[:1], self.ev_pyr, self.pending[1])
         self.pending = (si, ev)
