@@ -80,14 +80,19 @@ __device__ __forceinline__ void row_pass_raw_shifted(const Raw3& R, f32x2& lo, f
     constexpr uint32_t A1 = 18u << 16 | 34u << 24, B1 = 49u | 55u << 8 | 49u << 16 | 34u << 24, C1 = 18u;
     constexpr uint32_t A2 = 18u << 24, B2 = 34u | 49u << 8 | 55u << 16 | 49u << 24, C2 = 34u | 18u << 8;
     constexpr uint32_t B3 = 18u | 34u << 8 | 49u << 16 | 55u << 24, C3 = 49u | 34u << 8 | 18u << 16;
-    const uint32_t s0 = __builtin_amdgcn_udot4(R.b, B0, __builtin_amdgcn_udot4(R.a, A0, 0u, false), false);
+    // the sums accumulate onto the bits of 2^23 (0x4B000000), so each is the
+    // float 2^23 + s as it stands (s < 2^16); one packed subtract per two
+    // columns (exact) replaces four integer-to-float conversions
+    constexpr uint32_t M = 0x4B000000u;
+    const uint32_t s0 = __builtin_amdgcn_udot4(R.b, B0, __builtin_amdgcn_udot4(R.a, A0, M, false), false);
     const uint32_t s1 = __builtin_amdgcn_udot4(
-        R.c, C1, __builtin_amdgcn_udot4(R.b, B1, __builtin_amdgcn_udot4(R.a, A1, 0u, false), false), false);
+        R.c, C1, __builtin_amdgcn_udot4(R.b, B1, __builtin_amdgcn_udot4(R.a, A1, M, false), false), false);
     const uint32_t s2 = __builtin_amdgcn_udot4(
-        R.c, C2, __builtin_amdgcn_udot4(R.b, B2, __builtin_amdgcn_udot4(R.a, A2, 0u, false), false), false);
-    const uint32_t s3 = __builtin_amdgcn_udot4(R.c, C3, __builtin_amdgcn_udot4(R.b, B3, 0u, false), false);
-    lo = f32x2{(float)s0, (float)s1};
-    hi = f32x2{(float)s2, (float)s3};
+        R.c, C2, __builtin_amdgcn_udot4(R.b, B2, __builtin_amdgcn_udot4(R.a, A2, M, false), false), false);
+    const uint32_t s3 = __builtin_amdgcn_udot4(R.c, C3, __builtin_amdgcn_udot4(R.b, B3, M, false), false);
+    const f32x2 m = {8388608.f, 8388608.f};
+    lo = f32x2{__uint_as_float(s0), __uint_as_float(s1)} - m;
+    hi = f32x2{__uint_as_float(s2), __uint_as_float(s3)} - m;
 }
 
 // The same sums with the windows cut out by v_alignbyte_b32 ([x-3, x]
