@@ -470,7 +470,7 @@ constexpr int kDescWaves = ORBGPU_DESC_WAVES;  // keypoints (waves) per block
 // One wave per (frame, slot) item, four items per block.  Blocks are
 // XCD-swizzled so one frame's keypoints (whose neighbourhoods overlap) are
 // described on one XCD and its level rows are fetched into one L2.
-__global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int items,
+__global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int items, int f0,
                                                                    const uint8_t* __restrict__ img0, size_t row0,
                                                                    size_t frame0, const uint8_t* __restrict__ pyr,
                                                                    const uint32_t* __restrict__ oct_out,
@@ -499,7 +499,8 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
 #endif
     DSTAMP(0);
     const int per_frame = (g.slots_frame + kKeysPerWave - 1) / kKeysPerWave;
-    const int f = item / per_frame, slot0 = (item - f * per_frame) * kKeysPerWave;
+    const int fl = item / per_frame, slot0 = (item - fl * per_frame) * kKeysPerWave;
+    const int f = f0 + fl;  // frame of the whole batch (a chunk's launch starts at frame f0)
     if (item >= items) return;
     KeyRef K[kKeysPerWave];
     bool valid[kKeysPerWave];
@@ -594,11 +595,11 @@ extern "C" int orbgpu_debug_desc_stamps(unsigned long long* out, int reset) {
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                            const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
-                           hipStream_t stream, int* err_word, int* err_copy) {
-    const int items = (g.slots_frame + kKeysPerWave - 1) / kKeysPerWave * batch;  // waves
+                           hipStream_t stream, int* err_word, int* err_copy, int f0) {
+    const int items = (g.slots_frame + kKeysPerWave - 1) / kKeysPerWave * batch;  // waves (frames f0 .. f0+batch-1)
     if (row0 >= (1u << 24)) return hipErrorInvalidValue;  // row offsets by 24-bit multiplies
     const int blocks = (items + kDescWaves - 1) / kDescWaves;
-    hipLaunchKernelGGL(describe_kernel, dim3(blocks), dim3(64 * kDescWaves), 0, stream, g, items, img0, row0, frame0,
+    hipLaunchKernelGGL(describe_kernel, dim3(blocks), dim3(64 * kDescWaves), 0, stream, g, items, f0, img0, row0, frame0,
                        pyr, oct_out, oct_count, kps, desc, counts, kp_cap, err_word, err_copy);
     return hipGetLastError();
 }

@@ -178,6 +178,10 @@ struct orbgpu_extractor {
     uint8_t* d_desc1 = nullptr;
     int* d_count1 = nullptr;
     hipStream_t stream = nullptr;
+    // octree / describe chunk pipeline (run_batch): describe of chunk c on aux_stream
+    // while the octree of chunk c+1 runs on the batch stream
+    hipStream_t aux_stream = nullptr;
+    std::array<hipEvent_t, 9> od_ev{};  // [c]: octree of chunk c done; [8]: the describes done
     // stage timing
     bool profile = false;
     hipEvent_t stage_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // orbgpu_extractor_set_stage_event
@@ -198,6 +202,9 @@ struct orbgpu_extractor {
         if (h_img) (void)hipHostFree(h_img);
         if (h_levels) (void)hipHostFree(h_levels);
         if (stream) (void)hipStreamDestroy(stream);
+        if (aux_stream) (void)hipStreamDestroy(aux_stream);
+        for (hipEvent_t x : od_ev)
+            if (x) (void)hipEventDestroy(x);
         for (auto& a : ev)
             for (hipEvent_t x : a) (void)hipEventDestroy(x);
     }
@@ -433,6 +440,15 @@ int pyr_levels_max_batch() {
     return v;
 }
 
+// chunks of the octree / describe pipeline (ORBGPU_OD_CHUNKS, 1..8; 1 = the plain
+// sequence): the octree of chunk c+1 (latency bound) runs beside the describe of
+// chunk c (VALU bound)
+int od_chunks() {  // read per batch (a test switches it within one process)
+    const char* s = std::getenv("ORBGPU_OD_CHUNKS");
+    const int n = s ? std::atoi(s) : 1;
+    return n < 1 ? 1 : (n > 8 ? 8 : n);
+}
+
 // the single-frame path moves the frame in and the results out by kernels over
 // PCIe (a copy kernel reading pinned memory; describe writing the results into
 // pinned memory) -- ORBGPU_SINGLE_ZEROCOPY=0 selects copy-engine transfers
@@ -479,14 +495,43 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
     ORB_HIP(launch_fast_cells(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_cand, e->d_cell_counts, e->d_err, s));
     if (evs) ORB_HIP(hipEventRecord(evs[2], s));
     if (e->stage_ev[1]) ORB_HIP(hipEventRecord(e->stage_ev[1], s));
-    ORB_HIP(launch_octree(g, batch, e->d_cand, e->d_cell_counts, e->d_gkeys, e->d_gknode, e->d_oct_out,
-                          e->d_oct_count, e->d_err, e->oct_groups, 2, e->d_trace, s));
-    if (evs) ORB_HIP(hipEventRecord(evs[3], s));
-    if (e->stage_ev[2]) ORB_HIP(hipEventRecord(e->stage_ev[2], s));
-    // GaussianBlur is fused into describe (blur of each keypoint's patch);
-    // whole blurred levels exist only for the debug API
-    ORB_HIP(launch_describe(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_oct_out, e->d_oct_count, kps, desc,
-                            counts, kp_cap, s, err_copy ? e->d_err : nullptr, err_copy));
+    const int nch = (err_copy || batch < 16 * od_chunks()) ? 1 : od_chunks();
+    if (nch == 1) {
+        ORB_HIP(launch_octree(g, batch, e->d_cand, e->d_cell_counts, e->d_gkeys, e->d_gknode, e->d_oct_out,
+                              e->d_oct_count, e->d_err, e->oct_groups, 2, e->d_trace, s));
+        if (evs) ORB_HIP(hipEventRecord(evs[3], s));
+        if (e->stage_ev[2]) ORB_HIP(hipEventRecord(e->stage_ev[2], s));
+        // GaussianBlur is fused into describe (blur of each keypoint's patch);
+        // whole blurred levels exist only for the debug API
+        ORB_HIP(launch_describe(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_oct_out, e->d_oct_count, kps,
+                                desc, counts, kp_cap, s, err_copy ? e->d_err : nullptr, err_copy));
+    } else {
+        // the octree chunks in order on s, each chunk's describe on the aux stream after
+        // its octree: describe(c) overlaps octree(c+1); s joins the aux stream at the end
+        if (!e->aux_stream) {
+            int lo = 0, hi = 0;
+            ORB_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            ORB_HIP(hipStreamCreateWithPriority(&e->aux_stream, hipStreamNonBlocking, hi));
+            for (hipEvent_t& x : e->od_ev) ORB_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+        }
+        hipStream_t a = e->aux_stream;
+        for (int c = 0; c < nch; ++c) {
+            const int f0 = batch * c / nch, f1 = batch * (c + 1) / nch, nb = f1 - f0;
+            ORB_HIP(launch_octree(g, nb, e->d_cand + (size_t)f0 * g.cand_frame,
+                                  e->d_cell_counts + (size_t)f0 * g.total_cells,
+                                  e->d_gkeys + (size_t)f0 * g.cand_frame, e->d_gknode + (size_t)f0 * g.cand_frame,
+                                  e->d_oct_out + (size_t)f0 * g.slots_frame, e->d_oct_count + (size_t)f0 * kOcStride,
+                                  e->d_err, e->oct_groups, 2, c == 0 ? e->d_trace : nullptr, s));
+            if (c == 0 && evs) ORB_HIP(hipEventRecord(evs[3], s));  // (the octree stage: the first chunk's)
+            ORB_HIP(hipEventRecord(e->od_ev[c], s));
+            ORB_HIP(hipStreamWaitEvent(a, e->od_ev[c], 0));
+            ORB_HIP(launch_describe(g, nb, imgs, row_step, frame_step, e->d_pyr, e->d_oct_out, e->d_oct_count, kps,
+                                    desc, counts, kp_cap, a, nullptr, nullptr, f0));
+        }
+        if (e->stage_ev[2]) ORB_HIP(hipEventRecord(e->stage_ev[2], s));
+        ORB_HIP(hipEventRecord(e->od_ev[8], a));
+        ORB_HIP(hipStreamWaitEvent(s, e->od_ev[8], 0));
+    }
     if (evs) ORB_HIP(hipEventRecord(evs[4], s));
     if (e->stage_ev[3]) ORB_HIP(hipEventRecord(e->stage_ev[3], s));
     e->last_img = imgs;

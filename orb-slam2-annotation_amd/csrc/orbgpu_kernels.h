@@ -58,7 +58,7 @@ hipError_t launch_octree(const Geom& g, int batch, const uint32_t* cand, const i
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                            const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
-                           hipStream_t stream, int* err_word = nullptr, int* err_copy = nullptr);
+                           hipStream_t stream, int* err_word = nullptr, int* err_copy = nullptr, int f0 = 0);
 
 hipError_t launch_match_init(int batch, float minX, float maxX, float minY, float maxY,
                              const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,

@@ -171,6 +171,32 @@ def test_batch_device_matches_single(mono_frames):
         _assert_same_kps(kg, dd[b, :cc[b]], kr, dr)
 
 
+@pytest.mark.parametrize("chunks", [2, 4])
+def test_batch_octree_describe_chunks_match_oracle(monkeypatch, chunks):
+    """ORBGPU_OD_CHUNKS: the octree of chunk c+1 on the batch stream beside the
+    describe of chunk c on a second stream (run_batch); every frame of a
+    64-frame batch equals the oracle, the chunk boundaries included."""
+    og = _gpu()
+    monkeypatch.setenv("ORBGPU_OD_CHUNKS", str(chunks))
+    B = 64
+    frames = synth.mono_stream(B, 640, 480, seed=91)
+    ex = og.Extractor(max_batch=B)
+    imgs = torch.from_numpy(np.ascontiguousarray(frames)).cuda()
+    cap = ex.max_keypoints
+    kps = torch.zeros((B, cap, 7), dtype=torch.float32, device="cuda")
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(B, dtype=torch.int32, device="cuda")
+    ex.extract_batch(imgs, kps, desc, counts)
+    ex.sync()
+    ref = orbref.Extractor()
+    kk, dd, cc = kps.cpu().numpy(), desc.cpu().numpy(), counts.cpu().numpy()
+    step = B // chunks
+    for b in sorted({0, 1, step - 1, step, step + 1, B - 1, B // 2 + 3}):
+        kr, dr = ref.extract(frames[b])
+        kg = og.keypoints_from_raw(kk[b, :cc[b]])
+        _assert_same_kps(kg, dd[b, :cc[b]], kr, dr)
+
+
 @pytest.mark.parametrize("check_ori,annotated", [(True, False), (False, False), (True, True)])
 def test_search_for_initialization(mono_frames, check_ori, annotated):
     og = _gpu()
