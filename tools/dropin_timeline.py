@@ -6,6 +6,7 @@ position in a call the median duration and the median gap since the
 previous event ended.
 
 usage: dropin_timeline.py <rocprofv3 output dir> [--skip N]
+       [--anchor NAME --before B --after A]   (calls found around a kernel)
 """
 import csv
 import glob
@@ -27,11 +28,24 @@ def main():
     skip = int(sys.argv[sys.argv.index("--skip") + 1]) if "--skip" in sys.argv else 20
     ev = []
     for r in _rows(os.path.join(d, "**", "*kernel_trace.csv")):
-        ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0][-48:]))
+        ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][-48:]))
     for r in _rows(os.path.join(d, "**", "*memory_copy_trace.csv")):
         name = r.get("Direction", "copy")
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
     ev.sort()
+    if "--anchor" in sys.argv:
+        # calls without copy-engine transfers: the events from `before` events ahead
+        # of each event whose name contains ANCHOR to `after` events behind it
+        anchor = sys.argv[sys.argv.index("--anchor") + 1]
+        before = int(sys.argv[sys.argv.index("--before") + 1]) if "--before" in sys.argv else 1
+        after = int(sys.argv[sys.argv.index("--after") + 1]) if "--after" in sys.argv else 3
+        idx = [i for i, e in enumerate(ev) if anchor in e[2] and i >= before and i + after < len(ev)]
+        group = [ev[i - before:i + after + 1] for i in idx]
+        group = group[skip:] if len(group) > 2 * skip else group
+        key = tuple(x[2] for x in group[0])
+        group = [c for c in group if tuple(x[2] for x in c) == key]
+        _report(key, group, len(idx))
+        return
     calls, cur, last_d2h = [], [], False
     for e in ev:
         h2d = "HOST_TO_DEVICE" in e[2].upper()
@@ -47,7 +61,11 @@ def main():
         shape.setdefault(tuple(x[2] for x in c), []).append(c)
     key, group = max(shape.items(), key=lambda kv: len(kv[1]))
     group = group[skip:] if len(group) > 2 * skip else group
-    print(f"{len(calls)} calls, {len(group)} of the most common shape ({len(key)} events)")
+    _report(key, group, len(calls))
+
+
+def _report(key, group, ncalls):
+    print(f"{ncalls} calls, {len(group)} of the most common shape ({len(key)} events)")
     spans = [c[-1][1] - c[0][0] for c in group]
     print(f"call span (first event start -> last event end): median {statistics.median(spans) / 1e3:.1f} us, "
           f"p90 {sorted(spans)[int(0.9 * len(spans))] / 1e3:.1f} us")
