@@ -75,24 +75,31 @@ struct Raw3 {
 // they are, against the kernel shifted by m bytes -- m = 0: a[1..3] b[0..3];
 // m = 1: a[2..3] b c[0]; m = 2: a[3] b c[0..1]; m = 3: b c[0..2] -- ten
 // v_dot4_u32_u8 in all (2 + 3 + 3 + 2), exact (at most 255 * 257 = 65535).
-__device__ __forceinline__ void row_pass_raw_shifted(const Raw3& R, f32x2& lo, f32x2& hi) {
+// The four sums as integers, each added to `acc`.
+__device__ __forceinline__ void row_sums_shifted(const Raw3& R, uint32_t acc, uint32_t (&s)[4]) {
     constexpr uint32_t A0 = 0u | 18u << 8 | 34u << 16 | 49u << 24, B0 = 55u | 49u << 8 | 34u << 16 | 18u << 24;
     constexpr uint32_t A1 = 18u << 16 | 34u << 24, B1 = 49u | 55u << 8 | 49u << 16 | 34u << 24, C1 = 18u;
     constexpr uint32_t A2 = 18u << 24, B2 = 34u | 49u << 8 | 55u << 16 | 49u << 24, C2 = 34u | 18u << 8;
     constexpr uint32_t B3 = 18u | 34u << 8 | 49u << 16 | 55u << 24, C3 = 49u | 34u << 8 | 18u << 16;
+    s[0] = __builtin_amdgcn_udot4(R.b, B0, __builtin_amdgcn_udot4(R.a, A0, acc, false), false);
+    s[1] = __builtin_amdgcn_udot4(R.c, C1,
+                                  __builtin_amdgcn_udot4(R.b, B1, __builtin_amdgcn_udot4(R.a, A1, acc, false), false),
+                                  false);
+    s[2] = __builtin_amdgcn_udot4(R.c, C2,
+                                  __builtin_amdgcn_udot4(R.b, B2, __builtin_amdgcn_udot4(R.a, A2, acc, false), false),
+                                  false);
+    s[3] = __builtin_amdgcn_udot4(R.c, C3, __builtin_amdgcn_udot4(R.b, B3, acc, false), false);
+}
+
+__device__ __forceinline__ void row_pass_raw_shifted(const Raw3& R, f32x2& lo, f32x2& hi) {
     // the sums accumulate onto the bits of 2^23 (0x4B000000), so each is the
     // float 2^23 + s as it stands (s < 2^16); one packed subtract per two
     // columns (exact) replaces four integer-to-float conversions
-    constexpr uint32_t M = 0x4B000000u;
-    const uint32_t s0 = __builtin_amdgcn_udot4(R.b, B0, __builtin_amdgcn_udot4(R.a, A0, M, false), false);
-    const uint32_t s1 = __builtin_amdgcn_udot4(
-        R.c, C1, __builtin_amdgcn_udot4(R.b, B1, __builtin_amdgcn_udot4(R.a, A1, M, false), false), false);
-    const uint32_t s2 = __builtin_amdgcn_udot4(
-        R.c, C2, __builtin_amdgcn_udot4(R.b, B2, __builtin_amdgcn_udot4(R.a, A2, M, false), false), false);
-    const uint32_t s3 = __builtin_amdgcn_udot4(R.c, C3, __builtin_amdgcn_udot4(R.b, B3, M, false), false);
+    uint32_t s[4];
+    row_sums_shifted(R, 0x4B000000u, s);
     const f32x2 m = {8388608.f, 8388608.f};
-    lo = f32x2{__uint_as_float(s0), __uint_as_float(s1)} - m;
-    hi = f32x2{__uint_as_float(s2), __uint_as_float(s3)} - m;
+    lo = f32x2{__uint_as_float(s[0]), __uint_as_float(s[1])} - m;
+    hi = f32x2{__uint_as_float(s[2]), __uint_as_float(s[3])} - m;
 }
 
 // The same sums with the windows cut out by v_alignbyte_b32 ([x-3, x]
