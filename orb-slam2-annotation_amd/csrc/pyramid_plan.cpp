@@ -34,9 +34,6 @@ namespace {
 #ifndef ORBGPU_PYR_T0
 #define ORBGPU_PYR_T0 8  // level-0 rows per chunk (per tick)
 #endif
-#ifndef ORBGPU_PYR_BANKORDER
-#define ORBGPU_PYR_BANKORDER 0  // lane order spreading the horizontal-pass reads over the LDS banks (A/B)
-#endif
 #ifndef ORBGPU_PYR_LANES
 #define ORBGPU_PYR_LANES 576  // compute lanes the row-group split may use (9 waves + the tail wave + the producer: two blocks per CU)
 #endif
@@ -268,47 +265,6 @@ int plan_pyramid(Geom& g, const std::vector<int2>& ytab, const std::vector<int4>
             for (int gi = 0; gi < GT[l]; ++gi) tails.push_back(Ent{l, -1 - gi, Q - 2, Q - 1});  // gi < 0: tail groups
     }
     if (tails.size() > 64) return fail(ORBGPU_ERR_UNSUPPORTED, "pyramid: more than 64 scalar-tail columns");
-#if ORBGPU_PYR_BANKORDER
-    // Lane order for the LDS banks: the horizontal pass of a 32-lane half reads
-    // the dwords (w0 / 4) of its lanes' 12-byte windows, one instruction per
-    // dword.  Consecutive octs sit about 2.4 dwords apart (the 1.2x downscale),
-    // so octs ~13 apart share a bank (w0 / 4 mod 32) and the reads conflict
-    // 2-3 ways.  Each half takes, from the next 64 entries in order, the first
-    // whose quad-A and quad-B windows start on banks no earlier lane of the half
-    // uses (else the first in order): lanes are independent, the runs of one
-    // (level, group) stay together within the look-ahead.
-    {
-        auto bank = [&](const Ent& e, int q) {
-            const LevelGeom& v = g.lv[e.l];
-            return (ptab[(size_t)v.ptab_offset + 3 * (size_t)q].x >> 2) & 31;
-        };
-        std::vector<Ent> pend(ents.begin(), ents.end()), out;
-        out.reserve(pend.size());
-        size_t head = 0;
-        std::vector<char> used(pend.size(), 0);
-        while (out.size() < pend.size()) {
-            uint32_t ma = 0, mb = 0;
-            for (int lane = 0; lane < 32 && out.size() < pend.size(); ++lane) {
-                while (used[head]) ++head;
-                size_t pick = head;
-                for (size_t k = head, seen = 0; k < pend.size() && seen < 64; ++k) {
-                    if (used[k]) continue;
-                    ++seen;
-                    const uint32_t ba = 1u << bank(pend[k], pend[k].qa), bb = 1u << bank(pend[k], pend[k].qb);
-                    if (!(ma & ba) && !(mb & bb)) {
-                        pick = k;
-                        break;
-                    }
-                }
-                used[pick] = 1;
-                ma |= 1u << bank(pend[pick], pend[pick].qa);
-                mb |= 1u << bank(pend[pick], pend[pick].qb);
-                out.push_back(pend[pick]);
-            }
-        }
-        ents.swap(out);
-    }
-#endif
     while (!tails.empty() && ents.size() % 64 != 0) ents.push_back(Ent{0, 0, 0, 0});  // padding lanes
     ents.insert(ents.end(), tails.begin(), tails.end());
     const int n = (int)ents.size();
