@@ -1,6 +1,7 @@
 """The header-only C++ drop-in (include/orbslam2_amd/ORBextractor.h,
 ORBmatcher.h) used the way ORB-SLAM2's Frame / Initializer use the
 reference classes, driven by tests/cpp/adapter_main.cpp."""
+import os
 import struct
 import subprocess
 from pathlib import Path
@@ -58,14 +59,21 @@ def _read_frame(buf, off):
 
 
 @pytest.mark.gpu
-def test_adapter_extract_and_match_vs_oracle(exe, tmp_path):
+@pytest.mark.parametrize("copy_engine", [False, True])
+def test_adapter_extract_and_match_vs_oracle(exe, tmp_path, copy_engine):
+    """ORBextractor (with the host pyramid copy) + SearchForInitialization
+    through the C++ classes; transfers by copy kernels (default) and, with
+    ORBGPU_SINGLE_ZEROCOPY=0 ORBGPU_HOST_ZEROCOPY=0, by the copy engine."""
     w, h, nf = 640, 480, 1000
     frames = synth.mono_stream(2, w, h, seed=0x0B5E)
     for i, f in enumerate(frames):
         (tmp_path / f"f{i}.raw").write_bytes(f.tobytes())
     out = tmp_path / "out.bin"
+    env = dict(os.environ)
+    if copy_engine:
+        env.update(ORBGPU_SINGLE_ZEROCOPY="0", ORBGPU_HOST_ZEROCOPY="0")
     r = subprocess.run([exe, "extract", str(w), str(h), str(nf), str(tmp_path / "f0.raw"),
-                        str(tmp_path / "f1.raw"), str(out)], capture_output=True, text=True, timeout=300)
+                        str(tmp_path / "f1.raw"), str(out)], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     buf = out.read_bytes()
     k0, d0, off = _read_frame(buf, 0)
