@@ -27,7 +27,8 @@ for rep in 1 2; do
     ORBGPU_LIBRARY=$L/liborbgpu_$v.so timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-extras --deliver gpu0 > gpurun_out/${tag}_${v}_$rep.log 2>&1
   done
 done
-for pp in "2 fast_cells 0" "2 fast_cells -1" "1 pyramid -1" "2 pyramid -1"; do
+for pp in ${AB_LIGHT:+} "2 fast_cells 0" "2 fast_cells -1" "1 pyramid -1" "2 pyramid -1"; do
+  [ -n "$AB_LIGHT" ] && break
   set -- $pp
   timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-extras --deliver gpu0 --parts $1 --part-stage $2 --match-priority $3 > gpurun_out/${tag}_parts$1_$2_m$3.log 2>&1 || echo "parts $pp rc $?"
 done
@@ -38,9 +39,11 @@ for v in "$@"; do
   ORBGPU_LIBRARY=$L/liborbgpu_$v.so timeout -k 10 120 rocprofv3 --pmc SQ_BUSY_CU_CYCLES SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAVES --output-format csv -d gpurun_out/${tag}_pmc_$v -o q -- $B > gpurun_out/${tag}_pmc_$v.log 2>&1
 done
 echo ABDONE
-if [ -f tools/split_probe.py ]; then
+if [ -z "$AB_LIGHT" ] && [ -f tools/split_probe.py ]; then
   timeout -k 10 300 python3 -u tools/split_probe.py > gpurun_out/${tag}_split.log 2>&1 || echo "split probe rc $?"
 fi
 echo SPLITDONE
-timeout -k 10 400 bash tools/gpu_r4_dropin.sh ${tag} > gpurun_out/${tag}_dropin.log 2>&1 || echo "dropin rc $?"
+if [ -z "$AB_LIGHT" ]; then
+  timeout -k 10 400 bash tools/gpu_r4_dropin.sh ${tag} > gpurun_out/${tag}_dropin.log 2>&1 || echo "dropin rc $?"
+fi
 echo ABALLDONE
