@@ -409,7 +409,7 @@ class StreamBench:
             ev[0].record(ms)
         self.og.search_for_initialization_batch(self.W, self.H, kps_all[:-1], desc_all[:-1], counts_all[:-1],
                                                 kps_all[1:], desc_all[1:], counts_all[1:], m12, nmatch,
-                                                flags=self.flags, stream=ms)
+                                                flags=self.flags, stream=ms, max_level0=self.ex.level_capacity[0])
         if ev is not None:
             ev[1].record(ms)
         # delivery (packing on this stream, after the match; the copies or sends on the

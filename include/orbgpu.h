@@ -52,6 +52,9 @@ typedef struct orbgpu_extractor_info {
     int max_keypoints;              /* per-frame upper bound of output N   */
     int level_width[32], level_height[32];
     int features_per_level[32];     /* mnFeaturesPerLevel                  */
+    int level_capacity[32];         /* output slots per level: no frame yields more keypoints
+                                       at that level (DistributeOctTree keeps at most
+                                       mnFeaturesPerLevel + 3, or 4 per initial node)   */
 } orbgpu_extractor_info;
 
 const char* orbgpu_last_error(void);
@@ -179,6 +182,18 @@ int orbgpu_search_for_initialization_batch_device(
     const orbgpu_keypoint* d_kps1, const uint8_t* d_desc1, const int* d_n1, size_t stride1,
     const orbgpu_keypoint* d_kps2, const uint8_t* d_desc2, const int* d_n2, size_t stride2,
     float* d_prev_xy, int window, float nnratio, int flags,
+    int* d_matches12, int* d_nmatches, void* stream);
+
+/* The same with max_level0 > 0: a bound the caller knows on every frame's
+ * level-0 keypoints (e.g. orbgpu_extractor_info.level_capacity[0] of the
+ * extractor that produced them), so the larger-LDS passes are launched only
+ * when max_level0 exceeds 512 (1024); max_level0 = 0 is the form above.  A
+ * pair above the last pass launched reports d_nmatches[b] = -1. */
+int orbgpu_search_for_initialization_batch_device_bounded(
+    int batch, orbgpu_grid_bounds bounds,
+    const orbgpu_keypoint* d_kps1, const uint8_t* d_desc1, const int* d_n1, size_t stride1,
+    const orbgpu_keypoint* d_kps2, const uint8_t* d_desc2, const int* d_n2, size_t stride2,
+    float* d_prev_xy, int window, float nnratio, int flags, int max_level0,
     int* d_matches12, int* d_nmatches, void* stream);
 
 /* Host-pointer convenience form for one pair; returns nmatches in *n.

@@ -14,6 +14,7 @@
 // GetFeaturesInArea order (cell ix outer, iy inner, index) -- and a second
 // reduction for bestDist2.  The rotation histogram, ComputeThreeMaxima and
 // the cull run on the same wave.
+#include <cstdlib>
 #include <type_traits>
 
 #include "orbgpu_internal.h"
@@ -52,7 +53,7 @@ __device__ inline int wave_min_i(int v) {
     return v;
 }
 
-constexpr int kMatchThreads = 1024;
+constexpr int kBatchThreads = 256;
 constexpr int kTopK = 4;  // best candidate keys kept per query by the parallel phase
 
 // (dist, grid order) of a candidate as one ordered key: dist <= 256 (9 bits),
@@ -65,7 +66,7 @@ __device__ inline uint32_t cand_key(int dist, int cell, int j) {
 __device__ inline int key_dist(uint32_t key) { return (int)(key >> (12 + kKeyJBits)); }
 __device__ inline int key_j(uint32_t key) { return (int)(key & kKeyJMask); }
 
-// Two phases per frame pair (one 256-thread block):
+// Two phases per frame pair (one block of kMatchThreads threads):
 //  1 parallel, one thread per F1 query: the F2 level-0 keypoints of the
 //    query's window, walked through a cell CSR of F2 (the window's 64x48
 //    grid columns are contiguous runs, so a query visits only the keypoints
@@ -95,9 +96,9 @@ __device__ unsigned long long g_match_stamps[16];
 #define MSTAMP(k) ((void)0)
 #endif
 
-template <int kMaxK0>
+template <int kMaxK0, int kMatchThreads>
 __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
-    float minX, float maxX, float minY, float maxY, const orbgpu_keypoint* __restrict__ kps1,
+    int more, float minX, float maxX, float minY, float maxY, const orbgpu_keypoint* __restrict__ kps1,
     const uint8_t* __restrict__ desc1, const int* __restrict__ n1p, size_t stride1,
     const orbgpu_keypoint* __restrict__ kps2, const uint8_t* __restrict__ desc2, const int* __restrict__ n2p,
     size_t stride2, float* __restrict__ prev_xy, int window, float nnratio, int flags, int* __restrict__ matches12,
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
         // exceeded); no match is reported for the pair
         for (int i = tid; i < n1; i += kMatchThreads) M12[i] = -1;
         if (tid == 0)
-            nmatches_out[b] = kMaxK0 == kMaxK0Small ? kNeedLarge : kMaxK0 == kMaxK0Large ? kNeedHuge : -1;
+            nmatches_out[b] = !more ? -1 : kMaxK0 == kMaxK0Small ? kNeedLarge : kNeedHuge;
         return;
     }
     const unsigned long long* D2q = reinterpret_cast<const unsigned long long*>(D2);
@@ -521,6 +522,31 @@ __global__ __launch_bounds__(256) void hamming_pairs_kernel(const uint8_t* __res
     dist[i] = __popcll(x.x ^ y.x) + __popcll(x.y ^ y.y) + __popcll(x.z ^ y.z) + __popcll(x.w ^ y.w);
 }
 
+// Threads per pair block.  Phase 2 runs on one wave while the block's other
+// waves keep their slots, so a batch that fills the chip (the stream bench:
+// the matcher beside the next batch's extraction) takes the block size
+// ORBGPU_MATCH_THREADS names (256, 512 or 1024; default kBatchThreads) and
+// leaves more of the chip to the kernels beside it; a few pairs (the
+// drop-in's one) take 1024 threads, the shortest phase 1.
+constexpr int kChipFill = 256;
+int match_batch_threads() {
+    const char* s = std::getenv("ORBGPU_MATCH_THREADS");
+    const int v = s ? std::atoi(s) : kBatchThreads;
+    return v == 256 || v == 512 || v == 1024 ? v : kBatchThreads;
+}
+
+template <int kMaxK0, int kThreads>
+hipError_t launch_variant(int batch, int more, float minX, float maxX, float minY, float maxY,
+                          const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,
+                          const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2, size_t stride2,
+                          float* prev_xy, int window, float nnratio, int flags, int* matches12, int* nmatches,
+                          hipStream_t stream) {
+    hipLaunchKernelGGL((match_init_kernel<kMaxK0, kThreads>), dim3(batch), dim3(kThreads), 0, stream, more, minX, maxX,
+                       minY, maxY, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags,
+                       matches12, nmatches);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 #ifdef MATCH_STAMPS
@@ -541,25 +567,29 @@ hipError_t launch_match_init(int batch, float minX, float maxX, float minY, floa
                              float* prev_xy, int window, float nnratio, int flags,
                              int* matches12, int* nmatches, hipStream_t stream, size_t level0_bound) {
     // small variant for every pair, then the larger ones for the pairs handed
-    // over (a no-op block per other pair); a larger variant is launched only
-    // when a frame's level-0 keypoints can exceed the previous limit: bounded
-    // by its capacity (stride), or by level0_bound when the caller knows it
-    // (the host form counts them)
+    // over (a no-op block per other pair, which still waits for a CU with the
+    // variant's LDS free); a larger variant is launched only when a frame's
+    // level-0 keypoints can exceed the previous limit: bounded by its capacity
+    // (stride), or by level0_bound when the caller knows it (the host form
+    // counts them; a batch caller passes its extractor's level-0 output
+    // capacity).  The last variant launched reports a pair above its limit as -1.
     const size_t cap = level0_bound ? level0_bound : (stride1 > stride2 ? stride1 : stride2);
-    hipLaunchKernelGGL(match_init_kernel<kMaxK0Small>, dim3(batch), dim3(kMatchThreads), 0, stream, minX, maxX, minY,
-                       maxY, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags,
-                       matches12, nmatches);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || cap <= (size_t)kMaxK0Small) return e;
-    hipLaunchKernelGGL(match_init_kernel<kMaxK0Large>, dim3(batch), dim3(kMatchThreads), 0, stream, minX, maxX, minY,
-                       maxY, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags,
-                       matches12, nmatches);
-    e = hipGetLastError();
-    if (e != hipSuccess || cap <= (size_t)kMaxK0Large) return e;
-    hipLaunchKernelGGL(match_init_kernel<kMaxK0Huge>, dim3(batch), dim3(kMatchThreads), 0, stream, minX, maxX, minY,
-                       maxY, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags,
-                       matches12, nmatches);
-    return hipGetLastError();
+    const int more_large = cap > (size_t)kMaxK0Small, more_huge = cap > (size_t)kMaxK0Large;
+    const int threads = batch >= kChipFill ? match_batch_threads() : 1024;
+    hipError_t e;
+#define ORBGPU_MATCH_ARGS                                                                                         \
+    minX, maxX, minY, maxY, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags, \
+        matches12, nmatches, stream
+    if (threads == 256)
+        e = launch_variant<kMaxK0Small, 256>(batch, more_large, ORBGPU_MATCH_ARGS);
+    else if (threads == 512)
+        e = launch_variant<kMaxK0Small, 512>(batch, more_large, ORBGPU_MATCH_ARGS);
+    else
+        e = launch_variant<kMaxK0Small, 1024>(batch, more_large, ORBGPU_MATCH_ARGS);
+    if (e == hipSuccess && more_large) e = launch_variant<kMaxK0Large, 1024>(batch, more_huge, ORBGPU_MATCH_ARGS);
+    if (e == hipSuccess && more_huge) e = launch_variant<kMaxK0Huge, 1024>(batch, 0, ORBGPU_MATCH_ARGS);
+#undef ORBGPU_MATCH_ARGS
+    return e;
 }
 
 }  // namespace orbgpu

@@ -684,6 +684,7 @@ int orbgpu_extractor_get_info(const orbgpu_extractor* e, orbgpu_extractor_info* 
         info->level_width[l] = e->g.lv[l].w;
         info->level_height[l] = e->g.lv[l].h;
         info->features_per_level[l] = e->g.lv[l].nfeat;
+        info->level_capacity[l] = e->g.lv[l].ocap;
     }
     return ORBGPU_OK;
 }
@@ -905,17 +906,26 @@ int orbgpu_pack_rows_device(int batch, int cap, int ntensors, const orbgpu_pack_
     return ORBGPU_OK;
 }
 
+int orbgpu_search_for_initialization_batch_device_bounded(
+    int batch, orbgpu_grid_bounds bd, const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,
+    const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2, size_t stride2, float* prev_xy, int window,
+    float nnratio, int flags, int max_level0, int* matches12, int* nmatches, void* stream) {
+    if (batch <= 0 || !kps1 || !kps2 || !desc1 || !desc2 || !n1 || !n2 || !matches12 || !nmatches ||
+        !(bd.max_x > bd.min_x) || !(bd.max_y > bd.min_y) || max_level0 < 0)
+        return fail(ORBGPU_ERR_ARG, "invalid argument");
+    ORB_HIP(launch_match_init(batch, bd.min_x, bd.max_x, bd.min_y, bd.max_y, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy,
+                              window, nnratio, flags, matches12, nmatches, (hipStream_t)stream, (size_t)max_level0));
+    return ORBGPU_OK;
+}
+
 int orbgpu_search_for_initialization_batch_device(int batch, orbgpu_grid_bounds bd, const orbgpu_keypoint* kps1,
                                                   const uint8_t* desc1, const int* n1, size_t stride1,
                                                   const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2,
                                                   size_t stride2, float* prev_xy, int window, float nnratio,
                                                   int flags, int* matches12, int* nmatches, void* stream) {
-    if (batch <= 0 || !kps1 || !kps2 || !desc1 || !desc2 || !n1 || !n2 || !matches12 || !nmatches ||
-        !(bd.max_x > bd.min_x) || !(bd.max_y > bd.min_y))
-        return fail(ORBGPU_ERR_ARG, "invalid argument");
-    ORB_HIP(launch_match_init(batch, bd.min_x, bd.max_x, bd.min_y, bd.max_y, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy,
-                              window, nnratio, flags, matches12, nmatches, (hipStream_t)stream));
-    return ORBGPU_OK;
+    return orbgpu_search_for_initialization_batch_device_bounded(batch, bd, kps1, desc1, n1, stride1, kps2, desc2, n2,
+                                                                 stride2, prev_xy, window, nnratio, flags, 0,
+                                                                 matches12, nmatches, stream);
 }
 
 int orbgpu_search_for_initialization(orbgpu_grid_bounds bd, const orbgpu_keypoint* kps1, const uint8_t* desc1,

@@ -77,7 +77,7 @@ class _Info(ctypes.Structure):
     _fields_ = [("nlevels", ctypes.c_int), ("width", ctypes.c_int), ("height", ctypes.c_int),
                 ("max_batch", ctypes.c_int), ("max_keypoints", ctypes.c_int),
                 ("level_width", ctypes.c_int * 32), ("level_height", ctypes.c_int * 32),
-                ("features_per_level", ctypes.c_int * 32)]
+                ("features_per_level", ctypes.c_int * 32), ("level_capacity", ctypes.c_int * 32)]
 
 
 def lib() -> ctypes.CDLL:
@@ -112,6 +112,8 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_pack_rows_device.argtypes = [i, i, i, ctypes.POINTER(PackDesc), vp]
         L.orbgpu_search_for_initialization_batch_device.argtypes = [
             i, GridBounds, vp, vp, vp, sz, vp, vp, vp, sz, vp, i, f, i, vp, vp, vp]
+        L.orbgpu_search_for_initialization_batch_device_bounded.argtypes = [
+            i, GridBounds, vp, vp, vp, sz, vp, vp, vp, sz, vp, i, f, i, i, vp, vp, vp]
         L.orbgpu_debug_level_candidates.argtypes = [vp, i, i, vp, i]
         L.orbgpu_debug_level_blur.argtypes = [vp, i, i, vp, sz]
         L.orbgpu_debug_level_octree.argtypes = [vp, i, i, vp, i]
@@ -239,6 +241,7 @@ class Extractor:
         self.max_keypoints = info.max_keypoints
         self.level_sizes = [(info.level_width[l], info.level_height[l]) for l in range(self.nlevels)]
         self.features_per_level = [info.features_per_level[l] for l in range(self.nlevels)]
+        self.level_capacity = [info.level_capacity[l] for l in range(self.nlevels)]
 
     def close(self):
         if getattr(self, "h", None):
@@ -379,14 +382,16 @@ def search_for_initialization(kps1, desc1, kps2, desc2, img_w, img_h, prev_xy=No
 
 def search_for_initialization_batch(img_w, img_h, kps1, desc1, n1, kps2, desc2, n2, matches12, nmatches,
                                     prev_xy=None, window=100, nnratio=0.9, flags=MATCH_CHECK_ORI, stream=None,
-                                    bounds=None):
-    """Device form over B pairs (tensors on the GPU, see include/orbgpu.h)."""
+                                    bounds=None, max_level0=0):
+    """Device form over B pairs (tensors on the GPU, see include/orbgpu.h).
+    max_level0 > 0: a known bound on every frame's level-0 keypoints (an
+    Extractor's level_capacity[0]); pairs above it report nmatches -1."""
     B = n2.shape[0]
     bd = bounds if bounds is not None else bounds_for(img_w, img_h)
-    _check(lib().orbgpu_search_for_initialization_batch_device(
+    _check(lib().orbgpu_search_for_initialization_batch_device_bounded(
         B, bd, _ptr(kps1), _ptr(desc1), _ptr(n1), desc1.shape[1], _ptr(kps2), _ptr(desc2), _ptr(n2),
-        desc2.shape[1], _ptr(prev_xy) if prev_xy is not None else None, window, nnratio, flags,
-        _ptr(matches12), _ptr(nmatches), _stream_ptr(stream)), "orbgpu_search_for_initialization_batch_device")
+        desc2.shape[1], _ptr(prev_xy) if prev_xy is not None else None, window, nnratio, flags, max_level0,
+        _ptr(matches12), _ptr(nmatches), _stream_ptr(stream)), "orbgpu_search_for_initialization_batch_device_bounded")
 
 
 def hamming_pairs(a, b, out, stream=None):

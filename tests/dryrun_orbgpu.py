@@ -40,6 +40,7 @@ class Extractor:
         self.ex = orbref.Extractor(nfeatures, scale_factor, nlevels, ini_th, min_th)
         self.args = (nfeatures, scale_factor, nlevels, ini_th, min_th)
         self.max_keypoints = nfeatures + 3 * nlevels + 64
+        self.level_capacity = [self.max_keypoints] * nlevels
         _, inv, _, _ = self.ex.scale_factors()
         self.level_sizes = [(_round_half_even(width * inv[l]), _round_half_even(height * inv[l]))
                             for l in range(nlevels)]
@@ -73,7 +74,7 @@ def _kp(t, n):
 
 def search_for_initialization_batch(img_w, img_h, kps1, desc1, n1, kps2, desc2, n2, matches12, nmatches,
                                     prev_xy=None, window=100, nnratio=0.9, flags=MATCH_CHECK_ORI, stream=None,
-                                    bounds=None):
+                                    bounds=None, max_level0=0):
     for b in range(n2.shape[0]):
         a, c = int(n1[b]), int(n2[b])
         matches12[b] = -1

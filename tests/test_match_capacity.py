@@ -159,3 +159,38 @@ def test_pack_rows_device_equals_host_unpack():
             ref[b, cnt[b]:] = 0
         assert np.array_equal(back, ref)
         assert not packed[n:].cpu().numpy().any()  # nothing written past the used rows
+
+
+@pytest.mark.parametrize("threads", ["256", "512", "1024"])
+def test_batch_block_sizes_and_level0_bound(mono_frames, monkeypatch, threads):
+    """A batch that fills the chip (>= 256 pairs) runs the small variant with
+    ORBGPU_MATCH_THREADS threads per pair: every block size equals the
+    oracle.  With max_level0 (the extractor's level-0 capacity) the larger
+    variants are launched only when the bound needs them; a pair above the
+    last variant launched reports -1."""
+    og = _gpu()
+    monkeypatch.setenv("ORBGPU_MATCH_THREADS", threads)
+    ref = orbref.Extractor()
+    f0, f1 = ref.extract(mono_frames[0]), ref.extract(mono_frames[1])
+    mid1, mid2 = _crowded(800, 11), _crowded(800, 12)
+    big1, big2 = _crowded(1900, 13), _crowded(1500, 14)
+    kinds = [(f0, f1), (mid1, mid2), (big1, big2)]
+    want = [orbref.search_for_initialization(a[0], a[1], c[0], c[1], 640, 480)[:2] for a, c in kinds]
+    B, cap = 258, 1900
+    order = [b % 3 if b % 8 == 0 else 0 for b in range(B)]  # mostly normal pairs, as a stream has
+    K1, D1, N1 = _pack([kinds[k][0] for k in order], cap)
+    K2, D2, N2 = _pack([kinds[k][1] for k in order], cap)
+    for bound, ok in ((0, (True, True, True)), (600, (True, True, False)), (300, (True, False, False))):
+        m12 = torch.full((B, cap), -7, dtype=torch.int32, device="cuda")
+        nm = torch.full((B,), 99, dtype=torch.int32, device="cuda")
+        og.search_for_initialization_batch(640, 480, K1, D1, N1, K2, D2, N2, m12, nm, max_level0=bound)
+        torch.cuda.synchronize()
+        nm_h, m12_h = nm.cpu().numpy(), m12.cpu().numpy()
+        for b, k in enumerate(order):
+            n1 = len(kinds[k][0][0])
+            if ok[k]:
+                assert nm_h[b] == want[k][0], (bound, b, k)
+                np.testing.assert_array_equal(m12_h[b, :n1], want[k][1])
+            else:
+                assert nm_h[b] == -1, (bound, b, k)
+                assert (m12_h[b, :n1] == -1).all()
