@@ -7,7 +7,8 @@ wrote -- so the select takes a stale SCC from an earlier scalar op
 (reproducer: tools/scc_repro.hip).  This script scans device assembly
 (`hipcc -S --cuda-device-only`) and reports every s_cselect / s_cbranch_scc*
 whose nearest preceding definition of SCC-or-VCC in the same basic block is
-a VALU compare into VCC, unless the compare's VCC is read by an instruction before the consumer,
+a VALU compare into VCC, unless the compare's VCC is read by an instruction before the consumer or
+by the consumer itself (vcc / vcc_lo / vcc_hi as a source operand),
 or after it before VCC is redefined in the same block (then the compare has its own user and the
 consumer's SCC comes from an earlier scalar op), or the SCC the consumer actually reads was set
 in that block by `s_and_b64 s, vcc, exec` -- the compiler's uniform lowering
@@ -37,7 +38,7 @@ def vcc_read(lines, lo, hi):
         if ins.startswith(";") or VCC_CMP.match(ins):
             continue
         ops = ins.split(None, 1)
-        if len(ops) == 2 and re.search(r"\bvcc\b", ops[1].split(",", 1)[1] if "," in ops[1] else ""):
+        if len(ops) == 2 and re.search(r"\bvcc(_lo|_hi)?\b", ops[1].split(",", 1)[1] if "," in ops[1] else ""):
             return True
     return False
 
@@ -81,7 +82,9 @@ def scan(lines):
                     hits.append((i + 1, line.strip(), cmp_at + 1, lines[cmp_at].strip()))
                 cmp_at = None
                 break
-            if VCC_CMP.match(prev) and cmp_at is None and not vcc_read(lines, j + 1, i) and \
+            # (the consumer itself reading VCC as a source, e.g. s_cselect_b32 s, vcc_hi, 0
+            # after s_cmp: the compare's mask is its data, its SCC the earlier scalar compare)
+            if VCC_CMP.match(prev) and cmp_at is None and not vcc_read(lines, j + 1, i + 1) and \
                     not vcc_read_after(lines, i):
                 cmp_at = j
         if cmp_at is not None:  # reached the block start: SCC comes from another block
