@@ -36,6 +36,17 @@ constexpr DivTab make_div_tab() {
 }
 __constant__ DivTab c_div = make_div_tab();
 
+#ifndef ORBGPU_FAST_BANDS
+#define ORBGPU_FAST_BANDS 1
+#endif
+// survivor-list entries per cell wave: every pixel of a cell, or with
+// ORBGPU_FAST_BANDS a list that keeps the wave's LDS within 4,864 B (32 waves
+// per CU; at least 256 entries)
+__host__ __device__ constexpr int fast_list_len(int P, int R, int det_max) {
+    const int c = ((4864 - 2 * P * R - 16) / 2 - 1) & ~7;
+    return !ORBGPU_FAST_BANDS || c >= det_max ? det_max : (c >= 256 ? c : det_max);
+}
+
 // The waves of a block work on different cells, so stages are ordered with
 // a wave-local LDS fence, never a block barrier.
 __device__ inline void wave_sync() {
@@ -80,8 +91,9 @@ struct CellTiles {
 //   pairwise max is; both brighter than v + t <=> the largest pairwise min
 //   is; dark < v - t <=> sat(v - dark) > t, bright > v + t <=> sat(bright - v) > t
 // Returns the number of survivors, listed (tile offsets, row-major) in T.la.
-template <int P, int LPR>
-__device__ int compass_pass(const CellTiles& T, int dw, int dh, int ox, int t, int lane) {
+template <int P, int LPR, bool kBand = false>
+__device__ int compass_pass(const CellTiles& T, int dw, int dh, int ox, int t, int lane, int row0 = 0, int start = 0,
+                            int* row_end = nullptr) {
     constexpr int kStep = 64 / LPR;  // rows between a lane's two pixels
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
     auto compass2 = [&](const uint8_t* p) -> uint32_t {
@@ -115,9 +127,11 @@ __device__ int compass_pass(const CellTiles& T, int dw, int dh, int ox, int t, i
     const int rsub = LPR == 32 ? lane >> 5 : 0, col = lane & (LPR - 1);
     const unsigned long long colmask = __builtin_amdgcn_uicmp((uint32_t)col, (uint32_t)dw, 36 /* ult */);
     constexpr unsigned long long sub0 = LPR == 32 ? 0xFFFFFFFFull : ~0ull;  // lanes of row rsub = 0
-    int o = (3 + rsub) * P + 3 + ox + col;  // tile offset of the lane's first pixel
-    int na = 0;
-    for (int rr = 0; rr < dh; rr += 2 * kStep, o += 2 * kStep * P) {
+    int o = (3 + rsub + row0) * P + 3 + ox + col;  // tile offset of the lane's first pixel
+    int na = start;
+    int rr = row0;
+    for (; rr < dh; rr += 2 * kStep, o += 2 * kStep * P) {
+        if (kBand && na + 128 > T.dump) break;  // a pass adds at most 128 entries: the band ends here
         const uint32_t y = compass2(T.win + o);
         const int rem = dh - rr;  // rows left, >= 1
         const unsigned long long rows0 = rem >= 2 ? ~0ull : sub0;
@@ -129,6 +143,7 @@ __device__ int compass_pass(const CellTiles& T, int dw, int dh, int ox, int t, i
         T.la[na + lane_select(m1, below(m1), T.dump - na)] = (uint16_t)(o + kStep * P);
         na += __popcll(m1);
     }
+    if (kBand) *row_end = rr;
     return na;
 }
 
@@ -217,9 +232,8 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
 // the detection region count 0), emitted in lb order = row-major.
 template <int P>
 __device__ int nms_emit(const CellTiles& T, int nb, int ox, int t, int lane, int iniX, int iniY,
-                        uint32_t* out, int cap, int* err) {
-    int total = 0;
-    for (int base = 0; base < nb; base += 64) {
+                        uint32_t* out, int cap, int* err, int jbeg = 0, int total = 0) {
+    for (int base = jbeg; base < nb; base += 64) {
         const int j = base + lane;
         bool keep = false;
         int s = 0, off = 0;
@@ -258,6 +272,103 @@ __device__ int nms_emit(const CellTiles& T, int nb, int ox, int t, int lane, int
     return total;
 }
 
+// FAST + NMS of one cell with a survivor list shorter than the detection
+// region (ORBGPU_FAST_BANDS: less LDS per wave, more waves per CU).  The
+// compass runs in row bands that fit the list after the pending corners;
+// each band's survivors go through the arc pass (corners compacted behind the
+// pending ones); when rows remain, the corners whose 3x3 neighbourhood is
+// complete (region rows < row - 1) are emitted -- they lead the row-major
+// list, so the emission order is cv::FAST's -- and the others move to the
+// front.  Returns the keypoints emitted; *pending = corners left in the
+// list, *dropped = whether emitted corners left the list (their scores stay
+// in the tile).
+template <int P>
+__device__ int fast_cell_banded(const CellTiles& T, int dw, int dh, int ox, int t, int lane, int iniX, int iniY,
+                                uint32_t* out, int cap, int* err, int* pending, bool* dropped) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    typedef short i16x2 __attribute__((ext_vector_type(2)));
+    const int ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+    const int ring_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+    auto max3 = [](h2 x, h2 y, h2 z) { return __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z); };
+    auto min3 = [](h2 x, h2 y, h2 z) { return __builtin_elementwise_minimum(__builtin_elementwise_minimum(x, y), z); };
+    int nb = 0, total = 0, row = 0;
+    bool drop = false;
+    while (true) {
+        int row_end = dh;
+        const int na = dw > 32 ? compass_pass<P, 64, true>(T, dw, dh, ox, t, lane, row, nb, &row_end)
+                               : compass_pass<P, 32, true>(T, dw, dh, ox, t, lane, row, nb, &row_end);
+        wave_sync();
+        int nc = nb;
+        for (int base = nb; base < na; base += 128) {
+            const int j0 = base + lane, j1 = j0 + 64;
+            const int off0 = T.la[min(j0, na - 1)], off1 = T.la[min(j1, na - 1)];
+            int a0 = off0 - (3 * P + 3), a1 = off1 - (3 * P + 3);
+            asm volatile("" : "+v"(a0), "+v"(a1));
+            const uint8_t* p0 = T.win + a0;
+            const uint8_t* p1 = T.win + a1;
+            auto pair = [&](int o) { return (uint32_t)p0[o] | ((uint32_t)p1[o] << 16); };
+            const uint32_t vv = pair(3 * P + 3);
+            h2 r[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) r[k] = __builtin_bit_cast(h2, pair((ring_dy[k] + 3) * P + ring_dx[k] + 3));
+            h2 hi3[16], lo3[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                hi3[k] = max3(r[k], r[(k + 1) & 15], r[(k + 2) & 15]);
+                lo3[k] = min3(r[k], r[(k + 1) & 15], r[(k + 2) & 15]);
+            }
+            h2 hi9[16], lo9[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                hi9[k] = max3(hi3[k], hi3[(k + 3) & 15], hi3[(k + 6) & 15]);
+                lo9[k] = min3(lo3[k], lo3[(k + 3) & 15], lo3[(k + 6) & 15]);
+            }
+            h2 A = min3(hi9[0], hi9[1], hi9[2]), B = max3(lo9[0], lo9[1], lo9[2]);
+#pragma unroll
+            for (int k = 3; k < 16; k += 2) {
+                A = k + 1 < 16 ? min3(A, hi9[k], hi9[k + 1]) : __builtin_elementwise_minimum(A, hi9[k]);
+                B = k + 1 < 16 ? max3(B, lo9[k], lo9[k + 1]) : __builtin_elementwise_maximum(B, lo9[k]);
+            }
+            const i16x2 v = __builtin_bit_cast(i16x2, vv), ia = __builtin_bit_cast(i16x2, A),
+                        ib = __builtin_bit_cast(i16x2, B);
+            const i16x2 sc = __builtin_elementwise_max(v - ia, ib - v);
+            const bool c0 = (j0 < na) & (sc.x > t), c1 = (j1 < na) & (sc.y > t);
+            if (c0) T.sc[off0] = (uint8_t)sc.x;
+            if (c1) T.sc[off1] = (uint8_t)sc.y;
+            nc = wave_append(c0, (uint16_t)off0, T.lb, nc, lane);
+            nc = wave_append(c1, (uint16_t)off1, T.lb, nc, lane);
+        }
+        wave_sync();
+        nb = nc;
+        row = row_end;
+        // corners to emit now: all of them at the end, else those above row - 1
+        int k = nb;
+        if (row < dh) {
+            const int lim = (3 + row - 1) * P;  // tile offsets of region rows < row - 1
+            k = 0;
+            for (int base = 0; base < nb; base += 64) {
+                const int j = base + lane;
+                k += __popcll(__ballot(j < nb && (int)T.lb[j] < lim));
+            }
+        }
+        total = nms_emit<P>(T, k, ox, t, lane, iniX, iniY, out, cap, err, 0, total);
+        if (row >= dh) break;
+        if (k > 0) {  // the rest to the front (each chunk read before its writes; later chunks read above)
+            for (int base = 0; base < nb - k; base += 64) {
+                const int j = base + lane;
+                const uint16_t e = j < nb - k ? T.lb[k + j] : 0;
+                if (j < nb - k) T.lb[j] = e;
+            }
+            nb -= k;
+            drop = true;
+            wave_sync();
+        }
+    }
+    *pending = nb;
+    *dropped = drop;
+    return total;
+}
+
 // Diagnostic build (-DFAST_STAMPS): every 16th cell's wave adds its phase
 // durations (s_memtime cycles) to g_fast_stamps[phase] and its survivor /
 // corner counts to [8] / [9]; [15] counts the sampled waves
@@ -286,14 +397,14 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     const int R = g.win_rows;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: metadata in SGPRs
-    const size_t per_wave = (((size_t)2 * P * R + 2 * ((size_t)g.det_max + 1) + 15) & ~(size_t)15);
+    const size_t per_wave = (((size_t)2 * P * R + 2 * ((size_t)fast_list_len(P, R, g.det_max) + 1) + 15) & ~(size_t)15);
     uint8_t* ws = smem + wave * per_wave;
     CellTiles T;
     T.win = ws;
     T.sc = ws + P * R;
     T.la = reinterpret_cast<uint16_t*>(ws + 2 * P * R);
     T.lb = T.la;
-    T.dump = g.det_max;  // in-place: iteration `base` writes below base + 64 after reading la[base .. base + 64)
+    T.dump = fast_list_len(P, R, g.det_max);  // in-place: iteration `base` writes below base + 64 after reading la[base .. base + 64)
     uint8_t* s_win = ws;
 
     // one cell per wave; waves of a block take consecutive cells of a frame;
@@ -389,7 +500,24 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     int st_nb = 0, st_retry = 0;
     unsigned long long cst[2] = {0, 0};
 #endif
+#if ORBGPU_FAST_BANDS
     if (dw > 0 && dh > 0) {
+        int nb = 0;
+        bool dropped = false;
+        total = fast_cell_banded<P>(T, dw, dh, ox, g.ini_th, lane, iniX, iniY, out, L.cell_cap, err, &nb, &dropped);
+        if (total == 0) {  // ORBextractor.cpp:821-825: retry the cell at minThFAST
+            if (!dropped)
+                for (int j = lane; j < nb; j += 64) T.sc[T.lb[j]] = 0;
+            else
+                for (int idx = lane; idx < P * R / 4; idx += 64) reinterpret_cast<uint32_t*>(T.sc)[idx] = 0u;
+            wave_sync();
+            total = fast_cell_banded<P>(T, dw, dh, ox, g.min_th, lane, iniX, iniY, out, L.cell_cap, err, &nb, &dropped);
+        }
+    }
+    if (false) {
+#else
+    if (dw > 0 && dh > 0) {
+#endif
 #ifdef FAST_STAMPS
         int nb = fast_corners<P>(T, dw, dh, ox, g.ini_th, lane, stamp_on ? cst : nullptr);
 #else
@@ -449,7 +577,7 @@ hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size
     const int items = g.total_cells * batch;
     if (row0 >= (1u << 24)) return hipErrorInvalidValue;  // row offsets by 24-bit multiplies
     const size_t per_wave =
-        (((size_t)2 * g.win_pitch * g.win_rows + 2 * ((size_t)g.det_max + 1) + 15) & ~(size_t)15);
+        (((size_t)2 * g.win_pitch * g.win_rows + 2 * ((size_t)fast_list_len(g.win_pitch, g.win_rows, g.det_max) + 1) + 15) & ~(size_t)15);
     dim3 grid((items + kCellWaves - 1) / kCellWaves);
     const size_t lds = per_wave * kCellWaves;
 #define ORBGPU_FAST_CASE(PP)                                                                                        \
