@@ -142,6 +142,8 @@ def parse(argv=None):
     ap.add_argument("--part-stage", default="pyramid", choices=["pyramid", "fast_cells", "octree"])
     ap.add_argument("--match-priority", type=int, default=0, choices=[0, -1],
                     help="matcher stream priority (0: default, below the extraction streams; -1: high)")
+    ap.add_argument("--other-delivery", type=int, default=1, choices=[0, 1],
+                    help="N > 1: also run the stream with the other --deliver mode (a second leg in the line)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     ap.add_argument("--cpu-dry-run", default=None, metavar="ENGINE.py",
                     help="tests only: gloo on the CPU with ENGINE.py standing in for orbgpu")
@@ -257,10 +259,10 @@ def gather_delivery_stats(rep, world, device=None):
     """per-rank delivery numbers -> rank 0: the bytes every rank moved per
     step and the owner waits, max over ranks (no-op at N = 1)"""
     import torch.distributed as dist
-    keys = ["bytes_per_step", "recv_bytes_per_step", "owner_wait_ms_per_step", "delivery_latency_ms"]
+    keys = ["bytes_per_step", "recv_bytes_per_step", "owner_wait_ms_per_step", "delivery_latency_ms", "ms_per_step"]
     if not (dist.is_available() and dist.is_initialized()) or world == 1:
-        return {**rep, "per_rank": [{k: rep[k] for k in keys}]}
-    t = torch.tensor([float(rep[k]) for k in keys], dtype=torch.float64, device=device)
+        return {**rep, "per_rank": [{k: rep[k] for k in keys if k in rep}]}
+    t = torch.tensor([float(rep.get(k, 0.0)) for k in keys], dtype=torch.float64, device=device)
     allt = [torch.zeros_like(t) for _ in range(world)]
     dist.all_gather(allt, t)
     per = [{k: (int(v) if "bytes" in k else round(float(v), 4)) for k, v in zip(keys, x.tolist())} for x in allt]
@@ -301,11 +303,56 @@ class _Dumper:
 # mono stream: extract + SearchForInitialization(t-1, t)
 # ---------------------------------------------------------------------------
 
+NSETS = 3  # output sets in rotation (StreamBench)
+
+
+class OutSet:
+    """One step's outputs in HBM: keypoints (B, cap, 7) f32 (orbgpu_keypoint),
+    descriptors (B, cap, 32) u8, counts (B,), SearchForInitialization's m12
+    (B, cap) / nmatch (B,), the F1 count of each pair (B,: the delivery trims
+    m12 rows to it), and `inb`, the boundary frame received from another rank
+    (kps (cap, 7), desc (cap, 32), count (1,)).  `prev` names the frame
+    before the set's batch (pair 0's F1), read in place wherever it lives."""
+
+    def __init__(self, B, cap, dev):
+        z = torch.zeros
+        self.kps = z((B, cap, 7), dtype=torch.float32, device=dev)
+        self.desc = z((B, cap, 32), dtype=torch.uint8, device=dev)
+        self.counts = z(B, dtype=torch.int32, device=dev)
+        self.m12 = z((B, cap), dtype=torch.int32, device=dev)
+        self.nmatch = z(B, dtype=torch.int32, device=dev)
+        self.c1 = z(B, dtype=torch.int32, device=dev)
+        self.inb = (z((cap, 7), dtype=torch.float32, device=dev), z((cap, 32), dtype=torch.uint8, device=dev),
+                    z(1, dtype=torch.int32, device=dev))
+        self.prev = None   # (kps, desc, count) of the frame before this set's batch
+        self.pidx = None   # pool index of the step the set holds
+        self.ev_ext = None  # end of the step's extraction (and boundary exchange)
+        self.dslot = 0      # delivery ring slot of the set's last step
+
+    def last(self):
+        """the set's last frame, in place"""
+        B = self.counts.shape[0]
+        return self.kps[B - 1], self.desc[B - 1], self.counts[B - 1:B]
+
+
 class StreamBench:
-    """Extract + SearchForInitialization over one sharded frame stream."""
+    """Extract + SearchForInitialization over one sharded frame stream.
+
+    Output sets rotate over NSETS = 3 steps.  Step k extracts into set k % 3;
+    its match (pairs (F_{t-1}, F_t) over the batch, src/Tracking.cpp:768-769)
+    runs on the matcher stream one step behind, and pair 0's F1 -- the frame
+    before the batch -- is read in place: at N = 1 the previous step's last
+    frame in set (k-1) % 3, at N > 1 the boundary frame received straight into
+    the set's `inb` buffers (rank r > 0: rank r-1's last frame of the same
+    step; rank 0: rank N-1's last frame of the previous step).  So nothing is
+    copied on the extraction stream.  Step k writes set k % 3, which the
+    matches of steps k-3 (as F2) and k-2 (its last frame as pair 0's F1) read:
+    it waits for the last match issued before it, step k-2's (matches run in
+    order on one stream) -- the same distance as with two sets and the copy.
+    """
 
     def __init__(self, og, D: Dev, W, H, NF, B, rank, world, stream, dump=None, deliver="host", feed="hbm",
-                 parts=1, part_stage="pyramid"):
+                 parts=1, part_stage="pyramid", dump_tag=""):
         import shard
         import synth
         self.og, self.D = og, D
@@ -342,47 +389,40 @@ class StreamBench:
             self.inbuf = [torch.empty_like(self.pool[0], device=dev) for _ in range(2)]
             self.h2d = D.stream()
             self.ev_h2d = [D.event() for _ in range(2)]
+            self.ev_in_read = [None, None]  # the extraction that last read each input buffer
             self.h2d_time = []  # (start, end) timing events per copy in the timed region
             self.h2d_issued = -1
-        # slot 0 = the frame before this chunk (boundary exchange), slots 1..B this chunk
-        self.sets = []
-        for _ in range(2):  # two output sets: the gather of step k overlaps step k+1
-            kps_all = torch.zeros((B + 1, cap, 7), dtype=torch.float32, device=dev)
-            desc_all = torch.zeros((B + 1, cap, 32), dtype=torch.uint8, device=dev)
-            counts_all = torch.zeros(B + 1, dtype=torch.int32, device=dev)
-            m12 = torch.zeros((B, cap), dtype=torch.int32, device=dev)
-            nmatch = torch.zeros(B, dtype=torch.int32, device=dev)
-            self.sets.append((kps_all, desc_all, counts_all, m12, nmatch))
-        k0, d0, c0 = self.sets[0][0], self.sets[0][1], self.sets[0][2]
-        self.bx = shard.BoundaryExchange(rank, world, [k0[0], d0[0], c0[0:1]])
+        self.sets = [OutSet(B, cap, dev) for _ in range(NSETS)]
+        z = torch.zeros
+        self.empty = (z((cap, 7), dtype=torch.float32, device=dev), z((cap, 32), dtype=torch.uint8, device=dev),
+                      z(1, dtype=torch.int32, device=dev))  # before the stream's first frame: no keypoints
+        self.bx = shard.BoundaryExchange(rank, world)
         # every step's keypoints, descriptors (trimmed to the counts) and m12 rows (trimmed to the
         # matched-against frames' counts) plus counts / match counts go to the Tracking owner
         # (shard.Delivery: "host" over each rank's own PCIe link, or "gpu0" to rank 0's HBM)
-        group = None
+        groups = None
         if deliver == "gpu0" and world > 1:
             import torch.distributed as dist
-            group = dist.new_group(list(range(world)))
+            groups = (dist.new_group(list(range(world))), dist.new_group(list(range(world))))
+        S0 = self.sets[0]
         self.delivery = shard.Delivery(deliver, rank, world, dev,
                                        [shard.RowSpec("kps", 0), shard.RowSpec("desc", 0), shard.RowSpec("m12", 1)],
-                                       B, cap, [k0[1:], d0[1:], self.sets[0][3]], 3 * B, group=group,
+                                       B, cap, [S0.kps, S0.desc, S0.m12], 3 * B, groups=groups,
                                        packer=getattr(og, "pack_rows", None))
         self.flags = og.MATCH_CHECK_ORI
         self.step_no = 0
         # dumps (tests): host mode -- every rank its own delivered frames; gpu0 -- rank 0 all ranks'
         per_rank = deliver == "host" and world > 1
-        self.dump = (_Dumper(dump, f"mono_{W}x{H}" + (f"_rank{rank}" if per_rank else ""))
+        self.dump = (_Dumper(dump, f"mono_{W}x{H}{dump_tag}" + (f"_rank{rank}" if per_rank else ""))
                      if (dump and (rank == 0 or per_rank)) else None)
         self.dump_all = bool(dump)
         # The matcher runs on its own stream, one step behind: SearchForInitialization of
         # step k-1 (a few hundred latency-bound blocks) starts once step k's FAST pass is
         # done (--match-after; never during the pyramid pass, which wants every CU).
-        # The two output sets keep step k+1's extraction off the buffers step k-1's match
-        # reads (it waits for that match).  run() flushes the last match inside the timed
-        # region.
+        # run() flushes the last match inside the timed region.
         self.mstream = D.stream(priority=MATCH_PRIORITY[0])
         self.ev_pyr = D.event()
-        # the previous step's match starts once the first sub-batch has passed
-        # MATCH_AFTER: the next step's extraction into its output set waits for it
+        # the previous step's match starts once the first sub-batch has passed MATCH_AFTER
         self.exs[0].set_stage_event(MATCH_AFTER[0], self.ev_pyr)
         self.ev_part = [None] * parts
         self.ev_part_done = [D.event() for _ in range(parts)]
@@ -393,69 +433,84 @@ class StreamBench:
                 else:
                     self.ev_part[i] = D.event()
                     e.set_stage_event(part_stage, self.ev_part[i])
-        self.ev_ext = [D.event() for _ in range(2)]
-        self.ev_match = [None, None]
+        for S in self.sets:
+            S.ev_ext = D.event()
+        self.ev_match_last = None  # the last match issued (with its delivery packing)
         self.pending = None  # (set index, timing events) of the step whose match is not issued yet
         self.timing_h2d = False
-        self.dslot = [0, 0]  # delivery ring slot of each output set's last step
 
     def _match(self, si, after, ev=None):
-        kps_all, desc_all, counts_all, m12, nmatch = self.sets[si]
+        S = self.sets[si]
         ms = self.mstream
         ms.wait_event(after)
-        if after is not self.ev_ext[si]:
-            ms.wait_event(self.ev_ext[si])  # its step's tail (on its own stream when the step is split)
+        if after is not S.ev_ext:
+            ms.wait_event(S.ev_ext)  # its step's tail (on its own stream when the step is split)
+        pk, pd, pn = S.prev
+        with self.D.use_stream(ms):  # F1 count of each pair (the delivery's m12 rows), beside the matcher
+            torch.cat([pn, S.counts[:-1]], out=S.c1)
         if ev is not None:
             ev[0].record(ms)
-        self.og.search_for_initialization_batch(self.W, self.H, kps_all[:-1], desc_all[:-1], counts_all[:-1],
-                                                kps_all[1:], desc_all[1:], counts_all[1:], m12, nmatch,
-                                                flags=self.flags, stream=ms, max_level0=self.ex.level_capacity[0])
+        self.og.search_for_initialization_stream(self.W, self.H, S.kps, S.desc, S.counts, pk, pd, pn, S.m12,
+                                                 S.nmatch, flags=self.flags, stream=ms,
+                                                 max_level0=self.ex.level_capacity[0])
         if ev is not None:
             ev[1].record(ms)
         # delivery (packing on this stream, after the match; the copies or sends on the
-        # delivery thread's own stream)
-        self.dslot[si] = self.delivery.start([kps_all[1:], desc_all[1:], m12], [counts_all[1:], counts_all[:-1], nmatch],
-                                             [counts_all[1:], counts_all[:-1]], stream=None if not self.D.cuda else ms)
+        # delivery's own stream)
+        S.dslot = self.delivery.start([S.kps, S.desc, S.m12], [S.counts, S.c1, S.nmatch], [S.counts, S.c1],
+                                      stream=None if not self.D.cuda else ms)
         em = self.D.event()
-        em.record(ms)  # the next extraction into this set waits for the match and the packing
-        self.ev_match[si] = em
+        em.record(ms)  # the extraction two steps later (into the set this match read) waits for it
+        self.ev_match_last = em
 
     def step(self, ev=None):
         B, st = self.B, self.stream
-        si = self.step_no % 2
-        kps_all, desc_all, counts_all, m12, nmatch = self.sets[si]
-        if self.ev_match[si] is not None:  # ... and the match that read it (step k-2)
-            st.wait_event(self.ev_match[si])
-        pidx = self.step_no % POOL_STEPS
-        frames = self.pool[pidx] if self.feed == "hbm" else self._fed(self.step_no)
+        k = self.step_no
+        si = k % NSETS
+        S = self.sets[si]
+        if self.ev_match_last is not None:  # step k-2's match: it read S's last frame (k-3's read all of S)
+            st.wait_event(self.ev_match_last)
+        pidx = k % POOL_STEPS
+        S.pidx = pidx
+        frames = self.pool[pidx] if self.feed == "hbm" else self._fed(k)
         n = self.part_n
         for i, (e, ps) in enumerate(zip(self.exs, self.pstreams)):
-            if i > 0 and self.ev_match[si] is not None:
-                ps.wait_event(self.ev_match[si])
-            if self.parts > 1 and (i > 0 or self.step_no > 0):
+            if i > 0 and self.ev_match_last is not None:
+                ps.wait_event(self.ev_match_last)
+            if self.parts > 1 and (i > 0 or k > 0):
                 ps.wait_event(self.ev_part[i - 1])  # i = 0: the previous step's last sub-batch
             lo, hi = i * n, (i + 1) * n
-            e.extract_batch(frames[lo:hi], kps_all[1 + lo:1 + hi], desc_all[1 + lo:1 + hi], counts_all[1 + lo:1 + hi],
+            e.extract_batch(frames[lo:hi], S.kps[lo:hi], S.desc[lo:hi], S.counts[lo:hi],
                             stream=ps, row_step=self.pitch, frame_step=self.pitch * self.H)
         ts = self.tstream
         if self.parts > 1:  # the rest of the step (exchange, match) after every sub-batch
             for i in range(self.parts):
                 self.ev_part_done[i].record(self.pstreams[i])
                 ts.wait_event(self.ev_part_done[i])
-        with self.D.use_stream(ts):
-            prev = self.bx.exchange([kps_all[B], desc_all[B], counts_all[B:B + 1]])
-            kps_all[0].copy_(prev[0])
-            desc_all[0].copy_(prev[1])
-            counts_all[0:1].copy_(prev[2])
-        self.ev_ext[si].record(ts)
+        if self.feed == "host":  # the input buffer is free again after this extraction
+            e_in = self.D.event()
+            e_in.record(ts)
+            self.ev_in_read[k % 2] = e_in
+        # the frame before this batch (pair 0's F1), read in place
+        if self.world == 1:
+            S.prev = self.sets[(k - 1) % NSETS].last() if k > 0 else self.empty
+        else:
+            with self.D.use_stream(ts):
+                if self.rank == 0:  # rank N-1's last frame: the one before our NEXT chunk
+                    self.bx.exchange(S.last(), self.sets[(k + 1) % NSETS].inb)
+                    S.prev = S.inb if k > 0 else self.empty
+                else:
+                    self.bx.exchange(S.last(), S.inb)
+                    S.prev = S.inb
+        S.ev_ext.record(ts)
         if self.pending is not None:  # step k-1's match, after step k's FAST pass
-            self._match(*self.pending[:1], self.ev_pyr, self.pending[1])
+            self._match(self.pending[0], self.ev_pyr, self.pending[1])
         self.pending = (si, ev)
         if self.dump_all:  # test mode: finish the step and record what was delivered
             self.flush()
             self.delivery.finish()
             if self.dump is not None:
-                self._record(si, pidx)
+                self._record(si)
         self.step_no += 1
 
     def _issue_h2d(self, k):
@@ -463,8 +518,8 @@ class StreamBench:
         the copy stream, after the extraction that last read that buffer (step k-2)"""
         b = k % 2
         h = self.h2d
-        if self.ev_ext[b] is not None and k >= 2:
-            h.wait_event(self.ev_ext[b])
+        if self.ev_in_read[b] is not None:
+            h.wait_event(self.ev_in_read[b])
         timed = self.timing_h2d
         if timed:
             e0, e1 = self.D.event(True), self.D.event(True)
@@ -486,9 +541,10 @@ class StreamBench:
         self._issue_h2d(k + 1)  # prefetch: overlaps this step's extraction
         return self.inbuf[k % 2]
 
-    def _record(self, si, pidx):
+    def _record(self, si):
         import shard
         B, cap = self.B, self.cap
+        S = self.sets[si]
 
         def unpack(rows, small):
             sm = small.cpu().numpy()
@@ -498,24 +554,22 @@ class StreamBench:
             m = shard.unpack_rows(rows[2].cpu().numpy(), cp, cap)
             return k, d, c, m, nm
 
-        ds = self.dslot[si]
         if self.deliver == "host":
-            rows, small = self.delivery.host_rows(ds)
+            rows, small = self.delivery.host_rows(S.dslot)
             chunks = [(self.rank, unpack([r for r, _ in rows], small))]
         else:
-            own = [t.cpu().numpy() for t in (self.sets[si][0][1:], self.sets[si][1][1:], self.sets[si][2][1:],
-                                             self.sets[si][3], self.sets[si][4])]
+            own = [t.cpu().numpy() for t in (S.kps, S.desc, S.counts, S.m12, S.nmatch)]
             chunks = [(0, own)] + [(r + 1, unpack(rows, small))
-                                   for r, (rows, small) in enumerate(self.delivery.received(ds))]
+                                   for r, (rows, small) in enumerate(self.delivery.received(S.dslot))]
         for r, (k, d, c, m, n) in chunks:
-            for b, f in enumerate(shard.chunk_frames(pidx, r, self.world, self.B)):
+            for b, f in enumerate(shard.chunk_frames(S.pidx, r, self.world, self.B)):
                 self.dump.add(f, count=int(c[b]), kps=k[b], desc=d[b], nmatch=int(n[b]), m12=m[b])
 
     def flush(self):
         """issue the match of the last extracted step"""
         if self.pending is not None:
             si, ev = self.pending
-            self._match(si, self.ev_ext[si], ev)
+            self._match(si, self.sets[si].ev_ext, ev)
             self.pending = None
 
     def run(self, warmup, steps):
@@ -530,7 +584,8 @@ class StreamBench:
             e.sync(ps)
             e.profile(True)
             e.stage_times(reset=True)
-        self.timing_h2d, self.h2d_time = True, []
+        if self.feed == "host":
+            self.timing_h2d, self.h2d_time = True, []
         evs = [(D.event(True), D.event(True)) for _ in range(steps)]
         _barrier(self.world)
         D.synchronize()
@@ -543,6 +598,7 @@ class StreamBench:
         elapsed = time.perf_counter() - t0
         self.timing_h2d = False
         delivery = self.delivery.report(steps)
+        delivery["ms_per_step"] = round(elapsed / steps * 1e3, 4)  # this rank's own step time
         elapsed, frames_total = aggregate(elapsed, self.B * steps, device=self.dev)
         delivery = gather_delivery_stats(delivery, self.world, self.dev)
         _barrier(self.world)
@@ -562,7 +618,7 @@ class StreamBench:
         pyr_bytes = pyramid_bytes_per_frame(self.ex.level_sizes) * self.B
         pyr_s = per_step["pyramid"] / 1e3
         achieved = pyr_bytes / pyr_s / 1e9 if pyr_s > 0 else None
-        last = self.sets[(self.step_no - 1) % 2]
+        last = self.sets[(self.step_no - 1) % NSETS]
         h2d = None
         if self.feed == "host" and self.h2d_time:
             ms = [a.elapsed_time(b) for a, b in self.h2d_time]  # the copies issued inside the timed region
@@ -570,25 +626,54 @@ class StreamBench:
             h2d = {"bytes_per_step": int(nbytes), "ms_per_copy_mean": round(float(np.mean(ms)), 4),
                    "gb_per_s": round(nbytes / (float(np.mean(ms)) / 1e3) / 1e9, 2), "copies": len(ms)}
         return {"fps": frames_total / elapsed, "elapsed": elapsed, "per_step": per_step, "pyr_bytes": pyr_bytes,
-                "achieved": achieved, "keypoints": float(last[2][1:].float().mean().item()),
-                "matches": float(last[4].float().mean().item()), "frames_total": frames_total,
+                "achieved": achieved, "keypoints": float(last.counts.float().mean().item()),
+                "matches": float(last.nmatch.float().mean().item()), "frames_total": frames_total,
                 "delivery": delivery, "h2d": h2d}
 
     def close(self):
         self.delivery.close()
 
-    def parity_frame0(self):
-        """pool frame 0 of this rank against the oracle (untimed)."""
+    def parity_timed(self):
+        """The timed path's own outputs against the oracle (untimed, after run()):
+        in the last step's output set -- written by the very extractor, batch size and
+        kernel configuration that was timed -- frames 0, 1, B-2 and B-1 (keypoints as
+        bits, all 7 fields, and descriptors) and the matches of pairs (0, 1) and
+        (B-2, B-1); at N = 1 also pair 0, whose F1 is the previous step's last frame
+        read in place from the previous output set (src/Tracking.cpp:768-769)."""
         import orbgpu
         import orbref
         try:
-            ex1 = orbgpu.Extractor(nfeatures=self.NF, width=self.W, height=self.H, max_batch=1)
-            f0 = self.pool[0][0, :, :self.W].cpu().numpy()
-            kg, dg = ex1.extract(f0)
-            kr, dr = orbref.Extractor(nfeatures=self.NF).extract(f0)
-            return bool(len(kg) == len(kr) and kg.tobytes() == kr.tobytes() and np.array_equal(dg, dr))
+            self.D.synchronize()
+            B, W = self.B, self.W
+            S = self.sets[(self.step_no - 1) % NSETS]
+            ex = orbref.Extractor(nfeatures=self.NF)
+
+            def ref(pidx, b):
+                return ex.extract(np.ascontiguousarray(self.pool[pidx][b, :, :W].cpu().numpy()))
+
+            def same(kd, k, d):
+                return len(kd[0]) == len(k) and kd[0].tobytes() == k.tobytes() and np.array_equal(kd[1], d)
+
+            idx = sorted({0, 1, B - 2, B - 1} & set(range(B)))
+            R = {b: ref(S.pidx, b) for b in idx}
+            kps, desc, cnt = S.kps.cpu().numpy(), S.desc.cpu().numpy(), S.counts.cpu().numpy()
+            m12, nm = S.m12.cpu().numpy(), S.nmatch.cpu().numpy()
+            got = {b: (orbgpu.keypoints_from_raw(kps[b, :cnt[b]]), desc[b, :cnt[b]]) for b in idx}
+            ok_frames = {b: bool(same(got[b], *R[b])) for b in idx}
+
+            def pair_ok(b, f1):
+                n_r, m_r, _ = orbref.search_for_initialization(f1[0], f1[1], R[b][0], R[b][1], W, self.H)
+                return bool(int(nm[b]) == n_r and np.array_equal(m12[b, :len(f1[0])], m_r))
+
+            ok_pairs = {f"({b - 1},{b})": pair_ok(b, R[b - 1]) for b in idx if b - 1 in R}
+            if self.world == 1 and self.step_no >= 2 and 0 in R:
+                P = self.sets[(self.step_no - 2) % NSETS]
+                ok_pairs["(prev step's B-1, 0)"] = pair_ok(0, ref(P.pidx, B - 1))
+            ok = all(ok_frames.values()) and all(ok_pairs.values())
+            return {"ok": ok, "frames": ok_frames, "pairs": ok_pairs,
+                    "from": f"output set of the last timed step (batch {B}, the timed extractor and matcher)"}
         except Exception as e:  # report, never hide
-            return f"error: {e}"
+            return {"ok": False, "error": str(e)}
 
 
 # ---------------------------------------------------------------------------
@@ -1232,7 +1317,6 @@ def main_mono(args, og, D, rank, world, stream):
     MATCH_PRIORITY[0] = args.match_priority
     sb = StreamBench(og, D, W, H, NF, B, rank, world, stream, dump=args.dump, deliver=args.deliver, feed=args.feed,
                      parts=args.parts, part_stage=args.part_stage)
-    parity = sb.parity_frame0() if (rank == 0 and D.cuda) else None
     extras = {}
     if not args.no_extras and D.cuda:
         # sustained leg, before the headline: the same stream for SUSTAINED_STEPS steps
@@ -1248,9 +1332,26 @@ def main_mono(args, og, D, rank, world, stream):
                                "stages_ms_per_step": {k: round(v, 4) for k, v in rs["per_step"].items()},
                                "order": "run before the headline's warm-up and timed steps"}
     r = sb.run(args.warmup, args.steps)
+    # the timed configuration's own outputs against the oracle (rank 0, untimed)
+    parity = sb.parity_timed() if rank == 0 else None
     sb.close()
     del sb
     D.empty_cache()
+    if world > 1 and args.other_delivery:
+        # the other delivery mode on the same stream (N > 1): per rank ms_per_step and the
+        # owner's waits for both modes in one line
+        other = "host" if args.deliver == "gpu0" else "gpu0"
+        ob = StreamBench(og, D, W, H, NF, B, rank, world, stream, dump=args.dump, deliver=other, feed=args.feed,
+                         dump_tag="_other")
+        orr = ob.run(args.warmup, args.steps)
+        ob.close()
+        del ob
+        D.empty_cache()
+        extras["delivery_other_mode"] = {
+            "mode": other, "frames_per_s": round(orr["fps"], 1),
+            "ms_per_step": round(orr["elapsed"] / args.steps * 1e3, 3), "delivery": orr["delivery"],
+            "stages_ms_per_step_rank0": {k: round(v, 4) for k, v in orr["per_step"].items()},
+            "note": "the same stream and steps with the other delivery mode, run after the headline"}
     if not args.no_extras and D.cuda and args.feed == "hbm":
         # host-fed leg: the same stream with every step's frames copied from pinned host
         # memory (double-buffered H2D on a copy stream, overlapped with extraction) and the
@@ -1306,7 +1407,8 @@ def main_mono(args, og, D, rank, world, stream):
         "stages_ms_per_step": {k: round(v, 4) for k, v in r["per_step"].items()},
         "keypoints_per_frame": round(r["keypoints"], 1),
         "matches_per_pair": round(r["matches"], 1),
-        "parity_frame0_vs_oracle": parity,
+        "parity_vs_oracle": parity,
+        "parity_frame0_vs_oracle": None if parity is None else bool(parity.get("ok")),
         "world_size_checked": world,
         "input": "frames resident in HBM" if args.feed == "hbm" else
                  "frames copied from pinned host memory every step (double-buffered H2D)",

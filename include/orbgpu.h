@@ -196,6 +196,24 @@ int orbgpu_search_for_initialization_batch_device_bounded(
     float* d_prev_xy, int window, float nnratio, int flags, int max_level0,
     int* d_matches12, int* d_nmatches, void* stream);
 
+/* The stream form, as Tracking runs the matcher on consecutive frames
+ * (mInitialFrame, mCurrentFrame) = (F_{t-1}, F_t) (src/Tracking.cpp:768-769,
+ * ORBmatcher.cpp:474-590): `batch` frames of one extraction at d_kps + b*stride
+ * (descriptors d_desc + b*stride*32, counts d_n[b]); pair b matches F1 =
+ * frame b-1 against F2 = frame b, and pair 0 matches the frame BEFORE the
+ * batch -- d_prev_kps / d_prev_desc / *d_prev_n, read in place (e.g. the last
+ * frame of the previous batch's output set, or a boundary frame received from
+ * another GPU), so no copy of it into the batch is needed.  m12 row b
+ * (d_matches12 + b*stride, F1's keypoints) and d_nmatches[b] as above;
+ * d_prev_xy (nullable) is vbPrevMatched per pair at + b*stride*2.  The prev
+ * frame's capacity must not exceed `stride`.  max_level0 as in _bounded. */
+int orbgpu_search_for_initialization_stream_device(
+    int batch, orbgpu_grid_bounds bounds,
+    const orbgpu_keypoint* d_kps, const uint8_t* d_desc, const int* d_n, size_t stride,
+    const orbgpu_keypoint* d_prev_kps, const uint8_t* d_prev_desc, const int* d_prev_n,
+    float* d_prev_xy, int window, float nnratio, int flags, int max_level0,
+    int* d_matches12, int* d_nmatches, void* stream);
+
 /* Host-pointer convenience form for one pair; returns nmatches in *n.
  * ORBGPU_ERR_CAPACITY (and *nmatches = 0) for more than 2048 level-0
  * keypoints in either frame. */

@@ -102,7 +102,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     const uint8_t* __restrict__ desc1, const int* __restrict__ n1p, size_t stride1,
     const orbgpu_keypoint* __restrict__ kps2, const uint8_t* __restrict__ desc2, const int* __restrict__ n2p,
     size_t stride2, float* __restrict__ prev_xy, int window, float nnratio, int flags, int* __restrict__ matches12,
-    int* __restrict__ nmatches_out) {
+    int* __restrict__ nmatches_out, MatchFirstF1 first) {
     constexpr int kCells = kGC * kGR;
     __shared__ float s_x[kMaxK0], s_y[kMaxK0];
     __shared__ int s_cell[kMaxK0];           // grid cell ix*48+iy, or -1 when not in the grid
@@ -128,11 +128,17 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.x;
     MSTAMP(0);
-    const orbgpu_keypoint* K1 = kps1 + (size_t)b * stride1;
+    // F1 of pair b: frame b of the F1 arrays, or in the stream form (first.kps
+    // set) frame b - 1 of them and, for pair 0, the frame before the batch
+    // read in place (Tracking's (F_{t-1}, F_t), src/Tracking.cpp:768-769)
+    const bool chained = first.kps != nullptr;
+    const bool own_first = chained && b == 0;
+    const size_t f1 = chained ? (size_t)(b > 0 ? b - 1 : 0) : (size_t)b;
+    const orbgpu_keypoint* K1 = own_first ? first.kps : kps1 + f1 * stride1;
     const orbgpu_keypoint* K2 = kps2 + (size_t)b * stride2;
-    const uint8_t* D1 = desc1 + (size_t)b * stride1 * 32;
+    const uint8_t* D1 = own_first ? first.desc : desc1 + f1 * stride1 * 32;
     const uint8_t* D2 = desc2 + (size_t)b * stride2 * 32;
-    const int n1 = n1p[b], n2 = n2p[b];
+    const int n1 = own_first ? *first.n : n1p[f1], n2 = n2p[b];
     int* M12 = matches12 + (size_t)b * stride1;
     float* prev = prev_xy ? prev_xy + (size_t)b * stride1 * 2 : nullptr;
     // a larger variant only takes the pairs the previous one handed over
@@ -540,10 +546,10 @@ hipError_t launch_variant(int batch, int more, float minX, float maxX, float min
                           const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,
                           const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2, size_t stride2,
                           float* prev_xy, int window, float nnratio, int flags, int* matches12, int* nmatches,
-                          hipStream_t stream) {
+                          hipStream_t stream, MatchFirstF1 first) {
     hipLaunchKernelGGL((match_init_kernel<kMaxK0, kThreads>), dim3(batch), dim3(kThreads), 0, stream, more, minX, maxX,
                        minY, maxY, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags,
-                       matches12, nmatches);
+                       matches12, nmatches, first);
     return hipGetLastError();
 }
 
@@ -565,7 +571,8 @@ hipError_t launch_match_init(int batch, float minX, float maxX, float minY, floa
                              const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,
                              const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2, size_t stride2,
                              float* prev_xy, int window, float nnratio, int flags,
-                             int* matches12, int* nmatches, hipStream_t stream, size_t level0_bound) {
+                             int* matches12, int* nmatches, hipStream_t stream, size_t level0_bound,
+                             MatchFirstF1 first) {
     // small variant for every pair, then the larger ones for the pairs handed
     // over (a no-op block per other pair, which still waits for a CU with the
     // variant's LDS free); a larger variant is launched only when a frame's
@@ -579,7 +586,7 @@ hipError_t launch_match_init(int batch, float minX, float maxX, float minY, floa
     hipError_t e;
 #define ORBGPU_MATCH_ARGS                                                                                         \
     minX, maxX, minY, maxY, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags, \
-        matches12, nmatches, stream
+        matches12, nmatches, stream, first
     if (threads == 256)
         e = launch_variant<kMaxK0Small, 256>(batch, more_large, ORBGPU_MATCH_ARGS);
     else if (threads == 512)

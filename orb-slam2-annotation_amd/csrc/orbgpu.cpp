@@ -522,7 +522,9 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
                                   e->d_gkeys + (size_t)f0 * g.cand_frame, e->d_gknode + (size_t)f0 * g.cand_frame,
                                   e->d_oct_out + (size_t)f0 * g.slots_frame, e->d_oct_count + (size_t)f0 * kOcStride,
                                   e->d_err, e->oct_groups, 2, c == 0 ? e->d_trace : nullptr, s));
-            if (c == 0 && evs) ORB_HIP(hipEventRecord(evs[3], s));  // (the octree stage: the first chunk's)
+            // the octree stage ends with the last chunk's octree (the describes of the
+            // earlier chunks overlap it on the aux stream; describe = the rest)
+            if (c == nch - 1 && evs) ORB_HIP(hipEventRecord(evs[3], s));
             ORB_HIP(hipEventRecord(e->od_ev[c], s));
             ORB_HIP(hipStreamWaitEvent(a, e->od_ev[c], 0));
             ORB_HIP(launch_describe(g, nb, imgs, row_step, frame_step, e->d_pyr, e->d_oct_out, e->d_oct_count, kps,
@@ -915,6 +917,25 @@ int orbgpu_search_for_initialization_batch_device_bounded(
         return fail(ORBGPU_ERR_ARG, "invalid argument");
     ORB_HIP(launch_match_init(batch, bd.min_x, bd.max_x, bd.min_y, bd.max_y, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy,
                               window, nnratio, flags, matches12, nmatches, (hipStream_t)stream, (size_t)max_level0));
+    return ORBGPU_OK;
+}
+
+int orbgpu_search_for_initialization_stream_device(int batch, orbgpu_grid_bounds bd, const orbgpu_keypoint* kps,
+                                                   const uint8_t* desc, const int* n, size_t stride,
+                                                   const orbgpu_keypoint* prev_kps, const uint8_t* prev_desc,
+                                                   const int* prev_n, float* prev_xy, int window, float nnratio,
+                                                   int flags, int max_level0, int* matches12, int* nmatches,
+                                                   void* stream) {
+    if (batch <= 0 || !kps || !desc || !n || !prev_kps || !prev_desc || !prev_n || !matches12 || !nmatches ||
+        stride == 0 || !(bd.max_x > bd.min_x) || !(bd.max_y > bd.min_y) || max_level0 < 0)
+        return fail(ORBGPU_ERR_ARG, "invalid argument");
+    MatchFirstF1 first;
+    first.kps = prev_kps;
+    first.desc = prev_desc;
+    first.n = prev_n;
+    ORB_HIP(launch_match_init(batch, bd.min_x, bd.max_x, bd.min_y, bd.max_y, kps, desc, n, stride, kps, desc, n,
+                              stride, prev_xy, window, nnratio, flags, matches12, nmatches, (hipStream_t)stream,
+                              (size_t)max_level0, first));
     return ORBGPU_OK;
 }
 

@@ -60,11 +60,21 @@ hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
                            hipStream_t stream, int* err_word = nullptr, int* err_copy = nullptr, int f0 = 0);
 
+// The stream form of SearchForInitialization (orbgpu_search_for_initialization_stream_device):
+// with kps set, pair b takes F1 = frame b - 1 of the F1 arrays and pair 0 this frame
+// (the one before the batch, read in place); kps == nullptr: pair b takes F1 frame b.
+struct MatchFirstF1 {
+    const orbgpu_keypoint* kps = nullptr;
+    const uint8_t* desc = nullptr;
+    const int* n = nullptr;
+};
+
 hipError_t launch_match_init(int batch, float minX, float maxX, float minY, float maxY,
                              const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,
                              const orbgpu_keypoint* kps2, const uint8_t* desc2, const int* n2, size_t stride2,
                              float* prev_xy, int window, float nnratio, int flags,
-                             int* matches12, int* nmatches, hipStream_t stream, size_t level0_bound = 0);
+                             int* matches12, int* nmatches, hipStream_t stream, size_t level0_bound = 0,
+                             MatchFirstF1 first = MatchFirstF1());
 
 hipError_t launch_hamming_pairs(const uint8_t* a, const uint8_t* b, int n, int* dist, hipStream_t stream);
 hipError_t launch_pack_rows(int batch, int cap, int ntensors, const ::orbgpu_pack_desc* d, hipStream_t stream);

@@ -25,9 +25,11 @@ __global__ __launch_bounds__(kPackThreads) void pack_rows_kernel(orbgpu_pack_des
     const orbgpu_pack_desc& D = t == 0 ? d0 : t == 1 ? d1 : t == 2 ? d2 : d3;
     const int b = blockIdx.x;
     __shared__ int s_part[kPackThreads / 64];
-    // offset of frame b: the counts of frames 0 .. b-1 (B <= a few thousand)
+    // offset of frame b: the counts of frames 0 .. b-1 (B <= a few thousand), each
+    // clamped to [0, cap] exactly as a frame's own row count below, so an
+    // out-of-range count (an error sentinel) can leave neither gaps nor overlaps
     int part = 0;
-    for (int j = threadIdx.x; j < b; j += kPackThreads) part += D.counts[j];
+    for (int j = threadIdx.x; j < b; j += kPackThreads) part += min(max(D.counts[j], 0), cap);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
     if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = part;

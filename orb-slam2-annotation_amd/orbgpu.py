@@ -114,6 +114,8 @@ def lib() -> ctypes.CDLL:
             i, GridBounds, vp, vp, vp, sz, vp, vp, vp, sz, vp, i, f, i, vp, vp, vp]
         L.orbgpu_search_for_initialization_batch_device_bounded.argtypes = [
             i, GridBounds, vp, vp, vp, sz, vp, vp, vp, sz, vp, i, f, i, i, vp, vp, vp]
+        L.orbgpu_search_for_initialization_stream_device.argtypes = [
+            i, GridBounds, vp, vp, vp, sz, vp, vp, vp, vp, i, f, i, i, vp, vp, vp]
         L.orbgpu_debug_level_candidates.argtypes = [vp, i, i, vp, i]
         L.orbgpu_debug_level_blur.argtypes = [vp, i, i, vp, sz]
         L.orbgpu_debug_level_octree.argtypes = [vp, i, i, vp, i]
@@ -392,6 +394,23 @@ def search_for_initialization_batch(img_w, img_h, kps1, desc1, n1, kps2, desc2, 
         B, bd, _ptr(kps1), _ptr(desc1), _ptr(n1), desc1.shape[1], _ptr(kps2), _ptr(desc2), _ptr(n2),
         desc2.shape[1], _ptr(prev_xy) if prev_xy is not None else None, window, nnratio, flags, max_level0,
         _ptr(matches12), _ptr(nmatches), _stream_ptr(stream)), "orbgpu_search_for_initialization_batch_device_bounded")
+
+
+def search_for_initialization_stream(img_w, img_h, kps, desc, n, prev_kps, prev_desc, prev_n, matches12, nmatches,
+                                     prev_xy=None, window=100, nnratio=0.9, flags=MATCH_CHECK_ORI, stream=None,
+                                     bounds=None, max_level0=0):
+    """Stream form over the B frames of one extraction (Tracking's (F_{t-1},
+    F_t), Tracking.cpp:768-769): pair b matches frame b-1 against frame b, pair
+    0 the frame (prev_kps (cap, 7), prev_desc (cap, 32), prev_n (1,)) before
+    the batch, read in place.  matches12 (B, cap): row b has F1's keypoints."""
+    B, cap = n.shape[0], desc.shape[1]
+    assert kps.shape[0] >= B and desc.shape[0] >= B and prev_desc.shape[0] <= cap
+    assert matches12.shape[0] >= B and matches12.shape[1] == cap and nmatches.shape[0] >= B
+    bd = bounds if bounds is not None else bounds_for(img_w, img_h)
+    _check(lib().orbgpu_search_for_initialization_stream_device(
+        B, bd, _ptr(kps), _ptr(desc), _ptr(n), cap, _ptr(prev_kps), _ptr(prev_desc), _ptr(prev_n),
+        _ptr(prev_xy) if prev_xy is not None else None, window, nnratio, flags, max_level0,
+        _ptr(matches12), _ptr(nmatches), _stream_ptr(stream)), "orbgpu_search_for_initialization_stream_device")
 
 
 def hamming_pairs(a, b, out, stream=None):

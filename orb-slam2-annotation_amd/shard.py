@@ -47,35 +47,29 @@ def _pg_active(world: int) -> bool:
 
 
 class BoundaryExchange:
-    """The chunk-boundary frame: ``exchange(last)`` sends this rank's last
-    frame to rank+1 and returns the frame that precedes this rank's first
-    frame (for rank 0: the one received at the previous step; an empty
-    frame -- count 0 -- before the first step)."""
+    """The chunk-boundary frame between ranks, with no copies.
+    ``exchange(last, into)`` sends this rank's last frame (`last`: its
+    keypoints, descriptors and count, read in place from the output set) to
+    rank+1 and receives rank-1's last frame of the same step straight into
+    `into`, the buffers the matcher then reads as the frame before this
+    rank's first frame.  For rank 0 that frame is rank N-1's last frame of
+    the step, i.e. the one before rank 0's NEXT chunk: the caller passes the
+    next step's buffers as `into`.  At N = 1 there is nothing to exchange
+    (the previous step's last frame is read in place from its output set)
+    and ``exchange`` returns False."""
 
-    def __init__(self, rank: int, world: int, templates):
-        """templates: tensors shaped like one frame's outputs (e.g. kps
-        (cap, 7) f32, desc (cap, 32) u8, count (1,) i32)."""
+    def __init__(self, rank: int, world: int):
         self.rank, self.world = rank, world
-        self.incoming = [torch.zeros_like(t) for t in templates]
-        self.stored = [torch.zeros_like(t) for t in templates]  # rank 0: previous step's boundary
 
-    def exchange(self, last):
+    def exchange(self, last, into) -> bool:
         if not _pg_active(self.world):
-            prev = [s.clone() for s in self.stored]
-            for s, t in zip(self.stored, last):
-                s.copy_(t)
-            return prev
+            return False
         nxt, prv = (self.rank + 1) % self.world, (self.rank - 1) % self.world
-        ops = [dist.P2POp(dist.isend, t.contiguous(), nxt) for t in last]
-        ops += [dist.P2POp(dist.irecv, t, prv) for t in self.incoming]
+        ops = [dist.P2POp(dist.isend, t, nxt) for t in last]
+        ops += [dist.P2POp(dist.irecv, t, prv) for t in into]
         for w in dist.batch_isend_irecv(ops):
             w.wait()
-        if self.rank > 0:
-            return self.incoming
-        prev = [s.clone() for s in self.stored]
-        for s, t in zip(self.stored, self.incoming):
-            s.copy_(t)
-        return prev
+        return True
 
 
 class OwnerGather:
@@ -129,9 +123,15 @@ class RowSpec:
         self.name, self.which = name, which
 
 
-def pack_offsets(counts):
-    """exclusive prefix sums of the per-frame counts (device, int64)"""
-    c = counts.to(torch.int64)
+def clamped_counts(counts, cap):
+    """per-frame row counts as the pack kernel uses them: clamped to [0, cap]
+    (csrc/pack.hip), so an out-of-range count cannot shift other frames' rows"""
+    return counts.to(torch.int64).clamp(0, cap)
+
+
+def pack_offsets(counts, cap):
+    """exclusive prefix sums of the clamped per-frame counts (device, int64)"""
+    c = clamped_counts(counts, cap)
     return torch.cumsum(c, 0) - c
 
 
@@ -141,9 +141,9 @@ def pack_rows(rows, counts, out):
     for the rows past each frame's count.  Returns nothing: the number of
     used rows is sum(counts), which the caller learns from the counts copy."""
     B, cap = rows.shape[0], rows.shape[1]
-    off = pack_offsets(counts)
+    off = pack_offsets(counts, cap)
     j = torch.arange(cap, device=rows.device, dtype=torch.int64)
-    idx = torch.where(j[None, :] < counts.to(torch.int64)[:, None], off[:, None] + j[None, :],
+    idx = torch.where(j[None, :] < clamped_counts(counts, cap)[:, None], off[:, None] + j[None, :],
                       torch.full((), B * cap, device=rows.device, dtype=torch.int64))
     out.index_copy_(0, idx.reshape(-1), rows.reshape(B * cap, *rows.shape[2:]))
 
@@ -163,15 +163,20 @@ class Delivery:
     how many rows are used and queues exactly those --
       host: copies into pinned host memory, over this rank's own PCIe link;
       gpu0: rank r > 0 sends them to rank 0, which receives each rank's
-            rows after its counts (a process group of its own, so the order
-            of these operations is the same on every rank).
+            rows after its counts.  Point-to-point operations between a pair
+            of ranks are matched in the order they are posted, and the two
+            sides post them at different times (rank r posts step k's rows as
+            soon as its own counts are out, rank 0 only after step k's counts
+            have arrived, possibly after posting step k+1's counts receive), so
+            the counts and the rows travel on TWO process groups: on each, both
+            sides post one kind of operation in step order.
     Slots form a ring of `sets` (the producer's device buffers are free
     again once the packing on `stream` is done); a slot is waited for only
     when it is reused or at ``finish()``: that wait is the owner's wait.
     """
 
-    def __init__(self, mode, rank, world, device, specs, B, cap, row_templates, small_len, sets=4, group=None,
-                 packer=None):
+    def __init__(self, mode, rank, world, device, specs, B, cap, row_templates, small_len, sets=4, groups=None,
+                 packer=None, on_delivered=None):
         import collections
         import time
         assert mode in ("host", "gpu0"), mode
@@ -182,8 +187,15 @@ class Delivery:
         self.specs, self.B, self.cap, self.sets = specs, B, cap, sets
         self.cuda = device.type == "cuda"
         self._time = time.perf_counter
-        self.group = group
+        # gpu0 with N > 1: (counts group, rows group) -- see the class comment
         self.remote = mode == "gpu0" and _pg_active(world)
+        if self.remote:
+            assert groups is not None and len(groups) == 2 and groups[0] is not groups[1], \
+                "gpu0 delivery needs two process groups (counts, rows)"
+        self.g_small, self.g_rows = groups if groups is not None else (None, None)
+        # on_delivered(slot, seq): called when the seq-th start()'s rows are delivered, before
+        # the slot can be reused (tests read rank 0's received rows there)
+        self.on_delivered = on_delivered
         self.owner_local = mode == "gpu0" and rank == 0  # the owner's own rows stay where they are
         pin = self.cuda
         self.packed = [[torch.zeros((B * cap + 1, *t.shape[2:]), dtype=t.dtype, device=device) for t in row_templates]
@@ -229,7 +241,7 @@ class Delivery:
 
     def _used_rows(self, small_host):
         B = self.B
-        c = small_host[:2 * B].to(torch.int64)
+        c = clamped_counts(small_host[:2 * B], self.cap)
         tot = [int(c[:B].sum()), int(c[B:2 * B].sum())]
         return [tot[w] for w in self.counts_which]
 
@@ -258,16 +270,16 @@ class Delivery:
             if self.cuda:
                 ready = torch.cuda.Event()
                 ready.record(stream if stream is not None else torch.cuda.current_stream(self.device))
-        st = {"slot": si, "t0": self._time(), "works": [], "ev": None, "bytes": 0}
+        st = {"slot": si, "seq": self.next - 1, "t0": self._time(), "works": [], "ev": None, "bytes": 0}
         with self._ctx():
             if self.cuda:
                 self.copy_stream.wait_event(ready)
             if self.remote and self.rank > 0:
-                st["works"] = [dist.isend(self.small[si], 0, group=self.group)]
+                st["works"] = [dist.isend(self.small[si], 0, group=self.g_small)]
                 self.small_host[si].copy_(self.small[si], non_blocking=self.cuda)
                 st["stage"] = "sent_small"
             elif self.remote:  # rank 0: every other rank's small tensor for this step
-                st["works"] = [dist.irecv(self.recv_small[si][r - 1], r, group=self.group)
+                st["works"] = [dist.irecv(self.recv_small[si][r - 1], r, group=self.g_small)
                                for r in range(1, self.world)]
                 st["stage"] = "recv_small"
             else:
@@ -315,7 +327,7 @@ class Delivery:
                     nbytes = self.small[si].numel() * 4
                     for dev, n in zip(self.packed[si], used):
                         if n:
-                            works.append(dist.isend(dev[:n], 0, group=self.group))
+                            works.append(dist.isend(dev[:n], 0, group=self.g_rows))
                         nbytes += n * dev[0].numel() * dev.element_size()
                     st["bytes"], st["stage"], st["works"], st["ev"] = nbytes, "rows", works, None
                 elif stage == "recv_small":  # rank 0: the counts received -> to the host
@@ -328,7 +340,7 @@ class Delivery:
                         smh = self.recv_small_host[si][r - 1]
                         for buf, n in zip(self.recv_rows[si][r - 1], self._used_rows(smh)):
                             if n:
-                                works.append(dist.irecv(buf[:n], r, group=self.group))
+                                works.append(dist.irecv(buf[:n], r, group=self.g_rows))
                             rb += n * buf[0].numel() * buf.element_size()
                     st["recv_bytes"] = rb
                     st["stage"], st["works"], st["ev"] = "rows", works, None
@@ -341,6 +353,8 @@ class Delivery:
                     if "copy" in st and self.cuda:
                         self.stats["copy_ms"] += st["copy"][0].elapsed_time(st["copy"][1])
                     self.state[si] = None
+                    if self.on_delivered is not None:
+                        self.on_delivered(si, st["seq"])
                     if block:
                         return
 
@@ -397,7 +411,7 @@ def unpack_rows(packed, counts, cap):
     zero rows past each count"""
     import numpy as np
     packed = np.asarray(packed)
-    counts = np.asarray(counts, np.int64)
+    counts = np.clip(np.asarray(counts, np.int64), 0, cap)
     out = np.zeros((len(counts), cap, *packed.shape[1:]), packed.dtype)
     off = 0
     for b, c in enumerate(counts):

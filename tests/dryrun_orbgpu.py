@@ -89,6 +89,18 @@ def search_for_initialization_batch(img_w, img_h, kps1, desc1, n1, kps2, desc2, 
         nmatches[b] = nm
 
 
+def search_for_initialization_stream(img_w, img_h, kps, desc, n, prev_kps, prev_desc, prev_n, matches12, nmatches,
+                                     prev_xy=None, window=100, nnratio=0.9, flags=MATCH_CHECK_ORI, stream=None,
+                                     bounds=None, max_level0=0):
+    """the stream form: pair b matches frame b-1 (pair 0: the prev frame) against frame b"""
+    B = n.shape[0]
+    k1 = torch.cat([prev_kps[None], kps[:B - 1]])
+    d1 = torch.cat([prev_desc[None], desc[:B - 1]])
+    n1 = torch.cat([prev_n.reshape(1), n[:B - 1]])
+    search_for_initialization_batch(img_w, img_h, k1, d1, n1, kps, desc, n, matches12, nmatches, prev_xy, window,
+                                    nnratio, flags, stream, bounds, max_level0)
+
+
 def stereo_matches_batch(ex: Extractor, images, npairs, kps, desc, counts, bf, min_z, uright, depth, stream=None,
                          row_step=None, frame_step=None):
     """Frame::ComputeStereoMatches of pairs (2p, 2p+1): the oracle stereo

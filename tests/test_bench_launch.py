@@ -58,33 +58,12 @@ def _merge_rank_dumps(tmp_path, name, world):
     return {k: np.concatenate([p[k] for p in parts])[order] for k in parts[0].files}
 
 
-@pytest.mark.parametrize("deliver,parts", [("host", 1), ("gpu0", 1), ("gpu0", 2)])
-def test_mono_stream_two_ranks_equals_single_process(tmp_path, deliver, parts):
-    """both delivery modes (shard.Delivery): host -- each rank's trimmed
-    outputs in its own host memory (merged here from the per-rank dumps);
-    gpu0 -- counts first, then the used rows, received by rank 0; and the
-    step as two sub-batches (--parts 2: each on its own extractor and stream)"""
+def _oracle_stream(world, B, steps):
+    """the whole stream in one process: per global frame (keypoints,
+    descriptors, nmatches, m12 over the previous frame's keypoints)"""
     import orbref
     import shard
     import synth
-    import torch
-    world, B, steps = 2, 2 * parts, 2
-    line = _run_bench(tmp_path, "--config", "mono640", "--batch", str(B), "--steps", str(steps), "--warmup", "0",
-                      "--deliver", deliver, "--parts", str(parts))
-    assert line["n_gpus"] == 2 and line["world_size_checked"] == 2
-    assert line["config"]["frames_per_gpu_per_step"] == B
-    assert line["config"]["sub_batches"]["parts"] == parts
-    dl = line["delivery"]
-    assert dl["mode"] == deliver and len(dl["per_rank"]) == 2
-    if deliver == "host":  # every rank moves its own outputs
-        assert all(p["bytes_per_step"] > 0 for p in dl["per_rank"])
-        got = _merge_rank_dumps(tmp_path, "mono_640x480", world)
-    else:  # rank 1 sends, rank 0 receives exactly that
-        assert dl["per_rank"][1]["bytes_per_step"] > 0 and dl["per_rank"][0]["bytes_per_step"] == 0
-        assert dl["per_rank"][0]["recv_bytes_per_step"] + 4 * 3 * B == dl["per_rank"][1]["bytes_per_step"]
-        got = np.load(tmp_path / "mono_640x480.npz")
-    n_frames = world * B * steps
-    assert list(got["units"]) == list(range(n_frames))
     frames = {}
     for s in range(steps):
         for r in range(world):
@@ -93,24 +72,70 @@ def test_mono_stream_two_ranks_equals_single_process(tmp_path, deliver, parts):
             for b, f in enumerate(ids):
                 frames[f] = imgs[b].numpy()
     ex = orbref.Extractor(1000)
-    prev = None
-    cross = 0
-    for f in range(n_frames):
+    out, prev = [], None
+    for f in range(world * B * steps):
         k, d = ex.extract(frames[f])
+        if prev is None:
+            nm, m12 = 0, np.full(0, -1, np.int32)
+        else:
+            nm, m12, _ = orbref.search_for_initialization(prev[0], prev[1], k, d, 640, 480)
+        out.append((k, d, nm, m12))
+        prev = (k, d)
+    return out
+
+
+def _check_stream(got, ref, B):
+    assert list(got["units"]) == list(range(len(ref)))
+    cross = 0
+    for f, (k, d, nm, m12) in enumerate(ref):
         n = len(k)
         assert got["count"][f] == n, f
         assert got["kps"][f][:n].tobytes() == k.tobytes(), f
         assert np.array_equal(got["desc"][f][:n], d), f
-        if prev is None:
-            nm, m12 = 0, np.full(n, -1, np.int32)
-        else:
-            nm, m12, _ = orbref.search_for_initialization(prev[0], prev[1], k, d, 640, 480)
         assert got["nmatch"][f] == nm, f
-        if prev is not None:
-            assert np.array_equal(got["m12"][f][:len(prev[0])], m12), f
+        assert np.array_equal(got["m12"][f][:len(m12)], m12), f
         cross += f % B == 0 and f > 0 and nm > 0
-        prev = (k, d)
-    assert cross == n_frames // B - 1  # every chunk's first frame matched against another rank's / step's last
+    assert cross == len(ref) // B - 1  # every chunk's first frame matched against another rank's / step's last
+
+
+def _load_dump(tmp_path, deliver, world, tag=""):
+    if deliver == "host":  # every rank's own delivered frames
+        return _merge_rank_dumps(tmp_path, f"mono_640x480{tag}", world)
+    return np.load(tmp_path / f"mono_640x480{tag}.npz")  # what rank 0 received
+
+
+@pytest.mark.parametrize("deliver,parts", [("host", 1), ("gpu0", 1), ("gpu0", 2)])
+def test_mono_stream_two_ranks_equals_single_process(tmp_path, deliver, parts):
+    """both delivery modes (shard.Delivery): host -- each rank's trimmed
+    outputs in its own host memory (merged here from the per-rank dumps);
+    gpu0 -- counts first, then the used rows, received by rank 0; and the
+    step as two sub-batches (--parts 2: each on its own extractor and stream).
+    At N > 1 the line also runs the OTHER delivery mode over the same stream
+    (`delivery_other_mode`, per-rank ms_per_step and owner waits); its
+    delivered frames are checked the same way.  Pair 0 of every chunk reads
+    the frame before it in place (the previous step's set at N = 1, the
+    boundary frame received straight into the set at N > 1)."""
+    world, B, steps = 2, 2 * parts, 2
+    line = _run_bench(tmp_path, "--config", "mono640", "--batch", str(B), "--steps", str(steps), "--warmup", "0",
+                      "--deliver", deliver, "--parts", str(parts))
+    assert line["n_gpus"] == 2 and line["world_size_checked"] == 2
+    assert line["config"]["frames_per_gpu_per_step"] == B
+    assert line["config"]["sub_batches"]["parts"] == parts
+    assert line["parity_vs_oracle"]["ok"] is True and line["parity_frame0_vs_oracle"] is True
+    other = "gpu0" if deliver == "host" else "host"
+    ol = line["delivery_other_mode"]
+    assert ol["mode"] == other and ol["frames_per_s"] > 0
+    for dl, mode in ((line["delivery"], deliver), (ol["delivery"], other)):
+        assert dl["mode"] == mode and len(dl["per_rank"]) == 2
+        assert all(p["ms_per_step"] > 0 for p in dl["per_rank"])
+        if mode == "host":  # every rank moves its own outputs
+            assert all(p["bytes_per_step"] > 0 for p in dl["per_rank"])
+        else:  # rank 1 sends, rank 0 receives exactly that
+            assert dl["per_rank"][1]["bytes_per_step"] > 0 and dl["per_rank"][0]["bytes_per_step"] == 0
+            assert dl["per_rank"][0]["recv_bytes_per_step"] + 4 * 3 * B == dl["per_rank"][1]["bytes_per_step"]
+    ref = _oracle_stream(world, B, steps)
+    _check_stream(_load_dump(tmp_path, deliver, world), ref, B)
+    _check_stream(_load_dump(tmp_path, other, world, "_other"), ref, B)
 
 
 def test_stereo_pairs_two_ranks_equal_single_process(tmp_path):

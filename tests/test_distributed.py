@@ -93,8 +93,13 @@ def _shard_worker(rank, world, port, steps, B, q):
     import synth
     frames = synth.mono_stream(steps * world * B)
     ex = orbref.Extractor()
-    bx = shard.BoundaryExchange(rank, world, [torch.zeros((CAP, 7)), torch.zeros((CAP, 32), dtype=torch.uint8),
-                                              torch.zeros(1, dtype=torch.int32)])
+    bx = shard.BoundaryExchange(rank, world)
+
+    def frame_bufs():
+        return (torch.zeros((CAP, 7)), torch.zeros((CAP, 32), dtype=torch.uint8), torch.zeros(1, dtype=torch.int32))
+
+    inb = [frame_bufs() for _ in range(3)]  # per step (mod 3), as bench.py's output sets
+    empty = frame_bufs()
     tmpl = [torch.zeros((B, CAP, 7)), torch.zeros((B, CAP, 32), dtype=torch.uint8), torch.zeros(B, dtype=torch.int32),
             torch.zeros((B, CAP), dtype=torch.int32), torch.zeros(B, dtype=torch.int32)]
     gather = shard.OwnerGather(rank, world, tmpl)
@@ -105,7 +110,13 @@ def _shard_worker(rank, world, port, steps, B, q):
         for b, f in enumerate(ids):
             kps[b], desc[b], n = _extract(ex, frames[f])
             cnt[b] = n
-        prev = bx.exchange([kps[B - 1], desc[B - 1], cnt[B - 1:B]])
+        last = (kps[B - 1], desc[B - 1], cnt[B - 1:B])
+        if rank == 0:  # rank N-1's last frame precedes our next chunk
+            assert bx.exchange(last, inb[(s + 1) % 3])
+            prev = inb[s % 3] if s > 0 else empty
+        else:
+            assert bx.exchange(last, inb[s % 3])
+            prev = inb[s % 3]
         m12, nm = torch.full((B, CAP), -1, dtype=torch.int32), torch.zeros(B, dtype=torch.int32)
         for b in range(B):
             p = (prev[0], prev[1], int(prev[2][0])) if b == 0 else (kps[b - 1], desc[b - 1], int(cnt[b - 1]))
@@ -180,8 +191,30 @@ def test_pack_rows_torch_path_matches_unpack():
         for b in range(B):
             ref[b, counts[b]:] = 0
         assert np.array_equal(back, ref)
-        assert np.array_equal(shard.pack_offsets(torch.from_numpy(counts)).numpy(),
+        assert np.array_equal(shard.pack_offsets(torch.from_numpy(counts), cap).numpy(),
                               np.concatenate([[0], np.cumsum(counts)[:-1]]))
+
+
+def test_pack_rows_clamps_out_of_range_counts():
+    """A count below 0 or above cap (an error sentinel, or counts from a
+    foreign producer) is clamped to [0, cap] for the frame's own rows AND for
+    every later frame's offset (csrc/pack.hip does the same), so the other
+    frames' rows neither overlap nor leave gaps."""
+    import shard
+    B, cap = 5, 6
+    counts = np.array([3, -1, cap + 4, 2, 0], np.int32)
+    rows = torch.arange(B * cap, dtype=torch.int32).reshape(B, cap)
+    out = torch.full((B * cap + 1,), -7, dtype=torch.int32)
+    shard.pack_rows(rows, torch.from_numpy(counts), out)
+    cl = np.clip(counts, 0, cap)
+    n = int(cl.sum())
+    assert np.array_equal(shard.pack_offsets(torch.from_numpy(counts), cap).numpy(),
+                          np.concatenate([[0], np.cumsum(cl)[:-1]]))
+    exp = np.concatenate([rows[b, :cl[b]].numpy() for b in range(B)])
+    assert np.array_equal(out[:n].numpy(), exp)
+    back = shard.unpack_rows(out[:n].numpy(), counts, cap)
+    for b in range(B):
+        assert np.array_equal(back[b, :cl[b]], rows[b, :cl[b]].numpy())
 
 
 def test_delivery_host_mode_single_process_round_trip():
@@ -216,3 +249,96 @@ def test_delivery_host_mode_single_process_round_trip():
     rep = d.report(steps)
     assert rep["mode"] == "host" and rep["bytes_per_step"] > 0
     d.close()
+
+
+def _gpu0_pipeline_worker(rank, world, port, steps, sets, adversarial, q):
+    """shard.Delivery("gpu0") driven like bench.py's headline: start() every
+    step with no finish() in between, ranks staggered by different delays, so
+    rank r > 0 posts step k's rows while rank 0 may already have posted the
+    counts receive of step k+1.  `adversarial` forces that order: rank 0 posts
+    every step's counts receive first (a ring as long as the run), while the
+    other ranks start late and push each step's rows out before the next
+    step's counts."""
+    import time
+    _init(rank, world, port)
+    import shard
+    B, cap = 3, 8
+    groups = (dist.new_group(list(range(world))), dist.new_group(list(range(world))))
+    tmpl = [torch.zeros((B, cap, 7)), torch.zeros((B, cap, 32), dtype=torch.uint8),
+            torch.zeros((B, cap), dtype=torch.int32)]
+    got = {}
+
+    def on_delivered(si, seq):  # rank 0: what arrived for step `seq`, before the slot is reused
+        if rank == 0:
+            got[seq] = [(smh.numpy().copy(), [r.numpy().copy() for r in rows])
+                        for rows, smh in d.received(si)]
+
+    d = shard.Delivery("gpu0", rank, world, torch.device("cpu"),
+                       [shard.RowSpec("kps", 0), shard.RowSpec("desc", 0), shard.RowSpec("m12", 1)],
+                       B, cap, tmpl, 3 * B, sets=sets, groups=groups, on_delivered=on_delivered)
+    rng = np.random.default_rng(100 + rank)
+    delays = [0.002, 0.013, 0.005][rank % 3]
+    if adversarial and rank > 0:
+        time.sleep(0.3)
+    for s in range(steps):
+        g = np.random.default_rng(1000 * s + rank)  # the data rank r sends at step s (rank 0 can rebuild it)
+        c = torch.from_numpy(g.integers(0, cap + 1, B).astype(np.int32))
+        cp = torch.from_numpy(g.integers(0, cap + 1, B).astype(np.int32))
+        nm = torch.from_numpy(g.integers(0, 5, B).astype(np.int32))
+        k = torch.from_numpy(g.standard_normal((B, cap, 7)).astype(np.float32))
+        de = torch.from_numpy(g.integers(0, 255, (B, cap, 32)).astype(np.uint8))
+        m = torch.from_numpy(g.integers(-1, 50, (B, cap)).astype(np.int32))
+        d.start([k, de, m], [c, cp, nm], [c, cp])
+        if adversarial:
+            if rank > 0:
+                d.poll(block=True)  # this step's rows are posted before the next step's counts
+            continue
+        time.sleep(delays * (1 + rng.random()))
+        d.poll()
+    d.finish()
+    dist.barrier()
+    if rank == 0:
+        q.put(got)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,sets,adversarial", [(2, 2, False), (3, 3, False), (2, 9, True), (3, 9, True)])
+def test_delivery_gpu0_pipelined_ranks(world, sets, adversarial):
+    """with the counts and the rows of gpu0 delivery on one group,
+    the two sides could post their point-to-point operations in different
+    orders; on two groups every step's rows reach rank 0 intact while the
+    ring is kept full (no finish() per step) and the ranks run at different
+    speeds."""
+    import shard
+    steps, B, cap = 9, 3, 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu0_pipeline_worker, args=(r, world, port, steps, sets, adversarial, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert sorted(got) == list(range(steps))
+    for s in range(steps):
+        assert len(got[s]) == world - 1
+        for r in range(1, world):
+            g = np.random.default_rng(1000 * s + r)
+            c = g.integers(0, cap + 1, B).astype(np.int32)
+            cp = g.integers(0, cap + 1, B).astype(np.int32)
+            nm = g.integers(0, 5, B).astype(np.int32)
+            k = g.standard_normal((B, cap, 7)).astype(np.float32)
+            de = g.integers(0, 255, (B, cap, 32)).astype(np.uint8)
+            m = g.integers(-1, 50, (B, cap)).astype(np.int32)
+            small, rows = got[s][r - 1]
+            assert np.array_equal(small, np.concatenate([c, cp, nm])), (s, r)
+            for t, ref, cnt in zip(rows, (k, de, m), (c, c, cp)):
+                n = int(cnt.sum())
+                back = shard.unpack_rows(t[:n], cnt, cap)
+                exp = ref.copy()
+                for b in range(B):
+                    exp[b, cnt[b]:] = 0
+                assert np.array_equal(back, exp), (s, r)

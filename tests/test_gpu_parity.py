@@ -197,6 +197,59 @@ def test_batch_octree_describe_chunks_match_oracle(monkeypatch, chunks):
         _assert_same_kps(kg, dd[b, :cc[b]], kr, dr)
 
 
+def test_timed_headline_batch_512_vs_oracle():
+    """The configuration bench.py times, checked at full size:
+    two consecutive 512-frame batches of the bench's bounded 640x480 stream at
+    the bench's pitch, one extractor with max_batch 512 (the tick pyramid, the
+    octree's 256-thread level groups, the XCD-swizzled describe grid), then the
+    stream-form SearchForInitialization over the second batch (512 pairs:
+    256-thread pair blocks, the extractor's level-0 bound), whose pair 0 reads
+    the first batch's last frame in place (src/Tracking.cpp:768-769).  Frames
+    across the batch -- both ends, the 64-frame and 256-frame boundaries --
+    and the pairs between them equal the oracle bit for bit."""
+    og = _gpu()
+    B, W, H, NF = 512, 640, 480, 1000
+    pitch = (W + 15) // 16 * 16
+    ex = og.Extractor(nfeatures=NF, width=W, height=H, max_batch=B)
+    cap = ex.max_keypoints
+    sets = []
+    for t0 in (0, B):
+        imgs = synth.torch_stream(B, W, H, device="cuda", pitch=pitch, bounded=True, t0=t0)
+        kps = torch.zeros((B, cap, 7), dtype=torch.float32, device="cuda")
+        desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+        counts = torch.zeros(B, dtype=torch.int32, device="cuda")
+        ex.extract_batch(imgs, kps, desc, counts, row_step=pitch, frame_step=pitch * H)
+        ex.sync()
+        sets.append((imgs, kps, desc, counts))
+    (ia, ka, da, ca), (ib, kb, db, cb) = sets
+    m12 = torch.full((B, cap), -7, dtype=torch.int32, device="cuda")
+    nm = torch.zeros(B, dtype=torch.int32, device="cuda")
+    og.search_for_initialization_stream(W, H, kb, db, cb, ka[B - 1], da[B - 1], ca[B - 1:B], m12, nm,
+                                        max_level0=ex.level_capacity[0])
+    torch.cuda.synchronize()
+    assert int(cb.min()) > 900 and int(nm.min()) >= 0
+    ref = orbref.Extractor(nfeatures=NF)
+
+    def host(t, b):
+        return np.ascontiguousarray(t[b, :, :W].cpu().numpy())
+
+    kk, dd, cc = kb.cpu().numpy(), db.cpu().numpy(), cb.cpu().numpy()
+    mm, nn = m12.cpu().numpy(), nm.cpu().numpy()
+    R = {}
+    for b in (0, 1, 63, 64, 65, 255, 256, 257, 510, 511):
+        R[b] = ref.extract(host(ib, b))
+        _assert_same_kps(og.keypoints_from_raw(kk[b, :cc[b]]), dd[b, :cc[b]], *R[b])
+    R[-1] = ref.extract(host(ia, B - 1))
+    n = int(ca[B - 1])
+    _assert_same_kps(og.keypoints_from_raw(ka[B - 1, :n].cpu().numpy()), da[B - 1, :n].cpu().numpy(), *R[-1])
+    for b in (0, 1, 64, 65, 256, 257, 511):
+        f1 = R[b - 1]
+        n_r, m_r, _ = orbref.search_for_initialization(f1[0], f1[1], R[b][0], R[b][1], W, H)
+        assert int(nn[b]) == n_r, (b, int(nn[b]), n_r)
+        np.testing.assert_array_equal(mm[b, :len(f1[0])], m_r)
+        assert n_r > 50  # consecutive frames of the stream really match
+
+
 @pytest.mark.parametrize("check_ori,annotated", [(True, False), (False, False), (True, True)])
 def test_search_for_initialization(mono_frames, check_ori, annotated):
     og = _gpu()
