@@ -55,6 +55,7 @@ typedef struct orbgpu_extractor_info {
     int level_capacity[32];         /* output slots per level: no frame yields more keypoints
                                        at that level (DistributeOctTree keeps at most
                                        mnFeaturesPerLevel + 3, or 4 per initial node)   */
+    int device;                     /* HIP device ordinal the handle lives on           */
 } orbgpu_extractor_info;
 
 const char* orbgpu_last_error(void);
@@ -72,7 +73,27 @@ int orbgpu_device_arch(char* buf, int buflen);
 int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels,
                             int ini_th_fast, int min_th_fast, int width, int height,
                             int max_batch, orbgpu_extractor** out);
+/* The same on HIP device `device` (0 .. orbgpu_device_count()-1), whatever
+ * the calling thread's current device: every later call on the handle runs on
+ * that device (the reference runs one ORBextractor per camera thread,
+ * src/Frame.cpp:84-87, src/Tracking.cpp:141-149; this places each on a GPU of
+ * the host's choosing without the host linking HIP).  ORBGPU_ERR_ARG for an
+ * ordinal outside the visible devices. */
+int orbgpu_extractor_create_on_device(int device, int nfeatures, float scale_factor, int nlevels,
+                                      int ini_th_fast, int min_th_fast, int width, int height,
+                                      int max_batch, orbgpu_extractor** out);
 int orbgpu_extractor_destroy(orbgpu_extractor* ex);
+
+/* Device placement of the host-form calls (matchers, solvers, Initializer,
+ * vocabulary; include/orbgpu_*.h): they run on the calling thread's device,
+ * each (thread, device) with its own stream and staging.
+ * orbgpu_set_thread_device makes `device` that device for the calling thread
+ * (ORBGPU_ERR_ARG for an ordinal outside [0, count), ORBGPU_ERR_NO_DEVICE
+ * without devices or for a non-gfx950 one); orbgpu_get_thread_device returns
+ * it; orbgpu_device_count the visible devices (0 without any). */
+int orbgpu_device_count(int* n);
+int orbgpu_set_thread_device(int device);
+int orbgpu_get_thread_device(int* device);
 int orbgpu_extractor_get_info(const orbgpu_extractor* ex, orbgpu_extractor_info* info);
 
 /* GetScaleFactors / GetInverseScaleFactors / GetScaleSigmaSquares /

@@ -27,14 +27,16 @@
 #include <vector>
 
 #include "../orbgpu_init.h"
+#include "Device.h"
 
 namespace ORB_SLAM2 {
 
 class Initializer {
 public:
     template <class FrameT>
-    Initializer(const FrameT& ReferenceFrame, float sigma = 1.0, int iterations = 200)
-        : mSigma(sigma), mSigma2(sigma * sigma), mMaxIterations(iterations) {
+    // device (adapter-only, Device.h): the GPU Initialize() runs on (-1: the thread's)
+    Initializer(const FrameT& ReferenceFrame, float sigma = 1.0, int iterations = 200, int device = -1)
+        : device_(device), mSigma(sigma), mSigma2(sigma * sigma), mMaxIterations(iterations) {
         const cv::Mat& K = ReferenceFrame.mK;
         for (int r = 0; r < 3; ++r)
             for (int c = 0; c < 3; ++c) mK[3 * r + c] = K.template at<float>(r, c);
@@ -67,6 +69,7 @@ public:
         int model = 0;
         std::vector<float> p3d(3 * (size_t)(n1 > 0 ? n1 : 1));
         std::vector<unsigned char> tri(n1 > 0 ? n1 : 1);
+        orbslam2_amd::use_device(device_);
         const int rc = orbgpu_init_initialize(p1.data(), n1, p2.data(), n2, vMatches12.data(), mK, mSigma,
                                               mMaxIterations, &rec, &rh, &model, p3d.data(), tri.data());
         if (rc != ORBGPU_OK) throw std::runtime_error(std::string("orbgpu: ") + orbgpu_last_error());
@@ -93,6 +96,7 @@ public:
     int mModel = -1;
 
 private:
+    int device_ = -1;
     std::vector<cv::KeyPoint> mvKeys1;
     float mK[9];
     float mSigma, mSigma2;

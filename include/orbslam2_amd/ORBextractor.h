@@ -40,6 +40,7 @@
 #include <vector>
 
 #include "../orbgpu.h"
+#include "Device.h"
 
 #ifndef ORBGPU_HOST_PYRAMID
 #define ORBGPU_HOST_PYRAMID 0
@@ -106,9 +107,11 @@ public:
     // ORBextractor.cpp:412-434 -- the scale tables are set up here exactly as
     // the reference does (double chain stored as float) so the accessors work
     // before the first frame.
-    ORBextractor(int nfeatures_, float scaleFactor_, int nlevels_, int iniThFAST_, int minThFAST_)
+    // device (adapter-only, Device.h): the GPU the extractor's handle lives on (-1: the
+    // creating thread's current device when the first frame arrives)
+    ORBextractor(int nfeatures_, float scaleFactor_, int nlevels_, int iniThFAST_, int minThFAST_, int device = -1)
         : nfeatures(nfeatures_), scaleFactor(scaleFactor_), nlevels(nlevels_), iniThFAST(iniThFAST_),
-          minThFAST(minThFAST_) {
+          minThFAST(minThFAST_), device_(device) {
         mvScaleFactor.resize(nlevels);
         mvLevelSigma2.resize(nlevels);
         mvScaleFactor[0] = 1.0f;
@@ -171,6 +174,8 @@ public:
     // adapter-only
     void SetCopyPyramid(bool on) { copy_pyramid_ = on; }
     orbgpu_extractor* handle() { return ex_; }  // the last frame's pyramid lives here (HBM)
+    // the device the handle lives on (-1 before the first frame)
+    int device() const { return ex_ ? info_.device : device_; }
 
     HostPyramid mvImagePyramid;
 
@@ -193,9 +198,14 @@ private:
         if (ex_ && info_.width == w && info_.height == h) return;
         if (ex_) orbgpu_extractor_destroy(ex_);
         ex_ = nullptr;
-        check(orbgpu_extractor_create(nfeatures, (float)scaleFactor, nlevels, iniThFAST, minThFAST, w, h, 1, &ex_));
+        if (device_ >= 0)
+            check(orbgpu_extractor_create_on_device(device_, nfeatures, (float)scaleFactor, nlevels, iniThFAST,
+                                                    minThFAST, w, h, 1, &ex_));
+        else
+            check(orbgpu_extractor_create(nfeatures, (float)scaleFactor, nlevels, iniThFAST, minThFAST, w, h, 1, &ex_));
         check(orbgpu_extractor_get_info(ex_, &info_));
     }
+    int device_ = -1;
     orbgpu_extractor* ex_ = nullptr;
     orbgpu_extractor_info info_{};
     std::vector<orbgpu_keypoint> kp_buf_;

@@ -67,6 +67,7 @@
 #include "../orbgpu.h"
 #include "../orbgpu_bow.h"
 #include "../orbgpu_proj.h"
+#include "Device.h"
 
 namespace orbslam2_amd {
 
@@ -141,7 +142,9 @@ namespace ORB_SLAM2 {
 
 class ORBmatcher {
 public:
-    ORBmatcher(float nnratio = 0.6, bool checkOri = true) : mfNNratio(nnratio), mbCheckOrientation(checkOri) {}
+    // device (adapter-only, Device.h): the GPU the matcher's calls run on (-1: the thread's)
+    ORBmatcher(float nnratio = 0.6, bool checkOri = true, int device = -1)
+        : device_(device), mfNNratio(nnratio), mbCheckOrientation(checkOri) {}
 
     static const int TH_LOW = 50;
     static const int TH_HIGH = 100;
@@ -320,6 +323,7 @@ public:
         std::vector<int> match(F.N > 0 ? F.N : 1);
         int nm = 0;
         const orbgpu_bow_frame fa = a.frame(), fb = b.frame();
+        orbslam2_amd::use_device(device_);
         check(orbgpu_search_by_bow(ORBGPU_BOW_KF_F, &fa, &fb, mfNNratio, mbCheckOrientation ? 1 : 0, match.data(),
                                    &nm));
         vpMapPointMatches = std::vector<MapPointT*>(F.N, static_cast<MapPointT*>(nullptr));
@@ -347,6 +351,7 @@ public:
         std::vector<int> match(vp1.empty() ? 1 : vp1.size());
         int nm = 0;
         const orbgpu_bow_frame fa = a.frame(), fb = b.frame();
+        orbslam2_amd::use_device(device_);
         check(orbgpu_search_by_bow(ORBGPU_BOW_KF_KF, &fa, &fb, mfNNratio, mbCheckOrientation ? 1 : 0,
                                    match.data(), &nm));
         vpMatches12 = std::vector<MapPointT*>(vp1.size(), static_cast<MapPointT*>(nullptr));
@@ -378,6 +383,7 @@ public:
         const int flags = (mbCheckOrientation ? ORBGPU_MATCH_CHECK_ORI : 0) |
                           (mbAnnotatedHisto ? ORBGPU_MATCH_ANNOTATED_HISTO : 0);
         int nmatches = 0;
+        orbslam2_amd::use_device(device_);
         check(orbgpu_search_for_initialization(bd, k1.data(), d1.data(), (int)n1, k2.data(), d2.data(), (int)n2,
                                                prev.data(), windowSize, mfNNratio, flags, vnMatches12.data(),
                                                &nmatches));
@@ -433,6 +439,7 @@ public:
         P.only_stereo = bOnlyStereo ? 1 : 0;
         std::vector<int> m12(n1 > 0 ? n1 : 1);
         int nm = 0;
+        orbslam2_amd::use_device(device_);
         check(orbgpu_search_for_triangulation(&P, mbCheckOrientation ? 1 : 0, m12.data(), &nm));
         vMatchedPairs.clear();
         vMatchedPairs.reserve(nm);
@@ -567,6 +574,7 @@ public:
     bool mbAnnotatedHisto = false;
 
 protected:
+    int device_ = -1;
     float mfNNratio;
     bool mbCheckOrientation;
 
@@ -696,8 +704,9 @@ private:
         return c;
     }
 
-    static int run(const orbgpu_proj_call& c, std::vector<int>& match) {
+    int run(const orbgpu_proj_call& c, std::vector<int>& match) const {
         int nm = 0;
+        orbslam2_amd::use_device(device_);
         orbslam2_amd::detail::check(orbgpu_search_by_projection(&c, match.data(), &nm));
         return nm;
     }

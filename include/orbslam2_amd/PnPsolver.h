@@ -35,14 +35,16 @@
 #include <vector>
 
 #include "../orbgpu_ransac.h"
+#include "Device.h"
 
 namespace ORB_SLAM2 {
 
 class PnPsolver {
 public:
     template <class FrameT, class MapPointT>
-    PnPsolver(const FrameT& F, const std::vector<MapPointT*>& vpMapPointMatches)
-        : mnMatches((int)vpMapPointMatches.size()) {
+    // device (adapter-only, Device.h): the GPU iterate() runs on (-1: the thread's)
+    PnPsolver(const FrameT& F, const std::vector<MapPointT*>& vpMapPointMatches, int device = -1)
+        : device_(device), mnMatches((int)vpMapPointMatches.size()) {
         // PnPsolver.cpp:104-139: correspondences of the good MapPoints
         for (size_t i = 0; i < vpMapPointMatches.size(); ++i) {
             MapPointT* pMP = vpMapPointMatches[i];
@@ -122,6 +124,7 @@ public:
         std::vector<uint8_t> best = mvbBestInliers, refined(N > 0 ? N : 1, 0);
         if (best.empty()) best.assign(1, 0);
         orbgpu_pnp_result r;
+        orbslam2_amd::use_device(device_);
         check(orbgpu_pnp_ransac_batch(1, &p, N, mvP3Dw.data(), mvP2D.data(), mvMaxError.data(), n_hyp,
                                       samples.empty() ? nullptr : samples.data(), &r, best.data(), refined.data()));
         orbgpu_rand_set_state(&snap);  // consume exactly the iterations the reference ran
@@ -160,6 +163,7 @@ public:
     int Correspondences() const { return N; }
 
 private:
+    int device_ = -1;
     static void check(int rc) {
         if (rc != ORBGPU_OK) throw std::runtime_error(std::string("orbgpu: ") + orbgpu_last_error());
     }

@@ -35,15 +35,17 @@
 #include <vector>
 
 #include "../orbgpu_ransac.h"
+#include "Device.h"
 
 namespace ORB_SLAM2 {
 
 class Sim3Solver {
 public:
     template <class KeyFrameT, class MapPointT>
+    // device (adapter-only, Device.h): the GPU iterate() runs on (-1: the thread's)
     Sim3Solver(KeyFrameT* pKF1, KeyFrameT* pKF2, const std::vector<MapPointT*>& vpMatched12,
-               const bool bFixScale = true)
-        : mN1((int)vpMatched12.size()), mbFixScale(bFixScale) {
+               const bool bFixScale = true, int device = -1)
+        : device_(device), mN1((int)vpMatched12.size()), mbFixScale(bFixScale) {
         const std::vector<MapPointT*> vpKeyFrameMP1 = pKF1->GetMapPointMatches();
         const cv::Mat Rcw1 = pKF1->GetRotation(), tcw1 = pKF1->GetTranslation();
         const cv::Mat Rcw2 = pKF2->GetRotation(), tcw2 = pKF2->GetTranslation();
@@ -131,6 +133,7 @@ public:
         }
         std::vector<uint8_t> mask = mvbBestInliers;
         orbgpu_sim3_result r;
+        orbslam2_amd::use_device(device_);
         check(orbgpu_sim3_ransac_batch(1, &p, N, mvX3Dc1.data(), mvX3Dc2.data(), mvnMaxError1.data(),
                                        mvnMaxError2.data(), n_hyp, samples.empty() ? nullptr : samples.data(), &r,
                                        mask.data()));
@@ -171,6 +174,7 @@ public:
     int Correspondences() const { return N; }
 
 private:
+    int device_ = -1;
     static void check(int rc) {
         if (rc != ORBGPU_OK) throw std::runtime_error(std::string("orbgpu: ") + orbgpu_last_error());
     }

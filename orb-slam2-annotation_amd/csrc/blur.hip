@@ -96,14 +96,14 @@ __device__ __noinline__ void blur_strip_edge(const uint8_t* __restrict__ src, ui
 // Walking down the strip it keeps the last 7 row-pass results (as floats)
 // in registers -- the window rotates statically (the row loop is unrolled
 // by 7) -- so every input row is read once per strip (+6 halo rows).
-__global__ __launch_bounds__(256) void blur_levels_kernel(Geom g, int items_frame, int items_total,
+__global__ __launch_bounds__(256) void blur_levels_kernel(Geom g, int tile0, int items_frame, int items_total,
                                                           const uint8_t* __restrict__ img0, size_t row0,
                                                           size_t frame0, const uint8_t* __restrict__ pyr,
                                                           uint8_t* __restrict__ blur) {
     const int item = blockIdx.x * 256 + threadIdx.x;
     if (item >= items_total) return;
     const int f = item / items_frame;
-    const int it = item - f * items_frame;
+    const int it = tile0 + item - f * items_frame;  // tile of the frame (levels from tile0's)
     int l = 0;
     while (l + 1 < g.nlevels && it >= g.lv[l + 1].blur_tile_base) ++l;
     const LevelGeom& L = g.lv[l];
@@ -124,9 +124,12 @@ __global__ __launch_bounds__(256) void blur_levels_kernel(Geom g, int items_fram
 }  // namespace
 
 hipError_t launch_blur_levels(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
-                              const uint8_t* pyr, uint8_t* blur, hipStream_t stream) {
-    const int items = g.blur_tiles_frame * batch;
-    hipLaunchKernelGGL(blur_levels_kernel, dim3((items + 255) / 256), dim3(256), 0, stream, g, g.blur_tiles_frame,
+                              const uint8_t* pyr, uint8_t* blur, hipStream_t stream, int level_from) {
+    if (level_from >= g.nlevels) return hipSuccess;
+    const int tile0 = level_from > 0 ? g.lv[level_from].blur_tile_base : 0;
+    const int per_frame = g.blur_tiles_frame - tile0;
+    const int items = per_frame * batch;
+    hipLaunchKernelGGL(blur_levels_kernel, dim3((items + 255) / 256), dim3(256), 0, stream, g, tile0, per_frame,
                        items, img0, row0, frame0, pyr, blur);
     return hipGetLastError();
 }

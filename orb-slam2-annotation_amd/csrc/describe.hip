@@ -236,7 +236,7 @@ __device__ bool key_ref(const Geom& g, int f, int slot, int lane, const uint32_t
 // returns (m10, m01), wave-uniform.
 __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, DescLds& S, uint8_t* blur_out,
                                const uint8_t* __restrict__ img0, size_t row0, size_t frame0,
-                               const uint8_t* __restrict__ pyr) {
+                               const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ lblur, int lblur_from) {
     const int l = K.l, cx = K.cx, cy = K.cy;
     const LevelGeom& L = g.lv[l];
     const uint8_t* raw = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
@@ -328,6 +328,32 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
     // modulo-2^32 sums, exact since the totals fit)
     const int m10 = (int)wave_total(cp - (uint32_t)(od + 15) * sp);
     const int m01 = (int)wave_total(vp - 15u * sp);
+
+    // 3a. Levels whose whole blurred level was computed before this launch
+    // (blur.hip over levels >= lblur_from: where the keypoints' 37x37 patches
+    // cover the level several times over, one blur of the level is cheaper than
+    // one per keypoint): the 37 rows of 40 bytes from xb are staged from it --
+    // lane -> (row lane / 10, dword lane % 10), 6 rows per pass at LDS offset
+    // 4 * lane + 240 * pass (lanes 60..63 stage the next pass's first row); the
+    // 7th pass stores row 36 only.  The rows lie inside the level (cy +- 18 with
+    // cy in [19, h - 20]); the 40-byte span may run up to 2 bytes past a row's
+    // end (into its pitch padding, or the buffer's slack).
+    if (l >= lblur_from) {
+        const uint32_t bp = (uint32_t)L.pitch;  // blurred levels: the pyramid's row pitch (level 0 too)
+        const uint8_t* bl = lblur + L.blur_offset + (size_t)f * L.blur_frame_bytes + (size_t)(cy - kBlurR) * bp + xb;
+        const uint32_t rl = __umul24((uint32_t)lane, 6554u) >> 16, q = (uint32_t)lane - 10u * rl;
+        const uint32_t off0 = __umul24(rl, bp) + 4u * q;
+        constexpr int kPasses = (kBlur + 5) / 6;  // 7
+        uint32_t v[kPasses];
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k)
+            v[k] = *reinterpret_cast<const uint32_t*>(bl + (off0 + (uint32_t)(6 * k) * bp));
+#pragma unroll
+        for (int k = 0; k < kPasses; ++k)
+            if (k < kPasses - 1 || lane < 10) *reinterpret_cast<uint32_t*>(blur_out + 4 * lane + 6 * kBPitch * k) = v[k];
+        static_assert(kBPitch == 40 && 6 * (kPasses - 1) == kBlur - 1, "blurred patch staging map");
+        return int2{m10, m01};
+    }
 
     // 3. Blur (blur_device.h, the arithmetic of blur.hip) of the 37x37 patch:
     // lane = (output quad q, chunk c of 7 blurred rows); row passes from the
@@ -479,7 +505,8 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
                                                                    uint8_t* __restrict__ desc,
                                                                    int* __restrict__ counts, int kp_cap,
                                                                    int* __restrict__ err_word,
-                                                                   int* __restrict__ err_copy) {
+                                                                   int* __restrict__ err_copy,
+                                                                   const uint8_t* __restrict__ lblur, int lblur_from) {
     __shared__ DescLds s_lds[kDescWaves];
     // single-frame path: the error word of this extraction (FAST / octree ran
     // before on the stream) moves into the output block and is cleared, so
@@ -546,7 +573,8 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
         if (k > 0) wave_sync();  // the previous keypoint's blur has read the raw buffer
         int lane_k = lane;
         asm volatile("" : "+v"(lane_k));  // per iteration: no lane-derived invariant is hoisted out (VGPRs 82 -> 50)
-        const int2 mm = describe_patch(g, f, Kk, lane_k, s_lds[wave], s_lds[wave].blur[k], img0, row0, frame0, pyr);
+        const int2 mm = describe_patch(g, f, Kk, lane_k, s_lds[wave], s_lds[wave].blur[k], img0, row0, frame0, pyr,
+                                       lblur, lblur_from);
         if (kKeysPerWave == 1 || lane == k) {  // one keypoint: wave-uniform moments, uniform branches below
             mx = mm.x;
             my = mm.y;
@@ -595,12 +623,14 @@ extern "C" int orbgpu_debug_desc_stamps(unsigned long long* out, int reset) {
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                            const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
-                           hipStream_t stream, int* err_word, int* err_copy, int f0) {
+                           hipStream_t stream, int* err_word, int* err_copy, int f0, const uint8_t* lblur,
+                           int lblur_from) {
     const int items = (g.slots_frame + kKeysPerWave - 1) / kKeysPerWave * batch;  // waves (frames f0 .. f0+batch-1)
     if (row0 >= (1u << 24)) return hipErrorInvalidValue;  // row offsets by 24-bit multiplies
     const int blocks = (items + kDescWaves - 1) / kDescWaves;
     hipLaunchKernelGGL(describe_kernel, dim3(blocks), dim3(64 * kDescWaves), 0, stream, g, items, f0, img0, row0, frame0,
-                       pyr, oct_out, oct_count, kps, desc, counts, kp_cap, err_word, err_copy);
+                       pyr, oct_out, oct_count, kps, desc, counts, kp_cap, err_word, err_copy, lblur,
+                       lblur ? lblur_from : kMaxLevels);
     return hipGetLastError();
 }
 

@@ -14,27 +14,11 @@
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
 
+#include <type_traits>
+
 namespace orbgpu {
 
 namespace {
-
-// q = n / d via one full-rate v_mul_u32_u24 (not the quarter-rate
-// v_mul_lo_u32): m = floor(2^23 / d) + 1 < 2^24 for every d >= 1 (a cell
-// clipped at the level's right edge can be one chunk wide), exact while
-// n < 2^23 / d and n * m < 2^32 -- here n < 512, d <= 5
-__host__ __device__ constexpr uint32_t fast_div_m(uint32_t d) { return (1u << 23) / d + 1u; }
-// (both operands masked to 24 bits, so the product is one v_mul_u32_u24 even
-// with m in a scalar register)
-__device__ inline uint32_t fast_div(uint32_t n, uint32_t m) { return __umul24(n & 0xFFFFFFu, m & 0xFFFFFFu) >> 23; }
-// m for the divisors the staging uses (chunks or dwords per window row, <= 24),
-// a scalar table load instead of a VALU integer division
-struct DivTab { uint32_t m[25]; };
-constexpr DivTab make_div_tab() {
-    DivTab t{};
-    for (int d = 1; d < 25; ++d) t.m[d] = fast_div_m((uint32_t)d);
-    return t;
-}
-__constant__ DivTab c_div = make_div_tab();
 
 #ifndef ORBGPU_FAST_BANDS
 #define ORBGPU_FAST_BANDS 1
@@ -45,6 +29,31 @@ __constant__ DivTab c_div = make_div_tab();
 __host__ __device__ constexpr int fast_list_len(int P, int R, int det_max) {
     const int c = ((4864 - 2 * P * R - 16) / 2 - 1) & ~7;
     return !ORBGPU_FAST_BANDS || c >= det_max ? det_max : (c >= 256 ? c : det_max);
+}
+
+// a wave-uniform pointer held in scalar registers (loads then take the
+// saddr + 32-bit vector offset form: no 64-bit vector address arithmetic)
+__device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return (const uint8_t*)(((uint64_t)hi << 32) | lo);
+}
+
+// Window staging geometry (fast_cells_kernel): chunks of CB bytes, NC per
+// P-byte row, RPI rows per pass of 64 lanes, kGroup passes' loads in flight.
+template <int P>
+struct FastStage {
+    static constexpr int CB = P % 16 == 0 ? 16 : 4, NC = P / CB, RPI = 64 / NC, kGroup = CB == 16 ? 2 : 4;
+};
+// LDS rows the staging writes for windows of up to R rows: whole groups of
+// passes plus the row the lanes past RPI * NC stage (must fit in the window and
+// the score tile behind it, 2R rows)
+template <int P>
+constexpr int fast_stage_rows(int R) {
+    using S = FastStage<P>;
+    const int passes = (R + S::RPI - 1) / S::RPI;
+    return S::RPI * ((passes + S::kGroup - 1) / S::kGroup * S::kGroup + 1);
 }
 
 // The waves of a block work on different cells, so stages are ordered with
@@ -384,7 +393,6 @@ __device__ unsigned long long g_fast_stamps[16];
 #define ORBGPU_FAST_CELL_WAVES 1
 #endif
 constexpr int kCellWaves = ORBGPU_FAST_CELL_WAVES;  // cells (one per wave) per block: 1 measured fastest (4: 0.839 ms, 2: 0.857, 1: 0.817 per 512 frames)
-constexpr int kStageLoads = 8;  // window dwords per lane in flight
 
 template <int P>
 __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int ncells_total,
@@ -444,46 +452,46 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     // stage rows: dwords covering [xa, maxX), xa = iniX & ~3 (row pitch and
     // frame base are 16-byte aligned; maxX <= w - 16, so no over-read)
     const int xa = iniX & ~3, ox = iniX - xa;
-    const int nd = (maxX - xa + 3) >> 2;
-    // all of a lane's loads are issued before any is consumed, so the
-    // window costs one memory round trip, not one per row group; (row,
-    // column) of an index by one 24-bit multiply, computed once for the load
-    // (row clamped into the window) and the store
-    const uint8_t* wbase = base + (size_t)iniY * pitch + xa;
-    if constexpr (P % 16 == 0) {
-        // 16-byte chunks (P a multiple of 16: a row's chunks stay inside its LDS row; the
-        // last chunk reads at most 12 bytes past maxX, still inside the level row since
-        // maxX <= w - 16); one load per lane for ~64 of a window's ~115 chunks
-        const uint32_t nc = (uint32_t)(maxX - xa + 15) >> 4, total = nc * (uint32_t)wh;
-        const uint32_t mnc = c_div.m[nc];
-        for (uint32_t b0 = 0; b0 < total; b0 += 64 * 2) {
-            uint4 v[2];
-            uint32_t loff[2];
+    // Every window row is staged as P bytes: NC chunks of CB bytes (16 when P is
+    // a multiple of 16, else 4), so LDS chunk (r, q) sits at CB * (r * NC + q)
+    // and a fixed lane -> (row rl, chunk q) map covers RPI = 64 / NC rows per
+    // pass at LDS offset CB * lane + pass * RPI * P: the stores take immediate
+    // offsets, and a load's address costs a row clamp and one 24-bit multiply-
+    // add (the map is computed once per lane; round 4's per-load division and
+    // offset arithmetic was ~16 VALU per load, 128 per wave).  Lanes past
+    // RPI * NC map to row RPI with the same formula, i.e. they stage the next
+    // pass's first row (the same bytes).  Chunks past the window's last needed
+    // one re-read that chunk (column clamp: no read past maxX + 15 <= w - 1),
+    // rows past the window re-read its last row; both land in LDS the detection
+    // never reads: rows >= wh, inside the score tile (zeroed after) -- the
+    // launcher checks that the whole groups of passes fit there
+    // (fast_stage_rows), so every store is unconditional and no load is sunk
+    // behind a branch.  All of a lane's loads of a group are issued before any
+    // is stored.
+    const uint8_t* wbase = uniform_ptr(base + (size_t)iniY * pitch + xa);
+    {
+        constexpr int CB = FastStage<P>::CB, NC = FastStage<P>::NC, RPI = FastStage<P>::RPI,
+                      kGroup = FastStage<P>::kGroup;
+        const int rl = lane / NC, q = lane - rl * NC;  // compile-time divisor
+        const int ncneed = (maxX - xa + CB - 1) / CB;
+        const uint32_t col = (uint32_t)(CB * min(q, ncneed - 1));
+        const int passes = (wh + RPI - 1) / RPI;  // wave-uniform
+        uint8_t* dst = s_win + CB * lane;
+        typedef typename std::conditional<CB == 16, uint4, uint32_t>::type Chunk;
+#pragma unroll 1
+        for (int p0 = 0; p0 < passes; p0 += kGroup) {
+            Chunk v[kGroup];
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const uint32_t idx = b0 + (uint32_t)(lane + 64 * k), r = fast_div(idx, mnc), q = idx - __umul24(r, nc);
-                loff[k] = idx < total ? __umul24(r, (uint32_t)P) + 16u * q : (uint32_t)(P * R);
-                v[k] = load16_a4(wbase + (__umul24(min(r, (uint32_t)wh - 1u), pitch) + 16u * q));
+            for (int k = 0; k < kGroup; ++k) {
+                const uint32_t r = (uint32_t)min(rl + RPI * (p0 + k), wh - 1);
+                const uint8_t* src = wbase + (__umul24(r, pitch) + col);
+                if constexpr (CB == 16)
+                    v[k] = load16_a4(src);
+                else
+                    v[k] = *reinterpret_cast<const uint32_t*>(src);
             }
-            // unconditional stores (lanes past the window write into the score
-            // tile, zeroed below): no branch the loads could be sunk into
 #pragma unroll
-            for (int k = 0; k < 2; ++k) *reinterpret_cast<uint4*>(s_win + loff[k]) = v[k];
-        }
-    } else {
-        const uint32_t total = (uint32_t)(nd * wh), mnd = c_div.m[nd];
-        for (uint32_t b0 = 0; b0 < total; b0 += 64 * kStageLoads) {
-            uint32_t v[kStageLoads];
-            uint32_t loff[kStageLoads];
-#pragma unroll
-            for (int k = 0; k < kStageLoads; ++k) {  // unconditional (row-clamped) loads: no waits between them
-                const uint32_t idx = b0 + (uint32_t)(lane + 64 * k), r = fast_div(idx, mnd),
-                               q = idx - __umul24(r, (uint32_t)nd);
-                loff[k] = idx < total ? __umul24(r, (uint32_t)P) + 4u * q : (uint32_t)(P * R);
-                v[k] = *reinterpret_cast<const uint32_t*>(wbase + (__umul24(min(r, (uint32_t)wh - 1u), pitch) + 4u * q));
-            }
-#pragma unroll
-            for (int k = 0; k < kStageLoads; ++k) *reinterpret_cast<uint32_t*>(s_win + loff[k]) = v[k];
+            for (int k = 0; k < kGroup; ++k) *reinterpret_cast<Chunk*>(dst + (p0 + k) * RPI * P) = v[k];
         }
     }
     // (T.sc is 16-byte aligned when P * R is: then 16-byte stores, else dwords)
@@ -582,6 +590,7 @@ hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size
     const size_t lds = per_wave * kCellWaves;
 #define ORBGPU_FAST_CASE(PP)                                                                                        \
     case PP:                                                                                                        \
+        if (fast_stage_rows<PP>(g.win_rows) > 2 * g.win_rows) return hipErrorInvalidValue;                        \
         hipLaunchKernelGGL(fast_cells_kernel<PP>, grid, dim3(64 * kCellWaves), lds, stream, g, items, img0, row0, \
                            frame0, pyr, cand, cell_counts, err);                                                   \
         break;

@@ -7,6 +7,7 @@
 namespace orbgpu {
 
 HostCtx::~HostCtx() {
+    DeviceScope ds(device);
     // errors are ignored: at process exit the runtime may already be gone
     if (stream) (void)hipStreamSynchronize(stream);
     if (dev) (void)hipFree(dev);
@@ -30,13 +31,21 @@ int HostCtx::reserve(size_t bytes) {
 }
 
 int host_ctx(HostCtx** out) {
-    static thread_local std::unique_ptr<HostCtx> t;
-    if (!t) {
-        auto c = std::make_unique<HostCtx>();
-        ORB_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        t = std::move(c);
+    // one context per (thread, device): the thread's current device -- the one
+    // orbgpu_set_thread_device chose -- owns the stream, arena and mirror
+    constexpr int kMaxDevices = 64;
+    static thread_local std::unique_ptr<HostCtx> t[kMaxDevices];
+    int dev = 0;
+    ORB_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= kMaxDevices) return fail(ORBGPU_ERR_UNSUPPORTED, "device ordinal above 63");
+    std::unique_ptr<HostCtx>& c = t[dev];
+    if (!c) {
+        auto n = std::make_unique<HostCtx>();
+        n->device = dev;
+        ORB_HIP(hipStreamCreateWithFlags(&n->stream, hipStreamNonBlocking));
+        c = std::move(n);
     }
-    *out = t.get();
+    *out = c.get();
     return ORBGPU_OK;
 }
 

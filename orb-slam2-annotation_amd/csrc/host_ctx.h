@@ -39,6 +39,7 @@ inline bool host_copy_kernels() {
 
 struct HostCtx {
     hipStream_t stream = nullptr;
+    int device = -1;  // the HIP device the stream and arena belong to
     uint8_t* dev = nullptr;
     uint8_t* pin = nullptr;
     size_t cap = 0;

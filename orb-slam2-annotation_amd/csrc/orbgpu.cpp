@@ -58,6 +58,16 @@ int check_device() {
     return ORBGPU_OK;
 }
 
+int validate_device(int device) {
+    if (device < 0) return fail(ORBGPU_ERR_ARG, "device ordinal must be >= 0");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(ORBGPU_ERR_NO_DEVICE, "no HIP device visible");
+    if (device >= n)
+        return fail(ORBGPU_ERR_ARG, "device ordinal " + std::to_string(device) + " >= visible devices (" +
+                                        std::to_string(n) + ")");
+    return ORBGPU_OK;
+}
+
 }  // namespace orbgpu
 
 namespace {
@@ -184,6 +194,7 @@ struct orbgpu_extractor {
     std::array<hipEvent_t, 9> od_ev{};  // [c]: octree of chunk c done; [8]: the describes done
     // stage timing
     bool profile = false;
+    int device = -1;  // the HIP device the handle's buffers and stream live on
     hipEvent_t stage_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // orbgpu_extractor_set_stage_event
     std::vector<std::array<hipEvent_t, 5>> ev;
     size_t ev_used = 0;
@@ -193,6 +204,7 @@ struct orbgpu_extractor {
     int last_batch = 0;
 
     ~orbgpu_extractor() {
+        DeviceScope ds(device);
         void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_ent, d_pyr_tab, d_xtab, d_ytab, d_band, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
                         d_oct_count, d_err, d_trace, d_img, d_single, d_tab};
         for (void* p : ptrs)
@@ -469,6 +481,24 @@ bool pyr_bands_off() {
     return v;
 }
 
+// first level whose keypoints describe reads from the whole blurred level
+// (blur.hip over levels >= it, one launch before describe) instead of blurring
+// each keypoint's 37x37 patch: ORBGPU_DESC_LEVEL_BLUR = L in [1, nlevels) takes
+// levels >= L that way (any other value: none); unset, batches above the
+// small-batch pyramid limit take kDescLevelBlur (the drop-in single frame: none)
+#ifndef ORBGPU_DESC_LEVEL_BLUR_DEFAULT
+#define ORBGPU_DESC_LEVEL_BLUR_DEFAULT 3
+#endif
+int desc_level_blur(int batch, int nlevels) {  // read per batch (tests switch it within one process)
+    const char* s = std::getenv("ORBGPU_DESC_LEVEL_BLUR");
+    if (s) {
+        const int v = std::atoi(s);
+        return v >= 1 && v < nlevels ? v : nlevels;
+    }
+    const int d = ORBGPU_DESC_LEVEL_BLUR_DEFAULT;
+    return batch > pyr_levels_max_batch() && d >= 1 && d < nlevels ? d : nlevels;
+}
+
 int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_step, size_t frame_step,
               orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap, hipStream_t s, int* err_copy = nullptr) {
     const Geom& g = e->g;
@@ -496,15 +526,24 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
     if (evs) ORB_HIP(hipEventRecord(evs[2], s));
     if (e->stage_ev[1]) ORB_HIP(hipEventRecord(e->stage_ev[1], s));
     const int nch = (err_copy || batch < 16 * od_chunks()) ? 1 : od_chunks();
+    // the upper levels' whole-level blur (describe samples it), after the octree
+    const int lbf = desc_level_blur(batch, e->nlevels);
+    if (lbf < e->nlevels && !e->d_blur) {
+        int rc = dalloc(&e->d_blur, e->blur_bytes);
+        if (rc) return rc;
+    }
+    const uint8_t* lblur = lbf < e->nlevels ? e->d_blur : nullptr;
     if (nch == 1) {
         ORB_HIP(launch_octree(g, batch, e->d_cand, e->d_cell_counts, e->d_gkeys, e->d_gknode, e->d_oct_out,
                               e->d_oct_count, e->d_err, e->oct_groups, 2, e->d_trace, s));
         if (evs) ORB_HIP(hipEventRecord(evs[3], s));
         if (e->stage_ev[2]) ORB_HIP(hipEventRecord(e->stage_ev[2], s));
-        // GaussianBlur is fused into describe (blur of each keypoint's patch);
-        // whole blurred levels exist only for the debug API
+        // GaussianBlur: the levels below lbf fused into describe (blur of each
+        // keypoint's patch), the levels from lbf blurred whole just before it
+        if (lblur)
+            ORB_HIP(launch_blur_levels(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_blur, s, lbf));
         ORB_HIP(launch_describe(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_oct_out, e->d_oct_count, kps,
-                                desc, counts, kp_cap, s, err_copy ? e->d_err : nullptr, err_copy));
+                                desc, counts, kp_cap, s, err_copy ? e->d_err : nullptr, err_copy, 0, lblur, lbf));
     } else {
         // the octree chunks in order on s, each chunk's describe on the aux stream after
         // its octree: describe(c) overlaps octree(c+1); s joins the aux stream at the end
@@ -515,6 +554,8 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
             for (hipEvent_t& x : e->od_ev) ORB_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
         }
         hipStream_t a = e->aux_stream;
+        if (lblur)
+            ORB_HIP(launch_blur_levels(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_blur, s, lbf));
         for (int c = 0; c < nch; ++c) {
             const int f0 = batch * c / nch, f1 = batch * (c + 1) / nch, nb = f1 - f0;
             ORB_HIP(launch_octree(g, nb, e->d_cand + (size_t)f0 * g.cand_frame,
@@ -528,7 +569,7 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
             ORB_HIP(hipEventRecord(e->od_ev[c], s));
             ORB_HIP(hipStreamWaitEvent(a, e->od_ev[c], 0));
             ORB_HIP(launch_describe(g, nb, imgs, row_step, frame_step, e->d_pyr, e->d_oct_out, e->d_oct_count, kps,
-                                    desc, counts, kp_cap, a, nullptr, nullptr, f0));
+                                    desc, counts, kp_cap, a, nullptr, nullptr, f0, lblur, lbf));
         }
         if (e->stage_ev[2]) ORB_HIP(hipEventRecord(e->stage_ev[2], s));
         ORB_HIP(hipEventRecord(e->od_ev[8], a));
@@ -592,6 +633,7 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
     int rc = check_device();
     if (rc) return rc;
     orbgpu_extractor* e = new orbgpu_extractor();
+    ORB_HIP(hipGetDevice(&e->device));
     e->nfeatures = nfeatures;
     e->scale_factor = scale_factor;
     e->nlevels = nlevels;
@@ -669,8 +711,40 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
     return ORBGPU_OK;
 }
 
+int orbgpu_extractor_create_on_device(int device, int nfeatures, float scale_factor, int nlevels, int ini_th,
+                                      int min_th, int width, int height, int max_batch, orbgpu_extractor** out) {
+    if (out) *out = nullptr;
+    int rc = validate_device(device);
+    if (rc) return rc;
+    DeviceScope ds(device);
+    return orbgpu_extractor_create(nfeatures, scale_factor, nlevels, ini_th, min_th, width, height, max_batch, out);
+}
+
 int orbgpu_extractor_destroy(orbgpu_extractor* e) {
     delete e;
+    return ORBGPU_OK;
+}
+
+int orbgpu_device_count(int* n) {
+    if (!n) return fail(ORBGPU_ERR_ARG, "n is NULL");
+    *n = 0;
+    if (hipGetDeviceCount(n) != hipSuccess) *n = 0;
+    return ORBGPU_OK;
+}
+
+int orbgpu_set_thread_device(int device) {
+    int rc = validate_device(device);
+    if (rc) return rc;
+    ORB_HIP(hipSetDevice(device));
+    return check_device();
+}
+
+int orbgpu_get_thread_device(int* device) {
+    if (!device) return fail(ORBGPU_ERR_ARG, "device is NULL");
+    *device = -1;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(ORBGPU_ERR_NO_DEVICE, "no HIP device visible");
+    ORB_HIP(hipGetDevice(device));
     return ORBGPU_OK;
 }
 
@@ -682,6 +756,7 @@ int orbgpu_extractor_get_info(const orbgpu_extractor* e, orbgpu_extractor_info* 
     info->height = e->H;
     info->max_batch = e->max_batch;
     info->max_keypoints = e->max_kps;
+    info->device = e->device;
     for (int l = 0; l < e->nlevels && l < 32; ++l) {
         info->level_width[l] = e->g.lv[l].w;
         info->level_height[l] = e->g.lv[l].h;
@@ -706,6 +781,7 @@ int orbgpu_extract_batch_device(orbgpu_extractor* e, const uint8_t* imgs, int ba
                                 size_t frame_step, orbgpu_keypoint* kps, uint8_t* desc, int* counts,
                                 int kp_cap, void* stream) {
     if (!e || !imgs || !kps || !desc || !counts) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    DeviceScope ds_(e->device);
     if (batch <= 0 || batch > e->max_batch) return fail(ORBGPU_ERR_ARG, "batch outside [1, max_batch]");
     if (kp_cap < e->max_kps) return fail(ORBGPU_ERR_CAPACITY, "kp_capacity < max_keypoints");
     if (row_step < (size_t)e->W || row_step % 16 || ((uintptr_t)imgs & 15) || (batch > 1 && frame_step % 16) ||
@@ -716,12 +792,14 @@ int orbgpu_extract_batch_device(orbgpu_extractor* e, const uint8_t* imgs, int ba
 
 int orbgpu_extractor_sync(orbgpu_extractor* e, void* stream) {
     if (!e) return fail(ORBGPU_ERR_ARG, "NULL extractor");
+    DeviceScope ds_(e->device);
     return collect_errors(e, (hipStream_t)stream);
 }
 
 int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int height, size_t step,
                    orbgpu_keypoint* keypoints, uint8_t* descriptors, int capacity, int* n) {
     if (!e || !n) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    DeviceScope ds_(e->device);
     if (!image || width <= 0 || height <= 0) {  // ORBextractor.cpp:1056
         *n = -1;
         return ORBGPU_OK;
@@ -797,6 +875,7 @@ int orbgpu_extractor_set_stage_event(orbgpu_extractor* e, int stage, void* event
 
 int orbgpu_extractor_stage_times(orbgpu_extractor* e, float* ms4, int* nbatches, int reset) {
     if (!e) return fail(ORBGPU_ERR_ARG, "NULL extractor");
+    DeviceScope ds_(e->device);
     float acc[4] = {0, 0, 0, 0};
     for (size_t i = 0; i < e->ev_used; ++i) {
         ORB_HIP(hipEventSynchronize(e->ev[i][4]));
@@ -815,6 +894,7 @@ int orbgpu_extractor_stage_times(orbgpu_extractor* e, float* ms4, int* nbatches,
 
 int orbgpu_extractor_copy_level(orbgpu_extractor* e, int frame, int level, uint8_t* dst, size_t dst_step) {
     if (!e || !dst) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    DeviceScope ds_(e->device);
     if (!e->last_img || frame < 0 || frame >= e->last_batch || level < 0 || level >= e->nlevels)
         return fail(ORBGPU_ERR_ARG, "no such frame/level in the last extraction");
     const LevelGeom& v = e->g.lv[level];
@@ -832,6 +912,7 @@ int orbgpu_extractor_copy_level(orbgpu_extractor* e, int frame, int level, uint8
 // into the caller's rows (a pageable 2-D copy per level costs ~1 ms)
 int orbgpu_extractor_copy_levels(orbgpu_extractor* e, int frame, uint8_t* const* dst, const size_t* dst_step) {
     if (!e || !dst || !dst_step) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    DeviceScope ds_(e->device);
     if (!e->last_img || frame < 0 || frame >= e->last_batch)
         return fail(ORBGPU_ERR_ARG, "no such frame in the last extraction");
     size_t total = 0, off[kMaxLevels];
@@ -871,6 +952,7 @@ int orbgpu_extractor_copy_levels(orbgpu_extractor* e, int frame, uint8_t* const*
 
 int orbgpu_debug_level_blur(orbgpu_extractor* e, int frame, int level, uint8_t* dst, size_t dst_step) {
     if (!e || !dst) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    DeviceScope ds_(e->device);
     if (!e->last_img || frame < 0 || frame >= e->last_batch || level < 0 || level >= e->nlevels)
         return fail(ORBGPU_ERR_ARG, "no such frame/level in the last extraction");
     const LevelGeom& v = e->g.lv[level];
@@ -1002,6 +1084,7 @@ int orbgpu_search_for_initialization(orbgpu_grid_bounds bd, const orbgpu_keypoin
 int orbgpu_debug_level_candidates(orbgpu_extractor* e, int frame, int level, int* xys, int cap) {
     if (!e || frame < 0 || frame >= e->last_batch || level < 0 || level >= e->nlevels)
         return fail(ORBGPU_ERR_ARG, "no such frame/level in the last extraction");
+    DeviceScope ds_(e->device);
     const Geom& g = e->g;
     const LevelGeom& v = g.lv[level];
     const int ncells = v.ncols * v.nrows;
@@ -1025,6 +1108,7 @@ int orbgpu_debug_level_candidates(orbgpu_extractor* e, int frame, int level, int
 
 int orbgpu_debug_octree_trace(orbgpu_extractor* e, int enable, int* out, int cap) {
     if (!e) return fail(ORBGPU_ERR_ARG, "NULL extractor");
+    DeviceScope ds_(e->device);
     const size_t n = (size_t)kMaxLevels * 512;
     if (enable && !e->d_trace) {
         ORB_HIP(hipMalloc((void**)&e->d_trace, n * sizeof(int)));
@@ -1040,6 +1124,7 @@ int orbgpu_debug_octree_trace(orbgpu_extractor* e, int enable, int* out, int cap
 int orbgpu_debug_level_octree(orbgpu_extractor* e, int frame, int level, int* xys, int cap) {
     if (!e || frame < 0 || frame >= e->last_batch || level < 0 || level >= e->nlevels)
         return fail(ORBGPU_ERR_ARG, "no such frame/level in the last extraction");
+    DeviceScope ds_(e->device);
     const Geom& g = e->g;
     const LevelGeom& v = g.lv[level];
     int n = 0;
@@ -1136,6 +1221,7 @@ int orbgpu_stereo_matches_batch_device(orbgpu_extractor* e, const uint8_t* d_ima
                                        float min_z, float* d_uright, float* d_depth, void* stream) {
     if (!e || !d_images || !d_kps || !d_desc || !d_counts || !d_uright || !d_depth)
         return fail(ORBGPU_ERR_ARG, "NULL argument");
+    DeviceScope ds_(e->device);
     if (npairs < 0 || 2 * npairs > e->max_batch) return fail(ORBGPU_ERR_ARG, "npairs exceeds max_batch / 2");
     if (kp_capacity < e->max_kps || kp_capacity > 65535)
         return fail(ORBGPU_ERR_ARG, "kp_capacity must be >= max_keypoints and < 65536");
@@ -1182,6 +1268,7 @@ int orbgpu_stereo_matches_pair(orbgpu_extractor* left, orbgpu_extractor* right, 
     if (!left || !right || n_l < 0 || n_r < 0 || (n_l > 0 && (!kps_l || !desc_l || !uright || !depth)) ||
         (n_r > 0 && (!kps_r || !desc_r)))
         return fail(ORBGPU_ERR_ARG, "invalid argument");
+    DeviceScope ds_(left->device);
     if (left->W != right->W || left->H != right->H || left->nlevels != right->nlevels ||
         left->scale_factor != right->scale_factor)
         return fail(ORBGPU_ERR_ARG, "left and right extractors differ in geometry");

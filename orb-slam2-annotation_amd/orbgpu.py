@@ -77,7 +77,8 @@ class _Info(ctypes.Structure):
     _fields_ = [("nlevels", ctypes.c_int), ("width", ctypes.c_int), ("height", ctypes.c_int),
                 ("max_batch", ctypes.c_int), ("max_keypoints", ctypes.c_int),
                 ("level_width", ctypes.c_int * 32), ("level_height", ctypes.c_int * 32),
-                ("features_per_level", ctypes.c_int * 32), ("level_capacity", ctypes.c_int * 32)]
+                ("features_per_level", ctypes.c_int * 32), ("level_capacity", ctypes.c_int * 32),
+                ("device", ctypes.c_int)]
 
 
 def lib() -> ctypes.CDLL:
@@ -98,7 +99,11 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_last_error.restype = ctypes.c_char_p
         L.orbgpu_device_arch.argtypes = [ctypes.c_char_p, i]
         L.orbgpu_extractor_create.argtypes = [i, f, i, i, i, i, i, i, ctypes.POINTER(vp)]
+        L.orbgpu_extractor_create_on_device.argtypes = [i, i, f, i, i, i, i, i, i, ctypes.POINTER(vp)]
         L.orbgpu_extractor_destroy.argtypes = [vp]
+        L.orbgpu_device_count.argtypes = [ctypes.POINTER(i)]
+        L.orbgpu_set_thread_device.argtypes = [i]
+        L.orbgpu_get_thread_device.argtypes = [ctypes.POINTER(i)]
         L.orbgpu_extractor_get_info.argtypes = [vp, ctypes.POINTER(_Info)]
         L.orbgpu_extractor_get_scales.argtypes = [vp, vp, vp, vp, vp]
         L.orbgpu_extract.argtypes = [vp, vp, i, i, sz, vp, vp, i, ctypes.POINTER(i)]
@@ -184,6 +189,24 @@ def device_arch() -> str:
     return buf.value.decode()
 
 
+def device_count() -> int:
+    """visible HIP devices (0 without any)"""
+    n = ctypes.c_int()
+    _check(lib().orbgpu_device_count(ctypes.byref(n)), "orbgpu_device_count")
+    return n.value
+
+
+def set_thread_device(device: int) -> None:
+    """the calling thread's device for the host-form calls (orbgpu_set_thread_device)"""
+    _check(lib().orbgpu_set_thread_device(int(device)), "orbgpu_set_thread_device")
+
+
+def get_thread_device() -> int:
+    d = ctypes.c_int()
+    _check(lib().orbgpu_get_thread_device(ctypes.byref(d)), "orbgpu_get_thread_device")
+    return d.value
+
+
 def pyramid_plan_emulate(img: np.ndarray, nfeatures=1000, scale_factor=1.2, nlevels=8):
     """Levels 1..nlevels-1 of `img` computed on the CPU by the fused pyramid
     kernel's own plan (orbgpu_debug_pyramid_emulate: same LDS ring slots, row
@@ -229,11 +252,18 @@ class Extractor:
     frames of a fixed width x height, batched up to ``max_batch`` frames."""
 
     def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7,
-                 width=640, height=480, max_batch=1):
+                 width=640, height=480, max_batch=1, device=None):
+        """device: a HIP ordinal to place the extractor on (orbgpu_extractor_create_on_device);
+        None: the calling thread's current device"""
         h = ctypes.c_void_p()
-        _check(lib().orbgpu_extractor_create(nfeatures, scale_factor, nlevels, ini_th, min_th,
-                                             width, height, max_batch, ctypes.byref(h)),
-               "orbgpu_extractor_create")
+        if device is None:
+            _check(lib().orbgpu_extractor_create(nfeatures, scale_factor, nlevels, ini_th, min_th,
+                                                 width, height, max_batch, ctypes.byref(h)),
+                   "orbgpu_extractor_create")
+        else:
+            _check(lib().orbgpu_extractor_create_on_device(int(device), nfeatures, scale_factor, nlevels, ini_th,
+                                                           min_th, width, height, max_batch, ctypes.byref(h)),
+                   "orbgpu_extractor_create_on_device")
         self.h = h
         info = _Info()
         _check(lib().orbgpu_extractor_get_info(self.h, ctypes.byref(info)), "get_info")
@@ -244,6 +274,7 @@ class Extractor:
         self.level_sizes = [(info.level_width[l], info.level_height[l]) for l in range(self.nlevels)]
         self.features_per_level = [info.features_per_level[l] for l in range(self.nlevels)]
         self.level_capacity = [info.level_capacity[l] for l in range(self.nlevels)]
+        self.device = info.device
 
     def close(self):
         if getattr(self, "h", None):

@@ -979,6 +979,23 @@ int main(int argc, char** argv) {
         for (size_t i = 0; i < s.size(); ++i) printf("%a %a %a %a\n", s[i], is[i], s2[i], is2[i]);
         return 0;
     }
+    if (argc >= 3 && !strcmp(argv[1], "device")) {
+        // an extractor placed on device argv[2]: a bad ordinal throws when the handle is
+        // created (first frame); prints the device the handle reports
+        try {
+            ORB_SLAM2::ORBextractor ex(500, 1.2f, 8, 20, 7, atoi(argv[2]));
+            std::vector<unsigned char> buf(64 * 64, 128);
+            cv::Mat img(64, 64, CV_8UC1, buf.data(), (size_t)64);
+            std::vector<cv::KeyPoint> k;
+            cv::Mat d;
+            ex(img, cv::Mat(), k, d);
+            printf("%d\n", ex.device());
+            return 0;
+        } catch (const std::exception& e) {
+            fprintf(stderr, "exception: %s\n", e.what());
+            return 3;
+        }
+    }
     if (argc >= 2 && !strcmp(argv[1], "empty")) {
         ORB_SLAM2::ORBextractor ex(1000, 1.2f, 8, 20, 7);
         std::vector<cv::KeyPoint> kps(3);
@@ -995,7 +1012,9 @@ int main(int argc, char** argv) {
             return 2;
         }
         try {
-            ORB_SLAM2::ORBextractor ex(nf, 1.2f, 8, 20, 7);
+            // ADAPTER_DEVICE: the GPU the extractor and the matcher are placed on (Device.h)
+            const int dev = std::getenv("ADAPTER_DEVICE") ? atoi(std::getenv("ADAPTER_DEVICE")) : -1;
+            ORB_SLAM2::ORBextractor ex(nf, 1.2f, 8, 20, 7, dev);
             ex.SetCopyPyramid(true);  // this mode writes mvImagePyramid[1] for the test
             MiniFrame F[2];
             for (int f = 0; f < 2; ++f) {
@@ -1007,8 +1026,12 @@ int main(int argc, char** argv) {
             std::vector<cv::Point2f> prev;
             for (const cv::KeyPoint& k : F[0].mvKeysUn) prev.push_back(k.pt);
             std::vector<int> m12;
-            ORB_SLAM2::ORBmatcher matcher(0.9f, true);  // Tracking.cpp:766-769
+            ORB_SLAM2::ORBmatcher matcher(0.9f, true, dev);  // Tracking.cpp:766-769
             const int nm = matcher.SearchForInitialization(F[0], F[1], prev, m12, 100);
+            if (dev >= 0 && ex.device() != dev) {
+                fprintf(stderr, "extractor on device %d, asked for %d\n", ex.device(), dev);
+                return 4;
+            }
             {
                 ORB_SLAM2::ORBextractor tx(nf, 1.2f, 8, 20, 7);  // default: pyramid stays in HBM
                 cv::Mat img(h, w, CV_8UC1, im[1].data(), (size_t)w);

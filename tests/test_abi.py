@@ -45,3 +45,56 @@ def test_no_device_fails_loudly():
     with pytest.raises(orbgpu.OrbGpuError):
         orbgpu.search_for_initialization(np.zeros(0, orbgpu.KP_DTYPE), np.zeros((0, 32), np.uint8),
                                          np.zeros(0, orbgpu.KP_DTYPE), np.zeros((0, 32), np.uint8), 640, 480)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure path")
+def test_device_placement_validation_without_device():
+    """ordinals are validated before any device is touched
+    (negative -> ORBGPU_ERR_ARG), and without a device every placement call
+    fails loudly (ORBGPU_ERR_NO_DEVICE); the count is 0."""
+    import orbgpu
+    L = orbgpu.lib()
+    assert orbgpu.device_count() == 0
+    assert L.orbgpu_set_thread_device(-1) == orbgpu.ERR_ARG
+    assert "ordinal" in orbgpu.last_error()
+    assert L.orbgpu_set_thread_device(0) == orbgpu.ERR_NO_DEVICE
+    h = ctypes.c_void_p(12345)
+    assert L.orbgpu_extractor_create_on_device(-2, 1000, 1.2, 8, 20, 7, 640, 480, 1, ctypes.byref(h)) == orbgpu.ERR_ARG
+    assert h.value is None  # *out cleared on failure
+    assert L.orbgpu_extractor_create_on_device(0, 1000, 1.2, 8, 20, 7, 640, 480, 1,
+                                               ctypes.byref(h)) == orbgpu.ERR_NO_DEVICE
+    d = ctypes.c_int(7)
+    assert L.orbgpu_get_thread_device(ctypes.byref(d)) == orbgpu.ERR_NO_DEVICE and d.value == -1
+    with pytest.raises(orbgpu.OrbGpuError):
+        orbgpu.Extractor(device=0)
+
+
+@pytest.mark.gpu
+def test_device_placement_on_gpu():
+    """An extractor placed on device 0 reports it, works from a thread whose
+    current device was never set, and equals the oracle; ordinals outside the
+    visible devices are refused; the thread device round-trips."""
+    import threading
+    import orbgpu
+    import orbref
+    import synth
+    n = orbgpu.device_count()
+    assert n >= 1
+    orbgpu.set_thread_device(0)
+    assert orbgpu.get_thread_device() == 0
+    with pytest.raises(orbgpu.OrbGpuError) as e:
+        orbgpu.set_thread_device(n)
+    assert e.value.code == orbgpu.ERR_ARG
+    with pytest.raises(orbgpu.OrbGpuError) as e:
+        orbgpu.Extractor(device=n)
+    assert e.value.code == orbgpu.ERR_ARG
+    ex = orbgpu.Extractor(device=0)
+    assert ex.device == 0
+    img = synth.mono_stream(1)[0]
+    out = {}
+    t = threading.Thread(target=lambda: out.update(r=ex.extract(img)))
+    t.start()
+    t.join()
+    kr, dr = orbref.Extractor().extract(img)
+    kg, dg = out["r"]
+    assert kg.tobytes() == kr.tobytes() and np.array_equal(dg, dr)

@@ -49,6 +49,17 @@ def test_adapter_without_device_throws(exe):
     assert r.returncode == 0 and "threw" in r.stdout, r.stdout + r.stderr
 
 
+@pytest.mark.gpu
+def test_adapter_device_argument(exe):
+    """ORBextractor(..., device): the handle is created on that GPU; an
+    ordinal outside the visible devices throws (runtime_error carrying the
+    library's message) instead of running elsewhere."""
+    r = subprocess.run([exe, "device", "0"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "0", r.stdout + r.stderr
+    r = subprocess.run([exe, "device", "99"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 3 and "ordinal 99" in r.stderr, r.stdout + r.stderr
+
+
 def _read_frame(buf, off):
     n, = struct.unpack_from("<i", buf, off)
     off += 4
@@ -59,11 +70,13 @@ def _read_frame(buf, off):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("copy_engine", [False, True])
-def test_adapter_extract_and_match_vs_oracle(exe, tmp_path, copy_engine):
+@pytest.mark.parametrize("copy_engine,device", [(False, None), (True, None), (False, 0)])
+def test_adapter_extract_and_match_vs_oracle(exe, tmp_path, copy_engine, device):
     """ORBextractor (with the host pyramid copy) + SearchForInitialization
     through the C++ classes; transfers by copy kernels (default) and, with
-    ORBGPU_SINGLE_ZEROCOPY=0 ORBGPU_HOST_ZEROCOPY=0, by the copy engine."""
+    ORBGPU_SINGLE_ZEROCOPY=0 ORBGPU_HOST_ZEROCOPY=0, by the copy engine; and
+    with both objects placed on device 0 through their `device` constructor
+    argument (include/orbslam2_amd/Device.h)."""
     w, h, nf = 640, 480, 1000
     frames = synth.mono_stream(2, w, h, seed=0x0B5E)
     for i, f in enumerate(frames):
@@ -72,6 +85,8 @@ def test_adapter_extract_and_match_vs_oracle(exe, tmp_path, copy_engine):
     env = dict(os.environ)
     if copy_engine:
         env.update(ORBGPU_SINGLE_ZEROCOPY="0", ORBGPU_HOST_ZEROCOPY="0")
+    if device is not None:
+        env["ADAPTER_DEVICE"] = str(device)
     r = subprocess.run([exe, "extract", str(w), str(h), str(nf), str(tmp_path / "f0.raw"),
                         str(tmp_path / "f1.raw"), str(out)], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr

@@ -197,6 +197,33 @@ def test_batch_octree_describe_chunks_match_oracle(monkeypatch, chunks):
         _assert_same_kps(kg, dd[b, :cc[b]], kr, dr)
 
 
+@pytest.mark.parametrize("from_level", ["1", "3", "0"])
+def test_describe_level_blur_paths(monkeypatch, from_level):
+    """ORBGPU_DESC_LEVEL_BLUR: keypoints of levels >= L sample a whole blurred
+    level (blur.hip over those levels, one launch before describe) instead of
+    blurring their own 37x37 patch; "0" keeps every level on the fused patch
+    blur.  A 12-frame batch (8 stream frames, a noise frame, 3 stereo-geometry
+    frames would need another extractor: here 640x480) equals the oracle."""
+    og = _gpu()
+    monkeypatch.setenv("ORBGPU_DESC_LEVEL_BLUR", from_level)
+    frames = np.concatenate([synth.mono_stream(10, 640, 480, seed=77), synth.noise_image()[None],
+                             synth.flat_image()[None]])
+    B = len(frames)
+    ex = og.Extractor(max_batch=B)
+    imgs = torch.from_numpy(np.ascontiguousarray(frames)).cuda()
+    cap = ex.max_keypoints
+    kps = torch.zeros((B, cap, 7), dtype=torch.float32, device="cuda")
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(B, dtype=torch.int32, device="cuda")
+    ex.extract_batch(imgs, kps, desc, counts)
+    ex.sync()
+    ref = orbref.Extractor()
+    kk, dd, cc = kps.cpu().numpy(), desc.cpu().numpy(), counts.cpu().numpy()
+    for b in range(B):
+        kr, dr = ref.extract(frames[b])
+        _assert_same_kps(og.keypoints_from_raw(kk[b, :cc[b]]), dd[b, :cc[b]], kr, dr)
+
+
 def test_timed_headline_batch_512_vs_oracle():
     """The configuration bench.py times, checked at full size:
     two consecutive 512-frame batches of the bench's bounded 640x480 stream at
