@@ -20,6 +20,7 @@
 #include "../../include/orbgpu.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace orbgpu {
@@ -173,12 +174,16 @@ constexpr int kRawWords = kPatch * (kRWidth / 4);   // 43 rows x 12 dwords
 constexpr int kQuads = kBPitch / 4;                 // 10 output quads per blurred row
 constexpr int kColChunks = (kBlur + 6) / 7;         // 6 chunks of <= 7 blurred rows
 
-// The 4 waves of a block process different keypoints: stages are ordered
-// with a wave-local LDS fence, never a block barrier.
+// The 4 waves of a block process different keypoints in LDS regions of their
+// own: stages are ordered within the wave, never with a block barrier.  A
+// wave's DS instructions execute in order, so only the compiler must keep
+// memory operations on their side (the asm's memory clobber) and the wave's
+// own LDS operations are waited for; no VMEM wait (a workgroup-scope fence
+// here waited for every outstanding global access, vmcnt(0): in
+// describe_dma_kernel that is the next keypoint's neighbourhood streaming in).
 __device__ inline void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 __device__ inline int reflect101(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
@@ -210,10 +215,21 @@ __device__ bool key_ref(const Geom& g, int f, int slot, int lane, const uint32_t
     // level and index of the slot: one scalar load; the frame's per-level
     // counts on lanes 0..15 (each 16-lane row holds them all), prefix sums by
     // DPP row shifts, the values this slot needs read out of lane l / 15
-    const uint32_t se = g.slot_tab[slot];
-    const int l = (int)(se & 15u), i = (int)(se >> 4);
+    // the three loads (slot table entry, the slot's key, the frame's per-level
+    // counts) are independent: issued together, waited for once (the empty asm
+    // uses them all, so the compiler can neither sink the key's load behind the
+    // count test nor wait for each load in turn).  A slot past its level's
+    // count reads a stale key that is never used; the counts record has
+    // kOcStride = 16 entries, so every lane's read is in bounds.
+    uint32_t se = g.slot_tab[slot];
+    uint32_t key = oct_out[(size_t)f * g.slots_frame + slot];
     const int ll = lane & 15;
-    const int c = ll < g.nlevels ? oct_count[(size_t)f * kOcStride + ll] : 0;
+    int c = oct_count[(size_t)f * kOcStride + ll];
+    se = (uint32_t)__builtin_amdgcn_readfirstlane((int)se);
+    key = (uint32_t)__builtin_amdgcn_readfirstlane((int)key);
+    asm volatile("" ::"s"(se), "s"(key), "v"(c));
+    c = ll < g.nlevels ? c : 0;
+    const int l = (int)(se & 15u), i = (int)(se >> 4);
     int sc = c;
     sc += __builtin_amdgcn_update_dpp(0, sc, 0x111, 0xF, 0xF, true);  // row_shr:1
     sc += __builtin_amdgcn_update_dpp(0, sc, 0x112, 0xF, 0xF, true);  // row_shr:2
@@ -226,7 +242,7 @@ __device__ bool key_ref(const Geom& g, int f, int slot, int lane, const uint32_t
     K.l = l;
     K.i = i;
     K.before = before;
-    K.key = oct_out[(size_t)f * g.slots_frame + slot];
+    K.key = key;
     K.cx = key_x(K.key) + kBorder;
     K.cy = key_y(K.key) + kBorder;
     return true;
@@ -234,13 +250,24 @@ __device__ bool key_ref(const Geom& g, int f, int slot, int lane, const uint32_t
 
 // Stage the neighbourhood, IC_Angle's moments, the blurred patch into S.blur;
 // returns (m10, m01), wave-uniform.
-__device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, DescLds& S, uint8_t* blur_out,
+// rawbuf: the wave's raw-neighbourhood buffer (kPatch rows of kRPitch bytes);
+// prestaged: it already holds this keypoint's neighbourhood (LDS-DMA, the
+// describe_dma_kernel), else it is staged here.
+__device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, uint8_t* rawbuf, uint8_t* blur_out,
                                const uint8_t* __restrict__ img0, size_t row0, size_t frame0,
-                               const uint8_t* __restrict__ pyr, const uint8_t* __restrict__ lblur, int lblur_from) {
+                               const uint8_t* __restrict__ pyr, bool prestaged = false) {
     const int l = K.l, cx = K.cx, cy = K.cy;
     const LevelGeom& L = g.lv[l];
+#ifdef DESC_PROBE_SAMEFRAME
+    // latency probe (diagnostic build only; wrong results): every keypoint's
+    // neighbourhood comes from frame 0's level 0 (L2-resident)
+    const uint8_t* raw = img0;
+    const size_t rp = row0;
+    (void)frame0;
+#else
     const uint8_t* raw = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
     const size_t rp = l == 0 ? row0 : (size_t)L.pitch;
+#endif
 
     // 1. Stage the raw neighbourhood: rows cy-21 .. cy+21, columns xb-4 ..
     // xb+43 (xb = the blurred patch's 4-aligned first column), reflected at
@@ -251,22 +278,22 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
     const int xb = (cx - kBlurR) & ~3, x0 = xb - 4;
     // a neighbourhood entirely inside the level (wave-uniform; most keypoints): three
     // 16-byte chunks per row, two loads per lane, no reflection
-    if (x0 >= 0 && x0 + kRWidth <= L.w && cy - kPatchR >= 0 && cy + kPatchR < L.h) {
+    if (prestaged) {
+    } else if (x0 >= 0 && x0 + kRWidth <= L.w && cy - kPatchR >= 0 && cy + kPatchR < L.h) {
         constexpr int kChunks = kPatch * (kRWidth / 16);  // 129
         const uint8_t* top = raw + (size_t)(cy - kPatchR) * rp + x0;
         uint4 c[3];
-        uint32_t loff[3];
-        // the dump for lanes past the patch: the wave's last blurred patch,
-        // written only after this staging (earlier keypoints' patches are final)
-        constexpr uint32_t kDump =
-            (uint32_t)((offsetof(DescLds, blur) + (kKeysPerWave - 1) * kBlur * kBPitch + 15) & ~size_t(15));
+        uint8_t* dst[3];
+        // the dump for lanes past the patch: this keypoint's blurred patch,
+        // written only after this staging
+        uint8_t* const dump = blur_out;
         // r = idx / 3 by a 24-bit multiply (exact for idx < 4096), row offsets
         // by 24-bit multiplies (rp < 2^24: launcher check), unsigned 32-bit
         // offsets (no sign extension); lanes past the patch load its last row
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const uint32_t idx = (uint32_t)(lane + 64 * k), r = __umul24(idx, 21846u) >> 16, q = idx - 3u * r;
-            loff[k] = idx < (uint32_t)kChunks ? __umul24(r, (uint32_t)kRPitch) + 16u * q : kDump;
+            dst[k] = idx < (uint32_t)kChunks ? rawbuf + (__umul24(r, (uint32_t)kRPitch) + 16u * q) : dump;
             c[k] = load16_a4(top + (__umul24(min(r, (uint32_t)kPatch - 1u), (uint32_t)rp) + 16u * q));
         }
         // unconditional stores (lanes past the patch write into kDump): no
@@ -274,9 +301,9 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             if constexpr (kRPitch % 16 == 0) {
-                *reinterpret_cast<uint4*>(S.raw + loff[k]) = c[k];
+                *reinterpret_cast<uint4*>(dst[k]) = c[k];
             } else {
-                uint32_t* d = reinterpret_cast<uint32_t*>(S.raw + loff[k]);
+                uint32_t* d = reinterpret_cast<uint32_t*>(dst[k]);
                 d[0] = c[k].x;
                 d[1] = c[k].y;
                 d[2] = c[k].z;
@@ -302,7 +329,7 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
 #pragma unroll
     for (int k = 0; k < kLoads; ++k) {
         const int idx = lane + 64 * k, r = idx / 12, q = idx - r * 12;
-        if (idx < kRawWords) reinterpret_cast<uint32_t*>(S.raw)[r * (kRPitch / 4) + q] = v[k];
+        if (idx < kRawWords) reinterpret_cast<uint32_t*>(rawbuf)[r * (kRPitch / 4) + q] = v[k];
     }
     }
     wave_sync();
@@ -313,7 +340,7 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
     // m10 = Σc·p - (od+15)Σp, m01 = Σ(v+15)·p - 15Σp.  Integer moments:
     // order-free, exact.
     const int xd = (cx - 15) & ~3, od = cx - 15 - xd;
-    const uint8_t* disc = S.raw + (kPatchR - 15) * kRPitch + (xd - x0);
+    const uint8_t* disc = rawbuf + (kPatchR - 15) * kRPitch + (xd - x0);
     uint32_t sp = 0u, cp = 0u, vp = 0u;
 #pragma unroll
     for (int k = 0; k < kDiscLoads; ++k) {
@@ -328,32 +355,6 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
     // modulo-2^32 sums, exact since the totals fit)
     const int m10 = (int)wave_total(cp - (uint32_t)(od + 15) * sp);
     const int m01 = (int)wave_total(vp - 15u * sp);
-
-    // 3a. Levels whose whole blurred level was computed before this launch
-    // (blur.hip over levels >= lblur_from: where the keypoints' 37x37 patches
-    // cover the level several times over, one blur of the level is cheaper than
-    // one per keypoint): the 37 rows of 40 bytes from xb are staged from it --
-    // lane -> (row lane / 10, dword lane % 10), 6 rows per pass at LDS offset
-    // 4 * lane + 240 * pass (lanes 60..63 stage the next pass's first row); the
-    // 7th pass stores row 36 only.  The rows lie inside the level (cy +- 18 with
-    // cy in [19, h - 20]); the 40-byte span may run up to 2 bytes past a row's
-    // end (into its pitch padding, or the buffer's slack).
-    if (l >= lblur_from) {
-        const uint32_t bp = (uint32_t)L.pitch;  // blurred levels: the pyramid's row pitch (level 0 too)
-        const uint8_t* bl = lblur + L.blur_offset + (size_t)f * L.blur_frame_bytes + (size_t)(cy - kBlurR) * bp + xb;
-        const uint32_t rl = __umul24((uint32_t)lane, 6554u) >> 16, q = (uint32_t)lane - 10u * rl;
-        const uint32_t off0 = __umul24(rl, bp) + 4u * q;
-        constexpr int kPasses = (kBlur + 5) / 6;  // 7
-        uint32_t v[kPasses];
-#pragma unroll
-        for (int k = 0; k < kPasses; ++k)
-            v[k] = *reinterpret_cast<const uint32_t*>(bl + (off0 + (uint32_t)(6 * k) * bp));
-#pragma unroll
-        for (int k = 0; k < kPasses; ++k)
-            if (k < kPasses - 1 || lane < 10) *reinterpret_cast<uint32_t*>(blur_out + 4 * lane + 6 * kBPitch * k) = v[k];
-        static_assert(kBPitch == 40 && 6 * (kPasses - 1) == kBlur - 1, "blurred patch staging map");
-        return int2{m10, m01};
-    }
 
     // 3. Blur (blur_device.h, the arithmetic of blur.hip) of the 37x37 patch:
     // lane = (output quad q, chunk c of 7 blurred rows); row passes from the
@@ -381,7 +382,7 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
         const uint32_t raw0 = __umul24((uint32_t)r0, (uint32_t)kRPitch) + 4u * (uint32_t)q;
         const uint32_t out0 = __umul24((uint32_t)r0, (uint32_t)kBPitch) + 4u * (uint32_t)q;
         auto row = [&](int k, blurdev::f32x2& lo, blurdev::f32x2& hi) {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(S.raw + raw0 + k * kRPitch);
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(rawbuf + raw0 + k * kRPitch);
             blurdev::Raw3 R3;
             R3.a = w[0];
             R3.b = w[1];
@@ -488,6 +489,9 @@ __device__ unsigned long long g_desc_stamps[16];
 #define DSTAMP(k) ((void)0)
 #endif
 
+#ifndef ORBGPU_DESC_REVERSE
+#define ORBGPU_DESC_REVERSE 0
+#endif
 #ifndef ORBGPU_DESC_WAVES
 #define ORBGPU_DESC_WAVES 4
 #endif
@@ -505,8 +509,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
                                                                    uint8_t* __restrict__ desc,
                                                                    int* __restrict__ counts, int kp_cap,
                                                                    int* __restrict__ err_word,
-                                                                   int* __restrict__ err_copy,
-                                                                   const uint8_t* __restrict__ lblur, int lblur_from) {
+                                                                   int* __restrict__ err_copy) {
     __shared__ DescLds s_lds[kDescWaves];
     // single-frame path: the error word of this extraction (FAST / octree ran
     // before on the stream) moves into the output block and is cleared, so
@@ -526,7 +529,14 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
 #endif
     DSTAMP(0);
     const int per_frame = (g.slots_frame + kKeysPerWave - 1) / kKeysPerWave;
-    const int fl = item / per_frame, slot0 = (item - fl * per_frame) * kKeysPerWave;
+    const int fi = item / per_frame, slot0 = (item - fi * per_frame) * kKeysPerWave;
+    // frames in reverse order (ORBGPU_DESC_REVERSE): the ones the kernels before
+    // touched last first
+#if ORBGPU_DESC_REVERSE
+    const int fl = items / per_frame - 1 - fi;
+#else
+    const int fl = fi;
+#endif
     const int f = f0 + fl;  // frame of the whole batch (a chunk's launch starts at frame f0)
     if (item >= items) return;
     KeyRef K[kKeysPerWave];
@@ -573,8 +583,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
         if (k > 0) wave_sync();  // the previous keypoint's blur has read the raw buffer
         int lane_k = lane;
         asm volatile("" : "+v"(lane_k));  // per iteration: no lane-derived invariant is hoisted out (VGPRs 82 -> 50)
-        const int2 mm = describe_patch(g, f, Kk, lane_k, s_lds[wave], s_lds[wave].blur[k], img0, row0, frame0, pyr,
-                                       lblur, lblur_from);
+        const int2 mm = describe_patch(g, f, Kk, lane_k, s_lds[wave].raw, s_lds[wave].blur[k], img0, row0, frame0, pyr);
         if (kKeysPerWave == 1 || lane == k) {  // one keypoint: wave-uniform moments, uniform branches below
             mx = mm.x;
             my = mm.y;
@@ -607,6 +616,117 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// describe with the neighbourhood load latency hidden inside the wave
+// (ORBGPU_DESC_DMA = keypoint slots per wave, read per launch; 0: describe_kernel).
+// A wave walks `kpw` consecutive slots of a frame; the raw 43x48 neighbourhood
+// of slot k+1 streams into the other of two LDS buffers by LDS-DMA
+// (global_load_lds_dwordx4: lane l's 16 bytes land at buffer + 16 l, so pass p
+// of 64 lanes fills rows 21p .. 21p+20 -- the layout of the register staging;
+// the last pass is row 42's three chunks on lanes 0..2) while slot k's moments,
+// blur and tests run from its buffer.  A neighbourhood that crosses the level
+// border (BORDER_REFLECT_101 bytes) is staged through registers as before.
+struct alignas(16) DescLdsDma {
+    uint8_t raw[2][kPatch * kRPitch];
+    uint8_t blur[kBlur * kBPitch];
+};
+static_assert(kRPitch == 48 && kRWidth == 48, "the DMA layout assumes 48-byte raw rows");
+typedef __attribute__((address_space(3))) void desc_lds_void;
+
+__device__ __forceinline__ const uint8_t* desc_uniform_ptr(const uint8_t* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return (const uint8_t*)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ bool key_in_level(const Geom& g, const KeyRef& K) {
+    const LevelGeom& L = g.lv[K.l];
+    const int x0 = ((K.cx - kBlurR) & ~3) - 4;
+    return x0 >= 0 && x0 + kRWidth <= L.w && K.cy - kPatchR >= 0 && K.cy + kPatchR < L.h;
+}
+
+constexpr int kRawDmaOps = 3;  // DMA instructions per neighbourhood (vmcnt)
+
+__device__ __forceinline__ void raw_dma_issue(const Geom& g, int f, const KeyRef& K, int lane, uint8_t* rawbuf,
+                                              const uint8_t* __restrict__ img0, size_t row0, size_t frame0,
+                                              const uint8_t* __restrict__ pyr) {
+    const LevelGeom& L = g.lv[K.l];
+    const uint8_t* raw = K.l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
+    const uint32_t rp = K.l == 0 ? (uint32_t)row0 : (uint32_t)L.pitch;
+    const int x0 = ((K.cx - kBlurR) & ~3) - 4;
+    const uint8_t* top = desc_uniform_ptr(raw + (size_t)(K.cy - kPatchR) * rp + x0);
+    const uint32_t rl = __umul24((uint32_t)lane, 21846u) >> 16, q = (uint32_t)lane - 3u * rl;  // lane / 3, lane % 3
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(top + (__umul24(rl + 21u * p, rp) + 16u * q)),
+                                         (desc_lds_void*)(rawbuf + p * 21 * kRPitch), 16, 0, 0);
+    if (lane < 3)  // row 42 (lane 63 of pass 1 already wrote its first chunk)
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(top + (__umul24(42u, rp) + 16u * (uint32_t)lane)),
+                                         (desc_lds_void*)(rawbuf + 42 * kRPitch), 16, 0, 0);
+}
+
+__global__ __launch_bounds__(64 * kDescWaves) void describe_dma_kernel(Geom g, int items, int kpw, int f0,
+                                                                       const uint8_t* __restrict__ img0, size_t row0,
+                                                                       size_t frame0, const uint8_t* __restrict__ pyr,
+                                                                       const uint32_t* __restrict__ oct_out,
+                                                                       const int* __restrict__ oct_count,
+                                                                       orbgpu_keypoint* __restrict__ kps,
+                                                                       uint8_t* __restrict__ desc,
+                                                                       int* __restrict__ counts, int kp_cap,
+                                                                       int* __restrict__ err_word,
+                                                                       int* __restrict__ err_copy) {
+    __shared__ DescLdsDma s_lds[kDescWaves];
+    if (err_copy && blockIdx.x == 0 && threadIdx.x == 0) *err_copy = atomicExch(err_word, 0);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if ORBGPU_DESC_SWIZZLE
+    const int blk = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
+#else
+    const int blk = (int)blockIdx.x;
+#endif
+    const int item = blk * kDescWaves + wave;  // this wave: slots [slot0, slot0 + kpw) of one frame
+    if (item >= items) return;
+    const int per_frame = (g.slots_frame + kpw - 1) / kpw;
+    const int fi = item / per_frame, slot0 = (item - fi * per_frame) * kpw;
+    const int f = f0 + fi;
+    const int n = min(kpw, g.slots_frame - slot0);
+    DescLdsDma& S = s_lds[wave];
+    KeyRef cur;
+    bool vcur = key_ref(g, f, slot0, lane, oct_out, oct_count, counts, cur);
+    bool dcur = vcur && key_in_level(g, cur);
+    if (dcur) raw_dma_issue(g, f, cur, lane, S.raw[0], img0, row0, frame0, pyr);
+    for (int k = 0; k < n; ++k) {
+        KeyRef nxt;
+        bool vn = false, dn = false;
+        if (k + 1 < n) {
+            vn = key_ref(g, f, slot0 + k + 1, lane, oct_out, oct_count, counts, nxt);
+            dn = vn && key_in_level(g, nxt);
+            if (dn) raw_dma_issue(g, f, nxt, lane, S.raw[(k + 1) & 1], img0, row0, frame0, pyr);
+        }
+        if (vcur) {
+            // this slot's neighbourhood has landed: only the next slot's loads may remain
+            if (dn)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRawDmaOps) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            int lane_k = lane;
+            asm volatile("" : "+v"(lane_k));
+            const int2 mm = describe_patch(g, f, cur, lane_k, S.raw[k & 1], S.blur, img0, row0, frame0, pyr, dcur);
+            const float ang = fast_atan2((float)mm.y, (float)mm.x);
+            float sa, ca;
+            glibc_sincosf(__fmul_rn(ang, (float)(M_PI / 180.f)), &sa, &ca);
+            wave_sync();  // blurred patch complete
+            describe_tests(g, f, cur, lane, S.blur, float4{ang, ca, sa, 0.f}, kps, desc, kp_cap);
+            wave_sync();  // the blurred patch is rewritten by the next slot
+        }
+        cur = nxt;
+        vcur = vn;
+        dcur = dn;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outstanding at exit
+}
+
 }  // namespace
 
 #ifdef DESC_STAMPS
@@ -620,17 +740,29 @@ extern "C" int orbgpu_debug_desc_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
+// slots per wave of describe_dma_kernel (ORBGPU_DESC_DMA, read per launch; 0 or unset: describe_kernel)
+static int desc_dma_slots() {
+    const char* s = std::getenv("ORBGPU_DESC_DMA");
+    const int v = s ? std::atoi(s) : 0;
+    return v < 0 ? 0 : (v > 64 ? 64 : v);
+}
+
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                            const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
-                           hipStream_t stream, int* err_word, int* err_copy, int f0, const uint8_t* lblur,
-                           int lblur_from) {
-    const int items = (g.slots_frame + kKeysPerWave - 1) / kKeysPerWave * batch;  // waves (frames f0 .. f0+batch-1)
+                           hipStream_t stream, int* err_word, int* err_copy, int f0) {
     if (row0 >= (1u << 24)) return hipErrorInvalidValue;  // row offsets by 24-bit multiplies
+    if (const int kpw = desc_dma_slots()) {
+        const int waves = (g.slots_frame + kpw - 1) / kpw * batch;
+        hipLaunchKernelGGL(describe_dma_kernel, dim3((waves + kDescWaves - 1) / kDescWaves), dim3(64 * kDescWaves), 0,
+                           stream, g, waves, kpw, f0, img0, row0, frame0, pyr, oct_out, oct_count, kps, desc, counts,
+                           kp_cap, err_word, err_copy);
+        return hipGetLastError();
+    }
+    const int items = (g.slots_frame + kKeysPerWave - 1) / kKeysPerWave * batch;  // waves (frames f0 .. f0+batch-1)
     const int blocks = (items + kDescWaves - 1) / kDescWaves;
     hipLaunchKernelGGL(describe_kernel, dim3(blocks), dim3(64 * kDescWaves), 0, stream, g, items, f0, img0, row0, frame0,
-                       pyr, oct_out, oct_count, kps, desc, counts, kp_cap, err_word, err_copy, lblur,
-                       lblur ? lblur_from : kMaxLevels);
+                       pyr, oct_out, oct_count, kps, desc, counts, kp_cap, err_word, err_copy);
     return hipGetLastError();
 }
 

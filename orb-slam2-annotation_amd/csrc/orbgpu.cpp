@@ -481,24 +481,6 @@ bool pyr_bands_off() {
     return v;
 }
 
-// first level whose keypoints describe reads from the whole blurred level
-// (blur.hip over levels >= it, one launch before describe) instead of blurring
-// each keypoint's 37x37 patch: ORBGPU_DESC_LEVEL_BLUR = L in [1, nlevels) takes
-// levels >= L that way (any other value: none); unset, batches above the
-// small-batch pyramid limit take kDescLevelBlur (the drop-in single frame: none)
-#ifndef ORBGPU_DESC_LEVEL_BLUR_DEFAULT
-#define ORBGPU_DESC_LEVEL_BLUR_DEFAULT 3
-#endif
-int desc_level_blur(int batch, int nlevels) {  // read per batch (tests switch it within one process)
-    const char* s = std::getenv("ORBGPU_DESC_LEVEL_BLUR");
-    if (s) {
-        const int v = std::atoi(s);
-        return v >= 1 && v < nlevels ? v : nlevels;
-    }
-    const int d = ORBGPU_DESC_LEVEL_BLUR_DEFAULT;
-    return batch > pyr_levels_max_batch() && d >= 1 && d < nlevels ? d : nlevels;
-}
-
 int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_step, size_t frame_step,
               orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap, hipStream_t s, int* err_copy = nullptr) {
     const Geom& g = e->g;
@@ -526,24 +508,16 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
     if (evs) ORB_HIP(hipEventRecord(evs[2], s));
     if (e->stage_ev[1]) ORB_HIP(hipEventRecord(e->stage_ev[1], s));
     const int nch = (err_copy || batch < 16 * od_chunks()) ? 1 : od_chunks();
-    // the upper levels' whole-level blur (describe samples it), after the octree
-    const int lbf = desc_level_blur(batch, e->nlevels);
-    if (lbf < e->nlevels && !e->d_blur) {
-        int rc = dalloc(&e->d_blur, e->blur_bytes);
-        if (rc) return rc;
-    }
-    const uint8_t* lblur = lbf < e->nlevels ? e->d_blur : nullptr;
     if (nch == 1) {
         ORB_HIP(launch_octree(g, batch, e->d_cand, e->d_cell_counts, e->d_gkeys, e->d_gknode, e->d_oct_out,
                               e->d_oct_count, e->d_err, e->oct_groups, 2, e->d_trace, s));
         if (evs) ORB_HIP(hipEventRecord(evs[3], s));
         if (e->stage_ev[2]) ORB_HIP(hipEventRecord(e->stage_ev[2], s));
-        // GaussianBlur: the levels below lbf fused into describe (blur of each
-        // keypoint's patch), the levels from lbf blurred whole just before it
-        if (lblur)
-            ORB_HIP(launch_blur_levels(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_blur, s, lbf));
+        // GaussianBlur is fused into describe (blur of each keypoint's patch);
+        // whole blurred levels exist only for the debug API (round 5: blurring
+        // the upper levels whole and sampling them was slower)
         ORB_HIP(launch_describe(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_oct_out, e->d_oct_count, kps,
-                                desc, counts, kp_cap, s, err_copy ? e->d_err : nullptr, err_copy, 0, lblur, lbf));
+                                desc, counts, kp_cap, s, err_copy ? e->d_err : nullptr, err_copy));
     } else {
         // the octree chunks in order on s, each chunk's describe on the aux stream after
         // its octree: describe(c) overlaps octree(c+1); s joins the aux stream at the end
@@ -554,8 +528,6 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
             for (hipEvent_t& x : e->od_ev) ORB_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
         }
         hipStream_t a = e->aux_stream;
-        if (lblur)
-            ORB_HIP(launch_blur_levels(g, batch, imgs, row_step, frame_step, e->d_pyr, e->d_blur, s, lbf));
         for (int c = 0; c < nch; ++c) {
             const int f0 = batch * c / nch, f1 = batch * (c + 1) / nch, nb = f1 - f0;
             ORB_HIP(launch_octree(g, nb, e->d_cand + (size_t)f0 * g.cand_frame,
@@ -569,7 +541,7 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
             ORB_HIP(hipEventRecord(e->od_ev[c], s));
             ORB_HIP(hipStreamWaitEvent(a, e->od_ev[c], 0));
             ORB_HIP(launch_describe(g, nb, imgs, row_step, frame_step, e->d_pyr, e->d_oct_out, e->d_oct_count, kps,
-                                    desc, counts, kp_cap, a, nullptr, nullptr, f0, lblur, lbf));
+                                    desc, counts, kp_cap, a, nullptr, nullptr, f0));
         }
         if (e->stage_ev[2]) ORB_HIP(hipEventRecord(e->stage_ev[2], s));
         ORB_HIP(hipEventRecord(e->od_ev[8], a));

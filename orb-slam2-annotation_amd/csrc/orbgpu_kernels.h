@@ -42,8 +42,7 @@ hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size
                              const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err,
                              hipStream_t stream);
 
-// level_from: blur levels level_from .. nlevels-1 only (describe's whole-level
-// blur of the upper levels); 0 = every level (the debug API)
+// level_from: blur levels level_from .. nlevels-1 only; 0 = every level (the debug API)
 hipError_t launch_blur_levels(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                               const uint8_t* pyr, uint8_t* blur, hipStream_t stream, int level_from = 0);
 
@@ -60,8 +59,7 @@ hipError_t launch_octree(const Geom& g, int batch, const uint32_t* cand, const i
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                            const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
-                           hipStream_t stream, int* err_word = nullptr, int* err_copy = nullptr, int f0 = 0,
-                           const uint8_t* lblur = nullptr, int lblur_from = kMaxLevels);
+                           hipStream_t stream, int* err_word = nullptr, int* err_copy = nullptr, int f0 = 0);
 
 // The stream form of SearchForInitialization (orbgpu_search_for_initialization_stream_device):
 // with kps set, pair b takes F1 = frame b - 1 of the F1 arrays and pair 0 this frame

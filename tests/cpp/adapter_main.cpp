@@ -984,8 +984,8 @@ int main(int argc, char** argv) {
         // created (first frame); prints the device the handle reports
         try {
             ORB_SLAM2::ORBextractor ex(500, 1.2f, 8, 20, 7, atoi(argv[2]));
-            std::vector<unsigned char> buf(64 * 64, 128);
-            cv::Mat img(64, 64, CV_8UC1, buf.data(), (size_t)64);
+            std::vector<unsigned char> buf(640 * 480, 128);
+            cv::Mat img(480, 640, CV_8UC1, buf.data(), (size_t)640);
             std::vector<cv::KeyPoint> k;
             cv::Mat d;
             ex(img, cv::Mat(), k, d);
@@ -1094,6 +1094,19 @@ int main(int argc, char** argv) {
             timed("ComputeStereoMatches", [] {}, [&] {
                 ORB_SLAM2::ComputeStereoMatchesGPU(&exL, &exR, kL, dL, kR, dR, bf, 0.0f, uR, dep);
             }, "Frame.cpp:540-748 on the HBM pyramids");
+            // attribution of the stereo Frame's tail: the two threads' spawn + join alone
+            // (the reference starts two threads per Frame), and the same work with no threads
+            timed("stereo Frame: thread pair spawn + join, no work", [] {}, [] {
+                std::thread tl([] {});
+                std::thread tr([] {});
+                tl.join();
+                tr.join();
+            }, "the std::thread pair of Frame.cpp:84-87 without the extractions");
+            timed("stereo Frame: ORBextractor L then R on one thread + ComputeStereoMatches", [] {}, [&] {
+                exL(imL, cv::Mat(), kL, dL);
+                exR(imR, cv::Mat(), kR, dR);
+                ORB_SLAM2::ComputeStereoMatchesGPU(&exL, &exR, kL, dL, kR, dR, bf, 0.0f, uR, dep);
+            }, "no threads: the two extractions back to back");
             FILE* out = fopen(argv[8], "wb");
             for (int f = 0; f < 2; ++f) {
                 const std::vector<cv::KeyPoint>& k = f ? kR : kL;
