@@ -179,8 +179,7 @@ constexpr int kColChunks = (kBlur + 6) / 7;         // 6 chunks of <= 7 blurred 
 // wave's DS instructions execute in order, so only the compiler must keep
 // memory operations on their side (the asm's memory clobber) and the wave's
 // own LDS operations are waited for; no VMEM wait (a workgroup-scope fence
-// here waited for every outstanding global access, vmcnt(0): in
-// describe_dma_kernel that is the next keypoint's neighbourhood streaming in).
+// here waited for every outstanding global access, vmcnt(0), stores included).
 __device__ inline void wave_sync() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -250,12 +249,10 @@ __device__ bool key_ref(const Geom& g, int f, int slot, int lane, const uint32_t
 
 // Stage the neighbourhood, IC_Angle's moments, the blurred patch into S.blur;
 // returns (m10, m01), wave-uniform.
-// rawbuf: the wave's raw-neighbourhood buffer (kPatch rows of kRPitch bytes);
-// prestaged: it already holds this keypoint's neighbourhood (LDS-DMA, the
-// describe_dma_kernel), else it is staged here.
+// rawbuf: the wave's raw-neighbourhood buffer (kPatch rows of kRPitch bytes).
 __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, uint8_t* rawbuf, uint8_t* blur_out,
                                const uint8_t* __restrict__ img0, size_t row0, size_t frame0,
-                               const uint8_t* __restrict__ pyr, bool prestaged = false) {
+                               const uint8_t* __restrict__ pyr) {
     const int l = K.l, cx = K.cx, cy = K.cy;
     const LevelGeom& L = g.lv[l];
 #ifdef DESC_PROBE_SAMEFRAME
@@ -278,8 +275,7 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
     const int xb = (cx - kBlurR) & ~3, x0 = xb - 4;
     // a neighbourhood entirely inside the level (wave-uniform; most keypoints): three
     // 16-byte chunks per row, two loads per lane, no reflection
-    if (prestaged) {
-    } else if (x0 >= 0 && x0 + kRWidth <= L.w && cy - kPatchR >= 0 && cy + kPatchR < L.h) {
+    if (x0 >= 0 && x0 + kRWidth <= L.w && cy - kPatchR >= 0 && cy + kPatchR < L.h) {
         constexpr int kChunks = kPatch * (kRWidth / 16);  // 129
         const uint8_t* top = raw + (size_t)(cy - kPatchR) * rp + x0;
         uint4 c[3];
@@ -616,117 +612,6 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
 #endif
 }
 
-// ---------------------------------------------------------------------------
-// describe with the neighbourhood load latency hidden inside the wave
-// (ORBGPU_DESC_DMA = keypoint slots per wave, read per launch; 0: describe_kernel).
-// A wave walks `kpw` consecutive slots of a frame; the raw 43x48 neighbourhood
-// of slot k+1 streams into the other of two LDS buffers by LDS-DMA
-// (global_load_lds_dwordx4: lane l's 16 bytes land at buffer + 16 l, so pass p
-// of 64 lanes fills rows 21p .. 21p+20 -- the layout of the register staging;
-// the last pass is row 42's three chunks on lanes 0..2) while slot k's moments,
-// blur and tests run from its buffer.  A neighbourhood that crosses the level
-// border (BORDER_REFLECT_101 bytes) is staged through registers as before.
-struct alignas(16) DescLdsDma {
-    uint8_t raw[2][kPatch * kRPitch];
-    uint8_t blur[kBlur * kBPitch];
-};
-static_assert(kRPitch == 48 && kRWidth == 48, "the DMA layout assumes 48-byte raw rows");
-typedef __attribute__((address_space(3))) void desc_lds_void;
-
-__device__ __forceinline__ const uint8_t* desc_uniform_ptr(const uint8_t* p) {
-    const uint64_t v = (uint64_t)p;
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-    return (const uint8_t*)(((uint64_t)hi << 32) | lo);
-}
-
-__device__ __forceinline__ bool key_in_level(const Geom& g, const KeyRef& K) {
-    const LevelGeom& L = g.lv[K.l];
-    const int x0 = ((K.cx - kBlurR) & ~3) - 4;
-    return x0 >= 0 && x0 + kRWidth <= L.w && K.cy - kPatchR >= 0 && K.cy + kPatchR < L.h;
-}
-
-constexpr int kRawDmaOps = 3;  // DMA instructions per neighbourhood (vmcnt)
-
-__device__ __forceinline__ void raw_dma_issue(const Geom& g, int f, const KeyRef& K, int lane, uint8_t* rawbuf,
-                                              const uint8_t* __restrict__ img0, size_t row0, size_t frame0,
-                                              const uint8_t* __restrict__ pyr) {
-    const LevelGeom& L = g.lv[K.l];
-    const uint8_t* raw = K.l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
-    const uint32_t rp = K.l == 0 ? (uint32_t)row0 : (uint32_t)L.pitch;
-    const int x0 = ((K.cx - kBlurR) & ~3) - 4;
-    const uint8_t* top = desc_uniform_ptr(raw + (size_t)(K.cy - kPatchR) * rp + x0);
-    const uint32_t rl = __umul24((uint32_t)lane, 21846u) >> 16, q = (uint32_t)lane - 3u * rl;  // lane / 3, lane % 3
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-        __builtin_amdgcn_global_load_lds(static_cast<const void*>(top + (__umul24(rl + 21u * p, rp) + 16u * q)),
-                                         (desc_lds_void*)(rawbuf + p * 21 * kRPitch), 16, 0, 0);
-    if (lane < 3)  // row 42 (lane 63 of pass 1 already wrote its first chunk)
-        __builtin_amdgcn_global_load_lds(static_cast<const void*>(top + (__umul24(42u, rp) + 16u * (uint32_t)lane)),
-                                         (desc_lds_void*)(rawbuf + 42 * kRPitch), 16, 0, 0);
-}
-
-__global__ __launch_bounds__(64 * kDescWaves) void describe_dma_kernel(Geom g, int items, int kpw, int f0,
-                                                                       const uint8_t* __restrict__ img0, size_t row0,
-                                                                       size_t frame0, const uint8_t* __restrict__ pyr,
-                                                                       const uint32_t* __restrict__ oct_out,
-                                                                       const int* __restrict__ oct_count,
-                                                                       orbgpu_keypoint* __restrict__ kps,
-                                                                       uint8_t* __restrict__ desc,
-                                                                       int* __restrict__ counts, int kp_cap,
-                                                                       int* __restrict__ err_word,
-                                                                       int* __restrict__ err_copy) {
-    __shared__ DescLdsDma s_lds[kDescWaves];
-    if (err_copy && blockIdx.x == 0 && threadIdx.x == 0) *err_copy = atomicExch(err_word, 0);
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if ORBGPU_DESC_SWIZZLE
-    const int blk = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
-#else
-    const int blk = (int)blockIdx.x;
-#endif
-    const int item = blk * kDescWaves + wave;  // this wave: slots [slot0, slot0 + kpw) of one frame
-    if (item >= items) return;
-    const int per_frame = (g.slots_frame + kpw - 1) / kpw;
-    const int fi = item / per_frame, slot0 = (item - fi * per_frame) * kpw;
-    const int f = f0 + fi;
-    const int n = min(kpw, g.slots_frame - slot0);
-    DescLdsDma& S = s_lds[wave];
-    KeyRef cur;
-    bool vcur = key_ref(g, f, slot0, lane, oct_out, oct_count, counts, cur);
-    bool dcur = vcur && key_in_level(g, cur);
-    if (dcur) raw_dma_issue(g, f, cur, lane, S.raw[0], img0, row0, frame0, pyr);
-    for (int k = 0; k < n; ++k) {
-        KeyRef nxt;
-        bool vn = false, dn = false;
-        if (k + 1 < n) {
-            vn = key_ref(g, f, slot0 + k + 1, lane, oct_out, oct_count, counts, nxt);
-            dn = vn && key_in_level(g, nxt);
-            if (dn) raw_dma_issue(g, f, nxt, lane, S.raw[(k + 1) & 1], img0, row0, frame0, pyr);
-        }
-        if (vcur) {
-            // this slot's neighbourhood has landed: only the next slot's loads may remain
-            if (dn)
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRawDmaOps) : "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            int lane_k = lane;
-            asm volatile("" : "+v"(lane_k));
-            const int2 mm = describe_patch(g, f, cur, lane_k, S.raw[k & 1], S.blur, img0, row0, frame0, pyr, dcur);
-            const float ang = fast_atan2((float)mm.y, (float)mm.x);
-            float sa, ca;
-            glibc_sincosf(__fmul_rn(ang, (float)(M_PI / 180.f)), &sa, &ca);
-            wave_sync();  // blurred patch complete
-            describe_tests(g, f, cur, lane, S.blur, float4{ang, ca, sa, 0.f}, kps, desc, kp_cap);
-            wave_sync();  // the blurred patch is rewritten by the next slot
-        }
-        cur = nxt;
-        vcur = vn;
-        dcur = dn;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outstanding at exit
-}
-
 }  // namespace
 
 #ifdef DESC_STAMPS
@@ -740,25 +625,11 @@ extern "C" int orbgpu_debug_desc_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
-// slots per wave of describe_dma_kernel (ORBGPU_DESC_DMA, read per launch; 0 or unset: describe_kernel)
-static int desc_dma_slots() {
-    const char* s = std::getenv("ORBGPU_DESC_DMA");
-    const int v = s ? std::atoi(s) : 0;
-    return v < 0 ? 0 : (v > 64 ? 64 : v);
-}
-
 hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                            const uint8_t* pyr, const uint32_t* oct_out, const int* oct_count,
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
                            hipStream_t stream, int* err_word, int* err_copy, int f0) {
     if (row0 >= (1u << 24)) return hipErrorInvalidValue;  // row offsets by 24-bit multiplies
-    if (const int kpw = desc_dma_slots()) {
-        const int waves = (g.slots_frame + kpw - 1) / kpw * batch;
-        hipLaunchKernelGGL(describe_dma_kernel, dim3((waves + kDescWaves - 1) / kDescWaves), dim3(64 * kDescWaves), 0,
-                           stream, g, waves, kpw, f0, img0, row0, frame0, pyr, oct_out, oct_count, kps, desc, counts,
-                           kp_cap, err_word, err_copy);
-        return hipGetLastError();
-    }
     const int items = (g.slots_frame + kKeysPerWave - 1) / kKeysPerWave * batch;  // waves (frames f0 .. f0+batch-1)
     const int blocks = (items + kDescWaves - 1) / kDescWaves;
     hipLaunchKernelGGL(describe_kernel, dim3(blocks), dim3(64 * kDescWaves), 0, stream, g, items, f0, img0, row0, frame0,

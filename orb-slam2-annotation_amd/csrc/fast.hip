@@ -45,10 +45,17 @@ __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
 }
 
 // Window staging geometry (fast_cells_kernel): chunks of CB bytes, NC per
-// P-byte row, RPI rows per pass of 64 lanes, kGroup passes' loads in flight.
+// P-byte row, RPI rows per pass of 64 lanes, kGroup passes' loads in flight:
+// a window of up to 42 rows is one group, i.e. one memory round trip (P = 40,
+// the 640x480 case, took 7 dword passes in two serial groups of 4 before
+// ORBGPU_FAST_CHUNK8; now 4 passes of 8-byte chunks, 8 VGPRs).
+#ifndef ORBGPU_FAST_CHUNK8
+#define ORBGPU_FAST_CHUNK8 1
+#endif
 template <int P>
 struct FastStage {
-    static constexpr int CB = P % 16 == 0 ? 16 : 4, NC = P / CB, RPI = 64 / NC, kGroup = CB == 16 ? 2 : 4;
+    static constexpr int CB = P % 16 == 0 ? 16 : (ORBGPU_FAST_CHUNK8 && P % 8 == 0 ? 8 : 4), NC = P / CB,
+                         RPI = 64 / NC, kGroup = ORBGPU_FAST_CHUNK8 ? (42 + RPI - 1) / RPI : (CB == 16 ? 2 : 4);
 };
 // LDS rows the staging writes for windows of up to R rows (at most): its
 // passes plus the row the lanes past RPI * NC stage; they must fit in the
@@ -65,8 +72,7 @@ constexpr int fast_stage_rows(int R) {
 // reads: only the compiler must keep memory operations on their side of this
 // point (the asm's memory clobber), plus a wait for the wave's own LDS
 // operations.  No VMEM wait: a workgroup-scope fence here waited for every
-// outstanding global access (vmcnt(0)), which in the LDS-DMA kernel is the
-// next cell's window still streaming in.
+// outstanding global access (vmcnt(0)), stores included.
 __device__ inline void wave_sync() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -504,7 +510,8 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
         const uint32_t col = (uint32_t)(CB * min(q, ncneed - 1));
         const int passes = (wh + RPI - 1) / RPI;  // wave-uniform
         uint8_t* dst = s_win + CB * lane;
-        typedef typename std::conditional<CB == 16, uint4, uint32_t>::type Chunk;
+        typedef typename std::conditional<CB == 16, uint4, typename std::conditional<CB == 8, uint2, uint32_t>::type>::type
+            Chunk;
 #pragma unroll 1
         for (int p0 = 0; p0 < passes; p0 += kGroup) {
             Chunk v[kGroup];
@@ -518,6 +525,8 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
 #endif
                 if constexpr (CB == 16)
                     v[k] = load16_a4(src);
+                else if constexpr (CB == 8)
+                    v[k] = load8_a4(src);
                 else
                     v[k] = *reinterpret_cast<const uint32_t*>(src);
             }
@@ -602,160 +611,6 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
 #endif
 }
 
-// ---------------------------------------------------------------------------
-// The same FAST per cell with the window load latency hidden inside the wave
-// (ORBGPU_FAST_DMA = cells per wave, read per launch; 0: fast_cells_kernel).
-// Each wave walks `cpw` consecutive cells.  The window of cell i+1 streams into
-// the other of two LDS buffers by LDS-DMA (global_load_lds: each lane's chunk
-// lands at buffer + CB * lane + pass * RPI * P, the staging layout above, and
-// no VGPR holds it) while cell i is computed from its buffer; a counted vmcnt
-// then waits for exactly cell i+1's loads.  Measured motivation: with every
-// window L2-resident (FAST_PROBE_SAMEWIN) fast_cells ran 0.408 instead of
-// 0.518 ms, i.e. a fifth of the kernel was window-load latency that the other
-// resident waves did not cover.  Costs: a second window buffer per wave (fewer
-// resident waves) and a shorter survivor list (more row bands).
-template <int P>
-struct FastDma {
-    using S = FastStage<P>;
-    static constexpr int kMaxRows = 42;                               // win_rows bound (launcher check)
-    static constexpr int NPASS = (kMaxRows + S::RPI - 1) / S::RPI;    // DMA instructions per window
-    static constexpr int WROWS = NPASS * S::RPI + 1;                  // rows a buffer receives (+1: lanes past RPI*NC)
-    static constexpr int WBYTES = (WROWS * P + 15) & ~15;
-};
-#ifndef ORBGPU_FAST_DMA_WAVE_LDS
-#define ORBGPU_FAST_DMA_WAVE_LDS 6816  // LDS per cell wave: 24 waves per CU
-#endif
-// survivor-list entries of the DMA kernel's waves: what the per-wave budget
-// leaves after two window buffers and the score tile (>= 256, else 0: unsupported)
-__host__ __device__ constexpr int fast_dma_list_len(int P, int R, int det_max, int wbytes) {
-    const int c = ((ORBGPU_FAST_DMA_WAVE_LDS - 2 * wbytes - P * R - 16) / 2 - 1) & ~7;
-    return c >= det_max ? det_max : (c >= 256 ? c : 0);
-}
-
-typedef __attribute__((address_space(3))) void fast_lds_void;
-
-struct FastCellGeo {
-    int f, gc, l, ci, cj, iniX, iniY, maxX, wh, xa, ox;
-    bool empty;
-    const uint8_t* wbase;  // window row 0 at column xa (wave-uniform)
-    uint32_t pitch;
-};
-
-__device__ __forceinline__ FastCellGeo fast_cell_geo(const Geom& g, int item, const uint8_t* __restrict__ img0,
-                                                     size_t row0, size_t frame0, const uint8_t* __restrict__ pyr) {
-    FastCellGeo c;
-    c.f = item / g.total_cells;
-    c.gc = item - c.f * g.total_cells;
-    const uint32_t ce = g.cell_tab[c.gc];
-    c.l = (int)(ce & 15u);
-    c.ci = (int)((ce >> 4) & 0x3FFFu);
-    c.cj = (int)(ce >> 18);
-    const LevelGeom& L = g.lv[c.l];
-    c.iniY = kBorder + c.ci * L.hcell;
-    c.iniX = kBorder + c.cj * L.wcell;
-    c.empty = c.iniY >= L.max_by - 3 || c.iniX >= L.max_bx - 6;
-    const int maxY = min(c.iniY + L.hcell + 6, L.max_by);
-    c.maxX = min(c.iniX + L.wcell + 6, L.max_bx);
-    c.wh = maxY - c.iniY;
-    c.xa = c.iniX & ~3;
-    c.ox = c.iniX - c.xa;
-    const uint8_t* base = c.l == 0 ? img0 + (size_t)c.f * frame0 : pyr + L.offset + (size_t)c.f * L.frame_bytes;
-    c.pitch = c.l == 0 ? (uint32_t)row0 : (uint32_t)L.pitch;
-    c.wbase = uniform_ptr(base + (size_t)c.iniY * c.pitch + c.xa);
-    return c;
-}
-
-// the window of cell c into `buf` by LDS-DMA: NPASS instructions, rows past the
-// window re-read its last row, chunks past its last needed one re-read that one
-template <int P>
-__device__ __forceinline__ void fast_dma_issue(const FastCellGeo& c, uint8_t* buf, int lane) {
-    using S = FastStage<P>;
-    const int rl = lane / S::NC, q = lane - rl * S::NC;
-    const int ncneed = (c.maxX - c.xa + S::CB - 1) / S::CB;
-    const uint32_t col = (uint32_t)(S::CB * min(q, ncneed - 1));
-#pragma unroll
-    for (int k = 0; k < FastDma<P>::NPASS; ++k) {
-        const uint32_t r = (uint32_t)min(rl + S::RPI * k, c.wh - 1);
-        __builtin_amdgcn_global_load_lds(static_cast<const void*>(c.wbase + (__umul24(r, c.pitch) + col)),
-                                         (fast_lds_void*)(buf + k * S::RPI * P), S::CB, 0, 0);
-    }
-}
-
-template <int P>
-__global__ __launch_bounds__(64) void fast_cells_dma_kernel(Geom g, int ncells_total, int cpw,
-                                                            const uint8_t* __restrict__ img0, size_t row0,
-                                                            size_t frame0, const uint8_t* __restrict__ pyr,
-                                                            uint32_t* __restrict__ cand,
-                                                            int* __restrict__ cell_counts, int* __restrict__ err) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    using D = FastDma<P>;
-    const int R = g.win_rows;
-    const int lane = threadIdx.x & 63;
-    // buffer b of the two window buffers (no pointer array: a local array of
-    // LDS addresses would be folded into a constant initializer)
-    auto buf = [&](int b) { return smem + (b & 1) * D::WBYTES; };
-    CellTiles T;
-    T.sc = smem + 2 * D::WBYTES;
-    T.la = reinterpret_cast<uint16_t*>(smem + 2 * D::WBYTES + P * R);
-    T.lb = T.la;
-    T.dump = fast_dma_list_len(P, R, g.det_max, D::WBYTES);
-    const int item0 = (int)blockIdx.x * cpw;
-    if (item0 >= ncells_total) return;
-    const int n = min(cpw, ncells_total - item0);
-    FastCellGeo cur = fast_cell_geo(g, item0, img0, row0, frame0, pyr);
-    if (!cur.empty) fast_dma_issue<P>(cur, buf(0), lane);
-    for (int i = 0; i < n; ++i) {
-        // the next cell's window streams in while this one is computed
-        FastCellGeo nxt;
-        const bool more = i + 1 < n;
-        bool issued = false;
-        if (more) {
-            nxt = fast_cell_geo(g, item0 + i + 1, img0, row0, frame0, pyr);
-            if (!nxt.empty) {
-                fast_dma_issue<P>(nxt, buf(i + 1), lane);
-                issued = true;
-            }
-        }
-        const LevelGeom& L = g.lv[cur.l];
-        int* cnt_out = cell_counts + (size_t)cur.f * g.total_cells + cur.gc;
-        if (cur.empty) {
-            if (lane == 0) *cnt_out = 0;
-        } else {
-            // this cell's window has landed: only the next cell's NPASS loads may remain
-            if (issued)
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D::NPASS) : "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            T.win = buf(i);
-            for (int idx = lane; idx < P * R / 4; idx += 64) reinterpret_cast<uint32_t*>(T.sc)[idx] = 0u;
-            wave_sync();
-            uint32_t* out = cand + (size_t)cur.f * g.cand_frame + L.cand_offset +
-                            (size_t)(cur.ci * L.ncols + cur.cj) * L.cell_cap;
-            const int dw = cur.maxX - cur.iniX - 6, dh = cur.wh - 6;
-            int total = 0;
-            if (dw > 0 && dh > 0) {
-                int nb = 0;
-                bool dropped = false;
-                total = fast_cell_banded<P>(T, dw, dh, cur.ox, g.ini_th, lane, cur.iniX, cur.iniY, out, L.cell_cap,
-                                            err, &nb, &dropped);
-                if (total == 0) {  // ORBextractor.cpp:821-825: retry the cell at minThFAST
-                    if (!dropped)
-                        for (int j = lane; j < nb; j += 64) T.sc[T.lb[j]] = 0;
-                    else
-                        for (int idx = lane; idx < P * R / 4; idx += 64) reinterpret_cast<uint32_t*>(T.sc)[idx] = 0u;
-                    wave_sync();
-                    total = fast_cell_banded<P>(T, dw, dh, cur.ox, g.min_th, lane, cur.iniX, cur.iniY, out,
-                                                L.cell_cap, err, &nb, &dropped);
-                }
-            }
-            if (lane == 0) *cnt_out = min(total, L.cell_cap);
-            wave_sync();  // this buffer and the tiles are reused two / one cells later
-        }
-        if (more) cur = nxt;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outstanding at exit
-}
-
 }  // namespace
 
 #ifdef FAST_STAMPS
@@ -770,41 +625,11 @@ extern "C" int orbgpu_debug_fast_stamps(unsigned long long* out, int reset) {
 #endif
 
 
-// cells per wave of the LDS-DMA kernel (ORBGPU_FAST_DMA, read per launch so a
-// test can switch it; 0 or unset: the one-cell kernel)
-static int fast_dma_cells() {
-    const char* s = std::getenv("ORBGPU_FAST_DMA");
-    const int v = s ? std::atoi(s) : 0;
-    return v < 0 ? 0 : (v > 64 ? 64 : v);
-}
-
-template <int P>
-static hipError_t launch_fast_dma(const Geom& g, int items, int cpw, const uint8_t* img0, size_t row0, size_t frame0,
-                                  const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err, hipStream_t stream) {
-    using D = FastDma<P>;
-    if (g.win_rows > D::kMaxRows || fast_dma_list_len(P, g.win_rows, g.det_max, D::WBYTES) == 0)
-        return hipErrorInvalidValue;
-    const size_t lds = (size_t)ORBGPU_FAST_DMA_WAVE_LDS;
-    hipLaunchKernelGGL(fast_cells_dma_kernel<P>, dim3((items + cpw - 1) / cpw), dim3(64), lds, stream, g, items, cpw,
-                       img0, row0, frame0, pyr, cand, cell_counts, err);
-    return hipGetLastError();
-}
-
 hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size_t row0, size_t frame0,
                              const uint8_t* pyr, uint32_t* cand, int* cell_counts, int* err,
                              hipStream_t stream) {
     const int items = g.total_cells * batch;
     if (row0 >= (1u << 24)) return hipErrorInvalidValue;  // row offsets by 24-bit multiplies
-    if (const int cpw = fast_dma_cells()) {
-        switch (g.win_pitch) {
-            case 40: return launch_fast_dma<40>(g, items, cpw, img0, row0, frame0, pyr, cand, cell_counts, err, stream);
-            case 48: return launch_fast_dma<48>(g, items, cpw, img0, row0, frame0, pyr, cand, cell_counts, err, stream);
-            case 56: return launch_fast_dma<56>(g, items, cpw, img0, row0, frame0, pyr, cand, cell_counts, err, stream);
-            case 64: return launch_fast_dma<64>(g, items, cpw, img0, row0, frame0, pyr, cand, cell_counts, err, stream);
-            case 72: return launch_fast_dma<72>(g, items, cpw, img0, row0, frame0, pyr, cand, cell_counts, err, stream);
-            default: return hipErrorInvalidValue;
-        }
-    }
     const size_t per_wave =
         (((size_t)2 * g.win_pitch * g.win_rows + 2 * ((size_t)fast_list_len(g.win_pitch, g.win_rows, g.det_max) + 1) + 15) & ~(size_t)15);
     dim3 grid((items + kCellWaves - 1) / kCellWaves);

@@ -197,63 +197,6 @@ def test_batch_octree_describe_chunks_match_oracle(monkeypatch, chunks):
         _assert_same_kps(kg, dd[b, :cc[b]], kr, dr)
 
 
-@pytest.mark.parametrize("cpw", ["1", "3", "8"])
-@pytest.mark.parametrize("w,h,nf", [(640, 480, 1000), (1241, 376, 2000)])
-def test_fast_dma_kernel_matches_oracle(monkeypatch, cpw, w, h, nf):
-    """ORBGPU_FAST_DMA = cells per wave: the FAST kernel that streams the next
-    cell's window into a second LDS buffer by LDS-DMA while computing the
-    current one (shorter survivor list: more row bands).  Stream frames, an
-    i.i.d.-noise frame (every level-0 cell banded) and a flat frame equal the
-    oracle, including the cells where a wave's run of cells crosses levels
-    and frames."""
-    og = _gpu()
-    monkeypatch.setenv("ORBGPU_FAST_DMA", cpw)
-    frames = np.concatenate([synth.mono_stream(5, w, h, seed=78), synth.noise_image(w, h)[None],
-                             synth.flat_image(w, h)[None]])
-    B = len(frames)
-    ex = og.Extractor(nfeatures=nf, width=w, height=h, max_batch=B)
-    imgs = torch.from_numpy(np.ascontiguousarray(frames)).cuda()
-    cap = ex.max_keypoints
-    kps = torch.zeros((B, cap, 7), dtype=torch.float32, device="cuda")
-    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
-    counts = torch.zeros(B, dtype=torch.int32, device="cuda")
-    ex.extract_batch(imgs, kps, desc, counts)
-    ex.sync()
-    ref = orbref.Extractor(nfeatures=nf)
-    kk, dd, cc = kps.cpu().numpy(), desc.cpu().numpy(), counts.cpu().numpy()
-    for b in range(B):
-        kr, dr = ref.extract(frames[b])
-        _assert_same_kps(og.keypoints_from_raw(kk[b, :cc[b]]), dd[b, :cc[b]], kr, dr)
-
-
-@pytest.mark.parametrize("kpw", ["1", "4", "16"])
-@pytest.mark.parametrize("w,h,nf", [(640, 480, 1000), (1241, 376, 2000)])
-def test_describe_dma_kernel_matches_oracle(monkeypatch, kpw, w, h, nf):
-    """ORBGPU_DESC_DMA = keypoint slots per wave: describe streaming the next
-    slot's raw neighbourhood into a second LDS buffer by LDS-DMA while the
-    current slot is blurred and tested; neighbourhoods that cross a level
-    border (reflected bytes: the noise frame has keypoints at every border)
-    take the register staging.  Equal to the oracle on every frame."""
-    og = _gpu()
-    monkeypatch.setenv("ORBGPU_DESC_DMA", kpw)
-    frames = np.concatenate([synth.mono_stream(5, w, h, seed=79), synth.noise_image(w, h)[None],
-                             synth.flat_image(w, h)[None]])
-    B = len(frames)
-    ex = og.Extractor(nfeatures=nf, width=w, height=h, max_batch=B)
-    imgs = torch.from_numpy(np.ascontiguousarray(frames)).cuda()
-    cap = ex.max_keypoints
-    kps = torch.zeros((B, cap, 7), dtype=torch.float32, device="cuda")
-    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
-    counts = torch.zeros(B, dtype=torch.int32, device="cuda")
-    ex.extract_batch(imgs, kps, desc, counts)
-    ex.sync()
-    ref = orbref.Extractor(nfeatures=nf)
-    kk, dd, cc = kps.cpu().numpy(), desc.cpu().numpy(), counts.cpu().numpy()
-    for b in range(B):
-        kr, dr = ref.extract(frames[b])
-        _assert_same_kps(og.keypoints_from_raw(kk[b, :cc[b]]), dd[b, :cc[b]], kr, dr)
-
-
 def test_timed_headline_batch_512_vs_oracle():
     """The configuration bench.py times, checked at full size:
     two consecutive 512-frame batches of the bench's bounded 640x480 stream at
