@@ -1052,6 +1052,8 @@ class DropIn:
         kl, dl, kr, dr, _, _ = orbref.stereo_frame(eL, eR, st[0], st[1], bf)
         res["stereo Frame: ORBextractor L || R + ComputeStereoMatches"] = (
             t(lambda: orbref.stereo_frame(eL, eR, st[0], st[1], bf)), "C++ oracle, L and R sequential")
+        res["stereo Frame: ORBextractor::ExtractPair (both frames from one thread) + ComputeStereoMatches"] = \
+            res["stereo Frame: ORBextractor L || R + ComputeStereoMatches"]
         res["ComputeStereoMatches"] = (t(lambda: orbref.stereo_matches(eL, eR, kl, dl, kr, dr, bf)), "C++ oracle")
         tgt, pts = self.scen["proj_local"]
         res["ORBmatcher::SearchByProjection(F, vpLocalMapPoints, th)"] = (

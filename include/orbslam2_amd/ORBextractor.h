@@ -147,21 +147,36 @@ public:
         int n = 0;
         check(orbgpu_extract(ex_, image.data, image.cols, image.rows, image.step, kp_buf_.data(), desc_buf_.data(),
                              info_.max_keypoints, &n));
-        _keypoints.clear();
-        _keypoints.reserve((size_t)n);
-        for (int i = 0; i < n; ++i) {
-            const orbgpu_keypoint& k = kp_buf_[(size_t)i];
-            _keypoints.push_back(cv::KeyPoint(k.x, k.y, k.size, k.angle, k.response, k.octave, k.class_id));
+        finish_frame(n, _keypoints, _descriptors);
+    }
+
+    // adapter-only: the stereo Frame's two extractions (Frame.cpp:84-87, two
+    // std::threads running ExtractORB(0) / ExtractORB(1)) from the calling
+    // thread -- both frames in flight on the GPU at once, no thread spawn per
+    // frame (orbgpu_extract_pair).  Results as two operator() calls.
+    static void ExtractPair(ORBextractor& left, ORBextractor& right, cv::InputArray imLeft, cv::InputArray imRight,
+                            std::vector<cv::KeyPoint>& keysLeft, cv::OutputArray descLeft,
+                            std::vector<cv::KeyPoint>& keysRight, cv::OutputArray descRight) {
+        if (imLeft.empty() || imRight.empty()) {  // ORBextractor.cpp:1056, per image
+            left(imLeft, cv::Mat(), keysLeft, descLeft);
+            right(imRight, cv::Mat(), keysRight, descRight);
+            return;
         }
-        if (n == 0) {
-            _descriptors.release();
-        } else {
-            _descriptors.create(n, 32, CV_8U);
-            cv::Mat d = _descriptors.getMat();
-            for (int i = 0; i < n; ++i) std::memcpy(d.ptr<unsigned char>(i), &desc_buf_[(size_t)i * 32], 32);
+        cv::Mat L = imLeft.getMat(), R = imRight.getMat();
+        if (L.type() != CV_8UC1 || R.type() != CV_8UC1) throw std::invalid_argument("ORBextractor: image must be CV_8UC1");
+        if (L.cols != R.cols || L.rows != R.rows) throw std::invalid_argument("ORBextractor: stereo images differ in size");
+        left.ensure_handle(L.cols, L.rows);
+        right.ensure_handle(R.cols, R.rows);
+        for (ORBextractor* e : {&left, &right}) {
+            e->kp_buf_.resize((size_t)e->info_.max_keypoints);
+            e->desc_buf_.resize((size_t)e->info_.max_keypoints * 32);
         }
-        mvImagePyramid.mark(ex_, &info_);
-        if (copy_pyramid_) mvImagePyramid.fill();
+        int nl = 0, nr = 0;
+        check(orbgpu_extract_pair(left.ex_, L.data, L.step, left.kp_buf_.data(), left.desc_buf_.data(),
+                                  left.info_.max_keypoints, &nl, right.ex_, R.data, R.step, right.kp_buf_.data(),
+                                  right.desc_buf_.data(), right.info_.max_keypoints, &nr, L.cols, L.rows));
+        left.finish_frame(nl, keysLeft, descLeft);
+        right.finish_frame(nr, keysRight, descRight);
     }
 
     int inline GetLevels() { return nlevels; }
@@ -191,6 +206,26 @@ protected:
     std::vector<float> mvInvLevelSigma2;
 
 private:
+    // the results of the last extraction (n keypoints in kp_buf_ / desc_buf_) into the caller's
+    // vectors, as ORBextractor.cpp:1069-1116 leaves them
+    void finish_frame(int n, std::vector<cv::KeyPoint>& _keypoints, cv::OutputArray _descriptors) {
+        _keypoints.clear();
+        _keypoints.reserve((size_t)n);
+        for (int i = 0; i < n; ++i) {
+            const orbgpu_keypoint& k = kp_buf_[(size_t)i];
+            _keypoints.push_back(cv::KeyPoint(k.x, k.y, k.size, k.angle, k.response, k.octave, k.class_id));
+        }
+        if (n == 0) {
+            _descriptors.release();
+        } else {
+            _descriptors.create(n, 32, CV_8U);
+            cv::Mat d = _descriptors.getMat();
+            for (int i = 0; i < n; ++i) std::memcpy(d.ptr<unsigned char>(i), &desc_buf_[(size_t)i * 32], 32);
+        }
+        mvImagePyramid.mark(ex_, &info_);
+        if (copy_pyramid_) mvImagePyramid.fill();
+    }
+
     static void check(int rc) {
         if (rc != ORBGPU_OK) throw std::runtime_error(std::string("orbgpu: ") + orbgpu_last_error());
     }

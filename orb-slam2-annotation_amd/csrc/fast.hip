@@ -45,17 +45,10 @@ __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
 }
 
 // Window staging geometry (fast_cells_kernel): chunks of CB bytes, NC per
-// P-byte row, RPI rows per pass of 64 lanes, kGroup passes' loads in flight:
-// a window of up to 42 rows is one group, i.e. one memory round trip (P = 40,
-// the 640x480 case, took 7 dword passes in two serial groups of 4 before
-// ORBGPU_FAST_CHUNK8; now 4 passes of 8-byte chunks, 8 VGPRs).
-#ifndef ORBGPU_FAST_CHUNK8
-#define ORBGPU_FAST_CHUNK8 1
-#endif
+// P-byte row, RPI rows per pass of 64 lanes, kGroup passes' loads in flight.
 template <int P>
 struct FastStage {
-    static constexpr int CB = P % 16 == 0 ? 16 : (ORBGPU_FAST_CHUNK8 && P % 8 == 0 ? 8 : 4), NC = P / CB,
-                         RPI = 64 / NC, kGroup = ORBGPU_FAST_CHUNK8 ? (42 + RPI - 1) / RPI : (CB == 16 ? 2 : 4);
+    static constexpr int CB = P % 16 == 0 ? 16 : 4, NC = P / CB, RPI = 64 / NC, kGroup = CB == 16 ? 2 : 4;
 };
 // LDS rows the staging writes for windows of up to R rows (at most): its
 // passes plus the row the lanes past RPI * NC stage; they must fit in the
@@ -170,6 +163,90 @@ __device__ int compass_pass(const CellTiles& T, int dw, int dh, int ox, int t, i
     return na;
 }
 
+// The same compass pre-test on dword groups (ORBGPU_FAST_COMPASS_DW): a lane
+// takes 4 adjacent pixels of a row -- the 4-aligned tile columns 4g .. 4g+3
+// of the detection region's NG groups, RPI = 64 / NG rows per iteration, lanes
+// row-major over (row, group) -- and reads its centre, c0 and c8 as one dword
+// each and c4 / c12 from the dwords either side (v_alignbyte): 5 LDS reads per
+// 4 pixels instead of 10 byte reads per 2.  Each dword splits into two packed
+// u16 pairs (v_perm), so the test is the packed arithmetic above on bytes
+// (0, 1) and (2, 3).  Survivors are listed row-major: a pixel's position is
+// the survivors of the lanes below it (mbcnt over the four byte masks) plus
+// those of the lower bytes of its own lane.  Pixels of a group outside the
+// detection columns, and rows past the region, are masked.
+__constant__ uint32_t c_ng_magic[18] = {0,     65536, 32769, 21846, 16385, 13108, 10923, 9363, 8193,
+                                        7282,  6554,  5958,  5462,  5042,  4682,  4370,  4097, 3856};
+template <int P, bool kBand = false>
+__device__ int compass_pass_dw(const CellTiles& T, int dw, int dh, int ox, int t, int lane, int row0 = 0,
+                               int start = 0, int* row_end = nullptr) {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const int c_lo = 3 + ox, c_hi = 3 + ox + dw;  // detection columns [c_lo, c_hi) of the tile
+    const int g_lo = c_lo >> 2, ng = ((c_hi - 1) >> 2) - g_lo + 1;  // <= 17 (dw <= 64)
+    const int rpi = 64 / ng;                                          // wave-uniform (scalar)
+    const uint32_t magic = c_ng_magic[ng];
+    const int rl = (int)(__umul24((uint32_t)lane, magic) >> 16), g = lane - rl * ng;  // lane / ng, lane % ng
+    const int col0 = 4 * (g_lo + g);
+    // per-byte column masks (lanes of the rpi rows whose byte b is a detection column)
+    unsigned long long cm[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        cm[b] = __builtin_amdgcn_uicmp((uint32_t)(col0 + b - c_lo), (uint32_t)dw, 36 /* ult */) &
+                __builtin_amdgcn_uicmp((uint32_t)rl, (uint32_t)rpi, 36);
+    auto split = [](uint32_t x, bool hi) {  // bytes (0, 1) or (2, 3) of x as a packed u16 pair
+        return __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, x, hi ? 0x0C030C02u : 0x0C010C00u));
+    };
+    auto test = [&](u16x2 v, u16x2 c0, u16x2 c4, u16x2 c8, u16x2 c12) -> uint32_t {
+        const u16x2 dark = __builtin_elementwise_max(__builtin_elementwise_min(c0, c8), __builtin_elementwise_min(c4, c12));
+        const u16x2 bright =
+            __builtin_elementwise_min(__builtin_elementwise_max(c0, c8), __builtin_elementwise_max(c4, c12));
+        const u16x2 x = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, dark),
+                                                  __builtin_elementwise_sub_sat(bright, v));
+        const u16x2 tt = {(unsigned short)t, (unsigned short)t};
+        return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x, tt));
+    };
+    auto addc = [](int a, unsigned long long m) {  // a + (this lane's bit of m)
+        int r;
+        unsigned long long co;
+        asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(co) : "v"(a), "s"(m));
+        return r;
+    };
+    int o = (3 + row0 + rl) * P + col0;  // tile offset of the lane's byte 0
+    int na = start;
+    int rr = row0;
+    const int per_iter = dw * rpi;  // most entries one iteration can add
+    for (; rr < dh; rr += rpi, o += rpi * P) {
+        if (kBand && na + per_iter > T.dump) break;  // the band ends here
+        const uint8_t* p = T.win + o;
+        const uint32_t V = *reinterpret_cast<const uint32_t*>(p), Vm = *reinterpret_cast<const uint32_t*>(p - 4),
+                       Vp = *reinterpret_cast<const uint32_t*>(p + 4), D = *reinterpret_cast<const uint32_t*>(p + 3 * P),
+                       U = *reinterpret_cast<const uint32_t*>(p - 3 * P);
+        const uint32_t c4 = __builtin_amdgcn_alignbyte(Vp, V, 3), c12 = __builtin_amdgcn_alignbyte(V, Vm, 1);
+        const uint32_t ylo = test(split(V, false), split(D, false), split(c4, false), split(U, false), split(c12, false));
+        const uint32_t yhi = test(split(V, true), split(D, true), split(c4, true), split(U, true), split(c12, true));
+        const unsigned long long rows = __builtin_amdgcn_uicmp((uint32_t)rl, (uint32_t)(dh - rr), 36 /* ult */);
+        const unsigned long long m0 = __builtin_amdgcn_uicmp(ylo & 0xFFFFu, 0u, 33 /* ne */) & cm[0] & rows;
+        const unsigned long long m1 = __builtin_amdgcn_uicmp(ylo, 0x10000u, 35 /* uge */) & cm[1] & rows;
+        const unsigned long long m2 = __builtin_amdgcn_uicmp(yhi & 0xFFFFu, 0u, 33 /* ne */) & cm[2] & rows;
+        const unsigned long long m3 = __builtin_amdgcn_uicmp(yhi, 0x10000u, 35 /* uge */) & cm[3] & rows;
+        uint32_t s = 0u;
+        s = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, s));
+        s = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, s));
+        s = __builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m2, s));
+        s = __builtin_amdgcn_mbcnt_hi((uint32_t)(m3 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m3, s));
+        const int p0 = na + (int)s, p1 = addc(p0, m0), p2 = addc(p1, m1), p3 = addc(p2, m2);
+        T.la[lane_select(m0, p0, T.dump)] = (uint16_t)o;
+        T.la[lane_select(m1, p1, T.dump)] = (uint16_t)(o + 1);
+        T.la[lane_select(m2, p2, T.dump)] = (uint16_t)(o + 2);
+        T.la[lane_select(m3, p3, T.dump)] = (uint16_t)(o + 3);
+        na += __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+    }
+    if (kBand) *row_end = rr;
+    return na;
+}
+#ifndef ORBGPU_FAST_COMPASS_DW
+#define ORBGPU_FAST_COMPASS_DW 1
+#endif
+
 // FAST at threshold t on the cell's detection region: returns the number
 // of corners, their tile offsets in lb[] (row-major) and scores in sc[].
 // Stages are separated by wave compaction so each runs on dense lanes:
@@ -178,7 +255,9 @@ __device__ int compass_pass(const CellTiles& T, int dw, int dh, int ox, int t, i
 template <int P>
 __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, int lane,
                             unsigned long long* stamp = nullptr) {
-    const int na = dw > 32 ? compass_pass<P, 64>(T, dw, dh, ox, t, lane) : compass_pass<P, 32>(T, dw, dh, ox, t, lane);
+    const int na = ORBGPU_FAST_COMPASS_DW ? compass_pass_dw<P>(T, dw, dh, ox, t, lane)
+                   : dw > 32              ? compass_pass<P, 64>(T, dw, dh, ox, t, lane)
+                                          : compass_pass<P, 32>(T, dw, dh, ox, t, lane);
     wave_sync();
 #ifdef FAST_STAMPS
     if (stamp) {
@@ -318,8 +397,9 @@ __device__ int fast_cell_banded(const CellTiles& T, int dw, int dh, int ox, int 
     bool drop = false;
     while (true) {
         int row_end = dh;
-        const int na = dw > 32 ? compass_pass<P, 64, true>(T, dw, dh, ox, t, lane, row, nb, &row_end)
-                               : compass_pass<P, 32, true>(T, dw, dh, ox, t, lane, row, nb, &row_end);
+        const int na = ORBGPU_FAST_COMPASS_DW ? compass_pass_dw<P, true>(T, dw, dh, ox, t, lane, row, nb, &row_end)
+                       : dw > 32              ? compass_pass<P, 64, true>(T, dw, dh, ox, t, lane, row, nb, &row_end)
+                                              : compass_pass<P, 32, true>(T, dw, dh, ox, t, lane, row, nb, &row_end);
         wave_sync();
         int nc = nb;
         for (int base = nb; base < na; base += 128) {
@@ -510,8 +590,7 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
         const uint32_t col = (uint32_t)(CB * min(q, ncneed - 1));
         const int passes = (wh + RPI - 1) / RPI;  // wave-uniform
         uint8_t* dst = s_win + CB * lane;
-        typedef typename std::conditional<CB == 16, uint4, typename std::conditional<CB == 8, uint2, uint32_t>::type>::type
-            Chunk;
+        typedef typename std::conditional<CB == 16, uint4, uint32_t>::type Chunk;
 #pragma unroll 1
         for (int p0 = 0; p0 < passes; p0 += kGroup) {
             Chunk v[kGroup];
@@ -525,8 +604,6 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
 #endif
                 if constexpr (CB == 16)
                     v[k] = load16_a4(src);
-                else if constexpr (CB == 8)
-                    v[k] = load8_a4(src);
                 else
                     v[k] = *reinterpret_cast<const uint32_t*>(src);
             }

@@ -768,14 +768,12 @@ int orbgpu_extractor_sync(orbgpu_extractor* e, void* stream) {
     return collect_errors(e, (hipStream_t)stream);
 }
 
-int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int height, size_t step,
-                   orbgpu_keypoint* keypoints, uint8_t* descriptors, int capacity, int* n) {
-    if (!e || !n) return fail(ORBGPU_ERR_ARG, "NULL argument");
-    DeviceScope ds_(e->device);
-    if (!image || width <= 0 || height <= 0) {  // ORBextractor.cpp:1056
-        *n = -1;
-        return ORBGPU_OK;
-    }
+// orbgpu_extract in two halves: issue (host image -> staging -> HBM,
+// extraction, results towards the pinned output block; nothing waited for)
+// and finish (one stream synchronisation, then the results out of the pinned
+// block).  orbgpu_extract_pair issues two extractors' frames from one thread
+// before finishing either.
+static int extract_issue(orbgpu_extractor* e, const uint8_t* image, int width, int height, size_t step) {
     if (width != e->W || height != e->H) return fail(ORBGPU_ERR_ARG, "image size differs from the extractor geometry");
     if (step < (size_t)width) return fail(ORBGPU_ERR_ARG, "step < width");
     hipStream_t s = e->stream;
@@ -784,23 +782,21 @@ int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int hei
         // host image -> pinned staging (one memcpy for a continuous image) ->
         // a copy kernel into HBM; extraction with describe writing keypoints,
         // descriptors, the count and the error word straight into the pinned
-        // output block; one synchronisation
+        // output block
         if (step == e->img_pitch)
             std::memcpy(e->h_img, image, step * (size_t)height);
         else
             for (int y = 0; y < height; ++y)
                 std::memcpy(e->h_img + (size_t)y * e->img_pitch, image + (size_t)y * step, width);
         ORB_HIP(launch_copy16(e->d_img, e->h_img, e->img_pitch * (size_t)height, s));
-        int rc = run_batch(e, e->d_img, 1, e->img_pitch, e->img_pitch * height,
-                           reinterpret_cast<orbgpu_keypoint*>(e->h_single + 16), e->h_single + e->single_desc_off,
-                           reinterpret_cast<int*>(e->h_single), e->max_kps, s, reinterpret_cast<int*>(e->h_single + 4));
-        if (rc) return rc;
-        ORB_HIP(hipStreamSynchronize(s));
-    } else {
-    // the drop-in (Frame constructor) path: host image -> pinned staging ->
-    // one async H2D; extraction; the error word folded into the output
-    // block; one async D2H of the whole block; one synchronisation
-    // (in four row bands: the DMA of band i overlaps the host copy of band i+1)
+        return run_batch(e, e->d_img, 1, e->img_pitch, e->img_pitch * height,
+                         reinterpret_cast<orbgpu_keypoint*>(e->h_single + 16), e->h_single + e->single_desc_off,
+                         reinterpret_cast<int*>(e->h_single), e->max_kps, s, reinterpret_cast<int*>(e->h_single + 4));
+    }
+    // the drop-in path with copy-engine transfers: host image -> pinned
+    // staging -> one async H2D; extraction; the error word folded into the
+    // output block; one async D2H of the whole block (in four row bands: the
+    // DMA of band i overlaps the host copy of band i+1)
     constexpr int kBands = 4;
     for (int b = 0; b < kBands; ++b) {
         const int y0 = height * b / kBands, y1 = height * (b + 1) / kBands;
@@ -818,8 +814,12 @@ int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int hei
                        e->max_kps, s, reinterpret_cast<int*>(e->d_single + 4));
     if (rc) return rc;
     ORB_HIP(hipMemcpyAsync(e->h_single, e->d_single, e->single_bytes, hipMemcpyDeviceToHost, s));
-    ORB_HIP(hipStreamSynchronize(s));
-    }
+    return ORBGPU_OK;
+}
+
+static int extract_finish(orbgpu_extractor* e, orbgpu_keypoint* keypoints, uint8_t* descriptors, int capacity,
+                          int* n) {
+    ORB_HIP(hipStreamSynchronize(e->stream));
     int count = 0, err = 0;
     std::memcpy(&count, e->h_single, sizeof(int));
     std::memcpy(&err, e->h_single + 4, sizeof(int));
@@ -831,6 +831,63 @@ int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int hei
     }
     *n = count;
     return ORBGPU_OK;
+}
+
+int orbgpu_extract(orbgpu_extractor* e, const uint8_t* image, int width, int height, size_t step,
+                   orbgpu_keypoint* keypoints, uint8_t* descriptors, int capacity, int* n) {
+    if (!e || !n) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    DeviceScope ds_(e->device);
+    if (!image || width <= 0 || height <= 0) {  // ORBextractor.cpp:1056
+        *n = -1;
+        return ORBGPU_OK;
+    }
+    int rc = extract_issue(e, image, width, height, step);
+    if (rc) return rc;
+    return extract_finish(e, keypoints, descriptors, capacity, n);
+}
+
+int orbgpu_extract_pair(orbgpu_extractor* e0, const uint8_t* image0, size_t step0, orbgpu_keypoint* keypoints0,
+                        uint8_t* descriptors0, int capacity0, int* n0, orbgpu_extractor* e1, const uint8_t* image1,
+                        size_t step1, orbgpu_keypoint* keypoints1, uint8_t* descriptors1, int capacity1, int* n1,
+                        int width, int height) {
+    if (!e0 || !e1 || !n0 || !n1) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    if (e0 == e1) return fail(ORBGPU_ERR_ARG, "the two frames need two extractors");
+    const bool empty = !image0 || !image1 || width <= 0 || height <= 0;
+    if (empty) {  // ORBextractor.cpp:1056, per image
+        *n0 = *n1 = -1;
+        int rc = ORBGPU_OK;
+        if (image0 && width > 0 && height > 0)
+            rc = orbgpu_extract(e0, image0, width, height, step0, keypoints0, descriptors0, capacity0, n0);
+        if (!rc && image1 && width > 0 && height > 0)
+            rc = orbgpu_extract(e1, image1, width, height, step1, keypoints1, descriptors1, capacity1, n1);
+        return rc;
+    }
+    int rc;
+    {
+        DeviceScope ds_(e0->device);
+        rc = extract_issue(e0, image0, width, height, step0);
+    }
+    if (rc) {
+        DeviceScope ds_(e0->device);
+        hipStreamSynchronize(e0->stream);  // nothing of frame 0 is left in flight
+        return rc;
+    }
+    int rc1;
+    {
+        DeviceScope ds_(e1->device);
+        rc1 = extract_issue(e1, image1, width, height, step1);
+    }
+    {
+        DeviceScope ds_(e0->device);
+        rc = extract_finish(e0, keypoints0, descriptors0, capacity0, n0);
+    }
+    DeviceScope ds_(e1->device);
+    if (rc1) {
+        hipStreamSynchronize(e1->stream);
+        return rc1;
+    }
+    const int r1 = extract_finish(e1, keypoints1, descriptors1, capacity1, n1);
+    return rc ? rc : r1;
 }
 
 int orbgpu_extractor_profile(orbgpu_extractor* e, int enable) {

@@ -51,11 +51,6 @@ __device__ inline uint4 load16_a4(const uint8_t* p) {
     const u32x4_a4 v = *reinterpret_cast<const u32x4_a4*>(p);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
-typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
-__device__ inline uint2 load8_a4(const uint8_t* p) {
-    const u32x2_a4 v = *reinterpret_cast<const u32x2_a4*>(p);
-    return make_uint2(v.x, v.y);
-}
 
 // Candidate key packing (FAST output, octree input/output):
 //   bits 0..10  x relative to minBorderX (level x - 16)

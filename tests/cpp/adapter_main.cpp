@@ -88,9 +88,14 @@ void log_times(const char* op, std::vector<double> us, const char* note = "") {
     const double p99 = us[std::min(us.size() - 1, us.size() * 99 / 100)];
     FILE* f = std::fopen(path, "a");
     if (!f) return;
+    // the five slowest repetitions too (what a p99 of 100 repetitions is made of)
+    char top[128];
+    int k = 0;
+    for (size_t i = 0; i < std::min<size_t>(5, us.size()); ++i)
+        k += std::snprintf(top + k, sizeof(top) - (size_t)k, "%s%.1f", i ? ", " : "", us[us.size() - 1 - i]);
     std::fprintf(f, "{\"op\": \"%s\", \"median_us\": %.2f, \"p90_us\": %.2f, \"p99_us\": %.2f, \"min_us\": %.2f, "
-                    "\"max_us\": %.2f, \"reps\": %zu, \"note\": \"%s\"}\n",
-                 op, med, p90, p99, us.front(), us.back(), us.size(), note);
+                    "\"max_us\": %.2f, \"slowest_us\": [%s], \"reps\": %zu, \"note\": \"%s\"}\n",
+                 op, med, p90, p99, us.front(), us.back(), top, us.size(), note);
     std::fclose(f);
 }
 
@@ -1107,6 +1112,11 @@ int main(int argc, char** argv) {
                 exR(imR, cv::Mat(), kR, dR);
                 ORB_SLAM2::ComputeStereoMatchesGPU(&exL, &exR, kL, dL, kR, dR, bf, 0.0f, uR, dep);
             }, "no threads: the two extractions back to back");
+            timed("stereo Frame: ORBextractor::ExtractPair (both frames from one thread) + ComputeStereoMatches", [] {},
+                  [&] {
+                      ORB_SLAM2::ORBextractor::ExtractPair(exL, exR, imL, imR, kL, dL, kR, dR);
+                      ORB_SLAM2::ComputeStereoMatchesGPU(&exL, &exR, kL, dL, kR, dR, bf, 0.0f, uR, dep);
+                  }, "orbgpu_extract_pair: both extractions in flight at once, no thread spawn per frame");
             FILE* out = fopen(argv[8], "wb");
             for (int f = 0; f < 2; ++f) {
                 const std::vector<cv::KeyPoint>& k = f ? kR : kL;
@@ -1143,6 +1153,27 @@ int main(int argc, char** argv) {
             }
             const long c1[2] = {exL.mvImagePyramid.copies(), exR.mvImagePyramid.copies()};
             fwrite(c1, 8, 2, out);
+            // the same Frame with both extractions issued from this thread (ExtractPair)
+            std::vector<cv::KeyPoint> kL2, kR2;
+            cv::Mat dL2, dR2;
+            std::vector<float> uR2, dep2;
+            ORB_SLAM2::ORBextractor::ExtractPair(exL, exR, imL, imR, kL2, dL2, kR2, dR2);
+            ORB_SLAM2::ComputeStereoMatchesGPU(&exL, &exR, kL2, dL2, kR2, dR2, bf, 0.0f, uR2, dep2);
+            for (int f = 0; f < 2; ++f) {
+                const std::vector<cv::KeyPoint>& k = f ? kR2 : kL2;
+                const cv::Mat& d = f ? dR2 : dL2;
+                const int n = (int)k.size();
+                fwrite(&n, 4, 1, out);
+                for (const cv::KeyPoint& q : k) {
+                    const float v[5] = {q.pt.x, q.pt.y, q.size, q.angle, q.response};
+                    fwrite(v, 4, 5, out);
+                    fwrite(&q.octave, 4, 1, out);
+                    fwrite(&q.class_id, 4, 1, out);
+                }
+                for (int i = 0; i < n; ++i) fwrite(d.ptr<unsigned char>(i), 1, 32, out);
+            }
+            fwrite(uR2.data(), 4, uR2.size(), out);
+            fwrite(dep2.data(), 4, dep2.size(), out);
             fclose(out);
         } catch (const std::exception& e) {
             fprintf(stderr, "exception: %s\n", e.what());

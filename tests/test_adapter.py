@@ -635,7 +635,8 @@ def test_adapter_stereo_frame_vs_oracle(exe, tmp_path, w, h, nf, bf, base):
     """The stereo Frame through the drop-in classes: two ORBextractor objects
     on two threads, then ComputeStereoMatchesGPU on their HBM pyramids
     (StereoMatcher.h, orbgpu_stereo_matches_pair) vs the oracle stereo Frame
-    (two oracle extractors + oracle/stereo_ref.cpp), bit-exact"""
+    (two oracle extractors + oracle/stereo_ref.cpp), bit-exact; and the same
+    Frame with both extractions issued from one thread (ExtractPair)"""
     pair = synth.stereo_stream(1, w, h, 0x5E7, base)[0]
     (tmp_path / "l.raw").write_bytes(pair[0].tobytes())
     (tmp_path / "r.raw").write_bytes(pair[1].tobytes())
@@ -672,6 +673,17 @@ def test_adapter_stereo_frame_vs_oracle(exe, tmp_path, w, h, nf, bf, base):
             off += 8 + lw * lh
             np.testing.assert_array_equal(got, ex.level(lv))
     assert list(np.frombuffer(buf, np.int64, 2, off)) == [1, 1]
+    # the same Frame with both extractions issued from one thread
+    # (ORBextractor::ExtractPair, orbgpu_extract_pair): the oracle's results too
+    off += 16
+    kl2, dl2, off = _read_frame(buf, off)
+    kr2, dr2, off = _read_frame(buf, off)
+    ur2 = np.frombuffer(buf, np.float32, len(kl2), off)
+    dp2 = np.frombuffer(buf, np.float32, len(kl2), off + 4 * len(kl2))
+    assert off + 8 * len(kl2) == len(buf)
+    assert kl2.tobytes() == rk[0].tobytes() and np.array_equal(dl2, rk[1])
+    assert kr2.tobytes() == rk[2].tobytes() and np.array_equal(dr2, rk[3])
+    assert ur2.tobytes() == rk[4].tobytes() and dp2.tobytes() == rk[5].tobytes()
 
 
 def test_adapter_initializer_fewer_than_8_matches_returns_false(exe, tmp_path):
