@@ -485,9 +485,6 @@ __device__ unsigned long long g_desc_stamps[16];
 #define DSTAMP(k) ((void)0)
 #endif
 
-#ifndef ORBGPU_DESC_REVERSE
-#define ORBGPU_DESC_REVERSE 0
-#endif
 #ifndef ORBGPU_DESC_WAVES
 #define ORBGPU_DESC_WAVES 4
 #endif
@@ -526,14 +523,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
     DSTAMP(0);
     const int per_frame = (g.slots_frame + kKeysPerWave - 1) / kKeysPerWave;
     const int fi = item / per_frame, slot0 = (item - fi * per_frame) * kKeysPerWave;
-    // frames in reverse order (ORBGPU_DESC_REVERSE): the ones the kernels before
-    // touched last first
-#if ORBGPU_DESC_REVERSE
-    const int fl = items / per_frame - 1 - fi;
-#else
-    const int fl = fi;
-#endif
-    const int f = f0 + fl;  // frame of the whole batch (a chunk's launch starts at frame f0)
+    const int f = f0 + fi;  // frame of the whole batch (a chunk's launch starts at frame f0)
     if (item >= items) return;
     KeyRef K[kKeysPerWave];
     bool valid[kKeysPerWave];

@@ -21,9 +21,6 @@ namespace orbgpu {
 
 namespace {
 
-#ifndef ORBGPU_FAST_REVERSE
-#define ORBGPU_FAST_REVERSE 0
-#endif
 #ifndef ORBGPU_FAST_BANDS
 #define ORBGPU_FAST_BANDS 1
 #endif
@@ -247,6 +244,23 @@ __device__ int compass_pass_dw(const CellTiles& T, int dw, int dh, int ox, int t
 #define ORBGPU_FAST_COMPASS_DW 1
 #endif
 
+// The 16 ring bytes and the centre of two survivors (top-left corners of
+// their 7x7 neighbourhoods p0, p1) as packed pairs: survivor 0 in the low
+// 16-bit half, survivor 1 in the high half (f16 denormal bit patterns).  One
+// byte read per point: unaligned wide LDS reads (one dword for rows 0 and 6,
+// 8 bytes for rows 1..5: 7 reads per survivor instead of 17) were correct on
+// gfx950 but ran fast_cells in 1.485 ms instead of 0.500 (round 5, r5l).
+typedef _Float16 fast_h2 __attribute__((ext_vector_type(2)));
+template <int P>
+__device__ __forceinline__ uint32_t ring_pairs(const uint8_t* p0, const uint8_t* p1, fast_h2 (&r)[16]) {
+    const int ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+    const int ring_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+    auto pair = [&](int o) { return (uint32_t)p0[o] | ((uint32_t)p1[o] << 16); };
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r[k] = __builtin_bit_cast(fast_h2, pair((ring_dy[k] + 3) * P + ring_dx[k] + 3));
+    return pair(3 * P + 3);
+}
+
 // FAST at threshold t on the cell's detection region: returns the number
 // of corners, their tile offsets in lb[] (row-major) and scores in sc[].
 // Stages are separated by wave compaction so each runs on dense lanes:
@@ -279,8 +293,6 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
     // their scores go to the score tile.
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     typedef short i16x2 __attribute__((ext_vector_type(2)));
-    const int ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-    const int ring_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
     auto max3 = [](h2 x, h2 y, h2 z) { return __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z); };
     auto min3 = [](h2 x, h2 y, h2 z) { return __builtin_elementwise_minimum(__builtin_elementwise_minimum(x, y), z); };
     int nb = 0;
@@ -294,11 +306,8 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
         asm volatile("" : "+v"(a0), "+v"(a1));
         const uint8_t* p0 = T.win + a0;
         const uint8_t* p1 = T.win + a1;
-        auto pair = [&](int o) { return (uint32_t)p0[o] | ((uint32_t)p1[o] << 16); };
-        const uint32_t vv = pair(3 * P + 3);
         h2 r[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) r[k] = __builtin_bit_cast(h2, pair((ring_dy[k] + 3) * P + ring_dx[k] + 3));
+        const uint32_t vv = ring_pairs<P>(p0, p1, r);
         h2 hi3[16], lo3[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
@@ -389,8 +398,6 @@ __device__ int fast_cell_banded(const CellTiles& T, int dw, int dh, int ox, int 
                                 uint32_t* out, int cap, int* err, int* pending, bool* dropped) {
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     typedef short i16x2 __attribute__((ext_vector_type(2)));
-    const int ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-    const int ring_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
     auto max3 = [](h2 x, h2 y, h2 z) { return __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z); };
     auto min3 = [](h2 x, h2 y, h2 z) { return __builtin_elementwise_minimum(__builtin_elementwise_minimum(x, y), z); };
     int nb = 0, total = 0, row = 0;
@@ -409,11 +416,8 @@ __device__ int fast_cell_banded(const CellTiles& T, int dw, int dh, int ox, int 
             asm volatile("" : "+v"(a0), "+v"(a1));
             const uint8_t* p0 = T.win + a0;
             const uint8_t* p1 = T.win + a1;
-            auto pair = [&](int o) { return (uint32_t)p0[o] | ((uint32_t)p1[o] << 16); };
-            const uint32_t vv = pair(3 * P + 3);
             h2 r[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) r[k] = __builtin_bit_cast(h2, pair((ring_dy[k] + 3) * P + ring_dx[k] + 3));
+            const uint32_t vv = ring_pairs<P>(p0, p1, r);
             h2 hi3[16], lo3[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
@@ -522,20 +526,8 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     unsigned long long ts[8] = {};
 #endif
     FSTAMP(0);
-    // frames in reverse order (ORBGPU_FAST_REVERSE): the pyramid pass wrote the
-    // last frames' levels last, so they are the ones still in the MALL / L2
-    // when this launch starts
-#if ORBGPU_FAST_REVERSE == 1
-    const int f = ncells_total / g.total_cells - 1 - item / g.total_cells;
-    const int gc = item % g.total_cells;
-#elif ORBGPU_FAST_REVERSE == 2  // cell-major, last cells first: one cell of every frame, then the previous cell
-    const int nb = ncells_total / g.total_cells;
-    const int f = item % nb;
-    const int gc = g.total_cells - 1 - item / nb;
-#else
     const int f = item / g.total_cells;
     const int gc = item % g.total_cells;
-#endif
     // level and cell coordinates of the frame's cell gc: one scalar load
     const uint32_t ce = g.cell_tab[gc];
     const int l = (int)(ce & 15u), ci = (int)((ce >> 4) & 0x3FFFu), cj = (int)(ce >> 18);
