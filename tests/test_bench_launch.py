@@ -29,13 +29,13 @@ ROOT = Path(__file__).resolve().parents[1]
 ENGINE = ROOT / "tests" / "dryrun_orbgpu.py"
 
 
-def _run_bench(tmp_path, *args, timeout=420):
+def _run_bench(tmp_path, *args, timeout=420, world=2):
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     env.pop("RANK", None)
     env.pop("LOCAL_RANK", None)
     env["OMP_NUM_THREADS"] = "2"
-    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--cpu-dry-run", str(ENGINE), "--dump",
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", str(world), "--cpu-dry-run", str(ENGINE), "--dump",
            str(tmp_path), "--no-cpu-baseline", "--no-extras", *args]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=str(ROOT))
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
@@ -136,6 +136,28 @@ def test_mono_stream_two_ranks_equals_single_process(tmp_path, deliver, parts):
     ref = _oracle_stream(world, B, steps)
     _check_stream(_load_dump(tmp_path, deliver, world), ref, B)
     _check_stream(_load_dump(tmp_path, other, world, "_other"), ref, B)
+
+
+def test_mono_stream_four_ranks_equals_single_process(tmp_path):
+    """Four ranks (the driver's N = 4 launch, gloo here): the boundary frame
+    passes along a ring of three chunk boundaries per step plus the step
+    boundary, and in gpu0 mode rank 0 takes counts and rows from three senders
+    at once (two process groups, each one op type in step order).  Both
+    delivery legs equal the single-process oracle stream frame by frame, and
+    rank 0's received bytes equal the three senders' rows."""
+    world, B, steps = 4, 2, 2
+    line = _run_bench(tmp_path, "--config", "mono640", "--batch", str(B), "--steps", str(steps), "--warmup", "0",
+                      "--deliver", "gpu0", world=world, timeout=600)
+    assert line["n_gpus"] == world and line["world_size_checked"] == world
+    dl, ol = line["delivery"], line["delivery_other_mode"]
+    assert dl["mode"] == "gpu0" and ol["mode"] == "host" and len(dl["per_rank"]) == world
+    sent = [p["bytes_per_step"] for p in dl["per_rank"]]
+    assert sent[0] == 0 and all(b > 0 for b in sent[1:])
+    assert dl["per_rank"][0]["recv_bytes_per_step"] + 4 * 3 * B * (world - 1) == sum(sent[1:])
+    assert all(p["bytes_per_step"] > 0 for p in ol["delivery"]["per_rank"])
+    ref = _oracle_stream(world, B, steps)
+    _check_stream(_load_dump(tmp_path, "gpu0", world), ref, B)
+    _check_stream(_load_dump(tmp_path, "host", world, "_other"), ref, B)
 
 
 def test_stereo_pairs_two_ranks_equal_single_process(tmp_path):
