@@ -152,6 +152,8 @@ def parse(argv=None):
 
 
 SUSTAINED_STEPS = 400  # the sustained leg of the mono line
+PROFILED_TAIL = 40     # a deferred leg's stage times: its last steps only (StreamBench.run)
+STEP_TRACE = [os.environ.get("BENCH_STEP_TRACE") == "1"]  # diagnostics: per-step times of each timed leg
 MATCH_AFTER = ["fast_cells"]  # set from --match-after
 MATCH_PRIORITY = [0]  # set from --match-priority (0: default, -1: high, as the extraction streams)
 
@@ -438,7 +440,7 @@ class StreamBench:
         self.ev_match_last = None  # the last match issued (with its delivery packing)
         self.pending = None  # (set index, timing events) of the step whose match is not issued yet
         self.timing_h2d = False
-        self._sus = None  # a deferred sustained leg (run_sustained) not yet read
+        self._sus = None  # a deferred leg (run(defer=True)) whose stage times the next run() reads
 
     def _match(self, si, after, ev=None):
         S = self.sets[si]
@@ -573,119 +575,147 @@ class StreamBench:
             self._match(si, self.sets[si].ev_ext, ev)
             self.pending = None
 
-    def run(self, warmup, steps):
+    def run(self, warmup, steps, defer=False):
+        """W untimed warm-up steps, then exactly `steps` timed steps bracketed by a
+        barrier + synchronisation on both sides.  defer=True (the sustained leg,
+        run straight before the headline): return at once after the timed region,
+        with profiling switched off, and a function that produces the leg's
+        numbers later -- its stage times come from the next run()'s stage-times
+        reset (profiling was off for that run's warm-up), its statistics and
+        collectives run after the next leg -- so the GPU goes from this leg into
+        the next one's warm-up without the host bookkeeping in between (an idle
+        gap of >= 10 ms leaves the next ~60 steps ~5 % slower,
+        profiles/r05_notes_ab.txt r5n)."""
         D = self.D
+        evs = [(D.event(True), D.event(True)) for _ in range(steps)]  # created before the warm-up
         for _ in range(warmup):
             self.step()
         self.flush()
         self.delivery.finish()
         D.synchronize()
+        t_idle = time.perf_counter()  # the GPU is idle from here until the timed steps start
         self.delivery.reset_stats()
-        sus = self._sus
+        sus, self._sus = self._sus, None
+        if sus is not None:
+            sus["stage_ms"], sus["nb"] = {}, 0
         for e, ps in zip(self.exs, self.pstreams):
             e.sync(ps)
             e.profile(True)
             ms_i, nb_i = e.stage_times(reset=True)
-            if sus is not None and "stage_ms" not in sus:  # the deferred sustained leg's own launches
-                sus["stage_ms"], sus["nb"] = ms_i, nb_i
+            if sus is not None:  # a deferred leg's own launches (profiling was off since)
+                for k, v in ms_i.items():
+                    sus["stage_ms"][k] = sus["stage_ms"].get(k, 0.0) + v
+                sus["nb"] = nb_i
         if self.feed == "host":
             self.timing_h2d, self.h2d_time = True, []
-        evs = [(D.event(True), D.event(True)) for _ in range(steps)]
+        # a deferred leg records stage times over its last PROFILED_TAIL steps only, so the
+        # next leg's stage-times reset (between its warm-up and its timed steps) reads few events
+        n_prof = min(steps, PROFILED_TAIL) if defer else steps
+        if n_prof < steps:
+            for e in self.exs:
+                e.profile(False)
         _barrier(self.world)
         D.synchronize()
+        if defer and self._event_timed_ok():
+            # one rank, nothing to deliver: the leg is timed by events on the streams (its
+            # first step's issue on the extraction stream to its last match's end on the
+            # matcher stream) and the host never waits for its end -- the next leg's
+            # warm-up steps are queued behind it (r5o: no idle GPU at all between them)
+            e0, e1 = D.event(True), D.event(True)
+            e0.record(self.stream)
+            for i in range(steps):
+                if i == steps - n_prof and n_prof < steps:
+                    for e in self.exs:
+                        e.profile(True)
+                self.step(evs[i])
+            self.flush()
+            e1.record(self.mstream)
+            last = self.sets[(self.step_no - 1) % NSETS]
+            raw = {"elapsed": None, "span": (e0, e1), "steps": steps, "evs": evs,
+                   "delivery": self.delivery.report(steps), "h2d": None,
+                   "kp": last.counts.float().mean(), "nm": last.nmatch.float().mean()}
+            for e in self.exs:
+                e.profile(False)
+            self._sus = raw
+            return lambda: self._finish(raw)
+        marks = [D.event(True) for _ in range(steps + 1)] if STEP_TRACE[0] else None
         t0 = time.perf_counter()
+        self.host_gap_ms = round((t0 - t_idle) * 1e3, 3)
         for i in range(steps):
+            if i == steps - n_prof and n_prof < steps:
+                for e in self.exs:
+                    e.profile(True)
+            if marks:
+                marks[i].record(self.stream)
             self.step(evs[i])
         self.flush()
+        if marks:
+            marks[steps].record(self.mstream)
         self.delivery.finish()
         D.synchronize()
         elapsed = time.perf_counter() - t0
+        self.step_ms = [round(marks[i].elapsed_time(marks[i + 1]), 4) for i in range(steps)] if marks else None
         self.timing_h2d = False
         delivery = self.delivery.report(steps)
         delivery["ms_per_step"] = round(elapsed / steps * 1e3, 4)  # this rank's own step time
-        elapsed, frames_total = aggregate(elapsed, self.B * steps, device=self.dev)
-        delivery = gather_delivery_stats(delivery, self.world, self.dev)
-        _barrier(self.world)
-        # stage times summed over the sub-batches (per launch: a stage's duration on its
-        # stream; with P > 1 sub-batches overlap, so the sum exceeds the step)
-        stage_ms, nb = {}, 0
+        last = self.sets[(self.step_no - 1) % NSETS]
+        raw = {"elapsed": elapsed, "steps": steps, "evs": evs, "delivery": delivery,
+               "h2d": list(self.h2d_time) if self.feed == "host" else None,
+               "kp": last.counts.float().mean(), "nm": last.nmatch.float().mean()}
+        if defer:
+            for e in self.exs:
+                e.profile(False)
+            self._sus = raw
+            return lambda: self._finish(raw)
+        raw["stage_ms"], raw["nb"] = {}, 0
         for e, ps in zip(self.exs, self.pstreams):
             e.sync(ps)
-            ms_i, nb = e.stage_times(reset=True)
+            ms_i, nb_i = e.stage_times(reset=True)
             e.profile(False)
             for k, v in ms_i.items():
-                stage_ms[k] = stage_ms.get(k, 0.0) + v
+                raw["stage_ms"][k] = raw["stage_ms"].get(k, 0.0) + v
+            raw["nb"] = nb_i
+        return self._finish(raw)
+
+    def _event_timed_ok(self):
+        """a leg may end without a host wait (run(defer=True)): one rank, nothing to
+        deliver (gpu0 at N = 1 moves nothing), frames already in HBM"""
+        return self.D.cuda and self.world == 1 and self.deliver == "gpu0" and self.feed == "hbm"
+
+    def _finish(self, raw):
+        """a timed leg's numbers: max elapsed / summed frames over ranks, the
+        delivery numbers gathered to rank 0, stage and match times, the pyramid's
+        achieved bandwidth"""
+        steps, elapsed = raw["steps"], raw["elapsed"]
+        if elapsed is None:  # an event-timed leg
+            self.D.synchronize()
+            elapsed = raw["span"][0].elapsed_time(raw["span"][1]) / 1e3
+            raw["delivery"]["ms_per_step"] = round(elapsed / steps * 1e3, 4)
+        elapsed, frames_total = aggregate(elapsed, self.B * steps, device=self.dev)
+        delivery = gather_delivery_stats(raw["delivery"], self.world, self.dev)
+        _barrier(self.world)
         if self.dump is not None:
             self.dump.write()
-        per_step = {k: v / max(nb, 1) for k, v in stage_ms.items()}
-        per_step["match"] = sum(a.elapsed_time(b) for a, b in evs) / steps
+        # stage times summed over the sub-batches (per launch: a stage's duration on its
+        # stream; with P > 1 sub-batches overlap, so the sum exceeds the step)
+        per_step = {k: v / max(raw.get("nb", 0), 1) for k, v in raw.get("stage_ms", {}).items()}
+        per_step["match"] = sum(a.elapsed_time(b) for a, b in raw["evs"]) / steps
         pyr_bytes = pyramid_bytes_per_frame(self.ex.level_sizes) * self.B
-        pyr_s = per_step["pyramid"] / 1e3
+        pyr_s = per_step.get("pyramid", 0.0) / 1e3
         achieved = pyr_bytes / pyr_s / 1e9 if pyr_s > 0 else None
-        last = self.sets[(self.step_no - 1) % NSETS]
         h2d = None
-        if self.feed == "host" and self.h2d_time:
-            ms = [a.elapsed_time(b) for a, b in self.h2d_time]  # the copies issued inside the timed region
+        if raw["h2d"]:
+            ms = [a.elapsed_time(b) for a, b in raw["h2d"]]  # the copies issued inside the timed region
             nbytes = self.inbuf[0].numel()
             h2d = {"bytes_per_step": int(nbytes), "ms_per_copy_mean": round(float(np.mean(ms)), 4),
                    "gb_per_s": round(nbytes / (float(np.mean(ms)) / 1e3) / 1e9, 2), "copies": len(ms)}
         return {"fps": frames_total / elapsed, "elapsed": elapsed, "per_step": per_step, "pyr_bytes": pyr_bytes,
-                "achieved": achieved, "keypoints": float(last.counts.float().mean().item()),
-                "matches": float(last.nmatch.float().mean().item()), "frames_total": frames_total,
-                "delivery": delivery, "h2d": h2d}
-
-    def deferred_sustained_ok(self):
-        """the sustained leg may run back to back with the next leg (see run_sustained):
-        one rank, nothing to deliver (gpu0 at N = 1 moves nothing), frames in HBM, one part"""
-        return self.D.cuda and self.world == 1 and self.deliver == "gpu0" and self.feed == "hbm" and self.parts == 1
-
-    def run_sustained(self, warmup, steps):
-        """The sustained leg issued back to back with the leg that follows (the
-        headline's warm-up steps): the same prologue as run(), then `steps`
-        steps timed by events on the streams -- from the first step's issue on
-        the extraction stream to the end of the last step's match on the
-        matcher stream -- with no host synchronisation at its end, so the GPU
-        goes from this leg straight into the next one's warm-up (measured: an
-        idle gap of 10 ms before 5 warm-up steps leaves the next 20 steps ~5 %
-        slower than the same steps straight after a long run,
-        profiles/r05_notes_ab.txt).  Profiling is switched off after its last
-        launch, so the next run()'s stage-times reset returns exactly this
-        leg's stage times; sustained_result() reads everything afterwards."""
-        assert self.deferred_sustained_ok()
-        D = self.D
-        for _ in range(warmup):
-            self.step()
-        self.flush()
-        self.delivery.finish()
-        D.synchronize()
-        self.delivery.reset_stats()
-        for e, ps in zip(self.exs, self.pstreams):
-            e.sync(ps)
-            e.profile(True)
-            e.stage_times(reset=True)
-        evs = [(D.event(True), D.event(True)) for _ in range(steps)]
-        D.synchronize()
-        e0, e1 = D.event(True), D.event(True)
-        e0.record(self.stream)
-        for i in range(steps):
-            self.step(evs[i])
-        self.flush()
-        e1.record(self.mstream)  # after the last match
-        for e in self.exs:
-            e.profile(False)
-        self._sus = {"e0": e0, "e1": e1, "evs": evs, "steps": steps, "warmup": warmup}
-
-    def sustained_result(self):
-        sus, self._sus = self._sus, None
-        self.D.synchronize()
-        elapsed = sus["e0"].elapsed_time(sus["e1"]) / 1e3
-        nb = max(sus.get("nb", 0), 1)
-        per_step = {k: v / nb for k, v in sus.get("stage_ms", {}).items()}
-        per_step["match"] = sum(a.elapsed_time(b) for a, b in sus["evs"]) / sus["steps"]
-        return {"fps": self.B * sus["steps"] / elapsed, "elapsed": elapsed, "per_step": per_step}
+                "achieved": achieved, "keypoints": float(raw["kp"].item()), "matches": float(raw["nm"].item()),
+                "frames_total": frames_total, "delivery": delivery, "h2d": h2d}
 
     def close(self):
         self.delivery.close()
+
 
     def parity_timed(self):
         """The timed path's own outputs against the oracle (untimed, after run()):
@@ -1381,22 +1411,18 @@ def main_mono(args, og, D, rank, world, stream):
         # this load (5 warm-up steps after an idle GPU leave the 20 timed steps
         # ~4 % slower than the same steps after 60)
         n_sus = max(args.steps, SUSTAINED_STEPS)
-        deferred = sb.deferred_sustained_ok()
-        if deferred:  # back to back with the headline's warm-up steps (no idle GPU in between)
-            sb.run_sustained(args.warmup, n_sus)
-            r = sb.run(args.warmup, args.steps)
-            rs = sb.sustained_result()
-        else:
-            rs = sb.run(args.warmup, n_sus)
+        # straight into the headline's warm-up steps: the leg's bookkeeping after the headline
+        sustained_done = sb.run(args.warmup, n_sus, defer=True)
+        r = sb.run(args.warmup, args.steps)
+        rs = sustained_done()
         extras["sustained"] = {"steps": n_sus, "warmup": args.warmup, "seconds": round(rs["elapsed"], 3),
                                "frames_per_s": round(rs["fps"], 1),
                                "ms_per_step": round(rs["elapsed"] / n_sus * 1e3, 3),
                                "stages_ms_per_step": {k: round(v, 4) for k, v in rs["per_step"].items()},
-                               "order": "run before the headline's warm-up and timed steps"
-                                        + (", issued back to back with them and timed by events on the streams "
-                                           "(first step's issue to the last match's end)" if deferred else "")}
-        if not deferred:
-            r = sb.run(args.warmup, args.steps)
+                               "stages_over_last_steps": min(n_sus, PROFILED_TAIL),
+                               "headline_host_gap_ms": sb.host_gap_ms,
+                               "order": "run before the headline's warm-up and timed steps, its bookkeeping "
+                                        "after them (no host work between its last step and their first)"}
     else:
         r = sb.run(args.warmup, args.steps)
     # the timed configuration's own outputs against the oracle (rank 0, untimed)
