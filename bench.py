@@ -151,7 +151,7 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-SUSTAINED_STEPS = 400  # the sustained leg of the mono line
+SUSTAINED_STEPS = int(os.environ.get("BENCH_SUSTAINED_STEPS", "400"))  # the sustained leg of the mono line
 PROFILED_TAIL = 40     # a deferred leg's stage times: its last steps only (StreamBench.run)
 STEP_TRACE = [os.environ.get("BENCH_STEP_TRACE") == "1"]  # diagnostics: per-step times of each timed leg
 MATCH_AFTER = ["fast_cells"]  # set from --match-after
@@ -655,11 +655,12 @@ class StreamBench:
         D.synchronize()
         elapsed = time.perf_counter() - t0
         self.step_ms = [round(marks[i].elapsed_time(marks[i + 1]), 4) for i in range(steps)] if marks else None
+        raw_step_ms = self.step_ms
         self.timing_h2d = False
         delivery = self.delivery.report(steps)
         delivery["ms_per_step"] = round(elapsed / steps * 1e3, 4)  # this rank's own step time
         last = self.sets[(self.step_no - 1) % NSETS]
-        raw = {"elapsed": elapsed, "steps": steps, "evs": evs, "delivery": delivery,
+        raw = {"elapsed": elapsed, "steps": steps, "evs": evs, "delivery": delivery, "step_ms": raw_step_ms,
                "h2d": list(self.h2d_time) if self.feed == "host" else None,
                "kp": last.counts.float().mean(), "nm": last.nmatch.float().mean()}
         if defer:
@@ -711,7 +712,7 @@ class StreamBench:
                    "gb_per_s": round(nbytes / (float(np.mean(ms)) / 1e3) / 1e9, 2), "copies": len(ms)}
         return {"fps": frames_total / elapsed, "elapsed": elapsed, "per_step": per_step, "pyr_bytes": pyr_bytes,
                 "achieved": achieved, "keypoints": float(raw["kp"].item()), "matches": float(raw["nm"].item()),
-                "frames_total": frames_total, "delivery": delivery, "h2d": h2d}
+                "frames_total": frames_total, "delivery": delivery, "h2d": h2d, "step_ms": raw.get("step_ms")}
 
     def close(self):
         self.delivery.close()
@@ -1498,6 +1499,7 @@ def main_mono(args, og, D, rank, world, stream):
                      "traffic": traffic_for(args.traffic_json, args.config, B),
                      "algorithmic_bytes_per_step": r["pyr_bytes"]},
         "stages_ms_per_step": {k: round(v, 4) for k, v in r["per_step"].items()},
+        **({"step_ms": r["step_ms"]} if r.get("step_ms") else {}),
         "keypoints_per_frame": round(r["keypoints"], 1),
         "matches_per_pair": round(r["matches"], 1),
         "parity_vs_oracle": parity,

@@ -28,7 +28,10 @@ namespace orbgpu {
 
 namespace {
 
-constexpr int kThreads = 256;       // large batches: 4 workgroups per CU (LDS-bound)
+#ifndef ORBGPU_OCT_THREADS
+#define ORBGPU_OCT_THREADS 256
+#endif
+constexpr int kThreads = ORBGPU_OCT_THREADS;  // large batches: 4 workgroups per CU (LDS-bound)
 constexpr int kThreadsSmall = 1024;  // a few frames: one workgroup per (frame, level) on its own CU
 constexpr int kSmallBatch = 8;       // batches up to this size take kThreadsSmall
 

@@ -21,14 +21,16 @@ def main():
     torch.cuda.set_stream(stream)
     W, H, NF, _ = bench.CONFIGS["mono640"]
     sb = bench.StreamBench(og, D, W, H, NF, 512, 0, 1, stream, deliver="gpu0")
-    for rep in range(3):
-        for name, w, k in (("long", 5, 400), ("short", 5, 20), ("short", 5, 20)):
+    for rep in range(2):
+        for name, w, k in (("long", 5, 1000), ("short", 5, 20), ("short", 5, 20)):
             r = sb.run(w, k)
             st = sb.step_ms
             print(json.dumps({"rep": rep, "leg": name, "fps": round(r["fps"], 1),
                               "stages": {a: round(b, 4) for a, b in r["per_step"].items()},
                               "first10": st[:10], "last10": st[-10:],
-                              "mean_mid": round(sum(st[5:-5]) / max(len(st) - 10, 1), 4)}), flush=True)
+                              "mean_mid": round(sum(st[5:-5]) / max(len(st) - 10, 1), 4),
+                              "means_per_50": [round(sum(st[i:i + 50]) / len(st[i:i + 50]), 4)
+                                               for i in range(0, len(st), 50)]}), flush=True)
     sb.close()
 
 
