@@ -869,7 +869,7 @@ int orbgpu_extract_pair(orbgpu_extractor* e0, const uint8_t* image0, size_t step
     }
     if (rc) {
         DeviceScope ds_(e0->device);
-        hipStreamSynchronize(e0->stream);  // nothing of frame 0 is left in flight
+        (void)hipStreamSynchronize(e0->stream);  // nothing of frame 0 is left in flight
         return rc;
     }
     int rc1;
@@ -883,7 +883,7 @@ int orbgpu_extract_pair(orbgpu_extractor* e0, const uint8_t* image0, size_t step
     }
     DeviceScope ds_(e1->device);
     if (rc1) {
-        hipStreamSynchronize(e1->stream);
+        (void)hipStreamSynchronize(e1->stream);
         return rc1;
     }
     const int r1 = extract_finish(e1, keypoints1, descriptors1, capacity1, n1);
