@@ -142,6 +142,9 @@ def parse(argv=None):
     ap.add_argument("--part-stage", default="pyramid", choices=["pyramid", "fast_cells", "octree"])
     ap.add_argument("--match-priority", type=int, default=0, choices=[0, -1],
                     help="matcher stream priority (0: default, below the extraction streams; -1: high)")
+    ap.add_argument("--sustained-steps", type=int, default=None,
+                    help="length of the mono line's sustained leg (default: BENCH_SUSTAINED_STEPS or 400 with the "
+                         "extra legs on a GPU, none otherwise; > 0 forces it, e.g. in the CPU launcher tests)")
     ap.add_argument("--other-delivery", type=int, default=1, choices=[0, 1],
                     help="N > 1: also run the stream with the other --deliver mode (a second leg in the line)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"))
@@ -1405,13 +1408,14 @@ def main_mono(args, og, D, rank, world, stream):
     sb = StreamBench(og, D, W, H, NF, B, rank, world, stream, dump=args.dump, deliver=args.deliver, feed=args.feed,
                      parts=args.parts, part_stage=args.part_stage)
     extras = {}
-    if not args.no_extras and D.cuda:
+    n_sus = args.sustained_steps if args.sustained_steps is not None else (
+        max(args.steps, SUSTAINED_STEPS) if not args.no_extras and D.cuda else 0)
+    if n_sus > 0:
         # sustained leg, before the headline: the same stream for SUSTAINED_STEPS steps
         # (~0.55 s at 640x480; the headline's timed region is steps x ms_per_step, ~30 ms at
         # the driver's 20).  Run first, it also brings the GPU to the clock it holds under
         # this load (5 warm-up steps after an idle GPU leave the 20 timed steps
         # ~4 % slower than the same steps after 60)
-        n_sus = max(args.steps, SUSTAINED_STEPS)
         # straight into the headline's warm-up steps: the leg's bookkeeping after the headline
         sustained_done = sb.run(args.warmup, n_sus, defer=True)
         r = sb.run(args.warmup, args.steps)

@@ -138,6 +138,24 @@ def test_mono_stream_two_ranks_equals_single_process(tmp_path, deliver, parts):
     _check_stream(_load_dump(tmp_path, other, world, "_other"), ref, B)
 
 
+def test_sustained_leg_deferred_two_ranks(tmp_path):
+    """The sustained leg handed over to the headline without host bookkeeping in
+    between (StreamBench.run(defer=True); at N > 1 its collectives and
+    statistics run after the headline, in the same order on every rank): with
+    two gloo ranks the run completes (no collective mismatched between the
+    ranks), the line carries both legs, and the headline's output set equals
+    the oracle."""
+    world, B, steps = 2, 2, 2
+    line = _run_bench(tmp_path, "--config", "mono640", "--batch", str(B), "--steps", str(steps), "--warmup", "1",
+                      "--deliver", "gpu0", "--sustained-steps", "3", "--other-delivery", "0")
+    sus = line["sustained"]
+    assert sus["steps"] == 3 and sus["frames_per_s"] > 0 and sus["ms_per_step"] > 0
+    assert sus["headline_host_gap_ms"] >= 0 and line["value"] > 0
+    # the headline's own output set (the last step) against the oracle, pairs across the
+    # chunk boundary included (bench.py parity_timed)
+    assert line["parity_vs_oracle"]["ok"] is True and line["n_gpus"] == world
+
+
 def test_mono_stream_four_ranks_equals_single_process(tmp_path):
     """Four ranks (the driver's N = 4 launch, gloo here): the boundary frame
     passes along a ring of three chunk boundaries per step plus the step
