@@ -66,6 +66,7 @@ from __future__ import annotations
 
 import argparse
 import contextlib
+import gc
 import importlib.util
 import json
 import math
@@ -590,6 +591,8 @@ class StreamBench:
         gap of >= 10 ms leaves the next ~60 steps ~5 % slower,
         profiles/r05_notes_ab.txt r5n)."""
         D = self.D
+        # no garbage-collector pause inside a leg (collected between legs, in _finish)
+        gc.disable()
         evs = [(D.event(True), D.event(True)) for _ in range(steps)]  # created before the warm-up
         for _ in range(warmup):
             self.step()
@@ -642,6 +645,7 @@ class StreamBench:
             self._sus = raw
             return lambda: self._finish(raw)
         marks = [D.event(True) for _ in range(steps + 1)] if STEP_TRACE[0] else None
+        host_t = []
         t0 = time.perf_counter()
         self.host_gap_ms = round((t0 - t_idle) * 1e3, 3)
         for i in range(steps):
@@ -650,6 +654,7 @@ class StreamBench:
                     e.profile(True)
             if marks:
                 marks[i].record(self.stream)
+                host_t.append(time.perf_counter())
             self.step(evs[i])
         self.flush()
         if marks:
@@ -658,6 +663,10 @@ class StreamBench:
         D.synchronize()
         elapsed = time.perf_counter() - t0
         self.step_ms = [round(marks[i].elapsed_time(marks[i + 1]), 4) for i in range(steps)] if marks else None
+        if marks:  # the host's issue interval of each step (a cold host CPU can starve the GPU)
+            host_t.append(time.perf_counter())
+            self.step_ms = {"gpu": self.step_ms,
+                            "host_issue": [round((host_t[i + 1] - host_t[i]) * 1e3, 4) for i in range(steps)]}
         raw_step_ms = self.step_ms
         self.timing_h2d = False
         delivery = self.delivery.report(steps)
@@ -691,6 +700,9 @@ class StreamBench:
         delivery numbers gathered to rank 0, stage and match times, the pyramid's
         achieved bandwidth"""
         steps, elapsed = raw["steps"], raw["elapsed"]
+        if self._sus is None:  # no leg handed over to a next one: collect now, outside any timed region
+            gc.enable()
+            gc.collect()
         if elapsed is None:  # an event-timed leg
             self.D.synchronize()
             elapsed = raw["span"][0].elapsed_time(raw["span"][1]) / 1e3

@@ -583,11 +583,12 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
         const int passes = (wh + RPI - 1) / RPI;  // wave-uniform
         uint8_t* dst = s_win + CB * lane;
         typedef typename std::conditional<CB == 16, uint4, uint32_t>::type Chunk;
-#pragma unroll 1
-        for (int p0 = 0; p0 < passes; p0 += kGroup) {
-            Chunk v[kGroup];
+        // one group of NG passes: all its loads issued, then its stores
+        auto stage_group = [&](auto ngc, int p0) {
+            constexpr int NG = decltype(ngc)::value;
+            Chunk v[NG];
 #pragma unroll
-            for (int k = 0; k < kGroup; ++k) {
+            for (int k = 0; k < NG; ++k) {
                 const uint32_t r = (uint32_t)min(rl + RPI * (p0 + k), wh - 1);
 #ifdef FAST_PROBE_SAMEWIN
                 const uint8_t* src = wbase + (__umul24(r, (uint32_t)row0) + col);
@@ -599,15 +600,17 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
                 else
                     v[k] = *reinterpret_cast<const uint32_t*>(src);
             }
-            if (p0 + kGroup <= passes) {  // a whole group (wave-uniform): unconditional stores
+            if (p0 + NG <= passes) {  // a whole group (wave-uniform): unconditional stores
 #pragma unroll
-                for (int k = 0; k < kGroup; ++k) *reinterpret_cast<Chunk*>(dst + (p0 + k) * RPI * P) = v[k];
+                for (int k = 0; k < NG; ++k) *reinterpret_cast<Chunk*>(dst + (p0 + k) * RPI * P) = v[k];
             } else {  // the last, partial group
 #pragma unroll
-                for (int k = 0; k < kGroup; ++k)
+                for (int k = 0; k < NG; ++k)
                     if (p0 + k < passes) *reinterpret_cast<Chunk*>(dst + (p0 + k) * RPI * P) = v[k];
             }
-        }
+        };
+#pragma unroll 1
+        for (int p0 = 0; p0 < passes; p0 += kGroup) stage_group(std::integral_constant<int, kGroup>{}, p0);
     }
     // (T.sc is 16-byte aligned when P * R is: then 16-byte stores, else dwords)
     const int nz16 = (P * R) % 16 == 0 ? P * R / 16 : 0;

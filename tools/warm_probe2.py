@@ -24,7 +24,7 @@ def main():
     for rep in range(2):
         for name, w, k in (("long", 5, 1000), ("short", 5, 20), ("short", 5, 20)):
             r = sb.run(w, k)
-            st = sb.step_ms
+            st = sb.step_ms["gpu"]
             print(json.dumps({"rep": rep, "leg": name, "fps": round(r["fps"], 1),
                               "stages": {a: round(b, 4) for a, b in r["per_step"].items()},
                               "first10": st[:10], "last10": st[-10:],
