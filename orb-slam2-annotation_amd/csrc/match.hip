@@ -34,6 +34,7 @@ namespace {
 // variant is launched only when a frame's keypoint capacity can exceed the
 // previous one's limit.
 constexpr int kMaxK0Small = 512, kMaxK0Large = 1024, kMaxK0Huge = 2048;
+constexpr int kMaxK0Tiny = 256;  // launched alone, when the caller bounds level 0 by 256
 constexpr int kNeedLarge = -2;  // nmatches sentinel: the pair waits for the large variant
 constexpr int kNeedHuge = -3;   // ... for the huge variant
 constexpr int kGC = 64, kGR = 48, kHL = 30, kThLow = 50;
@@ -541,6 +542,11 @@ int match_batch_threads() {
     return v == 256 || v == 512 || v == 1024 ? v : kBatchThreads;
 }
 
+bool match_tiny_enabled() {
+    const char* s = std::getenv("ORBGPU_MATCH_TINY");  // read per launch (A/B)
+    return !s || std::atoi(s) != 0;
+}
+
 template <int kMaxK0, int kThreads>
 hipError_t launch_variant(int batch, int more, float minX, float maxX, float minY, float maxY,
                           const orbgpu_keypoint* kps1, const uint8_t* desc1, const int* n1, size_t stride1,
@@ -587,6 +593,18 @@ hipError_t launch_match_init(int batch, float minX, float maxX, float minY, floa
 #define ORBGPU_MATCH_ARGS                                                                                         \
     minX, maxX, minY, maxY, kps1, desc1, n1, stride1, kps2, desc2, n2, stride2, prev_xy, window, nnratio, flags, \
         matches12, nmatches, stream, first
+    // a level-0 bound of at most 256 keypoints (1000 features: 220 slots): the 256 variant alone,
+    // ~38 KB of LDS per block instead of ~62 KB, so the matcher's blocks take less room beside
+    // the extraction kernels they overlap (ORBGPU_MATCH_TINY=0: the 512 variant)
+    if (cap <= (size_t)kMaxK0Tiny && batch >= kChipFill && match_tiny_enabled()) {
+        if (threads == 256)
+            e = launch_variant<kMaxK0Tiny, 256>(batch, 0, ORBGPU_MATCH_ARGS);
+        else if (threads == 512)
+            e = launch_variant<kMaxK0Tiny, 512>(batch, 0, ORBGPU_MATCH_ARGS);
+        else
+            e = launch_variant<kMaxK0Tiny, 1024>(batch, 0, ORBGPU_MATCH_ARGS);
+        return e;
+    }
     if (threads == 256)
         e = launch_variant<kMaxK0Small, 256>(batch, more_large, ORBGPU_MATCH_ARGS);
     else if (threads == 512)

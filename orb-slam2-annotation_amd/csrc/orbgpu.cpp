@@ -435,8 +435,18 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     ncap_b = (int)round_up((size_t)std::max(ncap_b, 1), 16);
     const long budget_b = std::min<long>(65536, (long)octree_lds_bytes(g, 2048, ncap_b)) -
                           (long)octree_lds_bytes(g, 0, ncap_b) - 64;
-    // levels 0..1: keys in LDS up to 4096 (about 40 KiB, four workgroups per CU)
-    const long budget_a = std::min<long>(65536, (long)octree_lds_bytes(g, 4096, e->ncap)) -
+    // levels 0..1: keys in LDS up to ~2560 (about 31 KiB at 640x480: five workgroups
+    // per CU; with 4096, 41 KiB, only three fit -- round 5: octree 0.158 -> 0.141 ms per
+    // 512 frames, profiles/r05_notes_ab.txt r6c).  The bench stream's levels 0-1 have
+    // ~1,000-1,300 candidates; a level with more than the capacity takes the HBM-scratch
+    // path (correct, slower), as an oversized level always did.  ORBGPU_OCT_KCAP_A
+    // overrides the 2560 (256..4096).
+    const int kcap_a_req = [] {
+        const char* s = std::getenv("ORBGPU_OCT_KCAP_A");
+        const int v = s ? std::atoi(s) : 2560;
+        return v >= 256 && v <= 4096 ? v : 2560;
+    }();
+    const long budget_a = std::min<long>(65536, (long)octree_lds_bytes(g, kcap_a_req, e->ncap)) -
                           (long)octree_lds_bytes(g, 0, e->ncap) - 64;
     e->oct_groups[0] = OctreeGroup{0, split, budget_a > 0 ? (int)(budget_a / 6) & ~63 : 0, e->ncap};
     e->oct_groups[1] = OctreeGroup{split, L - split, budget_b > 0 ? (int)(budget_b / 6) & ~63 : 0, ncap_b};
