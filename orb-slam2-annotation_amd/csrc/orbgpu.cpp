@@ -436,7 +436,7 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     const long budget_b = std::min<long>(65536, (long)octree_lds_bytes(g, 2048, ncap_b)) -
                           (long)octree_lds_bytes(g, 0, ncap_b) - 64;
     // levels 0..1: keys in LDS up to ~2560 (about 31 KiB at 640x480: five workgroups
-    // per CU; with 4096, 41 KiB, only three fit -- round 5: octree 0.158 -> 0.141 ms per
+    // per CU; with 4096, 40.3 KiB, four -- round 5: octree 0.158 -> 0.141 ms per
     // 512 frames, profiles/r05_notes_ab.txt r6c).  The bench stream's levels 0-1 have
     // ~1,000-1,300 candidates; a level with more than the capacity takes the HBM-scratch
     // path (correct, slower), as an oversized level always did.  ORBGPU_OCT_KCAP_A
