@@ -174,7 +174,7 @@ constexpr int kRawWords = kPatch * (kRWidth / 4);   // 43 rows x 12 dwords
 constexpr int kQuads = kBPitch / 4;                 // 10 output quads per blurred row
 constexpr int kColChunks = (kBlur + 6) / 7;         // 6 chunks of <= 7 blurred rows
 
-// The 4 waves of a block process different keypoints in LDS regions of their
+// The waves of a block process different keypoints in LDS regions of their
 // own: stages are ordered within the wave, never with a block barrier.  A
 // wave's DS instructions execute in order, so only the compiler must keep
 // memory operations on their side (the asm's memory clobber) and the wave's
@@ -485,12 +485,15 @@ __device__ unsigned long long g_desc_stamps[16];
 #define DSTAMP(k) ((void)0)
 #endif
 
+// keypoints (waves) per block: 2 since round 5 (with the 256-keypoint matcher beside
+// describe: 396.1k vs 394.3k frames/s, describe 0.487 vs 0.492 ms; 1: 396.3k; 8: slower;
+// profiles/r05_notes_ab.txt r6g/r6h)
 #ifndef ORBGPU_DESC_WAVES
-#define ORBGPU_DESC_WAVES 4
+#define ORBGPU_DESC_WAVES 2
 #endif
-constexpr int kDescWaves = ORBGPU_DESC_WAVES;  // keypoints (waves) per block
+constexpr int kDescWaves = ORBGPU_DESC_WAVES;
 
-// One wave per (frame, slot) item, four items per block.  Blocks are
+// One wave per (frame, slot) item, kDescWaves items per block.  Blocks are
 // XCD-swizzled so one frame's keypoints (whose neighbourhoods overlap) are
 // described on one XCD and its level rows are fetched into one L2.
 __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int items, int f0,
