@@ -113,6 +113,47 @@ struct KeyStore {
     __device__ void set_node(int k, int v) const { nodes[k] = (uint16_t)v; }
 };
 
+// The quadrant histogram of each node (4 counters per node; after the push
+// the counters hold the children's list positions).  With the keys in LDS a
+// level has at most kcap (< 2^16) keys, so the counters are u16, bumped with
+// a 32-bit LDS atomic on the pair's dword; the HBM-scratch path (any number
+// of keys) keeps u32 counters, in the LDS region the keys would have used.
+template <bool LDS>
+struct QuadCounts;
+
+template <>
+struct QuadCounts<true> {
+    uint16_t* h;
+    __device__ void zero(int nodes, int tid, int nt) const {
+        uint32_t* w = reinterpret_cast<uint32_t*>(h);
+        for (int i = tid; i < nodes * 2; i += nt) w[i] = 0u;
+    }
+    __device__ void add(int i, int q) const {
+        atomicAdd(reinterpret_cast<uint32_t*>(h) + i * 2 + (q >> 1), 1u << ((q & 1) << 4));
+    }
+    __device__ uint32_t get(int i, int q) const { return h[i * 4 + q]; }
+    __device__ void set(int i, int q, int v) const { h[i * 4 + q] = (uint16_t)v; }
+    __device__ int nonzero(int i) const {  // children a divided node would have
+        const uint2 v = reinterpret_cast<const uint2*>(h)[i];
+        return ((v.x & 0xFFFFu) != 0) + ((v.x >> 16) != 0) + ((v.y & 0xFFFFu) != 0) + ((v.y >> 16) != 0);
+    }
+};
+
+template <>
+struct QuadCounts<false> {
+    uint32_t* w;
+    __device__ void zero(int nodes, int tid, int nt) const {
+        for (int i = tid; i < nodes * 4; i += nt) w[i] = 0u;
+    }
+    __device__ void add(int i, int q) const { atomicAdd(&w[i * 4 + q], 1u); }
+    __device__ uint32_t get(int i, int q) const { return w[i * 4 + q]; }
+    __device__ void set(int i, int q, int v) const { w[i * 4 + q] = (uint32_t)v; }
+    __device__ int nonzero(int i) const {
+        const uint4 v = reinterpret_cast<const uint4*>(w)[i];
+        return (v.x != 0) + (v.y != 0) + (v.z != 0) + (v.w != 0);
+    }
+};
+
 __device__ inline int pow2ceil(int v) {
     int p = 1;
     while (p < v) p <<= 1;
@@ -139,9 +180,8 @@ template <int NT, bool LDS>
 __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int nk, int ncells, int ncap, int ncap2,
                             const uint32_t* __restrict__ cand, uint32_t* __restrict__ out,
                             int* __restrict__ oct_count, int* __restrict__ err, int* __restrict__ trace,
-                            KeyStore<LDS> ks, int* s_misc, unsigned long long* s_sortk, ONode* s_node0,
-                            ONode* s_node1, uint32_t* s_qc, int* s_aux0, int* s_aux1, uint8_t* s_flag,
-                            int* s_cellofs) {
+                            KeyStore<LDS> ks, QuadCounts<LDS> qc, int* s_misc, ONode* s_node0, ONode* s_node1,
+                            int* s_aux0, int* s_aux1, uint8_t* s_flag, int* s_cellofs) {
     const int tid = threadIdx.x;
     int* s_tmp = s_misc;
 
@@ -223,17 +263,20 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
     for (int guard = 0; guard < 4096; ++guard) {
         ONode* old = cur ? s_node1 : s_node0;
         ONode* nw = cur ? s_node0 : s_node1;
+        // the inner pass's sort keys live in the next list's buffer: it is
+        // written only after the last sort-key read (ncap2 <= 2 ncap keys fit)
+        unsigned long long* s_sortk = reinterpret_cast<unsigned long long*>(nw);
         // quadrant histogram of every node with > 1 key; the counter of
         // children with > 1 key alternates between two slots, so this pass
         // resets its own while the previous pass's may still be read
         int* s_nexp = s_misc + 25 + (guard & 1);
-        for (int i = tid; i < nL * 4; i += NT) s_qc[i] = 0;
+        qc.zero(nL, tid, NT);
         if (tid == 0) *s_nexp = 0;
         __syncthreads();
         for (int k = tid; k < nk; k += NT) {
             const int i = ks.node(k);
             const ONode nd = old[i];
-            if (nd.cnt > 1) atomicAdd(&s_qc[i * 4 + node_quad(nd, ks.key(k))], 1u);
+            if (nd.cnt > 1) qc.add(i, node_quad(nd, ks.key(k)));
         }
         __syncthreads();
         OCT_T(3 + 4 * guard);
@@ -244,9 +287,7 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
             // positions together (C <= 4 nL and S <= nL stay below 2^16)
             for (int i = tid; i < nL; i += NT) {
                 const bool div = old[i].cnt > 1;
-                int nch = 0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) nch += s_qc[i * 4 + q] > 0;
+                const int nch = qc.nonzero(i);
                 s_aux0[i] = div ? nch << 16 : 1;
                 s_flag[i] = div;
             }
@@ -307,20 +348,14 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
             // rank r -> (nch - 1); inclusive scan; first r reaching N
             for (int r = tid; r < m; r += NT) {
                 const int i = (int)(s_sortk[r] & 0xFFF);
-                int nch = 0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) nch += s_qc[i * 4 + q] > 0;
-                s_aux1[r] = nch - 1;
+                s_aux1[r] = qc.nonzero(i) - 1;
             }
             if (tid == 0) s_misc[24] = m - 1;
             __syncthreads();
             block_scan<NT>(s_aux1, m, s_tmp);  // exclusive prefix of (nch-1)
             for (int r = tid; r < m; r += NT) {
                 const int i = (int)(s_sortk[r] & 0xFFF);
-                int nch = 0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) nch += s_qc[i * 4 + q] > 0;
-                if (nL + s_aux1[r] + nch - 1 >= N) atomicMin(&s_misc[24], r);
+                if (nL + s_aux1[r] + qc.nonzero(i) - 1 >= N) atomicMin(&s_misc[24], r);
             }
             for (int i = tid; i < nL; i += NT) { s_flag[i] = 0; s_aux0[i] = 0; }
             __syncthreads();
@@ -328,10 +363,7 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
             // push bases over ranks 0..kstop, scattered to node index
             for (int r = tid; r < m; r += NT) {
                 const int i = (int)(s_sortk[r] & 0xFFF);
-                int nch = 0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) nch += s_qc[i * 4 + q] > 0;
-                s_aux1[r] = r <= kstop ? nch : 0;
+                s_aux1[r] = r <= kstop ? qc.nonzero(i) : 0;
             }
             __syncthreads();
             C = block_scan<NT>(s_aux1, m, s_tmp);
@@ -360,14 +392,14 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
                 int p = inner ? pk : pk >> 16;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const uint32_t c = s_qc[i * 4 + q];
+                    const uint32_t c = qc.get(i, q);
                     if (c > 0) {
                         const int pos = C - 1 - p;
                         ONode ch = child_rect(nd, q);
                         ch.cnt = c;
                         ch.seq = (uint32_t)(nseq + p);
                         nw[pos] = ch;
-                        s_qc[i * 4 + q] = (uint32_t)pos;
+                        qc.set(i, q, pos);
                         if (c > 1) atomicAdd(s_nexp, 1);
                         ++p;
                     }
@@ -382,7 +414,7 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
         OCT_T(5 + 4 * guard);
         for (int k = tid; k < nk; k += NT) {
             const int i = ks.node(k);
-            ks.set_node(k, s_flag[i] ? (int)s_qc[i * 4 + node_quad(old[i], ks.key(k))] : s_aux1[i]);
+            ks.set_node(k, s_flag[i] ? (int)qc.get(i, node_quad(old[i], ks.key(k))) : s_aux1[i]);
         }
         __syncthreads();
         OCT_T(6 + 4 * guard);
@@ -403,16 +435,17 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
     }
 
     // 4. best key per node (max response, first in candidate order)
-    for (int i = tid; i < nL; i += NT) s_qc[i] = 0;
+    uint32_t* s_best = reinterpret_cast<uint32_t*>(s_aux0);
+    for (int i = tid; i < nL; i += NT) s_best[i] = 0;
     __syncthreads();
     for (int k = tid; k < nk; k += NT)
-        atomicMax(&s_qc[ks.node(k)], ((uint32_t)key_s(ks.key(k)) << 24) | (0xFFFFFFu - (uint32_t)k));
+        atomicMax(&s_best[ks.node(k)], ((uint32_t)key_s(ks.key(k)) << 24) | (0xFFFFFFu - (uint32_t)k));
     __syncthreads();
     if (nL > L.ocap) {
         if (tid == 0) { atomicOr(err, kErrNodeCap); oct_count[f * kOcStride + l] = 0; }
         return;
     }
-    for (int i = tid; i < nL; i += NT) out[i] = ks.key((int)(0xFFFFFFu - (s_qc[i] & 0xFFFFFFu)));
+    for (int i = tid; i < nL; i += NT) out[i] = ks.key((int)(0xFFFFFFu - (s_best[i] & 0xFFFFFFu)));
     if (tid == 0) oct_count[f * kOcStride + l] = nL;
     OCT_T(63);
 }
@@ -441,26 +474,27 @@ __global__ __launch_bounds__(NT) void octree_kernel(Geom g, const uint32_t* __re
     const int ncap2 = pow2ceil(ncap);
     OCT_T(0);
 
-    // LDS carve (byte offsets must match octree_lds_bytes)
-    const size_t o_sortk = 128;
-    const size_t o_node0 = o_sortk + (size_t)ncap2 * 8;
+    // LDS carve (byte offsets must match octree_lds_bytes).  ncap is a
+    // multiple of 16, so every region below starts 16-byte aligned.  Regions
+    // shared by phases that never overlap: the cell offsets (roots phase
+    // only) sit in node buffer 1, the inner pass's sort keys in the next
+    // list's node buffer, the final best-key words in aux0, and the HBM-path
+    // quadrant counters in the key region.
+    const size_t o_node0 = 128;
     const size_t o_node1 = o_node0 + (size_t)ncap * 16;
-    const size_t o_qc = o_node1 + (size_t)ncap * 16;
-    const size_t o_aux0 = o_qc + (size_t)ncap * 16;
+    const size_t o_qc = o_node1 + std::max((size_t)ncap * 16, (((size_t)(g.max_cells_level + 1) * 4 + 15) & ~(size_t)15));
+    const size_t o_aux0 = o_qc + (size_t)ncap * 8;
     const size_t o_aux1 = o_aux0 + (size_t)ncap * 4;
     const size_t o_flag = o_aux1 + (size_t)ncap * 4;
-    const size_t o_cell = o_flag + (((size_t)ncap + 15) & ~(size_t)15);
-    const size_t o_keys = o_cell + (((size_t)(g.max_cells_level + 1) * 4 + 15) & ~(size_t)15);
+    const size_t o_keys = o_flag + (size_t)ncap;
     const size_t o_knode = o_keys + (size_t)kcap * 4;
     int* s_misc = reinterpret_cast<int*>(smem);
-    unsigned long long* s_sortk = reinterpret_cast<unsigned long long*>(smem + o_sortk);
     ONode* s_node0 = reinterpret_cast<ONode*>(smem + o_node0);
     ONode* s_node1 = reinterpret_cast<ONode*>(smem + o_node1);
-    uint32_t* s_qc = reinterpret_cast<uint32_t*>(smem + o_qc);
     int* s_aux0 = reinterpret_cast<int*>(smem + o_aux0);
     int* s_aux1 = reinterpret_cast<int*>(smem + o_aux1);
     uint8_t* s_flag = smem + o_flag;
-    int* s_cellofs = reinterpret_cast<int*>(smem + o_cell);
+    int* s_cellofs = reinterpret_cast<int*>(smem + o_node1);
     int* s_tmp = s_misc;  // [0..15] scan scratch (a wave total each), [24..25] scalars
 
     // 1. candidate order: cells row-major, within a cell FAST order (:797-838)
@@ -472,25 +506,29 @@ __global__ __launch_bounds__(NT) void octree_kernel(Geom g, const uint32_t* __re
     uint32_t* out = oct_out + (size_t)f * g.slots_frame + L.out_offset;
     if (nk <= kcap) {
         KeyStore<true> ks{reinterpret_cast<uint32_t*>(smem + o_keys), reinterpret_cast<uint16_t*>(smem + o_knode)};
-        octree_body<NT, true>(g, L, l, f, nk, ncells, ncap, ncap2, cand, out, oct_count, err, trace, ks, s_misc, s_sortk,
-                          s_node0, s_node1, s_qc, s_aux0, s_aux1, s_flag, s_cellofs);
+        QuadCounts<true> qc{reinterpret_cast<uint16_t*>(smem + o_qc)};
+        octree_body<NT, true>(g, L, l, f, nk, ncells, ncap, ncap2, cand, out, oct_count, err, trace, ks, qc, s_misc,
+                              s_node0, s_node1, s_aux0, s_aux1, s_flag, s_cellofs);
     } else {  // too many candidates for LDS: the same algorithm on an HBM scratch region
         KeyStore<false> ks{gkeys + (size_t)f * g.cand_frame + L.cand_offset,
                            gknode + (size_t)f * g.cand_frame + L.cand_offset};
-        octree_body<NT, false>(g, L, l, f, nk, ncells, ncap, ncap2, cand, out, oct_count, err, trace, ks, s_misc, s_sortk,
-                           s_node0, s_node1, s_qc, s_aux0, s_aux1, s_flag, s_cellofs);
+        QuadCounts<false> qc{reinterpret_cast<uint32_t*>(smem + o_keys)};
+        octree_body<NT, false>(g, L, l, f, nk, ncells, ncap, ncap2, cand, out, oct_count, err, trace, ks, qc, s_misc,
+                               s_node0, s_node1, s_aux0, s_aux1, s_flag, s_cellofs);
     }
 }
 
 }  // namespace
 
 size_t octree_lds_bytes(const Geom& g, int kcap, int ncap) {
+    // misc, node 0, node 1 (or the cell offsets), u16 quadrant counters,
+    // aux0, aux1, flags, keys + key nodes (or u32 quadrant counters); ncap
+    // is a multiple of 16 and kcap of 64 (see the kernel's carve)
     auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
-    int ncap2 = 1;
-    while (ncap2 < ncap) ncap2 <<= 1;
-    return r16(32 * 4) + r16((size_t)ncap2 * 8) + 2 * r16((size_t)ncap * 16) + r16((size_t)ncap * 16) +
-           2 * r16((size_t)ncap * 4) + r16((size_t)ncap) + r16((size_t)(g.max_cells_level + 1) * 4) +
-           r16((size_t)kcap * 4) + r16((size_t)kcap * 2);
+    const size_t n = (size_t)ncap;
+    return r16(32 * 4) + r16(n * 16) + std::max(r16(n * 16), r16((size_t)(g.max_cells_level + 1) * 4)) +
+           r16(n * 8) + 2 * r16(n * 4) + r16(n) +
+           std::max(r16((size_t)kcap * 4) + r16((size_t)kcap * 2), r16(n * 16));
 }
 
 hipError_t launch_octree(const Geom& g, int batch, const uint32_t* cand, const int* cell_counts,

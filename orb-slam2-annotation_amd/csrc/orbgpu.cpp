@@ -141,7 +141,7 @@ struct orbgpu_extractor {
     float scale_factor = 0.f;
     std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
     int W = 0, H = 0, max_batch = 0, max_kps = 0;
-    int kcap = 0, ncap = 0;
+    int ncap = 0;
     OctreeGroup oct_groups[2] = {};  // the octree launches (big levels / small levels)
     // device buffers
     uint8_t* d_pyr = nullptr;
@@ -421,11 +421,16 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     // C <= 4 * nodes must stay below 2^15 and S <= nodes below 2^16
     static_assert(4 * 4096 < (1 << 15), "octree packed scan bound");
     if (4 * e->ncap >= (1 << 15)) return fail(ORBGPU_ERR_UNSUPPORTED, "octree node capacity exceeds the packed scan");
-    // keys in LDS up to a 64 KiB workgroup budget; larger levels use HBM scratch
-    const size_t fixed = octree_lds_bytes(g, 0, e->ncap);
-    const long budget = 65536 - (long)fixed - 64;
-    e->kcap = budget > 0 ? (int)(budget / 6) & ~63 : 0;
-    // Two octree launches: levels 0..1 (below), the
+    // Key capacity (a multiple of 64) for a requested one: the keys and their node
+    // indices (6 bytes a key) in the requested LDS bytes less 64, and the whole
+    // workgroup within 64 KiB; a level with more candidates uses HBM scratch.
+    auto key_capacity = [&g](int req, int ncap_) {
+        const long bytes = (long)round_up((size_t)req * 4, 16) + (long)round_up((size_t)req * 2, 16) - 64;
+        int kc = bytes > 0 ? (int)(bytes / 6) & ~63 : 0;
+        while (kc > 0 && octree_lds_bytes(g, kc, ncap_) > 65536) kc -= 64;
+        return kc;
+    };
+    // Two level groups in one octree launch: levels 0..1 (below), the
     // smaller levels with node arrays for their own feature counts and keys in LDS up to
     // 2048 (about 28 KiB: five workgroups per CU); a level with more candidates takes the
     // same HBM-scratch path as an oversized big level.
@@ -433,8 +438,6 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     int ncap_b = 0;
     for (int l = split; l < L; ++l) ncap_b = std::max(ncap_b, std::max(g.lv[l].ocap, g.lv[l].nini));
     ncap_b = (int)round_up((size_t)std::max(ncap_b, 1), 16);
-    const long budget_b = std::min<long>(65536, (long)octree_lds_bytes(g, 2048, ncap_b)) -
-                          (long)octree_lds_bytes(g, 0, ncap_b) - 64;
     // levels 0..1: keys in LDS up to ~2560 (about 31 KiB at 640x480: five workgroups
     // per CU; with 4096, 40.3 KiB, four -- round 5: octree 0.158 -> 0.141 ms per
     // 512 frames, profiles/r05_notes_ab.txt r6c).  The bench stream's levels 0-1 have
@@ -446,10 +449,8 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
         const int v = s ? std::atoi(s) : 2560;
         return v >= 256 && v <= 4096 ? v : 2560;
     }();
-    const long budget_a = std::min<long>(65536, (long)octree_lds_bytes(g, kcap_a_req, e->ncap)) -
-                          (long)octree_lds_bytes(g, 0, e->ncap) - 64;
-    e->oct_groups[0] = OctreeGroup{0, split, budget_a > 0 ? (int)(budget_a / 6) & ~63 : 0, e->ncap};
-    e->oct_groups[1] = OctreeGroup{split, L - split, budget_b > 0 ? (int)(budget_b / 6) & ~63 : 0, ncap_b};
+    e->oct_groups[0] = OctreeGroup{0, split, key_capacity(kcap_a_req, e->ncap), e->ncap};
+    e->oct_groups[1] = OctreeGroup{split, L - split, key_capacity(2048, ncap_b), ncap_b};
     return ORBGPU_OK;
 }
 

@@ -197,6 +197,31 @@ def test_batch_octree_describe_chunks_match_oracle(monkeypatch, chunks):
         _assert_same_kps(kg, dd[b, :cc[b]], kr, dr)
 
 
+@pytest.mark.parametrize("B", [1, 16])
+def test_octree_key_scratch_path_matches_oracle(monkeypatch, B):
+    """ORBGPU_OCT_KCAP_A=256 leaves levels 0-1 a 192-key LDS capacity, so
+    every level-0/1 octree runs on the HBM-scratch key store with u32
+    quadrant counters (the in-LDS path keeps u16 counters), in 1024-thread
+    (B=1) and 256-thread (B=16) workgroups; every frame equals the oracle."""
+    og = _gpu()
+    monkeypatch.setenv("ORBGPU_OCT_KCAP_A", "256")
+    frames = synth.mono_stream(B, 640, 480, seed=57)
+    ex = og.Extractor(max_batch=B)
+    imgs = torch.from_numpy(np.ascontiguousarray(frames)).cuda()
+    cap = ex.max_keypoints
+    kps = torch.zeros((B, cap, 7), dtype=torch.float32, device="cuda")
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(B, dtype=torch.int32, device="cuda")
+    ex.extract_batch(imgs, kps, desc, counts)
+    ex.sync()
+    ref = orbref.Extractor()
+    kk, dd, cc = kps.cpu().numpy(), desc.cpu().numpy(), counts.cpu().numpy()
+    for b in sorted({0, B // 2, B - 1}):
+        kr, dr = ref.extract(frames[b])
+        kg = og.keypoints_from_raw(kk[b, :cc[b]])
+        _assert_same_kps(kg, dd[b, :cc[b]], kr, dr)
+
+
 def test_timed_headline_batch_512_vs_oracle():
     """The configuration bench.py times, checked at full size:
     two consecutive 512-frame batches of the bench's bounded 640x480 stream at
