@@ -31,7 +31,7 @@ namespace {
 #ifndef ORBGPU_OCT_THREADS
 #define ORBGPU_OCT_THREADS 256
 #endif
-constexpr int kThreads = ORBGPU_OCT_THREADS;  // large batches: 4 workgroups per CU (LDS-bound)
+constexpr int kThreads = ORBGPU_OCT_THREADS;  // large batches: 6 workgroups per CU at 640x480 (LDS-bound)
 constexpr int kThreadsSmall = 1024;  // a few frames: one workgroup per (frame, level) on its own CU
 constexpr int kSmallBatch = 8;       // batches up to this size take kThreadsSmall
 

@@ -432,15 +432,15 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     };
     // Two level groups in one octree launch: levels 0..1 (below), the
     // smaller levels with node arrays for their own feature counts and keys in LDS up to
-    // 2048 (about 28 KiB: five workgroups per CU); a level with more candidates takes the
-    // same HBM-scratch path as an oversized big level.
+    // ~2048; a level with more candidates takes the same HBM-scratch path as an oversized
+    // big level.  The launch's LDS per workgroup is the larger group's.
     const int split = std::min(2, L);
     int ncap_b = 0;
     for (int l = split; l < L; ++l) ncap_b = std::max(ncap_b, std::max(g.lv[l].ocap, g.lv[l].nini));
     ncap_b = (int)round_up((size_t)std::max(ncap_b, 1), 16);
-    // levels 0..1: keys in LDS up to ~2560 (about 31 KiB at 640x480: five workgroups
-    // per CU; with 4096, 40.3 KiB, four -- round 5: octree 0.158 -> 0.141 ms per
-    // 512 frames, profiles/r05_notes_ab.txt r6c).  The bench stream's levels 0-1 have
+    // levels 0..1: keys in LDS up to ~2560 (26.1 KiB at 640x480: six workgroups per CU;
+    // with 4096, four -- round 5: octree 0.158 -> 0.136 ms per 512 frames,
+    // profiles/r05_notes_ab.txt r6c, r7a).  The bench stream's levels 0-1 have
     // ~1,000-1,300 candidates; a level with more than the capacity takes the HBM-scratch
     // path (correct, slower), as an oversized level always did.  ORBGPU_OCT_KCAP_A
     // overrides the 2560 (256..4096).
