@@ -156,6 +156,9 @@ def parse(argv=None):
 
 
 SUSTAINED_STEPS = int(os.environ.get("BENCH_SUSTAINED_STEPS", "400"))  # the sustained leg of the mono line
+HEADLINE_PROFILED = 5  # a timed leg's stage and match times: HIP events on its last 5 steps
+PROF_STEPS = int(os.environ.get("BENCH_PROF_STEPS", "-1"))  # diagnostics: overrides HEADLINE_PROFILED
+SETTLE_STEPS = int(os.environ.get("BENCH_SETTLE_STEPS", "0"))  # diagnostics: an untimed leg before the headline
 PROFILED_TAIL = 40     # a deferred leg's stage times: its last steps only (StreamBench.run)
 STEP_TRACE = [os.environ.get("BENCH_STEP_TRACE") == "1"]  # diagnostics: per-step times of each timed leg
 MATCH_AFTER = ["fast_cells"]  # set from --match-after
@@ -593,7 +596,11 @@ class StreamBench:
         D = self.D
         # no garbage-collector pause inside a leg (collected between legs, in _finish)
         gc.disable()
-        evs = [(D.event(True), D.event(True)) for _ in range(steps)]  # created before the warm-up
+        # timing events on the profiled tail only (PROFILED_TAIL / HEADLINE_PROFILED steps): every
+        # timed HIP event between the step's kernels costs the stream time (r7e: events on all 20
+        # headline steps 373-388k frames/s, on the last one 391.4-391.8k, one box)
+        n_prof = min(steps, PROFILED_TAIL if defer else (PROF_STEPS if PROF_STEPS >= 0 else HEADLINE_PROFILED))
+        evs = [(D.event(True), D.event(True)) for _ in range(n_prof)]  # created before the warm-up
         for _ in range(warmup):
             self.step()
         self.flush()
@@ -614,9 +621,8 @@ class StreamBench:
                 sus["nb"] = nb_i
         if self.feed == "host":
             self.timing_h2d, self.h2d_time = True, []
-        # a deferred leg records stage times over its last PROFILED_TAIL steps only, so the
-        # next leg's stage-times reset (between its warm-up and its timed steps) reads few events
-        n_prof = min(steps, PROFILED_TAIL) if defer else steps
+        # stage times over the last n_prof steps only (a deferred leg: so the next leg's
+        # stage-times reset, between its warm-up and its timed steps, also reads few events)
         if n_prof < steps:
             for e in self.exs:
                 e.profile(False)
@@ -633,7 +639,7 @@ class StreamBench:
                 if i == steps - n_prof and n_prof < steps:
                     for e in self.exs:
                         e.profile(True)
-                self.step(evs[i])
+                self.step(evs[i - (steps - n_prof)] if i >= steps - n_prof else None)
             self.flush()
             e1.record(self.mstream)
             last = self.sets[(self.step_no - 1) % NSETS]
@@ -655,7 +661,7 @@ class StreamBench:
             if marks:
                 marks[i].record(self.stream)
                 host_t.append(time.perf_counter())
-            self.step(evs[i])
+            self.step(evs[i - (steps - n_prof)] if i >= steps - n_prof else None)
         self.flush()
         if marks:
             marks[steps].record(self.mstream)
@@ -715,7 +721,7 @@ class StreamBench:
         # stage times summed over the sub-batches (per launch: a stage's duration on its
         # stream; with P > 1 sub-batches overlap, so the sum exceeds the step)
         per_step = {k: v / max(raw.get("nb", 0), 1) for k, v in raw.get("stage_ms", {}).items()}
-        per_step["match"] = sum(a.elapsed_time(b) for a, b in raw["evs"]) / steps
+        per_step["match"] = sum(a.elapsed_time(b) for a, b in raw["evs"]) / max(len(raw["evs"]), 1)
         pyr_bytes = pyramid_bytes_per_frame(self.ex.level_sizes) * self.B
         pyr_s = per_step.get("pyramid", 0.0) / 1e3
         achieved = pyr_bytes / pyr_s / 1e9 if pyr_s > 0 else None
@@ -1430,6 +1436,7 @@ def main_mono(args, og, D, rank, world, stream):
         # ~4 % slower than the same steps after 60)
         # straight into the headline's warm-up steps: the leg's bookkeeping after the headline
         sustained_done = sb.run(args.warmup, n_sus, defer=True)
+        settle = sb.run(args.warmup, SETTLE_STEPS) if SETTLE_STEPS > 0 else None
         r = sb.run(args.warmup, args.steps)
         rs = sustained_done()
         extras["sustained"] = {"steps": n_sus, "warmup": args.warmup, "seconds": round(rs["elapsed"], 3),
@@ -1438,6 +1445,9 @@ def main_mono(args, og, D, rank, world, stream):
                                "stages_ms_per_step": {k: round(v, 4) for k, v in rs["per_step"].items()},
                                "stages_over_last_steps": min(n_sus, PROFILED_TAIL),
                                "headline_host_gap_ms": sb.host_gap_ms,
+                               "settle_leg": None if settle is None else {
+                                   "steps": SETTLE_STEPS, "frames_per_s": round(settle["fps"], 1),
+                                   "step_ms": settle.get("step_ms")},
                                "order": "run before the headline's warm-up and timed steps, its bookkeeping "
                                         "after them (no host work between its last step and their first)"}
     else:
@@ -1515,6 +1525,7 @@ def main_mono(args, og, D, rank, world, stream):
                      "traffic": traffic_for(args.traffic_json, args.config, B),
                      "algorithmic_bytes_per_step": r["pyr_bytes"]},
         "stages_ms_per_step": {k: round(v, 4) for k, v in r["per_step"].items()},
+        "stages_over_last_steps": min(args.steps, PROF_STEPS if PROF_STEPS >= 0 else HEADLINE_PROFILED),
         **({"step_ms": r["step_ms"]} if r.get("step_ms") else {}),
         "keypoints_per_frame": round(r["keypoints"], 1),
         "matches_per_pair": round(r["matches"], 1),
