@@ -721,7 +721,10 @@ class StreamBench:
         # stage times summed over the sub-batches (per launch: a stage's duration on its
         # stream; with P > 1 sub-batches overlap, so the sum exceeds the step)
         per_step = {k: v / max(raw.get("nb", 0), 1) for k, v in raw.get("stage_ms", {}).items()}
-        per_step["match"] = sum(a.elapsed_time(b) for a, b in raw["evs"]) / max(len(raw["evs"]), 1)
+        # the matcher's time beside the extraction: the leg's last match (flushed after the
+        # last extraction) runs alone, so it counts only when it is the one timed
+        mev = raw["evs"][:-1] if len(raw["evs"]) > 1 else raw["evs"]
+        per_step["match"] = sum(a.elapsed_time(b) for a, b in mev) / max(len(mev), 1)
         pyr_bytes = pyramid_bytes_per_frame(self.ex.level_sizes) * self.B
         pyr_s = per_step.get("pyramid", 0.0) / 1e3
         achieved = pyr_bytes / pyr_s / 1e9 if pyr_s > 0 else None
