@@ -23,6 +23,7 @@
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
 #include <algorithm>
+#include <type_traits>
 
 namespace orbgpu {
 
@@ -321,10 +322,27 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
                     mine[u] = s_sortk[min(tid + u * NT, max(m - 1, 0))];
                     rank[u] = 0;
                 }
-                for (int j = 0; j < m; ++j) {
-                    const unsigned long long kj = s_sortk[j];
+                // two keys per 16-byte read, several reads in flight; only the
+                // key slots that exist (the second when m > NT), and a wave
+                // whose threads hold no key skips the loop (wave-uniform)
+                auto rank_keys = [&](auto nu_c) {
+                    constexpr int NU = decltype(nu_c)::value;
+                    int j = 0;
+#pragma unroll 4
+                    for (; j + 1 < m; j += 2) {
+                        const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(s_sortk + j);
 #pragma unroll
-                    for (int u = 0; u < kRankPer; ++u) rank[u] += kj > mine[u];
+                        for (int u = 0; u < NU; ++u) rank[u] += (kk.x > mine[u]) + (kk.y > mine[u]);
+                    }
+                    if (j < m) {
+                        const unsigned long long kj = s_sortk[j];
+#pragma unroll
+                        for (int u = 0; u < NU; ++u) rank[u] += kj > mine[u];
+                    }
+                };
+                if ((tid & ~63) < m) {
+                    if (m > NT) rank_keys(std::integral_constant<int, 2>{});
+                    else rank_keys(std::integral_constant<int, 1>{});
                 }
                 __syncthreads();
 #pragma unroll
