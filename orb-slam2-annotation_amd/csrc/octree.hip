@@ -209,6 +209,9 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
     __syncthreads();
     OCT_T(61);
     const uint32_t* cbase = cand + (size_t)f * g.cand_frame + L.cand_offset;
+    // one root (4:3 and narrower levels): every key's root is 0 and its count
+    // nk -- no per-key LDS atomic on one address, no root remap sweep
+    const bool one_root = nini == 1;
     constexpr int kGather = 8;
     for (int k0 = tid; k0 < nk; k0 += kGather * NT) {
         uint32_t key[kGather];
@@ -223,13 +226,18 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
             const int k = k0 + u * NT;
             if (k < nk) {
                 ks.set_key(k, key[u]);
-                int r = (int)__fdiv_rn((float)key_x(key[u]), L.hx);
-                r = min(r, nini - 1);
-                ks.set_node(k, r);
-                atomicAdd(&s_aux0[r], 1);
+                if (one_root) {
+                    ks.set_node(k, 0);
+                } else {
+                    int r = (int)__fdiv_rn((float)key_x(key[u]), L.hx);
+                    r = min(r, nini - 1);
+                    ks.set_node(k, r);
+                    atomicAdd(&s_aux0[r], 1);
+                }
             }
         }
     }
+    if (one_root && tid == 0) s_aux0[0] = nk;
     __syncthreads();
     OCT_T(1);
     // non-empty roots keep their order; empty ones are erased.  Computed by
@@ -253,7 +261,8 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
         s_aux1[r] = c > 0 ? pos : -1;
     }
     __syncthreads();
-    for (int k = tid; k < nk; k += NT) ks.set_node(k, s_aux1[ks.node(k)]);
+    if (!one_root)  // one root: root 0 is node 0 (when there are keys at all)
+        for (int k = tid; k < nk; k += NT) ks.set_node(k, s_aux1[ks.node(k)]);
     __syncthreads();
 
     OCT_T(2);
