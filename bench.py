@@ -875,6 +875,47 @@ class StereoBench:
         return {"pairs_per_s": pairs_total / elapsed, "elapsed": elapsed, "pairs_total": pairs_total,
                 "keypoints_per_frame": float(n.mean()), "left_keypoints_with_depth": with_depth}
 
+    def parity_timed(self):
+        """The timed path's own outputs against the oracle (untimed, after run()):
+        in the last step's output set -- written by the timed extractor (batch
+        2P) and the timed ComputeStereoMatches launch (P pairs, so the kernel's
+        S-blocks-per-pair split of csrc/stereo.hip is the timed one) -- pairs 0,
+        1, P-2 and P-1: both frames' keypoints (all 7 fields as bits) and
+        descriptors, and uRight / depth as bits against the C++ oracle's stereo
+        Frame (oracle/stereo_ref.cpp, src/Frame.cpp:540-748).  Rank 0's own
+        pairs."""
+        import orbgpu
+        import orbref
+        try:
+            self.D.synchronize()
+            P, W = self.P, self.W
+            si = (self.step_no - 1) % 2
+            pidx = (self.step_no - 1) % POOL_STEPS
+            kps, desc, counts, ur, dp = [t.cpu().numpy() for t in self.sets[si]]
+            exL, exR = orbref.Extractor(nfeatures=self.NF), orbref.Extractor(nfeatures=self.NF)
+            imgs = self.pool[pidx]
+            out = {}
+            for p in sorted({0, 1, P - 2, P - 1} & set(range(P))):
+                left = np.ascontiguousarray(imgs[2 * p, :, :W].cpu().numpy())
+                right = np.ascontiguousarray(imgs[2 * p + 1, :, :W].cpu().numpy())
+                kl, dl, kr, dr, ur_r, dp_r = orbref.stereo_frame(exL, exR, left, right, self.bf)
+                nl, nr = int(counts[2 * p]), int(counts[2 * p + 1])
+                gl = orbgpu.keypoints_from_raw(kps[2 * p, :nl])
+                gr = orbgpu.keypoints_from_raw(kps[2 * p + 1, :nr])
+                frames_ok = (nl == len(kl) and nr == len(kr) and gl.tobytes() == kl.tobytes() and
+                             gr.tobytes() == kr.tobytes() and np.array_equal(desc[2 * p, :nl], dl) and
+                             np.array_equal(desc[2 * p + 1, :nr], dr))
+                n = min(nl, len(ur_r))
+                stereo_ok = (n == len(ur_r) and ur[p, :n].view(np.uint32).tobytes() == ur_r.view(np.uint32).tobytes()
+                             and dp[p, :n].view(np.uint32).tobytes() == dp_r.view(np.uint32).tobytes())
+                out[f"pair {p}"] = {"frames": bool(frames_ok), "uright_depth": bool(stereo_ok),
+                                    "with_depth": int((ur_r >= 0).sum())}
+            ok = all(v["frames"] and v["uright_depth"] for v in out.values())
+            return {"ok": ok, "pairs": out,
+                    "from": f"output set of the last timed step ({P} pairs, the timed extractor and stereo launch)"}
+        except Exception as e:  # report, never hide
+            return {"ok": False, "error": str(e)}
+
     def summary(self, r, steps):
         return {"pairs_per_s": round(r["pairs_per_s"], 1), "ms_per_step": round(r["elapsed"] / steps * 1e3, 3),
                 "pairs_per_gpu_per_step": self.P, "n_gpus": self.world, "width": self.W, "height": self.H,
@@ -1300,6 +1341,8 @@ class LoopLeg:
                  for j, k in enumerate(["search_by_bow", "sim3_setup", "compute_sim3"])}
         res = lb.query_results()
         states = lb.candidate_states()
+        # the timed burst's own outputs against the oracle (untimed): rank 0's first and last query
+        self.last_parity = self.parity_timed(lb, mix, my_q, res, states) if self.rank == 0 else None
         n_kp = 1000
         npairs = len(my_q) * nc
         sbb_bytes = 2 * n_kp * (32 + 4 + 1 + 4 + 4) + n_kp * 4
@@ -1316,7 +1359,65 @@ class LoopLeg:
                 "queries_matched_rank0": int(sum(r.matched >= 0 for r in res)),
                 "mean_round_of_match_rank0": round(float(np.mean([r.round for r in res if r.matched >= 0] or [0])), 2),
                 "ransac_iterations_per_step_rank0": int(sum(r.hypotheses for r in res)),
-                "mean_searchbybow_matches": round(float(lb.nmatches.float().mean().item()), 1)}
+                "mean_searchbybow_matches": round(float(lb.nmatches.float().mean().item()), 1),
+                "parity_vs_oracle": self.last_parity}
+
+    def oracle_vocabulary(self):
+        import orbref
+        if getattr(self, "_ovoc", None) is None:
+            p, l, d, w = self.voc_arrays
+            self._ovoc = orbref.Vocabulary(10, 6, p, l, d, w)
+        return self._ovoc
+
+    def parity_timed(self, lb, mix, my_q, res, states):
+        """The timed burst's outputs (the last timed step's LoopBurst: the batch
+        size, kernels and launch configuration that were timed) against the C++
+        oracle (oracle/loop_ref.cpp, random_r stream per query) for this rank's
+        first and last query (queries 0 and 99 at N = 1): every candidate's
+        SearchByBoW(KF, KF) match count and vpMatches12, the solvers' (N, max
+        iterations, iterations, best inliers), the matched candidate, round,
+        inlier count, hypotheses and draws, the stream after the draws, and the
+        returned Sim3 within tests/test_ransac.py's tolerance
+        (src/LoopClosing.cpp:273-356)."""
+        import ctypes
+        import orbgpu
+        import orbref
+        import ransac
+        try:
+            scene = self.scene(mix)
+            fix = LOOP_MIXES[mix][2]
+            nq, nc = self.nq, self.nc
+            voc = self.oracle_vocabulary()
+            match, nm = lb.match.cpu().numpy(), lb.nmatches.cpu().numpy()
+            out = {}
+            for j in sorted({0, len(my_q) - 1}):
+                q = my_q[j]
+                r = orbref.compute_sim3_query_ex(voc, scene, q, [nq + q * nc + c for c in range(nc)], 1000 + q, fix)
+                g = res[j]
+                chk = {}
+                chk["searchbybow"] = bool(all(int(nm[j * nc + c]) == int(r["nmatches"][c]) and
+                                              np.array_equal(match[j * nc + c, :1000], r["m12"][c])
+                                              for c in range(nc)))
+                chk["solvers"] = bool(all((states[j * nc + c].n, states[j * nc + c].max_iterations,
+                                           states[j * nc + c].iterations, states[j * nc + c].best_inliers) ==
+                                          tuple(int(v) for v in r["cand_state"][c][:4])
+                                          for c in range(nc) if r["nmatches"][c] >= 20))
+                chk["outcome"] = bool((g.matched, g.round, g.n_inliers, g.hypotheses) ==
+                                      (r["matched"], r["round"], r["n_inliers"], r["hypotheses"])
+                                      and g.draws == 3 * r["hypotheses"])
+                after = ransac.RandState.from_buffer_copy(bytes(g.rng_after))
+                chk["stream_after"] = bool(orbgpu.lib().orbgpu_rand_r(ctypes.byref(after)) == r["rand_after"])
+                if r["matched"] >= 0:
+                    tol = 2e-4 * (1 + float(np.abs(r["t12"]).max()))
+                    chk["pose"] = bool(np.abs(np.array(g.R12) - r["R12"].reshape(9)).max() <= 2e-4 and
+                                       abs(g.s12 - r["s12"]) <= 2e-4 and
+                                       np.abs(np.array(g.t12) - r["t12"]).max() <= tol)
+                out[f"query {q}"] = {"ok": all(chk.values()), **chk, "matched": r["matched"]}
+            return {"ok": all(v["ok"] for v in out.values()), "queries": out,
+                    "from": f"the last timed step's LoopBurst ({len(my_q)} queries x {nc} candidates on this rank)",
+                    "tolerance": "integers and matches exact; R12, s12 to 2e-4, t12 to 2e-4*(1+|t|)"}
+        except Exception as e:  # report, never hide
+            return {"ok": False, "error": str(e)}
 
     def cpu_baseline(self, mix, seconds, info):
         """The oracle pipeline in C++ (oracle/liborbref.so: DBoW2 transform,
@@ -1324,8 +1425,7 @@ class LoopLeg:
         with host glibc rand()) over whole queries, 1 thread and all threads."""
         import orbref
         scene = self.scene(mix)
-        p, l, d, w = self.voc_arrays
-        voc = orbref.Vocabulary(10, 6, p, l, d, w)
+        voc = self.oracle_vocabulary()
         nq, nc = self.nq, self.nc
         fix = LOOP_MIXES[mix][2]
 
@@ -1396,7 +1496,9 @@ def main_loopburst(args, rank, world, dev):
             "roofline": {"bound": "hbm", "kernel": b["dominant_kernel"], "frac": b["dominant_hbm_frac"],
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
                          "note": "latency-bound (sequential per-node merge walks / per-query RANSAC chain)"},
-            "mixes": legs}
+            "mixes": legs,
+            "parity_vs_oracle": {m: legs[m].get("parity_vs_oracle") for m in legs if isinstance(legs[m], dict)
+                                 and "parity_vs_oracle" in legs[m]}}
     if "cpu_baseline" in b:
         line["cpu_baseline"] = b["cpu_baseline"]
     return line
@@ -1408,6 +1510,7 @@ def main_stereo(args, og, D, rank, world, stream):
     r = sb.run(args.warmup, args.steps)
     if rank != 0:
         return None
+    parity = sb.parity_timed()
     W, H, NF, desc = CONFIGS[args.config]
     line = {"metric": f"pairs/sec stereo Frame (extract L+R + ComputeStereoMatches, {W}x{H}, {NF} feat)",
             "value": round(r["pairs_per_s"], 1), "unit": "pairs/s", **common_line(args, world),
@@ -1415,7 +1518,8 @@ def main_stereo(args, og, D, rank, world, stream):
             "config": {"workload": desc, "config": args.config, "pairs_per_gpu_per_step": P, "width": W, "height": H,
                        "nfeatures": NF, "parallelism": sb.summary(r, args.steps)["parallelism"]},
             "keypoints_per_frame": round(r["keypoints_per_frame"], 1),
-            "left_keypoints_with_depth": round(r["left_keypoints_with_depth"], 3)}
+            "left_keypoints_with_depth": round(r["left_keypoints_with_depth"], 3),
+            "parity_vs_oracle": parity}
     if D.cuda and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_stereo(args.config, args.cpu_seconds, cpu_info())
     return line
@@ -1498,6 +1602,8 @@ def main_mono(args, og, D, rank, world, stream):
         esb = StereoBench(og, D, "euroc_stereo", 128, rank, world, stream)
         er = esb.run(2, 10)
         extras["stereo_euroc_sharded"] = esb.summary(er, 10)
+        if rank == 0:
+            extras["stereo_euroc_sharded"]["parity_vs_oracle"] = esb.parity_timed()
         del esb
         D.empty_cache()
         # config 5: loop-closure bursts, queries round-robin over all ranks
@@ -1555,6 +1661,7 @@ def main_mono(args, og, D, rank, world, stream):
         other = {}
         kb = StreamBench(og, D, *CONFIGS["kitti"][:3], 256, 0, 1, stream, deliver=args.deliver)
         kr = kb.run(2, 10)
+        k_par = kb.parity_timed()
         kb.close()
         other["mono1241x376"] = {
             "frames_per_s": round(kr["fps"], 1), "ms_per_step": round(kr["elapsed"] / 10 * 1e3, 3),
@@ -1564,11 +1671,12 @@ def main_mono(args, og, D, rank, world, stream):
                                  "algorithmic_bytes_per_step": kr["pyr_bytes"]},
             "stages_ms_per_step": {k: round(v, 4) for k, v in kr["per_step"].items()},
             "keypoints_per_frame": round(kr["keypoints"], 1), "matches_per_pair": round(kr["matches"], 1),
-            "workload": CONFIGS["kitti"][3]}
+            "parity_vs_oracle": k_par, "workload": CONFIGS["kitti"][3]}
         del kb
         D.empty_cache()
         ksb = StereoBench(og, D, "kitti_stereo", 128, 0, 1, stream)
         other["stereo_kitti"] = ksb.summary(ksb.run(2, 10), 10)
+        other["stereo_kitti"]["parity_vs_oracle"] = ksb.parity_timed()
         del ksb
         D.empty_cache()
         line["other_geometries"] = other

@@ -27,6 +27,12 @@
 extern "C" {
 #endif
 
+/* ABI version of this header.  Bumped whenever a struct the library writes
+ * changes layout (round 5 appended orbgpu_extractor_info.device): a host
+ * compares it with orbgpu_abi_version() of the library it loaded, or passes
+ * its own struct size to orbgpu_extractor_get_info_sized. */
+#define ORBGPU_ABI_VERSION 6
+
 enum {
     ORBGPU_OK = 0,
     ORBGPU_ERR_ARG = -1,         /* invalid argument                         */
@@ -59,6 +65,8 @@ typedef struct orbgpu_extractor_info {
 } orbgpu_extractor_info;
 
 const char* orbgpu_last_error(void);
+/* ORBGPU_ABI_VERSION of the header the library was built from. */
+int orbgpu_abi_version(void);
 /* 0 on success; fills the gfx arch name of the current device */
 int orbgpu_device_arch(char* buf, int buflen);
 
@@ -95,6 +103,10 @@ int orbgpu_device_count(int* n);
 int orbgpu_set_thread_device(int device);
 int orbgpu_get_thread_device(int* device);
 int orbgpu_extractor_get_info(const orbgpu_extractor* ex, orbgpu_extractor_info* info);
+/* The same for a caller built against another header version: writes at most
+ * info_size bytes (the caller's sizeof(orbgpu_extractor_info)), so an older,
+ * shorter struct gets its own fields and nothing past them. */
+int orbgpu_extractor_get_info_sized(const orbgpu_extractor* ex, orbgpu_extractor_info* info, size_t info_size);
 
 /* GetScaleFactors / GetInverseScaleFactors / GetScaleSigmaSquares /
  * GetInverseScaleSigmaSquares (ORBextractor.h:63-83).  Arrays of nlevels. */
@@ -240,7 +252,10 @@ int orbgpu_search_for_initialization_batch_device_bounded(
  * another GPU), so no copy of it into the batch is needed.  m12 row b
  * (d_matches12 + b*stride, F1's keypoints) and d_nmatches[b] as above;
  * d_prev_xy (nullable) is vbPrevMatched per pair at + b*stride*2.  The prev
- * frame's capacity must not exceed `stride`.  max_level0 as in _bounded. */
+ * frame's capacity must not exceed `stride`.  max_level0 as in _bounded, and
+ * it must bound the prev frame's level-0 keypoints too (a boundary frame from
+ * another extractor: pass the larger of the two extractors'
+ * level_capacity[0]); a pair above it reports d_nmatches[b] = -1. */
 int orbgpu_search_for_initialization_stream_device(
     int batch, orbgpu_grid_bounds bounds,
     const orbgpu_keypoint* d_kps, const uint8_t* d_desc, const int* d_n, size_t stride,

@@ -14,12 +14,32 @@
 
 namespace orbslam2_amd {
 
-// make `device` the calling thread's device for the host-form calls that follow
-// (orbgpu_set_thread_device; device < 0: leave the thread's device alone)
-inline void use_device(int device) {
-    if (device >= 0 && orbgpu_set_thread_device(device) != ORBGPU_OK)
-        throw std::runtime_error(std::string("orbgpu: ") + orbgpu_last_error());
-}
+// Makes `device` the calling thread's device for the guard's scope (one
+// member call) and restores the thread's previous device at its end, as the
+// extractor entry points do inside the library (DeviceScope): an object placed
+// on GPU k never moves the thread -- or the default (device = -1) objects the
+// thread uses after it -- to GPU k.  device < 0: the thread's device is left
+// alone (the default objects run wherever the thread's device is).
+class DeviceGuard {
+  public:
+    explicit DeviceGuard(int device) {
+        if (device < 0) return;
+        int cur = -1;
+        if (orbgpu_get_thread_device(&cur) != ORBGPU_OK) cur = -1;
+        if (cur == device) return;
+        if (orbgpu_set_thread_device(device) != ORBGPU_OK)
+            throw std::runtime_error(std::string("orbgpu: ") + orbgpu_last_error());
+        prev_ = cur;
+    }
+    ~DeviceGuard() {
+        if (prev_ >= 0) (void)orbgpu_set_thread_device(prev_);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+
+  private:
+    int prev_ = -1;
+};
 
 }  // namespace orbslam2_amd
 

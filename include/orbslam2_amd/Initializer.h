@@ -69,7 +69,7 @@ public:
         int model = 0;
         std::vector<float> p3d(3 * (size_t)(n1 > 0 ? n1 : 1));
         std::vector<unsigned char> tri(n1 > 0 ? n1 : 1);
-        orbslam2_amd::use_device(device_);
+        const orbslam2_amd::DeviceGuard device_guard(device_);
         const int rc = orbgpu_init_initialize(p1.data(), n1, p2.data(), n2, vMatches12.data(), mK, mSigma,
                                               mMaxIterations, &rec, &rh, &model, p3d.data(), tri.data());
         if (rc != ORBGPU_OK) throw std::runtime_error(std::string("orbgpu: ") + orbgpu_last_error());

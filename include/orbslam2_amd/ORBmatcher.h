@@ -323,7 +323,7 @@ public:
         std::vector<int> match(F.N > 0 ? F.N : 1);
         int nm = 0;
         const orbgpu_bow_frame fa = a.frame(), fb = b.frame();
-        orbslam2_amd::use_device(device_);
+        const orbslam2_amd::DeviceGuard device_guard(device_);
         check(orbgpu_search_by_bow(ORBGPU_BOW_KF_F, &fa, &fb, mfNNratio, mbCheckOrientation ? 1 : 0, match.data(),
                                    &nm));
         vpMapPointMatches = std::vector<MapPointT*>(F.N, static_cast<MapPointT*>(nullptr));
@@ -351,7 +351,7 @@ public:
         std::vector<int> match(vp1.empty() ? 1 : vp1.size());
         int nm = 0;
         const orbgpu_bow_frame fa = a.frame(), fb = b.frame();
-        orbslam2_amd::use_device(device_);
+        const orbslam2_amd::DeviceGuard device_guard(device_);
         check(orbgpu_search_by_bow(ORBGPU_BOW_KF_KF, &fa, &fb, mfNNratio, mbCheckOrientation ? 1 : 0,
                                    match.data(), &nm));
         vpMatches12 = std::vector<MapPointT*>(vp1.size(), static_cast<MapPointT*>(nullptr));
@@ -383,7 +383,7 @@ public:
         const int flags = (mbCheckOrientation ? ORBGPU_MATCH_CHECK_ORI : 0) |
                           (mbAnnotatedHisto ? ORBGPU_MATCH_ANNOTATED_HISTO : 0);
         int nmatches = 0;
-        orbslam2_amd::use_device(device_);
+        const orbslam2_amd::DeviceGuard device_guard(device_);
         check(orbgpu_search_for_initialization(bd, k1.data(), d1.data(), (int)n1, k2.data(), d2.data(), (int)n2,
                                                prev.data(), windowSize, mfNNratio, flags, vnMatches12.data(),
                                                &nmatches));
@@ -439,7 +439,7 @@ public:
         P.only_stereo = bOnlyStereo ? 1 : 0;
         std::vector<int> m12(n1 > 0 ? n1 : 1);
         int nm = 0;
-        orbslam2_amd::use_device(device_);
+        const orbslam2_amd::DeviceGuard device_guard(device_);
         check(orbgpu_search_for_triangulation(&P, mbCheckOrientation ? 1 : 0, m12.data(), &nm));
         vMatchedPairs.clear();
         vMatchedPairs.reserve(nm);
@@ -706,7 +706,7 @@ private:
 
     int run(const orbgpu_proj_call& c, std::vector<int>& match) const {
         int nm = 0;
-        orbslam2_amd::use_device(device_);
+        const orbslam2_amd::DeviceGuard device_guard(device_);
         orbslam2_amd::detail::check(orbgpu_search_by_projection(&c, match.data(), &nm));
         return nm;
     }

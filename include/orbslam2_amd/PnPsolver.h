@@ -124,7 +124,7 @@ public:
         std::vector<uint8_t> best = mvbBestInliers, refined(N > 0 ? N : 1, 0);
         if (best.empty()) best.assign(1, 0);
         orbgpu_pnp_result r;
-        orbslam2_amd::use_device(device_);
+        const orbslam2_amd::DeviceGuard device_guard(device_);
         check(orbgpu_pnp_ransac_batch(1, &p, N, mvP3Dw.data(), mvP2D.data(), mvMaxError.data(), n_hyp,
                                       samples.empty() ? nullptr : samples.data(), &r, best.data(), refined.data()));
         orbgpu_rand_set_state(&snap);  // consume exactly the iterations the reference ran

@@ -133,7 +133,7 @@ public:
         }
         std::vector<uint8_t> mask = mvbBestInliers;
         orbgpu_sim3_result r;
-        orbslam2_amd::use_device(device_);
+        const orbslam2_amd::DeviceGuard device_guard(device_);
         check(orbgpu_sim3_ransac_batch(1, &p, N, mvX3Dc1.data(), mvX3Dc2.data(), mvnMaxError1.data(),
                                        mvnMaxError2.data(), n_hyp, samples.empty() ? nullptr : samples.data(), &r,
                                        mask.data()));

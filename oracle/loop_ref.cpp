@@ -312,11 +312,26 @@ int orbref_search_by_bow_kf_f(const int* nodes_a, const int* start_a, const int*
  * cands[0..n_cand) of a scene laid out as synth.loop_burst_scene: desc
  * (n_kf, n_kp, 32), angle/valid (n_kf, n_kp), octave (n_kf, n_kp) i32,
  * mp_world (n_kf, n_kp, 3), Tcw (n_kf, 12), K (4), sigma2 (levels).
- * out: {matched, round, n_inliers, hypotheses}; nmatches: int[n_cand]. */
+ * out: {matched, round, n_inliers, hypotheses}; nmatches: int[n_cand].
+ * The _ex form also returns, when the pointers are not null: every
+ * candidate's vpMatches12 (m12: int[n_cand][n_kp], -1 = none), the returned
+ * Sim3 (pose: R12[9], t12[3], s12; zeros when no candidate returned one),
+ * the solvers' (N, max_its, iterations, best inliers, discarded) per
+ * candidate (cand_state: int[n_cand][5]) and the next random_r value of the
+ * query's stream after its draws (rand_after). */
 int orbref_compute_sim3_query(const orbref_vocabulary* h, int n_kp, const uint8_t* desc, const float* angle,
                               const int32_t* octave, const uint8_t* valid, const float* mp_world, const float* Tcw,
                               const float* K, const float* sigma2, int cur, const int* cands, int n_cand,
                               unsigned seed, int fix_scale, int* out, int* nmatches) {
+    return orbref_compute_sim3_query_ex(h, n_kp, desc, angle, octave, valid, mp_world, Tcw, K, sigma2, cur, cands,
+                                        n_cand, seed, fix_scale, out, nmatches, nullptr, nullptr, nullptr, nullptr);
+}
+
+int orbref_compute_sim3_query_ex(const orbref_vocabulary* h, int n_kp, const uint8_t* desc, const float* angle,
+                                 const int32_t* octave, const uint8_t* valid, const float* mp_world,
+                                 const float* Tcw, const float* K, const float* sigma2, int cur, const int* cands,
+                                 int n_cand, unsigned seed, int fix_scale, int* out, int* nmatches, int* m12_out,
+                                 float* pose, int* cand_state, int* rand_after) {
     const int min_matches = 20, min_inliers = 20, max_its = 300, per_call = 5;
     const double prob = 0.99;
     auto kf = [&](int i, size_t per) { return (size_t)i * (size_t)n_kp * per; };
@@ -332,6 +347,7 @@ int orbref_compute_sim3_query(const orbref_vocabulary* h, int n_kp, const uint8_
                                            f2, desc + kf(k2, 32), angle + kf(k2, 1), valid + kf(k2, 1), n_kp, 0.75f,
                                            true, m12.data());
         nmatches[c] = nm;
+        if (m12_out) std::memcpy(m12_out + (size_t)c * n_kp, m12.data(), sizeof(int) * (size_t)n_kp);
         Solver& s = sol[c];
         if (nm < min_matches) { s.discarded = true; continue; }
         // Sim3Solver ctor (S3:37-107)
@@ -354,6 +370,7 @@ int orbref_compute_sim3_query(const orbref_vocabulary* h, int n_kp, const uint8_
     for (auto& s : sol) n_live += !s.discarded;
     int rnd = -1;
     out[0] = -1; out[1] = -1; out[2] = 0;
+    if (pose) std::memset(pose, 0, 13 * sizeof(float));
     int ints[4];
     float T[16], R[9], t[3], sc;
     std::vector<uint8_t> inl;
@@ -392,12 +409,28 @@ int orbref_compute_sim3_query(const orbref_vocabulary* h, int n_kp, const uint8_
             if (found) {
                 out[0] = c; out[1] = rnd; out[2] = s.best;
                 matched = true;
+                if (pose) {
+                    std::memcpy(pose, R, 9 * sizeof(float));
+                    std::memcpy(pose + 9, t, 3 * sizeof(float));
+                    pose[12] = sc;
+                }
             }
         }
     }
     int hyp = 0;
     for (auto& s : sol) hyp += s.iterations;
     out[3] = hyp;
+    if (cand_state)
+        for (int c = 0; c < n_cand; ++c) {
+            const Solver& s = sol[c];
+            int* o = cand_state + 5 * c;
+            o[0] = s.N; o[1] = s.max_its; o[2] = s.iterations; o[3] = s.best; o[4] = s.discarded ? 1 : 0;
+        }
+    if (rand_after) {
+        int32_t r;
+        random_r(&rng.rd, &r);
+        *rand_after = r;
+    }
     return out[0];
 }
 

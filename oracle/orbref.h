@@ -138,6 +138,11 @@ int orbref_compute_sim3_query(const orbref_vocabulary* voc, int n_kp, const uint
                               const int32_t* octave, const uint8_t* valid, const float* mp_world, const float* Tcw,
                               const float* K, const float* sigma2, int cur, const int* cands, int n_cand,
                               unsigned seed, int fix_scale, int* out, int* nmatches);
+int orbref_compute_sim3_query_ex(const orbref_vocabulary* voc, int n_kp, const uint8_t* desc, const float* angle,
+                                 const int32_t* octave, const uint8_t* valid, const float* mp_world,
+                                 const float* Tcw, const float* K, const float* sigma2, int cur, const int* cands,
+                                 int n_cand, unsigned seed, int fix_scale, int* out, int* nmatches, int* m12_out,
+                                 float* pose, int* cand_state, int* rand_after);
 
 #ifdef __cplusplus
 }

@@ -74,6 +74,8 @@ def lib() -> ctypes.CDLL:
                                                   vp, vp, f, f, i, i, vp]
         L.orbref_compute_sim3_query.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, i, ctypes.c_uint, i,
                                                 vp, vp]
+        L.orbref_compute_sim3_query_ex.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, i, ctypes.c_uint,
+                                                   i, vp, vp, vp, vp, vp, vp]
         _LIB = L
     return _LIB
 
@@ -364,3 +366,28 @@ def compute_sim3_query(voc: Vocabulary, scene, cur, cands, seed, fix_scale=False
     lib().orbref_compute_sim3_query(voc.h, c[0].shape[1], *[_p(a) for a in c], int(cur), _p(cd), len(cd),
                                     int(seed) & 0xFFFFFFFF, int(fix_scale), _p(out), _p(nm))
     return int(out[0]), int(out[1]), int(out[2]), int(out[3]), nm
+
+
+def compute_sim3_query_ex(voc: Vocabulary, scene, cur, cands, seed, fix_scale=False):
+    """compute_sim3_query with everything a parity check compares: a dict of
+    matched, round, n_inliers, hypotheses, nmatches[n_cand], m12[n_cand, n_kp]
+    (vpMatches12 of SearchByBoW(KF, KF)), cand_state[n_cand, 5] (N, max_its,
+    iterations, best inliers, discarded), R12/t12/s12 of the returned Sim3 and
+    rand_after (the next value of the query's glibc stream after its draws)."""
+    c = scene.get("_c")
+    if c is None:
+        c = scene["_c"] = [np.ascontiguousarray(scene[k], t) for k, t in _SCENE_KEYS]
+    n_kp = c[0].shape[1]
+    cd = np.ascontiguousarray(cands, np.int32)
+    out = np.zeros(4, np.int32)
+    nm = np.zeros(len(cd), np.int32)
+    m12 = np.zeros((len(cd), n_kp), np.int32)
+    pose = np.zeros(13, np.float32)
+    cs = np.zeros((len(cd), 5), np.int32)
+    ra = np.zeros(1, np.int32)
+    lib().orbref_compute_sim3_query_ex(voc.h, n_kp, *[_p(a) for a in c], int(cur), _p(cd), len(cd),
+                                       int(seed) & 0xFFFFFFFF, int(fix_scale), _p(out), _p(nm), _p(m12), _p(pose),
+                                       _p(cs), _p(ra))
+    return {"matched": int(out[0]), "round": int(out[1]), "n_inliers": int(out[2]), "hypotheses": int(out[3]),
+            "nmatches": nm, "m12": m12, "cand_state": cs, "R12": pose[:9].reshape(3, 3), "t12": pose[9:12],
+            "s12": float(pose[12]), "rand_after": int(ra[0])}

@@ -27,6 +27,7 @@
 //                          monocular pairs, CheckDistEpipolarLine :166-190).
 #include "../../include/orbgpu_bow.h"
 #include "bow_kernels.h"
+#include "device_state.h"
 
 namespace orbgpu {
 
@@ -843,14 +844,16 @@ hipError_t launch_search_by_bow(int mode, int batch, const orbgpu_bow_frame* a, 
                                 float nnratio, int check_ori, int stride, int* match, int* nmatches,
                                 hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
-    static const hipError_t attr = [] {
+    // the staged variants' LDS limit, once per device (device_state.h)
+    static PerDeviceOnce attr_once;
+    const hipError_t attr = attr_once.get([](int) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&search_by_bow_kernel<1>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, kBowStageMaxLds);
         if (e == hipSuccess)
             e = hipFuncSetAttribute(reinterpret_cast<const void*>(&search_by_bow_kernel<2>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, kBowStageMaxLds);
         return e;
-    }();
+    });
     if (attr != hipSuccess) return attr;
     if (bow_stage_bytes(stride, 2) <= (size_t)kBowStageMaxLds)
         hipLaunchKernelGGL(search_by_bow_kernel<2>, dim3(batch), dim3(kBowThreads), bow_stage_bytes(stride, 2), stream, mode,

@@ -20,6 +20,7 @@
 #include "../../include/orbgpu.h"
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdlib>
 #include <type_traits>
 
@@ -197,10 +198,18 @@ static_assert(kKeysPerWave == 1 || kKeysPerWave == 2 || kKeysPerWave == 4, "ORBG
 
 // Per-wave LDS: the raw 43x48 neighbourhood (re-staged per keypoint) and one
 // blurred 37x40 patch per keypoint of the wave.
+// Every region starts on a 16-byte boundary: lanes past the raw patch dump
+// their 16-byte staging chunk into the keypoint's blur region with a 128-bit
+// store, so each blur slot is padded to 16 bytes (1480 -> 1488 at the default
+// pitches; one slot per wave by default, where the struct's alignment already
+// rounded it up).
+constexpr int kRawBytes = (kPatch * kRPitch + 15) & ~15;
+constexpr int kBlurSlotBytes = (kBlur * kBPitch + 15) & ~15;
 struct alignas(16) DescLds {
-    uint8_t raw[kPatch * kRPitch];
-    uint8_t blur[kKeysPerWave][kBlur * kBPitch];
+    uint8_t raw[kRawBytes];
+    uint8_t blur[kKeysPerWave][kBlurSlotBytes];
 };
+static_assert(offsetof(DescLds, blur) % 16 == 0 && kBlurSlotBytes % 16 == 0, "16-byte dump stores into blur[k]");
 
 // A keypoint slot of a frame: its level, index within the level and output
 // position; false when the slot is past the level's octree count.

@@ -543,8 +543,11 @@ int match_batch_threads() {
 }
 
 bool match_tiny_enabled() {
-    const char* s = std::getenv("ORBGPU_MATCH_TINY");  // read per launch (A/B)
-    return !s || std::atoi(s) != 0;
+    static const bool v = [] {  // read once per process (A/B runs set it per process)
+        const char* s = std::getenv("ORBGPU_MATCH_TINY");
+        return !s || std::atoi(s) != 0;
+    }();
+    return v;
 }
 
 template <int kMaxK0, int kThreads>

@@ -424,8 +424,11 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     // Key capacity (a multiple of 64) for a requested one: the keys and their node
     // indices (6 bytes a key) in the requested LDS bytes less 64, and the whole
     // workgroup within 64 KiB; a level with more candidates uses HBM scratch.
+    // keys in LDS (4 B key + 2 B node id each) for a request of `req` keys, in
+    // steps of 64, shrunk until the workgroup's LDS fits 64 KiB: a request of
+    // 2560 yields 2560 (round 5 subtracted a leftover 64 B and got 2496)
     auto key_capacity = [&g](int req, int ncap_) {
-        const long bytes = (long)round_up((size_t)req * 4, 16) + (long)round_up((size_t)req * 2, 16) - 64;
+        const long bytes = (long)round_up((size_t)req * 4, 16) + (long)round_up((size_t)req * 2, 16);
         int kc = bytes > 0 ? (int)(bytes / 6) & ~63 : 0;
         while (kc > 0 && octree_lds_bytes(g, kc, ncap_) > 65536) kc -= 64;
         return kc;
@@ -728,6 +731,18 @@ int orbgpu_get_thread_device(int* device) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(ORBGPU_ERR_NO_DEVICE, "no HIP device visible");
     ORB_HIP(hipGetDevice(device));
+    return ORBGPU_OK;
+}
+
+int orbgpu_abi_version(void) { return ORBGPU_ABI_VERSION; }
+
+int orbgpu_extractor_get_info_sized(const orbgpu_extractor* e, orbgpu_extractor_info* info, size_t info_size) {
+    if (!e || !info) return fail(ORBGPU_ERR_ARG, "NULL argument");
+    if (info_size == 0) return fail(ORBGPU_ERR_ARG, "info_size is 0");
+    orbgpu_extractor_info full;
+    const int rc = orbgpu_extractor_get_info(e, &full);
+    if (rc) return rc;
+    std::memcpy(info, &full, std::min(info_size, sizeof(full)));
     return ORBGPU_OK;
 }
 

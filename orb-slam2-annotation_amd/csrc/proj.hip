@@ -11,6 +11,7 @@
 // 20 | grid position) reproduce the reference's first-best-in-order choice.
 #include "../../include/orbgpu_proj.h"
 #include "proj_kernels.h"
+#include "device_state.h"
 
 namespace orbgpu {
 
@@ -848,8 +849,12 @@ int proj_max_keypoints() { return kMaxKps; }
 hipError_t launch_search_by_projection(int ncalls, const orbgpu_proj_call* calls, int stride, int* match,
                                        int* nmatches, hipStream_t stream) {
     if (ncalls <= 0) return hipSuccess;
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&proj_kernel),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, kProjDynLds);
+    // the kernel's LDS limit, once per device (device_state.h)
+    static PerDeviceOnce attr_once;
+    const hipError_t attr = attr_once.get([](int) {
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&proj_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, kProjDynLds);
+    });
     if (attr != hipSuccess) return attr;
     hipLaunchKernelGGL(proj_kernel, dim3(ncalls), dim3(kProjThreads), kProjDynLds, stream, calls, stride, match,
                        nmatches);

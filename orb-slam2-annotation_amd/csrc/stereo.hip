@@ -35,6 +35,7 @@
 #include "../../include/orbgpu.h"
 #include "orbgpu_internal.h"
 #include "stereo_kernels.h"
+#include "device_state.h"
 
 namespace orbgpu {
 
@@ -319,20 +320,15 @@ int stereo_split_max() {
 hipError_t launch_stereo(const StereoArgs& a, int npairs, hipStream_t stream) {
     if (npairs <= 0) return hipSuccess;
     const size_t lds = stereo_lds_bytes(a.cap, a.lvl_h[0]);
-    // per-process state (the drop-in calls this per frame): the kernel's LDS
-    // attribute only grows, the CU count is read once
-    static thread_local size_t lds_set = 0;
-    if (lds > lds_set) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&stereo_kernel),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    // per-device state (device_state.h; the drop-in calls this per frame, from
+    // any thread, on any device): the kernel's LDS limit only grows, the CU
+    // count is read once per device
+    static PerDeviceLdsLimit lds_limit;
+    {
+        const hipError_t e = lds_limit.ensure(reinterpret_cast<const void*>(&stereo_kernel), lds);
         if (e != hipSuccess) return e;
-        lds_set = lds;
     }
-    static const int ncu = [] {
-        int dev = 0, n = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        return n;
-    }();
+    const int ncu = current_device_cus();
     // blocks per pair: at least two 1024-thread blocks per CU over the launch
     const int S = std::min(stereo_split_max(), std::max(1, (2 * ncu + npairs - 1) / npairs));
     hipLaunchKernelGGL(stereo_kernel, dim3(npairs * S), dim3(kStThreads), lds, stream, a, S);

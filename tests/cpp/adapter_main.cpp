@@ -1001,6 +1001,52 @@ int main(int argc, char** argv) {
             return 3;
         }
     }
+    if (argc >= 2 && !strcmp(argv[1], "devguard")) {
+        // Device.h's DeviceGuard: an object placed on GPU k runs its call on k and
+        // leaves the thread's device as it was, so a default (device = -1) object used after it
+        // on the same thread still runs on the thread's device.  Prints "ok <devices>".
+        try {
+            int n = 0, cur = -1;
+            if (orbgpu_device_count(&n) != ORBGPU_OK || n <= 0) return 2;
+            if (orbgpu_set_thread_device(0) != ORBGPU_OK) return 2;
+            for (int d = n - 1; d >= 0; --d) {
+                {
+                    orbslam2_amd::DeviceGuard g(d);
+                    if (orbgpu_get_thread_device(&cur) != ORBGPU_OK || cur != d) return 4;
+                }
+                if (orbgpu_get_thread_device(&cur) != ORBGPU_OK || cur != 0) return 5;
+            }
+            // a matcher placed on the last device, then a default one, on one thread
+            std::vector<unsigned char> buf(640 * 480);
+            for (size_t i = 0; i < buf.size(); ++i) buf[i] = (unsigned char)((i * 2654435761u) >> 24);
+            cv::Mat img(480, 640, CV_8UC1, buf.data(), (size_t)640);
+            ORB_SLAM2::ORBextractor ex(500, 1.2f, 8, 20, 7);
+            MiniFrame F[2];
+            for (int f = 0; f < 2; ++f) {
+                ex(img, cv::Mat(), F[f].mvKeysUn, F[f].mDescriptors);
+                F[f].mnMaxX = 640.f;
+                F[f].mnMaxY = 480.f;
+            }
+            std::vector<cv::Point2f> prev;
+            for (const cv::KeyPoint& k : F[0].mvKeysUn) prev.push_back(k.pt);
+            std::vector<cv::Point2f> prev2 = prev;
+            std::vector<int> m12, m12b;
+            ORB_SLAM2::ORBmatcher placed(0.9f, true, n - 1), plain(0.9f, true);
+            const int a = placed.SearchForInitialization(F[0], F[1], prev, m12, 100);
+            if (orbgpu_get_thread_device(&cur) != ORBGPU_OK || cur != 0) return 6;
+            const int b = plain.SearchForInitialization(F[0], F[1], prev2, m12b, 100);
+            if (orbgpu_get_thread_device(&cur) != ORBGPU_OK || cur != 0) return 7;
+            if (a != b || m12 != m12b || a < 100) {
+                fprintf(stderr, "placed %d vs default %d matches\n", a, b);
+                return 8;
+            }
+            printf("ok %d\n", n);
+            return 0;
+        } catch (const std::exception& e) {
+            fprintf(stderr, "exception: %s\n", e.what());
+            return 3;
+        }
+    }
     if (argc >= 2 && !strcmp(argv[1], "empty")) {
         ORB_SLAM2::ORBextractor ex(1000, 1.2f, 8, 20, 7);
         std::vector<cv::KeyPoint> kps(3);

@@ -98,3 +98,36 @@ def test_device_placement_on_gpu():
     kr, dr = orbref.Extractor().extract(img)
     kg, dg = out["r"]
     assert kg.tobytes() == kr.tobytes() and np.array_equal(dg, dr)
+
+
+def test_abi_version_matches_header():
+    """ORBGPU_ABI_VERSION of include/orbgpu.h equals what the loaded library
+    reports (no device needed): a host built against another header can tell."""
+    import re
+    import orbgpu
+    hdr = (Path(__file__).resolve().parents[1] / "include" / "orbgpu.h").read_text()
+    v = int(re.search(r"#define ORBGPU_ABI_VERSION (\d+)", hdr).group(1))
+    assert orbgpu.lib().orbgpu_abi_version() == v
+
+
+@pytest.mark.gpu
+def test_get_info_sized_writes_no_more_than_the_callers_struct():
+    """A caller built against the round-4 header (orbgpu_extractor_info
+    without the trailing `device`) passes its own size: the library fills
+    its fields and leaves the bytes past them untouched."""
+    import orbgpu
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ex = orbgpu.Extractor()
+    L = orbgpu.lib()
+    full = ctypes.sizeof(orbgpu._Info)
+    old = full - 4  # the struct before the device field
+    buf = (ctypes.c_uint8 * (full + 16))(*([0xAB] * (full + 16)))
+    assert L.orbgpu_extractor_get_info_sized(ex.h, ctypes.cast(buf, ctypes.c_void_p),
+                                             ctypes.c_size_t(old)) == 0
+    raw = bytes(buf)
+    assert raw[old:] == b"\xAB" * (full + 16 - old)
+    info = orbgpu._Info.from_buffer_copy(raw[:old] + b"\0" * 4)
+    assert (info.nlevels, info.width, info.height) == (8, 640, 480)
+    assert L.orbgpu_extractor_get_info_sized(ex.h, ctypes.cast(buf, ctypes.c_void_p),
+                                             ctypes.c_size_t(0)) == orbgpu.ERR_ARG

@@ -60,6 +60,16 @@ def test_adapter_device_argument(exe):
     assert r.returncode == 3 and "ordinal 99" in r.stderr, r.stdout + r.stderr
 
 
+@pytest.mark.gpu
+def test_adapter_device_guard_restores_thread_device(exe):
+    """Device.h: a member call of an object placed on GPU k runs on
+    k and restores the thread's device afterwards, so a default object used
+    next on the same thread stays on the thread's device; both matchers give
+    the same SearchForInitialization result."""
+    r = subprocess.run([exe, "devguard"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("ok "), (r.returncode, r.stdout + r.stderr)
+
+
 def _read_frame(buf, off):
     n, = struct.unpack_from("<i", buf, off)
     off += 4

@@ -196,3 +196,98 @@ def test_gpu_loop_burst_slice_vs_oracle(big_vocab, fracs, ofracs, fix_scale):
     if np.ndim(fracs) == 0 and fracs == 0.0:
         assert all(r.matched == -1 for r in results[:nq])
         assert all(st.discarded for st in states[:nq * nc])
+
+
+def test_cpp_query_ex_matches_python_pipeline():
+    """orbref.compute_sim3_query_ex (oracle/loop_ref.cpp: what bench.py's
+    loop-burst parity and the 100 x 5 GPU test compare against) equals the
+    Python oracle pipeline: matches, solver states, outcome, pose and the
+    stream after the query's draws."""
+    import orbref
+    k, L, p, l, d, w = 10, 4, *synth.synthetic_vocabulary_fast(10, 4, 5)
+    avoc = loop_ref.ArrayVocabulary(k, L, 0, 0, p, l, d, w)
+    cvoc = orbref.Vocabulary(k, L, p, l, d, w)
+    nq, nc = 3, 4
+    scene = synth.loop_burst_scene(nq, nc, d[l == 1], n_kp=500, inlier_frac=[0.0, 0.05, 0.4, 0.4],
+                                   outlier_frac=[0.0, 0.1, 0.5, 0.5], seed=23)
+    queries = [(q, [nq + q * nc + c for c in range(nc)]) for q in range(nq)]
+    seeds = [41 + q for q in range(nq)]
+    ref = _oracle_pipeline(scene, avoc, queries, seeds)
+    matched = 0
+    for (cur, cands), seed, (per, solvers, r) in zip(queries, seeds, ref):
+        got = orbref.compute_sim3_query_ex(cvoc, scene, cur, cands, seed)
+        for c in range(nc):
+            assert got["nmatches"][c] == per[c][0]
+            np.testing.assert_array_equal(got["m12"][c], per[c][1])
+            if solvers[c] is not None:
+                s = solvers[c]
+                assert tuple(got["cand_state"][c][:4]) == (s.N, s.max_its, s.iterations, s.best)
+        assert (got["matched"], got["round"], got["n_inliers"], got["hypotheses"]) == \
+            (r["matched"], r["round"], r["n_inliers"], r["hypotheses"])
+        assert got["rand_after"] == r["after"]
+        if r["matched"] >= 0:
+            matched += 1
+            pose = solvers[r["matched"]].best_pose
+            np.testing.assert_allclose(got["R12"], pose["R12"], atol=1e-6)
+            np.testing.assert_allclose(got["t12"], pose["t12"], atol=1e-6 * (1 + np.abs(pose["t12"]).max()))
+            assert abs(got["s12"] - pose["s12"]) < 1e-6
+    assert matched > 0
+
+
+@pytest.mark.gpu
+def test_gpu_loop_burst_bench_size_vs_oracle(big_vocab):
+    """bench.py's loop_burst leg at its timed size: 100 ComputeSim3 queries x 5
+    candidates in one burst (the bench mix: 40 % true correspondences), every
+    query against the C++ oracle (oracle/loop_ref.cpp, per-query random_r
+    stream): SearchByBoW match counts and vpMatches12, solver states, the
+    outcome (candidate, round, inliers, hypotheses, draws), the stream after
+    the draws and the returned Sim3 within tests/test_ransac.py's tolerance."""
+    torch = _gpu()
+    from concurrent.futures import ThreadPoolExecutor
+
+    import bow
+    import loop
+    import orbgpu
+    import orbref
+    import ransac
+    path, (p, l, d, w) = big_vocab
+    voc = bow.Vocabulary.load_text(str(path))
+    nq, nc = 100, 5
+    scene = synth.loop_burst_scene(nq, nc, d[l == 1], n_kp=1000, inlier_frac=0.4, outlier_frac=0.6, seed=55,
+                                   fix_scale=False)
+    kfs = loop.Keyframes(scene["desc"], scene["angle"], scene["octave"], scene["valid"], scene["mp_world"],
+                         scene["Tcw"], scene["K"], scene["sigma2"])
+    kfs.compute_bow(voc)
+    queries = [(q, [nq + q * nc + c for c in range(nc)], 1000 + q) for q in range(nq)]
+    lb = loop.LoopBurst(kfs, queries, fix_scale=False)
+    lb.step()
+    torch.cuda.synchronize()
+    cvoc = orbref.Vocabulary(10, 6, p, l, d, w)
+    scene["_c"] = None
+    orbref.compute_sim3_query_ex(cvoc, scene, 0, queries[0][1], 1000)  # lays out the scene arrays once
+    with ThreadPoolExecutor(8) as pool:  # ctypes releases the GIL; each query has its own random_r state
+        refs = list(pool.map(lambda qc: orbref.compute_sim3_query_ex(cvoc, scene, qc[0], qc[1], qc[2]), queries))
+    match, nm = lb.match.cpu().numpy(), lb.nmatches.cpu().numpy()
+    results, states = lb.query_results(), lb.candidate_states()
+    n_matched = 0
+    for q, r in enumerate(refs):
+        for c in range(nc):
+            pc = q * nc + c
+            assert nm[pc] == r["nmatches"][c], (q, c)
+            np.testing.assert_array_equal(match[pc, :1000], r["m12"][c])
+            if r["nmatches"][c] >= 20:
+                st = states[pc]
+                assert (st.n, st.max_iterations, st.iterations, st.best_inliers) == \
+                    tuple(int(v) for v in r["cand_state"][c][:4]), (q, c)
+        g = results[q]
+        assert (g.matched, g.round, g.n_inliers, g.hypotheses) == \
+            (r["matched"], r["round"], r["n_inliers"], r["hypotheses"]), q
+        assert g.draws == 3 * r["hypotheses"]
+        after = ransac.RandState.from_buffer_copy(bytes(g.rng_after))
+        assert orbgpu.lib().orbgpu_rand_r(ctypes.byref(after)) == r["rand_after"], q
+        if r["matched"] >= 0:
+            n_matched += 1
+            np.testing.assert_allclose(np.array(g.R12).reshape(3, 3), r["R12"], atol=2e-4)
+            assert abs(g.s12 - r["s12"]) < 2e-4
+            np.testing.assert_allclose(np.array(g.t12), r["t12"], atol=2e-4 * (1 + np.abs(r["t12"]).max()))
+    assert n_matched >= 50
