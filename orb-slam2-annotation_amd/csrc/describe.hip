@@ -194,6 +194,17 @@ __device__ inline int reflect101(int p, int n) { return p < 0 ? -p : (p >= n ? 2
 #define ORBGPU_DESC_KEYS 1
 #endif
 constexpr int kKeysPerWave = ORBGPU_DESC_KEYS;
+
+// Diagnostic builds (-DDESC_LDS_PROBE=mask; wrong results by design): the
+// LDS accesses of the phases in `mask` are redirected to conflict-free
+// addresses (consecutive dwords per lane, or a coprime stride) with the same
+// instructions, so SQ_LDS_BANK_CONFLICT of a probe build against the product
+// build is that phase's share of the bank conflicts, and its time what they
+// cost.  1: the rBRIEF test reads, 2: the blur's row-pass reads, 4: the
+// moments' disc reads, 8: the blurred-patch stores.
+#ifndef DESC_LDS_PROBE
+#define DESC_LDS_PROBE 0
+#endif
 static_assert(kKeysPerWave == 1 || kKeysPerWave == 2 || kKeysPerWave == 4, "ORBGPU_DESC_KEYS: 1, 2 or 4");
 
 // Per-wave LDS: the raw 43x48 neighbourhood (re-staged per keypoint) and one
@@ -350,7 +361,11 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
 #pragma unroll
     for (int k = 0; k < kDiscLoads; ++k) {
         const DiscWord e = c_disc.w[od][lane + 64 * k];
+#if DESC_LDS_PROBE & 4
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(rawbuf + 4 * lane + 256 * k + (e.off & 0));
+#else
         const uint32_t w = *reinterpret_cast<const uint32_t*>(disc + e.off);
+#endif
         sp = __builtin_amdgcn_udot4(w, e.m1, sp, false);
         cp = __builtin_amdgcn_udot4(w, e.mc, cp, false);
         vp = __builtin_amdgcn_udot4(w, e.mv, vp, false);
@@ -384,7 +399,11 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
         const int qq = (int)(__umul24((uint32_t)lane, 10923u) >> 16), c = lane - qq * kColChunks;
         const int q = min(qq, kQuads - 1), r0 = c * 7;
         const bool simd = xb + 4 * q < simd_end, store = qq < kQuads;
+#if DESC_LDS_PROBE & 2
+        const uint32_t raw0 = 12u * (uint32_t)lane + 0u * (uint32_t)(r0 + q);
+#else
         const uint32_t raw0 = __umul24((uint32_t)r0, (uint32_t)kRPitch) + 4u * (uint32_t)q;
+#endif
         const uint32_t out0 = __umul24((uint32_t)r0, (uint32_t)kBPitch) + 4u * (uint32_t)q;
         auto row = [&](int k, blurdev::f32x2& lo, blurdev::f32x2& hi) {
             const uint32_t* w = reinterpret_cast<const uint32_t*>(rawbuf + raw0 + k * kRPitch);
@@ -413,8 +432,13 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
                     blurdev::col_pass(wl[j], wl[j + 1], wl[j + 2], wl[j + 3], wl[j + 4], wl[j + 5], wl[j + 6]);
                 const blurdev::f32x2 hi =
                     blurdev::col_pass(wh[j], wh[j + 1], wh[j + 2], wh[j + 3], wh[j + 4], wh[j + 5], wh[j + 6]);
+#if DESC_LDS_PROBE & 8
+                *reinterpret_cast<uint32_t*>(blur_out + ((4 * lane + 256 * j) & 1023) + (out0 & 0)) =
+                    all_simd ? blurdev::pack4_simd(lo, hi) : blurdev::pack4(lo, hi, simd);
+#else
                 *reinterpret_cast<uint32_t*>(blur_out + out0 + j * kBPitch) =
                     all_simd ? blurdev::pack4_simd(lo, hi) : blurdev::pack4(lo, hi, simd);
+#endif
             }
         }
     };
@@ -457,7 +481,11 @@ __device__ void describe_tests(const Geom& g, int f, const KeyRef& K, int lane, 
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) {
             const uint32_t iy = __float_as_uint(pp ? my.y : my.x), ix = __float_as_uint(pp ? mx.y : mx.x);
+#if DESC_LDS_PROBE & 1
+            val[pp] = blur[(int)(4u * (uint32_t)lane + (uint32_t)pp + ((__umul24(iy, (uint32_t)kBPitch) + ix + cb) & 0x300u))];
+#else
             val[pp] = blur[(int)(__umul24(iy, (uint32_t)kBPitch) + ix + cb)];
+#endif
         }
         words[rnd] = __ballot(val[0] < val[1]);
     }

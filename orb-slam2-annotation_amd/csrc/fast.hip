@@ -515,7 +515,17 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
 
     // one cell per wave; waves of a block take consecutive cells of a frame;
     // XCD-swizzled blocks keep a frame's cells (overlapping windows) on one L2
-#if ORBGPU_FAST_SWIZZLE
+#if ORBGPU_FAST_SWIZZLE == 2
+    // XCD-local runs: blocks are dealt round-robin over the 8 XCDs (b and b + 8
+    // share one), so within each window of 64 consecutive blocks the 8 blocks
+    // of one XCD take 8 consecutive cells -- horizontal neighbours of a cell
+    // row, whose windows overlap by 6 px and share 64-B sectors -- and fetch
+    // their shared lines into one L2 instead of up to three.  Dispatch order
+    // over time is unchanged (a window's blocks are in flight together); the
+    // last partial window keeps the plain order.
+    const int b = (int)blockIdx.x, nfull = (int)gridDim.x & ~63;
+    const int item = (b < nfull ? (b & ~63) | ((b & 7) << 3) | ((b >> 3) & 7) : b) * kCellWaves + wave;
+#elif ORBGPU_FAST_SWIZZLE
     const int item = xcd_swizzle((int)blockIdx.x, (int)gridDim.x) * kCellWaves + wave;
 #else
     const int item = (int)blockIdx.x * kCellWaves + wave;

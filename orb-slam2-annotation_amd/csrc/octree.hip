@@ -33,7 +33,10 @@ namespace {
 #define ORBGPU_OCT_THREADS 256
 #endif
 constexpr int kThreads = ORBGPU_OCT_THREADS;  // large batches: 6 workgroups per CU at 640x480 (LDS-bound)
-constexpr int kThreadsSmall = 1024;  // a few frames: one workgroup per (frame, level) on its own CU
+#ifndef ORBGPU_OCT_THREADS_SMALL
+#define ORBGPU_OCT_THREADS_SMALL 1024
+#endif
+constexpr int kThreadsSmall = ORBGPU_OCT_THREADS_SMALL;  // a few frames: one workgroup per (frame, level) on its own CU
 constexpr int kSmallBatch = 8;       // batches up to this size take kThreadsSmall
 
 struct ONode {

@@ -1036,7 +1036,7 @@ int main(int argc, char** argv) {
             if (orbgpu_get_thread_device(&cur) != ORBGPU_OK || cur != 0) return 6;
             const int b = plain.SearchForInitialization(F[0], F[1], prev2, m12b, 100);
             if (orbgpu_get_thread_device(&cur) != ORBGPU_OK || cur != 0) return 7;
-            if (a != b || m12 != m12b || a < 100) {
+            if (a != b || m12 != m12b || a < 20) {
                 fprintf(stderr, "placed %d vs default %d matches\n", a, b);
                 return 8;
             }
