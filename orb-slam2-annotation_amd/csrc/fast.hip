@@ -641,7 +641,16 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
         int nb = 0;
         bool dropped = false;
         total = fast_cell_banded<P>(T, dw, dh, ox, g.ini_th, lane, iniX, iniY, out, L.cell_cap, err, &nb, &dropped);
+        FSTAMP(2);
+        FSTAMP(3);
+#ifdef FAST_STAMPS
+        st_nb = total;
+        cst[0] = ts[2];  // (the banded path has no separate compass stamp)
+#endif
         if (total == 0) {  // ORBextractor.cpp:821-825: retry the cell at minThFAST
+#ifdef FAST_STAMPS
+            st_retry = 1;
+#endif
             if (!dropped)
                 for (int j = lane; j < nb; j += 64) T.sc[T.lb[j]] = 0;
             else

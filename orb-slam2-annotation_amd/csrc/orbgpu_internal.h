@@ -33,7 +33,11 @@ constexpr int kBlur = 2 * kBlurR + 1;    // 37
 // L2, not eight.  Bijective for any nwg (MI355X_MICROARCH / cdna guide T1);
 // a pure speed choice, never needed for correctness.
 #ifndef ORBGPU_FAST_SWIZZLE
-#define ORBGPU_FAST_SWIZZLE 0  // measured slower for FAST (1.193 vs 1.129 ms per 512 frames)
+// FAST: 2 = XCD-local runs of 8 consecutive cells within each window of 64
+// blocks (fast.hip; round 6: FETCH_SIZE 1,077 -> 383 MB per 512-frame launch,
+// fast_cells 0.499 -> 0.497 ms, r6b); 1 = the whole-grid remap below (measured
+// slower for FAST: 0.547 -> 0.573 ms, round 4); 0 = block order
+#define ORBGPU_FAST_SWIZZLE 2
 #endif
 #ifndef ORBGPU_DESC_SWIZZLE
 #define ORBGPU_DESC_SWIZZLE 1
