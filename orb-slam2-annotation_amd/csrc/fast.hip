@@ -68,14 +68,6 @@ __device__ inline void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// Wave-level stream compaction: lanes holding `pred` append `v` to list[]
-// after `n` entries (order = lane order); returns the new length.
-__device__ inline int wave_append(bool pred, uint16_t v, uint16_t* list, int n, int lane) {
-    const unsigned long long m = __ballot(pred);
-    if (pred) list[n + __popcll(m & ((1ull << lane) - 1ull))] = v;
-    return n + __popcll(m);
-}
-
 // a where this lane's bit of the mask m (scalar registers) is set, else b:
 // one v_cndmask on the mask as it is (a bool built from it would be turned
 // back into a vector value and compared again)
@@ -192,15 +184,21 @@ __device__ int compass_pass_dw(const CellTiles& T, int dw, int dh, int ox, int t
     auto split = [](uint32_t x, bool hi) {  // bytes (0, 1) or (2, 3) of x as a packed u16 pair
         return __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, x, hi ? 0x0C030C02u : 0x0C010C00u));
     };
-    auto test = [&](u16x2 v, u16x2 c0, u16x2 c4, u16x2 c8, u16x2 c12) -> uint32_t {
+    // the compass strength of both pixels (packed u16): a pixel passes iff its
+    // half exceeds t (compared per half below: no packed subtract of t)
+    auto test = [&](u16x2 v, u16x2 c0, u16x2 c4, u16x2 c8, u16x2 c12) -> u16x2 {
         const u16x2 dark = __builtin_elementwise_max(__builtin_elementwise_min(c0, c8), __builtin_elementwise_min(c4, c12));
         const u16x2 bright =
             __builtin_elementwise_min(__builtin_elementwise_max(c0, c8), __builtin_elementwise_max(c4, c12));
-        const u16x2 x = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, dark),
-                                                  __builtin_elementwise_sub_sat(bright, v));
-        const u16x2 tt = {(unsigned short)t, (unsigned short)t};
-        return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x, tt));
+        return __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, dark), __builtin_elementwise_sub_sat(bright, v));
     };
+    // c4 (pixel + 3) and c12 (pixel - 3) as packed pairs straight from the
+    // neighbouring dwords by one v_perm each (no v_alignbyte first):
+    // c4 = (V3, Vp0 | Vp1, Vp2), c12 = (Vm1, Vm2 | Vm3, V0)
+    auto pick = [](uint32_t hi, uint32_t lo, uint32_t sel) {
+        return __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(hi, lo, sel));
+    };
+    const uint32_t tq = (uint32_t)t;
     auto addc = [](int a, unsigned long long m) {  // a + (this lane's bit of m)
         int r;
         unsigned long long co;
@@ -217,14 +215,15 @@ __device__ int compass_pass_dw(const CellTiles& T, int dw, int dh, int ox, int t
         const uint32_t V = *reinterpret_cast<const uint32_t*>(p), Vm = *reinterpret_cast<const uint32_t*>(p - 4),
                        Vp = *reinterpret_cast<const uint32_t*>(p + 4), D = *reinterpret_cast<const uint32_t*>(p + 3 * P),
                        U = *reinterpret_cast<const uint32_t*>(p - 3 * P);
-        const uint32_t c4 = __builtin_amdgcn_alignbyte(Vp, V, 3), c12 = __builtin_amdgcn_alignbyte(V, Vm, 1);
-        const uint32_t ylo = test(split(V, false), split(D, false), split(c4, false), split(U, false), split(c12, false));
-        const uint32_t yhi = test(split(V, true), split(D, true), split(c4, true), split(U, true), split(c12, true));
+        const u16x2 ylo = test(split(V, false), split(D, false), pick(Vp, V, 0x0C040C03u), split(U, false),
+                               pick(V, Vm, 0x0C020C01u));
+        const u16x2 yhi = test(split(V, true), split(D, true), pick(Vp, V, 0x0C060C05u), split(U, true),
+                               pick(V, Vm, 0x0C040C03u));
         const unsigned long long rows = __builtin_amdgcn_uicmp((uint32_t)rl, (uint32_t)(dh - rr), 36 /* ult */);
-        const unsigned long long m0 = __builtin_amdgcn_uicmp(ylo & 0xFFFFu, 0u, 33 /* ne */) & cm[0] & rows;
-        const unsigned long long m1 = __builtin_amdgcn_uicmp(ylo, 0x10000u, 35 /* uge */) & cm[1] & rows;
-        const unsigned long long m2 = __builtin_amdgcn_uicmp(yhi & 0xFFFFu, 0u, 33 /* ne */) & cm[2] & rows;
-        const unsigned long long m3 = __builtin_amdgcn_uicmp(yhi, 0x10000u, 35 /* uge */) & cm[3] & rows;
+        const unsigned long long m0 = __builtin_amdgcn_uicmp((uint32_t)ylo.x, tq, 34 /* ugt */) & cm[0] & rows;
+        const unsigned long long m1 = __builtin_amdgcn_uicmp((uint32_t)ylo.y, tq, 34 /* ugt */) & cm[1] & rows;
+        const unsigned long long m2 = __builtin_amdgcn_uicmp((uint32_t)yhi.x, tq, 34 /* ugt */) & cm[2] & rows;
+        const unsigned long long m3 = __builtin_amdgcn_uicmp((uint32_t)yhi.y, tq, 34 /* ugt */) & cm[3] & rows;
         uint32_t s = 0u;
         s = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, s));
         s = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, s));
@@ -253,12 +252,80 @@ __device__ int compass_pass_dw(const CellTiles& T, int dw, int dh, int ox, int t
 typedef _Float16 fast_h2 __attribute__((ext_vector_type(2)));
 template <int P>
 __device__ __forceinline__ uint32_t ring_pairs(const uint8_t* p0, const uint8_t* p1, fast_h2 (&r)[16]) {
+    // (each pair by one v_lshl_or: ds_read_u8_d16 / _d16_hi would assemble it in
+    // the LDS unit, but with SRAM ECC enabled -- MI355X -- a D16 load zeroes the
+    // other half instead of preserving it; round 6 measured the wrong results)
     const int ring_dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
     const int ring_dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
     auto pair = [&](int o) { return (uint32_t)p0[o] | ((uint32_t)p1[o] << 16); };
 #pragma unroll
     for (int k = 0; k < 16; ++k) r[k] = __builtin_bit_cast(fast_h2, pair((ring_dy[k] + 3) * P + ring_dx[k] + 3));
     return pair(3 * P + 3);
+}
+
+// One chunk of the arc pass: list entries base + lane and base + 64 + lane
+// (one per 16-bit half) -> arc strength, corners at t appended to T.lb after
+// nb (list order: the low halves' corners, then the high halves'), their
+// scores into the score tile.  With d = v - ring, the arc strength max over
+// arcs of max(min d, -max d) is
+//   s = max(v - min_k max9_k(ring), max_k min9_k(ring) - v)
+// (max9_k / min9_k over the 9-arc starting at ring position k); corner at
+// t <=> s >= t + 1.  The ring bytes of both pixels sit in the two halves
+// of a register as f16 denormals (order-preserving bit patterns; the
+// kernel keeps f16 denormals, and minimum/maximum only select), so every
+// 3-way min/max is one v_pk_minimum3_f16 / v_pk_maximum3_f16: a 9-arc is
+// three 3-runs.  The corner appends take the lane masks as they are (one
+// mbcnt pair each, exec-masked stores; a bool re-materialised into vcc and
+// counted with masked popcounts cost 7 VALU per append).
+template <int P>
+__device__ __forceinline__ int arc_chunk(const CellTiles& T, int na, int base, int t, int lane, int nb) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    typedef short i16x2 __attribute__((ext_vector_type(2)));
+    auto max3 = [](h2 x, h2 y, h2 z) { return __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z); };
+    auto min3 = [](h2 x, h2 y, h2 z) { return __builtin_elementwise_minimum(__builtin_elementwise_minimum(x, y), z); };
+    const int j0 = base + lane, j1 = j0 + 64;
+    const int off0 = T.la[min(j0, na - 1)], off1 = T.la[min(j1, na - 1)];  // clamped: real pixels
+    // ring reads from the circle's top-left corner: every read is the base
+    // register plus a non-negative immediate
+    int a0 = off0 - (3 * P + 3), a1 = off1 - (3 * P + 3);
+    asm volatile("" : "+v"(a0), "+v"(a1));  // (keeps the bias out of the per-read adds)
+    h2 r[16];
+    const uint32_t vv = ring_pairs<P>(T.win + a0, T.win + a1, r);
+    h2 hi3[16], lo3[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        hi3[k] = max3(r[k], r[(k + 1) & 15], r[(k + 2) & 15]);
+        lo3[k] = min3(r[k], r[(k + 1) & 15], r[(k + 2) & 15]);
+    }
+    h2 hi9[16], lo9[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        hi9[k] = max3(hi3[k], hi3[(k + 3) & 15], hi3[(k + 6) & 15]);
+        lo9[k] = min3(lo3[k], lo3[(k + 3) & 15], lo3[(k + 6) & 15]);
+    }
+    h2 A = min3(hi9[0], hi9[1], hi9[2]), B = max3(lo9[0], lo9[1], lo9[2]);
+#pragma unroll
+    for (int k = 3; k < 16; k += 2) {
+        A = k + 1 < 16 ? min3(A, hi9[k], hi9[k + 1]) : __builtin_elementwise_minimum(A, hi9[k]);
+        B = k + 1 < 16 ? max3(B, lo9[k], lo9[k + 1]) : __builtin_elementwise_maximum(B, lo9[k]);
+    }
+    const i16x2 v = __builtin_bit_cast(i16x2, vv), ia = __builtin_bit_cast(i16x2, A), ib = __builtin_bit_cast(i16x2, B);
+    const i16x2 sc = __builtin_elementwise_max(v - ia, ib - v);  // arc strength (cornerScore + 1)
+    const bool c0 = (j0 < na) & (sc.x > t), c1 = (j1 < na) & (sc.y > t);
+    const unsigned long long m0 = __ballot(c0), m1 = __ballot(c1);
+    auto below = [](unsigned long long m) {  // set bits of m in lanes below this one
+        return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    };
+    const int p0 = nb + below(m0), nb1 = nb + __popcll(m0), p1 = nb1 + below(m1);
+    if (c0) {
+        T.sc[off0] = (uint8_t)sc.x;
+        T.lb[p0] = (uint16_t)off0;
+    }
+    if (c1) {
+        T.sc[off1] = (uint8_t)sc.y;
+        T.lb[p1] = (uint16_t)off1;
+    }
+    return nb1 + __popcll(m1);
 }
 
 // FAST at threshold t on the cell's detection region: returns the number
@@ -279,62 +346,10 @@ __device__ int fast_corners(const CellTiles& T, int dw, int dh, int ox, int t, i
         stamp[1] = (unsigned long long)na;
     }
 #endif
-    // Survivors -> corners, two per lane (list entries base + lane and
-    // base + 64 + lane, one per 16-bit half).  With d = v - ring, the arc
-    // strength max over arcs of max(min d, -max d) is
-    //   s = max(v - min_k max9_k(ring), max_k min9_k(ring) - v)
-    // (max9_k / min9_k over the 9-arc starting at ring position k); corner at
-    // t <=> s >= t + 1.  The ring bytes of both pixels sit in the two halves
-    // of a register as f16 denormals (order-preserving bit patterns; the
-    // kernel keeps f16 denormals, and minimum/maximum only select), so every
-    // 3-way min/max is one v_pk_minimum3_f16 / v_pk_maximum3_f16: a 9-arc is
-    // three 3-runs.  Corners are compacted in list order (the low halves'
-    // entries precede the high halves') behind the survivors being read, and
-    // their scores go to the score tile.
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    typedef short i16x2 __attribute__((ext_vector_type(2)));
-    auto max3 = [](h2 x, h2 y, h2 z) { return __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z); };
-    auto min3 = [](h2 x, h2 y, h2 z) { return __builtin_elementwise_minimum(__builtin_elementwise_minimum(x, y), z); };
+    // survivors -> corners, two per lane (arc_chunk), compacted in place
+    // behind the survivors being read
     int nb = 0;
-    for (int base = 0; base < na; base += 128) {
-        const int j0 = base + lane, j1 = j0 + 64;
-        const int off0 = T.la[min(j0, na - 1)], off1 = T.la[min(j1, na - 1)];  // clamped: real pixels
-        // ring reads from the circle's top-left corner: every read is the base
-        // register plus a non-negative immediate (the empty asm keeps the
-        // compiler from folding the bias back into per-read adds)
-        int a0 = off0 - (3 * P + 3), a1 = off1 - (3 * P + 3);
-        asm volatile("" : "+v"(a0), "+v"(a1));
-        const uint8_t* p0 = T.win + a0;
-        const uint8_t* p1 = T.win + a1;
-        h2 r[16];
-        const uint32_t vv = ring_pairs<P>(p0, p1, r);
-        h2 hi3[16], lo3[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            hi3[k] = max3(r[k], r[(k + 1) & 15], r[(k + 2) & 15]);
-            lo3[k] = min3(r[k], r[(k + 1) & 15], r[(k + 2) & 15]);
-        }
-        h2 hi9[16], lo9[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            hi9[k] = max3(hi3[k], hi3[(k + 3) & 15], hi3[(k + 6) & 15]);
-            lo9[k] = min3(lo3[k], lo3[(k + 3) & 15], lo3[(k + 6) & 15]);
-        }
-        h2 A = min3(hi9[0], hi9[1], hi9[2]), B = max3(lo9[0], lo9[1], lo9[2]);
-#pragma unroll
-        for (int k = 3; k < 16; k += 2) {
-            A = k + 1 < 16 ? min3(A, hi9[k], hi9[k + 1]) : __builtin_elementwise_minimum(A, hi9[k]);
-            B = k + 1 < 16 ? max3(B, lo9[k], lo9[k + 1]) : __builtin_elementwise_maximum(B, lo9[k]);
-        }
-        const i16x2 v = __builtin_bit_cast(i16x2, vv), ia = __builtin_bit_cast(i16x2, A),
-                    ib = __builtin_bit_cast(i16x2, B);
-        const i16x2 sc = __builtin_elementwise_max(v - ia, ib - v);  // arc strength (cornerScore + 1)
-        const bool c0 = (j0 < na) & (sc.x > t), c1 = (j1 < na) & (sc.y > t);
-        if (c0) T.sc[off0] = (uint8_t)sc.x;
-        if (c1) T.sc[off1] = (uint8_t)sc.y;
-        nb = wave_append(c0, (uint16_t)off0, T.lb, nb, lane);
-        nb = wave_append(c1, (uint16_t)off1, T.lb, nb, lane);
-    }
+    for (int base = 0; base < na; base += 128) nb = arc_chunk<P>(T, na, base, t, lane, nb);
     wave_sync();
     return nb;
 }
@@ -396,10 +411,6 @@ __device__ int nms_emit(const CellTiles& T, int nb, int ox, int t, int lane, int
 template <int P>
 __device__ int fast_cell_banded(const CellTiles& T, int dw, int dh, int ox, int t, int lane, int iniX, int iniY,
                                 uint32_t* out, int cap, int* err, int* pending, bool* dropped) {
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    typedef short i16x2 __attribute__((ext_vector_type(2)));
-    auto max3 = [](h2 x, h2 y, h2 z) { return __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z); };
-    auto min3 = [](h2 x, h2 y, h2 z) { return __builtin_elementwise_minimum(__builtin_elementwise_minimum(x, y), z); };
     int nb = 0, total = 0, row = 0;
     bool drop = false;
     while (true) {
@@ -409,42 +420,7 @@ __device__ int fast_cell_banded(const CellTiles& T, int dw, int dh, int ox, int 
                                               : compass_pass<P, 32, true>(T, dw, dh, ox, t, lane, row, nb, &row_end);
         wave_sync();
         int nc = nb;
-        for (int base = nb; base < na; base += 128) {
-            const int j0 = base + lane, j1 = j0 + 64;
-            const int off0 = T.la[min(j0, na - 1)], off1 = T.la[min(j1, na - 1)];
-            int a0 = off0 - (3 * P + 3), a1 = off1 - (3 * P + 3);
-            asm volatile("" : "+v"(a0), "+v"(a1));
-            const uint8_t* p0 = T.win + a0;
-            const uint8_t* p1 = T.win + a1;
-            h2 r[16];
-            const uint32_t vv = ring_pairs<P>(p0, p1, r);
-            h2 hi3[16], lo3[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                hi3[k] = max3(r[k], r[(k + 1) & 15], r[(k + 2) & 15]);
-                lo3[k] = min3(r[k], r[(k + 1) & 15], r[(k + 2) & 15]);
-            }
-            h2 hi9[16], lo9[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                hi9[k] = max3(hi3[k], hi3[(k + 3) & 15], hi3[(k + 6) & 15]);
-                lo9[k] = min3(lo3[k], lo3[(k + 3) & 15], lo3[(k + 6) & 15]);
-            }
-            h2 A = min3(hi9[0], hi9[1], hi9[2]), B = max3(lo9[0], lo9[1], lo9[2]);
-#pragma unroll
-            for (int k = 3; k < 16; k += 2) {
-                A = k + 1 < 16 ? min3(A, hi9[k], hi9[k + 1]) : __builtin_elementwise_minimum(A, hi9[k]);
-                B = k + 1 < 16 ? max3(B, lo9[k], lo9[k + 1]) : __builtin_elementwise_maximum(B, lo9[k]);
-            }
-            const i16x2 v = __builtin_bit_cast(i16x2, vv), ia = __builtin_bit_cast(i16x2, A),
-                        ib = __builtin_bit_cast(i16x2, B);
-            const i16x2 sc = __builtin_elementwise_max(v - ia, ib - v);
-            const bool c0 = (j0 < na) & (sc.x > t), c1 = (j1 < na) & (sc.y > t);
-            if (c0) T.sc[off0] = (uint8_t)sc.x;
-            if (c1) T.sc[off1] = (uint8_t)sc.y;
-            nc = wave_append(c0, (uint16_t)off0, T.lb, nc, lane);
-            nc = wave_append(c1, (uint16_t)off1, T.lb, nc, lane);
-        }
+        for (int base = nb; base < na; base += 128) nc = arc_chunk<P>(T, na, base, t, lane, nc);
         wave_sync();
         nb = nc;
         row = row_end;

@@ -38,6 +38,14 @@ OP_KERNEL(k_pkadd16, "v_pk_add_u16 %0, %0, %1")
 OP_KERNEL(k_cvtsdwa, "v_cvt_f32_u32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1")
 OP_KERNEL(k_cvtpku8, "v_cvt_pk_u8_f32 %0, %1, 1, %0")
 OP_KERNEL(k_min3, "v_min3_i32 %0, %0, %1, %1")
+// round 6: the ops FAST's compass / arc pass and describe's blur / moments issue most
+OP_KERNEL(k_pkmaxu16, "v_pk_max_u16 %0, %0, %1")
+OP_KERNEL(k_pksubu16, "v_pk_sub_u16 %0, %0, %1 clamp")
+OP_KERNEL(k_pkmax3f16, "v_pk_maximum3_f16 %0, %0, %1, %1")
+OP_KERNEL(k_dot4, "v_dot4_u32_u8 %0, %0, %1, %0")
+OP_KERNEL(k_alignbyte, "v_alignbyte_b32 %0, %0, %1, 3")
+OP_KERNEL(k_lshlor, "v_lshl_or_b32 %0, %0, 16, %1")
+OP_KERNEL(k_mbcnt, "v_mbcnt_lo_u32_b32 %0, %1, %0")
 
 // scalar ALU: 8 independent 64-bit chains per wave
 __global__ __launch_bounds__(256) void k_salu(unsigned* out, unsigned seed, int iters) {
@@ -91,7 +99,9 @@ int main() {
         {"v_mul_hi_u32_u24", k_mulhi24}, {"v_mul_u32_u24", k_mul24}, {"v_mul_lo_u32", k_mullo},
         {"v_lshrrev_b32_sdwa", k_sdwa}, {"v_add3_u32", k_add3}, {"v_fma_f32", k_fma}, {"v_mad_u32_u24", k_mad24},
         {"v_pk_mad_u16", k_pkmad16}, {"v_pk_add_u16", k_pkadd16}, {"v_cvt_f32_u32_sdwa", k_cvtsdwa},
-        {"v_cvt_pk_u8_f32", k_cvtpku8}, {"v_min3_i32", k_min3}, {"v_pk_fma_f32", k_pkfma}, {"v_pk_add_f32", k_pkaddf}, {"s_and_b64 (SALU)", k_salu}};
+        {"v_cvt_pk_u8_f32", k_cvtpku8}, {"v_min3_i32", k_min3}, {"v_pk_max_u16", k_pkmaxu16}, {"v_pk_sub_u16 clamp", k_pksubu16},
+        {"v_pk_maximum3_f16", k_pkmax3f16}, {"v_dot4_u32_u8", k_dot4}, {"v_alignbyte_b32", k_alignbyte},
+        {"v_lshl_or_b32", k_lshlor}, {"v_mbcnt_lo_u32_b32", k_mbcnt}, {"v_pk_fma_f32", k_pkfma}, {"v_pk_add_f32", k_pkaddf}, {"s_and_b64 (SALU)", k_salu}};
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
