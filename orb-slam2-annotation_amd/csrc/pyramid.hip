@@ -559,11 +559,15 @@ __global__ __launch_bounds__(kBandThreads) void pyramid_band_kernel(const Geom g
         uint8_t* drow = s_rows + v.bd_lds_off;
         const bool keep = l + 1 < L;
         const int quads = (v.w + 3) >> 2, n = (r.y - r.x) * quads;
+        // i / quads by a multiply-high with ceil(2^32 / quads) (exact while
+        // i * (quads - 1) < 2^32; quads >= 2: plan_pyramid_bands); the
+        // per-element integer division was ~25 VALU on each level's chain
+        const uint32_t qmagic = (uint32_t)((0x100000000ull + (uint64_t)quads - 1u) / (uint64_t)quads);
         const int2* xt = xtab + v.xtab_offset;
         const int2* yt = ytab + v.ytab_offset;
         uint8_t* out = pyr + v.offset + (size_t)f * v.frame_bytes;
         for (int i = tid; i < n; i += kBandThreads) {
-            const int yy = i / quads, q = i - yy * quads, y = r.x + yy;
+            const int yy = (int)__umulhi((uint32_t)i, qmagic), q = i - yy * quads, y = r.x + yy;
             const int2 ty = yt[y];
             const uint8_t* r0 = srow + ((ty.x & 0xFFFF) - src_lo) * p.bd_pitch;
             const uint8_t* r1 = srow + ((int)((uint32_t)ty.x >> 16) - src_lo) * p.bd_pitch;
@@ -608,7 +612,7 @@ void plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, std::vector<int4
     // least one own row per band at every level
     for (int nb : {32, 24, 16, 8}) {
         bool ok = true;
-        for (int l = 1; l < L; ++l) ok = ok && g.lv[l].h >= nb;
+        for (int l = 1; l < L; ++l) ok = ok && g.lv[l].h >= nb && g.lv[l].w > 4;  // (the kernel's row division needs >= 2 quads)
         if (!ok) continue;
         std::vector<int4> b((size_t)nb * L);
         std::vector<int> cap(L, 0);
