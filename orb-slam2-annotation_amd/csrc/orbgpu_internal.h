@@ -110,6 +110,7 @@ struct LevelGeom {
     // this level's rows of a band live in LDS at bd_lds_off with pitch bd_pitch
     // (levels 0..L-2)
     int bd_lds_off, bd_pitch;
+    uint32_t bd_qmagic;       // ceil(2^32 / quads): row index of a band element by a multiply-high
     // blurred level (all levels, incl. 0): same row pitch as the pyramid
     size_t blur_offset, blur_frame_bytes;
     int blur_tiles_x, blur_tile_base;   // blur work items: 4-column x 64-row strips

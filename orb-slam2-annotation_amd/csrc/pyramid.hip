@@ -559,10 +559,10 @@ __global__ __launch_bounds__(kBandThreads) void pyramid_band_kernel(const Geom g
         uint8_t* drow = s_rows + v.bd_lds_off;
         const bool keep = l + 1 < L;
         const int quads = (v.w + 3) >> 2, n = (r.y - r.x) * quads;
-        // i / quads by a multiply-high with ceil(2^32 / quads) (exact while
-        // i * (quads - 1) < 2^32; quads >= 2: plan_pyramid_bands); the
+        // i / quads by a multiply-high with the host's ceil(2^32 / quads) (exact
+        // while i * (quads - 1) < 2^32; quads >= 2: plan_pyramid_bands); the
         // per-element integer division was ~25 VALU on each level's chain
-        const uint32_t qmagic = (uint32_t)((0x100000000ull + (uint64_t)quads - 1u) / (uint64_t)quads);
+        const uint32_t qmagic = v.bd_qmagic;
         const int2* xt = xtab + v.xtab_offset;
         const int2* yt = ytab + v.ytab_offset;
         uint8_t* out = pyr + v.offset + (size_t)f * v.frame_bytes;
@@ -634,6 +634,10 @@ void plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, std::vector<int4
                 }
             }
             for (int l = 0; l + 1 < L; ++l) cap[l] = std::max(cap[l], B[l].y - B[l].x);
+        }
+        for (int l = 1; l < L; ++l) {
+            const uint64_t quads = (uint64_t)((g.lv[l].w + 3) >> 2);
+            g.lv[l].bd_qmagic = (uint32_t)(((1ull << 32) + quads - 1) / quads);
         }
         int off = 0;
         for (int l = 0; l + 1 < L; ++l) {
