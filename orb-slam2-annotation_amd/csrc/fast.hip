@@ -533,9 +533,13 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     const uint8_t* base = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
     const uint32_t pitch = l == 0 ? (uint32_t)row0 : (uint32_t)L.pitch;  // < 2^24 (launcher check)
 
-    // stage rows: dwords covering [xa, maxX), xa = iniX & ~3 (row pitch and
-    // frame base are 16-byte aligned; maxX <= w - 16, so no over-read)
-    const int xa = iniX & ~3, ox = iniX - xa;
+    // stage rows: bytes [xa - sh, maxX) at tile column 0.., xa = iniX & ~3, where the
+    // shift sh puts the detection region's first column (iniX + 3) on a 4-aligned
+    // tile column (4 or 8): the dword compass then needs ceil(dw / 4) groups per
+    // row -- 8 for the 30-32 px cells, so 8 rows per pass on all 64 lanes instead
+    // of 9 groups and 7 rows for about half of them (round 6).  The loads start
+    // at any byte (one unaligned vector load each); maxX <= w - 16, so no over-read.
+    const int xa = iniX & ~3, sh = (1 - (iniX - xa)) & 3, ox = iniX - xa + sh;  // ox: tile column of iniX
     // Every window row is staged as P bytes: NC chunks of CB bytes (16 when P is
     // a multiple of 16, else 4), so LDS chunk (r, q) sits at CB * (r * NC + q)
     // and a fixed lane -> (row rl, chunk q) map covers RPI = 64 / NC rows per
@@ -558,13 +562,13 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     const uint8_t* wbase = uniform_ptr(img0 + (size_t)kBorder * row0 + kBorder);
     (void)base;
 #else
-    const uint8_t* wbase = uniform_ptr(base + (size_t)iniY * pitch + xa);
+    const uint8_t* wbase = uniform_ptr(base + (size_t)iniY * pitch + (xa - sh));
 #endif
     {
         constexpr int CB = FastStage<P>::CB, NC = FastStage<P>::NC, RPI = FastStage<P>::RPI,
                       kGroup = FastStage<P>::kGroup;
         const int rl = lane / NC, q = lane - rl * NC;  // compile-time divisor
-        const int ncneed = (maxX - xa + CB - 1) / CB;
+        const int ncneed = (maxX - xa + sh + CB - 1) / CB;
         const uint32_t col = (uint32_t)(CB * min(q, ncneed - 1));
         const int passes = (wh + RPI - 1) / RPI;  // wave-uniform
         uint8_t* dst = s_win + CB * lane;
@@ -582,9 +586,9 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
                 const uint8_t* src = wbase + (__umul24(r, pitch) + col);
 #endif
                 if constexpr (CB == 16)
-                    v[k] = load16_a4(src);
+                    v[k] = load16_a1(src);
                 else
-                    v[k] = *reinterpret_cast<const uint32_t*>(src);
+                    v[k] = load4_a1(src);
             }
             if (p0 + NG <= passes) {  // a whole group (wave-uniform): unconditional stores
 #pragma unroll

@@ -405,8 +405,9 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     g.win_rows = 0;
     g.det_max = 0;
     for (int l = 0; l < L; ++l) {
-        if (g.lv[l].wcell > 63) return fail(ORBGPU_ERR_UNSUPPORTED, "FAST cell wider than 63 px");
-        g.win_pitch = std::max(g.win_pitch, (int)round_up((size_t)g.lv[l].wcell + 9, 4));
+        if (g.lv[l].wcell > 61) return fail(ORBGPU_ERR_UNSUPPORTED, "FAST cell wider than 61 px");
+        // window = cell + 6 px, starting at tile column 1 or 5 (fast.hip's column shift)
+        g.win_pitch = std::max(g.win_pitch, (int)round_up((size_t)g.lv[l].wcell + 11, 4));
         g.win_rows = std::max(g.win_rows, g.lv[l].hcell + 6);
         g.det_max = std::max(g.det_max, (int)round_up((size_t)g.lv[l].wcell * g.lv[l].hcell, 8));
     }

@@ -56,6 +56,19 @@ __device__ inline uint4 load16_a4(const uint8_t* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// 16 / 4 bytes from any byte address of global memory (gfx950 serves unaligned
+// vector loads in one instruction; FAST's column-shifted window staging).  The
+// pointer is cast to the global address space: a pointer rebuilt from scalars
+// (uniform_ptr) is generic, and its loads were flat_load (counted in lgkmcnt too,
+// 64-bit vector addresses) instead of global_load with a scalar base.
+typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t u32_a1 __attribute__((aligned(1)));
+__device__ inline uint4 load16_a1(const uint8_t* p) {
+    const u32x4_a1 v = *(const __attribute__((address_space(1))) u32x4_a1*)(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ inline uint32_t load4_a1(const uint8_t* p) { return *(const __attribute__((address_space(1))) u32_a1*)(p); }
+
 // Candidate key packing (FAST output, octree input/output):
 //   bits 0..10  x relative to minBorderX (level x - 16)
 //   bits 11..21 y relative to minBorderY
