@@ -87,6 +87,18 @@ constexpr DiscLut make_disc_lut() {
     return L;
 }
 __constant__ DiscLut c_disc = make_disc_lut();
+// words 256.. of each od (the fifth load) as a table of their own: its own
+// scalar base, as global immediate offsets stop at 4095
+struct DiscTail { DiscWord w[4][64]; };
+constexpr DiscTail make_disc_tail() {
+    DiscTail T{};
+    const DiscLut L = make_disc_lut();
+    for (int od = 0; od < 4; ++od)
+        for (int i = 0; i < 64; ++i) T.w[od][i] = L.w[od][256 + i];
+    return T;
+}
+__constant__ DiscTail c_disc_tail = make_disc_tail();
+static_assert(kDiscLoads == 5, "the disc loads are four from c_disc and one from c_disc_tail");
 
 // OpenCV 2.4 fastAtan2 (mathfuncs.cpp); explicit _rn ops: never contracted.
 __device__ inline float fast_atan2(float y, float x) {
@@ -158,13 +170,14 @@ __device__ inline void glibc_sincosf(float y, float* sinp, float* cosp) {
 }
 
 // wave total of an unsigned int, wave-uniform: 16-lane row sums on DPP
-// (quad xor 1, xor 2, half mirror, mirror: full-rate VALU moves), then the
-// four row totals read into scalars (integer: order-free, exact)
+// (quad xor 1, xor 2, half mirror, mirror; update_dpp with bound_ctrl so the
+// compiler folds each move into its add: one v_add_u32_dpp per step), then
+// the four row totals read into scalars (integer: order-free, exact)
 __device__ inline uint32_t wave_total(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppXor1, 0xF, 0xF, false);
-    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppXor2, 0xF, 0xF, false);
-    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppHalfMirror, 0xF, 0xF, false);
-    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppMirror, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppXor1, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppXor2, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppHalfMirror, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppMirror, 0xF, 0xF, true);
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
            (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
@@ -309,7 +322,11 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             const uint32_t idx = (uint32_t)(lane + 64 * k), r = __umul24(idx, 21846u) >> 16, q = idx - 3u * r;
-            dst[k] = idx < (uint32_t)kChunks ? rawbuf + (__umul24(r, (uint32_t)kRPitch) + 16u * q) : dump;
+            // chunk (r, q) at r * 48 + 16 q = 16 idx when the row pitch is 48 (three
+            // chunks a row): no per-chunk multiply; chunks 0..127 (k = 0, 1) always
+            // exist, so only k = 2 selects the dump (VALU-bound kernel: round 6)
+            const uint32_t doff = kRPitch == 48 ? 16u * idx : __umul24(r, (uint32_t)kRPitch) + 16u * q;
+            dst[k] = (k < 2 && 64 * 2 <= kChunks) || idx < (uint32_t)kChunks ? rawbuf + doff : dump;
             c[k] = load16_a4(top + (__umul24(min(r, (uint32_t)kPatch - 1u), (uint32_t)rp) + 16u * q));
         }
         // unconditional stores (lanes past the patch write into kDump): no
@@ -358,9 +375,18 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
     const int xd = (cx - 15) & ~3, od = cx - 15 - xd;
     const uint8_t* disc = rawbuf + (kPatchR - 15) * kRPitch + (xd - x0);
     uint32_t sp = 0u, cp = 0u, vp = 0u;
+    // uniform table bases + 32-bit lane offset: saddr loads, no per-load
+    // 64-bit address arithmetic
+    const __attribute__((address_space(1))) uint8_t* dtab =
+        (const __attribute__((address_space(1))) uint8_t*)&c_disc.w[od][0];
+    const __attribute__((address_space(1))) uint8_t* dtab4 =
+        (const __attribute__((address_space(1))) uint8_t*)&c_disc_tail.w[od][0];
 #pragma unroll
     for (int k = 0; k < kDiscLoads; ++k) {
-        const DiscWord e = c_disc.w[od][lane + 64 * k];
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 t = *(const __attribute__((address_space(1))) u32x4*)((k < 4 ? dtab : dtab4) + 16u * (uint32_t)lane +
+                                                                          1024u * (k % 4));
+        const DiscWord e{t.x, t.y, t.z, t.w};
 #if DESC_LDS_PROBE & 4
         const uint32_t w = *reinterpret_cast<const uint32_t*>(rawbuf + 4 * lane + 256 * k + (e.off & 0));
 #else

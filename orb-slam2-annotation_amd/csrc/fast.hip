@@ -219,7 +219,10 @@ __device__ int compass_pass_dw(const CellTiles& T, int dw, int dh, int ox, int t
                                pick(V, Vm, 0x0C020C01u));
         const u16x2 yhi = test(split(V, true), split(D, true), pick(Vp, V, 0x0C060C05u), split(U, true),
                                pick(V, Vm, 0x0C040C03u));
-        const unsigned long long rows = __builtin_amdgcn_uicmp((uint32_t)rl, (uint32_t)(dh - rr), 36 /* ult */);
+        // rows past the region: only the last pass has any (cm[] already drops
+        // the lanes past rpi rows), so the per-lane row compare runs there alone
+        unsigned long long rows = ~0ull;
+        if (dh - rr < rpi) rows = __builtin_amdgcn_uicmp((uint32_t)rl, (uint32_t)(dh - rr), 36 /* ult */);
         const unsigned long long m0 = __builtin_amdgcn_uicmp((uint32_t)ylo.x, tq, 34 /* ugt */) & cm[0] & rows;
         const unsigned long long m1 = __builtin_amdgcn_uicmp((uint32_t)ylo.y, tq, 34 /* ugt */) & cm[1] & rows;
         const unsigned long long m2 = __builtin_amdgcn_uicmp((uint32_t)yhi.x, tq, 34 /* ugt */) & cm[2] & rows;
@@ -287,10 +290,10 @@ __device__ __forceinline__ int arc_chunk(const CellTiles& T, int na, int base, i
     const int off0 = T.la[min(j0, na - 1)], off1 = T.la[min(j1, na - 1)];  // clamped: real pixels
     // ring reads from the circle's top-left corner: every read is the base
     // register plus a non-negative immediate
-    int a0 = off0 - (3 * P + 3), a1 = off1 - (3 * P + 3);
-    asm volatile("" : "+v"(a0), "+v"(a1));  // (keeps the bias out of the per-read adds)
+    // (one scalar base: the window's LDS offset less the circle's 3P+3 bias)
+    const uint8_t* winb = T.win - (3 * P + 3);
     h2 r[16];
-    const uint32_t vv = ring_pairs<P>(T.win + a0, T.win + a1, r);
+    const uint32_t vv = ring_pairs<P>(winb + off0, winb + off1, r);
     h2 hi3[16], lo3[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {

@@ -26,6 +26,7 @@
 // pass.
 // The vertical pass is four SDWA/op_sel instructions per pixel.
 #include <algorithm>
+#include <cstdlib>
 
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
@@ -609,8 +610,14 @@ void plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, std::vector<int4
         return int2{yt[lo].x & 0xFFFF, (int)((uint32_t)yt[hi - 1].x >> 16) + 1};
     };
     // the most bands (smallest halo share) whose rows fit the LDS budget; at
-    // least one own row per band at every level
-    for (int nb : {32, 24, 16, 8}) {
+    // least one own row per band at every level.  ORBGPU_PYR_BANDS_MAX caps the
+    // count (A/B: more, smaller bands shorten each workgroup's level chain)
+    static const int nb_max = [] {
+        const char* s = std::getenv("ORBGPU_PYR_BANDS_MAX");
+        return s ? std::atoi(s) : 32;
+    }();
+    for (int nb : {128, 96, 64, 48, 32, 24, 16, 8}) {
+        if (nb > nb_max) continue;
         bool ok = true;
         for (int l = 1; l < L; ++l) ok = ok && g.lv[l].h >= nb && g.lv[l].w > 4;  // (the kernel's row division needs >= 2 quads)
         if (!ok) continue;
