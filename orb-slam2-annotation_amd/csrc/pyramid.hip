@@ -610,11 +610,13 @@ void plan_pyramid_bands(Geom& g, const std::vector<int2>& ytab, std::vector<int4
         return int2{yt[lo].x & 0xFFFF, (int)((uint32_t)yt[hi - 1].x >> 16) + 1};
     };
     // the most bands (smallest halo share) whose rows fit the LDS budget; at
-    // least one own row per band at every level.  ORBGPU_PYR_BANDS_MAX caps the
-    // count (A/B: more, smaller bands shorten each workgroup's level chain)
+    // least one own row per band at every level.  At most 64 (ORBGPU_PYR_BANDS_MAX
+    // overrides): a workgroup's level chain is latency bound, so more, smaller
+    // bands finish sooner -- one 640x480 frame: 19.2 us at 32 bands, 16.3 us at
+    // 64; 96 measured slower again (profiles/r06_notes_ab.txt r6k, r6m)
     static const int nb_max = [] {
         const char* s = std::getenv("ORBGPU_PYR_BANDS_MAX");
-        return s ? std::atoi(s) : 32;
+        return s ? std::atoi(s) : 64;
     }();
     for (int nb : {128, 96, 64, 48, 32, 24, 16, 8}) {
         if (nb > nb_max) continue;

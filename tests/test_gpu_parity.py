@@ -152,6 +152,27 @@ def test_pyramid_paths_agree(w, h, nf):
                 assert len(d[0]) == 0, f"B={B} pitch={pitch} frame {f} level {l}: {len(d[0])} pixels differ"
 
 
+@pytest.mark.parametrize("w,h,nf", [(640, 480, 1000), (1241, 376, 2000), (752, 480, 1200), (640, 224, 500)])
+def test_single_frame_host_path_levels_and_keypoints(w, h, nf):
+    """The single-frame host path (orbgpu_extract: pinned staging, copy kernel,
+    band pyramid with 64 bands -- 48 at 640x224, whose level 7 has 63 rows).
+    Every level, level 0 included, and the keypoints and descriptors equal the
+    oracle's, over consecutive calls of one extractor (a call must not see the
+    previous frame's rows)."""
+    og = _gpu()
+    frames = synth.mono_stream(3, w, h, seed=29)
+    ref = orbref.Extractor(nfeatures=nf)
+    ex = og.Extractor(nfeatures=nf, width=w, height=h, max_batch=1)
+    for img in frames:
+        kg, dg = ex.extract(img)
+        kr, dr = ref.extract(img)
+        for l in range(8):
+            a = ex.level(l)
+            d = np.nonzero(a != ref.level(l))
+            assert len(d[0]) == 0, f"{w}x{h} level {l}: {len(d[0])} pixels differ"
+        _assert_same_kps(kg, dg, kr, dr)
+
+
 def test_batch_device_matches_single(mono_frames):
     og = _gpu()
     B = len(mono_frames)

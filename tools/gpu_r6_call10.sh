@@ -1,0 +1,11 @@
+# Round-6 call 10: the whole -m gpu suite on the default build (single-frame upload
+# fused into the band pyramid, 64 bands), then the single-frame A/B.
+set -e
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -v --timeout 200 --timeout-method thread -m gpu tests > gpurun_out/r6l_tests.log 2>&1 || { rc=$?; echo "tests rc=$rc"; tail -30 gpurun_out/r6l_tests.log; exit $rc; }
+tail -2 gpurun_out/r6l_tests.log
+ROUNDS=3 bash tools/gpu_r6_single3.sh r6l new:liborbgpu head:liborbgpu_base new_spin:liborbgpu:ORBGPU_SINGLE_WAIT=1 \
+  new_nofuse:liborbgpu:ORBGPU_SINGLE_FUSED_UPLOAD=0 new_b96:liborbgpu:ORBGPU_PYR_BANDS_MAX=96 new_b128:liborbgpu:ORBGPU_PYR_BANDS_MAX=128
+echo CALL10DONE
