@@ -13,8 +13,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <climits>
 #include <array>
+#include <atomic>
+#include <chrono>
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -175,6 +177,7 @@ struct orbgpu_extractor {
     std::mutex stereo_mu;
     // host-image path
     uint8_t* d_img = nullptr;
+    uint8_t* fg_img = nullptr;  // host-mapped fine-grained HBM staging of the single-frame upload (knob)
     size_t img_pitch = 0;
     // one device block [count, err, pad, pad | keypoints(cap) | descriptors(cap)]
     // mirrored by one pinned host block, so a frame's outputs come back in a
@@ -182,6 +185,8 @@ struct orbgpu_extractor {
     uint8_t* d_single = nullptr;
     uint8_t* h_single = nullptr;  // pinned
     uint8_t* h_img = nullptr;     // pinned staging of the host image (img_pitch rows)
+    unsigned long long* h_done = nullptr;  // pinned coherent: the single-frame completion flag (done_flag_kernel)
+    unsigned long long done_seq = 0;       // the last issued call's flag value (0: none pending)
     uint8_t* h_levels = nullptr;  // pinned staging of one frame's pyramid (copy_levels), on first use
     size_t single_bytes = 0, single_desc_off = 0;
     orbgpu_keypoint* d_kps1 = nullptr;
@@ -206,12 +211,13 @@ struct orbgpu_extractor {
     ~orbgpu_extractor() {
         DeviceScope ds(device);
         void* ptrs[] = {d_pyr, d_blur, d_ptab, d_pyr_ent, d_pyr_tab, d_xtab, d_ytab, d_band, d_cand, d_cell_counts, d_gkeys, d_gknode, d_oct_out,
-                        d_oct_count, d_err, d_trace, d_img, d_single, d_tab};
+                        d_oct_count, d_err, d_trace, d_img, fg_img, d_single, d_tab};
         for (void* p : ptrs)
             if (p) (void)hipFree(p);
         for (auto& sc : stereo_sad) (void)hipFree(sc.d);
         if (h_single) (void)hipHostFree(h_single);
         if (h_img) (void)hipHostFree(h_img);
+        if (h_done) (void)hipHostFree(h_done);
         if (h_levels) (void)hipHostFree(h_levels);
         if (stream) (void)hipStreamDestroy(stream);
         if (aux_stream) (void)hipStreamDestroy(aux_stream);
@@ -487,6 +493,31 @@ bool single_zero_copy() {
     return v;
 }
 
+// the single-frame call waits on a completion flag written by a one-wave kernel
+// after the extraction (ORBGPU_SINGLE_DONE_FLAG=0: hipStreamSynchronize)
+bool single_done_flag() {
+    static const bool v = [] {
+        const char* s = std::getenv("ORBGPU_SINGLE_DONE_FLAG");
+        return !(s && std::atoi(s) == 0);
+    }();
+    return v;
+}
+
+// The single-frame upload: the host writes the frame straight into host-mapped
+// fine-grained HBM (write-combined over PCIe, ~7.5 us for 640x480) and the
+// extraction reads it there -- no copy kernel (a memcpy into pinned memory,
+// 2 us, then a copy kernel reading it over PCIe, 9.5 us).  Drop-in
+// ORBextractor::operator() 87-91 -> 78-81 us with the completion flag
+// (profiles/r06_notes_ab.txt r6p).  ORBGPU_SINGLE_VRAM_STAGING=0, or an
+// allocation the device refuses: the pinned staging and the copy kernel.
+bool single_vram_staging() {
+    static const bool v = [] {
+        const char* s = std::getenv("ORBGPU_SINGLE_VRAM_STAGING");
+        return !(s && std::atoi(s) == 0);
+    }();
+    return v;
+}
+
 // ORBGPU_PYR_BANDS=0 selects the level-by-level launches (A/B and parity checks)
 bool pyr_bands_off() {
     static const bool v = [] {
@@ -675,11 +706,19 @@ int orbgpu_extractor_create(int nfeatures, float scale_factor, int nlevels, int 
     e->d_count1 = reinterpret_cast<int*>(e->d_single);
     e->d_kps1 = reinterpret_cast<orbgpu_keypoint*>(e->d_single + 16);
     e->d_desc1 = e->d_single + e->single_desc_off;
-    if (hipHostMalloc((void**)&e->h_single, e->single_bytes, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&e->h_img, e->img_pitch * height, hipHostMallocDefault) != hipSuccess) {
+    // (the output block coherent with the flag: describe's stores go straight
+    // to host memory, so the flag written after them orders them for the host)
+    if (hipHostMalloc((void**)&e->h_single, e->single_bytes,
+                      single_done_flag() ? hipHostMallocCoherent : hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&e->h_img, e->img_pitch * height, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&e->h_done, 64, hipHostMallocCoherent) != hipSuccess) {
         delete e;
         return fail(ORBGPU_ERR_HIP, "pinned staging allocation failed");
     }
+    __atomic_store_n(e->h_done, 0ull, __ATOMIC_RELEASE);
+    if (single_vram_staging() &&
+        hipExtMallocWithFlags((void**)&e->fg_img, e->img_pitch * height, hipDeviceMallocFinegrained) != hipSuccess)
+        e->fg_img = nullptr;  // (the pinned staging and the copy kernel then)
     if (hipMemcpy(e->d_ptab, ptab.data(), ptab.size() * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess ||
         (!xtab.empty() && hipMemcpy(e->d_xtab, xtab.data(), xtab.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess) ||
         (!ytab.empty() && hipMemcpy(e->d_ytab, ytab.data(), ytab.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess) ||
@@ -810,15 +849,23 @@ static int extract_issue(orbgpu_extractor* e, const uint8_t* image, int width, i
         // a copy kernel into HBM; extraction with describe writing keypoints,
         // descriptors, the count and the error word straight into the pinned
         // output block
+        uint8_t* stage = e->fg_img ? e->fg_img : e->h_img;
         if (step == e->img_pitch)
-            std::memcpy(e->h_img, image, step * (size_t)height);
+            std::memcpy(stage, image, step * (size_t)height);
         else
             for (int y = 0; y < height; ++y)
-                std::memcpy(e->h_img + (size_t)y * e->img_pitch, image + (size_t)y * step, width);
-        ORB_HIP(launch_copy16(e->d_img, e->h_img, e->img_pitch * (size_t)height, s));
-        return run_batch(e, e->d_img, 1, e->img_pitch, e->img_pitch * height,
-                         reinterpret_cast<orbgpu_keypoint*>(e->h_single + 16), e->h_single + e->single_desc_off,
-                         reinterpret_cast<int*>(e->h_single), e->max_kps, s, reinterpret_cast<int*>(e->h_single + 4));
+                std::memcpy(stage + (size_t)y * e->img_pitch, image + (size_t)y * step, width);
+        if (!e->fg_img) ORB_HIP(launch_copy16(e->d_img, e->h_img, e->img_pitch * (size_t)height, s));
+        const int rc = run_batch(e, e->fg_img ? e->fg_img : e->d_img, 1, e->img_pitch, e->img_pitch * height,
+                                 reinterpret_cast<orbgpu_keypoint*>(e->h_single + 16), e->h_single + e->single_desc_off,
+                                 reinterpret_cast<int*>(e->h_single), e->max_kps, s,
+                                 reinterpret_cast<int*>(e->h_single + 4));
+        if (rc || !single_done_flag()) return rc;
+        static std::atomic<unsigned long long> next_seq{1};  // distinct across extractors and calls
+        const unsigned long long seq = next_seq.fetch_add(1, std::memory_order_relaxed);
+        ORB_HIP(launch_done_flag(e->h_done, seq, s));
+        e->done_seq = seq;
+        return ORBGPU_OK;
     }
     // the drop-in path with copy-engine transfers: host image -> pinned
     // staging -> one async H2D; extraction; the error word folded into the
@@ -844,9 +891,26 @@ static int extract_issue(orbgpu_extractor* e, const uint8_t* image, int width, i
     return ORBGPU_OK;
 }
 
+// the call's completion: its flag (spun on; after 20 ms, or with no flag
+// pending, the stream is synchronised, which also reports a failed kernel)
+static int wait_single(orbgpu_extractor* e) {
+    const unsigned long long seq = e->done_seq;
+    e->done_seq = 0;
+    if (seq) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned it = 1;; ++it) {
+            if (__atomic_load_n(e->h_done, __ATOMIC_ACQUIRE) == seq) return ORBGPU_OK;
+            if ((it & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+            __builtin_ia32_pause();
+        }
+    }
+    ORB_HIP(hipStreamSynchronize(e->stream));
+    return ORBGPU_OK;
+}
+
 static int extract_finish(orbgpu_extractor* e, orbgpu_keypoint* keypoints, uint8_t* descriptors, int capacity,
                           int* n) {
-    ORB_HIP(hipStreamSynchronize(e->stream));
+    if (int rc = wait_single(e)) return rc;
     int count = 0, err = 0;
     std::memcpy(&count, e->h_single, sizeof(int));
     std::memcpy(&err, e->h_single + 4, sizeof(int));

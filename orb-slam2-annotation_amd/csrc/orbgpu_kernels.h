@@ -82,6 +82,7 @@ hipError_t launch_pack_rows(int batch, int cap, int ntensors, const ::orbgpu_pac
 // nbytes (a multiple of 16, both pointers 16-byte aligned) from src to dst by a kernel;
 // src may be pinned host memory
 hipError_t launch_copy16(void* dst, const void* src, size_t nbytes, hipStream_t stream);
+hipError_t launch_done_flag(unsigned long long* flag, unsigned long long v, hipStream_t stream);
 // several such copies (each a multiple of 16 bytes, 16-byte aligned) in one launch
 constexpr int kCopyList = 16;
 struct CopyDesc16 {

@@ -53,6 +53,14 @@ __global__ __launch_bounds__(256) void copy16_kernel(uint4* __restrict__ dst, co
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) dst[i] = src[i];
 }
 
+// The single-frame completion flag: launched after the extraction on its
+// stream, so every output store of the call has completed (kernel boundary)
+// when it publishes the call's sequence number to coherent pinned memory; the
+// host spins on it instead of waking from hipStreamSynchronize.
+__global__ void done_flag_kernel(unsigned long long* flag, unsigned long long v) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // up to kCopyList such copies in one launch (blockIdx.y = the copy)
 __global__ __launch_bounds__(256) void copy16_list_kernel(CopyList16 L) {
     const CopyDesc16& d = L.d[blockIdx.y];
@@ -63,6 +71,11 @@ __global__ __launch_bounds__(256) void copy16_list_kernel(CopyList16 L) {
 }
 
 }  // namespace
+
+hipError_t launch_done_flag(unsigned long long* flag, unsigned long long v, hipStream_t stream) {
+    hipLaunchKernelGGL(done_flag_kernel, dim3(1), dim3(64), 0, stream, flag, v);
+    return hipGetLastError();
+}
 
 hipError_t launch_copy16_list(const CopyList16& L, hipStream_t stream) {
     if (L.n <= 0) return hipSuccess;

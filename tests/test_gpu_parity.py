@@ -173,6 +173,28 @@ def test_single_frame_host_path_levels_and_keypoints(w, h, nf):
         _assert_same_kps(kg, dg, kr, dr)
 
 
+def test_single_frame_repeated_calls_read_complete_results():
+    """The single-frame call returns when its completion flag (written after
+    the extraction by a one-wave kernel into coherent pinned memory) arrives,
+    not after a stream synchronisation: 120 calls alternating two frames on
+    two extractors (the stereo pair's pattern) must each return exactly that
+    frame's keypoints and descriptors -- a result read before all of the
+    call's output stores landed would differ."""
+    og = _gpu()
+    frames = synth.mono_stream(2, 640, 480, seed=31)
+    ref = orbref.Extractor(nfeatures=1000)
+    exs = [og.Extractor(nfeatures=1000, width=640, height=480, max_batch=1) for _ in range(2)]
+    want = []
+    for f in frames:
+        kg, dg = exs[0].extract(f)
+        _assert_same_kps(kg, dg, *ref.extract(f))
+        want.append((kg.tobytes(), dg.tobytes()))
+    for it in range(120):
+        j = (it // 2) % 2 if it % 3 else it % 2
+        kg, dg = exs[it % 2].extract(frames[j])
+        assert (kg.tobytes(), dg.tobytes()) == want[j], f"call {it} (frame {j}, extractor {it % 2}) differs"
+
+
 def test_batch_device_matches_single(mono_frames):
     og = _gpu()
     B = len(mono_frames)
