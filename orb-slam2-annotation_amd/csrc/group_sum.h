@@ -43,4 +43,19 @@ __device__ __forceinline__ double group_sum_dpp(double x) {
     return x;
 }
 
+// inclusive prefix sum over the 64 lanes of a wave (integer: exact in any
+// order) on DPP: row_shr 1, 2, 4, 8 inside each 16-lane row, then row 0's
+// total broadcast into rows 1 and 3 and rows 0-1's into rows 2 and 3
+// (row_bcast:15 / :31).  Six full-rate VALU ops instead of six ds_bpermute
+// round trips; every lane of the wave must be active.
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false); // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false); // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 }  // namespace orbgpu

@@ -32,6 +32,7 @@
 #include "epnp.h"
 #include "host_common.h"
 #include "host_ctx.h"
+#include "group_sum.h"
 
 namespace orbgpu {
 
@@ -182,12 +183,7 @@ __global__ __launch_bounds__(kSelThreads) void rt_parallax_kernel(const unsigned
                 c[q] = s_hist[4 * lane + q];
                 sum += c[q];
             }
-            int incl = sum;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int t = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += t;
-            }
+            const int incl = wave_incl_scan_dpp(sum);
             const int k = s_k;
             int below = incl - sum;
             if (below <= k && k < incl) {  // exactly one lane

@@ -20,6 +20,7 @@
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
 #include "../../include/orbgpu.h"
+#include "group_sum.h"
 
 namespace orbgpu {
 
@@ -240,12 +241,7 @@ __global__ __launch_bounds__(kMatchThreads) void match_init_kernel(
             loc[k] = run;
             run += s_cend[kPer * tid + k];
         }
-        int incl = run;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += t;
-        }
+        const int incl = wave_incl_scan_dpp(run);
         if (lane == 63) s_wsum[wave] = incl;
         __syncthreads();
         int base = incl - run;

@@ -22,6 +22,7 @@
 // identical to the oracle.
 #include "orbgpu_internal.h"
 #include "orbgpu_kernels.h"
+#include "group_sum.h"
 #include <algorithm>
 #include <type_traits>
 
@@ -70,15 +71,7 @@ __device__ inline ONode child_rect(const ONode& n, int q) {
     return c;
 }
 
-__device__ inline int wave_incl_scan(int v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
-}
+__device__ inline int wave_incl_scan(int v) { return wave_incl_scan_dpp(v); }
 
 // In-place exclusive scan of a[0..n) in LDS by the whole block; returns total.
 template <int NT>

@@ -1044,15 +1044,21 @@ int orbgpu_extractor_copy_levels(orbgpu_extractor* e, int frame, uint8_t* const*
     }
     if (!e->h_levels) ORB_HIP(hipHostMalloc((void**)&e->h_levels, total, hipHostMallocDefault));
     // level 0 of the last single-frame call is still in the pinned upload
-    // staging (zero-copy path); other levels (and level 0 otherwise) come back
-    // by one copy kernel writing the pinned staging (no copy-engine transfers)
+    // staging (pinned-staging path); other levels, and level 0 otherwise (the
+    // fine-grained HBM staging, a batch), come back by one copy kernel writing
+    // the pinned staging (no copy-engine transfers; a level 0 whose rows do not
+    // fit the staging's level-0 pitch by a 2-D copy)
     const bool l0_host = single_zero_copy() && e->last_img == e->d_img && e->last_batch == 1;
-    if (!l0_host)
-        ORB_HIP(hipMemcpy2DAsync(e->h_levels, (size_t)e->g.lv[0].pitch, e->last_img + (size_t)frame * e->last_frame,
-                                 e->last_row, e->g.lv[0].w, e->g.lv[0].h, hipMemcpyDeviceToHost, e->stream));
-    if (e->nlevels > 1) {
+    const uint8_t* l0_dev = e->last_img + (size_t)frame * e->last_frame;
+    const bool l0_kernel = !l0_host && e->last_row <= (size_t)e->g.lv[0].pitch &&
+                           (((uintptr_t)l0_dev | e->last_row * e->g.lv[0].h) & 15) == 0;
+    if (!l0_host && !l0_kernel)
+        ORB_HIP(hipMemcpy2DAsync(e->h_levels, (size_t)e->g.lv[0].pitch, l0_dev, e->last_row, e->g.lv[0].w,
+                                 e->g.lv[0].h, hipMemcpyDeviceToHost, e->stream));
+    if (e->nlevels > 1 || l0_kernel) {
         CopyList16 L{};
         L.n = 0;
+        if (l0_kernel) L.d[L.n++] = CopyDesc16{l0_dev, e->h_levels + off[0], e->last_row * e->g.lv[0].h};
         for (int l = 1; l < e->nlevels && L.n < kCopyList; ++l) {
             const LevelGeom& v = e->g.lv[l];
             L.d[L.n++] = CopyDesc16{e->d_pyr + v.offset + (size_t)frame * v.frame_bytes, e->h_levels + off[l],
@@ -1064,7 +1070,7 @@ int orbgpu_extractor_copy_levels(orbgpu_extractor* e, int frame, uint8_t* const*
     for (int l = 0; l < e->nlevels; ++l) {
         const LevelGeom& v = e->g.lv[l];
         const uint8_t* src = l == 0 && l0_host ? e->h_img : e->h_levels + off[l];
-        const size_t sp = l == 0 && l0_host ? e->img_pitch : (size_t)v.pitch;
+        const size_t sp = l == 0 && (l0_host || l0_kernel) ? (l0_host ? e->img_pitch : e->last_row) : (size_t)v.pitch;
         for (int y = 0; y < v.h; ++y) std::memcpy(dst[l] + (size_t)y * dst_step[l], src + (size_t)y * sp, (size_t)v.w);
     }
     return ORBGPU_OK;

@@ -12,6 +12,7 @@
 #include "../../include/orbgpu_proj.h"
 #include "proj_kernels.h"
 #include "device_state.h"
+#include "group_sum.h"
 
 namespace orbgpu {
 
@@ -521,12 +522,7 @@ __global__ __launch_bounds__(kProjThreads) void proj_kernel(const orbgpu_proj_ca
             c3[k] = s_cnt[kCPT * tid + k];
             loc += c3[k];
         }
-        int v = loc;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(v, o, 64);
-            if (lane >= o) v += t;
-        }
+        const int v = wave_incl_scan_dpp(loc);
         int* s_wsum = s_ncand[0];  // 16 wave totals (s_ncand is free until the lists)
         if (lane == 63) s_wsum[wave] = v;
         __syncthreads();

@@ -36,6 +36,7 @@
 #include "orbgpu_internal.h"
 #include "stereo_kernels.h"
 #include "device_state.h"
+#include "group_sum.h"
 
 namespace orbgpu {
 
@@ -104,12 +105,7 @@ __global__ __launch_bounds__(kStThreads) void stereo_kernel(StereoArgs a, int S)
     for (int base = 0; base < H; base += kStThreads) {
         const int i = base + tid;
         const int x = i < H ? s_cnt[i] : 0;
-        int v = x;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(v, o, 64);
-            if (lane >= o) v += y;
-        }
+        const int v = wave_incl_scan_dpp(x);
         if (lane == 63) s_wsum[wave] = v;
         __syncthreads();
         if (tid == 0) {
