@@ -177,6 +177,121 @@ __device__ inline int pow2ceil(int v) {
 #define OCT_T(k) ((void)0)
 #endif
 
+__device__ inline void wave_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ inline int lanes_below(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// One pass over a list of nL <= 64 nodes by wave 0 alone (lane = node): the
+// same ordering, push bases, kept-node positions and pushes as the block path
+// below, with wave scans and ballots instead of block scans and barriers.
+//   main pass (:610-669): every node with > 1 key is divided, in list order;
+//   inner pass (:681-743): the nodes with > 1 key in descending (size, seq)
+//   order, up to and including the division that makes the list reach N.
+// Publishes C, S and an error code in s_misc[20..22], the children with > 1
+// key in *s_nexp; s_flag / s_aux1 / the quadrant counters as the remap reads
+// them.  (Inner-pass scratch: the sort keys in the next list's buffer, the
+// rank-ordered child counts in s_aux1 and push bases in s_aux0 -- all read
+// before the pushes and the kept positions overwrite them, in wave order.)
+template <class QC>
+__device__ void wave_small_pass(const ONode* old, ONode* nw, unsigned long long* s_sortk, const QC& qc, int* s_aux0,
+                                int* s_aux1, uint8_t* s_flag, int* s_misc, int* s_nexp, int nL, int N, int ncap,
+                                int nseq, bool inner, int lane) {
+    const bool valid = lane < nL;
+    ONode nd{};
+    if (valid) nd = old[lane];
+    const bool div = valid && nd.cnt > 1;
+    const int nch = div ? qc.nonzero(lane) : 0;
+    bool flag;
+    int C, S, base, spos;
+    if (!inner) {
+        // (children << 16 | kept) scanned together, as the block path
+        const int v = valid ? (div ? nch << 16 : 1) : 0;
+        const int incl = wave_incl_scan_dpp(v);
+        const int tot = __builtin_amdgcn_readlane(incl, 63);
+        C = tot >> 16;
+        S = tot & 0xFFFF;
+        flag = div;
+        base = (incl - v) >> 16;
+        spos = (incl - v) & 0xFFFF;
+    } else {
+        // descending (cnt, seq) rank among the dividing nodes (keys distinct:
+        // they end in the node index)
+        const unsigned long long key =
+            div ? ((unsigned long long)min(nd.cnt, 0xFFFFFFu) << 40) | ((unsigned long long)(nd.seq & 0xFFFFFFFu) << 12) |
+                      (unsigned)lane
+                : 0ull;
+        if (valid) s_sortk[lane] = key;
+        wave_sync();
+        int rank = 0;
+        int j = 0;
+#pragma unroll 4
+        for (; j + 1 < nL; j += 2) {
+            const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(s_sortk + j);
+            rank += (kk.x > key) + (kk.y > key);
+        }
+        if (j < nL) rank += s_sortk[j] > key;
+        const int m = __popcll(__ballot(div));
+        // children per rank, their prefix; the first rank whose division makes
+        // the list reach N (nL + sum of (children - 1) up to it >= N)
+        if (div) s_aux1[rank] = nch;
+        wave_sync();
+        const int x = lane < m ? s_aux1[lane] : 0;
+        const int incl = wave_incl_scan_dpp(x);
+        const int ex = incl - x;
+        const unsigned long long br = __ballot(lane < m && nL + (ex - lane) + x - 1 >= N);
+        const int kstop = br ? (int)__builtin_ctzll(br) : m - 1;
+        C = kstop >= 0 ? __builtin_amdgcn_readlane(incl, kstop) : 0;
+        if (lane == 0) s_misc[24] = kstop;  // (the debug trace's kstop)
+        if (lane < m) s_aux0[lane] = ex;
+        wave_sync();
+        flag = div && rank <= kstop;
+        base = flag ? s_aux0[rank] : 0;
+        const unsigned long long bs = __ballot(valid && !flag);
+        S = __popcll(bs);
+        spos = lanes_below(bs);
+        wave_sync();  // (the rank scratch is read before the kept positions overwrite s_aux1)
+    }
+    const bool bad = C + S > ncap || nseq + C > 0x0FFFFFFF;
+    if (lane == 0) {
+        s_misc[20] = C;
+        s_misc[21] = S;
+        s_misc[22] = bad ? (C + S > ncap ? kErrNodeCap : kErrSeqCap) : 0;
+    }
+    int nexp = 0;  // this node's children with > 1 key
+    if (!bad && valid) {
+        s_flag[lane] = flag;
+        if (flag) {
+            int p = base;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t c = qc.get(lane, q);
+                if (c > 0) {
+                    const int pos = C - 1 - p;
+                    ONode ch = child_rect(nd, q);
+                    ch.cnt = c;
+                    ch.seq = (uint32_t)(nseq + p);
+                    nw[pos] = ch;
+                    qc.set(lane, q, pos);
+                    nexp += c > 1;
+                    ++p;
+                }
+            }
+        } else {
+            const int pos = C + spos;
+            nw[pos] = nd;
+            s_aux1[lane] = pos;
+        }
+    }
+    const int tot_exp = __popcll(__ballot(nexp >= 1)) + __popcll(__ballot(nexp >= 2)) + __popcll(__ballot(nexp >= 3)) +
+                        __popcll(__ballot(nexp >= 4));
+    if (lane == 0) *s_nexp = tot_exp;
+}
+
 template <int NT, bool LDS>
 __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int nk, int ncells, int ncap, int ncap2,
                             const uint32_t* __restrict__ cand, uint32_t* __restrict__ out,
@@ -322,152 +437,170 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
         OCT_T(3 + 4 * guard);
         // processing order and push bases
         int C, S;  // children pushed this pass, surviving nodes
-        if (!inner) {
-            // one scan of (children << 16 | survives): push bases and survivor
-            // positions together (C <= 4 nL and S <= nL stay below 2^16)
-            for (int i = tid; i < nL; i += NT) {
-                const bool div = old[i].cnt > 1;
-                const int nch = qc.nonzero(i);
-                s_aux0[i] = div ? nch << 16 : 1;
-                s_flag[i] = div;
-            }
+        // (nL is block-uniform; read as a scalar so the branch is a scalar
+        // compare: tools/check_scc.py)
+        if (__builtin_amdgcn_readfirstlane(nL) <= 64) {
+            // a list of at most 64 nodes (every main pass of a 640x480 level
+            // and most inner passes): wave 0 alone orders, scans and pushes
+            // it, lane = node, with wave scans and ballots -- one block barrier
+            // before the remap instead of a scan's and a phase's each
+            if (tid < 64) wave_small_pass(old, nw, s_sortk, qc, s_aux0, s_aux1, s_flag, s_misc, s_nexp, nL, N, ncap,
+                                          nseq, inner, tid);
             __syncthreads();
-            const int tot = block_scan<NT>(s_aux0, nL, s_tmp);
-            C = tot >> 16;
-            S = tot & 0xFFFF;
+            C = s_misc[20];
+            S = s_misc[21];
+            if (s_misc[22]) {
+                if (tid == 0) { atomicOr(err, s_misc[22]); oct_count[f * kOcStride + l] = 0; }
+                return;
+            }
         } else {
-            // compact the nodes with > 1 key, sort descending by (cnt, seq)
-            for (int i = tid; i < nL; i += NT) s_aux1[i] = old[i].cnt > 1;
-            __syncthreads();
-            const int m = block_scan<NT>(s_aux1, nL, s_tmp);
-            const int P = pow2ceil(max(m, 1));
-            constexpr int kRankPer = 2;  // up to 2 keys per thread: rank sort, else bitonic
-            const bool by_rank = m <= kRankPer * NT;
-            for (int i = tid; i < nL; i += NT)
-                if (old[i].cnt > 1)
-                    s_sortk[s_aux1[i]] = ((unsigned long long)min(old[i].cnt, 0xFFFFFFu) << 40) |
-                                         ((unsigned long long)(old[i].seq & 0xFFFFFFFu) << 12) | (unsigned)i;
-            if (!by_rank)
-                for (int i = m + tid; i < P; i += NT) s_sortk[i] = 0ull;
-            __syncthreads();
-            if (by_rank) {
-                // descending order by rank = the number of larger keys (the keys
-                // are distinct: they end in the node index); every thread reads
-                // the same key per step (LDS broadcast), no barrier per step
-                unsigned long long mine[kRankPer];
-                int rank[kRankPer];
-#pragma unroll
-                for (int u = 0; u < kRankPer; ++u) {
-                    mine[u] = s_sortk[min(tid + u * NT, max(m - 1, 0))];
-                    rank[u] = 0;
-                }
-                // two keys per 16-byte read, several reads in flight; only the
-                // key slots that exist (the second when m > NT), and a wave
-                // whose threads hold no key skips the loop (wave-uniform)
-                auto rank_keys = [&](auto nu_c) {
-                    constexpr int NU = decltype(nu_c)::value;
-                    int j = 0;
-#pragma unroll 4
-                    for (; j + 1 < m; j += 2) {
-                        const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(s_sortk + j);
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) rank[u] += (kk.x > mine[u]) + (kk.y > mine[u]);
-                    }
-                    if (j < m) {
-                        const unsigned long long kj = s_sortk[j];
-#pragma unroll
-                        for (int u = 0; u < NU; ++u) rank[u] += kj > mine[u];
-                    }
-                };
-                if ((tid & ~63) < m) {
-                    if (m > NT) rank_keys(std::integral_constant<int, 2>{});
-                    else rank_keys(std::integral_constant<int, 1>{});
+            if (!inner) {
+                // one scan of (children << 16 | survives): push bases and survivor
+                // positions together (C <= 4 nL and S <= nL stay below 2^16)
+                for (int i = tid; i < nL; i += NT) {
+                    const bool div = old[i].cnt > 1;
+                    const int nch = qc.nonzero(i);
+                    s_aux0[i] = div ? nch << 16 : 1;
+                    s_flag[i] = div;
                 }
                 __syncthreads();
-#pragma unroll
-                for (int u = 0; u < kRankPer; ++u)
-                    if (tid + u * NT < m) s_sortk[rank[u]] = mine[u];
-                __syncthreads();
+                const int tot = block_scan<NT>(s_aux0, nL, s_tmp);
+                C = tot >> 16;
+                S = tot & 0xFFFF;
             } else {
-                for (int k = 2; k <= P; k <<= 1)
-                    for (int j = k >> 1; j > 0; j >>= 1) {
-                        for (int i = tid; i < P; i += NT) {
-                            const int ixj = i ^ j;
-                            if (ixj > i) {
-                                const unsigned long long a = s_sortk[i], b = s_sortk[ixj];
-                                const bool desc = (i & k) == 0;
-                                if (desc ? (a < b) : (a > b)) { s_sortk[i] = b; s_sortk[ixj] = a; }
-                            }
-                        }
-                        __syncthreads();
+                // compact the nodes with > 1 key, sort descending by (cnt, seq)
+                for (int i = tid; i < nL; i += NT) s_aux1[i] = old[i].cnt > 1;
+                __syncthreads();
+                const int m = block_scan<NT>(s_aux1, nL, s_tmp);
+                const int P = pow2ceil(max(m, 1));
+                constexpr int kRankPer = 2;  // up to 2 keys per thread: rank sort, else bitonic
+                const bool by_rank = m <= kRankPer * NT;
+                for (int i = tid; i < nL; i += NT)
+                    if (old[i].cnt > 1)
+                        s_sortk[s_aux1[i]] = ((unsigned long long)min(old[i].cnt, 0xFFFFFFu) << 40) |
+                                             ((unsigned long long)(old[i].seq & 0xFFFFFFFu) << 12) | (unsigned)i;
+                if (!by_rank)
+                    for (int i = m + tid; i < P; i += NT) s_sortk[i] = 0ull;
+                __syncthreads();
+                if (by_rank) {
+                    // descending order by rank = the number of larger keys (the keys
+                    // are distinct: they end in the node index); every thread reads
+                    // the same key per step (LDS broadcast), no barrier per step
+                    unsigned long long mine[kRankPer];
+                    int rank[kRankPer];
+    #pragma unroll
+                    for (int u = 0; u < kRankPer; ++u) {
+                        mine[u] = s_sortk[min(tid + u * NT, max(m - 1, 0))];
+                        rank[u] = 0;
                     }
+                    // two keys per 16-byte read, several reads in flight; only the
+                    // key slots that exist (the second when m > NT), and a wave
+                    // whose threads hold no key skips the loop (wave-uniform)
+                    auto rank_keys = [&](auto nu_c) {
+                        constexpr int NU = decltype(nu_c)::value;
+                        int j = 0;
+    #pragma unroll 4
+                        for (; j + 1 < m; j += 2) {
+                            const ulonglong2 kk = *reinterpret_cast<const ulonglong2*>(s_sortk + j);
+    #pragma unroll
+                            for (int u = 0; u < NU; ++u) rank[u] += (kk.x > mine[u]) + (kk.y > mine[u]);
+                        }
+                        if (j < m) {
+                            const unsigned long long kj = s_sortk[j];
+    #pragma unroll
+                            for (int u = 0; u < NU; ++u) rank[u] += kj > mine[u];
+                        }
+                    };
+                    if ((tid & ~63) < m) {
+                        if (m > NT) rank_keys(std::integral_constant<int, 2>{});
+                        else rank_keys(std::integral_constant<int, 1>{});
+                    }
+                    __syncthreads();
+    #pragma unroll
+                    for (int u = 0; u < kRankPer; ++u)
+                        if (tid + u * NT < m) s_sortk[rank[u]] = mine[u];
+                    __syncthreads();
+                } else {
+                    for (int k = 2; k <= P; k <<= 1)
+                        for (int j = k >> 1; j > 0; j >>= 1) {
+                            for (int i = tid; i < P; i += NT) {
+                                const int ixj = i ^ j;
+                                if (ixj > i) {
+                                    const unsigned long long a = s_sortk[i], b = s_sortk[ixj];
+                                    const bool desc = (i & k) == 0;
+                                    if (desc ? (a < b) : (a > b)) { s_sortk[i] = b; s_sortk[ixj] = a; }
+                                }
+                            }
+                            __syncthreads();
+                        }
+                }
+                // rank r -> (nch - 1); inclusive scan; first r reaching N
+                for (int r = tid; r < m; r += NT) {
+                    const int i = (int)(s_sortk[r] & 0xFFF);
+                    s_aux1[r] = qc.nonzero(i) - 1;
+                }
+                if (tid == 0) s_misc[24] = m - 1;
+                __syncthreads();
+                block_scan<NT>(s_aux1, m, s_tmp);  // exclusive prefix of (nch-1)
+                for (int r = tid; r < m; r += NT) {
+                    const int i = (int)(s_sortk[r] & 0xFFF);
+                    if (nL + s_aux1[r] + qc.nonzero(i) - 1 >= N) atomicMin(&s_misc[24], r);
+                }
+                for (int i = tid; i < nL; i += NT) { s_flag[i] = 0; s_aux0[i] = 0; }
+                __syncthreads();
+                const int kstop = s_misc[24];
+                // push bases over ranks 0..kstop, scattered to node index
+                for (int r = tid; r < m; r += NT) {
+                    const int i = (int)(s_sortk[r] & 0xFFF);
+                    s_aux1[r] = r <= kstop ? qc.nonzero(i) : 0;
+                }
+                __syncthreads();
+                C = block_scan<NT>(s_aux1, m, s_tmp);
+                for (int r = tid; r <= kstop && r < m; r += NT) {
+                    const int i = (int)(s_sortk[r] & 0xFFF);
+                    s_aux0[i] = s_aux1[r];
+                    s_flag[i] = 1;
+                }
+                __syncthreads();
             }
-            // rank r -> (nch - 1); inclusive scan; first r reaching N
-            for (int r = tid; r < m; r += NT) {
-                const int i = (int)(s_sortk[r] & 0xFFF);
-                s_aux1[r] = qc.nonzero(i) - 1;
+            OCT_T(4 + 4 * guard);
+            if (inner) {  // survivors keep their order after the C pushed children
+                for (int i = tid; i < nL; i += NT) s_aux1[i] = s_flag[i] ? 0 : 1;
+                __syncthreads();
+                S = block_scan<NT>(s_aux1, nL, s_tmp);
             }
-            if (tid == 0) s_misc[24] = m - 1;
-            __syncthreads();
-            block_scan<NT>(s_aux1, m, s_tmp);  // exclusive prefix of (nch-1)
-            for (int r = tid; r < m; r += NT) {
-                const int i = (int)(s_sortk[r] & 0xFFF);
-                if (nL + s_aux1[r] + qc.nonzero(i) - 1 >= N) atomicMin(&s_misc[24], r);
+            if (C + S > ncap || nseq + C > 0x0FFFFFFF) {
+                if (tid == 0) { atomicOr(err, C + S > ncap ? kErrNodeCap : kErrSeqCap); oct_count[f * kOcStride + l] = 0; }
+                return;
             }
-            for (int i = tid; i < nL; i += NT) { s_flag[i] = 0; s_aux0[i] = 0; }
-            __syncthreads();
-            const int kstop = s_misc[24];
-            // push bases over ranks 0..kstop, scattered to node index
-            for (int r = tid; r < m; r += NT) {
-                const int i = (int)(s_sortk[r] & 0xFFF);
-                s_aux1[r] = r <= kstop ? qc.nonzero(i) : 0;
+            for (int i = tid; i < nL; i += NT) {
+                const ONode nd = old[i];
+                const int pk = s_aux0[i];  // main pass: packed prefix; inner pass: push base
+                if (s_flag[i]) {
+                    int p = inner ? pk : pk >> 16;
+    #pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t c = qc.get(i, q);
+                        if (c > 0) {
+                            const int pos = C - 1 - p;
+                            ONode ch = child_rect(nd, q);
+                            ch.cnt = c;
+                            ch.seq = (uint32_t)(nseq + p);
+                            nw[pos] = ch;
+                            qc.set(i, q, pos);
+                            if (c > 1) atomicAdd(s_nexp, 1);
+                            ++p;
+                        }
+                    }
+                } else {
+                    const int pos = C + (inner ? s_aux1[i] : (pk & 0xFFFF));
+                    nw[pos] = nd;
+                    s_aux1[i] = pos;
+                }
             }
             __syncthreads();
-            C = block_scan<NT>(s_aux1, m, s_tmp);
-            for (int r = tid; r <= kstop && r < m; r += NT) {
-                const int i = (int)(s_sortk[r] & 0xFFF);
-                s_aux0[i] = s_aux1[r];
-                s_flag[i] = 1;
-            }
-            __syncthreads();
-        }
-        OCT_T(4 + 4 * guard);
-        if (inner) {  // survivors keep their order after the C pushed children
-            for (int i = tid; i < nL; i += NT) s_aux1[i] = s_flag[i] ? 0 : 1;
-            __syncthreads();
-            S = block_scan<NT>(s_aux1, nL, s_tmp);
         }
         const int nNew = C + S;
-        if (nNew > ncap || nseq + C > 0x0FFFFFFF) {
-            if (tid == 0) { atomicOr(err, nNew > ncap ? kErrNodeCap : kErrSeqCap); oct_count[f * kOcStride + l] = 0; }
-            return;
-        }
-        for (int i = tid; i < nL; i += NT) {
-            const ONode nd = old[i];
-            const int pk = s_aux0[i];  // main pass: packed prefix; inner pass: push base
-            if (s_flag[i]) {
-                int p = inner ? pk : pk >> 16;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t c = qc.get(i, q);
-                    if (c > 0) {
-                        const int pos = C - 1 - p;
-                        ONode ch = child_rect(nd, q);
-                        ch.cnt = c;
-                        ch.seq = (uint32_t)(nseq + p);
-                        nw[pos] = ch;
-                        qc.set(i, q, pos);
-                        if (c > 1) atomicAdd(s_nexp, 1);
-                        ++p;
-                    }
-                }
-            } else {
-                const int pos = C + (inner ? s_aux1[i] : (pk & 0xFFFF));
-                nw[pos] = nd;
-                s_aux1[i] = pos;
-            }
-        }
-        __syncthreads();
         OCT_T(5 + 4 * guard);
         for (int k = tid; k < nk; k += NT) {
             const int i = ks.node(k);
