@@ -290,6 +290,12 @@ __device__ void wave_small_pass(const ONode* old, ONode* nw, unsigned long long*
     const int tot_exp = __popcll(__ballot(nexp >= 1)) + __popcll(__ballot(nexp >= 2)) + __popcll(__ballot(nexp >= 3)) +
                         __popcll(__ballot(nexp >= 4));
     if (lane == 0) *s_nexp = tot_exp;
+    // the last pass (:673 / :740): the best-key words of the final list, in
+    // s_aux0 (its scratch reads are behind, in this wave's order), zeroed here
+    // so the remap sweep can take every key's response straight away
+    const int nNew = C + S;
+    if (!bad && (nNew >= N || nNew == nL))
+        for (int i = lane; i < nNew; i += 64) s_aux0[i] = 0;
 }
 
 template <int NT, bool LDS>
@@ -358,24 +364,41 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
     // non-empty roots keep their order; empty ones are erased.  Computed by
     // thread r (no single-lane loop: see tools/check_scc.py for the ROCm 7.2
     // miscompile a uniform-address select in such a loop triggered).
-    for (int r = tid; r < nini; r += NT) s_aux1[r] = s_aux0[r] > 0 ? 1 : 0;
-    __syncthreads();
-    const int nroots = block_scan<NT>(s_aux1, nini, s_tmp);
-    for (int r = tid; r < nini; r += NT) {
-        const int c = s_aux0[r];
-        const int pos = s_aux1[r];
-        if (c > 0) {
-            ONode nd;
-            const int x0 = (int)(L.hx * (float)r), x1 = (int)(L.hx * (float)(r + 1));
-            nd.r0 = (uint32_t)x0;
-            nd.r1 = (uint32_t)x1 | ((uint32_t)(L.max_by - kBorder) << 16);
-            nd.cnt = (uint32_t)c;
-            nd.seq = (uint32_t)r;
-            s_node0[pos] = nd;
+    auto make_root = [&](int r, int c, int pos) {
+        ONode nd;
+        const int x0 = (int)(L.hx * (float)r), x1 = (int)(L.hx * (float)(r + 1));
+        nd.r0 = (uint32_t)x0;
+        nd.r1 = (uint32_t)x1 | ((uint32_t)(L.max_by - kBorder) << 16);
+        nd.cnt = (uint32_t)c;
+        nd.seq = (uint32_t)r;
+        s_node0[pos] = nd;
+    };
+    int nroots;
+    if (__builtin_amdgcn_readfirstlane(nini) <= 64) {
+        // up to 64 roots (every level of 640x480 .. 1241x376): wave 0 alone
+        // (lane = root), positions by ballot -- one block barrier
+        if (tid < 64) {
+            const int c = tid < nini ? s_aux0[tid] : 0;
+            const unsigned long long b = __ballot(c > 0);
+            const int pos = lanes_below(b);
+            if (c > 0) make_root(tid, c, pos);
+            if (tid < nini) s_aux1[tid] = c > 0 ? pos : -1;
+            if (tid == 0) s_misc[23] = __popcll(b);
         }
-        s_aux1[r] = c > 0 ? pos : -1;
+        __syncthreads();
+        nroots = s_misc[23];
+    } else {
+        for (int r = tid; r < nini; r += NT) s_aux1[r] = s_aux0[r] > 0 ? 1 : 0;
+        __syncthreads();
+        nroots = block_scan<NT>(s_aux1, nini, s_tmp);
+        for (int r = tid; r < nini; r += NT) {
+            const int c = s_aux0[r];
+            const int pos = s_aux1[r];
+            if (c > 0) make_root(r, c, pos);
+            s_aux1[r] = c > 0 ? pos : -1;
+        }
+        __syncthreads();
     }
-    __syncthreads();
     if (!one_root)  // one root: root 0 is node 0 (when there are keys at all)
         for (int k = tid; k < nk; k += NT) ks.set_node(k, s_aux1[ks.node(k)]);
     __syncthreads();
@@ -385,6 +408,8 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
     // in registers: every thread derives it from the same block-scan totals.
     int nL = nroots, cur = 0, nseq = nini;
     bool inner = false;
+    uint32_t* s_best = reinterpret_cast<uint32_t*>(s_aux0);  // (step 4's words, in aux0)
+    int best_state = 0;  // 1: zeroed by the last pass, 2: filled by its remap
     for (int guard = 0; guard < 4096; ++guard) {
         ONode* old = cur ? s_node1 : s_node0;
         ONode* nw = cur ? s_node0 : s_node1;
@@ -439,7 +464,8 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
         int C, S;  // children pushed this pass, surviving nodes
         // (nL is block-uniform; read as a scalar so the branch is a scalar
         // compare: tools/check_scc.py)
-        if (__builtin_amdgcn_readfirstlane(nL) <= 64) {
+        const bool small = __builtin_amdgcn_readfirstlane(nL) <= 64;
+        if (small) {
             // a list of at most 64 nodes (every main pass of a 640x480 level
             // and most inner passes): wave 0 alone orders, scans and pushes
             // it, lane = node, with wave scans and ballots -- one block barrier
@@ -601,10 +627,28 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
             __syncthreads();
         }
         const int nNew = C + S;
+        const bool done = nNew >= N || nNew == nL;  // :673 / :740
         OCT_T(5 + 4 * guard);
-        for (int k = tid; k < nk; k += NT) {
-            const int i = ks.node(k);
-            ks.set_node(k, s_flag[i] ? (int)qc.get(i, node_quad(old[i], ks.key(k))) : s_aux1[i]);
+        if (done && small) {
+            // the last pass after the wave path: the best-key words are zeroed,
+            // so each key's response goes to its final node in the remap sweep
+            for (int k = tid; k < nk; k += NT) {
+                const int i = ks.node(k);
+                const uint32_t key = ks.key(k);
+                const int ni = s_flag[i] ? (int)qc.get(i, node_quad(old[i], key)) : s_aux1[i];
+                ks.set_node(k, ni);
+                atomicMax(&s_best[ni], ((uint32_t)key_s(key) << 24) | (0xFFFFFFu - (uint32_t)k));
+            }
+            best_state = 2;
+        } else {
+            for (int k = tid; k < nk; k += NT) {
+                const int i = ks.node(k);
+                ks.set_node(k, s_flag[i] ? (int)qc.get(i, node_quad(old[i], ks.key(k))) : s_aux1[i]);
+            }
+            if (done) {  // (s_aux0 is not read by the remap)
+                for (int i = tid; i < nNew; i += NT) s_best[i] = 0;
+                best_state = 1;
+            }
         }
         __syncthreads();
         OCT_T(6 + 4 * guard);
@@ -614,7 +658,6 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
             trace[l * 512] = guard + 1;
         }
         const int nexp = *s_nexp;  // children with > 1 key (nToExpand)
-        const bool done = nNew >= N || nNew == nL;  // :673 / :740
         if (!inner && nNew + nexp * 3 > N) inner = true;  // :678
         nseq += C;
         cur ^= 1;
@@ -624,13 +667,17 @@ __device__ void octree_body(const Geom& g, const LevelGeom& L, int l, int f, int
         if (done) break;
     }
 
-    // 4. best key per node (max response, first in candidate order)
-    uint32_t* s_best = reinterpret_cast<uint32_t*>(s_aux0);
-    for (int i = tid; i < nL; i += NT) s_best[i] = 0;
-    __syncthreads();
-    for (int k = tid; k < nk; k += NT)
-        atomicMax(&s_best[ks.node(k)], ((uint32_t)key_s(ks.key(k)) << 24) | (0xFFFFFFu - (uint32_t)k));
-    __syncthreads();
+    // 4. best key per node (max response, first in candidate order); usually
+    // zeroed (best_state 1) or filled (2) by the last pass already
+    if (best_state == 0) {
+        for (int i = tid; i < nL; i += NT) s_best[i] = 0;
+        __syncthreads();
+    }
+    if (best_state < 2) {
+        for (int k = tid; k < nk; k += NT)
+            atomicMax(&s_best[ks.node(k)], ((uint32_t)key_s(ks.key(k)) << 24) | (0xFFFFFFu - (uint32_t)k));
+        __syncthreads();
+    }
     if (nL > L.ocap) {
         if (tid == 0) { atomicOr(err, kErrNodeCap); oct_count[f * kOcStride + l] = 0; }
         return;
