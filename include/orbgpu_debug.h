@@ -43,6 +43,14 @@ int orbgpu_debug_octree_trace(orbgpu_extractor* ex, int enable, int* out, int ca
 int orbgpu_debug_pyramid_emulate(int nfeatures, float scale_factor, int nlevels, int width, int height,
                                  const uint8_t* img, size_t img_step, uint8_t* out, size_t out_bytes, int* info);
 
+/* The fused pyramid plan's work per tick (no GPU; tools/pyr_plan_cost.py):
+ * rows[k * lanes + i] = output rows compute lane i (entry 0, then entry 1 at
+ * i + lanes / entries) computes at tick k, lane_info[i] = level | tail << 8
+ * (level 0: an idle lane), dims[0..3] = {ticks, lanes, compute waves,
+ * entries per lane}.  rows / lane_info may be NULL (dims only). */
+int orbgpu_debug_pyramid_plan_rows(int nfeatures, float scale_factor, int nlevels, int width, int height, int* rows,
+                                   size_t rows_n, int* lane_info, size_t lanes_n, int* dims);
+
 /* PnPsolver::qr_solve (PnPsolver.cpp:955-1047) as the GPU's EPnP runs it
  * (csrc/epnp.h qr_solve_6x4), on n independent 6 x 4 systems in HBM: A (n x
  * 24 doubles, row-major), b (n x 6), X (n x 4, read as the initial x: a

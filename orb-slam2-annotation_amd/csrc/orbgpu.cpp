@@ -1304,6 +1304,45 @@ int orbgpu_debug_pyramid_emulate(int nfeatures, float scale_factor, int nlevels,
     return ORBGPU_OK;
 }
 
+// The fused pyramid plan's work per tick (tools/pyr_plan_cost.py): rows[k *
+// lanes + i] = the rows lane i (entry 0, then entry 1 at i + CL) computes at
+// tick k; lane_info[i] = level | tail << 8 (level 0: an idle lane); dims =
+// {ticks, lanes, compute waves, entries per lane}.
+extern "C" int orbgpu_debug_pyramid_plan_rows(int nfeatures, float scale_factor, int nlevels, int width, int height,
+                                              int* rows, size_t rows_n, int* lane_info, size_t lanes_n, int* dims) {
+    if (!dims || nfeatures <= 0 || nlevels < 2 || nlevels > kMaxLevels || !(scale_factor > 1.f) || width <= 0 ||
+        height <= 0)
+        return fail(ORBGPU_ERR_ARG, "invalid plan arguments");
+    orbgpu_extractor e;
+    e.nfeatures = nfeatures;
+    e.scale_factor = scale_factor;
+    e.nlevels = nlevels;
+    e.ini_th = 20;
+    e.min_th = 7;
+    e.W = width;
+    e.H = height;
+    e.max_batch = 1;
+    std::vector<int4> ptab;
+    std::vector<int2> ytab;
+    int rc = build_geometry(&e, ptab, ytab, nullptr);
+    if (rc) return rc;
+    const Geom& g = e.g;
+    const int K = g.tk_ticks, CL = 64 * g.tk_cwaves, E = g.tk_e, n = CL * E;
+    dims[0] = K;
+    dims[1] = n;
+    dims[2] = g.tk_cwaves;
+    dims[3] = E;
+    if (!rows || !lane_info) return ORBGPU_OK;
+    if (rows_n < (size_t)K * n || lanes_n < (size_t)n) return fail(ORBGPU_ERR_CAPACITY, "plan output too small");
+    const uint32_t* rng = reinterpret_cast<const uint32_t*>(e.pyr_plan.tab.data()) + g.tk_rng;
+    for (int i = 0; i < n; ++i) {
+        const int4* r = &e.pyr_plan.ent[(size_t)i * 9];
+        lane_info[i] = r[2].w | (r[0].y ? 1 << 8 : 0);
+        for (int k = 0; k < K; ++k) rows[(size_t)k * n + i] = (int)((rng[(size_t)k * g.tk_rs + r[0].x] >> 11) & 31u);
+    }
+    return ORBGPU_OK;
+}
+
 namespace {
 
 // StereoArgs common to both entry points: level sizes and scales, thresholds,
