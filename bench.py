@@ -163,6 +163,7 @@ PROFILED_TAIL = 40     # a deferred leg's stage times: its last steps only (Stre
 STEP_TRACE = [os.environ.get("BENCH_STEP_TRACE") == "1"]  # diagnostics: per-step times of each timed leg
 MATCH_AFTER = ["fast_cells"]  # set from --match-after
 MATCH_PRIORITY = [0]  # set from --match-priority (0: default, -1: high, as the extraction streams)
+DEVICE_EVENTS = os.environ.get("BENCH_DEVICE_EVENTS", "1") != "0"  # Dev.event: device-scope ordering events
 
 
 # ---------------------------------------------------------------------------
@@ -219,7 +220,16 @@ class Dev:
         return torch.cuda.current_stream(self.device) if self.cuda else _NullStream()
 
     def event(self, timing=False):
-        return torch.cuda.Event(enable_timing=timing) if self.cuda else _NullEvent()
+        """a timing event (torch), or for stream-to-stream ordering a device-scope
+        one (orbgpu.DeviceEvent: a default event's system-scope fence stalled the
+        extraction stream ~7 us per record, profiles/r06_notes_ab.txt r6x;
+        BENCH_DEVICE_EVENTS=0 restores torch's)"""
+        if not self.cuda:
+            return _NullEvent()
+        if timing or not DEVICE_EVENTS:
+            return torch.cuda.Event(enable_timing=timing)
+        import orbgpu
+        return orbgpu.DeviceEvent()
 
     def synchronize(self):
         if self.cuda:

@@ -165,6 +165,20 @@ int orbgpu_extractor_stage_times(orbgpu_extractor* ex, float* ms4, int* nbatches
  * done. */
 int orbgpu_extractor_set_stage_event(orbgpu_extractor* ex, int stage, void* event);
 
+/* Device-scope events for ordering streams of one GPU (the stage hook above,
+ * a matcher stream behind the extraction stream): created with
+ * hipEventDisableTiming | hipEventDisableSystemFence, so recording one does
+ * not write the caches back to system scope -- a default event's marker
+ * costs the stream about 7 us before its next kernel on the MI355X
+ * (profiles/r06_notes_ab.txt r6x).  Kernel completion already makes a
+ * kernel's writes visible to later kernels of the device; an event the host
+ * synchronises on to read host memory must be a default one.  `stream` is a
+ * hipStream_t (NULL: the calling thread's default stream). */
+int orbgpu_device_event_create(void** event);
+int orbgpu_device_event_destroy(void* event);
+int orbgpu_device_event_record(void* event, void* stream);
+int orbgpu_stream_wait_device_event(void* stream, void* event);
+
 /* mvImagePyramid[level] of frame `frame` of the last extraction, copied to
  * host (ORBextractor.h:85; read by Frame::ComputeStereoMatches). */
 int orbgpu_extractor_copy_level(orbgpu_extractor* ex, int frame, int level, uint8_t* dst,

@@ -534,7 +534,9 @@ int run_batch(orbgpu_extractor* e, const uint8_t* imgs, int batch, size_t row_st
     if (e->profile) {
         if (e->ev_used == e->ev.size()) {
             std::array<hipEvent_t, 5> a;
-            for (hipEvent_t& x : a) ORB_HIP(hipEventCreate(&x));
+            // (timing only: no system-scope fence on record, which stalled the
+            // stream before its next kernel)
+            for (hipEvent_t& x : a) ORB_HIP(hipEventCreateWithFlags(&x, hipEventDisableSystemFence));
             e->ev.push_back(a);
         }
         evs = e->ev[e->ev_used++].data();
@@ -990,6 +992,31 @@ int orbgpu_extractor_profile(orbgpu_extractor* e, int enable) {
 int orbgpu_extractor_set_stage_event(orbgpu_extractor* e, int stage, void* event) {
     if (!e || stage < 0 || stage > 3) return fail(ORBGPU_ERR_ARG, "invalid argument");
     e->stage_ev[stage] = (hipEvent_t)event;
+    return ORBGPU_OK;
+}
+
+int orbgpu_device_event_create(void** event) {
+    if (!event) return fail(ORBGPU_ERR_ARG, "NULL event");
+    hipEvent_t e = nullptr;
+    ORB_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence));
+    *event = e;
+    return ORBGPU_OK;
+}
+
+int orbgpu_device_event_destroy(void* event) {
+    if (event) ORB_HIP(hipEventDestroy((hipEvent_t)event));
+    return ORBGPU_OK;
+}
+
+int orbgpu_device_event_record(void* event, void* stream) {
+    if (!event) return fail(ORBGPU_ERR_ARG, "NULL event");
+    ORB_HIP(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
+    return ORBGPU_OK;
+}
+
+int orbgpu_stream_wait_device_event(void* stream, void* event) {
+    if (!event) return fail(ORBGPU_ERR_ARG, "NULL event");
+    ORB_HIP(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0));
     return ORBGPU_OK;
 }
 

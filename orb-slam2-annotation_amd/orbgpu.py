@@ -101,6 +101,10 @@ def lib() -> ctypes.CDLL:
         L.orbgpu_extractor_create.argtypes = [i, f, i, i, i, i, i, i, ctypes.POINTER(vp)]
         L.orbgpu_extractor_create_on_device.argtypes = [i, i, f, i, i, i, i, i, i, ctypes.POINTER(vp)]
         L.orbgpu_extractor_destroy.argtypes = [vp]
+        L.orbgpu_device_event_create.argtypes = [ctypes.POINTER(vp)]
+        L.orbgpu_device_event_destroy.argtypes = [vp]
+        L.orbgpu_device_event_record.argtypes = [vp, vp]
+        L.orbgpu_stream_wait_device_event.argtypes = [vp, vp]
         L.orbgpu_device_count.argtypes = [ctypes.POINTER(i)]
         L.orbgpu_set_thread_device.argtypes = [i]
         L.orbgpu_get_thread_device.argtypes = [ctypes.POINTER(i)]
@@ -245,6 +249,41 @@ def _stream_ptr(stream) -> int | None:
     if stream is None:
         return None
     return getattr(stream, "cuda_stream", stream)
+
+
+class DeviceEvent:
+    """A device-scope hipEvent_t (orbgpu_device_event_create: no timing, no
+    system-scope fence when recorded) for ordering streams of one GPU.  It has
+    torch.cuda.Event's record / wait / cuda_event, so torch streams take it
+    (Stream.wait_event calls event.wait(stream)) and the extractor's stage
+    hook can record it.  Not for a host that synchronises on it to read host
+    memory: use a default event there."""
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        _check(lib().orbgpu_device_event_create(ctypes.byref(h)), "device_event_create")
+        self.cuda_event = h.value
+        self._lib = lib()
+
+    @staticmethod
+    def _stream(stream):
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream()
+        return stream.cuda_stream
+
+    def record(self, stream=None):
+        _check(lib().orbgpu_device_event_record(self.cuda_event, self._stream(stream)), "device_event_record")
+
+    def wait(self, stream=None):
+        _check(lib().orbgpu_stream_wait_device_event(self._stream(stream), self.cuda_event), "stream_wait_device_event")
+
+    def __del__(self):
+        try:
+            if self.cuda_event:
+                self._lib.orbgpu_device_event_destroy(self.cuda_event)
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
 
 
 class Extractor:
