@@ -131,3 +131,43 @@ def test_get_info_sized_writes_no_more_than_the_callers_struct():
     assert (info.nlevels, info.width, info.height) == (8, 640, 480)
     assert L.orbgpu_extractor_get_info_sized(ex.h, ctypes.cast(buf, ctypes.c_void_p),
                                              ctypes.c_size_t(0)) == orbgpu.ERR_ARG
+
+
+@pytest.mark.gpu
+def test_device_event_orders_two_streams():
+    """orbgpu.DeviceEvent (orbgpu_device_event_*: no system-scope fence) orders
+    a second stream behind a batch extraction on the first: the counts the
+    second stream copies after waiting on the event are the extraction's, and
+    the extractor's stage hook takes the event too."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import orbgpu
+    import synth
+    B = 16
+    frames = torch.from_numpy(np.ascontiguousarray(synth.mono_stream(B, 640, 480, seed=77))).cuda()
+    ex = orbgpu.Extractor(max_batch=B)
+    cap = ex.max_keypoints
+    kps = torch.zeros((B, cap, 7), dtype=torch.float32, device="cuda")
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
+    counts = torch.zeros(B, dtype=torch.int32, device="cuda")
+    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    ev, ev_fast = orbgpu.DeviceEvent(), orbgpu.DeviceEvent()
+    ex.set_stage_event("fast_cells", ev_fast)
+    out = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+    ref = []
+    for rep in range(3):
+        torch.cuda.synchronize()
+        counts.fill_(-5)
+        torch.cuda.synchronize()
+        ex.extract_batch(frames, kps, desc, counts, stream=a)
+        ev.record(a)
+        b.wait_event(ev)  # torch streams call event.wait(stream)
+        with torch.cuda.stream(b):
+            out.copy_(counts)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        assert (got > 0).all(), got
+        if rep == 0:
+            ref = got.copy()
+        assert (got == ref).all()
+    ex.set_stage_event("fast_cells", None)
