@@ -45,17 +45,22 @@ namespace {
 constexpr int kStThreads = 1024;
 constexpr int kStWaves = kStThreads / 64;
 
+// wave minimum, wave-uniform: 16-lane row minima on DPP (quad xor 1, xor 2,
+// half mirror, mirror: VALU lane moves), then the four row minima by readlane
+// (six ds_bpermute round trips before)
 __device__ __forceinline__ int wave_min(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
+    v = min(v, __builtin_amdgcn_mov_dpp(v, kDppXor1, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, kDppXor2, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, kDppHalfMirror, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, kDppMirror, 0xF, 0xF, false));
+    return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+               min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
 }
 
-// pixel (x, y) of level lvl of pair p's left (right = false) or right image
-__device__ __forceinline__ uint8_t px(const StereoArgs& a, int p, bool right, int lvl, int y, int x) {
-    const uint8_t* b = right ? a.lvl_base_r[lvl] : a.lvl_base[lvl];
-    return b[(size_t)p * a.lvl_pair[lvl] + (size_t)y * a.lvl_pitch[lvl] + x];
-}
+// the SAD windows of one left keypoint in its wave's LDS scratch: the left
+// 11x11 window and the right 11x21 band (rows iv-5..iv+5) as the aligned
+// dwords that hold them (left: 4 dwords a row, right: 7 in an 8-dword row)
+constexpr int kWinL = 16, kWinR = 32, kWinBytes = 11 * (kWinL + kWinR);
 
 __global__ __launch_bounds__(kStThreads) void stereo_kernel(StereoArgs a, int S) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_mem[];
@@ -70,7 +75,8 @@ __global__ __launch_bounds__(kStThreads) void stereo_kernel(StereoArgs a, int S)
     int* s_cur = s_cnt + (H + 1);                                        // H fill cursors
     uint16_t* s_ent = reinterpret_cast<uint16_t*>(s_cur + H);            // cap entries
     int* s_scr = reinterpret_cast<int*>(s_ent + ((cap + 1) & ~1));      // per wave 128 SAD partials
-    int* s_wsum = s_scr + kStWaves * 128;                                // row-scan wave totals
+    uint8_t* s_win = reinterpret_cast<uint8_t*>(s_scr + kStWaves * 128);  // per wave the SAD windows
+    int* s_wsum = reinterpret_cast<int*>(s_win + kStWaves * kWinBytes);   // row-scan wave totals
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const orbgpu_keypoint* kl = a.kps + (size_t)fl * cap;
     const orbgpu_keypoint* kr = a.kps + (size_t)fr * cap;
@@ -181,18 +187,44 @@ __global__ __launch_bounds__(kStThreads) void stereo_kernel(StereoArgs a, int S)
         const float iniu = __fadd_rn(sr, 0.0f), endu = __fadd_rn(sr, 11.0f);   // scaleduR0 + L - w, + L + w + 1
         if (iniu < 0.f || endu >= (float)lw) continue;                            // :668-671
         if (ir - 10 < 0) continue;                                                 // spec: IR inside the level
-        const int cL = px(a, p, false, lvl, iv, iu);
+        // the windows into LDS by aligned dword loads, 121 of them over the wave
+        // (24 byte loads per lane before: the address unit set the kernel's
+        // time); a dword is loaded only when it holds a window byte, so every
+        // load lies inside its row (pitches are multiples of 4)
+        uint8_t* wl = s_win + wave * kWinBytes;
+        uint8_t* wr = wl + 11 * kWinL;
+        {
+            const uint8_t* lb = a.lvl_base[lvl] + (size_t)p * a.lvl_pair[lvl];
+            const uint8_t* rb = a.lvl_base_r[lvl] + (size_t)p * a.lvl_pair[lvl];
+            const size_t pitch = (size_t)a.lvl_pitch[lvl];
+            const int lx0 = (iu - 5) & ~3, rx0 = (ir - 10) & ~3;
+            for (int t = lane; t < 121; t += 64) {
+                if (t < 44) {
+                    const int row = t >> 2, c = t & 3;
+                    if (lx0 + 4 * c <= iu + 5)
+                        *reinterpret_cast<uint32_t*>(wl + row * kWinL + 4 * c) =
+                            load4_a1(lb + (size_t)(iv - 5 + row) * pitch + lx0 + 4 * c);
+                } else {
+                    const int u = t - 44, row = u / 7, c = u - row * 7;
+                    if (rx0 + 4 * c <= ir + 10)
+                        *reinterpret_cast<uint32_t*>(wr + row * kWinR + 4 * c) =
+                            load4_a1(rb + (size_t)(iv - 5 + row) * pitch + rx0 + 4 * c);
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the windows are in LDS
+            __builtin_amdgcn_wave_barrier();
+            wl += (iu - 5) - lx0;  // byte 0 = column iu - 5 / ir - 10
+            wr += (ir - 10) - rx0;
+        }
+        const int cL = wl[5 * kWinL + 5];
         for (int c = lane; c < 121; c += 64) {
             const int inc = c / 11 - 5, rr = c - (c / 11) * 11;
-            const int y = iv - 5 + rr;
-            const int cR = px(a, p, true, lvl, iv, ir + inc);
+            const int cR = wr[5 * kWinR + inc + 10];
+            const uint8_t* lrow = wl + rr * kWinL;
+            const uint8_t* rrow = wr + rr * kWinR + inc + 5;
             int s = 0;
 #pragma unroll
-            for (int col = 0; col < 11; ++col) {
-                const int l = (int)px(a, p, false, lvl, y, iu - 5 + col) - cL;
-                const int rv = (int)px(a, p, true, lvl, y, ir + inc - 5 + col) - cR;
-                s += abs(l - rv);
-            }
+            for (int col = 0; col < 11; ++col) s += abs(((int)lrow[col] - cL) - ((int)rrow[col] - cR));
             scr[c] = s;
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's partials are in LDS
@@ -201,10 +233,10 @@ __global__ __launch_bounds__(kStThreads) void stereo_kernel(StereoArgs a, int S)
         if (lane < 11)
             for (int rr = 0; rr < 11; ++rr) dsum += scr[lane * 11 + rr];
         __builtin_amdgcn_wave_barrier();
-        // gather the 11 shift sums to every lane
+        // the 11 shift sums, wave-uniform (readlane: no LDS round trip)
         int dists[11];
 #pragma unroll
-        for (int j = 0; j < 11; ++j) dists[j] = __shfl(dsum, j, 64);
+        for (int j = 0; j < 11; ++j) dists[j] = __builtin_amdgcn_readlane(dsum, j);
         if (lane == 0) {
             int bestSad = 0x7FFFFFFF, bestInc = 0;
 #pragma unroll
@@ -298,7 +330,7 @@ __global__ __launch_bounds__(kMedThreads) void stereo_median_kernel(StereoArgs a
 
 size_t stereo_lds_bytes(int cap, int H) {
     return (size_t)cap * 16 + (size_t)(2 * H + 1) * 4 + (size_t)((cap + 1) & ~1) * 2 + (size_t)kStWaves * 128 * 4 +
-           (kStWaves + 4) * 4;
+           (size_t)kStWaves * kWinBytes + (kStWaves + 4) * 4;
 }
 
 // blocks per pair at most (ORBGPU_STEREO_SPLIT_MAX overrides): a single pair
@@ -315,6 +347,11 @@ int stereo_split_max() {
 
 hipError_t launch_stereo(const StereoArgs& a, int npairs, hipStream_t stream) {
     if (npairs <= 0) return hipSuccess;
+    // the SAD windows are staged by aligned dword loads: 4-byte aligned rows
+    for (int l = 0; l < kMaxLevels; ++l)
+        if (a.lvl_base[l] && ((((uintptr_t)a.lvl_base[l] | (uintptr_t)a.lvl_base_r[l] | a.lvl_pair[l]) & 3) ||
+                              (a.lvl_pitch[l] & 3)))
+            return hipErrorInvalidValue;
     const size_t lds = stereo_lds_bytes(a.cap, a.lvl_h[0]);
     // per-device state (device_state.h; the drop-in calls this per frame, from
     // any thread, on any device): the kernel's LDS limit only grows, the CU
