@@ -47,5 +47,6 @@ lib.orbgpu_debug_desc_stamps(st.ctypes.data, 0)
 n = max(int(st[15]), 1)
 out["describe"] = {"sampled_waves": n, "key_ref_cycles": float(st[0]) / n,
                    "stage_moments_blur_cycles": float(st[1]) / n, "orientation_cycles": float(st[2]) / n,
-                   "tests_store_cycles": float(st[3]) / n}
+                   "tests_store_cycles": float(st[3]) / n,
+                   "raw_phase_means": [round(float(st[k]) / n, 1) for k in range(8)]}
 print(json.dumps(out, indent=1))
