@@ -188,63 +188,6 @@ constexpr int kRawWords = kPatch * (kRWidth / 4);   // 43 rows x 12 dwords
 constexpr int kQuads = kBPitch / 4;                 // 10 output quads per blurred row
 constexpr int kColChunks = (kBlur + 6) / 7;         // 6 chunks of <= 7 blurred rows
 
-// The blur of a patch on the matrix cores (ORBGPU_DESC_MFMA, default on): the
-// two passes of the separable 7x7 kernel as two exact matrix products.
-//   row pass   R = P x Tr on v_mfma_i32_16x16x64_i8: P the raw 48x48 patch
-//              (rows 43..47 and columns 48..63 are never weighted), Tr[c][x]
-//              = t[c - x - 1] the banded tap matrix; bytes enter as p - 128
-//              (staged xor 0x80) and the accumulator starts at 128 x 257 (the taps'
-//              sum), so R is the integer row sum (<= 255 * 257 < 2^16)
-//   column pass  Out^T = R^T x Tc^T on v_mfma_f32_16x16x32_f16: R's low and
-//              high bytes as two k-slots each, entering as f16 subnormals (a
-//              byte b in the low bits of an f16 is b * 2^-24: one v_perm per
-//              two values), Tc's taps scaled 4 (low byte) and 1024 (high byte);
-//              every product and partial sum is a multiple of 2^-22 below 4
-//              unless the total is (then the result saturates to 255 either
-//              way), so the f32 accumulator is exact and 64x it is the blurred
-//              value in grey levels (x 2^-16 of the two passes' fixed point):
-//              v_cvt_pk_u8_f32 rounds half to even, the SIMD-path rounding of
-//              blur_device.h.
-// The row pass's output tile (rows on the lane's 4 registers, a column per
-// lane) is the column pass's A fragment as it stands: no lane movement, no
-// LDS round trip.  Tap matrices: c_blur_mfma (per-lane fragments; both are
-// Toeplitz, so the column pass needs only the diagonal and upper blocks).
-#ifndef ORBGPU_DESC_MFMA
-#define ORBGPU_DESC_MFMA 1
-#endif
-constexpr int kTap[7] = {18, 34, 49, 55, 49, 34, 18};
-constexpr uint32_t f16_bits_of_int(int v) {  // an integer below 65504 with <= 11 significant bits
-    int e = 0;
-    while ((v >> (e + 1)) != 0) ++e;
-    const uint32_t m = e >= 10 ? (uint32_t)(v >> (e - 10)) : (uint32_t)(v << (10 - e));
-    return (uint32_t)((e + 15) << 10) | (m & 0x3FFu);
-}
-struct BlurMfmaTab {
-    uint32_t row[3][64][4];  // i8 B fragment of output-column tile nt: byte j of lane (g, c) = Tr[16g + j][16nt + c]
-    uint32_t col[2][64][4];  // f16 B fragment, k-step s = ny + d: element j of lane (g, c) = the tap of
-                             // R row 16s + 4g + (j & 3) for output row 16ny + c, (j >> 2) ? high byte : low byte
-};
-constexpr BlurMfmaTab make_blur_mfma_tab() {
-    BlurMfmaTab T{};
-    for (int l = 0; l < 64; ++l) {
-        const int g = l >> 4, c = l & 15;
-        for (int nt = 0; nt < 3; ++nt)
-            for (int j = 0; j < 16; ++j) {
-                const int d = 16 * g + j - (16 * nt + c) - 1;
-                if (d >= 0 && d <= 6) T.row[nt][l][j / 4] |= (uint32_t)kTap[d] << (8 * (j % 4));
-            }
-        for (int dd = 0; dd < 2; ++dd)
-            for (int j = 0; j < 8; ++j) {
-                const int d = 16 * dd + 4 * g + (j & 3) - c;
-                if (d >= 0 && d <= 6)
-                    T.col[dd][l][j / 2] |= f16_bits_of_int(kTap[d] * ((j >> 2) ? 1024 : 4)) << (16 * (j % 2));
-            }
-    }
-    return T;
-}
-__constant__ BlurMfmaTab c_blur_mfma = make_blur_mfma_tab();
-static_assert(kRPitchC == 48 && kBPitch == 40 && kPatch <= 48 && kBlur <= 48, "the MFMA blur's tiling");
-
 // The waves of a block process different keypoints in LDS regions of their
 // own: stages are ordered within the wave, never with a block barrier.  A
 // wave's DS instructions execute in order, so only the compiler must keep
@@ -292,102 +235,6 @@ struct alignas(16) DescLds {
 };
 static_assert(offsetof(DescLds, blur) % 16 == 0 && kBlurSlotBytes % 16 == 0, "16-byte dump stores into blur[k]");
 
-#if ORBGPU_DESC_MFMA
-typedef int mi32x4 __attribute__((ext_vector_type(4)));
-typedef float mf32x4 __attribute__((ext_vector_type(4)));
-typedef _Float16 mf16x8 __attribute__((ext_vector_type(8)));
-
-// The blurred patch (blur_out, 37 rows of kBPitch) of the raw patch staged at
-// rawbuf (the wave's buffer: rows of 48 bytes followed by its blur slots, so
-// the never-weighted rows 43..47 and columns 48..63 read inside it), on the
-// matrix cores (see c_blur_mfma).  Every patch column is on the SIMD path.
-// tail_x: the first patch column on the scalar path of the level (x >= 4 *
-// floor(w / 4), FixedPtCastEx: half up), >= 40 when there is none.
-// this lane's tap fragments (uniform table base + 32-bit lane offset), loaded
-// where the wave's disc-table loads are (their latency under the moments)
-struct BlurTabs {
-    mi32x4 row[3];
-    mf16x8 col[2];
-};
-__device__ inline BlurTabs load_blur_tabs(int lane) {
-    typedef const __attribute__((address_space(1))) mi32x4* TabPtr;
-    const __attribute__((address_space(1))) uint8_t* tab =
-        (const __attribute__((address_space(1))) uint8_t*)&c_blur_mfma.row[0][0][0] + 16u * (uint32_t)lane;
-    BlurTabs T;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) T.row[k] = *(TabPtr)(tab + 1024 * k);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) T.col[k] = __builtin_bit_cast(mf16x8, *(TabPtr)(tab + 1024 * (3 + k)));
-    return T;
-}
-
-#ifndef ORBGPU_DESC_TILE_SCHED
-#define ORBGPU_DESC_TILE_SCHED 0
-#endif
-template <bool kTail>
-__device__ inline void blur_mfma(const uint8_t* rawbuf, uint8_t* blur_out, int lane, int tail_x, const BlurTabs& T) {
-    const int g = lane >> 4, c = lane & 15;
-    const mf16x8 b2d0 = T.col[0], b2d1 = T.col[1];
-    const mi32x4 c1 = {128 * 257, 128 * 257, 128 * 257, 128 * 257};  // 128 x the taps' sum
-    const bool col_ok = 4 * g < kBPitch - 32;  // the last column tile's quads inside the pitch
-#pragma unroll
-    for (int mx = 0; mx < 3; ++mx) {
-        // one column tile at a time (no scheduling across tiles: register pressure),
-        // but for the LDS reads (ORBGPU_DESC_TILE_SCHED: the mask of what may cross)
-        __builtin_amdgcn_sched_barrier(ORBGPU_DESC_TILE_SCHED);
-        const mi32x4 b1 = T.row[mx];
-        // R rows 16 s + 4 g + r (register r), column 16 mx + c, as the column pass's A fragment:
-        // (low byte r0, low r1), (low r2, low r3), (high r0, high r1), (high r2, high r3)
-        auto row_tile = [&](int s) {
-            // row-pass A fragment: raw row 16 s + c, bytes 16 g .. 16 g + 15 (p - 128), re-read
-            // per column tile (LDS reads, no registers held across the tiles)
-            const mi32x4 a1 = *reinterpret_cast<const mi32x4*>(rawbuf + (16 * s + c) * kRPitch + 16 * g);
-            const mi32x4 d = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, b1, c1, 0, 0, 0);
-            const mi32x4 p = {(int)__builtin_amdgcn_perm((uint32_t)d.y, (uint32_t)d.x, 0x0c040c00u),
-                              (int)__builtin_amdgcn_perm((uint32_t)d.w, (uint32_t)d.z, 0x0c040c00u),
-                              (int)__builtin_amdgcn_perm((uint32_t)d.y, (uint32_t)d.x, 0x0c050c01u),
-                              (int)__builtin_amdgcn_perm((uint32_t)d.w, (uint32_t)d.z, 0x0c050c01u)};
-            return __builtin_bit_cast(mf16x8, p);
-        };
-        // output rows 16 ny + c, columns 16 mx + 4 g .. + 3 (register r): the sum over k-steps
-        // s = ny (diagonal taps) and s = ny + 1 (the taps below)
-        auto out_tile = [&](int ny, mf16x8 a_diag, const mf16x8* a_next) {
-            mf32x4 acc = {0.f, 0.f, 0.f, 0.f};
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_diag, b2d0, acc, 0, 0, 0);
-            if (a_next) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(*a_next, b2d1, acc, 0, 0, 0);
-            typedef float f2 __attribute__((ext_vector_type(2)));
-            const f2 k64 = {64.f, 64.f};
-            const f2 lo = f2{acc.x, acc.y} * k64, hi = f2{acc.z, acc.w} * k64;  // exact: powers of two
-            uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(lo.x, 0, 0u);
-            q = __builtin_amdgcn_cvt_pk_u8_f32(lo.y, 1, q);
-            q = __builtin_amdgcn_cvt_pk_u8_f32(hi.x, 2, q);
-            q = __builtin_amdgcn_cvt_pk_u8_f32(hi.y, 3, q);
-            if (kTail) {  // a level's right edge: the tail columns (x >= tail_x) round half up
-                // byte masks from the sign of tail_x - 1 - x (arithmetic, no compares)
-                const int x = 16 * mx + 4 * g;
-                const uint32_t t = blurdev::pack4(lo, hi, false);
-                const uint32_t m = ((uint32_t)((tail_x - 1 - x) >> 31) & 0x000000FFu) |
-                                   ((uint32_t)((tail_x - 2 - x) >> 31) & 0x0000FF00u) |
-                                   ((uint32_t)((tail_x - 3 - x) >> 31) & 0x00FF0000u) |
-                                   ((uint32_t)((tail_x - 4 - x) >> 31) & 0xFF000000u);
-                q = (q & ~m) | (t & m);
-            }
-            if ((ny < 2 || c < kBlur - 32) && (mx < 2 || col_ok))
-                *reinterpret_cast<uint32_t*>(blur_out + (16 * ny + c) * kBPitch + 16 * mx + 4 * g) = q;
-        };
-        // in the order that keeps two A fragments live
-        const mf16x8 r0 = row_tile(0), r1 = row_tile(1);
-        out_tile(0, r0, &r1);
-        const mf16x8 r2 = row_tile(2);
-        out_tile(1, r1, &r2);
-        out_tile(2, r2, nullptr);
-    }
-}
-#else
-struct BlurTabs {};
-__device__ inline BlurTabs load_blur_tabs(int) { return BlurTabs{}; }
-#endif
-
 // A keypoint slot of a frame: its level, index within the level and output
 // position; false when the slot is past the level's octree count.
 struct KeyRef {
@@ -433,102 +280,70 @@ __device__ bool key_ref(const Geom& g, int f, int slot, int lane, const uint32_t
     return true;
 }
 
-// Where a keypoint's level lives: the frame's level 0 (the input) or its
-// pyramid level, and the row pitch.
-struct PatchSrc {
-    const uint8_t* raw;
-    size_t rp;
-};
-__device__ inline PatchSrc patch_src(const Geom& g, int f, int l, const uint8_t* __restrict__ img0, size_t row0,
-                                     size_t frame0, const uint8_t* __restrict__ pyr) {
+// Stage the neighbourhood, IC_Angle's moments, the blurred patch into S.blur;
+// returns (m10, m01), wave-uniform.
+// rawbuf: the wave's raw-neighbourhood buffer (kPatch rows of kRPitch bytes).
+__device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, uint8_t* rawbuf, uint8_t* blur_out,
+                               const uint8_t* __restrict__ img0, size_t row0, size_t frame0,
+                               const uint8_t* __restrict__ pyr) {
+    const int l = K.l, cx = K.cx, cy = K.cy;
     const LevelGeom& L = g.lv[l];
 #ifdef DESC_PROBE_SAMEFRAME
     // latency probe (diagnostic build only; wrong results): every keypoint's
     // neighbourhood comes from frame 0's level 0 (L2-resident)
-    (void)f;
+    const uint8_t* raw = img0;
+    const size_t rp = row0;
     (void)frame0;
-    (void)L;
-    (void)pyr;
-    return PatchSrc{img0, row0};
 #else
-    return l == 0 ? PatchSrc{img0 + (size_t)f * frame0, row0}
-                  : PatchSrc{pyr + L.offset + (size_t)f * L.frame_bytes, (size_t)L.pitch};
+    const uint8_t* raw = l == 0 ? img0 + (size_t)f * frame0 : pyr + L.offset + (size_t)f * L.frame_bytes;
+    const size_t rp = l == 0 ? row0 : (size_t)L.pitch;
 #endif
-}
 
-// Staging of the raw neighbourhood: rows cy-21 .. cy+21, columns xb-4 ..
-// xb+43 (xb = the blurred patch's 4-aligned first column), reflected at the
-// level border (BORDER_REFLECT_101 of GaussianBlur on the level clone,
-// ORBextractor.cpp:1097-1098).  Dwords inside the level are one load each; a
-// dword that crosses the border is assembled from reflected bytes.  All loads
-// of a lane are issued before any is stored.
-//
-// A neighbourhood entirely inside the level (wave-uniform; most keypoints):
-// three 16-byte chunks per row, no reflection.
-__device__ inline bool patch_interior(const LevelGeom& L, int cx, int cy) {
-    const int x0 = ((cx - kBlurR) & ~3) - 4;
-    return x0 >= 0 && x0 + kRWidth <= L.w && cy - kPatchR >= 0 && cy + kPatchR < L.h;
-}
-
-// the interior neighbourhood's loads (issued, not waited for): chunk k of the
-// lane is chunk idx = lane + 64 k of the patch, row idx / 3
-__device__ inline void stage_interior_issue(PatchSrc src, int cx, int cy, int lane, uint4 (&c)[3]) {
-    const int x0 = ((cx - kBlurR) & ~3) - 4;
-    const uint8_t* top = src.raw + (size_t)(cy - kPatchR) * src.rp + x0;
-    // r = idx / 3 by a 24-bit multiply (exact for idx < 4096), row offsets
-    // by 24-bit multiplies (rp < 2^24: launcher check), unsigned 32-bit
-    // offsets (no sign extension); lanes past the patch load its last row
+    // 1. Stage the raw neighbourhood: rows cy-21 .. cy+21, columns xb-4 ..
+    // xb+43 (xb = the blurred patch's 4-aligned first column), reflected at
+    // the level border (BORDER_REFLECT_101 of GaussianBlur on the level
+    // clone, ORBextractor.cpp:1097-1098).  Dwords inside the level are one
+    // load each; a dword that crosses the border is assembled from reflected
+    // bytes.  All loads of a lane are issued before any is stored.
+    const int xb = (cx - kBlurR) & ~3, x0 = xb - 4;
+    // a neighbourhood entirely inside the level (wave-uniform; most keypoints): three
+    // 16-byte chunks per row, two loads per lane, no reflection
+    if (x0 >= 0 && x0 + kRWidth <= L.w && cy - kPatchR >= 0 && cy + kPatchR < L.h) {
+        constexpr int kChunks = kPatch * (kRWidth / 16);  // 129
+        const uint8_t* top = raw + (size_t)(cy - kPatchR) * rp + x0;
+        uint4 c[3];
+        uint8_t* dst[3];
+        // the dump for lanes past the patch: this keypoint's blurred patch,
+        // written only after this staging
+        uint8_t* const dump = blur_out;
+        // r = idx / 3 by a 24-bit multiply (exact for idx < 4096), row offsets
+        // by 24-bit multiplies (rp < 2^24: launcher check), unsigned 32-bit
+        // offsets (no sign extension); lanes past the patch load its last row
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const uint32_t idx = (uint32_t)(lane + 64 * k), r = __umul24(idx, 21846u) >> 16, q = idx - 3u * r;
-        c[k] = load16_a4(top + (__umul24(min(r, (uint32_t)kPatch - 1u), (uint32_t)src.rp) + 16u * q));
-    }
-}
-
-// The staged patch holds p - 128 as signed bytes (xor 0x80) in the MFMA build:
-// the row pass's A operand as it stands; IC_Angle's moments are the same
-// with signed dot products (the disc is symmetric: the -128 terms of Σc·p -
-// (od+15)Σp and Σ(v+15)·p - 15Σp cancel).
-#if ORBGPU_DESC_MFMA
-constexpr uint32_t kStageBias = 0x80808080u;
-#else
-constexpr uint32_t kStageBias = 0u;
-#endif
-__device__ inline uint4 stage_bias(uint4 v) {
-    return kStageBias ? make_uint4(v.x ^ kStageBias, v.y ^ kStageBias, v.z ^ kStageBias, v.w ^ kStageBias) : v;
-}
-
-// ... and their LDS stores; lanes past the patch dump their chunk into `dump`
-// (the keypoint's blurred patch, written only after this staging)
-__device__ inline void stage_interior_store(const uint4 (&c)[3], uint8_t* rawbuf, uint8_t* dump, int lane) {
-    constexpr int kChunks = kPatch * (kRWidth / 16);  // 129
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const uint32_t idx = (uint32_t)(lane + 64 * k), r = __umul24(idx, 21846u) >> 16, q = idx - 3u * r;
-        // chunk (r, q) at r * 48 + 16 q = 16 idx when the row pitch is 48 (three
-        // chunks a row): no per-chunk multiply; chunks 0..127 (k = 0, 1) always
-        // exist, so only k = 2 selects the dump (VALU-bound kernel: round 6)
-        const uint32_t doff = kRPitch == 48 ? 16u * idx : __umul24(r, (uint32_t)kRPitch) + 16u * q;
-        uint8_t* dst = (k < 2 && 64 * 2 <= kChunks) || idx < (uint32_t)kChunks ? rawbuf + doff : dump;
-        // unconditional stores (lanes past the patch write into the dump): no
-        // branch the loads could be sunk into
-        if constexpr (kRPitch % 16 == 0) {
-            *reinterpret_cast<uint4*>(dst) = stage_bias(c[k]);
-        } else {
-            uint32_t* d = reinterpret_cast<uint32_t*>(dst);
-            d[0] = c[k].x;
-            d[1] = c[k].y;
-            d[2] = c[k].z;
-            d[3] = c[k].w;
+        for (int k = 0; k < 3; ++k) {
+            const uint32_t idx = (uint32_t)(lane + 64 * k), r = __umul24(idx, 21846u) >> 16, q = idx - 3u * r;
+            // chunk (r, q) at r * 48 + 16 q = 16 idx when the row pitch is 48 (three
+            // chunks a row): no per-chunk multiply; chunks 0..127 (k = 0, 1) always
+            // exist, so only k = 2 selects the dump (VALU-bound kernel: round 6)
+            const uint32_t doff = kRPitch == 48 ? 16u * idx : __umul24(r, (uint32_t)kRPitch) + 16u * q;
+            dst[k] = (k < 2 && 64 * 2 <= kChunks) || idx < (uint32_t)kChunks ? rawbuf + doff : dump;
+            c[k] = load16_a4(top + (__umul24(min(r, (uint32_t)kPatch - 1u), (uint32_t)rp) + 16u * q));
         }
-    }
-}
-
-// a neighbourhood at the level border: dword loads, reflected bytes
-__device__ inline void stage_generic(const LevelGeom& L, PatchSrc src, int cx, int cy, int lane, uint8_t* rawbuf) {
-    const uint8_t* raw = src.raw;
-    const size_t rp = src.rp;
-    const int x0 = ((cx - kBlurR) & ~3) - 4;
+        // unconditional stores (lanes past the patch write into kDump): no
+        // branch the loads could be sunk into
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if constexpr (kRPitch % 16 == 0) {
+                *reinterpret_cast<uint4*>(dst[k]) = c[k];
+            } else {
+                uint32_t* d = reinterpret_cast<uint32_t*>(dst[k]);
+                d[0] = c[k].x;
+                d[1] = c[k].y;
+                d[2] = c[k].z;
+                d[3] = c[k].w;
+            }
+        }
+    } else {
     constexpr int kLoads = (kRawWords + 63) / 64;
     uint32_t v[kLoads];
 #pragma unroll
@@ -547,70 +362,47 @@ __device__ inline void stage_generic(const LevelGeom& L, PatchSrc src, int cx, i
 #pragma unroll
     for (int k = 0; k < kLoads; ++k) {
         const int idx = lane + 64 * k, r = idx / 12, q = idx - r * 12;
-        if (idx < kRawWords) reinterpret_cast<uint32_t*>(rawbuf)[r * (kRPitch / 4) + q] = v[k] ^ kStageBias;
+        if (idx < kRawWords) reinterpret_cast<uint32_t*>(rawbuf)[r * (kRPitch / 4) + q] = v[k];
     }
-}
+    }
+    wave_sync();
 
-// IC_Angle's disc table entries for this lane (c_disc, c_disc_tail)
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-struct DiscRegs {
-    u32x4 t[kDiscLoads];
-};
-__device__ inline DiscRegs disc_load(int cx, int lane) {
-    const int od = cx - 15 - ((cx - 15) & ~3);
+    // 2. Intensity centroid (IC_Angle, ORBextractor.cpp:79-106) from the raw
+    // patch: per disc word (c_disc: offset and byte weights for this od)
+    // three v_dot4_u32_u8 accumulate Σp, Σc·p and Σ(v+15)·p; then
+    // m10 = Σc·p - (od+15)Σp, m01 = Σ(v+15)·p - 15Σp.  Integer moments:
+    // order-free, exact.
+    const int xd = (cx - 15) & ~3, od = cx - 15 - xd;
+    const uint8_t* disc = rawbuf + (kPatchR - 15) * kRPitch + (xd - x0);
+    uint32_t sp = 0u, cp = 0u, vp = 0u;
     // uniform table bases + 32-bit lane offset: saddr loads, no per-load
     // 64-bit address arithmetic
     const __attribute__((address_space(1))) uint8_t* dtab =
         (const __attribute__((address_space(1))) uint8_t*)&c_disc.w[od][0];
     const __attribute__((address_space(1))) uint8_t* dtab4 =
         (const __attribute__((address_space(1))) uint8_t*)&c_disc_tail.w[od][0];
-    DiscRegs D;
-#pragma unroll
-    for (int k = 0; k < kDiscLoads; ++k)
-        D.t[k] = *(const __attribute__((address_space(1))) u32x4*)((k < 4 ? dtab : dtab4) + 16u * (uint32_t)lane +
-                                                                   1024u * (k % 4));
-    return D;
-}
-
-// Intensity centroid (IC_Angle, ORBextractor.cpp:79-106) from the staged raw
-// patch: per disc word (c_disc: offset and byte weights for this od) three
-// v_dot4_u32_u8 accumulate Σp, Σc·p and Σ(v+15)·p; then m10 = Σc·p -
-// (od+15)Σp, m01 = Σ(v+15)·p - 15Σp.  Integer moments: order-free, exact.
-// Returns (m10, m01), wave-uniform.
-__device__ inline int2 patch_moments(const DiscRegs& D, const uint8_t* rawbuf, int cx, int lane) {
-    const int x0 = ((cx - kBlurR) & ~3) - 4;
-    const int xd = (cx - 15) & ~3, od = cx - 15 - xd;
-    const uint8_t* disc = rawbuf + (kPatchR - 15) * kRPitch + (xd - x0);
-    uint32_t sp = 0u, cp = 0u, vp = 0u;
 #pragma unroll
     for (int k = 0; k < kDiscLoads; ++k) {
-        const DiscWord e{D.t[k].x, D.t[k].y, D.t[k].z, D.t[k].w};
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 t = *(const __attribute__((address_space(1))) u32x4*)((k < 4 ? dtab : dtab4) + 16u * (uint32_t)lane +
+                                                                          1024u * (k % 4));
+        const DiscWord e{t.x, t.y, t.z, t.w};
 #if DESC_LDS_PROBE & 4
         const uint32_t w = *reinterpret_cast<const uint32_t*>(rawbuf + 4 * lane + 256 * k + (e.off & 0));
 #else
         const uint32_t w = *reinterpret_cast<const uint32_t*>(disc + e.off);
 #endif
-#if ORBGPU_DESC_MFMA
-        sp = (uint32_t)__builtin_amdgcn_sdot4((int)w, (int)e.m1, (int)sp, false);
-        cp = (uint32_t)__builtin_amdgcn_sdot4((int)w, (int)e.mc, (int)cp, false);
-        vp = (uint32_t)__builtin_amdgcn_sdot4((int)w, (int)e.mv, (int)vp, false);
-#else
         sp = __builtin_amdgcn_udot4(w, e.m1, sp, false);
         cp = __builtin_amdgcn_udot4(w, e.mc, cp, false);
         vp = __builtin_amdgcn_udot4(w, e.mv, vp, false);
-#endif
     }
-    // wave totals now (scalars): the blur then has every VGPR (the per-lane
-    // combinations first: two wave totals instead of three; modulo-2^32 sums,
-    // exact since the totals fit)
-    return int2{(int)wave_total(cp - (uint32_t)(od + 15) * sp), (int)wave_total(vp - 15u * sp)};
-}
+    // wave totals now (scalars): the blur below then has every VGPR
+    // (the per-lane combinations first: two wave totals instead of three;
+    // modulo-2^32 sums, exact since the totals fit)
+    const int m10 = (int)wave_total(cp - (uint32_t)(od + 15) * sp);
+    const int m01 = (int)wave_total(vp - 15u * sp);
 
-// The blurred 37x37 patch into blur_out from the staged raw patch.
-__device__ inline void blur_patch(const LevelGeom& L, int cx, int lane, const uint8_t* rawbuf, uint8_t* blur_out,
-                                  const BlurTabs& tabs) {
-    const int xb = (cx - kBlurR) & ~3;
-    // Blur (blur_device.h, the arithmetic of blur.hip) of the 37x37 patch:
+    // 3. Blur (blur_device.h, the arithmetic of blur.hip) of the 37x37 patch:
     // lane = (output quad q, chunk c of 7 blurred rows); row passes from the
     // raw patch in LDS, the column pass in registers, rounding per path (quad
     // columns x < 4*floor(w/4): the SIMD path).  No intermediate array, no
@@ -676,43 +468,11 @@ __device__ inline void blur_patch(const LevelGeom& L, int cx, int lane, const ui
             }
         }
     };
-#if ORBGPU_DESC_MFMA
-    // every patch on the matrix cores, the right-edge ones with their tail rounding
-    (void)passes;
-    const int tail_x = __builtin_amdgcn_readfirstlane(simd_end - xb);
-    if (tail_x < kBPitch)
-        blur_mfma<true>(rawbuf, blur_out, lane, tail_x, tabs);
-    else
-        blur_mfma<false>(rawbuf, blur_out, lane, tail_x, tabs);
-#else
     if (xb + 4 * (kQuads - 1) < simd_end)
         passes(std::true_type{});
     else
         passes(std::false_type{});
-#endif
-}
-
-// Stage the neighbourhood, IC_Angle's moments, the blurred patch into
-// blur_out; returns (m10, m01), wave-uniform.  rawbuf: the wave's
-// raw-neighbourhood buffer (kPatch rows of kRPitch bytes).
-__device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, uint8_t* rawbuf, uint8_t* blur_out,
-                               const uint8_t* __restrict__ img0, size_t row0, size_t frame0,
-                               const uint8_t* __restrict__ pyr) {
-    const LevelGeom& L = g.lv[K.l];
-    const PatchSrc src = patch_src(g, f, K.l, img0, row0, frame0, pyr);
-    if (patch_interior(L, K.cx, K.cy)) {
-        uint4 c[3];
-        stage_interior_issue(src, K.cx, K.cy, lane, c);
-        stage_interior_store(c, rawbuf, blur_out, lane);
-    } else {
-        stage_generic(L, src, K.cx, K.cy, lane, rawbuf);
-    }
-    wave_sync();
-    const DiscRegs D = disc_load(K.cx, lane);
-    const BlurTabs tabs = load_blur_tabs(lane);
-    const int2 mm = patch_moments(D, rawbuf, K.cx, lane);
-    blur_patch(L, K.cx, lane, rawbuf, blur_out, tabs);
-    return mm;
+    return int2{m10, m01};
 }
 
 // rBRIEF (computeOrbDescriptor, ORBextractor.cpp:110-149) on the blurred
@@ -799,15 +559,7 @@ constexpr int kDescWaves = ORBGPU_DESC_WAVES;
 // One wave per (frame, slot) item, kDescWaves items per block.  Blocks are
 // XCD-swizzled so one frame's keypoints (whose neighbourhoods overlap) are
 // described on one XCD and its level rows are fetched into one L2.
-#ifndef ORBGPU_DESC_MIN_WAVES
-#define ORBGPU_DESC_MIN_WAVES 0
-#endif
-#if ORBGPU_DESC_MIN_WAVES
-#define DESC_BOUNDS __launch_bounds__(64 * kDescWaves) __attribute__((amdgpu_waves_per_eu(ORBGPU_DESC_MIN_WAVES)))
-#else
-#define DESC_BOUNDS __launch_bounds__(64 * kDescWaves)
-#endif
-__global__ DESC_BOUNDS void describe_kernel(Geom g, int items, int f0,
+__global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int items, int f0,
                                                                    const uint8_t* __restrict__ img0, size_t row0,
                                                                    size_t frame0, const uint8_t* __restrict__ pyr,
                                                                    const uint32_t* __restrict__ oct_out,
@@ -916,140 +668,6 @@ __global__ DESC_BOUNDS void describe_kernel(Geom g, int items, int f0,
 #endif
 }
 
-// Keypoint slots per wave in the grouped kernel (ORBGPU_DESC_GROUP > 1): a
-// wave takes kDescGroup consecutive slots, issues all their key loads, then
-// all their neighbourhood loads, and describes them one after the other --
-// one memory round trip of staging latency per group instead of per slot
-// (with the blur on the matrix cores the VALU work left no longer covers one
-// per slot).  The later slots' staged chunks wait in registers.
-#ifndef ORBGPU_DESC_GROUP
-#define ORBGPU_DESC_GROUP 2
-#endif
-constexpr int kDescGroup = ORBGPU_DESC_GROUP;
-static_assert(kDescGroup == 1 || kKeysPerWave == 1, "the grouped kernel takes one keypoint at a time");
-
-// a slot's key loads (issued; key_decode waits for them)
-struct KeyLoad {
-    uint32_t se, key;
-    int c;
-};
-__device__ inline KeyLoad key_load(const Geom& g, int f, int slot, int lane, const uint32_t* __restrict__ oct_out,
-                                   const int* __restrict__ oct_count) {
-    KeyLoad r;
-    r.se = g.slot_tab[slot];
-    r.key = oct_out[(size_t)f * g.slots_frame + slot];
-    r.c = oct_count[(size_t)f * kOcStride + (lane & 15)];
-    return r;
-}
-// key_ref's decoding of the loaded values
-__device__ inline bool key_decode(const Geom& g, int f, int slot, int lane, const KeyLoad& r, int* __restrict__ counts,
-                                  KeyRef& K) {
-    const uint32_t se = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.se);
-    const uint32_t key = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.key);
-    const int ll = lane & 15;
-    const int c = ll < g.nlevels ? r.c : 0;
-    const int l = (int)(se & 15u), i = (int)(se >> 4);
-    int sc = c;
-    sc += __builtin_amdgcn_update_dpp(0, sc, 0x111, 0xF, 0xF, true);  // row_shr:1
-    sc += __builtin_amdgcn_update_dpp(0, sc, 0x112, 0xF, 0xF, true);  // row_shr:2
-    sc += __builtin_amdgcn_update_dpp(0, sc, 0x114, 0xF, 0xF, true);  // row_shr:4
-    sc += __builtin_amdgcn_update_dpp(0, sc, 0x118, 0xF, 0xF, true);  // row_shr:8
-    const int mine = __builtin_amdgcn_readlane(c, l);
-    const int before = __builtin_amdgcn_readlane(sc, l) - mine;
-    if (slot == 0 && lane == 0) counts[f] = __builtin_amdgcn_readlane(sc, 15);
-    if (i >= mine) return false;
-    K.l = l;
-    K.i = i;
-    K.before = before;
-    K.key = key;
-    K.cx = key_x(key) + kBorder;
-    K.cy = key_y(key) + kBorder;
-    return true;
-}
-
-__global__ DESC_BOUNDS void describe_group_kernel(Geom g, int slots, int f0, const uint8_t* __restrict__ img0,
-                                                  size_t row0, size_t frame0, const uint8_t* __restrict__ pyr,
-                                                  const uint32_t* __restrict__ oct_out,
-                                                  const int* __restrict__ oct_count, orbgpu_keypoint* __restrict__ kps,
-                                                  uint8_t* __restrict__ desc, int* __restrict__ counts, int kp_cap,
-                                                  int* __restrict__ err_word, int* __restrict__ err_copy) {
-    __shared__ DescLds s_lds[kDescWaves];
-    if (err_copy && blockIdx.x == 0 && threadIdx.x == 0) *err_copy = atomicExch(err_word, 0);
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if ORBGPU_DESC_SWIZZLE
-    const int blk = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
-#else
-    const int blk = (int)blockIdx.x;
-#endif
-    const int s0 = (blk * kDescWaves + wave) * kDescGroup;  // flat slots s0 .. s0 + kDescGroup - 1 (frame-major)
-    if (s0 >= slots) return;
-#ifdef DESC_STAMPS
-    // phases of the group's first slot: keys + staging issued, staged, moments, blur, orientation, tests
-    const bool stamp_on = ((s0 / kDescGroup) & 63) == 0;
-    unsigned long long ts[8] = {};
-#endif
-    DSTAMP(0);
-    uint8_t* const rawbuf = s_lds[wave].raw;
-    uint8_t* const blur_out = s_lds[wave].blur[0];
-    int f[kDescGroup], slot[kDescGroup];
-    KeyLoad kl[kDescGroup];
-#pragma unroll
-    for (int k = 0; k < kDescGroup; ++k) {
-        const int it = min(s0 + k, slots - 1), fi = it / g.slots_frame;
-        f[k] = f0 + fi;
-        slot[k] = it - fi * g.slots_frame;
-        kl[k] = key_load(g, f[k], slot[k], lane, oct_out, oct_count);
-    }
-    KeyRef K[kDescGroup];
-    bool valid[kDescGroup], pre[kDescGroup];
-    uint4 c[kDescGroup][3];
-#pragma unroll
-    for (int k = 0; k < kDescGroup; ++k) {
-        valid[k] = s0 + k < slots && key_decode(g, f[k], slot[k], lane, kl[k], counts, K[k]);
-        pre[k] = valid[k] && patch_interior(g.lv[K[k].l], K[k].cx, K[k].cy);
-        if (pre[k])
-            stage_interior_issue(patch_src(g, f[k], K[k].l, img0, row0, frame0, pyr), K[k].cx, K[k].cy, lane, c[k]);
-    }
-    DSTAMP(1);
-#pragma unroll
-    for (int k = 0; k < kDescGroup; ++k) {
-        if (!valid[k]) continue;
-        // the previous slot's tests have read the blurred patch the staging's
-        // dump overwrites: DS operations of a wave run in order; this keeps
-        // the compiler from moving them
-        if (k > 0) asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);  // one slot at a time (register pressure)
-        int lk = lane;
-        asm volatile("" : "+v"(lk));  // per slot: lane-derived values are not kept live across the slots
-        const LevelGeom& L = g.lv[K[k].l];
-        if (pre[k])
-            stage_interior_store(c[k], rawbuf, blur_out, lk);
-        else
-            stage_generic(L, patch_src(g, f[k], K[k].l, img0, row0, frame0, pyr), K[k].cx, K[k].cy, lk, rawbuf);
-        wave_sync();
-        if (k == 0) DSTAMP(2);
-        const DiscRegs D = disc_load(K[k].cx, lk);
-        const BlurTabs tabs = load_blur_tabs(lk);
-        const int2 mm = patch_moments(D, rawbuf, K[k].cx, lk);
-        if (k == 0) DSTAMP(3);
-        blur_patch(L, K[k].cx, lk, rawbuf, blur_out, tabs);
-        const float ang = fast_atan2((float)mm.y, (float)mm.x);
-        float sa, ca;
-        glibc_sincosf(__fmul_rn(ang, (float)(M_PI / 180.f)), &sa, &ca);
-        wave_sync();  // the blurred patch
-        if (k == 0) DSTAMP(4);
-        describe_tests(g, f[k], K[k], lk, blur_out, float4{ang, ca, sa, 0.f}, kps, desc, kp_cap);
-        if (k == 0) DSTAMP(5);
-    }
-#ifdef DESC_STAMPS
-    if (stamp_on && lane == 0 && valid[0]) {
-        for (int k = 1; k <= 5; ++k) atomicAdd(&g_desc_stamps[k - 1], ts[k] - ts[k - 1]);
-        atomicAdd(&g_desc_stamps[15], 1ull);
-    }
-#endif
-}
-
 }  // namespace
 
 #ifdef DESC_STAMPS
@@ -1068,14 +686,6 @@ hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
                            hipStream_t stream, int* err_word, int* err_copy, int f0) {
     if (row0 >= (1u << 24)) return hipErrorInvalidValue;  // row offsets by 24-bit multiplies
-    if constexpr (kKeysPerWave == 1) {  // the grouped kernel (one slot per wave when kDescGroup == 1)
-        const int slots = g.slots_frame * batch;  // frames f0 .. f0+batch-1
-        const int waves = (slots + kDescGroup - 1) / kDescGroup;
-        hipLaunchKernelGGL(describe_group_kernel, dim3((waves + kDescWaves - 1) / kDescWaves), dim3(64 * kDescWaves), 0,
-                           stream, g, slots, f0, img0, row0, frame0, pyr, oct_out, oct_count, kps, desc, counts, kp_cap,
-                           err_word, err_copy);
-        return hipGetLastError();
-    }
     const int items = (g.slots_frame + kKeysPerWave - 1) / kKeysPerWave * batch;  // waves (frames f0 .. f0+batch-1)
     const int blocks = (items + kDescWaves - 1) / kDescWaves;
     hipLaunchKernelGGL(describe_kernel, dim3(blocks), dim3(64 * kDescWaves), 0, stream, g, items, f0, img0, row0, frame0,
