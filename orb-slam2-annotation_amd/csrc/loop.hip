@@ -43,6 +43,8 @@ struct Workspace {  // SoA, candidate c at c * stride
     float* e1;
     float* e2;
     int* idx1;
+    float2* P1;     // mvP1im1 / mvP2im2: FromCameraToImage of X1 / X2 (the ctor's, Sim3Solver.cpp:97-98)
+    float2* P2;
 };
 
 __host__ __device__ inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
@@ -60,12 +62,16 @@ __host__ __device__ inline Workspace carve(void* base, int n_cand, int stride) {
     w.e2 = reinterpret_cast<float*>(p);
     p += align256(n * 4);
     w.idx1 = reinterpret_cast<int*>(p);
+    p += align256(n * 4);
+    w.P1 = reinterpret_cast<float2*>(p);
+    p += align256(n * 8);
+    w.P2 = reinterpret_cast<float2*>(p);
     return w;
 }
 
 size_t workspace_bytes(int n_cand, int stride) {
     const size_t n = (size_t)(n_cand > 0 ? n_cand : 1) * (stride > 0 ? stride : 1);
-    return 2 * align256(n * 12) + 3 * align256(n * 4);
+    return 2 * align256(n * 12) + 3 * align256(n * 4) + 2 * align256(n * 8);
 }
 
 // mvnMaxError = 9.210*sigma^2 kept in a vector<size_t> (Sim3Solver.cpp:92-93)
@@ -105,12 +111,17 @@ __global__ __launch_bounds__(kThreads) void sim3_setup_kernel(const orbgpu_sim3_
         if (ok) {
             const int j = before + (int)__popcll(m & ((1ull << lane) - 1));
             float Xw[3], Xc[3];
+            float u, v;  // mvP1im1 / mvP2im2: FromCameraToImage (the per-hypothesis test's fixed half)
             for (int k = 0; k < 3; ++k) Xw[k] = K1.mp_world[3 * (size_t)i1 + k];
             for (int k = 0; k < 3; ++k) Xc[k] = gemv_row(&K1.Rcw[3 * k], Xw) + K1.tcw[k];
             for (int k = 0; k < 3; ++k) ws.X1[3 * (o + j) + k] = Xc[k];
+            to_image(K1.K, Xc, u, v);
+            ws.P1[o + j] = make_float2(u, v);
             for (int k = 0; k < 3; ++k) Xw[k] = K2.mp_world[3 * (size_t)i2 + k];
             for (int k = 0; k < 3; ++k) Xc[k] = gemv_row(&K2.Rcw[3 * k], Xw) + K2.tcw[k];
             for (int k = 0; k < 3; ++k) ws.X2[3 * (o + j) + k] = Xc[k];
+            to_image(K2.K, Xc, u, v);
+            ws.P2[o + j] = make_float2(u, v);
             ws.e1[o + j] = max_error(K1.sigma2[K1.octave[i1]]);
             ws.e2[o + j] = max_error(K2.sigma2[K2.octave[i2]]);
             ws.idx1[o + j] = i1;
@@ -156,12 +167,18 @@ __global__ __launch_bounds__(kQThreads) void compute_sim3_kernel(
     // (the last 31 raw values are the generator's whole state)
     __shared__ int32_t s_snap[31], s_gen[3 * kWin];
     __shared__ int s_nslots, s_done, s_matched, s_round, s_total;
+    __shared__ float s_K[kMaxC][8];  // each candidate's K1, K2 (fx, fy, cx, cy): no dependent loads per hypothesis
     const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const orbgpu_compute_sim3_query Q = queries[q];
     const int nc = Q.n_cand;
     const int c0 = Q.first_cand;
     const int ipc = prm.iterations_per_call;
     if (tid < nc) {  // Sim3Solver::SetRansacParameters (Sim3Solver.cpp:111-141)
+        const orbgpu_sim3_candidate cd = cands[c0 + tid];
+        for (int k = 0; k < 4; ++k) {
+            s_K[tid][k] = kfs[cd.kf1].K[k];
+            s_K[tid][4 + k] = kfs[cd.kf2].K[k];
+        }
         const int N = n_corr[c0 + tid];
         c_n[tid] = N;
         int max_its = 0;
@@ -280,9 +297,8 @@ __global__ __launch_bounds__(kQThreads) void compute_sim3_kernel(
         __syncthreads();
         for (int h = wave; h < ns; h += kQThreads / 64) {  // CheckInliers
             const int c = s_slot_c[h];
-            const orbgpu_sim3_candidate cd = cands[c0 + c];
-            const float* K1 = kfs[cd.kf1].K;
-            const float* K2 = kfs[cd.kf2].K;
+            const float* K1 = s_K[c];
+            const float* K2 = s_K[c] + 4;
             const size_t o = (size_t)(c0 + c) * stride;
             const int N = c_n[c];
             int cnt = 0;
@@ -294,8 +310,8 @@ __global__ __launch_bounds__(kQThreads) void compute_sim3_kernel(
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int i = min(i0 + 64 * u, N - 1);
-                    in[u] = is_inlier(s_hyp[h], K1, K2, ws.X1 + 3 * (o + i), ws.X2 + 3 * (o + i), ws.e1[o + i],
-                                      ws.e2[o + i]);
+                    in[u] = is_inlier_pre(s_hyp[h], K1, K2, ws.X1 + 3 * (o + i), ws.X2 + 3 * (o + i), ws.P1[o + i],
+                                          ws.P2[o + i], ws.e1[o + i], ws.e2[o + i]);
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) cnt += __popcll(__ballot(in[u] && i0 + 64 * u < N));
@@ -327,13 +343,12 @@ __global__ __launch_bounds__(kQThreads) void compute_sim3_kernel(
     __syncthreads();
     const int mc = s_matched;
     if (mc >= 0) {  // mvbBestInliers of the returning candidate
-        const orbgpu_sim3_candidate cd = cands[c0 + mc];
-        const float* K1 = kfs[cd.kf1].K;
-        const float* K2 = kfs[cd.kf2].K;
+        const float* K1 = s_K[mc];
+        const float* K2 = s_K[mc] + 4;
         const size_t o = (size_t)(c0 + mc) * stride;
         for (int i = tid; i < c_n[mc]; i += kQThreads)
-            inliers[o + i] = is_inlier(s_best[mc], K1, K2, ws.X1 + 3 * (o + i), ws.X2 + 3 * (o + i), ws.e1[o + i],
-                                       ws.e2[o + i]) ? 1 : 0;
+            inliers[o + i] = is_inlier_pre(s_best[mc], K1, K2, ws.X1 + 3 * (o + i), ws.X2 + 3 * (o + i), ws.P1[o + i],
+                                           ws.P2[o + i], ws.e1[o + i], ws.e2[o + i]) ? 1 : 0;
     }
     if (tid < nc) {
         orbgpu_sim3_candidate_state& S = states[c0 + tid];

@@ -186,5 +186,18 @@ __device__ __forceinline__ bool is_inlier(const Hyp& H, const float* K1, const f
     return err1 < e1max && err2 < e2max;
 }
 
+// the same test with the correspondence's own projections mvP1im1 / mvP2im2
+// precomputed (the ctor's FromCameraToImage, identical arithmetic)
+__device__ __forceinline__ bool is_inlier_pre(const Hyp& H, const float* K1, const float* K2, const float* X1,
+                                              const float* X2, float2 p1, float2 p2, float e1max, float e2max) {
+    float pu1, pv1, pu2, pv2;
+    project(H.sR, H.t, K1, X2, pu1, pv1);    // vP2im1 = T12 X2
+    project(H.sRi, H.ti, K2, X1, pu2, pv2);  // vP1im2 = T21 X1
+    const float d1x = p1.x - pu1, d1y = p1.y - pv1, d2x = pu2 - p2.x, d2y = pv2 - p2.y;
+    const float err1 = (float)((double)d1x * d1x + (double)d1y * d1y);
+    const float err2 = (float)((double)d2x * d2x + (double)d2y * d2y);
+    return err1 < e1max && err2 < e2max;
+}
+
 }  // namespace sim3dev
 }  // namespace orbgpu
