@@ -295,28 +295,53 @@ __global__ __launch_bounds__(kQThreads) void compute_sim3_kernel(
             compute_sim3(A, B, prm.fix_scale != 0, s_hyp[tid]);
         }
         __syncthreads();
-        for (int h = wave; h < ns; h += kQThreads / 64) {  // CheckInliers
-            const int c = s_slot_c[h];
-            const float* K1 = s_K[c];
-            const float* K2 = s_K[c] + 4;
-            const size_t o = (size_t)(c0 + c) * stride;
-            const int N = c_n[c];
-            int cnt = 0;
-            // four correspondences per lane in flight (one wave per SIMD here: the
-            // test's loads and FP64 chains are latency bound, so independent work
-            // is what hides them); indices past N are clamped and masked
-            for (int i0 = lane; i0 < N; i0 += 256) {
-                bool in[4];
+        // CheckInliers: a wave takes the hypotheses 2p and 2p + 1 (pairs p = wave,
+        // wave + 8, ..); consecutive hypotheses are mostly one candidate's iterate(5)
+        // run, and then one pass over its correspondences tests both (each
+        // correspondence loaded once).  Four correspondences per lane in flight (one
+        // wave per SIMD here: the test's loads and FP64 chains are latency bound, so
+        // independent work is what hides them); indices past N are clamped and masked.
+        for (int p = wave; 2 * p < ns; p += kQThreads / 64) {
+            const int h0 = 2 * p, h1 = 2 * p + 1;
+            const int c = s_slot_c[h0];
+            const bool both = h1 < ns && s_slot_c[h1] == c;  // wave-uniform
+            auto check = [&](int h, int hb, bool two) {  // hypotheses h (and hb when two) of candidate s_slot_c[h]
+                const int cc = s_slot_c[h];
+                const float* K1 = s_K[cc];
+                const float* K2 = s_K[cc] + 4;
+                const size_t o = (size_t)(c0 + cc) * stride;
+                const int N = c_n[cc];
+                int cnt = 0, cntb = 0;
+                for (int i0 = lane; i0 < N; i0 += 256) {
+                    bool in[4], inb[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int i = min(i0 + 64 * u, N - 1);
-                    in[u] = is_inlier_pre(s_hyp[h], K1, K2, ws.X1 + 3 * (o + i), ws.X2 + 3 * (o + i), ws.P1[o + i],
-                                          ws.P2[o + i], ws.e1[o + i], ws.e2[o + i]);
+                    for (int u = 0; u < 4; ++u) {
+                        const int i = min(i0 + 64 * u, N - 1);
+                        const float* X1 = ws.X1 + 3 * (o + i);
+                        const float* X2 = ws.X2 + 3 * (o + i);
+                        const float2 p1 = ws.P1[o + i], p2 = ws.P2[o + i];
+                        const float e1 = ws.e1[o + i], e2 = ws.e2[o + i];
+                        in[u] = is_inlier_pre(s_hyp[h], K1, K2, X1, X2, p1, p2, e1, e2);
+                        inb[u] = two && is_inlier_pre(s_hyp[hb], K1, K2, X1, X2, p1, p2, e1, e2);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const bool live = i0 + 64 * u < N;
+                        cnt += __popcll(__ballot(in[u] && live));
+                        if (two) cntb += __popcll(__ballot(inb[u] && live));
+                    }
                 }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) cnt += __popcll(__ballot(in[u] && i0 + 64 * u < N));
+                if (lane == 0) {
+                    s_cnt[h] = cnt;
+                    if (two) s_cnt[hb] = cntb;
+                }
+            };
+            if (both) {
+                check(h0, h1, true);
+            } else {
+                check(h0, h0, false);
+                if (h1 < ns) check(h1, h1, false);
             }
-            if (lane == 0) s_cnt[h] = cnt;
         }
         __syncthreads();
         if (tid == 0) {  // the reference's acceptance, in stream order (Sim3Solver.cpp:199-212)
