@@ -70,13 +70,14 @@ typedef struct orbgpu_sim3_candidate {
 } orbgpu_sim3_candidate;
 
 /* Device workspace of orbgpu_sim3_setup_batch_device: per candidate up to
- * match_stride correspondences (X1, X2, max errors, KF1 slot). */
+ * match_stride correspondences (X1, X2, max errors, KF1 slot, and their image
+ * projections mvP1im1 / mvP2im2).  Query it: the layout is the library's. */
 size_t orbgpu_sim3_setup_workspace_bytes(int n_cand, int match_stride);
 
 /* Sim3Solver constructors for n_cand candidates: for i1 ascending with
  * vpMatched12[i1] and both MapPoints valid, mvX3Dc1 = Rcw1*X3D1w + tcw1,
  * mvX3Dc2 likewise, mvnMaxError = (size_t)(9.210*sigma^2) (kept as float),
- * mvnIndices1 = i1 (:54-99).  d_n_corr[c] = N (mvpMapPoints1.size()).
+ * mvnIndices1 = i1, mvP1im1 / mvP2im2 = FromCameraToImage (:54-99).  d_n_corr[c] = N (mvpMapPoints1.size()).
  * Candidates with d_nmatches[c] < min_matches get N = -1 (discarded before
  * a solver is built, LoopClosing.cpp:314-318).  The workspace keeps the
  * correspondences for orbgpu_compute_sim3_batch_device. */
