@@ -327,7 +327,11 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
             // exist, so only k = 2 selects the dump (VALU-bound kernel: round 6)
             const uint32_t doff = kRPitch == 48 ? 16u * idx : __umul24(r, (uint32_t)kRPitch) + 16u * q;
             dst[k] = (k < 2 && 64 * 2 <= kChunks) || idx < (uint32_t)kChunks ? rawbuf + doff : dump;
-            c[k] = load16_a4(top + (__umul24(min(r, (uint32_t)kPatch - 1u), (uint32_t)rp) + 16u * q));
+            // the source offset r * rp + 16 q = r * (rp - 48) + 16 idx: one 24-bit
+            // multiply-add (rp >= w >= 48 here), no quarter-rate v_mul_lo_u32 for
+            // q; lanes past the patch load its last chunk (idx clamped to 128)
+            const uint32_t idxc = k < 2 ? idx : min(idx, (uint32_t)kChunks - 1u), rc = __umul24(idxc, 21846u) >> 16;
+            c[k] = load16_a4(top + (uint32_t)(__umul24(rc, (uint32_t)rp - 48u) + 16u * idxc));
         }
         // unconditional stores (lanes past the patch write into kDump): no
         // branch the loads could be sunk into
@@ -399,8 +403,9 @@ __device__ int2 describe_patch(const Geom& g, int f, const KeyRef& K, int lane, 
     // wave totals now (scalars): the blur below then has every VGPR
     // (the per-lane combinations first: two wave totals instead of three;
     // modulo-2^32 sums, exact since the totals fit)
-    const int m10 = (int)wave_total(cp - (uint32_t)(od + 15) * sp);
-    const int m01 = (int)wave_total(vp - 15u * sp);
+    // (24-bit multiplies: sp <= 255 x 709 disc pixels)
+    const int m10 = (int)wave_total(cp - __umul24((uint32_t)(od + 15), sp));
+    const int m01 = (int)wave_total(vp - __umul24(15u, sp));
 
     // 3. Blur (blur_device.h, the arithmetic of blur.hip) of the 37x37 patch:
     // lane = (output quad q, chunk c of 7 blurred rows); row passes from the
