@@ -593,7 +593,8 @@ __global__ __launch_bounds__(64 * kDescWaves) void describe_kernel(Geom g, int i
 #endif
     DSTAMP(0);
     const int per_frame = (g.slots_frame + kKeysPerWave - 1) / kKeysPerWave;
-    const int fi = item / per_frame, slot0 = (item - fi * per_frame) * kKeysPerWave;
+    const int fi = kKeysPerWave == 1 ? (int)udiv40((uint32_t)item, g.slots_magic) : item / per_frame;
+    const int slot0 = (item - fi * per_frame) * kKeysPerWave;
     const int f = f0 + fi;  // frame of the whole batch (a chunk's launch starts at frame f0)
     if (item >= items) return;
     KeyRef K[kKeysPerWave];
@@ -691,6 +692,8 @@ hipError_t launch_describe(const Geom& g, int batch, const uint8_t* img0, size_t
                            orbgpu_keypoint* kps, uint8_t* desc, int* counts, int kp_cap,
                            hipStream_t stream, int* err_word, int* err_copy, int f0) {
     if (row0 >= (1u << 24)) return hipErrorInvalidValue;  // row offsets by 24-bit multiplies
+    if ((size_t)g.slots_frame * batch >= (1u << 24) || g.slots_frame >= (1 << 16))
+        return hipErrorInvalidValue;  // udiv40's range
     const int items = (g.slots_frame + kKeysPerWave - 1) / kKeysPerWave * batch;  // waves (frames f0 .. f0+batch-1)
     const int blocks = (items + kDescWaves - 1) / kDescWaves;
     hipLaunchKernelGGL(describe_kernel, dim3(blocks), dim3(64 * kDescWaves), 0, stream, g, items, f0, img0, row0, frame0,

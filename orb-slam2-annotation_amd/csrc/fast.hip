@@ -515,8 +515,8 @@ __global__ __launch_bounds__(64 * kCellWaves) void fast_cells_kernel(Geom g, int
     unsigned long long ts[8] = {};
 #endif
     FSTAMP(0);
-    const int f = item / g.total_cells;
-    const int gc = item % g.total_cells;
+    const int f = (int)udiv40((uint32_t)item, g.cells_magic);  // item / total_cells
+    const int gc = item - f * g.total_cells;
     // level and cell coordinates of the frame's cell gc: one scalar load
     const uint32_t ce = g.cell_tab[gc];
     const int l = (int)(ce & 15u), ci = (int)((ce >> 4) & 0x3FFFu), cj = (int)(ce >> 18);
@@ -704,6 +704,7 @@ hipError_t launch_fast_cells(const Geom& g, int batch, const uint8_t* img0, size
                              hipStream_t stream) {
     const int items = g.total_cells * batch;
     if (row0 >= (1u << 24)) return hipErrorInvalidValue;  // row offsets by 24-bit multiplies
+    if (items >= (1 << 24) || g.total_cells >= (1 << 16)) return hipErrorInvalidValue;  // udiv40's range
     const size_t per_wave =
         (((size_t)2 * g.win_pitch * g.win_rows + 2 * ((size_t)fast_list_len(g.win_pitch, g.win_rows, g.det_max) + 1) + 15) & ~(size_t)15);
     dim3 grid((items + kCellWaves - 1) / kCellWaves);

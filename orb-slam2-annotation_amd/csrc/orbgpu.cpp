@@ -389,6 +389,8 @@ int build_geometry(orbgpu_extractor* e, std::vector<int4>& ptab, std::vector<int
     g.total_cells = cell_base;
     g.cand_frame = cand_off;
     g.slots_frame = out_off;
+    g.cells_magic = udiv40_magic((uint32_t)cell_base);
+    g.slots_magic = udiv40_magic((uint32_t)out_off);
     for (int l = 0; l < kMaxLevels; ++l) {
         g.lvl_cell_base[l] = l < L ? g.lv[l].cell_base : INT_MAX;
         g.lvl_out_offset[l] = l < L ? g.lv[l].out_offset : INT_MAX;

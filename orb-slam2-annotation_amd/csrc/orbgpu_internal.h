@@ -129,6 +129,11 @@ struct LevelGeom {
     int blur_tiles_x, blur_tile_base;   // blur work items: 4-column x 64-row strips
 };
 
+// n / d for the divisor whose udiv40_magic(d) is m: exact for n * d < 2^40
+// (m * d - 2^40 < d); the launchers keep n < 2^24 and d < 2^16
+__host__ __device__ constexpr uint64_t udiv40_magic(uint32_t d) { return ((1ull << 40) + d - 1) / d; }
+__host__ __device__ inline uint32_t udiv40(uint32_t n, uint64_t m) { return (uint32_t)(((uint64_t)n * m) >> 40); }
+
 struct Geom {
     int nlevels;
     // level lookup tables, packed so one scalar load brings a whole table and the
@@ -147,6 +152,9 @@ struct Geom {
     int total_cells;          // cells per frame over all levels
     size_t cand_frame;        // u32 candidate slots per frame
     int slots_frame;          // octree output slots per frame (= sum ocap)
+    // n / total_cells and n / slots_frame as ((u64)n * magic) >> 40 (udiv40):
+    // scalar multiplies instead of a VALU reciprocal sequence per wave
+    uint64_t cells_magic, slots_magic;
     int max_cells_level;
     int win_pitch, win_rows;  // FAST LDS tile: max over levels of (wCell+9) rounded to 4, (hCell+6)
     int blur_tiles_frame;     // blur tiles per frame over all levels
