@@ -523,13 +523,18 @@ __device__ void describe_tests(const Geom& g, int f, const KeyRef& K, int lane, 
 
     const size_t o = (size_t)f * kp_cap + K.before + K.i;
     if (lane == 0) {
-        // the four ballot words (scalars) from lane 0 as two 16-byte stores: 8
-        // moves, where selecting words[lane] on lanes 0..3 took 17 VALU
-        uint4* d = reinterpret_cast<uint4*>(desc + o * 32);
-        d[0] = make_uint4((uint32_t)words[0], (uint32_t)(words[0] >> 32), (uint32_t)words[1],
-                          (uint32_t)(words[1] >> 32));
-        d[1] = make_uint4((uint32_t)words[2], (uint32_t)(words[2] >> 32), (uint32_t)words[3],
-                          (uint32_t)(words[3] >> 32));
+        // the four ballot words (scalars) from lane 0 as two 16-byte stores of
+        // 64-bit pairs (v_mov_b64 from the SGPR pairs), where selecting
+        // words[lane] on lanes 0..3 took 17 VALU
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        auto vmov64 = [](unsigned long long x) {  // one v_mov_b64 (the compiler moved the halves apart)
+            unsigned long long v;
+            asm("v_mov_b64 %0, %1" : "=v"(v) : "s"(x));
+            return v;
+        };
+        u64x2* d = reinterpret_cast<u64x2*>(desc + o * 32);
+        d[0] = u64x2{vmov64(words[0]), vmov64(words[1])};
+        d[1] = u64x2{vmov64(words[2]), vmov64(words[3])};
         orbgpu_keypoint kp;
         const float fx = (float)K.cx, fy = (float)K.cy;
         kp.x = K.l == 0 ? fx : __fmul_rn(fx, L.scale);
