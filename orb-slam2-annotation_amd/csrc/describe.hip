@@ -235,6 +235,10 @@ struct alignas(16) DescLds {
 };
 static_assert(offsetof(DescLds, blur) % 16 == 0 && kBlurSlotBytes % 16 == 0, "16-byte dump stores into blur[k]");
 
+#ifndef ORBGPU_DESC_SCALAR_COUNTS
+#define ORBGPU_DESC_SCALAR_COUNTS 1
+#endif
+
 // A keypoint slot of a frame: its level, index within the level and output
 // position; false when the slot is past the level's octree count.
 struct KeyRef {
@@ -255,6 +259,28 @@ __device__ bool key_ref(const Geom& g, int f, int slot, int lane, const uint32_t
     // kOcStride = 16 entries, so every lane's read is in bounds.
     uint32_t se = g.slot_tab[slot];
     uint32_t key = oct_out[(size_t)f * g.slots_frame + slot];
+#if ORBGPU_DESC_SCALAR_COUNTS
+    // the frame's per-level counts as scalar loads (one s_load_dwordx16), the
+    // level's start and count and the frame total by scalar adds: no VALU
+    // (the vector form took a lane load, four DPP adds and the readlanes)
+    (void)lane;
+    se = (uint32_t)__builtin_amdgcn_readfirstlane((int)se);
+    key = (uint32_t)__builtin_amdgcn_readfirstlane((int)key);
+    const int l = (int)(se & 15u), i = (int)(se >> 4);
+    const int* cr = oct_count + (size_t)f * kOcStride;
+    int cv[kMaxLevels];  // all kOcStride entries (in bounds): one wide scalar load, then masked
+#pragma unroll
+    for (int j = 0; j < kMaxLevels; ++j) cv[j] = cr[j];
+    int before = 0, mine = 0, total = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxLevels; ++j) {
+        const int cj = j < g.nlevels ? cv[j] : 0;
+        before += j < l ? cj : 0;
+        mine = j == l ? cj : mine;
+        total += cj;
+    }
+    if (slot == 0 && lane == 0) counts[f] = total;
+#else
     const int ll = lane & 15;
     int c = oct_count[(size_t)f * kOcStride + ll];
     se = (uint32_t)__builtin_amdgcn_readfirstlane((int)se);
@@ -270,6 +296,7 @@ __device__ bool key_ref(const Geom& g, int f, int slot, int lane, const uint32_t
     const int mine = __builtin_amdgcn_readlane(c, l);
     const int before = __builtin_amdgcn_readlane(sc, l) - mine;
     if (slot == 0 && lane == 0) counts[f] = __builtin_amdgcn_readlane(sc, 15);
+#endif
     if (i >= mine) return false;
     K.l = l;
     K.i = i;
