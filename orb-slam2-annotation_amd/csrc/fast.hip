@@ -165,13 +165,15 @@ __device__ int compass_pass(const CellTiles& T, int dw, int dh, int ox, int t, i
 // detection columns, and rows past the region, are masked.
 __constant__ uint32_t c_ng_magic[18] = {0,     65536, 32769, 21846, 16385, 13108, 10923, 9363, 8193,
                                         7282,  6554,  5958,  5462,  5042,  4682,  4370,  4097, 3856};
+// 64 / ng (a scalar load: the division took a VALU reciprocal sequence per pass)
+__constant__ int c_ng_rpi[18] = {0, 64, 32, 21, 16, 12, 10, 9, 8, 7, 6, 5, 5, 4, 4, 4, 4, 3};
 template <int P, bool kBand = false>
 __device__ int compass_pass_dw(const CellTiles& T, int dw, int dh, int ox, int t, int lane, int row0 = 0,
                                int start = 0, int* row_end = nullptr) {
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
     const int c_lo = 3 + ox, c_hi = 3 + ox + dw;  // detection columns [c_lo, c_hi) of the tile
     const int g_lo = c_lo >> 2, ng = ((c_hi - 1) >> 2) - g_lo + 1;  // <= 17 (dw <= 64)
-    const int rpi = 64 / ng;                                          // wave-uniform (scalar)
+    const int rpi = c_ng_rpi[ng];                                     // 64 / ng, wave-uniform (scalar)
     const uint32_t magic = c_ng_magic[ng];
     const int rl = (int)(__umul24((uint32_t)lane, magic) >> 16), g = lane - rl * ng;  // lane / ng, lane % ng
     const int col0 = 4 * (g_lo + g);
