@@ -172,14 +172,17 @@ __device__ inline void glibc_sincosf(float y, float* sinp, float* cosp) {
 // wave total of an unsigned int, wave-uniform: 16-lane row sums on DPP
 // (quad xor 1, xor 2, half mirror, mirror; update_dpp with bound_ctrl so the
 // compiler folds each move into its add: one v_add_u32_dpp per step), then
-// the four row totals read into scalars (integer: order-free, exact)
+// the row totals combined by row broadcasts (integer: order-free, exact)
 __device__ inline uint32_t wave_total(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppXor1, 0xF, 0xF, true);
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppXor2, 0xF, 0xF, true);
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppHalfMirror, 0xF, 0xF, true);
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppMirror, 0xF, 0xF, true);
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
-           (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+    // the four row totals into row 3 (row_bcast:15 into rows 1, 3, then
+    // row_bcast:31 into rows 2, 3), one readlane: 3 VALU instead of 4 readlanes
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 constexpr int kBPitch = 40;      // 37-px blurred rows, from a 4-aligned column
